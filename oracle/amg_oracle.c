@@ -1,0 +1,964 @@
+/*
+ * amg_oracle.c -- TEST INFRASTRUCTURE ONLY (see amg_oracle.h header comment).
+ *
+ * CPU restatement of the jwp3/async-multigrid solve-phase hot path.  Each
+ * function names the reference file:line it restates (paths relative to
+ * /root/reference/src).  Loop bodies keep the reference's floating-point
+ * expression order so results are bit-comparable; OpenMP is used only on
+ * row-independent loops (the reference's `omp for` loops), which does not
+ * change any per-row result.
+ */
+#include "amg_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define OMP_MIN_ROWS 32768
+
+int or_num_threads(void)
+{
+#ifdef _OPENMP
+   return omp_get_max_threads();
+#else
+   return 1;
+#endif
+}
+
+/* ------------------------------------------------------------------------- */
+/* RNG: Misc.cpp:282-285 RandDouble; RHS SMEM_Setup.cpp:1729-1745            */
+/* ------------------------------------------------------------------------- */
+void or_srand(unsigned seed) { srand(seed); }
+
+double or_rand_double(double low, double high)
+{
+   return low + (high - low) * ((double)rand() / RAND_MAX);
+}
+
+void or_rhs_rand(int n, double low, double high, double *f)
+{
+   srand(0);
+   for (int i = 0; i < n; i++) f[i] = or_rand_double(low, high);
+}
+
+/* ------------------------------------------------------------------------- */
+/* SpMV family                                                                */
+/* ------------------------------------------------------------------------- */
+
+/* SEQ_MatVec.cpp:3-24 (and SMEM_Sync_Parfor_MatVec SMEM_MatVec.cpp:5-25) */
+void or_seq_matvec(const or_csr *A, const double *x, double *y)
+{
+   or_smem_matvec(A, x, y, 0, A->nrows);
+}
+
+/* SEQ_MatVec.cpp:26-46 */
+void or_seq_matvec_t(const or_csr *A, const double *x, double *y)
+{
+   for (int i = 0; i < A->ncols; i++) y[i] = 0;
+   for (int i = 0; i < A->nrows; i++) {
+      for (int jj = A->i[i]; jj < A->i[i + 1]; jj++) {
+         int j = A->j[jj];
+         y[j] += A->data[jj] * x[i];
+      }
+   }
+}
+
+/* SEQ_MatVec.cpp:48-63 */
+void or_seq_residual(const or_csr *A, const double *b, const double *x, double *y, double *r)
+{
+   or_seq_matvec(A, x, y);
+   for (int i = 0; i < A->nrows; i++) r[i] = b[i] - y[i];
+}
+
+/* SMEM_MatVec.cpp:302-323 */
+void or_smem_matvec(const or_csr *A, const double *x, double *y, int ns, int ne)
+{
+   const int *A_i = A->i, *A_j = A->j;
+   const double *A_data = A->data;
+#pragma omp parallel for schedule(static) if (ne - ns > OMP_MIN_ROWS)
+   for (int i = ns; i < ne; i++) {
+      double Axi = 0.0;
+      for (int jj = A_i[i]; jj < A_i[i + 1]; jj++) Axi += A_data[jj] * x[A_j[jj]];
+      y[i] = Axi;
+   }
+}
+
+/* SMEM_MatVec.cpp:27-58: per-thread expansion buffer, libgomp static chunks */
+void or_smem_matvec_t_expand(const or_csr *A, const double *x, double *y, int T)
+{
+   int n = A->nrows, nc = A->ncols;
+   double *y_expand = (double *)calloc((size_t)nc * (size_t)T, sizeof(double));
+   int q = n / T, rem = n % T;
+   for (int t = 0; t < T; t++) {
+      int s = t < rem ? t * (q + 1) : t * q + rem;
+      int e = s + (t < rem ? q + 1 : q);
+      double *ye = y_expand + (size_t)nc * t;
+      for (int i = s; i < e; i++)
+         for (int jj = A->i[i]; jj < A->i[i + 1]; jj++) ye[A->j[jj]] += A->data[jj] * x[i];
+   }
+   for (int i = 0; i < nc; i++) {
+      y[i] = 0;
+      for (int t = 0; t < T; t++) y[i] += y_expand[(size_t)t * nc + i];
+   }
+   free(y_expand);
+}
+
+/* SMEM_MatVec.cpp:123-259 SMEM_SpGEMV: y = alpha*A*x + beta*b, specialised on
+ * temp = beta/alpha in {0,-1,1,other} x alpha in {1,-1,other}.  Each branch's
+ * initial value and accumulate sign are restated verbatim. */
+void or_smem_spgemv(const or_csr *A, const double *x, const double *b, double alpha, double beta,
+                    double *y, int ib, int ie)
+{
+   const int *A_i = A->i, *A_j = A->j;
+   const double *A_data = A->data;
+   double temp = beta / alpha;
+   int tcase = (temp == 0) ? 0 : (temp == -1) ? 1 : (temp == 1) ? 2 : 3;
+   int acase = (alpha == 1) ? 0 : (alpha == -1) ? 1 : 2;
+#pragma omp parallel for schedule(static) if (ie - ib > OMP_MIN_ROWS)
+   for (int i = ib; i < ie; i++) {
+      double tempx;
+      switch (tcase) {
+      case 0: tempx = 0.0; break;
+      case 1: tempx = (acase == 1) ? b[i] : -b[i]; break;
+      case 2: tempx = (acase == 1) ? -b[i] : b[i]; break;
+      default: tempx = (acase == 1) ? -b[i] * temp : b[i] * temp; break;
+      }
+      if (acase == 1) {
+         for (int jj = A_i[i]; jj < A_i[i + 1]; jj++) tempx -= A_data[jj] * x[A_j[jj]];
+      } else {
+         for (int jj = A_i[i]; jj < A_i[i + 1]; jj++) tempx += A_data[jj] * x[A_j[jj]];
+      }
+      y[i] = (acase == 2) ? alpha * tempx : tempx;
+   }
+}
+
+/* SMEM_MatVec.cpp:362-378 SMEM_Residual: two passes, y = A x then r = b - y */
+void or_smem_residual(const or_csr *A, const double *b, const double *x, double *y, double *r,
+                      int ns, int ne)
+{
+   or_smem_matvec(A, x, y, ns, ne);
+   for (int i = ns; i < ne; i++) {
+      double ri = b[i] - y[i];
+      r[i] = ri;
+   }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Smoothers                                                                  */
+/* ------------------------------------------------------------------------- */
+
+/* SMEM_Smooth.cpp:6-49 (Parfor, ns=0 ne=n) and :365-407 (row range) */
+void or_smem_jacobi(const or_csr *A, const double *f, double *u, double *u_prev, double omega,
+                    int sweeps, int zero_flag, int ns, int ne)
+{
+   const int *A_i = A->i, *A_j = A->j;
+   const double *A_data = A->data;
+   for (int k = 0; k < sweeps; k++) {
+      if (k == 0 && zero_flag == 1) {
+#pragma omp parallel for schedule(static) if (ne - ns > OMP_MIN_ROWS)
+         for (int i = ns; i < ne; i++)
+            if (A_data[A_i[i]] != 0.0) u[i] = omega * f[i] / A_data[A_i[i]];
+      } else {
+#pragma omp parallel for schedule(static) if (ne - ns > OMP_MIN_ROWS)
+         for (int i = ns; i < ne; i++) u_prev[i] = u[i];
+#pragma omp parallel for schedule(static) if (ne - ns > OMP_MIN_ROWS)
+         for (int i = ns; i < ne; i++) {
+            if (A_data[A_i[i]] != 0.0) {
+               double res = f[i];
+               for (int jj = A_i[i]; jj < A_i[i + 1]; jj++) res -= A_data[jj] * u_prev[A_j[jj]];
+               u[i] += omega * res / A_data[A_i[i]];
+            }
+         }
+      }
+   }
+}
+
+/* SMEM_Smooth.cpp:96-133 (Parfor) and :409-443 (row range) */
+void or_smem_l1jacobi(const or_csr *A, const double *f, double *u, double *u_prev, const double *l1,
+                      int sweeps, int zero_flag, int ns, int ne)
+{
+   const int *A_i = A->i, *A_j = A->j;
+   const double *A_data = A->data;
+   for (int k = 0; k < sweeps; k++) {
+      if (k == 0 && zero_flag == 1) {
+#pragma omp parallel for schedule(static) if (ne - ns > OMP_MIN_ROWS)
+         for (int i = ns; i < ne; i++) u[i] = f[i] / l1[i];
+      } else {
+#pragma omp parallel for schedule(static) if (ne - ns > OMP_MIN_ROWS)
+         for (int i = ns; i < ne; i++) u_prev[i] = u[i];
+#pragma omp parallel for schedule(static) if (ne - ns > OMP_MIN_ROWS)
+         for (int i = ns; i < ne; i++) {
+            double res = f[i];
+            for (int jj = A_i[i]; jj < A_i[i + 1]; jj++) res -= A_data[jj] * u_prev[A_j[jj]];
+            u[i] += res / l1[i];
+         }
+      }
+   }
+}
+
+/* SEQ_Smooth.cpp:4-46: the zero-guess sweep ADDS omega*f/a_ii */
+void or_seq_jacobi(const or_csr *A, const double *f, double *u, double *u_prev, double omega,
+                   int sweeps, int zero_flag)
+{
+   int n = A->nrows;
+   for (int k = 0; k < sweeps; k++) {
+      if (k == 0 && zero_flag == 1) {
+         for (int i = 0; i < n; i++)
+            if (A->data[A->i[i]] != 0.0) {
+               double res = f[i];
+               u[i] += omega * res / A->data[A->i[i]];
+            }
+      } else {
+         for (int i = 0; i < n; i++) u_prev[i] = u[i];
+         for (int i = 0; i < n; i++) {
+            if (A->data[A->i[i]] != 0.0) {
+               double res = f[i];
+               for (int jj = A->i[i]; jj < A->i[i + 1]; jj++) res -= A->data[jj] * u_prev[A->j[jj]];
+               u[i] += omega * res / A->data[A->i[i]];
+            }
+         }
+      }
+   }
+}
+
+/* SEQ_Smooth.cpp:48-87 */
+void or_seq_l1jacobi(const or_csr *A, const double *f, double *u, double *u_prev, const double *l1,
+                     int sweeps, int zero_flag)
+{
+   int n = A->nrows;
+   for (int k = 0; k < sweeps; k++) {
+      if (k == 0 && zero_flag == 1) {
+         for (int i = 0; i < n; i++)
+            if (A->data[A->i[i]] != 0.0) {
+               double res = f[i];
+               u[i] += res / l1[i];
+            }
+      } else {
+         for (int i = 0; i < n; i++) u_prev[i] = u[i];
+         for (int i = 0; i < n; i++) {
+            double res = f[i];
+            for (int jj = A->i[i]; jj < A->i[i + 1]; jj++) res -= A->data[jj] * u_prev[A->j[jj]];
+            u[i] += res / l1[i];
+         }
+      }
+   }
+}
+
+/* SEQ_Smooth.cpp:89-117 */
+void or_seq_gauss_seidel(const or_csr *A, const double *f, double *u, int sweeps)
+{
+   for (int k = 0; k < sweeps; k++)
+      for (int i = 0; i < A->nrows; i++)
+         if (A->data[A->i[i]] != 0.0) {
+            double res = f[i];
+            for (int jj = A->i[i]; jj < A->i[i + 1]; jj++) res -= A->data[jj] * u[A->j[jj]];
+            u[i] += res / A->data[A->i[i]];
+         }
+}
+
+/* Hybrid Jacobi/Gauss-Seidel over a block partition blk[0..nblk]:
+ *   SMEM_Smooth.cpp:222-305 Parfor (diag_scale = A_diag = a_ii/omega, weight 1),
+ *   SMEM_Smooth.cpp:533-586 row range (diag_scale = a_ii, weight 1),
+ *   reverse != 0: the "T" variants :307-363 / :588-641 (rows visited ne-1..ns).
+ * diag_scale == NULL means divide by a_ii.  Blocks are independent within a
+ * sweep (in-block terms read u, out-of-block terms read u_prev copied before
+ * the barrier), so visiting them in order is the reference's result. */
+void or_hybrid_jgs(const or_csr *A, const double *f, double *u, double *u_prev, const int *blk,
+                   int nblk, const double *diag_scale, double weight, int sweeps, int zero_flag,
+                   int reverse)
+{
+   const int *A_i = A->i, *A_j = A->j;
+   const double *A_data = A->data;
+   for (int k = 0; k < sweeps; k++) {
+      int zero = (k == 0 && zero_flag == 1);
+      if (!zero) {
+         for (int b = 0; b < nblk; b++)
+            for (int i = blk[b]; i < blk[b + 1]; i++) u_prev[i] = u[i];
+      }
+#pragma omp parallel for schedule(dynamic, 1) if (nblk > 64)
+      for (int b = 0; b < nblk; b++) {
+         int ns = blk[b], ne = blk[b + 1];
+         if (zero)
+            for (int i = ns; i < ne; i++) u[i] = 0.0;
+         for (int c = 0; c < ne - ns; c++) {
+            int i = reverse ? ne - 1 - c : ns + c;
+            if (A_data[A_i[i]] == 0.0) continue;
+            double ds = diag_scale ? diag_scale[i] : A_data[A_i[i]];
+            double res = f[i];
+            for (int jj = A_i[i]; jj < A_i[i + 1]; jj++) {
+               int ii = A_j[jj];
+               if (ii >= ns && ii < ne)
+                  res -= A_data[jj] * u[ii];
+               else if (!zero)
+                  res -= A_data[jj] * u_prev[ii];
+            }
+            if (zero)
+               u[i] = weight * res / ds;
+            else
+               u[i] += weight * res / ds;
+         }
+      }
+   }
+}
+
+/* SEQ_Smooth.cpp:119-155 */
+void or_seq_sym_jacobi(const or_csr *A, const double *f, double *u, double *y, double *r,
+                       double omega, int sweeps)
+{
+   int n = A->nrows, k = 0;
+   for (int i = 0; i < n; i++) r[i] = f[i];
+   while (1) {
+      for (int i = 0; i < n; i++)
+         if (A->data[A->i[i]] != 0.0) r[i] *= omega / A->data[A->i[i]];
+      or_seq_matvec(A, r, y);
+      for (int i = 0; i < n; i++) {
+         if (A->data[A->i[i]] != 0.0) {
+            r[i] = (2.0 * A->data[A->i[i]] * r[i] / omega) - y[i];
+            r[i] *= omega / A->data[A->i[i]];
+         }
+         u[i] += r[i];
+      }
+      k++;
+      if (k == sweeps) break;
+      or_seq_residual(A, f, u, y, r);
+   }
+}
+
+/* SEQ_Smooth.cpp:157-189 */
+void or_seq_sym_l1jacobi(const or_csr *A, const double *f, double *u, double *y, double *r,
+                         const double *l1, int sweeps)
+{
+   int n = A->nrows, k = 0;
+   for (int i = 0; i < n; i++) r[i] = f[i];
+   while (1) {
+      for (int i = 0; i < n; i++) r[i] /= l1[i];
+      or_seq_matvec(A, r, y);
+      for (int i = 0; i < n; i++) {
+         r[i] = (2.0 * l1[i] * r[i]) - y[i];
+         r[i] /= l1[i];
+         u[i] += r[i];
+      }
+      k++;
+      if (k == sweeps) break;
+      or_seq_residual(A, f, u, y, r);
+   }
+}
+
+/* SMEM_Smooth.cpp:643-702 (one level group, res_compute_type LOCAL: ms=ns, me=ne).
+ * zero_flag is level state that the function does not reset, so with
+ * sweeps > 1 every sweep overwrites u (reference quirk, kept). */
+void or_smem_sym_jacobi(const or_csr *A, const double *f, double *u, double *y, double *r,
+                        double omega, int sweeps, int zero_flag, int ns, int ne)
+{
+   const int *A_i = A->i;
+   const double *A_data = A->data;
+   int k = 0;
+   if (zero_flag == 1) {
+      for (int i = ns; i < ne; i++) r[i] = f[i];
+   } else {
+      or_smem_residual(A, f, u, y, r, ns, ne);
+   }
+   while (1) {
+      for (int i = ns; i < ne; i++) r[i] *= omega / A_data[A_i[i]];
+      or_smem_matvec(A, r, y, ns, ne);
+      for (int i = ns; i < ne; i++) {
+         r[i] = (2.0 * A_data[A_i[i]] * r[i] / omega) - y[i];
+         r[i] *= omega / A_data[A_i[i]];
+      }
+      if (zero_flag == 1) {
+         for (int i = ns; i < ne; i++) u[i] = r[i];
+      } else {
+         for (int i = ns; i < ne; i++) u[i] += r[i];
+      }
+      k++;
+      if (k == sweeps) break;
+      or_smem_residual(A, f, u, y, r, ns, ne);
+   }
+}
+
+/* SMEM_Smooth.cpp:704-762 */
+void or_smem_sym_l1jacobi(const or_csr *A, const double *f, double *u, double *y, double *r,
+                          const double *l1, int sweeps, int zero_flag, int ns, int ne)
+{
+   int k = 0;
+   if (zero_flag == 1) {
+      for (int i = ns; i < ne; i++) r[i] = f[i];
+   } else {
+      or_smem_residual(A, f, u, y, r, ns, ne);
+   }
+   while (1) {
+      for (int i = ns; i < ne; i++) r[i] /= l1[i];
+      or_smem_matvec(A, r, y, ns, ne);
+      for (int i = ns; i < ne; i++) {
+         r[i] = (2.0 * l1[i] * r[i]) - y[i];
+         r[i] /= l1[i];
+      }
+      if (zero_flag == 1) {
+         for (int i = ns; i < ne; i++) u[i] = r[i];
+      } else {
+         for (int i = ns; i < ne; i++) u[i] += r[i];
+      }
+      k++;
+      if (k == sweeps) break;
+      or_smem_residual(A, f, u, y, r, ns, ne);
+   }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Setup helpers                                                              */
+/* ------------------------------------------------------------------------- */
+
+/* SMEM_Setup.cpp:234-237 A_diag[l][i] = a_ii / smooth_weight */
+void or_a_diag(const or_csr *A, double omega, double *out)
+{
+   for (int i = 0; i < A->nrows; i++) out[i] = A->data[A->i[i]] / omega;
+}
+
+/* SMEM_Setup.cpp:222-232 L1_row_norm[l][i] = sum_j |a_ij| */
+void or_l1_norms(const or_csr *A, double *out)
+{
+   for (int i = 0; i < A->nrows; i++) {
+      out[i] = 0;
+      for (int jj = A->i[i]; jj < A->i[i + 1]; jj++) out[i] += fabs(A->data[jj]);
+   }
+}
+
+/* SMEM_Setup.cpp:1018-1030 (ONE_LEVEL thread ranges) */
+void or_partition_equal(int n, int T, int *blk)
+{
+   int size = n / T, rest = n - size * T;
+   for (int t = 0; t < T; t++) blk[t] = (t < rest) ? t * size + t : t * size + rest;
+   blk[T] = n;
+}
+
+static int lower_bound_int(const int *a, int n, long long v)
+{
+   int lo = 0, hi = n;
+   while (lo < hi) {
+      int mid = lo + (hi - lo) / 2;
+      if ((long long)a[mid] < v) lo = mid + 1; else hi = mid;
+   }
+   return lo;
+}
+
+/* SMEM_Setup.cpp:870-893 with nnz_per_thread = ceil(nnz/T) (:940-946) */
+void or_partition_nnz(const or_csr *A, int T, int *blk)
+{
+   int n = A->nrows;
+   long long nnz = A->i[n];
+   long long per = (nnz + T - 1) / T;
+   blk[0] = 0;
+   for (int t = 1; t < T; t++) blk[t] = lower_bound_int(A->i, n, per * t);
+   blk[T] = n;
+}
+
+/* SMEM_Solve.cpp:199-203: sqrt(sum r_i*r_i) */
+double or_norm2(const double *x, int n)
+{
+   double s = 0;
+#pragma omp parallel for schedule(static) reduction(+ : s) if (n > OMP_MIN_ROWS)
+   for (int i = 0; i < n; i++) s += x[i] * x[i];
+   return sqrt(s);
+}
+
+void or_csr_free_owned(or_csr_owned *M)
+{
+   free(M->i); free(M->j); free(M->data);
+   M->i = NULL; M->j = NULL; M->data = NULL;
+}
+
+/* move the diagonal entry of each row of a square matrix to the front
+ * (SMEM_Setup.cpp:1405-1419 StdVector_to_CSR convention) */
+static void diag_first(or_csr_owned *M)
+{
+   if (M->nrows != M->ncols) return;
+   for (int r = 0; r < M->nrows; r++) {
+      int s = M->i[r], e = M->i[r + 1];
+      for (int k = s; k < e; k++) {
+         if (M->j[k] == r) {
+            int cj = M->j[k]; double cv = M->data[k];
+            for (int q = k; q > s; q--) { M->j[q] = M->j[q - 1]; M->data[q] = M->data[q - 1]; }
+            M->j[s] = cj; M->data[s] = cv;
+            break;
+         }
+      }
+   }
+}
+
+/* counting-sort transpose; rows of the result hold ascending source rows */
+void or_csr_transpose(const or_csr *A, or_csr_owned *T)
+{
+   int n = A->nrows, m = A->ncols;
+   long long nnz = A->i[n];
+   T->nrows = m; T->ncols = n; T->nnz = nnz;
+   T->i = (int *)calloc((size_t)m + 1, sizeof(int));
+   T->j = (int *)malloc((size_t)(nnz ? nnz : 1) * sizeof(int));
+   T->data = (double *)malloc((size_t)(nnz ? nnz : 1) * sizeof(double));
+   for (long long k = 0; k < nnz; k++) T->i[A->j[k] + 1]++;
+   for (int c = 0; c < m; c++) T->i[c + 1] += T->i[c];
+   int *pos = (int *)malloc(((size_t)m + 1) * sizeof(int));
+   memcpy(pos, T->i, ((size_t)m + 1) * sizeof(int));
+   for (int r = 0; r < n; r++)
+      for (int k = A->i[r]; k < A->i[r + 1]; k++) {
+         int c = A->j[k];
+         T->j[pos[c]] = r; T->data[pos[c]] = A->data[k]; pos[c]++;
+      }
+   free(pos);
+}
+
+/* Gustavson SpGEMM, sorted columns, diag first when square.  Accumulation is
+ * in the order (A row entry, B row entry), like a row-by-row product. */
+void or_csr_spgemm(const or_csr *A, const or_csr *B, or_csr_owned *C)
+{
+   int n = A->nrows, m = B->ncols;
+   int *mark = (int *)malloc((size_t)m * sizeof(int));
+   double *acc = (double *)calloc((size_t)m, sizeof(double));
+   int *cols = (int *)malloc((size_t)m * sizeof(int));
+   for (int c = 0; c < m; c++) mark[c] = -1;
+   C->nrows = n; C->ncols = m;
+   C->i = (int *)malloc(((size_t)n + 1) * sizeof(int));
+   long long cap = 16 + (long long)A->i[n] * 4, nnz = 0;
+   C->j = (int *)malloc((size_t)cap * sizeof(int));
+   C->data = (double *)malloc((size_t)cap * sizeof(double));
+   C->i[0] = 0;
+   for (int r = 0; r < n; r++) {
+      int nc = 0;
+      for (int ka = A->i[r]; ka < A->i[r + 1]; ka++) {
+         int k = A->j[ka]; double av = A->data[ka];
+         for (int kb = B->i[k]; kb < B->i[k + 1]; kb++) {
+            int c = B->j[kb];
+            if (mark[c] != r) { mark[c] = r; acc[c] = 0.0; cols[nc++] = c; }
+            acc[c] += av * B->data[kb];
+         }
+      }
+      /* insertion sort of the (small) column list */
+      for (int a = 1; a < nc; a++) {
+         int v = cols[a], b = a - 1;
+         while (b >= 0 && cols[b] > v) { cols[b + 1] = cols[b]; b--; }
+         cols[b + 1] = v;
+      }
+      if (nnz + nc > cap) {
+         while (nnz + nc > cap) cap *= 2;
+         C->j = (int *)realloc(C->j, (size_t)cap * sizeof(int));
+         C->data = (double *)realloc(C->data, (size_t)cap * sizeof(double));
+      }
+      for (int a = 0; a < nc; a++) { C->j[nnz] = cols[a]; C->data[nnz] = acc[cols[a]]; nnz++; }
+      C->i[r + 1] = (int)nnz;
+   }
+   C->nnz = nnz;
+   free(mark); free(acc); free(cols);
+   diag_first(C);
+}
+
+/* 7-point Laplacian, diag 6 / off -1, lexicographic x fastest, row entries in
+ * the hypre GenerateLaplacian order: diag, -z, -y, -x, +x, +y, +z
+ * (BuildHypreMatrix.cpp:250-275 with ax=ay=az=0 calls it; hypre itself is
+ * not in the reference tree, so the entry order is restated, unpinned). */
+void or_laplace_7pt(int nx, int ny, int nz, or_csr_owned *A)
+{
+   long long n = (long long)nx * ny * nz;
+   A->nrows = A->ncols = (int)n;
+   A->i = (int *)malloc((size_t)(n + 1) * sizeof(int));
+   A->j = (int *)malloc((size_t)(7 * n) * sizeof(int));
+   A->data = (double *)malloc((size_t)(7 * n) * sizeof(double));
+   long long nnz = 0;
+   A->i[0] = 0;
+   for (int z = 0; z < nz; z++)
+      for (int y = 0; y < ny; y++)
+         for (int x = 0; x < nx; x++) {
+            long long r = x + (long long)nx * (y + (long long)ny * z);
+            A->j[nnz] = (int)r; A->data[nnz++] = 6.0;
+            if (z > 0) { A->j[nnz] = (int)(r - (long long)nx * ny); A->data[nnz++] = -1.0; }
+            if (y > 0) { A->j[nnz] = (int)(r - nx); A->data[nnz++] = -1.0; }
+            if (x > 0) { A->j[nnz] = (int)(r - 1); A->data[nnz++] = -1.0; }
+            if (x < nx - 1) { A->j[nnz] = (int)(r + 1); A->data[nnz++] = -1.0; }
+            if (y < ny - 1) { A->j[nnz] = (int)(r + nx); A->data[nnz++] = -1.0; }
+            if (z < nz - 1) { A->j[nnz] = (int)(r + (long long)nx * ny); A->data[nnz++] = -1.0; }
+            A->i[r + 1] = (int)nnz;
+         }
+   A->nnz = nnz;
+}
+
+/* SMEM_Setup.cpp:1173-1254 SmoothTransfer (JACOBI smooth_interp_type):
+ * G = I - omega D^-1 A with G_ii = 1-omega, Ps = G P, Rs = P^T G^T. */
+void or_smooth_transfer(const or_csr *A, const or_csr *P, double omega, or_csr_owned *Ps,
+                        or_csr_owned *Rs)
+{
+   int n = A->nrows;
+   long long nnz = A->i[n];
+   double *G = (double *)malloc((size_t)nnz * sizeof(double));
+   double *GT = (double *)malloc((size_t)nnz * sizeof(double));
+   for (int i = 0; i < n; i++) {
+      G[A->i[i]] = GT[A->i[i]] = 1.0 - omega;
+      for (int jj = A->i[i] + 1; jj < A->i[i + 1]; jj++) {
+         G[jj] = -omega * A->data[jj] / A->data[A->i[i]];
+         GT[jj] = -omega * A->data[jj] / A->data[A->i[A->j[jj]]];
+      }
+   }
+   or_csr Gm = {n, A->ncols, nnz, A->i, A->j, G};
+   or_csr GTm = {n, A->ncols, nnz, A->i, A->j, GT};
+   or_csr_spgemm(&Gm, P, Ps);
+   or_csr_owned PT;
+   or_csr_transpose(P, &PT);
+   or_csr PTm = {PT.nrows, PT.ncols, PT.nnz, PT.i, PT.j, PT.data};
+   or_csr_spgemm(&PTm, &GTm, Rs);
+   or_csr_free_owned(&PT);
+   free(G); free(GT);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Hierarchy, cycles, solve driver                                            */
+/* ------------------------------------------------------------------------- */
+struct or_hier {
+   int L;
+   or_opts o;
+   int precond_flag;
+   or_csr *A, *P, *R;
+   int *n;
+   double **A_diag, **L1;
+   /* vector (ONE_LEVEL) */
+   double **f, **u, **u_prev, **y, **r, **r_fine, **e;
+   /* level_vector (ALL_LEVELS): lv[k][l] for l < min(k+2, L) */
+   double ***lv_r, ***lv_e, ***lv_u_prev, ***lv_y, ***lv_rr, ***lv_u_fine, ***lv_u_coarse,
+      ***lv_u_fine_prev, ***lv_u_coarse_prev, ***lv_r_fine;
+   int *zero_flags;
+   int **blk; int *nblk;
+   double *u_outer, *y_outer;
+};
+
+static double *dvec(int n) { return (double *)calloc((size_t)(n > 0 ? n : 1), sizeof(double)); }
+
+or_hier *or_hier_create(int L, const or_csr *A, const or_csr *P, const or_csr *R,
+                        const or_opts *opts)
+{
+   or_hier *H = (or_hier *)calloc(1, sizeof(or_hier));
+   H->L = L;
+   H->o = *opts;
+   H->precond_flag = opts->cheby_flag ? 1 : 0;
+   H->A = (or_csr *)malloc(L * sizeof(or_csr));
+   H->P = (or_csr *)malloc(L * sizeof(or_csr));
+   H->R = (or_csr *)malloc(L * sizeof(or_csr));
+   H->n = (int *)malloc(L * sizeof(int));
+   H->A_diag = (double **)malloc(L * sizeof(double *));
+   H->L1 = (double **)malloc(L * sizeof(double *));
+   double ***vs[] = {&H->f, &H->u, &H->u_prev, &H->y, &H->r, &H->r_fine, &H->e};
+   for (unsigned q = 0; q < sizeof(vs) / sizeof(vs[0]); q++) *vs[q] = (double **)malloc(L * sizeof(double *));
+   H->zero_flags = (int *)calloc(L, sizeof(int));
+   H->blk = (int **)malloc(L * sizeof(int *));
+   H->nblk = (int *)malloc(L * sizeof(int));
+   int T = opts->num_threads > 0 ? opts->num_threads : 1;
+   for (int l = 0; l < L; l++) {
+      H->A[l] = A[l];
+      if (l < L - 1) { H->P[l] = P[l]; H->R[l] = R[l]; }
+      int n = A[l].nrows;
+      H->n[l] = n;
+      H->A_diag[l] = dvec(n); or_a_diag(&A[l], opts->smooth_weight, H->A_diag[l]);
+      H->L1[l] = dvec(n); or_l1_norms(&A[l], H->L1[l]);
+      for (unsigned q = 0; q < sizeof(vs) / sizeof(vs[0]); q++) (*vs[q])[l] = dvec(n);
+      H->blk[l] = (int *)malloc((T + 1) * sizeof(int));
+      H->nblk[l] = T;
+      or_partition_equal(n, T, H->blk[l]);
+   }
+   double ****lvs[] = {&H->lv_r, &H->lv_e, &H->lv_u_prev, &H->lv_y, &H->lv_rr, &H->lv_u_fine,
+                       &H->lv_u_coarse, &H->lv_u_fine_prev, &H->lv_u_coarse_prev, &H->lv_r_fine};
+   for (unsigned q = 0; q < sizeof(lvs) / sizeof(lvs[0]); q++) {
+      *lvs[q] = (double ***)malloc(L * sizeof(double **));
+      for (int k = 0; k < L; k++) {
+         (*lvs[q])[k] = (double **)malloc(L * sizeof(double *));
+         for (int l = 0; l < L; l++) (*lvs[q])[k][l] = (l < k + 2) ? dvec(H->n[l]) : NULL;
+      }
+   }
+   H->u_outer = dvec(H->n[0]);
+   H->y_outer = dvec(H->n[0]);
+   return H;
+}
+
+void or_hier_free(or_hier *H)
+{
+   if (!H) return;
+   int L = H->L;
+   double ***vs[] = {&H->f, &H->u, &H->u_prev, &H->y, &H->r, &H->r_fine, &H->e};
+   for (int l = 0; l < L; l++) {
+      free(H->A_diag[l]); free(H->L1[l]); free(H->blk[l]);
+      for (unsigned q = 0; q < sizeof(vs) / sizeof(vs[0]); q++) free((*vs[q])[l]);
+   }
+   for (unsigned q = 0; q < sizeof(vs) / sizeof(vs[0]); q++) free(*vs[q]);
+   double ****lvs[] = {&H->lv_r, &H->lv_e, &H->lv_u_prev, &H->lv_y, &H->lv_rr, &H->lv_u_fine,
+                       &H->lv_u_coarse, &H->lv_u_fine_prev, &H->lv_u_coarse_prev, &H->lv_r_fine};
+   for (unsigned q = 0; q < sizeof(lvs) / sizeof(lvs[0]); q++) {
+      for (int k = 0; k < L; k++) {
+         for (int l = 0; l < L; l++) free((*lvs[q])[k][l]);
+         free((*lvs[q])[k]);
+      }
+      free(*lvs[q]);
+   }
+   free(H->A); free(H->P); free(H->R); free(H->n); free(H->A_diag); free(H->L1);
+   free(H->zero_flags); free(H->blk); free(H->nblk); free(H->u_outer); free(H->y_outer);
+   free(H);
+}
+
+void or_hier_set_blocks(or_hier *H, int level, const int *blk, int nblk)
+{
+   free(H->blk[level]);
+   H->blk[level] = (int *)malloc((nblk + 1) * sizeof(int));
+   memcpy(H->blk[level], blk, (nblk + 1) * sizeof(int));
+   H->nblk[level] = nblk;
+}
+
+int or_hier_levels(or_hier *H) { return H->L; }
+
+double *or_hier_vec(or_hier *H, const char *name, int level)
+{
+   if (!strcmp(name, "u")) return H->u[level];
+   if (!strcmp(name, "f")) return H->f[level];
+   if (!strcmp(name, "r")) return H->r[level];
+   if (!strcmp(name, "u_prev")) return H->u_prev[level];
+   if (!strcmp(name, "y")) return H->y[level];
+   if (!strcmp(name, "e")) return H->e[level];
+   if (!strcmp(name, "r_fine")) return H->r_fine[level];
+   return NULL;
+}
+
+/* SMEM_Solve.cpp:264-377 SMEM_Smooth dispatcher.  Parameter names follow the
+ * reference: (u, y, r) receive the caller's (u, u_prev, y). */
+static void smooth(or_hier *H, int Alevel, const double *f, double *u, double *y, double *r,
+                   int sweeps, int level, int all_levels, int ns, int ne)
+{
+   const or_csr *A = &H->A[Alevel];
+   const or_opts *o = &H->o;
+   int zf = H->zero_flags[level];
+   int multadd = (o->solver == OR_MULTADD || o->solver == OR_ASYNC_MULTADD);
+   int sym = multadd && o->num_post > 0 && o->num_pre > 0;
+   if (all_levels) {
+      if (o->smoother == OR_HYBRID_JACOBI_GAUSS_SEIDEL) {
+         int blk1[2] = {ns, ne};
+         const int *blk = H->blk[Alevel];
+         int nb = H->nblk[Alevel];
+         if (ns != 0 || ne != A->nrows) { blk = blk1; nb = 1; }
+         or_hybrid_jgs(A, f, u, y, blk, nb, NULL, 1.0, sweeps, zf, 0);
+      } else if (o->smoother == OR_L1_JACOBI) {
+         if (sym) or_smem_sym_l1jacobi(A, f, u, y, r, H->L1[Alevel], sweeps, zf, ns, ne);
+         else or_smem_l1jacobi(A, f, u, y, H->L1[Alevel], sweeps, zf, ns, ne);
+      } else {
+         if (sym) or_smem_sym_jacobi(A, f, u, y, r, o->smooth_weight, sweeps, zf, ns, ne);
+         else or_smem_jacobi(A, f, u, y, o->smooth_weight, sweeps, zf, ns, ne);
+      }
+   } else {
+      if (o->smoother == OR_HYBRID_JACOBI_GAUSS_SEIDEL ||
+          o->smoother == OR_L1_HYBRID_JACOBI_GAUSS_SEIDEL) {
+         /* Parfor variant: diag_scale = A_diag (a_ii/omega) or L1 norms, weight 1 */
+         const double *ds = (o->smoother == OR_L1_HYBRID_JACOBI_GAUSS_SEIDEL) ? H->L1[Alevel]
+                                                                               : H->A_diag[Alevel];
+         or_hybrid_jgs(A, f, u, y, H->blk[Alevel], H->nblk[Alevel], ds, 1.0, sweeps, zf, 0);
+      } else if (o->smoother == OR_L1_JACOBI) {
+         or_smem_l1jacobi(A, f, u, y, H->L1[Alevel], sweeps, zf, 0, A->nrows);
+      } else {
+         or_smem_jacobi(A, f, u, y, o->smooth_weight, sweeps, zf, 0, A->nrows);
+      }
+   }
+}
+
+/* SMEM_Sync_AMG.cpp:8-145 SMEM_Sync_Parfor_Vcycle (ONE_LEVEL) */
+void or_vcycle(or_hier *H)
+{
+   int L = H->L;
+   const or_opts *o = &H->o;
+   for (int level = 0; level < L - 1; level++) {
+      int fg = level, cg = level + 1;
+      H->zero_flags[level] = 1;
+      if (level == 0 && H->precond_flag == 0) H->zero_flags[level] = 0;
+      double *f_fine = (fg == 0 && H->precond_flag == 1) ? H->r[fg] : H->f[fg];
+      smooth(H, fg, f_fine, H->u[fg], H->u_prev[fg], H->y[fg], o->num_pre, fg, 0, 0, 0);
+      /* SMEM_Sync_Residual -> SpGEMV(alpha=-1, beta=1) */
+      or_smem_spgemv(&H->A[fg], H->u[fg], f_fine, -1.0, 1.0, H->r_fine[fg], 0, H->n[fg]);
+      /* SMEM_Sync_Parfor_Restrict, construct_R_flag = 1 */
+      or_smem_matvec(&H->R[fg], H->r_fine[fg], H->f[cg], 0, H->n[cg]);
+   }
+   int cl = L - 1;
+   smooth(H, cl, H->f[cl], H->u[cl], H->u_prev[cl], H->y[cl], o->num_pre + o->num_post, cl, 0, 0, 0);
+   for (int level = L - 2; level > -1; level--) {
+      H->zero_flags[level] = 0;
+      int fg = level, cg = level + 1;
+      or_smem_spgemv(&H->P[fg], H->u[cg], H->u[fg], 1.0, 1.0, H->u[fg], 0, H->n[fg]);
+      double *f_fine = (fg == 0 && H->precond_flag == 1) ? H->r[fg] : H->f[fg];
+      smooth(H, fg, f_fine, H->u[fg], H->u_prev[fg], H->y[fg], o->num_post, fg, 0, 0, 0);
+   }
+}
+
+/* SMEM_Sync_AMG.cpp:408-621 SMEM_Sync_Add_Vcycle (ALL_LEVELS, res LOCAL).
+ * Level corrections are added to u in level order (the reference adds them
+ * from concurrent thread groups without atomics). */
+void or_sync_add_vcycle(or_hier *H)
+{
+   int L = H->L;
+   const or_opts *o = &H->o;
+   int multadd = (o->solver == OR_MULTADD || o->solver == OR_ASYNC_MULTADD);
+   for (int k = 0; k < L; k++) {
+      H->zero_flags[k] = 1;
+      int coarsest = multadd ? k : k + 1;
+      memcpy(H->lv_r[k][0], H->r[0], (size_t)H->n[0] * sizeof(double));
+      for (int level = 0; level < coarsest; level++) {
+         if (level < L - 1)
+            or_smem_matvec(&H->R[level], H->lv_r[k][level], H->lv_r[k][level + 1], 0, H->n[level + 1]);
+      }
+      if (k == L - 1) {
+         /* hypre_GaussElimSolve writes hypre's own U_array, which the cycle
+          * never reads: the coarsest correction stays at its initial zero. */
+      } else if (multadd) {
+         memset(H->lv_e[k][k], 0, (size_t)H->n[k] * sizeof(double));
+         smooth(H, k, H->lv_r[k][k], H->lv_e[k][k], H->lv_u_prev[k][k], H->lv_y[k][k],
+                o->num_fine, k, 1, 0, H->n[k]);
+      } else {
+         int fg = k, cg = k + 1;
+         memset(H->lv_u_fine[k][fg], 0, (size_t)H->n[fg] * sizeof(double));
+         memset(H->lv_u_coarse[k][cg], 0, (size_t)H->n[cg] * sizeof(double));
+         smooth(H, cg, H->lv_r[k][cg], H->lv_u_coarse[k][cg], H->lv_u_coarse_prev[k][cg],
+                H->lv_y[k][cg], o->num_coarse, k, 1, 0, H->n[cg]);
+         or_smem_matvec(&H->P[fg], H->lv_u_coarse[k][cg], H->lv_e[k][fg], 0, H->n[fg]);
+         or_smem_residual(&H->A[fg], H->lv_r[k][fg], H->lv_e[k][fg], H->lv_y[k][fg],
+                          H->lv_r_fine[k][fg], 0, H->n[fg]);
+         smooth(H, fg, H->lv_r_fine[k][fg], H->lv_u_fine[k][fg], H->lv_u_fine_prev[k][fg],
+                H->lv_y[k][fg], o->num_fine, k, 1, 0, H->n[fg]);
+         memcpy(H->lv_e[k][k], H->lv_u_fine[k][k], (size_t)H->n[k] * sizeof(double));
+      }
+      for (int level = k - 1; level > -1; level--)
+         or_smem_matvec(&H->P[level], H->lv_e[k][level + 1], H->lv_e[k][level], 0, H->n[level]);
+      for (int i = 0; i < H->n[0]; i++) H->u[0][i] += H->lv_e[k][0][i];
+   }
+}
+
+static void init_vectors(or_hier *H)
+{
+   /* Misc.cpp:565-692 InitVectors + InitSolve: every level vector to zero */
+   for (int l = 0; l < H->L; l++) {
+      size_t b = (size_t)H->n[l] * sizeof(double);
+      if (l > 0) memset(H->f[l], 0, b);
+      memset(H->u[l], 0, b); memset(H->u_prev[l], 0, b); memset(H->y[l], 0, b);
+      memset(H->r[l], 0, b); memset(H->r_fine[l], 0, b); memset(H->e[l], 0, b);
+      H->zero_flags[l] = 0;
+   }
+   for (int k = 0; k < H->L; k++)
+      for (int l = 0; l < H->L && l < k + 2; l++) {
+         size_t b = (size_t)H->n[l] * sizeof(double);
+         memset(H->lv_r[k][l], 0, b); memset(H->lv_e[k][l], 0, b);
+         memset(H->lv_u_prev[k][l], 0, b); memset(H->lv_y[k][l], 0, b);
+         memset(H->lv_rr[k][l], 0, b); memset(H->lv_u_fine[k][l], 0, b);
+         memset(H->lv_u_coarse[k][l], 0, b); memset(H->lv_u_fine_prev[k][l], 0, b);
+         memset(H->lv_u_coarse_prev[k][l], 0, b); memset(H->lv_r_fine[k][l], 0, b);
+      }
+}
+
+/* SMEM_Solve.cpp:11-262, synchronous branch (async_flag == 0) */
+int or_solve(or_hier *H, const double *f, double *u, double *reshist)
+{
+   const or_opts *o = &H->o;
+   int n0 = H->n[0];
+   init_vectors(H);
+   memcpy(H->f[0], f, (size_t)n0 * sizeof(double));
+   memcpy(H->u[0], u, (size_t)n0 * sizeof(double));
+   memset(H->u_outer, 0, (size_t)n0 * sizeof(double));
+   memset(H->y_outer, 0, (size_t)n0 * sizeof(double));
+   double mu24 = 4.0 * pow(o->cheby_mu, 2.0);
+   double delta = o->cheby_delta;
+   double *r = H->r[0];
+   or_smem_spgemv(&H->A[0], H->u[0], H->f[0], -1.0, 1.0, r, 0, n0);
+   double r0 = or_norm2(r, n0);
+   if (reshist) reshist[0] = r0;
+   double omega = 2.0;
+   int done = 0;
+   int all_levels = !(o->solver == OR_MULT || o->solver == OR_BPX);
+   for (int k = 1; k <= o->num_cycles; k++) {
+      if (all_levels) or_sync_add_vcycle(H);
+      else or_vcycle(H);
+      if (o->cheby_flag == 1) {
+         double *uu = H->u[0], *uo = H->u_outer, *yo = H->y_outer;
+#pragma omp parallel for schedule(static) if (n0 > OMP_MIN_ROWS)
+         for (int i = 0; i < n0; i++) {
+            double u_outer_prev = uo[i];
+            uo[i] = yo[i] + omega * (delta * uu[i] + uo[i] - yo[i]);
+            yo[i] = u_outer_prev;
+            uu[i] = uo[i];
+         }
+         omega = 1.0 / (1.0 - omega / mu24);
+      }
+      or_smem_spgemv(&H->A[0], H->u[0], H->f[0], -1.0, 1.0, r, 0, n0);
+      done = k;
+      if (o->check_resnorm == 1) {
+         double rn = or_norm2(r, n0);
+         if (reshist) reshist[k] = rn;
+         if (rn / r0 < o->tol) break;
+      }
+   }
+   memcpy(u, H->u[0], (size_t)n0 * sizeof(double));
+   return done;
+}
+
+/* M^{-1} = one V-cycle in preconditioner mode from a zero state (the
+ * reference uses HYPRE_BoomerAMGSolve here, SMEM_Cheby.cpp:458-459). */
+static void precond_apply(or_hier *H, const double *fin, double *out)
+{
+   int saved = H->precond_flag;
+   H->precond_flag = 1;
+   for (int l = 0; l < H->L; l++) {
+      memset(H->u[l], 0, (size_t)H->n[l] * sizeof(double));
+      H->zero_flags[l] = 0;
+   }
+   memcpy(H->r[0], fin, (size_t)H->n[0] * sizeof(double));
+   or_vcycle(H);
+   memcpy(out, H->u[0], (size_t)H->n[0] * sizeof(double));
+   H->precond_flag = saved;
+}
+
+static double dot(const double *a, const double *b, int n)
+{
+   double s = 0;
+   for (int i = 0; i < n; i++) s += a[i] * b[i];
+   return s;
+}
+
+/* SMEM_Cheby.cpp:410-518 EigsPower */
+void or_eigs_power(or_hier *H, int iters, double *eig_max, double *eig_min)
+{
+   int n = H->n[0];
+   double *u = dvec(n), *e = dvec(n), *fv = dvec(n), *v = dvec(n);
+   for (int i = 0; i < n; i++) u[i] = 1.0;
+   int it = 0;
+   while (1) {
+      double un = sqrt(dot(u, u, n));
+      for (int i = 0; i < n; i++) u[i] *= 1.0 / un;
+      for (int i = 0; i < n; i++) e[i] = u[i];
+      or_seq_matvec(&H->A[0], u, fv);
+      precond_apply(H, fv, u);
+      it++;
+      if (it == iters) break;
+   }
+   for (int i = 0; i < n; i++) v[i] = e[i];
+   double emax = dot(v, u, n);
+   for (int i = 0; i < n; i++) u[i] = 1.0;
+   it = 0;
+   while (1) {
+      double un = sqrt(dot(u, u, n));
+      for (int i = 0; i < n; i++) u[i] *= 1.0 / un;
+      for (int i = 0; i < n; i++) e[i] = u[i];
+      or_seq_matvec(&H->A[0], u, fv);
+      precond_apply(H, fv, u);
+      for (int i = 0; i < n; i++) v[i] = e[i];
+      it++;
+      if (it == iters) break;
+      for (int i = 0; i < n; i++) u[i] += -emax * v[i];
+   }
+   *eig_min = dot(v, u, n);
+   *eig_max = emax;
+   free(u); free(e); free(fv); free(v);
+}
+
+/* SMEM_Cheby.cpp:48-49 */
+void or_cheby_setup(double eig_min, double eig_max, double *mu, double *delta)
+{
+   *mu = (eig_max + eig_min) / (eig_max - eig_min);
+   *delta = 2.0 / (eig_max + eig_min);
+}

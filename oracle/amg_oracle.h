@@ -1,0 +1,159 @@
+/*
+ * amg_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C CPU restatement of the solve-phase hot path of jwp3/async-multigrid
+ * (reference mounted read-only at /root/reference; every function cites the
+ * reference file:line it restates).  It is the parity CHECKER for the MI355X
+ * library and the timed CPU baseline ("port") of bench.py.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it; the
+ * product library (async-multigrid_amd/) never links or calls it.
+ *
+ * Parity status (see DESIGN.md "Oracle"): the reference sources cannot be
+ * compiled here without stand-ins for hypre/METIS headers the image lacks, so
+ * there is no oracle/_ref build.  The reference ships no tests or fixtures.
+ * This restatement is pinned against the one known-answer value recorded from
+ * a run of the reference itself (SURVEY.md Sec.6 / BASELINE.md Sec.2: SMEM_Solve sync
+ * V(1,1), 16^3 7-pt, 2-level 2x2x2 aggregation, omega=0.8, 20 cycles ->
+ * relres 2.6446866599577e-03) and against closed-form properties; everything
+ * else is "parity unpinned" beyond that restatement.
+ *
+ * Floating point: compiled with -ffp-contract=off so every a*x product is
+ * rounded before it is accumulated, exactly as the reference's
+ * `tempx += A_data[jj] * x[A_j[jj]]` does on x86-64 SSE2.
+ */
+#ifndef AMG_ORACLE_H
+#define AMG_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* hypre_CSRMatrix subset used by the hot path (Main.hpp:34-39 types: int, double) */
+typedef struct {
+   int nrows;
+   int ncols;
+   long long nnz;
+   const int *i;      /* row pointer [nrows+1] */
+   const int *j;      /* column index [nnz]    */
+   const double *data;/* values [nnz], diagonal first in each row (hypre convention) */
+} or_csr;
+
+/* Reference enums (Main.hpp:47-144) -- only the values the hot path dispatches on */
+#define OR_JACOBI 0
+#define OR_GAUSS_SEIDEL 1
+#define OR_HYBRID_JACOBI_GAUSS_SEIDEL 2
+#define OR_SYMM_JACOBI 3
+#define OR_L1_JACOBI 6
+#define OR_L1_HYBRID_JACOBI_GAUSS_SEIDEL 12
+
+#define OR_MULT 0
+#define OR_AFACX 1
+#define OR_MULTADD 2
+#define OR_BPX 3
+#define OR_ASYNC_AFACX 5
+#define OR_ASYNC_MULTADD 6
+
+#define OR_ONE_LEVEL 0
+#define OR_ALL_LEVELS 1
+
+/* ---------------- RNG (Misc.cpp:282-285, SMEM_Setup.cpp:1729-1745) -------- */
+void or_srand(unsigned seed);
+double or_rand_double(double low, double high);
+void or_rhs_rand(int n, double low, double high, double *f); /* srand(0) then n draws */
+
+/* ---------------- kernels -------------------------------------------------- */
+void or_seq_matvec(const or_csr *A, const double *x, double *y);
+void or_seq_matvec_t(const or_csr *A, const double *x, double *y);
+void or_seq_residual(const or_csr *A, const double *b, const double *x, double *y, double *r);
+void or_smem_matvec(const or_csr *A, const double *x, double *y, int ns, int ne);
+void or_smem_matvec_t_expand(const or_csr *A, const double *x, double *y, int num_threads);
+void or_smem_spgemv(const or_csr *A, const double *x, const double *b, double alpha, double beta,
+                    double *y, int ib, int ie);
+void or_smem_residual(const or_csr *A, const double *b, const double *x, double *y, double *r,
+                      int ns, int ne);
+
+/* smoothers; zero_flag plays grid.zero_flags[level] */
+void or_smem_jacobi(const or_csr *A, const double *f, double *u, double *u_prev, double omega,
+                    int sweeps, int zero_flag, int ns, int ne);
+void or_smem_l1jacobi(const or_csr *A, const double *f, double *u, double *u_prev, const double *l1,
+                      int sweeps, int zero_flag, int ns, int ne);
+void or_seq_jacobi(const or_csr *A, const double *f, double *u, double *u_prev, double omega,
+                   int sweeps, int zero_flag);
+void or_seq_l1jacobi(const or_csr *A, const double *f, double *u, double *u_prev, const double *l1,
+                     int sweeps, int zero_flag);
+void or_seq_gauss_seidel(const or_csr *A, const double *f, double *u, int sweeps);
+void or_hybrid_jgs(const or_csr *A, const double *f, double *u, double *u_prev, const int *blk,
+                   int nblk, const double *diag_scale, double weight, int sweeps, int zero_flag,
+                   int reverse);
+void or_seq_sym_jacobi(const or_csr *A, const double *f, double *u, double *y, double *r,
+                       double omega, int sweeps);
+void or_seq_sym_l1jacobi(const or_csr *A, const double *f, double *u, double *y, double *r,
+                         const double *l1, int sweeps);
+void or_smem_sym_jacobi(const or_csr *A, const double *f, double *u, double *y, double *r,
+                        double omega, int sweeps, int zero_flag, int ns, int ne);
+void or_smem_sym_l1jacobi(const or_csr *A, const double *f, double *u, double *y, double *r,
+                          const double *l1, int sweeps, int zero_flag, int ns, int ne);
+
+/* ---------------- setup helpers -------------------------------------------- */
+void or_a_diag(const or_csr *A, double omega, double *out);     /* SMEM_Setup.cpp:234-237 */
+void or_l1_norms(const or_csr *A, double *out);                 /* SMEM_Setup.cpp:222-232 */
+void or_partition_equal(int n, int T, int *blk);                /* SMEM_Setup.cpp:1018-1030 */
+void or_partition_nnz(const or_csr *A, int T, int *blk);        /* SMEM_Setup.cpp:870-893,940-946 */
+double or_norm2(const double *x, int n);                        /* SMEM_Solve.cpp:199-203 */
+
+/* generic CSR products used to cross-check the product's structured hierarchy
+ * generator and to build MULTADD smoothed transfers (SMEM_Setup.cpp:1173-1339).
+ * Results are malloc'ed; free with or_csr_free_owned.  Columns sorted, and
+ * when square the diagonal entry is moved first (SMEM_Setup.cpp:1405-1419). */
+typedef struct {
+   int nrows, ncols; long long nnz;
+   int *i, *j; double *data;
+} or_csr_owned;
+void or_csr_free_owned(or_csr_owned *M);
+void or_csr_transpose(const or_csr *A, or_csr_owned *T);
+void or_csr_spgemm(const or_csr *A, const or_csr *B, or_csr_owned *C);
+void or_laplace_7pt(int nx, int ny, int nz, or_csr_owned *A);   /* BuildHypreMatrix.cpp:250-275 via hypre GenerateLaplacian */
+void or_smooth_transfer(const or_csr *A, const or_csr *P, double omega, or_csr_owned *Ps, or_csr_owned *Rs);
+
+/* ---------------- cycles and the solve driver ------------------------------- */
+typedef struct {
+   int solver;            /* OR_MULT, OR_MULTADD, OR_AFACX            */
+   int smoother;          /* OR_JACOBI, OR_L1_JACOBI, OR_HYBRID_...   */
+   int num_pre, num_post; /* num_pre/post_smooth_sweeps               */
+   int num_fine, num_coarse; /* num_fine/coarse_smooth_sweeps (additive) */
+   double smooth_weight;
+   int num_cycles;
+   double tol;
+   int check_resnorm;
+   int cheby_flag;        /* -cheby: also sets precond_flag (SMEM_Main.cpp:553-556) */
+   double cheby_mu, cheby_delta;
+   int num_threads;       /* T of the reference's partitions (hybrid JGS parity) */
+} or_opts;
+
+typedef struct or_hier or_hier;
+or_hier *or_hier_create(int num_levels, const or_csr *A, const or_csr *P, const or_csr *R,
+                        const or_opts *opts);
+void or_hier_free(or_hier *H);
+/* override a level's hybrid-JGS block partition (blk[nblk+1]) */
+void or_hier_set_blocks(or_hier *H, int level, const int *blk, int nblk);
+/* SMEM_Solve sync branch; f/u are level-0 vectors (u is the initial guess and
+ * receives the result).  reshist[k] = ||r_k||_2 for k = 0..cycles done.
+ * Returns the number of cycles performed. */
+int or_solve(or_hier *H, const double *f, double *u, double *reshist);
+/* one cycle on the hierarchy's current state (for kernel-level checks) */
+void or_vcycle(or_hier *H);
+void or_sync_add_vcycle(or_hier *H);
+/* SMEM_Cheby.cpp:410-518 (EigsPower) with this hierarchy's V-cycle as M^{-1} */
+void or_eigs_power(or_hier *H, int iters, double *eig_max, double *eig_min);
+void or_cheby_setup(double eig_min, double eig_max, double *mu, double *delta);
+/* access the hierarchy's level vectors (u, f) for tests */
+double *or_hier_vec(or_hier *H, const char *name, int level);
+int or_hier_levels(or_hier *H);
+
+/* number of OpenMP threads the oracle loops use (cpu_baseline "cores") */
+int or_num_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,337 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this
+module.  The product library never does.  See amg_oracle.h for the parity status.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+OR_JACOBI, OR_GAUSS_SEIDEL, OR_HYBRID_JGS, OR_SYMM_JACOBI = 0, 1, 2, 3
+OR_L1_JACOBI, OR_L1_HYBRID_JGS = 6, 12
+OR_MULT, OR_AFACX, OR_MULTADD = 0, 1, 2
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+
+
+class OrCsr(C.Structure):
+    _fields_ = [("nrows", C.c_int), ("ncols", C.c_int), ("nnz", C.c_longlong),
+                ("i", _ip), ("j", _ip), ("data", _dp)]
+
+
+class OrCsrOwned(C.Structure):
+    _fields_ = [("nrows", C.c_int), ("ncols", C.c_int), ("nnz", C.c_longlong),
+                ("i", _ip), ("j", _ip), ("data", _dp)]
+
+
+class OrOpts(C.Structure):
+    _fields_ = [("solver", C.c_int), ("smoother", C.c_int),
+                ("num_pre", C.c_int), ("num_post", C.c_int),
+                ("num_fine", C.c_int), ("num_coarse", C.c_int),
+                ("smooth_weight", C.c_double), ("num_cycles", C.c_int),
+                ("tol", C.c_double), ("check_resnorm", C.c_int),
+                ("cheby_flag", C.c_int), ("cheby_mu", C.c_double),
+                ("cheby_delta", C.c_double), ("num_threads", C.c_int)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.or_rand_double.restype = C.c_double
+        L.or_rand_double.argtypes = [C.c_double, C.c_double]
+        L.or_norm2.restype = C.c_double
+        L.or_hier_create.restype = C.c_void_p
+        L.or_hier_create.argtypes = [C.c_int, C.POINTER(OrCsr), C.POINTER(OrCsr),
+                                     C.POINTER(OrCsr), C.POINTER(OrOpts)]
+        L.or_hier_free.argtypes = [C.c_void_p]
+        L.or_hier_set_blocks.argtypes = [C.c_void_p, C.c_int, _ip, C.c_int]
+        L.or_solve.argtypes = [C.c_void_p, _dp, _dp, _dp]
+        L.or_solve.restype = C.c_int
+        L.or_vcycle.argtypes = [C.c_void_p]
+        L.or_sync_add_vcycle.argtypes = [C.c_void_p]
+        L.or_hier_vec.restype = _dp
+        L.or_hier_vec.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
+        L.or_eigs_power.argtypes = [C.c_void_p, C.c_int, _dp, _dp]
+        L.or_num_threads.restype = C.c_int
+        _LIB = L
+    return _LIB
+
+
+def dptr(a):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_dp)
+
+
+def iptr(a):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_ip)
+
+
+class Csr:
+    """Host CSR held as numpy arrays (int32 rowptr/col, float64 values)."""
+
+    def __init__(self, nrows, ncols, rowptr, col, val):
+        self.nrows, self.ncols = int(nrows), int(ncols)
+        self.rowptr = np.ascontiguousarray(rowptr, dtype=np.int32)
+        self.col = np.ascontiguousarray(col, dtype=np.int32)
+        self.val = np.ascontiguousarray(val, dtype=np.float64)
+        self.nnz = int(self.rowptr[-1])
+
+    def c(self):
+        return OrCsr(self.nrows, self.ncols, self.nnz, iptr(self.rowptr), iptr(self.col),
+                     dptr(self.val))
+
+    def to_scipy(self):
+        import scipy.sparse as sp
+        return sp.csr_matrix((self.val, self.col, self.rowptr), shape=(self.nrows, self.ncols))
+
+
+def _owned_to_csr(o):
+    n, nnz = o.nrows, o.nnz
+    rp = np.ctypeslib.as_array(o.i, shape=(n + 1,)).copy()
+    cj = np.ctypeslib.as_array(o.j, shape=(max(nnz, 1),))[:nnz].copy()
+    cv = np.ctypeslib.as_array(o.data, shape=(max(nnz, 1),))[:nnz].copy()
+    lib().or_csr_free_owned(C.byref(o))
+    return Csr(n, o.ncols, rp, cj, cv)
+
+
+def laplace_7pt(nx, ny=None, nz=None):
+    ny = nx if ny is None else ny
+    nz = nx if nz is None else nz
+    o = OrCsrOwned()
+    lib().or_laplace_7pt(nx, ny, nz, C.byref(o))
+    return _owned_to_csr(o)
+
+
+def transpose(A):
+    o = OrCsrOwned()
+    ac = A.c()
+    lib().or_csr_transpose(C.byref(ac), C.byref(o))
+    return _owned_to_csr(o)
+
+
+def spgemm(A, B):
+    o = OrCsrOwned()
+    ac, bc = A.c(), B.c()
+    lib().or_csr_spgemm(C.byref(ac), C.byref(bc), C.byref(o))
+    return _owned_to_csr(o)
+
+
+def smooth_transfer(A, P, omega):
+    ps, rs = OrCsrOwned(), OrCsrOwned()
+    ac, pc = A.c(), P.c()
+    lib().or_smooth_transfer(C.byref(ac), C.byref(pc), C.c_double(omega), C.byref(ps), C.byref(rs))
+    return _owned_to_csr(ps), _owned_to_csr(rs)
+
+
+def rhs_rand(n, lo=-1.0, hi=1.0):
+    f = np.empty(n, dtype=np.float64)
+    lib().or_rhs_rand(C.c_int(n), C.c_double(lo), C.c_double(hi), dptr(f))
+    return f
+
+
+# ---- kernels ---------------------------------------------------------------
+def seq_matvec(A, x):
+    y = np.zeros(A.nrows)
+    ac = A.c()
+    lib().or_seq_matvec(C.byref(ac), dptr(x), dptr(y))
+    return y
+
+
+def seq_matvec_t(A, x):
+    y = np.zeros(A.ncols)
+    ac = A.c()
+    lib().or_seq_matvec_t(C.byref(ac), dptr(x), dptr(y))
+    return y
+
+
+def smem_matvec_t_expand(A, x, T):
+    y = np.zeros(A.ncols)
+    ac = A.c()
+    lib().or_smem_matvec_t_expand(C.byref(ac), dptr(x), dptr(y), C.c_int(T))
+    return y
+
+
+def smem_matvec(A, x, y, ns=0, ne=None):
+    ne = A.nrows if ne is None else ne
+    ac = A.c()
+    lib().or_smem_matvec(C.byref(ac), dptr(x), dptr(y), C.c_int(ns), C.c_int(ne))
+    return y
+
+
+def smem_spgemv(A, x, b, alpha, beta, y, ib=0, ie=None):
+    ie = A.nrows if ie is None else ie
+    ac = A.c()
+    bp = dptr(b) if b is not None else None
+    lib().or_smem_spgemv(C.byref(ac), dptr(x), bp, C.c_double(alpha), C.c_double(beta),
+                         dptr(y), C.c_int(ib), C.c_int(ie))
+    return y
+
+
+def smem_residual(A, b, x, y, r, ns=0, ne=None):
+    ne = A.nrows if ne is None else ne
+    ac = A.c()
+    lib().or_smem_residual(C.byref(ac), dptr(b), dptr(x), dptr(y), dptr(r), C.c_int(ns), C.c_int(ne))
+    return r
+
+
+def seq_residual(A, b, x, y, r):
+    ac = A.c()
+    lib().or_seq_residual(C.byref(ac), dptr(b), dptr(x), dptr(y), dptr(r))
+    return r
+
+
+def smem_jacobi(A, f, u, u_prev, omega, sweeps, zero_flag, ns=0, ne=None):
+    ne = A.nrows if ne is None else ne
+    ac = A.c()
+    lib().or_smem_jacobi(C.byref(ac), dptr(f), dptr(u), dptr(u_prev), C.c_double(omega),
+                         C.c_int(sweeps), C.c_int(zero_flag), C.c_int(ns), C.c_int(ne))
+
+
+def smem_l1jacobi(A, f, u, u_prev, l1, sweeps, zero_flag, ns=0, ne=None):
+    ne = A.nrows if ne is None else ne
+    ac = A.c()
+    lib().or_smem_l1jacobi(C.byref(ac), dptr(f), dptr(u), dptr(u_prev), dptr(l1),
+                           C.c_int(sweeps), C.c_int(zero_flag), C.c_int(ns), C.c_int(ne))
+
+
+def seq_jacobi(A, f, u, u_prev, omega, sweeps, zero_flag):
+    ac = A.c()
+    lib().or_seq_jacobi(C.byref(ac), dptr(f), dptr(u), dptr(u_prev), C.c_double(omega),
+                        C.c_int(sweeps), C.c_int(zero_flag))
+
+
+def seq_l1jacobi(A, f, u, u_prev, l1, sweeps, zero_flag):
+    ac = A.c()
+    lib().or_seq_l1jacobi(C.byref(ac), dptr(f), dptr(u), dptr(u_prev), dptr(l1),
+                          C.c_int(sweeps), C.c_int(zero_flag))
+
+
+def seq_gauss_seidel(A, f, u, sweeps):
+    ac = A.c()
+    lib().or_seq_gauss_seidel(C.byref(ac), dptr(f), dptr(u), C.c_int(sweeps))
+
+
+def hybrid_jgs(A, f, u, u_prev, blk, diag_scale, weight, sweeps, zero_flag, reverse=0):
+    ac = A.c()
+    blk = np.ascontiguousarray(blk, dtype=np.int32)
+    ds = dptr(diag_scale) if diag_scale is not None else None
+    lib().or_hybrid_jgs(C.byref(ac), dptr(f), dptr(u), dptr(u_prev), iptr(blk),
+                        C.c_int(len(blk) - 1), ds, C.c_double(weight), C.c_int(sweeps),
+                        C.c_int(zero_flag), C.c_int(reverse))
+
+
+def seq_sym_jacobi(A, f, u, y, r, omega, sweeps):
+    ac = A.c()
+    lib().or_seq_sym_jacobi(C.byref(ac), dptr(f), dptr(u), dptr(y), dptr(r), C.c_double(omega),
+                            C.c_int(sweeps))
+
+
+def seq_sym_l1jacobi(A, f, u, y, r, l1, sweeps):
+    ac = A.c()
+    lib().or_seq_sym_l1jacobi(C.byref(ac), dptr(f), dptr(u), dptr(y), dptr(r), dptr(l1),
+                              C.c_int(sweeps))
+
+
+def smem_sym_jacobi(A, f, u, y, r, omega, sweeps, zero_flag, ns=0, ne=None):
+    ne = A.nrows if ne is None else ne
+    ac = A.c()
+    lib().or_smem_sym_jacobi(C.byref(ac), dptr(f), dptr(u), dptr(y), dptr(r), C.c_double(omega),
+                             C.c_int(sweeps), C.c_int(zero_flag), C.c_int(ns), C.c_int(ne))
+
+
+def smem_sym_l1jacobi(A, f, u, y, r, l1, sweeps, zero_flag, ns=0, ne=None):
+    ne = A.nrows if ne is None else ne
+    ac = A.c()
+    lib().or_smem_sym_l1jacobi(C.byref(ac), dptr(f), dptr(u), dptr(y), dptr(r), dptr(l1),
+                               C.c_int(sweeps), C.c_int(zero_flag), C.c_int(ns), C.c_int(ne))
+
+
+def a_diag(A, omega):
+    out = np.zeros(A.nrows)
+    ac = A.c()
+    lib().or_a_diag(C.byref(ac), C.c_double(omega), dptr(out))
+    return out
+
+
+def l1_norms(A):
+    out = np.zeros(A.nrows)
+    ac = A.c()
+    lib().or_l1_norms(C.byref(ac), dptr(out))
+    return out
+
+
+def partition_equal(n, T):
+    blk = np.zeros(T + 1, dtype=np.int32)
+    lib().or_partition_equal(C.c_int(n), C.c_int(T), iptr(blk))
+    return blk
+
+
+def partition_nnz(A, T):
+    blk = np.zeros(T + 1, dtype=np.int32)
+    ac = A.c()
+    lib().or_partition_nnz(C.byref(ac), C.c_int(T), iptr(blk))
+    return blk
+
+
+def norm2(x):
+    return lib().or_norm2(dptr(x), C.c_int(len(x)))
+
+
+# ---- hierarchy / solve -------------------------------------------------------
+def make_opts(solver=OR_MULT, smoother=OR_JACOBI, num_pre=1, num_post=1, num_fine=1,
+              num_coarse=1, smooth_weight=1.0, num_cycles=20, tol=0.0, check_resnorm=1,
+              cheby_flag=0, cheby_mu=0.0, cheby_delta=0.0, num_threads=1):
+    return OrOpts(solver, smoother, num_pre, num_post, num_fine, num_coarse, smooth_weight,
+                  num_cycles, tol, check_resnorm, cheby_flag, cheby_mu, cheby_delta, num_threads)
+
+
+class Hier:
+    """Oracle hierarchy over host CSR levels A[0..L-1], P/R[0..L-2]."""
+
+    def __init__(self, As, Ps, Rs, opts):
+        self.L = len(As)
+        self._keep = (As, Ps, Rs)
+        self.Ac = (OrCsr * self.L)(*[a.c() for a in As])
+        pr = Ps + [Ps[0]] if Ps else [As[0]]
+        rr = Rs + [Rs[0]] if Rs else [As[0]]
+        self.Pc = (OrCsr * self.L)(*[p.c() for p in pr[:self.L]])
+        self.Rc = (OrCsr * self.L)(*[r.c() for r in rr[:self.L]])
+        self.opts = opts
+        self.h = lib().or_hier_create(self.L, self.Ac, self.Pc, self.Rc, C.byref(self.opts))
+
+    def set_blocks(self, level, blk):
+        blk = np.ascontiguousarray(blk, dtype=np.int32)
+        lib().or_hier_set_blocks(self.h, level, iptr(blk), len(blk) - 1)
+
+    def solve(self, f, u0=None):
+        n0 = self._keep[0][0].nrows
+        u = np.zeros(n0) if u0 is None else np.array(u0, dtype=np.float64)
+        hist = np.zeros(self.opts.num_cycles + 1)
+        k = lib().or_solve(self.h, dptr(np.ascontiguousarray(f)), dptr(u), dptr(hist))
+        return u, hist[:k + 1], k
+
+    def eigs_power(self, iters):
+        emax, emin = C.c_double(), C.c_double()
+        lib().or_eigs_power(self.h, iters, C.byref(emax), C.byref(emin))
+        return emax.value, emin.value
+
+    def __del__(self):
+        try:
+            lib().or_hier_free(self.h)
+        except Exception:
+            pass
