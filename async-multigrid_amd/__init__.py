@@ -1,0 +1,300 @@
+"""async-multigrid for AMD Instinct MI355X (gfx950): Python host binding.
+
+Thin object layer over the C-ABI of libamg_mi355x.so (include/amg_mi355x.h).
+All compute runs in the HIP library; this module only moves handles, host
+arrays and status codes.  There is no CPU fallback: importing the package
+without the built library raises ImportError, and every failed call raises
+AmgError with the library's message.
+
+Load it with ``_load_package()`` helpers (the directory name contains a dash):
+    import importlib.util, sys
+    spec = importlib.util.spec_from_file_location(
+        "async_multigrid_amd", "async-multigrid_amd/__init__.py",
+        submodule_search_locations=["async-multigrid_amd"])
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .abi import AmgError, AmgOpts  # noqa: F401
+from .abi import (AMG_JACOBI, AMG_GAUSS_SEIDEL, AMG_HYBRID_JGS, AMG_SYMM_JACOBI,  # noqa: F401
+                  AMG_L1_JACOBI, AMG_L1_HYBRID_JGS, AMG_MULT, AMG_AFACX, AMG_MULTADD,
+                  AMG_ASYNC_AFACX, AMG_ASYNC_MULTADD, AMG_INTERP_LINEAR, AMG_INTERP_AGGREGATE,
+                  AMG_GEN_A, AMG_GEN_P, AMG_GEN_R, AMG_VEC_F, AMG_VEC_U, AMG_VEC_R)
+
+lib = abi.load()
+
+
+def check(status):
+    if status != 0:
+        msg = lib.amg_last_error()
+        raise AmgError(f"status {status}: {msg.decode() if msg else ''}")
+    return status
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+def default_opts(**kw):
+    o = AmgOpts()
+    lib.amg_opts_default(C.byref(o))
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise AttributeError(k)
+        setattr(o, k, v)
+    return o
+
+
+class Context:
+    """Device, compute stream and level streams (amg_init)."""
+
+    def __init__(self, device=0, nstreams=16):
+        h = C.c_void_p()
+        check(lib.amg_init(C.byref(h), device, nstreams))
+        self.h = h
+        self.device = device
+
+    def sync(self):
+        check(lib.amg_sync(self.h))
+
+    def csr(self, nrows, ncols, rowptr, col, val, diag_first=1):
+        return Mat.register(self, nrows, ncols, rowptr, col, val, diag_first)
+
+    def vec(self, n_or_array):
+        if isinstance(n_or_array, (int, np.integer)):
+            return Vec(self, int(n_or_array))
+        a = np.ascontiguousarray(n_or_array, dtype=np.float64)
+        v = Vec(self, a.size)
+        v.upload(a)
+        return v
+
+    def close(self):
+        if self.h:
+            lib.amg_finalize(self.h)
+            self.h = None
+
+
+class Mat:
+    """Device CSR registered once (amg_csr_register)."""
+
+    def __init__(self, ctx, handle):
+        self.ctx, self.h = ctx, handle
+        nr, nc, nz = C.c_int(), C.c_int(), C.c_longlong()
+        check(lib.amg_mat_info(handle, C.byref(nr), C.byref(nc), C.byref(nz)))
+        self.nrows, self.ncols, self.nnz = nr.value, nc.value, nz.value
+
+    @classmethod
+    def register(cls, ctx, nrows, ncols, rowptr, col, val, diag_first=1):
+        rp = np.ascontiguousarray(rowptr, dtype=np.int32)
+        cj = np.ascontiguousarray(col, dtype=np.int32)
+        cv = np.ascontiguousarray(val, dtype=np.float64)
+        h = C.c_void_p()
+        check(lib.amg_csr_register(ctx.h, int(nrows), int(ncols), int(rp[-1]), _ip(rp), _ip(cj),
+                                   _dp(cv), diag_first, C.byref(h)))
+        return cls(ctx, h)
+
+    def download(self):
+        rp = np.empty(self.nrows + 1, dtype=np.int32)
+        cj = np.empty(max(self.nnz, 1), dtype=np.int32)
+        cv = np.empty(max(self.nnz, 1), dtype=np.float64)
+        check(lib.amg_mat_download(self.ctx.h, self.h, _ip(rp), _ip(cj), _dp(cv)))
+        return rp, cj[:self.nnz], cv[:self.nnz]
+
+    def free(self):
+        if self.h:
+            lib.amg_mat_free(self.h)
+            self.h = None
+
+
+class Vec:
+    """Device fp64 vector (amg_vec_create)."""
+
+    def __init__(self, ctx, n, handle=None, owns=True):
+        self.ctx, self.n = ctx, n
+        if handle is None:
+            h = C.c_void_p()
+            check(lib.amg_vec_create(ctx.h, n, C.byref(h)))
+            handle = h
+        self.h = handle
+        self._owns = owns
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        assert a.size == self.n
+        check(lib.amg_vec_upload(self.ctx.h, self.h, _dp(a)))
+        return self
+
+    def download(self):
+        out = np.empty(self.n, dtype=np.float64)
+        check(lib.amg_vec_download(self.ctx.h, self.h, _dp(out)))
+        return out
+
+    def set(self, a):
+        check(lib.amg_vec_set(self.ctx.h, self.h, float(a)))
+
+    def norm2(self):
+        r = C.c_double()
+        check(lib.amg_vec_norm2(self.ctx.h, self.h, C.byref(r)))
+        return r.value
+
+    def free(self):
+        if self.h and self._owns:
+            lib.amg_vec_free(self.h)
+        self.h = None
+
+
+class Hier:
+    """Level hierarchy + SMEM_Solve driver state (amg_hier_create)."""
+
+    def __init__(self, ctx, As, Ps, Rs, opts):
+        L = len(As)
+        self.ctx, self.L, self.opts = ctx, L, opts
+        self._keep = (As, Ps, Rs)
+        arrA = (C.c_void_p * L)(*[a.h for a in As])
+        arrP = (C.c_void_p * max(L, 1))(*([p.h for p in Ps] + [None] * (max(L, 1) - len(Ps))))
+        arrR = (C.c_void_p * max(L, 1))(*([r.h for r in Rs] + [None] * (max(L, 1) - len(Rs))))
+        h = C.c_void_p()
+        check(lib.amg_hier_create(ctx.h, L, arrA, arrP, arrR, C.byref(opts), C.byref(h)))
+        self.h = h
+        self.n0 = As[0].nrows
+
+    def set_opts(self, opts):
+        check(lib.amg_hier_set_opts(self.h, C.byref(opts)))
+        self.opts = opts
+
+    def set_blocks(self, level, blk):
+        blk = np.ascontiguousarray(blk, dtype=np.int32)
+        check(lib.amg_hier_set_blocks(self.h, level, _ip(blk), blk.size - 1))
+
+    def vec(self, which, level):
+        h = C.c_void_p()
+        check(lib.amg_hier_vec(self.h, which, level, C.byref(h)))
+        n = lib.amg_vec_size(h)
+        return Vec(self.ctx, n, h)
+
+    def solve(self, f, u0=None):
+        """SMEM_Solve: returns (u, residual-norm history, cycles)."""
+        fv = f if isinstance(f, Vec) else self.ctx.vec(f)
+        uv = self.ctx.vec(np.zeros(self.n0) if u0 is None else u0)
+        hist = np.zeros(self.opts.num_cycles + 1)
+        k = C.c_int()
+        check(lib.amg_solve(self.h, fv.h, uv.h, _dp(hist), C.byref(k)))
+        u = uv.download()
+        return u, hist[:k.value + 1], k.value
+
+    def solve_start(self, f, u0):
+        r0 = C.c_double()
+        check(lib.amg_solve_start(self.h, f.h, u0.h, C.byref(r0)))
+        return r0.value
+
+    def iterate(self, k):
+        check(lib.amg_solve_iterate(self.h, k))
+
+    def resnorm(self):
+        r = C.c_double()
+        check(lib.amg_solve_resnorm(self.h, C.byref(r)))
+        return r.value
+
+    def get_u(self, out):
+        check(lib.amg_solve_get_u(self.h, out.h))
+
+    def vcycle(self):
+        check(lib.amg_vcycle(self.h))
+
+    def async_solve(self, f, u0=None):
+        fv = f if isinstance(f, Vec) else self.ctx.vec(f)
+        uv = self.ctx.vec(np.zeros(self.n0) if u0 is None else u0)
+        cnt = np.zeros(self.L, dtype=np.int32)
+        rel = C.c_double()
+        check(lib.amg_async_solve(self.h, fv.h, uv.h, _ip(cnt), C.byref(rel)))
+        return uv.download(), rel.value, cnt
+
+    def eigs_power(self, iters):
+        emax, emin = C.c_double(), C.c_double()
+        check(lib.amg_eigs_power(self.h, iters, C.byref(emax), C.byref(emin)))
+        return emax.value, emin.value
+
+    def profile(self, reset=True):
+        ms = np.zeros(4)
+        n = np.zeros(4, dtype=np.int64)
+        check(lib.amg_hier_profile_read(self.h, _dp(ms),
+                                        n.ctypes.data_as(C.POINTER(C.c_longlong)), int(reset)))
+        return ms, n
+
+    def free(self):
+        if self.h:
+            lib.amg_hier_free(self.h)
+            self.h = None
+
+
+class Gen:
+    """Structured 7-pt problem + geometric Galerkin hierarchy (amg_gen_create)."""
+
+    def __init__(self, nx, ny=None, nz=None, interp=AMG_INTERP_LINEAR, max_levels=25, max_coarse=9):
+        ny = nx if ny is None else ny
+        nz = nx if nz is None else nz
+        h = C.c_void_p()
+        check(lib.amg_gen_create(nx, ny, nz, interp, max_levels, max_coarse, C.byref(h)))
+        self.h = h
+        self.L = lib.amg_gen_num_levels(h)
+
+    def dims(self, level):
+        a, b, c = C.c_int(), C.c_int(), C.c_int()
+        check(lib.amg_gen_dims(self.h, level, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
+
+    def rows(self, which, level):
+        d = self.dims(level + 1 if which == AMG_GEN_R else level)
+        return d[0] * d[1] * d[2]
+
+    def host_csr(self, which, level, z0=0, z1=None, nthreads=0):
+        """(nrows, ncols, rowptr, col, val) of operator rows in planes [z0,z1)."""
+        d = self.dims(level + 1 if which == AMG_GEN_R else level)
+        z1 = d[2] if z1 is None else z1
+        nnz = lib.amg_gen_nnz(self.h, which, level, z0, z1)
+        if nnz < 0:
+            raise AmgError(lib.amg_last_error().decode())
+        nrows = d[0] * d[1] * (z1 - z0)
+        rp = np.empty(nrows + 1, dtype=np.int32)
+        cj = np.empty(max(nnz, 1), dtype=np.int32)
+        cv = np.empty(max(nnz, 1), dtype=np.float64)
+        check(lib.amg_gen_fill(self.h, which, level, z0, z1, _ip(rp), _ip(cj), _dp(cv), nthreads))
+        cd = self.dims(level) if which == AMG_GEN_R else (
+            self.dims(level + 1) if which == AMG_GEN_P else self.dims(level))
+        return nrows, cd[0] * cd[1] * cd[2], rp, cj[:nnz], cv[:nnz]
+
+    def register(self, ctx, which, level, z0=0, z1=None):
+        d = self.dims(level + 1 if which == AMG_GEN_R else level)
+        z1 = d[2] if z1 is None else z1
+        h = C.c_void_p()
+        check(lib.amg_gen_register(ctx.h, self.h, which, level, z0, z1, C.byref(h)))
+        return Mat(ctx, h)
+
+    def free(self):
+        if self.h:
+            lib.amg_gen_free(self.h)
+            self.h = None
+
+
+def rhs_rand(r0, r1, lo=-1.0, hi=1.0):
+    out = np.empty(r1 - r0, dtype=np.float64)
+    check(lib.amg_rhs_rand(r0, r1, lo, hi, _dp(out)))
+    return out
+
+
+def build_hierarchy(ctx, gen, opts, levels=None):
+    """Register every level operator of a generator on the device and build a Hier."""
+    L = gen.L if levels is None else levels
+    As = [gen.register(ctx, AMG_GEN_A, l) for l in range(L)]
+    Ps = [gen.register(ctx, AMG_GEN_P, l) for l in range(L - 1)]
+    Rs = [gen.register(ctx, AMG_GEN_R, l) for l in range(L - 1)]
+    return Hier(ctx, As, Ps, Rs, opts)
+
+
+from . import smem  # noqa: E402,F401  (reference-named kernel mirror)

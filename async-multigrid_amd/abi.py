@@ -1,0 +1,144 @@
+"""ctypes prototypes of every entry point declared in include/amg_mi355x.h.
+
+The library is loaded from the package's lib/ directory (built in-tree by
+__graft_entry__.build()).  There is no fallback: if the shared object is
+missing, importing the package raises.
+"""
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libamg_mi355x.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "amg_mi355x.h")
+
+_p = C.c_void_p
+_i = C.c_int
+_ll = C.c_longlong
+_d = C.c_double
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+_llp = C.POINTER(C.c_longlong)
+_pp = C.POINTER(C.c_void_p)
+
+AMG_OK = 0
+AMG_JACOBI, AMG_GAUSS_SEIDEL, AMG_HYBRID_JGS, AMG_SYMM_JACOBI = 0, 1, 2, 3
+AMG_L1_JACOBI, AMG_L1_HYBRID_JGS = 6, 12
+AMG_MULT, AMG_AFACX, AMG_MULTADD, AMG_ASYNC_AFACX, AMG_ASYNC_MULTADD = 0, 1, 2, 5, 6
+AMG_FULL_ASYNC, AMG_SEMI_ASYNC = 0, 1
+AMG_VEC_F, AMG_VEC_U, AMG_VEC_R = 0, 1, 2
+AMG_INTERP_LINEAR, AMG_INTERP_AGGREGATE = 0, 1
+AMG_GEN_A, AMG_GEN_P, AMG_GEN_R = 0, 1, 2
+
+
+class AmgOpts(C.Structure):
+    _fields_ = [("solver", _i), ("smoother", _i),
+                ("num_pre_smooth_sweeps", _i), ("num_post_smooth_sweeps", _i),
+                ("num_fine_smooth_sweeps", _i), ("num_coarse_smooth_sweeps", _i),
+                ("smooth_weight", _d), ("num_cycles", _i), ("tol", _d),
+                ("check_resnorm", _i), ("cheby_flag", _i), ("cheby_mu", _d),
+                ("cheby_delta", _d), ("num_threads", _i), ("jgs_block_rows", _i),
+                ("reuse_outer_residual", _i), ("async_type", _i), ("profile", _i)]
+
+
+# name -> (restype, argtypes)
+PROTOTYPES = {
+    "amg_opts_default": (None, [C.POINTER(AmgOpts)]),
+    "amg_init": (_i, [_pp, _i, _i]),
+    "amg_finalize": (_i, [_p]),
+    "amg_sync": (_i, [_p]),
+    "amg_last_error": (C.c_char_p, []),
+    "amg_version": (_i, []),
+    "amg_csr_register": (_i, [_p, _i, _i, _ll, _ip, _ip, _dp, _i, _pp]),
+    "amg_mat_free": (_i, [_p]),
+    "amg_mat_info": (_i, [_p, _ip, _ip, _llp]),
+    "amg_mat_download": (_i, [_p, _p, _ip, _ip, _dp]),
+    "amg_vec_create": (_i, [_p, _i, _pp]),
+    "amg_vec_free": (_i, [_p]),
+    "amg_vec_size": (_i, [_p]),
+    "amg_vec_upload": (_i, [_p, _p, _dp]),
+    "amg_vec_download": (_i, [_p, _p, _dp]),
+    "amg_vec_set": (_i, [_p, _p, _d]),
+    "amg_vec_copy": (_i, [_p, _p, _p]),
+    "amg_vec_axpy": (_i, [_p, _d, _p, _p]),
+    "amg_vec_ivaxpy": (_i, [_p, _p, _p, _p]),
+    "amg_vec_scale": (_i, [_p, _d, _p]),
+    "amg_vec_norm2": (_i, [_p, _p, _dp]),
+    "amg_vec_dot": (_i, [_p, _p, _p, _dp]),
+    "amg_matvec": (_i, [_p, _p, _p, _p, _i, _i]),
+    "amg_matvec_t": (_i, [_p, _p, _p, _p, _i]),
+    "amg_spgemv": (_i, [_p, _p, _p, _p, _d, _d, _p, _i, _i]),
+    "amg_matvec_timed": (_i, [_p, _p, _p, _p, _i, _dp]),
+    "amg_residual": (_i, [_p, _p, _p, _p, _p, _p, _i, _i]),
+    "amg_jacobi": (_i, [_p, _p, _p, _p, _p, _d, _i, _i, _i, _i, _i]),
+    "amg_l1_jacobi": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i]),
+    "amg_hybrid_jgs": (_i, [_p, _p, _p, _p, _p, _ip, _i, _p, _d, _i, _i, _i]),
+    "amg_gauss_seidel": (_i, [_p, _p, _p, _p, _i]),
+    "amg_sym_jacobi": (_i, [_p, _p, _p, _p, _p, _p, _d, _p, _i, _i, _i, _i, _i]),
+    "amg_l1_norms": (_i, [_p, _p, _p]),
+    "amg_a_diag": (_i, [_p, _p, _d, _p]),
+    "amg_hier_create": (_i, [_p, _i, _pp, _pp, _pp, C.POINTER(AmgOpts), _pp]),
+    "amg_hier_free": (_i, [_p]),
+    "amg_hier_set_opts": (_i, [_p, C.POINTER(AmgOpts)]),
+    "amg_hier_set_blocks": (_i, [_p, _i, _ip, _i]),
+    "amg_hier_vec": (_i, [_p, _i, _i, _pp]),
+    "amg_solve": (_i, [_p, _p, _p, _dp, _ip]),
+    "amg_solve_start": (_i, [_p, _p, _p, _dp]),
+    "amg_solve_iterate": (_i, [_p, _i]),
+    "amg_solve_resnorm": (_i, [_p, _dp]),
+    "amg_solve_get_u": (_i, [_p, _p]),
+    "amg_vcycle": (_i, [_p]),
+    "amg_async_solve": (_i, [_p, _p, _p, _ip, _dp]),
+    "amg_eigs_power": (_i, [_p, _i, _dp, _dp]),
+    "amg_hier_profile_read": (_i, [_p, _dp, _llp, _i]),
+    "amg_gen_create": (_i, [_i, _i, _i, _i, _i, _i, _pp]),
+    "amg_gen_free": (_i, [_p]),
+    "amg_gen_num_levels": (_i, [_p]),
+    "amg_gen_dims": (_i, [_p, _i, _ip, _ip, _ip]),
+    "amg_gen_nnz": (_ll, [_p, _i, _i, _i, _i]),
+    "amg_gen_fill": (_i, [_p, _i, _i, _i, _i, _ip, _ip, _dp, _i]),
+    "amg_gen_register": (_i, [_p, _p, _i, _i, _i, _i, _pp]),
+    "amg_rhs_rand": (_i, [_ll, _ll, _d, _d, _dp]),
+    # distributed (RCCL) interface
+    "amg_dist_unique_id_size": (_i, []),
+    "amg_dist_get_unique_id": (_i, [C.c_char_p]),
+    "amg_dist_init": (_i, [_p, _i, _i, C.c_char_p]),
+    "amg_dist_finalize": (_i, [_p]),
+    "amg_dist_allreduce_sum": (_i, [_p, _dp, _i]),
+    "amg_dist_barrier": (_i, [_p]),
+    "amg_dist_hier_create_structured": (_i, [_p, _p, C.POINTER(AmgOpts), _pp]),
+    "amg_dist_hier_local_rows": (_i, [_p, _i, _ip, _ip]),
+    "amg_dist_solve_start": (_i, [_p, _dp, _dp]),
+    "amg_dist_solve_iterate": (_i, [_p, _i]),
+    "amg_dist_solve_resnorm": (_i, [_p, _dp]),
+    "amg_dist_get_u": (_i, [_p, _dp]),
+    "amg_dist_hier_free": (_i, [_p]),
+    "amg_dist_profile_read": (_i, [_p, _dp, _llp, _i]),
+    "amg_dist_fine_spmv": (_i, [_p, _dp, _dp]),
+}
+
+
+def header_symbols(path=HEADER):
+    """Names of every function the public header declares."""
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(amg_[a-z_0-9]+)\s*\(", txt, flags=re.M)
+    return sorted(set(names))
+
+
+class AmgError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build the HIP library first (python -c 'import __graft_entry__ as g; g.build()')")
+    lib = C.CDLL(path)
+    for name, (res, args) in PROTOTYPES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    return lib

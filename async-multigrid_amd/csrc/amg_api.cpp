@@ -1,0 +1,564 @@
+// amg_api.cpp -- C-ABI: context, matrices, vectors and the per-kernel entry
+// points that replace the reference's SEQ_* / SMEM_* kernels.
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "amg_internal.h"
+
+static thread_local std::string g_last_error;
+
+int amg_set_error(int code, const char *fmt, ...)
+{
+   char buf[1024];
+   va_list ap;
+   va_start(ap, fmt);
+   vsnprintf(buf, sizeof(buf), fmt, ap);
+   va_end(ap);
+   g_last_error = buf;
+   return code;
+}
+
+extern "C" const char *amg_last_error(void) { return g_last_error.c_str(); }
+extern "C" int amg_version(void) { return 1; }
+
+extern "C" void amg_opts_default(amg_opts *o)
+{
+   std::memset(o, 0, sizeof(*o));
+   // SMEM_Main.cpp:65-105
+   o->solver = AMG_MULT;
+   o->smoother = AMG_JACOBI;
+   o->num_pre_smooth_sweeps = 1;
+   o->num_post_smooth_sweeps = 1;
+   o->num_fine_smooth_sweeps = 1;
+   o->num_coarse_smooth_sweeps = 1;
+   o->smooth_weight = 1.0;
+   o->num_cycles = 20;
+   o->tol = 1e-9;
+   o->check_resnorm = 1;
+   o->cheby_flag = 0;
+   o->num_threads = 1;
+   o->jgs_block_rows = 64;
+   o->reuse_outer_residual = 0;
+   o->async_type = AMG_FULL_ASYNC;
+   o->profile = 0;
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
+{
+   AMG_ARG(out, "amg_init: null out");
+   int ndev = 0;
+   AMG_HIP(hipGetDeviceCount(&ndev));
+   AMG_ARG(device >= 0 && device < ndev, "amg_init: device %d of %d", device, ndev);
+   AMG_HIP(hipSetDevice(device));
+   amg_ctx *c = new amg_ctx();
+   c->device = device;
+   AMG_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+   AMG_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+   for (int i = 0; i < std::max(0, nstreams); i++) {
+      hipStream_t s;
+      AMG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      c->level_streams.push_back(s);
+   }
+   AMG_HIP(hipMalloc(&c->d_scalars, 8192 * sizeof(double)));
+   AMG_HIP(hipMemset(c->d_scalars, 0, 8192 * sizeof(double)));
+   AMG_HIP(hipHostMalloc(&c->h_pinned, 1024 * sizeof(double)));
+   hipDeviceProp_t prop;
+   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+   *out = c;
+   return AMG_OK;
+}
+
+extern "C" int amg_finalize(amg_ctx *c)
+{
+   if (!c) return AMG_OK;
+   hipSetDevice(c->device);
+   hipStreamSynchronize(c->stream);
+   for (auto s : c->level_streams) {
+      hipStreamSynchronize(s);
+      hipStreamDestroy(s);
+   }
+   if (c->comm_stream) hipStreamDestroy(c->comm_stream);
+   hipStreamDestroy(c->stream);
+   hipFree(c->d_partials);
+   hipFree(c->d_scalars);
+   hipHostFree(c->h_pinned);
+   delete c;
+   return AMG_OK;
+}
+
+extern "C" int amg_sync(amg_ctx *c)
+{
+   AMG_ARG(c, "amg_sync: null ctx");
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   return AMG_OK;
+}
+
+int amg_ctx_partials(amg_ctx *c, size_t n, double **out)
+{
+   if (n > c->partials_cap) {
+      // grow only at points where the stream may be synchronised
+      AMG_HIP(hipStreamSynchronize(c->stream));
+      hipFree(c->d_partials);
+      c->d_partials = nullptr;
+      size_t cap = std::max<size_t>(n, 1 << 16);
+      AMG_HIP(hipMalloc(&c->d_partials, cap * sizeof(double)));
+      c->partials_cap = cap;
+   }
+   *out = c->d_partials;
+   return AMG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// matrices
+// ---------------------------------------------------------------------------
+static int mat_alloc(amg_ctx *c, int nrows, int ncols, long long nnz, amg_mat **out)
+{
+   amg_mat *A = new amg_mat();
+   A->ctx = c;
+   A->nrows = nrows;
+   A->ncols = ncols;
+   A->nnz = nnz;
+   size_t np = (size_t)nnz + AMG_NNZ_PAD;
+   hipError_t e = hipMalloc(&A->rowptr, ((size_t)nrows + 1) * sizeof(int));
+   if (e == hipSuccess) e = hipMalloc(&A->col, np * sizeof(int));
+   if (e == hipSuccess) e = hipMalloc(&A->val, np * sizeof(double));
+   if (e == hipSuccess) e = hipMalloc(&A->diag, std::max(1, nrows) * sizeof(double));
+   if (e != hipSuccess) {
+      hipFree(A->rowptr); hipFree(A->col); hipFree(A->val); hipFree(A->diag);
+      delete A;
+      return amg_set_error(AMG_ERR_OOM, "amg_csr_register: device allocation of %lld nnz failed: %s",
+                           nnz, hipGetErrorString(e));
+   }
+   // padding: col 0 (a valid x index), val 0
+   AMG_HIP(hipMemsetAsync(A->col + nnz, 0, AMG_NNZ_PAD * sizeof(int), c->stream));
+   AMG_HIP(hipMemsetAsync(A->val + nnz, 0, AMG_NNZ_PAD * sizeof(double), c->stream));
+   *out = A;
+   return AMG_OK;
+}
+
+int amg_mat_finish(amg_mat *A)
+{
+   amgk::extract_diag(A->ctx->stream, A);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+int amg_mat_create_device(amg_ctx *c, int nrows, int ncols, long long nnz, amg_mat **out)
+{
+   return mat_alloc(c, nrows, ncols, nnz, out);
+}
+
+extern "C" int amg_csr_register(amg_ctx *c, int nrows, int ncols, long long nnz, const int *rowptr,
+                                const int *col, const double *val, int diag_first, amg_mat **out)
+{
+   AMG_ARG(c && out && rowptr && (nnz == 0 || (col && val)), "amg_csr_register: null argument");
+   AMG_ARG(nrows >= 0 && ncols >= 0 && nnz >= 0, "amg_csr_register: negative size");
+   AMG_ARG(nnz < (1LL << 31) - AMG_NNZ_PAD, "amg_csr_register: nnz %lld exceeds int32 CSR", nnz);
+   AMG_ARG(rowptr[nrows] == nnz && rowptr[0] == 0, "amg_csr_register: rowptr[0]=%d rowptr[n]=%d nnz=%lld",
+           rowptr[0], rowptr[nrows], nnz);
+   AMG_ARG(nrows == 0 || ncols > 0, "amg_csr_register: ncols must be positive");
+   amg_mat *A = nullptr;
+   AMG_TRY(mat_alloc(c, nrows, ncols, nnz, &A));
+   A->diag_first = diag_first;
+   AMG_HIP(hipMemcpyAsync(A->rowptr, rowptr, ((size_t)nrows + 1) * sizeof(int),
+                          hipMemcpyHostToDevice, c->stream));
+   if (nnz) {
+      AMG_HIP(hipMemcpyAsync(A->col, col, (size_t)nnz * sizeof(int), hipMemcpyHostToDevice, c->stream));
+      AMG_HIP(hipMemcpyAsync(A->val, val, (size_t)nnz * sizeof(double), hipMemcpyHostToDevice,
+                             c->stream));
+   }
+   AMG_TRY(amg_mat_finish(A));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   *out = A;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_free(amg_mat *A)
+{
+   if (!A) return AMG_OK;
+   if (A->trans) amg_mat_free(A->trans);
+   hipFree(A->rowptr);
+   hipFree(A->col);
+   hipFree(A->val);
+   hipFree(A->diag);
+   delete A;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz)
+{
+   AMG_ARG(A, "amg_mat_info: null matrix");
+   if (nrows) *nrows = A->nrows;
+   if (ncols) *ncols = A->ncols;
+   if (nnz) *nnz = A->nnz;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_download(amg_ctx *c, const amg_mat *A, int *rowptr, int *col, double *val)
+{
+   AMG_ARG(c && A, "amg_mat_download: null argument");
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   if (rowptr)
+      AMG_HIP(hipMemcpy(rowptr, A->rowptr, ((size_t)A->nrows + 1) * sizeof(int), hipMemcpyDeviceToHost));
+   if (col && A->nnz) AMG_HIP(hipMemcpy(col, A->col, (size_t)A->nnz * sizeof(int), hipMemcpyDeviceToHost));
+   if (val && A->nnz) AMG_HIP(hipMemcpy(val, A->val, (size_t)A->nnz * sizeof(double), hipMemcpyDeviceToHost));
+   return AMG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// vectors
+// ---------------------------------------------------------------------------
+extern "C" int amg_vec_create(amg_ctx *c, int n, amg_vec **out)
+{
+   AMG_ARG(c && out && n >= 0, "amg_vec_create: bad argument");
+   amg_vec *v = new amg_vec();
+   v->ctx = c;
+   v->n = n;
+   hipError_t e = hipMalloc(&v->d, std::max(1, n) * sizeof(double));
+   if (e != hipSuccess) {
+      delete v;
+      return amg_set_error(AMG_ERR_OOM, "amg_vec_create(%d): %s", n, hipGetErrorString(e));
+   }
+   AMG_HIP(hipMemsetAsync(v->d, 0, std::max(1, n) * sizeof(double), c->stream));
+   *out = v;
+   return AMG_OK;
+}
+
+extern "C" int amg_vec_free(amg_vec *v)
+{
+   if (!v) return AMG_OK;
+   if (v->owns) hipFree(v->d);
+   delete v;
+   return AMG_OK;
+}
+
+extern "C" int amg_vec_size(const amg_vec *v) { return v ? v->n : -1; }
+
+extern "C" int amg_vec_upload(amg_ctx *c, amg_vec *v, const double *h)
+{
+   AMG_ARG(c && v && h, "amg_vec_upload: null argument");
+   AMG_HIP(hipMemcpyAsync(v->d, h, (size_t)v->n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   return AMG_OK;
+}
+
+extern "C" int amg_vec_download(amg_ctx *c, const amg_vec *v, double *h)
+{
+   AMG_ARG(c && v && h, "amg_vec_download: null argument");
+   AMG_HIP(hipMemcpyAsync(h, v->d, (size_t)v->n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   return AMG_OK;
+}
+
+extern "C" int amg_vec_set(amg_ctx *c, amg_vec *v, double a)
+{
+   AMG_ARG(c && v, "amg_vec_set: null argument");
+   amgk::vset(c->stream, v->d, a, 0, v->n);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_vec_copy(amg_ctx *c, const amg_vec *x, amg_vec *y)
+{
+   AMG_ARG(c && x && y && x->n == y->n, "amg_vec_copy: size mismatch");
+   amgk::vcopy(c->stream, x->d, y->d, 0, x->n);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_vec_axpy(amg_ctx *c, double a, const amg_vec *x, amg_vec *y)
+{
+   AMG_ARG(c && x && y && x->n == y->n, "amg_vec_axpy: size mismatch");
+   amgk::vaxpy(c->stream, a, x->d, y->d, 0, x->n);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_vec_ivaxpy(amg_ctx *c, const amg_vec *x, const amg_vec *s, amg_vec *y)
+{
+   AMG_ARG(c && x && s && y && x->n == y->n && s->n == y->n, "amg_vec_ivaxpy: size mismatch");
+   amgk::vivaxpy(c->stream, x->d, s->d, y->d, 0, y->n);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_vec_scale(amg_ctx *c, double a, amg_vec *y)
+{
+   AMG_ARG(c && y, "amg_vec_scale: null argument");
+   amgk::vscale(c->stream, a, y->d, 0, y->n);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+int amg_reduce_to_host(amg_ctx *c, const double *partials, int np, int do_sqrt, double *out)
+{
+   amgk::reduce_partials(c->stream, partials, np, c->d_scalars, do_sqrt, c->d_scalars + 4096);
+   AMG_HIP(hipGetLastError());
+   AMG_HIP(hipMemcpyAsync(c->h_pinned, c->d_scalars, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   *out = c->h_pinned[0];
+   return AMG_OK;
+}
+
+extern "C" int amg_vec_norm2(amg_ctx *c, const amg_vec *x, double *out)
+{
+   AMG_ARG(c && x && out, "amg_vec_norm2: null argument");
+   double *p;
+   AMG_TRY(amg_ctx_partials(c, 1024, &p));
+   int np = 0;
+   amgk::sumsq_partials(c->stream, x->d, x->n, p, &np);
+   return amg_reduce_to_host(c, p, np, 1, out);
+}
+
+extern "C" int amg_vec_dot(amg_ctx *c, const amg_vec *x, const amg_vec *y, double *out)
+{
+   AMG_ARG(c && x && y && out && x->n == y->n, "amg_vec_dot: size mismatch");
+   double *p;
+   AMG_TRY(amg_ctx_partials(c, 1024, &p));
+   int np = 0;
+   amgk::dot_partials(c->stream, x->d, y->d, x->n, p, &np);
+   return amg_reduce_to_host(c, p, np, 0, out);
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+static int check_range(const amg_mat *A, int rb, int re)
+{
+   AMG_ARG(rb >= 0 && re <= A->nrows && rb <= re, "row range [%d,%d) outside [0,%d)", rb, re,
+           A->nrows);
+   return AMG_OK;
+}
+
+extern "C" int amg_matvec(amg_ctx *c, const amg_mat *A, const amg_vec *x, amg_vec *y, int rb, int re)
+{
+   AMG_ARG(c && A && x && y, "amg_matvec: null argument");
+   AMG_ARG(x->n >= A->ncols && y->n >= A->nrows, "amg_matvec: vector sizes %d/%d vs %dx%d", x->n,
+           y->n, A->nrows, A->ncols);
+   AMG_TRY(check_range(A, rb, re));
+   amgk::spgemv(c->stream, A, x->d, nullptr, amgk::gemv_mode(1.0, 0.0), y->d, rb, re, nullptr);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_matvec_timed(amg_ctx *c, const amg_mat *A, const amg_vec *x, amg_vec *y,
+                                int reps, double *ms)
+{
+   AMG_ARG(c && A && x && y && ms && reps >= 1, "amg_matvec_timed: bad argument");
+   AMG_ARG(x->n >= A->ncols && y->n >= A->nrows, "amg_matvec_timed: vector sizes");
+   hipEvent_t a, b;
+   AMG_HIP(hipEventCreate(&a));
+   AMG_HIP(hipEventCreate(&b));
+   const amgk::Gemv g = amgk::gemv_mode(1.0, 0.0);
+   AMG_HIP(hipEventRecord(a, c->stream));
+   for (int r = 0; r < reps; r++)
+      amgk::spgemv(c->stream, A, x->d, nullptr, g, y->d, 0, A->nrows, nullptr);
+   AMG_HIP(hipEventRecord(b, c->stream));
+   AMG_HIP(hipEventSynchronize(b));
+   float t = 0.f;
+   AMG_HIP(hipEventElapsedTime(&t, a, b));
+   hipEventDestroy(a);
+   hipEventDestroy(b);
+   *ms = (double)t / reps;
+   return AMG_OK;
+}
+
+extern "C" int amg_spgemv(amg_ctx *c, const amg_mat *A, const amg_vec *x, const amg_vec *b,
+                          double alpha, double beta, amg_vec *y, int rb, int re)
+{
+   AMG_ARG(c && A && x && y, "amg_spgemv: null argument");
+   AMG_ARG(x->n >= A->ncols && y->n >= A->nrows, "amg_spgemv: vector sizes");
+   AMG_TRY(check_range(A, rb, re));
+   amgk::Gemv g = amgk::gemv_mode(alpha, beta);
+   AMG_ARG(g.init == 0 || (b && b->n >= A->nrows), "amg_spgemv: b required when beta != 0");
+   amgk::spgemv(c->stream, A, x->d, b ? b->d : nullptr, g, y->d, rb, re, nullptr);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_residual(amg_ctx *c, const amg_mat *A, const amg_vec *b, const amg_vec *x,
+                            amg_vec *y, amg_vec *r, int rb, int re)
+{
+   AMG_ARG(c && A && b && x && y && r, "amg_residual: null argument");
+   AMG_TRY(check_range(A, rb, re));
+   // SMEM_Residual: y = A x over [rb,re), then r = b - y
+   amgk::spgemv(c->stream, A, x->d, nullptr, amgk::gemv_mode(1.0, 0.0), y->d, rb, re, nullptr);
+   amgk::vsub(c->stream, b->d, y->d, r->d, rb, re);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+static int build_transpose(amg_mat *A);
+
+extern "C" int amg_matvec_t(amg_ctx *c, const amg_mat *A, const amg_vec *x, amg_vec *y, int T)
+{
+   AMG_ARG(c && A && x && y, "amg_matvec_t: null argument");
+   AMG_ARG(x->n >= A->nrows && y->n >= A->ncols, "amg_matvec_t: vector sizes");
+   amg_mat *Am = const_cast<amg_mat *>(A);
+   if (!Am->trans) AMG_TRY(build_transpose(Am));
+   amgk::matvec_t_chunked(c->stream, Am->trans, x->d, y->d, A->nrows, T);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+// transpose on the host once (setup-time; rows of A^T list source rows ascending)
+static int build_transpose(amg_mat *A)
+{
+   amg_ctx *c = A->ctx;
+   std::vector<int> rp(A->nrows + 1), cj(A->nnz);
+   std::vector<double> cv(A->nnz);
+   AMG_TRY(amg_mat_download(c, A, rp.data(), cj.data(), cv.data()));
+   std::vector<int> trp(A->ncols + 1, 0), tcj(A->nnz);
+   std::vector<double> tcv(A->nnz);
+   for (long long k = 0; k < A->nnz; k++) trp[cj[k] + 1]++;
+   for (int i = 0; i < A->ncols; i++) trp[i + 1] += trp[i];
+   std::vector<int> pos(trp.begin(), trp.end());
+   for (int r = 0; r < A->nrows; r++)
+      for (int k = rp[r]; k < rp[r + 1]; k++) {
+         int col = cj[k];
+         tcj[pos[col]] = r;
+         tcv[pos[col]] = cv[k];
+         pos[col]++;
+      }
+   return amg_csr_register(c, A->ncols, A->nrows, A->nnz, trp.data(), tcj.data(), tcv.data(), 0,
+                           &A->trans);
+}
+
+extern "C" int amg_jacobi(amg_ctx *c, const amg_mat *A, const amg_vec *f, amg_vec *u,
+                          amg_vec *u_prev, double omega, int sweeps, int zero_first, int rb,
+                          int re, int variant)
+{
+   AMG_ARG(c && A && f && u && u_prev, "amg_jacobi: null argument");
+   AMG_TRY(check_range(A, rb, re));
+   for (int k = 0; k < sweeps; k++) {
+      if (k == 0 && zero_first == 1) {
+         amgk::jacobi_zero(c->stream, A->diag, f->d, nullptr, omega, u->d, rb, re, variant);
+      } else {
+         // u_prev = u; u = J(u_prev) (SMEM_Smooth.cpp:33-46)
+         amgk::vcopy(c->stream, u->d, u_prev->d, 0, u->n);
+         amgk::jacobi_sweep(c->stream, A, f->d, u_prev->d, nullptr, omega, u->d, rb, re);
+      }
+   }
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_l1_jacobi(amg_ctx *c, const amg_mat *A, const amg_vec *f, amg_vec *u,
+                             amg_vec *u_prev, const amg_vec *l1, int sweeps, int zero_first,
+                             int rb, int re, int variant)
+{
+   AMG_ARG(c && A && f && u && u_prev && l1, "amg_l1_jacobi: null argument");
+   AMG_TRY(check_range(A, rb, re));
+   for (int k = 0; k < sweeps; k++) {
+      if (k == 0 && zero_first == 1) {
+         amgk::jacobi_zero(c->stream, A->diag, f->d, l1->d, 1.0, u->d, rb, re, variant);
+      } else {
+         amgk::vcopy(c->stream, u->d, u_prev->d, 0, u->n);
+         amgk::jacobi_sweep(c->stream, A, f->d, u_prev->d, l1->d, 1.0, u->d, rb, re);
+      }
+   }
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+int amg_hybrid_jgs_dev(amg_ctx *c, hipStream_t s, const amg_mat *A, const double *f, double *u,
+                       double *u_prev, int n_vec, const int *d_blk, int nblk, int blk_lo,
+                       int blk_hi, const double *ds, double weight, int sweeps, int zero_first,
+                       int reverse)
+{
+   for (int k = 0; k < sweeps; k++) {
+      const int zero = (k == 0 && zero_first == 1);
+      if (!zero) amgk::vcopy(s, u, u_prev, blk_lo, blk_hi);
+      amgk::hybrid_jgs(s, A, f, u, u_prev, d_blk, nblk, ds, weight, zero, reverse);
+   }
+   (void)n_vec;
+   (void)c;
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_hybrid_jgs(amg_ctx *c, const amg_mat *A, const amg_vec *f, amg_vec *u,
+                              amg_vec *u_prev, const int *blk, int nblk, const amg_vec *diag_scale,
+                              double weight, int sweeps, int zero_first, int reverse)
+{
+   AMG_ARG(c && A && f && u && u_prev && blk && nblk > 0, "amg_hybrid_jgs: null argument");
+   for (int b = 0; b < nblk; b++)
+      AMG_ARG(blk[b] <= blk[b + 1] && blk[b] >= 0 && blk[b + 1] <= A->nrows,
+              "amg_hybrid_jgs: bad block %d [%d,%d)", b, blk[b], blk[b + 1]);
+   int *d_blk = nullptr;
+   AMG_HIP(hipMallocAsync((void **)&d_blk, (nblk + 1) * sizeof(int), c->stream));
+   AMG_HIP(hipMemcpyAsync(d_blk, blk, (nblk + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream));
+   int s = amg_hybrid_jgs_dev(c, c->stream, A, f->d, u->d, u_prev->d, u->n, d_blk, nblk, blk[0],
+                              blk[nblk], diag_scale ? diag_scale->d : nullptr, weight, sweeps,
+                              zero_first, reverse);
+   AMG_HIP(hipFreeAsync(d_blk, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   return s;
+}
+
+extern "C" int amg_gauss_seidel(amg_ctx *c, const amg_mat *A, const amg_vec *f, amg_vec *u,
+                                int sweeps)
+{
+   AMG_ARG(c && A && f && u, "amg_gauss_seidel: null argument");
+   // SEQ_GaussSeidel == one hybrid block covering every row (no out-of-block terms)
+   int blk[2] = {0, A->nrows};
+   return amg_hybrid_jgs(c, A, f, u, u, blk, 1, nullptr, 1.0, sweeps, 0, 0);
+}
+
+int amg_sym_jacobi_dev(hipStream_t s, const amg_mat *A, const double *f, double *u, double *y,
+                       double *r, double omega, const double *l1, int sweeps, int zero_first,
+                       int rb, int re, int variant)
+{
+   const int seq = (variant == 1);
+   amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   int k = 0;
+   if (seq || zero_first == 1) {
+      amgk::vcopy(s, f, r, rb, re);
+   } else {
+      amgk::spgemv(s, A, u, nullptr, mv, y, rb, re, nullptr);
+      amgk::vsub(s, f, y, r, rb, re);
+   }
+   while (true) {
+      amgk::sym_scale(s, A->diag, l1, omega, r, rb, re, seq);
+      amgk::spgemv(s, A, r, nullptr, mv, y, rb, re, nullptr);
+      amgk::sym_update(s, A->diag, l1, omega, r, y, u, rb, re, seq, (!seq && zero_first == 1));
+      k++;
+      if (k == sweeps) break;
+      amgk::spgemv(s, A, u, nullptr, mv, y, rb, re, nullptr);
+      amgk::vsub(s, f, y, r, rb, re);
+   }
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_sym_jacobi(amg_ctx *c, const amg_mat *A, const amg_vec *f, amg_vec *u,
+                              amg_vec *y, amg_vec *r, double omega, const amg_vec *l1, int sweeps,
+                              int zero_first, int rb, int re, int variant)
+{
+   AMG_ARG(c && A && f && u && y && r && sweeps >= 1, "amg_sym_jacobi: bad argument");
+   AMG_TRY(check_range(A, rb, re));
+   return amg_sym_jacobi_dev(c->stream, A, f->d, u->d, y->d, r->d, omega, l1 ? l1->d : nullptr,
+                             sweeps, zero_first, rb, re, variant);
+}
+
+extern "C" int amg_l1_norms(amg_ctx *c, const amg_mat *A, amg_vec *out)
+{
+   AMG_ARG(c && A && out && out->n >= A->nrows, "amg_l1_norms: bad argument");
+   amgk::l1_norms(c->stream, A, out->d);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_a_diag(amg_ctx *c, const amg_mat *A, double omega, amg_vec *out)
+{
+   AMG_ARG(c && A && out && out->n >= A->nrows, "amg_a_diag: bad argument");
+   amgk::a_diag(c->stream, A->diag, omega, out->d, A->nrows);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}

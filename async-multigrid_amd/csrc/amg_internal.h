@@ -1,0 +1,148 @@
+// amg_internal.h -- shared internals of libamg_mi355x (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "amg_mi355x.h"
+
+// ---------------------------------------------------------------------------
+// error plumbing: every C-ABI entry returns AMG_OK or a negative status and
+// leaves a thread-local message for amg_last_error().
+// ---------------------------------------------------------------------------
+int amg_set_error(int code, const char *fmt, ...);
+
+#define AMG_HIP(call)                                                                      \
+   do {                                                                                    \
+      hipError_t _e = (call);                                                              \
+      if (_e != hipSuccess)                                                                \
+         return amg_set_error(AMG_ERR_HIP, "%s:%d %s -> %s", __FILE__, __LINE__, #call,   \
+                              hipGetErrorString(_e));                                      \
+   } while (0)
+
+#define AMG_TRY(call)                                                                      \
+   do {                                                                                    \
+      int _s = (call);                                                                     \
+      if (_s != AMG_OK) return _s;                                                         \
+   } while (0)
+
+#define AMG_ARG(cond, ...)                                                                 \
+   do {                                                                                    \
+      if (!(cond)) return amg_set_error(AMG_ERR_ARG, __VA_ARGS__);                         \
+   } while (0)
+
+// rows handled by one workgroup of the CSR tile kernels (one row per lane)
+constexpr int AMG_TILE_ROWS = 256;
+// products staged per LDS chunk in the CSR tile kernels (16 KiB of fp64)
+constexpr int AMG_CHUNK = 2048;
+// device arrays of col/val are padded so 16-byte vector loads past nnz stay in bounds
+constexpr int AMG_NNZ_PAD = 8;
+
+struct amg_ctx {
+   int device = 0;
+   hipStream_t stream = nullptr;           // compute stream (all sync work)
+   std::vector<hipStream_t> level_streams; // async additive: one per level
+   hipStream_t comm_stream = nullptr;      // halo exchange (distributed)
+   double *d_partials = nullptr;           // per-workgroup partial sums
+   size_t partials_cap = 0;
+   double *d_scalars = nullptr;            // device scalars (norms, dots)
+   double *h_pinned = nullptr;             // pinned host mirror of scalars
+   int num_cus = 256;
+};
+
+struct amg_mat {
+   amg_ctx *ctx = nullptr;
+   int nrows = 0, ncols = 0;
+   long long nnz = 0;
+   int *rowptr = nullptr;
+   int *col = nullptr;
+   double *val = nullptr;
+   double *diag = nullptr; // val[rowptr[i]] (the reference's a_ii), or 0 for empty rows
+   int diag_first = 1;
+   amg_mat *trans = nullptr; // lazily built transpose for amg_matvec_t
+};
+
+struct amg_vec {
+   amg_ctx *ctx = nullptr;
+   int n = 0;
+   double *d = nullptr;
+   bool owns = true;
+};
+
+// workspace
+int amg_ctx_partials(amg_ctx *ctx, size_t n, double **out);
+
+// ---------------------------------------------------------------------------
+// kernel launchers (amg_kernels.hip); all asynchronous on stream s
+// ---------------------------------------------------------------------------
+namespace amgk {
+
+// SMEM_SpGEMV branch selection (SMEM_MatVec.cpp:140-258)
+struct Gemv {
+   int init;     // 0: 0.0, 1: b, 2: -b, 3: b*temp, 4: -b*temp
+   int negacc;   // 1: tempx -= a*x ; 0: tempx += a*x
+   int scale;    // 1: y = alpha*tempx
+   double alpha, temp;
+};
+Gemv gemv_mode(double alpha, double beta);
+
+// y[rb,re) per the Gemv mode; if partials != nullptr also writes per-workgroup
+// sum of y_i^2 to partials[0..nblocks) (fixed order)
+void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, const Gemv &g,
+            double *y, int rb, int re, double *partials);
+int tile_blocks(int rb, int re);
+
+// Jacobi sweep out[i] = x[i] + (omega*(f_i - sum a_ij x_j))/a_ii  (a_ii != 0)
+//   l1 != nullptr: out[i] = x[i] + (f_i - sum)/l1[i]   (no a_ii test)
+void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double *x,
+                  const double *l1, double omega, double *out, int rb, int re);
+// zero-guess sweep: variant 0 (SMEM) u = omega*f/a (a != 0) | u = f/l1
+//                   variant 1 (SEQ)  u += omega*f/a (a != 0) | u += f/l1 (a != 0)
+void jacobi_zero(hipStream_t s, const double *diag, const double *f, const double *l1,
+                 double omega, double *u, int rb, int re, int variant);
+// u_new = u + (omega*r)/a (a != 0): Jacobi sweep from a precomputed residual
+void jacobi_from_residual(hipStream_t s, const double *diag, const double *r, const double *l1,
+                          double omega, double *u, int rb, int re);
+// hybrid JGS: one lane per block, blocks d_blk[0..nblk] (device), in place on u
+void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
+                const int *d_blk, int nblk, const double *diag_scale, double weight, int zero,
+                int reverse);
+// transpose-product with the expansion-buffer order of T static chunks
+void matvec_t_chunked(hipStream_t s, const amg_mat *AT, const double *x, double *y, int n_src,
+                      int T);
+
+// vector kernels
+void vcopy(hipStream_t s, const double *x, double *y, int rb, int re);
+void vset(hipStream_t s, double *y, double a, int rb, int re);
+void vaxpy(hipStream_t s, double a, const double *x, double *y, int rb, int re);
+void vivaxpy(hipStream_t s, const double *x, const double *sc, double *y, int rb, int re);
+void vscale(hipStream_t s, double a, double *y, int rb, int re);
+void vsub(hipStream_t s, const double *b, const double *y, double *r, int rb, int re); // r = b - y
+void vadd_into(hipStream_t s, const double *r, double *u, int rb, int re, int overwrite);
+void l1_norms(hipStream_t s, const amg_mat *A, double *out);
+void a_diag(hipStream_t s, const double *diag, double omega, double *out, int n);
+void extract_diag(hipStream_t s, const amg_mat *A);
+// symmetric Jacobi pieces (SMEM_Smooth.cpp:665,682-683 / SEQ_Smooth.cpp:136,144-145)
+void sym_scale(hipStream_t s, const double *diag, const double *l1, double omega, double *r,
+               int rb, int re, int seq);
+void sym_update(hipStream_t s, const double *diag, const double *l1, double omega, double *r,
+                const double *y, double *u, int rb, int re, int seq, int overwrite);
+// Chebyshev outer update SMEM_Solve.cpp:179-186
+void cheby_update(hipStream_t s, double *u, double *u_outer, double *y_outer, double omega,
+                  double delta, int n);
+// atomic correction: u += e (device-scope fp64 atomics), u_priv = value after the add
+void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n);
+
+// deterministic reductions
+void sumsq_partials(hipStream_t s, const double *x, int n, double *partials, int *nparts);
+void dot_partials(hipStream_t s, const double *x, const double *y, int n, double *partials,
+                  int *nparts);
+// out[0] = sum(partials[0..np)) in fixed order; if do_sqrt, out[0] = sqrt(sum)
+void reduce_partials(hipStream_t s, const double *partials, int np, double *out, int do_sqrt,
+                     double *scratch);
+
+} // namespace amgk

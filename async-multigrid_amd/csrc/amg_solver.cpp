@@ -1,0 +1,762 @@
+// amg_solver.cpp -- host-side orchestration on the device: the level
+// hierarchy (AllData analogue), the synchronous multiplicative V-cycle
+// (SMEM_Sync_Parfor_Vcycle), the synchronous additive cycle
+// (SMEM_Sync_Add_Vcycle), the SMEM_Solve outer loop with the Chebyshev
+// update, and the asynchronous additive solver (SMEM_Async_Add_AMG) with one
+// HIP stream per level.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <utility>
+#include <vector>
+
+#include "amg_internal.h"
+
+int amg_reduce_to_host(amg_ctx *c, const double *partials, int np, int do_sqrt, double *out);
+int amg_hybrid_jgs_dev(amg_ctx *c, hipStream_t s, const amg_mat *A, const double *f, double *u,
+                       double *u_prev, int n_vec, const int *d_blk, int nblk, int blk_lo,
+                       int blk_hi, const double *ds, double weight, int sweeps, int zero_first,
+                       int reverse);
+int amg_sym_jacobi_dev(hipStream_t s, const amg_mat *A, const double *f, double *u, double *y,
+                       double *r, double omega, const double *l1, int sweeps, int zero_first,
+                       int rb, int re, int variant);
+
+namespace {
+
+enum ProfCat { PROF_FINE_SPMV = 0, PROF_FINE_SMOOTH = 1, PROF_RESTRICT0 = 2, PROF_PROLONG0 = 3,
+               PROF_NCAT = 4 };
+
+struct Level {
+   amg_mat *A = nullptr, *P = nullptr, *R = nullptr;
+   int n = 0;
+   double *f = nullptr, *u = nullptr, *u_alt = nullptr, *u_prev = nullptr, *y = nullptr,
+          *r_fine = nullptr;
+   double *l1 = nullptr, *adiag = nullptr;
+   std::vector<int> blk;
+   int *d_blk = nullptr;
+   int zero_flag = 0;
+};
+
+// per-level private vectors of the additive cycles (level_vector[k], SMEM_Setup.cpp:292-341)
+struct AddLevel {
+   std::vector<double *> r, e; // r[l], e[l] for l <= min(k+1, L-1)
+   double *u_prev = nullptr, *y = nullptr, *u_priv = nullptr, *y_fine = nullptr, *scratch = nullptr;
+   double *u_fine = nullptr, *u_coarse = nullptr, *u_coarse_prev = nullptr, *u_fine_prev = nullptr,
+          *r_fine = nullptr;
+};
+
+} // namespace
+
+struct amg_hier {
+   amg_ctx *ctx = nullptr;
+   int L = 0;
+   amg_opts o{};
+   std::vector<Level> lv;
+   std::vector<AddLevel> al;
+   double *r0 = nullptr; // vector.r[0]: the outer residual
+   double *u_outer = nullptr, *y_outer = nullptr;
+   double *d_hist = nullptr; // device residual-norm history
+   int hist_cap = 0;
+   double r0norm = 0.0;
+   double cheby_omega = 2.0;
+   int iter = 0;
+   bool have_state = false;
+   std::vector<void *> allocs;
+   // profiling
+   std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[PROF_NCAT];
+   double prof_ms[PROF_NCAT] = {0, 0, 0, 0};
+   long long prof_n[PROF_NCAT] = {0, 0, 0, 0};
+};
+
+static int dalloc(amg_hier *H, size_t n, double **p)
+{
+   hipError_t e = hipMalloc(p, std::max<size_t>(n, 1) * sizeof(double));
+   if (e != hipSuccess)
+      return amg_set_error(AMG_ERR_OOM, "amg_hier: allocation of %zu doubles: %s", n,
+                           hipGetErrorString(e));
+   H->allocs.push_back(*p);
+   e = hipMemsetAsync(*p, 0, std::max<size_t>(n, 1) * sizeof(double), H->ctx->stream);
+   if (e != hipSuccess) return amg_set_error(AMG_ERR_HIP, "memset: %s", hipGetErrorString(e));
+   return AMG_OK;
+}
+
+static bool is_all_levels(const amg_opts &o)
+{
+   return !(o.solver == AMG_MULT);
+}
+
+static bool is_multadd(const amg_opts &o)
+{
+   return o.solver == AMG_MULTADD || o.solver == AMG_ASYNC_MULTADD;
+}
+
+// ---- profiling helpers -----------------------------------------------------
+struct ProfScope {
+   amg_hier *H;
+   int cat;
+   hipStream_t s;
+   hipEvent_t a = nullptr, b = nullptr;
+   bool on;
+   ProfScope(amg_hier *H_, int cat_, hipStream_t s_, bool enabled = true)
+      : H(H_), cat(cat_), s(s_), on(enabled && H_->o.profile)
+   {
+      if (on) {
+         hipEventCreate(&a);
+         hipEventCreate(&b);
+         hipEventRecord(a, s);
+      }
+   }
+   ~ProfScope()
+   {
+      if (on) {
+         hipEventRecord(b, s);
+         H->pend[cat].push_back({a, b});
+      }
+   }
+};
+
+static void prof_drain(amg_hier *H)
+{
+   for (int c = 0; c < PROF_NCAT; c++) {
+      for (auto &p : H->pend[c]) {
+         float ms = 0.f;
+         hipEventSynchronize(p.second);
+         if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
+            H->prof_ms[c] += ms;
+            H->prof_n[c] += 1;
+         }
+         hipEventDestroy(p.first);
+         hipEventDestroy(p.second);
+      }
+      H->pend[c].clear();
+   }
+}
+
+extern "C" int amg_hier_profile_read(amg_hier *H, double *ms, long long *launches, int reset)
+{
+   AMG_ARG(H, "amg_hier_profile_read: null hierarchy");
+   AMG_HIP(hipStreamSynchronize(H->ctx->stream));
+   prof_drain(H);
+   for (int c = 0; c < PROF_NCAT; c++) {
+      if (ms) ms[c] = H->prof_ms[c];
+      if (launches) launches[c] = H->prof_n[c];
+      if (reset) {
+         H->prof_ms[c] = 0;
+         H->prof_n[c] = 0;
+      }
+   }
+   return AMG_OK;
+}
+
+// ---- block partitions --------------------------------------------------------
+static void partition_equal(int n, int T, std::vector<int> &blk)
+{
+   // SMEM_Setup.cpp:1018-1030
+   blk.assign(T + 1, 0);
+   int size = n / T, rest = n - size * T;
+   for (int t = 0; t < T; t++) blk[t] = (t < rest) ? t * size + t : t * size + rest;
+   blk[T] = n;
+}
+
+static int upload_blocks(amg_hier *H, Level &l)
+{
+   if (l.d_blk) {
+      hipFree(l.d_blk);
+      l.d_blk = nullptr;
+   }
+   AMG_HIP(hipMalloc(&l.d_blk, l.blk.size() * sizeof(int)));
+   AMG_HIP(hipMemcpyAsync(l.d_blk, l.blk.data(), l.blk.size() * sizeof(int), hipMemcpyHostToDevice,
+                          H->ctx->stream));
+   AMG_HIP(hipStreamSynchronize(H->ctx->stream));
+   return AMG_OK;
+}
+
+static int default_blocks(amg_hier *H, Level &l)
+{
+   if (H->o.num_threads > 0) {
+      partition_equal(l.n, H->o.num_threads, l.blk);
+   } else {
+      const int B = std::max(1, H->o.jgs_block_rows);
+      const int nb = std::max(1, (l.n + B - 1) / B);
+      l.blk.resize(nb + 1);
+      for (int b = 0; b <= nb; b++) l.blk[b] = std::min(l.n, b * B);
+   }
+   return upload_blocks(H, l);
+}
+
+extern "C" int amg_hier_set_blocks(amg_hier *H, int level, const int *blk, int nblk)
+{
+   AMG_ARG(H && blk && level >= 0 && level < H->L && nblk > 0, "amg_hier_set_blocks: bad argument");
+   Level &l = H->lv[level];
+   AMG_ARG(blk[0] == 0 && blk[nblk] == l.n, "amg_hier_set_blocks: blocks must cover [0,%d)", l.n);
+   for (int b = 0; b < nblk; b++) AMG_ARG(blk[b] <= blk[b + 1], "amg_hier_set_blocks: unsorted");
+   l.blk.assign(blk, blk + nblk + 1);
+   return upload_blocks(H, l);
+}
+
+// ---- creation ----------------------------------------------------------------
+static int hier_prepare_smoother_arrays(amg_hier *H)
+{
+   hipStream_t s = H->ctx->stream;
+   for (int l = 0; l < H->L; l++) {
+      Level &v = H->lv[l];
+      amgk::l1_norms(s, v.A, v.l1);
+      amgk::a_diag(s, v.A->diag, H->o.smooth_weight, v.adiag, v.n);
+   }
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_hier_create(amg_ctx *c, int L, amg_mat *const *A, amg_mat *const *P,
+                               amg_mat *const *R, const amg_opts *opts, amg_hier **out)
+{
+   AMG_ARG(c && A && out && L >= 1 && opts, "amg_hier_create: bad argument");
+   AMG_ARG(L == 1 || (P && R), "amg_hier_create: P and R required for L > 1");
+   for (int l = 0; l < L; l++) {
+      AMG_ARG(A[l] && A[l]->nrows == A[l]->ncols, "amg_hier_create: A[%d] must be square", l);
+      if (l < L - 1) {
+         AMG_ARG(P[l] && R[l], "amg_hier_create: P/R[%d] missing", l);
+         AMG_ARG(P[l]->nrows == A[l]->nrows && P[l]->ncols == A[l + 1]->nrows,
+                 "amg_hier_create: P[%d] is %dx%d, expected %dx%d", l, P[l]->nrows, P[l]->ncols,
+                 A[l]->nrows, A[l + 1]->nrows);
+         AMG_ARG(R[l]->nrows == A[l + 1]->nrows && R[l]->ncols == A[l]->nrows,
+                 "amg_hier_create: R[%d] is %dx%d", l, R[l]->nrows, R[l]->ncols);
+      }
+   }
+   amg_hier *H = new amg_hier();
+   H->ctx = c;
+   H->L = L;
+   H->o = *opts;
+   H->lv.resize(L);
+   for (int l = 0; l < L; l++) {
+      Level &v = H->lv[l];
+      v.A = A[l];
+      v.P = (l < L - 1) ? P[l] : nullptr;
+      v.R = (l < L - 1) ? R[l] : nullptr;
+      v.n = A[l]->nrows;
+      AMG_TRY(dalloc(H, v.n, &v.f));
+      AMG_TRY(dalloc(H, v.n, &v.u));
+      AMG_TRY(dalloc(H, v.n, &v.u_alt));
+      AMG_TRY(dalloc(H, v.n, &v.u_prev));
+      AMG_TRY(dalloc(H, v.n, &v.y));
+      AMG_TRY(dalloc(H, v.n, &v.r_fine));
+      AMG_TRY(dalloc(H, v.n, &v.l1));
+      AMG_TRY(dalloc(H, v.n, &v.adiag));
+      AMG_TRY(default_blocks(H, v));
+   }
+   AMG_TRY(dalloc(H, H->lv[0].n, &H->r0));
+   AMG_TRY(dalloc(H, H->lv[0].n, &H->u_outer));
+   AMG_TRY(dalloc(H, H->lv[0].n, &H->y_outer));
+   H->hist_cap = 1 << 16;
+   AMG_TRY(dalloc(H, H->hist_cap, &H->d_hist));
+   if (is_all_levels(H->o)) {
+      H->al.resize(L);
+      const int n0 = H->lv[0].n;
+      for (int k = 0; k < L; k++) {
+         AddLevel &a = H->al[k];
+         const int top = std::min(k + 1, L - 1);
+         a.r.assign(L, nullptr);
+         a.e.assign(L, nullptr);
+         for (int l = 0; l <= top; l++) {
+            AMG_TRY(dalloc(H, H->lv[l].n, &a.r[l]));
+            AMG_TRY(dalloc(H, H->lv[l].n, &a.e[l]));
+         }
+         const int nk = H->lv[k].n;
+         AMG_TRY(dalloc(H, std::max(nk, n0), &a.u_prev));
+         AMG_TRY(dalloc(H, std::max(nk, n0), &a.y));
+         AMG_TRY(dalloc(H, n0, &a.u_priv));
+         AMG_TRY(dalloc(H, n0, &a.y_fine));
+         AMG_TRY(dalloc(H, std::max(nk, n0), &a.scratch));
+         AMG_TRY(dalloc(H, nk, &a.u_fine));
+         AMG_TRY(dalloc(H, nk, &a.u_fine_prev));
+         AMG_TRY(dalloc(H, nk, &a.r_fine));
+         const int nc = H->lv[top].n;
+         AMG_TRY(dalloc(H, nc, &a.u_coarse));
+         AMG_TRY(dalloc(H, nc, &a.u_coarse_prev));
+      }
+   }
+   AMG_TRY(hier_prepare_smoother_arrays(H));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   *out = H;
+   return AMG_OK;
+}
+
+extern "C" int amg_hier_free(amg_hier *H)
+{
+   if (!H) return AMG_OK;
+   hipStreamSynchronize(H->ctx->stream);
+   for (auto s : H->ctx->level_streams) hipStreamSynchronize(s);
+   prof_drain(H);
+   for (void *p : H->allocs) hipFree(p);
+   for (auto &l : H->lv) hipFree(l.d_blk);
+   delete H;
+   return AMG_OK;
+}
+
+extern "C" int amg_hier_set_opts(amg_hier *H, const amg_opts *opts)
+{
+   AMG_ARG(H && opts, "amg_hier_set_opts: null argument");
+   AMG_ARG(is_all_levels(*opts) == is_all_levels(H->o),
+           "amg_hier_set_opts: cannot switch between ONE_LEVEL and ALL_LEVELS solvers");
+   const bool w = opts->smooth_weight != H->o.smooth_weight;
+   const bool t = opts->num_threads != H->o.num_threads || opts->jgs_block_rows != H->o.jgs_block_rows;
+   H->o = *opts;
+   if (w) AMG_TRY(hier_prepare_smoother_arrays(H));
+   if (t)
+      for (auto &l : H->lv) AMG_TRY(default_blocks(H, l));
+   return AMG_OK;
+}
+
+extern "C" int amg_hier_vec(amg_hier *H, int which, int level, amg_vec **out)
+{
+   AMG_ARG(H && out && level >= 0 && level < H->L, "amg_hier_vec: bad argument");
+   amg_vec *v = new amg_vec();
+   v->ctx = H->ctx;
+   v->n = H->lv[level].n;
+   v->owns = false;
+   switch (which) {
+   case AMG_VEC_F: v->d = H->lv[level].f; break;
+   case AMG_VEC_U: v->d = H->lv[level].u; break;
+   case AMG_VEC_R: v->d = level == 0 ? H->r0 : H->lv[level].r_fine; break;
+   default: delete v; return amg_set_error(AMG_ERR_ARG, "amg_hier_vec: unknown vector %d", which);
+   }
+   *out = v;
+   return AMG_OK;
+}
+
+// ---- smoothing (SMEM_Smooth dispatcher, SMEM_Solve.cpp:264-377) --------------
+// ONE_LEVEL (MULT) smoothing of level l's f/u; may swap u <-> u_alt.
+static void smooth_one_level(amg_hier *H, hipStream_t s, int l, const double *f, int sweeps,
+                             bool from_outer_residual)
+{
+   Level &v = H->lv[l];
+   const amg_opts &o = H->o;
+   const int zf = v.zero_flag;
+   const bool prof = (l == 0);
+   if (o.smoother == AMG_HYBRID_JACOBI_GAUSS_SEIDEL ||
+       o.smoother == AMG_L1_HYBRID_JACOBI_GAUSS_SEIDEL) {
+      const double *ds = (o.smoother == AMG_L1_HYBRID_JACOBI_GAUSS_SEIDEL) ? v.l1 : v.adiag;
+      ProfScope ps(H, PROF_FINE_SMOOTH, s, prof);
+      amg_hybrid_jgs_dev(H->ctx, s, v.A, f, v.u, v.u_prev, v.n, v.d_blk, (int)v.blk.size() - 1, 0,
+                         v.n, ds, 1.0, sweeps, zf, 0);
+      return;
+   }
+   const bool l1 = (o.smoother == AMG_L1_JACOBI);
+   for (int k = 0; k < sweeps; k++) {
+      if (k == 0 && zf == 1) {
+         amgk::jacobi_zero(s, v.A->diag, f, l1 ? v.l1 : nullptr, o.smooth_weight, v.u, 0, v.n, 0);
+      } else if (k == 0 && from_outer_residual) {
+         // r0 = f - A u was computed by the outer loop on this very u with the
+         // same summation order; the sweep is u += w r / a (bit-identical)
+         amgk::jacobi_from_residual(s, v.A->diag, H->r0, l1 ? v.l1 : nullptr, o.smooth_weight,
+                                    v.u, 0, v.n);
+      } else {
+         {
+            ProfScope ps(H, PROF_FINE_SMOOTH, s, prof);
+            amgk::jacobi_sweep(s, v.A, f, v.u, l1 ? v.l1 : nullptr, o.smooth_weight, v.u_alt, 0, v.n);
+         }
+         std::swap(v.u, v.u_alt);
+      }
+   }
+}
+
+// ALL_LEVELS smoothing of A[Alevel] with f -> u (row range version of the
+// smoothers), zero flag of `flag_level`
+static void smooth_all_levels(amg_hier *H, hipStream_t s, int Alevel, const double *f, double *u,
+                              double *u_prev, double *y, double *r, int sweeps, int flag_level)
+{
+   Level &v = H->lv[Alevel];
+   const amg_opts &o = H->o;
+   const int zf = H->lv[flag_level].zero_flag;
+   const bool sym = is_multadd(o) && o.num_post_smooth_sweeps > 0 && o.num_pre_smooth_sweeps > 0;
+   if (o.smoother == AMG_HYBRID_JACOBI_GAUSS_SEIDEL) {
+      amg_hybrid_jgs_dev(H->ctx, s, v.A, f, u, u_prev, v.n, v.d_blk, (int)v.blk.size() - 1, 0, v.n,
+                         nullptr, 1.0, sweeps, zf, 0);
+   } else if (o.smoother == AMG_L1_JACOBI) {
+      if (sym) {
+         amg_sym_jacobi_dev(s, v.A, f, u, y, r, 1.0, v.l1, sweeps, zf, 0, v.n, 0);
+      } else {
+         for (int k = 0; k < sweeps; k++) {
+            if (k == 0 && zf == 1) {
+               amgk::jacobi_zero(s, v.A->diag, f, v.l1, 1.0, u, 0, v.n, 0);
+            } else {
+               amgk::vcopy(s, u, u_prev, 0, v.n);
+               amgk::jacobi_sweep(s, v.A, f, u_prev, v.l1, 1.0, u, 0, v.n);
+            }
+         }
+      }
+   } else {
+      if (sym) {
+         amg_sym_jacobi_dev(s, v.A, f, u, y, r, o.smooth_weight, nullptr, sweeps, zf, 0, v.n, 0);
+      } else {
+         for (int k = 0; k < sweeps; k++) {
+            if (k == 0 && zf == 1) {
+               amgk::jacobi_zero(s, v.A->diag, f, nullptr, o.smooth_weight, u, 0, v.n, 0);
+            } else {
+               amgk::vcopy(s, u, u_prev, 0, v.n);
+               amgk::jacobi_sweep(s, v.A, f, u_prev, nullptr, o.smooth_weight, u, 0, v.n);
+            }
+         }
+      }
+   }
+}
+
+// ---- SMEM_Sync_Parfor_Vcycle (SMEM_Sync_AMG.cpp:8-145) -------------------------
+static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
+{
+   hipStream_t s = H->ctx->stream;
+   const amg_opts &o = H->o;
+   const int L = H->L;
+   const amgk::Gemv res_mode = amgk::gemv_mode(-1.0, 1.0);
+   const amgk::Gemv mv_mode = amgk::gemv_mode(1.0, 0.0);
+   const amgk::Gemv pro_mode = amgk::gemv_mode(1.0, 1.0);
+   for (int l = 0; l < L - 1; l++) {
+      Level &v = H->lv[l];
+      v.zero_flag = 1;
+      if (l == 0 && !precond) v.zero_flag = 0;
+      const double *f_fine = (l == 0 && precond) ? H->r0 : v.f;
+      smooth_one_level(H, s, l, f_fine, o.num_pre_smooth_sweeps, l == 0 && reuse_r0);
+      {
+         ProfScope ps(H, PROF_FINE_SPMV, s, l == 0);
+         amgk::spgemv(s, v.A, v.u, f_fine, res_mode, v.r_fine, 0, v.n, nullptr);
+      }
+      {
+         ProfScope ps(H, PROF_RESTRICT0, s, l == 0);
+         amgk::spgemv(s, v.R, v.r_fine, nullptr, mv_mode, H->lv[l + 1].f, 0, H->lv[l + 1].n,
+                      nullptr);
+      }
+   }
+   Level &c = H->lv[L - 1];
+   smooth_one_level(H, s, L - 1, c.f, o.num_pre_smooth_sweeps + o.num_post_smooth_sweeps, false);
+   for (int l = L - 2; l >= 0; l--) {
+      Level &v = H->lv[l];
+      v.zero_flag = 0;
+      {
+         ProfScope ps(H, PROF_PROLONG0, s, l == 0);
+         amgk::spgemv(s, v.P, H->lv[l + 1].u, v.u, pro_mode, v.u, 0, v.n, nullptr);
+      }
+      const double *f_fine = (l == 0 && precond) ? H->r0 : v.f;
+      smooth_one_level(H, s, l, f_fine, o.num_post_smooth_sweeps, false);
+   }
+}
+
+// ---- SMEM_Sync_Add_Vcycle (SMEM_Sync_AMG.cpp:408-621), res_compute LOCAL ------
+// The level corrections are accumulated into u in level order.
+static void add_level_correction(amg_hier *H, hipStream_t s, int k, const double *r_fine0)
+{
+   const int L = H->L;
+   const amg_opts &o = H->o;
+   const bool multadd = is_multadd(o);
+   AddLevel &a = H->al[k];
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   H->lv[k].zero_flag = 1;
+   const int coarsest = multadd ? k : k + 1;
+   amgk::vcopy(s, r_fine0, a.r[0], 0, H->lv[0].n);
+   for (int l = 0; l < coarsest; l++)
+      if (l < L - 1)
+         amgk::spgemv(s, H->lv[l].R, a.r[l], nullptr, mv, a.r[l + 1], 0, H->lv[l + 1].n, nullptr);
+   if (k == L - 1) {
+      // hypre_GaussElimSolve writes hypre's U_array, never read back by the
+      // reference's cycle: the coarsest correction e[k] keeps its zero value
+   } else if (multadd) {
+      amgk::vset(s, a.e[k], 0.0, 0, H->lv[k].n);
+      smooth_all_levels(H, s, k, a.r[k], a.e[k], a.u_prev, a.y, a.scratch, o.num_fine_smooth_sweeps, k);
+   } else {
+      const int fg = k, cg = k + 1;
+      amgk::vset(s, a.u_fine, 0.0, 0, H->lv[fg].n);
+      amgk::vset(s, a.u_coarse, 0.0, 0, H->lv[cg].n);
+      smooth_all_levels(H, s, cg, a.r[cg], a.u_coarse, a.u_coarse_prev, a.y, a.scratch,
+                        o.num_coarse_smooth_sweeps, k);
+      amgk::spgemv(s, H->lv[fg].P, a.u_coarse, nullptr, mv, a.e[fg], 0, H->lv[fg].n, nullptr);
+      // SMEM_Residual: y = A e; r_fine = r - y
+      amgk::spgemv(s, H->lv[fg].A, a.e[fg], nullptr, mv, a.y, 0, H->lv[fg].n, nullptr);
+      amgk::vsub(s, a.r[fg], a.y, a.r_fine, 0, H->lv[fg].n);
+      smooth_all_levels(H, s, fg, a.r_fine, a.u_fine, a.u_fine_prev, a.y, a.scratch,
+                        o.num_fine_smooth_sweeps, k);
+      amgk::vcopy(s, a.u_fine, a.e[k], 0, H->lv[k].n);
+   }
+   for (int l = k - 1; l >= 0; l--)
+      amgk::spgemv(s, H->lv[l].P, a.e[l + 1], nullptr, mv, a.e[l], 0, H->lv[l].n, nullptr);
+}
+
+static void sync_add_vcycle(amg_hier *H)
+{
+   hipStream_t s = H->ctx->stream;
+   for (int k = 0; k < H->L; k++) {
+      add_level_correction(H, s, k, H->r0);
+      if (k < H->L - 1) amgk::vaxpy(s, 1.0, H->al[k].e[0], H->lv[0].u, 0, H->lv[0].n);
+   }
+}
+
+// ---- SMEM_Solve (SMEM_Solve.cpp:11-262, synchronous branch) --------------------
+static int outer_residual(amg_hier *H, int slot)
+{
+   amg_ctx *c = H->ctx;
+   Level &v = H->lv[0];
+   double *p;
+   const int nb = amgk::tile_blocks(0, v.n);
+   AMG_TRY(amg_ctx_partials(c, nb, &p));
+   {
+      ProfScope ps(H, PROF_FINE_SPMV, c->stream);
+      amgk::spgemv(c->stream, v.A, v.u, v.f, amgk::gemv_mode(-1.0, 1.0), H->r0, 0, v.n, p);
+   }
+   amgk::reduce_partials(c->stream, p, nb, H->d_hist + slot, 1, c->d_scalars + 4096);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+static void init_vectors(amg_hier *H)
+{
+   // Misc.cpp:565-692 InitVectors / InitSolve
+   hipStream_t s = H->ctx->stream;
+   for (int l = 0; l < H->L; l++) {
+      Level &v = H->lv[l];
+      if (l > 0) amgk::vset(s, v.f, 0.0, 0, v.n);
+      amgk::vset(s, v.u, 0.0, 0, v.n);
+      amgk::vset(s, v.u_alt, 0.0, 0, v.n);
+      amgk::vset(s, v.u_prev, 0.0, 0, v.n);
+      amgk::vset(s, v.y, 0.0, 0, v.n);
+      amgk::vset(s, v.r_fine, 0.0, 0, v.n);
+      v.zero_flag = 0;
+   }
+   for (auto &a : H->al) {
+      for (size_t l = 0; l < a.r.size(); l++)
+         if (a.r[l]) {
+            amgk::vset(s, a.r[l], 0.0, 0, H->lv[l].n);
+            amgk::vset(s, a.e[l], 0.0, 0, H->lv[l].n);
+         }
+   }
+   amgk::vset(s, H->u_outer, 0.0, 0, H->lv[0].n);
+   amgk::vset(s, H->y_outer, 0.0, 0, H->lv[0].n);
+}
+
+static int solve_begin(amg_hier *H, const amg_vec *f, const amg_vec *u)
+{
+   amg_ctx *c = H->ctx;
+   Level &v = H->lv[0];
+   AMG_ARG(f->n == v.n && u->n == v.n, "amg_solve: vector size %d/%d vs %d", f->n, u->n, v.n);
+   init_vectors(H);
+   amgk::vcopy(c->stream, f->d, v.f, 0, v.n);
+   amgk::vcopy(c->stream, u->d, v.u, 0, v.n);
+   AMG_TRY(outer_residual(H, 0));
+   AMG_HIP(hipMemcpyAsync(c->h_pinned, H->d_hist, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   H->r0norm = c->h_pinned[0];
+   H->cheby_omega = 2.0;
+   H->iter = 0;
+   H->have_state = true;
+   return AMG_OK;
+}
+
+// one outer iteration: cycle, Chebyshev update, outer residual + norm (no sync)
+static int solve_step(amg_hier *H)
+{
+   amg_ctx *c = H->ctx;
+   const amg_opts &o = H->o;
+   const bool precond = o.cheby_flag == 1;
+   const bool one_level = !is_all_levels(o);
+   const bool reuse = one_level && !precond && o.reuse_outer_residual &&
+                      (o.smoother == AMG_JACOBI || o.smoother == AMG_SYMM_JACOBI ||
+                       o.smoother == AMG_L1_JACOBI) &&
+                      o.num_pre_smooth_sweeps > 0 && H->L > 1;
+   if (one_level)
+      vcycle(H, precond, reuse);
+   else
+      sync_add_vcycle(H);
+   if (o.cheby_flag == 1) {
+      const double mu24 = 4.0 * std::pow(o.cheby_mu, 2.0);
+      amgk::cheby_update(c->stream, H->lv[0].u, H->u_outer, H->y_outer, H->cheby_omega,
+                         o.cheby_delta, H->lv[0].n);
+      H->cheby_omega = 1.0 / (1.0 - H->cheby_omega / mu24);
+   }
+   H->iter++;
+   const int slot = H->iter % (H->hist_cap - 1);
+   return outer_residual(H, slot);
+}
+
+extern "C" int amg_solve(amg_hier *H, const amg_vec *f, amg_vec *u, double *reshist, int *cycles)
+{
+   AMG_ARG(H && f && u, "amg_solve: null argument");
+   amg_ctx *c = H->ctx;
+   AMG_TRY(solve_begin(H, f, u));
+   if (reshist) reshist[0] = H->r0norm;
+   int done = 0;
+   for (int k = 1; k <= H->o.num_cycles; k++) {
+      AMG_TRY(solve_step(H));
+      done = k;
+      if (H->o.check_resnorm == 1) {
+         AMG_HIP(hipMemcpyAsync(c->h_pinned, H->d_hist + (H->iter % (H->hist_cap - 1)),
+                                sizeof(double), hipMemcpyDeviceToHost, c->stream));
+         AMG_HIP(hipStreamSynchronize(c->stream));
+         const double rn = c->h_pinned[0];
+         if (reshist) reshist[k] = rn;
+         if (rn / H->r0norm < H->o.tol) break;
+      }
+   }
+   amgk::vcopy(c->stream, H->lv[0].u, u->d, 0, u->n);
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   if (cycles) *cycles = done;
+   return AMG_OK;
+}
+
+extern "C" int amg_solve_iterate(amg_hier *H, int k)
+{
+   AMG_ARG(H && H->have_state, "amg_solve_iterate: call amg_solve (or amg_solve_start) first");
+   for (int i = 0; i < k; i++) AMG_TRY(solve_step(H));
+   return AMG_OK;
+}
+
+extern "C" int amg_solve_start(amg_hier *H, const amg_vec *f, const amg_vec *u, double *r0norm)
+{
+   AMG_ARG(H && f && u, "amg_solve_start: null argument");
+   AMG_TRY(solve_begin(H, f, u));
+   if (r0norm) *r0norm = H->r0norm;
+   return AMG_OK;
+}
+
+extern "C" int amg_solve_resnorm(amg_hier *H, double *out)
+{
+   AMG_ARG(H && out && H->have_state, "amg_solve_resnorm: no solve state");
+   amg_ctx *c = H->ctx;
+   AMG_HIP(hipMemcpyAsync(c->h_pinned, H->d_hist + (H->iter % (H->hist_cap - 1)), sizeof(double),
+                          hipMemcpyDeviceToHost, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   *out = c->h_pinned[0];
+   return AMG_OK;
+}
+
+extern "C" int amg_solve_get_u(amg_hier *H, amg_vec *u)
+{
+   AMG_ARG(H && u && u->n == H->lv[0].n, "amg_solve_get_u: bad argument");
+   amgk::vcopy(H->ctx->stream, H->lv[0].u, u->d, 0, u->n);
+   AMG_HIP(hipStreamSynchronize(H->ctx->stream));
+   return AMG_OK;
+}
+
+extern "C" int amg_vcycle(amg_hier *H)
+{
+   AMG_ARG(H, "amg_vcycle: null hierarchy");
+   if (is_all_levels(H->o))
+      sync_add_vcycle(H);
+   else
+      vcycle(H, H->o.cheby_flag == 1, false);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+// ---- EigsPower (SMEM_Cheby.cpp:410-518) ------------------------------------------
+// M^{-1} f = one preconditioner-mode V-cycle from a zero state (the reference
+// uses HYPRE_BoomerAMGSolve here).
+static int precond_apply(amg_hier *H, const double *fin, double *out)
+{
+   hipStream_t s = H->ctx->stream;
+   for (int l = 0; l < H->L; l++) {
+      amgk::vset(s, H->lv[l].u, 0.0, 0, H->lv[l].n);
+      H->lv[l].zero_flag = 0;
+   }
+   amgk::vcopy(s, fin, H->r0, 0, H->lv[0].n);
+   vcycle(H, true, false);
+   amgk::vcopy(s, H->lv[0].u, out, 0, H->lv[0].n);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+extern "C" int amg_eigs_power(amg_hier *H, int iters, double *eig_max, double *eig_min)
+{
+   AMG_ARG(H && eig_max && eig_min && iters >= 1, "amg_eigs_power: bad argument");
+   AMG_ARG(!is_all_levels(H->o), "amg_eigs_power: MULT hierarchies only");
+   amg_ctx *c = H->ctx;
+   const int n = H->lv[0].n;
+   amg_vec U{c, n, nullptr, false}, E{c, n, nullptr, false}, Fv{c, n, nullptr, false},
+      V{c, n, nullptr, false};
+   double *tmp;
+   AMG_TRY(dalloc(H, 4 * (size_t)n, &tmp));
+   U.d = tmp;
+   E.d = tmp + n;
+   Fv.d = tmp + 2 * (size_t)n;
+   V.d = tmp + 3 * (size_t)n;
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   double dd;
+   for (int pass = 0; pass < 2; pass++) {
+      amgk::vset(c->stream, U.d, 1.0, 0, n);
+      int it = 0;
+      while (true) {
+         AMG_TRY(amg_vec_dot(c, &U, &U, &dd));
+         amgk::vscale(c->stream, 1.0 / std::sqrt(dd), U.d, 0, n);
+         amgk::vcopy(c->stream, U.d, E.d, 0, n);
+         amgk::spgemv(c->stream, H->lv[0].A, U.d, nullptr, mv, Fv.d, 0, n, nullptr);
+         AMG_TRY(precond_apply(H, Fv.d, U.d));
+         if (pass == 1) amgk::vcopy(c->stream, E.d, V.d, 0, n);
+         it++;
+         if (it == iters) break;
+         if (pass == 1) amgk::vaxpy(c->stream, -(*eig_max), V.d, U.d, 0, n);
+      }
+      if (pass == 0) {
+         amgk::vcopy(c->stream, E.d, V.d, 0, n);
+         AMG_TRY(amg_vec_dot(c, &V, &U, eig_max));
+      } else {
+         AMG_TRY(amg_vec_dot(c, &V, &U, eig_min));
+      }
+   }
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   return AMG_OK;
+}
+
+// ---- SMEM_Async_Add_AMG (SMEM_Async_AMG.cpp:7-437) ---------------------------------
+// FULL_ASYNC, read_type READ_SOL, res_compute LOCAL, converge LOCAL: every
+// level runs num_cycles corrections on its own stream with no inter-level
+// synchronisation.  Corrections land in u through device-scope fp64 atomics
+// and each level recomputes its private residual f - A u_k from the value of
+// u it observed at its own update (SMEM_Async_AMG.cpp:284-301, 338-351).
+extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *level_corrections,
+                               double *relres)
+{
+   AMG_ARG(H && f && u, "amg_async_solve: null argument");
+   AMG_ARG(is_all_levels(H->o), "amg_async_solve: ASYNC_MULTADD / ASYNC_AFACX hierarchies only");
+   AMG_ARG(H->o.async_type == AMG_FULL_ASYNC, "amg_async_solve: SEMI_ASYNC not supported");
+   amg_ctx *c = H->ctx;
+   const int L = H->L;
+   AMG_ARG((int)c->level_streams.size() >= L, "amg_async_solve: context has %d level streams, need %d",
+           (int)c->level_streams.size(), L);
+   AMG_TRY(solve_begin(H, f, u));
+   Level &v0 = H->lv[0];
+   const int n0 = v0.n;
+   hipEvent_t ready;
+   AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+   AMG_HIP(hipEventRecord(ready, c->stream));
+   // the finest level whose correction is nonzero is L-2 (see add_level_correction)
+   const int active = std::max(1, L - 1);
+   for (int k = 0; k < active; k++) {
+      AMG_HIP(hipStreamWaitEvent(c->level_streams[k], ready, 0));
+      // level_vector[k].r[0] = vector.r[0] (SMEM_Async_AMG.cpp:10-15)
+      amgk::vcopy(c->level_streams[k], H->r0, H->al[k].y_fine, 0, n0);
+   }
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   for (int cyc = 0; cyc < H->o.num_cycles; cyc++) {
+      for (int k = 0; k < active; k++) {
+         hipStream_t s = c->level_streams[k];
+         AddLevel &a = H->al[k];
+         add_level_correction(H, s, k, a.y_fine);
+         amgk::atomic_correct(s, v0.u, a.e[0], a.u_priv, n0);
+         // SMEM_Residual(A0, f, u_k, y, r_k): y = A u_k; r = f - y
+         amgk::spgemv(s, v0.A, a.u_priv, nullptr, mv, a.y, 0, n0, nullptr);
+         amgk::vsub(s, v0.f, a.y, a.y_fine, 0, n0);
+      }
+   }
+   for (int k = 0; k < active; k++) {
+      hipEvent_t e;
+      AMG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      AMG_HIP(hipEventRecord(e, c->level_streams[k]));
+      AMG_HIP(hipStreamWaitEvent(c->stream, e, 0));
+      AMG_HIP(hipEventDestroy(e));
+   }
+   AMG_HIP(hipEventDestroy(ready));
+   AMG_TRY(outer_residual(H, 1));
+   AMG_HIP(hipMemcpyAsync(c->h_pinned, H->d_hist + 1, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+   amgk::vcopy(c->stream, v0.u, u->d, 0, n0);
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   if (relres) *relres = c->h_pinned[0] / H->r0norm;
+   if (level_corrections)
+      for (int k = 0; k < L; k++) level_corrections[k] = H->o.num_cycles;
+   return AMG_OK;
+}

@@ -1,0 +1,184 @@
+"""bench.py -- V-cycle iterations/s and fine-grid SpMV HBM GB/s on the 512^3
+7-pt Laplacian (BASELINE.json metric), one process per GPU.
+
+A step is one outer iteration of SMEM_Solve (SMEM_Solve.cpp:128-240): one
+multiplicative V(1,1) cycle with weighted Jacobi (w = 0.8) over the whole
+9-level geometric Galerkin hierarchy, the outer residual f - A u and its
+2-norm.  Inputs (matrices, RHS, iterate) are resident in HBM before the timed
+region.  Scaling is strong: the 512^3 problem is split into z-slabs across
+ranks.  Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--n", type=int, default=512)
+    p.add_argument("--smooth-weight", type=float, default=0.8)
+    p.add_argument("--reuse-outer-residual", type=int, default=1)
+    p.add_argument("--cpu-baseline", type=int, default=1)
+    p.add_argument("--cpu-cycles", type=int, default=2)
+    p.add_argument("--spmv-reps", type=int, default=20)
+    return p.parse_args()
+
+
+def load_traffic(n):
+    """HBM bytes per launch of the fine residual kernel measured with rocprofv3
+    --pmc (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), if profiled for n."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        d = json.load(open(path))
+        return d.get(str(n), {}).get("fine_residual_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(gen, amg, f, args):
+    """The oracle (C restatement of SMEM_Solve, OpenMP) on the host cores, on a
+    bounded sample of the same workload: args.cpu_cycles outer iterations of
+    the same 512^3 solve."""
+    from oracle import pyoracle as po
+    t0 = time.time()
+    L = gen.L
+    host = {}
+    for tag, code, cnt in (("A", amg.AMG_GEN_A, L), ("P", amg.AMG_GEN_P, L - 1),
+                           ("R", amg.AMG_GEN_R, L - 1)):
+        host[tag] = [po.Csr(*gen.host_csr(code, l)) for l in range(cnt)]
+    log(f"[cpu] host hierarchy built in {time.time() - t0:.1f}s")
+    opts = po.make_opts(smooth_weight=args.smooth_weight, num_cycles=args.cpu_cycles, tol=0.0)
+    H = po.Hier(host["A"], host["P"], host["R"], opts)
+    u, hist, k = H.solve(f)
+    secs = po.lib().or_last_loop_seconds()
+    threads = po.lib().or_num_threads()
+    del H, host
+    return {"value": k / secs, "unit": "V-cycle iters/s", "cores": threads, "kind": "port",
+            "sample": f"{k} outer iterations (V(1,1) Jacobi + residual + norm) of the same "
+                      f"{args.n}^3 solve, oracle/amg_oracle.c OpenMP, {threads} threads",
+            "seconds": secs}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import bench_dist
+        return bench_dist.main(args, world, rank)
+
+    from conftest import load_package
+    amg = load_package()
+    n = args.n
+    t0 = time.time()
+    ctx = amg.Context(device=0, nstreams=4)
+    gen = amg.Gen(n, interp=amg.AMG_INTERP_LINEAR)
+    L = gen.L
+    As = [gen.register(ctx, amg.AMG_GEN_A, l) for l in range(L)]
+    Ps = [gen.register(ctx, amg.AMG_GEN_P, l) for l in range(L - 1)]
+    Rs = [gen.register(ctx, amg.AMG_GEN_R, l) for l in range(L - 1)]
+    log(f"[gpu] {L}-level hierarchy registered in {time.time() - t0:.1f}s; "
+        f"nnz(A0)={As[0].nnz} nnz(P0)={Ps[0].nnz}")
+    opts = amg.default_opts(smooth_weight=args.smooth_weight, num_cycles=1 << 30, tol=0.0,
+                            reuse_outer_residual=args.reuse_outer_residual, profile=1)
+    H = amg.Hier(ctx, As, Ps, Rs, opts)
+    f_host = amg.rhs_rand(0, n ** 3)
+    f = ctx.vec(f_host)
+    u0 = ctx.vec(n ** 3)
+    r0 = H.solve_start(f, u0)
+    H.iterate(args.warmup)
+    ctx.sync()
+    H.profile(reset=True)
+    ctx.sync()
+    t1 = time.perf_counter()
+    H.iterate(args.steps)
+    ctx.sync()
+    t2 = time.perf_counter()
+    rn = H.resnorm()
+    ms, launches = H.profile(reset=True)
+    dt = t2 - t1
+    value = args.steps / dt
+    log(f"[gpu] {args.steps} steps in {dt * 1e3:.2f} ms -> {value:.2f} it/s; relres {rn / r0:.3e}")
+
+    n0 = As[0].nrows
+    z0 = As[0].nnz
+    # dominant kernel: fine-grid residual SpGEMV r = f - A u (12 z + 28 n + 4 algorithmic bytes)
+    res_bytes = 12 * z0 + 28 * n0 + 4
+    res_ms = ms[0] / max(launches[0], 1)
+    achieved = res_bytes / (res_ms * 1e-3) / 1e9
+    # fine-grid SpMV y = A x (12 z + 20 n + 4 bytes), events on the same stream
+    x = ctx.vec(n0)
+    x.set(1.0)
+    y = ctx.vec(n0)
+    import ctypes as C
+    spmv_ms = C.c_double()
+    amg.check(amg.lib.amg_matvec_timed(ctx.h, As[0].h, x.h, y.h, args.spmv_reps, C.byref(spmv_ms)))
+    spmv_bytes = 12 * z0 + 20 * n0 + 4
+    spmv_gbs = spmv_bytes / (spmv_ms.value * 1e-3) / 1e9
+    log(f"[gpu] fine residual {res_ms:.3f} ms ({achieved:.0f} GB/s), fine SpMV {spmv_ms.value:.3f} ms "
+        f"({spmv_gbs:.0f} GB/s); smoother {ms[1] / max(launches[1], 1):.3f} ms, "
+        f"R0 {ms[2] / max(launches[2], 1):.3f} ms, P0 {ms[3] / max(launches[3], 1):.3f} ms")
+    x.free()
+    y.free()
+    H.free()
+    for M in As + Ps + Rs:
+        M.free()
+    ctx.close()
+
+    cpu = None
+    if args.cpu_baseline:
+        try:
+            cpu = cpu_baseline(gen, amg, f_host, args)
+            log(f"[cpu] {cpu['value']:.4f} it/s on {cpu['cores']} threads")
+        except Exception as e:  # the GPU number stands on its own
+            log(f"[cpu] baseline failed: {e!r}")
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "V-cycle iters/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (7-pt Laplacian, RandDouble(-1,1) RHS after srand(0))",
+        "config": {"workload": f"{n}^3 7-pt Laplacian, SMEM_Solve MULT V(1,1) Jacobi w={args.smooth_weight}, "
+                               f"{L}-level geometric Galerkin hierarchy, outer residual + norm per step",
+                   "n": n, "levels": L, "nnz_A0": z0, "rows": n0,
+                   "reuse_outer_residual": args.reuse_outer_residual,
+                   "parallelism": "single GPU"},
+        "fine_spmv": {"gbs": spmv_gbs, "ms": spmv_ms.value, "bytes": spmv_bytes,
+                      "frac": spmv_gbs / HBM_PEAK_GBS},
+        "roofline": {"bound": "hbm", "kernel": "fine-grid residual SpGEMV r = f - A0 u",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(n),
+                     "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms},
+        "cpu_baseline": cpu,
+        "final_relres": rn / r0,
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,225 @@
+/*
+ * amg_mi355x.h -- C-ABI of the MI355X (gfx950) AMG solve-phase library.
+ *
+ * Drop-in boundary for the hot path of jwp3/async-multigrid: the reference's
+ * SEQ_* / SMEM_* / DMEM_* kernels are free C++ functions over hypre_CSRMatrix
+ * (fields i, j, data, num_rows, num_cols; diagonal first in each row) and raw
+ * HYPRE_Real* vectors.  Each entry point below names the
+ * reference function it replaces (paths relative to /root/reference/src).
+ *
+ * Conventions
+ *  - Every function returns AMG_OK (0) or a negative status; none aborts.
+ *    amg_last_error() returns a thread-local message for the last failure.
+ *  - Host arrays passed in are copied; the caller keeps ownership.  The
+ *    library owns device memory behind amg_mat / amg_vec handles.
+ *  - Compute calls are asynchronous on the context's stream; amg_sync() or
+ *    any download waits.  Call from ONE host thread per context (from an
+ *    OpenMP region use `#pragma omp master`).
+ *  - Row ranges [rb, re) keep the reference's thread-slice semantics
+ *    (SMEM_MatVec(..., ns, ne)); rb = 0, re = nrows is a full pass.
+ *  - All arithmetic is fp64 with the reference's per-row summation order:
+ *    results are bit-identical to the reference's loops (sums are never
+ *    re-associated and products are rounded before accumulation).
+ */
+#ifndef AMG_MI355X_H
+#define AMG_MI355X_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMG_OK 0
+#define AMG_ERR_ARG (-1)
+#define AMG_ERR_HIP (-2)
+#define AMG_ERR_OOM (-3)
+#define AMG_ERR_RCCL (-4)
+#define AMG_ERR_UNSUPPORTED (-5)
+
+typedef struct amg_ctx amg_ctx;   /* device, streams, workspace, RCCL comm */
+typedef struct amg_mat amg_mat;   /* device CSR (+ diagonal), registered once */
+typedef struct amg_vec amg_vec;   /* device fp64 vector */
+typedef struct amg_hier amg_hier; /* level hierarchy + solver state (AllData analogue) */
+typedef struct amg_gen amg_gen;   /* structured 7-pt problem + geometric hierarchy generator */
+
+/* Smoother / solver / option ids: the reference's values (Main.hpp:47-117). */
+#define AMG_JACOBI 0
+#define AMG_GAUSS_SEIDEL 1
+#define AMG_HYBRID_JACOBI_GAUSS_SEIDEL 2
+#define AMG_SYMM_JACOBI 3
+#define AMG_L1_JACOBI 6
+#define AMG_L1_HYBRID_JACOBI_GAUSS_SEIDEL 12
+
+#define AMG_MULT 0
+#define AMG_AFACX 1
+#define AMG_MULTADD 2
+#define AMG_ASYNC_AFACX 5
+#define AMG_ASYNC_MULTADD 6
+
+#define AMG_FULL_ASYNC 0
+#define AMG_SEMI_ASYNC 1
+
+/* Subset of the reference's InputData (Main.hpp:187-234) the hot path reads. */
+typedef struct {
+   int solver;                   /* input.solver                                  */
+   int smoother;                 /* input.smoother                                */
+   int num_pre_smooth_sweeps;    /* input.num_pre_smooth_sweeps                   */
+   int num_post_smooth_sweeps;   /* input.num_post_smooth_sweeps                  */
+   int num_fine_smooth_sweeps;   /* input.num_fine_smooth_sweeps (additive)       */
+   int num_coarse_smooth_sweeps; /* input.num_coarse_smooth_sweeps (AFACx)        */
+   double smooth_weight;         /* input.smooth_weight                           */
+   int num_cycles;               /* input.num_cycles                              */
+   double tol;                   /* input.tol (relative residual)                 */
+   int check_resnorm;            /* input.check_resnorm_flag                      */
+   int cheby_flag;               /* -cheby (also sets precond_flag)               */
+   double cheby_mu, cheby_delta; /* cheby.mu, cheby.delta (SMEM_Cheby.cpp:48-49)  */
+   int num_threads;              /* T of the reference's row partitions; hybrid
+                                    JGS blocks follow PartitionGrids for T; 0 =
+                                    device partition of jgs_block_rows rows     */
+   int jgs_block_rows;           /* block size of the device partition (>=1)      */
+   int reuse_outer_residual;     /* 1: the level-0 pre-smoother consumes the
+                                    outer-loop residual f - A u already in r
+                                    (bit-identical; saves one A_0 pass/cycle)  */
+   int async_type;               /* AMG_FULL_ASYNC / AMG_SEMI_ASYNC               */
+   int profile;                  /* 1: HIP-event timing of the fine-level kernels */
+} amg_opts;
+
+void amg_opts_default(amg_opts *o); /* SMEM_Main.cpp:65-105 defaults */
+
+/* ---- context -------------------------------------------------------------- */
+int amg_init(amg_ctx **ctx, int device, int nstreams);
+int amg_finalize(amg_ctx *ctx);
+int amg_sync(amg_ctx *ctx);
+const char *amg_last_error(void);
+int amg_version(void);
+
+/* ---- matrices: replaces handing hypre_CSRMatrix* to the kernels ----------- */
+int amg_csr_register(amg_ctx *ctx, int nrows, int ncols, long long nnz, const int *rowptr,
+                     const int *col, const double *val, int diag_first, amg_mat **out);
+int amg_mat_free(amg_mat *A);
+int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz);
+int amg_mat_download(amg_ctx *ctx, const amg_mat *A, int *rowptr, int *col, double *val);
+
+/* ---- vectors: replaces the driver's calloc'ed HYPRE_Real* ------------------ */
+int amg_vec_create(amg_ctx *ctx, int n, amg_vec **out);
+int amg_vec_free(amg_vec *v);
+int amg_vec_size(const amg_vec *v);
+int amg_vec_upload(amg_ctx *ctx, amg_vec *v, const double *host);
+int amg_vec_download(amg_ctx *ctx, const amg_vec *v, double *host);
+int amg_vec_set(amg_ctx *ctx, amg_vec *v, double alpha);
+int amg_vec_copy(amg_ctx *ctx, const amg_vec *x, amg_vec *y);
+int amg_vec_axpy(amg_ctx *ctx, double alpha, const amg_vec *x, amg_vec *y);     /* y += a x   */
+int amg_vec_ivaxpy(amg_ctx *ctx, const amg_vec *x, const amg_vec *s, amg_vec *y);/* y += x./s DMEM_Misc.cpp:462-478 */
+int amg_vec_scale(amg_ctx *ctx, double alpha, amg_vec *y);
+int amg_vec_norm2(amg_ctx *ctx, const amg_vec *x, double *out); /* sqrt(sum x_i^2), fixed order */
+int amg_vec_dot(amg_ctx *ctx, const amg_vec *x, const amg_vec *y, double *out);
+
+/* ---- kernels ---------------------------------------------------------------- */
+/* y = A x on rows [rb,re): SEQ_MatVec SEQ_MatVec.cpp:3-24, SMEM_Sync_Parfor_MatVec
+ * SMEM_MatVec.cpp:5-25, SMEM_MatVec :302-323, SMEM_Sync_Parfor_Restrict :380-392 */
+int amg_matvec(amg_ctx *ctx, const amg_mat *A, const amg_vec *x, amg_vec *y, int rb, int re);
+/* y = A^T x: SEQ_MatVecT SEQ_MatVec.cpp:26-46 (deterministic, via a transpose
+ * built once; num_threads > 1 restates the expansion-buffer order of
+ * SMEM_Sync_Parfor_MatVecT SMEM_MatVec.cpp:27-58) */
+int amg_matvec_t(amg_ctx *ctx, const amg_mat *A, const amg_vec *x, amg_vec *y, int num_threads);
+/* y = alpha A x + beta b: SMEM_SpGEMV SMEM_MatVec.cpp:123-259 (all branches;
+ * b may alias y: prolong+correct SMEM_Sync_AMG.cpp:118-123) */
+int amg_spgemv(amg_ctx *ctx, const amg_mat *A, const amg_vec *x, const amg_vec *b, double alpha,
+               double beta, amg_vec *y, int rb, int re);
+/* y = A x; r = b - y: SEQ_Residual SEQ_MatVec.cpp:48-63, SMEM_Residual SMEM_MatVec.cpp:362-378 */
+int amg_residual(amg_ctx *ctx, const amg_mat *A, const amg_vec *b, const amg_vec *x, amg_vec *y,
+                 amg_vec *r, int rb, int re);
+/* weighted Jacobi: variant 0 = SMEM_Sync_Parfor_Jacobi SMEM_Smooth.cpp:6-49 /
+ * SMEM_Sync_Jacobi :365-407 (zero sweep overwrites u); variant 1 = SEQ_Jacobi
+ * SEQ_Smooth.cpp:4-46 (zero sweep adds) */
+int amg_jacobi(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, amg_vec *u_prev,
+               double omega, int sweeps, int zero_first, int rb, int re, int variant);
+/* L1 Jacobi with l1 = amg_l1_norms: SMEM_Sync_Parfor_L1Jacobi SMEM_Smooth.cpp:96-133,
+ * SMEM_Sync_L1Jacobi :409-443 (variant 0), SEQ_L1Jacobi SEQ_Smooth.cpp:48-87 (variant 1) */
+int amg_l1_jacobi(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, amg_vec *u_prev,
+                  const amg_vec *l1, int sweeps, int zero_first, int rb, int re, int variant);
+/* hybrid Jacobi/Gauss-Seidel over blocks blk[0..nblk] (host array):
+ * SMEM_Sync_Parfor_HybridJacobiGaussSeidel[T] SMEM_Smooth.cpp:222-363 (diag_scale =
+ * A_diag, weight 1) and SMEM_Sync_HybridJacobiGaussSeidel[T] :533-641
+ * (diag_scale NULL = a_ii); reverse selects the [T] variants */
+int amg_hybrid_jgs(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, amg_vec *u_prev,
+                   const int *blk, int nblk, const amg_vec *diag_scale, double weight, int sweeps,
+                   int zero_first, int reverse);
+/* forward Gauss-Seidel: SEQ_GaussSeidel SEQ_Smooth.cpp:89-117 */
+int amg_gauss_seidel(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, int sweeps);
+/* 2-step symmetric Jacobi: variant 0 = SMEM_Sync_Symmetric[L1]Jacobi
+ * SMEM_Smooth.cpp:643-762, variant 1 = SEQ_Symmetric[L1]Jacobi SEQ_Smooth.cpp:119-189;
+ * l1 != NULL selects the L1 form */
+int amg_sym_jacobi(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, amg_vec *y,
+                   amg_vec *r, double omega, const amg_vec *l1, int sweeps, int zero_first,
+                   int rb, int re, int variant);
+/* measurement helper: reps back-to-back y = A x launches on the context's
+ * stream bracketed by HIP events; *ms = average device milliseconds per launch */
+int amg_matvec_timed(amg_ctx *ctx, const amg_mat *A, const amg_vec *x, amg_vec *y, int reps,
+                     double *ms);
+/* setup arrays: L1_row_norm SMEM_Setup.cpp:222-232, A_diag :234-237 */
+int amg_l1_norms(amg_ctx *ctx, const amg_mat *A, amg_vec *out);
+int amg_a_diag(amg_ctx *ctx, const amg_mat *A, double omega, amg_vec *out);
+
+/* ---- hierarchy, cycles, solve driver ----------------------------------------- */
+/* A[0..L-1], P[0..L-2], R[0..L-2] (R = explicit P^T, construct_R_flag = 1) */
+int amg_hier_create(amg_ctx *ctx, int num_levels, amg_mat *const *A, amg_mat *const *P,
+                    amg_mat *const *R, const amg_opts *opts, amg_hier **out);
+int amg_hier_free(amg_hier *H);
+int amg_hier_set_opts(amg_hier *H, const amg_opts *opts);
+/* override level `level`'s hybrid-JGS block partition (thread.A_ns/A_ne) */
+int amg_hier_set_blocks(amg_hier *H, int level, const int *blk, int nblk);
+#define AMG_VEC_F 0
+#define AMG_VEC_U 1
+#define AMG_VEC_R 2
+int amg_hier_vec(amg_hier *H, int which, int level, amg_vec **out);
+/* SMEM_Solve SMEM_Solve.cpp:11-262 (sync branch: SMEM_Sync_Parfor_Vcycle
+ * SMEM_Sync_AMG.cpp:8-145 for MULT, SMEM_Sync_Add_Vcycle :408-621 for MULTADD /
+ * AFACX, Chebyshev update :169-188).  reshist[0..cycles] (may be NULL). */
+int amg_solve(amg_hier *H, const amg_vec *f, amg_vec *u, double *reshist, int *cycles_done);
+/* split form of amg_solve for timed loops: start = InitSolve + initial
+ * residual (returns ||r0||); iterate enqueues k outer iterations (cycle,
+ * Chebyshev, residual + norm into a device history) with no host sync;
+ * get_u copies the current iterate out */
+int amg_solve_start(amg_hier *H, const amg_vec *f, const amg_vec *u, double *r0norm);
+int amg_solve_iterate(amg_hier *H, int k);
+int amg_solve_get_u(amg_hier *H, amg_vec *u);
+/* ||r||_2 of the current outer residual (host sync) */
+int amg_solve_resnorm(amg_hier *H, double *out);
+/* asynchronous additive AMG: SMEM_Async_Add_AMG SMEM_Async_AMG.cpp:7-437
+ * (ASYNC_MULTADD / ASYNC_AFACX, LOCAL convergence: every level performs
+ * num_cycles corrections on its own stream).  level_corrections[L] out. */
+int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *level_corrections,
+                    double *relres);
+/* EigsPower SMEM_Cheby.cpp:410-518 with this hierarchy's V-cycle as M^{-1} */
+int amg_eigs_power(amg_hier *H, int iters, double *eig_max, double *eig_min);
+/* profile: accumulated device milliseconds and launch counts of the fine-level
+ * kernels (index 0 = A_0 SpMV-class passes) since the last reset */
+int amg_hier_profile_read(amg_hier *H, double *ms, long long *launches, int reset);
+
+/* ---- structured problem generator (replaces SMEM_BuildMatrix/BoomerAMGSetup
+ * inputs for -problem 7pt; BuildHypreMatrix.cpp:250-275) ---------------------- */
+#define AMG_INTERP_LINEAR 0
+#define AMG_INTERP_AGGREGATE 1
+#define AMG_GEN_A 0
+#define AMG_GEN_P 1
+#define AMG_GEN_R 2
+int amg_gen_create(int nx, int ny, int nz, int interp, int max_levels, int max_coarse,
+                   amg_gen **out);
+int amg_gen_free(amg_gen *g);
+int amg_gen_num_levels(const amg_gen *g);
+int amg_gen_dims(const amg_gen *g, int level, int *nx, int *ny, int *nz);
+/* rows of z-planes [z0,z1) of operator `which` at `level` (P/R: the fine /
+ * coarse grid of that level), global column ids, rowptr starting at 0 */
+long long amg_gen_nnz(const amg_gen *g, int which, int level, int z0, int z1);
+int amg_gen_fill(const amg_gen *g, int which, int level, int z0, int z1, int *rowptr, int *col,
+                 double *val, int nthreads);
+/* same, generated directly in device memory and registered */
+int amg_gen_register(amg_ctx *ctx, const amg_gen *g, int which, int level, int z0, int z1,
+                     amg_mat **out);
+/* RHS: RandDouble(lo,hi) after srand(0) (SMEM_Setup.cpp:1729-1745), rows [r0,r1) of the global sequence */
+int amg_rhs_rand(long long r0, long long r1, double lo, double hi, double *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

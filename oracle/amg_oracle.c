@@ -665,11 +665,15 @@ or_hier *or_hier_create(int L, const or_csr *A, const or_csr *P, const or_csr *R
    }
    double ****lvs[] = {&H->lv_r, &H->lv_e, &H->lv_u_prev, &H->lv_y, &H->lv_rr, &H->lv_u_fine,
                        &H->lv_u_coarse, &H->lv_u_fine_prev, &H->lv_u_coarse_prev, &H->lv_r_fine};
+   /* level_vector sets exist only for the ALL_LEVELS (additive) solvers
+    * (SMEM_Setup.cpp:292-341) */
+   int all_levels = !(opts->solver == OR_MULT || opts->solver == OR_BPX);
    for (unsigned q = 0; q < sizeof(lvs) / sizeof(lvs[0]); q++) {
       *lvs[q] = (double ***)malloc(L * sizeof(double **));
       for (int k = 0; k < L; k++) {
          (*lvs[q])[k] = (double **)malloc(L * sizeof(double *));
-         for (int l = 0; l < L; l++) (*lvs[q])[k][l] = (l < k + 2) ? dvec(H->n[l]) : NULL;
+         for (int l = 0; l < L; l++)
+            (*lvs[q])[k][l] = (all_levels && l < k + 2) ? dvec(H->n[l]) : NULL;
       }
    }
    H->u_outer = dvec(H->n[0]);
@@ -843,6 +847,7 @@ static void init_vectors(or_hier *H)
    }
    for (int k = 0; k < H->L; k++)
       for (int l = 0; l < H->L && l < k + 2; l++) {
+         if (!H->lv_r[k][l]) continue;
          size_t b = (size_t)H->n[l] * sizeof(double);
          memset(H->lv_r[k][l], 0, b); memset(H->lv_e[k][l], 0, b);
          memset(H->lv_u_prev[k][l], 0, b); memset(H->lv_y[k][l], 0, b);
@@ -851,6 +856,9 @@ static void init_vectors(or_hier *H)
          memset(H->lv_u_coarse_prev[k][l], 0, b); memset(H->lv_r_fine[k][l], 0, b);
       }
 }
+
+static double g_loop_seconds = 0.0;
+double or_last_loop_seconds(void) { return g_loop_seconds; }
 
 /* SMEM_Solve.cpp:11-262, synchronous branch (async_flag == 0) */
 int or_solve(or_hier *H, const double *f, double *u, double *reshist)
@@ -871,6 +879,9 @@ int or_solve(or_hier *H, const double *f, double *u, double *reshist)
    double omega = 2.0;
    int done = 0;
    int all_levels = !(o->solver == OR_MULT || o->solver == OR_BPX);
+#ifdef _OPENMP
+   double t_start = omp_get_wtime();
+#endif
    for (int k = 1; k <= o->num_cycles; k++) {
       if (all_levels) or_sync_add_vcycle(H);
       else or_vcycle(H);
@@ -893,6 +904,9 @@ int or_solve(or_hier *H, const double *f, double *u, double *reshist)
          if (rn / r0 < o->tol) break;
       }
    }
+#ifdef _OPENMP
+   g_loop_seconds = omp_get_wtime() - t_start;
+#endif
    memcpy(u, H->u[0], (size_t)n0 * sizeof(double));
    return done;
 }

@@ -150,6 +150,8 @@ void or_cheby_setup(double eig_min, double eig_max, double *mu, double *delta);
 double *or_hier_vec(or_hier *H, const char *name, int level);
 int or_hier_levels(or_hier *H);
 
+/* wall seconds of the last or_solve's cycle loop (excludes setup/initial residual) */
+double or_last_loop_seconds(void);
 /* number of OpenMP threads the oracle loops use (cpu_baseline "cores") */
 int or_num_threads(void);
 

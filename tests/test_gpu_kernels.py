@@ -1,0 +1,282 @@
+"""Per-kernel parity: every HIP kernel against the CPU oracle, bit for bit.
+
+Bar: the integer/index work and the fp64 per-row sums are reproduced exactly
+(the library keeps the reference's summation order and rounds every product
+before accumulating), so results must be bitwise identical to the oracle's
+restatement of the reference loops.
+"""
+import numpy as np
+import pytest
+
+from conftest import random_csr, rng
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.uint64)
+
+
+def assert_bitwise(gpu, ref, what=""):
+    gpu = np.asarray(gpu)
+    ref = np.asarray(ref)
+    assert gpu.shape == ref.shape, what
+    bad = np.nonzero(bits(gpu) != bits(ref))[0]
+    assert bad.size == 0, (f"{what}: {bad.size} mismatches, first at {bad[:5]}: "
+                           f"gpu={gpu[bad[:5]]} ref={ref[bad[:5]]}")
+
+
+def matrices(oracle, amg):
+    """Test operators: 7-pt Laplacian, generated coarse operators, P, R,
+    random CSR with empty rows / zero diagonals, and a long-row matrix that
+    exercises the multi-chunk path of the tile kernel."""
+    out = {}
+    out["lap16"] = oracle.laplace_7pt(16)
+    out["lap_rect"] = oracle.laplace_7pt(13, 7, 5)
+    g = amg.Gen(24, interp=amg.AMG_INTERP_LINEAR)
+    for which, name in ((amg.AMG_GEN_A, "A"), (amg.AMG_GEN_P, "P"), (amg.AMG_GEN_R, "R")):
+        for lev in (0, 1) if which != amg.AMG_GEN_A else (1, 2):
+            nr, nc, rp, cj, cv = g.host_csr(which, lev)
+            out[f"{name}{lev}"] = oracle.Csr(nr, nc, rp, cj, cv)
+    out["rand_sq"] = random_csr(oracle, 3000, 3000, 9, seed=1, with_zero_diag=True)
+    out["rand_nz"] = random_csr(oracle, 2500, 2500, 9, seed=4)
+    out["rand_rect"] = random_csr(oracle, 1777, 901, 5, seed=2, diag_first=False)
+    # long rows: > AMG_CHUNK (2048) entries in one row and in one tile
+    g2 = rng(3)
+    n = 600
+    rows = []
+    for i in range(n):
+        k = 5000 if i in (7, 300) else int(g2.integers(1, 40))
+        c = sorted(set(g2.integers(0, n, size=k).tolist()) - {i})
+        rows.append([i] + c)
+    rp = np.cumsum([0] + [len(r) for r in rows])
+    cj = np.concatenate([np.array(r, dtype=np.int32) for r in rows])
+    cv = g2.uniform(-1, 1, size=cj.size)
+    cv[rp[:-1]] = 50.0
+    out["longrows"] = oracle.Csr(n, n, rp, cj, cv)
+    return out
+
+
+@pytest.fixture(scope="module")
+def mats(oracle, amg, ctx):
+    host = matrices(oracle, amg)
+    dev = {k: ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val) for k, A in host.items()}
+    return host, dev
+
+
+SQUARE = ["lap16", "A1", "A2", "rand_sq", "longrows"]
+ALL = SQUARE + ["lap_rect", "P0", "P1", "R0", "R1", "rand_rect"]
+
+
+def _vecs(n, seed):
+    g = rng(seed)
+    return g.uniform(-1, 1, n)
+
+
+@pytest.mark.parametrize("name", ALL)
+def test_matvec(mats, ctx, oracle, amg, name):
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    x = _vecs(A.ncols, 10)
+    ref = oracle.smem_matvec(A, x, np.zeros(A.nrows))
+    y = ctx.vec(A.nrows)
+    amg.smem.SMEM_Sync_Parfor_MatVec(ctx, dA, ctx.vec(x), y)
+    assert_bitwise(y.download(), ref, name)
+
+
+@pytest.mark.parametrize("name", ["lap16", "rand_rect", "longrows", "P0"])
+@pytest.mark.parametrize("ab", [(1, 0), (-1, 0), (2.5, 0), (1, -1), (-1, 1), (0.5, -0.5),
+                                (1, 1), (-1, -1), (3, 3), (1, 0.3), (-1, 0.7), (1.7, -0.4)])
+def test_spgemv_branches(mats, ctx, oracle, amg, name, ab):
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    alpha, beta = ab
+    x = _vecs(A.ncols, 11)
+    b = _vecs(A.nrows, 12)
+    ref = oracle.smem_spgemv(A, x, b, alpha, beta, np.zeros(A.nrows))
+    y = ctx.vec(A.nrows)
+    amg.smem.SMEM_SpGEMV(ctx, dA, ctx.vec(x), ctx.vec(b), alpha, beta, y, 0, A.nrows)
+    assert_bitwise(y.download(), ref, f"{name} {ab}")
+
+
+def test_spgemv_row_range_and_inplace(mats, ctx, oracle, amg):
+    """Row slices leave other rows untouched; b may alias y (prolong+correct)."""
+    host, dev = mats
+    A, dA = host["P0"], dev["P0"]
+    x = _vecs(A.ncols, 13)
+    u = _vecs(A.nrows, 14)
+    ref = u.copy()
+    oracle.smem_spgemv(A, x, ref.copy(), 1.0, 1.0, ref, 37, A.nrows - 101)
+    du = ctx.vec(u)
+    amg.smem.SMEM_SpGEMV(ctx, dA, ctx.vec(x), du, 1.0, 1.0, du, 37, A.nrows - 101)
+    assert_bitwise(du.download(), ref)
+
+
+@pytest.mark.parametrize("name", ["lap16", "A1", "rand_sq"])
+def test_residual_two_pass(mats, ctx, oracle, amg, name):
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    x, b = _vecs(A.ncols, 15), _vecs(A.nrows, 16)
+    y0, r0 = np.zeros(A.nrows), np.zeros(A.nrows)
+    oracle.smem_residual(A, b, x, y0, r0, 3, A.nrows - 5)
+    y, r = ctx.vec(A.nrows), ctx.vec(A.nrows)
+    amg.smem.SMEM_Residual(ctx, dA, ctx.vec(b), ctx.vec(x), y, r, 3, A.nrows - 5)
+    assert_bitwise(y.download(), y0, "y")
+    assert_bitwise(r.download(), r0, "r")
+
+
+@pytest.mark.parametrize("name", ["P0", "R1", "rand_rect", "lap16"])
+@pytest.mark.parametrize("T", [1, 4, 7])
+def test_matvec_t(mats, ctx, oracle, amg, name, T):
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    x = _vecs(A.nrows, 17)
+    ref = oracle.seq_matvec_t(A, x) if T == 1 else oracle.smem_matvec_t_expand(A, x, T)
+    y = ctx.vec(A.ncols)
+    amg.smem.SMEM_Sync_Parfor_MatVecT(ctx, dA, ctx.vec(x), y, T)
+    assert_bitwise(y.download(), ref, f"{name} T={T}")
+
+
+@pytest.mark.parametrize("name", SQUARE)
+@pytest.mark.parametrize("zero", [0, 1])
+@pytest.mark.parametrize("variant", ["smem", "seq"])
+def test_jacobi(mats, ctx, oracle, amg, name, zero, variant):
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    f, u = _vecs(A.nrows, 18), _vecs(A.nrows, 19)
+    ru, rp = u.copy(), np.zeros(A.nrows)
+    w = 0.8
+    if variant == "smem":
+        oracle.smem_jacobi(A, f, ru, rp, w, 3, zero)
+    else:
+        oracle.seq_jacobi(A, f, ru, rp, w, 3, zero)
+    du, dp = ctx.vec(u), ctx.vec(A.nrows)
+    fn = amg.smem.SMEM_Sync_Parfor_Jacobi if variant == "smem" else amg.smem.SEQ_Jacobi
+    fn(ctx, dA, ctx.vec(f), du, dp, 3, zero, w)
+    assert_bitwise(du.download(), ru, f"{name} u")
+    assert_bitwise(dp.download(), rp, f"{name} u_prev")
+
+
+@pytest.mark.parametrize("name", ["lap16", "A2", "rand_sq"])
+@pytest.mark.parametrize("zero", [0, 1])
+def test_l1_jacobi(mats, ctx, oracle, amg, name, zero):
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    f, u = _vecs(A.nrows, 20), _vecs(A.nrows, 21)
+    l1 = oracle.l1_norms(A)
+    dl1 = ctx.vec(A.nrows)
+    amg.smem.L1_row_norm(ctx, dA, dl1)
+    assert_bitwise(dl1.download(), l1, "l1 norms")
+    for variant in ("smem", "seq"):
+        ru, rp = u.copy(), np.zeros(A.nrows)
+        if variant == "smem":
+            oracle.smem_l1jacobi(A, f, ru, rp, l1, 2, zero)
+        else:
+            oracle.seq_l1jacobi(A, f, ru, rp, l1, 2, zero)
+        du, dp = ctx.vec(u), ctx.vec(A.nrows)
+        fn = amg.smem.SMEM_Sync_Parfor_L1Jacobi if variant == "smem" else amg.smem.SEQ_L1Jacobi
+        fn(ctx, dA, ctx.vec(f), du, dp, dl1, 2, zero)
+        assert_bitwise(du.download(), ru, f"{name} {variant}")
+
+
+@pytest.mark.parametrize("name", ["lap16", "A1", "rand_sq"])
+@pytest.mark.parametrize("T", [1, 4, 8, "perf64"])
+@pytest.mark.parametrize("zero", [0, 1])
+def test_hybrid_jgs(mats, ctx, oracle, amg, name, T, zero):
+    """Hybrid Jacobi/GS is partition dependent: the same blocks must give the
+    same bits -- the reference's thread ranges (T) and the device partition."""
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    if T == "perf64":
+        blk = np.minimum(np.arange(0, A.nrows + 64, 64), A.nrows).astype(np.int32)
+        blk = np.unique(blk)
+    else:
+        blk = oracle.partition_equal(A.nrows, T)
+    f, u = _vecs(A.nrows, 22), _vecs(A.nrows, 23)
+    w = 0.7
+    ds = oracle.a_diag(A, w)
+    dds = ctx.vec(A.nrows)
+    amg.smem.A_diag(ctx, dA, w, dds)
+    assert_bitwise(dds.download(), ds, "A_diag")
+    for reverse in (0, 1):
+        for parfor in (True, False):
+            ru, rp = u.copy(), np.zeros(A.nrows)
+            oracle.hybrid_jgs(A, f, ru, rp, blk, ds if parfor else None, 1.0, 2, zero, reverse)
+            du, dp = ctx.vec(u), ctx.vec(A.nrows)
+            if parfor:
+                amg.smem.SMEM_Sync_Parfor_HybridJacobiGaussSeidel(ctx, dA, ctx.vec(f), du, dp, blk,
+                                                                 dds, 2, zero, reverse)
+            else:
+                amg.smem.SMEM_Sync_HybridJacobiGaussSeidel(ctx, dA, ctx.vec(f), du, dp, 2, zero,
+                                                          blk, reverse)
+            assert_bitwise(du.download(), ru, f"{name} T={T} rev={reverse} parfor={parfor}")
+
+
+def test_gauss_seidel(mats, ctx, oracle, amg):
+    host, dev = mats
+    A, dA = host["lap16"], dev["lap16"]
+    f, u = _vecs(A.nrows, 24), _vecs(A.nrows, 25)
+    ru = u.copy()
+    oracle.seq_gauss_seidel(A, f, ru, 2)
+    du = ctx.vec(u)
+    amg.smem.SEQ_GaussSeidel(ctx, dA, ctx.vec(f), du, 2)
+    assert_bitwise(du.download(), ru)
+
+
+@pytest.mark.parametrize("name", ["lap16", "A1", "rand_nz"])
+@pytest.mark.parametrize("sweeps", [1, 2])
+@pytest.mark.parametrize("zero", [0, 1])
+def test_symmetric_jacobi(mats, ctx, oracle, amg, name, sweeps, zero):
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    f, u = _vecs(A.nrows, 26), _vecs(A.nrows, 27)
+    w = 0.9
+    n = A.nrows
+    l1 = oracle.l1_norms(A)
+    dl1 = ctx.vec(l1)
+    cases = [
+        ("smem", lambda ru, y, r: oracle.smem_sym_jacobi(A, f, ru, y, r, w, sweeps, zero),
+         lambda du, dy, dr: amg.smem.SMEM_Sync_SymmetricJacobi(ctx, dA, ctx.vec(f), du, dy, dr,
+                                                                sweeps, zero, w, 0, n)),
+        ("smem_l1", lambda ru, y, r: oracle.smem_sym_l1jacobi(A, f, ru, y, r, l1, sweeps, zero),
+         lambda du, dy, dr: amg.smem.SMEM_Sync_SymmetricL1Jacobi(ctx, dA, ctx.vec(f), du, dy, dr,
+                                                                  dl1, sweeps, zero, 0, n)),
+        ("seq", lambda ru, y, r: oracle.seq_sym_jacobi(A, f, ru, y, r, w, sweeps),
+         lambda du, dy, dr: amg.smem.SEQ_SymmetricJacobi(ctx, dA, ctx.vec(f), du, dy, dr, sweeps, w)),
+        ("seq_l1", lambda ru, y, r: oracle.seq_sym_l1jacobi(A, f, ru, y, r, l1, sweeps),
+         lambda du, dy, dr: amg.smem.SEQ_SymmetricL1Jacobi(ctx, dA, ctx.vec(f), du, dy, dr, dl1,
+                                                            sweeps)),
+    ]
+    for tag, ref_fn, gpu_fn in cases:
+        if tag.startswith("seq") and zero == 1:
+            continue
+        ru, y, r = u.copy(), np.zeros(n), np.zeros(n)
+        ref_fn(ru, y, r)
+        du, dy, dr = ctx.vec(u), ctx.vec(n), ctx.vec(n)
+        gpu_fn(du, dy, dr)
+        assert_bitwise(du.download(), ru, f"{name} {tag} u")
+        assert_bitwise(dr.download(), r, f"{name} {tag} r")
+
+
+def test_vector_ops_and_norm(ctx, amg):
+    g = rng(30)
+    n = 100003
+    x, y, s = g.uniform(-1, 1, n), g.uniform(-1, 1, n), g.uniform(1, 2, n)
+    dx, dy, ds = ctx.vec(x), ctx.vec(y), ctx.vec(s)
+    amg.smem.DMEM_HypreParVector_Ivaxpy(ctx, dy, dx, ds)
+    assert_bitwise(dy.download(), y + x / s, "ivaxpy")
+    amg.smem.DMEM_HypreRealArray_Axpy(ctx, dy, dx, 0.25)
+    assert_bitwise(dy.download(), (y + x / s) + 0.25 * x, "axpy")
+    nrm = dx.norm2()
+    assert abs(nrm - np.sqrt(np.sum(x * x))) <= 1e-13 * nrm
+    assert nrm == dx.norm2()  # deterministic
+
+
+def test_error_reporting(ctx, amg, mats):
+    host, dev = mats
+    dA = dev["lap16"]
+    small = ctx.vec(10)
+    with pytest.raises(amg.AmgError, match="vector sizes"):
+        amg.smem.SMEM_Sync_Parfor_MatVec(ctx, dA, small, small)
+    with pytest.raises(amg.AmgError, match="row range"):
+        amg.smem.SMEM_MatVec(ctx, dA, ctx.vec(dA.ncols), ctx.vec(dA.nrows), 5, dA.nrows + 1)

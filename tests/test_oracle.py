@@ -1,0 +1,109 @@
+"""CPU: the oracle restatement against the reference's known answer and
+against independent closed-form / numpy restatements."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import random_csr, rng
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def aggregation_hierarchy(oracle, n):
+    A = oracle.laplace_7pt(n)
+    nc = n // 2
+    rows = np.arange(n ** 3)
+    x, y, z = rows % n, (rows // n) % n, rows // (n * n)
+    c = (x // 2) + nc * ((y // 2) + nc * (z // 2))
+    P = oracle.Csr(n ** 3, nc ** 3, np.arange(n ** 3 + 1), c, np.ones(n ** 3))
+    R = oracle.transpose(P)
+    A1 = oracle.spgemm(oracle.spgemm(R, A), P)
+    return A, A1, P, R
+
+
+def test_known_answer_pin(oracle):
+    """SMEM_Solve known answer recorded from the reference itself."""
+    ka = json.load(open(os.path.join(HERE, "golden", "known_answer.json")))
+    case = ka["smem_solve_16cube_aggregation"]
+    A, A1, P, R = aggregation_hierarchy(oracle, 16)
+    f = oracle.rhs_rand(16 ** 3)
+    opts = oracle.make_opts(smooth_weight=0.8, num_cycles=20)
+    H = oracle.Hier([A, A1], [P], [R], opts)
+    u, hist, k = H.solve(f)
+    assert k == 20
+    rel = hist[-1] / hist[0]
+    assert abs(rel - case["relres"]) <= 1e-12 * case["relres"]
+
+
+def test_laplacian_closed_form(oracle):
+    n = 9
+    A = oracle.laplace_7pt(n)
+    assert A.nnz == 7 * n ** 3 - 6 * n ** 2
+    y = oracle.seq_matvec(A, np.ones(n ** 3))
+    # row sum = number of missing neighbours (Dirichlet boundary)
+    idx = np.arange(n ** 3)
+    x, yy, z = idx % n, (idx // n) % n, idx // (n * n)
+    missing = sum(((v == 0).astype(int) + (v == n - 1).astype(int)) for v in (x, yy, z))
+    np.testing.assert_array_equal(y, missing.astype(float))
+    assert np.all(A.val[A.rowptr[:-1]] == 6.0)
+
+
+def test_matvec_against_numpy(oracle):
+    A = random_csr(oracle, 500, 300, 6, seed=5, diag_first=False)
+    x = rng(1).uniform(-1, 1, 300)
+    y = oracle.seq_matvec(A, x)
+    ref = np.array([sum(A.val[k] * x[A.col[k]] for k in range(A.rowptr[i], A.rowptr[i + 1]))
+                    for i in range(A.nrows)])
+    np.testing.assert_array_equal(y, ref)   # same sequential order -> same bits
+    yt = oracle.seq_matvec_t(A, rng(2).uniform(-1, 1, 500))
+    assert yt.shape == (300,)
+
+
+@pytest.mark.parametrize("alpha,beta", [(1, 0), (-1, 1), (1, 1), (2, -3), (-1, -1), (0.5, 0.5)])
+def test_spgemv_math(oracle, alpha, beta):
+    A = random_csr(oracle, 400, 400, 7, seed=6)
+    g = rng(3)
+    x, b = g.uniform(-1, 1, 400), g.uniform(-1, 1, 400)
+    y = oracle.smem_spgemv(A, x, b, alpha, beta, np.zeros(400))
+    ref = alpha * A.to_scipy().dot(x) + beta * b
+    np.testing.assert_allclose(y, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_jacobi_fixed_point_and_gs(oracle):
+    A = oracle.laplace_7pt(6)
+    n = A.nrows
+    u_star = rng(4).uniform(-1, 1, n)
+    f = oracle.seq_matvec(A, u_star)
+    u, up = u_star.copy(), np.zeros(n)
+    oracle.smem_jacobi(A, f, u, up, 0.8, 3, 0)
+    np.testing.assert_allclose(u, u_star, atol=1e-14)
+    u = np.zeros(n)
+    oracle.seq_gauss_seidel(A, f, u, 200)
+    np.testing.assert_allclose(u, u_star, atol=1e-9)
+    # hybrid JGS with one block per row == Jacobi with weight 1
+    blk = np.arange(n + 1, dtype=np.int32)
+    u1, u2, p = np.zeros(n), np.zeros(n), np.zeros(n)
+    oracle.hybrid_jgs(A, f, u1, p, blk, None, 1.0, 2, 0)
+    oracle.smem_jacobi(A, f, u2, np.zeros(n), 1.0, 2, 0)
+    np.testing.assert_array_equal(u1, u2)
+
+
+def test_partitions(oracle):
+    A = random_csr(oracle, 1001, 1001, 8, seed=7)
+    for T in (1, 3, 8):
+        blk = oracle.partition_nnz(A, T)
+        per = (A.nnz + T - 1) // T
+        ref = [0] + [int(np.searchsorted(A.rowptr[:-1], per * t, side="left")) for t in range(1, T)] + [1001]
+        np.testing.assert_array_equal(blk, ref)
+        eq = oracle.partition_equal(1001, T)
+        assert eq[0] == 0 and eq[-1] == 1001 and np.all(np.diff(eq) >= 1001 // T)
+
+
+def test_rhs_is_glibc_sequence(oracle):
+    import ctypes
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(0)
+    ref = [-1 + 2 * (libc.rand() / 2147483647) for _ in range(10)]
+    np.testing.assert_array_equal(oracle.rhs_rand(10), ref)
