@@ -492,13 +492,14 @@ extern "C" int amg_hybrid_jgs(amg_ctx *c, const amg_mat *A, const amg_vec *f, am
       AMG_ARG(blk[b] <= blk[b + 1] && blk[b] >= 0 && blk[b + 1] <= A->nrows,
               "amg_hybrid_jgs: bad block %d [%d,%d)", b, blk[b], blk[b + 1]);
    int *d_blk = nullptr;
-   AMG_HIP(hipMallocAsync((void **)&d_blk, (nblk + 1) * sizeof(int), c->stream));
-   AMG_HIP(hipMemcpyAsync(d_blk, blk, (nblk + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   AMG_HIP(hipMalloc((void **)&d_blk, (nblk + 1) * sizeof(int)));
+   AMG_HIP(hipMemcpy(d_blk, blk, (nblk + 1) * sizeof(int), hipMemcpyHostToDevice));
    int s = amg_hybrid_jgs_dev(c, c->stream, A, f->d, u->d, u_prev->d, u->n, d_blk, nblk, blk[0],
                               blk[nblk], diag_scale ? diag_scale->d : nullptr, weight, sweeps,
                               zero_first, reverse);
-   AMG_HIP(hipFreeAsync(d_blk, c->stream));
    AMG_HIP(hipStreamSynchronize(c->stream));
+   AMG_HIP(hipFree(d_blk));
    return s;
 }
 

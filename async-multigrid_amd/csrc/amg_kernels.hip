@@ -280,11 +280,20 @@ __global__ void hybrid_jgs_k(const int *__restrict__ rowptr, const int *__restri
                              const int *__restrict__ blk, int nblk,
                              const double *__restrict__ ds, double weight, int zero, int reverse)
 {
+   // A lane re-reads values of u it stored earlier in this sweep.  Plain
+   // global loads may be served by a stale line of the CU's vector L1 (gfx950
+   // stores write through to L2 without refreshing L1), so every access to u
+   // is a relaxed atomic: same-location coherence then holds by the memory
+   // model (agent-scope loads are L2-served).
+   auto ld = [u](int k) { return __hip_atomic_load(u + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+   auto st = [u](int k, double v) {
+      __hip_atomic_store(u + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+   };
    const int b = blockIdx.x * blockDim.x + threadIdx.x;
    if (b >= nblk) return;
    const int ns = blk[b], ne = blk[b + 1];
    if (zero)
-      for (int i = ns; i < ne; i++) u[i] = 0.0;
+      for (int i = ns; i < ne; i++) st(i, 0.0);
    for (int c = 0; c < ne - ns; c++) {
       const int i = reverse ? ne - 1 - c : ns + c;
       const int rs = rowptr[i], rend = rowptr[i + 1];
@@ -295,14 +304,14 @@ __global__ void hybrid_jgs_k(const int *__restrict__ rowptr, const int *__restri
       for (int jj = rs; jj < rend; jj++) {
          const int ii = col[jj];
          if (ii >= ns && ii < ne)
-            res -= val[jj] * u[ii];
+            res -= val[jj] * ld(ii);
          else if (!zero)
             res -= val[jj] * u_prev[ii];
       }
       if (zero)
-         u[i] = weight * res / d;
+         st(i, weight * res / d);
       else
-         u[i] += weight * res / d;
+         st(i, ld(i) + weight * res / d);
    }
 }
 
