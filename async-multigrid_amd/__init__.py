@@ -221,8 +221,8 @@ class Hier:
         return emax.value, emin.value
 
     def profile(self, reset=True):
-        ms = np.zeros(4)
-        n = np.zeros(4, dtype=np.int64)
+        ms = np.zeros(5)
+        n = np.zeros(5, dtype=np.int64)
         check(lib.amg_hier_profile_read(self.h, _dp(ms),
                                         n.ctypes.data_as(C.POINTER(C.c_longlong)), int(reset)))
         return ms, n

@@ -369,6 +369,37 @@ extern "C" int amg_matvec_timed(amg_ctx *c, const amg_mat *A, const amg_vec *x, 
    return AMG_OK;
 }
 
+// development-only tuning entry points (tools/tune_spmv.py); not in the header
+namespace amgk {
+int num_tune_variants();
+const char *tune_variant_name(int v);
+void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y);
+} // namespace amgk
+
+extern "C" int amg_dev_tune_count(void) { return amgk::num_tune_variants(); }
+extern "C" const char *amg_dev_tune_name(int v) { return amgk::tune_variant_name(v); }
+
+extern "C" int amg_dev_tune_spmv(amg_ctx *c, const amg_mat *A, const amg_vec *x, amg_vec *y,
+                                 int variant, int reps, double *ms)
+{
+   AMG_ARG(c && A && x && y && ms && reps >= 1, "amg_dev_tune_spmv: bad argument");
+   AMG_ARG(variant >= 0 && variant < amgk::num_tune_variants(), "amg_dev_tune_spmv: variant");
+   hipEvent_t a, b;
+   AMG_HIP(hipEventCreate(&a));
+   AMG_HIP(hipEventCreate(&b));
+   AMG_HIP(hipEventRecord(a, c->stream));
+   for (int r = 0; r < reps; r++) amgk::launch_tune_variant(c->stream, variant, A, x->d, y->d);
+   AMG_HIP(hipEventRecord(b, c->stream));
+   AMG_HIP(hipEventSynchronize(b));
+   AMG_HIP(hipGetLastError());
+   float t = 0.f;
+   AMG_HIP(hipEventElapsedTime(&t, a, b));
+   hipEventDestroy(a);
+   hipEventDestroy(b);
+   *ms = (double)t / reps;
+   return AMG_OK;
+}
+
 extern "C" int amg_spgemv(amg_ctx *c, const amg_mat *A, const amg_vec *x, const amg_vec *b,
                           double alpha, double beta, amg_vec *y, int rb, int re)
 {

@@ -100,6 +100,11 @@ int tile_blocks(int rb, int re);
 //   l1 != nullptr: out[i] = x[i] + (f_i - sum)/l1[i]   (no a_ii test)
 void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double *x,
                   const double *l1, double omega, double *out, int rb, int re);
+// outer residual r = f - A x fused with the next cycle's first Jacobi sweep on
+// the same x: unext = x + w r / a_ii (l1: x + r / l1); partials of sum r_i^2
+void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const double *x,
+                     const double *l1, double omega, double *r, double *unext, int rb, int re,
+                     double *partials);
 // zero-guess sweep: variant 0 (SMEM) u = omega*f/a (a != 0) | u = f/l1
 //                   variant 1 (SEQ)  u += omega*f/a (a != 0) | u += f/l1 (a != 0)
 void jacobi_zero(hipStream_t s, const double *diag, const double *f, const double *l1,

@@ -39,66 +39,176 @@ __device__ __forceinline__ double block_sum_256(double v, double *lds4)
 // ---------------------------------------------------------------------------
 // CSR tile kernel
 // ---------------------------------------------------------------------------
-template <int NEG, bool NEED_DIAG, class Epi>
-__global__ __launch_bounds__(AMG_TILE_ROWS) void csr_tile_kernel(
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+// Tile configuration: RPT rows per lane (tile = 256*RPT rows), CH products
+// per LDS chunk, NT non-temporal val/col streams (read once; keep L2 for x),
+// XCD contiguous-range tile remap (T1; speed only, any placement is correct).
+template <int RPT, int CH, bool NT, bool XCD, bool UNR = false, bool SKIPSYNC = false,
+          bool SHFL = false>
+struct TileCfg {
+   static constexpr int rpt = RPT, ch = CH;
+   static constexpr bool nt = NT, xcd = XCD;
+   static constexpr bool unr = UNR;       // issue two staging groups' loads before storing
+   static constexpr bool skipsync = SKIPSYNC; // no barrier after the tile's last chunk
+   static constexpr bool shfl = SHFL;     // rowptr[row+1] from the neighbour lane
+};
+
+template <bool NT>
+__device__ __forceinline__ void stage4(const int *__restrict__ col, const double *__restrict__ val,
+                                       int k, v4i &c4, v2d &v01, v2d &v23)
+{
+   if (NT) {
+      c4 = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(col + k));
+      v01 = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(val + k));
+      v23 = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(val + k + 2));
+   } else {
+      c4 = *reinterpret_cast<const v4i *>(col + k);
+      v01 = *reinterpret_cast<const v2d *>(val + k);
+      v23 = *reinterpret_cast<const v2d *>(val + k + 2);
+   }
+}
+
+template <class Cfg, int NEG, bool NEED_DIAG, class Epi>
+__global__ __launch_bounds__(256) void csr_tile_kernel(
    const int *__restrict__ rowptr, const int *__restrict__ col, const double *__restrict__ val,
    const double *__restrict__ x, int rb, int re, Epi epi, double *__restrict__ partials)
 {
-   __shared__ __attribute__((aligned(16))) double prod[AMG_CHUNK];
+   constexpr int RPT = Cfg::rpt, CH = Cfg::ch, TROWS = 256 * RPT;
+   __shared__ __attribute__((aligned(16))) double prod[CH];
    __shared__ double red[4];
-   const int r0 = rb + blockIdx.x * AMG_TILE_ROWS;
-   const int r1 = min(r0 + AMG_TILE_ROWS, re);
-   const int row = r0 + (int)threadIdx.x;
-   const bool active = row < r1;
+   int tile = blockIdx.x;
+   if (Cfg::xcd) {
+      // bijective remap: the blocks dealt to one XCD (b % 8) get a contiguous tile range
+      const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xg = tile & 7, idx = tile >> 3;
+      tile = (xg < r ? xg * (q + 1) : r * (q + 1) + (xg - r) * q) + idx;
+   }
+   const int r0 = rb + tile * TROWS;
+   const int r1 = min(r0 + TROWS, re);
    const int tb = rowptr[r0];
    const int te = rowptr[r1];
-   int rs = 0, rend = 0;
-   if (active) {
-      rs = rowptr[row];
-      rend = rowptr[row + 1];
+   int rs[RPT], rend[RPT];
+   double acc[RPT], dg[RPT], pf[RPT];
+#pragma unroll
+   for (int q = 0; q < RPT; q++) {
+      const int row = r0 + q * 256 + (int)threadIdx.x;
+      rs[q] = rend[q] = 0;
+      acc[q] = dg[q] = pf[q] = 0.0;
+      if (Cfg::shfl) {
+         // rows r0+q*256+lane are consecutive within a wave: rowptr[row+1] is
+         // the next lane's rowptr[row]; lane 63 loads its own
+         const int rr = min(row, r1);
+         const int v = rowptr[rr];
+         int nxt = __shfl_down(v, 1, 64);
+         if ((threadIdx.x & 63) == 63) nxt = rowptr[min(row + 1, r1)];
+         if (row < r1) {
+            rs[q] = v;
+            rend[q] = nxt;
+            acc[q] = epi.init(row);
+         }
+      } else if (row < r1) {
+         rs[q] = rowptr[row];
+         rend[q] = rowptr[row + 1];
+         acc[q] = epi.init(row);
+      }
+      // epilogue operands issued before the stream so their latency hides
+      if (row < r1) {
+         if (NEED_DIAG) dg[q] = val[rs[q]];
+         pf[q] = epi.pf(row);
+      }
    }
-   double acc = active ? epi.init(row) : 0.0;
    const int base = tb & ~3;
-   for (int cs = base; cs < te; cs += AMG_CHUNK) {
-      const int ce = min(cs + AMG_CHUNK, te);
-      for (int k = cs + 4 * (int)threadIdx.x; k < ce; k += 4 * AMG_TILE_ROWS) {
-         const int4 c4 = *reinterpret_cast<const int4 *>(col + k);
-         const double2 v01 = *reinterpret_cast<const double2 *>(val + k);
-         const double2 v23 = *reinterpret_cast<const double2 *>(val + k + 2);
-         const double x0 = x[c4.x];
-         const double x1 = x[c4.y];
-         const double x2 = x[c4.z];
-         const double x3 = x[c4.w];
-         double2 p01, p23;
-         p01.x = v01.x * x0;
-         p01.y = v01.y * x1;
-         p23.x = v23.x * x2;
-         p23.y = v23.y * x3;
-         double2 *dst = reinterpret_cast<double2 *>(prod + (k - cs));
-         dst[0] = p01;
-         dst[1] = p23;
+   for (int cs = base; cs < te; cs += CH) {
+      const int ce = min(cs + CH, te);
+      if (Cfg::unr) {
+         for (int k = cs + 4 * (int)threadIdx.x; k < ce; k += 8 * 256) {
+            const int k2 = k + 4 * 256;
+            const bool has2 = k2 < ce;
+            v4i c4, d4;
+            v2d v01, v23, w01, w23;
+            stage4<Cfg::nt>(col, val, k, c4, v01, v23);
+            if (has2) stage4<Cfg::nt>(col, val, k2, d4, w01, w23);
+            const double x0 = x[c4.x], x1 = x[c4.y], x2 = x[c4.z], x3 = x[c4.w];
+            double y0 = 0, y1 = 0, y2 = 0, y3 = 0;
+            if (has2) {
+               y0 = x[d4.x];
+               y1 = x[d4.y];
+               y2 = x[d4.z];
+               y3 = x[d4.w];
+            }
+            v2d p01, p23;
+            p01.x = v01.x * x0;
+            p01.y = v01.y * x1;
+            p23.x = v23.x * x2;
+            p23.y = v23.y * x3;
+            v2d *dst = reinterpret_cast<v2d *>(prod + (k - cs));
+            dst[0] = p01;
+            dst[1] = p23;
+            if (has2) {
+               v2d q01, q23;
+               q01.x = w01.x * y0;
+               q01.y = w01.y * y1;
+               q23.x = w23.x * y2;
+               q23.y = w23.y * y3;
+               v2d *dst2 = reinterpret_cast<v2d *>(prod + (k2 - cs));
+               dst2[0] = q01;
+               dst2[1] = q23;
+            }
+         }
+      } else {
+         for (int k = cs + 4 * (int)threadIdx.x; k < ce; k += 4 * 256) {
+            v4i c4;
+            v2d v01, v23;
+            stage4<Cfg::nt>(col, val, k, c4, v01, v23);
+            const double x0 = x[c4.x];
+            const double x1 = x[c4.y];
+            const double x2 = x[c4.z];
+            const double x3 = x[c4.w];
+            v2d p01, p23;
+            p01.x = v01.x * x0;
+            p01.y = v01.y * x1;
+            p23.x = v23.x * x2;
+            p23.y = v23.y * x3;
+            v2d *dst = reinterpret_cast<v2d *>(prod + (k - cs));
+            dst[0] = p01;
+            dst[1] = p23;
+         }
       }
       __syncthreads();
-      const int a = max(rs, cs), e = min(rend, ce);
-      for (int k = a; k < e; ++k) {
-         if (NEG)
-            acc -= prod[k - cs];
-         else
-            acc += prod[k - cs];
+#pragma unroll
+      for (int q = 0; q < RPT; q++) {
+         const int a = max(rs[q], cs), e = min(rend[q], ce);
+         for (int k = a; k < e; ++k) {
+            if (NEG)
+               acc[q] -= prod[k - cs];
+            else
+               acc[q] += prod[k - cs];
+         }
       }
-      __syncthreads();
+      if (!Cfg::skipsync || ce < te) __syncthreads(); // WAR on prod before the next chunk
    }
-   double out = 0.0;
-   if (active) {
-      double d = 0.0;
-      if (NEED_DIAG) d = val[rs];
-      out = epi.finish(row, acc, d);
+   double sq = 0.0;
+#pragma unroll
+   for (int q = 0; q < RPT; q++) {
+      const int row = r0 + q * 256 + (int)threadIdx.x;
+      if (row < r1) {
+         const double out = epi.finish(row, acc[q], dg[q], pf[q]);
+         sq += out * out;
+      }
    }
    if (partials) {
-      const double s = block_sum_256(out * out, red);
-      if (threadIdx.x == 0) partials[blockIdx.x] = s;
+      const double s = block_sum_256(sq, red);
+      if (threadIdx.x == 0) partials[tile] = s;
    }
 }
+
+// production configuration (tools/tune_spmv.py picks it on the MI355X)
+using ProdCfg = TileCfg<1, 2048, false, false>;
+
+// Epilogue interface: init(i) -> accumulator start value; pf(i) -> one
+// operand prefetched before the stream; finish(i, acc, a_ii, pf) writes the
+// row's outputs and returns the value whose square feeds the norm partials.
 
 // y = SpGEMV epilogue (SMEM_MatVec.cpp:140-258)
 struct EpiGemv {
@@ -107,7 +217,7 @@ struct EpiGemv {
    int imode;
    int scale;
    double alpha, temp;
-   __device__ __forceinline__ double init_val(int i) const
+   __device__ __forceinline__ double init(int i) const
    {
       switch (imode) {
       case 0: return 0.0;
@@ -117,8 +227,8 @@ struct EpiGemv {
       default: return -b[i] * temp;
       }
    }
-   __device__ __forceinline__ double init(int i) const { return init_val(i); }
-   __device__ __forceinline__ double finish(int i, double acc, double) const
+   __device__ __forceinline__ double pf(int) const { return 0.0; }
+   __device__ __forceinline__ double finish(int i, double acc, double, double) const
    {
       const double v = scale ? alpha * acc : acc;
       y[i] = v;
@@ -133,9 +243,9 @@ struct EpiJacobi {
    double *out;
    double omega;
    __device__ __forceinline__ double init(int i) const { return f[i]; }
-   __device__ __forceinline__ double finish(int i, double res, double a) const
+   __device__ __forceinline__ double pf(int i) const { return x[i]; }
+   __device__ __forceinline__ double finish(int i, double res, double a, double xi) const
    {
-      const double xi = x[i];
       const double v = (a != 0.0) ? xi + omega * res / a : xi;
       out[i] = v;
       return v;
@@ -149,15 +259,45 @@ struct EpiL1Jacobi {
    const double *l1;
    double *out;
    __device__ __forceinline__ double init(int i) const { return f[i]; }
-   __device__ __forceinline__ double finish(int i, double res, double) const
+   __device__ __forceinline__ double pf(int i) const { return x[i]; }
+   __device__ __forceinline__ double finish(int i, double res, double, double xi) const
    {
-      const double v = x[i] + res / l1[i];
+      const double v = xi + res / l1[i];
       out[i] = v;
       return v;
    }
 };
 
-int tile_blocks(int rb, int re) { return (re - rb + AMG_TILE_ROWS - 1) / AMG_TILE_ROWS; }
+// Outer residual r = f - A u (SMEM_Sync_Residual, SMEM_Solve.cpp:192-197) fused
+// with the NEXT cycle's first level-0 Jacobi sweep, which on this same u
+// computes res = f - A u in the same order (SMEM_Smooth.cpp:38-44):
+// u_next = u + w*r/a_ii (L1: u + r/l1).  Writes r and u_next, returns r for
+// the norm.
+struct EpiResJacobi {
+   const double *f;
+   const double *x;
+   const double *l1;
+   double *r;
+   double *unext;
+   double omega;
+   __device__ __forceinline__ double init(int i) const { return f[i]; }
+   __device__ __forceinline__ double pf(int i) const { return x[i]; }
+   __device__ __forceinline__ double finish(int i, double res, double a, double xi) const
+   {
+      r[i] = res;
+      unext[i] = l1 ? xi + res / l1[i] : ((a != 0.0) ? xi + omega * res / a : xi);
+      return res;
+   }
+};
+
+template <class Cfg>
+static inline int cfg_blocks(int rb, int re)
+{
+   constexpr int T = 256 * Cfg::rpt;
+   return (re - rb + T - 1) / T;
+}
+
+int tile_blocks(int rb, int re) { return cfg_blocks<ProdCfg>(rb, re); }
 
 Gemv gemv_mode(double alpha, double beta)
 {
@@ -186,11 +326,11 @@ void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, c
    EpiGemv e{b, y, g.init, g.scale, g.alpha, g.temp};
    const int nb = tile_blocks(rb, re);
    if (g.negacc)
-      csr_tile_kernel<1, false, EpiGemv>
-         <<<nb, AMG_TILE_ROWS, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, partials);
+      csr_tile_kernel<ProdCfg, 1, false, EpiGemv>
+         <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, partials);
    else
-      csr_tile_kernel<0, false, EpiGemv>
-         <<<nb, AMG_TILE_ROWS, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, partials);
+      csr_tile_kernel<ProdCfg, 0, false, EpiGemv>
+         <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, partials);
 }
 
 void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double *x,
@@ -200,12 +340,137 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
    const int nb = tile_blocks(rb, re);
    if (l1) {
       EpiL1Jacobi e{f, x, l1, out};
-      csr_tile_kernel<1, false, EpiL1Jacobi>
-         <<<nb, AMG_TILE_ROWS, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, nullptr);
+      csr_tile_kernel<ProdCfg, 1, false, EpiL1Jacobi>
+         <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, nullptr);
    } else {
       EpiJacobi e{f, x, out, omega};
-      csr_tile_kernel<1, true, EpiJacobi>
-         <<<nb, AMG_TILE_ROWS, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, nullptr);
+      csr_tile_kernel<ProdCfg, 1, true, EpiJacobi>
+         <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, nullptr);
+   }
+}
+
+void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const double *x,
+                     const double *l1, double omega, double *r, double *unext, int rb, int re,
+                     double *partials)
+{
+   if (re <= rb) return;
+   const int nb = tile_blocks(rb, re);
+   EpiResJacobi e{f, x, l1, r, unext, omega};
+   if (l1)
+      csr_tile_kernel<ProdCfg, 1, false, EpiResJacobi>
+         <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, partials);
+   else
+      csr_tile_kernel<ProdCfg, 1, true, EpiResJacobi>
+         <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, partials);
+}
+
+// ---------------------------------------------------------------------------
+// tuning harness: time y = A x under several tile configurations, interleaved
+// (development entry point used by tools/tune_spmv.py; not part of the C-ABI)
+// ---------------------------------------------------------------------------
+template <class Cfg>
+static void launch_matvec_cfg(hipStream_t s, const amg_mat *A, const double *x, double *y)
+{
+   EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
+   csr_tile_kernel<Cfg, 0, false, EpiGemv>
+      <<<cfg_blocks<Cfg>(0, A->nrows), 256, 0, s>>>(A->rowptr, A->col, A->val, x, 0, A->nrows, e,
+                                                   nullptr);
+}
+
+// ablations (wrong results, timing only): 1 = x gathered from a 64 KiB window
+// (L1/L2 resident), 2 = no LDS round trip (lane sums its own products),
+// 3 = pure stream of rowptr/col/val (no x, no LDS)
+template <int ABL>
+__global__ __launch_bounds__(256) void ablation_kernel(const int *__restrict__ rowptr,
+                                                        const int *__restrict__ col,
+                                                        const double *__restrict__ val,
+                                                        const double *__restrict__ x, int n,
+                                                        double *__restrict__ y)
+{
+   __shared__ __attribute__((aligned(16))) double prod[2048];
+   const int r0 = blockIdx.x * 256;
+   const int r1 = min(r0 + 256, n);
+   const int row = r0 + (int)threadIdx.x;
+   const int tb = rowptr[r0], te = rowptr[r1];
+   int rs = 0, rend = 0;
+   if (row < r1) {
+      rs = rowptr[row];
+      rend = rowptr[row + 1];
+   }
+   double acc = 0.0;
+   const int base = tb & ~3;
+   for (int k = base + 4 * (int)threadIdx.x; k < te; k += 1024) {
+      v4i c4 = *reinterpret_cast<const v4i *>(col + k);
+      v2d v01 = *reinterpret_cast<const v2d *>(val + k);
+      v2d v23 = *reinterpret_cast<const v2d *>(val + k + 2);
+      double x0, x1, x2, x3;
+      if (ABL == 1) {
+         x0 = x[c4.x & 8191];
+         x1 = x[c4.y & 8191];
+         x2 = x[c4.z & 8191];
+         x3 = x[c4.w & 8191];
+      } else if (ABL == 3) {
+         x0 = (double)c4.x;
+         x1 = (double)c4.y;
+         x2 = (double)c4.z;
+         x3 = (double)c4.w;
+      } else {
+         x0 = x[c4.x];
+         x1 = x[c4.y];
+         x2 = x[c4.z];
+         x3 = x[c4.w];
+      }
+      const double p0 = v01.x * x0, p1 = v01.y * x1, p2 = v23.x * x2, p3 = v23.y * x3;
+      if (ABL == 1) {
+         v2d *dst = reinterpret_cast<v2d *>(prod + (k - base));
+         dst[0] = v2d{p0, p1};
+         dst[1] = v2d{p2, p3};
+      } else {
+         acc += (p0 + p1) + (p2 + p3);
+      }
+   }
+   if (ABL == 1) {
+      __syncthreads();
+      for (int k = rs; k < rend; ++k) acc += prod[k - base];
+   }
+   if (row < r1) y[row] = acc;
+}
+
+int num_tune_variants() { return 11; }
+
+const char *tune_variant_name(int v)
+{
+   static const char *names[] = {"base",          "unroll2",          "unroll2_skipsync",
+                                 "unr_skip_shfl", "skipsync",         "unr_skip_shfl_xcd",
+                                 "rpt2_ch4096",   "unr_skip_shfl_ch4096",
+                                 "ABL_localgather", "ABL_noLDS",      "ABL_streamonly"};
+   return (v >= 0 && v < 11) ? names[v] : "?";
+}
+
+void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y)
+{
+   switch (v) {
+   case 0: launch_matvec_cfg<TileCfg<1, 2048, false, false>>(s, A, x, y); break;
+   case 1: launch_matvec_cfg<TileCfg<1, 2048, false, false, true>>(s, A, x, y); break;
+   case 2: launch_matvec_cfg<TileCfg<1, 2048, false, false, true, true>>(s, A, x, y); break;
+   case 3: launch_matvec_cfg<TileCfg<1, 2048, false, false, true, true, true>>(s, A, x, y); break;
+   case 4: launch_matvec_cfg<TileCfg<1, 2048, false, false, false, true>>(s, A, x, y); break;
+   case 5: launch_matvec_cfg<TileCfg<1, 2048, false, true, true, true, true>>(s, A, x, y); break;
+   case 6: launch_matvec_cfg<TileCfg<2, 4096, false, false>>(s, A, x, y); break;
+   case 7: launch_matvec_cfg<TileCfg<1, 4096, false, false, true, true, true>>(s, A, x, y); break;
+   case 8:
+      ablation_kernel<1><<<(A->nrows + 255) / 256, 256, 0, s>>>(A->rowptr, A->col, A->val, x,
+                                                               A->nrows, y);
+      break;
+   case 9:
+      ablation_kernel<2><<<(A->nrows + 255) / 256, 256, 0, s>>>(A->rowptr, A->col, A->val, x,
+                                                               A->nrows, y);
+      break;
+   case 10:
+      ablation_kernel<3><<<(A->nrows + 255) / 256, 256, 0, s>>>(A->rowptr, A->col, A->val, x,
+                                                                A->nrows, y);
+      break;
+   default: break;
    }
 }
 

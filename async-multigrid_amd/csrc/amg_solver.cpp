@@ -24,7 +24,8 @@ int amg_sym_jacobi_dev(hipStream_t s, const amg_mat *A, const double *f, double 
 namespace {
 
 enum ProfCat { PROF_FINE_SPMV = 0, PROF_FINE_SMOOTH = 1, PROF_RESTRICT0 = 2, PROF_PROLONG0 = 3,
-               PROF_NCAT = 4 };
+               PROF_OUTER = 4,
+               PROF_NCAT = 5 };
 
 struct Level {
    amg_mat *A = nullptr, *P = nullptr, *R = nullptr;
@@ -61,11 +62,12 @@ struct amg_hier {
    double cheby_omega = 2.0;
    int iter = 0;
    bool have_state = false;
+   bool pre_ready = false; // lv[0].u_alt holds u + w r0 / a_ii for the current u
    std::vector<void *> allocs;
    // profiling
    std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[PROF_NCAT];
-   double prof_ms[PROF_NCAT] = {0, 0, 0, 0};
-   long long prof_n[PROF_NCAT] = {0, 0, 0, 0};
+   double prof_ms[PROF_NCAT] = {0, 0, 0, 0, 0};
+   long long prof_n[PROF_NCAT] = {0, 0, 0, 0, 0};
 };
 
 static int dalloc(amg_hier *H, size_t n, double **p)
@@ -345,6 +347,11 @@ static void smooth_one_level(amg_hier *H, hipStream_t s, int l, const double *f,
    for (int k = 0; k < sweeps; k++) {
       if (k == 0 && zf == 1) {
          amgk::jacobi_zero(s, v.A->diag, f, l1 ? v.l1 : nullptr, o.smooth_weight, v.u, 0, v.n, 0);
+      } else if (k == 0 && from_outer_residual && H->pre_ready) {
+         // the outer-residual kernel already produced u + w r / a_ii from this
+         // very u and r = f - A u (same summation order): take it
+         std::swap(v.u, v.u_alt);
+         H->pre_ready = false;
       } else if (k == 0 && from_outer_residual) {
          // r0 = f - A u was computed by the outer loop on this very u with the
          // same summation order; the sweep is u += w r / a (bit-identical)
@@ -489,6 +496,19 @@ static void sync_add_vcycle(amg_hier *H)
 }
 
 // ---- SMEM_Solve (SMEM_Solve.cpp:11-262, synchronous branch) --------------------
+// Can the next cycle's first level-0 sweep come from the outer residual?
+// (MULT, no preconditioner mode, Jacobi / L1 Jacobi, pre-smoothing on)
+static bool reuse_applies(const amg_hier *H)
+{
+   const amg_opts &o = H->o;
+   return !is_all_levels(o) && o.cheby_flag != 1 && o.reuse_outer_residual &&
+          (o.smoother == AMG_JACOBI || o.smoother == AMG_SYMM_JACOBI ||
+           o.smoother == AMG_L1_JACOBI) &&
+          o.num_pre_smooth_sweeps > 0 && H->L > 1;
+}
+
+// r = f - A u and ||r|| into d_hist[slot].  With reuse, the same kernel also
+// emits the next cycle's first Jacobi sweep u_alt = u + w r / a_ii.
 static int outer_residual(amg_hier *H, int slot)
 {
    amg_ctx *c = H->ctx;
@@ -497,8 +517,16 @@ static int outer_residual(amg_hier *H, int slot)
    const int nb = amgk::tile_blocks(0, v.n);
    AMG_TRY(amg_ctx_partials(c, nb, &p));
    {
-      ProfScope ps(H, PROF_FINE_SPMV, c->stream);
-      amgk::spgemv(c->stream, v.A, v.u, v.f, amgk::gemv_mode(-1.0, 1.0), H->r0, 0, v.n, p);
+      ProfScope ps(H, PROF_OUTER, c->stream);
+      if (reuse_applies(H)) {
+         const bool l1 = (H->o.smoother == AMG_L1_JACOBI);
+         amgk::residual_jacobi(c->stream, v.A, v.f, v.u, l1 ? v.l1 : nullptr, H->o.smooth_weight,
+                               H->r0, v.u_alt, 0, v.n, p);
+         H->pre_ready = true;
+      } else {
+         amgk::spgemv(c->stream, v.A, v.u, v.f, amgk::gemv_mode(-1.0, 1.0), H->r0, 0, v.n, p);
+         H->pre_ready = false;
+      }
    }
    amgk::reduce_partials(c->stream, p, nb, H->d_hist + slot, 1, c->d_scalars + 4096);
    AMG_HIP(hipGetLastError());
@@ -555,10 +583,7 @@ static int solve_step(amg_hier *H)
    const amg_opts &o = H->o;
    const bool precond = o.cheby_flag == 1;
    const bool one_level = !is_all_levels(o);
-   const bool reuse = one_level && !precond && o.reuse_outer_residual &&
-                      (o.smoother == AMG_JACOBI || o.smoother == AMG_SYMM_JACOBI ||
-                       o.smoother == AMG_L1_JACOBI) &&
-                      o.num_pre_smooth_sweeps > 0 && H->L > 1;
+   const bool reuse = reuse_applies(H);
    if (one_level)
       vcycle(H, precond, reuse);
    else
@@ -636,6 +661,7 @@ extern "C" int amg_solve_get_u(amg_hier *H, amg_vec *u)
 extern "C" int amg_vcycle(amg_hier *H)
 {
    AMG_ARG(H, "amg_vcycle: null hierarchy");
+   H->pre_ready = false;
    if (is_all_levels(H->o))
       sync_add_vcycle(H);
    else
@@ -650,6 +676,7 @@ extern "C" int amg_vcycle(amg_hier *H)
 static int precond_apply(amg_hier *H, const double *fin, double *out)
 {
    hipStream_t s = H->ctx->stream;
+   H->pre_ready = false;
    for (int l = 0; l < H->L; l++) {
       amgk::vset(s, H->lv[l].u, 0.0, 0, H->lv[l].n);
       H->lv[l].zero_flag = 0;

@@ -193,7 +193,9 @@ int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *level_correc
 /* EigsPower SMEM_Cheby.cpp:410-518 with this hierarchy's V-cycle as M^{-1} */
 int amg_eigs_power(amg_hier *H, int iters, double *eig_max, double *eig_min);
 /* profile: accumulated device milliseconds and launch counts of the fine-level
- * kernels (index 0 = A_0 SpMV-class passes) since the last reset */
+s * kernels since the last reset: [0] level-0 residual in the cycle, [1] level-0
+ * smoother sweeps, [2] R_0 restriction, [3] P_0 prolongation, [4] outer residual
+ * (+ fused next pre-sweep when reuse_outer_residual) */
 int amg_hier_profile_read(amg_hier *H, double *ms, long long *launches, int reset);
 
 /* ---- structured problem generator (replaces SMEM_BuildMatrix/BoomerAMGSetup

@@ -1,0 +1,47 @@
+"""Interleaved A/B timing of CSR tile-kernel configurations on the 512^3
+fine operator (y = A0 x); also checks every variant returns identical bits."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from conftest import load_package  # noqa: E402
+
+amg = load_package()
+lib = amg.lib
+lib.amg_dev_tune_name.restype = C.c_char_p
+lib.amg_dev_tune_spmv.argtypes = [C.c_void_p] * 4 + [C.c_int, C.c_int, C.POINTER(C.c_double)]
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+ctx = amg.Context(0, 2)
+g = amg.Gen(n)
+mats = {"A0": g.register(ctx, amg.AMG_GEN_A, 0), "A1": g.register(ctx, amg.AMG_GEN_A, 1),
+        "R0": g.register(ctx, amg.AMG_GEN_R, 0), "P0": g.register(ctx, amg.AMG_GEN_P, 0)}
+nv = lib.amg_dev_tune_count()
+for name, A in mats.items():
+    x = ctx.vec(np.random.default_rng(0).uniform(-1, 1, A.ncols))
+    y = ctx.vec(A.nrows)
+    ref = None
+    res = {v: [] for v in range(nv)}
+    vlist = [v for v in range(nv) if name == "A0" or not lib.amg_dev_tune_name(v).startswith(b"ABL")]
+    for r in range(rounds):
+        for v in vlist:
+            ms = C.c_double()
+            amg.check(lib.amg_dev_tune_spmv(ctx.h, A.h, x.h, y.h, v, 10, C.byref(ms)))
+            res[v].append(ms.value)
+            out = y.download()
+            if lib.amg_dev_tune_name(v).startswith(b"ABL"):
+                continue
+            if ref is None:
+                ref = out
+            elif not np.array_equal(out.view(np.uint64), ref.view(np.uint64)):
+                print(f"{name} variant {v}: RESULT MISMATCH")
+    nbytes = 12 * A.nnz + 4 * (A.nrows + 1) + 8 * A.ncols + 8 * A.nrows
+    for v in vlist:
+        t = np.median(res[v])
+        print(f"{name:3s} {lib.amg_dev_tune_name(v).decode():22s} median {t:.3f} ms  min {min(res[v]):.3f}"
+              f"  {nbytes / t / 1e6:.0f} GB/s")
+    x.free(); y.free()
