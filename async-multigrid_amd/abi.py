@@ -114,8 +114,13 @@ PROTOTYPES = {
     "amg_dist_get_u": (_i, [_p, _dp]),
     "amg_dist_hier_free": (_i, [_p]),
     "amg_dist_profile_read": (_i, [_p, _dp, _llp, _i]),
-    "amg_dist_fine_spmv": (_i, [_p, _dp, _dp]),
+    "amg_dist_fine_spmv": (_i, [_p, _i, _dp]),
+    "amg_dist_init_host": (_i, [_p, _i, _i, C.c_void_p, _p]),
+    "amg_dist_hier_set_replicate_rows": (_i, [_p, _ll]),
 }
+
+# amg_host_xchg_fn: (user, op, npeers, peers, send, send_bytes, recv, recv_bytes) -> int
+HOST_XCHG_FN = C.CFUNCTYPE(_i, _p, _i, _i, _ip, _pp, _llp, _pp, _llp)
 
 
 def header_symbols(path=HEADER):

@@ -525,7 +525,8 @@ extern "C" int amg_hybrid_jgs(amg_ctx *c, const amg_mat *A, const amg_vec *f, am
    int *d_blk = nullptr;
    AMG_HIP(hipStreamSynchronize(c->stream));
    AMG_HIP(hipMalloc((void **)&d_blk, (nblk + 1) * sizeof(int)));
-   AMG_HIP(hipMemcpy(d_blk, blk, (nblk + 1) * sizeof(int), hipMemcpyHostToDevice));
+   AMG_HIP(hipMemcpyAsync(d_blk, blk, (nblk + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
    int s = amg_hybrid_jgs_dev(c, c->stream, A, f->d, u->d, u_prev->d, u->n, d_blk, nblk, blk[0],
                               blk[nblk], diag_scale ? diag_scale->d : nullptr, weight, sweeps,
                               zero_first, reverse);

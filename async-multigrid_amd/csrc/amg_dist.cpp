@@ -1,2 +1,986 @@
-// amg_dist.cpp -- multi-GPU row-slab partition and RCCL halo exchange (placeholder, filled in next).
+// amg_dist.cpp -- multi-GPU solve phase: one process per GPU, z-slab
+// partition of every level, RCCL point-to-point ghost exchange over xGMI on a
+// communication stream overlapped with the slab-interior SpMV on the compute
+// stream, replicated coarse levels, RCCL allreduce for the residual norm.
+//
+// Reference counterparts: the DMEM message engine (DMEM_Comm.cpp:81-382
+// SendRecv / CheckInFlight / CompleteRecv), the ParCSR halo exchange hypre
+// performs inside hypre_ParCSRMatrixMatvec (called from DMEM_Add.cpp:230-308,
+// DMEM_Mult.cpp:95-261), the comm-plan construction CreateCommData_LocalRes
+// (DMEM_Setup.cpp:666-1265) and InnerProdFlag's MPI_Allreduce
+// (DMEM_Misc.cpp:414-433).  The cycle itself is SMEM_Sync_Parfor_Vcycle
+// (SMEM_Sync_AMG.cpp:8-145) with SMEM_Solve's outer loop (SMEM_Solve.cpp:128-240):
+// the same kernels as the single-GPU path on slab-local CSR whose column ids
+// were remapped to [owned | ghost] without reordering any row, so every row
+// sum keeps its order and the iterates are bit-identical to one GPU.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <vector>
+
 #include "amg_internal.h"
+
+// ---------------------------------------------------------------------------
+// transport
+// ---------------------------------------------------------------------------
+struct amg_transport {
+   int nranks = 1, rank = 0;
+   ncclComm_t comm = nullptr;
+   amg_host_xchg_fn fn = nullptr; // test transport through host memory
+   void *user = nullptr;
+   bool host() const { return fn != nullptr; }
+};
+
+#define AMG_NCCL(call)                                                                     \
+   do {                                                                                    \
+      ncclResult_t _r = (call);                                                            \
+      if (_r != ncclSuccess)                                                               \
+         return amg_set_error(AMG_ERR_RCCL, "%s:%d %s -> %s", __FILE__, __LINE__, #call,  \
+                              ncclGetErrorString(_r));                                     \
+   } while (0)
+
+extern "C" int amg_dist_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+extern "C" int amg_dist_get_unique_id(char *id)
+{
+   AMG_ARG(id, "amg_dist_get_unique_id: null buffer");
+   ncclUniqueId u;
+   AMG_NCCL(ncclGetUniqueId(&u));
+   std::memcpy(id, &u, sizeof(u));
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_init(amg_ctx *c, int nranks, int rank, const char *id)
+{
+   AMG_ARG(c && id && nranks >= 1 && rank >= 0 && rank < nranks, "amg_dist_init: bad argument");
+   AMG_ARG(!c->xport, "amg_dist_init: already initialised");
+   ncclUniqueId u;
+   std::memcpy(&u, id, sizeof(u));
+   AMG_HIP(hipSetDevice(c->device));
+   auto *t = new amg_transport();
+   t->nranks = nranks;
+   t->rank = rank;
+   ncclResult_t r = ncclCommInitRank(&t->comm, nranks, u, rank);
+   if (r != ncclSuccess) {
+      delete t;
+      return amg_set_error(AMG_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+   }
+   c->xport = t;
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_init_host(amg_ctx *c, int nranks, int rank, amg_host_xchg_fn fn, void *user)
+{
+   AMG_ARG(c && fn && nranks >= 1 && rank >= 0 && rank < nranks, "amg_dist_init_host: bad argument");
+   AMG_ARG(!c->xport, "amg_dist_init_host: already initialised");
+   auto *t = new amg_transport();
+   t->nranks = nranks;
+   t->rank = rank;
+   t->fn = fn;
+   t->user = user;
+   c->xport = t;
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_finalize(amg_ctx *c)
+{
+   if (!c || !c->xport) return AMG_OK;
+   hipStreamSynchronize(c->stream);
+   hipStreamSynchronize(c->comm_stream);
+   if (c->xport->comm) ncclCommDestroy(c->xport->comm);
+   delete c->xport;
+   c->xport = nullptr;
+   return AMG_OK;
+}
+
+// host -> device copy ordered on stream s and complete on return (a pageable
+// hipMemcpy on the null stream is not ordered against the non-blocking
+// context streams, e.g. a pending hipMemsetAsync of the same buffer)
+static int h2d(hipStream_t s, void *dst, const void *src, size_t bytes)
+{
+   if (bytes == 0) return AMG_OK;
+   AMG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   return AMG_OK;
+}
+
+static int d2h(hipStream_t s, void *dst, const void *src, size_t bytes)
+{
+   if (bytes == 0) return AMG_OK;
+   AMG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   return AMG_OK;
+}
+
+// point-to-point byte exchange with peers[i] (device buffers), on stream s
+static int xp_p2p(amg_ctx *c, hipStream_t s, int np, const int *peers, void *const *send,
+                  const long long *sbytes, void *const *recv, const long long *rbytes)
+{
+   amg_transport *t = c->xport;
+   if (np == 0) return AMG_OK;
+   if (!t->host()) {
+      AMG_NCCL(ncclGroupStart());
+      for (int i = 0; i < np; i++) {
+         if (sbytes[i] > 0) AMG_NCCL(ncclSend(send[i], (size_t)sbytes[i], ncclChar, peers[i], t->comm, s));
+         if (rbytes[i] > 0) AMG_NCCL(ncclRecv(recv[i], (size_t)rbytes[i], ncclChar, peers[i], t->comm, s));
+      }
+      AMG_NCCL(ncclGroupEnd());
+      return AMG_OK;
+   }
+   AMG_HIP(hipStreamSynchronize(s));
+   std::vector<std::vector<char>> hs(np), hr(np);
+   std::vector<const void *> sp(np);
+   std::vector<void *> rp(np);
+   for (int i = 0; i < np; i++) {
+      hs[i].resize(std::max(1LL, sbytes[i]));
+      hr[i].resize(std::max(1LL, rbytes[i]));
+      if (sbytes[i] > 0) AMG_TRY(d2h(s, hs[i].data(), send[i], sbytes[i]));
+      sp[i] = hs[i].data();
+      rp[i] = hr[i].data();
+   }
+   int st = t->fn(t->user, 0, np, peers, sp.data(), sbytes, rp.data(), rbytes);
+   if (st != 0) return amg_set_error(AMG_ERR_RCCL, "host transport p2p failed (%d)", st);
+   for (int i = 0; i < np; i++)
+      if (rbytes[i] > 0) AMG_TRY(h2d(s, recv[i], hr[i].data(), rbytes[i]));
+   return AMG_OK;
+}
+
+// in-place sum of n doubles (device) across ranks, on stream s
+static int xp_allreduce(amg_ctx *c, hipStream_t s, double *dev, int n)
+{
+   amg_transport *t = c->xport;
+   if (t->nranks == 1) return AMG_OK;
+   if (!t->host()) {
+      AMG_NCCL(ncclAllReduce(dev, dev, (size_t)n, ncclDouble, ncclSum, t->comm, s));
+      return AMG_OK;
+   }
+   AMG_HIP(hipStreamSynchronize(s));
+   std::vector<double> h(n);
+   AMG_TRY(d2h(s, h.data(), dev, n * sizeof(double)));
+   void *rp[1] = {h.data()};
+   long long b[1] = {(long long)n * 8};
+   int st = t->fn(t->user, 1, 0, nullptr, nullptr, nullptr, rp, b);
+   if (st != 0) return amg_set_error(AMG_ERR_RCCL, "host transport allreduce failed (%d)", st);
+   AMG_TRY(h2d(s, dev, h.data(), n * sizeof(double)));
+   return AMG_OK;
+}
+
+// allgather of equal-size byte blocks: recv = [rank0 block | rank1 block | ...]
+static int xp_allgather(amg_ctx *c, hipStream_t s, const void *send, void *recv, long long bytes)
+{
+   amg_transport *t = c->xport;
+   if (!t->host()) {
+      AMG_NCCL(ncclAllGather(send, recv, (size_t)bytes, ncclChar, t->comm, s));
+      return AMG_OK;
+   }
+   AMG_HIP(hipStreamSynchronize(s));
+   std::vector<char> hs(std::max(1LL, bytes)), hr(std::max(1LL, bytes * t->nranks));
+   if (bytes > 0) AMG_TRY(d2h(s, hs.data(), send, bytes));
+   const void *sp[1] = {hs.data()};
+   void *rp[1] = {hr.data()};
+   long long sb[1] = {bytes}, rb[1] = {bytes * t->nranks};
+   int st = t->fn(t->user, 2, 0, nullptr, sp, sb, rp, rb);
+   if (st != 0) return amg_set_error(AMG_ERR_RCCL, "host transport allgather failed (%d)", st);
+   if (bytes > 0)
+      AMG_TRY(h2d(s, recv, hr.data(), bytes * t->nranks));
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_allreduce_sum(amg_ctx *c, double *h, int n)
+{
+   AMG_ARG(c && c->xport && h && n >= 0, "amg_dist_allreduce_sum: not initialised");
+   double *d = c->d_scalars + 2048;
+   AMG_ARG(n <= 1024, "amg_dist_allreduce_sum: at most 1024 values");
+   AMG_HIP(hipMemcpyAsync(d, h, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+   AMG_TRY(xp_allreduce(c, c->stream, d, n));
+   AMG_HIP(hipMemcpyAsync(h, d, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_barrier(amg_ctx *c)
+{
+   double z = 0;
+   return amg_dist_allreduce_sum(c, &z, 1);
+}
+
+extern "C" int amg_dist_hier_set_replicate_rows(amg_ctx *c, long long rows)
+{
+   AMG_ARG(c && rows >= 0, "amg_dist_hier_set_replicate_rows: bad argument");
+   c->replicate_rows = rows;
+   return AMG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+__global__ void gather_k(const double *__restrict__ x, const int *__restrict__ idx,
+                         double *__restrict__ out, int n)
+{
+   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+      out[i] = x[idx[i]];
+}
+
+__global__ void scatter_blocks_k(const double *__restrict__ src, int blk, const int *__restrict__ cnt,
+                                 const int *__restrict__ dsp, int nranks, double *__restrict__ dst)
+{
+   // src = [rank q block of blk doubles], keep the first cnt[q] of each at dsp[q]
+   const int total = blk * nranks;
+   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+      const int q = i / blk, k = i - q * blk;
+      if (k < cnt[q]) dst[dsp[q] + k] = src[i];
+   }
+}
+
+__global__ void sqrt_to_k(const double *__restrict__ in, double *__restrict__ out)
+{
+   out[0] = sqrt(in[0]);
+}
+
+// ---------------------------------------------------------------------------
+// distributed matrix: slab-local rows, columns remapped to [owned | ghost]
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Partition {
+   // per level: first owned plane of every rank (size nranks + 1) and plane size
+   std::vector<std::vector<int>> z0;
+   std::vector<long long> plane;
+   long long rows_begin(int l, int r) const { return (long long)z0[l][r] * plane[l]; }
+   long long rows_end(int l, int r) const { return (long long)z0[l][r + 1] * plane[l]; }
+};
+
+struct DistMat {
+   amg_mat *A = nullptr;        // local rows, remapped columns
+   long long row0 = 0;          // first global row
+   int nrows = 0;
+   int ncol_own = 0;            // owned columns (x region [0, ncol_own))
+   int nghost = 0;              // ghost region [ncol_own, ncol_own + nghost)
+   bool replicated_cols = false; // columns index a full replicated vector
+   int b0 = 0, b1 = 0;          // interior rows [b0, b1): no ghost column
+   std::vector<int> peers;      // union of send/recv peers
+   std::vector<long long> scnt, rcnt; // doubles per peer
+   std::vector<long long> soff, roff; // offsets into sendbuf / ghost region
+   int *d_send_idx = nullptr;   // owned-column index list of all sends
+   long long nsend = 0;
+   double *sendbuf = nullptr;
+};
+
+struct DLevel {
+   int n = 0;                  // owned rows
+   long long row0 = 0;
+   int cap = 0;                // vector capacity (owned + max ghosts)
+   DistMat A, P, R;            // P: level l -> l+1 (rows = level l), R: rows = level l+1
+   double *f = nullptr, *u = nullptr, *u_alt = nullptr, *r_fine = nullptr, *l1 = nullptr;
+   int zero_flag = 0;
+};
+
+} // namespace
+
+struct amg_dist_hier {
+   amg_ctx *ctx = nullptr;
+   amg_opts o{};
+   int L = 0, Ld = 0; // levels [0, Ld) distributed, [Ld, L) replicated
+   Partition part;
+   std::vector<DLevel> lv;
+   // replicated coarse part
+   amg_hier *coarse = nullptr;
+   std::vector<amg_mat *> coarse_mats;
+   double *f_rep = nullptr;   // full level-Ld vector (allgathered restriction)
+   double *gath_buf = nullptr;
+   int gath_blk = 0;
+   int *d_gcnt = nullptr, *d_gdsp = nullptr;
+   // outer loop state
+   double *r0 = nullptr;
+   double *d_hist = nullptr;
+   int hist_cap = 1 << 16;
+   double r0norm = 0;
+   int iter = 0;
+   bool pre_ready = false, have_state = false;
+   hipEvent_t ev_pack = nullptr, ev_comm = nullptr;
+   std::vector<void *> allocs;
+   // profiling: [0] fine residual, [1] fine smoother, [2] R0, [3] P0, [4] outer residual
+   std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[5];
+   double prof_ms[5] = {0, 0, 0, 0, 0};
+   long long prof_n[5] = {0, 0, 0, 0, 0};
+};
+
+namespace {
+
+int dalloc(amg_dist_hier *D, size_t bytes, void **p)
+{
+   hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 8));
+   if (e != hipSuccess)
+      return amg_set_error(AMG_ERR_OOM, "amg_dist: allocation of %zu bytes: %s", bytes,
+                           hipGetErrorString(e));
+   D->allocs.push_back(*p);
+   AMG_HIP(hipMemsetAsync(*p, 0, std::max<size_t>(bytes, 8), D->ctx->stream));
+   return AMG_OK;
+}
+
+int dvec(amg_dist_hier *D, size_t n, double **p)
+{
+   return dalloc(D, n * sizeof(double), (void **)p);
+}
+
+// owner of global column g of a level's column space
+int owner_of(const Partition &pt, int level, long long g)
+{
+   // the rank r with z[r] <= plane < z[r+1] (empty ranges are skipped)
+   const auto &z = pt.z0[level];
+   const int zp = (int)(g / pt.plane[level]);
+   return (int)(std::upper_bound(z.begin(), z.end(), zp) - z.begin()) - 1;
+}
+
+// Build a DistMat from host CSR rows (global columns) of column level `cl`.
+int build_distmat(amg_dist_hier *D, DistMat &M, long long row0, int nrows, std::vector<int> &rp,
+                  std::vector<int> &cj, std::vector<double> &cv, int cl, bool replicated_cols)
+{
+   amg_ctx *c = D->ctx;
+   amg_transport *t = c->xport;
+   const int R = t->nranks, me = t->rank;
+   M.row0 = row0;
+   M.nrows = nrows;
+   M.replicated_cols = replicated_cols;
+   const long long nnz = rp[nrows];
+   int ncols_dev = 0;
+   std::vector<long long> ghosts;
+   if (replicated_cols) {
+      // columns index the full replicated level-cl vector
+      long long full = (long long)D->part.z0[cl][R] * D->part.plane[cl];
+      M.ncol_own = (int)full;
+      M.nghost = 0;
+      ncols_dev = (int)full;
+      M.b0 = 0;
+      M.b1 = nrows;
+   } else {
+      const long long c0 = D->part.rows_begin(cl, me), c1 = D->part.rows_end(cl, me);
+      M.ncol_own = (int)(c1 - c0);
+      for (long long k = 0; k < nnz; k++) {
+         const long long g = cj[k];
+         if (g < c0 || g >= c1) ghosts.push_back(g);
+      }
+      std::sort(ghosts.begin(), ghosts.end());
+      ghosts.erase(std::unique(ghosts.begin(), ghosts.end()), ghosts.end());
+      M.nghost = (int)ghosts.size();
+      // remap; rows keep their entry order
+      std::vector<char> has_ghost(nrows, 0);
+      for (int i = 0; i < nrows; i++)
+         for (int k = rp[i]; k < rp[i + 1]; k++) {
+            const long long g = cj[k];
+            if (g >= c0 && g < c1) {
+               cj[k] = (int)(g - c0);
+            } else {
+               const long long gi = std::lower_bound(ghosts.begin(), ghosts.end(), g) - ghosts.begin();
+               cj[k] = (int)(M.ncol_own + gi);
+               has_ghost[i] = 1;
+            }
+         }
+      // interior: the longest run of rows without ghost columns
+      int best0 = 0, best1 = 0, cur0 = 0;
+      for (int i = 0; i <= nrows; i++) {
+         if (i == nrows || has_ghost[i]) {
+            if (i - cur0 > best1 - best0) {
+               best0 = cur0;
+               best1 = i;
+            }
+            cur0 = i + 1;
+         }
+      }
+      M.b0 = best0;
+      M.b1 = best1;
+      ncols_dev = M.ncol_own + M.nghost;
+   }
+   // device CSR
+   AMG_TRY(amg_mat_create_device(c, nrows, std::max(1, ncols_dev), nnz, &M.A));
+   AMG_TRY(h2d(c->stream, M.A->rowptr, rp.data(), ((size_t)nrows + 1) * sizeof(int)));
+   if (nnz) {
+      AMG_TRY(h2d(c->stream, M.A->col, cj.data(), nnz * sizeof(int)));
+      AMG_TRY(h2d(c->stream, M.A->val, cv.data(), nnz * sizeof(double)));
+   }
+   AMG_TRY(amg_mat_finish(M.A));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   if (replicated_cols) return AMG_OK;
+
+   // ---- communication plan (CreateCommData_LocalRes analogue) ----
+   // requests per owner
+   std::vector<long long> need(R, 0);
+   std::vector<int> gown(M.nghost);
+   for (int i = 0; i < M.nghost; i++) {
+      gown[i] = owner_of(D->part, cl, ghosts[i]);
+      need[gown[i]]++;
+   }
+   // everybody learns how much every rank needs from it
+   long long *d_need = nullptr, *d_all = nullptr;
+   AMG_HIP(hipMalloc(&d_need, R * sizeof(long long)));
+   AMG_HIP(hipMalloc(&d_all, (size_t)R * R * sizeof(long long)));
+   AMG_TRY(h2d(c->stream, d_need, need.data(), R * sizeof(long long)));
+   AMG_TRY(xp_allgather(c, c->stream, d_need, d_all, R * sizeof(long long)));
+   std::vector<long long> all((size_t)R * R);
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   AMG_TRY(d2h(c->stream, all.data(), d_all, (size_t)R * R * sizeof(long long)));
+   hipFree(d_need);
+   hipFree(d_all);
+   // peers: ranks I receive from or send to
+   for (int q = 0; q < R; q++) {
+      if (q == me) continue;
+      const long long rc = need[q], sc = all[(size_t)q * R + me];
+      if (rc > 0 || sc > 0) {
+         M.peers.push_back(q);
+         M.rcnt.push_back(rc);
+         M.scnt.push_back(sc);
+      }
+   }
+   const int np = (int)M.peers.size();
+   M.roff.assign(np, 0);
+   M.soff.assign(np, 0);
+   {
+      long long ro = 0, so = 0;
+      for (int i = 0; i < np; i++) {
+         M.roff[i] = ro;
+         ro += M.rcnt[i];
+         M.soff[i] = so;
+         so += M.scnt[i];
+      }
+      M.nsend = so;
+   }
+   // exchange the request lists (global ids) and turn them into send index lists
+   std::vector<long long> req_host(M.nghost);
+   for (int i = 0; i < M.nghost; i++) req_host[i] = ghosts[i]; // already grouped by owner
+   long long *d_req = nullptr, *d_inc = nullptr;
+   AMG_HIP(hipMalloc(&d_req, std::max<long long>(1, M.nghost) * sizeof(long long)));
+   AMG_HIP(hipMalloc(&d_inc, std::max<long long>(1, M.nsend) * sizeof(long long)));
+   if (M.nghost)
+      AMG_TRY(h2d(c->stream, d_req, req_host.data(), M.nghost * sizeof(long long)));
+   {
+      std::vector<void *> sp(np), rq(np);
+      std::vector<long long> sb(np), rb(np);
+      for (int i = 0; i < np; i++) {
+         // my requests to peer i live where its ghosts start in the sorted list
+         const long long first =
+            std::lower_bound(gown.begin(), gown.end(), M.peers[i]) - gown.begin();
+         sp[i] = d_req + first;
+         sb[i] = M.rcnt[i] * (long long)sizeof(long long);
+         rq[i] = d_inc + M.soff[i];
+         rb[i] = M.scnt[i] * (long long)sizeof(long long);
+         // the ghost region for this peer starts at the same sorted position
+         M.roff[i] = first;
+      }
+      AMG_TRY(xp_p2p(c, c->stream, np, M.peers.data(), sp.data(), sb.data(), rq.data(), rb.data()));
+   }
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   std::vector<long long> inc(std::max<long long>(1, M.nsend));
+   if (M.nsend) AMG_TRY(d2h(c->stream, inc.data(), d_inc, M.nsend * sizeof(long long)));
+   hipFree(d_req);
+   hipFree(d_inc);
+   const long long c0 = D->part.rows_begin(cl, me);
+   std::vector<int> sidx(std::max<long long>(1, M.nsend));
+   for (long long k = 0; k < M.nsend; k++) {
+      const long long li = inc[k] - c0;
+      AMG_ARG(li >= 0 && li < M.ncol_own, "amg_dist: request %lld outside owned columns", inc[k]);
+      sidx[k] = (int)li;
+   }
+   AMG_TRY(dalloc(D, std::max<long long>(1, M.nsend) * sizeof(int), (void **)&M.d_send_idx));
+   if (M.nsend)
+      AMG_TRY(h2d(c->stream, M.d_send_idx, sidx.data(), M.nsend * sizeof(int)));
+   AMG_TRY(dvec(D, std::max<long long>(1, M.nsend), &M.sendbuf));
+   return AMG_OK;
+}
+
+// ghost exchange of x (owned region filled) for M: pack on the compute stream,
+// RCCL send/recv on the comm stream; the caller waits on ev_comm before the
+// boundary rows
+int halo_begin(amg_dist_hier *D, DistMat &M, double *x)
+{
+   amg_ctx *c = D->ctx;
+   if (M.replicated_cols || M.peers.empty()) return AMG_OK;
+   if (M.nsend > 0) {
+      const int nb = (int)std::min<long long>(4096, (M.nsend + 255) / 256);
+      gather_k<<<nb, 256, 0, c->stream>>>(x, M.d_send_idx, M.sendbuf, (int)M.nsend);
+   }
+   AMG_HIP(hipEventRecord(D->ev_pack, c->stream));
+   AMG_HIP(hipStreamWaitEvent(c->comm_stream, D->ev_pack, 0));
+   const int np = (int)M.peers.size();
+   std::vector<void *> sp(np), rp(np);
+   std::vector<long long> sb(np), rb(np);
+   for (int i = 0; i < np; i++) {
+      sp[i] = M.sendbuf + M.soff[i];
+      sb[i] = M.scnt[i] * 8;
+      rp[i] = x + M.ncol_own + M.roff[i];
+      rb[i] = M.rcnt[i] * 8;
+   }
+   AMG_TRY(xp_p2p(c, c->comm_stream, np, M.peers.data(), sp.data(), sb.data(), rp.data(), rb.data()));
+   AMG_HIP(hipEventRecord(D->ev_comm, c->comm_stream));
+   return AMG_OK;
+}
+
+int halo_end(amg_dist_hier *D, DistMat &M)
+{
+   if (M.replicated_cols || M.peers.empty()) return AMG_OK;
+   AMG_HIP(hipStreamWaitEvent(D->ctx->stream, D->ev_comm, 0));
+   return AMG_OK;
+}
+
+struct DProf {
+   amg_dist_hier *D;
+   int cat;
+   bool on;
+   hipEvent_t a = nullptr, b = nullptr;
+   DProf(amg_dist_hier *D_, int cat_, bool en) : D(D_), cat(cat_), on(en && D_->o.profile)
+   {
+      if (on) {
+         hipEventCreate(&a);
+         hipEventCreate(&b);
+         hipEventRecord(a, D->ctx->stream);
+      }
+   }
+   ~DProf()
+   {
+      if (on) {
+         hipEventRecord(b, D->ctx->stream);
+         D->pend[cat].push_back({a, b});
+      }
+   }
+};
+
+// interior rows first (overlapping the exchange), boundary rows after it
+template <class F>
+int split_launch(amg_dist_hier *D, DistMat &M, double *x, F launch)
+{
+   AMG_TRY(halo_begin(D, M, x));
+   launch(M.b0, M.b1, 0);
+   AMG_TRY(halo_end(D, M));
+   const int t0 = amgk::tile_blocks(M.b0, M.b1);
+   launch(0, M.b0, t0);
+   launch(M.b1, M.nrows, t0 + amgk::tile_blocks(0, M.b0));
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+int nparts(const DistMat &M)
+{
+   return amgk::tile_blocks(M.b0, M.b1) + amgk::tile_blocks(0, M.b0) +
+          amgk::tile_blocks(M.b1, M.nrows);
+}
+
+} // namespace
+
+// ---------------------------------------------------------------------------
+// construction
+// ---------------------------------------------------------------------------
+extern "C" int amg_dist_hier_create_structured(amg_ctx *c, const amg_gen *g, const amg_opts *opts,
+                                               amg_dist_hier **out)
+{
+   AMG_ARG(c && c->xport && g && opts && out, "amg_dist_hier_create_structured: bad argument");
+   AMG_ARG(opts->solver == AMG_MULT && opts->cheby_flag == 0 &&
+              (opts->smoother == AMG_JACOBI || opts->smoother == AMG_L1_JACOBI),
+           "amg_dist: MULT with Jacobi / L1 Jacobi is supported");
+   amg_transport *t = c->xport;
+   const int R = t->nranks, me = t->rank;
+   auto D = std::make_unique<amg_dist_hier>();
+   D->ctx = c;
+   D->o = *opts;
+   D->L = amg_gen_num_levels(g);
+   const int L = D->L;
+   // plane partition: level 0 split evenly; coarse plane k follows the owner
+   // of fine plane 2k+1 (the fine point it is injected from under linear
+   // interpolation; 2k under aggregation)
+   D->part.z0.resize(L);
+   D->part.plane.resize(L);
+   std::vector<std::array<int, 3>> dims(L);
+   for (int l = 0; l < L; l++) {
+      amg_gen_dims(g, l, &dims[l][0], &dims[l][1], &dims[l][2]);
+      D->part.plane[l] = (long long)dims[l][0] * dims[l][1];
+   }
+   {
+      const int nz = dims[0][2];
+      D->part.z0[0].resize(R + 1);
+      for (int r = 0; r <= R; r++) D->part.z0[0][r] = (int)((long long)nz * r / R);
+      for (int l = 1; l < L; l++) {
+         const int nzc = dims[l][2], nzf = dims[l - 1][2];
+         std::vector<int> own(nzc);
+         for (int k = 0; k < nzc; k++) {
+            const int fz = std::min(nzf - 1, 2 * k + (nzc * 2 <= nzf ? 1 : 0));
+            const auto &zf = D->part.z0[l - 1];
+            int r = 0;
+            while (r + 1 < R && zf[r + 1] <= fz) r++;
+            own[k] = r;
+         }
+         D->part.z0[l].assign(R + 1, nzc);
+         for (int r = R - 1; r >= 0; r--) {
+            // first plane owned by r (planes are monotone in r)
+            int first = D->part.z0[l][r + 1];
+            for (int k = 0; k < nzc; k++)
+               if (own[k] >= r) {
+                  first = k;
+                  break;
+               }
+            D->part.z0[l][r] = std::min(first, D->part.z0[l][r + 1]);
+         }
+         D->part.z0[l][0] = 0;
+      }
+   }
+   // replicated coarse levels: total rows below the threshold (and always the coarsest)
+   D->Ld = L;
+   for (int l = 0; l < L; l++)
+      if ((long long)dims[l][0] * dims[l][1] * dims[l][2] < c->replicate_rows) {
+         D->Ld = l;
+         break;
+      }
+   if (D->Ld == 0) D->Ld = 1; // the fine level is always distributed
+   if (D->Ld > L - 1 && L > 1) D->Ld = L - 1; // keep at least the coarsest replicated
+   if (L == 1) D->Ld = 1;
+   const int Ld = D->Ld;
+   D->lv.resize(Ld);
+   AMG_HIP(hipEventCreateWithFlags(&D->ev_pack, hipEventDisableTiming));
+   AMG_HIP(hipEventCreateWithFlags(&D->ev_comm, hipEventDisableTiming));
+
+   auto host_rows = [&](int which, int level, int z0, int z1, std::vector<int> &rp,
+                        std::vector<int> &cj, std::vector<double> &cv) -> int {
+      const long long nnz = amg_gen_nnz(g, which, level, z0, z1);
+      AMG_ARG(nnz >= 0, "amg_dist: generator: %s", amg_last_error());
+      const auto &d = (which == AMG_GEN_R) ? dims[level + 1] : dims[level];
+      const long long nr = (long long)d[0] * d[1] * (z1 - z0);
+      rp.assign(nr + 1, 0);
+      cj.assign(std::max(1LL, nnz), 0);
+      cv.assign(std::max(1LL, nnz), 0.0);
+      if (nr > 0) AMG_TRY(amg_gen_fill(g, which, level, z0, z1, rp.data(), cj.data(), cv.data(), 0));
+      return AMG_OK;
+   };
+
+   std::vector<int> rp, cj;
+   std::vector<double> cv;
+   for (int l = 0; l < Ld; l++) {
+      DLevel &v = D->lv[l];
+      const int z0 = D->part.z0[l][me], z1 = D->part.z0[l][me + 1];
+      v.row0 = (long long)z0 * D->part.plane[l];
+      v.n = (int)((long long)(z1 - z0) * D->part.plane[l]);
+      AMG_TRY(host_rows(AMG_GEN_A, l, z0, z1, rp, cj, cv));
+      AMG_TRY(build_distmat(D.get(), v.A, v.row0, v.n, rp, cj, cv, l, false));
+      if (l < L - 1) {
+         AMG_TRY(host_rows(AMG_GEN_P, l, z0, z1, rp, cj, cv));
+         AMG_TRY(build_distmat(D.get(), v.P, v.row0, v.n, rp, cj, cv, l + 1, l + 1 >= Ld));
+         const int cz0 = D->part.z0[l + 1][me], cz1 = D->part.z0[l + 1][me + 1];
+         AMG_TRY(host_rows(AMG_GEN_R, l, cz0, cz1, rp, cj, cv));
+         AMG_TRY(build_distmat(D.get(), v.R, (long long)cz0 * D->part.plane[l + 1],
+                               (int)((long long)(cz1 - cz0) * D->part.plane[l + 1]), rp, cj, cv, l,
+                               false));
+      }
+   }
+   // vector capacities: owned + the largest ghost region of any matrix reading them
+   for (int l = 0; l < Ld; l++) {
+      DLevel &v = D->lv[l];
+      int g_max = v.A.nghost;
+      if (l < L - 1) g_max = std::max(g_max, v.R.nghost);
+      if (l > 0) g_max = std::max(g_max, D->lv[l - 1].P.nghost);
+      v.cap = v.n + g_max;
+      AMG_TRY(dvec(D.get(), v.cap, &v.f));
+      AMG_TRY(dvec(D.get(), v.cap, &v.u));
+      AMG_TRY(dvec(D.get(), v.cap, &v.u_alt));
+      AMG_TRY(dvec(D.get(), v.cap, &v.r_fine));
+      AMG_TRY(dvec(D.get(), std::max(1, v.n), &v.l1));
+      amgk::l1_norms(c->stream, v.A.A, v.l1);
+   }
+   AMG_TRY(dvec(D.get(), D->lv[0].cap, &D->r0));
+   AMG_TRY(dvec(D.get(), D->hist_cap, &D->d_hist));
+   // replicated coarse hierarchy (identical on every rank, no communication)
+   if (Ld < L) {
+      const int Lc = L - Ld;
+      std::vector<amg_mat *> As(Lc), Ps(std::max(1, Lc - 1)), Rs(std::max(1, Lc - 1));
+      for (int l = Ld; l < L; l++) {
+         AMG_TRY(amg_gen_register(c, g, AMG_GEN_A, l, 0, dims[l][2], &As[l - Ld]));
+         D->coarse_mats.push_back(As[l - Ld]);
+         if (l < L - 1) {
+            AMG_TRY(amg_gen_register(c, g, AMG_GEN_P, l, 0, dims[l][2], &Ps[l - Ld]));
+            AMG_TRY(amg_gen_register(c, g, AMG_GEN_R, l, 0, dims[l + 1][2], &Rs[l - Ld]));
+            D->coarse_mats.push_back(Ps[l - Ld]);
+            D->coarse_mats.push_back(Rs[l - Ld]);
+         }
+      }
+      amg_opts co = *opts;
+      co.profile = 0;
+      co.reuse_outer_residual = 0;
+      AMG_TRY(amg_hier_create(c, Lc, As.data(), Ps.data(), Rs.data(), &co, &D->coarse));
+      const long long nfull = (long long)dims[Ld][0] * dims[Ld][1] * dims[Ld][2];
+      AMG_TRY(dvec(D.get(), nfull, &D->f_rep));
+      // allgather blocks padded to the largest owned row count at level Ld
+      int blk = 0;
+      std::vector<int> cnt(R), dsp(R);
+      for (int r = 0; r < R; r++) {
+         cnt[r] = (int)(D->part.rows_end(Ld, r) - D->part.rows_begin(Ld, r));
+         dsp[r] = (int)D->part.rows_begin(Ld, r);
+         blk = std::max(blk, cnt[r]);
+      }
+      D->gath_blk = blk;
+      AMG_TRY(dvec(D.get(), (size_t)blk * (R + 1), &D->gath_buf));
+      AMG_TRY(dalloc(D.get(), R * sizeof(int), (void **)&D->d_gcnt));
+      AMG_TRY(dalloc(D.get(), R * sizeof(int), (void **)&D->d_gdsp));
+      AMG_TRY(h2d(c->stream, D->d_gcnt, cnt.data(), R * sizeof(int)));
+      AMG_TRY(h2d(c->stream, D->d_gdsp, dsp.data(), R * sizeof(int)));
+   }
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   *out = D.release();
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_hier_free(amg_dist_hier *D)
+{
+   if (!D) return AMG_OK;
+   hipStreamSynchronize(D->ctx->stream);
+   hipStreamSynchronize(D->ctx->comm_stream);
+   for (auto &v : D->lv)
+      for (DistMat *M : {&v.A, &v.P, &v.R})
+         if (M->A) amg_mat_free(M->A);
+   if (D->coarse) amg_hier_free(D->coarse);
+   for (auto *m : D->coarse_mats) amg_mat_free(m);
+   for (void *p : D->allocs) hipFree(p);
+   for (int k = 0; k < 5; k++)
+      for (auto &e : D->pend[k]) {
+         hipEventDestroy(e.first);
+         hipEventDestroy(e.second);
+      }
+   if (D->ev_pack) hipEventDestroy(D->ev_pack);
+   if (D->ev_comm) hipEventDestroy(D->ev_comm);
+   delete D;
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_hier_local_rows(amg_dist_hier *D, int level, int *row0, int *nrows)
+{
+   AMG_ARG(D && level >= 0 && level < D->L, "amg_dist_hier_local_rows: bad level");
+   const int me = D->ctx->xport->rank;
+   if (row0) *row0 = (int)D->part.rows_begin(level, me);
+   if (nrows) *nrows = (int)(D->part.rows_end(level, me) - D->part.rows_begin(level, me));
+   return AMG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// cycle
+// ---------------------------------------------------------------------------
+namespace {
+
+int d_spgemv(amg_dist_hier *D, DistMat &M, double *x, const double *b, const amgk::Gemv &g,
+             double *y, double *partials)
+{
+   hipStream_t s = D->ctx->stream;
+   return split_launch(D, M, x, [&](int rb, int re, int poff) {
+      amgk::spgemv(s, M.A, x, b, g, y, rb, re, partials ? partials + poff : nullptr);
+   });
+}
+
+bool d_reuse(const amg_dist_hier *D)
+{
+   return D->o.reuse_outer_residual && D->o.num_pre_smooth_sweeps > 0;
+}
+
+// SMEM_Sync_Parfor_Jacobi on a distributed level (ping-pong)
+int d_smooth(amg_dist_hier *D, int l, const double *f, int sweeps, bool allow_reuse)
+{
+   DLevel &v = D->lv[l];
+   hipStream_t s = D->ctx->stream;
+   const bool l1 = D->o.smoother == AMG_L1_JACOBI;
+   for (int k = 0; k < sweeps; k++) {
+      if (k == 0 && v.zero_flag == 1) {
+         amgk::jacobi_zero(s, v.A.A->diag, f, l1 ? v.l1 : nullptr, D->o.smooth_weight, v.u, 0, v.n, 0);
+      } else if (k == 0 && allow_reuse && D->pre_ready) {
+         std::swap(v.u, v.u_alt);
+         D->pre_ready = false;
+      } else {
+         DProf pr(D, 1, l == 0);
+         double *x = v.u, *out = v.u_alt;
+         AMG_TRY(split_launch(D, v.A, x, [&](int rb, int re, int) {
+            amgk::jacobi_sweep(s, v.A.A, f, x, l1 ? v.l1 : nullptr, D->o.smooth_weight, out, rb, re);
+         }));
+         std::swap(v.u, v.u_alt);
+      }
+   }
+   return AMG_OK;
+}
+
+int d_vcycle(amg_dist_hier *D)
+{
+   amg_ctx *c = D->ctx;
+   hipStream_t s = c->stream;
+   const int L = D->L, Ld = D->Ld;
+   const amgk::Gemv res_mode = amgk::gemv_mode(-1.0, 1.0);
+   const amgk::Gemv mv_mode = amgk::gemv_mode(1.0, 0.0);
+   const amgk::Gemv pro_mode = amgk::gemv_mode(1.0, 1.0);
+   for (int l = 0; l < Ld && l < L - 1; l++) {
+      DLevel &v = D->lv[l];
+      v.zero_flag = (l == 0) ? 0 : 1;
+      AMG_TRY(d_smooth(D, l, v.f, D->o.num_pre_smooth_sweeps, l == 0 && d_reuse(D)));
+      {
+         DProf pr(D, 0, l == 0);
+         AMG_TRY(d_spgemv(D, v.A, v.u, v.f, res_mode, v.r_fine, nullptr));
+      }
+      {
+         DProf pr(D, 2, l == 0);
+         double *dst = (l + 1 < Ld) ? D->lv[l + 1].f : D->gath_buf + (size_t)D->gath_blk * c->xport->nranks;
+         AMG_TRY(d_spgemv(D, v.R, v.r_fine, nullptr, mv_mode, dst, nullptr));
+         if (l + 1 == Ld) {
+            // assemble the replicated level-Ld right-hand side on every rank
+            const int R = c->xport->nranks;
+            AMG_TRY(xp_allgather(c, s, dst, D->gath_buf, (long long)D->gath_blk * 8));
+            scatter_blocks_k<<<std::max(1, std::min(4096, (D->gath_blk * R + 255) / 256)), 256, 0, s>>>(
+               D->gath_buf, D->gath_blk, D->d_gcnt, D->d_gdsp, R, D->f_rep);
+         }
+      }
+   }
+   const double *u_rep = nullptr;
+   if (Ld < L) {
+      AMG_TRY(amg_hier_subcycle(D->coarse, s, D->f_rep, &u_rep));
+   } else {
+      // single distributed level: SMEM_Sync_Parfor_Vcycle smooths the coarsest
+      DLevel &v = D->lv[L - 1];
+      AMG_TRY(d_smooth(D, L - 1, v.f, D->o.num_pre_smooth_sweeps + D->o.num_post_smooth_sweeps, false));
+   }
+   for (int l = std::min(Ld, L - 1) - 1; l >= 0; l--) {
+      DLevel &v = D->lv[l];
+      v.zero_flag = 0;
+      {
+         DProf pr(D, 3, l == 0);
+         double *xc = (l + 1 < Ld) ? D->lv[l + 1].u : const_cast<double *>(u_rep);
+         AMG_TRY(d_spgemv(D, v.P, xc, v.u, pro_mode, v.u, nullptr));
+      }
+      AMG_TRY(d_smooth(D, l, v.f, D->o.num_post_smooth_sweeps, false));
+   }
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+int d_outer_residual(amg_dist_hier *D, int slot)
+{
+   amg_ctx *c = D->ctx;
+   hipStream_t s = c->stream;
+   DLevel &v = D->lv[0];
+   double *p;
+   const int np = nparts(v.A);
+   AMG_TRY(amg_ctx_partials(c, np + 1, &p));
+   {
+      DProf pr(D, 4, true);
+      if (d_reuse(D) && D->L > 1) {
+         const bool l1 = D->o.smoother == AMG_L1_JACOBI;
+         double *x = v.u, *un = v.u_alt;
+         AMG_TRY(split_launch(D, v.A, x, [&](int rb, int re, int poff) {
+            amgk::residual_jacobi(s, v.A.A, v.f, x, l1 ? v.l1 : nullptr, D->o.smooth_weight, D->r0,
+                                  un, rb, re, p + poff);
+         }));
+         D->pre_ready = true;
+      } else {
+         AMG_TRY(d_spgemv(D, v.A, v.u, v.f, amgk::gemv_mode(-1.0, 1.0), D->r0, p));
+         D->pre_ready = false;
+      }
+   }
+   double *sum = D->d_hist + slot;
+   amgk::reduce_partials(s, p, np, sum, 0, c->d_scalars + 4096);
+   AMG_TRY(xp_allreduce(c, s, sum, 1));
+   sqrt_to_k<<<1, 1, 0, s>>>(sum, sum);
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+} // namespace
+
+extern "C" int amg_dist_solve_start(amg_dist_hier *D, const double *f_local, double *r0norm)
+{
+   AMG_ARG(D && f_local, "amg_dist_solve_start: null argument");
+   amg_ctx *c = D->ctx;
+   for (auto &v : D->lv) {
+      for (double *p : {v.f, v.u, v.u_alt, v.r_fine}) amgk::vset(c->stream, p, 0.0, 0, v.cap);
+      v.zero_flag = 0;
+   }
+   AMG_TRY(h2d(D->ctx->stream, D->lv[0].f, f_local, (size_t)D->lv[0].n * sizeof(double)));
+   // InitVectors on the replicated levels (the coarsest iterate carries over
+   // between cycles, so a new solve starts it from zero as one GPU does)
+   if (D->coarse) AMG_TRY(amg_hier_reset(D->coarse));
+   D->iter = 0;
+   AMG_TRY(d_outer_residual(D, 0));
+   AMG_HIP(hipMemcpyAsync(c->h_pinned, D->d_hist, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   D->r0norm = c->h_pinned[0];
+   D->have_state = true;
+   if (r0norm) *r0norm = D->r0norm;
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_solve_iterate(amg_dist_hier *D, int k)
+{
+   AMG_ARG(D && D->have_state, "amg_dist_solve_iterate: call amg_dist_solve_start first");
+   for (int i = 0; i < k; i++) {
+      AMG_TRY(d_vcycle(D));
+      D->iter++;
+      AMG_TRY(d_outer_residual(D, D->iter % (D->hist_cap - 1)));
+   }
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_solve_resnorm(amg_dist_hier *D, double *out)
+{
+   AMG_ARG(D && out && D->have_state, "amg_dist_solve_resnorm: no solve state");
+   amg_ctx *c = D->ctx;
+   AMG_HIP(hipMemcpyAsync(c->h_pinned, D->d_hist + D->iter % (D->hist_cap - 1), sizeof(double),
+                          hipMemcpyDeviceToHost, c->stream));
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   *out = c->h_pinned[0];
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_get_u(amg_dist_hier *D, double *u_local)
+{
+   AMG_ARG(D && u_local, "amg_dist_get_u: null argument");
+   AMG_HIP(hipStreamSynchronize(D->ctx->stream));
+   AMG_TRY(d2h(D->ctx->stream, u_local, D->lv[0].u, (size_t)D->lv[0].n * sizeof(double)));
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_profile_read(amg_dist_hier *D, double *ms, long long *launches, int reset)
+{
+   AMG_ARG(D, "amg_dist_profile_read: null hierarchy");
+   AMG_HIP(hipStreamSynchronize(D->ctx->stream));
+   for (int k = 0; k < 5; k++) {
+      for (auto &e : D->pend[k]) {
+         float t = 0.f;
+         hipEventSynchronize(e.second);
+         if (hipEventElapsedTime(&t, e.first, e.second) == hipSuccess) {
+            D->prof_ms[k] += t;
+            D->prof_n[k]++;
+         }
+         hipEventDestroy(e.first);
+         hipEventDestroy(e.second);
+      }
+      D->pend[k].clear();
+      if (ms) ms[k] = D->prof_ms[k];
+      if (launches) launches[k] = D->prof_n[k];
+      if (reset) {
+         D->prof_ms[k] = 0;
+         D->prof_n[k] = 0;
+      }
+   }
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_fine_spmv(amg_dist_hier *D, int reps, double *ms)
+{
+   AMG_ARG(D && ms && reps >= 1, "amg_dist_fine_spmv: bad argument");
+   amg_ctx *c = D->ctx;
+   DLevel &v = D->lv[0];
+   hipEvent_t a, b;
+   AMG_HIP(hipEventCreate(&a));
+   AMG_HIP(hipEventCreate(&b));
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   AMG_HIP(hipEventRecord(a, c->stream));
+   for (int r = 0; r < reps; r++) AMG_TRY(d_spgemv(D, v.A, v.u, nullptr, mv, v.r_fine, nullptr));
+   AMG_HIP(hipEventRecord(b, c->stream));
+   AMG_HIP(hipEventSynchronize(b));
+   float t = 0.f;
+   AMG_HIP(hipEventElapsedTime(&t, a, b));
+   hipEventDestroy(a);
+   hipEventDestroy(b);
+   *ms = (double)t / reps;
+   return AMG_OK;
+}

@@ -42,7 +42,11 @@ constexpr int AMG_CHUNK = 2048;
 // device arrays of col/val are padded so 16-byte vector loads past nnz stay in bounds
 constexpr int AMG_NNZ_PAD = 8;
 
+struct amg_transport; // amg_dist.cpp: RCCL communicator or host-callback test transport
+
 struct amg_ctx {
+   amg_transport *xport = nullptr;
+   long long replicate_rows = 1LL << 18;
    int device = 0;
    hipStream_t stream = nullptr;           // compute stream (all sync work)
    std::vector<hipStream_t> level_streams; // async additive: one per level
@@ -75,6 +79,15 @@ struct amg_vec {
 
 // workspace
 int amg_ctx_partials(amg_ctx *ctx, size_t n, double **out);
+// device CSR allocation (+ diagonal extraction) for in-library builders
+int amg_mat_create_device(amg_ctx *c, int nrows, int ncols, long long nnz, amg_mat **out);
+int amg_mat_finish(amg_mat *A);
+// coarse sub-cycle of a hierarchy whose level 0 is an inner level of a larger
+// one: f_dev -> level-0 correction (zero start, SMEM_Sync_Parfor_Vcycle from
+// that level down); returns the level-0 iterate pointer in *u_dev
+int amg_hier_subcycle(amg_hier *H, hipStream_t s, const double *f_dev, const double **u_dev);
+// InitVectors: zero every level vector of H (start of a new solve)
+int amg_hier_reset(amg_hier *H);
 
 // ---------------------------------------------------------------------------
 // kernel launchers (amg_kernels.hip); all asynchronous on stream s

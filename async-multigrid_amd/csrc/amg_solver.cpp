@@ -658,6 +658,29 @@ extern "C" int amg_solve_get_u(amg_hier *H, amg_vec *u)
    return AMG_OK;
 }
 
+int amg_hier_subcycle(amg_hier *H, hipStream_t, const double *f_dev, const double **u_dev)
+{
+   // level 0 of H is an inner level of a larger cycle: zero-guess pre-sweep
+   // (zero_flags = 1 for l > 0, SMEM_Sync_AMG.cpp:29-32) on the restricted
+   // residual, which precond mode reads from r0 -- except a one-level H, whose
+   // only level is the coarsest and smooths its own f
+   amgk::vcopy(H->ctx->stream, f_dev, H->L == 1 ? H->lv[0].f : H->r0, 0, H->lv[0].n);
+   H->pre_ready = false;
+   vcycle(H, true, false);
+   *u_dev = H->lv[0].u;
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
+int amg_hier_reset(amg_hier *H)
+{
+   init_vectors(H);
+   H->pre_ready = false;
+   H->have_state = false;
+   AMG_HIP(hipGetLastError());
+   return AMG_OK;
+}
+
 extern "C" int amg_vcycle(amg_hier *H)
 {
    AMG_ARG(H, "amg_vcycle: null hierarchy");

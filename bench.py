@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-cycles", type=int, default=2)
     p.add_argument("--spmv-reps", type=int, default=20)
+    p.add_argument("--force-dist", type=int, default=0,
+                   help="run the distributed (RCCL) path even at one rank")
     return p.parse_args()
 
 
@@ -81,7 +83,10 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world > 1:
+    if world > 1 or args.force_dist:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
         import bench_dist
         return bench_dist.main(args, world, rank)
 

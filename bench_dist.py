@@ -1,0 +1,121 @@
+"""bench_dist.py -- the N>1 leg of bench.py (launched by torchrun, one rank per GPU).
+
+The 512^3 problem is split into z-slabs (strong scaling).  Every rank builds
+its slab rows of every distributed level from the structured generator, the
+RCCL communicator is created from a unique id broadcast over the gloo group
+torchrun sets up, and each step is one SMEM_Solve outer iteration of the
+slab-distributed V-cycle (ghost rows over RCCL p2p on a communication stream,
+overlapped with the slab interior; replicated coarse levels; RCCL allreduce
+of the residual norm).  Time = max over ranks of the K timed steps, bracketed
+by barriers and device synchronisation.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main(args, world, rank):
+    import torch
+    import torch.distributed as tdist
+    from conftest import load_package
+    from bench import METRIC, HBM_PEAK_GBS
+
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    amg = load_package()
+    n = args.n
+    t0 = time.time()
+    ctx = amg.Context(device=local, nstreams=2)
+
+    def bcast(obj):
+        lst = [obj]
+        tdist.broadcast_object_list(lst, src=0)
+        return lst[0]
+
+    amg.dist.init_rccl(ctx, world, rank, bcast)
+    gen = amg.Gen(n, interp=amg.AMG_INTERP_LINEAR)
+    opts = amg.default_opts(smooth_weight=args.smooth_weight, num_cycles=1 << 30, tol=0.0,
+                            reuse_outer_residual=args.reuse_outer_residual, profile=1)
+    D = amg.dist.DistHier(ctx, gen, opts)
+    z0, z1 = D.row0 // (n * n), (D.row0 + D.n0) // (n * n)
+    nnz_local = amg.lib.amg_gen_nnz(gen.h, amg.AMG_GEN_A, 0, z0, z1)
+    if rank == 0:
+        log(f"[dist] {world} ranks, {gen.L} levels, slab {D.n0} rows / {nnz_local} nnz on rank 0; "
+            f"setup {time.time() - t0:.1f}s")
+    f = amg.rhs_rand(D.row0, D.row0 + D.n0)
+    r0 = D.solve_start(f)
+    D.iterate(args.warmup)
+    amg.dist.barrier(ctx)
+    D.profile(reset=True)
+    tdist.barrier()
+    torch.cuda.synchronize(local)
+    t1 = time.perf_counter()
+    D.iterate(args.steps)
+    amg.dist.barrier(ctx)
+    torch.cuda.synchronize(local)
+    t2 = time.perf_counter()
+    tdist.barrier()
+    dt = torch.tensor([t2 - t1], dtype=torch.float64)
+    tdist.all_reduce(dt, op=tdist.ReduceOp.MAX)
+    dt = float(dt.item())
+    rn = D.resnorm()
+    ms, launches = D.profile(reset=True)
+    res_ms = ms[0] / max(launches[0], 1)
+    res_bytes = 12 * nnz_local + 28 * D.n0 + 4
+    spmv_ms = D.fine_spmv_ms(args.spmv_reps)
+    spmv_bytes = 12 * nnz_local + 20 * D.n0 + 4
+    # aggregate fine SpMV rate: all ranks' algorithmic bytes over the slowest rank's time
+    agg = torch.tensor([float(spmv_bytes), spmv_ms, float(res_bytes), res_ms], dtype=torch.float64)
+    parts = [torch.zeros_like(agg) for _ in range(world)]
+    tdist.all_gather(parts, agg)
+    P = torch.stack(parts).numpy()
+    D.free()
+    amg.dist.finalize(ctx)
+    ctx.close()
+    if rank == 0:
+        value = args.steps / dt
+        spmv_gbs = P[:, 0].sum() / (P[:, 1].max() * 1e-3) / 1e9
+        res_gbs = P[:, 2].sum() / (P[:, 3].max() * 1e-3) / 1e9
+        ach0 = res_bytes / (res_ms * 1e-3) / 1e9
+        log(f"[dist] {args.steps} steps in {dt * 1e3:.2f} ms -> {value:.2f} it/s; relres {rn / r0:.3e}; "
+            f"fine SpMV aggregate {spmv_gbs:.0f} GB/s")
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "V-cycle iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (7-pt Laplacian, RandDouble(-1,1) RHS after srand(0))",
+            "config": {"workload": f"{n}^3 7-pt Laplacian, SMEM_Solve MULT V(1,1) Jacobi "
+                                   f"w={args.smooth_weight}, {gen.L}-level geometric Galerkin "
+                                   f"hierarchy, z-slab partition, RCCL ghost exchange",
+                       "n": n, "levels": gen.L, "parallelism": f"slab{world}",
+                       "reuse_outer_residual": args.reuse_outer_residual},
+            "fine_spmv": {"gbs_aggregate": spmv_gbs, "ms_max": float(P[:, 1].max()),
+                          "frac_per_gpu": spmv_gbs / world / HBM_PEAK_GBS},
+            "roofline": {"bound": "hbm", "kernel": "fine-grid residual SpGEMV r = f - A0 u (rank 0 slab, "
+                                                   "incl. ghost exchange wait)",
+                         "achieved": ach0, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach0 / HBM_PEAK_GBS, "traffic": None,
+                         "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms,
+                         "aggregate_gbs": res_gbs},
+            "cpu_baseline": None,
+            "final_relres": rn / r0,
+        }
+        print(json.dumps(out), flush=True)
+    tdist.destroy_process_group()

@@ -221,6 +221,51 @@ int amg_gen_register(amg_ctx *ctx, const amg_gen *g, int which, int level, int z
 /* RHS: RandDouble(lo,hi) after srand(0) (SMEM_Setup.cpp:1729-1745), rows [r0,r1) of the global sequence */
 int amg_rhs_rand(long long r0, long long r1, double lo, double hi, double *out);
 
+/* ---- multi-GPU (one process per GPU) ------------------------------------------
+ * Replaces the DMEM_* communication of the reference (DMEM_Comm.cpp:81-382
+ * SendRecv/CompleteRecv, the hypre ParCSR halo exchange inside
+ * hypre_ParCSRMatrixMatvec called from DMEM_Add.cpp:230-308, and the
+ * InnerProdFlag allreduce DMEM_Misc.cpp:414-433).  Every level is split into
+ * z-plane slabs; each SpMV exchanges its ghost rows point-to-point over RCCL
+ * (xGMI) on a communication stream while the slab interior is computed on the
+ * compute stream.  Levels below a size threshold are replicated on every rank
+ * (one allgather of the restricted residual per cycle) so the coarse cycle
+ * needs no communication.  Per-row summation order is unchanged, so iterates
+ * are bit-identical to the single-GPU solve. */
+int amg_dist_unique_id_size(void);
+int amg_dist_get_unique_id(char *id);                 /* rank 0, then broadcast the bytes */
+int amg_dist_init(amg_ctx *ctx, int nranks, int rank, const char *id); /* RCCL communicator */
+/* test transport: exchanges go through host memory and a user callback
+ * (lets several ranks share one GPU); op 0 = point-to-point (send[i] to
+ * peers[i], recv[i] from peers[i]), 1 = allreduce-sum of ndouble doubles in
+ * recv[0], 2 = allgather of equal-size byte blocks (send[0] -> recv[0]) */
+typedef int (*amg_host_xchg_fn)(void *user, int op, int npeers, const int *peers,
+                                const void *const *send, const long long *send_bytes,
+                                void *const *recv, const long long *recv_bytes);
+int amg_dist_init_host(amg_ctx *ctx, int nranks, int rank, amg_host_xchg_fn fn, void *user);
+int amg_dist_finalize(amg_ctx *ctx);
+int amg_dist_allreduce_sum(amg_ctx *ctx, double *host_vals, int n);
+int amg_dist_barrier(amg_ctx *ctx);
+/* distributed hierarchy of a structured problem: rank r owns the z-planes
+ * the partition gives it at every level; levels with fewer than
+ * replicate_rows rows are replicated (0: default 2^18) */
+typedef struct amg_dist_hier amg_dist_hier;
+int amg_dist_hier_create_structured(amg_ctx *ctx, const amg_gen *gen, const amg_opts *opts,
+                                    amg_dist_hier **out);
+int amg_dist_hier_set_replicate_rows(amg_ctx *ctx, long long rows);
+int amg_dist_hier_free(amg_dist_hier *D);
+/* rows [row0, row0 + nrows) of the global level-0 vector this rank owns */
+int amg_dist_hier_local_rows(amg_dist_hier *D, int level, int *row0, int *nrows);
+/* SMEM_Solve on the distributed hierarchy: f/u are this rank's level-0 rows */
+int amg_dist_solve_start(amg_dist_hier *D, const double *f_local, double *r0norm);
+int amg_dist_solve_iterate(amg_dist_hier *D, int k);
+int amg_dist_solve_resnorm(amg_dist_hier *D, double *out);
+int amg_dist_get_u(amg_dist_hier *D, double *u_local);
+int amg_dist_profile_read(amg_dist_hier *D, double *ms, long long *launches, int reset);
+/* y = A_0 x on the distributed fine operator (halo exchange + interior/boundary
+ * split); *ms = average device milliseconds over reps */
+int amg_dist_fine_spmv(amg_dist_hier *D, int reps, double *ms);
+
 #ifdef __cplusplus
 }
 #endif

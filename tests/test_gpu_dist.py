@@ -1,0 +1,187 @@
+"""Multi-rank solve phase on the MI355X: slab-distributed V-cycle vs one GPU.
+
+Several ranks run as threads of this one process, each with its own context
+(compute + communication streams) on cuda:0, exchanging ghost rows, the
+replicated-level right-hand side and norms through ``dist.ThreadMailbox``
+(the host transport; RCCL refuses two ranks on one device, and the
+ring/xGMI path is exercised by bench.py --gpus N).  The distributed cycle
+keeps every row sum in the single-GPU order, so the assembled iterate must be
+BIT-IDENTICAL to the single-GPU SMEM_Solve iterate (which the solve tests pin
+to the oracle); residual norms are sums over ranks, compared at rtol 1e-12.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from test_gpu_kernels import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+def run_ranks(nranks, fn):
+    out, errs = [None] * nranks, []
+
+    def body(r):
+        try:
+            out[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errs.append((r, e))
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not errs, errs
+    return out
+
+
+def single_gpu(amg, ctx, gen, opts, f, cycles):
+    H = amg.build_hierarchy(ctx, gen, opts)
+    fv, uv = ctx.vec(f), ctx.vec(np.zeros(f.size))
+    r0 = H.solve_start(fv, uv)
+    hist = [r0]
+    for _ in range(cycles):
+        H.iterate(1)
+        hist.append(H.resnorm())
+    out = ctx.vec(f.size)
+    H.get_u(out)
+    u = out.download()
+    H.free()
+    return u, np.array(hist)
+
+
+def distributed(amg, gen, opts, f, cycles, nranks, replicate_rows):
+    hub = amg.dist.ThreadMailbox(nranks)
+
+    def rank(r):
+        ctx = amg.Context(0, nstreams=2)
+        tr = amg.dist.HostTransport(hub, r)
+        amg.dist.init_host(ctx, nranks, r, tr)
+        amg.dist.set_replicate_rows(ctx, replicate_rows)
+        D = amg.dist.DistHier(ctx, gen, opts)
+        r0 = D.solve_start(f[D.row0:D.row0 + D.n0])
+        hist = [r0]
+        for _ in range(cycles):
+            D.iterate(1)
+            hist.append(D.resnorm())
+        u = D.get_u()
+        row0 = D.row0
+        D.free()
+        amg.dist.finalize(ctx)
+        ctx.close()
+        if tr.error is not None:
+            raise tr.error
+        return row0, u, np.array(hist)
+
+    res = run_ranks(nranks, rank)
+    res.sort(key=lambda t: t[0])
+    u = np.concatenate([t[1] for t in res])
+    for t in res[1:]:
+        np.testing.assert_array_equal(t[2], res[0][2])  # every rank sees the same norms
+    return u, res[0][2]
+
+
+CASES = [
+    # (dims, interp, nranks, replicate_rows, opts)
+    ((32, 32, 32), "linear", 2, 1 << 18, {}),          # fine level distributed only
+    ((32, 32, 32), "linear", 2, 0, {}),                # all but the coarsest distributed
+    ((32, 32, 32), "linear", 4, 0, {}),                # empty slabs on coarse levels
+    ((24, 20, 37), "linear", 3, 0, {}),                # ragged planes per rank
+    ((16, 16, 16), "aggregate", 2, 0, {"smooth_weight": 0.8}),
+    ((32, 32, 32), "linear", 3, 512, {"smoother": "l1"}),
+    ((32, 32, 32), "linear", 2, 0, {"reuse_outer_residual": 0}),
+    ((20, 24, 40), "linear", 4, 0, {"num_pre_smooth_sweeps": 2, "num_post_smooth_sweeps": 3}),
+]
+
+
+@pytest.mark.parametrize("dims,interp,nranks,rep,extra", CASES)
+def test_dist_matches_single_gpu(amg, ctx, dims, interp, nranks, rep, extra):
+    kw = dict(extra)
+    if kw.pop("smoother", None) == "l1":
+        kw["smoother"] = amg.AMG_L1_JACOBI
+    opts = amg.default_opts(num_cycles=8, tol=0.0, **kw)
+    it = amg.AMG_INTERP_AGGREGATE if interp == "aggregate" else amg.AMG_INTERP_LINEAR
+    gen = amg.Gen(dims[0], dims[1], dims[2], interp=it)
+    n = dims[0] * dims[1] * dims[2]
+    f = amg.rhs_rand(0, n)
+    cycles = 8
+    u1, h1 = single_gpu(amg, ctx, gen, opts, f, cycles)
+    ud, hd = distributed(amg, gen, opts, f, cycles, nranks, rep)
+    assert_bitwise(ud, u1, "distributed iterate")
+    np.testing.assert_allclose(hd, h1, rtol=1e-12, atol=0)
+    assert hd[-1] < 0.5 * hd[0]
+    gen.free()
+
+
+def test_dist_restart_is_fresh(amg, ctx):
+    """A second solve on the same distributed hierarchy starts from zero on every
+    level (replicated coarsest included): identical to the first."""
+    gen = amg.Gen(24)
+    opts = amg.default_opts(num_cycles=4, tol=0.0)
+    f = amg.rhs_rand(0, 24 ** 3)
+    hub = amg.dist.ThreadMailbox(2)
+
+    def rank(r):
+        c = amg.Context(0, nstreams=2)
+        tr = amg.dist.HostTransport(hub, r)
+        amg.dist.init_host(c, 2, r, tr)
+        amg.dist.set_replicate_rows(c, 4096)
+        D = amg.dist.DistHier(c, gen, opts)
+        outs = []
+        for _ in range(2):
+            D.solve_start(f[D.row0:D.row0 + D.n0])
+            D.iterate(4)
+            outs.append(D.get_u())
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        return outs
+
+    for a, b in run_ranks(2, rank):
+        assert_bitwise(a, b, "restart")
+    gen.free()
+
+
+def test_dist_allreduce(amg):
+    hub = amg.dist.ThreadMailbox(3)
+
+    def rank(r):
+        c = amg.Context(0, nstreams=1)
+        amg.dist.init_host(c, 3, r, amg.dist.HostTransport(hub, r))
+        out = amg.dist.allreduce_sum(c, [r + 1.0, 2.0 * r])
+        amg.dist.barrier(c)
+        amg.dist.finalize(c)
+        c.close()
+        return out
+
+    for o in run_ranks(3, rank):
+        np.testing.assert_array_equal(o, [6.0, 6.0])
+
+
+def test_dist_rccl_single_rank(amg, ctx):
+    """The RCCL transport itself (unique id, communicator, allreduce/allgather on
+    the stream) at world size 1 -- the only RCCL shape one GPU allows."""
+    gen = amg.Gen(32)
+    opts = amg.default_opts(num_cycles=6, tol=0.0)
+    f = amg.rhs_rand(0, 32 ** 3)
+    u1, h1 = single_gpu(amg, ctx, gen, opts, f, 6)
+    c = amg.Context(0, nstreams=2)
+    amg.dist.init_rccl(c, 1, 0, lambda b: b)
+    amg.dist.set_replicate_rows(c, 0)
+    D = amg.dist.DistHier(c, gen, opts)
+    r0 = D.solve_start(f)
+    hist = [r0]
+    for _ in range(6):
+        D.iterate(1)
+        hist.append(D.resnorm())
+    u = D.get_u()
+    assert D.fine_spmv_ms(3) > 0
+    D.free()
+    np.testing.assert_array_equal(amg.dist.allreduce_sum(c, [1.5, 2.5]), [1.5, 2.5])
+    amg.dist.finalize(c)
+    c.close()
+    assert_bitwise(u, u1, "rccl single rank")
+    np.testing.assert_allclose(hist, h1, rtol=1e-12, atol=0)
+    gen.free()
