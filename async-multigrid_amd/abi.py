@@ -117,7 +117,15 @@ PROTOTYPES = {
     "amg_dist_fine_spmv": (_i, [_p, _i, _dp]),
     "amg_dist_init_host": (_i, [_p, _i, _i, C.c_void_p, _p]),
     "amg_dist_hier_set_replicate_rows": (_i, [_p, _ll]),
+    "amg_dist_structured_row_starts": (_i, [_p, _i, _llp]),
+    "amg_dist_hier_create": (_i, [_p, _i, _llp, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.POINTER(AmgOpts), _pp]),
 }
+
+
+class AmgCsrPart(C.Structure):
+    _fields_ = [("nrows", _i), ("nnz", _ll), ("rowptr", _ip), ("col", _ip), ("val", _dp)]
+
 
 # amg_host_xchg_fn: (user, op, npeers, peers, send, send_bytes, recv, recv_bytes) -> int
 HOST_XCHG_FN = C.CFUNCTYPE(_i, _p, _i, _i, _ip, _pp, _llp, _pp, _llp)

@@ -19,6 +19,7 @@
 #include <array>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <vector>
@@ -248,11 +249,11 @@ __global__ void sqrt_to_k(const double *__restrict__ in, double *__restrict__ ou
 namespace {
 
 struct Partition {
-   // per level: first owned plane of every rank (size nranks + 1) and plane size
-   std::vector<std::vector<int>> z0;
-   std::vector<long long> plane;
-   long long rows_begin(int l, int r) const { return (long long)z0[l][r] * plane[l]; }
-   long long rows_end(int l, int r) const { return (long long)z0[l][r + 1] * plane[l]; }
+   // per level: first global row of every rank (size nranks + 1)
+   std::vector<std::vector<long long>> rs;
+   long long rows_begin(int l, int r) const { return rs[l][r]; }
+   long long rows_end(int l, int r) const { return rs[l][r + 1]; }
+   long long total(int l) const { return rs[l].back(); }
 };
 
 struct DistMat {
@@ -328,13 +329,12 @@ int dvec(amg_dist_hier *D, size_t n, double **p)
    return dalloc(D, n * sizeof(double), (void **)p);
 }
 
-// owner of global column g of a level's column space
+// owner of global column g of a level's column space: the rank r with
+// rs[r] <= g < rs[r+1] (empty ranges are skipped)
 int owner_of(const Partition &pt, int level, long long g)
 {
-   // the rank r with z[r] <= plane < z[r+1] (empty ranges are skipped)
-   const auto &z = pt.z0[level];
-   const int zp = (int)(g / pt.plane[level]);
-   return (int)(std::upper_bound(z.begin(), z.end(), zp) - z.begin()) - 1;
+   const auto &z = pt.rs[level];
+   return (int)(std::upper_bound(z.begin(), z.end(), g) - z.begin()) - 1;
 }
 
 // Build a DistMat from host CSR rows (global columns) of column level `cl`.
@@ -352,7 +352,7 @@ int build_distmat(amg_dist_hier *D, DistMat &M, long long row0, int nrows, std::
    std::vector<long long> ghosts;
    if (replicated_cols) {
       // columns index the full replicated level-cl vector
-      long long full = (long long)D->part.z0[cl][R] * D->part.plane[cl];
+      const long long full = D->part.total(cl);
       M.ncol_own = (int)full;
       M.nghost = 0;
       ncols_dev = (int)full;
@@ -573,103 +573,72 @@ int nparts(const DistMat &M)
 // ---------------------------------------------------------------------------
 // construction
 // ---------------------------------------------------------------------------
-extern "C" int amg_dist_hier_create_structured(amg_ctx *c, const amg_gen *g, const amg_opts *opts,
-                                               amg_dist_hier **out)
+namespace {
+
+// host CSR rows with global column ids
+struct HostRows {
+   std::vector<int> rp, cj;
+   std::vector<double> cv;
+};
+// local rows of operator `which` (AMG_GEN_A/P/R) of level l on this rank
+using LocalFn = std::function<int(int which, int level, HostRows &out)>;
+// every row of operator `which` of level l (replicated levels), registered on the device
+using FullFn = std::function<int(int which, int level, amg_mat **out)>;
+
+int check_opts(const amg_opts *o)
 {
-   AMG_ARG(c && c->xport && g && opts && out, "amg_dist_hier_create_structured: bad argument");
-   AMG_ARG(opts->solver == AMG_MULT && opts->cheby_flag == 0 &&
-              (opts->smoother == AMG_JACOBI || opts->smoother == AMG_L1_JACOBI),
-           "amg_dist: MULT with Jacobi / L1 Jacobi is supported");
+   AMG_ARG(o->solver == AMG_MULT && o->cheby_flag == 0 &&
+              (o->smoother == AMG_JACOBI || o->smoother == AMG_L1_JACOBI),
+           "amg_dist: the distributed cycle supports MULT with Jacobi / L1 Jacobi");
+   return AMG_OK;
+}
+
+// levels [0, Ld) distributed, [Ld, L) replicated: the first level with fewer
+// rows than replicate_rows, at least level 1, at most L-1 (coarsest replicated)
+int split_level(const Partition &pt, int L, long long replicate_rows)
+{
+   if (L == 1) return 1;
+   int Ld = L;
+   for (int l = 0; l < L; l++)
+      if (pt.total(l) < replicate_rows) {
+         Ld = l;
+         break;
+      }
+   return std::min(std::max(Ld, 1), L - 1);
+}
+
+int build_hier(amg_ctx *c, int L, Partition part, const amg_opts *opts, const LocalFn &local,
+               const FullFn &full, amg_dist_hier **out)
+{
    amg_transport *t = c->xport;
    const int R = t->nranks, me = t->rank;
    auto D = std::make_unique<amg_dist_hier>();
    D->ctx = c;
    D->o = *opts;
-   D->L = amg_gen_num_levels(g);
-   const int L = D->L;
-   // plane partition: level 0 split evenly; coarse plane k follows the owner
-   // of fine plane 2k+1 (the fine point it is injected from under linear
-   // interpolation; 2k under aggregation)
-   D->part.z0.resize(L);
-   D->part.plane.resize(L);
-   std::vector<std::array<int, 3>> dims(L);
-   for (int l = 0; l < L; l++) {
-      amg_gen_dims(g, l, &dims[l][0], &dims[l][1], &dims[l][2]);
-      D->part.plane[l] = (long long)dims[l][0] * dims[l][1];
-   }
-   {
-      const int nz = dims[0][2];
-      D->part.z0[0].resize(R + 1);
-      for (int r = 0; r <= R; r++) D->part.z0[0][r] = (int)((long long)nz * r / R);
-      for (int l = 1; l < L; l++) {
-         const int nzc = dims[l][2], nzf = dims[l - 1][2];
-         std::vector<int> own(nzc);
-         for (int k = 0; k < nzc; k++) {
-            const int fz = std::min(nzf - 1, 2 * k + (nzc * 2 <= nzf ? 1 : 0));
-            const auto &zf = D->part.z0[l - 1];
-            int r = 0;
-            while (r + 1 < R && zf[r + 1] <= fz) r++;
-            own[k] = r;
-         }
-         D->part.z0[l].assign(R + 1, nzc);
-         for (int r = R - 1; r >= 0; r--) {
-            // first plane owned by r (planes are monotone in r)
-            int first = D->part.z0[l][r + 1];
-            for (int k = 0; k < nzc; k++)
-               if (own[k] >= r) {
-                  first = k;
-                  break;
-               }
-            D->part.z0[l][r] = std::min(first, D->part.z0[l][r + 1]);
-         }
-         D->part.z0[l][0] = 0;
-      }
-   }
-   // replicated coarse levels: total rows below the threshold (and always the coarsest)
-   D->Ld = L;
-   for (int l = 0; l < L; l++)
-      if ((long long)dims[l][0] * dims[l][1] * dims[l][2] < c->replicate_rows) {
-         D->Ld = l;
-         break;
-      }
-   if (D->Ld == 0) D->Ld = 1; // the fine level is always distributed
-   if (D->Ld > L - 1 && L > 1) D->Ld = L - 1; // keep at least the coarsest replicated
-   if (L == 1) D->Ld = 1;
+   D->L = L;
+   D->part = std::move(part);
+   D->Ld = split_level(D->part, L, c->replicate_rows);
    const int Ld = D->Ld;
    D->lv.resize(Ld);
    AMG_HIP(hipEventCreateWithFlags(&D->ev_pack, hipEventDisableTiming));
    AMG_HIP(hipEventCreateWithFlags(&D->ev_comm, hipEventDisableTiming));
-
-   auto host_rows = [&](int which, int level, int z0, int z1, std::vector<int> &rp,
-                        std::vector<int> &cj, std::vector<double> &cv) -> int {
-      const long long nnz = amg_gen_nnz(g, which, level, z0, z1);
-      AMG_ARG(nnz >= 0, "amg_dist: generator: %s", amg_last_error());
-      const auto &d = (which == AMG_GEN_R) ? dims[level + 1] : dims[level];
-      const long long nr = (long long)d[0] * d[1] * (z1 - z0);
-      rp.assign(nr + 1, 0);
-      cj.assign(std::max(1LL, nnz), 0);
-      cv.assign(std::max(1LL, nnz), 0.0);
-      if (nr > 0) AMG_TRY(amg_gen_fill(g, which, level, z0, z1, rp.data(), cj.data(), cv.data(), 0));
-      return AMG_OK;
-   };
-
-   std::vector<int> rp, cj;
-   std::vector<double> cv;
+   HostRows h;
    for (int l = 0; l < Ld; l++) {
       DLevel &v = D->lv[l];
-      const int z0 = D->part.z0[l][me], z1 = D->part.z0[l][me + 1];
-      v.row0 = (long long)z0 * D->part.plane[l];
-      v.n = (int)((long long)(z1 - z0) * D->part.plane[l]);
-      AMG_TRY(host_rows(AMG_GEN_A, l, z0, z1, rp, cj, cv));
-      AMG_TRY(build_distmat(D.get(), v.A, v.row0, v.n, rp, cj, cv, l, false));
+      v.row0 = D->part.rows_begin(l, me);
+      v.n = (int)(D->part.rows_end(l, me) - v.row0);
+      AMG_TRY(local(AMG_GEN_A, l, h));
+      AMG_ARG((int)h.rp.size() == v.n + 1, "amg_dist: level %d A has %zu rows, partition says %d",
+              l, h.rp.size() - 1, v.n);
+      AMG_TRY(build_distmat(D.get(), v.A, v.row0, v.n, h.rp, h.cj, h.cv, l, false));
       if (l < L - 1) {
-         AMG_TRY(host_rows(AMG_GEN_P, l, z0, z1, rp, cj, cv));
-         AMG_TRY(build_distmat(D.get(), v.P, v.row0, v.n, rp, cj, cv, l + 1, l + 1 >= Ld));
-         const int cz0 = D->part.z0[l + 1][me], cz1 = D->part.z0[l + 1][me + 1];
-         AMG_TRY(host_rows(AMG_GEN_R, l, cz0, cz1, rp, cj, cv));
-         AMG_TRY(build_distmat(D.get(), v.R, (long long)cz0 * D->part.plane[l + 1],
-                               (int)((long long)(cz1 - cz0) * D->part.plane[l + 1]), rp, cj, cv, l,
-                               false));
+         AMG_TRY(local(AMG_GEN_P, l, h));
+         AMG_ARG((int)h.rp.size() == v.n + 1, "amg_dist: level %d P row count", l);
+         AMG_TRY(build_distmat(D.get(), v.P, v.row0, v.n, h.rp, h.cj, h.cv, l + 1, l + 1 >= Ld));
+         const long long c0 = D->part.rows_begin(l + 1, me), c1 = D->part.rows_end(l + 1, me);
+         AMG_TRY(local(AMG_GEN_R, l, h));
+         AMG_ARG((long long)h.rp.size() == c1 - c0 + 1, "amg_dist: level %d R row count", l);
+         AMG_TRY(build_distmat(D.get(), v.R, c0, (int)(c1 - c0), h.rp, h.cj, h.cv, l, false));
       }
    }
    // vector capacities: owned + the largest ghost region of any matrix reading them
@@ -693,12 +662,12 @@ extern "C" int amg_dist_hier_create_structured(amg_ctx *c, const amg_gen *g, con
       const int Lc = L - Ld;
       std::vector<amg_mat *> As(Lc), Ps(std::max(1, Lc - 1)), Rs(std::max(1, Lc - 1));
       for (int l = Ld; l < L; l++) {
-         AMG_TRY(amg_gen_register(c, g, AMG_GEN_A, l, 0, dims[l][2], &As[l - Ld]));
+         AMG_TRY(full(AMG_GEN_A, l, &As[l - Ld]));
          D->coarse_mats.push_back(As[l - Ld]);
          if (l < L - 1) {
-            AMG_TRY(amg_gen_register(c, g, AMG_GEN_P, l, 0, dims[l][2], &Ps[l - Ld]));
-            AMG_TRY(amg_gen_register(c, g, AMG_GEN_R, l, 0, dims[l + 1][2], &Rs[l - Ld]));
+            AMG_TRY(full(AMG_GEN_P, l, &Ps[l - Ld]));
             D->coarse_mats.push_back(Ps[l - Ld]);
+            AMG_TRY(full(AMG_GEN_R, l, &Rs[l - Ld]));
             D->coarse_mats.push_back(Rs[l - Ld]);
          }
       }
@@ -706,8 +675,7 @@ extern "C" int amg_dist_hier_create_structured(amg_ctx *c, const amg_gen *g, con
       co.profile = 0;
       co.reuse_outer_residual = 0;
       AMG_TRY(amg_hier_create(c, Lc, As.data(), Ps.data(), Rs.data(), &co, &D->coarse));
-      const long long nfull = (long long)dims[Ld][0] * dims[Ld][1] * dims[Ld][2];
-      AMG_TRY(dvec(D.get(), nfull, &D->f_rep));
+      AMG_TRY(dvec(D.get(), D->part.total(Ld), &D->f_rep));
       // allgather blocks padded to the largest owned row count at level Ld
       int blk = 0;
       std::vector<int> cnt(R), dsp(R);
@@ -726,6 +694,182 @@ extern "C" int amg_dist_hier_create_structured(amg_ctx *c, const amg_gen *g, con
    AMG_HIP(hipStreamSynchronize(c->stream));
    *out = D.release();
    return AMG_OK;
+}
+
+// allgather of variable-size host byte blobs through the transport (setup only)
+int host_allgatherv(amg_ctx *c, const void *mine, long long bytes, std::vector<char> &all,
+                    std::vector<long long> &sizes)
+{
+   const int R = c->xport->nranks;
+   long long *d = nullptr;
+   AMG_HIP(hipMalloc(&d, (size_t)(R + 1) * sizeof(long long)));
+   AMG_TRY(h2d(c->stream, d + R, &bytes, sizeof(long long)));
+   AMG_TRY(xp_allgather(c, c->stream, d + R, d, sizeof(long long)));
+   sizes.resize(R);
+   AMG_TRY(d2h(c->stream, sizes.data(), d, R * sizeof(long long)));
+   hipFree(d);
+   long long mx = 1;
+   for (long long v : sizes) mx = std::max(mx, v);
+   char *db = nullptr;
+   AMG_HIP(hipMalloc(&db, (size_t)mx * (R + 1)));
+   char *mine_d = db + (size_t)mx * R;
+   AMG_TRY(h2d(c->stream, mine_d, mine, bytes));
+   AMG_TRY(xp_allgather(c, c->stream, mine_d, db, mx));
+   std::vector<char> padded((size_t)mx * R);
+   AMG_TRY(d2h(c->stream, padded.data(), db, (size_t)mx * R));
+   hipFree(db);
+   all.clear();
+   for (int r = 0; r < R; r++)
+      all.insert(all.end(), padded.begin() + (size_t)mx * r, padded.begin() + (size_t)mx * r + sizes[r]);
+   return AMG_OK;
+}
+
+} // namespace
+
+// z-plane slabs of the structured problem: level-0 planes split evenly; coarse
+// plane k follows the owner of the fine plane it is injected from (2k+1 under
+// linear interpolation, the aggregate's second plane under aggregation), so
+// restriction and prolongation only touch neighbouring slabs
+static void structured_planes(const amg_gen *g, int R, std::vector<std::vector<int>> &z0)
+{
+   const int L = amg_gen_num_levels(g);
+   std::vector<int> nz(L);
+   for (int l = 0; l < L; l++) {
+      int a, b;
+      amg_gen_dims(g, l, &a, &b, &nz[l]);
+   }
+   z0.assign(L, std::vector<int>(R + 1));
+   for (int r = 0; r <= R; r++) z0[0][r] = (int)((long long)nz[0] * r / R);
+   for (int l = 1; l < L; l++) {
+      std::vector<int> own(nz[l]);
+      for (int k = 0; k < nz[l]; k++) {
+         const int fz = std::min(nz[l - 1] - 1, 2 * k + 1);
+         own[k] = (int)(std::upper_bound(z0[l - 1].begin(), z0[l - 1].end(), fz) - z0[l - 1].begin()) - 1;
+      }
+      // z0[l][r] = first coarse plane owned by a rank >= r (own[] is monotone)
+      for (int r = 0; r <= R; r++)
+         z0[l][r] = (int)(std::lower_bound(own.begin(), own.end(), r) - own.begin());
+   }
+}
+
+extern "C" int amg_dist_structured_row_starts(const amg_gen *g, int nranks, long long *row_starts)
+{
+   AMG_ARG(g && nranks >= 1 && row_starts, "amg_dist_structured_row_starts: bad argument");
+   std::vector<std::vector<int>> z0;
+   structured_planes(g, nranks, z0);
+   for (size_t l = 0; l < z0.size(); l++) {
+      int a, b, c;
+      amg_gen_dims(g, (int)l, &a, &b, &c);
+      for (int r = 0; r <= nranks; r++)
+         row_starts[l * (nranks + 1) + r] = (long long)z0[l][r] * a * b;
+   }
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_hier_create_structured(amg_ctx *c, const amg_gen *g, const amg_opts *opts,
+                                               amg_dist_hier **out)
+{
+   AMG_ARG(c && c->xport && g && opts && out, "amg_dist_hier_create_structured: bad argument");
+   AMG_TRY(check_opts(opts));
+   const int R = c->xport->nranks, me = c->xport->rank;
+   const int L = amg_gen_num_levels(g);
+   std::vector<std::array<int, 3>> dims(L);
+   for (int l = 0; l < L; l++) amg_gen_dims(g, l, &dims[l][0], &dims[l][1], &dims[l][2]);
+   std::vector<std::vector<int>> z0;
+   structured_planes(g, R, z0);
+   Partition part;
+   part.rs.resize(L);
+   for (int l = 0; l < L; l++) {
+      part.rs[l].resize(R + 1);
+      for (int r = 0; r <= R; r++) part.rs[l][r] = (long long)z0[l][r] * dims[l][0] * dims[l][1];
+   }
+   auto local = [&](int which, int level, HostRows &h) -> int {
+      const int pl = (which == AMG_GEN_R) ? level + 1 : level;
+      const int a = z0[pl][me], b = z0[pl][me + 1];
+      const long long nnz = amg_gen_nnz(g, which, level, a, b);
+      AMG_ARG(nnz >= 0, "amg_dist: generator: %s", amg_last_error());
+      const long long nr = (long long)dims[pl][0] * dims[pl][1] * (b - a);
+      h.rp.assign(nr + 1, 0);
+      h.cj.assign(std::max(1LL, nnz), 0);
+      h.cv.assign(std::max(1LL, nnz), 0.0);
+      if (nr > 0) AMG_TRY(amg_gen_fill(g, which, level, a, b, h.rp.data(), h.cj.data(), h.cv.data(), 0));
+      return AMG_OK;
+   };
+   auto full = [&](int which, int level, amg_mat **m) -> int {
+      const int pl = (which == AMG_GEN_R) ? level + 1 : level;
+      return amg_gen_register(c, g, which, level, 0, dims[pl][2], m);
+   };
+   return build_hier(c, L, std::move(part), opts, local, full, out);
+}
+
+extern "C" int amg_dist_hier_create(amg_ctx *c, int L, const long long *row_starts,
+                                    const amg_csr_part *A, const amg_csr_part *P,
+                                    const amg_csr_part *Rm, const amg_opts *opts, amg_dist_hier **out)
+{
+   AMG_ARG(c && c->xport && L >= 1 && row_starts && A && opts && out && (L == 1 || (P && Rm)),
+           "amg_dist_hier_create: bad argument");
+   AMG_TRY(check_opts(opts));
+   const int R = c->xport->nranks, me = c->xport->rank;
+   Partition part;
+   part.rs.resize(L);
+   for (int l = 0; l < L; l++) {
+      part.rs[l].assign(row_starts + (size_t)l * (R + 1), row_starts + (size_t)(l + 1) * (R + 1));
+      AMG_ARG(part.rs[l][0] == 0, "amg_dist_hier_create: row_starts of level %d must start at 0", l);
+      for (int r = 0; r < R; r++)
+         AMG_ARG(part.rs[l][r] <= part.rs[l][r + 1], "amg_dist_hier_create: level %d row_starts not monotone", l);
+      AMG_ARG(part.rs[l][R] < (1LL << 31), "amg_dist_hier_create: level %d exceeds int32 rows", l);
+   }
+   auto pick = [&](int which, int level) -> const amg_csr_part & {
+      return which == AMG_GEN_A ? A[level] : which == AMG_GEN_P ? P[level] : Rm[level];
+   };
+   auto rows_of = [&](int which, int level) {
+      const int pl = (which == AMG_GEN_R) ? level + 1 : level;
+      return part.rs[pl][me + 1] - part.rs[pl][me];
+   };
+   auto local = [&](int which, int level, HostRows &h) -> int {
+      const amg_csr_part &m = pick(which, level);
+      AMG_ARG(m.nrows == rows_of(which, level) && m.rowptr && (m.nnz == 0 || (m.col && m.val)),
+              "amg_dist_hier_create: operator %d of level %d: %d local rows, partition says %lld",
+              which, level, m.nrows, (long long)rows_of(which, level));
+      AMG_ARG(m.rowptr[0] == 0 && m.rowptr[m.nrows] == m.nnz,
+              "amg_dist_hier_create: operator %d of level %d: rowptr must run 0..nnz", which, level);
+      h.rp.assign(m.rowptr, m.rowptr + m.nrows + 1);
+      h.cj.assign(m.col, m.col + m.nnz);
+      h.cv.assign(m.val, m.val + m.nnz);
+      if (h.cj.empty()) {
+         h.cj.push_back(0);
+         h.cv.push_back(0.0);
+      }
+      return AMG_OK;
+   };
+   auto full = [&](int which, int level, amg_mat **mout) -> int {
+      // gather every rank's rows of this (small) operator
+      const amg_csr_part &m = pick(which, level);
+      AMG_ARG(m.nrows == rows_of(which, level), "amg_dist_hier_create: operator %d of level %d row count",
+              which, level);
+      std::vector<char> all;
+      std::vector<long long> sz;
+      std::vector<int> rl(m.rowptr + 1, m.rowptr + m.nrows + 1); // row lengths via ends
+      for (int i = m.nrows - 1; i >= 0; i--) rl[i] -= m.rowptr[i];
+      AMG_TRY(host_allgatherv(c, rl.data(), (long long)rl.size() * 4, all, sz));
+      std::vector<int> rp(1, 0);
+      for (size_t k = 0; k < all.size() / 4; k++) rp.push_back(rp.back() + ((int *)all.data())[k]);
+      AMG_TRY(host_allgatherv(c, m.col, m.nnz * 4, all, sz));
+      std::vector<int> cj((int *)all.data(), (int *)all.data() + all.size() / 4);
+      AMG_TRY(host_allgatherv(c, m.val, m.nnz * 8, all, sz));
+      std::vector<double> cv((double *)all.data(), (double *)all.data() + all.size() / 8);
+      const int pl_rows = (which == AMG_GEN_R) ? level + 1 : level;
+      const int pl_cols = (which == AMG_GEN_P) ? level + 1 : level;
+      const long long nr = part.total(pl_rows), nc = part.total(pl_cols);
+      AMG_ARG((long long)rp.size() == nr + 1 && (long long)cj.size() == rp.back(),
+              "amg_dist_hier_create: gathered operator %d of level %d is inconsistent", which, level);
+      if (cj.empty()) {
+         cj.push_back(0);
+         cv.push_back(0.0);
+      }
+      return amg_csr_register(c, (int)nr, (int)nc, rp.back(), rp.data(), cj.data(), cv.data(), 1, mout);
+   };
+   return build_hier(c, L, part, opts, local, full, out); // the lambdas read part: copy it
 }
 
 extern "C" int amg_dist_hier_free(amg_dist_hier *D)

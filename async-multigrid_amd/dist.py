@@ -189,6 +189,13 @@ def set_replicate_rows(ctx, rows):
     check(lib.amg_dist_hier_set_replicate_rows(ctx.h, int(rows)))
 
 
+def structured_row_starts(gen, nranks):
+    """The z-slab row partition amg_dist_hier_create_structured uses: (L, nranks+1)."""
+    rs = np.zeros((gen.L, nranks + 1), dtype=np.int64)
+    check(lib.amg_dist_structured_row_starts(gen.h, nranks, rs.ctypes.data_as(C.POINTER(C.c_longlong))))
+    return rs
+
+
 def barrier(ctx):
     check(lib.amg_dist_barrier(ctx.h))
 
@@ -199,15 +206,49 @@ def allreduce_sum(ctx, vals):
     return a
 
 
-class DistHier:
-    """Slab-distributed hierarchy of a structured problem + SMEM_Solve loop."""
+def _part(nrows, rowptr, col, val):
+    rp = np.ascontiguousarray(rowptr, dtype=np.int32)
+    cj = np.ascontiguousarray(col, dtype=np.int32)
+    cv = np.ascontiguousarray(val, dtype=np.float64)
+    p = abi.AmgCsrPart(int(nrows), int(rp[-1]), _ip(rp), _ip(cj), _dp(cv))
+    return p, (rp, cj, cv)
 
-    def __init__(self, ctx, gen, opts):
+
+class DistHier:
+    """Row-distributed hierarchy + SMEM_Solve loop.
+
+    ``DistHier(ctx, gen, opts)`` builds the structured problem slab by slab;
+    ``DistHier.from_parts`` takes this rank's rows of every operator with
+    global column ids and the per-level row partition (ParCSR row_starts)."""
+
+    def __init__(self, ctx, gen, opts, _handle=None):
         self.ctx, self.gen, self.opts = ctx, gen, opts
-        h = C.c_void_p()
-        check(lib.amg_dist_hier_create_structured(ctx.h, gen.h, C.byref(opts), C.byref(h)))
-        self.h = h
+        if _handle is None:
+            h = C.c_void_p()
+            check(lib.amg_dist_hier_create_structured(ctx.h, gen.h, C.byref(opts), C.byref(h)))
+            _handle = h
+        self.h = _handle
         self.row0, self.n0 = self.local_rows(0)
+
+    @classmethod
+    def from_parts(cls, ctx, row_starts, A, P, R, opts):
+        """row_starts: (L, nranks+1) ints; A/P/R: lists of (nrows, rowptr, col, val)."""
+        rs = np.ascontiguousarray(row_starts, dtype=np.int64)
+        L = rs.shape[0]
+        keep = []
+
+        def arr(parts, n):
+            out = (abi.AmgCsrPart * max(n, 1))()
+            for i, t in enumerate(parts):
+                out[i], k = _part(*t)
+                keep.append(k)
+            return out
+        a, p, r = arr(A, L), arr(P, L - 1), arr(R, L - 1)
+        h = C.c_void_p()
+        check(lib.amg_dist_hier_create(ctx.h, L, rs.ctypes.data_as(C.POINTER(C.c_longlong)),
+                                       C.cast(a, C.c_void_p), C.cast(p, C.c_void_p),
+                                       C.cast(r, C.c_void_p), C.byref(opts), C.byref(h)))
+        return cls(ctx, None, opts, _handle=h)
 
     def local_rows(self, level):
         r0, n = C.c_int(), C.c_int()

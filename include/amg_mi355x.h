@@ -226,7 +226,7 @@ int amg_rhs_rand(long long r0, long long r1, double lo, double hi, double *out);
  * SendRecv/CompleteRecv, the hypre ParCSR halo exchange inside
  * hypre_ParCSRMatrixMatvec called from DMEM_Add.cpp:230-308, and the
  * InnerProdFlag allreduce DMEM_Misc.cpp:414-433).  Every level is split into
- * z-plane slabs; each SpMV exchanges its ghost rows point-to-point over RCCL
+ * contiguous row ranges (z-plane slabs for the structured problem); each SpMV exchanges its ghost rows point-to-point over RCCL
  * (xGMI) on a communication stream while the slab interior is computed on the
  * compute stream.  Levels below a size threshold are replicated on every rank
  * (one allgather of the restricted residual per cycle) so the coarse cycle
@@ -246,12 +246,33 @@ int amg_dist_init_host(amg_ctx *ctx, int nranks, int rank, amg_host_xchg_fn fn, 
 int amg_dist_finalize(amg_ctx *ctx);
 int amg_dist_allreduce_sum(amg_ctx *ctx, double *host_vals, int n);
 int amg_dist_barrier(amg_ctx *ctx);
-/* distributed hierarchy of a structured problem: rank r owns the z-planes
- * the partition gives it at every level; levels with fewer than
- * replicate_rows rows are replicated (0: default 2^18) */
 typedef struct amg_dist_hier amg_dist_hier;
+/* one rank's rows of a distributed operator: local rows, GLOBAL column ids of
+ * the operator's column level (what a hypre_ParCSRMatrix's diag + offd with
+ * col_map_offd describe, DMEM_Setup.cpp:169-173); diagonal first in A rows */
+typedef struct amg_csr_part {
+   int nrows;
+   long long nnz;
+   const int *rowptr; /* [nrows + 1], 0 .. nnz */
+   const int *col;    /* [nnz] global column ids */
+   const double *val; /* [nnz] */
+} amg_csr_part;
+/* distributed hierarchy from per-rank CSR pieces (the ParCSR row partition:
+ * row_starts[l * (nranks + 1) + r] = first global row of rank r on level l,
+ * hypre_ParCSRMatrixRowStarts).  A[l]: rows of level l; P[l]: rows of level l,
+ * columns of level l+1; R[l]: rows of level l+1, columns of level l.  Levels
+ * with fewer than replicate_rows rows are gathered and replicated. */
+int amg_dist_hier_create(amg_ctx *ctx, int num_levels, const long long *row_starts,
+                         const amg_csr_part *A, const amg_csr_part *P, const amg_csr_part *R,
+                         const amg_opts *opts, amg_dist_hier **out);
+/* the same for the structured problem, built slab by slab from the generator:
+ * level-0 z-planes split evenly, coarse plane k owned by the owner of fine
+ * plane 2k+1 */
 int amg_dist_hier_create_structured(amg_ctx *ctx, const amg_gen *gen, const amg_opts *opts,
                                     amg_dist_hier **out);
+/* that partition (host only, no device): row_starts[l * (nranks + 1) + r] */
+int amg_dist_structured_row_starts(const amg_gen *gen, int nranks, long long *row_starts);
+/* levels with fewer rows than this are replicated on every rank (default 2^18) */
 int amg_dist_hier_set_replicate_rows(amg_ctx *ctx, long long rows);
 int amg_dist_hier_free(amg_dist_hier *D);
 /* rows [row0, row0 + nrows) of the global level-0 vector this rank owns */

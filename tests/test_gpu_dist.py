@@ -185,3 +185,69 @@ def test_dist_rccl_single_rank(amg, ctx):
     assert_bitwise(u, u1, "rccl single rank")
     np.testing.assert_allclose(hist, h1, rtol=1e-12, atol=0)
     gen.free()
+
+
+def row_parts(amg, gen, cuts):
+    """Per-level row partitions (arbitrary, not plane-aligned) and each rank's
+    rows of A/P/R with global column ids, cut from the full host operators."""
+    L = gen.L
+    full = {w: [gen.host_csr(w, l) for l in range(L if w == amg.AMG_GEN_A else L - 1)]
+            for w in (amg.AMG_GEN_A, amg.AMG_GEN_P, amg.AMG_GEN_R)}
+    nranks = len(cuts) + 1
+    rs = np.zeros((L, nranks + 1), dtype=np.int64)
+    for l in range(L):
+        n = gen.rows(amg.AMG_GEN_A, l)
+        rs[l, 1:-1] = [int(round(c * n)) for c in cuts]
+        rs[l, -1] = n
+
+    def rows(w, l, a, b):
+        nr, nc, rp, cj, cv = full[w][l]
+        lo, hi = rp[a], rp[b]
+        return (b - a, rp[a:b + 1] - lo, cj[lo:hi], cv[lo:hi])
+
+    parts = []
+    for r in range(nranks):
+        A = [rows(amg.AMG_GEN_A, l, rs[l, r], rs[l, r + 1]) for l in range(L)]
+        P = [rows(amg.AMG_GEN_P, l, rs[l, r], rs[l, r + 1]) for l in range(L - 1)]
+        R = [rows(amg.AMG_GEN_R, l, rs[l + 1, r], rs[l + 1, r + 1]) for l in range(L - 1)]
+        parts.append((A, P, R))
+    return rs, parts
+
+
+@pytest.mark.parametrize("cuts,rep", [((0.37,), 0), ((0.2, 0.5, 0.51), 0), ((0.6, 0.9), 4096)])
+def test_dist_from_parts_any_partition(amg, ctx, cuts, rep):
+    """The general entry (ParCSR-style row_starts + local CSR with global
+    columns): any contiguous row partition, empty or ragged ranks included,
+    gives the single-GPU iterate bit for bit."""
+    gen = amg.Gen(24, 20, 28)
+    opts = amg.default_opts(num_cycles=6, tol=0.0)
+    n = 24 * 20 * 28
+    f = amg.rhs_rand(0, n)
+    u1, h1 = single_gpu(amg, ctx, gen, opts, f, 6)
+    rs, parts = row_parts(amg, gen, cuts)
+    nranks = len(cuts) + 1
+    hub = amg.dist.ThreadMailbox(nranks)
+
+    def rank(r):
+        c = amg.Context(0, nstreams=2)
+        tr = amg.dist.HostTransport(hub, r)
+        amg.dist.init_host(c, nranks, r, tr)
+        amg.dist.set_replicate_rows(c, rep)
+        A, P, R = parts[r]
+        D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
+        assert (D.row0, D.n0) == (rs[0, r], rs[0, r + 1] - rs[0, r])
+        D.solve_start(f[D.row0:D.row0 + D.n0])
+        hist = [D.resnorm()]
+        for _ in range(6):
+            D.iterate(1)
+            hist.append(D.resnorm())
+        u = D.get_u()
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        return u, np.array(hist)
+
+    res = run_ranks(nranks, rank)
+    assert_bitwise(np.concatenate([t[0] for t in res]), u1, "from_parts iterate")
+    np.testing.assert_allclose(res[0][1], h1, rtol=1e-12, atol=0)
+    gen.free()
