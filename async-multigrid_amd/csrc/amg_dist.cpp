@@ -24,26 +24,14 @@
 #include <memory>
 #include <vector>
 
-#include "amg_internal.h"
+#include "amg_dist_internal.h"
+
+using namespace amgd;
 
 // ---------------------------------------------------------------------------
 // transport
 // ---------------------------------------------------------------------------
-struct amg_transport {
-   int nranks = 1, rank = 0;
-   ncclComm_t comm = nullptr;
-   amg_host_xchg_fn fn = nullptr; // test transport through host memory
-   void *user = nullptr;
-   bool host() const { return fn != nullptr; }
-};
 
-#define AMG_NCCL(call)                                                                     \
-   do {                                                                                    \
-      ncclResult_t _r = (call);                                                            \
-      if (_r != ncclSuccess)                                                               \
-         return amg_set_error(AMG_ERR_RCCL, "%s:%d %s -> %s", __FILE__, __LINE__, #call,  \
-                              ncclGetErrorString(_r));                                     \
-   } while (0)
 
 extern "C" int amg_dist_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
 
@@ -93,6 +81,7 @@ extern "C" int amg_dist_finalize(amg_ctx *c)
    if (!c || !c->xport) return AMG_OK;
    hipStreamSynchronize(c->stream);
    hipStreamSynchronize(c->comm_stream);
+   for (auto &lc : c->xport->level_comms) ncclCommDestroy(lc);
    if (c->xport->comm) ncclCommDestroy(c->xport->comm);
    delete c->xport;
    c->xport = nullptr;
@@ -102,7 +91,7 @@ extern "C" int amg_dist_finalize(amg_ctx *c)
 // host -> device copy ordered on stream s and complete on return (a pageable
 // hipMemcpy on the null stream is not ordered against the non-blocking
 // context streams, e.g. a pending hipMemsetAsync of the same buffer)
-static int h2d(hipStream_t s, void *dst, const void *src, size_t bytes)
+int amgd::h2d(hipStream_t s, void *dst, const void *src, size_t bytes)
 {
    if (bytes == 0) return AMG_OK;
    AMG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
@@ -110,7 +99,7 @@ static int h2d(hipStream_t s, void *dst, const void *src, size_t bytes)
    return AMG_OK;
 }
 
-static int d2h(hipStream_t s, void *dst, const void *src, size_t bytes)
+int amgd::d2h(hipStream_t s, void *dst, const void *src, size_t bytes)
 {
    if (bytes == 0) return AMG_OK;
    AMG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
@@ -119,16 +108,18 @@ static int d2h(hipStream_t s, void *dst, const void *src, size_t bytes)
 }
 
 // point-to-point byte exchange with peers[i] (device buffers), on stream s
-static int xp_p2p(amg_ctx *c, hipStream_t s, int np, const int *peers, void *const *send,
-                  const long long *sbytes, void *const *recv, const long long *rbytes)
+int amgd::xp_p2p(amg_ctx *c, hipStream_t s, int np, const int *peers, void *const *send,
+                 const long long *sbytes, void *const *recv, const long long *rbytes,
+                 ncclComm_t comm)
 {
    amg_transport *t = c->xport;
    if (np == 0) return AMG_OK;
+   if (!comm) comm = t->comm;
    if (!t->host()) {
       AMG_NCCL(ncclGroupStart());
       for (int i = 0; i < np; i++) {
-         if (sbytes[i] > 0) AMG_NCCL(ncclSend(send[i], (size_t)sbytes[i], ncclChar, peers[i], t->comm, s));
-         if (rbytes[i] > 0) AMG_NCCL(ncclRecv(recv[i], (size_t)rbytes[i], ncclChar, peers[i], t->comm, s));
+         if (sbytes[i] > 0) AMG_NCCL(ncclSend(send[i], (size_t)sbytes[i], ncclChar, peers[i], comm, s));
+         if (rbytes[i] > 0) AMG_NCCL(ncclRecv(recv[i], (size_t)rbytes[i], ncclChar, peers[i], comm, s));
       }
       AMG_NCCL(ncclGroupEnd());
       return AMG_OK;
@@ -152,12 +143,13 @@ static int xp_p2p(amg_ctx *c, hipStream_t s, int np, const int *peers, void *con
 }
 
 // in-place sum of n doubles (device) across ranks, on stream s
-static int xp_allreduce(amg_ctx *c, hipStream_t s, double *dev, int n)
+int amgd::xp_allreduce(amg_ctx *c, hipStream_t s, double *dev, int n, ncclComm_t comm)
 {
    amg_transport *t = c->xport;
    if (t->nranks == 1) return AMG_OK;
+   if (!comm) comm = t->comm;
    if (!t->host()) {
-      AMG_NCCL(ncclAllReduce(dev, dev, (size_t)n, ncclDouble, ncclSum, t->comm, s));
+      AMG_NCCL(ncclAllReduce(dev, dev, (size_t)n, ncclDouble, ncclSum, comm, s));
       return AMG_OK;
    }
    AMG_HIP(hipStreamSynchronize(s));
@@ -172,11 +164,13 @@ static int xp_allreduce(amg_ctx *c, hipStream_t s, double *dev, int n)
 }
 
 // allgather of equal-size byte blocks: recv = [rank0 block | rank1 block | ...]
-static int xp_allgather(amg_ctx *c, hipStream_t s, const void *send, void *recv, long long bytes)
+int amgd::xp_allgather(amg_ctx *c, hipStream_t s, const void *send, void *recv, long long bytes,
+                       ncclComm_t comm)
 {
    amg_transport *t = c->xport;
+   if (!comm) comm = t->comm;
    if (!t->host()) {
-      AMG_NCCL(ncclAllGather(send, recv, (size_t)bytes, ncclChar, t->comm, s));
+      AMG_NCCL(ncclAllGather(send, recv, (size_t)bytes, ncclChar, comm, s));
       return AMG_OK;
    }
    AMG_HIP(hipStreamSynchronize(s));
@@ -243,77 +237,32 @@ __global__ void sqrt_to_k(const double *__restrict__ in, double *__restrict__ ou
    out[0] = sqrt(in[0]);
 }
 
+void amgd::launch_gather(hipStream_t s, const double *x, const int *idx, double *out, int n)
+{
+   if (n <= 0) return;
+   gather_k<<<std::min(4096, (n + 255) / 256), 256, 0, s>>>(x, idx, out, n);
+}
+
+void amgd::launch_scatter_blocks(hipStream_t s, const double *src, int blk, const int *cnt,
+                                 const int *dsp, int nranks, double *dst)
+{
+   const int total = blk * nranks;
+   if (total <= 0) return;
+   scatter_blocks_k<<<std::min(4096, (total + 255) / 256), 256, 0, s>>>(src, blk, cnt, dsp, nranks, dst);
+}
+
+void amgd::launch_sqrt(hipStream_t s, const double *in, double *out) { sqrt_to_k<<<1, 1, 0, s>>>(in, out); }
+
 // ---------------------------------------------------------------------------
 // distributed matrix: slab-local rows, columns remapped to [owned | ghost]
 // ---------------------------------------------------------------------------
+
+
 namespace {
-
-struct Partition {
-   // per level: first global row of every rank (size nranks + 1)
-   std::vector<std::vector<long long>> rs;
-   long long rows_begin(int l, int r) const { return rs[l][r]; }
-   long long rows_end(int l, int r) const { return rs[l][r + 1]; }
-   long long total(int l) const { return rs[l].back(); }
-};
-
-struct DistMat {
-   amg_mat *A = nullptr;        // local rows, remapped columns
-   long long row0 = 0;          // first global row
-   int nrows = 0;
-   int ncol_own = 0;            // owned columns (x region [0, ncol_own))
-   int nghost = 0;              // ghost region [ncol_own, ncol_own + nghost)
-   bool replicated_cols = false; // columns index a full replicated vector
-   int b0 = 0, b1 = 0;          // interior rows [b0, b1): no ghost column
-   std::vector<int> peers;      // union of send/recv peers
-   std::vector<long long> scnt, rcnt; // doubles per peer
-   std::vector<long long> soff, roff; // offsets into sendbuf / ghost region
-   int *d_send_idx = nullptr;   // owned-column index list of all sends
-   long long nsend = 0;
-   double *sendbuf = nullptr;
-};
-
-struct DLevel {
-   int n = 0;                  // owned rows
-   long long row0 = 0;
-   int cap = 0;                // vector capacity (owned + max ghosts)
-   DistMat A, P, R;            // P: level l -> l+1 (rows = level l), R: rows = level l+1
-   double *f = nullptr, *u = nullptr, *u_alt = nullptr, *r_fine = nullptr, *l1 = nullptr;
-   int zero_flag = 0;
-};
 
 } // namespace
 
-struct amg_dist_hier {
-   amg_ctx *ctx = nullptr;
-   amg_opts o{};
-   int L = 0, Ld = 0; // levels [0, Ld) distributed, [Ld, L) replicated
-   Partition part;
-   std::vector<DLevel> lv;
-   // replicated coarse part
-   amg_hier *coarse = nullptr;
-   std::vector<amg_mat *> coarse_mats;
-   double *f_rep = nullptr;   // full level-Ld vector (allgathered restriction)
-   double *gath_buf = nullptr;
-   int gath_blk = 0;
-   int *d_gcnt = nullptr, *d_gdsp = nullptr;
-   // outer loop state
-   double *r0 = nullptr;
-   double *d_hist = nullptr;
-   int hist_cap = 1 << 16;
-   double r0norm = 0;
-   int iter = 0;
-   bool pre_ready = false, have_state = false;
-   hipEvent_t ev_pack = nullptr, ev_comm = nullptr;
-   std::vector<void *> allocs;
-   // profiling: [0] fine residual, [1] fine smoother, [2] R0, [3] P0, [4] outer residual
-   std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[5];
-   double prof_ms[5] = {0, 0, 0, 0, 0};
-   long long prof_n[5] = {0, 0, 0, 0, 0};
-};
-
-namespace {
-
-int dalloc(amg_dist_hier *D, size_t bytes, void **p)
+int amgd::dalloc(amg_dist_hier *D, size_t bytes, void **p)
 {
    hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 8));
    if (e != hipSuccess)
@@ -324,10 +273,12 @@ int dalloc(amg_dist_hier *D, size_t bytes, void **p)
    return AMG_OK;
 }
 
-int dvec(amg_dist_hier *D, size_t n, double **p)
+int amgd::dvec(amg_dist_hier *D, size_t n, double **p)
 {
    return dalloc(D, n * sizeof(double), (void **)p);
 }
+
+namespace {
 
 // owner of global column g of a level's column space: the rank r with
 // rs[r] <= g < rs[r+1] (empty ranges are skipped)
@@ -587,9 +538,13 @@ using FullFn = std::function<int(int which, int level, amg_mat **out)>;
 
 int check_opts(const amg_opts *o)
 {
-   AMG_ARG(o->solver == AMG_MULT && o->cheby_flag == 0 &&
-              (o->smoother == AMG_JACOBI || o->smoother == AMG_L1_JACOBI),
-           "amg_dist: the distributed cycle supports MULT with Jacobi / L1 Jacobi");
+   AMG_ARG(o->cheby_flag == 0 && (o->smoother == AMG_JACOBI || o->smoother == AMG_L1_JACOBI ||
+                                   o->smoother == AMG_SYMM_JACOBI),
+           "amg_dist: the distributed cycles support the Jacobi / L1 Jacobi / symmetric Jacobi "
+           "smoothers without Chebyshev");
+   AMG_ARG(o->solver == AMG_MULT || o->solver == AMG_ASYNC_MULTADD || o->solver == AMG_ASYNC_AFACX,
+           "amg_dist: solver must be MULT (amg_dist_solve_*) or ASYNC_MULTADD / ASYNC_AFACX "
+           "(amg_dist_async_solve)");
    return AMG_OK;
 }
 
@@ -671,7 +626,11 @@ int build_hier(amg_ctx *c, int L, Partition part, const amg_opts *opts, const Lo
             D->coarse_mats.push_back(Rs[l - Ld]);
          }
       }
+      D->cA.assign(As.begin(), As.end());
+      D->cP.assign(Ps.begin(), Ps.begin() + (Lc - 1));
+      D->cR.assign(Rs.begin(), Rs.begin() + (Lc - 1));
       amg_opts co = *opts;
+      co.solver = AMG_MULT; // the replicated levels run the multiplicative sub-cycle
       co.profile = 0;
       co.reuse_outer_residual = 0;
       AMG_TRY(amg_hier_create(c, Lc, As.data(), Ps.data(), Rs.data(), &co, &D->coarse));
@@ -1030,24 +989,32 @@ int d_outer_residual(amg_dist_hier *D, int slot)
 
 } // namespace
 
-extern "C" int amg_dist_solve_start(amg_dist_hier *D, const double *f_local, double *r0norm)
+int amgd::dist_outer_residual(amg_dist_hier *D, int slot) { return d_outer_residual(D, slot); }
+
+int amgd::dist_solve_begin(amg_dist_hier *D, const double *f_local)
 {
-   AMG_ARG(D && f_local, "amg_dist_solve_start: null argument");
    amg_ctx *c = D->ctx;
    for (auto &v : D->lv) {
       for (double *p : {v.f, v.u, v.u_alt, v.r_fine}) amgk::vset(c->stream, p, 0.0, 0, v.cap);
       v.zero_flag = 0;
    }
-   AMG_TRY(h2d(D->ctx->stream, D->lv[0].f, f_local, (size_t)D->lv[0].n * sizeof(double)));
+   AMG_TRY(h2d(c->stream, D->lv[0].f, f_local, (size_t)D->lv[0].n * sizeof(double)));
    // InitVectors on the replicated levels (the coarsest iterate carries over
    // between cycles, so a new solve starts it from zero as one GPU does)
    if (D->coarse) AMG_TRY(amg_hier_reset(D->coarse));
    D->iter = 0;
    AMG_TRY(d_outer_residual(D, 0));
-   AMG_HIP(hipMemcpyAsync(c->h_pinned, D->d_hist, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-   AMG_HIP(hipStreamSynchronize(c->stream));
+   AMG_TRY(d2h(c->stream, c->h_pinned, D->d_hist, sizeof(double)));
    D->r0norm = c->h_pinned[0];
    D->have_state = true;
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_solve_start(amg_dist_hier *D, const double *f_local, double *r0norm)
+{
+   AMG_ARG(D && f_local, "amg_dist_solve_start: null argument");
+   AMG_ARG(D->o.solver == AMG_MULT, "amg_dist_solve_start: MULT hierarchies (ASYNC_*: amg_dist_async_solve)");
+   AMG_TRY(dist_solve_begin(D, f_local));
    if (r0norm) *r0norm = D->r0norm;
    return AMG_OK;
 }

@@ -1,0 +1,301 @@
+// amg_dist_async.cpp -- asynchronous additive AMG across GPUs.
+//
+// Reference: the DMEM asynchronous additive solver (DMEM_Add.cpp:20-178 driver,
+// AddCycle :180-329, DMEM_AddCorrect_LocalRes :391-458, DMEM_AddCheckComm
+// :460-528, DMEM_AddResidual_LocalRes :530-556; message engine DMEM_Comm.cpp)
+// and its shared-memory form SMEM_Async_Add_AMG (SMEM_Async_AMG.cpp:7-437).
+//
+// MI355X mapping.  The reference gives every level ("grid k") its own group of
+// MPI ranks holding a full copy of the fine problem and ships whole-vector
+// corrections between the groups.  Here every GPU owns a z-slab of every level
+// and every level k runs as its own HIP stream on every GPU:
+//   * level k restricts its private residual down to level k, smooths there
+//     (SMEM smoother semantics: zero-guess symmetric / L1 / weighted Jacobi),
+//     prolongs back and adds the correction into the shared slab of u with
+//     device-scope fp64 atomics -- the GPU-resident equivalent of the
+//     gridjToGridk correction messages, without moving vectors between GPUs;
+//   * it then recomputes its private residual f - A u_k from the value of u it
+//     observed at its own update (LOCAL residual, SMEM_Async_AMG.cpp:284-301);
+//   * every operator application of level k exchanges its ghost rows with the
+//     neighbouring slabs over RCCL point-to-point on level k's OWN
+//     communicator (ncclCommSplit), enqueued on level k's stream, so levels
+//     never wait for each other -- on the GPU or across GPUs;
+//   * levels below the replication threshold are computed redundantly on every
+//     rank after one allgather of the restricted residual.
+// Termination: each level performs num_cycles corrections (LOCAL convergence,
+// fixed count), then the streams join and the outer residual is formed.
+#include <algorithm>
+#include <vector>
+
+#include "amg_dist_internal.h"
+
+using namespace amgd;
+
+namespace {
+
+bool multadd_of(const amg_opts &o) { return o.solver == AMG_ASYNC_MULTADD || o.solver == AMG_MULTADD; }
+
+int level_n(const amg_dist_hier *D, int l)
+{
+   return l < D->Ld ? D->lv[l].n : D->cA[l - D->Ld]->nrows;
+}
+
+int level_cap(const amg_dist_hier *D, int l)
+{
+   return l < D->Ld ? D->lv[l].cap : D->cA[l - D->Ld]->nrows;
+}
+
+// ghost exchange of x for M on the level stream over the level's communicator
+int a_halo(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x)
+{
+   if (M.replicated_cols || M.peers.empty()) return AMG_OK;
+   double *&sb = a.sbuf[&M];
+   if (!sb) AMG_TRY(dvec(D, std::max<long long>(1, M.nsend), &sb));
+   launch_gather(a.s, x, M.d_send_idx, sb, (int)M.nsend);
+   const int np = (int)M.peers.size();
+   std::vector<void *> sp(np), rp(np);
+   std::vector<long long> sbytes(np), rbytes(np);
+   for (int i = 0; i < np; i++) {
+      sp[i] = sb + M.soff[i];
+      sbytes[i] = M.scnt[i] * 8;
+      rp[i] = x + M.ncol_own + M.roff[i];
+      rbytes[i] = M.rcnt[i] * 8;
+   }
+   return xp_p2p(D->ctx, a.s, np, M.peers.data(), sp.data(), sbytes.data(), rp.data(), rbytes.data(),
+                 a.comm);
+}
+
+int a_spgemv(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x, const double *b,
+             const amgk::Gemv &g, double *y)
+{
+   AMG_TRY(a_halo(D, a, M, x));
+   amgk::spgemv(a.s, M.A, x, b, g, y, 0, M.nrows, nullptr);
+   return AMG_OK;
+}
+
+// y = A_l x (+ b per g) on level l
+int apply_A(amg_dist_hier *D, AsyncLevel &a, int l, double *x, const double *b, const amgk::Gemv &g,
+            double *y)
+{
+   if (l < D->Ld) return a_spgemv(D, a, D->lv[l].A, x, b, g, y);
+   amgk::spgemv(a.s, D->cA[l - D->Ld], x, b, g, y, 0, level_n(D, l), nullptr);
+   return AMG_OK;
+}
+
+const double *diag_of(const amg_dist_hier *D, int l)
+{
+   return l < D->Ld ? D->lv[l].A.A->diag : D->cA[l - D->Ld]->diag;
+}
+
+const double *l1_of(const amg_dist_hier *D, int l)
+{
+   return l < D->Ld ? D->lv[l].l1 : D->cl1[l - D->Ld];
+}
+
+// r[l+1] = R_l r[l] (SMEM_Sync_Parfor_Restrict / hypre MatvecT in AddCycle)
+int restrict_to(amg_dist_hier *D, AsyncLevel &a, int l)
+{
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   const int Ld = D->Ld;
+   if (l + 1 < Ld) return a_spgemv(D, a, D->lv[l].R, a.r[l], nullptr, mv, a.r[l + 1]);
+   if (l + 1 == Ld) {
+      const int R = D->ctx->xport->nranks;
+      double *slot = a.gath + (size_t)D->gath_blk * R;
+      AMG_TRY(a_spgemv(D, a, D->lv[l].R, a.r[l], nullptr, mv, slot));
+      AMG_TRY(xp_allgather(D->ctx, a.s, slot, a.gath, (long long)D->gath_blk * 8, a.comm));
+      launch_scatter_blocks(a.s, a.gath, D->gath_blk, D->d_gcnt, D->d_gdsp, R, a.r[l + 1]);
+      return AMG_OK;
+   }
+   amgk::spgemv(a.s, D->cR[l - Ld], a.r[l], nullptr, mv, a.r[l + 1], 0, level_n(D, l + 1), nullptr);
+   return AMG_OK;
+}
+
+// out = P_l x (x on level l+1, out on level l)
+int prolong_to(amg_dist_hier *D, AsyncLevel &a, int l, double *x, double *out)
+{
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   if (l < D->Ld) return a_spgemv(D, a, D->lv[l].P, x, nullptr, mv, out);
+   amgk::spgemv(a.s, D->cP[l - D->Ld], x, nullptr, mv, out, 0, level_n(D, l), nullptr);
+   return AMG_OK;
+}
+
+// smooth_all_levels (amg_solver.cpp) on level l, zero initial guess (the add
+// cycle sets zero_flags[k] = 1): symmetric Jacobi for MULTADD with pre and
+// post sweeps (SMEM_Sync_Symmetric[L1]Jacobi, SMEM_Smooth.cpp:643-762, the
+// DMEM_AddSmooth 2-step form DMEM_Smooth.cpp:574-638), else L1 / weighted
+// Jacobi (SMEM_Sync_[L1]Jacobi :365-443).  u_prev / sy / sr: scratch with ghost room.
+int a_smooth(amg_dist_hier *D, AsyncLevel &a, int l, const double *f, double *u, int sweeps)
+{
+   const amg_opts &o = D->o;
+   hipStream_t s = a.s;
+   const int n = level_n(D, l);
+   const bool l1 = o.smoother == AMG_L1_JACOBI;
+   const double omega = l1 ? 1.0 : o.smooth_weight;
+   const double *l1v = l1 ? l1_of(D, l) : nullptr;
+   const double *dg = diag_of(D, l);
+   const bool sym = multadd_of(o) && o.num_post_smooth_sweeps > 0 && o.num_pre_smooth_sweeps > 0;
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   if (sweeps <= 0) return AMG_OK;
+   if (sym) {
+      // amg_sym_jacobi_dev with zero_first = 1, variant 0 (SMEM)
+      amgk::vcopy(s, f, a.sr, 0, n);
+      for (int k = 0;;) {
+         amgk::sym_scale(s, dg, l1v, omega, a.sr, 0, n, 0);
+         AMG_TRY(apply_A(D, a, l, a.sr, nullptr, mv, a.sy));
+         amgk::sym_update(s, dg, l1v, omega, a.sr, a.sy, u, 0, n, 0, 1);
+         if (++k == sweeps) break;
+         AMG_TRY(apply_A(D, a, l, u, nullptr, mv, a.sy));
+         amgk::vsub(s, f, a.sy, a.sr, 0, n);
+      }
+      return AMG_OK;
+   }
+   for (int k = 0; k < sweeps; k++) {
+      if (k == 0) {
+         amgk::jacobi_zero(s, dg, f, l1v, omega, u, 0, n, 0);
+      } else {
+         amgk::vcopy(s, u, a.u_prev, 0, n);
+         if (l < D->Ld) {
+            DistMat &M = D->lv[l].A;
+            AMG_TRY(a_halo(D, a, M, a.u_prev));
+            amgk::jacobi_sweep(s, M.A, f, a.u_prev, l1v, omega, u, 0, n);
+         } else {
+            amgk::jacobi_sweep(s, D->cA[l - D->Ld], f, a.u_prev, l1v, omega, u, 0, n);
+         }
+      }
+   }
+   return AMG_OK;
+}
+
+// one correction of level k (SMEM_Async_Add_AMG inner body / DMEM AddCycle)
+int level_correction(amg_dist_hier *D, int k)
+{
+   AsyncLevel &a = D->al[k];
+   const amg_opts &o = D->o;
+   const int L = D->L;
+   hipStream_t s = a.s;
+   const bool multadd = multadd_of(o);
+   const int coarsest = multadd ? k : k + 1;
+   for (int l = 0; l < coarsest && l < L - 1; l++) AMG_TRY(restrict_to(D, a, l));
+   if (multadd) {
+      amgk::vset(s, a.e[k], 0.0, 0, level_n(D, k));
+      AMG_TRY(a_smooth(D, a, k, a.r[k], a.e[k], o.num_fine_smooth_sweeps));
+   } else {
+      // AFACx (SMEM_Sync_AMG.cpp:296-406 per level): coarse smooth, prolong,
+      // fine residual, fine smooth
+      const int fg = k, cg = k + 1;
+      const int nf = level_n(D, fg), nc = level_n(D, cg);
+      amgk::vset(s, a.uf, 0.0, 0, nf);
+      amgk::vset(s, a.uc, 0.0, 0, nc);
+      AMG_TRY(a_smooth(D, a, cg, a.r[cg], a.uc, o.num_coarse_smooth_sweeps));
+      AMG_TRY(prolong_to(D, a, fg, a.uc, a.e[fg]));
+      AMG_TRY(apply_A(D, a, fg, a.e[fg], nullptr, amgk::gemv_mode(1.0, 0.0), a.sy));
+      amgk::vsub(s, a.r[fg], a.sy, a.rf, 0, nf);
+      AMG_TRY(a_smooth(D, a, fg, a.rf, a.uf, o.num_fine_smooth_sweeps));
+      amgk::vcopy(s, a.uf, a.e[k], 0, nf);
+   }
+   for (int l = k - 1; l >= 0; l--) AMG_TRY(prolong_to(D, a, l, a.e[l + 1], a.e[l]));
+   // correction into the shared slab; u_priv = the value each row saw
+   const int n0 = D->lv[0].n;
+   amgk::atomic_correct(s, D->lv[0].u, a.e[0], a.u_priv, n0);
+   // private residual r_k = f - A u_k  (SMEM_Residual on u_k)
+   AMG_TRY(a_spgemv(D, a, D->lv[0].A, a.u_priv, nullptr, amgk::gemv_mode(1.0, 0.0), a.y));
+   amgk::vsub(s, D->lv[0].f, a.y, a.r[0], 0, n0);
+   return AMG_OK;
+}
+
+int setup_async(amg_dist_hier *D)
+{
+   if (!D->al.empty()) return AMG_OK;
+   amg_ctx *c = D->ctx;
+   amg_transport *t = c->xport;
+   const int L = D->L, Ld = D->Ld;
+   const int active = std::max(1, L - 1);
+   AMG_ARG((int)c->level_streams.size() >= active,
+           "amg_dist_async_solve: context has %d level streams, need %d (amg_init nstreams)",
+           (int)c->level_streams.size(), active);
+   // l1 norms of the replicated levels
+   for (int l = Ld; l < L; l++) {
+      double *p;
+      AMG_TRY(dvec(D, std::max(1, level_n(D, l)), &p));
+      amgk::l1_norms(c->stream, D->cA[l - Ld], p);
+      D->cl1.push_back(p);
+   }
+   // one communicator per level stream: RCCL orders operations per
+   // communicator, so independent level streams need independent communicators
+   if (!t->host() && (int)t->level_comms.size() < active) {
+      for (int k = (int)t->level_comms.size(); k < active; k++) {
+         ncclComm_t nc;
+         AMG_NCCL(ncclCommSplit(t->comm, 0, t->rank, &nc, nullptr));
+         t->level_comms.push_back(nc);
+      }
+   }
+   const bool multadd = multadd_of(D->o);
+   D->al.resize(active);
+   for (int k = 0; k < active; k++) {
+      AsyncLevel &a = D->al[k];
+      a.s = c->level_streams[k];
+      a.comm = t->host() ? nullptr : t->level_comms[k];
+      const int coarsest = std::min(L - 1, multadd ? k : k + 1);
+      a.r.assign(coarsest + 1, nullptr);
+      a.e.assign(k + 1, nullptr);
+      for (int l = 0; l <= coarsest; l++) AMG_TRY(dvec(D, level_cap(D, l), &a.r[l]));
+      for (int l = 0; l <= k; l++) AMG_TRY(dvec(D, level_cap(D, l), &a.e[l]));
+      const int ck = level_cap(D, k), ck1 = level_cap(D, std::min(L - 1, k + 1));
+      const int cm = std::max(ck, ck1);
+      AMG_TRY(dvec(D, D->lv[0].cap, &a.u_priv));
+      AMG_TRY(dvec(D, std::max(cm, D->lv[0].n), &a.y));
+      AMG_TRY(dvec(D, cm, &a.u_prev));
+      AMG_TRY(dvec(D, cm, &a.sy));
+      AMG_TRY(dvec(D, cm, &a.sr));
+      if (!multadd) {
+         AMG_TRY(dvec(D, ck, &a.uf));
+         AMG_TRY(dvec(D, ck1, &a.uc));
+         AMG_TRY(dvec(D, ck, &a.rf));
+      }
+      if (Ld < L) AMG_TRY(dvec(D, (size_t)D->gath_blk * (t->nranks + 1), &a.gath));
+   }
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   return AMG_OK;
+}
+
+} // namespace
+
+extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int *level_corrections,
+                                    double *relres)
+{
+   AMG_ARG(D && f_local, "amg_dist_async_solve: null argument");
+   AMG_ARG(D->o.solver == AMG_ASYNC_MULTADD || D->o.solver == AMG_ASYNC_AFACX,
+           "amg_dist_async_solve: ASYNC_MULTADD / ASYNC_AFACX hierarchies only");
+   AMG_ARG(D->o.async_type == AMG_FULL_ASYNC, "amg_dist_async_solve: SEMI_ASYNC not supported");
+   AMG_ARG(D->L >= 2, "amg_dist_async_solve: needs at least two levels");
+   amg_ctx *c = D->ctx;
+   AMG_TRY(setup_async(D));
+   AMG_TRY(dist_solve_begin(D, f_local));
+   const int active = (int)D->al.size();
+   const int n0 = D->lv[0].n;
+   hipEvent_t ready;
+   AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+   AMG_HIP(hipEventRecord(ready, c->stream));
+   for (int k = 0; k < active; k++) {
+      AMG_HIP(hipStreamWaitEvent(D->al[k].s, ready, 0));
+      // level_vector[k].r[0] = vector.r[0] (SMEM_Async_AMG.cpp:10-15)
+      amgk::vcopy(D->al[k].s, D->r0, D->al[k].r[0], 0, n0);
+   }
+   // issue order cycle-major / level-minor: every rank enqueues the same
+   // sequence per level communicator; the GPU runs the level streams freely
+   for (int cyc = 0; cyc < D->o.num_cycles; cyc++)
+      for (int k = 0; k < active; k++) AMG_TRY(level_correction(D, k));
+   for (int k = 0; k < active; k++) {
+      AMG_HIP(hipEventRecord(ready, D->al[k].s));
+      AMG_HIP(hipStreamWaitEvent(c->stream, ready, 0));
+   }
+   AMG_HIP(hipEventDestroy(ready));
+   D->pre_ready = false;
+   AMG_TRY(dist_outer_residual(D, 1));
+   D->iter = 1;
+   AMG_TRY(d2h(c->stream, c->h_pinned, D->d_hist + 1, sizeof(double)));
+   if (relres) *relres = c->h_pinned[0] / D->r0norm;
+   if (level_corrections)
+      for (int k = 0; k < D->L; k++) level_corrections[k] = k < active ? D->o.num_cycles : 0;
+   return AMG_OK;
+}

@@ -1,0 +1,135 @@
+// amg_dist_internal.h -- shared internals of the multi-GPU solve phase
+// (amg_dist.cpp: transport, plans, synchronous cycle; amg_dist_async.cpp:
+// asynchronous additive cycle).  Not part of the C-ABI.
+#pragma once
+
+#include <rccl/rccl.h>
+
+#include <map>
+#include <vector>
+
+#include "amg_internal.h"
+
+struct amg_transport {
+   int nranks = 1, rank = 0;
+   ncclComm_t comm = nullptr;
+   amg_host_xchg_fn fn = nullptr; // test transport through host memory
+   void *user = nullptr;
+   std::vector<ncclComm_t> level_comms; // one per async level stream (ncclCommSplit)
+   bool host() const { return fn != nullptr; }
+};
+
+#define AMG_NCCL(call)                                                                     \
+   do {                                                                                    \
+      ncclResult_t _r = (call);                                                            \
+      if (_r != ncclSuccess)                                                               \
+         return amg_set_error(AMG_ERR_RCCL, "%s:%d %s -> %s", __FILE__, __LINE__, #call,  \
+                              ncclGetErrorString(_r));                                     \
+   } while (0)
+
+namespace amgd {
+
+
+struct Partition {
+   // per level: first global row of every rank (size nranks + 1)
+   std::vector<std::vector<long long>> rs;
+   long long rows_begin(int l, int r) const { return rs[l][r]; }
+   long long rows_end(int l, int r) const { return rs[l][r + 1]; }
+   long long total(int l) const { return rs[l].back(); }
+};
+
+struct DistMat {
+   amg_mat *A = nullptr;        // local rows, remapped columns
+   long long row0 = 0;          // first global row
+   int nrows = 0;
+   int ncol_own = 0;            // owned columns (x region [0, ncol_own))
+   int nghost = 0;              // ghost region [ncol_own, ncol_own + nghost)
+   bool replicated_cols = false; // columns index a full replicated vector
+   int b0 = 0, b1 = 0;          // interior rows [b0, b1): no ghost column
+   std::vector<int> peers;      // union of send/recv peers
+   std::vector<long long> scnt, rcnt; // doubles per peer
+   std::vector<long long> soff, roff; // offsets into sendbuf / ghost region
+   int *d_send_idx = nullptr;   // owned-column index list of all sends
+   long long nsend = 0;
+   double *sendbuf = nullptr;
+};
+
+struct DLevel {
+   int n = 0;                  // owned rows
+   long long row0 = 0;
+   int cap = 0;                // vector capacity (owned + max ghosts)
+   DistMat A, P, R;            // P: level l -> l+1 (rows = level l), R: rows = level l+1
+   double *f = nullptr, *u = nullptr, *u_alt = nullptr, *r_fine = nullptr, *l1 = nullptr;
+   int zero_flag = 0;
+};
+
+
+// per-stream exchange state of the asynchronous additive cycle (one per level)
+struct AsyncLevel {
+   hipStream_t s = nullptr;
+   ncclComm_t comm = nullptr;
+   std::map<const DistMat *, double *> sbuf; // pack buffers of this stream
+   std::vector<double *> r, e;               // r[l], e[l]: level-l residual / correction
+   double *u_priv = nullptr, *y = nullptr, *y_fine = nullptr;
+   double *u_prev = nullptr, *sy = nullptr, *sr = nullptr; // smoother scratch (level k)
+   double *uf = nullptr, *uc = nullptr, *rf = nullptr; // AFACx fine / coarse iterates, fine residual
+   double *gath = nullptr;                   // allgather staging at the replication level
+};
+
+// host <-> device copies ordered on stream s and complete on return
+int h2d(hipStream_t s, void *dst, const void *src, size_t bytes);
+int d2h(hipStream_t s, void *dst, const void *src, size_t bytes);
+// transport operations on stream s over communicator comm (nullptr: the main one)
+int xp_p2p(amg_ctx *c, hipStream_t s, int np, const int *peers, void *const *send,
+           const long long *sbytes, void *const *recv, const long long *rbytes,
+           ncclComm_t comm = nullptr);
+int xp_allreduce(amg_ctx *c, hipStream_t s, double *dev, int n, ncclComm_t comm = nullptr);
+int xp_allgather(amg_ctx *c, hipStream_t s, const void *send, void *recv, long long bytes,
+                 ncclComm_t comm = nullptr);
+void launch_gather(hipStream_t s, const double *x, const int *idx, double *out, int n);
+void launch_scatter_blocks(hipStream_t s, const double *src, int blk, const int *cnt,
+                           const int *dsp, int nranks, double *dst);
+void launch_sqrt(hipStream_t s, const double *in, double *out);
+
+} // namespace amgd
+
+struct amg_dist_hier {
+   amg_ctx *ctx = nullptr;
+   amg_opts o{};
+   int L = 0, Ld = 0; // levels [0, Ld) distributed, [Ld, L) replicated
+   amgd::Partition part;
+   std::vector<amgd::DLevel> lv;
+   // replicated coarse part
+   amg_hier *coarse = nullptr;
+   std::vector<amg_mat *> coarse_mats;
+   double *f_rep = nullptr;   // full level-Ld vector (allgathered restriction)
+   double *gath_buf = nullptr;
+   int gath_blk = 0;
+   int *d_gcnt = nullptr, *d_gdsp = nullptr;
+   // outer loop state
+   double *r0 = nullptr;
+   double *d_hist = nullptr;
+   int hist_cap = 1 << 16;
+   double r0norm = 0;
+   int iter = 0;
+   bool pre_ready = false, have_state = false;
+   hipEvent_t ev_pack = nullptr, ev_comm = nullptr;
+   std::vector<void *> allocs;
+   // profiling: [0] fine residual, [1] fine smoother, [2] R0, [3] P0, [4] outer residual
+   std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[5];
+   // asynchronous additive cycle (built on first use)
+   std::vector<amgd::AsyncLevel> al;
+   std::vector<amg_mat *> cA, cP, cR; // replicated levels' operators (level Ld + i)
+   std::vector<double *> cl1;         // and their l1 norms
+   double prof_ms[5] = {0, 0, 0, 0, 0};
+   long long prof_n[5] = {0, 0, 0, 0, 0};
+};
+
+namespace amgd {
+int dalloc(amg_dist_hier *D, size_t bytes, void **p);
+int dvec(amg_dist_hier *D, size_t n, double **p);
+// InitVectors + initial outer residual r0 = f - A u (u = 0) and its norm
+int dist_solve_begin(amg_dist_hier *D, const double *f_local);
+// r0 = f - A u, ||r0|| into d_hist[slot] (all ranks)
+int dist_outer_residual(amg_dist_hier *D, int slot);
+} // namespace amgd

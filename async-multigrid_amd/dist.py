@@ -270,6 +270,17 @@ class DistHier:
         check(lib.amg_dist_solve_resnorm(self.h, C.byref(r)))
         return r.value
 
+    def async_solve(self, f_local):
+        """Asynchronous additive solve (ASYNC_MULTADD / ASYNC_AFACX opts):
+        returns (relres, per-level correction counts); u via get_u()."""
+        f = np.ascontiguousarray(f_local, dtype=np.float64)
+        assert f.size == self.n0
+        L = self.gen.L if self.gen is not None else 64
+        cnt = np.zeros(max(L, 64), dtype=np.int32)
+        rel = C.c_double()
+        check(lib.amg_dist_async_solve(self.h, _dp(f), _ip(cnt), C.byref(rel)))
+        return rel.value, cnt
+
     def get_u(self):
         u = np.empty(self.n0)
         check(lib.amg_dist_get_u(self.h, _dp(u)))

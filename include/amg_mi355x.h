@@ -283,6 +283,15 @@ int amg_dist_solve_iterate(amg_dist_hier *D, int k);
 int amg_dist_solve_resnorm(amg_dist_hier *D, double *out);
 int amg_dist_get_u(amg_dist_hier *D, double *u_local);
 int amg_dist_profile_read(amg_dist_hier *D, double *ms, long long *launches, int reset);
+/* asynchronous additive AMG across GPUs (DMEM_Add DMEM_Add.cpp:20-178, AddCycle
+ * :180-329, DMEM_AddCorrect_LocalRes :391-458; SMEM_Async_Add_AMG semantics):
+ * hierarchy created with solver ASYNC_MULTADD or ASYNC_AFACX.  Every level runs
+ * num_cycles corrections on its own HIP stream with its own RCCL communicator
+ * (ghost rows per operator, never waiting for other levels), adding into the
+ * shared slab of u with fp64 atomics.  u starts at zero; read it with
+ * amg_dist_get_u.  *relres = ||f - A u|| / ||f|| after the levels joined. */
+int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int *level_corrections,
+                         double *relres);
 /* y = A_0 x on the distributed fine operator (halo exchange + interior/boundary
  * split); *ms = average device milliseconds over reps */
 int amg_dist_fine_spmv(amg_dist_hier *D, int reps, double *ms);

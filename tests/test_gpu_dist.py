@@ -251,3 +251,80 @@ def test_dist_from_parts_any_partition(amg, ctx, cuts, rep):
     assert_bitwise(np.concatenate([t[0] for t in res]), u1, "from_parts iterate")
     np.testing.assert_allclose(res[0][1], h1, rtol=1e-12, atol=0)
     gen.free()
+
+
+def split_host(host, cuts):
+    """row_starts + per-rank (A, P, R) pieces from full host operators (oracle Csr)."""
+    L = len(host["A"])
+    nranks = len(cuts) + 1
+    rs = np.zeros((L, nranks + 1), dtype=np.int64)
+    for l in range(L):
+        n = host["A"][l].nrows
+        rs[l, 1:-1] = [int(round(c * n)) for c in cuts]
+        rs[l, -1] = n
+
+    def rows(M, a, b):
+        lo, hi = M.rowptr[a], M.rowptr[b]
+        return (b - a, M.rowptr[a:b + 1] - lo, M.col[lo:hi], M.val[lo:hi])
+
+    parts = []
+    for r in range(nranks):
+        parts.append(([rows(host["A"][l], rs[l, r], rs[l, r + 1]) for l in range(L)],
+                      [rows(host["P"][l], rs[l, r], rs[l, r + 1]) for l in range(L - 1)],
+                      [rows(host["R"][l], rs[l + 1, r], rs[l + 1, r + 1]) for l in range(L - 1)]))
+    return rs, parts
+
+
+@pytest.mark.parametrize("solver,cuts,rep", [("multadd", (0.5,), 0), ("multadd", (0.3, 0.7), 1000),
+                                             ("afacx", (0.45,), 0), ("multadd", (), 0),
+                                             ("afacx", (), 1000)])
+def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
+    """Distributed asynchronous additive AMG (level streams x ranks, per-level
+    communicators): nondeterministic; its relres after N corrections per level
+    sits in the same band around the oracle's synchronous additive cycle as the
+    single-GPU async solver (test_gpu_solve.py::test_async_multadd_band)."""
+    from test_gpu_solve import hierarchy, oracle_opts
+    _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
+    w = 0.8
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs_ = oracle.smooth_transfer(host["A"][lev], host["P"][lev], w)
+        Ps.append(ps)
+        Rs.append(rs_)
+    host = {"A": host["A"], "P": Ps, "R": Rs}
+    N = 15
+    f = amg.rhs_rand(0, 24 ** 3)
+    sync_solver = amg.AMG_MULTADD if solver == "multadd" else amg.AMG_AFACX
+    sync_opts = amg.default_opts(solver=sync_solver, smooth_weight=w, num_cycles=N, tol=0.0)
+    _, h_c, _ = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, sync_opts)).solve(f)
+    sync_rel = h_c[-1] / h_c[0]
+    a_solver = amg.AMG_ASYNC_MULTADD if solver == "multadd" else amg.AMG_ASYNC_AFACX
+    opts = amg.default_opts(solver=a_solver, smooth_weight=w, num_cycles=N, tol=0.0)
+    rs, parts = split_host(host, cuts)
+    nranks = len(cuts) + 1
+    hub = amg.dist.ThreadMailbox(nranks)
+
+    def rank(r):
+        c = amg.Context(0, nstreams=L)
+        if nranks == 1:  # one rank: the RCCL transport itself (ncclCommSplit per level)
+            amg.dist.init_rccl(c, 1, 0, lambda b: b)
+        else:
+            amg.dist.init_host(c, nranks, r, amg.dist.HostTransport(hub, r))
+        amg.dist.set_replicate_rows(c, rep)
+        A, P, R = parts[r]
+        D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
+        rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
+        u = D.get_u()
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        return rel, u, cnt
+
+    res = run_ranks(nranks, rank)
+    rels = [t[0] for t in res]
+    assert all(r == rels[0] for r in rels)  # one allreduced norm
+    u = np.concatenate([t[1] for t in res])
+    assert np.all(np.isfinite(u))
+    assert list(res[0][2][:L - 1]) == [N] * (L - 1)
+    assert rels[0] < 1.0
+    assert sync_rel / 50 <= rels[0] <= sync_rel * 50, (rels[0], sync_rel)
