@@ -63,6 +63,10 @@ class Context:
     def sync(self):
         check(lib.amg_sync(self.h))
 
+    def set_value_index(self, enable):
+        """Value-indexed CSR for matrices registered from now on (default on)."""
+        check(lib.amg_set_value_index(self.h, int(enable)))
+
     def csr(self, nrows, ncols, rowptr, col, val, diag_first=1):
         return Mat.register(self, nrows, ncols, rowptr, col, val, diag_first)
 
@@ -88,6 +92,7 @@ class Mat:
         nr, nc, nz = C.c_int(), C.c_int(), C.c_longlong()
         check(lib.amg_mat_info(handle, C.byref(nr), C.byref(nc), C.byref(nz)))
         self.nrows, self.ncols, self.nnz = nr.value, nc.value, nz.value
+        self.value_index = lib.amg_mat_value_index(handle)  # table size, 0 = plain CSR
 
     @classmethod
     def register(cls, ctx, nrows, ncols, rowptr, col, val, diag_first=1):

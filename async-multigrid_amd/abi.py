@@ -51,6 +51,8 @@ PROTOTYPES = {
     "amg_version": (_i, []),
     "amg_csr_register": (_i, [_p, _i, _i, _ll, _ip, _ip, _dp, _i, _pp]),
     "amg_mat_free": (_i, [_p]),
+    "amg_set_value_index": (_i, [_p, _i]),
+    "amg_mat_value_index": (_i, [_p]),
     "amg_mat_info": (_i, [_p, _ip, _ip, _llp]),
     "amg_mat_download": (_i, [_p, _p, _ip, _ip, _dp]),
     "amg_vec_create": (_i, [_p, _i, _pp]),

@@ -70,6 +70,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    AMG_HIP(hipHostMalloc(&c->h_pinned, 1024 * sizeof(double)));
    hipDeviceProp_t prop;
    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+   if (const char *v = std::getenv("AMG_VALUE_INDEX")) c->value_index = std::atoi(v) != 0;
    *out = c;
    return AMG_OK;
 }
@@ -142,11 +143,76 @@ static int mat_alloc(amg_ctx *c, int nrows, int ncols, long long nnz, amg_mat **
    return AMG_OK;
 }
 
+// value-indexed CSR (CSR-VI): when the matrix holds at most 256 distinct
+// values (by bit pattern) the hot kernels stream one byte per entry instead
+// of eight and read the value from an LDS table -- bit-identical products.
+// val stays resident for the other kernels and for amg_mat_download.
+static int build_value_index(amg_mat *A)
+{
+   amg_ctx *c = A->ctx;
+   hipStream_t s = c->stream;
+   constexpr int NS = 4096;
+   unsigned long long *slots = nullptr;
+   AMG_HIP(hipMalloc(&slots, NS * sizeof(unsigned long long) + 64));
+   int *count = reinterpret_cast<int *>(slots + NS);
+   AMG_HIP(hipMemsetAsync(slots, 0xff, NS * sizeof(unsigned long long), s));
+   AMG_HIP(hipMemsetAsync(count, 0, sizeof(int), s));
+   amgk::vi_collect(s, A->val, A->nnz, slots, NS, count);
+   std::vector<unsigned long long> h(NS);
+   int cnt = 0;
+   AMG_HIP(hipMemcpyAsync(h.data(), slots, NS * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(&cnt, count, sizeof(int), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   if (cnt < 1 || cnt > 256) {
+      hipFree(slots);
+      return AMG_OK; // plain CSR
+   }
+   std::vector<unsigned long long> keys;
+   for (auto k : h)
+      if (k != ~0ULL) keys.push_back(k);
+   std::sort(keys.begin(), keys.end());
+   const int T = (int)keys.size();
+   std::vector<double> tab(256, 0.0);
+   std::memcpy(tab.data(), keys.data(), T * sizeof(double));
+   hipError_t e = hipMalloc(&A->vidx, (size_t)A->nnz + 64);
+   if (e == hipSuccess) e = hipMalloc(&A->vtab, 256 * sizeof(double));
+   if (e != hipSuccess) { // not enough room: keep plain CSR
+      hipFree(A->vidx);
+      hipFree(A->vtab);
+      A->vidx = nullptr;
+      A->vtab = nullptr;
+      hipFree(slots);
+      (void)hipGetLastError();
+      return AMG_OK;
+   }
+   AMG_HIP(hipMemcpyAsync(slots, keys.data(), T * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemcpyAsync(A->vtab, tab.data(), 256 * sizeof(double), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemsetAsync(A->vidx + A->nnz, 0, 64, s));
+   amgk::vi_encode(s, A->val, A->nnz, slots, T, A->vidx);
+   AMG_HIP(hipStreamSynchronize(s));
+   hipFree(slots);
+   A->vi_n = T;
+   return AMG_OK;
+}
+
 int amg_mat_finish(amg_mat *A)
 {
    amgk::extract_diag(A->ctx->stream, A);
    AMG_HIP(hipGetLastError());
+   if (A->ctx->value_index && A->nnz > 0) AMG_TRY(build_value_index(A));
    return AMG_OK;
+}
+
+extern "C" int amg_set_value_index(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_value_index: null context");
+   c->value_index = enable ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_value_index(const amg_mat *A)
+{
+   return A ? A->vi_n : 0;
 }
 
 int amg_mat_create_device(amg_ctx *c, int nrows, int ncols, long long nnz, amg_mat **out)
@@ -187,6 +253,8 @@ extern "C" int amg_mat_free(amg_mat *A)
    hipFree(A->col);
    hipFree(A->val);
    hipFree(A->diag);
+   hipFree(A->vidx);
+   hipFree(A->vtab);
    delete A;
    return AMG_OK;
 }
@@ -377,6 +445,20 @@ void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x
 } // namespace amgk
 
 extern "C" int amg_dev_tune_count(void) { return amgk::num_tune_variants(); }
+
+// development entry (tools/pmc_traffic.py): one calibration stream over a
+// fresh device buffer of `bytes` bytes
+extern "C" int amg_dev_calib(amg_ctx *c, int mode, long long bytes)
+{
+   AMG_ARG(c && mode >= 0 && mode <= 4 && bytes > 0, "amg_dev_calib: bad argument");
+   void *buf = nullptr;
+   AMG_HIP(hipMalloc(&buf, (size_t)bytes));
+   AMG_HIP(hipMemsetAsync(buf, 1, (size_t)bytes, c->stream));
+   amgk::calib_stream(c->stream, mode, buf, bytes, c->d_scalars + 8000);
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   hipFree(buf);
+   return AMG_OK;
+}
 extern "C" const char *amg_dev_tune_name(int v) { return amgk::tune_variant_name(v); }
 
 extern "C" int amg_dev_tune_spmv(amg_ctx *c, const amg_mat *A, const amg_vec *x, amg_vec *y,

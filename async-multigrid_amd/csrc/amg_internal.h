@@ -56,6 +56,7 @@ struct amg_ctx {
    double *d_scalars = nullptr;            // device scalars (norms, dots)
    double *h_pinned = nullptr;             // pinned host mirror of scalars
    int num_cus = 256;
+   int value_index = 1; // build value-indexed CSR for matrices with <= 256 distinct values
 };
 
 struct amg_mat {
@@ -68,6 +69,11 @@ struct amg_mat {
    double *diag = nullptr; // val[rowptr[i]] (the reference's a_ii), or 0 for empty rows
    int diag_first = 1;
    amg_mat *trans = nullptr; // lazily built transpose for amg_matvec_t
+   // value-indexed form (the hot kernels' format when the matrix has at most
+   // 256 distinct values): vidx[k] indexes vtab (256 doubles, sorted by bits)
+   unsigned char *vidx = nullptr;
+   double *vtab = nullptr;
+   int vi_n = 0;
 };
 
 struct amg_vec {
@@ -154,6 +160,15 @@ void cheby_update(hipStream_t s, double *u, double *u_outer, double *y_outer, do
                   double delta, int n);
 // atomic correction: u += e (device-scope fp64 atomics), u_priv = value after the add
 void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n);
+
+// PMC calibration streams: mode 0/1/2/3 = read bytes with 16/8/4/1-byte lanes, 4 = 8-byte writes
+void calib_stream(hipStream_t s, int mode, void *buf, long long bytes, double *out);
+
+// value-indexed CSR construction
+void vi_collect(hipStream_t s, const double *val, long long nnz, unsigned long long *slots, int nslots,
+                int *count);
+void vi_encode(hipStream_t s, const double *val, long long nnz, const unsigned long long *keys, int T,
+               unsigned char *vidx);
 
 // deterministic reductions
 void sumsq_partials(hipStream_t s, const double *x, int n, double *partials, int *nparts);

@@ -46,13 +46,16 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 // per LDS chunk, NT non-temporal val/col streams (read once; keep L2 for x),
 // XCD contiguous-range tile remap (T1; speed only, any placement is correct).
 template <int RPT, int CH, bool NT, bool XCD, bool UNR = false, bool SKIPSYNC = false,
-          bool SHFL = false>
+          bool SHFL = false, bool STR = false, bool W8 = false>
 struct TileCfg {
    static constexpr int rpt = RPT, ch = CH;
    static constexpr bool nt = NT, xcd = XCD;
    static constexpr bool unr = UNR;       // issue two staging groups' loads before storing
    static constexpr bool skipsync = SKIPSYNC; // no barrier after the tile's last chunk
    static constexpr bool shfl = SHFL;     // rowptr[row+1] from the neighbour lane
+   static constexpr bool w8 = W8;         // 8 consecutive entries per lane, all loads up front
+   static constexpr bool str = STR;       // lane-strided entries (dword loads): one gather
+                                          // instruction covers 64 consecutive entries
 };
 
 template <bool NT>
@@ -70,20 +73,37 @@ __device__ __forceinline__ void stage4(const int *__restrict__ col, const double
    }
 }
 
-template <class Cfg, int NEG, bool NEED_DIAG, class Epi>
-__global__ __launch_bounds__(256) void csr_tile_kernel(
-   const int *__restrict__ rowptr, const int *__restrict__ col, const double *__restrict__ val,
-   const double *__restrict__ x, int rb, int re, Epi epi, double *__restrict__ partials)
+// value-indexed CSR: 4 column ids (16 B) + 4 one-byte value indices (4 B);
+// the values come from the matrix's table of distinct values held in LDS
+template <bool NT>
+__device__ __forceinline__ void stage4_vi(const int *__restrict__ col,
+                                          const unsigned char *__restrict__ vidx,
+                                          const double *vtab, int k, v4i &c4, v2d &v01, v2d &v23)
+{
+   unsigned int b;
+   if (NT) {
+      c4 = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(col + k));
+      b = __builtin_nontemporal_load(reinterpret_cast<const unsigned int *>(vidx + k));
+   } else {
+      c4 = *reinterpret_cast<const v4i *>(col + k);
+      b = *reinterpret_cast<const unsigned int *>(vidx + k);
+   }
+   v01.x = vtab[b & 0xff];
+   v01.y = vtab[(b >> 8) & 0xff];
+   v23.x = vtab[(b >> 16) & 0xff];
+   v23.y = vtab[b >> 24];
+}
+
+// one 256*RPT-row tile (body shared by the one-tile-per-workgroup and the
+// persistent launch); vtab: the value table (LDS or global)
+template <class Cfg, int NEG, bool NEED_DIAG, class Epi, bool VI, bool STAGE_TAB = false>
+__device__ __forceinline__ void tile_body(
+   int tile, const int *__restrict__ rowptr, const int *__restrict__ col,
+   const double *__restrict__ val, const double *__restrict__ x, int rb, int re, const Epi &epi,
+   double *__restrict__ partials, const unsigned char *__restrict__ vidx, double *vtab,
+   double *prod, double *red, const double *__restrict__ vtab_g = nullptr)
 {
    constexpr int RPT = Cfg::rpt, CH = Cfg::ch, TROWS = 256 * RPT;
-   __shared__ __attribute__((aligned(16))) double prod[CH];
-   __shared__ double red[4];
-   int tile = blockIdx.x;
-   if (Cfg::xcd) {
-      // bijective remap: the blocks dealt to one XCD (b % 8) get a contiguous tile range
-      const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xg = tile & 7, idx = tile >> 3;
-      tile = (xg < r ? xg * (q + 1) : r * (q + 1) + (xg - r) * q) + idx;
-   }
    const int r0 = rb + tile * TROWS;
    const int r1 = min(r0 + TROWS, re);
    const int tb = rowptr[r0];
@@ -114,21 +134,62 @@ __global__ __launch_bounds__(256) void csr_tile_kernel(
       }
       // epilogue operands issued before the stream so their latency hides
       if (row < r1) {
-         if (NEED_DIAG) dg[q] = val[rs[q]];
+         if (NEED_DIAG && !VI) dg[q] = val[rs[q]];
          pf[q] = epi.pf(row);
       }
+   }
+   if (STAGE_TAB) {
+      // the value table, staged after the prologue's loads so its latency
+      // overlaps theirs (one barrier)
+      vtab[threadIdx.x] = vtab_g[threadIdx.x];
+      __syncthreads();
+   }
+   if (NEED_DIAG && VI) {
+#pragma unroll
+      for (int q = 0; q < RPT; q++)
+         if (r0 + q * 256 + (int)threadIdx.x < r1) dg[q] = vtab[vidx[rs[q]]];
    }
    const int base = tb & ~3;
    for (int cs = base; cs < te; cs += CH) {
       const int ce = min(cs + CH, te);
-      if (Cfg::unr) {
+      if (Cfg::w8) {
+         for (int k = cs + 8 * (int)threadIdx.x; k < ce; k += 8 * 256) {
+            v4i c4, d4;
+            v2d v01, v23, w01, w23;
+            if (VI) {
+               stage4_vi<Cfg::nt>(col, vidx, vtab, k, c4, v01, v23);
+               stage4_vi<Cfg::nt>(col, vidx, vtab, k + 4, d4, w01, w23);
+            } else {
+               stage4<Cfg::nt>(col, val, k, c4, v01, v23);
+               stage4<Cfg::nt>(col, val, k + 4, d4, w01, w23);
+            }
+            const double x0 = x[c4.x], x1 = x[c4.y], x2 = x[c4.z], x3 = x[c4.w];
+            const double x4 = x[d4.x], x5 = x[d4.y], x6 = x[d4.z], x7 = x[d4.w];
+            v2d *dst = reinterpret_cast<v2d *>(prod + (k - cs));
+            dst[0] = v2d{v01.x * x0, v01.y * x1};
+            dst[1] = v2d{v23.x * x2, v23.y * x3};
+            dst[2] = v2d{w01.x * x4, w01.y * x5};
+            dst[3] = v2d{w23.x * x6, w23.y * x7};
+         }
+      } else if (Cfg::str) {
+         for (int k = cs + (int)threadIdx.x; k < ce; k += 256) {
+            const int c = col[k];
+            const double v = VI ? vtab[vidx[k]] : val[k];
+            prod[k - cs] = v * x[c];
+         }
+      } else if (Cfg::unr) {
          for (int k = cs + 4 * (int)threadIdx.x; k < ce; k += 8 * 256) {
             const int k2 = k + 4 * 256;
             const bool has2 = k2 < ce;
             v4i c4, d4;
             v2d v01, v23, w01, w23;
-            stage4<Cfg::nt>(col, val, k, c4, v01, v23);
-            if (has2) stage4<Cfg::nt>(col, val, k2, d4, w01, w23);
+            if (VI) {
+               stage4_vi<Cfg::nt>(col, vidx, vtab, k, c4, v01, v23);
+               if (has2) stage4_vi<Cfg::nt>(col, vidx, vtab, k2, d4, w01, w23);
+            } else {
+               stage4<Cfg::nt>(col, val, k, c4, v01, v23);
+               if (has2) stage4<Cfg::nt>(col, val, k2, d4, w01, w23);
+            }
             const double x0 = x[c4.x], x1 = x[c4.y], x2 = x[c4.z], x3 = x[c4.w];
             double y0 = 0, y1 = 0, y2 = 0, y3 = 0;
             if (has2) {
@@ -160,7 +221,10 @@ __global__ __launch_bounds__(256) void csr_tile_kernel(
          for (int k = cs + 4 * (int)threadIdx.x; k < ce; k += 4 * 256) {
             v4i c4;
             v2d v01, v23;
-            stage4<Cfg::nt>(col, val, k, c4, v01, v23);
+            if (VI)
+               stage4_vi<Cfg::nt>(col, vidx, vtab, k, c4, v01, v23);
+            else
+               stage4<Cfg::nt>(col, val, k, c4, v01, v23);
             const double x0 = x[c4.x];
             const double x1 = x[c4.y];
             const double x2 = x[c4.z];
@@ -203,8 +267,56 @@ __global__ __launch_bounds__(256) void csr_tile_kernel(
    }
 }
 
+template <class Cfg, int NEG, bool NEED_DIAG, class Epi, bool VI = false, bool GTAB = false>
+__global__ __launch_bounds__(256) void csr_tile_kernel(
+   const int *__restrict__ rowptr, const int *__restrict__ col, const double *__restrict__ val,
+   const double *__restrict__ x, int rb, int re, Epi epi, double *__restrict__ partials,
+   const unsigned char *__restrict__ vidx = nullptr, const double *__restrict__ vtab_g = nullptr)
+{
+   __shared__ __attribute__((aligned(16))) double prod[Cfg::ch];
+   __shared__ double red[4];
+   __shared__ double vtab[(VI && !GTAB) ? 256 : 1];
+   int tile = blockIdx.x;
+   if (Cfg::xcd) {
+      // bijective remap: the blocks dealt to one XCD (b % 8) get a contiguous tile range
+      const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xg = tile & 7, idx = tile >> 3;
+      tile = (xg < r ? xg * (q + 1) : r * (q + 1) + (xg - r) * q) + idx;
+   }
+
+   tile_body<Cfg, NEG, NEED_DIAG, Epi, VI, VI && !GTAB>(tile, rowptr, col, val, x, rb, re, epi,
+                                                        partials, vidx,
+                                                        GTAB ? const_cast<double *>(vtab_g) : vtab,
+                                                        prod, red, vtab_g);
+}
+
+// persistent form: gridDim.x workgroups walk the tiles t, t + gridDim.x, ...
+template <class Cfg, int NEG, bool NEED_DIAG, class Epi, bool VI = false>
+__global__ __launch_bounds__(256) void csr_ptile_kernel(
+   const int *__restrict__ rowptr, const int *__restrict__ col, const double *__restrict__ val,
+   const double *__restrict__ x, int rb, int re, Epi epi, double *__restrict__ partials,
+   const unsigned char *__restrict__ vidx, const double *__restrict__ vtab_g, int ntiles)
+{
+   __shared__ __attribute__((aligned(16))) double prod[Cfg::ch];
+   __shared__ double red[4];
+   __shared__ double vtab[VI ? 256 : 1];
+   if (VI) {
+      vtab[threadIdx.x] = vtab_g[threadIdx.x];
+      __syncthreads();
+   }
+   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+      tile_body<Cfg, NEG, NEED_DIAG, Epi, VI>(tile, rowptr, col, val, x, rb, re, epi, partials, vidx,
+                                              vtab, prod, red);
+      __syncthreads();
+   }
+}
+
 // production configuration (tools/tune_spmv.py picks it on the MI355X)
 using ProdCfg = TileCfg<1, 2048, false, false>;
+// value-indexed matrices with short rows (< 12 entries on average: 7-pt
+// stencil, prolongation) stage 8 consecutive entries per lane with all loads
+// issued up front (-3..6 % there; +2..5 % on 27-entry rows, which keep ProdCfg)
+using ShortCfg = TileCfg<1, 2048, false, false, false, false, false, false, true>;
+static inline bool short_rows(const amg_mat *A) { return A->nnz < 12LL * A->nrows; }
 
 // Epilogue interface: init(i) -> accumulator start value; pf(i) -> one
 // operand prefetched before the stream; finish(i, acc, a_ii, pf) writes the
@@ -325,7 +437,26 @@ void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, c
    if (re <= rb) return;
    EpiGemv e{b, y, g.init, g.scale, g.alpha, g.temp};
    const int nb = tile_blocks(rb, re);
-   if (g.negacc)
+   if (A->vidx && !partials && !g.negacc && A->nnz < 5LL * A->nrows && nb > 4096) {
+      // short rows (prolongation): tiles carry little work, so 4096 persistent
+      // workgroups walking the tiles beat one workgroup per tile
+      csr_ptile_kernel<ShortCfg, 0, false, EpiGemv, true><<<4096, 256, 0, s>>>(
+         A->rowptr, A->col, A->val, x, rb, re, e, nullptr, A->vidx, A->vtab, nb);
+   } else if (A->vidx && short_rows(A)) {
+      if (g.negacc)
+         csr_tile_kernel<ShortCfg, 1, false, EpiGemv, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, partials, A->vidx, A->vtab);
+      else
+         csr_tile_kernel<ShortCfg, 0, false, EpiGemv, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, partials, A->vidx, A->vtab);
+   } else if (A->vidx) {
+      if (g.negacc)
+         csr_tile_kernel<ProdCfg, 1, false, EpiGemv, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, partials, A->vidx, A->vtab);
+      else
+         csr_tile_kernel<ProdCfg, 0, false, EpiGemv, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, partials, A->vidx, A->vtab);
+   } else if (g.negacc)
       csr_tile_kernel<ProdCfg, 1, false, EpiGemv>
          <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, partials);
    else
@@ -340,12 +471,23 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
    const int nb = tile_blocks(rb, re);
    if (l1) {
       EpiL1Jacobi e{f, x, l1, out};
-      csr_tile_kernel<ProdCfg, 1, false, EpiL1Jacobi>
-         <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, nullptr);
+      if (A->vidx)
+         csr_tile_kernel<ProdCfg, 1, false, EpiL1Jacobi, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, nullptr, A->vidx, A->vtab);
+      else
+         csr_tile_kernel<ProdCfg, 1, false, EpiL1Jacobi>
+            <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, nullptr);
    } else {
       EpiJacobi e{f, x, out, omega};
-      csr_tile_kernel<ProdCfg, 1, true, EpiJacobi>
-         <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, nullptr);
+      if (A->vidx && short_rows(A))
+         csr_tile_kernel<ShortCfg, 1, true, EpiJacobi, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, nullptr, A->vidx, A->vtab);
+      else if (A->vidx)
+         csr_tile_kernel<ProdCfg, 1, true, EpiJacobi, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, nullptr, A->vidx, A->vtab);
+      else
+         csr_tile_kernel<ProdCfg, 1, true, EpiJacobi>
+            <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, nullptr);
    }
 }
 
@@ -356,7 +498,21 @@ void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const dou
    if (re <= rb) return;
    const int nb = tile_blocks(rb, re);
    EpiResJacobi e{f, x, l1, r, unext, omega};
-   if (l1)
+   if (A->vidx && short_rows(A)) {
+      if (l1)
+         csr_tile_kernel<ShortCfg, 1, false, EpiResJacobi, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, partials, A->vidx, A->vtab);
+      else
+         csr_tile_kernel<ShortCfg, 1, true, EpiResJacobi, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, partials, A->vidx, A->vtab);
+   } else if (A->vidx) {
+      if (l1)
+         csr_tile_kernel<ProdCfg, 1, false, EpiResJacobi, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, partials, A->vidx, A->vtab);
+      else
+         csr_tile_kernel<ProdCfg, 1, true, EpiResJacobi, true><<<nb, 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, rb, re, e, partials, A->vidx, A->vtab);
+   } else if (l1)
       csr_tile_kernel<ProdCfg, 1, false, EpiResJacobi>
          <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, partials);
    else
@@ -368,13 +524,17 @@ void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const dou
 // tuning harness: time y = A x under several tile configurations, interleaved
 // (development entry point used by tools/tune_spmv.py; not part of the C-ABI)
 // ---------------------------------------------------------------------------
-template <class Cfg>
+template <class Cfg, bool VI = false>
 static void launch_matvec_cfg(hipStream_t s, const amg_mat *A, const double *x, double *y)
 {
    EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
-   csr_tile_kernel<Cfg, 0, false, EpiGemv>
-      <<<cfg_blocks<Cfg>(0, A->nrows), 256, 0, s>>>(A->rowptr, A->col, A->val, x, 0, A->nrows, e,
-                                                   nullptr);
+   if (VI && A->vidx)
+      csr_tile_kernel<Cfg, 0, false, EpiGemv, true><<<cfg_blocks<Cfg>(0, A->nrows), 256, 0, s>>>(
+         A->rowptr, A->col, A->val, x, 0, A->nrows, e, nullptr, A->vidx, A->vtab);
+   else
+      csr_tile_kernel<Cfg, 0, false, EpiGemv>
+         <<<cfg_blocks<Cfg>(0, A->nrows), 256, 0, s>>>(A->rowptr, A->col, A->val, x, 0, A->nrows,
+                                                      e, nullptr);
 }
 
 // ablations (wrong results, timing only): 1 = x gathered from a 64 KiB window
@@ -436,40 +596,112 @@ __global__ __launch_bounds__(256) void ablation_kernel(const int *__restrict__ r
    if (row < r1) y[row] = acc;
 }
 
-int num_tune_variants() { return 11; }
+int num_tune_variants() { return 19; }
+
+
 
 const char *tune_variant_name(int v)
 {
-   static const char *names[] = {"base",          "unroll2",          "unroll2_skipsync",
-                                 "unr_skip_shfl", "skipsync",         "unr_skip_shfl_xcd",
-                                 "rpt2_ch4096",   "unr_skip_shfl_ch4096",
-                                 "ABL_localgather", "ABL_noLDS",      "ABL_streamonly"};
-   return (v >= 0 && v < 11) ? names[v] : "?";
+   static const char *names[] = {"plain_base",   "vi_base",         "vi_strided",
+                                 "vi_unr_skip_shfl", "vi_rpt2_ch4096", "vi_xcd",
+                                 "vi_nt",        "vi_ch1024",       "plain_strided",
+                                 "ABL_localgather", "ABL_noLDS",    "ABL_streamonly",
+                                 "vi_gtab",      "vi_persist2048",  "vi_persist4096",
+                                 "vi_w8",        "plain_w8",        "vi_w8_nt",     "vi_w8_ch4096"};
+   return (v >= 0 && v < 19) ? names[v] : "?";
 }
 
 void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y)
 {
    switch (v) {
    case 0: launch_matvec_cfg<TileCfg<1, 2048, false, false>>(s, A, x, y); break;
-   case 1: launch_matvec_cfg<TileCfg<1, 2048, false, false, true>>(s, A, x, y); break;
-   case 2: launch_matvec_cfg<TileCfg<1, 2048, false, false, true, true>>(s, A, x, y); break;
-   case 3: launch_matvec_cfg<TileCfg<1, 2048, false, false, true, true, true>>(s, A, x, y); break;
-   case 4: launch_matvec_cfg<TileCfg<1, 2048, false, false, false, true>>(s, A, x, y); break;
-   case 5: launch_matvec_cfg<TileCfg<1, 2048, false, true, true, true, true>>(s, A, x, y); break;
-   case 6: launch_matvec_cfg<TileCfg<2, 4096, false, false>>(s, A, x, y); break;
-   case 7: launch_matvec_cfg<TileCfg<1, 4096, false, false, true, true, true>>(s, A, x, y); break;
-   case 8:
+   case 1: launch_matvec_cfg<TileCfg<1, 2048, false, false>, true>(s, A, x, y); break;
+   case 2: launch_matvec_cfg<TileCfg<1, 2048, false, false, false, false, false, true>, true>(s, A, x, y); break;
+   case 3: launch_matvec_cfg<TileCfg<1, 2048, false, false, true, true, true>, true>(s, A, x, y); break;
+   case 4: launch_matvec_cfg<TileCfg<2, 4096, false, false>, true>(s, A, x, y); break;
+   case 5: launch_matvec_cfg<TileCfg<1, 2048, false, true>, true>(s, A, x, y); break;
+   case 6: launch_matvec_cfg<TileCfg<1, 2048, true, false>, true>(s, A, x, y); break;
+   case 7: launch_matvec_cfg<TileCfg<1, 1024, false, false>, true>(s, A, x, y); break;
+   case 8: launch_matvec_cfg<TileCfg<1, 2048, false, false, false, false, false, true>>(s, A, x, y); break;
+   case 9:
       ablation_kernel<1><<<(A->nrows + 255) / 256, 256, 0, s>>>(A->rowptr, A->col, A->val, x,
                                                                A->nrows, y);
       break;
-   case 9:
+   case 10:
       ablation_kernel<2><<<(A->nrows + 255) / 256, 256, 0, s>>>(A->rowptr, A->col, A->val, x,
                                                                A->nrows, y);
       break;
-   case 10:
+   case 11:
       ablation_kernel<3><<<(A->nrows + 255) / 256, 256, 0, s>>>(A->rowptr, A->col, A->val, x,
                                                                 A->nrows, y);
       break;
+   case 12: {
+      EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
+      if (A->vidx)
+         csr_tile_kernel<ProdCfg, 0, false, EpiGemv, true, true><<<cfg_blocks<ProdCfg>(0, A->nrows), 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, 0, A->nrows, e, nullptr, A->vidx, A->vtab);
+      break;
+   }
+   case 13:
+   case 14: {
+      EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
+      const int nt = cfg_blocks<ProdCfg>(0, A->nrows);
+      if (A->vidx)
+         csr_ptile_kernel<ProdCfg, 0, false, EpiGemv, true><<<std::min(nt, v == 13 ? 2048 : 4096), 256, 0, s>>>(
+            A->rowptr, A->col, A->val, x, 0, A->nrows, e, nullptr, A->vidx, A->vtab, nt);
+      break;
+   }
+   case 15: launch_matvec_cfg<TileCfg<1, 2048, false, false, false, false, false, false, true>, true>(s, A, x, y); break;
+   case 16: launch_matvec_cfg<TileCfg<1, 2048, false, false, false, false, false, false, true>>(s, A, x, y); break;
+   case 17: launch_matvec_cfg<TileCfg<1, 2048, true, false, false, false, false, false, true>, true>(s, A, x, y); break;
+   case 18: launch_matvec_cfg<TileCfg<1, 4096, false, false, false, false, false, false, true>, true>(s, A, x, y); break;
+   default: break;
+   }
+}
+
+// ---------------------------------------------------------------------------
+// PMC calibration streams (tools/pmc_traffic.py): known byte counts read or
+// written with one access width per lane, to calibrate rocprofv3 FETCH_SIZE /
+// WRITE_SIZE per access width on gfx950 (MI355X_MICROARCH.md, HBM section)
+// ---------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(256) void calib_read_k(const unsigned char *__restrict__ buf,
+                                                   long long bytes, double *__restrict__ out)
+{
+   const long long n = bytes / W;
+   const long long stride = (long long)gridDim.x * blockDim.x;
+   double acc = 0.0;
+   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
+      if (W == 16) {
+         const v2d v = reinterpret_cast<const v2d *>(buf)[i];
+         acc += v.x + v.y;
+      } else if (W == 8) {
+         acc += reinterpret_cast<const double *>(buf)[i];
+      } else if (W == 4) {
+         acc += (double)reinterpret_cast<const int *>(buf)[i];
+      } else {
+         acc += (double)buf[i];
+      }
+   }
+   if (acc == 12345.678) out[0] = acc; // keep the loads
+}
+
+__global__ __launch_bounds__(256) void calib_write8_k(double *__restrict__ buf, long long n)
+{
+   const long long stride = (long long)gridDim.x * blockDim.x;
+   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
+      buf[i] = (double)i;
+}
+
+void calib_stream(hipStream_t s, int mode, void *buf, long long bytes, double *out)
+{
+   const int nb = 8192;
+   switch (mode) {
+   case 0: calib_read_k<16><<<nb, 256, 0, s>>>((const unsigned char *)buf, bytes, out); break;
+   case 1: calib_read_k<8><<<nb, 256, 0, s>>>((const unsigned char *)buf, bytes, out); break;
+   case 2: calib_read_k<4><<<nb, 256, 0, s>>>((const unsigned char *)buf, bytes, out); break;
+   case 3: calib_read_k<1><<<nb, 256, 0, s>>>((const unsigned char *)buf, bytes, out); break;
+   case 4: calib_write8_k<<<nb, 256, 0, s>>>((double *)buf, bytes / 8); break;
    default: break;
    }
 }
@@ -894,6 +1126,90 @@ void reduce_partials(hipStream_t s, const double *partials, int np, double *out,
       sum_partials_k<<<1, 256, 0, s>>>(partials, np, out);
    }
    if (do_sqrt) finish_k<<<1, 1, 0, s>>>(out, do_sqrt);
+}
+
+// ---------------------------------------------------------------------------
+// value-indexed CSR construction: the distinct values of val (by bit pattern)
+// collected into a device hash set, then every entry encoded as a one-byte
+// index into the sorted table of at most 256 values
+// ---------------------------------------------------------------------------
+constexpr unsigned long long VI_EMPTY = ~0ULL;
+
+__device__ __forceinline__ unsigned int vi_hash(unsigned long long k)
+{
+   k ^= k >> 33;
+   k *= 0xff51afd7ed558ccdULL;
+   k ^= k >> 33;
+   return (unsigned int)k;
+}
+
+__global__ void vi_collect_k(const double *__restrict__ val, long long nnz,
+                             unsigned long long *slots, int nslots, int *count)
+{
+   unsigned long long last0 = VI_EMPTY, last1 = VI_EMPTY;
+   const long long stride = (long long)gridDim.x * blockDim.x;
+   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nnz; i += stride) {
+      const unsigned long long key = (unsigned long long)__double_as_longlong(val[i]);
+      if (key == last0 || key == last1) continue;
+      last1 = last0;
+      last0 = key;
+      if (key == VI_EMPTY) {
+         atomicAdd(count, 1 << 20); // the sentinel pattern itself: give up on the table
+         continue;
+      }
+      unsigned int h = vi_hash(key) & (nslots - 1);
+      for (int probe = 0; probe < nslots; probe++) {
+         const unsigned long long cur = __atomic_load_n(&slots[h], __ATOMIC_RELAXED);
+         if (cur == key) break;
+         if (cur == VI_EMPTY) {
+            const unsigned long long prev = atomicCAS(&slots[h], VI_EMPTY, key);
+            if (prev == VI_EMPTY) {
+               atomicAdd(count, 1);
+               break;
+            }
+            if (prev == key) break;
+         }
+         h = (h + 1) & (nslots - 1);
+      }
+   }
+}
+
+__global__ void vi_encode_k(const double *__restrict__ val, long long nnz,
+                            const unsigned long long *__restrict__ keys, int T,
+                            unsigned char *__restrict__ vidx)
+{
+   __shared__ unsigned long long tk[256];
+   if (threadIdx.x < 256) tk[threadIdx.x] = threadIdx.x < T ? keys[threadIdx.x] : VI_EMPTY;
+   __syncthreads();
+   const long long stride = (long long)gridDim.x * blockDim.x;
+   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nnz; i += stride) {
+      const unsigned long long key = (unsigned long long)__double_as_longlong(val[i]);
+      int lo = 0, hi = T - 1;
+      while (lo < hi) {
+         const int mid = (lo + hi) >> 1;
+         if (tk[mid] < key)
+            lo = mid + 1;
+         else
+            hi = mid;
+      }
+      vidx[i] = (unsigned char)lo;
+   }
+}
+
+void vi_collect(hipStream_t s, const double *val, long long nnz, unsigned long long *slots, int nslots,
+                int *count)
+{
+   if (nnz <= 0) return;
+   const long long nb = std::min<long long>(8192, (nnz + 255) / 256);
+   vi_collect_k<<<(int)nb, 256, 0, s>>>(val, nnz, slots, nslots, count);
+}
+
+void vi_encode(hipStream_t s, const double *val, long long nnz, const unsigned long long *keys, int T,
+               unsigned char *vidx)
+{
+   if (nnz <= 0) return;
+   const long long nb = std::min<long long>(8192, (nnz + 255) / 256);
+   vi_encode_k<<<(int)nb, 256, 0, s>>>(val, nnz, keys, T, vidx);
 }
 
 } // namespace amgk

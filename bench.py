@@ -44,13 +44,14 @@ def parse():
     return p.parse_args()
 
 
-def load_traffic(n):
-    """HBM bytes per launch of the fine residual kernel measured with rocprofv3
-    --pmc (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), if profiled for n."""
+def load_traffic(n, fmt):
+    """HBM bytes per launch of the fine residual kernel from the rocprofv3 --pmc
+    passes (FETCH_SIZE and WRITE_SIZE, corrected per access width by calibration
+    streams: tools/pmc_traffic.py -> profiles/traffic.json), if profiled for n."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         d = json.load(open(path))
-        return d.get(str(n), {}).get("fine_residual_bytes_per_launch")
+        return d[str(n)]["csr-vi" if fmt.startswith("csr-vi") else "csr"]["fine_residual_bytes_per_launch"]
     except Exception:
         return None
 
@@ -125,19 +126,25 @@ def main():
 
     n0 = As[0].nrows
     z0 = As[0].nnz
-    # dominant kernel: fine-grid residual SpGEMV r = f - A u (12 z + 28 n + 4 algorithmic bytes)
-    res_bytes = 12 * z0 + 28 * n0 + 4
+    # bytes per stored entry of the format the kernels stream: 4 (col) + 8 (val)
+    # for CSR, 4 (col) + 1 (value index) for value-indexed CSR
+    vi = As[0].value_index
+    bpe = 5 if vi else 12
+    fmt = f"csr-vi ({vi}-entry value table)" if vi else "csr"
+    # dominant kernel: fine-grid residual SpGEMV r = f - A u (bpe z + 28 n + 4 algorithmic bytes)
+    res_bytes = bpe * z0 + 28 * n0 + 4
     res_ms = ms[0] / max(launches[0], 1)
     achieved = res_bytes / (res_ms * 1e-3) / 1e9
-    # fine-grid SpMV y = A x (12 z + 20 n + 4 bytes), events on the same stream
+    # fine-grid SpMV y = A x (bpe z + 20 n + 4 bytes), events on the same stream
     x = ctx.vec(n0)
     x.set(1.0)
     y = ctx.vec(n0)
     import ctypes as C
     spmv_ms = C.c_double()
     amg.check(amg.lib.amg_matvec_timed(ctx.h, As[0].h, x.h, y.h, args.spmv_reps, C.byref(spmv_ms)))
-    spmv_bytes = 12 * z0 + 20 * n0 + 4
+    spmv_bytes = bpe * z0 + 20 * n0 + 4
     spmv_gbs = spmv_bytes / (spmv_ms.value * 1e-3) / 1e9
+    csr_bytes = 12 * z0 + 20 * n0 + 4  # the reference's CSR format
     log(f"[gpu] fine residual {res_ms:.3f} ms ({achieved:.0f} GB/s), fine SpMV {spmv_ms.value:.3f} ms "
         f"({spmv_gbs:.0f} GB/s); smoother {ms[1] / max(launches[1], 1):.3f} ms, "
         f"R0 {ms[2] / max(launches[2], 1):.3f} ms, P0 {ms[3] / max(launches[3], 1):.3f} ms")
@@ -172,12 +179,13 @@ def main():
                                f"{L}-level geometric Galerkin hierarchy, outer residual + norm per step",
                    "n": n, "levels": L, "nnz_A0": z0, "rows": n0,
                    "reuse_outer_residual": args.reuse_outer_residual,
-                   "parallelism": "single GPU"},
+                   "matrix_format": fmt, "parallelism": "single GPU"},
         "fine_spmv": {"gbs": spmv_gbs, "ms": spmv_ms.value, "bytes": spmv_bytes,
-                      "frac": spmv_gbs / HBM_PEAK_GBS},
-        "roofline": {"bound": "hbm", "kernel": "fine-grid residual SpGEMV r = f - A0 u",
+                      "frac": spmv_gbs / HBM_PEAK_GBS, "format": fmt,
+                      "csr_equivalent_gbs": csr_bytes / (spmv_ms.value * 1e-3) / 1e9},
+        "roofline": {"bound": "hbm", "kernel": f"fine-grid residual SpGEMV r = f - A0 u ({fmt})",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(n),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(n, fmt),
                      "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms},
         "cpu_baseline": cpu,
         "final_relres": rn / r0,

@@ -96,6 +96,13 @@ int amg_version(void);
 int amg_csr_register(amg_ctx *ctx, int nrows, int ncols, long long nnz, const int *rowptr,
                      const int *col, const double *val, int diag_first, amg_mat **out);
 int amg_mat_free(amg_mat *A);
+/* storage of matrices registered from now on: 1 (default; env AMG_VALUE_INDEX=0
+ * turns it off) = value-indexed CSR when the matrix has at most 256 distinct
+ * values -- the hot kernels stream a one-byte index per entry instead of the
+ * 8-byte value and read the value from a table (bit-identical results) */
+int amg_set_value_index(amg_ctx *ctx, int enable);
+/* number of table entries of A's value index (0: plain CSR) */
+int amg_mat_value_index(const amg_mat *A);
 int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz);
 int amg_mat_download(amg_ctx *ctx, const amg_mat *A, int *rowptr, int *col, double *val);
 

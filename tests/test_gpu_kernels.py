@@ -57,6 +57,19 @@ def matrices(oracle, amg):
     cv = g2.uniform(-1, 1, size=cj.size)
     cv[rp[:-1]] = 50.0
     out["longrows"] = oracle.Csr(n, n, rp, cj, cv)
+    # value-indexed CSR: the same structures with values drawn from a small set
+    # (256 distinct values: the largest table; 257: falls back to plain CSR)
+    for name, src, nv in (("rand_q", "rand_sq", 256), ("longrows_q", "longrows", 37),
+                          ("rand_q257", "rand_nz", 257)):
+        A = out[src]
+        levels = np.linspace(-1.0, 1.0, nv) * (1.0 + 1.0 / 3.0)
+        q = levels[rng(nv).integers(0, nv, size=A.val.size)]
+        d = A.rowptr[:-1][np.diff(A.rowptr) > 0]
+        q[d] = levels[-1]  # diagonal entries: the largest level
+        off = np.ones(q.size, bool)
+        off[d] = False
+        q[np.nonzero(off)[0][:nv]] = levels  # every level present
+        out[name] = oracle.Csr(A.nrows, A.ncols, A.rowptr, A.col, q)
     return out
 
 
@@ -67,13 +80,45 @@ def mats(oracle, amg, ctx):
     return host, dev
 
 
-SQUARE = ["lap16", "A1", "A2", "rand_sq", "longrows"]
+SQUARE = ["lap16", "A1", "A2", "rand_sq", "longrows", "rand_q", "longrows_q", "rand_q257"]
 ALL = SQUARE + ["lap_rect", "P0", "P1", "R0", "R1", "rand_rect"]
 
 
 def _vecs(n, seed):
     g = rng(seed)
     return g.uniform(-1, 1, n)
+
+
+def test_value_index_selection(mats):
+    """Which registered matrices use the value-indexed form (table size) and
+    which stay plain CSR (0): decided by the number of distinct values."""
+    host, dev = mats
+    for name in ALL:
+        nd = np.unique(host[name].val.view(np.int64)).size
+        want = nd if nd <= 256 else 0
+        assert dev[name].value_index == want, (name, nd, dev[name].value_index)
+    assert dev["lap16"].value_index == 2
+    assert dev["rand_q"].value_index == 256 and dev["rand_q257"].value_index == 0
+
+
+@pytest.mark.parametrize("name", ["lap16", "rand_q", "longrows_q", "P0"])
+def test_value_index_matches_plain(mats, ctx, amg, name):
+    """The same matrix registered with and without the value index gives
+    bit-identical SpGEMV, Jacobi and fused residual+Jacobi results."""
+    host, dev = mats
+    A = host[name]
+    ctx.set_value_index(0)
+    plain = ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val)
+    ctx.set_value_index(1)
+    assert plain.value_index == 0 and dev[name].value_index > 0
+    x = ctx.vec(_vecs(A.ncols, 5))
+    b = ctx.vec(_vecs(A.nrows, 6))
+    for M in (plain, dev[name]):
+        y = ctx.vec(A.nrows)
+        amg.smem.SMEM_SpGEMV(ctx, M, x, b, -1.0, 1.0, y, 0, A.nrows)
+        M._y = y.download()
+    assert_bitwise(dev[name]._y, plain._y, name)
+    plain.free()
 
 
 @pytest.mark.parametrize("name", ALL)

@@ -1,0 +1,36 @@
+"""Workload for the rocprofv3 --pmc passes (tools/gpu_pmc.sh): PMC calibration
+streams of known size per access width, then 512^3 V-cycles (value-indexed
+CSR) and plain-CSR fine residuals.  tools/pmc_traffic.py reads the counters."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from conftest import load_package  # noqa: E402
+
+amg = load_package()
+lib = amg.lib
+lib.amg_dev_calib.argtypes = [C.c_void_p, C.c_int, C.c_longlong]
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+ctx = amg.Context(0, 4)
+CAL = 2 << 30  # 2 GiB per calibration stream, far beyond the 256 MiB Infinity Cache
+for mode in range(5):
+    amg.check(lib.amg_dev_calib(ctx.h, mode, CAL))
+g = amg.Gen(n)
+H = amg.build_hierarchy(ctx, g, amg.default_opts(smooth_weight=0.8, num_cycles=1 << 30, tol=0.0))
+f = ctx.vec(amg.rhs_rand(0, n ** 3))
+H.solve_start(f, ctx.vec(n ** 3))
+H.iterate(3)
+ctx.sync()
+H.free()
+ctx.set_value_index(0)
+A0 = g.register(ctx, amg.AMG_GEN_A, 0)
+x = ctx.vec(np.random.default_rng(0).uniform(-1, 1, A0.ncols))
+y = ctx.vec(A0.nrows)
+for _ in range(3):
+    amg.smem.SMEM_Sync_SpGEMV(ctx, A0, x, f, -1.0, 1.0, y)
+ctx.sync()
+print(f"pmc workload done: n={n} nnz={A0.nnz}")

@@ -39,8 +39,9 @@ for name, A in mats.items():
                 ref = out
             elif not np.array_equal(out.view(np.uint64), ref.view(np.uint64)):
                 print(f"{name} variant {v}: RESULT MISMATCH")
-    nbytes = 12 * A.nnz + 4 * (A.nrows + 1) + 8 * A.ncols + 8 * A.nrows
     for v in vlist:
+        vi = lib.amg_dev_tune_name(v).startswith(b"vi") and A.value_index > 0
+        nbytes = (5 if vi else 12) * A.nnz + 4 * (A.nrows + 1) + 8 * A.ncols + 8 * A.nrows
         t = np.median(res[v])
         print(f"{name:3s} {lib.amg_dev_tune_name(v).decode():22s} median {t:.3f} ms  min {min(res[v]):.3f}"
               f"  {nbytes / t / 1e6:.0f} GB/s")
