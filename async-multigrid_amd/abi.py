@@ -23,6 +23,7 @@ _pp = C.POINTER(C.c_void_p)
 
 AMG_OK = 0
 AMG_JACOBI, AMG_GAUSS_SEIDEL, AMG_HYBRID_JGS, AMG_SYMM_JACOBI = 0, 1, 2, 3
+AMG_SEMI_ASYNC_GS, AMG_ASYNC_GS = 4, 5
 AMG_L1_JACOBI, AMG_L1_HYBRID_JGS = 6, 12
 AMG_MULT, AMG_AFACX, AMG_MULTADD, AMG_ASYNC_AFACX, AMG_ASYNC_MULTADD = 0, 1, 2, 5, 6
 AMG_FULL_ASYNC, AMG_SEMI_ASYNC = 0, 1
@@ -76,6 +77,7 @@ PROTOTYPES = {
     "amg_l1_jacobi": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i]),
     "amg_hybrid_jgs": (_i, [_p, _p, _p, _p, _p, _ip, _i, _p, _d, _i, _i, _i]),
     "amg_gauss_seidel": (_i, [_p, _p, _p, _p, _i]),
+    "amg_async_gauss_seidel": (_i, [_p, _p, _p, _p, _ip, _i, _i, _i, _i]),
     "amg_sym_jacobi": (_i, [_p, _p, _p, _p, _p, _p, _d, _p, _i, _i, _i, _i, _i]),
     "amg_l1_norms": (_i, [_p, _p, _p]),
     "amg_a_diag": (_i, [_p, _p, _d, _p]),

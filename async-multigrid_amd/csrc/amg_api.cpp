@@ -626,6 +626,25 @@ extern "C" int amg_gauss_seidel(amg_ctx *c, const amg_mat *A, const amg_vec *f, 
    return amg_hybrid_jgs(c, A, f, u, u, blk, 1, nullptr, 1.0, sweeps, 0, 0);
 }
 
+extern "C" int amg_async_gauss_seidel(amg_ctx *c, const amg_mat *A, const amg_vec *f, amg_vec *u,
+                                      const int *blk, int nblk, int sweeps, int semi, int reverse)
+{
+   AMG_ARG(c && A && f && u && blk && nblk > 0 && sweeps >= 0, "amg_async_gauss_seidel: bad argument");
+   AMG_ARG(f->n >= A->nrows && u->n >= A->nrows && A->nrows == A->ncols,
+           "amg_async_gauss_seidel: square matrix and vectors of its size");
+   for (int b = 0; b < nblk; b++)
+      AMG_ARG(blk[b] <= blk[b + 1] && blk[b] >= 0 && blk[b + 1] <= A->nrows,
+              "amg_async_gauss_seidel: bad block %d [%d,%d)", b, blk[b], blk[b + 1]);
+   int *d_blk = nullptr;
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   AMG_HIP(hipMalloc((void **)&d_blk, (nblk + 1) * sizeof(int)));
+   AMG_HIP(hipMemcpyAsync(d_blk, blk, (nblk + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream));
+   amgk::async_gs(c->stream, A, f->d, u->d, d_blk, nblk, sweeps, semi, reverse);
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   AMG_HIP(hipFree(d_blk));
+   return AMG_OK;
+}
+
 int amg_sym_jacobi_dev(hipStream_t s, const amg_mat *A, const double *f, double *u, double *y,
                        double *r, double omega, const double *l1, int sweeps, int zero_first,
                        int rb, int re, int variant)

@@ -135,6 +135,9 @@ void jacobi_from_residual(hipStream_t s, const double *diag, const double *r, co
 void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
                 const int *d_blk, int nblk, const double *diag_scale, double weight, int zero,
                 int reverse);
+// asynchronous / semi-asynchronous Gauss-Seidel, one lane per block, live u
+void async_gs(hipStream_t s, const amg_mat *A, const double *f, double *u, const int *d_blk, int nblk,
+              int sweeps, int semi, int reverse);
 // transpose-product with the expansion-buffer order of T static chunks
 void matvec_t_chunked(hipStream_t s, const amg_mat *AT, const double *x, double *y, int n_src,
                       int T);

@@ -812,6 +812,45 @@ __global__ void hybrid_jgs_k(const int *__restrict__ rowptr, const int *__restri
    }
 }
 
+// asynchronous Gauss-Seidel (SMEM_Async_Parfor_GaussSeidel[T] SMEM_Smooth.cpp:164-220,
+// SMEM_Async_GaussSeidel[T] :475-531; semi-async: one sweep per launch,
+// SMEM_SemiAsync_* :135-162 / :445-473): one lane per block of rows, rows in
+// order (reverse: backwards), every u access a relaxed agent-scope atomic,
+// other blocks' rows read live -- the reference's racy in-place update.
+// No zero-guess special case and no weight (u_i += res / a_ii), as the
+// reference.  Blocks never wait for one another within a launch.
+__global__ void async_gs_k(const int *__restrict__ rowptr, const int *__restrict__ col,
+                           const double *__restrict__ val, const double *__restrict__ f, double *u,
+                           const int *__restrict__ blk, int nblk, int sweeps, int reverse)
+{
+   auto ld = [u](int k) { return __hip_atomic_load(u + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+   const int b = blockIdx.x * blockDim.x + threadIdx.x;
+   if (b >= nblk) return;
+   const int ns = blk[b], ne = blk[b + 1];
+   for (int k = 0; k < sweeps; k++)
+      for (int c = 0; c < ne - ns; c++) {
+         const int i = reverse ? ne - 1 - c : ns + c;
+         const int rs = rowptr[i], rend = rowptr[i + 1];
+         const double a = val[rs];
+         if (a == 0.0) continue;
+         double res = f[i];
+         for (int jj = rs; jj < rend; jj++) res -= val[jj] * ld(col[jj]);
+         __hip_atomic_store(u + i, ld(i) + res / a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+}
+
+void async_gs(hipStream_t s, const amg_mat *A, const double *f, double *u, const int *d_blk, int nblk,
+              int sweeps, int semi, int reverse)
+{
+   if (nblk <= 0 || sweeps <= 0) return;
+   const int tpb = 64, nb = (nblk + tpb - 1) / tpb;
+   if (semi)
+      for (int k = 0; k < sweeps; k++)
+         async_gs_k<<<nb, tpb, 0, s>>>(A->rowptr, A->col, A->val, f, u, d_blk, nblk, 1, reverse);
+   else
+      async_gs_k<<<nb, tpb, 0, s>>>(A->rowptr, A->col, A->val, f, u, d_blk, nblk, sweeps, reverse);
+}
+
 void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
                 const int *d_blk, int nblk, const double *diag_scale, double weight, int zero,
                 int reverse)

@@ -343,6 +343,14 @@ static void smooth_one_level(amg_hier *H, hipStream_t s, int l, const double *f,
                          v.n, ds, 1.0, sweeps, zf, 0);
       return;
    }
+   if (o.smoother == AMG_ASYNC_GAUSS_SEIDEL || o.smoother == AMG_SEMI_ASYNC_GAUSS_SEIDEL) {
+      // SMEM_Async_Parfor_GaussSeidel / SMEM_SemiAsync_Parfor_GaussSeidel
+      // (SMEM_Solve.cpp:342-347): in place, no zero-guess special case
+      ProfScope ps(H, PROF_FINE_SMOOTH, s, prof);
+      amgk::async_gs(s, v.A, f, v.u, v.d_blk, (int)v.blk.size() - 1, sweeps,
+                     o.smoother == AMG_SEMI_ASYNC_GAUSS_SEIDEL, 0);
+      return;
+   }
    const bool l1 = (o.smoother == AMG_L1_JACOBI);
    for (int k = 0; k < sweeps; k++) {
       if (k == 0 && zf == 1) {
@@ -379,6 +387,10 @@ static void smooth_all_levels(amg_hier *H, hipStream_t s, int Alevel, const doub
    if (o.smoother == AMG_HYBRID_JACOBI_GAUSS_SEIDEL) {
       amg_hybrid_jgs_dev(H->ctx, s, v.A, f, u, u_prev, v.n, v.d_blk, (int)v.blk.size() - 1, 0, v.n,
                          nullptr, 1.0, sweeps, zf, 0);
+   } else if (o.smoother == AMG_ASYNC_GAUSS_SEIDEL || o.smoother == AMG_SEMI_ASYNC_GAUSS_SEIDEL) {
+      // SMEM_Async_GaussSeidel / SMEM_SemiAsync_GaussSeidel (SMEM_Solve.cpp:281-286)
+      amgk::async_gs(s, v.A, f, u, v.d_blk, (int)v.blk.size() - 1, sweeps,
+                     o.smoother == AMG_SEMI_ASYNC_GAUSS_SEIDEL, 0);
    } else if (o.smoother == AMG_L1_JACOBI) {
       if (sym) {
          amg_sym_jacobi_dev(s, v.A, f, u, y, r, 1.0, v.l1, sweeps, zf, 0, v.n, 0);

@@ -183,3 +183,12 @@ def DMEM_HypreParVector_Ivaxpy(ctx, y, x, s):
 def DMEM_HypreRealArray_Axpy(ctx, y, x, alpha):
     """DMEM_Misc.cpp:527-548: y += alpha x"""
     check(lib.amg_vec_axpy(ctx.h, alpha, x.h, y.h))
+
+
+def SMEM_Async_Parfor_GaussSeidel(ctx, A, f, u, num_sweeps, blk=None, semi=0, reverse=0):
+    """SMEM_Smooth.cpp:164-220 (semi=1: SMEM_SemiAsync_Parfor_GaussSeidel :135-162,
+    reverse=1: the T form :193-220); blk = the threads' row blocks (default one)."""
+    import numpy as np
+    blk = np.array([0, A.nrows] if blk is None else blk, dtype=np.int32)
+    check(lib.amg_async_gauss_seidel(ctx.h, A.h, f.h, u.h, _ip(blk), blk.size - 1, num_sweeps,
+                                     semi, reverse))

@@ -46,6 +46,8 @@ typedef struct amg_gen amg_gen;   /* structured 7-pt problem + geometric hierarc
 #define AMG_GAUSS_SEIDEL 1
 #define AMG_HYBRID_JACOBI_GAUSS_SEIDEL 2
 #define AMG_SYMM_JACOBI 3
+#define AMG_SEMI_ASYNC_GAUSS_SEIDEL 4
+#define AMG_ASYNC_GAUSS_SEIDEL 5
 #define AMG_L1_JACOBI 6
 #define AMG_L1_HYBRID_JACOBI_GAUSS_SEIDEL 12
 
@@ -153,6 +155,13 @@ int amg_hybrid_jgs(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u,
                    int zero_first, int reverse);
 /* forward Gauss-Seidel: SEQ_GaussSeidel SEQ_Smooth.cpp:89-117 */
 int amg_gauss_seidel(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, int sweeps);
+/* asynchronous Gauss-Seidel over row blocks blk[0..nblk]: SMEM_Async_Parfor_GaussSeidel[T]
+ * SMEM_Smooth.cpp:164-220 and SMEM_Async_GaussSeidel[T] :475-531 (semi = 0: no
+ * barrier between sweeps), SMEM_SemiAsync_Parfor_GaussSeidel :135-162 and
+ * SMEM_SemiAsync_GaussSeidel :445-473 (semi = 1).  In place, racy across blocks
+ * exactly like the reference; deterministic for nblk = 1.  reverse: the "T" forms. */
+int amg_async_gauss_seidel(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u,
+                           const int *blk, int nblk, int sweeps, int semi, int reverse);
 /* 2-step symmetric Jacobi: variant 0 = SMEM_Sync_Symmetric[L1]Jacobi
  * SMEM_Smooth.cpp:643-762, variant 1 = SEQ_Symmetric[L1]Jacobi SEQ_Smooth.cpp:119-189;
  * l1 != NULL selects the L1 form */

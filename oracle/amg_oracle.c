@@ -260,6 +260,26 @@ void or_seq_gauss_seidel(const or_csr *A, const double *f, double *u, int sweeps
          }
 }
 
+/* Asynchronous / semi-asynchronous Gauss-Seidel over blocks blk[0..nblk]
+ * (SMEM_Async_Parfor_GaussSeidel[T] SMEM_Smooth.cpp:164-220, SMEM_Async_GaussSeidel[T]
+ * :475-531, SMEM_SemiAsync_* :135-162 / :445-473): each thread sweeps its block
+ * in place reading the live u of every row.  The restatement runs the blocks
+ * one after another -- one admissible interleaving of the racy reference, and
+ * THE result for a single block.  No zero-guess case, no weight. */
+void or_async_gs(const or_csr *A, const double *f, double *u, const int *blk, int nblk, int sweeps,
+                 int reverse)
+{
+   for (int k = 0; k < sweeps; k++)
+      for (int b = 0; b < nblk; b++)
+         for (int c = 0; c < blk[b + 1] - blk[b]; c++) {
+            const int i = reverse ? blk[b + 1] - 1 - c : blk[b] + c;
+            if (A->data[A->i[i]] == 0.0) continue;
+            double res = f[i];
+            for (int jj = A->i[i]; jj < A->i[i + 1]; jj++) res -= A->data[jj] * u[A->j[jj]];
+            u[i] += res / A->data[A->i[i]];
+         }
+}
+
 /* Hybrid Jacobi/Gauss-Seidel over a block partition blk[0..nblk]:
  *   SMEM_Smooth.cpp:222-305 Parfor (diag_scale = A_diag = a_ii/omega, weight 1),
  *   SMEM_Smooth.cpp:533-586 row range (diag_scale = a_ii, weight 1),
@@ -737,6 +757,15 @@ static void smooth(or_hier *H, int Alevel, const double *f, double *u, double *y
    int zf = H->zero_flags[level];
    int multadd = (o->solver == OR_MULTADD || o->solver == OR_ASYNC_MULTADD);
    int sym = multadd && o->num_post > 0 && o->num_pre > 0;
+   if (o->smoother == OR_ASYNC_GAUSS_SEIDEL || o->smoother == OR_SEMI_ASYNC_GAUSS_SEIDEL) {
+      /* SMEM_Solve.cpp:281-286 / 342-347 */
+      int blk1[2] = {ns, ne};
+      const int *blk = H->blk[Alevel];
+      int nb = H->nblk[Alevel];
+      if (all_levels && (ns != 0 || ne != A->nrows)) { blk = blk1; nb = 1; }
+      or_async_gs(A, f, u, blk, nb, sweeps, 0);
+      return;
+   }
    if (all_levels) {
       if (o->smoother == OR_HYBRID_JACOBI_GAUSS_SEIDEL) {
          int blk1[2] = {ns, ne};

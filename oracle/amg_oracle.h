@@ -42,6 +42,8 @@ typedef struct {
 #define OR_JACOBI 0
 #define OR_GAUSS_SEIDEL 1
 #define OR_HYBRID_JACOBI_GAUSS_SEIDEL 2
+#define OR_SEMI_ASYNC_GAUSS_SEIDEL 4
+#define OR_ASYNC_GAUSS_SEIDEL 5
 #define OR_SYMM_JACOBI 3
 #define OR_L1_JACOBI 6
 #define OR_L1_HYBRID_JACOBI_GAUSS_SEIDEL 12
@@ -82,6 +84,8 @@ void or_seq_jacobi(const or_csr *A, const double *f, double *u, double *u_prev, 
 void or_seq_l1jacobi(const or_csr *A, const double *f, double *u, double *u_prev, const double *l1,
                      int sweeps, int zero_flag);
 void or_seq_gauss_seidel(const or_csr *A, const double *f, double *u, int sweeps);
+void or_async_gs(const or_csr *A, const double *f, double *u, const int *blk, int nblk, int sweeps,
+                 int reverse);
 void or_hybrid_jgs(const or_csr *A, const double *f, double *u, double *u_prev, const int *blk,
                    int nblk, const double *diag_scale, double weight, int sweeps, int zero_flag,
                    int reverse);

@@ -227,6 +227,14 @@ def seq_gauss_seidel(A, f, u, sweeps):
     lib().or_seq_gauss_seidel(C.byref(ac), dptr(f), dptr(u), C.c_int(sweeps))
 
 
+def async_gs(A, f, u, blk, sweeps, reverse=0):
+    """or_async_gs: blocks run one after another (the single-block result is exact)."""
+    ac = A.c()
+    blk = np.ascontiguousarray(blk, dtype=np.int32)
+    lib().or_async_gs(C.byref(ac), dptr(f), dptr(u), iptr(blk), C.c_int(len(blk) - 1),
+                      C.c_int(sweeps), C.c_int(reverse))
+
+
 def hybrid_jgs(A, f, u, u_prev, blk, diag_scale, weight, sweeps, zero_flag, reverse=0):
     ac = A.c()
     blk = np.ascontiguousarray(blk, dtype=np.int32)

@@ -271,6 +271,39 @@ def test_gauss_seidel(mats, ctx, oracle, amg):
     assert_bitwise(du.download(), ru)
 
 
+@pytest.mark.parametrize("name", ["lap16", "rand_sq", "A1"])
+@pytest.mark.parametrize("semi", [0, 1])
+@pytest.mark.parametrize("reverse", [0, 1])
+def test_async_gauss_seidel_single_block(mats, ctx, oracle, amg, name, semi, reverse):
+    """One block (one thread): the asynchronous Gauss-Seidel is deterministic."""
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    f, u = _vecs(A.nrows, 40), _vecs(A.nrows, 41)
+    ru = u.copy()
+    oracle.async_gs(A, f, ru, [0, A.nrows], 3, reverse)
+    du = ctx.vec(u)
+    amg.smem.SMEM_Async_Parfor_GaussSeidel(ctx, dA, ctx.vec(f), du, 3, None, semi, reverse)
+    assert_bitwise(du.download(), ru, name)
+
+
+@pytest.mark.parametrize("semi", [0, 1])
+def test_async_gauss_seidel_many_blocks(mats, ctx, oracle, amg, semi):
+    """Many blocks: racy across blocks like the reference; the sweeps still
+    reduce the residual about as much as the serialised restatement."""
+    host, dev = mats
+    A, dA = host["A1"], dev["A1"]
+    f = _vecs(A.nrows, 42)
+    blk = np.linspace(0, A.nrows, 65).astype(np.int32)
+    ru = np.zeros(A.nrows)
+    oracle.async_gs(A, f, ru, blk, 4, 0)
+    du = ctx.vec(np.zeros(A.nrows))
+    amg.smem.SMEM_Async_Parfor_GaussSeidel(ctx, dA, ctx.vec(f), du, 4, blk, semi, 0)
+    u = du.download()
+    res = lambda x: np.linalg.norm(f - oracle.smem_matvec(A, x, np.zeros(A.nrows)))
+    r0, rg, rc = np.linalg.norm(f), res(u), res(ru)
+    assert rg < 0.5 * r0 and rg < 2.0 * rc, (r0, rg, rc)
+
+
 @pytest.mark.parametrize("name", ["lap16", "A1", "rand_nz"])
 @pytest.mark.parametrize("sweeps", [1, 2])
 @pytest.mark.parametrize("zero", [0, 1])

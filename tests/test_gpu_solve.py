@@ -81,12 +81,15 @@ def test_known_answer_relres(amg, oracle, ctx):
     ("hybrid", {"num_threads": 4}),
     ("hybrid", {"num_threads": 0, "jgs_block_rows": 32}),
     ("l1hybrid", {"num_threads": 8}),
+    ("asyncgs", {"num_threads": 1}),
+    ("semiasyncgs", {"num_threads": 1}),
 ])
 def test_mult_vcycle_linear(amg, oracle, ctx, smoother, extra):
     _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
     assert L >= 4
     sm = {"jacobi": amg.AMG_JACOBI, "l1": amg.AMG_L1_JACOBI, "hybrid": amg.AMG_HYBRID_JGS,
-          "l1hybrid": amg.AMG_L1_HYBRID_JGS}[smoother]
+          "l1hybrid": amg.AMG_L1_HYBRID_JGS, "asyncgs": amg.AMG_ASYNC_GS,
+          "semiasyncgs": amg.AMG_SEMI_ASYNC_GS}[smoother]
     opts = amg.default_opts(smoother=sm, smooth_weight=0.8, num_cycles=12, tol=0.0, **extra)
     f = amg.rhs_rand(0, 24 ** 3)
     blocks = None
@@ -98,6 +101,24 @@ def test_mult_vcycle_linear(amg, oracle, ctx, smoother, extra):
             blocks[lev] = np.unique(np.minimum(np.arange(0, n + 32, 32), n)).astype(np.int32)
     u, hist = compare_solve(amg, oracle, ctx, host, opts, f, blocks)
     assert hist[-1] / hist[0] < 1e-3  # it converges
+
+
+@pytest.mark.parametrize("sm", ["asyncgs", "semiasyncgs"])
+def test_mult_vcycle_async_gs_band(amg, oracle, ctx, sm):
+    """Asynchronous Gauss-Seidel smoother with many thread blocks: racy, so
+    the V-cycle is checked for convergence against the single-block run."""
+    _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
+    code = amg.AMG_ASYNC_GS if sm == "asyncgs" else amg.AMG_SEMI_ASYNC_GS
+    f = amg.rhs_rand(0, 24 ** 3)
+    opts = amg.default_opts(smoother=code, num_cycles=12, tol=0.0, num_threads=32)
+    H, _ = gpu_hier(amg, ctx, host, opts)
+    u, h, k = H.solve(f)
+    H.free()
+    rel = h[-1] / h[0]
+    # the oracle runs the 32 blocks one after another: one admissible interleaving
+    _, h_c, _ = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts)).solve(f)
+    rel_c = h_c[-1] / h_c[0]
+    assert np.all(np.isfinite(u)) and rel < 1e-4 and rel_c / 100 <= rel <= rel_c * 1000, (rel, rel_c)
 
 
 def test_reuse_outer_residual_is_bit_identical(amg, oracle, ctx):
