@@ -26,6 +26,7 @@ AMG_JACOBI, AMG_GAUSS_SEIDEL, AMG_HYBRID_JGS, AMG_SYMM_JACOBI = 0, 1, 2, 3
 AMG_SEMI_ASYNC_GS, AMG_ASYNC_GS = 4, 5
 AMG_L1_JACOBI, AMG_L1_HYBRID_JGS = 6, 12
 AMG_MULT, AMG_AFACX, AMG_MULTADD, AMG_ASYNC_AFACX, AMG_ASYNC_MULTADD = 0, 1, 2, 5, 6
+AMG_BPX = 3
 AMG_FULL_ASYNC, AMG_SEMI_ASYNC = 0, 1
 AMG_VEC_F, AMG_VEC_U, AMG_VEC_R = 0, 1, 2
 AMG_INTERP_LINEAR, AMG_INTERP_AGGREGATE = 0, 1

@@ -55,6 +55,7 @@ struct amg_hier {
    std::vector<Level> lv;
    std::vector<AddLevel> al;
    double *r0 = nullptr; // vector.r[0]: the outer residual
+   double *e0 = nullptr, *e0_alt = nullptr; // BPX: vector.e[0] (+ ping-pong partner)
    double *u_outer = nullptr, *y_outer = nullptr;
    double *d_hist = nullptr; // device residual-norm history
    int hist_cap = 0;
@@ -82,9 +83,11 @@ static int dalloc(amg_hier *H, size_t n, double **p)
    return AMG_OK;
 }
 
+// SMEM_Main.cpp:641-649: MULT and BPX run ONE_LEVEL (every thread on every
+// level), the additive solvers ALL_LEVELS (thread groups per level)
 static bool is_all_levels(const amg_opts &o)
 {
-   return !(o.solver == AMG_MULT);
+   return !(o.solver == AMG_MULT || o.solver == AMG_BPX);
 }
 
 static bool is_multadd(const amg_opts &o)
@@ -247,6 +250,10 @@ extern "C" int amg_hier_create(amg_ctx *c, int L, amg_mat *const *A, amg_mat *co
       AMG_TRY(default_blocks(H, v));
    }
    AMG_TRY(dalloc(H, H->lv[0].n, &H->r0));
+   if (H->o.solver == AMG_BPX) {
+      AMG_TRY(dalloc(H, H->lv[0].n, &H->e0));
+      AMG_TRY(dalloc(H, H->lv[0].n, &H->e0_alt));
+   }
    AMG_TRY(dalloc(H, H->lv[0].n, &H->u_outer));
    AMG_TRY(dalloc(H, H->lv[0].n, &H->y_outer));
    H->hist_cap = 1 << 16;
@@ -459,6 +466,48 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
    }
 }
 
+// ---- SMEM_Sync_Parfor_BPXcycle (SMEM_Sync_AMG.cpp:147-294), solver BPX ----------
+// r[0] (the outer residual) restricted to every level; every level (the
+// coarsest too) smoothed from a zero guess with num_pre sweeps into its
+// correction e[l]; e_fine += P e_coarse upwards; u += e[0] (u = e[0] in
+// preconditioner mode).  e[l] = lv[l].u and r[l] = lv[l].f for l > 0 (the
+// cycle uses neither for anything else); e[0] has its own pair.
+static void bpx_cycle(amg_hier *H, bool precond)
+{
+   hipStream_t s = H->ctx->stream;
+   const amg_opts &o = H->o;
+   const int L = H->L;
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   const amgk::Gemv pro_mode = amgk::gemv_mode(1.0, 1.0);
+   for (int l = 0; l < L - 1; l++) {
+      ProfScope ps(H, PROF_RESTRICT0, s, l == 0);
+      amgk::spgemv(s, H->lv[l].R, l == 0 ? H->r0 : H->lv[l].f, nullptr, mv, H->lv[l + 1].f, 0,
+                   H->lv[l + 1].n, nullptr);
+   }
+   Level &v0 = H->lv[0];
+   for (int l = 0; l < L; l++) {
+      H->lv[l].zero_flag = 1;
+      if (l == 0) {
+         std::swap(v0.u, H->e0);
+         std::swap(v0.u_alt, H->e0_alt);
+      }
+      smooth_one_level(H, s, l, l == 0 ? H->r0 : H->lv[l].f, o.num_pre_smooth_sweeps, false);
+      if (l == 0) {
+         std::swap(v0.u, H->e0);
+         std::swap(v0.u_alt, H->e0_alt);
+      }
+   }
+   for (int l = L - 2; l >= 0; l--) {
+      double *ef = (l == 0) ? H->e0 : H->lv[l].u;
+      ProfScope ps(H, PROF_PROLONG0, s, l == 0);
+      amgk::spgemv(s, H->lv[l].P, H->lv[l + 1].u, ef, pro_mode, ef, 0, H->lv[l].n, nullptr);
+   }
+   if (precond)
+      amgk::vcopy(s, H->e0, v0.u, 0, v0.n);
+   else
+      amgk::vaxpy(s, 1.0, H->e0, v0.u, 0, v0.n);
+}
+
 // ---- SMEM_Sync_Add_Vcycle (SMEM_Sync_AMG.cpp:408-621), res_compute LOCAL ------
 // The level corrections are accumulated into u in level order.
 static void add_level_correction(amg_hier *H, hipStream_t s, int k, const double *r_fine0)
@@ -513,7 +562,7 @@ static void sync_add_vcycle(amg_hier *H)
 static bool reuse_applies(const amg_hier *H)
 {
    const amg_opts &o = H->o;
-   return !is_all_levels(o) && o.cheby_flag != 1 && o.reuse_outer_residual &&
+   return o.solver == AMG_MULT && o.cheby_flag != 1 && o.reuse_outer_residual &&
           (o.smoother == AMG_JACOBI || o.smoother == AMG_SYMM_JACOBI ||
            o.smoother == AMG_L1_JACOBI) &&
           o.num_pre_smooth_sweeps > 0 && H->L > 1;
@@ -568,6 +617,10 @@ static void init_vectors(amg_hier *H)
    }
    amgk::vset(s, H->u_outer, 0.0, 0, H->lv[0].n);
    amgk::vset(s, H->y_outer, 0.0, 0, H->lv[0].n);
+   if (H->e0) {
+      amgk::vset(s, H->e0, 0.0, 0, H->lv[0].n);
+      amgk::vset(s, H->e0_alt, 0.0, 0, H->lv[0].n);
+   }
 }
 
 static int solve_begin(amg_hier *H, const amg_vec *f, const amg_vec *u)
@@ -596,7 +649,9 @@ static int solve_step(amg_hier *H)
    const bool precond = o.cheby_flag == 1;
    const bool one_level = !is_all_levels(o);
    const bool reuse = reuse_applies(H);
-   if (one_level)
+   if (o.solver == AMG_BPX)
+      bpx_cycle(H, precond); // SMEM_Solve.cpp:161-163
+   else if (one_level)
       vcycle(H, precond, reuse);
    else
       sync_add_vcycle(H);
@@ -700,7 +755,10 @@ extern "C" int amg_vcycle(amg_hier *H)
    if (is_all_levels(H->o))
       sync_add_vcycle(H);
    else
-      vcycle(H, H->o.cheby_flag == 1, false);
+      if (H->o.solver == AMG_BPX)
+         bpx_cycle(H, H->o.cheby_flag == 1);
+      else
+         vcycle(H, H->o.cheby_flag == 1, false);
    AMG_HIP(hipGetLastError());
    return AMG_OK;
 }

@@ -54,6 +54,7 @@ typedef struct amg_gen amg_gen;   /* structured 7-pt problem + geometric hierarc
 #define AMG_MULT 0
 #define AMG_AFACX 1
 #define AMG_MULTADD 2
+#define AMG_BPX 3
 #define AMG_ASYNC_AFACX 5
 #define AMG_ASYNC_MULTADD 6
 

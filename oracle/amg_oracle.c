@@ -822,6 +822,31 @@ void or_vcycle(or_hier *H)
    }
 }
 
+/* SMEM_Sync_AMG.cpp:147-294 SMEM_Sync_Parfor_BPXcycle (solver BPX, ONE_LEVEL):
+ * restrict r[0] to every level, smooth every level (coarsest included) from a
+ * zero guess with num_pre sweeps into e[l] (ONE_LEVEL smoothers), prolong
+ * e_fine += P e_coarse upwards, then u += e[0] (u = e[0] as a preconditioner). */
+void or_bpx_cycle(or_hier *H)
+{
+   int L = H->L;
+   const or_opts *o = &H->o;
+   for (int level = 0; level < L - 1; level++)
+      or_smem_matvec(&H->R[level], H->r[level], H->r[level + 1], 0, H->n[level + 1]);
+   for (int level = 0; level < L; level++) {
+      H->zero_flags[level] = 1;
+      smooth(H, level, H->r[level], H->e[level], H->u_prev[level], H->y[level], o->num_pre, level,
+             0, 0, 0);
+   }
+   for (int level = L - 2; level > -1; level--)
+      or_smem_spgemv(&H->P[level], H->e[level + 1], H->e[level], 1.0, 1.0, H->e[level], 0,
+                     H->n[level]);
+   int n0 = H->n[0];
+   if (H->precond_flag == 1)
+      memcpy(H->u[0], H->e[0], (size_t)n0 * sizeof(double));
+   else
+      for (int i = 0; i < n0; i++) H->u[0][i] += H->e[0][i];
+}
+
 /* SMEM_Sync_AMG.cpp:408-621 SMEM_Sync_Add_Vcycle (ALL_LEVELS, res LOCAL).
  * Level corrections are added to u in level order (the reference adds them
  * from concurrent thread groups without atomics). */
@@ -912,7 +937,8 @@ int or_solve(or_hier *H, const double *f, double *u, double *reshist)
    double t_start = omp_get_wtime();
 #endif
    for (int k = 1; k <= o->num_cycles; k++) {
-      if (all_levels) or_sync_add_vcycle(H);
+      if (o->solver == OR_BPX) or_bpx_cycle(H); /* SMEM_Solve.cpp:161-163 */
+      else if (all_levels) or_sync_add_vcycle(H);
       else or_vcycle(H);
       if (o->cheby_flag == 1) {
          double *uu = H->u[0], *uo = H->u_outer, *yo = H->y_outer;

@@ -147,6 +147,7 @@ int or_solve(or_hier *H, const double *f, double *u, double *reshist);
 /* one cycle on the hierarchy's current state (for kernel-level checks) */
 void or_vcycle(or_hier *H);
 void or_sync_add_vcycle(or_hier *H);
+void or_bpx_cycle(or_hier *H);
 /* SMEM_Cheby.cpp:410-518 (EigsPower) with this hierarchy's V-cycle as M^{-1} */
 void or_eigs_power(or_hier *H, int iters, double *eig_max, double *eig_min);
 void or_cheby_setup(double eig_min, double eig_max, double *mu, double *delta);

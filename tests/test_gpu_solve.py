@@ -103,6 +103,21 @@ def test_mult_vcycle_linear(amg, oracle, ctx, smoother, extra):
     assert hist[-1] / hist[0] < 1e-3  # it converges
 
 
+@pytest.mark.parametrize("smoother,extra", [
+    ("jacobi", {}), ("l1", {}), ("hybrid", {"num_threads": 4}), ("asyncgs", {"num_threads": 1}),
+    ("jacobi", {"num_pre_smooth_sweeps": 2}),
+])
+def test_bpx_cycle(amg, oracle, ctx, smoother, extra):
+    """SMEM_Sync_Parfor_BPXcycle (solver BPX, ONE_LEVEL smoothers): bitwise."""
+    _, L, host = hierarchy(amg, oracle, 20, amg.AMG_INTERP_LINEAR)
+    sm = {"jacobi": amg.AMG_JACOBI, "l1": amg.AMG_L1_JACOBI, "hybrid": amg.AMG_HYBRID_JGS,
+          "asyncgs": amg.AMG_ASYNC_GS}[smoother]
+    opts = amg.default_opts(solver=amg.AMG_BPX, smoother=sm, smooth_weight=0.6, num_cycles=8,
+                            tol=0.0, **extra)
+    f = amg.rhs_rand(0, 20 ** 3)
+    compare_solve(amg, oracle, ctx, host, opts, f)
+
+
 @pytest.mark.parametrize("sm", ["asyncgs", "semiasyncgs"])
 def test_mult_vcycle_async_gs_band(amg, oracle, ctx, sm):
     """Asynchronous Gauss-Seidel smoother with many thread blocks: racy, so
