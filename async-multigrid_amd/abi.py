@@ -123,6 +123,7 @@ PROTOTYPES = {
     "amg_dist_init_host": (_i, [_p, _i, _i, C.c_void_p, _p]),
     "amg_dist_hier_set_replicate_rows": (_i, [_p, _ll]),
     "amg_dist_async_solve": (_i, [_p, _dp, _ip, _dp]),
+    "amg_dist_async_jacobi": (_i, [_p, _dp, _i, _i, _dp]),
     "amg_dist_structured_row_starts": (_i, [_p, _i, _llp]),
     "amg_dist_hier_create": (_i, [_p, _i, _llp, C.c_void_p, C.c_void_p, C.c_void_p,
                                   C.POINTER(AmgOpts), _pp]),

@@ -299,3 +299,173 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
       for (int k = 0; k < D->L; k++) level_corrections[k] = k < active ? D->o.num_cycles : 0;
    return AMG_OK;
 }
+
+// ---------------------------------------------------------------------------
+// DMEM_AsyncSmooth (DMEM_Smooth.cpp:16-313), ASYNC_JACOBI / ASYNC_L1_JACOBI on
+// the fine grid: Jacobi in residual-update form with asynchronous ghost
+// deltas.  Per relaxation k:
+//    e = w .* r   (w = omega / a_ii, or 1 / l1_i)      u = r ./ s
+//    x += e;  r -= A_diag e                            (owned columns only)
+//    send e's boundary values to the neighbours       (finestIntra_outsideSend, ACCUMULATE)
+//    r -= A_offd g for every ghost delta g that HAS arrived  (finestIntra_outsideRecv)
+// The exchange runs on the communication stream, double-buffered over NBUF
+// slots; deltas that have not arrived are applied in a later relaxation, so a
+// rank never waits for its neighbours except when a slot must be reused.  At
+// the end every delta is drained and the true residual ||f - A x|| formed.
+// A_diag / A_offd are the [owned | ghost] column split of the slab CSR: the
+// products run through the tile kernel with the other region zeroed.
+// ---------------------------------------------------------------------------
+namespace {
+
+__global__ void ajac_update_k(const double *__restrict__ r, const double *__restrict__ w,
+                              double *__restrict__ e, double *__restrict__ x, int n)
+{
+   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+      const double d = r[i] * w[i];
+      e[i] = d;
+      x[i] += d;
+   }
+}
+
+__global__ void ajac_weights_k(const double *__restrict__ diag, const double *__restrict__ l1,
+                               double omega, double *__restrict__ w, int n)
+{
+   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+      if (l1)
+         w[i] = 1.0 / l1[i];
+      else
+         w[i] = diag[i] != 0.0 ? omega / diag[i] : 0.0;
+   }
+}
+
+constexpr int AJ_NBUF = 4;
+
+} // namespace
+
+extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, int sweeps, int l1,
+                                     double *relres)
+{
+   AMG_ARG(D && f_local && sweeps >= 0, "amg_dist_async_jacobi: bad argument");
+   amg_ctx *c = D->ctx;
+   hipStream_t s = c->stream, cs = c->comm_stream;
+   DLevel &v = D->lv[0];
+   DistMat &M = v.A;
+   const int n = v.n, ng = M.nghost, no = M.ncol_own;
+   const int np = (int)M.peers.size();
+   AMG_ARG(no == n, "amg_dist_async_jacobi: square fine operator expected");
+   // state: x (= u of level 0), r, e_ext = [e | 0], g_ext = [0 | g], w
+   double *x = v.u, *r = v.r_fine, *eext = v.u_alt, *gext = v.f, *w = v.l1;
+   std::vector<double *> dtmp;
+   auto tmp = [&](size_t cnt) -> double * {
+      double *p = nullptr;
+      if (hipMalloc(&p, std::max<size_t>(1, cnt) * sizeof(double)) != hipSuccess) return nullptr;
+      dtmp.push_back(p);
+      return p;
+   };
+   double *wv = tmp(n), *f = tmp(n), *sbuf = tmp((size_t)std::max<long long>(1, M.nsend) * AJ_NBUF),
+          *rbuf = tmp((size_t)std::max(1, ng) * AJ_NBUF);
+   (void)w;
+   int st = AMG_OK;
+   auto fail = [&](int code) {
+      hipStreamSynchronize(s);
+      hipStreamSynchronize(cs);
+      for (double *p : dtmp) hipFree(p);
+      return code;
+   };
+   if (!wv || !f || !sbuf || !rbuf) return fail(amg_set_error(AMG_ERR_OOM, "amg_dist_async_jacobi: workspace"));
+   if ((st = h2d(s, f, f_local, (size_t)n * sizeof(double))) != AMG_OK) return fail(st);
+   const int nb = std::max(1, std::min(65536, (n + 255) / 256));
+   ajac_weights_k<<<nb, 256, 0, s>>>(M.A->diag, l1 ? v.l1 : nullptr, D->o.smooth_weight, wv, n);
+   amgk::vset(s, x, 0.0, 0, v.cap);
+   amgk::vcopy(s, f, r, 0, n); // x = 0: r = b
+   amgk::vset(s, eext, 0.0, 0, v.cap);
+   amgk::vset(s, gext, 0.0, 0, v.cap);
+   const amgk::Gemv upd = amgk::gemv_mode(-1.0, 1.0); // r = r - A z
+   hipEvent_t packed[AJ_NBUF], sent[AJ_NBUF], arrived[AJ_NBUF];
+   for (int q = 0; q < AJ_NBUF; q++) {
+      hipEventCreateWithFlags(&packed[q], hipEventDisableTiming);
+      hipEventCreateWithFlags(&sent[q], hipEventDisableTiming);
+      hipEventCreateWithFlags(&arrived[q], hipEventDisableTiming);
+   }
+   std::vector<int> pending; // relaxations whose ghost deltas are not applied yet
+   auto apply = [&](int k) -> int {
+      const int q = k % AJ_NBUF;
+      AMG_HIP(hipStreamWaitEvent(s, arrived[q], 0));
+      AMG_HIP(hipMemcpyAsync(gext + no, rbuf + (size_t)q * std::max(1, ng), (size_t)ng * sizeof(double),
+                             hipMemcpyDeviceToDevice, s));
+      amgk::spgemv(s, M.A, gext, r, upd, r, 0, n, nullptr); // r -= A_offd g
+      return AMG_OK;
+   };
+   for (int k = 0; k < sweeps && st == AMG_OK; k++) {
+      const int q = k % AJ_NBUF;
+      // the slot's previous delta must be applied and its send finished
+      for (size_t i = 0; i < pending.size();) {
+         if (pending[i] <= k - AJ_NBUF) {
+            if ((st = apply(pending[i])) != AMG_OK) break;
+            pending.erase(pending.begin() + i);
+         } else {
+            i++;
+         }
+      }
+      if (st != AMG_OK) break;
+      AMG_HIP(hipStreamWaitEvent(s, sent[q], 0));
+      ajac_update_k<<<nb, 256, 0, s>>>(r, wv, eext, x, n);
+      if (np > 0) {
+         launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * std::max<long long>(1, M.nsend), (int)M.nsend);
+         AMG_HIP(hipEventRecord(packed[q], s));
+         AMG_HIP(hipStreamWaitEvent(cs, packed[q], 0));
+         std::vector<void *> sp(np), rp(np);
+         std::vector<long long> sb(np), rb(np);
+         for (int i = 0; i < np; i++) {
+            sp[i] = sbuf + (size_t)q * std::max<long long>(1, M.nsend) + M.soff[i];
+            sb[i] = M.scnt[i] * 8;
+            rp[i] = rbuf + (size_t)q * std::max(1, ng) + M.roff[i];
+            rb[i] = M.rcnt[i] * 8;
+         }
+         if ((st = xp_p2p(c, cs, np, M.peers.data(), sp.data(), sb.data(), rp.data(), rb.data())) != AMG_OK)
+            break;
+         AMG_HIP(hipEventRecord(sent[q], cs));
+         AMG_HIP(hipEventRecord(arrived[q], cs));
+         pending.push_back(k);
+      }
+      // r -= A_diag e (ghost region of e_ext stays zero), overlapping the exchange
+      amgk::spgemv(s, M.A, eext, r, upd, r, 0, n, nullptr);
+      // deltas that have already arrived (host poll: never blocks)
+      for (size_t i = 0; i < pending.size();) {
+         if (hipEventQuery(arrived[pending[i] % AJ_NBUF]) == hipSuccess) {
+            if ((st = apply(pending[i])) != AMG_OK) break;
+            pending.erase(pending.begin() + i);
+         } else {
+            break; // in order: later slots cannot have arrived first
+         }
+      }
+      D->iter = k + 1;
+   }
+   for (size_t i = 0; st == AMG_OK && i < pending.size(); i++) st = apply(pending[i]); // drain
+   for (int q = 0; q < AJ_NBUF; q++) {
+      hipEventDestroy(packed[q]);
+      hipEventDestroy(sent[q]);
+      hipEventDestroy(arrived[q]);
+   }
+   if (st != AMG_OK) return fail(st);
+   // true residual f - A x with a synchronous exchange, and its global norm
+   amgk::vcopy(s, f, v.f, 0, n);
+   if ((st = dist_outer_residual(D, 1)) != AMG_OK) return fail(st);
+   D->pre_ready = false;
+   double hn[2] = {0, 0};
+   if ((st = d2h(s, hn, D->d_hist + 1, sizeof(double))) != AMG_OK) return fail(st);
+   // ||f|| (x0 = 0): the initial residual norm
+   double *p;
+   if ((st = amg_ctx_partials(c, 65536, &p)) != AMG_OK) return fail(st);
+   int parts = 0;
+   amgk::sumsq_partials(s, f, n, p, &parts);
+   amgk::reduce_partials(s, p, parts, D->d_hist + 2, 0, c->d_scalars + 4096);
+   if ((st = xp_allreduce(c, s, D->d_hist + 2, 1)) != AMG_OK) return fail(st);
+   launch_sqrt(s, D->d_hist + 2, D->d_hist + 2);
+   if ((st = d2h(s, hn + 1, D->d_hist + 2, sizeof(double))) != AMG_OK) return fail(st);
+   D->r0norm = hn[1];
+   D->have_state = true;
+   if (relres) *relres = hn[1] > 0 ? hn[0] / hn[1] : 0.0;
+   for (double *q : dtmp) hipFree(q);
+   return AMG_OK;
+}

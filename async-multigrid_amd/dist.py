@@ -281,6 +281,14 @@ class DistHier:
         check(lib.amg_dist_async_solve(self.h, _dp(f), _ip(cnt), C.byref(rel)))
         return rel.value, cnt
 
+    def async_jacobi(self, f_local, sweeps, l1=False):
+        """DMEM_AsyncSmooth (ASYNC_JACOBI / ASYNC_L1_JACOBI) on the fine level: relres."""
+        f = np.ascontiguousarray(f_local, dtype=np.float64)
+        assert f.size == self.n0
+        rel = C.c_double()
+        check(lib.amg_dist_async_jacobi(self.h, _dp(f), int(sweeps), int(l1), C.byref(rel)))
+        return rel.value
+
     def get_u(self):
         u = np.empty(self.n0)
         check(lib.amg_dist_get_u(self.h, _dp(u)))

@@ -309,6 +309,14 @@ int amg_dist_profile_read(amg_dist_hier *D, double *ms, long long *launches, int
  * amg_dist_get_u.  *relres = ||f - A u|| / ||f|| after the levels joined. */
 int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int *level_corrections,
                          double *relres);
+/* DMEM_AsyncSmooth (DMEM_Smooth.cpp:16-313) with ASYNC_JACOBI (l1 = 0: u = r ./ (a_ii/omega))
+ * or ASYNC_L1_JACOBI (l1 = 1): `sweeps` relaxations of the fine level in residual-update
+ * form from x = 0; every relaxation sends its boundary deltas on the communication
+ * stream while the compute stream updates the residual from the owned columns, and
+ * applies neighbours' deltas once they have arrived (never waiting for them).  Read x
+ * with amg_dist_get_u.  *relres = ||f - A x|| / ||f|| after all deltas are drained. */
+int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, int sweeps, int l1,
+                          double *relres);
 /* y = A_0 x on the distributed fine operator (halo exchange + interior/boundary
  * split); *ms = average device milliseconds over reps */
 int amg_dist_fine_spmv(amg_dist_hier *D, int reps, double *ms);

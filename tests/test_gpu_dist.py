@@ -328,3 +328,56 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
     assert list(res[0][2][:L - 1]) == [N] * (L - 1)
     assert rels[0] < 1.0
     assert sync_rel / 50 <= rels[0] <= sync_rel * 50, (rels[0], sync_rel)
+
+
+@pytest.mark.parametrize("nranks,l1", [(1, 0), (2, 0), (3, 1)])
+def test_dist_async_jacobi(amg, oracle, ctx, nranks, l1):
+    """DMEM_AsyncSmooth: Jacobi in residual-update form with asynchronous ghost
+    deltas.  Every delta is applied exactly once (drained at the end), so the
+    result matches synchronous Jacobi up to the order of the additions; the
+    single-rank run goes through RCCL itself."""
+    n = 20
+    gen = amg.Gen(n)
+    f = amg.rhs_rand(0, n ** 3)
+    K, w = 15, 0.7
+    nr, nc, rp, cj, cv = gen.host_csr(amg.AMG_GEN_A, 0)
+    A = oracle.Csr(nr, nc, rp, cj, cv)
+    # synchronous reference: SMEM_Sync_Parfor_Jacobi from zero (zero_flag 0)
+    u = np.zeros(nr)
+    if l1:
+        l1n = oracle.l1_norms(A)
+        for _ in range(K):
+            oracle.smem_l1jacobi(A, f, u, np.zeros(nr), l1n, 1, 0, 0, nr)
+    else:
+        for _ in range(K):
+            oracle.smem_jacobi(A, f, u, np.zeros(nr), w, 1, 0, 0, nr)
+    r = f - oracle.smem_matvec(A, u, np.zeros(nr))
+    ref_rel = np.linalg.norm(r) / np.linalg.norm(f)
+    opts = amg.default_opts(smooth_weight=w)
+    hub = amg.dist.ThreadMailbox(nranks)
+
+    def rank(q):
+        c = amg.Context(0, nstreams=2)
+        if nranks == 1:
+            amg.dist.init_rccl(c, 1, 0, lambda b: b)
+        else:
+            amg.dist.init_host(c, nranks, q, amg.dist.HostTransport(hub, q))
+        D = amg.dist.DistHier(c, gen, opts)
+        rel = D.async_jacobi(f[D.row0:D.row0 + D.n0], K, l1)
+        x = D.get_u()
+        row0 = D.row0
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        return row0, x, rel
+
+    res = sorted(run_ranks(nranks, rank), key=lambda t: t[0])
+    x = np.concatenate([t[1] for t in res])
+    assert all(t[2] == res[0][2] for t in res)
+    if nranks == 1:  # nothing to wait for: exactly synchronous Jacobi, rounding aside
+        np.testing.assert_allclose(res[0][2], ref_rel, rtol=1e-8)
+        np.testing.assert_allclose(x, u, rtol=1e-9, atol=1e-12 * np.abs(u).max())
+    else:  # late deltas are applied one relaxation later: a band (SURVEY.md Sec.8(d))
+        assert 0.5 * ref_rel <= res[0][2] <= 2.0 * ref_rel, (res[0][2], ref_rel)
+        assert np.all(np.isfinite(x))
+    gen.free()
