@@ -68,6 +68,10 @@ class Context:
         """Value-indexed CSR for matrices registered from now on (default on)."""
         check(lib.amg_set_value_index(self.h, int(enable)))
 
+    def set_dict_index(self, enable):
+        """Dictionary-coded CSR for square operators registered from now on (default on)."""
+        check(lib.amg_set_dict_index(self.h, int(enable)))
+
     def csr(self, nrows, ncols, rowptr, col, val, diag_first=1):
         return Mat.register(self, nrows, ncols, rowptr, col, val, diag_first)
 
@@ -94,6 +98,7 @@ class Mat:
         check(lib.amg_mat_info(handle, C.byref(nr), C.byref(nc), C.byref(nz)))
         self.nrows, self.ncols, self.nnz = nr.value, nc.value, nz.value
         self.value_index = lib.amg_mat_value_index(handle)  # table size, 0 = plain CSR
+        self.dict_index = lib.amg_mat_dict_index(handle)    # dictionary size, 0 = not coded
 
     @classmethod
     def register(cls, ctx, nrows, ncols, rowptr, col, val, diag_first=1):

@@ -71,6 +71,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    hipDeviceProp_t prop;
    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
    if (const char *v = std::getenv("AMG_VALUE_INDEX")) c->value_index = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_DICT_INDEX")) c->dict_index = std::atoi(v) != 0;
    *out = c;
    return AMG_OK;
 }
@@ -195,12 +196,87 @@ static int build_value_index(amg_mat *A)
    return AMG_OK;
 }
 
+// dictionary-coded CSR (CSR-DC) on top of the value index: when every entry's
+// (col - row, value) pair comes from at most 256 distinct pairs and no row
+// holds more than AMG_DC_MAXROW entries, each entry becomes one byte and the
+// lane-per-row kernel reads x[row + off] coalesced across a wave.
+static int build_dict_index(amg_mat *A)
+{
+   amg_ctx *c = A->ctx;
+   hipStream_t s = c->stream;
+   constexpr int NS = 4096;
+   unsigned long long *slots = nullptr;
+   AMG_HIP(hipMalloc(&slots, NS * sizeof(unsigned long long) + 64));
+   int *count = reinterpret_cast<int *>(slots + NS);
+   AMG_HIP(hipMemsetAsync(slots, 0xff, NS * sizeof(unsigned long long), s));
+   AMG_HIP(hipMemsetAsync(count, 0, 2 * sizeof(int), s));
+   amgk::dc_collect(s, A, slots, NS, count, count + 1);
+   std::vector<unsigned long long> h(NS);
+   int cm[2] = {0, 0};
+   AMG_HIP(hipMemcpyAsync(h.data(), slots, NS * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(cm, count, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   if (cm[0] < 1 || cm[0] > 256 || cm[1] > AMG_DC_MAXROW) {
+      hipFree(slots);
+      return AMG_OK;
+   }
+   std::vector<unsigned long long> keys;
+   for (auto k : h)
+      if (k != ~0ULL) keys.push_back(k);
+   std::sort(keys.begin(), keys.end());
+   const int T = (int)keys.size();
+   std::vector<double> vt(256, 0.0);
+   AMG_HIP(hipMemcpy(vt.data(), A->vtab, 256 * sizeof(double), hipMemcpyDeviceToHost));
+   std::vector<int> off(256, 0);
+   std::vector<double> dv(256, 0.0);
+   for (int t = 0; t < T; t++) {
+      off[t] = (int)(unsigned int)(keys[t] >> 8);
+      dv[t] = vt[keys[t] & 0xff];
+   }
+   hipError_t e = hipMalloc(&A->didx, (size_t)A->nnz + 64);
+   if (e == hipSuccess) e = hipMalloc(&A->doff, 256 * sizeof(int));
+   if (e == hipSuccess) e = hipMalloc(&A->dval, 256 * sizeof(double));
+   if (e != hipSuccess) {
+      hipFree(A->didx);
+      hipFree(A->doff);
+      hipFree(A->dval);
+      A->didx = nullptr;
+      A->doff = nullptr;
+      A->dval = nullptr;
+      hipFree(slots);
+      (void)hipGetLastError();
+      return AMG_OK;
+   }
+   AMG_HIP(hipMemcpyAsync(slots, keys.data(), T * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemcpyAsync(A->doff, off.data(), 256 * sizeof(int), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemcpyAsync(A->dval, dv.data(), 256 * sizeof(double), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemsetAsync(A->didx + A->nnz, 0, 64, s));
+   amgk::dc_encode(s, A, slots, T, A->didx);
+   AMG_HIP(hipStreamSynchronize(s));
+   hipFree(slots);
+   A->dc_n = T;
+   return AMG_OK;
+}
+
 int amg_mat_finish(amg_mat *A)
 {
    amgk::extract_diag(A->ctx->stream, A);
    AMG_HIP(hipGetLastError());
    if (A->ctx->value_index && A->nnz > 0) AMG_TRY(build_value_index(A));
+   if (A->ctx->dict_index && A->vidx && A->nrows == A->ncols) AMG_TRY(build_dict_index(A));
    return AMG_OK;
+}
+
+extern "C" int amg_set_dict_index(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_dict_index: null context");
+   c->dict_index = enable ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_dict_index(const amg_mat *A)
+{
+   return A ? A->dc_n : 0;
 }
 
 extern "C" int amg_set_value_index(amg_ctx *c, int enable)
@@ -255,6 +331,9 @@ extern "C" int amg_mat_free(amg_mat *A)
    hipFree(A->diag);
    hipFree(A->vidx);
    hipFree(A->vtab);
+   hipFree(A->didx);
+   hipFree(A->doff);
+   hipFree(A->dval);
    delete A;
    return AMG_OK;
 }

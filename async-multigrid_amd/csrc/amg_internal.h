@@ -41,6 +41,8 @@ constexpr int AMG_TILE_ROWS = 256;
 constexpr int AMG_CHUNK = 2048;
 // device arrays of col/val are padded so 16-byte vector loads past nnz stay in bounds
 constexpr int AMG_NNZ_PAD = 8;
+// longest row the dictionary-coded kernel stages in LDS
+constexpr int AMG_DC_MAXROW = 32;
 
 struct amg_transport; // amg_dist.cpp: RCCL communicator or host-callback test transport
 
@@ -57,6 +59,7 @@ struct amg_ctx {
    double *h_pinned = nullptr;             // pinned host mirror of scalars
    int num_cus = 256;
    int value_index = 1; // build value-indexed CSR for matrices with <= 256 distinct values
+   int dict_index = 1;  // build dictionary-coded CSR for stencil-like square operators
 };
 
 struct amg_mat {
@@ -74,6 +77,13 @@ struct amg_mat {
    unsigned char *vidx = nullptr;
    double *vtab = nullptr;
    int vi_n = 0;
+   // dictionary-coded form (square operators whose (col - row, value) pairs
+   // fit 256 entries and whose rows hold <= AMG_DC_MAXROW entries):
+   // col = row + doff[didx[k]], a_ik = dval[didx[k]]
+   unsigned char *didx = nullptr;
+   int *doff = nullptr;
+   double *dval = nullptr;
+   int dc_n = 0;
 };
 
 struct amg_vec {
@@ -172,6 +182,12 @@ void vi_collect(hipStream_t s, const double *val, long long nnz, unsigned long l
                 int *count);
 void vi_encode(hipStream_t s, const double *val, long long nnz, const unsigned long long *keys, int T,
                unsigned char *vidx);
+
+// dictionary-coded CSR construction (needs the value index)
+void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,
+                int *maxlen);
+void dc_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
+               unsigned char *didx);
 
 // deterministic reductions
 void sumsq_partials(hipStream_t s, const double *x, int n, double *partials, int *nparts);

@@ -51,7 +51,7 @@ def load_traffic(n, fmt):
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         d = json.load(open(path))
-        return d[str(n)]["csr-vi" if fmt.startswith("csr-vi") else "csr"]["fine_residual_bytes_per_launch"]
+        return d[str(n)][fmt.split(" ")[0]]["fine_residual_bytes_per_launch"]
     except Exception:
         return None
 
@@ -127,10 +127,12 @@ def main():
     n0 = As[0].nrows
     z0 = As[0].nnz
     # bytes per stored entry of the format the kernels stream: 4 (col) + 8 (val)
-    # for CSR, 4 (col) + 1 (value index) for value-indexed CSR
-    vi = As[0].value_index
-    bpe = 5 if vi else 12
-    fmt = f"csr-vi ({vi}-entry value table)" if vi else "csr"
+    # for CSR, 4 (col) + 1 (value index) for value-indexed CSR, 1 (dictionary
+    # index) for dictionary-coded CSR
+    vi, dc = As[0].value_index, As[0].dict_index
+    bpe = 1 if dc else 5 if vi else 12
+    fmt = (f"csr-dc ({dc}-entry (offset, value) dictionary)" if dc else
+           f"csr-vi ({vi}-entry value table)" if vi else "csr")
     # dominant kernel: fine-grid residual SpGEMV r = f - A u (bpe z + 28 n + 4 algorithmic bytes)
     res_bytes = bpe * z0 + 28 * n0 + 4
     res_ms = ms[0] / max(launches[0], 1)

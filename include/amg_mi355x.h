@@ -106,6 +106,14 @@ int amg_mat_free(amg_mat *A);
 int amg_set_value_index(amg_ctx *ctx, int enable);
 /* number of table entries of A's value index (0: plain CSR) */
 int amg_mat_value_index(const amg_mat *A);
+/* dictionary-coded CSR for square operators registered from now on: 1 (default; env
+ * AMG_DICT_INDEX=0 turns it off) = when A has a value index, at most 256 distinct
+ * (column - row, value) pairs and rows of at most 32 entries (stencil and structured
+ * Galerkin operators), each entry is stored as one byte and the kernels run lane per
+ * row with coalesced x[row + offset] gathers (bit-identical results) */
+int amg_set_dict_index(amg_ctx *ctx, int enable);
+/* number of dictionary entries of A (0: not dictionary-coded) */
+int amg_mat_dict_index(const amg_mat *A);
 int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz);
 int amg_mat_download(amg_ctx *ctx, const amg_mat *A, int *rowptr, int *col, double *val);
 

@@ -99,9 +99,13 @@ def test_value_index_selection(mats):
         assert dev[name].value_index == want, (name, nd, dev[name].value_index)
     assert dev["lap16"].value_index == 2
     assert dev["rand_q"].value_index == 256 and dev["rand_q257"].value_index == 0
+    # dictionary-coded: square stencil / structured Galerkin operators only
+    assert dev["lap16"].dict_index == 7 and dev["A1"].dict_index == 54
+    for name in ("P0", "R0", "rand_sq", "rand_q", "longrows_q"):
+        assert dev[name].dict_index == 0, name
 
 
-@pytest.mark.parametrize("name", ["lap16", "rand_q", "longrows_q", "P0"])
+@pytest.mark.parametrize("name", ["lap16", "lap_rect", "A1", "rand_q", "longrows_q", "P0"])
 def test_value_index_matches_plain(mats, ctx, amg, name):
     """The same matrix registered with and without the value index gives
     bit-identical SpGEMV, Jacobi and fused residual+Jacobi results."""
@@ -110,15 +114,27 @@ def test_value_index_matches_plain(mats, ctx, amg, name):
     ctx.set_value_index(0)
     plain = ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val)
     ctx.set_value_index(1)
-    assert plain.value_index == 0 and dev[name].value_index > 0
+    ctx.set_dict_index(0)
+    vi_only = ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val)
+    ctx.set_dict_index(1)
+    assert plain.value_index == 0 and dev[name].value_index > 0 and vi_only.dict_index == 0
     x = ctx.vec(_vecs(A.ncols, 5))
     b = ctx.vec(_vecs(A.nrows, 6))
-    for M in (plain, dev[name]):
+    outs = []
+    for M in (plain, vi_only, dev[name]):
         y = ctx.vec(A.nrows)
         amg.smem.SMEM_SpGEMV(ctx, M, x, b, -1.0, 1.0, y, 0, A.nrows)
-        M._y = y.download()
-    assert_bitwise(dev[name]._y, plain._y, name)
+        outs.append(y.download())
+        if A.nrows == A.ncols:
+            u = ctx.vec(_vecs(A.nrows, 7))
+            amg.smem.SMEM_Sync_Parfor_Jacobi(ctx, M, b, u, ctx.vec(A.nrows), 2, 0, 0.7)
+            outs.append(u.download())
+    k = len(outs) // 3
+    for i in range(k):
+        assert_bitwise(outs[k + i], outs[i], name)
+        assert_bitwise(outs[2 * k + i], outs[i], name)
     plain.free()
+    vi_only.free()
 
 
 @pytest.mark.parametrize("name", ALL)

@@ -26,6 +26,15 @@ H.solve_start(f, ctx.vec(n ** 3))
 H.iterate(3)
 ctx.sync()
 H.free()
+# value-indexed (dictionary off) fine residuals
+ctx.set_dict_index(0)
+A0v = g.register(ctx, amg.AMG_GEN_A, 0)
+xv = ctx.vec(np.random.default_rng(0).uniform(-1, 1, A0v.ncols))
+yv = ctx.vec(A0v.nrows)
+for _ in range(3):
+    amg.smem.SMEM_Sync_SpGEMV(ctx, A0v, xv, f, -1.0, 1.0, yv)
+ctx.sync()
+A0v.free()
 ctx.set_value_index(0)
 A0 = g.register(ctx, amg.AMG_GEN_A, 0)
 x = ctx.vec(np.random.default_rng(0).uniform(-1, 1, A0.ncols))

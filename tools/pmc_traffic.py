@@ -52,21 +52,22 @@ def main():
     rows = n ** 3
     z = 7 * rows - 6 * n * n
     res = {}
-    for fmt, vi in (("csr-vi", "true"), ("csr", "false")):
-        pat = r"csr_tile_kernel<.*>, 1, false, amgk::EpiGemv, %s" % vi
+    for fmt, vi in (("csr-dc", "dc"), ("csr-vi", "true"), ("csr", "false")):
+        pat = (r"csr_dc_kernel<1, false, amgk::EpiGemv>" if vi == "dc" else
+               r"csr_tile_kernel<.*>, 1, false, amgk::EpiGemv, %s" % vi)
         F = pick(fetch, pat, rows)
         W = pick(write, pat, rows)
         if not F or not W:
             continue
         Fm, Wm = sum(F) / len(F), sum(W) / len(W)
-        s16 = 4 * z if vi == "true" else 12 * z
-        s4 = (z if vi == "true" else 0) + 4 * (rows + 1)
-        s8 = 8 * rows
+        s16 = {"dc": 0, "true": 4 * z, "false": 12 * z}[vi]
+        s4 = {"dc": 0, "true": z, "false": 0}[vi] + 4 * (rows + 1)
+        s8 = 8 * rows + (z if vi == "dc" else 0)  # dictionary bytes: staged with 8-byte lanes
         known_rep = s16 * fac["read16"] + s4 * fac["read4"] + s8 * fac["read8"]
         gather = (Fm - known_rep) / fac["read8"]
         writes = Wm / fac["write8"]
         traffic = s16 + s4 + s8 + gather + writes
-        alg = (5 if vi == "true" else 12) * z + 28 * rows + 4
+        alg = {"dc": 1, "true": 5, "false": 12}[vi] * z + 28 * rows + 4
         res[fmt] = {"fine_residual_bytes_per_launch": traffic, "alg_bytes_per_launch": alg,
                     "traffic_over_alg": traffic / alg, "fetch_size_raw": Fm, "write_size_raw": Wm,
                     "gather_bytes_est": gather, "gather_alg_bytes": 8 * rows, "launches": len(F)}
