@@ -209,12 +209,12 @@ static int build_dict_index(amg_mat *A)
    AMG_HIP(hipMalloc(&slots, NS * sizeof(unsigned long long) + 64));
    int *count = reinterpret_cast<int *>(slots + NS);
    AMG_HIP(hipMemsetAsync(slots, 0xff, NS * sizeof(unsigned long long), s));
-   AMG_HIP(hipMemsetAsync(count, 0, 2 * sizeof(int), s));
+   AMG_HIP(hipMemsetAsync(count, 0, 3 * sizeof(int), s));
    amgk::dc_collect(s, A, slots, NS, count, count + 1);
    std::vector<unsigned long long> h(NS);
-   int cm[2] = {0, 0};
+   int cm[3] = {0, 0, 0}; // distinct pairs, longest row, some anchor != row
    AMG_HIP(hipMemcpyAsync(h.data(), slots, NS * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-   AMG_HIP(hipMemcpyAsync(cm, count, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(cm, count, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
    AMG_HIP(hipStreamSynchronize(s));
    if (cm[0] < 1 || cm[0] > 256 || cm[1] > AMG_DC_MAXROW) {
       hipFree(slots);
@@ -233,16 +233,20 @@ static int build_dict_index(amg_mat *A)
       off[t] = (int)(unsigned int)(keys[t] >> 8);
       dv[t] = vt[keys[t] & 0xff];
    }
+   const bool need_anchor = cm[2] != 0 || A->nrows != A->ncols;
    hipError_t e = hipMalloc(&A->didx, (size_t)A->nnz + 64);
    if (e == hipSuccess) e = hipMalloc(&A->doff, 256 * sizeof(int));
    if (e == hipSuccess) e = hipMalloc(&A->dval, 256 * sizeof(double));
+   if (e == hipSuccess && need_anchor) e = hipMalloc(&A->danch, std::max(1, A->nrows) * sizeof(int));
    if (e != hipSuccess) {
       hipFree(A->didx);
       hipFree(A->doff);
       hipFree(A->dval);
+      hipFree(A->danch);
       A->didx = nullptr;
       A->doff = nullptr;
       A->dval = nullptr;
+      A->danch = nullptr;
       hipFree(slots);
       (void)hipGetLastError();
       return AMG_OK;
@@ -251,7 +255,7 @@ static int build_dict_index(amg_mat *A)
    AMG_HIP(hipMemcpyAsync(A->doff, off.data(), 256 * sizeof(int), hipMemcpyHostToDevice, s));
    AMG_HIP(hipMemcpyAsync(A->dval, dv.data(), 256 * sizeof(double), hipMemcpyHostToDevice, s));
    AMG_HIP(hipMemsetAsync(A->didx + A->nnz, 0, 64, s));
-   amgk::dc_encode(s, A, slots, T, A->didx);
+   amgk::dc_encode(s, A, slots, T, A->didx, A->danch);
    AMG_HIP(hipStreamSynchronize(s));
    hipFree(slots);
    A->dc_n = T;
@@ -263,7 +267,7 @@ int amg_mat_finish(amg_mat *A)
    amgk::extract_diag(A->ctx->stream, A);
    AMG_HIP(hipGetLastError());
    if (A->ctx->value_index && A->nnz > 0) AMG_TRY(build_value_index(A));
-   if (A->ctx->dict_index && A->vidx && A->nrows == A->ncols) AMG_TRY(build_dict_index(A));
+   if (A->ctx->dict_index && A->vidx) AMG_TRY(build_dict_index(A));
    return AMG_OK;
 }
 
@@ -334,6 +338,7 @@ extern "C" int amg_mat_free(amg_mat *A)
    hipFree(A->didx);
    hipFree(A->doff);
    hipFree(A->dval);
+   hipFree(A->danch);
    delete A;
    return AMG_OK;
 }

@@ -77,12 +77,14 @@ struct amg_mat {
    unsigned char *vidx = nullptr;
    double *vtab = nullptr;
    int vi_n = 0;
-   // dictionary-coded form (square operators whose (col - row, value) pairs
-   // fit 256 entries and whose rows hold <= AMG_DC_MAXROW entries):
-   // col = row + doff[didx[k]], a_ik = dval[didx[k]]
+   // dictionary-coded form (operators whose (col - anchor, value) pairs fit
+   // 256 entries and whose rows hold <= AMG_DC_MAXROW entries; the anchor of a
+   // row is its first column -- the row itself for diag-first square operators,
+   // then danch is null): col = anchor + doff[didx[k]], a_ik = dval[didx[k]]
    unsigned char *didx = nullptr;
    int *doff = nullptr;
    double *dval = nullptr;
+   int *danch = nullptr;
    int dc_n = 0;
 };
 
@@ -187,7 +189,7 @@ void vi_encode(hipStream_t s, const double *val, long long nnz, const unsigned l
 void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,
                 int *maxlen);
 void dc_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
-               unsigned char *didx);
+               unsigned char *didx, int *anch);
 
 // deterministic reductions
 void sumsq_partials(hipStream_t s, const double *x, int n, double *partials, int *nparts);

@@ -310,127 +310,6 @@ __global__ __launch_bounds__(256) void csr_ptile_kernel(
    }
 }
 
-// Pipelined persistent tile kernel for operators whose tiles fit one LDS
-// chunk with 8 entries per lane (short rows).  Each workgroup walks tiles
-// t, t+G, t+2G, ... and keeps three tiles in flight: while it gathers x for
-// tile n it has already issued the column / value-index loads of tile n+1
-// and the rowptr loads of tile n+2, so one memory latency per tile is
-// exposed instead of three (rowptr -> col -> x).  Per-row sums and epilogues
-// are those of tile_body: bit-identical.  A tile whose entries do not fit
-// the chunk (longer rows) falls back to tile_body.
-template <int NEG, bool NEED_DIAG, class Epi, bool VI>
-__global__ __launch_bounds__(256) void csr_pipe_kernel(
-   const int *__restrict__ rowptr, const int *__restrict__ col, const double *__restrict__ val,
-   const double *__restrict__ x, int rb, int re, Epi epi, double *__restrict__ partials,
-   const unsigned char *__restrict__ vidx, const double *__restrict__ vtab_g, int ntiles)
-{
-   using Cfg = TileCfg<1, 2048, false, false, false, false, false, false, true>;
-   __shared__ __attribute__((aligned(16))) double prod[2048];
-   __shared__ double red[4];
-   __shared__ double vtab[VI ? 256 : 1];
-   const int G = gridDim.x, tid = (int)threadIdx.x;
-   if (VI) vtab[tid] = vtab_g[tid];
-   struct Meta {
-      int tb, te, rs, rend;
-   };
-   struct Ent {
-      v4i c0, c1;
-      unsigned long long b; // VI: 8 value indices
-      v2d v0, v1, v2, v3;   // plain: 8 values
-   };
-   auto load_meta = [&](int t, Meta &m) {
-      m.tb = m.te = m.rs = m.rend = 0;
-      if (t < ntiles) {
-         const int r0 = rb + t * 256, r1 = min(r0 + 256, re), row = r0 + tid;
-         m.tb = rowptr[r0];
-         m.te = rowptr[r1];
-         if (row < r1) {
-            m.rs = rowptr[row];
-            m.rend = rowptr[row + 1];
-         }
-      }
-   };
-   auto fits = [](const Meta &m) { return m.te - (m.tb & ~3) <= 2048; };
-   auto load_ent = [&](const Meta &m, Ent &e) {
-      const int k = (m.tb & ~3) + 8 * tid;
-      if (k < m.te && fits(m)) {
-         e.c0 = *reinterpret_cast<const v4i *>(col + k);
-         e.c1 = *reinterpret_cast<const v4i *>(col + k + 4);
-         if (VI) {
-            e.b = *reinterpret_cast<const unsigned long long *>(vidx + k);
-         } else {
-            e.v0 = *reinterpret_cast<const v2d *>(val + k);
-            e.v1 = *reinterpret_cast<const v2d *>(val + k + 2);
-            e.v2 = *reinterpret_cast<const v2d *>(val + k + 4);
-            e.v3 = *reinterpret_cast<const v2d *>(val + k + 6);
-         }
-      }
-   };
-   int t = blockIdx.x;
-   Meta m0, m1;
-   Ent e0;
-   load_meta(t, m0);
-   load_meta(t + G, m1);
-   load_ent(m0, e0);
-   if (VI) __syncthreads();
-   for (; t < ntiles; t += G) {
-      Meta m2;
-      Ent e1;
-      load_meta(t + 2 * G, m2);
-      load_ent(m1, e1);
-      if (!fits(m0)) {
-         tile_body<Cfg, NEG, NEED_DIAG, Epi, VI>(t, rowptr, col, val, x, rb, re, epi, partials, vidx,
-                                                 vtab, prod, red);
-      } else {
-         const int r0 = rb + t * 256, r1 = min(r0 + 256, re), row = r0 + tid;
-         double acc = 0.0, dg = 0.0, pf = 0.0;
-         if (row < r1) {
-            acc = epi.init(row);
-            pf = epi.pf(row);
-            if (NEED_DIAG) dg = VI ? vtab[vidx[m0.rs]] : val[m0.rs];
-         }
-         const int base = m0.tb & ~3, k = base + 8 * tid;
-         if (k < m0.te) {
-            double v[8];
-            if (VI) {
-#pragma unroll
-               for (int j = 0; j < 8; j++) v[j] = vtab[(e0.b >> (8 * j)) & 0xff];
-            } else {
-               v[0] = e0.v0.x; v[1] = e0.v0.y; v[2] = e0.v1.x; v[3] = e0.v1.y;
-               v[4] = e0.v2.x; v[5] = e0.v2.y; v[6] = e0.v3.x; v[7] = e0.v3.y;
-            }
-            const double x0 = x[e0.c0.x], x1 = x[e0.c0.y], x2 = x[e0.c0.z], x3 = x[e0.c0.w];
-            const double x4 = x[e0.c1.x], x5 = x[e0.c1.y], x6 = x[e0.c1.z], x7 = x[e0.c1.w];
-            v2d *dst = reinterpret_cast<v2d *>(prod + (k - base));
-            dst[0] = v2d{v[0] * x0, v[1] * x1};
-            dst[1] = v2d{v[2] * x2, v[3] * x3};
-            dst[2] = v2d{v[4] * x4, v[5] * x5};
-            dst[3] = v2d{v[6] * x6, v[7] * x7};
-         }
-         __syncthreads();
-         for (int kk = m0.rs; kk < m0.rend; ++kk) {
-            if (NEG)
-               acc -= prod[kk - base];
-            else
-               acc += prod[kk - base];
-         }
-         double sq = 0.0;
-         if (row < r1) {
-            const double out = epi.finish(row, acc, dg, pf);
-            sq = out * out;
-         }
-         if (partials) {
-            const double sblk = block_sum_256(sq, red);
-            if (tid == 0) partials[t] = sblk;
-         }
-         __syncthreads(); // WAR on prod before the next tile
-      }
-      m0 = m1;
-      m1 = m2;
-      e0 = e1;
-   }
-}
-
 // Dictionary-coded CSR (CSR-DC) kernel, lane per row.  For operators whose
 // (column - row, value) pairs fit a 256-entry dictionary (stencil and
 // structured Galerkin operators) every entry is one byte: col = row +
@@ -441,69 +320,97 @@ __global__ __launch_bounds__(256) void csr_pipe_kernel(
 // for 64 consecutive rows: a coalesced gather.  Each lane sums its row
 // sequentially: bit-identical to the other kernels.  Rows of at most
 // AMG_DC_MAXROW entries (checked at registration).
-template <int NEG, bool NEED_DIAG, class Epi>
+template <int NEG, bool NEED_DIAG, class Epi, int RPL = 2, bool STAGE = true>
 __global__ __launch_bounds__(256) void csr_dc_kernel(
    const int *__restrict__ rowptr, const unsigned char *__restrict__ didx,
    const int *__restrict__ doff_g, const double *__restrict__ dval_g, const double *__restrict__ x,
-   int rb, int re, Epi epi, double *__restrict__ partials)
+   int rb, int re, Epi epi, double *__restrict__ partials, int T, const int *__restrict__ anch)
 {
+   // RPL rows per lane (lane owns rows r0 + q*256 + lane); STAGE: the tile's
+   // entry bytes go through LDS (coalesced 8-byte loads) instead of each lane
+   // reading its row's bytes from global memory
    __shared__ int otab[256];
    __shared__ double vtab[256];
-   __shared__ __attribute__((aligned(16))) unsigned char ent[256 * AMG_DC_MAXROW + 32];
+   __shared__ __attribute__((aligned(16))) unsigned char ent[STAGE ? 256 * RPL * AMG_DC_MAXROW + 32 : 8];
    __shared__ double red[4];
    const int tid = (int)threadIdx.x;
-   const int r0 = rb + (int)blockIdx.x * 256, r1 = min(r0 + 256, re), row = r0 + tid;
-   const int tb = rowptr[r0], te = rowptr[r1];
-   int rs = 0, rend = 0;
-   double acc = 0.0, pf = 0.0;
-   if (row < r1) {
-      rs = rowptr[row];
-      rend = rowptr[row + 1];
-      acc = epi.init(row);
-      pf = epi.pf(row);
+   const int r0 = rb + (int)blockIdx.x * 256 * RPL, r1 = min(r0 + 256 * RPL, re);
+   int rs[RPL], rend[RPL], an[RPL];
+   double acc[RPL], pf[RPL];
+#pragma unroll
+   for (int q = 0; q < RPL; q++) {
+      const int row = r0 + q * 256 + tid;
+      rs[q] = rend[q] = 0;
+      an[q] = row;
+      acc[q] = pf[q] = 0.0;
+      if (row < r1) {
+         rs[q] = rowptr[row];
+         rend[q] = rowptr[row + 1];
+         if (anch) an[q] = anch[row];
+         acc[q] = epi.init(row);
+         pf[q] = epi.pf(row);
+      }
    }
-   otab[tid] = doff_g[tid];
-   vtab[tid] = dval_g[tid];
-   const int base = tb & ~7;
-   const int nw = (te - base + 8 + 7) >> 3; // one extra word: a_ii of an empty last row
-   const unsigned long long *src = reinterpret_cast<const unsigned long long *>(didx + base);
-   unsigned long long *dst = reinterpret_cast<unsigned long long *>(ent);
-   for (int w = tid; w < nw; w += 256) dst[w] = src[w];
+   if (tid < T) {
+      otab[tid] = doff_g[tid];
+      vtab[tid] = dval_g[tid];
+   }
+   int base = 0;
+   if (STAGE) {
+      const int tb = rowptr[r0], te = rowptr[r1];
+      base = tb & ~7;
+      const int nw = (te - base + 8 + 7) >> 3; // one extra word: a_ii of an empty last row
+      const unsigned long long *src = reinterpret_cast<const unsigned long long *>(didx + base);
+      unsigned long long *dst = reinterpret_cast<unsigned long long *>(ent);
+      for (int w = tid; w < nw; w += 256) dst[w] = src[w];
+   }
    __syncthreads();
-   double sq = 0.0;
-   if (row < r1) {
+   double sq[RPL];
+#pragma unroll
+   for (int q = 0; q < RPL; q++) {
+      const int row = r0 + q * 256 + tid;
+      sq[q] = 0.0;
+      if (row >= r1) continue;
+      auto eb = [&](int k) -> int { return STAGE ? ent[k - base] : didx[k]; };
       double dg = 0.0;
-      if (NEED_DIAG) dg = vtab[ent[rs - base]]; // a_ii := A_data[A_i[i]]
-      for (int k = rs; k < rend; k += 8) {
-         const int m = rend - k;
+      if (NEED_DIAG) dg = vtab[eb(rs[q])]; // a_ii := A_data[A_i[i]]
+      for (int k = rs[q]; k < rend[q]; k += 8) {
+         const int m = rend[q] - k;
          double xv[8], vv[8];
 #pragma unroll
          for (int j = 0; j < 8; j++) {
             xv[j] = 0.0;
             vv[j] = 0.0;
             if (j < m) {
-               const int b = ent[k + j - base];
-               vv[j] = vtab[b];
-               xv[j] = x[row + otab[b]];
+               const int bb = eb(k + j);
+               vv[j] = vtab[bb];
+               xv[j] = x[an[q] + otab[bb]];
             }
          }
 #pragma unroll
          for (int j = 0; j < 8; j++)
             if (j < m) {
                if (NEG)
-                  acc -= vv[j] * xv[j];
+                  acc[q] -= vv[j] * xv[j];
                else
-                  acc += vv[j] * xv[j];
+                  acc[q] += vv[j] * xv[j];
             }
       }
-      const double out = epi.finish(row, acc, dg, pf);
-      sq = out * out;
+      const double out = epi.finish(row, acc[q], dg, pf[q]);
+      sq[q] = out * out;
    }
    if (partials) {
-      const double sblk = block_sum_256(sq, red);
-      if (tid == 0) partials[blockIdx.x] = sblk;
+      // one partial per 256-row tile, the layout of the tile kernel
+#pragma unroll
+      for (int q = 0; q < RPL; q++) {
+         const double sblk = block_sum_256(sq[q], red);
+         if (tid == 0 && r0 + q * 256 < r1) partials[blockIdx.x * RPL + q] = sblk;
+      }
    }
 }
+
+// dictionary-coded launches: two 256-row tiles per workgroup (see csr_dc_kernel)
+static inline int dc_blocks(int tiles) { return (tiles + 1) / 2; }
 
 // production configuration (tools/tune_spmv.py picks it on the MI355X)
 using ProdCfg = TileCfg<1, 2048, false, false>;
@@ -634,11 +541,11 @@ void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, c
    const int nb = tile_blocks(rb, re);
    if (A->didx) {
       if (g.negacc)
-         csr_dc_kernel<1, false, EpiGemv><<<nb, 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval, x,
-                                                              rb, re, e, partials);
+         csr_dc_kernel<1, false, EpiGemv><<<dc_blocks(nb), 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval, x,
+                                                              rb, re, e, partials, A->dc_n, A->danch);
       else
-         csr_dc_kernel<0, false, EpiGemv><<<nb, 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval, x,
-                                                              rb, re, e, partials);
+         csr_dc_kernel<0, false, EpiGemv><<<dc_blocks(nb), 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval, x,
+                                                              rb, re, e, partials, A->dc_n, A->danch);
    } else if (A->vidx && !partials && !g.negacc && A->nnz < 5LL * A->nrows && nb > 4096) {
       // short rows (prolongation): tiles carry little work, so 4096 persistent
       // workgroups walking the tiles beat one workgroup per tile
@@ -673,11 +580,13 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
    const int nb = tile_blocks(rb, re);
    if (A->didx) {
       if (l1)
-         csr_dc_kernel<1, false, EpiL1Jacobi><<<nb, 256, 0, s>>>(
-            A->rowptr, A->didx, A->doff, A->dval, x, rb, re, EpiL1Jacobi{f, x, l1, out}, nullptr);
+         csr_dc_kernel<1, false, EpiL1Jacobi><<<dc_blocks(nb), 256, 0, s>>>(
+            A->rowptr, A->didx, A->doff, A->dval, x, rb, re, EpiL1Jacobi{f, x, l1, out}, nullptr,
+            A->dc_n, A->danch);
       else
-         csr_dc_kernel<1, true, EpiJacobi><<<nb, 256, 0, s>>>(
-            A->rowptr, A->didx, A->doff, A->dval, x, rb, re, EpiJacobi{f, x, out, omega}, nullptr);
+         csr_dc_kernel<1, true, EpiJacobi><<<dc_blocks(nb), 256, 0, s>>>(
+            A->rowptr, A->didx, A->doff, A->dval, x, rb, re, EpiJacobi{f, x, out, omega}, nullptr,
+            A->dc_n, A->danch);
    } else if (l1) {
       EpiL1Jacobi e{f, x, l1, out};
       if (A->vidx)
@@ -709,11 +618,11 @@ void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const dou
    EpiResJacobi e{f, x, l1, r, unext, omega};
    if (A->didx) {
       if (l1)
-         csr_dc_kernel<1, false, EpiResJacobi><<<nb, 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval,
-                                                                  x, rb, re, e, partials);
+         csr_dc_kernel<1, false, EpiResJacobi><<<dc_blocks(nb), 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval,
+                                                                  x, rb, re, e, partials, A->dc_n, A->danch);
       else
-         csr_dc_kernel<1, true, EpiResJacobi><<<nb, 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval,
-                                                                 x, rb, re, e, partials);
+         csr_dc_kernel<1, true, EpiResJacobi><<<dc_blocks(nb), 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval,
+                                                                 x, rb, re, e, partials, A->dc_n, A->danch);
    } else if (A->vidx && short_rows(A)) {
       if (l1)
          csr_tile_kernel<ShortCfg, 1, false, EpiResJacobi, true><<<nb, 256, 0, s>>>(
@@ -814,14 +723,14 @@ __global__ __launch_bounds__(256) void ablation_kernel(const int *__restrict__ r
 
 int num_tune_variants() { return 23; }
 
-template <bool VI>
-static void launch_pipe(hipStream_t s, const amg_mat *A, const double *x, double *y, int grid)
+template <int RPL, bool STAGE>
+static void launch_dc(hipStream_t s, const amg_mat *A, const double *x, double *y)
 {
    EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
-   if (VI && !A->vidx) return;
-   const int nt = (A->nrows + 255) / 256;
-   csr_pipe_kernel<0, false, EpiGemv, VI><<<std::min(nt, grid), 256, 0, s>>>(
-      A->rowptr, A->col, A->val, x, 0, A->nrows, e, nullptr, A->vidx, A->vtab, nt);
+   if (!A->didx) return;
+   const int nt = (A->nrows + 256 * RPL - 1) / (256 * RPL);
+   csr_dc_kernel<0, false, EpiGemv, RPL, STAGE><<<nt, 256, 0, s>>>(
+      A->rowptr, A->didx, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->danch);
 }
 
 
@@ -834,7 +743,7 @@ const char *tune_variant_name(int v)
                                  "ABL_localgather", "ABL_noLDS",    "ABL_streamonly",
                                  "vi_gtab",      "vi_persist2048",  "vi_persist4096",
                                  "vi_w8",        "plain_w8",        "vi_w8_nt",     "vi_w8_ch4096",
-                                 "vi_pipe2048",  "vi_pipe4096",     "plain_pipe2048", "vi_pipe1024"};
+                                 "dc_base",      "dc_nostage",      "dc_rpl2",      "dc_rpl2_nostage"};
    return (v >= 0 && v < 23) ? names[v] : "?";
 }
 
@@ -882,10 +791,10 @@ void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x
    case 16: launch_matvec_cfg<TileCfg<1, 2048, false, false, false, false, false, false, true>>(s, A, x, y); break;
    case 17: launch_matvec_cfg<TileCfg<1, 2048, true, false, false, false, false, false, true>, true>(s, A, x, y); break;
    case 18: launch_matvec_cfg<TileCfg<1, 4096, false, false, false, false, false, false, true>, true>(s, A, x, y); break;
-   case 19: launch_pipe<true>(s, A, x, y, 2048); break;
-   case 20: launch_pipe<true>(s, A, x, y, 4096); break;
-   case 21: launch_pipe<false>(s, A, x, y, 2048); break;
-   case 22: launch_pipe<true>(s, A, x, y, 1024); break;
+   case 19: launch_dc<1, true>(s, A, x, y); break;
+   case 20: launch_dc<1, false>(s, A, x, y); break;
+   case 21: launch_dc<2, true>(s, A, x, y); break;
+   case 22: launch_dc<2, false>(s, A, x, y); break;
    default: break;
    }
 }
@@ -1438,17 +1347,21 @@ __device__ __forceinline__ unsigned long long dc_key(int off, unsigned char b)
    return ((unsigned long long)(unsigned int)off << 8) | b;
 }
 
+// anchor of row i: its first column (the diagonal for diag-first square
+// operators, the parent coarse point for interpolation rows)
 __global__ void dc_collect_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                              const unsigned char *__restrict__ vidx, int n,
                              unsigned long long *slots, int nslots, int *count, int *maxlen)
 {
    unsigned long long last0 = VI_EMPTY, last1 = VI_EMPTY;
-   int ml = 0;
+   int ml = 0, offrow = 0;
    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
       const int rs = rowptr[i], re = rowptr[i + 1];
       ml = max(ml, re - rs);
+      const int anc = rs < re ? col[rs] : i;
+      offrow |= (anc != i);
       for (int k = rs; k < re; k++) {
-         const unsigned long long key = dc_key(col[k] - i, vidx[k]);
+         const unsigned long long key = dc_key(col[k] - anc, vidx[k]);
          if (key == last0 || key == last1) continue;
          last1 = last0;
          last0 = key;
@@ -1456,19 +1369,23 @@ __global__ void dc_collect_k(const int *__restrict__ rowptr, const int *__restri
       }
    }
    atomicMax(maxlen, ml);
+   if (offrow) atomicOr(maxlen + 1, 1); // some row's anchor is not its own index
 }
 
 __global__ void dc_encode_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                             const unsigned char *__restrict__ vidx, int n,
                             const unsigned long long *__restrict__ keys, int T,
-                            unsigned char *__restrict__ didx)
+                            unsigned char *__restrict__ didx, int *__restrict__ anch)
 {
    __shared__ unsigned long long tk[256];
    if (threadIdx.x < 256) tk[threadIdx.x] = threadIdx.x < T ? keys[threadIdx.x] : VI_EMPTY;
    __syncthreads();
-   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-      for (int k = rowptr[i]; k < rowptr[i + 1]; k++) {
-         const unsigned long long key = dc_key(col[k] - i, vidx[k]);
+   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+      const int rs = rowptr[i], re = rowptr[i + 1];
+      const int anc = rs < re ? col[rs] : i;
+      if (anch) anch[i] = anc;
+      for (int k = rs; k < re; k++) {
+         const unsigned long long key = dc_key(col[k] - anc, vidx[k]);
          int lo = 0, hi = T - 1;
          while (lo < hi) {
             const int mid = (lo + hi) >> 1;
@@ -1479,6 +1396,7 @@ __global__ void dc_encode_k(const int *__restrict__ rowptr, const int *__restric
          }
          didx[k] = (unsigned char)lo;
       }
+   }
 }
 
 void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,
@@ -1490,11 +1408,11 @@ void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int 
 }
 
 void dc_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
-               unsigned char *didx)
+               unsigned char *didx, int *anch)
 {
    if (A->nrows <= 0) return;
    dc_encode_k<<<std::min(8192, (A->nrows + 255) / 256), 256, 0, s>>>(A->rowptr, A->col, A->vidx,
-                                                                        A->nrows, keys, T, didx);
+                                                                        A->nrows, keys, T, didx, anch);
 }
 
 __global__ void vi_collect_k(const double *__restrict__ val, long long nnz,

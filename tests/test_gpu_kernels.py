@@ -99,13 +99,15 @@ def test_value_index_selection(mats):
         assert dev[name].value_index == want, (name, nd, dev[name].value_index)
     assert dev["lap16"].value_index == 2
     assert dev["rand_q"].value_index == 256 and dev["rand_q257"].value_index == 0
-    # dictionary-coded: square stencil / structured Galerkin operators only
+    # dictionary-coded: stencil / structured Galerkin operators and their
+    # transfers (anchor = each row's first column); not random sparsity or long rows
     assert dev["lap16"].dict_index == 7 and dev["A1"].dict_index == 54
-    for name in ("P0", "R0", "rand_sq", "rand_q", "longrows_q"):
+    assert dev["P0"].dict_index == 20 and dev["R0"].dict_index == 27
+    for name in ("rand_sq", "rand_q", "rand_q257", "longrows_q", "rand_rect"):
         assert dev[name].dict_index == 0, name
 
 
-@pytest.mark.parametrize("name", ["lap16", "lap_rect", "A1", "rand_q", "longrows_q", "P0"])
+@pytest.mark.parametrize("name", ["lap16", "lap_rect", "A1", "rand_q", "longrows_q", "P0", "R1"])
 def test_value_index_matches_plain(mats, ctx, amg, name):
     """The same matrix registered with and without the value index gives
     bit-identical SpGEMV, Jacobi and fused residual+Jacobi results."""

@@ -40,8 +40,9 @@ for name, A in mats.items():
             elif not np.array_equal(out.view(np.uint64), ref.view(np.uint64)):
                 print(f"{name} variant {v}: RESULT MISMATCH")
     for v in vlist:
-        vi = lib.amg_dev_tune_name(v).startswith(b"vi") and A.value_index > 0
-        nbytes = (5 if vi else 12) * A.nnz + 4 * (A.nrows + 1) + 8 * A.ncols + 8 * A.nrows
+        nm = lib.amg_dev_tune_name(v)
+        bpe = 1 if nm.startswith(b"dc") and A.dict_index else 5 if nm.startswith(b"vi") and A.value_index else 12
+        nbytes = bpe * A.nnz + 4 * (A.nrows + 1) + 8 * A.ncols + 8 * A.nrows
         t = np.median(res[v])
         print(f"{name:3s} {lib.amg_dev_tune_name(v).decode():22s} median {t:.3f} ms  min {min(res[v]):.3f}"
               f"  {nbytes / t / 1e6:.0f} GB/s")
