@@ -259,6 +259,7 @@ static int build_dict_index(amg_mat *A)
    AMG_HIP(hipStreamSynchronize(s));
    hipFree(slots);
    A->dc_n = T;
+   A->dc_maxrow = cm[1];
    return AMG_OK;
 }
 

@@ -86,6 +86,7 @@ struct amg_mat {
    double *dval = nullptr;
    int *danch = nullptr;
    int dc_n = 0;
+   int dc_maxrow = 0; // longest row (selects the LDS staging size)
 };
 
 struct amg_vec {

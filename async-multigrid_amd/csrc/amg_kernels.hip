@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256) void csr_ptile_kernel(
 // for 64 consecutive rows: a coalesced gather.  Each lane sums its row
 // sequentially: bit-identical to the other kernels.  Rows of at most
 // AMG_DC_MAXROW entries (checked at registration).
-template <int NEG, bool NEED_DIAG, class Epi, int RPL = 2, bool STAGE = true>
+template <int NEG, bool NEED_DIAG, class Epi, int RPL = 2, bool STAGE = true, int MAXR = AMG_DC_MAXROW>
 __global__ __launch_bounds__(256) void csr_dc_kernel(
    const int *__restrict__ rowptr, const unsigned char *__restrict__ didx,
    const int *__restrict__ doff_g, const double *__restrict__ dval_g, const double *__restrict__ x,
@@ -331,10 +331,11 @@ __global__ __launch_bounds__(256) void csr_dc_kernel(
    // reading its row's bytes from global memory
    __shared__ int otab[256];
    __shared__ double vtab[256];
-   __shared__ __attribute__((aligned(16))) unsigned char ent[STAGE ? 256 * RPL * AMG_DC_MAXROW + 32 : 8];
+   __shared__ __attribute__((aligned(16))) unsigned char ent[STAGE ? 256 * RPL * MAXR + 32 : 8];
    __shared__ double red[4];
    const int tid = (int)threadIdx.x;
-   const int r0 = rb + (int)blockIdx.x * 256 * RPL, r1 = min(r0 + 256 * RPL, re);
+   const int wg = (int)blockIdx.x;
+   const int r0 = rb + wg * 256 * RPL, r1 = min(r0 + 256 * RPL, re);
    int rs[RPL], rend[RPL], an[RPL];
    double acc[RPL], pf[RPL];
 #pragma unroll
@@ -404,13 +405,25 @@ __global__ __launch_bounds__(256) void csr_dc_kernel(
 #pragma unroll
       for (int q = 0; q < RPL; q++) {
          const double sblk = block_sum_256(sq[q], red);
-         if (tid == 0 && r0 + q * 256 < r1) partials[blockIdx.x * RPL + q] = sblk;
+         if (tid == 0 && r0 + q * 256 < r1) partials[wg * RPL + q] = sblk;
       }
    }
 }
 
-// dictionary-coded launches: two 256-row tiles per workgroup (see csr_dc_kernel)
-static inline int dc_blocks(int tiles) { return (tiles + 1) / 2; }
+// dictionary-coded launches: rows of <= 8 entries (7-pt stencil, interpolation)
+// take four 256-row tiles per workgroup, longer rows (27-pt Galerkin,
+// restriction) two (tools/tune_spmv.py, profiles/r01/tune_spmv.log)
+template <int NEG, bool NEED_DIAG, class Epi>
+static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int rb, int re,
+                         const Epi &e, double *partials, int tiles)
+{
+   if (A->dc_maxrow <= 8)
+      csr_dc_kernel<NEG, NEED_DIAG, Epi, 4, true, 8><<<(tiles + 3) / 4, 256, 0, s>>>(
+         A->rowptr, A->didx, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
+   else
+      csr_dc_kernel<NEG, NEED_DIAG, Epi, 2, true, AMG_DC_MAXROW><<<(tiles + 1) / 2, 256, 0, s>>>(
+         A->rowptr, A->didx, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
+}
 
 // production configuration (tools/tune_spmv.py picks it on the MI355X)
 using ProdCfg = TileCfg<1, 2048, false, false>;
@@ -541,11 +554,9 @@ void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, c
    const int nb = tile_blocks(rb, re);
    if (A->didx) {
       if (g.negacc)
-         csr_dc_kernel<1, false, EpiGemv><<<dc_blocks(nb), 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval, x,
-                                                              rb, re, e, partials, A->dc_n, A->danch);
+         launch_dc_op<1, false>(s, A, x, rb, re, e, partials, nb);
       else
-         csr_dc_kernel<0, false, EpiGemv><<<dc_blocks(nb), 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval, x,
-                                                              rb, re, e, partials, A->dc_n, A->danch);
+         launch_dc_op<0, false>(s, A, x, rb, re, e, partials, nb);
    } else if (A->vidx && !partials && !g.negacc && A->nnz < 5LL * A->nrows && nb > 4096) {
       // short rows (prolongation): tiles carry little work, so 4096 persistent
       // workgroups walking the tiles beat one workgroup per tile
@@ -580,13 +591,9 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
    const int nb = tile_blocks(rb, re);
    if (A->didx) {
       if (l1)
-         csr_dc_kernel<1, false, EpiL1Jacobi><<<dc_blocks(nb), 256, 0, s>>>(
-            A->rowptr, A->didx, A->doff, A->dval, x, rb, re, EpiL1Jacobi{f, x, l1, out}, nullptr,
-            A->dc_n, A->danch);
+         launch_dc_op<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out}, nullptr, nb);
       else
-         csr_dc_kernel<1, true, EpiJacobi><<<dc_blocks(nb), 256, 0, s>>>(
-            A->rowptr, A->didx, A->doff, A->dval, x, rb, re, EpiJacobi{f, x, out, omega}, nullptr,
-            A->dc_n, A->danch);
+         launch_dc_op<1, true>(s, A, x, rb, re, EpiJacobi{f, x, out, omega}, nullptr, nb);
    } else if (l1) {
       EpiL1Jacobi e{f, x, l1, out};
       if (A->vidx)
@@ -618,11 +625,9 @@ void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const dou
    EpiResJacobi e{f, x, l1, r, unext, omega};
    if (A->didx) {
       if (l1)
-         csr_dc_kernel<1, false, EpiResJacobi><<<dc_blocks(nb), 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval,
-                                                                  x, rb, re, e, partials, A->dc_n, A->danch);
+         launch_dc_op<1, false>(s, A, x, rb, re, e, partials, nb);
       else
-         csr_dc_kernel<1, true, EpiResJacobi><<<dc_blocks(nb), 256, 0, s>>>(A->rowptr, A->didx, A->doff, A->dval,
-                                                                 x, rb, re, e, partials, A->dc_n, A->danch);
+         launch_dc_op<1, true>(s, A, x, rb, re, e, partials, nb);
    } else if (A->vidx && short_rows(A)) {
       if (l1)
          csr_tile_kernel<ShortCfg, 1, false, EpiResJacobi, true><<<nb, 256, 0, s>>>(
@@ -721,15 +726,15 @@ __global__ __launch_bounds__(256) void ablation_kernel(const int *__restrict__ r
    if (row < r1) y[row] = acc;
 }
 
-int num_tune_variants() { return 23; }
+int num_tune_variants() { return 24; }
 
-template <int RPL, bool STAGE>
+template <int RPL, bool STAGE, int MAXR = AMG_DC_MAXROW>
 static void launch_dc(hipStream_t s, const amg_mat *A, const double *x, double *y)
 {
    EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
-   if (!A->didx) return;
+   if (!A->didx || A->dc_maxrow > MAXR) return;
    const int nt = (A->nrows + 256 * RPL - 1) / (256 * RPL);
-   csr_dc_kernel<0, false, EpiGemv, RPL, STAGE><<<nt, 256, 0, s>>>(
+   csr_dc_kernel<0, false, EpiGemv, RPL, STAGE, MAXR><<<nt, 256, 0, s>>>(
       A->rowptr, A->didx, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->danch);
 }
 
@@ -743,8 +748,9 @@ const char *tune_variant_name(int v)
                                  "ABL_localgather", "ABL_noLDS",    "ABL_streamonly",
                                  "vi_gtab",      "vi_persist2048",  "vi_persist4096",
                                  "vi_w8",        "plain_w8",        "vi_w8_nt",     "vi_w8_ch4096",
-                                 "dc_base",      "dc_nostage",      "dc_rpl2",      "dc_rpl2_nostage"};
-   return (v >= 0 && v < 23) ? names[v] : "?";
+                                 "dc_rpl1",      "dc_rpl2_m8",      "dc_rpl2",      "dc_rpl4_m8",
+                                 "dc_rpl8_m8"};
+   return (v >= 0 && v < 24) ? names[v] : "?";
 }
 
 void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y)
@@ -792,9 +798,10 @@ void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x
    case 17: launch_matvec_cfg<TileCfg<1, 2048, true, false, false, false, false, false, true>, true>(s, A, x, y); break;
    case 18: launch_matvec_cfg<TileCfg<1, 4096, false, false, false, false, false, false, true>, true>(s, A, x, y); break;
    case 19: launch_dc<1, true>(s, A, x, y); break;
-   case 20: launch_dc<1, false>(s, A, x, y); break;
+   case 20: launch_dc<2, true, 8>(s, A, x, y); break;
    case 21: launch_dc<2, true>(s, A, x, y); break;
-   case 22: launch_dc<2, false>(s, A, x, y); break;
+   case 22: launch_dc<4, true, 8>(s, A, x, y); break;
+   case 23: launch_dc<8, true, 8>(s, A, x, y); break;
    default: break;
    }
 }

@@ -250,6 +250,12 @@ class DistHier:
                                        C.cast(r, C.c_void_p), C.byref(opts), C.byref(h)))
         return cls(ctx, None, opts, _handle=h)
 
+    def matrix_info(self, level):
+        """(local nnz, value-index table size, dictionary size) of this rank's A_level."""
+        nnz, vi, dc = C.c_longlong(), C.c_int(), C.c_int()
+        check(lib.amg_dist_hier_matrix_info(self.h, level, C.byref(nnz), C.byref(vi), C.byref(dc)))
+        return nnz.value, vi.value, dc.value
+
     def local_rows(self, level):
         r0, n = C.c_int(), C.c_int()
         check(lib.amg_dist_hier_local_rows(self.h, level, C.byref(r0), C.byref(n)))

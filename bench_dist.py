@@ -46,8 +46,10 @@ def main(args, world, rank):
     opts = amg.default_opts(smooth_weight=args.smooth_weight, num_cycles=1 << 30, tol=0.0,
                             reuse_outer_residual=args.reuse_outer_residual, profile=1)
     D = amg.dist.DistHier(ctx, gen, opts)
-    z0, z1 = D.row0 // (n * n), (D.row0 + D.n0) // (n * n)
-    nnz_local = amg.lib.amg_gen_nnz(gen.h, amg.AMG_GEN_A, 0, z0, z1)
+    nnz_local, vi, dc = D.matrix_info(0)
+    bpe = 1 if dc else 5 if vi else 12  # bytes per stored entry (bench.py)
+    fmt = (f"csr-dc ({dc}-entry (offset, value) dictionary)" if dc else
+           f"csr-vi ({vi}-entry value table)" if vi else "csr")
     if rank == 0:
         log(f"[dist] {world} ranks, {gen.L} levels, slab {D.n0} rows / {nnz_local} nnz on rank 0; "
             f"setup {time.time() - t0:.1f}s")
@@ -70,9 +72,9 @@ def main(args, world, rank):
     rn = D.resnorm()
     ms, launches = D.profile(reset=True)
     res_ms = ms[0] / max(launches[0], 1)
-    res_bytes = 12 * nnz_local + 28 * D.n0 + 4
+    res_bytes = bpe * nnz_local + 28 * D.n0 + 4
     spmv_ms = D.fine_spmv_ms(args.spmv_reps)
-    spmv_bytes = 12 * nnz_local + 20 * D.n0 + 4
+    spmv_bytes = bpe * nnz_local + 20 * D.n0 + 4
     # aggregate fine SpMV rate: all ranks' algorithmic bytes over the slowest rank's time
     agg = torch.tensor([float(spmv_bytes), spmv_ms, float(res_bytes), res_ms], dtype=torch.float64)
     parts = [torch.zeros_like(agg) for _ in range(world)]
@@ -104,12 +106,12 @@ def main(args, world, rank):
             "config": {"workload": f"{n}^3 7-pt Laplacian, SMEM_Solve MULT V(1,1) Jacobi "
                                    f"w={args.smooth_weight}, {gen.L}-level geometric Galerkin "
                                    f"hierarchy, z-slab partition, RCCL ghost exchange",
-                       "n": n, "levels": gen.L, "parallelism": f"slab{world}",
+                       "n": n, "levels": gen.L, "parallelism": f"slab{world}", "matrix_format": fmt,
                        "reuse_outer_residual": args.reuse_outer_residual},
             "fine_spmv": {"gbs_aggregate": spmv_gbs, "ms_max": float(P[:, 1].max()),
                           "frac_per_gpu": spmv_gbs / world / HBM_PEAK_GBS},
-            "roofline": {"bound": "hbm", "kernel": "fine-grid residual SpGEMV r = f - A0 u (rank 0 slab, "
-                                                   "incl. ghost exchange wait)",
+            "roofline": {"bound": "hbm", "kernel": f"fine-grid residual SpGEMV r = f - A0 u ({fmt}, rank 0 "
+                                                   "slab, incl. ghost exchange wait)",
                          "achieved": ach0, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach0 / HBM_PEAK_GBS, "traffic": None,
                          "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms,

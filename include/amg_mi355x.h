@@ -300,6 +300,10 @@ int amg_dist_structured_row_starts(const amg_gen *gen, int nranks, long long *ro
 /* levels with fewer rows than this are replicated on every rank (default 2^18) */
 int amg_dist_hier_set_replicate_rows(amg_ctx *ctx, long long rows);
 int amg_dist_hier_free(amg_dist_hier *D);
+/* this rank's operator of a level: stored entries and storage format (value-index
+ * table size, dictionary size; 0 = not used) */
+int amg_dist_hier_matrix_info(amg_dist_hier *D, int level, long long *nnz, int *value_index,
+                              int *dict_index);
 /* rows [row0, row0 + nrows) of the global level-0 vector this rank owns */
 int amg_dist_hier_local_rows(amg_dist_hier *D, int level, int *row0, int *nrows);
 /* SMEM_Solve on the distributed hierarchy: f/u are this rank's level-0 rows */

@@ -34,9 +34,16 @@ def load(path):
 
 
 def pick(rows, pattern, grid=None):
+    """per-dispatch values of kernels matching pattern; grid = rows of one launch
+    (a dictionary-coded workgroup covers RPL 256-row tiles)"""
     out = []
     for (name, g), vals in rows.items():
-        if re.search(pattern, name) and (grid is None or g == grid):
+        m = re.search(pattern, name)
+        if not m:
+            continue
+        rpl = re.search(r"csr_dc_kernel<\d, \w+, [\w:]+, (\d+),", name)
+        rows_done = g * (int(rpl.group(1)) if rpl else 1)
+        if grid is None or rows_done == grid:
             out += vals
     return out
 
@@ -53,7 +60,7 @@ def main():
     z = 7 * rows - 6 * n * n
     res = {}
     for fmt, vi in (("csr-dc", "dc"), ("csr-vi", "true"), ("csr", "false")):
-        pat = (r"csr_dc_kernel<1, false, amgk::EpiGemv>" if vi == "dc" else
+        pat = (r"csr_dc_kernel<1, false, amgk::EpiGemv," if vi == "dc" else
                r"csr_tile_kernel<.*>, 1, false, amgk::EpiGemv, %s" % vi)
         F = pick(fetch, pat, rows)
         W = pick(write, pat, rows)
