@@ -22,7 +22,8 @@ from .abi import (AMG_JACOBI, AMG_GAUSS_SEIDEL, AMG_HYBRID_JGS, AMG_SYMM_JACOBI,
                   AMG_L1_JACOBI, AMG_L1_HYBRID_JGS, AMG_MULT, AMG_AFACX, AMG_MULTADD,
                   AMG_ASYNC_AFACX, AMG_ASYNC_MULTADD, AMG_INTERP_LINEAR, AMG_INTERP_AGGREGATE,
                   AMG_GEN_A, AMG_GEN_P, AMG_GEN_R, AMG_VEC_F, AMG_VEC_U, AMG_VEC_R,
-                  AMG_ASYNC_GS, AMG_SEMI_ASYNC_GS, AMG_BPX)
+                  AMG_ASYNC_GS, AMG_SEMI_ASYNC_GS, AMG_BPX, AMG_NO_ACCEL, AMG_RICHARD_ACCEL,
+                  AMG_CHEBY_RECUR_ACCEL)
 
 lib = abi.load()
 

@@ -28,6 +28,7 @@ AMG_L1_JACOBI, AMG_L1_HYBRID_JGS = 6, 12
 AMG_MULT, AMG_AFACX, AMG_MULTADD, AMG_ASYNC_AFACX, AMG_ASYNC_MULTADD = 0, 1, 2, 5, 6
 AMG_BPX = 3
 AMG_FULL_ASYNC, AMG_SEMI_ASYNC = 0, 1
+AMG_NO_ACCEL, AMG_RICHARD_ACCEL, AMG_CHEBY_RECUR_ACCEL = 0, 1, 2
 AMG_VEC_F, AMG_VEC_U, AMG_VEC_R = 0, 1, 2
 AMG_INTERP_LINEAR, AMG_INTERP_AGGREGATE = 0, 1
 AMG_GEN_A, AMG_GEN_P, AMG_GEN_R = 0, 1, 2
@@ -40,7 +41,8 @@ class AmgOpts(C.Structure):
                 ("smooth_weight", _d), ("num_cycles", _i), ("tol", _d),
                 ("check_resnorm", _i), ("cheby_flag", _i), ("cheby_mu", _d),
                 ("cheby_delta", _d), ("num_threads", _i), ("jgs_block_rows", _i),
-                ("reuse_outer_residual", _i), ("async_type", _i), ("profile", _i)]
+                ("reuse_outer_residual", _i), ("async_type", _i), ("profile", _i),
+                ("accel_type", _i), ("cheby_grid", _i)]
 
 
 # name -> (restype, argtypes)

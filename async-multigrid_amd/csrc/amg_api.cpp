@@ -44,6 +44,8 @@ extern "C" void amg_opts_default(amg_opts *o)
    o->reuse_outer_residual = 0;
    o->async_type = AMG_FULL_ASYNC;
    o->profile = 0;
+   o->accel_type = AMG_NO_ACCEL; // DMEM_Main.cpp:130
+   o->cheby_grid = 0;            // DMEM_Main.cpp:142
 }
 
 // ---------------------------------------------------------------------------

@@ -541,7 +541,12 @@ int check_opts(const amg_opts *o)
    AMG_ARG(o->cheby_flag == 0 && (o->smoother == AMG_JACOBI || o->smoother == AMG_L1_JACOBI ||
                                    o->smoother == AMG_SYMM_JACOBI),
            "amg_dist: the distributed cycles support the Jacobi / L1 Jacobi / symmetric Jacobi "
-           "smoothers without Chebyshev");
+           "smoothers without the SMEM Chebyshev (use accel_type, DMEM_ChebyUpdate)");
+   AMG_ARG(o->accel_type == AMG_NO_ACCEL || o->accel_type == AMG_RICHARD_ACCEL ||
+              o->accel_type == AMG_CHEBY_RECUR_ACCEL,
+           "amg_dist: accel_type %d (AMG_NO_ACCEL / AMG_RICHARD_ACCEL / AMG_CHEBY_RECUR_ACCEL)",
+           o->accel_type);
+   AMG_ARG(o->cheby_grid >= 0, "amg_dist: cheby_grid %d < 0", o->cheby_grid);
    AMG_ARG(o->solver == AMG_MULT || o->solver == AMG_ASYNC_MULTADD || o->solver == AMG_ASYNC_AFACX,
            "amg_dist: solver must be MULT (amg_dist_solve_*) or ASYNC_MULTADD / ASYNC_AFACX "
            "(amg_dist_async_solve)");
@@ -612,6 +617,10 @@ int build_hier(amg_ctx *c, int L, Partition part, const amg_opts *opts, const Lo
    }
    AMG_TRY(dvec(D.get(), D->lv[0].cap, &D->r0));
    AMG_TRY(dvec(D.get(), D->hist_cap, &D->d_hist));
+   if (D->o.solver == AMG_MULT && D->o.accel_type != AMG_NO_ACCEL) {
+      AMG_TRY(dvec(D.get(), D->lv[0].cap, &D->x_acc));
+      AMG_TRY(dvec(D.get(), std::max(1, D->lv[0].n), &D->d_acc));
+   }
    // replicated coarse hierarchy (identical on every rank, no communication)
    if (Ld < L) {
       const int Lc = L - Ld;
@@ -889,7 +898,7 @@ int d_spgemv(amg_dist_hier *D, DistMat &M, double *x, const double *b, const amg
 
 bool d_reuse(const amg_dist_hier *D)
 {
-   return D->o.reuse_outer_residual && D->o.num_pre_smooth_sweeps > 0;
+   return D->o.reuse_outer_residual && D->o.num_pre_smooth_sweeps > 0 && !dist_mult_accel(D);
 }
 
 // SMEM_Sync_Parfor_Jacobi on a distributed level (ping-pong)
@@ -916,7 +925,11 @@ int d_smooth(amg_dist_hier *D, int l, const double *f, int sweeps, bool allow_re
    return AMG_OK;
 }
 
-int d_vcycle(amg_dist_hier *D)
+// SMEM_Sync_Parfor_Vcycle on the distributed levels.  precond: the cycle runs
+// on the outer residual r0 from a zero level-0 guess (precond_flag, the form
+// DMEM_MultCycle takes with precond_zero_init_guess = 1) and leaves the
+// correction in lv[0].u
+int d_vcycle(amg_dist_hier *D, bool precond)
 {
    amg_ctx *c = D->ctx;
    hipStream_t s = c->stream;
@@ -926,11 +939,12 @@ int d_vcycle(amg_dist_hier *D)
    const amgk::Gemv pro_mode = amgk::gemv_mode(1.0, 1.0);
    for (int l = 0; l < Ld && l < L - 1; l++) {
       DLevel &v = D->lv[l];
-      v.zero_flag = (l == 0) ? 0 : 1;
-      AMG_TRY(d_smooth(D, l, v.f, D->o.num_pre_smooth_sweeps, l == 0 && d_reuse(D)));
+      const double *fl = (l == 0 && precond) ? D->r0 : v.f;
+      v.zero_flag = (l == 0 && !precond) ? 0 : 1;
+      AMG_TRY(d_smooth(D, l, fl, D->o.num_pre_smooth_sweeps, l == 0 && d_reuse(D)));
       {
          DProf pr(D, 0, l == 0);
-         AMG_TRY(d_spgemv(D, v.A, v.u, v.f, res_mode, v.r_fine, nullptr));
+         AMG_TRY(d_spgemv(D, v.A, v.u, fl, res_mode, v.r_fine, nullptr));
       }
       {
          DProf pr(D, 2, l == 0);
@@ -951,7 +965,8 @@ int d_vcycle(amg_dist_hier *D)
    } else {
       // single distributed level: SMEM_Sync_Parfor_Vcycle smooths the coarsest
       DLevel &v = D->lv[L - 1];
-      AMG_TRY(d_smooth(D, L - 1, v.f, D->o.num_pre_smooth_sweeps + D->o.num_post_smooth_sweeps, false));
+      const double *fl = (L == 1 && precond) ? D->r0 : v.f;
+      AMG_TRY(d_smooth(D, L - 1, fl, D->o.num_pre_smooth_sweeps + D->o.num_post_smooth_sweeps, false));
    }
    for (int l = std::min(Ld, L - 1) - 1; l >= 0; l--) {
       DLevel &v = D->lv[l];
@@ -961,7 +976,7 @@ int d_vcycle(amg_dist_hier *D)
          double *xc = (l + 1 < Ld) ? D->lv[l + 1].u : const_cast<double *>(u_rep);
          AMG_TRY(d_spgemv(D, v.P, xc, v.u, pro_mode, v.u, nullptr));
       }
-      AMG_TRY(d_smooth(D, l, v.f, D->o.num_post_smooth_sweeps, false));
+      AMG_TRY(d_smooth(D, l, (l == 0 && precond) ? D->r0 : v.f, D->o.num_post_smooth_sweeps, false));
    }
    AMG_HIP(hipGetLastError());
    return AMG_OK;
@@ -986,7 +1001,7 @@ int d_outer_residual(amg_dist_hier *D, int slot)
          }));
          D->pre_ready = true;
       } else {
-         AMG_TRY(d_spgemv(D, v.A, v.u, v.f, amgk::gemv_mode(-1.0, 1.0), D->r0, p));
+         AMG_TRY(d_spgemv(D, v.A, dist_iterate(D), v.f, amgk::gemv_mode(-1.0, 1.0), D->r0, p));
          D->pre_ready = false;
       }
    }
@@ -1002,6 +1017,31 @@ int d_outer_residual(amg_dist_hier *D, int slot)
 
 int amgd::dist_outer_residual(amg_dist_hier *D, int slot) { return d_outer_residual(D, slot); }
 
+bool amgd::dist_mult_accel(const amg_dist_hier *D)
+{
+   return D->o.solver == AMG_MULT && D->o.accel_type != AMG_NO_ACCEL;
+}
+
+double *amgd::dist_iterate(amg_dist_hier *D) { return dist_mult_accel(D) ? D->x_acc : D->lv[0].u; }
+
+bool amgd::AccelState::next(const amg_opts &o, double *om1, double *omd)
+{
+   if (cycle++ == 0) return false; // DMEM_Misc.cpp:627-631
+   const double mu = o.cheby_mu, delta = o.cheby_delta;
+   double omega;
+   if (o.accel_type == AMG_RICHARD_ACCEL) {
+      omega = 2.0 / (1.0 + std::sqrt(1.0 - std::pow(mu, -2.0))); // :634-636
+   } else {
+      const double c_temp = c; // :638-641
+      c = 2.0 * mu * c - c_prev;
+      c_prev = c_temp;
+      omega = 2.0 * mu * c_prev / c;
+   }
+   *om1 = omega - 1.0;
+   *omd = omega * delta;
+   return true;
+}
+
 int amgd::dist_solve_begin(amg_dist_hier *D, const double *f_local)
 {
    amg_ctx *c = D->ctx;
@@ -1013,6 +1053,11 @@ int amgd::dist_solve_begin(amg_dist_hier *D, const double *f_local)
    // InitVectors on the replicated levels (the coarsest iterate carries over
    // between cycles, so a new solve starts it from zero as one GPU does)
    if (D->coarse) AMG_TRY(amg_hier_reset(D->coarse));
+   if (D->x_acc) {
+      amgk::vset(c->stream, D->x_acc, 0.0, 0, D->lv[0].cap);
+      amgk::vset(c->stream, D->d_acc, 0.0, 0, std::max(1, D->lv[0].n));
+   }
+   D->acc.reset(D->o);
    D->iter = 0;
    AMG_TRY(d_outer_residual(D, 0));
    AMG_TRY(d2h(c->stream, c->h_pinned, D->d_hist, sizeof(double)));
@@ -1033,8 +1078,19 @@ extern "C" int amg_dist_solve_start(amg_dist_hier *D, const double *f_local, dou
 extern "C" int amg_dist_solve_iterate(amg_dist_hier *D, int k)
 {
    AMG_ARG(D && D->have_state, "amg_dist_solve_iterate: call amg_dist_solve_start first");
+   const bool accel = dist_mult_accel(D);
    for (int i = 0; i < k; i++) {
-      AMG_TRY(d_vcycle(D));
+      if (accel) {
+         // DMEM_Mult.cpp:40-55: e = 0; e = M r; x += e; ChebyUpdate(d, e); x += d
+         DLevel &v = D->lv[0];
+         amgk::vset(D->ctx->stream, v.u, 0.0, 0, v.n);
+         AMG_TRY(d_vcycle(D, true));
+         double om1 = 0.0, omd = 0.0;
+         const bool upd = D->acc.next(D->o, &om1, &omd);
+         amgk::dmem_mult_accel(D->ctx->stream, D->x_acc, v.u, D->d_acc, v.n, upd ? 0 : 1, om1, omd);
+      } else {
+         AMG_TRY(d_vcycle(D, false));
+      }
       D->iter++;
       AMG_TRY(d_outer_residual(D, D->iter % (D->hist_cap - 1)));
    }
@@ -1056,7 +1112,7 @@ extern "C" int amg_dist_get_u(amg_dist_hier *D, double *u_local)
 {
    AMG_ARG(D && u_local, "amg_dist_get_u: null argument");
    AMG_HIP(hipStreamSynchronize(D->ctx->stream));
-   AMG_TRY(d2h(D->ctx->stream, u_local, D->lv[0].u, (size_t)D->lv[0].n * sizeof(double)));
+   AMG_TRY(d2h(D->ctx->stream, u_local, dist_iterate(D), (size_t)D->lv[0].n * sizeof(double)));
    return AMG_OK;
 }
 

@@ -166,6 +166,12 @@ int a_smooth(amg_dist_hier *D, AsyncLevel &a, int l, const double *f, double *u,
    return AMG_OK;
 }
 
+// DMEM_Setup.cpp:1911-1913: cheby_grid is clamped to the last grid
+int cheby_grid_of(const amg_dist_hier *D)
+{
+   return std::min(D->o.cheby_grid, (int)D->al.size() - 1);
+}
+
 // one correction of level k (SMEM_Async_Add_AMG inner body / DMEM AddCycle)
 int level_correction(amg_dist_hier *D, int k)
 {
@@ -194,8 +200,19 @@ int level_correction(amg_dist_hier *D, int k)
       amgk::vcopy(s, a.uf, a.e[k], 0, nf);
    }
    for (int l = k - 1; l >= 0; l--) AMG_TRY(prolong_to(D, a, l, a.e[l + 1], a.e[l]));
-   // correction into the shared slab; u_priv = the value each row saw
    const int n0 = D->lv[0].n;
+   if (o.accel_type != AMG_NO_ACCEL) {
+      // DMEM_Add.cpp:319-324: ChebyUpdate(gridk.d, U_array[0]) on the level's
+      // fine correction, async branch (DMEM_Misc.cpp:650-663): the cheby_grid
+      // level carries d, the others scale by w*delta; first cycle: d = u
+      const bool mine = k == cheby_grid_of(D);
+      double om1 = 0.0, omd = 0.0;
+      if (a.acc.next(o, &om1, &omd))
+         amgk::dmem_cheby_update(s, a.d_acc, a.e[0], n0, mine ? 1 : 2, om1, omd);
+      else if (mine)
+         amgk::vcopy(s, a.e[0], a.d_acc, 0, n0);
+   }
+   // correction into the shared slab; u_priv = the value each row saw
    amgk::atomic_correct(s, D->lv[0].u, a.e[0], a.u_priv, n0);
    // private residual r_k = f - A u_k  (SMEM_Residual on u_k)
    AMG_TRY(a_spgemv(D, a, D->lv[0].A, a.u_priv, nullptr, amgk::gemv_mode(1.0, 0.0), a.y));
@@ -254,6 +271,8 @@ int setup_async(amg_dist_hier *D)
       }
       if (Ld < L) AMG_TRY(dvec(D, (size_t)D->gath_blk * (t->nranks + 1), &a.gath));
    }
+   if (D->o.accel_type != AMG_NO_ACCEL)
+      AMG_TRY(dvec(D, std::max(1, D->lv[0].n), &D->al[cheby_grid_of(D)].d_acc));
    AMG_HIP(hipStreamSynchronize(c->stream));
    return AMG_OK;
 }
@@ -280,6 +299,7 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
       AMG_HIP(hipStreamWaitEvent(D->al[k].s, ready, 0));
       // level_vector[k].r[0] = vector.r[0] (SMEM_Async_AMG.cpp:10-15)
       amgk::vcopy(D->al[k].s, D->r0, D->al[k].r[0], 0, n0);
+      D->al[k].acc.reset(D->o);
    }
    // issue order cycle-major / level-minor: every rank enqueues the same
    // sequence per level communicator; the GPU runs the level streams freely
@@ -304,8 +324,9 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
 // DMEM_AsyncSmooth (DMEM_Smooth.cpp:16-313), ASYNC_JACOBI / ASYNC_L1_JACOBI on
 // the fine grid: Jacobi in residual-update form with asynchronous ghost
 // deltas.  Per relaxation k:
-//    e = w .* r   (w = omega / a_ii, or 1 / l1_i)      u = r ./ s
-//    x += e;  r -= A_diag e                            (owned columns only)
+//    u = r ./ s   (s = a_ii / omega, 1 if a_ii == 0; or l1_i)
+//    [accel_type: DMEM_ChebyUpdate(d, u), async branch -- the fine grid is grid 0]
+//    e = u;  x += e;  r -= A_diag e                    (owned columns only)
 //    send e's boundary values to the neighbours       (finestIntra_outsideSend, ACCUMULATE)
 //    r -= A_offd g for every ghost delta g that HAS arrived  (finestIntra_outsideRecv)
 // The exchange runs on the communication stream, double-buffered over NBUF
@@ -317,24 +338,42 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
 // ---------------------------------------------------------------------------
 namespace {
 
-__global__ void ajac_update_k(const double *__restrict__ r, const double *__restrict__ w,
-                              double *__restrict__ e, double *__restrict__ x, int n)
+// one relaxation's local update (DMEM_Smooth.cpp:100-112, 171-183, 229):
+//   u = 0 + r ./ s;  [ChebyUpdate(d, u), async branch of cheby_grid];
+//   e = 0 + u;  x += e
+// acc: 0 none, 1 first cycle (d = u), 2 recurrence with om1 = w - 1, omd = w delta
+// (this grid is cheby_grid), 3 recurrence on another grid (u = omd u)
+__global__ void ajac_update_k(const double *__restrict__ r, const double *__restrict__ sc,
+                              double *__restrict__ e, double *__restrict__ x, double *__restrict__ d,
+                              int n, int acc, double om1, double omd)
 {
    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-      const double d = r[i] * w[i];
-      e[i] = d;
-      x[i] += d;
+      double u = 0.0 + r[i] / sc[i];
+      if (acc == 1) {
+         d[i] = u;
+      } else if (acc == 2) {
+         const double dp = d[i];
+         d[i] = om1 * dp + omd * u;
+         u = om1 * dp + omd * u;
+      } else if (acc == 3) {
+         u = omd * u;
+      }
+      const double ei = 0.0 + 1.0 * u;
+      e[i] = ei;
+      x[i] += 1.0 * ei;
    }
 }
 
-__global__ void ajac_weights_k(const double *__restrict__ diag, const double *__restrict__ l1,
-                               double omega, double *__restrict__ w, int n)
+// wJacobi_scale_gridk (DMEM_Setup.cpp:474-480): a_ii / omega, 1 where a_ii == 0;
+// L1: L1_row_norm_gridk
+__global__ void ajac_scale_k(const double *__restrict__ diag, const double *__restrict__ l1,
+                             double omega, double *__restrict__ sc, int n)
 {
    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
       if (l1)
-         w[i] = 1.0 / l1[i];
+         sc[i] = l1[i];
       else
-         w[i] = diag[i] != 0.0 ? omega / diag[i] : 0.0;
+         sc[i] = diag[i] == 0.0 ? 1.0 : diag[i] / omega;
    }
 }
 
@@ -354,7 +393,7 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
    const int np = (int)M.peers.size();
    AMG_ARG(no == n, "amg_dist_async_jacobi: square fine operator expected");
    // state: x (= u of level 0), r, e_ext = [e | 0], g_ext = [0 | g], w
-   double *x = v.u, *r = v.r_fine, *eext = v.u_alt, *gext = v.f, *w = v.l1;
+   double *x = dist_iterate(D), *r = v.r_fine, *eext = v.u_alt, *gext = v.f, *w = v.l1;
    std::vector<double *> dtmp;
    auto tmp = [&](size_t cnt) -> double * {
       double *p = nullptr;
@@ -363,7 +402,10 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
       return p;
    };
    double *wv = tmp(n), *f = tmp(n), *sbuf = tmp((size_t)std::max<long long>(1, M.nsend) * AJ_NBUF),
-          *rbuf = tmp((size_t)std::max(1, ng) * AJ_NBUF);
+          *rbuf = tmp((size_t)std::max(1, ng) * AJ_NBUF), *dacc = tmp(n);
+   AccelState acc;
+   acc.reset(D->o);
+   const bool accel = D->o.accel_type != AMG_NO_ACCEL;
    (void)w;
    int st = AMG_OK;
    auto fail = [&](int code) {
@@ -372,10 +414,10 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
       for (double *p : dtmp) hipFree(p);
       return code;
    };
-   if (!wv || !f || !sbuf || !rbuf) return fail(amg_set_error(AMG_ERR_OOM, "amg_dist_async_jacobi: workspace"));
+   if (!wv || !f || !sbuf || !rbuf || !dacc) return fail(amg_set_error(AMG_ERR_OOM, "amg_dist_async_jacobi: workspace"));
    if ((st = h2d(s, f, f_local, (size_t)n * sizeof(double))) != AMG_OK) return fail(st);
    const int nb = std::max(1, std::min(65536, (n + 255) / 256));
-   ajac_weights_k<<<nb, 256, 0, s>>>(M.A->diag, l1 ? v.l1 : nullptr, D->o.smooth_weight, wv, n);
+   ajac_scale_k<<<nb, 256, 0, s>>>(M.A->diag, l1 ? v.l1 : nullptr, D->o.smooth_weight, wv, n);
    amgk::vset(s, x, 0.0, 0, v.cap);
    amgk::vcopy(s, f, r, 0, n); // x = 0: r = b
    amgk::vset(s, eext, 0.0, 0, v.cap);
@@ -409,7 +451,9 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
       }
       if (st != AMG_OK) break;
       AMG_HIP(hipStreamWaitEvent(s, sent[q], 0));
-      ajac_update_k<<<nb, 256, 0, s>>>(r, wv, eext, x, n);
+      double om1 = 0.0, omd = 0.0;
+      const int am = !accel ? 0 : !acc.next(D->o, &om1, &omd) ? 1 : D->o.cheby_grid == 0 ? 2 : 3;
+      ajac_update_k<<<nb, 256, 0, s>>>(r, wv, eext, x, dacc, n, am, om1, omd);
       if (np > 0) {
          launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * std::max<long long>(1, M.nsend), (int)M.nsend);
          AMG_HIP(hipEventRecord(packed[q], s));

@@ -64,6 +64,22 @@ struct DLevel {
 };
 
 
+// DMEM_ChebyUpdate scalars (DMEM_Setup.cpp:1905-1912, DMEM_Misc.cpp:624-642):
+// c / c_prev of the recurrence and the cycle counter it tests (iter.cycle)
+struct AccelState {
+   double c = 0.0, c_prev = 1.0;
+   int cycle = 0;
+   void reset(const amg_opts &o)
+   {
+      c = o.cheby_mu;
+      c_prev = 1.0;
+      cycle = 0;
+   }
+   // this cycle's update: false on the first cycle (d = u copy), else the
+   // factors om1 = w - 1 and omd = w * delta; advances the cycle counter
+   bool next(const amg_opts &o, double *om1, double *omd);
+};
+
 // per-stream exchange state of the asynchronous additive cycle (one per level)
 struct AsyncLevel {
    hipStream_t s = nullptr;
@@ -74,6 +90,8 @@ struct AsyncLevel {
    double *u_prev = nullptr, *sy = nullptr, *sr = nullptr; // smoother scratch (level k)
    double *uf = nullptr, *uc = nullptr, *rf = nullptr; // AFACx fine / coarse iterates, fine residual
    double *gath = nullptr;                   // allgather staging at the replication level
+   double *d_acc = nullptr;                  // ChebyUpdate d of the cheby_grid level
+   AccelState acc;
 };
 
 // host <-> device copies ordered on stream s and complete on return
@@ -121,6 +139,10 @@ struct amg_dist_hier {
    std::vector<amgd::AsyncLevel> al;
    std::vector<amg_mat *> cA, cP, cR; // replicated levels' operators (level Ld + i)
    std::vector<double *> cl1;         // and their l1 norms
+   // DMEM_Mult with acceleration (accel_type != 0): x (the iterate; lv[0].u
+   // then carries the cycle's correction e) and the ChebyUpdate direction d
+   double *x_acc = nullptr, *d_acc = nullptr;
+   amgd::AccelState acc;
    double prof_ms[5] = {0, 0, 0, 0, 0};
    long long prof_n[5] = {0, 0, 0, 0, 0};
 };
@@ -130,6 +152,9 @@ int dalloc(amg_dist_hier *D, size_t bytes, void **p);
 int dvec(amg_dist_hier *D, size_t n, double **p);
 // InitVectors + initial outer residual r0 = f - A u (u = 0) and its norm
 int dist_solve_begin(amg_dist_hier *D, const double *f_local);
-// r0 = f - A u, ||r0|| into d_hist[slot] (all ranks)
+// r0 = f - A x, ||r0|| into d_hist[slot] (all ranks); x = dist_iterate(D)
 int dist_outer_residual(amg_dist_hier *D, int slot);
+// the level-0 iterate: x_acc for accelerated MULT (DMEM_Mult), else lv[0].u
+bool dist_mult_accel(const amg_dist_hier *D);
+double *dist_iterate(amg_dist_hier *D);
 } // namespace amgd

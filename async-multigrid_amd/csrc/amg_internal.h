@@ -174,6 +174,12 @@ void sym_update(hipStream_t s, const double *diag, const double *l1, double omeg
 // Chebyshev outer update SMEM_Solve.cpp:179-186
 void cheby_update(hipStream_t s, double *u, double *u_outer, double *y_outer, double omega,
                   double delta, int n);
+// DMEM_ChebyUpdate (DMEM_Misc.cpp:612-666) after the first cycle; branch 0 sync
+// (d only), 1 async cheby_grid (d and u), 2 async other grid (u only)
+void dmem_cheby_update(hipStream_t s, double *d, double *u, int n, int branch, double om1, double omd);
+// DMEM_Mult accelerated update: x += e; d = first ? e : om1 d + omd e; x += d
+void dmem_mult_accel(hipStream_t s, double *x, const double *e, double *d, int n, int first, double om1,
+                     double omd);
 // atomic correction: u += e (device-scope fp64 atomics), u_priv = value after the add
 void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n);
 

@@ -1235,6 +1235,52 @@ void cheby_update(hipStream_t s, double *u, double *u_outer, double *y_outer, do
    if (n > 0) cheby_update_k<<<ew_blocks(n), 256, 0, s>>>(u, u_outer, y_outer, omega, delta, n);
 }
 
+// DMEM_Misc.cpp:612-666 DMEM_ChebyUpdate(d, u) after the first cycle:
+//   branch 0 (MULT / sync)      d = (w-1) d + w delta u
+//   branch 1 (async, cheby_grid) d' = (w-1) d + w delta u ; u = (w-1) d + w delta u
+//   branch 2 (async, other grid) u = w delta u
+// om1 = w - 1.0 and omd = w * delta are formed on the host, as the reference's
+// left-to-right `(omega - 1.0) * d + omega * delta * u` rounds them.
+__global__ void dmem_cheby_k(double *__restrict__ d, double *__restrict__ u, int n, int branch,
+                             double om1, double omd)
+{
+   EW_LOOP(i, 0, n)
+   {
+      const double ui = u[i];
+      if (branch == 2) {
+         u[i] = omd * ui;
+      } else {
+         const double dp = d[i];
+         d[i] = om1 * dp + omd * ui;
+         if (branch == 1) u[i] = om1 * dp + omd * ui;
+      }
+   }
+}
+void dmem_cheby_update(hipStream_t s, double *d, double *u, int n, int branch, double om1, double omd)
+{
+   if (n > 0) dmem_cheby_k<<<ew_blocks(n), 256, 0, s>>>(d, u, n, branch, om1, omd);
+}
+
+// DMEM_Mult.cpp:46-55 with acceleration: x += e; ChebyUpdate(d, e) (copy on the
+// first cycle); x += d -- one pass
+__global__ void dmem_mult_accel_k(double *__restrict__ x, const double *__restrict__ e,
+                                  double *__restrict__ d, int n, int first, double om1, double omd)
+{
+   EW_LOOP(i, 0, n)
+   {
+      const double ei = e[i];
+      const double xi = x[i] + 1.0 * ei;
+      const double di = first ? ei : om1 * d[i] + omd * ei;
+      d[i] = di;
+      x[i] = xi + 1.0 * di;
+   }
+}
+void dmem_mult_accel(hipStream_t s, double *x, const double *e, double *d, int n, int first, double om1,
+                     double omd)
+{
+   if (n > 0) dmem_mult_accel_k<<<ew_blocks(n), 256, 0, s>>>(x, e, d, n, first, om1, omd);
+}
+
 // SMEM_Async_AMG.cpp:296-299 (FULL_ASYNC): omp atomic u[i] += e[i]; u_k[i] = u[i]
 __global__ void atomic_correct_k(double *u, const double *__restrict__ e,
                                  double *__restrict__ u_priv, int n)

@@ -61,6 +61,15 @@ typedef struct amg_gen amg_gen;   /* structured 7-pt problem + geometric hierarc
 #define AMG_FULL_ASYNC 0
 #define AMG_SEMI_ASYNC 1
 
+/* DMEM outer acceleration (input.accel_type, DMEM_Misc.cpp:612-666).  The
+ * reference's -cheby and -richard both store 1 (Main.hpp:80-81 define
+ * CHEBY_ACCEL and RICHARD_ACCEL as 1), so its DMEM_ChebyUpdate always runs the
+ * Richardson branch: AMG_RICHARD_ACCEL.  AMG_CHEBY_RECUR_ACCEL selects the
+ * c_k = 2 mu c_{k-1} - c_{k-2} branch (:637-642) the reference CLI cannot reach. */
+#define AMG_NO_ACCEL 0
+#define AMG_RICHARD_ACCEL 1
+#define AMG_CHEBY_RECUR_ACCEL 2
+
 /* Subset of the reference's InputData (Main.hpp:187-234) the hot path reads. */
 typedef struct {
    int solver;                   /* input.solver                                  */
@@ -84,6 +93,11 @@ typedef struct {
                                     (bit-identical; saves one A_0 pass/cycle)  */
    int async_type;               /* AMG_FULL_ASYNC / AMG_SEMI_ASYNC               */
    int profile;                  /* 1: HIP-event timing of the fine-level kernels */
+   int accel_type;               /* DMEM input.accel_type (distributed solves):
+                                    AMG_NO_ACCEL / AMG_RICHARD_ACCEL /
+                                    AMG_CHEBY_RECUR_ACCEL, with cheby_mu/delta */
+   int cheby_grid;               /* DMEM input.cheby_grid: the async additive level
+                                    whose correction carries the d recurrence  */
 } amg_opts;
 
 void amg_opts_default(amg_opts *o); /* SMEM_Main.cpp:65-105 defaults */

@@ -1031,3 +1031,102 @@ void or_cheby_setup(double eig_min, double eig_max, double *mu, double *delta)
    *mu = (eig_max + eig_min) / (eig_max - eig_min);
    *delta = 2.0 / (eig_max + eig_min);
 }
+
+/* ------------------------------------------------------------------------- */
+/* DMEM outer acceleration and drivers                                        */
+/* ------------------------------------------------------------------------- */
+
+/* DMEM_Misc.cpp:612-666 DMEM_ChebyUpdate */
+void or_dmem_cheby_update(double *d, double *u, int n, int cycle, int accel, int branch, double mu,
+                          double delta, double *state)
+{
+   if (cycle == 0) { /* :627-631 DMEM_HypreParVector_Copy(d, u) */
+      memcpy(d, u, (size_t)n * sizeof(double));
+      return;
+   }
+   double omega;
+   if (accel == OR_RICHARD_ACCEL) { /* :634-636 */
+      omega = 2.0 / (1.0 + sqrt(1.0 - pow(mu, -2.0)));
+   } else { /* :637-642 */
+      double c_temp = state[0];
+      state[0] = 2.0 * mu * state[0] - state[1];
+      state[1] = c_temp;
+      omega = 2.0 * mu * state[1] / state[0];
+   }
+   if (branch == OR_CHEBY_SYNC) { /* :645-649 */
+      for (int i = 0; i < n; i++) d[i] = (omega - 1.0) * d[i] + omega * delta * u[i];
+   } else if (branch == OR_CHEBY_GRID) { /* :651-657 */
+      for (int i = 0; i < n; i++) {
+         double d_prev = d[i];
+         d[i] = (omega - 1.0) * d[i] + omega * delta * u[i];
+         u[i] = (omega - 1.0) * d_prev + omega * delta * u[i];
+      }
+   } else { /* :658-662 */
+      for (int i = 0; i < n; i++) u[i] = omega * delta * u[i];
+   }
+}
+
+/* DMEM_Mult.cpp:13-93 */
+int or_dmem_mult_solve(or_hier *H, const double *b, double *x, double *reshist, int accel, double mu,
+                       double delta)
+{
+   const or_opts *o = &H->o;
+   int n0 = H->n[0];
+   if (o->num_cycles <= 0) return 0;
+   init_vectors(H);
+   memcpy(H->f[0], b, (size_t)n0 * sizeof(double));
+   double *r = H->r[0], *e = H->u[0];
+   double *d = dvec(n0);
+   double state[2] = {mu, 1.0};
+   /* ResetNorms, DMEM_Setup.cpp:1455-1461: r = b - A x, r0 = ||r|| */
+   or_smem_spgemv(&H->A[0], x, b, -1.0, 1.0, r, 0, n0);
+   double r0 = or_norm2(r, n0);
+   if (reshist) reshist[0] = r0;
+   int saved = H->precond_flag;
+   H->precond_flag = 1; /* precond_zero_init_guess = 1: the cycle acts on r from e = 0 */
+   int cycle = 0;
+   while (1) {
+      memset(e, 0, (size_t)n0 * sizeof(double)); /* :41 Set(e, 0) */
+      or_vcycle(H);                                 /* :42-45 DMEM_MultCycle(r -> e) */
+      for (int i = 0; i < n0; i++) x[i] += 1.0 * e[i]; /* :46-48 Axpy(x, e, 1) */
+      if (accel != OR_NO_ACCEL) {                   /* :50-55 */
+         or_dmem_cheby_update(d, e, n0, cycle, accel, OR_CHEBY_SYNC, mu, delta, state);
+         for (int i = 0; i < n0; i++) x[i] += 1.0 * d[i];
+      }
+      or_smem_spgemv(&H->A[0], x, b, -1.0, 1.0, r, 0, n0); /* :68-73 */
+      double rn = or_norm2(r, n0);
+      cycle++;
+      if (reshist) reshist[cycle] = rn;
+      if (rn / r0 < o->tol || cycle == o->num_cycles) break; /* :84 */
+   }
+   H->precond_flag = saved;
+   free(d);
+   return cycle;
+}
+
+/* DMEM_Smooth.cpp:16-313, one rank, one grid */
+double or_dmem_async_jacobi(const or_csr *A, const double *b, double *x, int sweeps, double omega,
+                            const double *l1, int accel, double mu, double delta)
+{
+   int n = A->nrows;
+   double *s = dvec(n), *u = dvec(n), *e = dvec(n), *r = dvec(n), *d = dvec(n);
+   double state[2] = {mu, 1.0};
+   for (int i = 0; i < n; i++) {
+      double a = A->data[A->i[i]];
+      s[i] = l1 ? l1[i] : (a == 0 ? 1.0 : a / omega); /* DMEM_Setup.cpp:474-480 */
+      x[i] = 0.0;
+      r[i] = b[i];
+   }
+   for (int k = 0; k < sweeps; k++) {
+      for (int i = 0; i < n; i++) u[i] = 0.0 + r[i] / s[i]; /* :100-106 Set(u, 0); Ivaxpy(u, r, s) */
+      if (accel != OR_NO_ACCEL)                            /* :110-112 */
+         or_dmem_cheby_update(d, u, n, k, accel, OR_CHEBY_GRID, mu, delta, state);
+      for (int i = 0; i < n; i++) e[i] = 0.0 + 1.0 * u[i]; /* :171-183 Set(e, 0); Axpy(e, u, 1) */
+      or_smem_spgemv(A, e, r, -1.0, 1.0, r, 0, n);         /* :218-224 r -= A_diag e */
+      for (int i = 0; i < n; i++) x[i] += 1.0 * e[i];      /* :229 Axpy(x, e, 1) */
+   }
+   or_smem_spgemv(A, x, b, -1.0, 1.0, r, 0, n);
+   double rn = or_norm2(r, n);
+   free(s); free(u); free(e); free(r); free(d);
+   return rn;
+}

@@ -151,6 +151,38 @@ void or_bpx_cycle(or_hier *H);
 /* SMEM_Cheby.cpp:410-518 (EigsPower) with this hierarchy's V-cycle as M^{-1} */
 void or_eigs_power(or_hier *H, int iters, double *eig_max, double *eig_min);
 void or_cheby_setup(double eig_min, double eig_max, double *mu, double *delta);
+/* ---------------- DMEM outer acceleration and drivers ------------------------ */
+/* accel ids: the reference's -cheby and -richard both set accel_type = 1
+ * (Main.hpp:80-81 define CHEBY_ACCEL and RICHARD_ACCEL as 1), so
+ * DMEM_ChebyUpdate always takes its Richardson branch (DMEM_Misc.cpp:634-636);
+ * OR_CHEBY_RECUR_ACCEL selects the c_k recurrence branch (:637-642), unreachable
+ * from the reference CLI. */
+#define OR_NO_ACCEL 0
+#define OR_RICHARD_ACCEL 1
+#define OR_CHEBY_RECUR_ACCEL 2
+/* ChebyUpdate branches: 0 = MULT / sync solver (d only), 1 = async and this
+ * grid is cheby_grid (d and u), 2 = async, another grid (u only) */
+#define OR_CHEBY_SYNC 0
+#define OR_CHEBY_GRID 1
+#define OR_CHEBY_OTHER 2
+/* DMEM_Misc.cpp:612-666 DMEM_ChebyUpdate(d, u) at outer cycle `cycle`;
+ * state[0] = cheby.c, state[1] = cheby.c_prev (start mu, 1: DMEM_Setup.cpp:1909-1910) */
+void or_dmem_cheby_update(double *d, double *u, int n, int cycle, int accel, int branch, double mu,
+                          double delta, double *state);
+/* DMEM_Mult.cpp:13-93 (DMEM_Mult): r = b - A x; per cycle e = 0, e = M r
+ * (this hierarchy's V-cycle in preconditioner mode stands for DMEM_MultCycle),
+ * x += e, [ChebyUpdate(d, e); x += d], r = b - A x, ||r||.  x holds the
+ * initial guess on entry.  reshist[k] = ||r_k||.  Returns the cycles done. */
+int or_dmem_mult_solve(or_hier *H, const double *b, double *x, double *reshist, int accel, double mu,
+                       double delta);
+/* DMEM_Smooth.cpp:16-313 (DMEM_AsyncSmooth, ASYNC_JACOBI / ASYNC_L1_JACOBI) on one
+ * rank and one grid, where nothing is asynchronous: per relaxation u = r ./ s
+ * (s = a_ii/omega, or 1 if a_ii == 0, DMEM_Setup.cpp:474-480; s = l1 for L1),
+ * [ChebyUpdate(d, u), async branch of cheby_grid], e = u, r -= A e, x += e.
+ * x = 0 and r = b on entry.  Returns ||b - A x||. */
+double or_dmem_async_jacobi(const or_csr *A, const double *b, double *x, int sweeps, double omega,
+                            const double *l1, int accel, double mu, double delta);
+
 /* access the hierarchy's level vectors (u, f) for tests */
 double *or_hier_vec(or_hier *H, const char *name, int level);
 int or_hier_levels(or_hier *H);

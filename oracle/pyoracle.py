@@ -68,6 +68,13 @@ def lib():
         L.or_eigs_power.argtypes = [C.c_void_p, C.c_int, _dp, _dp]
         L.or_num_threads.restype = C.c_int
         L.or_last_loop_seconds.restype = C.c_double
+        L.or_dmem_cheby_update.argtypes = [_dp, _dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
+                                           C.c_double, _dp]
+        L.or_dmem_mult_solve.restype = C.c_int
+        L.or_dmem_mult_solve.argtypes = [C.c_void_p, _dp, _dp, _dp, C.c_int, C.c_double, C.c_double]
+        L.or_dmem_async_jacobi.restype = C.c_double
+        L.or_dmem_async_jacobi.argtypes = [C.POINTER(OrCsr), _dp, _dp, C.c_int, C.c_double, _dp,
+                                           C.c_int, C.c_double, C.c_double]
         _LIB = L
     return _LIB
 
@@ -301,6 +308,26 @@ def norm2(x):
     return lib().or_norm2(dptr(x), C.c_int(len(x)))
 
 
+# ---- DMEM outer acceleration (DMEM_Misc.cpp:612-666) ---------------------------
+OR_NO_ACCEL, OR_RICHARD_ACCEL, OR_CHEBY_RECUR_ACCEL = 0, 1, 2
+OR_CHEBY_SYNC, OR_CHEBY_GRID, OR_CHEBY_OTHER = 0, 1, 2
+
+
+def dmem_cheby_update(d, u, cycle, accel, branch, mu, delta, state):
+    """In place on d, u; state = [c, c_prev] (float64 array of 2)."""
+    lib().or_dmem_cheby_update(dptr(d), dptr(u), len(u), cycle, accel, branch, mu, delta, dptr(state))
+
+
+def dmem_async_jacobi(A, b, sweeps, omega, l1=None, accel=0, mu=0.0, delta=0.0):
+    """DMEM_AsyncSmooth on one rank (DMEM_Smooth.cpp:16-313): returns (x, ||b - A x||)."""
+    x = np.zeros(A.nrows)
+    Ac = A.c()
+    l1p = dptr(np.ascontiguousarray(l1, dtype=np.float64)) if l1 is not None else None
+    rn = lib().or_dmem_async_jacobi(C.byref(Ac), dptr(np.ascontiguousarray(b, dtype=np.float64)), dptr(x),
+                                    sweeps, omega, l1p, accel, mu, delta)
+    return x, rn
+
+
 # ---- hierarchy / solve -------------------------------------------------------
 def make_opts(solver=OR_MULT, smoother=OR_JACOBI, num_pre=1, num_post=1, num_fine=1,
               num_coarse=1, smooth_weight=1.0, num_cycles=20, tol=0.0, check_resnorm=1,
@@ -333,6 +360,15 @@ class Hier:
         hist = np.zeros(self.opts.num_cycles + 1)
         k = lib().or_solve(self.h, dptr(np.ascontiguousarray(f)), dptr(u), dptr(hist))
         return u, hist[:k + 1], k
+
+    def dmem_mult_solve(self, b, accel, mu=0.0, delta=0.0, x0=None):
+        """DMEM_Mult (DMEM_Mult.cpp:13-93) with DMEM_ChebyUpdate acceleration."""
+        n0 = self._keep[0][0].nrows
+        x = np.zeros(n0) if x0 is None else np.array(x0, dtype=np.float64)
+        hist = np.zeros(self.opts.num_cycles + 1)
+        k = lib().or_dmem_mult_solve(self.h, dptr(np.ascontiguousarray(b, dtype=np.float64)), dptr(x),
+                                     dptr(hist), accel, mu, delta)
+        return x, hist[:k + 1], k
 
     def eigs_power(self, iters):
         emax, emin = C.c_double(), C.c_double()

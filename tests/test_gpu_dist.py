@@ -381,3 +381,168 @@ def test_dist_async_jacobi(amg, oracle, ctx, nranks, l1):
         assert 0.5 * ref_rel <= res[0][2] <= 2.0 * ref_rel, (res[0][2], ref_rel)
         assert np.all(np.isfinite(x))
     gen.free()
+
+
+# ---------------------------------------------------------------------------
+# DMEM outer acceleration (DMEM_ChebyUpdate, DMEM_Misc.cpp:612-666)
+# ---------------------------------------------------------------------------
+def cheby_scalars(alpha, beta):
+    """DMEM_Setup.cpp:1905-1908: mu = (b + a) / (b - a), delta = 2 / (b + a)."""
+    return (beta + alpha) / (beta - alpha), 2.0 / (beta + alpha)
+
+
+@pytest.mark.parametrize("accel,nranks,rep,extra", [
+    ("richard", 1, 1 << 18, {}),
+    ("richard", 2, 0, {}),
+    ("recur", 3, 512, {}),
+    ("recur", 2, 0, {"smoother": "l1", "num_pre_smooth_sweeps": 2}),
+])
+def test_dist_mult_accel_matches_oracle(amg, oracle, accel, nranks, rep, extra):
+    """DMEM_Mult with -cheby / -richard: per cycle e = M r from zero, x += e,
+    ChebyUpdate(d, e), x += d.  The slab-distributed iterate is BIT-IDENTICAL
+    to the oracle's restatement (or_dmem_mult_solve), norms within 1e-12.
+    The reference adds both e and d (DMEM_Mult.cpp:46-55), so the update is
+    about twice the preconditioned correction: the eigenvalue bounds given
+    here (0.5, 4) are wider than M^-1 A's (about 0.48, 0.99) to keep it
+    convergent, as a user of the reference would have to."""
+    from test_gpu_solve import hierarchy, oracle_opts
+    kw = dict(extra)
+    if kw.pop("smoother", None) == "l1":
+        kw["smoother"] = amg.AMG_L1_JACOBI
+    mu, delta = cheby_scalars(0.5, 4.0)
+    acc = amg.AMG_RICHARD_ACCEL if accel == "richard" else amg.AMG_CHEBY_RECUR_ACCEL
+    cycles = 8
+    opts = amg.default_opts(num_cycles=cycles, tol=0.0, smooth_weight=0.8, accel_type=acc,
+                            cheby_mu=mu, cheby_delta=delta, reuse_outer_residual=1, **kw)
+    gen, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
+    f = amg.rhs_rand(0, 24 ** 3)
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    acc_o = oracle.OR_RICHARD_ACCEL if accel == "richard" else oracle.OR_CHEBY_RECUR_ACCEL
+    x_o, h_o, k = OH.dmem_mult_solve(f, acc_o, mu, delta)
+    assert k == cycles
+    xd, hd = distributed(amg, gen, opts, f, cycles, nranks, rep)
+    assert_bitwise(xd, x_o, "accelerated DMEM_Mult iterate")
+    np.testing.assert_allclose(hd, h_o, rtol=1e-12, atol=0)
+    # with these bounds the unaccelerated DMEM_Mult converges slower
+    _, h_plain, _ = OH.dmem_mult_solve(f, oracle.OR_NO_ACCEL)
+    assert h_o[-1] < h_plain[-1]
+    gen.free()
+
+
+@pytest.mark.parametrize("nranks,l1,accel,grid", [(1, 0, "richard", 0), (1, 1, "recur", 0),
+                                                   (1, 0, "recur", 1), (2, 0, "richard", 0),
+                                                   (3, 1, "recur", 0)])
+def test_dist_async_jacobi_accel(amg, oracle, ctx, nranks, l1, accel, grid):
+    """DMEM_AsyncSmooth with ChebyUpdate on the relaxation (async branch; the
+    fine grid is grid 0, so cheby_grid 0 carries d and any other value scales
+    u by w*delta).  One rank has nothing asynchronous: BIT-IDENTICAL to the
+    oracle (or_dmem_async_jacobi).  More ranks apply late ghost deltas one
+    relaxation later: a band around the one-rank result."""
+    n = 20
+    gen = amg.Gen(n)
+    f = amg.rhs_rand(0, n ** 3)
+    K, w = 25, 0.7
+    mu, delta = cheby_scalars(0.1 * w, 2.0 * w)
+    acc = amg.AMG_RICHARD_ACCEL if accel == "richard" else amg.AMG_CHEBY_RECUR_ACCEL
+    nr, nc, rp, cj, cv = gen.host_csr(amg.AMG_GEN_A, 0)
+    A = oracle.Csr(nr, nc, rp, cj, cv)
+    l1n = oracle.l1_norms(A) if l1 else None
+    acc_o = oracle.OR_RICHARD_ACCEL if accel == "richard" else oracle.OR_CHEBY_RECUR_ACCEL
+    if grid == 0:
+        x_o, rn_o = oracle.dmem_async_jacobi(A, f, K, w, l1n, acc_o, mu, delta)
+    else:  # cheby_grid != 0: u = w*delta*u after the first relaxation
+        x_o, rn_o = None, None
+    x_plain, rn_plain = oracle.dmem_async_jacobi(A, f, K, w, l1n)
+    fn = np.linalg.norm(f)
+    opts = amg.default_opts(smooth_weight=w, accel_type=acc, cheby_mu=mu, cheby_delta=delta,
+                            cheby_grid=grid)
+    hub = amg.dist.ThreadMailbox(nranks)
+
+    def rank(q):
+        c = amg.Context(0, nstreams=2)
+        if nranks == 1:
+            amg.dist.init_rccl(c, 1, 0, lambda b: b)
+        else:
+            amg.dist.init_host(c, nranks, q, amg.dist.HostTransport(hub, q))
+        D = amg.dist.DistHier(c, gen, opts)
+        rel = D.async_jacobi(f[D.row0:D.row0 + D.n0], K, l1)
+        x = D.get_u()
+        row0 = D.row0
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        return row0, x, rel
+
+    res = sorted(run_ranks(nranks, rank), key=lambda t: t[0])
+    x = np.concatenate([t[1] for t in res])
+    rel = res[0][2]
+    assert all(t[2] == rel for t in res)
+    assert np.all(np.isfinite(x))
+    if x_o is not None and nranks == 1:
+        assert_bitwise(x, x_o, "accelerated async Jacobi (one rank)")
+        np.testing.assert_allclose(rel, rn_o / fn, rtol=1e-12)
+    elif x_o is not None:
+        assert 0.5 * rn_o / fn <= rel <= 2.0 * rn_o / fn, (rel, rn_o / fn)
+    if grid == 0:
+        assert rel < rn_plain / fn  # the momentum helps on the Laplacian
+    gen.free()
+
+
+@pytest.mark.parametrize("solver,accel,cuts,grid,bounds", [
+    ("multadd", "richard", (0.5,), 0, (0.5, 4.0)),
+    ("afacx", "recur", (0.4,), 1, (0.2, 2.0)),
+    ("afacx", "richard", (), 0, (0.2, 2.0)),
+])
+def test_dist_async_additive_accel(amg, oracle, solver, accel, cuts, grid, bounds):
+    """Asynchronous additive AMG with ChebyUpdate on every level's fine
+    correction (DMEM_Add.cpp:319-324): the cheby_grid level carries d, the
+    others scale by w*delta.  Nondeterministic: it must converge and stay in a
+    band around the same solve without acceleration.  (Measured on one MI355X,
+    24^3, 15 corrections: AFACx gains ~10x with bounds (0.2, 2); MULTADD, whose
+    plain run already reaches ~5e-6, loses ~4x with (0.5, 4) --
+    tools/probe_accel.py.)"""
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
+    w = 0.8
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs_ = oracle.smooth_transfer(host["A"][lev], host["P"][lev], w)
+        Ps.append(ps)
+        Rs.append(rs_)
+    host = {"A": host["A"], "P": Ps, "R": Rs}
+    N = 15
+    f = amg.rhs_rand(0, 24 ** 3)
+    mu, delta = cheby_scalars(*bounds)
+    acc = amg.AMG_RICHARD_ACCEL if accel == "richard" else amg.AMG_CHEBY_RECUR_ACCEL
+    a_solver = amg.AMG_ASYNC_MULTADD if solver == "multadd" else amg.AMG_ASYNC_AFACX
+    rs, parts = split_host(host, cuts)
+    nranks = len(cuts) + 1
+
+    def solve(accel_type):
+        opts = amg.default_opts(solver=a_solver, smooth_weight=w, num_cycles=N, tol=0.0,
+                                accel_type=accel_type, cheby_mu=mu, cheby_delta=delta, cheby_grid=grid)
+        hub = amg.dist.ThreadMailbox(nranks)
+
+        def rank(r):
+            c = amg.Context(0, nstreams=L)
+            if nranks == 1:
+                amg.dist.init_rccl(c, 1, 0, lambda b: b)
+            else:
+                amg.dist.init_host(c, nranks, r, amg.dist.HostTransport(hub, r))
+            A, P, R = parts[r]
+            D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
+            rel, _ = D.async_solve(f[D.row0:D.row0 + D.n0])
+            u = D.get_u()
+            D.free()
+            amg.dist.finalize(c)
+            c.close()
+            return rel, u
+
+        res = run_ranks(nranks, rank)
+        assert all(t[0] == res[0][0] for t in res)
+        assert all(np.all(np.isfinite(t[1])) for t in res)
+        return res[0][0]
+
+    rel_acc, rel_plain = solve(acc), solve(amg.AMG_NO_ACCEL)
+    assert rel_acc < 1.0
+    assert rel_plain / 50 <= rel_acc <= rel_plain * 50, (rel_acc, rel_plain)

@@ -107,3 +107,48 @@ def test_rhs_is_glibc_sequence(oracle):
     libc.srand(0)
     ref = [-1 + 2 * (libc.rand() / 2147483647) for _ in range(10)]
     np.testing.assert_array_equal(oracle.rhs_rand(10), ref)
+
+
+def test_dmem_cheby_update(oracle):
+    """DMEM_Misc.cpp:612-666: first cycle copies u into d; later cycles use the
+    Richardson omega (the only branch the reference CLI reaches, since
+    CHEBY_ACCEL == RICHARD_ACCEL == 1) or the c_k recurrence, on the sync
+    (d only), cheby_grid (d and u) or other-grid (u only) branch."""
+    g = np.random.default_rng(3)
+    n, mu, delta = 257, 1.7, 0.6
+    u0, d0 = g.uniform(-1, 1, n), g.uniform(-1, 1, n)
+    for accel in (oracle.OR_RICHARD_ACCEL, oracle.OR_CHEBY_RECUR_ACCEL):
+        for branch in (oracle.OR_CHEBY_SYNC, oracle.OR_CHEBY_GRID, oracle.OR_CHEBY_OTHER):
+            d, u, st = d0.copy(), u0.copy(), np.array([mu, 1.0])
+            oracle.dmem_cheby_update(d, u, 0, accel, branch, mu, delta, st)
+            assert np.array_equal(d, u0) and np.array_equal(u, u0)
+            c, cp = mu, 1.0
+            d, u = d0.copy(), u0.copy()
+            for cyc in (1, 2, 3):
+                if accel == oracle.OR_RICHARD_ACCEL:
+                    w = 2.0 / (1.0 + np.sqrt(1.0 - mu ** -2.0))
+                else:
+                    c, cp = 2.0 * mu * c - cp, c
+                    w = 2.0 * mu * cp / c
+                dn = (w - 1.0) * d + w * delta * u
+                un = {oracle.OR_CHEBY_SYNC: u, oracle.OR_CHEBY_GRID: (w - 1.0) * d + w * delta * u,
+                      oracle.OR_CHEBY_OTHER: w * delta * u}[branch]
+                if branch == oracle.OR_CHEBY_OTHER:
+                    dn = d
+                oracle.dmem_cheby_update(d, u, cyc, accel, branch, mu, delta, st)
+                assert np.array_equal(d, dn) and np.array_equal(u, un)
+                d, u = dn.copy(), un.copy()
+
+
+def test_dmem_async_jacobi_one_rank(oracle):
+    """DMEM_AsyncSmooth on one rank without acceleration is weighted Jacobi in
+    residual form: same iterate as the SMEM sweep up to rounding."""
+    A = oracle.laplace_7pt(9)
+    b = oracle.rhs_rand(A.nrows)
+    x, rn = oracle.dmem_async_jacobi(A, b, 12, 0.7)
+    u = np.zeros(A.nrows)
+    for _ in range(12):
+        oracle.smem_jacobi(A, b, u, np.zeros(A.nrows), 0.7, 1, 0)
+    np.testing.assert_allclose(x, u, rtol=1e-10, atol=1e-13)
+    r = b - A.to_scipy() @ x
+    np.testing.assert_allclose(rn, np.linalg.norm(r), rtol=1e-10)
