@@ -546,6 +546,46 @@ extern "C" int amg_dev_calib(amg_ctx *c, int mode, long long bytes)
    hipFree(buf);
    return AMG_OK;
 }
+// development entry (bench.py): best-of-reps STREAM triad rate over three
+// fresh arrays of n doubles, GB/s of 24 n bytes per pass
+extern "C" int amg_dev_stream_triad(amg_ctx *c, long long n, int reps, double *gbs)
+{
+   AMG_ARG(c && n >= 2 && reps >= 1 && gbs, "amg_dev_stream_triad: bad argument");
+   n &= ~1LL;
+   double *a = nullptr, *b = nullptr, *d = nullptr;
+   AMG_HIP(hipMalloc(&a, (size_t)n * 8));
+   if (hipMalloc(&b, (size_t)n * 8) != hipSuccess || hipMalloc(&d, (size_t)n * 8) != hipSuccess) {
+      hipFree(a);
+      hipFree(b);
+      return amg_set_error(AMG_ERR_OOM, "amg_dev_stream_triad: %lld doubles", n);
+   }
+   hipEvent_t e0, e1;
+   hipEventCreate(&e0);
+   hipEventCreate(&e1);
+   hipMemsetAsync(b, 0, (size_t)n * 8, c->stream);
+   hipMemsetAsync(d, 0, (size_t)n * 8, c->stream);
+   amgk::stream_triad(c->stream, a, b, d, 3.0, n); // warm
+   float best = 1e30f;
+   for (int r = 0; r < reps; r++) {
+      hipEventRecord(e0, c->stream);
+      amgk::stream_triad(c->stream, a, b, d, 3.0, n);
+      hipEventRecord(e1, c->stream);
+      hipEventSynchronize(e1);
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, e0, e1);
+      best = std::min(best, ms);
+   }
+   const hipError_t err = hipGetLastError();
+   hipEventDestroy(e0);
+   hipEventDestroy(e1);
+   hipFree(a);
+   hipFree(b);
+   hipFree(d);
+   AMG_HIP(err);
+   *gbs = 24.0 * (double)n / (best * 1e-3) / 1e9;
+   return AMG_OK;
+}
+
 extern "C" const char *amg_dev_tune_name(int v) { return amgk::tune_variant_name(v); }
 
 extern "C" int amg_dev_tune_spmv(amg_ctx *c, const amg_mat *A, const amg_vec *x, amg_vec *y,

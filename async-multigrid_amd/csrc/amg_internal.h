@@ -183,6 +183,8 @@ void dmem_mult_accel(hipStream_t s, double *x, const double *e, double *d, int n
 // atomic correction: u += e (device-scope fp64 atomics), u_priv = value after the add
 void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n);
 
+// STREAM triad a = b + q c over n doubles (n even)
+void stream_triad(hipStream_t s, double *a, const double *b, const double *c, double q, long long n);
 // PMC calibration streams: mode 0/1/2/3 = read bytes with 16/8/4/1-byte lanes, 4 = 8-byte writes
 void calib_stream(hipStream_t s, int mode, void *buf, long long bytes, double *out);
 

@@ -840,6 +840,29 @@ __global__ __launch_bounds__(256) void calib_write8_k(double *__restrict__ buf, 
       buf[i] = (double)i;
 }
 
+// STREAM triad a = b + q c on 16-byte lanes, one double2 per thread (the
+// practical HBM ceiling bench.py reports beside the 8 TB/s peak)
+__global__ __launch_bounds__(256) void triad_k(v2d *__restrict__ a, const v2d *__restrict__ b,
+                                               const v2d *__restrict__ c, double q, long long n2)
+{
+   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+   if (i < n2) {
+      const v2d x = b[i], y = c[i];
+      v2d r;
+      r.x = x.x + q * y.x;
+      r.y = x.y + q * y.y;
+      a[i] = r;
+   }
+}
+void stream_triad(hipStream_t s, double *a, const double *b, const double *c, double q, long long n)
+{
+   const long long n2 = n / 2;
+   const long long nb = (n2 + 255) / 256;
+   if (nb > 0)
+      triad_k<<<(unsigned)nb, 256, 0, s>>>(reinterpret_cast<v2d *>(a), reinterpret_cast<const v2d *>(b),
+                                          reinterpret_cast<const v2d *>(c), q, n2);
+}
+
 void calib_stream(hipStream_t s, int mode, void *buf, long long bytes, double *out)
 {
    const int nb = 8192;

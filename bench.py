@@ -147,6 +147,13 @@ def main():
     spmv_bytes = bpe * z0 + 20 * n0 + 4
     spmv_gbs = spmv_bytes / (spmv_ms.value * 1e-3) / 1e9
     csr_bytes = 12 * z0 + 20 * n0 + 4  # the reference's CSR format
+    # SURVEY.md Sec.8(d) gate: fine SpMV at >= 0.60 of 8 TB/s on the CSR byte count
+    gate_ms = csr_bytes / (0.60 * HBM_PEAK_GBS * 1e9) * 1e3
+    # practical ceiling: STREAM triad over three 2 GiB arrays on the same device
+    triad = C.c_double()
+    amg.lib.amg_dev_stream_triad.argtypes = [C.c_void_p, C.c_longlong, C.c_int, C.POINTER(C.c_double)]
+    amg.check(amg.lib.amg_dev_stream_triad(ctx.h, 1 << 28, 10, C.byref(triad)))
+    log(f"[gpu] STREAM triad {triad.value:.0f} GB/s")
     log(f"[gpu] fine residual {res_ms:.3f} ms ({achieved:.0f} GB/s), fine SpMV {spmv_ms.value:.3f} ms "
         f"({spmv_gbs:.0f} GB/s); smoother {ms[1] / max(launches[1], 1):.3f} ms, "
         f"R0 {ms[2] / max(launches[2], 1):.3f} ms, P0 {ms[3] / max(launches[3], 1):.3f} ms")
@@ -184,11 +191,14 @@ def main():
                    "matrix_format": fmt, "parallelism": "single GPU"},
         "fine_spmv": {"gbs": spmv_gbs, "ms": spmv_ms.value, "bytes": spmv_bytes,
                       "frac": spmv_gbs / HBM_PEAK_GBS, "format": fmt,
-                      "csr_equivalent_gbs": csr_bytes / (spmv_ms.value * 1e-3) / 1e9},
+                      "csr_equivalent_gbs": csr_bytes / (spmv_ms.value * 1e-3) / 1e9,
+                      "gate_ms": gate_ms, "meets_gate": spmv_ms.value <= gate_ms},
+        "stream_triad_gbs": triad.value,
         "roofline": {"bound": "hbm", "kernel": f"fine-grid residual SpGEMV r = f - A0 u ({fmt})",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(n, fmt),
-                     "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms},
+                     "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms,
+                     "frac_of_stream_triad": achieved / triad.value},
         "cpu_baseline": cpu,
         "final_relres": rn / r0,
     }
