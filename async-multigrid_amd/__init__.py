@@ -73,6 +73,10 @@ class Context:
         """Dictionary-coded CSR for square operators registered from now on (default on)."""
         check(lib.amg_set_dict_index(self.h, int(enable)))
 
+    def set_row_pattern(self, enable):
+        """Row-pattern-coded CSR on top of the dictionary (default on)."""
+        check(lib.amg_set_row_pattern(self.h, int(enable)))
+
     def csr(self, nrows, ncols, rowptr, col, val, diag_first=1):
         return Mat.register(self, nrows, ncols, rowptr, col, val, diag_first)
 
@@ -100,6 +104,7 @@ class Mat:
         self.nrows, self.ncols, self.nnz = nr.value, nc.value, nz.value
         self.value_index = lib.amg_mat_value_index(handle)  # table size, 0 = plain CSR
         self.dict_index = lib.amg_mat_dict_index(handle)    # dictionary size, 0 = not coded
+        self.row_pattern = lib.amg_mat_row_pattern(handle)  # distinct row patterns, 0 = not coded
 
     @classmethod
     def register(cls, ctx, nrows, ncols, rowptr, col, val, diag_first=1):

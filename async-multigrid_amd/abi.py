@@ -59,6 +59,8 @@ PROTOTYPES = {
     "amg_mat_value_index": (_i, [_p]),
     "amg_set_dict_index": (_i, [_p, _i]),
     "amg_mat_dict_index": (_i, [_p]),
+    "amg_set_row_pattern": (_i, [_p, _i]),
+    "amg_mat_row_pattern": (_i, [_p]),
     "amg_mat_info": (_i, [_p, _ip, _ip, _llp]),
     "amg_mat_download": (_i, [_p, _p, _ip, _ip, _dp]),
     "amg_vec_create": (_i, [_p, _i, _pp]),
@@ -117,7 +119,7 @@ PROTOTYPES = {
     "amg_dist_barrier": (_i, [_p]),
     "amg_dist_hier_create_structured": (_i, [_p, _p, C.POINTER(AmgOpts), _pp]),
     "amg_dist_hier_local_rows": (_i, [_p, _i, _ip, _ip]),
-    "amg_dist_hier_matrix_info": (_i, [_p, _i, _llp, _ip, _ip]),
+    "amg_dist_hier_matrix_info": (_i, [_p, _i, _llp, _ip, _ip, _ip]),
     "amg_dist_solve_start": (_i, [_p, _dp, _dp]),
     "amg_dist_solve_iterate": (_i, [_p, _i]),
     "amg_dist_solve_resnorm": (_i, [_p, _dp]),

@@ -74,6 +74,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
    if (const char *v = std::getenv("AMG_VALUE_INDEX")) c->value_index = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_DICT_INDEX")) c->dict_index = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_ROW_PATTERN")) c->row_pattern = std::atoi(v) != 0;
    *out = c;
    return AMG_OK;
 }
@@ -265,13 +266,93 @@ static int build_dict_index(amg_mat *A)
    return AMG_OK;
 }
 
+// row-pattern-coded CSR: when every row is non-empty and the rows' dictionary
+// sequences take at most 256 distinct values, one byte per row names the
+// sequence.  Lossless: the kernels walk the same entries in
+// the same order.
+static int build_row_pattern(amg_mat *A)
+{
+   amg_ctx *c = A->ctx;
+   hipStream_t s = c->stream;
+   constexpr int NS = 4096;
+   unsigned long long *slots = nullptr;
+   AMG_HIP(hipMalloc(&slots, NS * sizeof(unsigned long long) + NS * sizeof(int) + 64));
+   int *rep = reinterpret_cast<int *>(slots + NS);
+   int *count = rep + NS;
+   AMG_HIP(hipMemsetAsync(slots, 0xff, NS * sizeof(unsigned long long), s));
+   AMG_HIP(hipMemsetAsync(count, 0, 2 * sizeof(int), s));
+   amgk::rp_collect(s, A, slots, rep, NS, count, count + 1);
+   std::vector<unsigned long long> h(NS);
+   std::vector<int> hr(NS);
+   int cb[2] = {0, 0}; // distinct row sequences, rows that cannot be coded
+   AMG_HIP(hipMemcpyAsync(h.data(), slots, NS * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(hr.data(), rep, NS * sizeof(int), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(cb, count, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   if (cb[0] < 1 || cb[0] > 256 || cb[1] != 0) {
+      hipFree(slots);
+      return AMG_OK;
+   }
+   std::vector<std::pair<unsigned long long, int>> kr;
+   for (int i = 0; i < NS; i++)
+      if (h[i] != ~0ULL) kr.push_back({h[i], hr[i]});
+   std::sort(kr.begin(), kr.end());
+   const int T = (int)kr.size();
+   std::vector<unsigned long long> keys(T);
+   std::vector<int> reps(T);
+   for (int t = 0; t < T; t++) {
+      keys[t] = kr[t].first;
+      reps[t] = kr[t].second;
+   }
+   hipError_t e = hipMalloc(&A->rpat, std::max(1, A->nrows));
+   if (e == hipSuccess) e = hipMalloc(&A->ptab, 256 * AMG_RP_STRIDE);
+   if (e != hipSuccess) {
+      hipFree(A->rpat);
+      hipFree(A->ptab);
+      A->rpat = A->ptab = nullptr;
+      hipFree(slots);
+      (void)hipGetLastError();
+      return AMG_OK;
+   }
+   AMG_HIP(hipMemsetAsync(A->ptab, 0, 256 * AMG_RP_STRIDE, s));
+   AMG_HIP(hipMemcpyAsync(slots, keys.data(), T * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemcpyAsync(rep, reps.data(), T * sizeof(int), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemsetAsync(count + 1, 0, sizeof(int), s));
+   amgk::rp_table(s, A, rep, T, A->ptab);
+   amgk::rp_encode(s, A, slots, T, A->ptab, A->rpat, count + 1);
+   AMG_HIP(hipMemcpyAsync(cb, count, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   hipFree(slots);
+   if (cb[1] != 0) { // a hash collision: keep the dictionary-coded form
+      hipFree(A->rpat);
+      hipFree(A->ptab);
+      A->rpat = A->ptab = nullptr;
+      return AMG_OK;
+   }
+   A->rp_n = T;
+   return AMG_OK;
+}
+
 int amg_mat_finish(amg_mat *A)
 {
    amgk::extract_diag(A->ctx->stream, A);
    AMG_HIP(hipGetLastError());
    if (A->ctx->value_index && A->nnz > 0) AMG_TRY(build_value_index(A));
    if (A->ctx->dict_index && A->vidx) AMG_TRY(build_dict_index(A));
+   if (A->ctx->row_pattern && A->didx) AMG_TRY(build_row_pattern(A));
    return AMG_OK;
+}
+
+extern "C" int amg_set_row_pattern(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_row_pattern: null context");
+   c->row_pattern = enable ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_row_pattern(const amg_mat *A)
+{
+   return A ? A->rp_n : 0;
 }
 
 extern "C" int amg_set_dict_index(amg_ctx *c, int enable)
@@ -342,6 +423,8 @@ extern "C" int amg_mat_free(amg_mat *A)
    hipFree(A->doff);
    hipFree(A->dval);
    hipFree(A->danch);
+   hipFree(A->rpat);
+   hipFree(A->ptab);
    delete A;
    return AMG_OK;
 }

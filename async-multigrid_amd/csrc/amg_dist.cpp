@@ -863,13 +863,14 @@ extern "C" int amg_dist_hier_free(amg_dist_hier *D)
 }
 
 extern "C" int amg_dist_hier_matrix_info(amg_dist_hier *D, int level, long long *nnz, int *value_index,
-                                         int *dict_index)
+                                         int *dict_index, int *row_pattern)
 {
    AMG_ARG(D && level >= 0 && level < D->L, "amg_dist_hier_matrix_info: bad level");
    const amg_mat *A = level < D->Ld ? D->lv[level].A.A : D->cA[level - D->Ld];
    if (nnz) *nnz = A->nnz;
    if (value_index) *value_index = A->vi_n;
    if (dict_index) *dict_index = A->dc_n;
+   if (row_pattern) *row_pattern = A->rp_n;
    return AMG_OK;
 }
 

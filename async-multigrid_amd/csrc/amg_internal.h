@@ -43,6 +43,8 @@ constexpr int AMG_CHUNK = 2048;
 constexpr int AMG_NNZ_PAD = 8;
 // longest row the dictionary-coded kernel stages in LDS
 constexpr int AMG_DC_MAXROW = 32;
+// bytes per row pattern of the row-pattern-coded form: length + entries (x4 aligned)
+constexpr int AMG_RP_STRIDE = 36;
 
 struct amg_transport; // amg_dist.cpp: RCCL communicator or host-callback test transport
 
@@ -60,6 +62,7 @@ struct amg_ctx {
    int num_cus = 256;
    int value_index = 1; // build value-indexed CSR for matrices with <= 256 distinct values
    int dict_index = 1;  // build dictionary-coded CSR for stencil-like square operators
+   int row_pattern = 1; // build row-pattern-coded CSR on top of the dictionary
 };
 
 struct amg_mat {
@@ -69,7 +72,7 @@ struct amg_mat {
    int *rowptr = nullptr;
    int *col = nullptr;
    double *val = nullptr;
-   double *diag = nullptr; // val[rowptr[i]] (the reference's a_ii), or 0 for empty rows
+   double *diag = nullptr; // val[rowptr[i]] (the reference's a_ii; the zero pad after the last row)
    int diag_first = 1;
    amg_mat *trans = nullptr; // lazily built transpose for amg_matvec_t
    // value-indexed form (the hot kernels' format when the matrix has at most
@@ -87,6 +90,12 @@ struct amg_mat {
    int *danch = nullptr;
    int dc_n = 0;
    int dc_maxrow = 0; // longest row (selects the LDS staging size)
+   // row-pattern-coded form (dictionary-coded operators with <= 256 distinct
+   // rows, none empty): rpat[i] names row i's dictionary sequence in ptab
+   // (AMG_RP_STRIDE bytes per pattern: length, then the entries)
+   unsigned char *rpat = nullptr;
+   unsigned char *ptab = nullptr;
+   int rp_n = 0;
 };
 
 struct amg_vec {
@@ -193,6 +202,13 @@ void vi_collect(hipStream_t s, const double *val, long long nnz, unsigned long l
                 int *count);
 void vi_encode(hipStream_t s, const double *val, long long nnz, const unsigned long long *keys, int T,
                unsigned char *vidx);
+
+// row-pattern construction (needs the dictionary index)
+void rp_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int *rep, int nslots, int *count,
+                int *bad);
+void rp_table(hipStream_t s, const amg_mat *A, const int *rep, int T, unsigned char *ptab);
+void rp_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
+               const unsigned char *ptab, unsigned char *rpat, int *bad);
 
 // dictionary-coded CSR construction (needs the value index)
 void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,

@@ -410,14 +410,111 @@ __global__ __launch_bounds__(256) void csr_dc_kernel(
    }
 }
 
+// Row-pattern-coded CSR (on top of the dictionary): every row is one byte
+// naming its sequence of dictionary entries (the pattern table holds <= 256
+// distinct sequences of <= MAXR entries), so the kernel streams one byte per
+// ROW and no row pointer.  Lane owns rows r0 + q*256 + tid; the row's entries
+// are walked in CSR order from the LDS pattern table, exactly as the
+// dictionary-coded kernel walks its staged bytes.  Every row is non-empty.
+template <int NEG, bool NEED_DIAG, class Epi, int RPL>
+__global__ __launch_bounds__(256) void csr_rp_kernel(
+   const unsigned char *__restrict__ rpat, const unsigned char *__restrict__ ptab_g, int np,
+   const int *__restrict__ doff_g, const double *__restrict__ dval_g, const double *__restrict__ x,
+   int rb, int re, Epi epi, double *__restrict__ partials, int T, const int *__restrict__ anch)
+{
+   constexpr int PS = AMG_RP_STRIDE; // bytes per pattern: length, then the entries
+   __shared__ int otab[256];
+   __shared__ double vtab[256];
+   __shared__ __attribute__((aligned(16))) unsigned char ptab[256 * PS];
+   __shared__ double red[4];
+   const int tid = (int)threadIdx.x;
+   const int wg = (int)blockIdx.x;
+   const int r0 = rb + wg * 256 * RPL, r1 = min(r0 + 256 * RPL, re);
+   int pid[RPL], an[RPL];
+   double acc[RPL], pf[RPL];
+#pragma unroll
+   for (int q = 0; q < RPL; q++) {
+      const int row = r0 + q * 256 + tid;
+      pid[q] = 0;
+      an[q] = row;
+      acc[q] = pf[q] = 0.0;
+      if (row < r1) {
+         pid[q] = rpat[row];
+         if (anch) an[q] = anch[row];
+         acc[q] = epi.init(row);
+         pf[q] = epi.pf(row);
+      }
+   }
+   if (tid < T) {
+      otab[tid] = doff_g[tid];
+      vtab[tid] = dval_g[tid];
+   }
+   {
+      const int nw = (np * PS) >> 2;
+      const unsigned int *src = reinterpret_cast<const unsigned int *>(ptab_g);
+      unsigned int *dst = reinterpret_cast<unsigned int *>(ptab);
+      for (int w = tid; w < nw; w += 256) dst[w] = src[w];
+   }
+   __syncthreads();
+   double sq[RPL];
+#pragma unroll
+   for (int q = 0; q < RPL; q++) {
+      const int row = r0 + q * 256 + tid;
+      sq[q] = 0.0;
+      if (row >= r1) continue;
+      const unsigned char *pp = ptab + pid[q] * PS;
+      const int len = pp[0];
+      double dg = 0.0;
+      if (NEED_DIAG) dg = vtab[pp[1]]; // a_ii := A_data[A_i[i]]
+      for (int k = 0; k < len; k += 8) {
+         const int m = len - k;
+         double xv[8], vv[8];
+#pragma unroll
+         for (int j = 0; j < 8; j++) {
+            xv[j] = 0.0;
+            vv[j] = 0.0;
+            if (j < m) {
+               const int bb = pp[1 + k + j];
+               vv[j] = vtab[bb];
+               xv[j] = x[an[q] + otab[bb]];
+            }
+         }
+#pragma unroll
+         for (int j = 0; j < 8; j++)
+            if (j < m) {
+               if (NEG)
+                  acc[q] -= vv[j] * xv[j];
+               else
+                  acc[q] += vv[j] * xv[j];
+            }
+      }
+      const double out = epi.finish(row, acc[q], dg, pf[q]);
+      sq[q] = out * out;
+   }
+   if (partials) {
+#pragma unroll
+      for (int q = 0; q < RPL; q++) {
+         const double sblk = block_sum_256(sq[q], red);
+         if (tid == 0 && r0 + q * 256 < r1) partials[wg * RPL + q] = sblk;
+      }
+   }
+}
+
 // dictionary-coded launches: rows of <= 8 entries (7-pt stencil, interpolation)
 // take four 256-row tiles per workgroup, longer rows (27-pt Galerkin,
-// restriction) two (tools/tune_spmv.py, profiles/r01/tune_spmv.log)
+// restriction) two (tools/tune_spmv.py, profiles/r01/tune_spmv.log); the
+// row-pattern form when the matrix has one
 template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int rb, int re,
                          const Epi &e, double *partials, int tiles)
 {
-   if (A->dc_maxrow <= 8)
+   if (A->rpat && A->dc_maxrow <= 8)
+      csr_rp_kernel<NEG, NEED_DIAG, Epi, 4><<<(tiles + 3) / 4, 256, 0, s>>>(
+         A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
+   else if (A->rpat)
+      csr_rp_kernel<NEG, NEED_DIAG, Epi, 2><<<(tiles + 1) / 2, 256, 0, s>>>(
+         A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
+   else if (A->dc_maxrow <= 8)
       csr_dc_kernel<NEG, NEED_DIAG, Epi, 4, true, 8><<<(tiles + 3) / 4, 256, 0, s>>>(
          A->rowptr, A->didx, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
    else
@@ -726,7 +823,17 @@ __global__ __launch_bounds__(256) void ablation_kernel(const int *__restrict__ r
    if (row < r1) y[row] = acc;
 }
 
-int num_tune_variants() { return 24; }
+int num_tune_variants() { return 28; }
+
+template <int RPL>
+static void launch_rp(hipStream_t s, const amg_mat *A, const double *x, double *y)
+{
+   EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
+   if (!A->rpat) return;
+   const int nt = (A->nrows + 256 * RPL - 1) / (256 * RPL);
+   csr_rp_kernel<0, false, EpiGemv, RPL><<<nt, 256, 0, s>>>(A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x,
+                                                            0, A->nrows, e, nullptr, A->dc_n, A->danch);
+}
 
 template <int RPL, bool STAGE, int MAXR = AMG_DC_MAXROW>
 static void launch_dc(hipStream_t s, const amg_mat *A, const double *x, double *y)
@@ -749,8 +856,9 @@ const char *tune_variant_name(int v)
                                  "vi_gtab",      "vi_persist2048",  "vi_persist4096",
                                  "vi_w8",        "plain_w8",        "vi_w8_nt",     "vi_w8_ch4096",
                                  "dc_rpl1",      "dc_rpl2_m8",      "dc_rpl2",      "dc_rpl4_m8",
-                                 "dc_rpl8_m8"};
-   return (v >= 0 && v < 24) ? names[v] : "?";
+                                 "dc_rpl8_m8",   "rp_rpl1",         "rp_rpl2",      "rp_rpl4",
+                                 "rp_rpl8"};
+   return (v >= 0 && v < 28) ? names[v] : "?";
 }
 
 void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y)
@@ -802,6 +910,10 @@ void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x
    case 21: launch_dc<2, true>(s, A, x, y); break;
    case 22: launch_dc<4, true, 8>(s, A, x, y); break;
    case 23: launch_dc<8, true, 8>(s, A, x, y); break;
+   case 24: launch_rp<1>(s, A, x, y); break;
+   case 25: launch_rp<2>(s, A, x, y); break;
+   case 26: launch_rp<4>(s, A, x, y); break;
+   case 27: launch_rp<8>(s, A, x, y); break;
    default: break;
    }
 }
@@ -1177,7 +1289,9 @@ void a_diag(hipStream_t s, const double *diag, double omega, double *out, int n)
 __global__ void extract_diag_k(const int *__restrict__ rowptr, const double *__restrict__ val,
                                double *__restrict__ diag, int n)
 {
-   EW_LOOP(i, 0, n) diag[i] = (rowptr[i + 1] > rowptr[i]) ? val[rowptr[i]] : 0.0;
+   // a_ii := A_data[A_i[i]] for every row, as the reference reads it: an empty
+   // row sees the next row's first value (the zero padding after the last row)
+   EW_LOOP(i, 0, n) diag[i] = val[rowptr[i]];
 }
 void extract_diag(hipStream_t s, const amg_mat *A)
 {
@@ -1473,6 +1587,124 @@ __global__ void dc_encode_k(const int *__restrict__ rowptr, const int *__restric
          didx[k] = (unsigned char)lo;
       }
    }
+}
+
+// ---- row-pattern construction ------------------------------------------------
+// key of row i's dictionary sequence: exact for <= 7 entries (length byte +
+// the entries), else a 56-bit hash above the length byte (verified after
+// encoding, so a collision only disables the format)
+__device__ __forceinline__ unsigned long long rp_key(const unsigned char *__restrict__ didx, int rs, int len)
+{
+   if (len <= 7) {
+      unsigned long long k = (unsigned long long)len;
+      for (int j = 0; j < len; j++) k |= (unsigned long long)didx[rs + j] << (8 * (j + 1));
+      return k;
+   }
+   unsigned long long h = 0xcbf29ce484222325ULL ^ (unsigned long long)len;
+   for (int j = 0; j < len; j++) h = (h ^ didx[rs + j]) * 0x100000001b3ULL;
+   h ^= h >> 29;
+   h *= 0xbf58476d1ce4e5b9ULL;
+   h ^= h >> 32;
+   return (h << 8) | (unsigned long long)len;
+}
+
+// distinct row keys into slots (first row of each into rep), and the number of
+// rows that cannot be coded (empty or longer than AMG_DC_MAXROW)
+__global__ void rp_collect_k(const int *__restrict__ rowptr, const unsigned char *__restrict__ didx, int n,
+                             unsigned long long *slots, int *rep, int nslots, int *count, int *bad)
+{
+   unsigned long long last = VI_EMPTY;
+   int nbad = 0;
+   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+      const int rs = rowptr[i], len = rowptr[i + 1] - rs;
+      if (len < 1 || len > AMG_DC_MAXROW) {
+         nbad++;
+         continue;
+      }
+      const unsigned long long key = rp_key(didx, rs, len);
+      if (key == last) continue;
+      last = key;
+      unsigned int h = vi_hash(key) & (nslots - 1);
+      for (int probe = 0; probe < nslots; probe++) {
+         const unsigned long long cur = __atomic_load_n(&slots[h], __ATOMIC_RELAXED);
+         if (cur == key) break;
+         if (cur == VI_EMPTY) {
+            const unsigned long long prev = atomicCAS(&slots[h], VI_EMPTY, key);
+            if (prev == VI_EMPTY) {
+               atomicAdd(count, 1);
+               rep[h] = i;
+               break;
+            }
+            if (prev == key) break;
+         }
+         h = (h + 1) & (nslots - 1);
+      }
+   }
+   if (nbad) atomicAdd(bad, nbad);
+}
+
+// pattern table: entry t = [length, dictionary bytes of representative row rep[t]]
+__global__ void rp_table_k(const int *__restrict__ rowptr, const unsigned char *__restrict__ didx,
+                           const int *__restrict__ rep, int T, unsigned char *__restrict__ ptab)
+{
+   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= T) return;
+   const int rs = rowptr[rep[t]], len = rowptr[rep[t] + 1] - rs;
+   unsigned char *pp = ptab + t * AMG_RP_STRIDE;
+   pp[0] = (unsigned char)len;
+   for (int j = 0; j < AMG_DC_MAXROW; j++) pp[1 + j] = j < len ? didx[rs + j] : 0;
+}
+
+// rpat[i] = index of row i's key among the T sorted keys; rows whose bytes
+// differ from their pattern (a hash collision) are counted in bad
+__global__ void rp_encode_k(const int *__restrict__ rowptr, const unsigned char *__restrict__ didx, int n,
+                            const unsigned long long *__restrict__ keys, int T,
+                            const unsigned char *__restrict__ ptab, unsigned char *__restrict__ rpat,
+                            int *bad)
+{
+   __shared__ unsigned long long tk[256];
+   if (threadIdx.x < 256) tk[threadIdx.x] = threadIdx.x < T ? keys[threadIdx.x] : VI_EMPTY;
+   __syncthreads();
+   int nbad = 0;
+   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+      const int rs = rowptr[i], len = rowptr[i + 1] - rs;
+      const unsigned long long key = rp_key(didx, rs, len);
+      int lo = 0, hi = T - 1;
+      while (lo < hi) {
+         const int mid = (lo + hi) >> 1;
+         if (tk[mid] < key)
+            lo = mid + 1;
+         else
+            hi = mid;
+      }
+      rpat[i] = (unsigned char)lo;
+      const unsigned char *pp = ptab + lo * AMG_RP_STRIDE;
+      bool ok = tk[lo] == key && pp[0] == len;
+      for (int j = 0; ok && j < len; j++) ok = pp[1 + j] == didx[rs + j];
+      nbad += !ok;
+   }
+   if (nbad) atomicAdd(bad, nbad);
+}
+
+void rp_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int *rep, int nslots, int *count,
+                int *bad)
+{
+   if (A->nrows <= 0) return;
+   rp_collect_k<<<std::min(8192, (A->nrows + 255) / 256), 256, 0, s>>>(A->rowptr, A->didx, A->nrows, slots,
+                                                                         rep, nslots, count, bad);
+}
+
+void rp_table(hipStream_t s, const amg_mat *A, const int *rep, int T, unsigned char *ptab)
+{
+   if (T > 0) rp_table_k<<<1, 256, 0, s>>>(A->rowptr, A->didx, rep, T, ptab);
+}
+
+void rp_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
+               const unsigned char *ptab, unsigned char *rpat, int *bad)
+{
+   if (A->nrows <= 0) return;
+   rp_encode_k<<<std::min(8192, (A->nrows + 255) / 256), 256, 0, s>>>(A->rowptr, A->didx, A->nrows, keys, T,
+                                                                        ptab, rpat, bad);
 }
 
 void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,

@@ -251,10 +251,12 @@ class DistHier:
         return cls(ctx, None, opts, _handle=h)
 
     def matrix_info(self, level):
-        """(local nnz, value-index table size, dictionary size) of this rank's A_level."""
-        nnz, vi, dc = C.c_longlong(), C.c_int(), C.c_int()
-        check(lib.amg_dist_hier_matrix_info(self.h, level, C.byref(nnz), C.byref(vi), C.byref(dc)))
-        return nnz.value, vi.value, dc.value
+        """(local nnz, value-index table size, dictionary size, row patterns) of
+        this rank's A_level (0 = that form is not used)."""
+        nnz, vi, dc, rp = C.c_longlong(), C.c_int(), C.c_int(), C.c_int()
+        check(lib.amg_dist_hier_matrix_info(self.h, level, C.byref(nnz), C.byref(vi), C.byref(dc),
+                                            C.byref(rp)))
+        return nnz.value, vi.value, dc.value, rp.value
 
     def local_rows(self, level):
         r0, n = C.c_int(), C.c_int()

@@ -44,6 +44,20 @@ def parse():
     return p.parse_args()
 
 
+def storage(nrows, nnz, vi, dc, rp):
+    """(matrix bytes the hot kernels stream per pass, format name), DESIGN.md Sec.4:
+    row-pattern-coded CSR reads one byte per row; dictionary-coded one byte per
+    entry + the row pointer; value-indexed 4 (col) + 1 per entry + the row
+    pointer; CSR 4 (col) + 8 (val) per entry + the row pointer."""
+    if rp:
+        return nrows, f"csr-rp ({rp} row patterns over a {dc}-entry (offset, value) dictionary)"
+    if dc:
+        return nnz + 4 * (nrows + 1), f"csr-dc ({dc}-entry (offset, value) dictionary)"
+    if vi:
+        return 5 * nnz + 4 * (nrows + 1), f"csr-vi ({vi}-entry value table)"
+    return 12 * nnz + 4 * (nrows + 1), "csr"
+
+
 def load_traffic(n, fmt):
     """HBM bytes per launch of the fine residual kernel from the rocprofv3 --pmc
     passes (FETCH_SIZE and WRITE_SIZE, corrected per access width by calibration
@@ -126,25 +140,20 @@ def main():
 
     n0 = As[0].nrows
     z0 = As[0].nnz
-    # bytes per stored entry of the format the kernels stream: 4 (col) + 8 (val)
-    # for CSR, 4 (col) + 1 (value index) for value-indexed CSR, 1 (dictionary
-    # index) for dictionary-coded CSR
-    vi, dc = As[0].value_index, As[0].dict_index
-    bpe = 1 if dc else 5 if vi else 12
-    fmt = (f"csr-dc ({dc}-entry (offset, value) dictionary)" if dc else
-           f"csr-vi ({vi}-entry value table)" if vi else "csr")
-    # dominant kernel: fine-grid residual SpGEMV r = f - A u (bpe z + 28 n + 4 algorithmic bytes)
-    res_bytes = bpe * z0 + 28 * n0 + 4
+    # matrix bytes per pass in the format the kernels stream
+    mat_bytes, fmt = storage(n0, z0, As[0].value_index, As[0].dict_index, As[0].row_pattern)
+    # dominant kernel: fine-grid residual SpGEMV r = f - A u (matrix + f, u, r)
+    res_bytes = mat_bytes + 24 * n0
     res_ms = ms[0] / max(launches[0], 1)
     achieved = res_bytes / (res_ms * 1e-3) / 1e9
-    # fine-grid SpMV y = A x (bpe z + 20 n + 4 bytes), events on the same stream
+    # fine-grid SpMV y = A x (matrix + x + y), events on the same stream
     x = ctx.vec(n0)
     x.set(1.0)
     y = ctx.vec(n0)
     import ctypes as C
     spmv_ms = C.c_double()
     amg.check(amg.lib.amg_matvec_timed(ctx.h, As[0].h, x.h, y.h, args.spmv_reps, C.byref(spmv_ms)))
-    spmv_bytes = bpe * z0 + 20 * n0 + 4
+    spmv_bytes = mat_bytes + 16 * n0
     spmv_gbs = spmv_bytes / (spmv_ms.value * 1e-3) / 1e9
     csr_bytes = 12 * z0 + 20 * n0 + 4  # the reference's CSR format
     # SURVEY.md Sec.8(d) gate: fine SpMV at >= 0.60 of 8 TB/s on the CSR byte count

@@ -27,7 +27,7 @@ def main(args, world, rank):
     import torch
     import torch.distributed as tdist
     from conftest import load_package
-    from bench import METRIC, HBM_PEAK_GBS
+    from bench import METRIC, HBM_PEAK_GBS, storage
 
     local = int(os.environ.get("LOCAL_RANK", rank))
     tdist.init_process_group("gloo", rank=rank, world_size=world)
@@ -46,10 +46,8 @@ def main(args, world, rank):
     opts = amg.default_opts(smooth_weight=args.smooth_weight, num_cycles=1 << 30, tol=0.0,
                             reuse_outer_residual=args.reuse_outer_residual, profile=1)
     D = amg.dist.DistHier(ctx, gen, opts)
-    nnz_local, vi, dc = D.matrix_info(0)
-    bpe = 1 if dc else 5 if vi else 12  # bytes per stored entry (bench.py)
-    fmt = (f"csr-dc ({dc}-entry (offset, value) dictionary)" if dc else
-           f"csr-vi ({vi}-entry value table)" if vi else "csr")
+    nnz_local, vi, dc, rp = D.matrix_info(0)
+    mat_bytes, fmt = storage(D.n0, nnz_local, vi, dc, rp)
     if rank == 0:
         log(f"[dist] {world} ranks, {gen.L} levels, slab {D.n0} rows / {nnz_local} nnz on rank 0; "
             f"setup {time.time() - t0:.1f}s")
@@ -72,9 +70,9 @@ def main(args, world, rank):
     rn = D.resnorm()
     ms, launches = D.profile(reset=True)
     res_ms = ms[0] / max(launches[0], 1)
-    res_bytes = bpe * nnz_local + 28 * D.n0 + 4
+    res_bytes = mat_bytes + 24 * D.n0
     spmv_ms = D.fine_spmv_ms(args.spmv_reps)
-    spmv_bytes = bpe * nnz_local + 20 * D.n0 + 4
+    spmv_bytes = mat_bytes + 16 * D.n0
     # aggregate fine SpMV rate: all ranks' algorithmic bytes over the slowest rank's time
     agg = torch.tensor([float(spmv_bytes), spmv_ms, float(res_bytes), res_ms], dtype=torch.float64)
     parts = [torch.zeros_like(agg) for _ in range(world)]

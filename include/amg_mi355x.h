@@ -128,6 +128,14 @@ int amg_mat_value_index(const amg_mat *A);
 int amg_set_dict_index(amg_ctx *ctx, int enable);
 /* number of dictionary entries of A (0: not dictionary-coded) */
 int amg_mat_dict_index(const amg_mat *A);
+/* row-pattern-coded CSR for matrices registered from now on: 1 (default; env
+ * AMG_ROW_PATTERN=0 turns it off) = when A is dictionary-coded, has no empty row
+ * and at most 256 distinct rows (as sequences of dictionary entries), each row is
+ * stored as one byte naming its sequence and the kernels read no row pointer
+ * (bit-identical results) */
+int amg_set_row_pattern(amg_ctx *ctx, int enable);
+/* number of distinct row patterns of A (0: not row-pattern-coded) */
+int amg_mat_row_pattern(const amg_mat *A);
 int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz);
 int amg_mat_download(amg_ctx *ctx, const amg_mat *A, int *rowptr, int *col, double *val);
 
@@ -315,9 +323,9 @@ int amg_dist_structured_row_starts(const amg_gen *gen, int nranks, long long *ro
 int amg_dist_hier_set_replicate_rows(amg_ctx *ctx, long long rows);
 int amg_dist_hier_free(amg_dist_hier *D);
 /* this rank's operator of a level: stored entries and storage format (value-index
- * table size, dictionary size; 0 = not used) */
+ * table size, dictionary size, row patterns; 0 = not used) */
 int amg_dist_hier_matrix_info(amg_dist_hier *D, int level, long long *nnz, int *value_index,
-                              int *dict_index);
+                              int *dict_index, int *row_pattern);
 /* rows [row0, row0 + nrows) of the global level-0 vector this rank owns */
 int amg_dist_hier_local_rows(amg_dist_hier *D, int level, int *row0, int *nrows);
 /* SMEM_Solve on the distributed hierarchy: f/u are this rank's level-0 rows */

@@ -36,6 +36,15 @@ def matrices(oracle, amg):
     out = {}
     out["lap16"] = oracle.laplace_7pt(16)
     out["lap_rect"] = oracle.laplace_7pt(13, 7, 5)
+    # 7-pt Laplacian with an empty row: dictionary-coded, but not row-pattern
+    # coded (a_ii of an empty row is the next row's first value, as in CSR)
+    L = oracle.laplace_7pt(12)
+    keep = np.ones(L.col.size, bool)
+    keep[L.rowptr[300]:L.rowptr[301]] = False
+    cnt = np.diff(L.rowptr)
+    cnt[300] = 0
+    out["lap_hole"] = oracle.Csr(L.nrows, L.ncols, np.concatenate([[0], np.cumsum(cnt)]),
+                                 L.col[keep], L.val[keep])
     g = amg.Gen(24, interp=amg.AMG_INTERP_LINEAR)
     for which, name in ((amg.AMG_GEN_A, "A"), (amg.AMG_GEN_P, "P"), (amg.AMG_GEN_R, "R")):
         for lev in (0, 1) if which != amg.AMG_GEN_A else (1, 2):
@@ -80,7 +89,7 @@ def mats(oracle, amg, ctx):
     return host, dev
 
 
-SQUARE = ["lap16", "A1", "A2", "rand_sq", "longrows", "rand_q", "longrows_q", "rand_q257"]
+SQUARE = ["lap16", "A1", "A2", "rand_sq", "longrows", "rand_q", "longrows_q", "rand_q257", "lap_hole"]
 ALL = SQUARE + ["lap_rect", "P0", "P1", "R0", "R1", "rand_rect"]
 
 
@@ -105,12 +114,28 @@ def test_value_index_selection(mats):
     assert dev["P0"].dict_index == 20 and dev["R0"].dict_index == 27
     for name in ("rand_sq", "rand_q", "rand_q257", "longrows_q", "rand_rect"):
         assert dev[name].dict_index == 0, name
+    # row-pattern-coded: dictionary-coded, no empty row, <= 256 distinct rows
+    # (a row = its sequence of (column - first column, value) pairs)
+    for name in ALL:
+        A = host[name]
+        pats = set()
+        for i in range(A.nrows):
+            c = A.col[A.rowptr[i]:A.rowptr[i + 1]].astype(np.int64)
+            v = A.val[A.rowptr[i]:A.rowptr[i + 1]].view(np.int64)
+            pats.add(tuple((c - c[0]).tolist()) + tuple(v.tolist()) if c.size else ())
+        ok = dev[name].dict_index > 0 and np.all(np.diff(A.rowptr) > 0) and len(pats) <= 256
+        assert dev[name].row_pattern == (len(pats) if ok else 0), (name, len(pats), dev[name].row_pattern)
+    assert dev["lap16"].row_pattern == 27  # interior, 6 faces, 12 edges, 8 corners
+    assert dev["lap_hole"].dict_index == 7 and dev["lap_hole"].row_pattern == 0
+    for name in ("A1", "P0", "R0"):
+        assert dev[name].row_pattern > 0, name
 
 
-@pytest.mark.parametrize("name", ["lap16", "lap_rect", "A1", "rand_q", "longrows_q", "P0", "R1"])
+@pytest.mark.parametrize("name", ["lap16", "lap_rect", "A1", "rand_q", "longrows_q", "P0", "R1",
+                                  "lap_hole"])
 def test_value_index_matches_plain(mats, ctx, amg, name):
-    """The same matrix registered with and without the value index gives
-    bit-identical SpGEMV, Jacobi and fused residual+Jacobi results."""
+    """The same matrix registered as plain CSR, value-indexed, dictionary-coded
+    and row-pattern-coded gives bit-identical SpGEMV and Jacobi results."""
     host, dev = mats
     A = host[name]
     ctx.set_value_index(0)
@@ -119,11 +144,16 @@ def test_value_index_matches_plain(mats, ctx, amg, name):
     ctx.set_dict_index(0)
     vi_only = ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val)
     ctx.set_dict_index(1)
+    ctx.set_row_pattern(0)
+    dc_only = ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val)
+    ctx.set_row_pattern(1)
     assert plain.value_index == 0 and dev[name].value_index > 0 and vi_only.dict_index == 0
+    assert dc_only.row_pattern == 0 and dc_only.dict_index == dev[name].dict_index
     x = ctx.vec(_vecs(A.ncols, 5))
     b = ctx.vec(_vecs(A.nrows, 6))
     outs = []
-    for M in (plain, vi_only, dev[name]):
+    variants = (plain, vi_only, dc_only, dev[name])
+    for M in variants:
         y = ctx.vec(A.nrows)
         amg.smem.SMEM_SpGEMV(ctx, M, x, b, -1.0, 1.0, y, 0, A.nrows)
         outs.append(y.download())
@@ -131,12 +161,13 @@ def test_value_index_matches_plain(mats, ctx, amg, name):
             u = ctx.vec(_vecs(A.nrows, 7))
             amg.smem.SMEM_Sync_Parfor_Jacobi(ctx, M, b, u, ctx.vec(A.nrows), 2, 0, 0.7)
             outs.append(u.download())
-    k = len(outs) // 3
+    k = len(outs) // len(variants)
     for i in range(k):
-        assert_bitwise(outs[k + i], outs[i], name)
-        assert_bitwise(outs[2 * k + i], outs[i], name)
+        for v in range(1, len(variants)):
+            assert_bitwise(outs[v * k + i], outs[i], f"{name} variant {v}")
     plain.free()
     vi_only.free()
+    dc_only.free()
 
 
 @pytest.mark.parametrize("name", ALL)

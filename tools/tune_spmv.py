@@ -16,6 +16,7 @@ lib.amg_dev_tune_name.restype = C.c_char_p
 lib.amg_dev_tune_spmv.argtypes = [C.c_void_p] * 4 + [C.c_int, C.c_int, C.POINTER(C.c_double)]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+prefixes = tuple(sys.argv[3].encode().split(b",")) if len(sys.argv) > 3 else None  # e.g. dc,rp
 ctx = amg.Context(0, 2)
 g = amg.Gen(n)
 mats = {"A0": g.register(ctx, amg.AMG_GEN_A, 0), "A1": g.register(ctx, amg.AMG_GEN_A, 1),
@@ -27,6 +28,8 @@ for name, A in mats.items():
     ref = None
     res = {v: [] for v in range(nv)}
     vlist = [v for v in range(nv) if name == "A0" or not lib.amg_dev_tune_name(v).startswith(b"ABL")]
+    if prefixes:
+        vlist = [v for v in vlist if lib.amg_dev_tune_name(v).startswith(prefixes)]
     for r in range(rounds):
         for v in vlist:
             ms = C.c_double()
@@ -43,6 +46,8 @@ for name, A in mats.items():
         nm = lib.amg_dev_tune_name(v)
         bpe = 1 if nm.startswith(b"dc") and A.dict_index else 5 if nm.startswith(b"vi") and A.value_index else 12
         nbytes = bpe * A.nnz + 4 * (A.nrows + 1) + 8 * A.ncols + 8 * A.nrows
+        if nm.startswith(b"rp") and A.row_pattern:
+            nbytes = A.nrows + 8 * A.ncols + 8 * A.nrows
         t = np.median(res[v])
         print(f"{name:3s} {lib.amg_dev_tune_name(v).decode():22s} median {t:.3f} ms  min {min(res[v]):.3f}"
               f"  {nbytes / t / 1e6:.0f} GB/s")
