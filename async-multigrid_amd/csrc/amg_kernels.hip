@@ -428,6 +428,16 @@ __global__ __launch_bounds__(256) void csr_rp_kernel(
    __shared__ __attribute__((aligned(16))) unsigned char ptab[256 * PS];
    __shared__ double red[4];
    const int tid = (int)threadIdx.x;
+   if (tid < T) {
+      otab[tid] = doff_g[tid];
+      vtab[tid] = dval_g[tid];
+   }
+   {
+      const int nw = (np * PS) >> 2;
+      const unsigned int *src = reinterpret_cast<const unsigned int *>(ptab_g);
+      unsigned int *dst = reinterpret_cast<unsigned int *>(ptab);
+      for (int w = tid; w < nw; w += 256) dst[w] = src[w];
+   }
    const int wg = (int)blockIdx.x;
    const int r0 = rb + wg * 256 * RPL, r1 = min(r0 + 256 * RPL, re);
    int pid[RPL], an[RPL];
@@ -444,16 +454,6 @@ __global__ __launch_bounds__(256) void csr_rp_kernel(
          acc[q] = epi.init(row);
          pf[q] = epi.pf(row);
       }
-   }
-   if (tid < T) {
-      otab[tid] = doff_g[tid];
-      vtab[tid] = dval_g[tid];
-   }
-   {
-      const int nw = (np * PS) >> 2;
-      const unsigned int *src = reinterpret_cast<const unsigned int *>(ptab_g);
-      unsigned int *dst = reinterpret_cast<unsigned int *>(ptab);
-      for (int w = tid; w < nw; w += 256) dst[w] = src[w];
    }
    __syncthreads();
    double sq[RPL];
@@ -823,17 +823,7 @@ __global__ __launch_bounds__(256) void ablation_kernel(const int *__restrict__ r
    if (row < r1) y[row] = acc;
 }
 
-int num_tune_variants() { return 28; }
-
-template <int RPL>
-static void launch_rp(hipStream_t s, const amg_mat *A, const double *x, double *y)
-{
-   EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
-   if (!A->rpat) return;
-   const int nt = (A->nrows + 256 * RPL - 1) / (256 * RPL);
-   csr_rp_kernel<0, false, EpiGemv, RPL><<<nt, 256, 0, s>>>(A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x,
-                                                            0, A->nrows, e, nullptr, A->dc_n, A->danch);
-}
+int num_tune_variants() { return 35; }
 
 template <int RPL, bool STAGE, int MAXR = AMG_DC_MAXROW>
 static void launch_dc(hipStream_t s, const amg_mat *A, const double *x, double *y)
@@ -847,6 +837,82 @@ static void launch_dc(hipStream_t s, const amg_mat *A, const double *x, double *
 
 
 
+template <int RPL>
+static void launch_rp(hipStream_t s, const amg_mat *A, const double *x, double *y)
+{
+   EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
+   if (!A->rpat) return;
+   const int nt = (A->nrows + 256 * RPL - 1) / (256 * RPL);
+   csr_rp_kernel<0, false, EpiGemv, RPL><<<nt, 256, 0, s>>>(A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x,
+                                                            0, A->nrows, e, nullptr, A->dc_n, A->danch);
+}
+
+// ablations of the row-pattern kernel on the 512^3 operator (timing only):
+// MODE 1: offsets forced to 0 (same table work, x read once per row);
+// MODE 2: matrix-free 7-pt stencil with offsets in registers (no tables);
+// MODE 3: MODE 2 with interior rows only (no bounds tests)
+template <int MODE, int RPL>
+__global__ __launch_bounds__(256) void abl_rp_k(const unsigned char *__restrict__ rpat,
+                                                const unsigned char *__restrict__ ptab_g, int np,
+                                                const int *__restrict__ doff_g, const double *__restrict__ dval_g,
+                                                const double *__restrict__ x, int n, double *__restrict__ y)
+{
+   constexpr int PS = AMG_RP_STRIDE;
+   __shared__ int otab[256];
+   __shared__ double vtab[256];
+   __shared__ __attribute__((aligned(16))) unsigned char ptab[256 * PS];
+   const int tid = (int)threadIdx.x;
+   const int r0 = blockIdx.x * 256 * RPL;
+   if (MODE == 1) {
+      if (tid < 256) {
+         otab[tid] = doff_g[tid];
+         vtab[tid] = dval_g[tid];
+      }
+      const int nw = (np * PS) >> 2;
+      for (int w = tid; w < nw; w += 256)
+         reinterpret_cast<unsigned int *>(ptab)[w] = reinterpret_cast<const unsigned int *>(ptab_g)[w];
+      __syncthreads();
+   }
+#pragma unroll
+   for (int q = 0; q < RPL; q++) {
+      const int row = r0 + q * 256 + tid;
+      if (row >= n) continue;
+      double acc = 0.0;
+      if (MODE == 1) {
+         const unsigned char *pp = ptab + rpat[row] * PS;
+         const int len = pp[0];
+         for (int j = 0; j < len; j++) {
+            const int bb = pp[1 + j];
+            acc += vtab[bb] * x[row + 0 * otab[bb]];
+         }
+      } else {
+         const int off[7] = {0, -262144, -512, -1, 1, 512, 262144};
+#pragma unroll
+         for (int j = 0; j < 7; j++) {
+            if (MODE == 4 && (j == 1 || j == 6)) continue; // no +-n^2
+            if (MODE == 5 && (j == 2 || j == 5)) continue; // no +-n
+            const int c = row + off[j];
+            if (MODE >= 3 || (c >= 0 && c < n)) acc += (j == 0 ? 6.0 : -1.0) * x[MODE >= 3 ? min(max(c, 0), n - 1) : c];
+         }
+      }
+      y[row] = acc;
+   }
+}
+
+// copy ablations with the row-pattern kernel's lane -> row mapping
+template <int MODE>
+__global__ __launch_bounds__(256) void abl_copy_k(const double *__restrict__ x, int n, double *__restrict__ y)
+{
+   const int r0 = blockIdx.x * 1024;
+#pragma unroll
+   for (int q = 0; q < 4; q++) {
+      const int row = r0 + q * 256 + (int)threadIdx.x;
+      if (row >= n) continue;
+      if (MODE == 0) y[row] = x[row];
+      else y[row] = x[row] + x[min(row + 1, n - 1)] + x[max(row - 1, 0)];
+   }
+}
+
 const char *tune_variant_name(int v)
 {
    static const char *names[] = {"plain_base",   "vi_base",         "vi_strided",
@@ -857,8 +923,9 @@ const char *tune_variant_name(int v)
                                  "vi_w8",        "plain_w8",        "vi_w8_nt",     "vi_w8_ch4096",
                                  "dc_rpl1",      "dc_rpl2_m8",      "dc_rpl2",      "dc_rpl4_m8",
                                  "dc_rpl8_m8",   "rp_rpl1",         "rp_rpl2",      "rp_rpl4",
-                                 "rp_rpl8"};
-   return (v >= 0 && v < 28) ? names[v] : "?";
+                                 "rp_rpl8",      "ABL_rp_off0",     "ABL_stencil",  "ABL_stencil_clamp",
+                                 "ABL_st_nonn",  "ABL_st_non",      "ABL_copy",     "ABL_copy3"};
+   return (v >= 0 && v < 35) ? names[v] : "?";
 }
 
 void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y)
@@ -914,6 +981,24 @@ void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x
    case 25: launch_rp<2>(s, A, x, y); break;
    case 26: launch_rp<4>(s, A, x, y); break;
    case 27: launch_rp<8>(s, A, x, y); break;
+   case 28:
+   case 29:
+   case 30:
+   case 31:
+   case 32: {
+      if (!A->rpat) break;
+      const int nt = (A->nrows + 1023) / 1024;
+      const unsigned char *rp = A->rpat, *pt = A->ptab;
+      const int np = A->rp_n, n = A->nrows;
+      if (v == 28) abl_rp_k<1, 4><<<nt, 256, 0, s>>>(rp, pt, np, A->doff, A->dval, x, n, y);
+      if (v == 29) abl_rp_k<2, 4><<<nt, 256, 0, s>>>(rp, pt, np, A->doff, A->dval, x, n, y);
+      if (v == 30) abl_rp_k<3, 4><<<nt, 256, 0, s>>>(rp, pt, np, A->doff, A->dval, x, n, y);
+      if (v == 31) abl_rp_k<4, 4><<<nt, 256, 0, s>>>(rp, pt, np, A->doff, A->dval, x, n, y);
+      if (v == 32) abl_rp_k<5, 4><<<nt, 256, 0, s>>>(rp, pt, np, A->doff, A->dval, x, n, y);
+      break;
+   }
+   case 33: abl_copy_k<0><<<(A->nrows + 1023) / 1024, 256, 0, s>>>(x, A->nrows, y); break;
+   case 34: abl_copy_k<2><<<(A->nrows + 1023) / 1024, 256, 0, s>>>(x, A->nrows, y); break;
    default: break;
    }
 }
