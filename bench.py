@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--smooth-weight", type=float, default=0.8)
     p.add_argument("--reuse-outer-residual", type=int, default=1)
     p.add_argument("--cpu-baseline", type=int, default=1)
-    p.add_argument("--cpu-cycles", type=int, default=2)
+    p.add_argument("--cpu-cycles", type=int, default=20)
     p.add_argument("--spmv-reps", type=int, default=20)
     p.add_argument("--force-dist", type=int, default=0,
                    help="run the distributed (RCCL) path even at one rank")

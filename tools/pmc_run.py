@@ -1,6 +1,8 @@
 """Workload for the rocprofv3 --pmc passes (tools/gpu_pmc.sh): PMC calibration
-streams of known size per access width, then 512^3 V-cycles (value-indexed
-CSR) and plain-CSR fine residuals.  tools/pmc_traffic.py reads the counters."""
+streams of known size per access width, then 512^3 V-cycles (default storage:
+row-pattern-coded) and fine residuals of the same operator stored
+dictionary-coded, value-indexed and as plain CSR.  tools/pmc_traffic.py reads
+the counters."""
 import ctypes as C
 import os
 import sys
@@ -26,6 +28,17 @@ H.solve_start(f, ctx.vec(n ** 3))
 H.iterate(3)
 ctx.sync()
 H.free()
+# dictionary-coded (row patterns off) fine residuals
+ctx.set_row_pattern(0)
+A0d = g.register(ctx, amg.AMG_GEN_A, 0)
+xd = ctx.vec(np.random.default_rng(0).uniform(-1, 1, A0d.ncols))
+yd = ctx.vec(A0d.nrows)
+for _ in range(3):
+    amg.smem.SMEM_Sync_SpGEMV(ctx, A0d, xd, f, -1.0, 1.0, yd)
+ctx.sync()
+A0d.free()
+xd.free()
+yd.free()
 # value-indexed (dictionary off) fine residuals
 ctx.set_dict_index(0)
 A0v = g.register(ctx, amg.AMG_GEN_A, 0)
