@@ -45,6 +45,15 @@ class AmgOpts(C.Structure):
                 ("accel_type", _i), ("cheby_grid", _i)]
 
 
+class AmgClassicalOpts(C.Structure):
+    _fields_ = [("coarsen_type", _i), ("interp_type", _i), ("strong_threshold", _d),
+                ("max_row_sum", _d), ("max_levels", _i), ("max_coarse_size", _i),
+                ("num_functions", _i), ("seed", C.c_ulonglong)]
+
+
+AMG_COARSEN_PMIS, AMG_COARSEN_PMIS_FIXED, AMG_COARSEN_HMIS = 8, 9, 10
+AMG_CLASSICAL_DIRECT, AMG_CLASSICAL_EXT_I = 3, 6
+
 # name -> (restype, argtypes)
 PROTOTYPES = {
     "amg_opts_default": (None, [C.POINTER(AmgOpts)]),
@@ -110,6 +119,14 @@ PROTOTYPES = {
     "amg_gen_fill": (_i, [_p, _i, _i, _i, _i, _ip, _ip, _dp, _i]),
     "amg_gen_register": (_i, [_p, _p, _i, _i, _i, _i, _pp]),
     "amg_rhs_rand": (_i, [_ll, _ll, _d, _d, _dp]),
+    "amg_classical_opts_default": (None, [C.POINTER(AmgClassicalOpts)]),
+    "amg_classical_setup": (_i, [C.POINTER(AmgClassicalOpts), _i, _ip, _ip, _dp, _pp]),
+    "amg_classical_levels": (_i, [_p]),
+    "amg_classical_get": (_i, [_p, _i, _i, _ip, _ip, _llp, C.POINTER(_ip), C.POINTER(_ip),
+                               C.POINTER(_dp)]),
+    "amg_classical_register": (_i, [_p, _p, _i, _i, _pp]),
+    "amg_classical_cf_marker": (_i, [_p, _i, _ip]),
+    "amg_classical_free": (_i, [_p]),
     # distributed (RCCL) interface
     "amg_dist_unique_id_size": (_i, []),
     "amg_dist_get_unique_id": (_i, [C.c_char_p]),

@@ -265,6 +265,40 @@ int amg_gen_fill(const amg_gen *g, int which, int level, int z0, int z1, int *ro
 /* same, generated directly in device memory and registered */
 int amg_gen_register(amg_ctx *ctx, const amg_gen *g, int which, int level, int z0, int z1,
                      amg_mat **out);
+/* ---- in-house classical AMG setup (replaces HYPRE_BoomerAMGSetup,
+ * SMEM_Setup.cpp:55-70 / DMEM_Setup.cpp:169-173, on the host).  hypre is not in
+ * the reference tree: its published algorithms are restated, parity with
+ * hypre's own hierarchies is unpinned.  Levels hold host CSR (A diagonal first,
+ * P with sorted columns, R = P^T) until amg_classical_free. ------------------ */
+#define AMG_COARSEN_PMIS 8        /* hypre coarsen_type 8                      */
+#define AMG_COARSEN_PMIS_FIXED 9  /* 9: PMIS with a fixed random sequence (DMEM) */
+#define AMG_COARSEN_HMIS 10       /* 10 (SMEM default)                         */
+#define AMG_CLASSICAL_DIRECT 3    /* hypre interp_type 3: direct               */
+#define AMG_CLASSICAL_EXT_I 6     /* interp_type 6: extended+i (both drivers)  */
+typedef struct amg_classical amg_classical;
+typedef struct {
+   int coarsen_type;        /* hypre.coarsen_type (SMEM_Main.cpp:30, DMEM_Main.cpp:41) */
+   int interp_type;         /* hypre.interp_type                                  */
+   double strong_threshold; /* hypre.strong_threshold (SMEM 0.25, DMEM 0.5)        */
+   double max_row_sum;      /* HYPRE_BoomerAMGSetMaxRowSum (1.0: no row-sum test)  */
+   int max_levels;          /* hypre.max_levels                                   */
+   int max_coarse_size;     /* stop when a level has at most this many rows       */
+   int num_functions;       /* hypre.num_functions: unknowns per node (dof i % k)  */
+   unsigned long long seed; /* PMIS random measure                                */
+} amg_classical_opts;
+void amg_classical_opts_default(amg_classical_opts *o); /* the SMEM parameters */
+int amg_classical_setup(const amg_classical_opts *o, int n, const int *rowptr, const int *col,
+                        const double *val, amg_classical **out);
+int amg_classical_levels(const amg_classical *h);
+/* operator which (AMG_GEN_A/P/R) of a level: sizes and pointers into h */
+int amg_classical_get(const amg_classical *h, int which, int level, int *nrows, int *ncols,
+                      long long *nnz, const int **rowptr, const int **col, const double **val);
+/* register it on the device (amg_csr_register) */
+int amg_classical_register(amg_ctx *ctx, const amg_classical *h, int which, int level, amg_mat **out);
+/* C/F splitting of a level (1 = C, -1 = F) */
+int amg_classical_cf_marker(const amg_classical *h, int level, int *cf);
+int amg_classical_free(amg_classical *h);
+
 /* RHS: RandDouble(lo,hi) after srand(0) (SMEM_Setup.cpp:1729-1745), rows [r0,r1) of the global sequence */
 int amg_rhs_rand(long long r0, long long r1, double lo, double hi, double *out);
 
