@@ -127,6 +127,9 @@ PROTOTYPES = {
     "amg_classical_register": (_i, [_p, _p, _i, _i, _pp]),
     "amg_classical_cf_marker": (_i, [_p, _i, _ip]),
     "amg_classical_free": (_i, [_p]),
+    "amg_elast_create": (_i, [_i, _pp]),
+    "amg_elast_get": (_i, [_p, _ip, _llp, C.POINTER(_ip), C.POINTER(_ip), C.POINTER(_dp), C.POINTER(_dp)]),
+    "amg_elast_free": (_i, [_p]),
     # distributed (RCCL) interface
     "amg_dist_unique_id_size": (_i, []),
     "amg_dist_get_unique_id": (_i, [C.c_char_p]),

@@ -11,6 +11,23 @@ from .abi import (AMG_CLASSICAL_DIRECT, AMG_CLASSICAL_EXT_I, AMG_COARSEN_HMIS,  
                   AMG_COARSEN_PMIS, AMG_COARSEN_PMIS_FIXED, AMG_GEN_A, AMG_GEN_P, AMG_GEN_R)
 
 
+def elasticity(refine):
+    """The DMEM elasticity problem (amg_elast_*): (n, rowptr, col, val, rhs) as
+    numpy copies; num_functions = 3 (byVDIM)."""
+    from . import check, lib
+    h = C.c_void_p()
+    check(lib.amg_elast_create(int(refine), C.byref(h)))
+    try:
+        n, nz = C.c_int(), C.c_longlong()
+        rp, cj, v, b = abi._ip(), abi._ip(), abi._dp(), abi._dp()
+        check(lib.amg_elast_get(h, C.byref(n), C.byref(nz), C.byref(rp), C.byref(cj), C.byref(v), C.byref(b)))
+        N, Z = n.value, nz.value
+        return (N, np.ctypeslib.as_array(rp, (N + 1,)).copy(), np.ctypeslib.as_array(cj, (Z,)).copy(),
+                np.ctypeslib.as_array(v, (Z,)).copy(), np.ctypeslib.as_array(b, (N,)).copy())
+    finally:
+        lib.amg_elast_free(h)
+
+
 def default_opts(**kw):
     """SMEM parameters (SMEM_Main.cpp:29-35): HMIS, ext+i, theta 0.25; DMEM uses
     coarsen_type=9, strong_threshold=0.5 (DMEM_Main.cpp:38-49)."""

@@ -299,6 +299,17 @@ int amg_classical_register(amg_ctx *ctx, const amg_classical *h, int which, int 
 int amg_classical_cf_marker(const amg_classical *h, int level, int *cf);
 int amg_classical_free(amg_classical *h);
 
+/* ---- DMEM elasticity problem (config 5; replaces DMEM_BuildMfemMatrix,
+ * DMEM_BuildMatrix.cpp:442-719, which assembles it with MFEM -- restated, parity
+ * unpinned): beam-hex [0,8]x[0,1]^2 refined `refine` times, Q1 vector H1 byVDIM
+ * (dof = 3 node + component), lambda = mu = 1 (x50 on the first half), x = 0
+ * fixed, pull -1e-2 in z on x = 8.  Host CSR (diagonal first) + load vector. */
+typedef struct amg_elast amg_elast;
+int amg_elast_create(int refine, amg_elast **out);
+int amg_elast_get(const amg_elast *e, int *n, long long *nnz, const int **rowptr, const int **col,
+                  const double **val, const double **rhs);
+int amg_elast_free(amg_elast *e);
+
 /* RHS: RandDouble(lo,hi) after srand(0) (SMEM_Setup.cpp:1729-1745), rows [r0,r1) of the global sequence */
 int amg_rhs_rand(long long r0, long long r1, double lo, double hi, double *out);
 

@@ -83,3 +83,20 @@ def test_classical_distributed(amg, oracle, ctx):
     ud, hd = distributed_parts(amg, host, opts, f, 6, (0.37, 0.71), 0)
     assert_bitwise(ud, u1, "distributed classical iterate")
     np.testing.assert_allclose(hd, h1, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("r,ct", [(2, 9), (3, 10)])
+def test_elasticity_solve_matches_oracle(amg, oracle, ctx, r, ct):
+    """The DMEM elasticity problem (81-entry rows, value-indexed: the two
+    materials give ~120 distinct values) on a classical num_functions = 3
+    hierarchy: bit-identical to the oracle, residual decreasing."""
+    n, rp, cj, v, b = amg.classical.elasticity(r)
+    H = amg.classical.ClassicalAMG(n, rp, cj, v, coarsen_type=ct, strong_threshold=0.5, num_functions=3)
+    lv = host_levels(amg, H)
+    host = {k: [oracle.Csr(*m) for m in lv_] for k, lv_ in lv.items()}
+    opts = amg.default_opts(smooth_weight=0.6, num_cycles=10, tol=0.0)
+    u, hist = compare_solve(amg, oracle, ctx, host, opts, b)
+    assert np.all(np.diff(hist) < 0)
+    M = ctx.csr(*lv["A"][0])
+    assert M.value_index > 0 and M.dict_index == 0
+    M.free()
