@@ -522,6 +522,119 @@ static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int r
          A->rowptr, A->didx, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
 }
 
+// Long-row operators (dense coarse levels of classical hierarchies: hundreds of
+// entries per row, few rows): a 256-row tile leaves most of the chip idle.
+// Here a workgroup of TB threads owns RW rows: all TB threads stream the rows'
+// entries in chunks and form the rounded products into LDS, then lane r < RW
+// adds its row's products in CSR order -- the tile kernel's exact summation
+// with many more workgroups and loads in flight.  Norm partials (one per
+// 256-row tile, the tile kernel's layout) only with RW = TB = 256.
+template <int NEG, bool NEED_DIAG, class Epi, bool VI, int TB, int RW>
+__global__ __launch_bounds__(TB) void csr_long_kernel(
+   const int *__restrict__ rowptr, const int *__restrict__ col, const double *__restrict__ val,
+   const unsigned char *__restrict__ vidx, const double *__restrict__ vtab_g, const double *__restrict__ x,
+   int rb, int re, Epi epi, double *__restrict__ partials = nullptr)
+{
+   constexpr int CH = 2048;
+   __shared__ double prod[CH];
+   __shared__ double vtab[VI ? 256 : 1];
+   __shared__ double red[4];
+   const int tid = (int)threadIdx.x;
+   const int r0 = rb + (int)blockIdx.x * RW, r1 = min(r0 + RW, re);
+   const int row = r0 + tid;
+   const bool own = tid < RW && row < r1;
+   int rs = 0, rend = 0;
+   double acc = 0.0, pf = 0.0, dg = 0.0;
+   if (own) {
+      rs = rowptr[row];
+      rend = rowptr[row + 1];
+      acc = epi.init(row);
+      pf = epi.pf(row);
+      if (NEED_DIAG && !VI) dg = val[rs];
+   }
+   const int tb = rowptr[r0], te = rowptr[r1];
+   if (VI) {
+      for (int t = tid; t < 256; t += TB) vtab[t] = vtab_g[t];
+      __syncthreads();
+      if (NEED_DIAG && own) dg = vtab[vidx[rs]];
+   }
+   for (int cs = tb; cs < te; cs += CH) {
+      const int ce = min(cs + CH, te);
+#pragma unroll 8
+      for (int k = cs + tid; k < ce; k += TB) {
+         const double a = VI ? vtab[vidx[k]] : val[k];
+         prod[k - cs] = a * x[col[k]];
+      }
+      __syncthreads();
+      if (own) {
+         // in CSR order; the LDS reads of 8 products are issued together so
+         // only the add chain is sequential
+         const int a0 = max(rs, cs), a1 = min(rend, ce);
+         int k = a0;
+         for (; k + 8 <= a1; k += 8) {
+            double p[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) p[j] = prod[k + j - cs];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+               if (NEG)
+                  acc -= p[j];
+               else
+                  acc += p[j];
+            }
+         }
+         for (; k < a1; k++) {
+            if (NEG)
+               acc -= prod[k - cs];
+            else
+               acc += prod[k - cs];
+         }
+      }
+      __syncthreads();
+   }
+   double out = 0.0;
+   if (own) out = epi.finish(row, acc, dg, pf);
+   if (RW == 256 && TB == 256 && partials) {
+      const double sblk = block_sum_256(out * out, red);
+      if (tid == 0) partials[blockIdx.x] = sblk;
+   }
+}
+
+// long rows: at least 64 entries per row on average
+static inline bool long_rows(const amg_mat *A) { return A->nnz >= 64LL * A->nrows; }
+
+template <int NEG, bool NEED_DIAG, int TB, int RW, class Epi>
+static void launch_long_cfg(hipStream_t s, const amg_mat *A, const double *x, int rb, int re, const Epi &e,
+                            double *partials = nullptr)
+{
+   const int nb = (re - rb + RW - 1) / RW;
+   if (A->vidx)
+      csr_long_kernel<NEG, NEED_DIAG, Epi, true, TB, RW><<<nb, TB, 0, s>>>(A->rowptr, A->col, A->val, A->vidx,
+                                                                          A->vtab, x, rb, re, e, partials);
+   else
+      csr_long_kernel<NEG, NEED_DIAG, Epi, false, TB, RW><<<nb, TB, 0, s>>>(A->rowptr, A->col, A->val, nullptr,
+                                                                           nullptr, x, rb, re, e, partials);
+}
+
+// rows per workgroup: the most that still gives >= 4096 workgroups (64 .. 8);
+// with norm partials one 256-row tile per workgroup (tools/tune_spmv.py -5)
+template <int NEG, bool NEED_DIAG, class Epi>
+static void launch_long(hipStream_t s, const amg_mat *A, const double *x, int rb, int re, const Epi &e,
+                        double *partials = nullptr)
+{
+   const int n = re - rb;
+   if (partials)
+      launch_long_cfg<NEG, NEED_DIAG, 256, 256>(s, A, x, rb, re, e, partials);
+   else if (n >= 64 * 4096)
+      launch_long_cfg<NEG, NEED_DIAG, 256, 64>(s, A, x, rb, re, e);
+   else if (n >= 32 * 4096)
+      launch_long_cfg<NEG, NEED_DIAG, 256, 32>(s, A, x, rb, re, e);
+   else if (n >= 16 * 4096)
+      launch_long_cfg<NEG, NEED_DIAG, 256, 16>(s, A, x, rb, re, e);
+   else
+      launch_long_cfg<NEG, NEED_DIAG, 256, 8>(s, A, x, rb, re, e);
+}
+
 // production configuration (tools/tune_spmv.py picks it on the MI355X)
 using ProdCfg = TileCfg<1, 2048, false, false>;
 // value-indexed matrices with short rows (< 12 entries on average: 7-pt
@@ -654,6 +767,11 @@ void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, c
          launch_dc_op<1, false>(s, A, x, rb, re, e, partials, nb);
       else
          launch_dc_op<0, false>(s, A, x, rb, re, e, partials, nb);
+   } else if (long_rows(A)) {
+      if (g.negacc)
+         launch_long<1, false>(s, A, x, rb, re, e, partials);
+      else
+         launch_long<0, false>(s, A, x, rb, re, e, partials);
    } else if (A->vidx && !partials && !g.negacc && A->nnz < 5LL * A->nrows && nb > 4096) {
       // short rows (prolongation): tiles carry little work, so 4096 persistent
       // workgroups walking the tiles beat one workgroup per tile
@@ -691,6 +809,11 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
          launch_dc_op<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out}, nullptr, nb);
       else
          launch_dc_op<1, true>(s, A, x, rb, re, EpiJacobi{f, x, out, omega}, nullptr, nb);
+   } else if (long_rows(A)) {
+      if (l1)
+         launch_long<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out});
+      else
+         launch_long<1, true>(s, A, x, rb, re, EpiJacobi{f, x, out, omega});
    } else if (l1) {
       EpiL1Jacobi e{f, x, l1, out};
       if (A->vidx)
@@ -725,6 +848,11 @@ void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const dou
          launch_dc_op<1, false>(s, A, x, rb, re, e, partials, nb);
       else
          launch_dc_op<1, true>(s, A, x, rb, re, e, partials, nb);
+   } else if (long_rows(A)) {
+      if (l1)
+         launch_long<1, false>(s, A, x, rb, re, e, partials);
+      else
+         launch_long<1, true>(s, A, x, rb, re, e, partials);
    } else if (A->vidx && short_rows(A)) {
       if (l1)
          csr_tile_kernel<ShortCfg, 1, false, EpiResJacobi, true><<<nb, 256, 0, s>>>(
@@ -823,7 +951,7 @@ __global__ __launch_bounds__(256) void ablation_kernel(const int *__restrict__ r
    if (row < r1) y[row] = acc;
 }
 
-int num_tune_variants() { return 35; }
+int num_tune_variants() { return 42; }
 
 template <int RPL, bool STAGE, int MAXR = AMG_DC_MAXROW>
 static void launch_dc(hipStream_t s, const amg_mat *A, const double *x, double *y)
@@ -924,8 +1052,10 @@ const char *tune_variant_name(int v)
                                  "dc_rpl1",      "dc_rpl2_m8",      "dc_rpl2",      "dc_rpl4_m8",
                                  "dc_rpl8_m8",   "rp_rpl1",         "rp_rpl2",      "rp_rpl4",
                                  "rp_rpl8",      "ABL_rp_off0",     "ABL_stencil",  "ABL_stencil_clamp",
-                                 "ABL_st_nonn",  "ABL_st_non",      "ABL_copy",     "ABL_copy3"};
-   return (v >= 0 && v < 35) ? names[v] : "?";
+                                 "ABL_st_nonn",  "ABL_st_non",      "ABL_copy",     "ABL_copy3",
+                                 "long_t64_r64",  "long_t256_r8",   "long_t256_r16", "long_t256_r32",
+                                 "long_t256_r64", "long_t128_r16", "long_t256_r256"};
+   return (v >= 0 && v < 42) ? names[v] : "?";
 }
 
 void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y)
@@ -999,6 +1129,13 @@ void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x
    }
    case 33: abl_copy_k<0><<<(A->nrows + 1023) / 1024, 256, 0, s>>>(x, A->nrows, y); break;
    case 34: abl_copy_k<2><<<(A->nrows + 1023) / 1024, 256, 0, s>>>(x, A->nrows, y); break;
+   case 35: launch_long_cfg<0, false, 64, 64>(s, A, x, 0, A->nrows, EpiGemv{nullptr, y, 0, 0, 1.0, 0.0}); break;
+   case 36: launch_long_cfg<0, false, 256, 8>(s, A, x, 0, A->nrows, EpiGemv{nullptr, y, 0, 0, 1.0, 0.0}); break;
+   case 37: launch_long_cfg<0, false, 256, 16>(s, A, x, 0, A->nrows, EpiGemv{nullptr, y, 0, 0, 1.0, 0.0}); break;
+   case 38: launch_long_cfg<0, false, 256, 32>(s, A, x, 0, A->nrows, EpiGemv{nullptr, y, 0, 0, 1.0, 0.0}); break;
+   case 39: launch_long_cfg<0, false, 256, 64>(s, A, x, 0, A->nrows, EpiGemv{nullptr, y, 0, 0, 1.0, 0.0}); break;
+   case 40: launch_long_cfg<0, false, 128, 16>(s, A, x, 0, A->nrows, EpiGemv{nullptr, y, 0, 0, 1.0, 0.0}); break;
+   case 41: launch_long_cfg<0, false, 256, 256>(s, A, x, 0, A->nrows, EpiGemv{nullptr, y, 0, 0, 1.0, 0.0}); break;
    default: break;
    }
 }
@@ -1600,6 +1737,7 @@ __device__ __forceinline__ unsigned int vi_hash(unsigned long long k)
 __device__ __forceinline__ void vi_insert(unsigned long long key, unsigned long long *slots,
                                           int nslots, int *count)
 {
+   if (__atomic_load_n(count, __ATOMIC_RELAXED) > 256) return; // table already useless
    unsigned int h = vi_hash(key) & (nslots - 1);
    for (int probe = 0; probe < nslots; probe++) {
       const unsigned long long cur = __atomic_load_n(&slots[h], __ATOMIC_RELAXED);
@@ -1709,6 +1847,7 @@ __global__ void rp_collect_k(const int *__restrict__ rowptr, const unsigned char
       const unsigned long long key = rp_key(didx, rs, len);
       if (key == last) continue;
       last = key;
+      if (__atomic_load_n(count, __ATOMIC_RELAXED) > 256) continue; // too many patterns: only count bad rows
       unsigned int h = vi_hash(key) & (nslots - 1);
       for (int probe = 0; probe < nslots; probe++) {
          const unsigned long long cur = __atomic_load_n(&slots[h], __ATOMIC_RELAXED);
@@ -1822,6 +1961,9 @@ __global__ void vi_collect_k(const double *__restrict__ val, long long nnz,
          atomicAdd(count, 1 << 20); // the sentinel pattern itself: give up on the table
          continue;
       }
+      // more than 256 distinct values: the table is useless, stop probing
+      // (a nearly full table would cost nslots probes per new value)
+      if (__atomic_load_n(count, __ATOMIC_RELAXED) > 256) return;
       unsigned int h = vi_hash(key) & (nslots - 1);
       for (int probe = 0; probe < nslots; probe++) {
          const unsigned long long cur = __atomic_load_n(&slots[h], __ATOMIC_RELAXED);

@@ -53,6 +53,8 @@ def matrices(oracle, amg):
     out["rand_sq"] = random_csr(oracle, 3000, 3000, 9, seed=1, with_zero_diag=True)
     out["rand_nz"] = random_csr(oracle, 2500, 2500, 9, seed=4)
     out["rand_rect"] = random_csr(oracle, 1777, 901, 5, seed=2, diag_first=False)
+    # >= 64 entries per row on average: the long-row kernel (classical coarse levels)
+    out["dense"] = random_csr(oracle, 2100, 2100, 90, seed=7, with_zero_diag=True)
     # long rows: > AMG_CHUNK (2048) entries in one row and in one tile
     g2 = rng(3)
     n = 600
@@ -69,7 +71,7 @@ def matrices(oracle, amg):
     # value-indexed CSR: the same structures with values drawn from a small set
     # (256 distinct values: the largest table; 257: falls back to plain CSR)
     for name, src, nv in (("rand_q", "rand_sq", 256), ("longrows_q", "longrows", 37),
-                          ("rand_q257", "rand_nz", 257)):
+                          ("rand_q257", "rand_nz", 257), ("dense_q", "dense", 200)):
         A = out[src]
         levels = np.linspace(-1.0, 1.0, nv) * (1.0 + 1.0 / 3.0)
         q = levels[rng(nv).integers(0, nv, size=A.val.size)]
@@ -89,7 +91,8 @@ def mats(oracle, amg, ctx):
     return host, dev
 
 
-SQUARE = ["lap16", "A1", "A2", "rand_sq", "longrows", "rand_q", "longrows_q", "rand_q257", "lap_hole"]
+SQUARE = ["lap16", "A1", "A2", "rand_sq", "longrows", "rand_q", "longrows_q", "rand_q257", "lap_hole",
+          "dense", "dense_q"]
 ALL = SQUARE + ["lap_rect", "P0", "P1", "R0", "R1", "rand_rect"]
 
 

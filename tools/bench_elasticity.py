@@ -1,0 +1,76 @@
+"""Config 5 on one MI355X: the DMEM elasticity problem (amg_elast_*, beam-hex
+refined r times, Q1 byVDIM) on the in-house classical hierarchy
+(num_functions = 3, PMIS fixed seed, extended+i, theta 0.5: the DMEM
+parameters), SMEM_Solve MULT V(1,1) weighted Jacobi.  Prints one JSON line:
+V-cycle iterations/s, fine SpMV time and its bytes in the stored format."""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, ROOT)
+from conftest import load_package  # noqa: E402
+from bench import storage, HBM_PEAK_GBS  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--refine", type=int, default=5)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--coarsen", type=int, default=9)
+    p.add_argument("--theta", type=float, default=0.5)
+    p.add_argument("--omega", type=float, default=0.6)
+    a = p.parse_args()
+    amg = load_package()
+    t0 = time.time()
+    n, rp, cj, v, b = amg.classical.elasticity(a.refine)
+    t1 = time.time()
+    H = amg.classical.ClassicalAMG(n, rp, cj, v, coarsen_type=a.coarsen, strong_threshold=a.theta,
+                                   num_functions=3)
+    t2 = time.time()
+    print(f"[elast] r={a.refine}: {n} dofs, {len(cj)} nnz; generated {t1 - t0:.1f}s, classical setup "
+          f"{t2 - t1:.1f}s, {H.L} levels", file=sys.stderr, flush=True)
+    ctx = amg.Context(0, 4)
+    opts = amg.default_opts(smooth_weight=a.omega, num_cycles=1 << 30, tol=0.0, profile=1)
+    Hd = H.hierarchy(ctx, opts)
+    As = Hd._keep[0]
+    sizes = [m.nrows for m in As]
+    opc = sum(m.nnz for m in As) / As[0].nnz
+    fv = ctx.vec(b)
+    r0 = Hd.solve_start(fv, ctx.vec(n))
+    Hd.iterate(a.warmup)
+    ctx.sync()
+    t3 = time.perf_counter()
+    Hd.iterate(a.steps)
+    ctx.sync()
+    t4 = time.perf_counter()
+    rn = Hd.resnorm()
+    x, y = ctx.vec(n), ctx.vec(n)
+    x.set(1.0)
+    ms = C.c_double()
+    amg.check(amg.lib.amg_matvec_timed(ctx.h, As[0].h, x.h, y.h, 20, C.byref(ms)))
+    A0 = As[0]
+    mat_bytes, fmt = storage(A0.nrows, A0.nnz, A0.value_index, A0.dict_index, A0.row_pattern)
+    spmv_bytes = mat_bytes + 16 * n
+    out = {"workload": f"DMEM elasticity (config 5 restated) r={a.refine}: {n} dofs, beam-hex Q1 byVDIM, "
+                       f"classical hierarchy (coarsen {a.coarsen}, ext+i, theta {a.theta}, 3 functions), "
+                       f"SMEM_Solve MULT V(1,1) Jacobi w={a.omega}",
+           "it_per_s": a.steps / (t4 - t3), "ms_per_step": (t4 - t3) * 1e3 / a.steps,
+           "dofs": n, "nnz_A0": int(A0.nnz), "levels": len(sizes), "level_rows": sizes,
+           "operator_complexity": opc, "matrix_format": fmt,
+           "fine_spmv": {"ms": ms.value, "bytes": spmv_bytes, "gbs": spmv_bytes / (ms.value * 1e-3) / 1e9,
+                         "frac": spmv_bytes / (ms.value * 1e-3) / 1e9 / HBM_PEAK_GBS},
+           "relres_after": rn / r0, "cycles": a.warmup + a.steps,
+           "setup_s": {"generate": t1 - t0, "classical_host": t2 - t1}}
+    print(json.dumps(out), flush=True)
+    Hd.free()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -18,9 +18,14 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 prefixes = tuple(sys.argv[3].encode().split(b",")) if len(sys.argv) > 3 else None  # e.g. dc,rp
 ctx = amg.Context(0, 2)
-g = amg.Gen(n)
-mats = {"A0": g.register(ctx, amg.AMG_GEN_A, 0), "A1": g.register(ctx, amg.AMG_GEN_A, 1),
-        "R0": g.register(ctx, amg.AMG_GEN_R, 0), "P0": g.register(ctx, amg.AMG_GEN_P, 0)}
+if n < 0:  # elasticity r = -n: the classical hierarchy's operators (long coarse rows)
+    ne, rp, cj, v, b = amg.classical.elasticity(-n)
+    H = amg.classical.ClassicalAMG(ne, rp, cj, v, coarsen_type=9, strong_threshold=0.5, num_functions=3)
+    mats = {f"E{l}": H.register(ctx, amg.AMG_GEN_A, l) for l in range(min(H.L, 5))}
+else:
+    g = amg.Gen(n)
+    mats = {"A0": g.register(ctx, amg.AMG_GEN_A, 0), "A1": g.register(ctx, amg.AMG_GEN_A, 1),
+            "R0": g.register(ctx, amg.AMG_GEN_R, 0), "P0": g.register(ctx, amg.AMG_GEN_P, 0)}
 nv = lib.amg_dev_tune_count()
 for name, A in mats.items():
     x = ctx.vec(np.random.default_rng(0).uniform(-1, 1, A.ncols))
