@@ -77,6 +77,10 @@ class Context:
         """Row-pattern-coded CSR on top of the dictionary (default on)."""
         check(lib.amg_set_row_pattern(self.h, int(enable)))
 
+    def set_pair_pattern(self, enable):
+        """Paired-row-pattern CSR on top of the row patterns (default on)."""
+        check(lib.amg_set_pair_pattern(self.h, int(enable)))
+
     def csr(self, nrows, ncols, rowptr, col, val, diag_first=1):
         return Mat.register(self, nrows, ncols, rowptr, col, val, diag_first)
 
@@ -105,6 +109,7 @@ class Mat:
         self.value_index = lib.amg_mat_value_index(handle)  # table size, 0 = plain CSR
         self.dict_index = lib.amg_mat_dict_index(handle)    # dictionary size, 0 = not coded
         self.row_pattern = lib.amg_mat_row_pattern(handle)  # distinct row patterns, 0 = not coded
+        self.pair_pattern = lib.amg_mat_pair_pattern(handle)  # distinct row-pair patterns, 0 = not coded
 
     @classmethod
     def register(cls, ctx, nrows, ncols, rowptr, col, val, diag_first=1):

@@ -75,6 +75,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_VALUE_INDEX")) c->value_index = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_DICT_INDEX")) c->dict_index = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_ROW_PATTERN")) c->row_pattern = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_PAIR_PATTERN")) c->pair_pattern = std::atoi(v) != 0;
    *out = c;
    return AMG_OK;
 }
@@ -333,6 +334,100 @@ static int build_row_pattern(amg_mat *A)
    return AMG_OK;
 }
 
+// paired-row-pattern CSR on top of the row patterns: rows 2t and 2t+1 of a
+// square operator share one merged entry list in which an entry both rows
+// hold at the same column offset is one 16-byte x load.
+// The merge is a shortest common supersequence of the two rows' entry lists
+// (matched on column offset), so each row still sums its own entries in its
+// CSR order: bit-identical to the single-row kernel.
+static void pair_merge(const unsigned char *a, int la, const unsigned char *b, int lb,
+                       const std::vector<int> &off, std::vector<unsigned int> &out)
+{
+   int dp[AMG_PP_MAXROW + 2][AMG_PP_MAXROW + 2] = {};
+   for (int i = la - 1; i >= 0; i--)
+      for (int j = lb - 1; j >= 0; j--)
+         dp[i][j] = off[a[i]] == off[b[j]] ? dp[i + 1][j + 1] + 1 : std::max(dp[i + 1][j], dp[i][j + 1]);
+   int i = 0, j = 0;
+   while (i < la || j < lb) {
+      if (i < la && j < lb && off[a[i]] == off[b[j]] && dp[i][j] == dp[i + 1][j + 1] + 1) {
+         out.push_back(a[i] | (unsigned)b[j] << 8 | 3u << 16);
+         i++;
+         j++;
+      } else if (j >= lb || (i < la && dp[i + 1][j] >= dp[i][j + 1])) {
+         out.push_back(a[i] | 1u << 16);
+         i++;
+      } else {
+         out.push_back((unsigned)b[j] << 8 | 2u << 16);
+         j++;
+      }
+   }
+}
+
+static int build_pair_pattern(amg_mat *A)
+{
+   amg_ctx *c = A->ctx;
+   hipStream_t s = c->stream;
+   constexpr int NK = 256 * 257; // key = p0 * 257 + p1 (p1 = 256: no row 2t+1)
+   unsigned char *flags = nullptr;
+   AMG_HIP(hipMalloc(&flags, 2 * NK));
+   unsigned char *map = flags + NK;
+   AMG_HIP(hipMemsetAsync(flags, 0, NK, s));
+   amgk::pp_collect(s, A, flags);
+   std::vector<unsigned char> hf(NK), pt(256 * AMG_RP_STRIDE);
+   std::vector<int> off(256);
+   AMG_HIP(hipMemcpyAsync(hf.data(), flags, NK, hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(pt.data(), A->ptab, pt.size(), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(off.data(), A->doff, 256 * sizeof(int), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   std::vector<unsigned char> hm(NK, 0);
+   std::vector<unsigned int> tab;
+   int T = 0;
+   for (int k = 0; k < NK && T <= 256; k++) {
+      if (!hf[k]) continue;
+      if (T == 256) {
+         T++;
+         break;
+      }
+      const int p0 = k / 257, p1 = k % 257;
+      const unsigned char *a = pt.data() + p0 * AMG_RP_STRIDE;
+      std::vector<unsigned int> el;
+      if (p1 < 256) {
+         const unsigned char *b = pt.data() + p1 * AMG_RP_STRIDE;
+         pair_merge(a + 1, a[0], b + 1, b[0], off, el);
+      } else {
+         for (int j = 0; j < a[0]; j++) el.push_back(a[1 + j] | 1u << 16);
+      }
+      std::vector<unsigned int> w(AMG_PP_STRIDE, 0);
+      w[0] = (unsigned)el.size() | (p1 < 256 ? 1u << 24 : 0u);
+      for (size_t e = 0; e < el.size(); e++) w[1 + e] = el[e];
+      tab.insert(tab.end(), w.begin(), w.end());
+      hm[k] = (unsigned char)T++;
+   }
+   if (T < 1 || T > 256) {
+      hipFree(flags);
+      return AMG_OK;
+   }
+   const size_t np = ((size_t)A->nrows + 1) / 2;
+   hipError_t e = hipMalloc(&A->ppat, std::max<size_t>(1, np));
+   if (e == hipSuccess) e = hipMalloc(&A->pptab, tab.size() * sizeof(unsigned int));
+   if (e != hipSuccess) {
+      hipFree(A->ppat);
+      hipFree(A->pptab);
+      A->ppat = nullptr;
+      A->pptab = nullptr;
+      hipFree(flags);
+      (void)hipGetLastError();
+      return AMG_OK;
+   }
+   AMG_HIP(hipMemcpyAsync(map, hm.data(), NK, hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemcpyAsync(A->pptab, tab.data(), tab.size() * sizeof(unsigned int), hipMemcpyHostToDevice, s));
+   amgk::pp_encode(s, A, map, A->ppat);
+   AMG_HIP(hipStreamSynchronize(s));
+   hipFree(flags);
+   A->pp_n = T;
+   return AMG_OK;
+}
+
 int amg_mat_finish(amg_mat *A)
 {
    amgk::extract_diag(A->ctx->stream, A);
@@ -340,6 +435,9 @@ int amg_mat_finish(amg_mat *A)
    if (A->ctx->value_index && A->nnz > 0) AMG_TRY(build_value_index(A));
    if (A->ctx->dict_index && A->vidx) AMG_TRY(build_dict_index(A));
    if (A->ctx->row_pattern && A->didx) AMG_TRY(build_row_pattern(A));
+   if (A->ctx->pair_pattern && A->rpat && !A->danch && A->nrows == A->ncols &&
+       A->dc_maxrow <= AMG_PP_MAXROW)
+      AMG_TRY(build_pair_pattern(A));
    return AMG_OK;
 }
 
@@ -353,6 +451,18 @@ extern "C" int amg_set_row_pattern(amg_ctx *c, int enable)
 extern "C" int amg_mat_row_pattern(const amg_mat *A)
 {
    return A ? A->rp_n : 0;
+}
+
+extern "C" int amg_set_pair_pattern(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_pair_pattern: null context");
+   c->pair_pattern = enable ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_pair_pattern(const amg_mat *A)
+{
+   return A ? A->pp_n : 0;
 }
 
 extern "C" int amg_set_dict_index(amg_ctx *c, int enable)
@@ -425,6 +535,8 @@ extern "C" int amg_mat_free(amg_mat *A)
    hipFree(A->danch);
    hipFree(A->rpat);
    hipFree(A->ptab);
+   hipFree(A->ppat);
+   hipFree(A->pptab);
    delete A;
    return AMG_OK;
 }

@@ -45,6 +45,10 @@ constexpr int AMG_NNZ_PAD = 8;
 constexpr int AMG_DC_MAXROW = 32;
 // bytes per row pattern of the row-pattern-coded form: length + entries (x4 aligned)
 constexpr int AMG_RP_STRIDE = 36;
+// paired row patterns (rows 2t, 2t+1 of operators whose rows hold <= 8
+// entries): one header word + up to 16 merged entry words per pair pattern
+constexpr int AMG_PP_MAXROW = 8;
+constexpr int AMG_PP_STRIDE = 1 + 2 * AMG_PP_MAXROW;
 
 struct amg_transport; // amg_dist.cpp: RCCL communicator or host-callback test transport
 
@@ -63,6 +67,7 @@ struct amg_ctx {
    int value_index = 1; // build value-indexed CSR for matrices with <= 256 distinct values
    int dict_index = 1;  // build dictionary-coded CSR for stencil-like square operators
    int row_pattern = 1; // build row-pattern-coded CSR on top of the dictionary
+   int pair_pattern = 1; // build paired-row-pattern CSR on top of the row patterns
 };
 
 struct amg_mat {
@@ -96,6 +101,16 @@ struct amg_mat {
    unsigned char *rpat = nullptr;
    unsigned char *ptab = nullptr;
    int rp_n = 0;
+   // paired-row-pattern form (square operators, anchor = row, rows of <= 8
+   // entries, <= 256 distinct (pattern of row 2t, pattern of row 2t+1) pairs):
+   // ppat[t] names the pair's merged entry list in pptab (AMG_PP_STRIDE words
+   // per pair: header nel | row1 present << 24, then entries
+   // d0 | d1 << 8 | has0 << 16 | has1 << 17).  An entry present in both rows
+   // has one column offset: the kernel reads x[2t + off], x[2t + 1 + off] with
+   // one 16-byte load.
+   unsigned char *ppat = nullptr;
+   unsigned int *pptab = nullptr;
+   int pp_n = 0;
 };
 
 struct amg_vec {
@@ -209,6 +224,8 @@ void rp_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int 
 void rp_table(hipStream_t s, const amg_mat *A, const int *rep, int T, unsigned char *ptab);
 void rp_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
                const unsigned char *ptab, unsigned char *rpat, int *bad);
+void pp_collect(hipStream_t s, const amg_mat *A, unsigned char *flags);
+void pp_encode(hipStream_t s, const amg_mat *A, const unsigned char *map, unsigned char *ppat);
 
 // dictionary-coded CSR construction (needs the value index)
 void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,

@@ -41,6 +41,8 @@ __device__ __forceinline__ double block_sum_256(double v, double *lds4)
 // ---------------------------------------------------------------------------
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef double v2d __attribute__((ext_vector_type(2)));
+// two consecutive doubles at an 8-byte aligned address (global_load_dwordx4)
+typedef double v2du __attribute__((ext_vector_type(2), aligned(8)));
 
 // Tile configuration: RPT rows per lane (tile = 256*RPT rows), CH products
 // per LDS chunk, NT non-temporal val/col streams (read once; keep L2 for x),
@@ -500,6 +502,138 @@ __global__ __launch_bounds__(256) void csr_rp_kernel(
    }
 }
 
+// Paired-row-pattern kernel: lane owns the row pair (2t, 2t+1) and reads the
+// pair's merged entry list (AMG_PP_STRIDE words in LDS).  An entry both rows
+// hold at the same column offset o reads x[2t+o] and x[2t+1+o] with ONE
+// 16-byte load (half the vector-memory instructions of one lane per row,
+// which bounds the single-row kernel: DESIGN.md Sec.4); an entry of one row
+// alone reads its x value by itself.  Each row still sums its own entries in
+// its CSR order (the merge keeps both orders), so results are bit-identical.
+// Workgroup slab q covers 512 rows = two 256-row norm tiles, reduced in the
+// single-row kernel's lane order through LDS.  rb must be even.
+template <int NEG, bool NEED_DIAG, class Epi, int RPL>
+__global__ __launch_bounds__(256) void csr_rpp_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned int *__restrict__ pptab_g, int np,
+   const int *__restrict__ doff_g, const double *__restrict__ dval_g, const double *__restrict__ x,
+   int rb, int re, Epi epi, double *__restrict__ partials, int T)
+{
+   constexpr int PS = AMG_PP_STRIDE;
+   __shared__ int otab[256];
+   __shared__ double vtab[256];
+   extern __shared__ unsigned int ptab[]; // np * PS words (dynamic)
+   __shared__ double sqs[512];
+   __shared__ double red[4];
+   const int tid = (int)threadIdx.x;
+   if (tid < T) {
+      otab[tid] = doff_g[tid];
+      vtab[tid] = dval_g[tid];
+   }
+   for (int w = tid; w < np * PS; w += 256) ptab[w] = pptab_g[w];
+   const int wg = (int)blockIdx.x;
+   int pid[RPL];
+#pragma unroll
+   for (int q = 0; q < RPL; q++) {
+      const int row = rb + (wg * RPL + q) * 512 + 2 * tid;
+      pid[q] = row < re ? ppat[row >> 1] : 0;
+   }
+   __syncthreads();
+#pragma unroll
+   for (int q = 0; q < RPL; q++) {
+      const int s0 = rb + (wg * RPL + q) * 512;
+      const int row = s0 + 2 * tid;
+      const bool a0 = row < re, a1 = row + 1 < re;
+      double sq0 = 0.0, sq1 = 0.0;
+      if (a0) {
+         const unsigned int *pp = ptab + pid[q] * PS;
+         const int nel = pp[0] & 0xff;
+         v2d acc, pf;
+         if (a1) {
+            acc = epi.init2(row);
+            pf = epi.pf2(row);
+         } else {
+            acc = v2d{epi.init(row), 0.0};
+            pf = v2d{epi.pf(row), 0.0};
+         }
+         double dg0 = 0.0, dg1 = 0.0;
+         for (int k = 0; k < nel; k += 8) {
+            const int m = nel - k;
+            v2d xv[8];
+            unsigned int ew[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+               ew[j] = 0;
+               xv[j] = v2d{0.0, 0.0};
+               if (j < m) {
+                  const unsigned int w = pp[1 + k + j];
+                  ew[j] = w;
+                  const int d0 = w & 0xff, d1 = (w >> 8) & 0xff;
+                  if ((w >> 16 & 3) == 3)
+                     xv[j] = *reinterpret_cast<const v2du *>(x + row + otab[d0]);
+                  else if (w >> 16 & 1)
+                     xv[j].x = x[row + otab[d0]];
+                  else
+                     xv[j].y = x[row + 1 + otab[d1]];
+               }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+               if (j < m) {
+                  const unsigned int w = ew[j];
+                  if (w >> 16 & 1) {
+                     const double v = vtab[w & 0xff];
+                     if (NEG)
+                        acc.x -= v * xv[j].x;
+                     else
+                        acc.x += v * xv[j].x;
+                  }
+                  if (w >> 17 & 1) {
+                     const double v = vtab[(w >> 8) & 0xff];
+                     if (NEG)
+                        acc.y -= v * xv[j].y;
+                     else
+                        acc.y += v * xv[j].y;
+                  }
+               }
+         }
+         if (NEED_DIAG) {
+            // a_ii := A_data[A_i[i]]: each row's first entry in the merged list
+            bool f0 = false, f1 = false;
+            for (int e = 0; e < nel && !(f0 && f1); e++) {
+               const unsigned int w = pp[1 + e];
+               if (!f0 && (w >> 16 & 1)) {
+                  dg0 = vtab[w & 0xff];
+                  f0 = true;
+               }
+               if (!f1 && (w >> 17 & 1)) {
+                  dg1 = vtab[(w >> 8) & 0xff];
+                  f1 = true;
+               }
+            }
+         }
+         if (a1) {
+            const v2d out = epi.finish2(row, acc, v2d{dg0, dg1}, pf);
+            sq0 = out.x * out.x;
+            sq1 = out.y * out.y;
+         } else {
+            const double out = epi.finish(row, acc.x, dg0, pf.x);
+            sq0 = out * out;
+         }
+      }
+      if (partials) {
+         // the 256-row tiles' sums in the single-row kernel's lane order
+         sqs[2 * tid] = sq0;
+         sqs[2 * tid + 1] = sq1;
+         __syncthreads();
+#pragma unroll
+         for (int h = 0; h < 2; h++) {
+            const double sblk = block_sum_256(sqs[h * 256 + tid], red);
+            if (tid == 0 && s0 + h * 256 < re) partials[(s0 - rb) / 256 + h] = sblk;
+         }
+         __syncthreads();
+      }
+   }
+}
+
 // dictionary-coded launches: rows of <= 8 entries (7-pt stencil, interpolation)
 // take four 256-row tiles per workgroup, longer rows (27-pt Galerkin,
 // restriction) two (tools/tune_spmv.py, profiles/r01/tune_spmv.log); the
@@ -508,7 +642,10 @@ template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int rb, int re,
                          const Epi &e, double *partials, int tiles)
 {
-   if (A->rpat && A->dc_maxrow <= 8)
+   if (A->ppat && (rb & 1) == 0)
+      csr_rpp_kernel<NEG, NEED_DIAG, Epi, 2><<<(re - rb + 1023) / 1024, 256, A->pp_n * AMG_PP_STRIDE * 4, s>>>(
+         A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n);
+   else if (A->rpat && A->dc_maxrow <= 8)
       csr_rp_kernel<NEG, NEED_DIAG, Epi, 4><<<(tiles + 3) / 4, 256, 0, s>>>(
          A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
    else if (A->rpat)
@@ -671,6 +808,25 @@ struct EpiGemv {
       y[i] = v;
       return v;
    }
+   // rows i, i+1 (paired-row kernel)
+   __device__ __forceinline__ v2d init2(int i) const
+   {
+      if (imode == 0) return v2d{0.0, 0.0};
+      const v2d bb = *reinterpret_cast<const v2du *>(b + i);
+      switch (imode) {
+      case 1: return bb;
+      case 2: return v2d{-bb.x, -bb.y};
+      case 3: return v2d{bb.x * temp, bb.y * temp};
+      default: return v2d{-bb.x * temp, -bb.y * temp};
+      }
+   }
+   __device__ __forceinline__ v2d pf2(int) const { return v2d{0.0, 0.0}; }
+   __device__ __forceinline__ v2d finish2(int i, v2d acc, v2d, v2d) const
+   {
+      const v2d v = scale ? v2d{alpha * acc.x, alpha * acc.y} : acc;
+      *reinterpret_cast<v2du *>(y + i) = v;
+      return v;
+   }
 };
 
 // Jacobi sweep epilogue (SMEM_Smooth.cpp:35-45): res = f - sum; u_new = u + w*res/a
@@ -687,6 +843,15 @@ struct EpiJacobi {
       out[i] = v;
       return v;
    }
+   __device__ __forceinline__ v2d init2(int i) const { return *reinterpret_cast<const v2du *>(f + i); }
+   __device__ __forceinline__ v2d pf2(int i) const { return *reinterpret_cast<const v2du *>(x + i); }
+   __device__ __forceinline__ v2d finish2(int i, v2d res, v2d a, v2d xi) const
+   {
+      const v2d v{(a.x != 0.0) ? xi.x + omega * res.x / a.x : xi.x,
+                  (a.y != 0.0) ? xi.y + omega * res.y / a.y : xi.y};
+      *reinterpret_cast<v2du *>(out + i) = v;
+      return v;
+   }
 };
 
 // L1 Jacobi sweep epilogue (SMEM_Smooth.cpp:122-130): u_new = u + res/l1
@@ -701,6 +866,15 @@ struct EpiL1Jacobi {
    {
       const double v = xi + res / l1[i];
       out[i] = v;
+      return v;
+   }
+   __device__ __forceinline__ v2d init2(int i) const { return *reinterpret_cast<const v2du *>(f + i); }
+   __device__ __forceinline__ v2d pf2(int i) const { return *reinterpret_cast<const v2du *>(x + i); }
+   __device__ __forceinline__ v2d finish2(int i, v2d res, v2d, v2d xi) const
+   {
+      const v2d l = *reinterpret_cast<const v2du *>(l1 + i);
+      const v2d v{xi.x + res.x / l.x, xi.y + res.y / l.y};
+      *reinterpret_cast<v2du *>(out + i) = v;
       return v;
    }
 };
@@ -721,8 +895,24 @@ struct EpiResJacobi {
    __device__ __forceinline__ double pf(int i) const { return x[i]; }
    __device__ __forceinline__ double finish(int i, double res, double a, double xi) const
    {
-      r[i] = res;
+      if (r) r[i] = res;
       unext[i] = l1 ? xi + res / l1[i] : ((a != 0.0) ? xi + omega * res / a : xi);
+      return res;
+   }
+   __device__ __forceinline__ v2d init2(int i) const { return *reinterpret_cast<const v2du *>(f + i); }
+   __device__ __forceinline__ v2d pf2(int i) const { return *reinterpret_cast<const v2du *>(x + i); }
+   __device__ __forceinline__ v2d finish2(int i, v2d res, v2d a, v2d xi) const
+   {
+      if (r) *reinterpret_cast<v2du *>(r + i) = res;
+      v2d v;
+      if (l1) {
+         const v2d l = *reinterpret_cast<const v2du *>(l1 + i);
+         v = v2d{xi.x + res.x / l.x, xi.y + res.y / l.y};
+      } else {
+         v = v2d{(a.x != 0.0) ? xi.x + omega * res.x / a.x : xi.x,
+                 (a.y != 0.0) ? xi.y + omega * res.y / a.y : xi.y};
+      }
+      *reinterpret_cast<v2du *>(unext + i) = v;
       return res;
    }
 };
@@ -951,7 +1141,7 @@ __global__ __launch_bounds__(256) void ablation_kernel(const int *__restrict__ r
    if (row < r1) y[row] = acc;
 }
 
-int num_tune_variants() { return 42; }
+int num_tune_variants() { return 49; }
 
 template <int RPL, bool STAGE, int MAXR = AMG_DC_MAXROW>
 static void launch_dc(hipStream_t s, const amg_mat *A, const double *x, double *y)
@@ -973,6 +1163,16 @@ static void launch_rp(hipStream_t s, const amg_mat *A, const double *x, double *
    const int nt = (A->nrows + 256 * RPL - 1) / (256 * RPL);
    csr_rp_kernel<0, false, EpiGemv, RPL><<<nt, 256, 0, s>>>(A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x,
                                                             0, A->nrows, e, nullptr, A->dc_n, A->danch);
+}
+
+template <int RPL>
+static void launch_rpp(hipStream_t s, const amg_mat *A, const double *x, double *y)
+{
+   EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
+   if (!A->ppat) return;
+   const int nt = (A->nrows + 512 * RPL - 1) / (512 * RPL);
+   csr_rpp_kernel<0, false, EpiGemv, RPL><<<nt, 256, A->pp_n * AMG_PP_STRIDE * 4, s>>>(A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x,
+                                                             0, A->nrows, e, nullptr, A->dc_n);
 }
 
 // ablations of the row-pattern kernel on the 512^3 operator (timing only):
@@ -1041,6 +1241,41 @@ __global__ __launch_bounds__(256) void abl_copy_k(const double *__restrict__ x, 
    }
 }
 
+// paired-row ablations: lane owns V consecutive rows and reads each x offset
+// with V/2 16-byte loads (8-byte aligned for odd offsets)
+template <int MODE, int V>
+__global__ __launch_bounds__(256) void abl_pair_k(const double *__restrict__ x, int n, double *__restrict__ y)
+{
+   const int r0 = blockIdx.x * 1024;
+#pragma unroll
+   for (int q = 0; q < 4 / V; q++) {
+      const int row = r0 + (q * 256 + (int)threadIdx.x) * V;
+      if (row >= n) continue;
+      v2d acc[V / 2];
+#pragma unroll
+      for (int h = 0; h < V / 2; h++) acc[h] = v2d{0.0, 0.0};
+      if (MODE == 0) {
+#pragma unroll
+         for (int h = 0; h < V / 2; h++) acc[h] = *reinterpret_cast<const v2d *>(x + row + 2 * h);
+      } else {
+         const int off[7] = {0, -262144, -512, -1, 1, 512, 262144};
+#pragma unroll
+         for (int j = 0; j < 7; j++) {
+            const int c = min(max(row + off[j], 0), n - V);
+#pragma unroll
+            for (int h = 0; h < V / 2; h++) {
+               const v2d xv = *reinterpret_cast<const v2du *>(x + c + 2 * h);
+               const double w = j == 0 ? 6.0 : -1.0;
+               acc[h].x += w * xv.x;
+               acc[h].y += w * xv.y;
+            }
+         }
+      }
+#pragma unroll
+      for (int h = 0; h < V / 2; h++) *reinterpret_cast<v2d *>(y + row + 2 * h) = acc[h];
+   }
+}
+
 const char *tune_variant_name(int v)
 {
    static const char *names[] = {"plain_base",   "vi_base",         "vi_strided",
@@ -1054,8 +1289,10 @@ const char *tune_variant_name(int v)
                                  "rp_rpl8",      "ABL_rp_off0",     "ABL_stencil",  "ABL_stencil_clamp",
                                  "ABL_st_nonn",  "ABL_st_non",      "ABL_copy",     "ABL_copy3",
                                  "long_t64_r64",  "long_t256_r8",   "long_t256_r16", "long_t256_r32",
-                                 "long_t256_r64", "long_t128_r16", "long_t256_r256"};
-   return (v >= 0 && v < 42) ? names[v] : "?";
+                                 "long_t256_r64", "long_t128_r16", "long_t256_r256",
+                                 "ABL_copy_v2", "ABL_pair_st_v2", "ABL_copy_v4", "ABL_pair_st_v4",
+                                 "rpp_rpl1", "rpp_rpl2", "rpp_rpl4"};
+   return (v >= 0 && v < 49) ? names[v] : "?";
 }
 
 void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y)
@@ -1136,6 +1373,13 @@ void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x
    case 39: launch_long_cfg<0, false, 256, 64>(s, A, x, 0, A->nrows, EpiGemv{nullptr, y, 0, 0, 1.0, 0.0}); break;
    case 40: launch_long_cfg<0, false, 128, 16>(s, A, x, 0, A->nrows, EpiGemv{nullptr, y, 0, 0, 1.0, 0.0}); break;
    case 41: launch_long_cfg<0, false, 256, 256>(s, A, x, 0, A->nrows, EpiGemv{nullptr, y, 0, 0, 1.0, 0.0}); break;
+   case 42: abl_pair_k<0, 2><<<(A->nrows + 1023) / 1024, 256, 0, s>>>(x, A->nrows, y); break;
+   case 43: abl_pair_k<1, 2><<<(A->nrows + 1023) / 1024, 256, 0, s>>>(x, A->nrows, y); break;
+   case 44: abl_pair_k<0, 4><<<(A->nrows + 1023) / 1024, 256, 0, s>>>(x, A->nrows, y); break;
+   case 45: abl_pair_k<1, 4><<<(A->nrows + 1023) / 1024, 256, 0, s>>>(x, A->nrows, y); break;
+   case 46: launch_rpp<1>(s, A, x, y); break;
+   case 47: launch_rpp<2>(s, A, x, y); break;
+   case 48: launch_rpp<4>(s, A, x, y); break;
    default: break;
    }
 }
@@ -1908,6 +2152,36 @@ __global__ void rp_encode_k(const int *__restrict__ rowptr, const unsigned char 
       nbad += !ok;
    }
    if (nbad) atomicAdd(bad, nbad);
+}
+
+// row-pair keys p0 * 257 + p1 (p1 = 256 when row 2t+1 does not exist)
+__global__ void pp_collect_k(const unsigned char *__restrict__ rpat, int n, unsigned char *flags)
+{
+   const int np = (n + 1) / 2;
+   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < np; t += gridDim.x * blockDim.x) {
+      const int k = rpat[2 * t] * 257 + (2 * t + 1 < n ? rpat[2 * t + 1] : 256);
+      if (!flags[k]) flags[k] = 1;
+   }
+}
+
+__global__ void pp_encode_k(const unsigned char *__restrict__ rpat, int n, const unsigned char *__restrict__ map,
+                            unsigned char *__restrict__ ppat)
+{
+   const int np = (n + 1) / 2;
+   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < np; t += gridDim.x * blockDim.x)
+      ppat[t] = map[rpat[2 * t] * 257 + (2 * t + 1 < n ? rpat[2 * t + 1] : 256)];
+}
+
+void pp_collect(hipStream_t s, const amg_mat *A, unsigned char *flags)
+{
+   if (A->nrows <= 0) return;
+   pp_collect_k<<<std::min(8192, (A->nrows + 511) / 512), 256, 0, s>>>(A->rpat, A->nrows, flags);
+}
+
+void pp_encode(hipStream_t s, const amg_mat *A, const unsigned char *map, unsigned char *ppat)
+{
+   if (A->nrows <= 0) return;
+   pp_encode_k<<<std::min(8192, (A->nrows + 511) / 512), 256, 0, s>>>(A->rpat, A->nrows, map, ppat);
 }
 
 void rp_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int *rep, int nslots, int *count,

@@ -64,6 +64,7 @@ struct amg_hier {
    int iter = 0;
    bool have_state = false;
    bool pre_ready = false; // lv[0].u_alt holds u + w r0 / a_ii for the current u
+   bool r0_stale = false;  // reuse_outer_residual 2: r0 not written for the current u
    std::vector<void *> allocs;
    // profiling
    std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[PROF_NCAT];
@@ -326,7 +327,18 @@ extern "C" int amg_hier_vec(amg_hier *H, int which, int level, amg_vec **out)
    switch (which) {
    case AMG_VEC_F: v->d = H->lv[level].f; break;
    case AMG_VEC_U: v->d = H->lv[level].u; break;
-   case AMG_VEC_R: v->d = level == 0 ? H->r0 : H->lv[level].r_fine; break;
+   case AMG_VEC_R:
+      if (level == 0 && H->r0_stale) {
+         // the outer residual of the current iterate, in the order of the
+         // fused kernel that skipped it (reuse_outer_residual 2)
+         Level &l0 = H->lv[0];
+         amgk::spgemv(H->ctx->stream, l0.A, l0.u, l0.f, amgk::gemv_mode(-1.0, 1.0), H->r0, 0, l0.n,
+                      nullptr);
+         AMG_HIP(hipStreamSynchronize(H->ctx->stream));
+         H->r0_stale = false;
+      }
+      v->d = level == 0 ? H->r0 : H->lv[level].r_fine;
+      break;
    default: delete v; return amg_set_error(AMG_ERR_ARG, "amg_hier_vec: unknown vector %d", which);
    }
    *out = v;
@@ -581,12 +593,15 @@ static int outer_residual(amg_hier *H, int slot)
       ProfScope ps(H, PROF_OUTER, c->stream);
       if (reuse_applies(H)) {
          const bool l1 = (H->o.smoother == AMG_L1_JACOBI);
+         const bool skip_r = H->o.reuse_outer_residual >= 2;
          amgk::residual_jacobi(c->stream, v.A, v.f, v.u, l1 ? v.l1 : nullptr, H->o.smooth_weight,
-                               H->r0, v.u_alt, 0, v.n, p);
+                               skip_r ? nullptr : H->r0, v.u_alt, 0, v.n, p);
          H->pre_ready = true;
+         H->r0_stale = skip_r;
       } else {
          amgk::spgemv(c->stream, v.A, v.u, v.f, amgk::gemv_mode(-1.0, 1.0), H->r0, 0, v.n, p);
          H->pre_ready = false;
+         H->r0_stale = false;
       }
    }
    amgk::reduce_partials(c->stream, p, nb, H->d_hist + slot, 1, c->d_scalars + 4096);
@@ -733,6 +748,7 @@ int amg_hier_subcycle(amg_hier *H, hipStream_t, const double *f_dev, const doubl
    // only level is the coarsest and smooths its own f
    amgk::vcopy(H->ctx->stream, f_dev, H->L == 1 ? H->lv[0].f : H->r0, 0, H->lv[0].n);
    H->pre_ready = false;
+   H->r0_stale = false;
    vcycle(H, true, false);
    *u_dev = H->lv[0].u;
    AMG_HIP(hipGetLastError());
@@ -775,6 +791,7 @@ static int precond_apply(amg_hier *H, const double *fin, double *out)
       H->lv[l].zero_flag = 0;
    }
    amgk::vcopy(s, fin, H->r0, 0, H->lv[0].n);
+   H->r0_stale = false;
    vcycle(H, true, false);
    amgk::vcopy(s, H->lv[0].u, out, 0, H->lv[0].n);
    AMG_HIP(hipGetLastError());

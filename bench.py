@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--n", type=int, default=512)
     p.add_argument("--smooth-weight", type=float, default=0.8)
-    p.add_argument("--reuse-outer-residual", type=int, default=1)
+    p.add_argument("--reuse-outer-residual", type=int, default=2)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-cycles", type=int, default=20)
     p.add_argument("--spmv-reps", type=int, default=20)
@@ -44,11 +44,15 @@ def parse():
     return p.parse_args()
 
 
-def storage(nrows, nnz, vi, dc, rp):
+def storage(nrows, nnz, vi, dc, rp, pp=0):
     """(matrix bytes the hot kernels stream per pass, format name), DESIGN.md Sec.4:
-    row-pattern-coded CSR reads one byte per row; dictionary-coded one byte per
+    paired-row-pattern CSR reads one byte per pair of rows; row-pattern-coded
+    CSR one byte per row; dictionary-coded one byte per
     entry + the row pointer; value-indexed 4 (col) + 1 per entry + the row
     pointer; CSR 4 (col) + 8 (val) per entry + the row pointer."""
+    if pp:
+        return (nrows + 1) // 2, (f"csr-rpp ({pp} row-pair patterns over {rp} row patterns and a "
+                                  f"{dc}-entry (offset, value) dictionary)")
     if rp:
         return nrows, f"csr-rp ({rp} row patterns over a {dc}-entry (offset, value) dictionary)"
     if dc:
@@ -141,7 +145,8 @@ def main():
     n0 = As[0].nrows
     z0 = As[0].nnz
     # matrix bytes per pass in the format the kernels stream
-    mat_bytes, fmt = storage(n0, z0, As[0].value_index, As[0].dict_index, As[0].row_pattern)
+    mat_bytes, fmt = storage(n0, z0, As[0].value_index, As[0].dict_index, As[0].row_pattern,
+                                 As[0].pair_pattern)
     # dominant kernel: fine-grid residual SpGEMV r = f - A u (matrix + f, u, r)
     res_bytes = mat_bytes + 24 * n0
     res_ms = ms[0] / max(launches[0], 1)

@@ -90,7 +90,11 @@ typedef struct {
    int jgs_block_rows;           /* block size of the device partition (>=1)      */
    int reuse_outer_residual;     /* 1: the level-0 pre-smoother consumes the
                                     outer-loop residual f - A u already in r
-                                    (bit-identical; saves one A_0 pass/cycle)  */
+                                    (bit-identical; saves one A_0 pass/cycle);
+                                    2: as 1, and the outer residual vector r
+                                    (dead: the cycle overwrites it) is only
+                                    written on request -- amg_hier_vec(R, 0)
+                                    recomputes it from the current u        */
    int async_type;               /* AMG_FULL_ASYNC / AMG_SEMI_ASYNC               */
    int profile;                  /* 1: HIP-event timing of the fine-level kernels */
    int accel_type;               /* DMEM input.accel_type (distributed solves):
@@ -136,6 +140,14 @@ int amg_mat_dict_index(const amg_mat *A);
 int amg_set_row_pattern(amg_ctx *ctx, int enable);
 /* number of distinct row patterns of A (0: not row-pattern-coded) */
 int amg_mat_row_pattern(const amg_mat *A);
+/* paired-row-pattern storage (default on; env AMG_PAIR_PATTERN=0 disables),
+ * built at registration on top of the row patterns for square operators whose
+ * rows hold <= 8 entries: rows 2t and 2t+1 share one byte naming their merged
+ * entry list, and an entry both rows hold at the same column offset reads both
+ * x values with one 16-byte load (bit-identical results) */
+int amg_set_pair_pattern(amg_ctx *ctx, int enable);
+/* number of distinct row-pair patterns of A (0: not pair-coded) */
+int amg_mat_pair_pattern(const amg_mat *A);
 int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz);
 int amg_mat_download(amg_ctx *ctx, const amg_mat *A, int *rowptr, int *col, double *val);
 

@@ -132,6 +132,18 @@ def test_value_index_selection(mats):
     assert dev["lap_hole"].dict_index == 7 and dev["lap_hole"].row_pattern == 0
     for name in ("A1", "P0", "R0"):
         assert dev[name].row_pattern > 0, name
+    # paired rows: square, anchor = row, rows of <= 8 entries, <= 256 distinct
+    # (pattern of row 2t, pattern of row 2t+1) pairs
+    for name in ALL:
+        A = host[name]
+        short = np.diff(A.rowptr).max() <= 8 if A.nrows else False
+        if dev[name].row_pattern and A.nrows == A.ncols and short and name not in ("P0", "P1", "R0", "R1"):
+            assert dev[name].pair_pattern > 0, name
+        elif not dev[name].row_pattern or not short or A.nrows != A.ncols:
+            assert dev[name].pair_pattern == 0, name
+    # 16^3 (x even): pairs (x=0,1), (2k,2k+1) interior, (14,15) times 9 (y,z) classes
+    assert dev["lap16"].pair_pattern == 27
+    assert dev["lap_rect"].pair_pattern > 0 and dev["lap_rect"].nrows % 2 == 1
 
 
 @pytest.mark.parametrize("name", ["lap16", "lap_rect", "A1", "rand_q", "longrows_q", "P0", "R1",
@@ -150,12 +162,16 @@ def test_value_index_matches_plain(mats, ctx, amg, name):
     ctx.set_row_pattern(0)
     dc_only = ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val)
     ctx.set_row_pattern(1)
+    ctx.set_pair_pattern(0)
+    rp_only = ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val)
+    ctx.set_pair_pattern(1)
     assert plain.value_index == 0 and dev[name].value_index > 0 and vi_only.dict_index == 0
     assert dc_only.row_pattern == 0 and dc_only.dict_index == dev[name].dict_index
+    assert rp_only.pair_pattern == 0 and rp_only.row_pattern == dev[name].row_pattern
     x = ctx.vec(_vecs(A.ncols, 5))
     b = ctx.vec(_vecs(A.nrows, 6))
     outs = []
-    variants = (plain, vi_only, dc_only, dev[name])
+    variants = (plain, vi_only, dc_only, rp_only, dev[name])
     for M in variants:
         y = ctx.vec(A.nrows)
         amg.smem.SMEM_SpGEMV(ctx, M, x, b, -1.0, 1.0, y, 0, A.nrows)
@@ -171,6 +187,48 @@ def test_value_index_matches_plain(mats, ctx, amg, name):
     plain.free()
     vi_only.free()
     dc_only.free()
+    rp_only.free()
+
+
+@pytest.mark.parametrize("name", ["lap16", "lap_rect"])
+@pytest.mark.parametrize("rng_", [(0, 0), (2, -5), (4, -4), (3, -6), (0, -1), (6, -2)])
+def test_pair_pattern_row_ranges(mats, ctx, oracle, amg, name, rng_):
+    """Paired-row kernel on row slices: even starts run paired (an odd end
+    leaves a half pair), odd starts the single-row kernel; residual, SpGEMV,
+    Jacobi and L1 Jacobi bit-identical to the oracle, rows outside untouched."""
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    assert dA.pair_pattern > 0
+    ns, ne = rng_[0], A.nrows + rng_[1]
+    x, b = _vecs(A.ncols, 40), _vecs(A.nrows, 41)
+    y0, r0 = _vecs(A.nrows, 42), _vecs(A.nrows, 43)
+    ry, rr = y0.copy(), r0.copy()
+    oracle.smem_residual(A, b, x, ry, rr, ns, ne)
+    y, r = ctx.vec(y0), ctx.vec(r0)
+    amg.smem.SMEM_Residual(ctx, dA, ctx.vec(b), ctx.vec(x), y, r, ns, ne)
+    assert_bitwise(y.download(), ry, "y")
+    assert_bitwise(r.download(), rr, "r")
+    for ab in ((1.0, 0.0), (-1.0, 1.0), (2.5, -0.5), (-1.0, 0.7)):
+        ref = y0.copy()
+        oracle.smem_spgemv(A, x, b, ab[0], ab[1], ref, ns, ne)
+        dy = ctx.vec(y0)
+        amg.smem.SMEM_SpGEMV(ctx, dA, ctx.vec(x), ctx.vec(b), ab[0], ab[1], dy, ns, ne)
+        assert_bitwise(dy.download(), ref, f"spgemv {ab}")
+    # amg_jacobi copies the whole u to u_prev (the team's slices together);
+    # the oracle's single slice copies only [ns, ne): start u_prev = u
+    for zero in (0, 1):
+        ru, rp = y0.copy(), y0.copy()
+        oracle.smem_jacobi(A, b, ru, rp, 0.8, 2, zero, ns, ne)
+        du, dp = ctx.vec(y0), ctx.vec(A.nrows)
+        amg.smem.SMEM_Sync_Jacobi(ctx, dA, ctx.vec(b), du, dp, 2, zero, 0.8, ns, ne)
+        assert_bitwise(du.download(), ru, f"jacobi zero={zero}")
+    l1 = oracle.l1_norms(A)
+    ru, rp = y0.copy(), y0.copy()
+    oracle.smem_l1jacobi(A, b, ru, rp, l1, 2, 0, ns, ne)
+    du, dp = ctx.vec(y0), ctx.vec(A.nrows)
+    check = amg.check
+    check(amg.lib.amg_l1_jacobi(ctx.h, dA.h, ctx.vec(b).h, du.h, dp.h, ctx.vec(l1).h, 2, 0, ns, ne, 0))
+    assert_bitwise(du.download(), ru, "l1 jacobi")
 
 
 @pytest.mark.parametrize("name", ALL)

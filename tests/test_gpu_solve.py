@@ -145,6 +145,39 @@ def test_reuse_outer_residual_is_bit_identical(amg, oracle, ctx):
         compare_solve(amg, oracle, ctx, host, opts, f)
 
 
+def test_pair_pattern_and_dead_residual_bit_identical(amg, oracle, ctx):
+    """The 7-pt fine operators run paired-row (16^3: even rows per line; 15^3:
+    odd n, a half pair at the end); with pairing off (single-row kernel) and
+    with reuse_outer_residual 2 (outer residual vector not written) the
+    iterate and the residual-norm history are bitwise the same, and the
+    residual vector amg_hier_vec(R, 0) recomputed on request matches the
+    oracle's r = f - A u of the final iterate."""
+    for n in (16, 15):
+        _, L, host = hierarchy(amg, oracle, n, amg.AMG_INTERP_LINEAR)
+        f = amg.rhs_rand(0, n ** 3)
+        runs = []
+        for pair, reuse, sm in ((1, 0, amg.AMG_JACOBI), (0, 0, amg.AMG_JACOBI), (1, 1, amg.AMG_JACOBI),
+                                (1, 2, amg.AMG_JACOBI), (0, 2, amg.AMG_JACOBI),
+                                (1, 2, amg.AMG_L1_JACOBI), (1, 0, amg.AMG_L1_JACOBI)):
+            ctx.set_pair_pattern(pair)
+            opts = amg.default_opts(smoother=sm, smooth_weight=0.8, num_cycles=8, tol=0.0,
+                                    reuse_outer_residual=reuse)
+            H, dev = gpu_hier(amg, ctx, host, opts)
+            ctx.set_pair_pattern(1)
+            assert (dev["A"][0].pair_pattern > 0) == bool(pair)
+            u, h, k = H.solve(f)
+            r = H.vec(amg.AMG_VEC_R, 0).download()
+            # SMEM_Sync_Residual = SpGEMV(alpha -1, beta 1): r_i = f_i - a_i1 u_1 - ...
+            rr = oracle.smem_spgemv(host["A"][0], u, f, -1.0, 1.0, np.zeros(n ** 3))
+            assert_bitwise(r, rr, f"outer residual pair={pair} reuse={reuse}")
+            runs.append((sm, u, h))
+            H.free()
+        for sm, u, h in runs[1:]:
+            base = [x for x in runs if x[0] == sm][0]
+            assert_bitwise(u, base[1], "iterate")
+            assert_bitwise(h, base[2], "residual history")
+
+
 def test_cheby_accelerated(amg, oracle, ctx):
     _, L, host = hierarchy(amg, oracle, 16, amg.AMG_INTERP_LINEAR)
     base = amg.default_opts(smooth_weight=0.8, num_cycles=10, tol=0.0)
