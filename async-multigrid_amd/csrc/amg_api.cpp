@@ -75,7 +75,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_VALUE_INDEX")) c->value_index = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_DICT_INDEX")) c->dict_index = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_ROW_PATTERN")) c->row_pattern = std::atoi(v) != 0;
-   if (const char *v = std::getenv("AMG_PAIR_PATTERN")) c->pair_pattern = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_PAIR_PATTERN")) c->pair_pattern = std::min(2, std::max(0, std::atoi(v)));
    *out = c;
    return AMG_OK;
 }
@@ -381,6 +381,7 @@ static int build_pair_pattern(amg_mat *A)
    AMG_HIP(hipStreamSynchronize(s));
    std::vector<unsigned char> hm(NK, 0);
    std::vector<unsigned int> tab;
+   const int PS = amg_pp_stride(A->dc_maxrow);
    int T = 0;
    for (int k = 0; k < NK && T <= 256; k++) {
       if (!hf[k]) continue;
@@ -397,13 +398,19 @@ static int build_pair_pattern(amg_mat *A)
       } else {
          for (int j = 0; j < a[0]; j++) el.push_back(a[1 + j] | 1u << 16);
       }
-      std::vector<unsigned int> w(AMG_PP_STRIDE, 0);
-      w[0] = (unsigned)el.size() | (p1 < 256 ? 1u << 24 : 0u);
+      // header: nel | first dictionary entry of row 2t << 8 | of row 2t+1 << 16
+      // | row 2t+1 present << 24 | (merged entry at offset 0 of both rows) + 1 << 25
+      unsigned int centre = 0;
+      for (size_t e = 0; e < el.size() && !centre; e++)
+         if ((el[e] >> 16 & 3) == 3 && off[el[e] & 0xff] == 0) centre = (unsigned)e + 1;
+      std::vector<unsigned int> w(PS, 0);
+      w[0] = (unsigned)el.size() | (unsigned)a[1] << 8 |
+             (p1 < 256 ? (unsigned)pt[p1 * AMG_RP_STRIDE + 1] << 16 | 1u << 24 : 0u) | centre << 25;
       for (size_t e = 0; e < el.size(); e++) w[1 + e] = el[e];
       tab.insert(tab.end(), w.begin(), w.end());
       hm[k] = (unsigned char)T++;
    }
-   if (T < 1 || T > 256) {
+   if (T < 1 || T > 256 || (size_t)T * PS * 4 > (size_t)AMG_PP_LDS) {
       hipFree(flags);
       return AMG_OK;
    }
@@ -425,6 +432,7 @@ static int build_pair_pattern(amg_mat *A)
    AMG_HIP(hipStreamSynchronize(s));
    hipFree(flags);
    A->pp_n = T;
+   A->pp_stride = PS;
    return AMG_OK;
 }
 
@@ -436,7 +444,8 @@ int amg_mat_finish(amg_mat *A)
    if (A->ctx->dict_index && A->vidx) AMG_TRY(build_dict_index(A));
    if (A->ctx->row_pattern && A->didx) AMG_TRY(build_row_pattern(A));
    if (A->ctx->pair_pattern && A->rpat && !A->danch && A->nrows == A->ncols &&
-       A->dc_maxrow <= AMG_PP_MAXROW)
+       A->dc_maxrow <= AMG_PP_MAXROW &&
+       (A->dc_maxrow <= 8 || A->nrows >= AMG_PP_LONG_MIN_ROWS || A->ctx->pair_pattern == 2))
       AMG_TRY(build_pair_pattern(A));
    return AMG_OK;
 }
@@ -456,7 +465,7 @@ extern "C" int amg_mat_row_pattern(const amg_mat *A)
 extern "C" int amg_set_pair_pattern(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_pair_pattern: null context");
-   c->pair_pattern = enable ? 1 : 0;
+   c->pair_pattern = enable < 0 ? 0 : enable > 2 ? 2 : enable;
    return AMG_OK;
 }
 

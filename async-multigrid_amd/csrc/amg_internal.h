@@ -45,10 +45,19 @@ constexpr int AMG_NNZ_PAD = 8;
 constexpr int AMG_DC_MAXROW = 32;
 // bytes per row pattern of the row-pattern-coded form: length + entries (x4 aligned)
 constexpr int AMG_RP_STRIDE = 36;
-// paired row patterns (rows 2t, 2t+1 of operators whose rows hold <= 8
-// entries): one header word + up to 16 merged entry words per pair pattern
-constexpr int AMG_PP_MAXROW = 8;
-constexpr int AMG_PP_STRIDE = 1 + 2 * AMG_PP_MAXROW;
+// paired row patterns (rows 2t, 2t+1 of operators whose rows hold <= 32
+// entries): one header word + up to 2 * maxrow merged entry words per pair
+// pattern, maxrow = 8 (7-pt) or 32 (27-pt Galerkin); the table must fit
+// AMG_PP_LDS bytes of LDS
+constexpr int AMG_PP_MAXROW = 32;
+constexpr int AMG_PP_LDS = 32 * 1024;
+// rows of > 8 entries are pair-coded from this size up (a pair lane walks
+// twice the entries: latency-bound grids below it run faster one row per lane)
+constexpr int AMG_PP_LONG_MIN_ROWS = 1 << 22;
+inline int amg_pp_stride(int maxrow) { return 1 + 2 * (maxrow <= 8 ? 8 : AMG_PP_MAXROW); }
+// paired kernel epilogue form (csr_rpp_kernel OPT, tools/tune_spmv.py ABL_jac_o*):
+// a_ii from the header word, x[i] from its own load
+constexpr int AMG_RPP_OPT = 2;
 
 struct amg_transport; // amg_dist.cpp: RCCL communicator or host-callback test transport
 
@@ -67,7 +76,7 @@ struct amg_ctx {
    int value_index = 1; // build value-indexed CSR for matrices with <= 256 distinct values
    int dict_index = 1;  // build dictionary-coded CSR for stencil-like square operators
    int row_pattern = 1; // build row-pattern-coded CSR on top of the dictionary
-   int pair_pattern = 1; // build paired-row-pattern CSR on top of the row patterns
+   int pair_pattern = 1; // paired-row-pattern CSR: 0 off, 1 size-gated for long rows, 2 always
 };
 
 struct amg_mat {
@@ -103,7 +112,7 @@ struct amg_mat {
    int rp_n = 0;
    // paired-row-pattern form (square operators, anchor = row, rows of <= 8
    // entries, <= 256 distinct (pattern of row 2t, pattern of row 2t+1) pairs):
-   // ppat[t] names the pair's merged entry list in pptab (AMG_PP_STRIDE words
+   // ppat[t] names the pair's merged entry list in pptab (pp_stride words
    // per pair: header nel | row1 present << 24, then entries
    // d0 | d1 << 8 | has0 << 16 | has1 << 17).  An entry present in both rows
    // has one column offset: the kernel reads x[2t + off], x[2t + 1 + off] with
@@ -111,6 +120,7 @@ struct amg_mat {
    unsigned char *ppat = nullptr;
    unsigned int *pptab = nullptr;
    int pp_n = 0;
+   int pp_stride = 0; // words per pair pattern (amg_pp_stride)
 };
 
 struct amg_vec {

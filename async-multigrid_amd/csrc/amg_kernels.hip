@@ -503,26 +503,58 @@ __global__ __launch_bounds__(256) void csr_rp_kernel(
 }
 
 // Paired-row-pattern kernel: lane owns the row pair (2t, 2t+1) and reads the
-// pair's merged entry list (AMG_PP_STRIDE words in LDS).  An entry both rows
+// pair's merged entry list (ps words in LDS).  An entry both rows
 // hold at the same column offset o reads x[2t+o] and x[2t+1+o] with ONE
 // 16-byte load (half the vector-memory instructions of one lane per row,
 // which bounds the single-row kernel: DESIGN.md Sec.4); an entry of one row
 // alone reads its x value by itself.  Each row still sums its own entries in
 // its CSR order (the merge keeps both orders), so results are bit-identical.
-// Workgroup slab q covers 512 rows = two 256-row norm tiles, reduced in the
-// single-row kernel's lane order through LDS.  rb must be even.
-template <int NEG, bool NEED_DIAG, class Epi, int RPL>
+// The header word carries each row's first dictionary entry (a_ii, no scan)
+// and the merged entry at offset 0 of both rows: when the epilogue's own
+// operand is x[i] (Jacobi forms) it comes from that gather, not a second load.
+// Workgroup slab q covers 512 rows = two 256-row norm tiles; the tiles' sums
+// are reduced after every slab is done (no barrier between slabs), in the
+// single-row kernel's lane order.  rb must be even.
+struct EpiJacobi;
+struct EpiL1Jacobi;
+struct EpiResJacobi;
+template <class Epi>
+struct pf_is_x {
+   static constexpr bool value = false;
+};
+// the epilogue's prefetched operand vector (found by ADL at instantiation)
+template <class Epi>
+__device__ __forceinline__ const double *epi_pf_vec(const Epi &)
+{
+   return nullptr;
+}
+template <>
+struct pf_is_x<EpiJacobi> {
+   static constexpr bool value = true;
+};
+template <>
+struct pf_is_x<EpiL1Jacobi> {
+   static constexpr bool value = true;
+};
+template <>
+struct pf_is_x<EpiResJacobi> {
+   static constexpr bool value = true;
+};
+
+// OPT bit 0: take the Jacobi operand x[i] from the centre gather; bit 1: a_ii
+// from the header (else scanned from the entry list)
+template <int NEG, bool NEED_DIAG, class Epi, int RPL, int OPT = AMG_RPP_OPT>
 __global__ __launch_bounds__(256) void csr_rpp_kernel(
    const unsigned char *__restrict__ ppat, const unsigned int *__restrict__ pptab_g, int np,
    const int *__restrict__ doff_g, const double *__restrict__ dval_g, const double *__restrict__ x,
-   int rb, int re, Epi epi, double *__restrict__ partials, int T)
+   int rb, int re, Epi epi, double *__restrict__ partials, int T, int PS)
 {
-   constexpr int PS = AMG_PP_STRIDE;
+   constexpr bool PFX = pf_is_x<Epi>::value && (OPT & 1);
    __shared__ int otab[256];
    __shared__ double vtab[256];
    extern __shared__ unsigned int ptab[]; // np * PS words (dynamic)
-   __shared__ double sqs[512];
-   __shared__ double red[4];
+   __shared__ double sqs[RPL * 512];
+   __shared__ double red[RPL * 8];
    const int tid = (int)threadIdx.x;
    if (tid < T) {
       otab[tid] = doff_g[tid];
@@ -530,6 +562,8 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
    }
    for (int w = tid; w < np * PS; w += 256) ptab[w] = pptab_g[w];
    const int wg = (int)blockIdx.x;
+   // the epilogue operand is the gathered vector itself (uniform test)
+   const bool xc_ok = PFX && epi_pf_vec(epi) == x;
    int pid[RPL];
 #pragma unroll
    for (int q = 0; q < RPL; q++) {
@@ -537,24 +571,26 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
       pid[q] = row < re ? ppat[row >> 1] : 0;
    }
    __syncthreads();
+   double sq[RPL][2];
 #pragma unroll
    for (int q = 0; q < RPL; q++) {
       const int s0 = rb + (wg * RPL + q) * 512;
       const int row = s0 + 2 * tid;
       const bool a0 = row < re, a1 = row + 1 < re;
-      double sq0 = 0.0, sq1 = 0.0;
+      sq[q][0] = sq[q][1] = 0.0;
       if (a0) {
          const unsigned int *pp = ptab + pid[q] * PS;
-         const int nel = pp[0] & 0xff;
-         v2d acc, pf;
+         const unsigned int hd = pp[0];
+         const int nel = hd & 0xff;
+         const int ci = xc_ok ? (int)(hd >> 25) : 0; // centre entry + 1 (0: none)
+         v2d acc, pf{0.0, 0.0};
          if (a1) {
             acc = epi.init2(row);
-            pf = epi.pf2(row);
+            if (ci == 0) pf = epi.pf2(row);
          } else {
             acc = v2d{epi.init(row), 0.0};
-            pf = v2d{epi.pf(row), 0.0};
+            if (ci == 0) pf = v2d{epi.pf(row), 0.0};
          }
-         double dg0 = 0.0, dg1 = 0.0;
          for (int k = 0; k < nel; k += 8) {
             const int m = nel - k;
             v2d xv[8];
@@ -579,6 +615,7 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
             for (int j = 0; j < 8; j++)
                if (j < m) {
                   const unsigned int w = ew[j];
+                  if (PFX && k + j + 1 == ci) pf = xv[j];
                   if (w >> 16 & 1) {
                      const double v = vtab[w & 0xff];
                      if (NEG)
@@ -595,8 +632,12 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
                   }
                }
          }
-         if (NEED_DIAG) {
-            // a_ii := A_data[A_i[i]]: each row's first entry in the merged list
+         // a_ii := A_data[A_i[i]]: each row's first dictionary entry
+         double dg0 = 0.0, dg1 = 0.0;
+         if (NEED_DIAG && (OPT & 2)) {
+            dg0 = vtab[(hd >> 8) & 0xff];
+            dg1 = a1 ? vtab[(hd >> 16) & 0xff] : 0.0;
+         } else if (NEED_DIAG) {
             bool f0 = false, f1 = false;
             for (int e = 0; e < nel && !(f0 && f1); e++) {
                const unsigned int w = pp[1 + e];
@@ -612,24 +653,35 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
          }
          if (a1) {
             const v2d out = epi.finish2(row, acc, v2d{dg0, dg1}, pf);
-            sq0 = out.x * out.x;
-            sq1 = out.y * out.y;
+            sq[q][0] = out.x * out.x;
+            sq[q][1] = out.y * out.y;
          } else {
             const double out = epi.finish(row, acc.x, dg0, pf.x);
-            sq0 = out * out;
+            sq[q][0] = out * out;
          }
       }
-      if (partials) {
-         // the 256-row tiles' sums in the single-row kernel's lane order
-         sqs[2 * tid] = sq0;
-         sqs[2 * tid + 1] = sq1;
-         __syncthreads();
+   }
+   if (partials) {
+      // the 256-row tiles' sums in block_sum_256's order (single-row kernel)
 #pragma unroll
-         for (int h = 0; h < 2; h++) {
-            const double sblk = block_sum_256(sqs[h * 256 + tid], red);
-            if (tid == 0 && s0 + h * 256 < re) partials[(s0 - rb) / 256 + h] = sblk;
-         }
-         __syncthreads();
+      for (int q = 0; q < RPL; q++) {
+         sqs[q * 512 + 2 * tid] = sq[q][0];
+         sqs[q * 512 + 2 * tid + 1] = sq[q][1];
+      }
+      __syncthreads();
+      const int lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+      for (int h = 0; h < 2 * RPL; h++) {
+         double v = sqs[h * 256 + tid];
+#pragma unroll
+         for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+         if (lane == 0) red[h * 4 + wid] = v;
+      }
+      __syncthreads();
+      if (tid < 2 * RPL) {
+         const int tile = wg * RPL * 2 + tid;
+         if (rb + tile * 256 < re)
+            partials[tile] = ((red[tid * 4] + red[tid * 4 + 1]) + red[tid * 4 + 2]) + red[tid * 4 + 3];
       }
    }
 }
@@ -643,8 +695,8 @@ static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int r
                          const Epi &e, double *partials, int tiles)
 {
    if (A->ppat && (rb & 1) == 0)
-      csr_rpp_kernel<NEG, NEED_DIAG, Epi, 2><<<(re - rb + 1023) / 1024, 256, A->pp_n * AMG_PP_STRIDE * 4, s>>>(
-         A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n);
+      csr_rpp_kernel<NEG, NEED_DIAG, Epi, 2><<<(re - rb + 1023) / 1024, 256, A->pp_n * A->pp_stride * 4, s>>>(
+         A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->pp_stride);
    else if (A->rpat && A->dc_maxrow <= 8)
       csr_rp_kernel<NEG, NEED_DIAG, Epi, 4><<<(tiles + 3) / 4, 256, 0, s>>>(
          A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
@@ -917,6 +969,10 @@ struct EpiResJacobi {
    }
 };
 
+__device__ __forceinline__ const double *epi_pf_vec(const EpiJacobi &e) { return e.x; }
+__device__ __forceinline__ const double *epi_pf_vec(const EpiL1Jacobi &e) { return e.x; }
+__device__ __forceinline__ const double *epi_pf_vec(const EpiResJacobi &e) { return e.x; }
+
 template <class Cfg>
 static inline int cfg_blocks(int rb, int re)
 {
@@ -1141,7 +1197,7 @@ __global__ __launch_bounds__(256) void ablation_kernel(const int *__restrict__ r
    if (row < r1) y[row] = acc;
 }
 
-int num_tune_variants() { return 49; }
+int num_tune_variants() { return 53; }
 
 template <int RPL, bool STAGE, int MAXR = AMG_DC_MAXROW>
 static void launch_dc(hipStream_t s, const amg_mat *A, const double *x, double *y)
@@ -1171,8 +1227,20 @@ static void launch_rpp(hipStream_t s, const amg_mat *A, const double *x, double 
    EpiGemv e{nullptr, y, 0, 0, 1.0, 0.0};
    if (!A->ppat) return;
    const int nt = (A->nrows + 512 * RPL - 1) / (512 * RPL);
-   csr_rpp_kernel<0, false, EpiGemv, RPL><<<nt, 256, A->pp_n * AMG_PP_STRIDE * 4, s>>>(A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x,
-                                                             0, A->nrows, e, nullptr, A->dc_n);
+   csr_rpp_kernel<0, false, EpiGemv, RPL><<<nt, 256, A->pp_n * A->pp_stride * 4, s>>>(
+      A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride);
+}
+
+// Jacobi sweep y = x + w (x - A x)/a_ii through the paired kernel, OPT as
+// csr_rpp_kernel (timing of the epilogue forms; f = x)
+template <int OPT>
+static void launch_rpp_jac(hipStream_t s, const amg_mat *A, const double *x, double *y)
+{
+   EpiJacobi e{x, x, y, 0.8};
+   if (!A->ppat) return;
+   const int nt = (A->nrows + 1023) / 1024;
+   csr_rpp_kernel<1, true, EpiJacobi, 2, OPT><<<nt, 256, A->pp_n * A->pp_stride * 4, s>>>(
+      A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride);
 }
 
 // ablations of the row-pattern kernel on the 512^3 operator (timing only):
@@ -1291,8 +1359,9 @@ const char *tune_variant_name(int v)
                                  "long_t64_r64",  "long_t256_r8",   "long_t256_r16", "long_t256_r32",
                                  "long_t256_r64", "long_t128_r16", "long_t256_r256",
                                  "ABL_copy_v2", "ABL_pair_st_v2", "ABL_copy_v4", "ABL_pair_st_v4",
-                                 "rpp_rpl1", "rpp_rpl2", "rpp_rpl4"};
-   return (v >= 0 && v < 49) ? names[v] : "?";
+                                 "rpp_rpl1", "rpp_rpl2", "rpp_rpl4",
+                                 "ABL_jac_o0", "ABL_jac_o1", "ABL_jac_o2", "ABL_jac_o3"};
+   return (v >= 0 && v < 53) ? names[v] : "?";
 }
 
 void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y)
@@ -1380,6 +1449,10 @@ void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x
    case 46: launch_rpp<1>(s, A, x, y); break;
    case 47: launch_rpp<2>(s, A, x, y); break;
    case 48: launch_rpp<4>(s, A, x, y); break;
+   case 49: launch_rpp_jac<0>(s, A, x, y); break;
+   case 50: launch_rpp_jac<1>(s, A, x, y); break;
+   case 51: launch_rpp_jac<2>(s, A, x, y); break;
+   case 52: launch_rpp_jac<3>(s, A, x, y); break;
    default: break;
    }
 }

@@ -142,9 +142,12 @@ int amg_set_row_pattern(amg_ctx *ctx, int enable);
 int amg_mat_row_pattern(const amg_mat *A);
 /* paired-row-pattern storage (default on; env AMG_PAIR_PATTERN=0 disables),
  * built at registration on top of the row patterns for square operators whose
- * rows hold <= 8 entries: rows 2t and 2t+1 share one byte naming their merged
+ * rows hold <= 32 entries: rows 2t and 2t+1 share one byte naming their merged
  * entry list, and an entry both rows hold at the same column offset reads both
- * x values with one 16-byte load (bit-identical results) */
+ * x values with one 16-byte load (bit-identical results).  enable = 1 builds
+ * it for rows of <= 8 entries at any size and for longer rows (27-pt Galerkin
+ * levels) only from 4M rows up, where the pair's longer latency per lane is
+ * hidden; enable = 2 builds it whenever it applies (tests). */
 int amg_set_pair_pattern(amg_ctx *ctx, int enable);
 /* number of distinct row-pair patterns of A (0: not pair-coded) */
 int amg_mat_pair_pattern(const amg_mat *A);

@@ -87,7 +87,13 @@ def matrices(oracle, amg):
 @pytest.fixture(scope="module")
 def mats(oracle, amg, ctx):
     host = matrices(oracle, amg)
+    ctx.set_pair_pattern(2)  # pair-code long rows at any size (the default gates them by size)
     dev = {k: ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val) for k, A in host.items()}
+    ctx.set_pair_pattern(1)
+    # the default builds no long-row pairs below 4M rows
+    A1 = ctx.csr(host["A1"].nrows, host["A1"].ncols, host["A1"].rowptr, host["A1"].col, host["A1"].val)
+    assert A1.row_pattern > 0 and A1.pair_pattern == 0
+    A1.free()
     return host, dev
 
 
@@ -132,17 +138,29 @@ def test_value_index_selection(mats):
     assert dev["lap_hole"].dict_index == 7 and dev["lap_hole"].row_pattern == 0
     for name in ("A1", "P0", "R0"):
         assert dev[name].row_pattern > 0, name
-    # paired rows: square, anchor = row, rows of <= 8 entries, <= 256 distinct
-    # (pattern of row 2t, pattern of row 2t+1) pairs
+    # paired rows: square, anchor = row, rows of <= 32 entries, <= 256 distinct
+    # (pattern of row 2t, pattern of row 2t+1) pairs whose table (17 words per
+    # pair for rows of <= 8 entries, 65 for <= 32) fits 32 KiB of LDS
     for name in ALL:
         A = host[name]
-        short = np.diff(A.rowptr).max() <= 8 if A.nrows else False
-        if dev[name].row_pattern and A.nrows == A.ncols and short and name not in ("P0", "P1", "R0", "R1"):
-            assert dev[name].pair_pattern > 0, name
-        elif not dev[name].row_pattern or not short or A.nrows != A.ncols:
+        if not dev[name].row_pattern or A.nrows != A.ncols or A.nrows == 0:
             assert dev[name].pair_pattern == 0, name
+            continue
+        lens = np.diff(A.rowptr)
+        anchored = bool(np.all(A.col[A.rowptr[:-1]] == np.arange(A.nrows)))
+        pat = []
+        for i in range(A.nrows):
+            c = A.col[A.rowptr[i]:A.rowptr[i + 1]].astype(np.int64)
+            v = A.val[A.rowptr[i]:A.rowptr[i + 1]].view(np.int64)
+            pat.append(tuple((c - c[0]).tolist()) + tuple(v.tolist()))
+        pairs = {(pat[2 * t], pat[2 * t + 1] if 2 * t + 1 < A.nrows else None)
+                 for t in range((A.nrows + 1) // 2)}
+        stride = 17 if lens.max() <= 8 else 65
+        ok = anchored and lens.max() <= 32 and len(pairs) <= 256 and len(pairs) * stride * 4 <= 32768
+        assert dev[name].pair_pattern == (len(pairs) if ok else 0), (name, len(pairs), dev[name].pair_pattern)
     # 16^3 (x even): pairs (x=0,1), (2k,2k+1) interior, (14,15) times 9 (y,z) classes
     assert dev["lap16"].pair_pattern == 27
+    assert dev["A1"].pair_pattern > 0  # the 27-pt Galerkin operator
     assert dev["lap_rect"].pair_pattern > 0 and dev["lap_rect"].nrows % 2 == 1
 
 
@@ -190,7 +208,7 @@ def test_value_index_matches_plain(mats, ctx, amg, name):
     rp_only.free()
 
 
-@pytest.mark.parametrize("name", ["lap16", "lap_rect"])
+@pytest.mark.parametrize("name", ["lap16", "lap_rect", "A1"])
 @pytest.mark.parametrize("rng_", [(0, 0), (2, -5), (4, -4), (3, -6), (0, -1), (6, -2)])
 def test_pair_pattern_row_ranges(mats, ctx, oracle, amg, name, rng_):
     """Paired-row kernel on row slices: even starts run paired (an odd end

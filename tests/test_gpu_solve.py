@@ -146,7 +146,8 @@ def test_reuse_outer_residual_is_bit_identical(amg, oracle, ctx):
 
 
 def test_pair_pattern_and_dead_residual_bit_identical(amg, oracle, ctx):
-    """The 7-pt fine operators run paired-row (16^3: even rows per line; 15^3:
+    """The 7-pt fine operators (and with the size gate off the 27-pt coarse
+    ones) run paired-row (16^3: even rows per line; 15^3:
     odd n, a half pair at the end); with pairing off (single-row kernel) and
     with reuse_outer_residual 2 (outer residual vector not written) the
     iterate and the residual-norm history are bitwise the same, and the
@@ -156,15 +157,17 @@ def test_pair_pattern_and_dead_residual_bit_identical(amg, oracle, ctx):
         _, L, host = hierarchy(amg, oracle, n, amg.AMG_INTERP_LINEAR)
         f = amg.rhs_rand(0, n ** 3)
         runs = []
-        for pair, reuse, sm in ((1, 0, amg.AMG_JACOBI), (0, 0, amg.AMG_JACOBI), (1, 1, amg.AMG_JACOBI),
-                                (1, 2, amg.AMG_JACOBI), (0, 2, amg.AMG_JACOBI),
-                                (1, 2, amg.AMG_L1_JACOBI), (1, 0, amg.AMG_L1_JACOBI)):
+        # pair 2: the 27-pt coarse levels pair-coded too (size gate off)
+        for pair, reuse, sm in ((1, 0, amg.AMG_JACOBI), (0, 0, amg.AMG_JACOBI), (2, 1, amg.AMG_JACOBI),
+                                (1, 2, amg.AMG_JACOBI), (0, 2, amg.AMG_JACOBI), (2, 2, amg.AMG_JACOBI),
+                                (2, 2, amg.AMG_L1_JACOBI), (1, 0, amg.AMG_L1_JACOBI)):
             ctx.set_pair_pattern(pair)
             opts = amg.default_opts(smoother=sm, smooth_weight=0.8, num_cycles=8, tol=0.0,
                                     reuse_outer_residual=reuse)
             H, dev = gpu_hier(amg, ctx, host, opts)
             ctx.set_pair_pattern(1)
             assert (dev["A"][0].pair_pattern > 0) == bool(pair)
+            assert (dev["A"][1].pair_pattern > 0) == (pair == 2)
             u, h, k = H.solve(f)
             r = H.vec(amg.AMG_VEC_R, 0).download()
             # SMEM_Sync_Residual = SpGEMV(alpha -1, beta 1): r_i = f_i - a_i1 u_1 - ...

@@ -41,8 +41,9 @@ def pick(rows, pattern, grid=None):
         m = re.search(pattern, name)
         if not m:
             continue
-        rpl = re.search(r"csr_(?:dc|rp)_kernel<\d, \w+, [\w:]+, (\d+)[,>]", name)
-        rows_done = g * (int(rpl.group(1)) if rpl else 1)
+        rpl = re.search(r"csr_(dc|rp|rpp)_kernel<\d, \w+, [\w:]+, (\d+)[,>]", name)
+        # a paired-row-pattern lane owns two rows
+        rows_done = g * (int(rpl.group(2)) * (2 if rpl.group(1) == "rpp" else 1) if rpl else 1)
         if grid is None or rows_done == grid:
             out += vals
     return out
@@ -59,8 +60,9 @@ def main():
     rows = n ** 3
     z = 7 * rows - 6 * n * n
     res = {}
-    for fmt, vi in (("csr-rp", "rp"), ("csr-dc", "dc"), ("csr-vi", "true"), ("csr", "false")):
-        pat = {"rp": r"csr_rp_kernel<1, false, amgk::EpiGemv,",
+    for fmt, vi in (("csr-rpp", "rpp"), ("csr-rp", "rp"), ("csr-dc", "dc"), ("csr-vi", "true"), ("csr", "false")):
+        pat = {"rpp": r"csr_rpp_kernel<1, false, amgk::EpiGemv,",
+               "rp": r"csr_rp_kernel<1, false, amgk::EpiGemv,",
                "dc": r"csr_dc_kernel<1, false, amgk::EpiGemv,"}.get(
                    vi, r"csr_tile_kernel<.*>, 1, false, amgk::EpiGemv, %s" % vi)
         F = pick(fetch, pat, rows)
@@ -68,15 +70,17 @@ def main():
         if not F or not W:
             continue
         Fm, Wm = sum(F) / len(F), sum(W) / len(W)
-        s16 = {"rp": 0, "dc": 0, "true": 4 * z, "false": 12 * z}[vi]
-        s4 = {"rp": 0, "dc": 0, "true": z, "false": 0}[vi] + (0 if vi == "rp" else 4 * (rows + 1))
-        s8 = 8 * rows + (z if vi == "dc" else 0)  # dictionary bytes: staged with 8-byte lanes
-        s1 = rows if vi == "rp" else 0  # row-pattern bytes: one per lane
+        # the paired kernel reads f with 16-byte lanes and one pattern byte per row pair
+        s16 = {"rpp": 8 * rows, "rp": 0, "dc": 0, "true": 4 * z, "false": 12 * z}[vi]
+        s4 = {"rpp": 0, "rp": 0, "dc": 0, "true": z, "false": 0}[vi] + (
+            0 if vi in ("rp", "rpp") else 4 * (rows + 1))
+        s8 = (0 if vi == "rpp" else 8 * rows) + (z if vi == "dc" else 0)  # dictionary: 8-byte lanes
+        s1 = {"rp": rows, "rpp": (rows + 1) // 2}.get(vi, 0)  # row-pattern bytes: one per lane
         known_rep = s16 * fac["read16"] + s4 * fac["read4"] + s8 * fac["read8"] + s1 * fac["read1"]
         gather = (Fm - known_rep) / fac["read8"]
         writes = Wm / fac["write8"]
         traffic = s16 + s4 + s8 + s1 + gather + writes
-        alg = (rows + 24 * rows if vi == "rp" else
+        alg = (rows + 24 * rows if vi == "rp" else (rows + 1) // 2 + 24 * rows if vi == "rpp" else
                {"dc": 1, "true": 5, "false": 12}[vi] * z + 28 * rows + 4)
         res[fmt] = {"fine_residual_bytes_per_launch": traffic, "alg_bytes_per_launch": alg,
                     "traffic_over_alg": traffic / alg, "fetch_size_raw": Fm, "write_size_raw": Wm,
