@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstdint>
 #include <cstring>
 #include <vector>
 
@@ -334,22 +335,25 @@ static int build_row_pattern(amg_mat *A)
    return AMG_OK;
 }
 
-// paired-row-pattern CSR on top of the row patterns: rows 2t and 2t+1 of a
-// square operator share one merged entry list in which an entry both rows
-// hold at the same column offset is one 16-byte x load.
-// The merge is a shortest common supersequence of the two rows' entry lists
-// (matched on column offset), so each row still sums its own entries in its
-// CSR order: bit-identical to the single-row kernel.
-static void pair_merge(const unsigned char *a, int la, const unsigned char *b, int lb,
+// paired-row-pattern CSR on top of the row patterns: rows 2t and 2t+1 share
+// one merged entry list in which an entry of row 2t at column c and an entry
+// of row 2t+1 at column c + 1 are one 16-byte x load.
+// Columns are relative to row 2t's anchor (the row itself for square
+// diagonal-first operators); row 2t+1's anchor is da further.  The merge is a
+// shortest common supersequence of the two rows' entry lists (matched on
+// column), so each row still sums its own entries in its CSR order:
+// bit-identical to the single-row kernel.
+static void pair_merge(const unsigned char *a, int la, const unsigned char *b, int lb, int da,
                        const std::vector<int> &off, std::vector<unsigned int> &out)
 {
    int dp[AMG_PP_MAXROW + 2][AMG_PP_MAXROW + 2] = {};
+   auto match = [&](int i, int j) { return off[b[j]] + da == off[a[i]] + 1; };
    for (int i = la - 1; i >= 0; i--)
       for (int j = lb - 1; j >= 0; j--)
-         dp[i][j] = off[a[i]] == off[b[j]] ? dp[i + 1][j + 1] + 1 : std::max(dp[i + 1][j], dp[i][j + 1]);
+         dp[i][j] = match(i, j) ? dp[i + 1][j + 1] + 1 : std::max(dp[i + 1][j], dp[i][j + 1]);
    int i = 0, j = 0;
    while (i < la || j < lb) {
-      if (i < la && j < lb && off[a[i]] == off[b[j]] && dp[i][j] == dp[i + 1][j + 1] + 1) {
+      if (i < la && j < lb && match(i, j) && dp[i][j] == dp[i + 1][j + 1] + 1) {
          out.push_back(a[i] | (unsigned)b[j] << 8 | 3u << 16);
          i++;
          j++;
@@ -367,45 +371,49 @@ static int build_pair_pattern(amg_mat *A)
 {
    amg_ctx *c = A->ctx;
    hipStream_t s = c->stream;
-   constexpr int NK = 256 * 257; // key = p0 * 257 + p1 (p1 = 256: no row 2t+1)
+   constexpr int NK = AMG_PP_NK;
    unsigned char *flags = nullptr;
-   AMG_HIP(hipMalloc(&flags, 2 * NK));
-   unsigned char *map = flags + NK;
-   AMG_HIP(hipMemsetAsync(flags, 0, NK, s));
+   AMG_HIP(hipMalloc(&flags, 2 * (size_t)NK + 1 + 256 * sizeof(unsigned long long) + 8));
+   unsigned char *map = flags + NK + 1;
+   unsigned long long *counts = reinterpret_cast<unsigned long long *>(
+      (reinterpret_cast<uintptr_t>(map + NK) + 7) & ~(uintptr_t)7);
+   AMG_HIP(hipMemsetAsync(flags, 0, NK + 1, s));
    amgk::pp_collect(s, A, flags);
-   std::vector<unsigned char> hf(NK), pt(256 * AMG_RP_STRIDE);
+   std::vector<unsigned char> hf(NK + 1), pt(256 * AMG_RP_STRIDE);
    std::vector<int> off(256);
-   AMG_HIP(hipMemcpyAsync(hf.data(), flags, NK, hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(hf.data(), flags, NK + 1, hipMemcpyDeviceToHost, s));
    AMG_HIP(hipMemcpyAsync(pt.data(), A->ptab, pt.size(), hipMemcpyDeviceToHost, s));
    AMG_HIP(hipMemcpyAsync(off.data(), A->doff, 256 * sizeof(int), hipMemcpyDeviceToHost, s));
    AMG_HIP(hipStreamSynchronize(s));
    std::vector<unsigned char> hm(NK, 0);
    std::vector<unsigned int> tab;
    const int PS = amg_pp_stride(A->dc_maxrow);
-   int T = 0;
+   int T = hf[NK] ? 257 : 0; // an anchor delta out of range: not pair-coded
+   std::vector<int> msz(256, 0), ssz(256, 0); // per pattern: merged entries, the longer row's
    for (int k = 0; k < NK && T <= 256; k++) {
       if (!hf[k]) continue;
       if (T == 256) {
          T++;
          break;
       }
-      const int p0 = k / 257, p1 = k % 257;
+      const int pk = k / AMG_PP_NDA, da = k % AMG_PP_NDA - AMG_PP_DA0;
+      const int p0 = pk / 257, p1 = pk % 257;
       const unsigned char *a = pt.data() + p0 * AMG_RP_STRIDE;
       std::vector<unsigned int> el;
       if (p1 < 256) {
          const unsigned char *b = pt.data() + p1 * AMG_RP_STRIDE;
-         pair_merge(a + 1, a[0], b + 1, b[0], off, el);
+         pair_merge(a + 1, a[0], b + 1, b[0], A->danch ? da : 1, off, el);
+         msz[T] = (int)el.size();
+         ssz[T] = std::max<int>(a[0], b[0]);
       } else {
          for (int j = 0; j < a[0]; j++) el.push_back(a[1 + j] | 1u << 16);
       }
       // header: nel | first dictionary entry of row 2t << 8 | of row 2t+1 << 16
-      // | row 2t+1 present << 24 | (merged entry at offset 0 of both rows) + 1 << 25
-      unsigned int centre = 0;
-      for (size_t e = 0; e < el.size() && !centre; e++)
-         if ((el[e] >> 16 & 3) == 3 && off[el[e] & 0xff] == 0) centre = (unsigned)e + 1;
+      // | row 2t+1 present << 24 | (anchor delta + 16) << 25
       std::vector<unsigned int> w(PS, 0);
       w[0] = (unsigned)el.size() | (unsigned)a[1] << 8 |
-             (p1 < 256 ? (unsigned)pt[p1 * AMG_RP_STRIDE + 1] << 16 | 1u << 24 : 0u) | centre << 25;
+             (p1 < 256 ? (unsigned)pt[p1 * AMG_RP_STRIDE + 1] << 16 | 1u << 24 : 0u) |
+             (unsigned)(da + 16) << 25;
       for (size_t e = 0; e < el.size(); e++) w[1 + e] = el[e];
       tab.insert(tab.end(), w.begin(), w.end());
       hm[k] = (unsigned char)T++;
@@ -428,9 +436,28 @@ static int build_pair_pattern(amg_mat *A)
    }
    AMG_HIP(hipMemcpyAsync(map, hm.data(), NK, hipMemcpyHostToDevice, s));
    AMG_HIP(hipMemcpyAsync(A->pptab, tab.data(), tab.size() * sizeof(unsigned int), hipMemcpyHostToDevice, s));
-   amgk::pp_encode(s, A, map, A->ppat);
+   AMG_HIP(hipMemsetAsync(counts, 0, 256 * sizeof(unsigned long long), s));
+   amgk::pp_encode(s, A, map, A->ppat, counts);
+   std::vector<unsigned long long> cnt(256);
+   AMG_HIP(hipMemcpyAsync(cnt.data(), counts, 256 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
    AMG_HIP(hipStreamSynchronize(s));
    hipFree(flags);
+   // a pair lane walks the merged list: worth it only when it is hardly
+   // longer than the longer of its rows, counted over all row pairs (7-pt /
+   // 27-pt operators and interpolation: as long; restriction, anchors 2
+   // apart: 4/3 as long, and slower than one row per lane)
+   double merged = 0.0, single = 0.0;
+   for (int t = 0; t < T; t++) {
+      merged += (double)cnt[t] * msz[t];
+      single += (double)cnt[t] * ssz[t];
+   }
+   if (merged > AMG_PP_MAXFILL * single) {
+      hipFree(A->ppat);
+      hipFree(A->pptab);
+      A->ppat = nullptr;
+      A->pptab = nullptr;
+      return AMG_OK;
+   }
    A->pp_n = T;
    A->pp_stride = PS;
    return AMG_OK;
@@ -443,8 +470,7 @@ int amg_mat_finish(amg_mat *A)
    if (A->ctx->value_index && A->nnz > 0) AMG_TRY(build_value_index(A));
    if (A->ctx->dict_index && A->vidx) AMG_TRY(build_dict_index(A));
    if (A->ctx->row_pattern && A->didx) AMG_TRY(build_row_pattern(A));
-   if (A->ctx->pair_pattern && A->rpat && !A->danch && A->nrows == A->ncols &&
-       A->dc_maxrow <= AMG_PP_MAXROW &&
+   if (A->ctx->pair_pattern && A->rpat && A->dc_maxrow <= AMG_PP_MAXROW &&
        (A->dc_maxrow <= 8 || A->nrows >= AMG_PP_LONG_MIN_ROWS || A->ctx->pair_pattern == 2))
       AMG_TRY(build_pair_pattern(A));
    return AMG_OK;

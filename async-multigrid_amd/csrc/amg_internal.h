@@ -55,8 +55,16 @@ constexpr int AMG_PP_LDS = 32 * 1024;
 // twice the entries: latency-bound grids below it run faster one row per lane)
 constexpr int AMG_PP_LONG_MIN_ROWS = 1 << 22;
 inline int amg_pp_stride(int maxrow) { return 1 + 2 * (maxrow <= 8 ? 8 : AMG_PP_MAXROW); }
+// anchored operators (interpolation, restriction): row 2t+1's anchor minus
+// row 2t's, + AMG_PP_DA0, must lie in [0, AMG_PP_NDA)
+constexpr int AMG_PP_NDA = 16;
+constexpr int AMG_PP_DA0 = 8;
+constexpr int AMG_PP_NK = 256 * 257 * AMG_PP_NDA; // pair keys
+// pair-coded only if the merged lists are at most this factor longer than the
+// longer row of each pair (summed over all row pairs)
+constexpr double AMG_PP_MAXFILL = 1.15;
 // paired kernel epilogue form (csr_rpp_kernel OPT, tools/tune_spmv.py ABL_jac_o*):
-// a_ii from the header word, x[i] from its own load
+// bit 1 = a_ii from the header word
 constexpr int AMG_RPP_OPT = 2;
 
 struct amg_transport; // amg_dist.cpp: RCCL communicator or host-callback test transport
@@ -110,13 +118,13 @@ struct amg_mat {
    unsigned char *rpat = nullptr;
    unsigned char *ptab = nullptr;
    int rp_n = 0;
-   // paired-row-pattern form (square operators, anchor = row, rows of <= 8
-   // entries, <= 256 distinct (pattern of row 2t, pattern of row 2t+1) pairs):
-   // ppat[t] names the pair's merged entry list in pptab (pp_stride words
-   // per pair: header nel | row1 present << 24, then entries
-   // d0 | d1 << 8 | has0 << 16 | has1 << 17).  An entry present in both rows
-   // has one column offset: the kernel reads x[2t + off], x[2t + 1 + off] with
-   // one 16-byte load.
+   // paired-row-pattern form (row-pattern-coded operators with rows of <= 32
+   // entries and <= 256 distinct (pattern of row 2t, pattern of row 2t+1,
+   // anchor delta) pairs): ppat[t] names the pair's merged entry list in
+   // pptab (pp_stride words per pair: header nel | first entry of row 2t << 8
+   // | of row 2t+1 << 16 | row 2t+1 present << 24 | (da + 16) << 25, then
+   // entries d0 | d1 << 8 | has0 << 16 | has1 << 17).  An entry present in
+   // both rows reads x[base + off], x[base + off + 1] with one 16-byte load.
    unsigned char *ppat = nullptr;
    unsigned int *pptab = nullptr;
    int pp_n = 0;
@@ -235,7 +243,8 @@ void rp_table(hipStream_t s, const amg_mat *A, const int *rep, int T, unsigned c
 void rp_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
                const unsigned char *ptab, unsigned char *rpat, int *bad);
 void pp_collect(hipStream_t s, const amg_mat *A, unsigned char *flags);
-void pp_encode(hipStream_t s, const amg_mat *A, const unsigned char *map, unsigned char *ppat);
+void pp_encode(hipStream_t s, const amg_mat *A, const unsigned char *map, unsigned char *ppat,
+               unsigned long long *counts);
 
 // dictionary-coded CSR construction (needs the value index)
 void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,

@@ -503,53 +503,27 @@ __global__ __launch_bounds__(256) void csr_rp_kernel(
 }
 
 // Paired-row-pattern kernel: lane owns the row pair (2t, 2t+1) and reads the
-// pair's merged entry list (ps words in LDS).  An entry both rows
-// hold at the same column offset o reads x[2t+o] and x[2t+1+o] with ONE
-// 16-byte load (half the vector-memory instructions of one lane per row,
-// which bounds the single-row kernel: DESIGN.md Sec.4); an entry of one row
-// alone reads its x value by itself.  Each row still sums its own entries in
-// its CSR order (the merge keeps both orders), so results are bit-identical.
-// The header word carries each row's first dictionary entry (a_ii, no scan)
-// and the merged entry at offset 0 of both rows: when the epilogue's own
-// operand is x[i] (Jacobi forms) it comes from that gather, not a second load.
-// Workgroup slab q covers 512 rows = two 256-row norm tiles; the tiles' sums
-// are reduced after every slab is done (no barrier between slabs), in the
-// single-row kernel's lane order.  rb must be even.
-struct EpiJacobi;
-struct EpiL1Jacobi;
-struct EpiResJacobi;
-template <class Epi>
-struct pf_is_x {
-   static constexpr bool value = false;
-};
-// the epilogue's prefetched operand vector (found by ADL at instantiation)
-template <class Epi>
-__device__ __forceinline__ const double *epi_pf_vec(const Epi &)
-{
-   return nullptr;
-}
-template <>
-struct pf_is_x<EpiJacobi> {
-   static constexpr bool value = true;
-};
-template <>
-struct pf_is_x<EpiL1Jacobi> {
-   static constexpr bool value = true;
-};
-template <>
-struct pf_is_x<EpiResJacobi> {
-   static constexpr bool value = true;
-};
-
-// OPT bit 0: take the Jacobi operand x[i] from the centre gather; bit 1: a_ii
-// from the header (else scanned from the entry list)
+// pair's merged entry list (ps words in LDS).  Columns are relative to the
+// pair's base: row 2t itself for square diagonal-first operators, else row
+// 2t's anchor (its first column; interpolation / restriction), with row 2t+1's
+// anchor at base + da (da = 1 for square operators, from the header word for
+// anchored ones).  An entry of row 2t at column c matched with an entry of row
+// 2t+1 at column c + 1 reads both x values with ONE 16-byte load (half the
+// vector-memory instructions of one lane per row, which bounds the single-row
+// kernel: DESIGN.md Sec.4); an entry of one row alone reads its x value by
+// itself.  Each row still sums its own entries in its CSR order (the merge
+// keeps both orders), so results are bit-identical.  The header word also
+// carries each row's first dictionary entry (a_ii, no scan).  Workgroup slab
+// q covers 512 rows = two 256-row norm tiles; the tiles' sums are reduced
+// after every slab is done (no barrier between slabs), in the single-row
+// kernel's lane order.  rb must be even.
+// OPT bit 1: a_ii from the header word (else scanned from the entry list)
 template <int NEG, bool NEED_DIAG, class Epi, int RPL, int OPT = AMG_RPP_OPT>
 __global__ __launch_bounds__(256) void csr_rpp_kernel(
    const unsigned char *__restrict__ ppat, const unsigned int *__restrict__ pptab_g, int np,
    const int *__restrict__ doff_g, const double *__restrict__ dval_g, const double *__restrict__ x,
-   int rb, int re, Epi epi, double *__restrict__ partials, int T, int PS)
+   int rb, int re, Epi epi, double *__restrict__ partials, int T, int PS, const int *__restrict__ anch)
 {
-   constexpr bool PFX = pf_is_x<Epi>::value && (OPT & 1);
    __shared__ int otab[256];
    __shared__ double vtab[256];
    extern __shared__ unsigned int ptab[]; // np * PS words (dynamic)
@@ -562,13 +536,13 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
    }
    for (int w = tid; w < np * PS; w += 256) ptab[w] = pptab_g[w];
    const int wg = (int)blockIdx.x;
-   // the epilogue operand is the gathered vector itself (uniform test)
-   const bool xc_ok = PFX && epi_pf_vec(epi) == x;
-   int pid[RPL];
+   int pid[RPL], base[RPL];
 #pragma unroll
    for (int q = 0; q < RPL; q++) {
       const int row = rb + (wg * RPL + q) * 512 + 2 * tid;
       pid[q] = row < re ? ppat[row >> 1] : 0;
+      base[q] = row;
+      if (anch && row < re) base[q] = anch[row];
    }
    __syncthreads();
    double sq[RPL][2];
@@ -582,14 +556,15 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
          const unsigned int *pp = ptab + pid[q] * PS;
          const unsigned int hd = pp[0];
          const int nel = hd & 0xff;
-         const int ci = xc_ok ? (int)(hd >> 25) : 0; // centre entry + 1 (0: none)
-         v2d acc, pf{0.0, 0.0};
+         // row 2t+1's columns: base + da + offset
+         const int b1 = base[q] + (anch ? (int)(hd >> 25) - 16 : 1);
+         v2d acc, pf;
          if (a1) {
             acc = epi.init2(row);
-            if (ci == 0) pf = epi.pf2(row);
+            pf = epi.pf2(row);
          } else {
             acc = v2d{epi.init(row), 0.0};
-            if (ci == 0) pf = v2d{epi.pf(row), 0.0};
+            pf = v2d{epi.pf(row), 0.0};
          }
          for (int k = 0; k < nel; k += 8) {
             const int m = nel - k;
@@ -604,18 +579,17 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
                   ew[j] = w;
                   const int d0 = w & 0xff, d1 = (w >> 8) & 0xff;
                   if ((w >> 16 & 3) == 3)
-                     xv[j] = *reinterpret_cast<const v2du *>(x + row + otab[d0]);
+                     xv[j] = *reinterpret_cast<const v2du *>(x + base[q] + otab[d0]);
                   else if (w >> 16 & 1)
-                     xv[j].x = x[row + otab[d0]];
+                     xv[j].x = x[base[q] + otab[d0]];
                   else
-                     xv[j].y = x[row + 1 + otab[d1]];
+                     xv[j].y = x[b1 + otab[d1]];
                }
             }
 #pragma unroll
             for (int j = 0; j < 8; j++)
                if (j < m) {
                   const unsigned int w = ew[j];
-                  if (PFX && k + j + 1 == ci) pf = xv[j];
                   if (w >> 16 & 1) {
                      const double v = vtab[w & 0xff];
                      if (NEG)
@@ -696,7 +670,7 @@ static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int r
 {
    if (A->ppat && (rb & 1) == 0)
       csr_rpp_kernel<NEG, NEED_DIAG, Epi, 2><<<(re - rb + 1023) / 1024, 256, A->pp_n * A->pp_stride * 4, s>>>(
-         A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->pp_stride);
+         A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->pp_stride, A->danch);
    else if (A->rpat && A->dc_maxrow <= 8)
       csr_rp_kernel<NEG, NEED_DIAG, Epi, 4><<<(tiles + 3) / 4, 256, 0, s>>>(
          A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
@@ -969,10 +943,6 @@ struct EpiResJacobi {
    }
 };
 
-__device__ __forceinline__ const double *epi_pf_vec(const EpiJacobi &e) { return e.x; }
-__device__ __forceinline__ const double *epi_pf_vec(const EpiL1Jacobi &e) { return e.x; }
-__device__ __forceinline__ const double *epi_pf_vec(const EpiResJacobi &e) { return e.x; }
-
 template <class Cfg>
 static inline int cfg_blocks(int rb, int re)
 {
@@ -1228,7 +1198,7 @@ static void launch_rpp(hipStream_t s, const amg_mat *A, const double *x, double 
    if (!A->ppat) return;
    const int nt = (A->nrows + 512 * RPL - 1) / (512 * RPL);
    csr_rpp_kernel<0, false, EpiGemv, RPL><<<nt, 256, A->pp_n * A->pp_stride * 4, s>>>(
-      A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride);
+      A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride, A->danch);
 }
 
 // Jacobi sweep y = x + w (x - A x)/a_ii through the paired kernel, OPT as
@@ -1237,10 +1207,10 @@ template <int OPT>
 static void launch_rpp_jac(hipStream_t s, const amg_mat *A, const double *x, double *y)
 {
    EpiJacobi e{x, x, y, 0.8};
-   if (!A->ppat) return;
+   if (!A->ppat || A->nrows != A->ncols) return;
    const int nt = (A->nrows + 1023) / 1024;
    csr_rpp_kernel<1, true, EpiJacobi, 2, OPT><<<nt, 256, A->pp_n * A->pp_stride * 4, s>>>(
-      A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride);
+      A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride, A->danch);
 }
 
 // ablations of the row-pattern kernel on the 512^3 operator (timing only):
@@ -2228,33 +2198,61 @@ __global__ void rp_encode_k(const int *__restrict__ rowptr, const unsigned char 
 }
 
 // row-pair keys p0 * 257 + p1 (p1 = 256 when row 2t+1 does not exist)
-__global__ void pp_collect_k(const unsigned char *__restrict__ rpat, int n, unsigned char *flags)
+// pair key: (pattern of row 2t, of row 2t+1 or 256 if none, anchor delta
+// da = anch[2t+1] - anch[2t] + AMG_PP_DA0 in [0, AMG_PP_NDA)); a delta out of
+// range flags the matrix (flags[AMG_PP_NK])
+__device__ __forceinline__ int pp_key(const unsigned char *__restrict__ rpat, const int *__restrict__ anch, int n,
+                                      int t)
+{
+   const bool two = 2 * t + 1 < n;
+   const int da = (two && anch) ? anch[2 * t + 1] - anch[2 * t] + AMG_PP_DA0 : AMG_PP_DA0;
+   if (da < 0 || da >= AMG_PP_NDA) return -1;
+   return (rpat[2 * t] * 257 + (two ? rpat[2 * t + 1] : 256)) * AMG_PP_NDA + da;
+}
+
+__global__ void pp_collect_k(const unsigned char *__restrict__ rpat, const int *__restrict__ anch, int n,
+                             unsigned char *flags)
 {
    const int np = (n + 1) / 2;
    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < np; t += gridDim.x * blockDim.x) {
-      const int k = rpat[2 * t] * 257 + (2 * t + 1 < n ? rpat[2 * t + 1] : 256);
+      int k = pp_key(rpat, anch, n, t);
+      if (k < 0) k = AMG_PP_NK;
       if (!flags[k]) flags[k] = 1;
    }
 }
 
-__global__ void pp_encode_k(const unsigned char *__restrict__ rpat, int n, const unsigned char *__restrict__ map,
-                            unsigned char *__restrict__ ppat)
+// ppat[t] = the pair's table index; counts[p] += pairs of pattern p
+__global__ __launch_bounds__(256) void pp_encode_k(const unsigned char *__restrict__ rpat,
+                                                   const int *__restrict__ anch, int n,
+                                                   const unsigned char *__restrict__ map,
+                                                   unsigned char *__restrict__ ppat,
+                                                   unsigned long long *__restrict__ counts)
 {
+   __shared__ unsigned int hist[256];
+   hist[threadIdx.x] = 0;
+   __syncthreads();
    const int np = (n + 1) / 2;
-   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < np; t += gridDim.x * blockDim.x)
-      ppat[t] = map[rpat[2 * t] * 257 + (2 * t + 1 < n ? rpat[2 * t + 1] : 256)];
+   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < np; t += gridDim.x * blockDim.x) {
+      const unsigned char p = map[pp_key(rpat, anch, n, t)];
+      ppat[t] = p;
+      atomicAdd(&hist[p], 1u);
+   }
+   __syncthreads();
+   if (hist[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)hist[threadIdx.x]);
 }
 
 void pp_collect(hipStream_t s, const amg_mat *A, unsigned char *flags)
 {
    if (A->nrows <= 0) return;
-   pp_collect_k<<<std::min(8192, (A->nrows + 511) / 512), 256, 0, s>>>(A->rpat, A->nrows, flags);
+   pp_collect_k<<<std::min(8192, (A->nrows + 511) / 512), 256, 0, s>>>(A->rpat, A->danch, A->nrows, flags);
 }
 
-void pp_encode(hipStream_t s, const amg_mat *A, const unsigned char *map, unsigned char *ppat)
+void pp_encode(hipStream_t s, const amg_mat *A, const unsigned char *map, unsigned char *ppat,
+               unsigned long long *counts)
 {
    if (A->nrows <= 0) return;
-   pp_encode_k<<<std::min(8192, (A->nrows + 511) / 512), 256, 0, s>>>(A->rpat, A->nrows, map, ppat);
+   pp_encode_k<<<std::min(8192, (A->nrows + 511) / 512), 256, 0, s>>>(A->rpat, A->danch, A->nrows, map, ppat,
+                                                                        counts);
 }
 
 void rp_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int *rep, int nslots, int *count,

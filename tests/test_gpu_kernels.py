@@ -138,29 +138,65 @@ def test_value_index_selection(mats):
     assert dev["lap_hole"].dict_index == 7 and dev["lap_hole"].row_pattern == 0
     for name in ("A1", "P0", "R0"):
         assert dev[name].row_pattern > 0, name
-    # paired rows: square, anchor = row, rows of <= 32 entries, <= 256 distinct
-    # (pattern of row 2t, pattern of row 2t+1) pairs whose table (17 words per
-    # pair for rows of <= 8 entries, 65 for <= 32) fits 32 KiB of LDS
+    # paired rows: row-pattern-coded, rows of <= 32 entries, <= 256 distinct
+    # (pattern of row 2t, pattern of row 2t+1, anchor delta in [-8, 8)) pairs
+    # (anchor = a row's first column) whose table (17 words per pair for rows
+    # of <= 8 entries, 65 for <= 32) fits 32 KiB of LDS
     for name in ALL:
         A = host[name]
-        if not dev[name].row_pattern or A.nrows != A.ncols or A.nrows == 0:
+        if not dev[name].row_pattern or A.nrows == 0:
             assert dev[name].pair_pattern == 0, name
             continue
         lens = np.diff(A.rowptr)
-        anchored = bool(np.all(A.col[A.rowptr[:-1]] == np.arange(A.nrows)))
+        anch = A.col[A.rowptr[:-1]].astype(np.int64)
+        # square diagonal-first: the row is its own anchor (no anchor array)
+        anch_is_row = A.nrows == A.ncols and bool(np.all(anch == np.arange(A.nrows)))
         pat = []
         for i in range(A.nrows):
             c = A.col[A.rowptr[i]:A.rowptr[i + 1]].astype(np.int64)
             v = A.val[A.rowptr[i]:A.rowptr[i + 1]].view(np.int64)
             pat.append(tuple((c - c[0]).tolist()) + tuple(v.tolist()))
-        pairs = {(pat[2 * t], pat[2 * t + 1] if 2 * t + 1 < A.nrows else None)
-                 for t in range((A.nrows + 1) // 2)}
+        pairs, da_ok = set(), True
+        # a row's entries as (column relative to its anchor) for the merge test
+        rel = [tuple((A.col[A.rowptr[i]:A.rowptr[i + 1]].astype(np.int64) - anch[i]).tolist())
+               for i in range(A.nrows)]
+        for t in range((A.nrows + 1) // 2):
+            if 2 * t + 1 < A.nrows:
+                da = int(anch[2 * t + 1] - anch[2 * t])
+                da_ok &= -8 <= da < 8
+                pairs.add((pat[2 * t], pat[2 * t + 1], da))
+            else:
+                pairs.add((pat[2 * t], None, 0))
         stride = 17 if lens.max() <= 8 else 65
-        ok = anchored and lens.max() <= 32 and len(pairs) <= 256 and len(pairs) * stride * 4 <= 32768
+        # merged list = shortest common supersequence: la + lb - LCS, entries
+        # matched when row 2t+1's column is row 2t's + 1 (anchor delta da)
+        merged = single = 0
+        seen = {}
+        for t in range(A.nrows // 2):
+            key = (pat[2 * t], pat[2 * t + 1], int(anch[2 * t + 1] - anch[2 * t]))
+            if key in seen:  # counted over all row pairs
+                merged += seen[key][0]
+                single += seen[key][1]
+                continue
+            ra, rb_ = rel[2 * t], rel[2 * t + 1]
+            da = key[2] if not anch_is_row else 1
+            L = np.zeros((len(ra) + 1, len(rb_) + 1), dtype=np.int64)
+            for i in range(len(ra) - 1, -1, -1):
+                for j in range(len(rb_) - 1, -1, -1):
+                    L[i, j] = L[i + 1, j + 1] + 1 if rb_[j] + da == ra[i] + 1 else max(L[i + 1, j], L[i, j + 1])
+            seen[key] = (len(ra) + len(rb_) - L[0, 0], max(len(ra), len(rb_)))
+            merged += seen[key][0]
+            single += seen[key][1]
+        ok = (da_ok and lens.max() <= 32 and len(pairs) <= 256 and len(pairs) * stride * 4 <= 32768
+              and merged <= 1.15 * single)
         assert dev[name].pair_pattern == (len(pairs) if ok else 0), (name, len(pairs), dev[name].pair_pattern)
     # 16^3 (x even): pairs (x=0,1), (2k,2k+1) interior, (14,15) times 9 (y,z) classes
     assert dev["lap16"].pair_pattern == 27
     assert dev["A1"].pair_pattern > 0  # the 27-pt Galerkin operator
+    for name in ("P0", "P1"):  # anchored: interpolation
+        assert dev[name].pair_pattern > 0, name
+    for name in ("R0", "R1"):  # restriction: anchors 2 apart, merged lists 5/4 as long
+        assert dev[name].pair_pattern == 0, name
     assert dev["lap_rect"].pair_pattern > 0 and dev["lap_rect"].nrows % 2 == 1
 
 
@@ -208,12 +244,13 @@ def test_value_index_matches_plain(mats, ctx, amg, name):
     rp_only.free()
 
 
-@pytest.mark.parametrize("name", ["lap16", "lap_rect", "A1"])
+@pytest.mark.parametrize("name", ["lap16", "lap_rect", "A1", "P0", "P1"])
 @pytest.mark.parametrize("rng_", [(0, 0), (2, -5), (4, -4), (3, -6), (0, -1), (6, -2)])
 def test_pair_pattern_row_ranges(mats, ctx, oracle, amg, name, rng_):
     """Paired-row kernel on row slices: even starts run paired (an odd end
     leaves a half pair), odd starts the single-row kernel; residual, SpGEMV,
-    Jacobi and L1 Jacobi bit-identical to the oracle, rows outside untouched."""
+    Jacobi and L1 Jacobi (square operators; interpolation and restriction run
+    anchored pairs) bit-identical to the oracle, rows outside untouched."""
     host, dev = mats
     A, dA = host[name], dev[name]
     assert dA.pair_pattern > 0
@@ -232,6 +269,8 @@ def test_pair_pattern_row_ranges(mats, ctx, oracle, amg, name, rng_):
         dy = ctx.vec(y0)
         amg.smem.SMEM_SpGEMV(ctx, dA, ctx.vec(x), ctx.vec(b), ab[0], ab[1], dy, ns, ne)
         assert_bitwise(dy.download(), ref, f"spgemv {ab}")
+    if A.nrows != A.ncols:  # interpolation / restriction: no smoother
+        return
     # amg_jacobi copies the whole u to u_prev (the team's slices together);
     # the oracle's single slice copies only [ns, ne): start u_prev = u
     for zero in (0, 1):
