@@ -527,7 +527,6 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
    __shared__ int otab[256];
    __shared__ double vtab[256];
    extern __shared__ unsigned int ptab[]; // np * PS words (dynamic)
-   __shared__ double sqs[RPL * 512];
    __shared__ double red[RPL * 8];
    const int tid = (int)threadIdx.x;
    if (tid < T) {
@@ -636,20 +635,20 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
       }
    }
    if (partials) {
-      // the 256-row tiles' sums in block_sum_256's order (single-row kernel)
+      // the 256-row tiles' sums in block_sum_256's order (single-row kernel):
+      // its wave tree over 64 rows v[r] += v[r + off], off = 32 .. 1, is run
+      // on the 32 lanes holding those rows (lane l: rows 2l, 2l+1), so every
+      // addition has the same operands; then ((g0 + g1) + g2) + g3 over the
+      // tile's four 64-row groups
 #pragma unroll
       for (int q = 0; q < RPL; q++) {
-         sqs[q * 512 + 2 * tid] = sq[q][0];
-         sqs[q * 512 + 2 * tid + 1] = sq[q][1];
-      }
-      __syncthreads();
-      const int lane = tid & 63, wid = tid >> 6;
+         double a = sq[q][0], b = sq[q][1];
 #pragma unroll
-      for (int h = 0; h < 2 * RPL; h++) {
-         double v = sqs[h * 256 + tid];
-#pragma unroll
-         for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-         if (lane == 0) red[h * 4 + wid] = v;
+         for (int off = 16; off > 0; off >>= 1) {
+            a += __shfl_down(a, off, 32);
+            b += __shfl_down(b, off, 32);
+         }
+         if ((tid & 31) == 0) red[q * 8 + (tid >> 5)] = a + b;
       }
       __syncthreads();
       if (tid < 2 * RPL) {
