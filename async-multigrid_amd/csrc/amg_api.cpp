@@ -389,6 +389,7 @@ static int build_pair_pattern(amg_mat *A)
    std::vector<unsigned int> tab;
    const int PS = amg_pp_stride(A->dc_maxrow);
    int T = hf[NK] ? 257 : 0; // an anchor delta out of range: not pair-coded
+   bool centre0 = !A->danch; // square diagonal-first: is entry 0 the diagonal of both rows?
    std::vector<int> msz(256, 0), ssz(256, 0); // per pattern: merged entries, the longer row's
    for (int k = 0; k < NK && T <= 256; k++) {
       if (!hf[k]) continue;
@@ -415,6 +416,8 @@ static int build_pair_pattern(amg_mat *A)
              (p1 < 256 ? (unsigned)pt[p1 * AMG_RP_STRIDE + 1] << 16 | 1u << 24 : 0u) |
              (unsigned)(da + 16) << 25;
       for (size_t e = 0; e < el.size(); e++) w[1 + e] = el[e];
+      centre0 = centre0 && !el.empty() && off[el[0] & 0xff] == 0 && (el[0] >> 16 & 1) &&
+                (p1 == 256 || (el[0] >> 16 & 3) == 3);
       tab.insert(tab.end(), w.begin(), w.end());
       hm[k] = (unsigned char)T++;
    }
@@ -460,6 +463,7 @@ static int build_pair_pattern(amg_mat *A)
    }
    A->pp_n = T;
    A->pp_stride = PS;
+   A->pp_centre0 = centre0 ? 1 : 0;
    return AMG_OK;
 }
 

@@ -129,6 +129,7 @@ struct amg_mat {
    unsigned int *pptab = nullptr;
    int pp_n = 0;
    int pp_stride = 0; // words per pair pattern (amg_pp_stride)
+   int pp_centre0 = 0; // every pair's first merged entry is both rows' diagonal
 };
 
 struct amg_vec {

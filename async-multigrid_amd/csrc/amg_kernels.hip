@@ -518,12 +518,43 @@ __global__ __launch_bounds__(256) void csr_rp_kernel(
 // after every slab is done (no barrier between slabs), in the single-row
 // kernel's lane order.  rb must be even.
 // OPT bit 1: a_ii from the header word (else scanned from the entry list)
+// Jacobi-form epilogues read x[i] of the gathered vector itself: when every
+// pair's first merged entry is both rows' diagonal (c0, square diag-first
+// operators), that operand is the first gather, not a load of its own.
+struct EpiJacobi;
+struct EpiL1Jacobi;
+struct EpiResJacobi;
+template <class Epi>
+struct pf_is_x {
+   static constexpr bool value = false;
+};
+template <>
+struct pf_is_x<EpiJacobi> {
+   static constexpr bool value = true;
+};
+template <>
+struct pf_is_x<EpiL1Jacobi> {
+   static constexpr bool value = true;
+};
+template <>
+struct pf_is_x<EpiResJacobi> {
+   static constexpr bool value = true;
+};
+// the epilogue's operand vector (found by ADL at instantiation)
+template <class Epi>
+__device__ __forceinline__ const double *epi_pf_vec(const Epi &)
+{
+   return nullptr;
+}
+
 template <int NEG, bool NEED_DIAG, class Epi, int RPL, int OPT = AMG_RPP_OPT>
 __global__ __launch_bounds__(256) void csr_rpp_kernel(
    const unsigned char *__restrict__ ppat, const unsigned int *__restrict__ pptab_g, int np,
    const int *__restrict__ doff_g, const double *__restrict__ dval_g, const double *__restrict__ x,
-   int rb, int re, Epi epi, double *__restrict__ partials, int T, int PS, const int *__restrict__ anch)
+   int rb, int re, Epi epi, double *__restrict__ partials, int T, int PS, const int *__restrict__ anch,
+   int c0)
 {
+   const bool xc = pf_is_x<Epi>::value && c0 && epi_pf_vec(epi) == x;
    __shared__ int otab[256];
    __shared__ double vtab[256];
    extern __shared__ unsigned int ptab[]; // np * PS words (dynamic)
@@ -557,13 +588,13 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
          const int nel = hd & 0xff;
          // row 2t+1's columns: base + da + offset
          const int b1 = base[q] + (anch ? (int)(hd >> 25) - 16 : 1);
-         v2d acc, pf;
+         v2d acc, pf{0.0, 0.0};
          if (a1) {
             acc = epi.init2(row);
-            pf = epi.pf2(row);
+            if (!xc) pf = epi.pf2(row);
          } else {
             acc = v2d{epi.init(row), 0.0};
-            pf = v2d{epi.pf(row), 0.0};
+            if (!xc) pf = v2d{epi.pf(row), 0.0};
          }
          for (int k = 0; k < nel; k += 8) {
             const int m = nel - k;
@@ -585,6 +616,7 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
                      xv[j].y = x[b1 + otab[d1]];
                }
             }
+            if (xc && k == 0) pf = xv[0]; // x[2t], x[2t+1]: the diagonal entry
 #pragma unroll
             for (int j = 0; j < 8; j++)
                if (j < m) {
@@ -669,7 +701,8 @@ static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int r
 {
    if (A->ppat && (rb & 1) == 0)
       csr_rpp_kernel<NEG, NEED_DIAG, Epi, 2><<<(re - rb + 1023) / 1024, 256, A->pp_n * A->pp_stride * 4, s>>>(
-         A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->pp_stride, A->danch);
+         A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->pp_stride, A->danch,
+         A->pp_centre0);
    else if (A->rpat && A->dc_maxrow <= 8)
       csr_rp_kernel<NEG, NEED_DIAG, Epi, 4><<<(tiles + 3) / 4, 256, 0, s>>>(
          A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
@@ -942,6 +975,10 @@ struct EpiResJacobi {
    }
 };
 
+__device__ __forceinline__ const double *epi_pf_vec(const EpiJacobi &e) { return e.x; }
+__device__ __forceinline__ const double *epi_pf_vec(const EpiL1Jacobi &e) { return e.x; }
+__device__ __forceinline__ const double *epi_pf_vec(const EpiResJacobi &e) { return e.x; }
+
 template <class Cfg>
 static inline int cfg_blocks(int rb, int re)
 {
@@ -1197,7 +1234,8 @@ static void launch_rpp(hipStream_t s, const amg_mat *A, const double *x, double 
    if (!A->ppat) return;
    const int nt = (A->nrows + 512 * RPL - 1) / (512 * RPL);
    csr_rpp_kernel<0, false, EpiGemv, RPL><<<nt, 256, A->pp_n * A->pp_stride * 4, s>>>(
-      A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride, A->danch);
+      A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride, A->danch,
+      A->pp_centre0);
 }
 
 // Jacobi sweep y = x + w (x - A x)/a_ii through the paired kernel, OPT as
@@ -1209,7 +1247,8 @@ static void launch_rpp_jac(hipStream_t s, const amg_mat *A, const double *x, dou
    if (!A->ppat || A->nrows != A->ncols) return;
    const int nt = (A->nrows + 1023) / 1024;
    csr_rpp_kernel<1, true, EpiJacobi, 2, OPT><<<nt, 256, A->pp_n * A->pp_stride * 4, s>>>(
-      A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride, A->danch);
+      A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride, A->danch,
+      A->pp_centre0);
 }
 
 // ablations of the row-pattern kernel on the 512^3 operator (timing only):
