@@ -142,6 +142,7 @@ PROTOTYPES = {
     "amg_dist_hier_create_structured": (_i, [_p, _p, C.POINTER(AmgOpts), _pp]),
     "amg_dist_hier_local_rows": (_i, [_p, _i, _ip, _ip]),
     "amg_dist_hier_matrix_info": (_i, [_p, _i, _llp, _ip, _ip, _ip]),
+    "amg_dist_hier_pair_pattern": (_i, [_p, _i, _ip]),
     "amg_dist_solve_start": (_i, [_p, _dp, _dp]),
     "amg_dist_solve_iterate": (_i, [_p, _i]),
     "amg_dist_solve_resnorm": (_i, [_p, _dp]),

@@ -238,7 +238,9 @@ static int build_dict_index(amg_mat *A)
       off[t] = (int)(unsigned int)(keys[t] >> 8);
       dv[t] = vt[keys[t] & 0xff];
    }
-   const bool need_anchor = cm[2] != 0 || A->nrows != A->ncols;
+   // anchors only where some row does not start at its own index (the
+   // transfers); a distributed slab [owned | ghost] keeps anchor = row
+   const bool need_anchor = cm[2] != 0;
    hipError_t e = hipMalloc(&A->didx, (size_t)A->nnz + 64);
    if (e == hipSuccess) e = hipMalloc(&A->doff, 256 * sizeof(int));
    if (e == hipSuccess) e = hipMalloc(&A->dval, 256 * sizeof(double));

@@ -874,6 +874,14 @@ extern "C" int amg_dist_hier_matrix_info(amg_dist_hier *D, int level, long long 
    return AMG_OK;
 }
 
+extern "C" int amg_dist_hier_pair_pattern(amg_dist_hier *D, int level, int *pair_pattern)
+{
+   AMG_ARG(D && pair_pattern && level >= 0 && level < D->L, "amg_dist_hier_pair_pattern: bad argument");
+   const amg_mat *A = level < D->Ld ? D->lv[level].A.A : D->cA[level - D->Ld];
+   *pair_pattern = A->pp_n;
+   return AMG_OK;
+}
+
 extern "C" int amg_dist_hier_local_rows(amg_dist_hier *D, int level, int *row0, int *nrows)
 {
    AMG_ARG(D && level >= 0 && level < D->L, "amg_dist_hier_local_rows: bad level");

@@ -258,6 +258,12 @@ class DistHier:
                                             C.byref(rp)))
         return nnz.value, vi.value, dc.value, rp.value
 
+    def pair_pattern(self, level):
+        """distinct row-pair patterns of this rank's A_level (0 = not pair-coded)"""
+        pp = C.c_int()
+        check(lib.amg_dist_hier_pair_pattern(self.h, level, C.byref(pp)))
+        return pp.value
+
     def local_rows(self, level):
         r0, n = C.c_int(), C.c_int()
         check(lib.amg_dist_hier_local_rows(self.h, level, C.byref(r0), C.byref(n)))

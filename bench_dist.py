@@ -47,7 +47,7 @@ def main(args, world, rank):
                             reuse_outer_residual=args.reuse_outer_residual, profile=1)
     D = amg.dist.DistHier(ctx, gen, opts)
     nnz_local, vi, dc, rp = D.matrix_info(0)
-    mat_bytes, fmt = storage(D.n0, nnz_local, vi, dc, rp)
+    mat_bytes, fmt = storage(D.n0, nnz_local, vi, dc, rp, D.pair_pattern(0))
     if rank == 0:
         log(f"[dist] {world} ranks, {gen.L} levels, slab {D.n0} rows / {nnz_local} nnz on rank 0; "
             f"setup {time.time() - t0:.1f}s")

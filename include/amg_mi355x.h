@@ -386,6 +386,8 @@ int amg_dist_hier_free(amg_dist_hier *D);
  * table size, dictionary size, row patterns; 0 = not used) */
 int amg_dist_hier_matrix_info(amg_dist_hier *D, int level, long long *nnz, int *value_index,
                               int *dict_index, int *row_pattern);
+/* distinct row-pair patterns of this rank's operator of a level (0 = not pair-coded) */
+int amg_dist_hier_pair_pattern(amg_dist_hier *D, int level, int *pair_pattern);
 /* rows [row0, row0 + nrows) of the global level-0 vector this rank owns */
 int amg_dist_hier_local_rows(amg_dist_hier *D, int level, int *row0, int *nrows);
 /* SMEM_Solve on the distributed hierarchy: f/u are this rank's level-0 rows */

@@ -149,8 +149,8 @@ def test_value_index_selection(mats):
             continue
         lens = np.diff(A.rowptr)
         anch = A.col[A.rowptr[:-1]].astype(np.int64)
-        # square diagonal-first: the row is its own anchor (no anchor array)
-        anch_is_row = A.nrows == A.ncols and bool(np.all(anch == np.arange(A.nrows)))
+        # every row starts at its own index: no anchor array (square, or a slab)
+        anch_is_row = bool(np.all(anch == np.arange(A.nrows)))
         pat = []
         for i in range(A.nrows):
             c = A.col[A.rowptr[i]:A.rowptr[i + 1]].astype(np.int64)
