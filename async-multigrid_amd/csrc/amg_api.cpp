@@ -77,6 +77,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_DICT_INDEX")) c->dict_index = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_ROW_PATTERN")) c->row_pattern = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_PAIR_PATTERN")) c->pair_pattern = std::min(2, std::max(0, std::atoi(v)));
+   if (const char *v = std::getenv("AMG_MASTER_PATTERN")) c->master_pattern = std::atoi(v) != 0;
    *out = c;
    return AMG_OK;
 }
@@ -469,6 +470,91 @@ static int build_pair_pattern(amg_mat *A)
    return AMG_OK;
 }
 
+// Master-pattern form on top of the pair patterns of a square,
+// diagonal-first operator: every row's column offsets (relative to the row)
+// must follow the master order -- 0 first, then ascending -- so a row's
+// entries are an ordered subsequence of the master list and walking the
+// master with per-row use bits adds exactly the row's products in its CSR
+// order (bit-identical).  Offsets then become wave-uniform scalars and the
+// per-entry LDS lookups of the pair kernel disappear.
+static int build_master_pattern(amg_mat *A)
+{
+   if (!A->ppat || A->danch || A->nrows != A->ncols || A->pp_n < 1) return AMG_OK;
+   hipStream_t s = A->ctx->stream;
+   const int T = A->pp_n, PS = A->pp_stride, D = A->dc_n;
+   std::vector<unsigned int> tab((size_t)T * PS);
+   std::vector<int> off(256);
+   std::vector<double> val(256);
+   AMG_HIP(hipMemcpyAsync(tab.data(), A->pptab, tab.size() * 4, hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(off.data(), A->doff, 256 * sizeof(int), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(val.data(), A->dval, 256 * sizeof(double), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   std::vector<int> mo;
+   for (int d = 0; d < D; d++) mo.push_back(off[d]);
+   std::sort(mo.begin(), mo.end());
+   mo.erase(std::unique(mo.begin(), mo.end()), mo.end());
+   auto z = std::find(mo.begin(), mo.end(), 0);
+   if (z == mo.end() || (int)mo.size() > AMG_MP_MAXJ) return AMG_OK;
+   mo.erase(z);
+   mo.insert(mo.begin(), 0);
+   const int J = (int)mo.size();
+   auto pos = [&](int o) { return (int)(std::find(mo.begin(), mo.end(), o) - mo.begin()); };
+   std::vector<unsigned long long> mask(T, 0);
+   std::vector<double> mv((size_t)T * J * 2, 0.0);
+   std::vector<unsigned long long> uni_bits(J, 0);
+   std::vector<int> uni_set(J, 0);
+   bool uni = true;
+   for (int t = 0; t < T; t++) {
+      const unsigned int *w = tab.data() + (size_t)t * PS;
+      const int nel = w[0] & 0xff;
+      const bool two = (w[0] >> 24) & 1;
+      int last[2] = {-1, -1};
+      for (int e = 0; e < nel; e++) {
+         const unsigned int en = w[1 + e];
+         for (int r = 0; r < 2; r++) {
+            if (!(en >> (16 + r) & 1)) continue;
+            const int d = r ? (en >> 8 & 0xff) : (en & 0xff);
+            const int j = pos(off[d]);
+            if (j <= last[r]) return AMG_OK; // not an ordered subsequence of the master
+            last[r] = j;
+            mask[t] |= 1ULL << (2 * j + r);
+            mv[((size_t)t * J + j) * 2 + r] = val[d];
+            unsigned long long bits;
+            std::memcpy(&bits, &val[d], 8);
+            if (!uni_set[j]) {
+               uni_set[j] = 1;
+               uni_bits[j] = bits;
+            } else if (uni_bits[j] != bits) {
+               uni = false;
+            }
+         }
+      }
+      // a_ii = A_data[A_i[i]] and x_i come from master entry 0 (the diagonal)
+      if (!(mask[t] & 1ULL) || (two && !(mask[t] & 2ULL))) return AMG_OK;
+   }
+   if (!uni && (size_t)T * J * 16 > (size_t)AMG_MP_LDS) return AMG_OK;
+   hipError_t e = hipMalloc(&A->mpmask, (size_t)T * 8);
+   if (e == hipSuccess && !uni) e = hipMalloc(&A->mpval, mv.size() * 8);
+   if (e != hipSuccess) {
+      hipFree(A->mpmask);
+      hipFree(A->mpval);
+      A->mpmask = nullptr;
+      A->mpval = nullptr;
+      (void)hipGetLastError();
+      return AMG_OK;
+   }
+   AMG_HIP(hipMemcpyAsync(A->mpmask, mask.data(), (size_t)T * 8, hipMemcpyHostToDevice, s));
+   if (!uni) AMG_HIP(hipMemcpyAsync(A->mpval, mv.data(), mv.size() * 8, hipMemcpyHostToDevice, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   for (int j = 0; j < J; j++) {
+      A->mp_off[j] = mo[j];
+      std::memcpy(&A->mp_val[j], &uni_bits[j], 8);
+   }
+   A->mp_uni = uni ? 1 : 0;
+   A->mp_J = J;
+   return AMG_OK;
+}
+
 int amg_mat_finish(amg_mat *A)
 {
    amgk::extract_diag(A->ctx->stream, A);
@@ -479,6 +565,7 @@ int amg_mat_finish(amg_mat *A)
    if (A->ctx->pair_pattern && A->rpat && A->dc_maxrow <= AMG_PP_MAXROW &&
        (A->dc_maxrow <= 8 || A->nrows >= AMG_PP_LONG_MIN_ROWS || A->ctx->pair_pattern == 2))
       AMG_TRY(build_pair_pattern(A));
+   if (A->ctx->master_pattern && A->ppat) AMG_TRY(build_master_pattern(A));
    return AMG_OK;
 }
 
@@ -504,6 +591,18 @@ extern "C" int amg_set_pair_pattern(amg_ctx *c, int enable)
 extern "C" int amg_mat_pair_pattern(const amg_mat *A)
 {
    return A ? A->pp_n : 0;
+}
+
+extern "C" int amg_set_master_pattern(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_master_pattern: null context");
+   c->master_pattern = enable ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_master_pattern(const amg_mat *A)
+{
+   return A ? A->mp_J * (A->mp_uni ? -1 : 1) : 0;
 }
 
 extern "C" int amg_set_dict_index(amg_ctx *c, int enable)
@@ -578,6 +677,8 @@ extern "C" int amg_mat_free(amg_mat *A)
    hipFree(A->ptab);
    hipFree(A->ppat);
    hipFree(A->pptab);
+   hipFree(A->mpmask);
+   hipFree(A->mpval);
    delete A;
    return AMG_OK;
 }

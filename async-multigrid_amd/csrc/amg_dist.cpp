@@ -1003,9 +1003,12 @@ int d_outer_residual(amg_dist_hier *D, int slot)
       DProf pr(D, 4, true);
       if (d_reuse(D) && D->L > 1) {
          const bool l1 = D->o.smoother == AMG_L1_JACOBI;
+         // reuse_outer_residual 2: the MULT cycle never reads r0 outside
+         // preconditioner mode (excluded by d_reuse), so it is not written
+         double *r0 = (D->o.reuse_outer_residual >= 2 && D->o.solver == AMG_MULT) ? nullptr : D->r0;
          double *x = v.u, *un = v.u_alt;
          AMG_TRY(split_launch(D, v.A, x, [&](int rb, int re, int poff) {
-            amgk::residual_jacobi(s, v.A.A, v.f, x, l1 ? v.l1 : nullptr, D->o.smooth_weight, D->r0,
+            amgk::residual_jacobi(s, v.A.A, v.f, x, l1 ? v.l1 : nullptr, D->o.smooth_weight, r0,
                                   un, rb, re, p + poff);
          }));
          D->pre_ready = true;

@@ -66,6 +66,10 @@ constexpr double AMG_PP_MAXFILL = 1.15;
 // paired kernel epilogue form (csr_rpp_kernel OPT, tools/tune_spmv.py ABL_jac_o*):
 // bit 1 = a_ii from the header word
 constexpr int AMG_RPP_OPT = 2;
+// master-pattern form: longest master list, LDS budget of the per-pattern
+// value table (pp_n * J * 16 bytes)
+constexpr int AMG_MP_MAXJ = 32;
+constexpr int AMG_MP_LDS = 48 * 1024;
 
 struct amg_transport; // amg_dist.cpp: RCCL communicator or host-callback test transport
 
@@ -85,6 +89,7 @@ struct amg_ctx {
    int dict_index = 1;  // build dictionary-coded CSR for stencil-like square operators
    int row_pattern = 1; // build row-pattern-coded CSR on top of the dictionary
    int pair_pattern = 1; // paired-row-pattern CSR: 0 off, 1 size-gated for long rows, 2 always
+   int master_pattern = 1; // master-pattern form of square pair-coded operators
 };
 
 struct amg_mat {
@@ -130,6 +135,19 @@ struct amg_mat {
    int pp_n = 0;
    int pp_stride = 0; // words per pair pattern (amg_pp_stride)
    int pp_centre0 = 0; // every pair's first merged entry is both rows' diagonal
+   // master-pattern form (square, diagonal-first pair-coded operators whose
+   // rows are all ordered subsequences of one master list of column offsets:
+   // the diagonal, then the offsets ascending).  The offsets are wave-uniform
+   // kernel arguments; mpmask[p] holds pair pattern p's row-use bits (bit 2j:
+   // row 2t uses master entry j, bit 2j+1: row 2t+1).  mp_uni: one value per
+   // offset over the whole matrix (values are kernel arguments too), else
+   // mpval[p * mp_J + j] = {row 2t's value, row 2t+1's value}.
+   int mp_J = 0; // master length (0: not master-coded)
+   int mp_uni = 0;
+   int mp_off[AMG_MP_MAXJ] = {};
+   double mp_val[AMG_MP_MAXJ] = {};
+   unsigned long long *mpmask = nullptr;
+   double *mpval = nullptr;
 };
 
 struct amg_vec {

@@ -691,6 +691,163 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
    }
 }
 
+// Master-pattern kernel (square diagonal-first operators, amg_internal.h):
+// the lane/row mapping, epilogues and norm partials of csr_rpp_kernel, but the
+// entry walk is over the master list, whose column offsets (and, when
+// UNI, values) are wave-uniform kernel arguments.  Per pair only the 64-bit
+// use mask (and, without UNI, the pattern's value pairs) comes from LDS.  An
+// entry both rows use is one 16-byte load of x[i+o], x[i+1+o]; each row adds
+// its used entries in master order = its CSR order (bit-identical).
+struct MpSten {
+   int off[AMG_MP_MAXJ];
+   double val[AMG_MP_MAXJ];
+};
+
+template <int NEG, bool NEED_DIAG, class Epi, int JM, bool UNI>
+__global__ __launch_bounds__(256) void csr_mp_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
+   const v2d *__restrict__ mval_g, int J, MpSten S, const double *__restrict__ x, int rb, int re, Epi epi,
+   double *__restrict__ partials)
+{
+   constexpr int RPL = 2;
+   const bool xc = pf_is_x<Epi>::value && epi_pf_vec(epi) == x;
+   __shared__ unsigned long long mtab[256];
+   extern __shared__ v2d mval[]; // np * J value pairs (UNI: unused)
+   __shared__ double red[RPL * 8];
+   const int tid = (int)threadIdx.x;
+   if (tid < np) mtab[tid] = mmask_g[tid];
+   if (!UNI)
+      for (int w = tid; w < np * J; w += 256) mval[w] = mval_g[w];
+   const int wg = (int)blockIdx.x;
+   int pid[RPL];
+#pragma unroll
+   for (int q = 0; q < RPL; q++) {
+      const int row = rb + (wg * RPL + q) * 512 + 2 * tid;
+      pid[q] = row < re ? ppat[row >> 1] : 0;
+   }
+   __syncthreads();
+   double sq[RPL][2];
+#pragma unroll
+   for (int q = 0; q < RPL; q++) {
+      const int row = rb + (wg * RPL + q) * 512 + 2 * tid;
+      const bool a0 = row < re, a1 = row + 1 < re;
+      sq[q][0] = sq[q][1] = 0.0;
+      if (a0) {
+         const unsigned long long mk = mtab[pid[q]];
+         const v2d *vp = mval + pid[q] * J;
+         v2d acc, pf{0.0, 0.0};
+         if (a1) {
+            acc = epi.init2(row);
+            if (!xc) pf = epi.pf2(row);
+         } else {
+            acc = v2d{epi.init(row), 0.0};
+            if (!xc) pf = v2d{epi.pf(row), 0.0};
+         }
+#pragma unroll
+         for (int k = 0; k < JM; k += 8) {
+            if (k < J) {
+               v2d xv[8];
+#pragma unroll
+               for (int j = 0; j < 8; j++) {
+                  xv[j] = v2d{0.0, 0.0};
+                  if (k + j < J) {
+                     const unsigned int b = (unsigned int)(mk >> (2 * (k + j))) & 3u;
+                     const double *xp = x + row + S.off[k + j];
+                     if (b == 3)
+                        xv[j] = *reinterpret_cast<const v2du *>(xp);
+                     else if (b == 1)
+                        xv[j].x = xp[0];
+                     else if (b == 2)
+                        xv[j].y = xp[1];
+                  }
+               }
+               if (k == 0 && xc) pf = xv[0]; // master entry 0: both rows' diagonal
+#pragma unroll
+               for (int j = 0; j < 8; j++)
+                  if (k + j < J) {
+                     const unsigned int b = (unsigned int)(mk >> (2 * (k + j))) & 3u;
+                     const v2d v = UNI ? v2d{S.val[k + j], S.val[k + j]} : vp[k + j];
+                     if (b & 1) {
+                        if (NEG)
+                           acc.x -= v.x * xv[j].x;
+                        else
+                           acc.x += v.x * xv[j].x;
+                     }
+                     if (b & 2) {
+                        if (NEG)
+                           acc.y -= v.y * xv[j].y;
+                        else
+                           acc.y += v.y * xv[j].y;
+                     }
+                  }
+            }
+         }
+         // a_ii := A_data[A_i[i]]: master entry 0 (every row's first entry)
+         v2d dg{0.0, 0.0};
+         if (NEED_DIAG) {
+            dg = UNI ? v2d{S.val[0], S.val[0]} : vp[0];
+            if (!a1) dg.y = 0.0;
+         }
+         if (a1) {
+            const v2d out = epi.finish2(row, acc, dg, pf);
+            sq[q][0] = out.x * out.x;
+            sq[q][1] = out.y * out.y;
+         } else {
+            const double out = epi.finish(row, acc.x, dg.x, pf.x);
+            sq[q][0] = out * out;
+         }
+      }
+   }
+   if (partials) {
+      // csr_rpp_kernel's tile sums (block_sum_256's order)
+#pragma unroll
+      for (int q = 0; q < RPL; q++) {
+         double a = sq[q][0], b = sq[q][1];
+#pragma unroll
+         for (int off = 16; off > 0; off >>= 1) {
+            a += __shfl_down(a, off, 32);
+            b += __shfl_down(b, off, 32);
+         }
+         if ((tid & 31) == 0) red[q * 8 + (tid >> 5)] = a + b;
+      }
+      __syncthreads();
+      if (tid < 2 * RPL) {
+         const int tile = wg * RPL * 2 + tid;
+         if (rb + tile * 256 < re)
+            partials[tile] = ((red[tid * 4] + red[tid * 4 + 1]) + red[tid * 4 + 2]) + red[tid * 4 + 3];
+      }
+   }
+}
+
+template <int NEG, bool NEED_DIAG, class Epi>
+static void launch_mp(hipStream_t s, const amg_mat *A, const double *x, int rb, int re, const Epi &e,
+                      double *partials)
+{
+   MpSten S;
+   for (int j = 0; j < AMG_MP_MAXJ; j++) {
+      S.off[j] = A->mp_off[j];
+      S.val[j] = A->mp_val[j];
+   }
+   const int nb = (re - rb + 1023) / 1024;
+   const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+   const size_t lds = A->mp_uni ? 0 : (size_t)A->pp_n * A->mp_J * sizeof(v2d);
+   if (A->mp_J <= 8) {
+      if (A->mp_uni)
+         csr_mp_kernel<NEG, NEED_DIAG, Epi, 8, true><<<nb, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, A->mp_J,
+                                                                      S, x, rb, re, e, partials);
+      else
+         csr_mp_kernel<NEG, NEED_DIAG, Epi, 8, false><<<nb, 256, lds, s>>>(A->ppat, A->mpmask, A->pp_n, mv,
+                                                                         A->mp_J, S, x, rb, re, e, partials);
+   } else {
+      if (A->mp_uni)
+         csr_mp_kernel<NEG, NEED_DIAG, Epi, AMG_MP_MAXJ, true><<<nb, 256, 0, s>>>(
+            A->ppat, A->mpmask, A->pp_n, mv, A->mp_J, S, x, rb, re, e, partials);
+      else
+         csr_mp_kernel<NEG, NEED_DIAG, Epi, AMG_MP_MAXJ, false><<<nb, 256, lds, s>>>(
+            A->ppat, A->mpmask, A->pp_n, mv, A->mp_J, S, x, rb, re, e, partials);
+   }
+}
+
 // dictionary-coded launches: rows of <= 8 entries (7-pt stencil, interpolation)
 // take four 256-row tiles per workgroup, longer rows (27-pt Galerkin,
 // restriction) two (tools/tune_spmv.py, profiles/r01/tune_spmv.log); the
@@ -699,7 +856,9 @@ template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int rb, int re,
                          const Epi &e, double *partials, int tiles)
 {
-   if (A->ppat && (rb & 1) == 0)
+   if (A->mp_J && (rb & 1) == 0)
+      launch_mp<NEG, NEED_DIAG>(s, A, x, rb, re, e, partials);
+   else if (A->ppat && (rb & 1) == 0)
       csr_rpp_kernel<NEG, NEED_DIAG, Epi, 2><<<(re - rb + 1023) / 1024, 256, A->pp_n * A->pp_stride * 4, s>>>(
          A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->pp_stride, A->danch,
          A->pp_centre0);

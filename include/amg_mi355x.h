@@ -151,6 +151,15 @@ int amg_mat_row_pattern(const amg_mat *A);
 int amg_set_pair_pattern(amg_ctx *ctx, int enable);
 /* number of distinct row-pair patterns of A (0: not pair-coded) */
 int amg_mat_pair_pattern(const amg_mat *A);
+/* master-pattern storage (default on; env AMG_MASTER_PATTERN=0 disables), built
+ * on top of the pair patterns of square diagonal-first operators whose rows'
+ * column offsets all follow one master order (the diagonal, then ascending):
+ * the offsets become wave-uniform kernel arguments and each pair pattern only
+ * says which master entries its two rows use (bit-identical results). */
+int amg_set_master_pattern(amg_ctx *ctx, int enable);
+/* master length J of A (0: not master-coded); negative (-J) when every master
+ * entry carries one value over the whole matrix */
+int amg_mat_master_pattern(const amg_mat *A);
 int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz);
 int amg_mat_download(amg_ctx *ctx, const amg_mat *A, int *rowptr, int *col, double *val);
 
