@@ -479,7 +479,7 @@ static int build_pair_pattern(amg_mat *A)
 // per-entry LDS lookups of the pair kernel disappear.
 static int build_master_pattern(amg_mat *A)
 {
-   if (!A->ppat || A->danch || A->nrows != A->ncols || A->pp_n < 1) return AMG_OK;
+   if (!A->ppat || A->danch || A->nrows != A->ncols || A->nrows < 2 || A->pp_n < 1) return AMG_OK;
    hipStream_t s = A->ctx->stream;
    const int T = A->pp_n, PS = A->pp_stride, D = A->dc_n;
    std::vector<unsigned int> tab((size_t)T * PS);

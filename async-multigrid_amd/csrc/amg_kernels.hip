@@ -703,13 +703,55 @@ struct MpSten {
    double val[AMG_MP_MAXJ];
 };
 
-template <int NEG, bool NEED_DIAG, class Epi, int JM, bool UNI>
+// exact per-entry gather (csr_mp_kernel FORM 1): row 2t's operand loaded only
+// when it uses the entry, row 2t+1's likewise, one 16-byte load when both do
+template <int NEG, int JM, bool UNI>
+__device__ __forceinline__ v2d mp_gather_exact(v2d acc, v2d &pf, bool xc, unsigned long long mk,
+                                               const v2d *vp, int J, const MpSten &S,
+                                               const double *__restrict__ x, int row)
+{
+#pragma unroll
+   for (int k = 0; k < JM; k += 8) {
+      if (k < J) {
+         v2d xv[8];
+#pragma unroll
+         for (int j = 0; j < 8; j++) {
+            xv[j] = v2d{0.0, 0.0};
+            if (k + j < J) {
+               const unsigned int b = (unsigned int)(mk >> (2 * (k + j))) & 3u;
+               const double *xp = x + row + S.off[k + j];
+               if (b == 3)
+                  xv[j] = *reinterpret_cast<const v2du *>(xp);
+               else if (b == 1)
+                  xv[j].x = xp[0];
+               else if (b == 2)
+                  xv[j].y = xp[1];
+            }
+         }
+         if (k == 0 && xc) pf = xv[0]; // master entry 0: both rows' diagonal
+#pragma unroll
+         for (int j = 0; j < 8; j++)
+            if (k + j < J) {
+               const unsigned int b = (unsigned int)(mk >> (2 * (k + j))) & 3u;
+               const v2d v = UNI ? v2d{S.val[k + j], S.val[k + j]} : vp[k + j];
+               if (b & 1) acc.x = NEG ? acc.x - v.x * xv[j].x : acc.x + v.x * xv[j].x;
+               if (b & 2) acc.y = NEG ? acc.y - v.y * xv[j].y : acc.y + v.y * xv[j].y;
+            }
+      }
+   }
+   return acc;
+}
+
+// FORM 3 (default): 16-byte gather of every entry, unused entries re-read the
+// pair's own x (no branches), edge waves through mp_gather_exact; FORM 1:
+// mp_gather_exact everywhere; FORM 0: branch-free clamped gather; FORM 2: as
+// FORM 3 with a branch per entry (tools/tune_spmv.py mp_*)
+template <int NEG, bool NEED_DIAG, class Epi, int JM, bool UNI, int FORM = 3, int RPL = 2>
 __global__ __launch_bounds__(256) void csr_mp_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
-   const v2d *__restrict__ mval_g, int J, MpSten S, const double *__restrict__ x, int rb, int re, Epi epi,
+   const v2d *__restrict__ mval_g, int J, MpSten S, const double *__restrict__ x, int N, int rb, int re, Epi epi,
    double *__restrict__ partials)
 {
-   constexpr int RPL = 2;
    const bool xc = pf_is_x<Epi>::value && epi_pf_vec(epi) == x;
    __shared__ unsigned long long mtab[256];
    extern __shared__ v2d mval[]; // np * J value pairs (UNI: unused)
@@ -743,44 +785,83 @@ __global__ __launch_bounds__(256) void csr_mp_kernel(
             acc = v2d{epi.init(row), 0.0};
             if (!xc) pf = v2d{epi.pf(row), 0.0};
          }
+         if constexpr (FORM == 1) {
+            acc = mp_gather_exact<NEG, JM, UNI>(acc, pf, xc, mk, vp, J, S, x, row);
+         } else if constexpr (FORM == 2 || FORM == 3) {
+         // A used entry is one 16-byte load of x[row + o], x[row + o + 1]
+         // whichever of the pair's rows use it: inside x whenever
+         // row + omin >= 0 and row + omax + 2 <= N (omin/omax over the master
+         // offsets; FORM 3's unused entries read x[row], x[row + 1]).  Waves
+         // holding a row outside that window (for the 7-pt stencil the first
+         // and last two planes) take the exact per-entry form.
+         int omin = 0, omax = 0;
+         for (int j = 0; j < J; j++) {
+            omin = min(omin, S.off[j]);
+            omax = max(omax, S.off[j]);
+         }
+         const bool edge = (long long)row + omin < 0 || (long long)row + omax + 2 > N;
+         if (__any(edge)) {
+            acc = mp_gather_exact<NEG, JM, UNI>(acc, pf, xc, mk, vp, J, S, x, row);
+         } else {
 #pragma unroll
          for (int k = 0; k < JM; k += 8) {
             if (k < J) {
                v2d xv[8];
 #pragma unroll
                for (int j = 0; j < 8; j++) {
-                  xv[j] = v2d{0.0, 0.0};
-                  if (k + j < J) {
-                     const unsigned int b = (unsigned int)(mk >> (2 * (k + j))) & 3u;
-                     const double *xp = x + row + S.off[k + j];
-                     if (b == 3)
-                        xv[j] = *reinterpret_cast<const v2du *>(xp);
-                     else if (b == 1)
-                        xv[j].x = xp[0];
-                     else if (b == 2)
-                        xv[j].y = xp[1];
+                  if (FORM == 3) {
+                     // unused entries re-read the pair's own x[row], x[row+1]
+                     const int o = ((mk >> (2 * (k + j))) & 3u) ? S.off[k + j] : 0;
+                     xv[j] = *reinterpret_cast<const v2du *>(x + row + o);
+                  } else {
+                     xv[j] = v2d{0.0, 0.0};
+                     if ((mk >> (2 * (k + j))) & 3u) xv[j] = *reinterpret_cast<const v2du *>(x + row + S.off[k + j]);
                   }
                }
-               if (k == 0 && xc) pf = xv[0]; // master entry 0: both rows' diagonal
+               if (k == 0 && xc) pf = xv[0];
 #pragma unroll
-               for (int j = 0; j < 8; j++)
-                  if (k + j < J) {
-                     const unsigned int b = (unsigned int)(mk >> (2 * (k + j))) & 3u;
-                     const v2d v = UNI ? v2d{S.val[k + j], S.val[k + j]} : vp[k + j];
-                     if (b & 1) {
-                        if (NEG)
-                           acc.x -= v.x * xv[j].x;
-                        else
-                           acc.x += v.x * xv[j].x;
-                     }
-                     if (b & 2) {
-                        if (NEG)
-                           acc.y -= v.y * xv[j].y;
-                        else
-                           acc.y += v.y * xv[j].y;
-                     }
-                  }
+               for (int j = 0; j < 8; j++) {
+                  const unsigned int b = (unsigned int)(mk >> (2 * (k + j))) & 3u;
+                  const v2d v = UNI ? v2d{S.val[k + j], S.val[k + j]} : vp[min(k + j, J - 1)];
+                  if (b & 1) acc.x = NEG ? acc.x - v.x * xv[j].x : acc.x + v.x * xv[j].x;
+                  if (b & 2) acc.y = NEG ? acc.y - v.y * xv[j].y : acc.y + v.y * xv[j].y;
+               }
             }
+         }
+         }
+         } else {
+#pragma unroll
+         for (int k = 0; k < JM; k += 8) {
+            if (k < J) {
+               // branch-free gather: every entry issues one 16-byte load at
+               // s = clamp(row + o, 0, N - 2), which covers the element(s) the
+               // pair's used rows need (row 2t: row + o, row 2t+1: row + 1 + o,
+               // both in [0, N)); unused entries load a harmless in-range word.
+               // All loads of a chunk are in flight together.
+               v2d xv[8];
+               bool lo[8];
+#pragma unroll
+               for (int j = 0; j < 8; j++) {
+                  const int base = row + S.off[k + j];
+                  const int sidx = min(max(base, 0), N - 2);
+                  lo[j] = sidx == base;
+                  xv[j] = *reinterpret_cast<const v2du *>(x + sidx);
+               }
+               // entries past J: offset 0 (a valid load), use bits 0
+#pragma unroll
+               for (int j = 0; j < 8; j++) {
+                     const unsigned int b = (unsigned int)(mk >> (2 * (k + j))) & 3u;
+                     const double x0 = lo[j] ? xv[j].x : xv[j].y; // row 2t's operand
+                     const double x1 = lo[j] ? xv[j].y : xv[j].x; // row 2t+1's operand
+                     if (k + j == 0 && xc) pf = v2d{x0, x1}; // master entry 0: both rows' diagonal
+                     const v2d v = UNI ? v2d{S.val[k + j], S.val[k + j]} : vp[min(k + j, J - 1)];
+                     const double s0 = NEG ? acc.x - v.x * x0 : acc.x + v.x * x0;
+                     const double s1 = NEG ? acc.y - v.y * x1 : acc.y + v.y * x1;
+                     acc.x = (b & 1) ? s0 : acc.x;
+                     acc.y = (b & 2) ? s1 : acc.y;
+               }
+            }
+         }
          }
          // a_ii := A_data[A_i[i]]: master entry 0 (every row's first entry)
          v2d dg{0.0, 0.0};
@@ -834,17 +915,17 @@ static void launch_mp(hipStream_t s, const amg_mat *A, const double *x, int rb, 
    if (A->mp_J <= 8) {
       if (A->mp_uni)
          csr_mp_kernel<NEG, NEED_DIAG, Epi, 8, true><<<nb, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, A->mp_J,
-                                                                      S, x, rb, re, e, partials);
+                                                                      S, x, A->ncols, rb, re, e, partials);
       else
          csr_mp_kernel<NEG, NEED_DIAG, Epi, 8, false><<<nb, 256, lds, s>>>(A->ppat, A->mpmask, A->pp_n, mv,
-                                                                         A->mp_J, S, x, rb, re, e, partials);
+                                                                         A->mp_J, S, x, A->ncols, rb, re, e, partials);
    } else {
       if (A->mp_uni)
          csr_mp_kernel<NEG, NEED_DIAG, Epi, AMG_MP_MAXJ, true><<<nb, 256, 0, s>>>(
-            A->ppat, A->mpmask, A->pp_n, mv, A->mp_J, S, x, rb, re, e, partials);
+            A->ppat, A->mpmask, A->pp_n, mv, A->mp_J, S, x, A->ncols, rb, re, e, partials);
       else
          csr_mp_kernel<NEG, NEED_DIAG, Epi, AMG_MP_MAXJ, false><<<nb, 256, lds, s>>>(
-            A->ppat, A->mpmask, A->pp_n, mv, A->mp_J, S, x, rb, re, e, partials);
+            A->ppat, A->mpmask, A->pp_n, mv, A->mp_J, S, x, A->ncols, rb, re, e, partials);
    }
 }
 
@@ -1002,12 +1083,23 @@ static inline bool short_rows(const amg_mat *A) { return A->nnz < 12LL * A->nrow
 // row's outputs and returns the value whose square feeds the norm partials.
 
 // y = SpGEMV epilogue (SMEM_MatVec.cpp:140-258)
+// 16-byte store of rows (i, i+1); nt: nontemporal (streamed past the
+// caches, for fine-grid outputs far larger than L2 + Infinity Cache)
+__device__ __forceinline__ void st2(double *p, v2d v, int nt)
+{
+   if (nt)
+      __builtin_nontemporal_store(v, reinterpret_cast<v2du *>(p));
+   else
+      *reinterpret_cast<v2du *>(p) = v;
+}
+
 struct EpiGemv {
    const double *b;
    double *y;
    int imode;
    int scale;
    double alpha, temp;
+   int nt = 0;
    __device__ __forceinline__ double init(int i) const
    {
       switch (imode) {
@@ -1041,7 +1133,7 @@ struct EpiGemv {
    __device__ __forceinline__ v2d finish2(int i, v2d acc, v2d, v2d) const
    {
       const v2d v = scale ? v2d{alpha * acc.x, alpha * acc.y} : acc;
-      *reinterpret_cast<v2du *>(y + i) = v;
+      st2(y + i, v, nt);
       return v;
    }
 };
@@ -1052,6 +1144,7 @@ struct EpiJacobi {
    const double *x;
    double *out;
    double omega;
+   int nt = 0;
    __device__ __forceinline__ double init(int i) const { return f[i]; }
    __device__ __forceinline__ double pf(int i) const { return x[i]; }
    __device__ __forceinline__ double finish(int i, double res, double a, double xi) const
@@ -1066,7 +1159,7 @@ struct EpiJacobi {
    {
       const v2d v{(a.x != 0.0) ? xi.x + omega * res.x / a.x : xi.x,
                   (a.y != 0.0) ? xi.y + omega * res.y / a.y : xi.y};
-      *reinterpret_cast<v2du *>(out + i) = v;
+      st2(out + i, v, nt);
       return v;
    }
 };
@@ -1108,6 +1201,7 @@ struct EpiResJacobi {
    double *r;
    double *unext;
    double omega;
+   int nt = 0;
    __device__ __forceinline__ double init(int i) const { return f[i]; }
    __device__ __forceinline__ double pf(int i) const { return x[i]; }
    __device__ __forceinline__ double finish(int i, double res, double a, double xi) const
@@ -1120,7 +1214,7 @@ struct EpiResJacobi {
    __device__ __forceinline__ v2d pf2(int i) const { return *reinterpret_cast<const v2du *>(x + i); }
    __device__ __forceinline__ v2d finish2(int i, v2d res, v2d a, v2d xi) const
    {
-      if (r) *reinterpret_cast<v2du *>(r + i) = res;
+      if (r) st2(r + i, res, nt);
       v2d v;
       if (l1) {
          const v2d l = *reinterpret_cast<const v2du *>(l1 + i);
@@ -1129,7 +1223,7 @@ struct EpiResJacobi {
          v = v2d{(a.x != 0.0) ? xi.x + omega * res.x / a.x : xi.x,
                  (a.y != 0.0) ? xi.y + omega * res.y / a.y : xi.y};
       }
-      *reinterpret_cast<v2du *>(unext + i) = v;
+      st2(unext + i, v, nt);
       return res;
    }
 };
@@ -1362,7 +1456,31 @@ __global__ __launch_bounds__(256) void ablation_kernel(const int *__restrict__ r
    if (row < r1) y[row] = acc;
 }
 
-int num_tune_variants() { return 53; }
+// tools/tune_spmv.py mp_* variants: y = A x (GEMV), r = x - A x (RES) or a
+// Jacobi sweep (JAC, f = x) through csr_mp_kernel forms
+template <int FORM, int RPL, int OP, int NT = 0>
+static void launch_mp_tune(hipStream_t s, const amg_mat *A, const double *x, double *y)
+{
+   if (!A->mp_J || !A->mp_uni || A->mp_J > 8) return;
+   MpSten S;
+   for (int j = 0; j < AMG_MP_MAXJ; j++) {
+      S.off[j] = A->mp_off[j];
+      S.val[j] = A->mp_val[j];
+   }
+   const int nb = (A->nrows + 512 * RPL - 1) / (512 * RPL);
+   const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+   if (OP == 2) {
+      EpiJacobi e{x, x, y, 0.8, NT};
+      csr_mp_kernel<1, true, EpiJacobi, 8, true, FORM, RPL><<<nb, 256, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, mv, A->mp_J, S, x, A->ncols, 0, A->nrows, e, nullptr);
+   } else {
+      EpiGemv e{x, y, OP == 1 ? 1 : 0, 0, 1.0, 0.0, NT};
+      csr_mp_kernel<OP == 1 ? 1 : 0, false, EpiGemv, 8, true, FORM, RPL><<<nb, 256, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, mv, A->mp_J, S, x, A->ncols, 0, A->nrows, e, nullptr);
+   }
+}
+
+int num_tune_variants() { return 71; }
 
 template <int RPL, bool STAGE, int MAXR = AMG_DC_MAXROW>
 static void launch_dc(hipStream_t s, const amg_mat *A, const double *x, double *y)
@@ -1527,8 +1645,13 @@ const char *tune_variant_name(int v)
                                  "long_t256_r64", "long_t128_r16", "long_t256_r256",
                                  "ABL_copy_v2", "ABL_pair_st_v2", "ABL_copy_v4", "ABL_pair_st_v4",
                                  "rpp_rpl1", "rpp_rpl2", "rpp_rpl4",
-                                 "ABL_jac_o0", "ABL_jac_o1", "ABL_jac_o2", "ABL_jac_o3"};
-   return (v >= 0 && v < 53) ? names[v] : "?";
+                                 "ABL_jac_o0", "ABL_jac_o1", "ABL_jac_o2", "ABL_jac_o3",
+                                 "mp_bf_rpl2", "mp_br_rpl2", "mp_bf_rpl1", "mp_bf_rpl4",
+                                 "ABL_mp_bf_res", "ABL_mp_br_res", "ABL_mp_bf_jac", "ABL_mp_br_jac",
+                                 "mp_f2_rpl2", "ABL_mp_f2_res", "ABL_mp_br_res_nt", "ABL_mp_br_jac_nt",
+                                 "ABL_mp_f2_res_nt", "ABL_mp_f2_jac", "mp_f3_rpl2", "ABL_mp_f3_res", "ABL_mp_f3_jac",
+                                 "mp_f3_rpl4"};
+   return (v >= 0 && v < 71) ? names[v] : "?";
 }
 
 void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y)
@@ -1620,6 +1743,24 @@ void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x
    case 50: launch_rpp_jac<1>(s, A, x, y); break;
    case 51: launch_rpp_jac<2>(s, A, x, y); break;
    case 52: launch_rpp_jac<3>(s, A, x, y); break;
+   case 53: launch_mp_tune<0, 2, 0>(s, A, x, y); break;
+   case 54: launch_mp_tune<1, 2, 0>(s, A, x, y); break;
+   case 55: launch_mp_tune<0, 1, 0>(s, A, x, y); break;
+   case 56: launch_mp_tune<0, 4, 0>(s, A, x, y); break;
+   case 57: launch_mp_tune<0, 2, 1>(s, A, x, y); break;
+   case 58: launch_mp_tune<1, 2, 1>(s, A, x, y); break;
+   case 59: launch_mp_tune<0, 2, 2>(s, A, x, y); break;
+   case 60: launch_mp_tune<1, 2, 2>(s, A, x, y); break;
+   case 61: launch_mp_tune<2, 2, 0>(s, A, x, y); break;
+   case 62: launch_mp_tune<2, 2, 1>(s, A, x, y); break;
+   case 63: launch_mp_tune<1, 2, 1, 1>(s, A, x, y); break;
+   case 64: launch_mp_tune<1, 2, 2, 1>(s, A, x, y); break;
+   case 65: launch_mp_tune<2, 2, 1, 1>(s, A, x, y); break;
+   case 66: launch_mp_tune<2, 2, 2>(s, A, x, y); break;
+   case 67: launch_mp_tune<3, 2, 0>(s, A, x, y); break;
+   case 68: launch_mp_tune<3, 2, 1>(s, A, x, y); break;
+   case 69: launch_mp_tune<3, 2, 2>(s, A, x, y); break;
+   case 70: launch_mp_tune<3, 4, 0>(s, A, x, y); break;
    default: break;
    }
 }

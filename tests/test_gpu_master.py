@@ -139,3 +139,54 @@ def test_master_solve_matches_oracle(amg, oracle, ctx, interp):
     for v in dev.values():
         for M in v:
             M.free()
+
+
+def test_master_long_range_edges(ctx, amg):
+    """Rows coupling at +-1 and +-L (L = 1000, N = 5001): the 16-byte gather
+    runs only in waves whose rows keep row + omin >= 0 and row + omax + 2 <= N;
+    the waves at both ends (and the half pair at the odd end) take the exact
+    per-entry form.  Bit-identical to plain CSR."""
+    N, L = 5001, 1000
+    rows, cols, vals = [], [], []
+    rp = [0]
+    for i in range(N):
+        ent = [(i, 4.0)]
+        for o in (-L, -1, 1, L):
+            if 0 <= i + o < N:
+                ent.append((i + o, -0.75 if abs(o) == 1 else -0.125))
+        cols += [c for c, _ in ent]
+        vals += [v for _, v in ent]
+        rp.append(len(cols))
+    rp = np.array(rp, np.int32)
+    cols = np.array(cols, np.int32)
+    vals = np.array(vals, np.float64)
+    ctx.set_pair_pattern(2)
+    try:
+        M = ctx.csr(N, N, rp, cols, vals)
+    finally:
+        ctx.set_pair_pattern(1)
+    ctx.set_value_index(0)
+    ctx.set_dict_index(0)
+    try:
+        P = ctx.csr(N, N, rp, cols, vals)
+    finally:
+        ctx.set_value_index(1)
+        ctx.set_dict_index(1)
+    assert M.master_pattern == -5 and P.master_pattern == 0
+    x = ctx.vec(_vecs(N, 21))
+    b = ctx.vec(_vecs(N, 22))
+    for ab in ((1.0, 0.0), (-1.0, 1.0), (2.5, -0.5)):
+        ys = []
+        for A in (P, M):
+            y = ctx.vec(N)
+            amg.smem.SMEM_SpGEMV(ctx, A, x, b, ab[0], ab[1], y, 0, N)
+            ys.append(y.download())
+        assert_bitwise(ys[1], ys[0], f"gemv {ab}")
+    us = []
+    for A in (P, M):
+        u = ctx.vec(_vecs(N, 23))
+        amg.smem.SMEM_Sync_Parfor_Jacobi(ctx, A, b, u, ctx.vec(N), 3, 0, 0.7)
+        us.append(u.download())
+    assert_bitwise(us[1], us[0], "jacobi")
+    M.free()
+    P.free()
