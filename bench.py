@@ -44,12 +44,16 @@ def parse():
     return p.parse_args()
 
 
-def storage(nrows, nnz, vi, dc, rp, pp=0):
+def storage(nrows, nnz, vi, dc, rp, pp=0, mp=0):
     """(matrix bytes the hot kernels stream per pass, format name), DESIGN.md Sec.4:
-    paired-row-pattern CSR reads one byte per pair of rows; row-pattern-coded
+    master-pattern and paired-row-pattern CSR read one byte per pair of rows; row-pattern-coded
     CSR one byte per row; dictionary-coded one byte per
     entry + the row pointer; value-indexed 4 (col) + 1 per entry + the row
     pointer; CSR 4 (col) + 8 (val) per entry + the row pointer."""
+    if pp and mp:
+        vals = "one value per offset" if mp < 0 else "per-pattern values"
+        return (nrows + 1) // 2, (f"csr-mp ({abs(mp)}-offset master list, {vals}, {pp} row-pair use masks "
+                                  f"over {rp} row patterns)")
     if pp:
         return (nrows + 1) // 2, (f"csr-rpp ({pp} row-pair patterns over {rp} row patterns and a "
                                   f"{dc}-entry (offset, value) dictionary)")
@@ -146,7 +150,7 @@ def main():
     z0 = As[0].nnz
     # matrix bytes per pass in the format the kernels stream
     mat_bytes, fmt = storage(n0, z0, As[0].value_index, As[0].dict_index, As[0].row_pattern,
-                                 As[0].pair_pattern)
+                             As[0].pair_pattern, As[0].master_pattern)
     # dominant kernel: fine-grid residual SpGEMV r = f - A u (matrix + f, u, r)
     res_bytes = mat_bytes + 24 * n0
     res_ms = ms[0] / max(launches[0], 1)

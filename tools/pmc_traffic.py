@@ -42,8 +42,12 @@ def pick(rows, pattern, grid=None):
         if not m:
             continue
         rpl = re.search(r"csr_(dc|rp|rpp)_kernel<\d, \w+, [\w:]+, (\d+)[,>]", name)
-        # a paired-row-pattern lane owns two rows
-        rows_done = g * (int(rpl.group(2)) * (2 if rpl.group(1) == "rpp" else 1) if rpl else 1)
+        mp = re.search(r"csr_mp_kernel<\d, \w+, [\w:]+, \d+, \w+, \d+, (\d+)>", name)
+        # a paired-row-pattern or master-pattern lane owns two rows per slab
+        if mp:
+            rows_done = g * int(mp.group(1)) * 2
+        else:
+            rows_done = g * (int(rpl.group(2)) * (2 if rpl.group(1) == "rpp" else 1) if rpl else 1)
         if grid is None or rows_done == grid:
             out += vals
     return out
@@ -60,8 +64,9 @@ def main():
     rows = n ** 3
     z = 7 * rows - 6 * n * n
     res = {}
-    for fmt, vi in (("csr-rpp", "rpp"), ("csr-rp", "rp"), ("csr-dc", "dc"), ("csr-vi", "true"), ("csr", "false")):
-        pat = {"rpp": r"csr_rpp_kernel<1, false, amgk::EpiGemv,",
+    for fmt, vi in (("csr-mp", "mp"), ("csr-rpp", "rpp"), ("csr-rp", "rp"), ("csr-dc", "dc"), ("csr-vi", "true"), ("csr", "false")):
+        pat = {"mp": r"csr_mp_kernel<1, false, amgk::EpiGemv,",
+               "rpp": r"csr_rpp_kernel<1, false, amgk::EpiGemv,",
                "rp": r"csr_rp_kernel<1, false, amgk::EpiGemv,",
                "dc": r"csr_dc_kernel<1, false, amgk::EpiGemv,"}.get(
                    vi, r"csr_tile_kernel<.*>, 1, false, amgk::EpiGemv, %s" % vi)
@@ -71,6 +76,8 @@ def main():
             continue
         Fm, Wm = sum(F) / len(F), sum(W) / len(W)
         # the paired kernel reads f with 16-byte lanes and one pattern byte per row pair
+        if vi == "mp":
+            vi = "rpp"  # same streams: f in 16-byte lanes, one pattern byte per row pair
         s16 = {"rpp": 8 * rows, "rp": 0, "dc": 0, "true": 4 * z, "false": 12 * z}[vi]
         s4 = {"rpp": 0, "rp": 0, "dc": 0, "true": z, "false": 0}[vi] + (
             0 if vi in ("rp", "rpp") else 4 * (rows + 1))
@@ -88,6 +95,14 @@ def main():
     doc = {str(n): {"factors": fac, **res,
                     "note": "FETCH_SIZE/WRITE_SIZE from separate rocprofv3 --pmc passes, corrected per "
                             "access width by calibration streams of known size (tools/pmc_traffic.py)"}}
+    try:  # keep formats profiled earlier (other storage forms) for this n
+        old = json.load(open(out))
+        for k, v in old.get(str(n), {}).items():
+            doc[str(n)].setdefault(k, v)
+        for k, v in old.items():
+            doc.setdefault(k, v)
+    except (OSError, ValueError):
+        pass
     json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps(doc, indent=1))
 
