@@ -81,6 +81,10 @@ class Context:
         """Paired-row-pattern CSR on top of the row patterns (default on)."""
         check(lib.amg_set_pair_pattern(self.h, int(enable)))
 
+    def set_pair_anchor16(self, enable):
+        """Slab-compressed anchors of pair-coded P/R registered from now on (default off)."""
+        check(lib.amg_set_pair_anchor16(self.h, int(enable)))
+
     def set_master_pattern(self, enable):
         """Master-pattern form of square pair-coded operators (default on)."""
         check(lib.amg_set_master_pattern(self.h, int(enable)))
@@ -114,6 +118,7 @@ class Mat:
         self.dict_index = lib.amg_mat_dict_index(handle)    # dictionary size, 0 = not coded
         self.row_pattern = lib.amg_mat_row_pattern(handle)  # distinct row patterns, 0 = not coded
         self.pair_pattern = lib.amg_mat_pair_pattern(handle)  # distinct row-pair patterns, 0 = not coded
+        self.pair_anchor16 = lib.amg_mat_pair_anchor16(handle)  # slab-compressed anchors
         self.master_pattern = lib.amg_mat_master_pattern(handle)  # master length J (-J: uniform values), 0 = not coded
 
     @classmethod

@@ -72,6 +72,8 @@ PROTOTYPES = {
     "amg_mat_row_pattern": (_i, [_p]),
     "amg_set_pair_pattern": (_i, [_p, _i]),
     "amg_mat_pair_pattern": (_i, [_p]),
+    "amg_set_pair_anchor16": (_i, [_p, _i]),
+    "amg_mat_pair_anchor16": (_i, [_p]),
     "amg_set_master_pattern": (_i, [_p, _i]),
     "amg_mat_master_pattern": (_i, [_p]),
     "amg_mat_info": (_i, [_p, _ip, _ip, _llp]),

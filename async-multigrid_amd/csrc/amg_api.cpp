@@ -78,6 +78,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_ROW_PATTERN")) c->row_pattern = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_PAIR_PATTERN")) c->pair_pattern = std::min(2, std::max(0, std::atoi(v)));
    if (const char *v = std::getenv("AMG_MASTER_PATTERN")) c->master_pattern = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_PAIR_ANCHOR16")) c->pair_anchor16 = std::atoi(v) != 0;
    *out = c;
    return AMG_OK;
 }
@@ -370,6 +371,36 @@ static void pair_merge(const unsigned char *a, int la, const unsigned char *b, i
    }
 }
 
+// Slab-compressed anchors for the paired kernel (amg_internal.h): anchor(2t)
+// = pbase[2t >> 9] + pdelta[t].  Kept only when every 512-row slab's anchors
+// span at most 65535 (interpolation: a fine line maps to half a coarse line).
+static int compress_pair_anchors(amg_mat *A)
+{
+   hipStream_t s = A->ctx->stream;
+   const size_t ns = ((size_t)A->nrows + 511) / 512, np = ((size_t)A->nrows + 1) / 2;
+   int *ok = nullptr;
+   hipError_t e = hipMalloc(&A->pbase, ns * sizeof(int));
+   if (e == hipSuccess) e = hipMalloc(&A->pdelta, np * sizeof(unsigned short));
+   if (e == hipSuccess) e = hipMalloc(&ok, sizeof(int));
+   int okh = 0;
+   if (e == hipSuccess) {
+      const int one = 1;
+      AMG_HIP(hipMemcpyAsync(ok, &one, sizeof(int), hipMemcpyHostToDevice, s));
+      amgk::pp_anchor_compress(s, A, A->pbase, A->pdelta, ok);
+      AMG_HIP(hipMemcpyAsync(&okh, ok, sizeof(int), hipMemcpyDeviceToHost, s));
+      AMG_HIP(hipStreamSynchronize(s));
+   }
+   hipFree(ok);
+   if (e != hipSuccess || !okh) {
+      hipFree(A->pbase);
+      hipFree(A->pdelta);
+      A->pbase = nullptr;
+      A->pdelta = nullptr;
+      (void)hipGetLastError();
+   }
+   return AMG_OK;
+}
+
 static int build_pair_pattern(amg_mat *A)
 {
    amg_ctx *c = A->ctx;
@@ -467,6 +498,7 @@ static int build_pair_pattern(amg_mat *A)
    A->pp_n = T;
    A->pp_stride = PS;
    A->pp_centre0 = centre0 ? 1 : 0;
+   if (A->ctx->pair_anchor16 && A->danch && A->nrows > 0) AMG_TRY(compress_pair_anchors(A));
    return AMG_OK;
 }
 
@@ -593,6 +625,18 @@ extern "C" int amg_mat_pair_pattern(const amg_mat *A)
    return A ? A->pp_n : 0;
 }
 
+extern "C" int amg_set_pair_anchor16(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_pair_anchor16: null context");
+   c->pair_anchor16 = enable ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_pair_anchor16(const amg_mat *A)
+{
+   return (A && A->pdelta) ? 1 : 0;
+}
+
 extern "C" int amg_set_master_pattern(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_master_pattern: null context");
@@ -679,6 +723,8 @@ extern "C" int amg_mat_free(amg_mat *A)
    hipFree(A->pptab);
    hipFree(A->mpmask);
    hipFree(A->mpval);
+   hipFree(A->pbase);
+   hipFree(A->pdelta);
    delete A;
    return AMG_OK;
 }

@@ -90,6 +90,7 @@ struct amg_ctx {
    int row_pattern = 1; // build row-pattern-coded CSR on top of the dictionary
    int pair_pattern = 1; // paired-row-pattern CSR: 0 off, 1 size-gated for long rows, 2 always
    int master_pattern = 1; // master-pattern form of square pair-coded operators
+   int pair_anchor16 = 0;  // slab-compressed anchors of pair-coded P/R (measured slower: off)
 };
 
 struct amg_mat {
@@ -142,6 +143,11 @@ struct amg_mat {
    // row 2t uses master entry j, bit 2j+1: row 2t+1).  mp_uni: one value per
    // offset over the whole matrix (values are kernel arguments too), else
    // mpval[p * mp_J + j] = {row 2t's value, row 2t+1's value}.
+   // slab-compressed anchors of pair-coded operators with an anchor array:
+   // anchor(2t) = pbase[2t >> 9] + pdelta[t] (every 512-row slab's anchors
+   // within 65535 of its least), 2 bytes per row pair instead of 4 per row
+   int *pbase = nullptr;
+   unsigned short *pdelta = nullptr;
    int mp_J = 0; // master length (0: not master-coded)
    int mp_uni = 0;
    int mp_off[AMG_MP_MAXJ] = {};
@@ -262,6 +268,9 @@ void rp_table(hipStream_t s, const amg_mat *A, const int *rep, int T, unsigned c
 void rp_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
                const unsigned char *ptab, unsigned char *rpat, int *bad);
 void pp_collect(hipStream_t s, const amg_mat *A, unsigned char *flags);
+// slab-compressed anchors (pbase, pdelta); ok set to 0 when a slab's range
+// exceeds 16 bits
+void pp_anchor_compress(hipStream_t s, const amg_mat *A, int *pbase, unsigned short *pdelta, int *ok);
 void pp_encode(hipStream_t s, const amg_mat *A, const unsigned char *map, unsigned char *ppat,
                unsigned long long *counts);
 

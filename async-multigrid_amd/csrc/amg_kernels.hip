@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
    const unsigned char *__restrict__ ppat, const unsigned int *__restrict__ pptab_g, int np,
    const int *__restrict__ doff_g, const double *__restrict__ dval_g, const double *__restrict__ x,
    int rb, int re, Epi epi, double *__restrict__ partials, int T, int PS, const int *__restrict__ anch,
-   int c0)
+   int c0, const int *__restrict__ pbase = nullptr, const unsigned short *__restrict__ pdelta = nullptr)
 {
    const bool xc = pf_is_x<Epi>::value && c0 && epi_pf_vec(epi) == x;
    __shared__ int otab[256];
@@ -572,7 +572,11 @@ __global__ __launch_bounds__(256) void csr_rpp_kernel(
       const int row = rb + (wg * RPL + q) * 512 + 2 * tid;
       pid[q] = row < re ? ppat[row >> 1] : 0;
       base[q] = row;
-      if (anch && row < re) base[q] = anch[row];
+      if (pdelta) {
+         if (row < re) base[q] = pbase[row >> 9] + (int)pdelta[row >> 1];
+      } else if (anch && row < re) {
+         base[q] = anch[row];
+      }
    }
    __syncthreads();
    double sq[RPL][2];
@@ -942,7 +946,7 @@ static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int r
    else if (A->ppat && (rb & 1) == 0)
       csr_rpp_kernel<NEG, NEED_DIAG, Epi, 2><<<(re - rb + 1023) / 1024, 256, A->pp_n * A->pp_stride * 4, s>>>(
          A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->pp_stride, A->danch,
-         A->pp_centre0);
+         A->pp_centre0, A->pbase, A->pdelta);
    else if (A->rpat && A->dc_maxrow <= 8)
       csr_rp_kernel<NEG, NEED_DIAG, Epi, 4><<<(tiles + 3) / 4, 256, 0, s>>>(
          A->rpat, A->ptab, A->rp_n, A->doff, A->dval, x, rb, re, e, partials, A->dc_n, A->danch);
@@ -1512,7 +1516,7 @@ static void launch_rpp(hipStream_t s, const amg_mat *A, const double *x, double 
    const int nt = (A->nrows + 512 * RPL - 1) / (512 * RPL);
    csr_rpp_kernel<0, false, EpiGemv, RPL><<<nt, 256, A->pp_n * A->pp_stride * 4, s>>>(
       A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride, A->danch,
-      A->pp_centre0);
+      A->pp_centre0, A->pbase, A->pdelta);
 }
 
 // Jacobi sweep y = x + w (x - A x)/a_ii through the paired kernel, OPT as
@@ -1525,7 +1529,7 @@ static void launch_rpp_jac(hipStream_t s, const amg_mat *A, const double *x, dou
    const int nt = (A->nrows + 1023) / 1024;
    csr_rpp_kernel<1, true, EpiJacobi, 2, OPT><<<nt, 256, A->pp_n * A->pp_stride * 4, s>>>(
       A->ppat, A->pptab, A->pp_n, A->doff, A->dval, x, 0, A->nrows, e, nullptr, A->dc_n, A->pp_stride, A->danch,
-      A->pp_centre0);
+      A->pp_centre0, A->pbase, A->pdelta);
 }
 
 // ablations of the row-pattern kernel on the 512^3 operator (timing only):
@@ -2583,6 +2587,39 @@ void pp_collect(hipStream_t s, const amg_mat *A, unsigned char *flags)
 {
    if (A->nrows <= 0) return;
    pp_collect_k<<<std::min(8192, (A->nrows + 511) / 512), 256, 0, s>>>(A->rpat, A->danch, A->nrows, flags);
+}
+
+// one workgroup per 512-row slab: least anchor of its even rows, then each
+// pair's 16-bit delta from it
+__global__ __launch_bounds__(256) void pp_anchor_k(const int *__restrict__ anch, int n, int *__restrict__ pbase,
+                                                  unsigned short *__restrict__ pdelta, int *__restrict__ ok)
+{
+   __shared__ int red[2][256];
+   const int slab = (int)blockIdx.x, tid = (int)threadIdx.x;
+   const long long row = (long long)slab * 512 + 2 * tid;
+   const int a = row < n ? anch[row] : INT_MAX;
+   red[0][tid] = a;
+   red[1][tid] = row < n ? a : INT_MIN;
+   __syncthreads();
+   for (int w = 128; w > 0; w >>= 1) {
+      if (tid < w) {
+         red[0][tid] = min(red[0][tid], red[0][tid + w]);
+         red[1][tid] = max(red[1][tid], red[1][tid + w]);
+      }
+      __syncthreads();
+   }
+   const int lo = red[0][0], hi = red[1][0];
+   if (tid == 0) {
+      pbase[slab] = lo;
+      if ((long long)hi - lo > 65535) *ok = 0;
+   }
+   if (row < n) pdelta[row >> 1] = (unsigned short)(a - lo);
+}
+
+void pp_anchor_compress(hipStream_t s, const amg_mat *A, int *pbase, unsigned short *pdelta, int *ok)
+{
+   const int ns = (A->nrows + 511) / 512;
+   if (ns > 0) pp_anchor_k<<<ns, 256, 0, s>>>(A->danch, A->nrows, pbase, pdelta, ok);
 }
 
 void pp_encode(hipStream_t s, const amg_mat *A, const unsigned char *map, unsigned char *ppat,

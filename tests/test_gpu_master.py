@@ -190,3 +190,48 @@ def test_master_long_range_edges(ctx, amg):
     assert_bitwise(us[1], us[0], "jacobi")
     M.free()
     P.free()
+
+
+def test_pair_anchor_compression(ctx, amg):
+    """With amg_set_pair_anchor16 (default off), pair-coded operators with
+    per-row anchors (interpolation) read them slab-compressed (anchor(2t) = pbase[2t >> 9] + uint16 delta); a matrix whose
+    512-row slabs span more than 65535 columns keeps the int32 anchors.  Both
+    bit-identical to plain CSR, over full ranges and row slices."""
+    g = amg.Gen(32)
+    N, M, rp, cj, v = g.host_csr(amg.AMG_GEN_P, 0)
+    # wide anchors: rows (2t, 2t+1) at a + {0, 1} and a + 1 + {0, 1}, a = (t % 2) * 100000
+    nw, mw = 2048, 200004
+    rpw = np.arange(0, 2 * nw + 1, 2, dtype=np.int32)
+    cw = np.empty(2 * nw, np.int32)
+    for i in range(nw):
+        a = ((i // 2) % 2) * 100000 + (i & 1)
+        cw[2 * i], cw[2 * i + 1] = a, a + 1
+    vw = np.tile([0.5, 0.25], nw)
+    for n, m, r, c, val, want in ((N, M, rp, cj, v, 1), (nw, mw, rpw, cw, vw, 0)):
+        ctx.set_pair_pattern(2)
+        ctx.set_pair_anchor16(1)
+        try:
+            Mp = ctx.csr(n, m, r, c, val)
+        finally:
+            ctx.set_pair_pattern(1)
+            ctx.set_pair_anchor16(0)
+        ctx.set_value_index(0)
+        ctx.set_dict_index(0)
+        try:
+            Pl = ctx.csr(n, m, r, c, val)
+        finally:
+            ctx.set_value_index(1)
+            ctx.set_dict_index(1)
+        assert Mp.pair_pattern > 0 and Mp.pair_anchor16 == want, (n, Mp.pair_pattern, Mp.pair_anchor16)
+        x = ctx.vec(_vecs(m, 31))
+        b = ctx.vec(_vecs(n, 32))
+        for ab, (ns, ne) in (((1.0, 0.0), (0, n)), ((1.0, 1.0), (0, n)), ((-1.0, 0.7), (0, n)),
+                             ((1.0, 1.0), (2, n - 3)), ((1.0, 1.0), (514, n - 1))):
+            ys = []
+            for A in (Pl, Mp):
+                y = ctx.vec(_vecs(n, 33))
+                amg.smem.SMEM_SpGEMV(ctx, A, x, b, ab[0], ab[1], y, ns, ne)
+                ys.append(y.download())
+            assert_bitwise(ys[1], ys[0], f"n={n} {ab} rows {ns}:{ne}")
+        Mp.free()
+        Pl.free()
