@@ -63,6 +63,83 @@ __global__ __launch_bounds__(256) void pair_mask_k(const double *__restrict__ f,
    *reinterpret_cast<v2d *>(r + i) = acc;
 }
 
+// pair per lane, f streamed in and r streamed out with nontemporal hints so
+// the L2 keeps the x windows (NT=1: f and r, NT=2: r only)
+template <int M, int NT, bool XCD>
+__global__ __launch_bounds__(256) void pair_nt_k(const double *__restrict__ f, const double *__restrict__ x,
+                                                 double *__restrict__ r, long long n, Sten s)
+{
+   int b = blockIdx.x;
+   if (XCD) {
+      const int nb = gridDim.x, per = nb / 8;
+      if (b < per * 8) b = (b % 8) * per + b / 8;
+   }
+   const long long i = 2 * ((long long)b * 256 + threadIdx.x);
+   if (i >= n) return;
+   v2d acc;
+   if (NT == 1)
+      acc = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(f + i));
+   else
+      acc = *reinterpret_cast<const v2d *>(f + i);
+   v2d xv[M];
+#pragma unroll
+   for (int j = 0; j < M; j++) xv[j] = *reinterpret_cast<const v2du *>(x + i + s.off[j]);
+#pragma unroll
+   for (int j = 0; j < M; j++) {
+      acc.x -= s.val[j] * xv[j].x;
+      acc.y -= s.val[j] * xv[j].y;
+   }
+   if (NT >= 1)
+      __builtin_nontemporal_store(acc, reinterpret_cast<v2d *>(r + i));
+   else
+      *reinterpret_cast<v2d *>(r + i) = acc;
+}
+
+// four rows per lane (two 16-byte loads per offset)
+template <int M, int NT>
+__global__ __launch_bounds__(256) void quad_k(const double *__restrict__ f, const double *__restrict__ x,
+                                              double *__restrict__ r, long long n, Sten s)
+{
+   const long long i = 4 * ((long long)blockIdx.x * 256 + threadIdx.x);
+   if (i >= n) return;
+   v2d a0 = *reinterpret_cast<const v2d *>(f + i), a1 = *reinterpret_cast<const v2d *>(f + i + 2);
+   v2d xv[M], xw[M];
+#pragma unroll
+   for (int j = 0; j < M; j++) {
+      xv[j] = *reinterpret_cast<const v2du *>(x + i + s.off[j]);
+      xw[j] = *reinterpret_cast<const v2du *>(x + i + 2 + s.off[j]);
+   }
+#pragma unroll
+   for (int j = 0; j < M; j++) {
+      a0.x -= s.val[j] * xv[j].x;
+      a0.y -= s.val[j] * xv[j].y;
+      a1.x -= s.val[j] * xw[j].x;
+      a1.y -= s.val[j] * xw[j].y;
+   }
+   if (NT) {
+      __builtin_nontemporal_store(a0, reinterpret_cast<v2d *>(r + i));
+      __builtin_nontemporal_store(a1, reinterpret_cast<v2d *>(r + i + 2));
+   } else {
+      *reinterpret_cast<v2d *>(r + i) = a0;
+      *reinterpret_cast<v2d *>(r + i + 2) = a1;
+   }
+}
+
+// triad a = b + s c, plain and nontemporal
+template <int NT>
+__global__ __launch_bounds__(256) void triad_k(const double *__restrict__ b, const double *__restrict__ c,
+                                               double *__restrict__ a, long long n)
+{
+   const long long i = 2 * ((long long)blockIdx.x * 256 + threadIdx.x);
+   if (i >= n) return;
+   const v2d bv = *reinterpret_cast<const v2d *>(b + i), cv = *reinterpret_cast<const v2d *>(c + i);
+   const v2d o = bv + 3.0 * cv;
+   if (NT)
+      __builtin_nontemporal_store(o, reinterpret_cast<v2d *>(a + i));
+   else
+      *reinterpret_cast<v2d *>(a + i) = o;
+}
+
 // one row per lane
 template <int M>
 __global__ __launch_bounds__(256) void row_k(const double *__restrict__ f, const double *__restrict__ x,
@@ -127,6 +204,23 @@ static void run(int nn, int pts)
    CK(hipMemcpy(mt, hm.data(), 32, hipMemcpyHostToDevice));
    const double bytes = 24.0 * n;
    const int gp = (int)((n / 2 + 255) / 256), gr = (int)((n + 255) / 256);
+   if (pts == 7) {
+      const int gq = (int)((n / 4 + 255) / 256);
+      for (int rep = 0; rep < 2; rep++) {
+         const float a = timeit([&] { pair_nt_k<7, 0, false><<<gp, 256>>>(f, xc, r, n, s); }, 20);
+         const float b = timeit([&] { pair_nt_k<7, 1, false><<<gp, 256>>>(f, xc, r, n, s); }, 20);
+         const float c = timeit([&] { pair_nt_k<7, 2, false><<<gp, 256>>>(f, xc, r, n, s); }, 20);
+         const float d = timeit([&] { pair_nt_k<7, 1, true><<<gp, 256>>>(f, xc, r, n, s); }, 20);
+         const float e = timeit([&] { quad_k<7, 0><<<gq, 256>>>(f, xc, r, n, s); }, 20);
+         const float g = timeit([&] { quad_k<7, 1><<<gq, 256>>>(f, xc, r, n, s); }, 20);
+         const float t0 = timeit([&] { triad_k<0><<<gp, 256>>>(f, xc, r, n); }, 20);
+         const float t1 = timeit([&] { triad_k<1><<<gp, 256>>>(f, xc, r, n); }, 20);
+         printf("%d^3 7-pt variants (GB/s of 24n): pair %.0f  nt(f,r) %.0f  nt(r) %.0f  nt+xcd %.0f  quad %.0f  "
+                "quad+nt %.0f | triad %.0f  triad+nt %.0f\n",
+                nn, bytes / a / 1e6, bytes / b / 1e6, bytes / c / 1e6, bytes / d / 1e6, bytes / e / 1e6,
+                bytes / g / 1e6, bytes / t0 / 1e6, bytes / t1 / 1e6);
+      }
+   }
    for (int rep = 0; rep < 3; rep++) {
       float t1, t2, t3;
       if (pts == 27) {
