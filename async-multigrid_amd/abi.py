@@ -10,6 +10,10 @@ import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libamg_mi355x.so")
+# development build with the SpMV tuning harness (make -C csrc dev); only the
+# tools/ tuning scripts select it, by setting AMG_DEV_LIB=1 before import
+if os.environ.get("AMG_DEV_LIB") == "1":
+    LIB_PATH = os.path.join(_HERE, "lib", "libamg_mi355x_dev.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "amg_mi355x.h")
 
 _p = C.c_void_p
@@ -94,6 +98,8 @@ PROTOTYPES = {
     "amg_matvec_t": (_i, [_p, _p, _p, _p, _i]),
     "amg_spgemv": (_i, [_p, _p, _p, _p, _d, _d, _p, _i, _i]),
     "amg_matvec_timed": (_i, [_p, _p, _p, _p, _i, _dp]),
+    "amg_stream_triad": (_i, [_p, _ll, _i, _dp]),
+    "amg_pmc_calib": (_i, [_p, _i, _ll]),
     "amg_residual": (_i, [_p, _p, _p, _p, _p, _p, _i, _i]),
     "amg_jacobi": (_i, [_p, _p, _p, _p, _p, _d, _i, _i, _i, _i, _i]),
     "amg_l1_jacobi": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i]),

@@ -907,20 +907,11 @@ extern "C" int amg_matvec_timed(amg_ctx *c, const amg_mat *A, const amg_vec *x, 
    return AMG_OK;
 }
 
-// development-only tuning entry points (tools/tune_spmv.py); not in the header
-namespace amgk {
-int num_tune_variants();
-const char *tune_variant_name(int v);
-void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y);
-} // namespace amgk
-
-extern "C" int amg_dev_tune_count(void) { return amgk::num_tune_variants(); }
-
-// development entry (tools/pmc_traffic.py): one calibration stream over a
-// fresh device buffer of `bytes` bytes
-extern "C" int amg_dev_calib(amg_ctx *c, int mode, long long bytes)
+// measurement helpers (declared in the header): PMC calibration streams
+// (tools/pmc_traffic.py) and the STREAM-triad ceiling bench.py reports
+extern "C" int amg_pmc_calib(amg_ctx *c, int mode, long long bytes)
 {
-   AMG_ARG(c && mode >= 0 && mode <= 4 && bytes > 0, "amg_dev_calib: bad argument");
+   AMG_ARG(c && mode >= 0 && mode <= 4 && bytes > 0, "amg_pmc_calib: bad argument");
    void *buf = nullptr;
    AMG_HIP(hipMalloc(&buf, (size_t)bytes));
    AMG_HIP(hipMemsetAsync(buf, 1, (size_t)bytes, c->stream));
@@ -929,18 +920,17 @@ extern "C" int amg_dev_calib(amg_ctx *c, int mode, long long bytes)
    hipFree(buf);
    return AMG_OK;
 }
-// development entry (bench.py): best-of-reps STREAM triad rate over three
-// fresh arrays of n doubles, GB/s of 24 n bytes per pass
-extern "C" int amg_dev_stream_triad(amg_ctx *c, long long n, int reps, double *gbs)
+
+extern "C" int amg_stream_triad(amg_ctx *c, long long n, int reps, double *gbs)
 {
-   AMG_ARG(c && n >= 2 && reps >= 1 && gbs, "amg_dev_stream_triad: bad argument");
+   AMG_ARG(c && n >= 2 && reps >= 1 && gbs, "amg_stream_triad: bad argument");
    n &= ~1LL;
    double *a = nullptr, *b = nullptr, *d = nullptr;
    AMG_HIP(hipMalloc(&a, (size_t)n * 8));
    if (hipMalloc(&b, (size_t)n * 8) != hipSuccess || hipMalloc(&d, (size_t)n * 8) != hipSuccess) {
       hipFree(a);
       hipFree(b);
-      return amg_set_error(AMG_ERR_OOM, "amg_dev_stream_triad: %lld doubles", n);
+      return amg_set_error(AMG_ERR_OOM, "amg_stream_triad: %lld doubles", n);
    }
    hipEvent_t e0, e1;
    hipEventCreate(&e0);
@@ -969,8 +959,18 @@ extern "C" int amg_dev_stream_triad(amg_ctx *c, long long n, int reps, double *g
    return AMG_OK;
 }
 
-extern "C" const char *amg_dev_tune_name(int v) { return amgk::tune_variant_name(v); }
+#ifdef AMG_DEV_TUNE
+// development-only tuning entry points (tools/tune_spmv.py), only in the
+// development build lib/libamg_mi355x_dev.so (make dev); not in the header
+namespace amgk {
+int num_tune_variants();
+const char *tune_variant_name(int v);
+void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x, double *y);
+} // namespace amgk
 
+extern "C" int amg_dev_tune_count(void) { return amgk::num_tune_variants(); }
+
+extern "C" const char *amg_dev_tune_name(int v) { return amgk::tune_variant_name(v); }
 extern "C" int amg_dev_tune_spmv(amg_ctx *c, const amg_mat *A, const amg_vec *x, amg_vec *y,
                                  int variant, int reps, double *ms)
 {
@@ -991,6 +991,7 @@ extern "C" int amg_dev_tune_spmv(amg_ctx *c, const amg_mat *A, const amg_vec *x,
    *ms = (double)t / reps;
    return AMG_OK;
 }
+#endif // AMG_DEV_TUNE
 
 extern "C" int amg_spgemv(amg_ctx *c, const amg_mat *A, const amg_vec *x, const amg_vec *b,
                           double alpha, double beta, amg_vec *y, int rb, int re)

@@ -1386,8 +1386,12 @@ void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const dou
 
 // ---------------------------------------------------------------------------
 // tuning harness: time y = A x under several tile configurations, interleaved
-// (development entry point used by tools/tune_spmv.py; not part of the C-ABI)
+// (development entry point used by tools/tune_spmv.py; not part of the C-ABI).
+// Only in the development build (make dev -> lib/libamg_mi355x_dev.so with
+// -DAMG_DEV_TUNE): the ablation kernels give wrong results by design and stay
+// out of the product library.
 // ---------------------------------------------------------------------------
+#ifdef AMG_DEV_TUNE
 template <class Cfg, bool VI = false>
 static void launch_matvec_cfg(hipStream_t s, const amg_mat *A, const double *x, double *y)
 {
@@ -1768,6 +1772,7 @@ void launch_tune_variant(hipStream_t s, int v, const amg_mat *A, const double *x
    default: break;
    }
 }
+#endif // AMG_DEV_TUNE
 
 // ---------------------------------------------------------------------------
 // PMC calibration streams (tools/pmc_traffic.py): known byte counts read or

@@ -169,8 +169,7 @@ def main():
     gate_ms = csr_bytes / (0.60 * HBM_PEAK_GBS * 1e9) * 1e3
     # practical ceiling: STREAM triad over three 2 GiB arrays on the same device
     triad = C.c_double()
-    amg.lib.amg_dev_stream_triad.argtypes = [C.c_void_p, C.c_longlong, C.c_int, C.POINTER(C.c_double)]
-    amg.check(amg.lib.amg_dev_stream_triad(ctx.h, 1 << 28, 10, C.byref(triad)))
+    amg.check(amg.lib.amg_stream_triad(ctx.h, 1 << 28, 10, C.byref(triad)))
     log(f"[gpu] STREAM triad {triad.value:.0f} GB/s")
     log(f"[gpu] fine residual {res_ms:.3f} ms ({achieved:.0f} GB/s), fine SpMV {spmv_ms.value:.3f} ms "
         f"({spmv_gbs:.0f} GB/s); smoother {ms[1] / max(launches[1], 1):.3f} ms, "

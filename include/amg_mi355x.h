@@ -233,6 +233,14 @@ int amg_sym_jacobi(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u,
  * stream bracketed by HIP events; *ms = average device milliseconds per launch */
 int amg_matvec_timed(amg_ctx *ctx, const amg_mat *A, const amg_vec *x, amg_vec *y, int reps,
                      double *ms);
+/* measurement helpers (no reference counterpart): best-of-reps STREAM triad
+ * a = b + q c over three fresh arrays of n doubles, *gbs = 24 n bytes / time
+ * (the practical HBM ceiling bench.py reports beside the 8 TB/s peak); and one
+ * PMC calibration stream over a fresh buffer of `bytes` bytes (mode 0/1/2/3:
+ * reads with 16/8/4/1-byte lanes, 4: 8-byte writes) for rocprofv3 FETCH_SIZE /
+ * WRITE_SIZE calibration (tools/pmc_traffic.py) */
+int amg_stream_triad(amg_ctx *ctx, long long n, int reps, double *gbs);
+int amg_pmc_calib(amg_ctx *ctx, int mode, long long bytes);
 /* setup arrays: L1_row_norm SMEM_Setup.cpp:222-232, A_diag :234-237 */
 int amg_l1_norms(amg_ctx *ctx, const amg_mat *A, amg_vec *out);
 int amg_a_diag(amg_ctx *ctx, const amg_mat *A, double omega, amg_vec *out);

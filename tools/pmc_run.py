@@ -15,12 +15,11 @@ from conftest import load_package  # noqa: E402
 
 amg = load_package()
 lib = amg.lib
-lib.amg_dev_calib.argtypes = [C.c_void_p, C.c_int, C.c_longlong]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 ctx = amg.Context(0, 4)
 CAL = 2 << 30  # 2 GiB per calibration stream, far beyond the 256 MiB Infinity Cache
 for mode in range(5):
-    amg.check(lib.amg_dev_calib(ctx.h, mode, CAL))
+    amg.check(lib.amg_pmc_calib(ctx.h, mode, CAL))
 g = amg.Gen(n)
 H = amg.build_hierarchy(ctx, g, amg.default_opts(smooth_weight=0.8, num_cycles=1 << 30, tol=0.0))
 f = ctx.vec(amg.rhs_rand(0, n ** 3))

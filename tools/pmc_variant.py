@@ -9,6 +9,7 @@ import numpy as np
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+os.environ["AMG_DEV_LIB"] = "1"  # tuning variants live in the development build
 from conftest import load_package  # noqa: E402
 
 amg = load_package()
