@@ -71,6 +71,22 @@ def main(args, world, rank):
     ms, launches = D.profile(reset=True)
     res_ms = ms[0] / max(launches[0], 1)
     res_bytes = mat_bytes + 24 * D.n0
+    u_par = None
+    if args.cpu_baseline:
+        # parity leg (untimed): restart and run exactly the oracle's cpu_cycles
+        # outer iterations; rank 0 gathers the slabs of the iterate
+        r0p = D.solve_start(f)
+        D.iterate(args.cpu_cycles)
+        rel_p = D.resnorm() / r0p
+        u_loc = torch.from_numpy(D.get_u())
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        tdist.all_gather(sizes, torch.tensor([u_loc.numel()], dtype=torch.int64))
+        if rank == 0:
+            parts = [torch.empty(int(sz.item()), dtype=torch.float64) for sz in sizes]
+            tdist.gather(u_loc, parts, dst=0)
+            u_par = (torch.cat(parts).numpy(), rel_p)
+        else:
+            tdist.gather(u_loc, None, dst=0)
     spmv_ms = D.fine_spmv_ms(args.spmv_reps)
     spmv_bytes = mat_bytes + 16 * D.n0
     # aggregate fine SpMV rate: all ranks' algorithmic bytes over the slowest rank's time
@@ -81,6 +97,15 @@ def main(args, world, rank):
     D.free()
     amg.dist.finalize(ctx)
     ctx.close()
+    cpu, parity = None, None
+    if rank == 0 and args.cpu_baseline:
+        from bench import cpu_baseline, check_parity
+        try:
+            cpu, u_cpu, rel_cpu = cpu_baseline(gen, amg, amg.rhs_rand(0, n ** 3), args)
+            parity = check_parity(u_par, u_cpu, rel_cpu, args.cpu_cycles)
+            log(f"[cpu] {cpu['value']:.4f} it/s on {cpu['cores']} threads; [parity] {parity}")
+        except Exception as e:
+            log(f"[cpu] baseline failed: {e!r}")
     if rank == 0:
         value = args.steps / dt
         spmv_gbs = P[:, 0].sum() / (P[:, 1].max() * 1e-3) / 1e9
@@ -114,8 +139,10 @@ def main(args, world, rank):
                          "frac": ach0 / HBM_PEAK_GBS, "traffic": None,
                          "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms,
                          "aggregate_gbs": res_gbs},
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
+            "parity": parity,
             "final_relres": rn / r0,
         }
         print(json.dumps(out), flush=True)
+    tdist.barrier()
     tdist.destroy_process_group()
