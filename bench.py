@@ -114,9 +114,9 @@ def check_parity(u_par, u_cpu, rel_cpu, cycles):
     same |= np.isnan(u_gpu) & np.isnan(u_cpu)
     nbad = int(u_gpu.size - np.count_nonzero(same))
     maxrel = float(np.max(np.abs(u_gpu - u_cpu)) / max(np.max(np.abs(u_cpu)), 1e-300))
-    return {"cycles": cycles, "iterate_bitwise": nbad == 0, "mismatched_entries": nbad,
-            "max_abs_diff_rel": maxrel, "relres_gpu": rel_gpu, "relres_oracle": rel_cpu,
-            "relres_rtol_ok": abs(rel_gpu - rel_cpu) <= 1e-12 * abs(rel_cpu)}
+    return {"cycles": cycles, "iterate_bitwise": bool(nbad == 0), "mismatched_entries": nbad,
+            "max_abs_diff_rel": maxrel, "relres_gpu": float(rel_gpu), "relres_oracle": float(rel_cpu),
+            "relres_rtol_ok": bool(abs(rel_gpu - rel_cpu) <= 1e-12 * abs(rel_cpu))}
 
 
 def launch_ranks(args):
