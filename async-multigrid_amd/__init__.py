@@ -89,6 +89,11 @@ class Context:
         """Master-pattern form of square pair-coded operators (default on)."""
         check(lib.amg_set_master_pattern(self.h, int(enable)))
 
+    def set_plane_march(self, enable, zc=0, xcd=-1):
+        """Plane-marching kernel for 7-pt box-grid masters (default on); zc planes
+        per chunk (0 keeps), xcd workgroup order (-1 keeps)."""
+        check(lib.amg_set_plane_march(self.h, int(enable), int(zc), int(xcd)))
+
     def csr(self, nrows, ncols, rowptr, col, val, diag_first=1):
         return Mat.register(self, nrows, ncols, rowptr, col, val, diag_first)
 
@@ -120,6 +125,7 @@ class Mat:
         self.pair_pattern = lib.amg_mat_pair_pattern(handle)  # distinct row-pair patterns, 0 = not coded
         self.pair_anchor16 = lib.amg_mat_pair_anchor16(handle)  # slab-compressed anchors
         self.master_pattern = lib.amg_mat_master_pattern(handle)  # master length J (-J: uniform values), 0 = not coded
+        self.plane_march = lib.amg_mat_plane_march(handle)  # plane size P of the marching kernel, 0 = not marched
 
     @classmethod
     def register(cls, ctx, nrows, ncols, rowptr, col, val, diag_first=1):

@@ -79,6 +79,11 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_PAIR_PATTERN")) c->pair_pattern = std::min(2, std::max(0, std::atoi(v)));
    if (const char *v = std::getenv("AMG_MASTER_PATTERN")) c->master_pattern = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_PAIR_ANCHOR16")) c->pair_anchor16 = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_PLANE_MARCH")) {
+      c->plane_march = std::atoi(v) > 0;
+      if (std::atoi(v) > 1) c->mz_zc = std::min(std::atoi(v), 64);
+   }
+   if (const char *v = std::getenv("AMG_PLANE_MARCH_XCD")) c->mz_xcd = std::atoi(v) != 0;
    *out = c;
    return AMG_OK;
 }
@@ -584,6 +589,14 @@ static int build_master_pattern(amg_mat *A)
    }
    A->mp_uni = uni ? 1 : 0;
    A->mp_J = J;
+   // plane-marching form: master [0, -P, -S, -1, +1, +S, +P], whole planes of
+   // P rows (P % 512 == 0: a workgroup's 512 positions never straddle planes)
+   if (A->ctx->plane_march && J == 7 && mo[3] == -1 && mo[4] == 1 && mo[1] == -mo[6] &&
+       mo[2] == -mo[5] && mo[5] > 1 && mo[6] > mo[5] && mo[6] % 512 == 0 && A->nrows % mo[6] == 0 &&
+       A->nrows / mo[6] >= 2) {
+      A->mz_P = mo[6];
+      A->mz_S = mo[5];
+   }
    return AMG_OK;
 }
 
@@ -647,6 +660,21 @@ extern "C" int amg_set_master_pattern(amg_ctx *c, int enable)
 extern "C" int amg_mat_master_pattern(const amg_mat *A)
 {
    return A ? A->mp_J * (A->mp_uni ? -1 : 1) : 0;
+}
+
+extern "C" int amg_set_plane_march(amg_ctx *c, int enable, int zc, int xcd)
+{
+   AMG_ARG(c, "amg_set_plane_march: null context");
+   AMG_ARG(zc >= 0 && zc <= 64, "amg_set_plane_march: planes per chunk %d outside [1, 64] (0: keep)", zc);
+   c->plane_march = enable ? 1 : 0;
+   if (zc > 0) c->mz_zc = zc;
+   if (xcd >= 0) c->mz_xcd = xcd ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_plane_march(const amg_mat *A)
+{
+   return A ? A->mz_P : 0;
 }
 
 extern "C" int amg_set_dict_index(amg_ctx *c, int enable)

@@ -91,6 +91,9 @@ struct amg_ctx {
    int pair_pattern = 1; // paired-row-pattern CSR: 0 off, 1 size-gated for long rows, 2 always
    int master_pattern = 1; // master-pattern form of square pair-coded operators
    int pair_anchor16 = 0;  // slab-compressed anchors of pair-coded P/R (measured slower: off)
+   int plane_march = 1;    // plane-marching kernel for 7-pt box-grid masters (csr_mz_kernel)
+   int mz_zc = 16;         // planes per workgroup chunk of the plane-marching kernel
+   int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
 };
 
 struct amg_mat {
@@ -154,6 +157,9 @@ struct amg_mat {
    double mp_val[AMG_MP_MAXJ] = {};
    unsigned long long *mpmask = nullptr;
    double *mpval = nullptr;
+   // plane-marching form (csr_mz_kernel): the master list is [0, -P, -S, -1, +1,
+   // +S, +P] with P % 512 == 0 and nrows = nz * P (0: not applicable)
+   int mz_P = 0, mz_S = 0;
 };
 
 struct amg_vec {

@@ -933,6 +933,139 @@ static void launch_mp(hipStream_t s, const amg_mat *A, const double *x, int rb, 
    }
 }
 
+// ---------------------------------------------------------------------------
+// Plane-marching master kernel (csr_mz_kernel): master-coded operators whose
+// 7-entry master list is [0, -P, -S, -1, +1, +S, +P] with N = nz * P and
+// P % 512 == 0 -- the 7-pt stencil of an nx * ny * nz box (S = nx, P = nx ny)
+// in the reference's diagonal-first row order.  The use masks (ppat + mpmask)
+// still decide which entries every row adds, so the result is exact for ANY
+// matrix with that master list; the geometry only decides where the operands
+// come from:
+//   * a workgroup owns 512 consecutive in-plane positions (lane t: rows
+//     pos = 2t, 2t + 1) and marches over a chunk of ZC planes;
+//   * x of planes k - 1, k, k + 1 stay in registers (the +-P entries and the
+//     diagonal), plane k + 2 is prefetched one iteration ahead, so every x
+//     element is loaded from HBM once per chunk instead of three times;
+//   * +-1 come from the neighbour lanes (ds_bpermute), the wave's two edge
+//     operands from one two-lane load; +-S are 16-byte loads of the lines the
+//     neighbouring workgroups stream at the same time (L2 hits with the
+//     XCD-contiguous workgroup order below).
+// Each row adds its used entries in master order = its CSR order, and the
+// norm partials are csr_mp_kernel's (one per 256-row tile, block_sum_256's
+// operand order), so every output and every partial is bit-identical.
+// Per pair of rows: 6 memory instructions (f, x[k+2], x[-S], x[+S], the
+// pattern byte, the store) against 10 in csr_mp_kernel.
+// ---------------------------------------------------------------------------
+constexpr int AMG_MZ_MAXZC = 64;
+
+template <int NEG, bool NEED_DIAG, class Epi, bool UNI>
+__global__ __launch_bounds__(256) void csr_mz_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
+   const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ x, int P, int S, int nz, int zc,
+   int npb, int xcd, Epi epi, double *__restrict__ partials)
+{
+   const bool xc_pf = pf_is_x<Epi>::value && epi_pf_vec(epi) == x;
+   __shared__ unsigned long long mtab[256];
+   __shared__ v2d mval[UNI ? 1 : 256 * 7];
+   __shared__ double red[AMG_MZ_MAXZC * 8];
+   const int tid = (int)threadIdx.x, lane = tid & 63;
+   if (tid < np) mtab[tid] = mmask_g[tid];
+   if (!UNI)
+      for (int w = tid; w < np * 7; w += 256) mval[w] = mval_g[w];
+   // XCD-contiguous order: hardware workgroup w runs on XCD w % 8; give XCD j
+   // the logical range [j G/8, (j+1) G/8) so neighbouring lines (the +-S
+   // operands) are streamed by the same L2
+   const int G = (int)gridDim.x;
+   int lg = (int)blockIdx.x;
+   if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
+   const int pblk = lg % npb, chunk = lg / npb;
+   const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
+   const long long N = (long long)nz * P;
+   const int pos = pblk * 512 + 2 * tid;
+   const double *xp0 = x + pos;
+   v2d xm = k0 > 0 ? *reinterpret_cast<const v2du *>(xp0 + (long long)(k0 - 1) * P) : v2d{0.0, 0.0};
+   v2d xc = *reinterpret_cast<const v2du *>(xp0 + (long long)k0 * P);
+   v2d xq = k0 + 1 < nz ? *reinterpret_cast<const v2du *>(xp0 + (long long)(k0 + 1) * P) : v2d{0.0, 0.0};
+   __syncthreads();
+   for (int k = k0; k < k1; k++) {
+      const long long row = (long long)k * P + pos;
+      // prefetch plane k + 2 (this chunk's last iteration needs plane k1)
+      v2d xn{0.0, 0.0};
+      if (k + 2 < nz && k + 1 < k1) xn = *reinterpret_cast<const v2du *>(x + row + 2LL * P);
+      const int pid = ppat[row >> 1];
+      v2d acc = epi.init2((int)row);
+      v2d pf = xc_pf ? xc : epi.pf2((int)row);
+      const v2d ym = *reinterpret_cast<const v2du *>(x + (row >= S ? row - S : 0));
+      const v2d yp = *reinterpret_cast<const v2du *>(x + (row + S + 2 <= N ? row + S : N - 2));
+      double e = 0.0;
+      if (lane == 0 && row > 0) e = x[row - 1];
+      if (lane == 63 && row + 2 < N) e = x[row + 2];
+      double lft = __shfl_up(xc.y, 1, 64);
+      double rgt = __shfl_down(xc.x, 1, 64);
+      if (lane == 0) lft = e;
+      if (lane == 63) rgt = e;
+      const unsigned long long mk = mtab[pid];
+      v2d xv[7];
+      xv[0] = xc;
+      xv[1] = xm;
+      xv[2] = ym;
+      xv[3] = v2d{lft, xc.x};
+      xv[4] = v2d{xc.y, rgt};
+      xv[5] = yp;
+      xv[6] = xq;
+#pragma unroll
+      for (int j = 0; j < 7; j++) {
+         const unsigned int b = (unsigned int)(mk >> (2 * j)) & 3u;
+         const v2d v = UNI ? v2d{Sv.val[j], Sv.val[j]} : mval[pid * 7 + j];
+         if (b & 1) acc.x = NEG ? acc.x - v.x * xv[j].x : acc.x + v.x * xv[j].x;
+         if (b & 2) acc.y = NEG ? acc.y - v.y * xv[j].y : acc.y + v.y * xv[j].y;
+      }
+      v2d dg{0.0, 0.0};
+      if (NEED_DIAG) dg = UNI ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 7];
+      const v2d out = epi.finish2((int)row, acc, dg, pf);
+      if (partials) {
+         // csr_mp_kernel's 64-row group sums
+         double a = out.x * out.x, b = out.y * out.y;
+#pragma unroll
+         for (int off = 16; off > 0; off >>= 1) {
+            a += __shfl_down(a, off, 32);
+            b += __shfl_down(b, off, 32);
+         }
+         if ((tid & 31) == 0) red[(k - k0) * 8 + (tid >> 5)] = a + b;
+      }
+      xm = xc;
+      xc = xq;
+      xq = xn;
+   }
+   if (partials) {
+      __syncthreads();
+      for (int w = tid; w < 2 * (k1 - k0); w += 256) {
+         const int it = w >> 1, h = w & 1;
+         const double *g = red + it * 8 + 4 * h;
+         partials[((long long)(k0 + it) * P + pblk * 512) / 256 + h] = ((g[0] + g[1]) + g[2]) + g[3];
+      }
+   }
+}
+
+template <int NEG, bool NEED_DIAG, class Epi>
+static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Epi &e, double *partials)
+{
+   MpSten S;
+   for (int j = 0; j < AMG_MP_MAXJ; j++) {
+      S.off[j] = A->mp_off[j];
+      S.val[j] = A->mp_val[j];
+   }
+   const int P = A->mz_P, nz = A->nrows / P, zc = std::max(1, std::min(A->ctx->mz_zc, AMG_MZ_MAXZC));
+   const int npb = P / 512, nch = (nz + zc - 1) / zc;
+   const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+   if (A->mp_uni)
+      csr_mz_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);
+   else
+      csr_mz_kernel<NEG, NEED_DIAG, Epi, false><<<npb * nch, 256, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);
+}
+
 // dictionary-coded launches: rows of <= 8 entries (7-pt stencil, interpolation)
 // take four 256-row tiles per workgroup, longer rows (27-pt Galerkin,
 // restriction) two (tools/tune_spmv.py, profiles/r01/tune_spmv.log); the
@@ -941,7 +1074,9 @@ template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int rb, int re,
                          const Epi &e, double *partials, int tiles)
 {
-   if (A->mp_J && (rb & 1) == 0)
+   if (A->mz_P && rb == 0 && re == A->nrows)
+      launch_mz<NEG, NEED_DIAG>(s, A, x, e, partials);
+   else if (A->mp_J && (rb & 1) == 0)
       launch_mp<NEG, NEED_DIAG>(s, A, x, rb, re, e, partials);
    else if (A->ppat && (rb & 1) == 0)
       csr_rpp_kernel<NEG, NEED_DIAG, Epi, 2><<<(re - rb + 1023) / 1024, 256, A->pp_n * A->pp_stride * 4, s>>>(

@@ -166,6 +166,18 @@ int amg_set_master_pattern(amg_ctx *ctx, int enable);
 /* master length J of A (0: not master-coded); negative (-J) when every master
  * entry carries one value over the whole matrix */
 int amg_mat_master_pattern(const amg_mat *A);
+/* plane-marching kernel (default on; env AMG_PLANE_MARCH=0 disables, =Z sets the
+ * planes per chunk, AMG_PLANE_MARCH_XCD=0 the plain workgroup order) for
+ * master-coded operators whose master list is [0, -P, -S, -1, +1, +S, +P] with
+ * P % 512 == 0 and nrows a multiple of P -- the reference's 7-pt Laplacian
+ * (Laplacian_3D_7pt, SEQ_MatVec.cpp:3-24 / SMEM_MatVec.cpp:140-258 /
+ * SMEM_Smooth.cpp:35-45 applied to it): x of three planes stays in registers
+ * while a workgroup marches through zc planes.  Bit-identical to every other
+ * form.  enable applies to matrices registered afterwards; zc (1..64, 0 keeps)
+ * and xcd (XCD-contiguous workgroup order, -1 keeps) apply to later launches.
+ * amg_mat_plane_march: the plane size P (0: not marched). */
+int amg_set_plane_march(amg_ctx *ctx, int enable, int zc, int xcd);
+int amg_mat_plane_march(const amg_mat *A);
 int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz);
 int amg_mat_download(amg_ctx *ctx, const amg_mat *A, int *rowptr, int *col, double *val);
 

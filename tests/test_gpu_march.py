@@ -1,0 +1,155 @@
+"""Plane-marching kernel (csr_mz_kernel) for master-coded operators whose
+master list is [0, -P, -S, -1, +1, +S, +P] (the reference's 7-pt Laplacian,
+Laplacian_3D_7pt, on an nx*ny*nz box: S = nx, P = nx*ny): which operators take
+it, and bit-identical results -- SpGEMV in every (alpha, beta) branch
+(SMEM_MatVec.cpp:140-258), Jacobi / L1 Jacobi sweeps (SMEM_Smooth.cpp:35-45,
+122-130), the fused outer residual + first sweep and its norm partials
+(SMEM_Solve.cpp:192-197) -- against plain CSR, the non-marched master form and
+the oracle, for every chunk length and workgroup order."""
+import numpy as np
+import pytest
+
+from test_gpu_kernels import assert_bitwise, _vecs
+
+pytestmark = pytest.mark.gpu
+
+
+def neumann_7pt(oracle, nx, ny, nz):
+    """7-pt operator with the diagonal = number of neighbours + 0.5 and
+    anisotropic off-diagonals: the master list of the Laplacian, but per-pattern
+    values (master-coded without uniform values)."""
+    L = oracle.laplace_7pt(nx, ny, nz)
+    val = L.val.copy()
+    rows = np.repeat(np.arange(L.nrows), np.diff(L.rowptr))
+    off = L.col.astype(np.int64) - rows
+    val[off == 1] = val[off == -1] = -1.0
+    val[np.abs(off) == nx] = -0.5
+    val[np.abs(off) == nx * ny] = -0.25
+    first = L.rowptr[:-1]
+    cnt = np.diff(L.rowptr)
+    s = np.add.reduceat(np.where(off == 0, 0.0, -val), first)
+    val[first] = s + 0.5 * (cnt > 0)
+    return oracle.Csr(L.nrows, L.ncols, L.rowptr, L.col, val)
+
+
+def register(ctx, A, march=1, plain=False):
+    ctx.set_plane_march(march)
+    if plain:
+        ctx.set_value_index(0)
+    try:
+        return ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val)
+    finally:
+        ctx.set_plane_march(1)
+        ctx.set_value_index(1)
+
+
+@pytest.fixture(scope="module")
+def boxes(oracle):
+    return {
+        "lap32": oracle.laplace_7pt(32),
+        "lap64x8x5": oracle.laplace_7pt(64, 8, 5),
+        "lap512x2x3": oracle.laplace_7pt(512, 2, 3),
+        "neu32x16x7": neumann_7pt(oracle, 32, 16, 7),
+    }
+
+
+def test_plane_march_selection(ctx, oracle, boxes):
+    want = {"lap32": 1024, "lap64x8x5": 512, "lap512x2x3": 1024, "neu32x16x7": 512}
+    for name, A in boxes.items():
+        M = register(ctx, A)
+        assert M.plane_march == want[name], (name, M.plane_march)
+        assert M.master_pattern == (-7 if name.startswith("lap") else 7), name
+        M.free()
+        M = register(ctx, A, march=0)
+        assert M.plane_march == 0
+        M.free()
+    # planes of 256 rows (16^3), 13*7 rows (odd box): the master kernel
+    for A in (oracle.laplace_7pt(16), oracle.laplace_7pt(13, 7, 5)):
+        M = register(ctx, A)
+        assert M.master_pattern == -7 and M.plane_march == 0
+        M.free()
+
+
+@pytest.mark.parametrize("zc,xcd", [(32, 1), (1, 0), (3, 1), (64, 0), (2, 1)])
+@pytest.mark.parametrize("name", ["lap32", "lap64x8x5", "lap512x2x3", "neu32x16x7"])
+def test_plane_march_bitwise(ctx, amg, boxes, name, zc, xcd):
+    A = boxes[name]
+    ctx.set_plane_march(1, zc, xcd)
+    try:
+        mz = register(ctx, A)
+        mp = register(ctx, A, march=0)
+        pl = register(ctx, A, plain=True)
+        assert mz.plane_march > 0 and mp.plane_march == 0 and pl.value_index == 0
+        n = A.nrows
+        x = ctx.vec(_vecs(n, 41))
+        b = ctx.vec(_vecs(n, 42))
+        outs = {}
+        for tag, M in (("plain", pl), ("master", mp), ("march", mz)):
+            o = []
+            for ab in ((1.0, 0.0), (-1.0, 1.0), (1.0, 1.0), (2.5, -0.5), (-1.0, 0.7), (0.3, 0.0)):
+                y = ctx.vec(n)
+                amg.smem.SMEM_SpGEMV(ctx, M, x, b, ab[0], ab[1], y, 0, n)
+                o.append(y.download())
+            # a row slice runs the master kernel (the march needs whole planes)
+            y = ctx.vec(_vecs(n, 43))
+            amg.smem.SMEM_SpGEMV(ctx, M, x, b, -1.0, 1.0, y, 2, n - 4)
+            o.append(y.download())
+            u = ctx.vec(_vecs(n, 44))
+            amg.smem.SMEM_Sync_Parfor_Jacobi(ctx, M, b, u, ctx.vec(n), 3, 0, 0.7)
+            o.append(u.download())
+            u = ctx.vec(_vecs(n, 45))
+            amg.smem.SMEM_Sync_Parfor_Jacobi(ctx, M, b, u, ctx.vec(n), 2, 1, 0.8)
+            o.append(u.download())
+            outs[tag] = o
+        for tag in ("master", "march"):
+            for k, (g, r) in enumerate(zip(outs[tag], outs["plain"])):
+                assert_bitwise(g, r, f"{name} zc={zc} {tag} output {k}")
+        for M in (mz, mp, pl):
+            M.free()
+    finally:
+        ctx.set_plane_march(1, 16, 1)
+
+
+@pytest.mark.parametrize("zc", [32, 5])
+@pytest.mark.parametrize("smoother", ["jacobi", "l1"])
+def test_plane_march_solve(ctx, amg, oracle, smoother, zc):
+    """SMEM_Solve on a 64^3 linear-interpolation hierarchy whose fine operator
+    is marched: the fused outer residual + first sweep, the level-0 residual,
+    the post-sweep; iterate bit-identical to the oracle after every cycle's
+    worth (12 cycles), the residual-norm history bit-identical to the
+    non-marched run (same per-tile partials) and to the oracle to 1e-12."""
+    from oracle import pyoracle as po
+    g = amg.Gen(64, interp=amg.AMG_INTERP_LINEAR)
+    host = {w: [po.Csr(*g.host_csr(c, l)) for l in range(cnt)]
+            for w, c, cnt in (("A", amg.AMG_GEN_A, g.L), ("P", amg.AMG_GEN_P, g.L - 1),
+                              ("R", amg.AMG_GEN_R, g.L - 1))}
+    sm = amg.AMG_JACOBI if smoother == "jacobi" else amg.AMG_L1_JACOBI
+    f = amg.rhs_rand(0, 64 ** 3)
+    res = {}
+    ctx.set_plane_march(1, zc, 1)
+    try:
+        for march in (1, 0):
+            ctx.set_plane_march(march)
+            dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v]
+                   for k, v in host.items()}
+            assert (dev["A"][0].plane_march > 0) == bool(march)
+            opts = amg.default_opts(smooth_weight=0.8, num_cycles=12, tol=0.0, reuse_outer_residual=2,
+                                    smoother=sm)
+            H = amg.Hier(ctx, dev["A"], dev["P"], dev["R"], opts)
+            res[march] = H.solve(f)
+            H.free()
+            for v in dev.values():
+                for M in v:
+                    M.free()
+    finally:
+        ctx.set_plane_march(1, 16, 1)
+    OH = po.Hier(host["A"], host["P"], host["R"],
+                 po.make_opts(smooth_weight=0.8, num_cycles=12, smoother=sm))
+    u_cpu, hist_cpu, _ = OH.solve(f)
+    u1, h1, k1 = res[1]
+    u0, h0, k0 = res[0]
+    assert k1 == k0 == 12
+    assert_bitwise(u1, u_cpu, "iterate vs oracle")
+    assert_bitwise(u1, u0, "iterate vs master kernel")
+    assert_bitwise(h1[:k1 + 1], h0[:k0 + 1], "norm history vs master kernel")
+    np.testing.assert_allclose(h1[:k1 + 1], hist_cpu[:k1 + 1], rtol=1e-12)
