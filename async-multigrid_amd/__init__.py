@@ -94,6 +94,10 @@ class Context:
         per chunk (0 keeps), xcd workgroup order (-1 keeps)."""
         check(lib.amg_set_plane_march(self.h, int(enable), int(zc), int(xcd)))
 
+    def set_fuse_transfer(self, enable):
+        """Fused level-0 residual + restriction on geometric hierarchies (default on)."""
+        check(lib.amg_set_fuse_transfer(self.h, int(enable)))
+
     def csr(self, nrows, ncols, rowptr, col, val, diag_first=1):
         return Mat.register(self, nrows, ncols, rowptr, col, val, diag_first)
 
@@ -201,6 +205,7 @@ class Hier:
         check(lib.amg_hier_create(ctx.h, L, arrA, arrP, arrR, C.byref(opts), C.byref(h)))
         self.h = h
         self.n0 = As[0].nrows
+        self.fused = lib.amg_hier_fused(h)  # 1: level-0 residual + restriction fused
 
     def set_opts(self, opts):
         check(lib.amg_hier_set_opts(self.h, C.byref(opts)))

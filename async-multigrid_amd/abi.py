@@ -113,6 +113,8 @@ PROTOTYPES = {
     "amg_a_diag": (_i, [_p, _p, _d, _p]),
     "amg_hier_create": (_i, [_p, _i, _pp, _pp, _pp, C.POINTER(AmgOpts), _pp]),
     "amg_hier_free": (_i, [_p]),
+    "amg_hier_fused": (_i, [_p]),
+    "amg_set_fuse_transfer": (_i, [_p, _i]),
     "amg_hier_set_opts": (_i, [_p, C.POINTER(AmgOpts)]),
     "amg_hier_set_blocks": (_i, [_p, _i, _ip, _i]),
     "amg_hier_vec": (_i, [_p, _i, _i, _pp]),

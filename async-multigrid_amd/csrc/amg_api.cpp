@@ -84,6 +84,8 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
       if (std::atoi(v) > 1) c->mz_zc = std::min(std::atoi(v), 64);
    }
    if (const char *v = std::getenv("AMG_PLANE_MARCH_XCD")) c->mz_xcd = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
    *out = c;
    return AMG_OK;
 }
@@ -669,6 +671,13 @@ extern "C" int amg_set_plane_march(amg_ctx *c, int enable, int zc, int xcd)
    c->plane_march = enable ? 1 : 0;
    if (zc > 0) c->mz_zc = zc;
    if (xcd >= 0) c->mz_xcd = xcd ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_set_fuse_transfer(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_fuse_transfer: null context");
+   c->fuse_transfer = enable ? 1 : 0;
    return AMG_OK;
 }
 

@@ -94,6 +94,8 @@ struct amg_ctx {
    int plane_march = 1;    // plane-marching kernel for 7-pt box-grid masters (csr_mz_kernel)
    int mz_zc = 16;         // planes per workgroup chunk of the plane-marching kernel
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
+   int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies
+   int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)
 };
 
 struct amg_mat {
@@ -224,6 +226,21 @@ void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
 // asynchronous / semi-asynchronous Gauss-Seidel, one lane per block, live u
 void async_gs(hipStream_t s, const amg_mat *A, const double *f, double *u, const int *d_blk, int nblk,
               int sweeps, int semi, int reverse);
+// geometric transfers of a marched level (R_0 = P_0^T of an nx*ny*nz box):
+// coarse K couples to fine 2K + d, d in {0,1,2}^3, weight w[dz*9 + dy*3 + dx]
+struct GeoT {
+   double w[27];
+   int nx, ny, nz;
+};
+// *bad |= 1 unless every row of M equals the geometric form (mode 0: M = R,
+// coarse rows; mode 1: M = P, fine rows): lengths, columns, value bits
+void geo_check(hipStream_t s, const amg_mat *M, int mode, const GeoT &g, int *bad);
+// fc = R (f - A u) for a plane-marched A with geometric R, without the fine
+// residual vector (bit-identical to the residual SpGEMV + R SpMV)
+void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, const double *u, const GeoT &g,
+                          const double *wdev, double *fc);
+// u += P e for the checked geometric P of GeoT g (bit-identical to the SpGEMV)
+void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u);
 // transpose-product with the expansion-buffer order of T static chunks
 void matvec_t_chunked(hipStream_t s, const amg_mat *AT, const double *x, double *y, int n_src,
                       int T);

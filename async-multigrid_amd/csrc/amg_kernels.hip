@@ -1066,6 +1066,324 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
          A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);
 }
 
+// ---------------------------------------------------------------------------
+// Geometric transfers of a marched level (SMEM_Sync_Parfor_Restrict /
+// SMEM_SpGEMV prolongation, SMEM_MatVec.cpp:380-392 / 140-258, on the
+// hierarchy's R_0 = P_0^T of the nx * ny * nz box): coarse point K couples to
+// the fine points 2K + d, d in {0,1,2}^3, with weight w[dz][dy][dx].  Both
+// matrices are checked entry for entry against this form at hierarchy
+// creation (geo_check_k), so the fused kernels below compute exactly what the
+// CSR kernels would.
+// ---------------------------------------------------------------------------
+// every row of R (mode 0, coarse rows) or P (mode 1, fine rows) equals the
+// geometric form: same length, same columns in CSR order, same value bits
+__global__ __launch_bounds__(256) void geo_check_k(const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                   const double *__restrict__ val, int nrows, int mode, GeoT g,
+                                                   int *__restrict__ bad)
+{
+   const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+   if (i >= nrows) return;
+   const int cx_n = g.nx / 2, cy_n = g.ny / 2, cz_n = g.nz / 2;
+   int k = rowptr[i];
+   const int e = rowptr[i + 1];
+   bool ok = true;
+   if (mode == 0) {
+      const int Kx = i % cx_n, Ky = (i / cx_n) % cy_n, Kz = i / (cx_n * cy_n);
+      for (int dz = 0; dz < 3; dz++)
+         for (int dy = 0; dy < 3; dy++)
+            for (int dx = 0; dx < 3; dx++) {
+               const int fz = 2 * Kz + dz, fy = 2 * Ky + dy, fx = 2 * Kx + dx;
+               if (fz >= g.nz || fy >= g.ny || fx >= g.nx) continue;
+               const int c = (fz * g.ny + fy) * g.nx + fx;
+               if (k >= e || col[k] != c ||
+                   __double_as_longlong(val[k]) != __double_as_longlong(g.w[dz * 9 + dy * 3 + dx]))
+                  ok = false;
+               k++;
+            }
+   } else {
+      const int fx = i % g.nx, fy = (i / g.nx) % g.ny, fz = i / (g.nx * g.ny);
+      // coarse candidates of one axis, ascending: odd f -> (f-1)/2; even f -> f/2-1, f/2
+      auto cand = [](int f, int nc, int *c) {
+         int m = 0;
+         if (f & 1) {
+            c[m++] = (f - 1) / 2;
+         } else {
+            if (f / 2 - 1 >= 0) c[m++] = f / 2 - 1;
+            if (f / 2 < nc) c[m++] = f / 2;
+         }
+         return m;
+      };
+      int czs[2], cys[2], cxs[2];
+      const int mz = cand(fz, cz_n, czs), my = cand(fy, cy_n, cys), mx = cand(fx, cx_n, cxs);
+      for (int a = 0; a < mz; a++)
+         for (int b = 0; b < my; b++)
+            for (int q = 0; q < mx; q++) {
+               const int dz = fz - 2 * czs[a], dy = fy - 2 * cys[b], dx = fx - 2 * cxs[q];
+               const int c = (czs[a] * cy_n + cys[b]) * cx_n + cxs[q];
+               if (k >= e || col[k] != c ||
+                   __double_as_longlong(val[k]) != __double_as_longlong(g.w[dz * 9 + dy * 3 + dx]))
+                  ok = false;
+               k++;
+            }
+   }
+   if (k != e) ok = false;
+   if (!ok) atomicOr(bad, 1);
+}
+
+void geo_check(hipStream_t s, const amg_mat *M, int mode, const GeoT &g, int *bad)
+{
+   geo_check_k<<<(M->nrows + 255) / 256, 256, 0, s>>>(M->rowptr, M->col, M->val, M->nrows, mode, g, bad);
+}
+
+// Fused level-0 residual + restriction: f_c = R (f - A u) without the fine
+// residual vector.  A lane owns fine columns 2cx, 2cx + 1 of the 2 LC + 1 fine
+// lines 2Ky0 .. 2Ky0 + 2 LC that LC consecutive coarse lines Ky0 .. Ky0 + LC - 1
+// restrict from (a workgroup holds 512 / nx such line groups) and marches
+// through the fine planes of a chunk of coarse planes, keeping x of planes
+// k - 1, k, k + 1 of its lines in registers (csr_mz_kernel's scheme; the halo
+// lines 2Ky0 - 1, 2Ky0 + 2 LC + 1 are loaded).  Each fine residual is
+// r = f - sum a_ij x_j in the row's master (= CSR) order, then coarse point
+// (Kz, Ky, cx) accumulates its 27 terms w * r in R's CSR order (fine column
+// ascending: dz, dy, dx), one fine plane at a time: even plane 2Kz closes
+// coarse plane Kz - 1 (dz = 2) and opens Kz (dz = 0), odd plane 2Kz + 1 adds
+// dz = 1.  r at fine column 2cx + 2 comes from lane t + 1 (the wave's last
+// lane reads it from LDS).  Line 2Ky0 + 2 LC is shared with the next group
+// (computed twice: (2 LC + 1) / 2 LC of the residual work).  Bit-identical to
+// the residual kernel followed by R's SpMV.
+struct Val7 {
+   double v[7];
+};
+
+template <bool UNI, int LC>
+__global__ __launch_bounds__(256) void mz_res_restrict_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
+   const v2d *__restrict__ mval_g, Val7 Sv, const double *__restrict__ x, const double *__restrict__ f,
+   const double *__restrict__ wg, int nx, int ny, int nz, int zcc, int nlb, int xcd,
+   double *__restrict__ fc)
+{
+   constexpr int NL = 2 * LC + 1; // fine lines per lane
+   __shared__ unsigned long long mtab[256];
+   __shared__ v2d mval[UNI ? 1 : 256 * 7];
+   __shared__ double xr[2][4][NL];
+   __shared__ double wl[27]; // R's weights (uniform LDS reads)
+   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+   if (tid < np) mtab[tid] = mmask_g[tid];
+   if (tid < 27) wl[tid] = wg[tid];
+   if (!UNI)
+      for (int w = tid; w < np * 7; w += 256) mval[w] = mval_g[w];
+   const int S = nx, P = nx * ny;
+   const long long N = (long long)nz * P;
+   const int lpl = nx >> 1; // lanes per line group
+   const int ncy = ny >> 1, ncz = nz >> 1;
+   const int G = (int)gridDim.x;
+   int lg = (int)blockIdx.x;
+   if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
+   const int lb = lg % nlb, chunk = lg / nlb;
+   const int Ky0 = (lb * (256 / lpl) + tid / lpl) * LC, cx = tid % lpl;
+   const int Kc0 = chunk * zcc, Kc1 = min(Kc0 + zcc, ncz);
+   const int kf0 = 2 * Kc0, kf1 = min(2 * Kc1, nz - 1); // fine planes, inclusive
+   const int y0 = 2 * Ky0;
+   const bool lastl = y0 + 2 * LC >= ny; // the group's last line is outside the box
+   const bool d2x = 2 * cx + 2 < nx;     // dx = 2 inside
+   const int pos0 = y0 * S + 2 * cx;      // line 0 offset in the plane
+   v2d xm[NL], xc[NL], xq[NL];
+#pragma unroll
+   for (int i = 0; i < NL; i++) {
+      const double *p = x + pos0 + (long long)i * S;
+      const bool ok = i < NL - 1 || !lastl;
+      xm[i] = (ok && kf0 > 0) ? *reinterpret_cast<const v2du *>(p + (long long)(kf0 - 1) * P) : v2d{0.0, 0.0};
+      xc[i] = ok ? *reinterpret_cast<const v2du *>(p + (long long)kf0 * P) : v2d{0.0, 0.0};
+      xq[i] = (ok && kf0 + 1 < nz) ? *reinterpret_cast<const v2du *>(p + (long long)(kf0 + 1) * P)
+                                   : v2d{0.0, 0.0};
+   }
+   double acc[LC];
+#pragma unroll
+   for (int c = 0; c < LC; c++) acc[c] = 0.0;
+   __syncthreads();
+   for (int k = kf0; k <= kf1; k++) {
+      const long long base = (long long)k * P + pos0;
+      v2d r[NL];
+      // halo lines 2Ky0 - 1 and 2Ky0 + 2 LC + 1 (entries outside the box are unused)
+      const v2d hm = *reinterpret_cast<const v2du *>(x + (base >= S ? base - S : 0));
+      const long long hp_i = base + (long long)NL * S;
+      const v2d hp = *reinterpret_cast<const v2du *>(x + (hp_i + 2 <= N ? hp_i : N - 2));
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+         const long long row = base + (long long)i * S;
+         r[i] = v2d{0.0, 0.0};
+         if (i == NL - 1 && lastl) continue;
+         const int pid = ppat[row >> 1];
+         v2d a2 = *reinterpret_cast<const v2du *>(f + row);
+         double e = 0.0;
+         if (lane == 0 && row > 0) e = x[row - 1];
+         if (lane == 63 && row + 2 < N) e = x[row + 2];
+         double lft = __shfl_up(xc[i].y, 1, 64);
+         double rgt = __shfl_down(xc[i].x, 1, 64);
+         if (lane == 0) lft = e;
+         if (lane == 63) rgt = e;
+         const unsigned long long mk = mtab[pid];
+         v2d xv[7];
+         xv[0] = xc[i];
+         xv[1] = xm[i];
+         xv[2] = i == 0 ? hm : xc[i == 0 ? 0 : i - 1];
+         xv[3] = v2d{lft, xc[i].x};
+         xv[4] = v2d{xc[i].y, rgt};
+         xv[5] = i == NL - 1 ? hp : xc[i == NL - 1 ? NL - 1 : i + 1];
+         xv[6] = xq[i];
+#pragma unroll
+         for (int j = 0; j < 7; j++) {
+            const unsigned int b = (unsigned int)(mk >> (2 * j)) & 3u;
+            const v2d v = UNI ? v2d{Sv.v[j], Sv.v[j]} : mval[pid * 7 + j];
+            if (b & 1) a2.x = a2.x - v.x * xv[j].x;
+            if (b & 2) a2.y = a2.y - v.y * xv[j].y;
+         }
+         r[i] = a2;
+      }
+      // next plane's operands: load plane k + 2 while the restriction runs
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+         xm[i] = xc[i];
+         xc[i] = xq[i];
+         xq[i] = v2d{0.0, 0.0};
+         if ((i < NL - 1 || !lastl) && k + 2 < nz && k + 1 <= kf1)
+            xq[i] = *reinterpret_cast<const v2du *>(x + base + (long long)i * S + 2LL * P);
+      }
+      // r at fine column 2cx + 2: lane t + 1 (LDS across waves for line groups
+      // of more than 64 lanes)
+      double r2[NL];
+#pragma unroll
+      for (int i = 0; i < NL; i++) r2[i] = __shfl_down(r[i].x, 1, 64);
+      if (lpl > 64) {
+         if (lane == 0)
+#pragma unroll
+            for (int i = 0; i < NL; i++) xr[k & 1][wv][i] = r[i].x;
+         __syncthreads();
+         if (lane == 63 && wv < 3)
+#pragma unroll
+            for (int i = 0; i < NL; i++) r2[i] = xr[k & 1][wv + 1][i];
+      }
+      const int Kz = k >> 1;
+      // coarse line c of the group reads fine lines 2c .. 2c + 2
+      auto add = [&](int c, int dzz) {
+#pragma unroll
+         for (int dy = 0; dy < 3; dy++) {
+            const int i = 2 * c + dy;
+            if (i == NL - 1 && lastl) continue;
+            acc[c] = acc[c] + wl[dzz * 9 + dy * 3 + 0] * r[i].x;
+            acc[c] = acc[c] + wl[dzz * 9 + dy * 3 + 1] * r[i].y;
+            if (d2x) acc[c] = acc[c] + wl[dzz * 9 + dy * 3 + 2] * r2[i];
+         }
+      };
+#pragma unroll
+      for (int c = 0; c < LC; c++) {
+         const long long ci = ((long long)(Ky0 + c)) * lpl + cx;
+         if (k & 1) {
+            add(c, 1);
+            if (k + 1 >= nz) fc[(long long)Kz * ncy * lpl + ci] = acc[c];
+         } else {
+            if (k > kf0) {
+               add(c, 2);
+               fc[(long long)(Kz - 1) * ncy * lpl + ci] = acc[c];
+            }
+            if (Kz < Kc1) {
+               acc[c] = 0.0;
+               add(c, 0);
+            }
+         }
+      }
+   }
+}
+
+void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, const double *u, const GeoT &g,
+                          const double *wdev, double *fc)
+{
+   Val7 S;
+   for (int j = 0; j < 7; j++) S.v[j] = A->mp_val[j];
+   const int lpl = g.nx / 2, groups = 256 / lpl;
+   const int LC = ((g.ny / 2) % (2 * groups) == 0 && A->ctx->rr_lines == 2) ? 2 : 1;
+   const int nlb = (g.ny / 2) / (groups * LC);
+   const int zcc = std::max(1, std::min(A->ctx->mz_zc / 2, 32));
+   const int nch = (g.nz / 2 + zcc - 1) / zcc;
+   const int nb = nlb * nch;
+   const int xcd = A->ctx->mz_xcd;
+   const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+#define AMG_RR(U, L) \
+   mz_res_restrict_kernel<U, L><<<nb, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, f, wdev, g.nx, g.ny, \
+                                                   g.nz, zcc, nlb, xcd, fc)
+   if (A->mp_uni) {
+      if (LC == 2) AMG_RR(true, 2);
+      else AMG_RR(true, 1);
+   } else {
+      if (LC == 2) AMG_RR(false, 2);
+      else AMG_RR(false, 1);
+   }
+#undef AMG_RR
+}
+
+// Geometric prolongation + correction u += P e (SMEM_Sync_SpGEMV(P, e, u, 1, 1,
+// u), SMEM_Sync_AMG.cpp:118-123) for the checked geometric P_0 of a marched
+// level: lane t owns fine rows (2t, 2t + 1) of a line; per coarse (plane, line)
+// pair of the row's interpolation stencil one 16-byte load brings coarse
+// columns cx - 1, cx.  Each row sums u_i + w * e_c over its coarse columns
+// ascending (P's CSR order: cz, cy, cx), the SpGEMV's (alpha = beta = 1) order.
+__global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ e, double *__restrict__ u,
+                                                     const double *__restrict__ wg, int nx, int ny, int nz,
+                                                     long long npairs)
+{
+   __shared__ double wl[27];
+   const int tid = (int)threadIdx.x;
+   if (tid < 27) wl[tid] = wg[tid];
+   __syncthreads();
+   const long long q = (long long)blockIdx.x * 256 + tid;
+   if (q >= npairs) return;
+   const long long i = 2 * q;
+   const int x = (int)(i % nx);
+   const long long yz = i / nx;
+   const int y = (int)(yz % ny), z = (int)(yz / ny);
+   const int ncx = nx >> 1, ncy = ny >> 1, ncz = nz >> 1;
+   const int t = x >> 1;
+   // coarse candidates of one axis (ascending) and their offsets d = f - 2c
+   int cz[2], dz[2], cy[2], dy[2];
+   int mz = 0, my = 0;
+   if (z & 1) {
+      cz[mz] = (z - 1) >> 1, dz[mz++] = 1;
+   } else {
+      if (z >= 2) cz[mz] = (z >> 1) - 1, dz[mz++] = 2;
+      if ((z >> 1) < ncz) cz[mz] = z >> 1, dz[mz++] = 0;
+   }
+   if (y & 1) {
+      cy[my] = (y - 1) >> 1, dy[my++] = 1;
+   } else {
+      if (y >= 2) cy[my] = (y >> 1) - 1, dy[my++] = 2;
+      if ((y >> 1) < ncy) cy[my] = y >> 1, dy[my++] = 0;
+   }
+   const bool lo = t >= 1, hi = t < ncx; // row 2t: coarse t - 1 (dx = 2), t (dx = 0)
+   v2d acc = *reinterpret_cast<const v2du *>(u + i);
+#pragma unroll
+   for (int a = 0; a < 2; a++) {
+      if (a >= mz) break;
+#pragma unroll
+      for (int b = 0; b < 2; b++) {
+         if (b >= my) break;
+         const long long cb = ((long long)cz[a] * ncy + cy[b]) * ncx + t;
+         // e[cb - 1], e[cb]; the first is unused (and clamped) at t = 0
+         const v2d ev = *reinterpret_cast<const v2du *>(e + (lo ? cb - 1 : cb));
+         const double em = lo ? ev.x : 0.0, ec = lo ? ev.y : ev.x;
+         const double *w = wl + dz[a] * 9 + dy[b] * 3;
+         if (lo) acc.x = acc.x + w[2] * em;
+         if (hi) acc.x = acc.x + w[0] * ec;
+         acc.y = acc.y + w[1] * ec;
+      }
+   }
+   *reinterpret_cast<v2du *>(u + i) = acc;
+}
+
+void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u)
+{
+   const long long np = (long long)g.nx * g.ny * g.nz / 2;
+   geo_prolong_k<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, np);
+}
+
 // dictionary-coded launches: rows of <= 8 entries (7-pt stencil, interpolation)
 // take four 256-row tiles per workgroup, longer rows (27-pt Galerkin,
 // restriction) two (tools/tune_spmv.py, profiles/r01/tune_spmv.log); the

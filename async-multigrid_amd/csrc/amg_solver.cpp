@@ -65,6 +65,10 @@ struct amg_hier {
    bool have_state = false;
    bool pre_ready = false; // lv[0].u_alt holds u + w r0 / a_ii for the current u
    bool r0_stale = false;  // reuse_outer_residual 2: r0 not written for the current u
+   // level 0 marched with geometric R_0 / P_0 (detect_geo0): fused transfer kernels
+   bool geo0 = false;
+   amgk::GeoT g0{};
+   double *d_geo_w = nullptr; // g0.w on the device
    std::vector<void *> allocs;
    // profiling
    std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[PROF_NCAT];
@@ -213,6 +217,60 @@ static int hier_prepare_smoother_arrays(amg_hier *H)
    return AMG_OK;
 }
 
+// Level 0 of a plane-marched A_0 (7-pt box nx * ny * nz) whose R_0 / P_0 are
+// the geometric transfers of that box (coarse K <-> fine 2K + {0,1,2}^3, one
+// weight per offset): checked entry for entry on the device, then the V-cycle
+// runs the level-0 residual and the restriction as one kernel.
+static int detect_geo0(amg_hier *H)
+{
+   H->geo0 = false;
+   if (H->L < 2 || !H->ctx->fuse_transfer) return AMG_OK;
+   const amg_mat *A = H->lv[0].A, *R = H->lv[0].R, *P = H->lv[0].P;
+   if (!A->mz_P || A->mz_P % A->mz_S) return AMG_OK;
+   const int nx = A->mz_S, ny = A->mz_P / A->mz_S, nz = A->nrows / A->mz_P;
+   if ((nx | ny | nz) & 1 || nx < 64 || nx > 512 || 512 % nx || ny < 6 || nz < 6) return AMG_OK;
+   if ((ny / 2) % (512 / nx)) return AMG_OK; // whole coarse lines per workgroup
+   const int ncx = nx / 2, ncy = ny / 2;
+   const long long nc = (long long)A->nrows / 8;
+   if (R->nrows != nc || R->ncols != A->nrows || P->nrows != A->nrows || P->ncols != nc) return AMG_OK;
+   hipStream_t s = H->ctx->stream;
+   // weights from coarse row (1, 1, 1): 27 entries at fine (2..4)^3, CSR order dz, dy, dx
+   const int K = (1 * ncy + 1) * ncx + 1;
+   int rp[2];
+   AMG_HIP(hipMemcpyAsync(rp, R->rowptr + K, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   if (rp[1] - rp[0] != 27) return AMG_OK;
+   int cols[27];
+   amgk::GeoT g{};
+   AMG_HIP(hipMemcpyAsync(cols, R->col + rp[0], sizeof(cols), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipMemcpyAsync(g.w, R->val + rp[0], sizeof(g.w), hipMemcpyDeviceToHost, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   g.nx = nx;
+   g.ny = ny;
+   g.nz = nz;
+   int *bad = nullptr;
+   AMG_HIP(hipMalloc(&bad, sizeof(int)));
+   AMG_HIP(hipMemsetAsync(bad, 0, sizeof(int), s));
+   amgk::geo_check(s, R, 0, g, bad);
+   amgk::geo_check(s, P, 1, g, bad);
+   int hbad = 1;
+   hipError_t e = hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, s);
+   if (e == hipSuccess) e = hipStreamSynchronize(s);
+   hipFree(bad);
+   if (e != hipSuccess) return amg_set_error(AMG_ERR_HIP, "detect_geo0: %s", hipGetErrorString(e));
+   if (hbad) return AMG_OK;
+   AMG_TRY(dalloc(H, 27, &H->d_geo_w));
+   AMG_HIP(hipMemcpyAsync(H->d_geo_w, g.w, sizeof(g.w), hipMemcpyHostToDevice, s));
+   H->g0 = g;
+   H->geo0 = true;
+   return AMG_OK;
+}
+
+extern "C" int amg_hier_fused(const amg_hier *H)
+{
+   return (H && H->geo0) ? 1 : 0;
+}
+
 extern "C" int amg_hier_create(amg_ctx *c, int L, amg_mat *const *A, amg_mat *const *P,
                                amg_mat *const *R, const amg_opts *opts, amg_hier **out)
 {
@@ -286,6 +344,7 @@ extern "C" int amg_hier_create(amg_ctx *c, int L, amg_mat *const *A, amg_mat *co
       }
    }
    AMG_TRY(hier_prepare_smoother_arrays(H));
+   AMG_TRY(detect_geo0(H));
    AMG_HIP(hipStreamSynchronize(c->stream));
    *out = H;
    return AMG_OK;
@@ -454,6 +513,12 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
       if (l == 0 && !precond) v.zero_flag = 0;
       const double *f_fine = (l == 0 && precond) ? H->r0 : v.f;
       smooth_one_level(H, s, l, f_fine, o.num_pre_smooth_sweeps, l == 0 && reuse_r0);
+      if (l == 0 && H->geo0) {
+         // level-0 residual and restriction in one pass (no r_fine vector)
+         ProfScope ps(H, PROF_FINE_SPMV, s);
+         amgk::mz_residual_restrict(s, v.A, f_fine, v.u, H->g0, H->d_geo_w, H->lv[1].f);
+         continue;
+      }
       {
          ProfScope ps(H, PROF_FINE_SPMV, s, l == 0);
          amgk::spgemv(s, v.A, v.u, f_fine, res_mode, v.r_fine, 0, v.n, nullptr);
@@ -471,7 +536,10 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
       v.zero_flag = 0;
       {
          ProfScope ps(H, PROF_PROLONG0, s, l == 0);
-         amgk::spgemv(s, v.P, H->lv[l + 1].u, v.u, pro_mode, v.u, 0, v.n, nullptr);
+         if (l == 0 && H->geo0)
+            amgk::geo_prolong(s, H->g0, H->d_geo_w, H->lv[1].u, v.u);
+         else
+            amgk::spgemv(s, v.P, H->lv[l + 1].u, v.u, pro_mode, v.u, 0, v.n, nullptr);
       }
       const double *f_fine = (l == 0 && precond) ? H->r0 : v.f;
       smooth_one_level(H, s, l, f_fine, o.num_post_smooth_sweeps, false);

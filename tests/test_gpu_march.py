@@ -153,3 +153,90 @@ def test_plane_march_solve(ctx, amg, oracle, smoother, zc):
     assert_bitwise(u1, u0, "iterate vs master kernel")
     assert_bitwise(h1[:k1 + 1], h0[:k0 + 1], "norm history vs master kernel")
     np.testing.assert_allclose(h1[:k1 + 1], hist_cpu[:k1 + 1], rtol=1e-12)
+
+
+def _hier_solve(ctx, amg, host, f, cycles, march, fuse, sm=0, zc=16):
+    ctx.set_plane_march(march, zc, 1)
+    ctx.set_fuse_transfer(fuse)
+    try:
+        dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v] for k, v in host.items()}
+        opts = amg.default_opts(smooth_weight=0.8, num_cycles=cycles, tol=0.0, reuse_outer_residual=2,
+                                smoother=sm)
+        H = amg.Hier(ctx, dev["A"], dev["P"], dev["R"], opts)
+        fused = H.fused
+        out = H.solve(f)
+        H.free()
+        for v in dev.values():
+            for M in v:
+                M.free()
+    finally:
+        ctx.set_plane_march(1, 16, 1)
+        ctx.set_fuse_transfer(1)
+    return fused, out
+
+
+@pytest.mark.parametrize("dims,zc", [((64, 64, 64), 16), ((512, 8, 6), 4), ((256, 12, 8), 2),
+                                     ((128, 16, 10), 6), ((64, 32, 14), 64), ((64, 64, 64), 3)])
+def test_fused_residual_restrict(ctx, amg, oracle, dims, zc):
+    """Level-0 residual + restriction fused (mz_res_restrict_kernel) on the
+    geometric linear-interpolation hierarchy of several boxes (lanes per coarse
+    line 32..256, chunks of 1..32 coarse planes, a chunk length not dividing
+    the plane count): the iterate bit-identical to the unfused run and to the
+    oracle after 8 cycles, the norm history bit-identical to the unfused run."""
+    from oracle import pyoracle as po
+    g = amg.Gen(*dims, interp=amg.AMG_INTERP_LINEAR)
+    host = {w: [po.Csr(*g.host_csr(c, l)) for l in range(cnt)]
+            for w, c, cnt in (("A", amg.AMG_GEN_A, g.L), ("P", amg.AMG_GEN_P, g.L - 1),
+                              ("R", amg.AMG_GEN_R, g.L - 1))}
+    n = dims[0] * dims[1] * dims[2]
+    f = amg.rhs_rand(0, n)
+    fz, (u1, h1, k1) = _hier_solve(ctx, amg, host, f, 8, 1, 1, zc=zc)
+    f0, (u0, h0, k0) = _hier_solve(ctx, amg, host, f, 8, 1, 0, zc=zc)
+    assert fz == 1 and f0 == 0
+    OH = po.Hier(host["A"], host["P"], host["R"], po.make_opts(smooth_weight=0.8, num_cycles=8))
+    u_cpu, hist_cpu, _ = OH.solve(f)
+    assert_bitwise(u1, u0, "fused vs unfused iterate")
+    assert_bitwise(u1, u_cpu, "fused vs oracle iterate")
+    assert_bitwise(h1[:k1 + 1], h0[:k0 + 1], "norm history")
+    np.testing.assert_allclose(h1[:k1 + 1], hist_cpu[:k1 + 1], rtol=1e-12)
+
+
+def test_fused_transfer_detection(ctx, amg, oracle):
+    """Only the geometric form fuses: aggregation transfers, a perturbed R_0
+    value, a perturbed P_0 column, and boxes whose lines do not fit (nx = 32, 96)
+    keep the two kernels."""
+    from oracle import pyoracle as po
+
+    def hier(g, tweak=None):
+        host = {w: [po.Csr(*g.host_csr(c, l)) for l in range(cnt)]
+                for w, c, cnt in (("A", amg.AMG_GEN_A, g.L), ("P", amg.AMG_GEN_P, g.L - 1),
+                                  ("R", amg.AMG_GEN_R, g.L - 1))}
+        if tweak:
+            tweak(host)
+        dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v] for k, v in host.items()}
+        H = amg.Hier(ctx, dev["A"], dev["P"], dev["R"], amg.default_opts(num_cycles=1))
+        fused = H.fused
+        H.free()
+        for v in dev.values():
+            for M in v:
+                M.free()
+        return fused
+
+    assert hier(amg.Gen(64, interp=amg.AMG_INTERP_LINEAR)) == 1
+    assert hier(amg.Gen(32, interp=amg.AMG_INTERP_LINEAR)) == 0  # lines of 32: below the kernel's range
+    assert hier(amg.Gen(64, interp=amg.AMG_INTERP_AGGREGATE)) == 0
+    assert hier(amg.Gen(96, 8, 8, interp=amg.AMG_INTERP_LINEAR)) == 0
+
+    def bump_r(host):
+        R = host["R"][0]
+        R.val[R.val.size // 2] *= 1.0000001
+
+    def move_p(host):
+        P = host["P"][0]
+        r = (5 * 64 + 7) * 64 + 9  # fine (5, 7, 9): all odd, one entry
+        i = P.rowptr[r]
+        assert P.rowptr[r + 1] - i == 1
+        P.col[i] = (P.col[i] + 1) % P.ncols
+
+    assert hier(amg.Gen(64, interp=amg.AMG_INTERP_LINEAR), bump_r) == 0
+    assert hier(amg.Gen(64, interp=amg.AMG_INTERP_LINEAR), move_p) == 0
