@@ -205,7 +205,7 @@ class Hier:
         check(lib.amg_hier_create(ctx.h, L, arrA, arrP, arrR, C.byref(opts), C.byref(h)))
         self.h = h
         self.n0 = As[0].nrows
-        self.fused = lib.amg_hier_fused(h)  # 1: level-0 residual + restriction fused
+        self.fused = lib.amg_hier_fused(h)  # bit 0: level-0 residual + restriction fused; bit l+1: level l geometric transfers
 
     def set_opts(self, opts):
         check(lib.amg_hier_set_opts(self.h, C.byref(opts)))

@@ -239,6 +239,8 @@ void geo_check(hipStream_t s, const amg_mat *M, int mode, const GeoT &g, int *ba
 // residual vector (bit-identical to the residual SpGEMV + R SpMV)
 void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, const double *u, const GeoT &g,
                           const double *wdev, double *fc);
+// f_c = R r for the checked geometric R of GeoT g (bit-identical to the SpMV)
+void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc);
 // u += P e for the checked geometric P of GeoT g (bit-identical to the SpGEMV)
 void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u);
 // transpose-product with the expansion-buffer order of T static chunks

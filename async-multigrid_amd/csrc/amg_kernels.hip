@@ -1384,6 +1384,48 @@ void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double 
    geo_prolong_k<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, np);
 }
 
+// Geometric restriction f_c = R r (SMEM_Sync_Parfor_Restrict,
+// SMEM_MatVec.cpp:380-392) for a checked geometric R: coarse point K sums
+// w * r over fine 2K + d in R's CSR order (dz, dy, dx), from 0.
+__global__ __launch_bounds__(256) void geo_restrict_k(const double *__restrict__ r, double *__restrict__ fc,
+                                                      const double *__restrict__ wg, int nx, int ny, int nz,
+                                                      long long nc)
+{
+   __shared__ double wl[27];
+   const int tid = (int)threadIdx.x;
+   if (tid < 27) wl[tid] = wg[tid];
+   __syncthreads();
+   const long long K = (long long)blockIdx.x * 256 + tid;
+   if (K >= nc) return;
+   const int ncx = nx >> 1, ncy = ny >> 1;
+   const int Kx = (int)(K % ncx);
+   const long long t = K / ncx;
+   const int Ky = (int)(t % ncy), Kz = (int)(t / ncy);
+   const bool dx2 = 2 * Kx + 2 < nx;
+   double acc = 0.0;
+#pragma unroll
+   for (int dz = 0; dz < 3; dz++) {
+      if (2 * Kz + dz >= nz) break;
+#pragma unroll
+      for (int dy = 0; dy < 3; dy++) {
+         if (2 * Ky + dy >= ny) break;
+         const double *p = r + ((long long)(2 * Kz + dz) * ny + 2 * Ky + dy) * nx + 2 * Kx;
+         const v2d a = *reinterpret_cast<const v2du *>(p);
+         const double *w = wl + dz * 9 + dy * 3;
+         acc = acc + w[0] * a.x;
+         acc = acc + w[1] * a.y;
+         if (dx2) acc = acc + w[2] * p[2];
+      }
+   }
+   fc[K] = acc;
+}
+
+void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc)
+{
+   const long long nc = (long long)g.nx * g.ny * g.nz / 8;
+   geo_restrict_k<<<(unsigned)((nc + 255) / 256), 256, 0, s>>>(r, fc, wdev, g.nx, g.ny, g.nz, nc);
+}
+
 // dictionary-coded launches: rows of <= 8 entries (7-pt stencil, interpolation)
 // take four 256-row tiles per workgroup, longer rows (27-pt Galerkin,
 // restriction) two (tools/tune_spmv.py, profiles/r01/tune_spmv.log); the

@@ -65,10 +65,13 @@ struct amg_hier {
    bool have_state = false;
    bool pre_ready = false; // lv[0].u_alt holds u + w r0 / a_ii for the current u
    bool r0_stale = false;  // reuse_outer_residual 2: r0 not written for the current u
-   // level 0 marched with geometric R_0 / P_0 (detect_geo0): fused transfer kernels
+   // geometric transfers (detect_geo): geo[l] when R_l / P_l equal the box
+   // transfers of level l (dims gl[l], weights d_geo_w[l] on the device);
+   // geo0: level 0 is also plane-marched and runs the fused residual + restriction
+   std::vector<char> geo;
+   std::vector<amgk::GeoT> gl;
+   std::vector<double *> d_geo_w;
    bool geo0 = false;
-   amgk::GeoT g0{};
-   double *d_geo_w = nullptr; // g0.w on the device
    std::vector<void *> allocs;
    // profiling
    std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[PROF_NCAT];
@@ -217,32 +220,29 @@ static int hier_prepare_smoother_arrays(amg_hier *H)
    return AMG_OK;
 }
 
-// Level 0 of a plane-marched A_0 (7-pt box nx * ny * nz) whose R_0 / P_0 are
-// the geometric transfers of that box (coarse K <-> fine 2K + {0,1,2}^3, one
-// weight per offset): checked entry for entry on the device, then the V-cycle
-// runs the level-0 residual and the restriction as one kernel.
-static int detect_geo0(amg_hier *H)
+// Geometric transfers: level 0's box comes from a plane-marched A_0 (7-pt on
+// nx * ny * nz: S = nx, P = nx ny); level l + 1's box is level l's halved
+// while every level above it was geometric.  R_l / P_l qualify when they equal,
+// entry for entry (checked on the device), coarse K <-> fine 2K + {0,1,2}^3
+// with one weight per offset (read from coarse row (1, 1, 1) of R_l).  Such
+// levels restrict / prolong with the geometric kernels; level 0 additionally
+// fuses its residual into the restriction when the box fits that kernel.
+static int check_geo_level(amg_hier *H, int l, int nx, int ny, int nz, bool *ok)
 {
-   H->geo0 = false;
-   if (H->L < 2 || !H->ctx->fuse_transfer) return AMG_OK;
-   const amg_mat *A = H->lv[0].A, *R = H->lv[0].R, *P = H->lv[0].P;
-   if (!A->mz_P || A->mz_P % A->mz_S) return AMG_OK;
-   const int nx = A->mz_S, ny = A->mz_P / A->mz_S, nz = A->nrows / A->mz_P;
-   if ((nx | ny | nz) & 1 || nx < 64 || nx > 512 || 512 % nx || ny < 6 || nz < 6) return AMG_OK;
-   if ((ny / 2) % (512 / nx)) return AMG_OK; // whole coarse lines per workgroup
+   *ok = false;
+   const amg_mat *A = H->lv[l].A, *R = H->lv[l].R, *P = H->lv[l].P;
+   if ((nx | ny | nz) & 1 || nx < 6 || ny < 6 || nz < 6) return AMG_OK;
+   if ((long long)nx * ny * nz != A->nrows) return AMG_OK;
    const int ncx = nx / 2, ncy = ny / 2;
    const long long nc = (long long)A->nrows / 8;
    if (R->nrows != nc || R->ncols != A->nrows || P->nrows != A->nrows || P->ncols != nc) return AMG_OK;
    hipStream_t s = H->ctx->stream;
-   // weights from coarse row (1, 1, 1): 27 entries at fine (2..4)^3, CSR order dz, dy, dx
    const int K = (1 * ncy + 1) * ncx + 1;
    int rp[2];
    AMG_HIP(hipMemcpyAsync(rp, R->rowptr + K, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
    AMG_HIP(hipStreamSynchronize(s));
    if (rp[1] - rp[0] != 27) return AMG_OK;
-   int cols[27];
    amgk::GeoT g{};
-   AMG_HIP(hipMemcpyAsync(cols, R->col + rp[0], sizeof(cols), hipMemcpyDeviceToHost, s));
    AMG_HIP(hipMemcpyAsync(g.w, R->val + rp[0], sizeof(g.w), hipMemcpyDeviceToHost, s));
    AMG_HIP(hipStreamSynchronize(s));
    g.nx = nx;
@@ -257,18 +257,46 @@ static int detect_geo0(amg_hier *H)
    hipError_t e = hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, s);
    if (e == hipSuccess) e = hipStreamSynchronize(s);
    hipFree(bad);
-   if (e != hipSuccess) return amg_set_error(AMG_ERR_HIP, "detect_geo0: %s", hipGetErrorString(e));
+   if (e != hipSuccess) return amg_set_error(AMG_ERR_HIP, "check_geo_level: %s", hipGetErrorString(e));
    if (hbad) return AMG_OK;
-   AMG_TRY(dalloc(H, 27, &H->d_geo_w));
-   AMG_HIP(hipMemcpyAsync(H->d_geo_w, g.w, sizeof(g.w), hipMemcpyHostToDevice, s));
-   H->g0 = g;
-   H->geo0 = true;
+   AMG_TRY(dalloc(H, 27, &H->d_geo_w[l]));
+   AMG_HIP(hipMemcpyAsync(H->d_geo_w[l], g.w, sizeof(g.w), hipMemcpyHostToDevice, s));
+   H->gl[l] = g;
+   *ok = true;
+   return AMG_OK;
+}
+
+static int detect_geo(amg_hier *H)
+{
+   H->geo.assign(H->L, 0);
+   H->gl.assign(H->L, amgk::GeoT{});
+   H->d_geo_w.assign(H->L, nullptr);
+   H->geo0 = false;
+   if (H->L < 2 || !H->ctx->fuse_transfer) return AMG_OK;
+   const amg_mat *A = H->lv[0].A;
+   if (!A->mz_P || A->mz_P % A->mz_S) return AMG_OK;
+   int nx = A->mz_S, ny = A->mz_P / A->mz_S, nz = A->nrows / A->mz_P;
+   for (int l = 0; l < H->L - 1; l++) {
+      bool ok = false;
+      AMG_TRY(check_geo_level(H, l, nx, ny, nz, &ok));
+      if (!ok) break;
+      H->geo[l] = 1;
+      nx /= 2;
+      ny /= 2;
+      nz /= 2;
+   }
+   const amgk::GeoT &g = H->gl[0];
+   H->geo0 = H->geo[0] && g.nx >= 64 && g.nx <= 512 && 512 % g.nx == 0 && (g.ny / 2) % (512 / g.nx) == 0;
    return AMG_OK;
 }
 
 extern "C" int amg_hier_fused(const amg_hier *H)
 {
-   return (H && H->geo0) ? 1 : 0;
+   if (!H) return 0;
+   int m = H->geo0 ? 1 : 0;
+   for (int l = 0; l < H->L; l++)
+      if (H->geo[l]) m |= 2 << l;
+   return m;
 }
 
 extern "C" int amg_hier_create(amg_ctx *c, int L, amg_mat *const *A, amg_mat *const *P,
@@ -344,7 +372,7 @@ extern "C" int amg_hier_create(amg_ctx *c, int L, amg_mat *const *A, amg_mat *co
       }
    }
    AMG_TRY(hier_prepare_smoother_arrays(H));
-   AMG_TRY(detect_geo0(H));
+   AMG_TRY(detect_geo(H));
    AMG_HIP(hipStreamSynchronize(c->stream));
    *out = H;
    return AMG_OK;
@@ -516,7 +544,7 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
       if (l == 0 && H->geo0) {
          // level-0 residual and restriction in one pass (no r_fine vector)
          ProfScope ps(H, PROF_FINE_SPMV, s);
-         amgk::mz_residual_restrict(s, v.A, f_fine, v.u, H->g0, H->d_geo_w, H->lv[1].f);
+         amgk::mz_residual_restrict(s, v.A, f_fine, v.u, H->gl[0], H->d_geo_w[0], H->lv[1].f);
          continue;
       }
       {
@@ -525,8 +553,11 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
       }
       {
          ProfScope ps(H, PROF_RESTRICT0, s, l == 0);
-         amgk::spgemv(s, v.R, v.r_fine, nullptr, mv_mode, H->lv[l + 1].f, 0, H->lv[l + 1].n,
-                      nullptr);
+         if (H->geo[l])
+            amgk::geo_restrict(s, H->gl[l], H->d_geo_w[l], v.r_fine, H->lv[l + 1].f);
+         else
+            amgk::spgemv(s, v.R, v.r_fine, nullptr, mv_mode, H->lv[l + 1].f, 0, H->lv[l + 1].n,
+                         nullptr);
       }
    }
    Level &c = H->lv[L - 1];
@@ -536,8 +567,8 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
       v.zero_flag = 0;
       {
          ProfScope ps(H, PROF_PROLONG0, s, l == 0);
-         if (l == 0 && H->geo0)
-            amgk::geo_prolong(s, H->g0, H->d_geo_w, H->lv[1].u, v.u);
+         if (H->geo[l])
+            amgk::geo_prolong(s, H->gl[l], H->d_geo_w[l], H->lv[l + 1].u, v.u);
          else
             amgk::spgemv(s, v.P, H->lv[l + 1].u, v.u, pro_mode, v.u, 0, v.n, nullptr);
       }

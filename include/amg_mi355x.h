@@ -262,12 +262,15 @@ int amg_a_diag(amg_ctx *ctx, const amg_mat *A, double omega, amg_vec *out);
 int amg_hier_create(amg_ctx *ctx, int num_levels, amg_mat *const *A, amg_mat *const *P,
                     amg_mat *const *R, const amg_opts *opts, amg_hier **out);
 int amg_hier_free(amg_hier *H);
-/* 1 when the hierarchy runs level 0's residual and restriction as one fused
- * kernel (SMEM_Sync_AMG.cpp:44-60's SMEM_Residual + SMEM_Restrict pair): A_0 is
- * plane-marched (amg_mat_plane_march) and R_0 / P_0 equal, entry for entry, the
- * geometric transfers of A_0's box (checked on the device at creation);
- * bit-identical to the two kernels.  amg_set_fuse_transfer(ctx, 0) (env
- * AMG_FUSE_TRANSFER=0) keeps them apart for hierarchies created afterwards. */
+/* Geometric transfers: bit 0 set when the hierarchy runs level 0's residual
+ * and restriction as one fused kernel (SMEM_Sync_AMG.cpp:44-60's SMEM_Residual
+ * + SMEM_Restrict pair); bit l + 1 when level l's R_l / P_l equal, entry for
+ * entry (checked on the device at creation), the linear-interpolation
+ * transfers of level l's box -- level 0's box from the plane-marched A_0
+ * (amg_mat_plane_march), each next level's halved -- and run as geometric
+ * restriction / prolongation kernels.  Bit-identical to the CSR kernels.
+ * amg_set_fuse_transfer(ctx, 0) (env AMG_FUSE_TRANSFER=0) keeps the CSR path
+ * for hierarchies created afterwards. */
 int amg_hier_fused(const amg_hier *H);
 int amg_set_fuse_transfer(amg_ctx *ctx, int enable);
 int amg_hier_set_opts(amg_hier *H, const amg_opts *opts);

@@ -192,7 +192,7 @@ def test_fused_residual_restrict(ctx, amg, oracle, dims, zc):
     f = amg.rhs_rand(0, n)
     fz, (u1, h1, k1) = _hier_solve(ctx, amg, host, f, 8, 1, 1, zc=zc)
     f0, (u0, h0, k0) = _hier_solve(ctx, amg, host, f, 8, 1, 0, zc=zc)
-    assert fz == 1 and f0 == 0
+    assert fz & 3 == 3 and f0 == 0  # fused level 0, geometric R_0 / P_0
     OH = po.Hier(host["A"], host["P"], host["R"], po.make_opts(smooth_weight=0.8, num_cycles=8))
     u_cpu, hist_cpu, _ = OH.solve(f)
     assert_bitwise(u1, u0, "fused vs unfused iterate")
@@ -202,9 +202,10 @@ def test_fused_residual_restrict(ctx, amg, oracle, dims, zc):
 
 
 def test_fused_transfer_detection(ctx, amg, oracle):
-    """Only the geometric form fuses: aggregation transfers, a perturbed R_0
-    value, a perturbed P_0 column, and boxes whose lines do not fit (nx = 32, 96)
-    keep the two kernels."""
+    """Only the geometric form takes the geometric kernels (amg_hier_fused bit
+    l + 1: level l's transfers, bit 0: level 0's fused residual + restriction):
+    aggregation transfers, a perturbed R_0 value, a perturbed P_0 column and
+    boxes whose planes are not marched (nx = 96) keep the CSR kernels."""
     from oracle import pyoracle as po
 
     def hier(g, tweak=None):
@@ -222,8 +223,11 @@ def test_fused_transfer_detection(ctx, amg, oracle):
                 M.free()
         return fused
 
-    assert hier(amg.Gen(64, interp=amg.AMG_INTERP_LINEAR)) == 1
-    assert hier(amg.Gen(32, interp=amg.AMG_INTERP_LINEAR)) == 0  # lines of 32: below the kernel's range
+    # 64^3: level 0 fused, geometric transfers on levels 0..3 (boxes 64..8;
+    # the 4^3 level is below the check's interior row)
+    assert hier(amg.Gen(64, interp=amg.AMG_INTERP_LINEAR)) == 0b11111
+    # lines of 32: below the fused kernel's range, transfers still geometric
+    assert hier(amg.Gen(32, interp=amg.AMG_INTERP_LINEAR)) == 0b1110
     assert hier(amg.Gen(64, interp=amg.AMG_INTERP_AGGREGATE)) == 0
     assert hier(amg.Gen(96, 8, 8, interp=amg.AMG_INTERP_LINEAR)) == 0
 
