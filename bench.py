@@ -66,16 +66,50 @@ def storage(nrows, nnz, vi, dc, rp, pp=0, mp=0):
     return 12 * nnz + 4 * (nrows + 1), "csr"
 
 
-def load_traffic(n, fmt):
-    """HBM bytes per launch of the fine residual kernel from the rocprofv3 --pmc
-    passes (FETCH_SIZE and WRITE_SIZE, corrected per access width by calibration
-    streams: tools/pmc_traffic.py -> profiles/traffic.json), if profiled for n."""
+def load_traffic(n, kernel):
+    """HBM bytes per launch of a fine-level kernel from the rocprofv3 --pmc passes
+    (FETCH_SIZE and WRITE_SIZE, corrected by calibration streams of known size:
+    tools/pmc_fine.py -> profiles/traffic.json "kernels"), if profiled for n."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         d = json.load(open(path))
-        return d[str(n)][fmt.split(" ")[0]]["fine_residual_bytes_per_launch"]
+        return d[str(n)]["kernels"][kernel]["bytes_per_launch"]
     except Exception:
         return None
+
+
+def fine_kernels(n0, mat_bytes, ms, launches, fused, fmt):
+    """Per-launch time (HIP events on the compute stream inside the timed loop)
+    and algorithmic bytes of each fine-level kernel of a step.
+    Profile categories: 0 level-0 residual (fused with R0 when fused & 1),
+    1 post-smoothing sweep, 2 R0, 3 P0 prolongation + correction, 4 outer
+    residual + norm (fused with the next cycle's first sweep)."""
+    def per(c):
+        return ms[c] / launches[c] if launches[c] else None
+    out = {}
+    out["outer_residual_sweep"] = (per(4), mat_bytes + 24 * n0,
+                                   "outer residual r = f - A0 u + norm partials, fused with the next "
+                                   f"cycle's first Jacobi sweep (reads f, u; writes u_next; {fmt})")
+    out["post_sweep"] = (per(1), mat_bytes + 24 * n0, f"post-smoothing Jacobi sweep (reads f, u; writes u_next; {fmt})")
+    if fused & 1:
+        out["residual_restrict"] = (per(0), mat_bytes + 16 * n0 + 8 * (n0 // 8),
+                                    "level-0 residual fused with the geometric restriction "
+                                    "(reads f, u; writes f_1)")
+    else:
+        out["residual"] = (per(0), mat_bytes + 24 * n0, f"level-0 residual ({fmt})")
+        out["restrict0"] = (per(2), None, "R0 restriction")
+    if fused & 2:
+        out["prolong0"] = (per(3), 16 * n0 + 8 * (n0 // 8),
+                           "geometric prolongation + correction u += P0 e (reads u, e; writes u)")
+    else:
+        out["prolong0"] = (per(3), None, "P0 prolongation + correction (CSR form)")
+    res = {}
+    for k, (t, b, what) in out.items():
+        if t is None or b is None:
+            continue
+        gbs = b / (t * 1e-3) / 1e9
+        res[k] = {"ms": t, "bytes": b, "gbs": gbs, "frac": gbs / HBM_PEAK_GBS, "what": what}
+    return res
 
 
 def cpu_baseline(gen, amg, f, args):
@@ -198,10 +232,9 @@ def main():
     # matrix bytes per pass in the format the kernels stream
     mat_bytes, fmt = storage(n0, z0, As[0].value_index, As[0].dict_index, As[0].row_pattern,
                              As[0].pair_pattern, As[0].master_pattern)
-    # dominant kernel: fine-grid residual SpGEMV r = f - A u (matrix + f, u, r)
-    res_bytes = mat_bytes + 24 * n0
-    res_ms = ms[0] / max(launches[0], 1)
-    achieved = res_bytes / (res_ms * 1e-3) / 1e9
+    fused = H.fused
+    plane_march = As[0].plane_march
+    kernels = fine_kernels(n0, mat_bytes, ms, launches, fused, fmt)
     # fine-grid SpMV y = A x (matrix + x + y), events on the same stream
     x = ctx.vec(n0)
     x.set(1.0)
@@ -239,9 +272,17 @@ def main():
     triad = C.c_double()
     amg.check(amg.lib.amg_stream_triad(ctx.h, 1 << 28, 10, C.byref(triad)))
     log(f"[gpu] STREAM triad {triad.value:.0f} GB/s")
-    log(f"[gpu] fine residual {res_ms:.3f} ms ({achieved:.0f} GB/s), fine SpMV {spmv_ms.value:.3f} ms "
-        f"({spmv_gbs:.0f} GB/s); smoother {ms[1] / max(launches[1], 1):.3f} ms, "
-        f"R0 {ms[2] / max(launches[2], 1):.3f} ms, P0 {ms[3] / max(launches[3], 1):.3f} ms")
+    for k, v in kernels.items():
+        log(f"[gpu] {k}: {v['ms']:.3f} ms, {v['gbs']:.0f} GB/s ({v['frac']:.3f} of peak, "
+            f"{v['gbs'] / triad.value:.3f} of triad)")
+    log(f"[gpu] fine SpMV {spmv_ms.value:.3f} ms ({spmv_gbs:.0f} GB/s)")
+    dom = max(kernels, key=lambda k: kernels[k]["ms"])
+    dk = kernels[dom]
+    roofline = {"bound": "hbm", "kernel": f"{dom}: {dk['what']}", "achieved": dk["gbs"], "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": dk["frac"], "traffic": load_traffic(n, dom),
+                "alg_bytes_per_launch": dk["bytes"], "avg_launch_ms": dk["ms"],
+                "frac_of_stream_triad": dk["gbs"] / triad.value,
+                "selection": "the fine-level kernel with the largest time per step (fine_kernels)"}
     x.free()
     y.free()
     H.free()
@@ -275,7 +316,8 @@ def main():
                                f"{L}-level geometric Galerkin hierarchy, outer residual + norm per step",
                    "n": n, "levels": L, "nnz_A0": z0, "rows": n0,
                    "reuse_outer_residual": args.reuse_outer_residual,
-                   "matrix_format": fmt, "parallelism": "single GPU"},
+                   "matrix_format": fmt, "plane_march": plane_march, "geometric_transfers": fused,
+                   "parallelism": "single GPU"},
         "fine_spmv": {"gbs": spmv_gbs, "ms": spmv_ms.value, "bytes": spmv_bytes,
                       "frac": spmv_gbs / HBM_PEAK_GBS, "format": fmt},
         "fine_spmv_csr": general["csr"],
@@ -285,11 +327,8 @@ def main():
                          "frac": general["csr"]["frac"], "alg_bytes_per_launch": general["csr"]["bytes"],
                          "avg_launch_ms": general["csr"]["ms"]},
         "stream_triad_gbs": triad.value,
-        "roofline": {"bound": "hbm", "kernel": f"fine-grid residual SpGEMV r = f - A0 u ({fmt})",
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(n, fmt),
-                     "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms,
-                     "frac_of_stream_triad": achieved / triad.value},
+        "roofline": roofline,
+        "fine_kernels": kernels,
         "cpu_baseline": cpu,
         "parity": parity,
         "final_relres": rn / r0,

@@ -11,11 +11,12 @@
  * Parity status (see DESIGN.md "Oracle"): the reference sources cannot be
  * compiled here without stand-ins for hypre/METIS headers the image lacks, so
  * there is no oracle/_ref build.  The reference ships no tests or fixtures.
- * This restatement is pinned against the one known-answer value recorded from
- * a run of the reference itself (SURVEY.md Sec.6 / BASELINE.md Sec.2: SMEM_Solve sync
- * V(1,1), 16^3 7-pt, 2-level 2x2x2 aggregation, omega=0.8, 20 cycles ->
- * relres 2.6446866599577e-03) and against closed-form properties; everything
- * else is "parity unpinned" beyond that restatement.
+ * PARITY UNPINNED: nothing pins this restatement to reference outputs.  The
+ * one value the survey session recorded (SMEM_Solve sync V(1,1), 16^3 7-pt,
+ * 2-level 2x2x2 aggregation, omega=0.8, 20 cycles -> relres
+ * 2.6446866599577e-03) came from a stand-in-header build of the reference and
+ * is kept only as a cross-check; agreement rests on the line-by-line
+ * restatement of the cited reference loops and on closed-form properties.
  *
  * Floating point: compiled with -ffp-contract=off so every a*x product is
  * rounded before it is accumulated, exactly as the reference's

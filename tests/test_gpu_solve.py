@@ -62,8 +62,9 @@ def compare_solve(amg, oracle, ctx, host, opts, f, blocks=None):
 
 
 def test_known_answer_relres(amg, oracle, ctx):
-    """The reference's own SMEM_Solve run (SURVEY.md Sec.6 / BASELINE.md Sec.2):
-    16^3 7-pt, 2-level 2x2x2 aggregation, omega 0.8, Jacobi V(1,1), 20 cycles."""
+    """The survey's cross-check value of SMEM_Solve (stand-in-header build of the
+    reference, so unpinned): 16^3 7-pt, 2-level 2x2x2
+    aggregation, omega 0.8, Jacobi V(1,1), 20 cycles."""
     ka = json.load(open(os.path.join(HERE, "golden", "known_answer.json")))
     case = ka["smem_solve_16cube_aggregation"]
     _, L, host = hierarchy(amg, oracle, 16, amg.AMG_INTERP_AGGREGATE, levels=2)
