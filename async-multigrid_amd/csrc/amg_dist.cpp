@@ -79,9 +79,11 @@ extern "C" int amg_dist_init_host(amg_ctx *c, int nranks, int rank, amg_host_xch
 extern "C" int amg_dist_finalize(amg_ctx *c)
 {
    if (!c || !c->xport) return AMG_OK;
+   // nothing may be in flight on any stream when the communicator goes
+   // (an async solve that returned early can leave level-stream work queued)
    hipStreamSynchronize(c->stream);
    hipStreamSynchronize(c->comm_stream);
-   for (auto &lc : c->xport->level_comms) ncclCommDestroy(lc);
+   for (auto s : c->level_streams) hipStreamSynchronize(s);
    if (c->xport->comm) ncclCommDestroy(c->xport->comm);
    delete c->xport;
    c->xport = nullptr;
@@ -845,6 +847,11 @@ extern "C" int amg_dist_hier_free(amg_dist_hier *D)
    if (!D) return AMG_OK;
    hipStreamSynchronize(D->ctx->stream);
    hipStreamSynchronize(D->ctx->comm_stream);
+   for (auto s : D->ctx->level_streams) hipStreamSynchronize(s);
+   for (auto &a : D->al) {
+      if (a.ev_ready) hipEventDestroy(a.ev_ready);
+      if (a.ev_done) hipEventDestroy(a.ev_done);
+   }
    for (auto &v : D->lv)
       for (DistMat *M : {&v.A, &v.P, &v.R})
          if (M->A) amg_mat_free(M->A);

@@ -17,9 +17,17 @@
 //   * it then recomputes its private residual f - A u_k from the value of u it
 //     observed at its own update (LOCAL residual, SMEM_Async_AMG.cpp:284-301);
 //   * every operator application of level k exchanges its ghost rows with the
-//     neighbouring slabs over RCCL point-to-point on level k's OWN
-//     communicator (ncclCommSplit), enqueued on level k's stream, so levels
-//     never wait for each other -- on the GPU or across GPUs;
+//     neighbouring slabs over RCCL point-to-point.  All exchanges of all levels
+//     go through ONE communicator on ONE communication stream, in the host's
+//     issue order (cycle-major, level-minor, the same on every rank): level
+//     k's stream packs its send buffer and records an event, the comm stream
+//     waits on it, runs the grouped send/recv and records completion, level
+//     k's stream waits on that.  Every RCCL operation thus has the same
+//     position in one sequence on every rank, so no cross-rank ordering of
+//     concurrent communicators (nor the multiplexing of level streams onto
+//     the 4 hardware queues) can deadlock; the compute of the levels still
+//     overlaps freely (DMEM_Comm.cpp:81-348 likewise drives every message
+//     class through one MPI communicator);
 //   * levels below the replication threshold are computed redundantly on every
 //     rank after one allgather of the restricted residual.
 // Termination: each level performs num_cycles corrections (LOCAL convergence,
@@ -45,7 +53,24 @@ int level_cap(const amg_dist_hier *D, int l)
    return l < D->Ld ? D->lv[l].cap : D->cA[l - D->Ld]->nrows;
 }
 
-// ghost exchange of x for M on the level stream over the level's communicator
+// hand the level stream's work to the comm stream (and back): the RCCL
+// operation runs on c->comm_stream after everything level k issued before it
+int to_comm(amg_dist_hier *D, AsyncLevel &a)
+{
+   AMG_HIP(hipEventRecord(a.ev_ready, a.s));
+   AMG_HIP(hipStreamWaitEvent(D->ctx->comm_stream, a.ev_ready, 0));
+   return AMG_OK;
+}
+
+int from_comm(amg_dist_hier *D, AsyncLevel &a)
+{
+   AMG_HIP(hipEventRecord(a.ev_done, D->ctx->comm_stream));
+   AMG_HIP(hipStreamWaitEvent(a.s, a.ev_done, 0));
+   return AMG_OK;
+}
+
+// ghost exchange of x for M: packed on the level stream, sent / received on
+// the comm stream over the main communicator
 int a_halo(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x)
 {
    if (M.replicated_cols || M.peers.empty()) return AMG_OK;
@@ -61,8 +86,10 @@ int a_halo(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x)
       rp[i] = x + M.ncol_own + M.roff[i];
       rbytes[i] = M.rcnt[i] * 8;
    }
-   return xp_p2p(D->ctx, a.s, np, M.peers.data(), sp.data(), sbytes.data(), rp.data(), rbytes.data(),
-                 a.comm);
+   AMG_TRY(to_comm(D, a));
+   AMG_TRY(xp_p2p(D->ctx, D->ctx->comm_stream, np, M.peers.data(), sp.data(), sbytes.data(), rp.data(),
+                  rbytes.data()));
+   return from_comm(D, a);
 }
 
 int a_spgemv(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x, const double *b,
@@ -102,7 +129,9 @@ int restrict_to(amg_dist_hier *D, AsyncLevel &a, int l)
       const int R = D->ctx->xport->nranks;
       double *slot = a.gath + (size_t)D->gath_blk * R;
       AMG_TRY(a_spgemv(D, a, D->lv[l].R, a.r[l], nullptr, mv, slot));
-      AMG_TRY(xp_allgather(D->ctx, a.s, slot, a.gath, (long long)D->gath_blk * 8, a.comm));
+      AMG_TRY(to_comm(D, a));
+      AMG_TRY(xp_allgather(D->ctx, D->ctx->comm_stream, slot, a.gath, (long long)D->gath_blk * 8));
+      AMG_TRY(from_comm(D, a));
       launch_scatter_blocks(a.s, a.gath, D->gath_blk, D->d_gcnt, D->d_gdsp, R, a.r[l + 1]);
       return AMG_OK;
    }
@@ -237,21 +266,13 @@ int setup_async(amg_dist_hier *D)
       amgk::l1_norms(c->stream, D->cA[l - Ld], p);
       D->cl1.push_back(p);
    }
-   // one communicator per level stream: RCCL orders operations per
-   // communicator, so independent level streams need independent communicators
-   if (!t->host() && (int)t->level_comms.size() < active) {
-      for (int k = (int)t->level_comms.size(); k < active; k++) {
-         ncclComm_t nc;
-         AMG_NCCL(ncclCommSplit(t->comm, 0, t->rank, &nc, nullptr));
-         t->level_comms.push_back(nc);
-      }
-   }
    const bool multadd = multadd_of(D->o);
    D->al.resize(active);
    for (int k = 0; k < active; k++) {
       AsyncLevel &a = D->al[k];
       a.s = c->level_streams[k];
-      a.comm = t->host() ? nullptr : t->level_comms[k];
+      AMG_HIP(hipEventCreateWithFlags(&a.ev_ready, hipEventDisableTiming));
+      AMG_HIP(hipEventCreateWithFlags(&a.ev_done, hipEventDisableTiming));
       const int coarsest = std::min(L - 1, multadd ? k : k + 1);
       a.r.assign(coarsest + 1, nullptr);
       a.e.assign(k + 1, nullptr);
@@ -302,7 +323,8 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
       D->al[k].acc.reset(D->o);
    }
    // issue order cycle-major / level-minor: every rank enqueues the same
-   // sequence per level communicator; the GPU runs the level streams freely
+   // sequence of RCCL operations on the one comm stream; the GPU runs the
+   // level streams' compute freely
    for (int cyc = 0; cyc < D->o.num_cycles; cyc++)
       for (int k = 0; k < active; k++) AMG_TRY(level_correction(D, k));
    for (int k = 0; k < active; k++) {

@@ -15,7 +15,6 @@ struct amg_transport {
    ncclComm_t comm = nullptr;
    amg_host_xchg_fn fn = nullptr; // test transport through host memory
    void *user = nullptr;
-   std::vector<ncclComm_t> level_comms; // one per async level stream (ncclCommSplit)
    bool host() const { return fn != nullptr; }
 };
 
@@ -83,7 +82,8 @@ struct AccelState {
 // per-stream exchange state of the asynchronous additive cycle (one per level)
 struct AsyncLevel {
    hipStream_t s = nullptr;
-   ncclComm_t comm = nullptr;
+   hipEvent_t ev_ready = nullptr; // level stream -> comm stream: send data packed
+   hipEvent_t ev_done = nullptr;  // comm stream -> level stream: exchange complete
    std::map<const DistMat *, double *> sbuf; // pack buffers of this stream
    std::vector<double *> r, e;               // r[l], e[l]: level-l residual / correction
    double *u_priv = nullptr, *y = nullptr, *y_fine = nullptr;
