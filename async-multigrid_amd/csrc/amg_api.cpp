@@ -86,6 +86,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_PLANE_MARCH_XCD")) c->mz_xcd = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
+   if (const char *v = std::getenv("AMG_RR_OCC")) c->rr_occ = std::atoi(v);
    *out = c;
    return AMG_OK;
 }
@@ -595,7 +596,7 @@ static int build_master_pattern(amg_mat *A)
    // P rows (P % 512 == 0: a workgroup's 512 positions never straddle planes)
    if (A->ctx->plane_march && J == 7 && mo[3] == -1 && mo[4] == 1 && mo[1] == -mo[6] &&
        mo[2] == -mo[5] && mo[5] > 1 && mo[6] > mo[5] && mo[6] % 512 == 0 && A->nrows % mo[6] == 0 &&
-       A->nrows / mo[6] >= 2) {
+       A->nrows / mo[6] >= 2 && A->nrows < (1 << 29)) { // 32-bit byte offsets in the kernels
       A->mz_P = mo[6];
       A->mz_S = mo[5];
    }

@@ -96,6 +96,7 @@ struct amg_ctx {
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies
    int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)
+   int rr_occ = 0;         // 5: the fused residual + restriction compiled for 5 waves / SIMD
 };
 
 struct amg_mat {

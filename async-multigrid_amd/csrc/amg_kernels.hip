@@ -958,6 +958,44 @@ static void launch_mp(hipStream_t s, const amg_mat *A, const double *x, int rb, 
 // ---------------------------------------------------------------------------
 constexpr int AMG_MZ_MAXZC = 64;
 
+// 16-byte / 8-byte loads at a 32-bit element index from a wave-uniform base:
+// the byte offset stays a zero-extended 32-bit VGPR (global_load ... off,
+// s[base] addressing: one VGPR per address, no 64-bit address arithmetic);
+// callers guarantee 8 * index < 2^32
+__device__ __forceinline__ v2d ld2u(const double *b, unsigned i)
+{
+   return *reinterpret_cast<const v2du *>(reinterpret_cast<const char *>(b) + (size_t)(i * 8u));
+}
+__device__ __forceinline__ double ld1u(const double *b, unsigned i)
+{
+   return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(b) + (size_t)(i * 8u));
+}
+
+// the 7 master entries of a row pair in master (= CSR) order; a wave whose
+// pairs all use every entry (the box interior) skips the per-entry use tests
+template <int NEG, bool UNI>
+__device__ __forceinline__ v2d mz_acc7(v2d acc, const v2d (&xv)[7], unsigned long long mk, const MpSten &Sv,
+                                       const v2d *mvp)
+{
+   if (__all(mk == 0x3FFFull)) {
+#pragma unroll
+      for (int j = 0; j < 7; j++) {
+         const v2d v = UNI ? v2d{Sv.val[j], Sv.val[j]} : mvp[j];
+         acc.x = NEG ? acc.x - v.x * xv[j].x : acc.x + v.x * xv[j].x;
+         acc.y = NEG ? acc.y - v.y * xv[j].y : acc.y + v.y * xv[j].y;
+      }
+   } else {
+#pragma unroll
+      for (int j = 0; j < 7; j++) {
+         const unsigned int b = (unsigned int)(mk >> (2 * j)) & 3u;
+         const v2d v = UNI ? v2d{Sv.val[j], Sv.val[j]} : mvp[j];
+         if (b & 1) acc.x = NEG ? acc.x - v.x * xv[j].x : acc.x + v.x * xv[j].x;
+         if (b & 2) acc.y = NEG ? acc.y - v.y * xv[j].y : acc.y + v.y * xv[j].y;
+      }
+   }
+   return acc;
+}
+
 template <int NEG, bool NEED_DIAG, class Epi, bool UNI>
 __global__ __launch_bounds__(256) void csr_mz_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
@@ -980,26 +1018,25 @@ __global__ __launch_bounds__(256) void csr_mz_kernel(
    if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
    const int pblk = lg % npb, chunk = lg / npb;
    const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
-   const long long N = (long long)nz * P;
    const int pos = pblk * 512 + 2 * tid;
-   const double *xp0 = x + pos;
-   v2d xm = k0 > 0 ? *reinterpret_cast<const v2du *>(xp0 + (long long)(k0 - 1) * P) : v2d{0.0, 0.0};
-   v2d xc = *reinterpret_cast<const v2du *>(xp0 + (long long)k0 * P);
-   v2d xq = k0 + 1 < nz ? *reinterpret_cast<const v2du *>(xp0 + (long long)(k0 + 1) * P) : v2d{0.0, 0.0};
+   const unsigned Nu = (unsigned)((long long)nz * P);
+   v2d xm = k0 > 0 ? ld2u(x, (unsigned)(k0 - 1) * P + pos) : v2d{0.0, 0.0};
+   v2d xc = ld2u(x, (unsigned)k0 * P + pos);
+   v2d xq = k0 + 1 < nz ? ld2u(x, (unsigned)(k0 + 1) * P + pos) : v2d{0.0, 0.0};
    __syncthreads();
    for (int k = k0; k < k1; k++) {
-      const long long row = (long long)k * P + pos;
+      const unsigned row = (unsigned)k * P + pos;
       // prefetch plane k + 2 (this chunk's last iteration needs plane k1)
       v2d xn{0.0, 0.0};
-      if (k + 2 < nz && k + 1 < k1) xn = *reinterpret_cast<const v2du *>(x + row + 2LL * P);
+      if (k + 2 < nz && k + 1 < k1) xn = ld2u(x, row + 2u * P);
       const int pid = ppat[row >> 1];
       v2d acc = epi.init2((int)row);
       v2d pf = xc_pf ? xc : epi.pf2((int)row);
-      const v2d ym = *reinterpret_cast<const v2du *>(x + (row >= S ? row - S : 0));
-      const v2d yp = *reinterpret_cast<const v2du *>(x + (row + S + 2 <= N ? row + S : N - 2));
+      const v2d ym = ld2u(x, row >= (unsigned)S ? row - S : 0u);
+      const v2d yp = ld2u(x, row + S + 2 <= Nu ? row + S : Nu - 2);
       double e = 0.0;
-      if (lane == 0 && row > 0) e = x[row - 1];
-      if (lane == 63 && row + 2 < N) e = x[row + 2];
+      if (lane == 0 && row > 0) e = ld1u(x, row - 1);
+      if (lane == 63 && row + 2 < Nu) e = ld1u(x, row + 2);
       double lft = __shfl_up(xc.y, 1, 64);
       double rgt = __shfl_down(xc.x, 1, 64);
       if (lane == 0) lft = e;
@@ -1013,13 +1050,7 @@ __global__ __launch_bounds__(256) void csr_mz_kernel(
       xv[4] = v2d{xc.y, rgt};
       xv[5] = yp;
       xv[6] = xq;
-#pragma unroll
-      for (int j = 0; j < 7; j++) {
-         const unsigned int b = (unsigned int)(mk >> (2 * j)) & 3u;
-         const v2d v = UNI ? v2d{Sv.val[j], Sv.val[j]} : mval[pid * 7 + j];
-         if (b & 1) acc.x = NEG ? acc.x - v.x * xv[j].x : acc.x + v.x * xv[j].x;
-         if (b & 2) acc.y = NEG ? acc.y - v.y * xv[j].y : acc.y + v.y * xv[j].y;
-      }
+      acc = mz_acc7<NEG, UNI>(acc, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
       v2d dg{0.0, 0.0};
       if (NEED_DIAG) dg = UNI ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 7];
       const v2d out = epi.finish2((int)row, acc, dg, pf);
@@ -1154,14 +1185,17 @@ struct Val7 {
    double v[7];
 };
 
-template <bool UNI, int LC>
-__global__ __launch_bounds__(256) void mz_res_restrict_kernel(
+template <bool UNI, int LC, int OCC = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void mz_res_restrict_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
-   const v2d *__restrict__ mval_g, Val7 Sv, const double *__restrict__ x, const double *__restrict__ f,
+   const v2d *__restrict__ mval_g, Val7 Sv7, const double *__restrict__ x, const double *__restrict__ f,
    const double *__restrict__ wg, int nx, int ny, int nz, int zcc, int nlb, int xcd,
    double *__restrict__ fc)
 {
    constexpr int NL = 2 * LC + 1; // fine lines per lane
+   MpSten Sv;
+#pragma unroll
+   for (int j = 0; j < 7; j++) Sv.val[j] = Sv7.v[j];
    __shared__ unsigned long long mtab[256];
    __shared__ v2d mval[UNI ? 1 : 256 * 7];
    __shared__ double xr[2][4][NL];
@@ -1186,37 +1220,37 @@ __global__ __launch_bounds__(256) void mz_res_restrict_kernel(
    const bool lastl = y0 + 2 * LC >= ny; // the group's last line is outside the box
    const bool d2x = 2 * cx + 2 < nx;     // dx = 2 inside
    const int pos0 = y0 * S + 2 * cx;      // line 0 offset in the plane
+   const unsigned Nu = (unsigned)N;
    v2d xm[NL], xc[NL], xq[NL];
 #pragma unroll
    for (int i = 0; i < NL; i++) {
-      const double *p = x + pos0 + (long long)i * S;
+      const unsigned p = (unsigned)pos0 + (unsigned)i * S;
       const bool ok = i < NL - 1 || !lastl;
-      xm[i] = (ok && kf0 > 0) ? *reinterpret_cast<const v2du *>(p + (long long)(kf0 - 1) * P) : v2d{0.0, 0.0};
-      xc[i] = ok ? *reinterpret_cast<const v2du *>(p + (long long)kf0 * P) : v2d{0.0, 0.0};
-      xq[i] = (ok && kf0 + 1 < nz) ? *reinterpret_cast<const v2du *>(p + (long long)(kf0 + 1) * P)
-                                   : v2d{0.0, 0.0};
+      xm[i] = (ok && kf0 > 0) ? ld2u(x, p + (unsigned)(kf0 - 1) * P) : v2d{0.0, 0.0};
+      xc[i] = ok ? ld2u(x, p + (unsigned)kf0 * P) : v2d{0.0, 0.0};
+      xq[i] = (ok && kf0 + 1 < nz) ? ld2u(x, p + (unsigned)(kf0 + 1) * P) : v2d{0.0, 0.0};
    }
    double acc[LC];
 #pragma unroll
    for (int c = 0; c < LC; c++) acc[c] = 0.0;
    __syncthreads();
    for (int k = kf0; k <= kf1; k++) {
-      const long long base = (long long)k * P + pos0;
+      const unsigned base = (unsigned)k * P + pos0;
       v2d r[NL];
       // halo lines 2Ky0 - 1 and 2Ky0 + 2 LC + 1 (entries outside the box are unused)
-      const v2d hm = *reinterpret_cast<const v2du *>(x + (base >= S ? base - S : 0));
-      const long long hp_i = base + (long long)NL * S;
-      const v2d hp = *reinterpret_cast<const v2du *>(x + (hp_i + 2 <= N ? hp_i : N - 2));
+      const v2d hm = ld2u(x, base >= (unsigned)S ? base - S : 0u);
+      const unsigned hp_i = base + (unsigned)NL * S;
+      const v2d hp = ld2u(x, hp_i + 2 <= Nu ? hp_i : Nu - 2);
 #pragma unroll
       for (int i = 0; i < NL; i++) {
-         const long long row = base + (long long)i * S;
+         const unsigned row = base + (unsigned)i * S;
          r[i] = v2d{0.0, 0.0};
          if (i == NL - 1 && lastl) continue;
          const int pid = ppat[row >> 1];
-         v2d a2 = *reinterpret_cast<const v2du *>(f + row);
+         v2d a2 = ld2u(f, row);
          double e = 0.0;
-         if (lane == 0 && row > 0) e = x[row - 1];
-         if (lane == 63 && row + 2 < N) e = x[row + 2];
+         if (lane == 0 && row > 0) e = ld1u(x, row - 1);
+         if (lane == 63 && row + 2 < Nu) e = ld1u(x, row + 2);
          double lft = __shfl_up(xc[i].y, 1, 64);
          double rgt = __shfl_down(xc[i].x, 1, 64);
          if (lane == 0) lft = e;
@@ -1230,14 +1264,7 @@ __global__ __launch_bounds__(256) void mz_res_restrict_kernel(
          xv[4] = v2d{xc[i].y, rgt};
          xv[5] = i == NL - 1 ? hp : xc[i == NL - 1 ? NL - 1 : i + 1];
          xv[6] = xq[i];
-#pragma unroll
-         for (int j = 0; j < 7; j++) {
-            const unsigned int b = (unsigned int)(mk >> (2 * j)) & 3u;
-            const v2d v = UNI ? v2d{Sv.v[j], Sv.v[j]} : mval[pid * 7 + j];
-            if (b & 1) a2.x = a2.x - v.x * xv[j].x;
-            if (b & 2) a2.y = a2.y - v.y * xv[j].y;
-         }
-         r[i] = a2;
+         r[i] = mz_acc7<1, UNI>(a2, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
       }
       // next plane's operands: load plane k + 2 while the restriction runs
 #pragma unroll
@@ -1246,7 +1273,7 @@ __global__ __launch_bounds__(256) void mz_res_restrict_kernel(
          xc[i] = xq[i];
          xq[i] = v2d{0.0, 0.0};
          if ((i < NL - 1 || !lastl) && k + 2 < nz && k + 1 <= kf1)
-            xq[i] = *reinterpret_cast<const v2du *>(x + base + (long long)i * S + 2LL * P);
+            xq[i] = ld2u(x, base + (unsigned)i * S + 2u * P);
       }
       // r at fine column 2cx + 2: lane t + 1 (LDS across waves for line groups
       // of more than 64 lanes)
@@ -1307,11 +1334,12 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
    const int nb = nlb * nch;
    const int xcd = A->ctx->mz_xcd;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
-#define AMG_RR(U, L) \
-   mz_res_restrict_kernel<U, L><<<nb, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, f, wdev, g.nx, g.ny, \
+#define AMG_RR(U, L, ...) \
+   mz_res_restrict_kernel<U, L, ##__VA_ARGS__><<<nb, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, f, wdev, g.nx, g.ny, \
                                                    g.nz, zcc, nlb, xcd, fc)
    if (A->mp_uni) {
       if (LC == 2) AMG_RR(true, 2);
+      else if (A->ctx->rr_occ == 5) AMG_RR(true, 1, 5);
       else AMG_RR(true, 1);
    } else {
       if (LC == 2) AMG_RR(false, 2);
