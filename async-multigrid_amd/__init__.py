@@ -23,7 +23,8 @@ from .abi import (AMG_JACOBI, AMG_GAUSS_SEIDEL, AMG_HYBRID_JGS, AMG_SYMM_JACOBI,
                   AMG_ASYNC_AFACX, AMG_ASYNC_MULTADD, AMG_INTERP_LINEAR, AMG_INTERP_AGGREGATE,
                   AMG_GEN_A, AMG_GEN_P, AMG_GEN_R, AMG_VEC_F, AMG_VEC_U, AMG_VEC_R,
                   AMG_ASYNC_GS, AMG_SEMI_ASYNC_GS, AMG_BPX, AMG_NO_ACCEL, AMG_RICHARD_ACCEL,
-                  AMG_CHEBY_RECUR_ACCEL)
+                  AMG_CHEBY_RECUR_ACCEL, AMG_FULL_ASYNC, AMG_SEMI_ASYNC, AMG_LOCAL, AMG_GLOBAL,
+                  AMG_READ_SOL, AMG_READ_RES)
 
 lib = abi.load()
 

@@ -32,6 +32,8 @@ AMG_L1_JACOBI, AMG_L1_HYBRID_JGS = 6, 12
 AMG_MULT, AMG_AFACX, AMG_MULTADD, AMG_ASYNC_AFACX, AMG_ASYNC_MULTADD = 0, 1, 2, 5, 6
 AMG_BPX = 3
 AMG_FULL_ASYNC, AMG_SEMI_ASYNC = 0, 1
+AMG_LOCAL, AMG_GLOBAL = 0, 1
+AMG_READ_SOL, AMG_READ_RES = 0, 1
 AMG_NO_ACCEL, AMG_RICHARD_ACCEL, AMG_CHEBY_RECUR_ACCEL = 0, 1, 2
 AMG_VEC_F, AMG_VEC_U, AMG_VEC_R = 0, 1, 2
 AMG_INTERP_LINEAR, AMG_INTERP_AGGREGATE = 0, 1
@@ -46,7 +48,8 @@ class AmgOpts(C.Structure):
                 ("check_resnorm", _i), ("cheby_flag", _i), ("cheby_mu", _d),
                 ("cheby_delta", _d), ("num_threads", _i), ("jgs_block_rows", _i),
                 ("reuse_outer_residual", _i), ("async_type", _i), ("profile", _i),
-                ("accel_type", _i), ("cheby_grid", _i)]
+                ("accel_type", _i), ("cheby_grid", _i), ("res_compute_type", _i),
+                ("read_type", _i), ("converge_test_type", _i)]
 
 
 class AmgClassicalOpts(C.Structure):

@@ -275,6 +275,12 @@ void dmem_mult_accel(hipStream_t s, double *x, const double *e, double *d, int n
                      double omd);
 // atomic correction: u += e (device-scope fp64 atomics), u_priv = value after the add
 void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n);
+// serialised (SEMI_ASYNC) form: u += e; u_priv = u (u_priv may be null)
+void semi_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n);
+// READ_RES: r -= y (atomic or serialised), r_priv = the updated value
+void res_update(hipStream_t s, double *r, const double *y, double *r_priv, int n, int atomic);
+// u[rb, re) += x[rb, re), device-scope atomics
+void atomic_add(hipStream_t s, double *u, const double *x, int rb, int re);
 
 // STREAM triad a = b + q c over n doubles (n even)
 void stream_triad(hipStream_t s, double *a, const double *b, const double *c, double q, long long n);

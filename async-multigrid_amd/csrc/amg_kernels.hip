@@ -2438,11 +2438,14 @@ __global__ void hybrid_jgs_k(const int *__restrict__ rowptr, const int *__restri
                              const int *__restrict__ blk, int nblk,
                              const double *__restrict__ ds, double weight, int zero, int reverse)
 {
-   // A lane re-reads values of u it stored earlier in this sweep.  Plain
-   // global loads may be served by a stale line of the CU's vector L1 (gfx950
-   // stores write through to L2 without refreshing L1), so every access to u
-   // is a relaxed atomic: same-location coherence then holds by the memory
-   // model (agent-scope loads are L2-served).
+   // In-block operands (SMEM_Smooth.cpp:253-263, 290-300): a column the lane
+   // has NOT updated yet this sweep holds its old value, which is u_prev's
+   // copy (0 in the zero-guess sweep); the row updated just before (the
+   // stencil's -1 / +1 neighbour) comes from a register; only older updated
+   // rows are re-read from u, as relaxed agent-scope atomics (gfx950 stores
+   // write through to L2 without refreshing the CU's L1).  Every operand is
+   // the value the reference's sequential loop reads, so results are
+   // bit-identical, and the row's loads no longer wait on the previous row.
    auto ld = [u](int k) { return __hip_atomic_load(u + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
    auto st = [u](int k, double v) {
       __hip_atomic_store(u + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2450,26 +2453,33 @@ __global__ void hybrid_jgs_k(const int *__restrict__ rowptr, const int *__restri
    const int b = blockIdx.x * blockDim.x + threadIdx.x;
    if (b >= nblk) return;
    const int ns = blk[b], ne = blk[b + 1];
-   if (zero)
-      for (int i = ns; i < ne; i++) st(i, 0.0);
+   int last_i = -1;
+   double last = 0.0;
    for (int c = 0; c < ne - ns; c++) {
       const int i = reverse ? ne - 1 - c : ns + c;
       const int rs = rowptr[i], rend = rowptr[i + 1];
       const double a = val[rs];
-      if (a == 0.0) continue;
-      const double d = ds ? ds[i] : a;
-      double res = f[i];
-      for (int jj = rs; jj < rend; jj++) {
-         const int ii = col[jj];
-         if (ii >= ns && ii < ne)
-            res -= val[jj] * ld(ii);
-         else if (!zero)
-            res -= val[jj] * u_prev[ii];
+      const double old = zero ? 0.0 : u_prev[i];
+      double v = old;
+      if (a != 0.0) {
+         const double d = ds ? ds[i] : a;
+         double res = f[i];
+         for (int jj = rs; jj < rend; jj++) {
+            const int ii = col[jj];
+            if (ii >= ns && ii < ne) {
+               const bool done = reverse ? ii > i : ii < i;
+               const double x = !done ? (zero ? 0.0 : u_prev[ii]) : (ii == last_i ? last : ld(ii));
+               res -= val[jj] * x;
+            } else if (!zero) {
+               res -= val[jj] * u_prev[ii];
+            }
+         }
+         v = zero ? weight * res / d : old + weight * res / d;
       }
-      if (zero)
-         st(i, weight * res / d);
-      else
-         st(i, ld(i) + weight * res / d);
+      // a_ii == 0: the row keeps its value (0 after the zero-guess reset)
+      if (a != 0.0 || zero) st(i, v);
+      last_i = i;
+      last = v;
    }
 }
 
@@ -2811,6 +2821,60 @@ __global__ void atomic_correct_k(double *u, const double *__restrict__ e,
 void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n)
 {
    if (n > 0) atomic_correct_k<<<ew_blocks(n), 256, 0, s>>>(u, e, u_priv, n);
+}
+
+// SEMI_ASYNC update (SMEM_Async_AMG.cpp:238-283, under the reference's lock;
+// here the updates of all levels are serialised on one stream): u += e,
+// u_priv = u -- plain read-modify-write, no other level touches u meanwhile
+__global__ void semi_correct_k(double *__restrict__ u, const double *__restrict__ e,
+                               double *__restrict__ u_priv, int n)
+{
+   EW_LOOP(i, 0, n)
+   {
+      const double v = u[i] + e[i];
+      u[i] = v;
+      if (u_priv) u_priv[i] = v;
+   }
+}
+void semi_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n)
+{
+   if (n > 0) semi_correct_k<<<ew_blocks(n), 256, 0, s>>>(u, e, u_priv, n);
+}
+
+// READ_RES residual update (SMEM_Async_AMG.cpp:288-295 / 270-275): the shared
+// residual r -= y (y = A e of the level's correction), the level's private
+// residual = the value after its update.  atomic: FULL_ASYNC (device-scope fp64
+// atomics); otherwise the serialised SEMI_ASYNC form.
+__global__ void res_update_k(double *r, const double *__restrict__ y, double *__restrict__ r_priv, int n,
+                             int atomic)
+{
+   EW_LOOP(i, 0, n)
+   {
+      const double yi = y[i];
+      double v;
+      if (atomic) {
+         v = atomicAdd(r + i, -yi) - yi;
+      } else {
+         v = r[i] - yi;
+         r[i] = v;
+      }
+      r_priv[i] = v;
+   }
+}
+void res_update(hipStream_t s, double *r, const double *y, double *r_priv, int n, int atomic)
+{
+   if (n > 0) res_update_k<<<ew_blocks(n), 256, 0, s>>>(r, y, r_priv, n, atomic);
+}
+
+// u[rb, re) += x[rb, re) with device-scope atomics (the GLOBAL residual
+// phase's fine-grid smoothing correction, SMEM_Async_AMG.cpp:61-70)
+__global__ void atomic_add_k(double *u, const double *__restrict__ x, int rb, int re)
+{
+   EW_LOOP(i, rb, re) atomicAdd(u + i, x[i]);
+}
+void atomic_add(hipStream_t s, double *u, const double *x, int rb, int re)
+{
+   if (re > rb) atomic_add_k<<<ew_blocks(re - rb), 256, 0, s>>>(u, x, rb, re);
 }
 
 // ---------------------------------------------------------------------------

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstring>
 #include <utility>
+#include <thread>
 #include <vector>
 
 #include "amg_internal.h"
@@ -44,6 +45,10 @@ struct AddLevel {
    double *u_prev = nullptr, *y = nullptr, *u_priv = nullptr, *y_fine = nullptr, *scratch = nullptr;
    double *u_fine = nullptr, *u_coarse = nullptr, *u_coarse_prev = nullptr, *u_fine_prev = nullptr,
           *r_fine = nullptr;
+   // asynchronous options: READ_RES private correction sum (level_vector[k].f[0]),
+   // GLOBAL residual phase's fine smoothing correction and scratch (n0 each)
+   double *f_acc = nullptr, *g_u = nullptr, *g_prev = nullptr, *g_y = nullptr, *g_r = nullptr;
+   hipEvent_t ev_a = nullptr, ev_b = nullptr; // level stream <-> update stream (SEMI_ASYNC)
 };
 
 } // namespace
@@ -384,6 +389,10 @@ extern "C" int amg_hier_free(amg_hier *H)
    hipStreamSynchronize(H->ctx->stream);
    for (auto s : H->ctx->level_streams) hipStreamSynchronize(s);
    prof_drain(H);
+   for (auto &a : H->al) {
+      if (a.ev_a) hipEventDestroy(a.ev_a);
+      if (a.ev_b) hipEventDestroy(a.ev_b);
+   }
    for (void *p : H->allocs) hipFree(p);
    for (auto &l : H->lv) hipFree(l.d_blk);
    delete H;
@@ -944,48 +953,241 @@ extern "C" int amg_eigs_power(amg_hier *H, int iters, double *eig_max, double *e
 // synchronisation.  Corrections land in u through device-scope fp64 atomics
 // and each level recomputes its private residual f - A u_k from the value of
 // u it observed at its own update (SMEM_Async_AMG.cpp:284-301, 338-351).
+// SMEM_Smooth over rows [blk[b0], blk[b1]) of the fine grid from a zero guess:
+// the GLOBAL residual phase's fine smoothing of level k's A_ns_global slice
+// (SMEM_Async_AMG.cpp:46-59), with level k's residual r.  Block-aligned slices
+// (the hybrid / asynchronous GS smoothers work on whole blocks).
+static void smooth_fine_slice(amg_hier *H, hipStream_t s, int k, const double *r, int b0, int b1)
+{
+   Level &v = H->lv[0];
+   AddLevel &a = H->al[k];
+   const amg_opts &o = H->o;
+   const int rb = v.blk[b0], re = v.blk[b1];
+   const int sweeps = o.num_fine_smooth_sweeps;
+   if (re <= rb || sweeps <= 0) return;
+   const bool sym = is_multadd(o) && o.num_post_smooth_sweeps > 0 && o.num_pre_smooth_sweeps > 0;
+   if (o.smoother == AMG_HYBRID_JACOBI_GAUSS_SEIDEL || o.smoother == AMG_L1_HYBRID_JACOBI_GAUSS_SEIDEL) {
+      amg_hybrid_jgs_dev(H->ctx, s, v.A, r, a.g_u, a.g_prev, v.n, v.d_blk + b0, b1 - b0, rb, re,
+                         o.smoother == AMG_L1_HYBRID_JACOBI_GAUSS_SEIDEL ? v.l1 : nullptr, 1.0, sweeps, 1, 0);
+   } else if (o.smoother == AMG_ASYNC_GAUSS_SEIDEL || o.smoother == AMG_SEMI_ASYNC_GAUSS_SEIDEL) {
+      amgk::vset(s, a.g_u, 0.0, rb, re);
+      amgk::async_gs(s, v.A, r, a.g_u, v.d_blk + b0, b1 - b0, sweeps, o.smoother == AMG_SEMI_ASYNC_GAUSS_SEIDEL, 0);
+   } else {
+      const bool l1 = o.smoother == AMG_L1_JACOBI;
+      const double w = l1 ? 1.0 : o.smooth_weight;
+      if (sym) {
+         amg_sym_jacobi_dev(s, v.A, r, a.g_u, a.g_y, a.g_r, w, l1 ? v.l1 : nullptr, sweeps, 1, rb, re, 0);
+      } else {
+         for (int q = 0; q < sweeps; q++) {
+            if (q == 0) {
+               amgk::jacobi_zero(s, v.A->diag, r, l1 ? v.l1 : nullptr, w, a.g_u, rb, re, 0);
+            } else {
+               amgk::vcopy(s, a.g_u, a.g_prev, 0, v.n);
+               amgk::jacobi_sweep(s, v.A, r, a.g_prev, l1 ? v.l1 : nullptr, w, a.g_u, rb, re);
+            }
+         }
+      }
+   }
+}
+
+// SMEM_Async_Add_AMG (SMEM_Async_AMG.cpp:7-437): every level k (its
+// correction is nonzero for k <= L-2) runs its correction loop on its own HIP
+// stream.  Options:
+//   async_type FULL_ASYNC: corrections enter the shared u (READ_SOL) or the
+//     shared residual (READ_RES) with device-scope fp64 atomics, racing like the
+//     reference's `omp atomic` updates;
+//   async_type SEMI_ASYNC: each level's whole update (u += e, u_k = u; or
+//     r -= A e, r_k = r) is exclusive -- the reference takes a lock
+//     (:238-283); here the updates of all levels run, in issue order, on one
+//     update stream (the context's comm stream), so no two levels' updates
+//     interleave;
+//   read_type READ_SOL: the level recomputes r_k = f - A u_k from the u it saw
+//     (:338-348); READ_RES (LOCAL residuals): it applies y = A e to the shared
+//     residual and reads that back (:227-236, 288-295), accumulating its
+//     corrections privately, added into u at the end (:416-426; SEMI_ASYNC
+//     updates u directly, :268-279);
+//   res_compute_type GLOBAL (ASYNC_MULTADD): each iteration first smooths the
+//     level's slice of the fine grid from its residual and adds that into u
+//     (:35-77), and ends with the level computing its slice of the global
+//     residual f - A u into the shared r and reading the whole shared r back
+//     (:356-414); slices = equal splits of the fine grid's blocks;
+//   converge_test_type LOCAL: every level stops after num_cycles corrections;
+//     GLOBAL: levels keep correcting until EVERY level has done num_cycles
+//     (CheckConverge's all-levels count, Misc.cpp:418-441; the reference's
+//     GLOBAL and ALL_LEVELS share the value 1) -- the host keeps up to two
+//     corrections in flight per level stream and polls their completion.
+// level_corrections[k] returns the corrections level k performed.
 extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *level_corrections,
                                double *relres)
 {
    AMG_ARG(H && f && u, "amg_async_solve: null argument");
    AMG_ARG(is_all_levels(H->o), "amg_async_solve: ASYNC_MULTADD / ASYNC_AFACX hierarchies only");
-   AMG_ARG(H->o.async_type == AMG_FULL_ASYNC, "amg_async_solve: SEMI_ASYNC not supported");
+   const amg_opts &o = H->o;
+   AMG_ARG(o.async_type == AMG_FULL_ASYNC || o.async_type == AMG_SEMI_ASYNC, "amg_async_solve: async_type %d",
+           o.async_type);
    amg_ctx *c = H->ctx;
    const int L = H->L;
    AMG_ARG((int)c->level_streams.size() >= L, "amg_async_solve: context has %d level streams, need %d",
            (int)c->level_streams.size(), L);
+   const bool semi = o.async_type == AMG_SEMI_ASYNC;
+   // SMEM_Main.cpp:650-660: GLOBAL residuals only for ASYNC_MULTADD
+   const bool global_res = o.res_compute_type == AMG_GLOBAL && o.solver == AMG_ASYNC_MULTADD;
+   const bool read_res = o.read_type == AMG_READ_RES && !global_res;
+   const bool conv_global = o.converge_test_type == AMG_GLOBAL;
    AMG_TRY(solve_begin(H, f, u));
    Level &v0 = H->lv[0];
    const int n0 = v0.n;
+   // levels with a correction loop: [k_lo, k_hi).  The finest level whose
+   // correction is nonzero is L-2 (see add_level_correction); with GLOBAL
+   // residuals no group runs level 0 -- the sliced fine-grid smoothing takes
+   // its place (PartitionLevels' finest_level = 1, SMEM_Setup.cpp:609-615)
+   const int k_lo = global_res ? 1 : 0;
+   const int k_hi = std::max(k_lo + 1, L - 1);
+   const int ngrp = k_hi - k_lo;
+   // global slices: equal splits of level 0's blocks (A_ns_global, SMEM_Setup.cpp:924-936)
+   std::vector<int> gb(L + 1, 0);
+   {
+      const int nb = (int)v0.blk.size() - 1;
+      for (int q = 0; q <= ngrp; q++) gb[k_lo + q] = (int)((long long)nb * q / ngrp);
+   }
+   for (int k = k_lo; k < k_hi; k++) {
+      AddLevel &a = H->al[k];
+      if (read_res && !a.f_acc) AMG_TRY(dalloc(H, n0, &a.f_acc));
+      if (global_res && !a.g_u) {
+         AMG_TRY(dalloc(H, n0, &a.g_u));
+         AMG_TRY(dalloc(H, n0, &a.g_prev));
+         AMG_TRY(dalloc(H, n0, &a.g_y));
+         AMG_TRY(dalloc(H, n0, &a.g_r));
+      }
+      if (!a.ev_a) {
+         AMG_HIP(hipEventCreateWithFlags(&a.ev_a, hipEventDisableTiming));
+         AMG_HIP(hipEventCreateWithFlags(&a.ev_b, hipEventDisableTiming));
+      }
+   }
    hipEvent_t ready;
    AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
    AMG_HIP(hipEventRecord(ready, c->stream));
-   // the finest level whose correction is nonzero is L-2 (see add_level_correction)
-   const int active = std::max(1, L - 1);
-   for (int k = 0; k < active; k++) {
-      AMG_HIP(hipStreamWaitEvent(c->level_streams[k], ready, 0));
+   for (int k = k_lo; k < k_hi; k++) {
+      hipStream_t s = c->level_streams[k];
+      AMG_HIP(hipStreamWaitEvent(s, ready, 0));
       // level_vector[k].r[0] = vector.r[0] (SMEM_Async_AMG.cpp:10-15)
-      amgk::vcopy(c->level_streams[k], H->r0, H->al[k].y_fine, 0, n0);
+      amgk::vcopy(s, H->r0, H->al[k].y_fine, 0, n0);
+      if (read_res) amgk::vset(s, H->al[k].f_acc, 0.0, 0, n0);
+      if (global_res) amgk::vset(s, H->al[k].g_u, 0.0, 0, n0);
    }
+   AMG_HIP(hipStreamWaitEvent(c->comm_stream, ready, 0));
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
-   for (int cyc = 0; cyc < H->o.num_cycles; cyc++) {
-      for (int k = 0; k < active; k++) {
-         hipStream_t s = c->level_streams[k];
-         AddLevel &a = H->al[k];
-         add_level_correction(H, s, k, a.y_fine);
-         amgk::atomic_correct(s, v0.u, a.e[0], a.u_priv, n0);
-         // SMEM_Residual(A0, f, u_k, y, r_k): y = A u_k; r = f - y
-         amgk::spgemv(s, v0.A, a.u_priv, nullptr, mv, a.y, 0, n0, nullptr);
-         amgk::vsub(s, v0.f, a.y, a.y_fine, 0, n0);
+   hipStream_t us = c->comm_stream; // SEMI_ASYNC update stream
+   // one correction of level k, issued on its stream
+   auto correction = [&](int k) -> int {
+      hipStream_t s = c->level_streams[k];
+      AddLevel &a = H->al[k];
+      auto to_update = [&]() -> int {
+         AMG_HIP(hipEventRecord(a.ev_a, s));
+         AMG_HIP(hipStreamWaitEvent(us, a.ev_a, 0));
+         return AMG_OK;
+      };
+      auto from_update = [&]() -> int {
+         AMG_HIP(hipEventRecord(a.ev_b, us));
+         AMG_HIP(hipStreamWaitEvent(s, a.ev_b, 0));
+         return AMG_OK;
+      };
+      const int grb = v0.blk[gb[k]], gre = v0.blk[gb[k + 1]];
+      if (global_res) {
+         smooth_fine_slice(H, s, k, a.y_fine, gb[k], gb[k + 1]);
+         if (!semi) amgk::atomic_add(s, v0.u, a.g_u, grb, gre);
       }
+      add_level_correction(H, s, k, a.y_fine);
+      if (read_res) {
+         amgk::spgemv(s, v0.A, a.e[0], nullptr, mv, a.y, 0, n0, nullptr);
+         if (semi) {
+            AMG_TRY(to_update());
+            amgk::semi_correct(us, v0.u, a.e[0], nullptr, n0);
+            amgk::res_update(us, H->r0, a.y, a.y_fine, n0, 0);
+            AMG_TRY(from_update());
+         } else {
+            amgk::vaxpy(s, 1.0, a.e[0], a.f_acc, 0, n0);
+            amgk::res_update(s, H->r0, a.y, a.y_fine, n0, 1);
+         }
+      } else {
+         if (semi) {
+            AMG_TRY(to_update());
+            if (global_res) amgk::semi_correct(us, v0.u, a.g_u, nullptr, n0); // :258-265 (g_u is 0 off the slice)
+            amgk::semi_correct(us, v0.u, a.e[0], a.u_priv, n0);
+            AMG_TRY(from_update());
+         } else {
+            amgk::atomic_correct(s, v0.u, a.e[0], a.u_priv, n0);
+         }
+         if (!global_res) {
+            // SMEM_Residual(A0, f, u_k, y, r_k): y = A u_k; r = f - y
+            amgk::spgemv(s, v0.A, a.u_priv, nullptr, mv, a.y, 0, n0, nullptr);
+            amgk::vsub(s, v0.f, a.y, a.y_fine, 0, n0);
+         }
+      }
+      if (global_res) {
+         // :356-414: u_k = u; the level's slice of r = f - A u_k into the shared
+         // r; then r_k = r (under the update stream for SEMI_ASYNC)
+         amgk::vcopy(s, v0.u, a.u_priv, 0, n0);
+         amgk::spgemv(s, v0.A, a.u_priv, v0.f, amgk::gemv_mode(-1.0, 1.0), a.y, grb, gre, nullptr);
+         if (semi) AMG_TRY(to_update());
+         hipStream_t ws = semi ? us : s;
+         amgk::vcopy(ws, a.y, H->r0, grb, gre);
+         amgk::vcopy(ws, H->r0, a.y_fine, 0, n0);
+         if (semi) AMG_TRY(from_update());
+      }
+      AMG_HIP(hipGetLastError());
+      return AMG_OK;
+   };
+   std::vector<int> issued(L, 0);
+   if (!conv_global) {
+      for (int cyc = 0; cyc < o.num_cycles; cyc++)
+         for (int k = k_lo; k < k_hi; k++) {
+            AMG_TRY(correction(k));
+            issued[k]++;
+         }
+   } else {
+      // run until every level has completed num_cycles corrections; faster
+      // levels keep correcting meanwhile (at most 2 in flight per level)
+      constexpr int DEPTH = 2;
+      std::vector<std::vector<hipEvent_t>> done(L, std::vector<hipEvent_t>(DEPTH));
+      for (auto &d : done)
+         for (auto &e : d) AMG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      std::vector<int> completed(L, 0);
+      const long long cap = 1000LL * std::max(1, o.num_cycles);
+      int st = AMG_OK;
+      for (;;) {
+         bool all = true;
+         for (int k = k_lo; k < k_hi; k++) {
+            while (completed[k] < issued[k] && hipEventQuery(done[k][completed[k] % DEPTH]) == hipSuccess)
+               completed[k]++;
+            if (completed[k] < o.num_cycles) all = false;
+         }
+         if (all) break;
+         bool progressed = false;
+         for (int k = k_lo; k < k_hi && st == AMG_OK; k++) {
+            if (issued[k] - completed[k] < DEPTH && issued[k] < cap) {
+               if ((st = correction(k)) != AMG_OK) break;
+               hipEventRecord(done[k][issued[k] % DEPTH], c->level_streams[k]);
+               issued[k]++;
+               progressed = true;
+            }
+         }
+         if (st != AMG_OK) break;
+         if (!progressed) std::this_thread::yield();
+      }
+      for (int k = k_lo; k < k_hi; k++) hipStreamSynchronize(c->level_streams[k]);
+      for (auto &d : done)
+         for (auto &e : d) hipEventDestroy(e);
+      if (st != AMG_OK) return st;
    }
-   for (int k = 0; k < active; k++) {
-      hipEvent_t e;
-      AMG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      AMG_HIP(hipEventRecord(e, c->level_streams[k]));
-      AMG_HIP(hipStreamWaitEvent(c->stream, e, 0));
-      AMG_HIP(hipEventDestroy(e));
+   for (int k = k_lo; k < k_hi; k++) {
+      AMG_HIP(hipEventRecord(ready, c->level_streams[k]));
+      AMG_HIP(hipStreamWaitEvent(c->stream, ready, 0));
    }
+   AMG_HIP(hipEventRecord(ready, us));
+   AMG_HIP(hipStreamWaitEvent(c->stream, ready, 0));
+   if (read_res && !semi)
+      for (int k = k_lo; k < k_hi; k++) amgk::vaxpy(c->stream, 1.0, H->al[k].f_acc, v0.u, 0, n0); // :416-426
    AMG_HIP(hipEventDestroy(ready));
    AMG_TRY(outer_residual(H, 1));
    AMG_HIP(hipMemcpyAsync(c->h_pinned, H->d_hist + 1, sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -993,6 +1195,6 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    AMG_HIP(hipStreamSynchronize(c->stream));
    if (relres) *relres = c->h_pinned[0] / H->r0norm;
    if (level_corrections)
-      for (int k = 0; k < L; k++) level_corrections[k] = H->o.num_cycles;
+      for (int k = 0; k < L; k++) level_corrections[k] = issued[k];
    return AMG_OK;
 }

@@ -61,6 +61,13 @@ typedef struct amg_gen amg_gen;   /* structured 7-pt problem + geometric hierarc
 #define AMG_FULL_ASYNC 0
 #define AMG_SEMI_ASYNC 1
 
+/* input.res_compute_type / converge_test_type (Main.hpp:89-90) and
+ * input.read_type (Main.hpp:110-111) of the asynchronous additive solver */
+#define AMG_LOCAL 0
+#define AMG_GLOBAL 1
+#define AMG_READ_SOL 0
+#define AMG_READ_RES 1
+
 /* DMEM outer acceleration (input.accel_type, DMEM_Misc.cpp:612-666).  The
  * reference's -cheby and -richard both store 1 (Main.hpp:80-81 define
  * CHEBY_ACCEL and RICHARD_ACCEL as 1), so its DMEM_ChebyUpdate always runs the
@@ -102,6 +109,12 @@ typedef struct {
                                     AMG_CHEBY_RECUR_ACCEL, with cheby_mu/delta */
    int cheby_grid;               /* DMEM input.cheby_grid: the async additive level
                                     whose correction carries the d recurrence  */
+   int res_compute_type;         /* input.res_compute_type: AMG_LOCAL / AMG_GLOBAL
+                                    (ASYNC_MULTADD only, SMEM_Main.cpp:650-660) */
+   int read_type;                /* input.read_type: AMG_READ_SOL / AMG_READ_RES   */
+   int converge_test_type;       /* input.converge_test_type: AMG_LOCAL (every level
+                                    num_cycles corrections) / AMG_GLOBAL (levels run
+                                    on until every level has done num_cycles)  */
 } amg_opts;
 
 void amg_opts_default(amg_opts *o); /* SMEM_Main.cpp:65-105 defaults */
