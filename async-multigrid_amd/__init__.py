@@ -99,6 +99,10 @@ class Context:
         """Fused level-0 residual + restriction on geometric hierarchies (default on)."""
         check(lib.amg_set_fuse_transfer(self.h, int(enable)))
 
+    def set_fuse_prolong(self, enable):
+        """Prolongation fused into the first post-smoothing sweep of marched geometric levels (default off: VALU-bound, slower)."""
+        check(lib.amg_set_fuse_prolong(self.h, int(enable)))
+
     def csr(self, nrows, ncols, rowptr, col, val, diag_first=1):
         return Mat.register(self, nrows, ncols, rowptr, col, val, diag_first)
 
@@ -131,6 +135,7 @@ class Mat:
         self.pair_anchor16 = lib.amg_mat_pair_anchor16(handle)  # slab-compressed anchors
         self.master_pattern = lib.amg_mat_master_pattern(handle)  # master length J (-J: uniform values), 0 = not coded
         self.plane_march = lib.amg_mat_plane_march(handle)  # plane size P of the marching kernel, 0 = not marched
+        self.march_points = lib.amg_mat_march_points(handle)  # 7 / 27-point marching kernel, 0 = not marched
 
     @classmethod
     def register(cls, ctx, nrows, ncols, rowptr, col, val, diag_first=1):
@@ -207,6 +212,7 @@ class Hier:
         self.h = h
         self.n0 = As[0].nrows
         self.fused = lib.amg_hier_fused(h)  # bit 0: level-0 residual + restriction fused; bit l+1: level l geometric transfers
+        self.fused_prolong = lib.amg_hier_fused_prolong(h)  # bit l: level l's prolongation fused into its post sweep
 
     def set_opts(self, opts):
         check(lib.amg_hier_set_opts(self.h, C.byref(opts)))

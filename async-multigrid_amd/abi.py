@@ -85,6 +85,7 @@ PROTOTYPES = {
     "amg_mat_master_pattern": (_i, [_p]),
     "amg_set_plane_march": (_i, [_p, _i, _i, _i]),
     "amg_mat_plane_march": (_i, [_p]),
+    "amg_mat_march_points": (_i, [_p]),
     "amg_mat_info": (_i, [_p, _ip, _ip, _llp]),
     "amg_mat_download": (_i, [_p, _p, _ip, _ip, _dp]),
     "amg_vec_create": (_i, [_p, _i, _pp]),
@@ -118,6 +119,8 @@ PROTOTYPES = {
     "amg_hier_free": (_i, [_p]),
     "amg_hier_fused": (_i, [_p]),
     "amg_set_fuse_transfer": (_i, [_p, _i]),
+    "amg_hier_fused_prolong": (_i, [_p]),
+    "amg_set_fuse_prolong": (_i, [_p, _i]),
     "amg_hier_set_opts": (_i, [_p, C.POINTER(AmgOpts)]),
     "amg_hier_set_blocks": (_i, [_p, _i, _ip, _i]),
     "amg_hier_vec": (_i, [_p, _i, _i, _pp]),

@@ -81,10 +81,11 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_PAIR_ANCHOR16")) c->pair_anchor16 = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_PLANE_MARCH")) {
       c->plane_march = std::atoi(v) > 0;
-      if (std::atoi(v) > 1) c->mz_zc = std::min(std::atoi(v), 64);
+      if (std::atoi(v) > 1) c->mz_zc = std::min(std::atoi(v), 64), c->mz_zc_auto = 0;
    }
    if (const char *v = std::getenv("AMG_PLANE_MARCH_XCD")) c->mz_xcd = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
    if (const char *v = std::getenv("AMG_RR_OCC")) c->rr_occ = std::atoi(v);
    *out = c;
@@ -594,13 +595,67 @@ static int build_master_pattern(amg_mat *A)
    A->mp_J = J;
    // plane-marching form: master [0, -P, -S, -1, +1, +S, +P], whole planes of
    // P rows (P % 512 == 0: a workgroup's 512 positions never straddle planes)
+   // (S even: every pair's +-S operand pair is one aligned-in-range 16-byte load)
    if (A->ctx->plane_march && J == 7 && mo[3] == -1 && mo[4] == 1 && mo[1] == -mo[6] &&
-       mo[2] == -mo[5] && mo[5] > 1 && mo[6] > mo[5] && mo[6] % 512 == 0 && A->nrows % mo[6] == 0 &&
-       A->nrows / mo[6] >= 2 && A->nrows < (1 << 29)) { // 32-bit byte offsets in the kernels
+       mo[2] == -mo[5] && mo[5] > 1 && mo[5] % 2 == 0 && mo[6] > mo[5] && mo[6] % 512 == 0 &&
+       A->nrows % mo[6] == 0 && A->nrows / mo[6] >= 2 && A->nrows < (1 << 29)) { // 32-bit byte offsets
       A->mz_P = mo[6];
       A->mz_S = mo[5];
    }
+   // 27-pt plane march: master [0, dz P + dy S + dx ascending (centre skipped)]
+   if (A->ctx->plane_march && J == 27 && A->nrows < (1 << 29) && (uni || T <= 64)) {
+      const int S = mo[16], P = mo[22];
+      bool ok = S >= 4 && S % 2 == 0 && P % 512 == 0 && P % S == 0 && P / S >= 3 && A->nrows % P == 0 &&
+                A->nrows / P >= 2;
+      for (int L = 0, j = 1; ok && L < 27; L++) {
+         if (L == 13) continue;
+         const int o = (L / 9 - 1) * P + ((L / 3) % 3 - 1) * S + (L % 3 - 1);
+         ok = mo[j++] == o;
+      }
+      int dom = -1;
+      if (ok && !uni) {
+         // the most frequent pattern using all 27 entries in both rows with
+         // bit-equal values in the two rows
+         std::vector<unsigned char> pp((size_t)(A->nrows / 2));
+         AMG_HIP(hipMemcpy(pp.data(), A->ppat, pp.size(), hipMemcpyDeviceToHost));
+         std::vector<long long> cnt(T, 0);
+         for (unsigned char q : pp) cnt[q]++;
+         const unsigned long long full = (1ull << 54) - 1;
+         for (int t = 0; t < T; t++) {
+            if (mask[t] != full) continue;
+            bool same = true;
+            for (int j = 0; j < J && same; j++)
+               same = std::memcmp(&mv[((size_t)t * J + j) * 2], &mv[((size_t)t * J + j) * 2 + 1], 8) == 0;
+            if (same && (dom < 0 || cnt[t] > cnt[dom])) dom = t;
+         }
+         if (dom >= 0)
+            for (int j = 0; j < J; j++) A->mz_domval[j] = mv[((size_t)dom * J + j) * 2];
+      }
+      if (ok) {
+         A->mz_P = P;
+         A->mz_S = S;
+         A->mz27 = 1;
+         A->mz_dom = dom;
+      }
+   }
    return AMG_OK;
+}
+
+// back to the row-pattern form (pair / master / march forms dropped)
+static void drop_pair_forms(amg_mat *A)
+{
+   hipFree(A->ppat);
+   hipFree(A->pptab);
+   hipFree(A->mpmask);
+   hipFree(A->mpval);
+   A->ppat = nullptr;
+   A->pptab = nullptr;
+   A->mpmask = nullptr;
+   A->mpval = nullptr;
+   A->pp_n = A->pp_stride = A->pp_centre0 = 0;
+   A->mp_J = A->mp_uni = 0;
+   A->mz_P = A->mz_S = A->mz27 = 0;
+   A->mz_dom = -1;
 }
 
 int amg_mat_finish(amg_mat *A)
@@ -610,10 +665,14 @@ int amg_mat_finish(amg_mat *A)
    if (A->ctx->value_index && A->nnz > 0) AMG_TRY(build_value_index(A));
    if (A->ctx->dict_index && A->vidx) AMG_TRY(build_dict_index(A));
    if (A->ctx->row_pattern && A->didx) AMG_TRY(build_row_pattern(A));
-   if (A->ctx->pair_pattern && A->rpat && A->dc_maxrow <= AMG_PP_MAXROW &&
-       (A->dc_maxrow <= 8 || A->nrows >= AMG_PP_LONG_MIN_ROWS || A->ctx->pair_pattern == 2))
+   const bool pp = A->dc_maxrow <= 8 || A->nrows >= AMG_PP_LONG_MIN_ROWS || A->ctx->pair_pattern == 2;
+   // long-row operators below the pair-coding size still try the 27-pt march
+   // (kept only if it applies: the pair kernel itself is slower there)
+   const bool try27 = !pp && A->ctx->plane_march && A->ctx->master_pattern;
+   if (A->ctx->pair_pattern && A->rpat && A->dc_maxrow <= AMG_PP_MAXROW && (pp || try27))
       AMG_TRY(build_pair_pattern(A));
    if (A->ctx->master_pattern && A->ppat) AMG_TRY(build_master_pattern(A));
+   if (try27 && A->ppat && !A->mz27 && !A->pbase) drop_pair_forms(A);
    return AMG_OK;
 }
 
@@ -668,10 +727,19 @@ extern "C" int amg_mat_master_pattern(const amg_mat *A)
 extern "C" int amg_set_plane_march(amg_ctx *c, int enable, int zc, int xcd)
 {
    AMG_ARG(c, "amg_set_plane_march: null context");
-   AMG_ARG(zc >= 0 && zc <= 64, "amg_set_plane_march: planes per chunk %d outside [1, 64] (0: keep)", zc);
+   AMG_ARG(zc >= -1 && zc <= 64, "amg_set_plane_march: planes per chunk %d outside [1, 64] (0: keep, -1: auto)",
+           zc);
    c->plane_march = enable ? 1 : 0;
-   if (zc > 0) c->mz_zc = zc;
+   if (zc > 0) c->mz_zc = zc, c->mz_zc_auto = 0;
+   if (zc == -1) c->mz_zc = 16, c->mz_zc_auto = 1;
    if (xcd >= 0) c->mz_xcd = xcd ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_set_fuse_prolong(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_fuse_prolong: null context");
+   c->fuse_prolong = enable ? 1 : 0;
    return AMG_OK;
 }
 
@@ -685,6 +753,11 @@ extern "C" int amg_set_fuse_transfer(amg_ctx *c, int enable)
 extern "C" int amg_mat_plane_march(const amg_mat *A)
 {
    return A ? A->mz_P : 0;
+}
+
+extern "C" int amg_mat_march_points(const amg_mat *A)
+{
+   return (A && A->mz_P) ? (A->mz27 ? 27 : 7) : 0;
 }
 
 extern "C" int amg_set_dict_index(amg_ctx *c, int enable)

@@ -93,8 +93,10 @@ struct amg_ctx {
    int pair_anchor16 = 0;  // slab-compressed anchors of pair-coded P/R (measured slower: off)
    int plane_march = 1;    // plane-marching kernel for 7-pt box-grid masters (csr_mz_kernel)
    int mz_zc = 16;         // planes per workgroup chunk of the plane-marching kernel
+   int mz_zc_auto = 1;     // shorten the chunks of small levels to keep >= 2048 workgroups
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies
+   int fuse_prolong = 0;   // prolongation fused into the first post sweep (measured slower: off)
    int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)
    int rr_occ = 0;         // 5: the fused residual + restriction compiled for 5 waves / SIMD
 };
@@ -163,6 +165,13 @@ struct amg_mat {
    // plane-marching form (csr_mz_kernel): the master list is [0, -P, -S, -1, +1,
    // +S, +P] with P % 512 == 0 and nrows = nz * P (0: not applicable)
    int mz_P = 0, mz_S = 0;
+   // 27-pt plane march (csr_mz27_kernel): master list [0, the 26 offsets
+   // dz P + dy S + dx ascending]; mz_dom = the most frequent pair pattern that
+   // uses every entry with one value per entry in both rows (-1: none), its
+   // values in master order (wave-uniform fast path)
+   int mz27 = 0;
+   int mz_dom = -1;
+   double mz_domval[27] = {};
 };
 
 struct amg_vec {
@@ -244,6 +253,10 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
 void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc);
 // u += P e for the checked geometric P of GeoT g (bit-identical to the SpGEMV)
 void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u);
+// u_out = first Jacobi (l1 == nullptr) / L1 Jacobi sweep of A on uc = u + P e,
+// P the checked geometric transfer of marched 7-pt level A (uc never stored)
+void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const double *u, const double *ec,
+                      const GeoT &g, const double *wdev, const double *l1, double omega, double *uout);
 // transpose-product with the expansion-buffer order of T static chunks
 void matvec_t_chunked(hipStream_t s, const amg_mat *AT, const double *x, double *y, int n_src,
                       int T);

@@ -1078,6 +1078,15 @@ __global__ __launch_bounds__(256) void csr_mz_kernel(
    }
 }
 
+// planes per workgroup chunk: the context's, shortened on small levels (when
+// automatic) so the launch keeps >= 2048 workgroups
+static int mz_chunk(const amg_mat *A, int nz, int npb)
+{
+   int zc = std::max(1, std::min(A->ctx->mz_zc, AMG_MZ_MAXZC));
+   if (A->ctx->mz_zc_auto) zc = (int)std::max(1LL, std::min((long long)zc, (long long)nz * npb / 2048));
+   return zc;
+}
+
 template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Epi &e, double *partials)
 {
@@ -1086,7 +1095,7 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
       S.off[j] = A->mp_off[j];
       S.val[j] = A->mp_val[j];
    }
-   const int P = A->mz_P, nz = A->nrows / P, zc = std::max(1, std::min(A->ctx->mz_zc, AMG_MZ_MAXZC));
+   const int P = A->mz_P, nz = A->nrows / P, zc = mz_chunk(A, nz, P / 512);
    const int npb = P / 512, nch = (nz + zc - 1) / zc;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
    if (A->mp_uni)
@@ -1095,6 +1104,178 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
    else
       csr_mz_kernel<NEG, NEED_DIAG, Epi, false><<<npb * nch, 256, 0, s>>>(
          A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);
+}
+
+// ---------------------------------------------------------------------------
+// 27-point plane-marching kernel (csr_mz27_kernel): master-coded operators
+// whose master list is [0, then the 26 offsets dz P + dy S + dx (dz, dy, dx in
+// {-1, 0, 1}, not all 0) ascending] -- the Galerkin coarse operators R A P of
+// the box hierarchy (27-pt stencils, diagonal-first rows).  As in
+// csr_mz_kernel a lane owns rows (2t, 2t + 1) of a workgroup's 512 in-plane
+// positions and marches over a chunk of planes, but here it keeps the three
+// lines y - 1, y, y + 1 of planes k - 1, k, k + 1 in registers, each with its
+// +-1 neighbours (ds_bpermute from the adjacent lanes, the wave's edges from
+// one scalar load): per plane step three 16-byte x loads (the new plane k + 2)
+// replace the master kernel's 27 gathers.  The use masks decide which entries
+// each row adds; a wave whose pairs all have the dominant interior pattern
+// (every entry used, one value per entry in both rows) takes the values from
+// kernel arguments (SGPRs) and skips the use tests.  Each row adds its used
+// entries in master (= CSR) order: bit-identical to every other form.
+// ---------------------------------------------------------------------------
+struct Ln4 {
+   double l, a, b, r; // x at the pair's positions - 1, + 0, + 1, + 2 (one line)
+};
+
+// master entry j -> lexicographic stencil slot (dz + 1) 9 + (dy + 1) 3 + dx + 1
+__device__ __forceinline__ constexpr int mz27_slot(int j)
+{
+   return j == 0 ? 13 : (j <= 13 ? j - 1 : j);
+}
+
+__device__ __forceinline__ v2d mz27_opnd(const Ln4 (&X)[3][3], int L)
+{
+   const Ln4 &q = X[L / 9][(L / 3) % 3];
+   const int dx = L % 3;
+   return dx == 0 ? v2d{q.l, q.a} : (dx == 1 ? v2d{q.a, q.b} : v2d{q.b, q.r});
+}
+
+// one line of plane data at element index idx (even; lines wholly outside the
+// box are clamped, their entries unused): the pair's 16-byte load plus the
+// wave-edge neighbours, then the +-1 shuffles
+__device__ __forceinline__ void mz27_load(const double *__restrict__ x, long long idx, unsigned Nu, int lane,
+                                          v2d &v, double &e)
+{
+   const unsigned i = idx < 0 ? 0u : (idx + 2 > (long long)Nu ? Nu - 2 : (unsigned)idx);
+   v = ld2u(x, i);
+   e = 0.0;
+   if (lane == 0 && i > 0) e = ld1u(x, i - 1);
+   if (lane == 63 && i + 2 < Nu) e = ld1u(x, i + 2);
+}
+
+__device__ __forceinline__ Ln4 mz27_line(v2d v, double e, int lane)
+{
+   double l = __shfl_up(v.y, 1, 64);
+   double r = __shfl_down(v.x, 1, 64);
+   if (lane == 0) l = e;
+   if (lane == 63) r = e;
+   return Ln4{l, v.x, v.y, r};
+}
+
+template <int NEG, bool NEED_DIAG, class Epi, bool UNI>
+__global__ __launch_bounds__(256) void csr_mz27_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
+   const v2d *__restrict__ mval_g, MpSten Sv, int dom, const double *__restrict__ x, int P, int S, int nz,
+   int zc, int npb, int xcd, Epi epi, double *__restrict__ partials)
+{
+   constexpr unsigned long long FULL = (1ull << 54) - 1;
+   const bool xc_pf = pf_is_x<Epi>::value && epi_pf_vec(epi) == x;
+   __shared__ unsigned long long mtab[256];
+   __shared__ v2d mval[UNI ? 1 : 64 * 27];
+   __shared__ double red[AMG_MZ_MAXZC * 8];
+   const int tid = (int)threadIdx.x, lane = tid & 63;
+   if (tid < np) mtab[tid] = mmask_g[tid];
+   if (!UNI)
+      for (int w = tid; w < np * 27; w += 256) mval[w] = mval_g[w];
+   const int G = (int)gridDim.x;
+   int lg = (int)blockIdx.x;
+   if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
+   const int pblk = lg % npb, chunk = lg / npb;
+   const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
+   const int pos = pblk * 512 + 2 * tid;
+   const unsigned Nu = (unsigned)((long long)nz * P);
+   Ln4 X[3][3];
+#pragma unroll
+   for (int m = 0; m < 3; m++) {
+      const int p = k0 - 1 + m;
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+         v2d v{0.0, 0.0};
+         double e = 0.0;
+         if (p >= 0 && p < nz) mz27_load(x, (long long)p * P + pos + (d - 1) * S, Nu, lane, v, e);
+         X[m][d] = mz27_line(v, e, lane);
+      }
+   }
+   __syncthreads();
+   for (int k = k0; k < k1; k++) {
+      const unsigned row = (unsigned)k * P + pos;
+      // prefetch plane k + 2 (the chunk's last iteration needs plane k1)
+      v2d nv[3] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+      double ne[3] = {0.0, 0.0, 0.0};
+      if (k + 2 < nz && k + 1 < k1) {
+#pragma unroll
+         for (int d = 0; d < 3; d++) mz27_load(x, (long long)row + 2LL * P + (d - 1) * S, Nu, lane, nv[d], ne[d]);
+      }
+      const int pid = ppat[row >> 1];
+      v2d acc = epi.init2((int)row);
+      const v2d pf = xc_pf ? v2d{X[1][1].a, X[1][1].b} : epi.pf2((int)row);
+      const bool fast = UNI ? __all(mtab[pid] == FULL) : __all(pid == dom);
+      if (fast) {
+#pragma unroll
+         for (int j = 0; j < 27; j++) {
+            const v2d o = mz27_opnd(X, mz27_slot(j));
+            const double v = Sv.val[j];
+            acc.x = NEG ? acc.x - v * o.x : acc.x + v * o.x;
+            acc.y = NEG ? acc.y - v * o.y : acc.y + v * o.y;
+         }
+      } else {
+         const unsigned long long mk = mtab[pid];
+         const v2d *vp = mval + (UNI ? 0 : pid * 27);
+#pragma unroll
+         for (int j = 0; j < 27; j++) {
+            const unsigned int b = (unsigned int)(mk >> (2 * j)) & 3u;
+            const v2d o = mz27_opnd(X, mz27_slot(j));
+            const v2d v = UNI ? v2d{Sv.val[j], Sv.val[j]} : vp[j];
+            if (b & 1) acc.x = NEG ? acc.x - v.x * o.x : acc.x + v.x * o.x;
+            if (b & 2) acc.y = NEG ? acc.y - v.y * o.y : acc.y + v.y * o.y;
+         }
+      }
+      v2d dg{0.0, 0.0};
+      if (NEED_DIAG) dg = (UNI || fast) ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 27];
+      const v2d out = epi.finish2((int)row, acc, dg, pf);
+      if (partials) {
+         double a = out.x * out.x, b = out.y * out.y;
+#pragma unroll
+         for (int off = 16; off > 0; off >>= 1) {
+            a += __shfl_down(a, off, 32);
+            b += __shfl_down(b, off, 32);
+         }
+         if ((tid & 31) == 0) red[(k - k0) * 8 + (tid >> 5)] = a + b;
+      }
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+         X[0][d] = X[1][d];
+         X[1][d] = X[2][d];
+         X[2][d] = mz27_line(nv[d], ne[d], lane);
+      }
+   }
+   if (partials) {
+      __syncthreads();
+      for (int w = tid; w < 2 * (k1 - k0); w += 256) {
+         const int it = w >> 1, h = w & 1;
+         const double *g = red + it * 8 + 4 * h;
+         partials[((long long)(k0 + it) * P + pblk * 512) / 256 + h] = ((g[0] + g[1]) + g[2]) + g[3];
+      }
+   }
+}
+
+template <int NEG, bool NEED_DIAG, class Epi>
+static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const Epi &e, double *partials)
+{
+   MpSten S;
+   for (int j = 0; j < AMG_MP_MAXJ; j++) {
+      S.off[j] = A->mp_off[j];
+      S.val[j] = A->mp_uni ? A->mp_val[j] : A->mz_domval[j];
+   }
+   const int P = A->mz_P, nz = A->nrows / P, zc = mz_chunk(A, nz, P / 512);
+   const int npb = P / 512, nch = (nz + zc - 1) / zc;
+   const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+   if (A->mp_uni)
+      csr_mz27_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, mv, S, -1, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);
+   else
+      csr_mz27_kernel<NEG, NEED_DIAG, Epi, false><<<npb * nch, 256, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, mv, S, A->mz_dom, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e,
+         partials);
 }
 
 // ---------------------------------------------------------------------------
@@ -1354,21 +1535,11 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
 // pair of the row's interpolation stencil one 16-byte load brings coarse
 // columns cx - 1, cx.  Each row sums u_i + w * e_c over its coarse columns
 // ascending (P's CSR order: cz, cy, cx), the SpGEMV's (alpha = beta = 1) order.
-__global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ e, double *__restrict__ u,
-                                                     const double *__restrict__ wg, int nx, int ny, int nz,
-                                                     long long npairs)
+// rows (i, i + 1) = fine (x, y, z), x even: u_i + sum w e_c over the coarse
+// columns of P's rows in CSR order (cz, cy, cx ascending), from the pair's u
+__device__ __forceinline__ v2d geo_prolong_pair(v2d acc, const double *__restrict__ e, const double *wl, int x,
+                                                int y, int z, int ncx, int ncy, int ncz)
 {
-   __shared__ double wl[27];
-   const int tid = (int)threadIdx.x;
-   if (tid < 27) wl[tid] = wg[tid];
-   __syncthreads();
-   const long long q = (long long)blockIdx.x * 256 + tid;
-   if (q >= npairs) return;
-   const long long i = 2 * q;
-   const int x = (int)(i % nx);
-   const long long yz = i / nx;
-   const int y = (int)(yz % ny), z = (int)(yz / ny);
-   const int ncx = nx >> 1, ncy = ny >> 1, ncz = nz >> 1;
    const int t = x >> 1;
    // coarse candidates of one axis (ascending) and their offsets d = f - 2c
    int cz[2], dz[2], cy[2], dy[2];
@@ -1386,7 +1557,6 @@ __global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ 
       if ((y >> 1) < ncy) cy[my] = y >> 1, dy[my++] = 0;
    }
    const bool lo = t >= 1, hi = t < ncx; // row 2t: coarse t - 1 (dx = 2), t (dx = 0)
-   v2d acc = *reinterpret_cast<const v2du *>(u + i);
 #pragma unroll
    for (int a = 0; a < 2; a++) {
       if (a >= mz) break;
@@ -1403,13 +1573,192 @@ __global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ 
          acc.y = acc.y + w[1] * ec;
       }
    }
-   *reinterpret_cast<v2du *>(u + i) = acc;
+   return acc;
+}
+
+// one fine point (x, y, z): u_i + sum w e_c in P's CSR order (scalar form of
+// geo_prolong_pair, for the marching kernels' wave-edge neighbours)
+__device__ __forceinline__ double geo_prolong_point(double acc, const double *__restrict__ e, const double *wl,
+                                                    int x, int y, int z, int ncx, int ncy, int ncz)
+{
+   int c[3][2], d[3][2], m[3];
+   const int f[3] = {z, y, x}, nc[3] = {ncz, ncy, ncx};
+#pragma unroll
+   for (int q = 0; q < 3; q++) {
+      m[q] = 0;
+      if (f[q] & 1) {
+         c[q][m[q]] = (f[q] - 1) >> 1, d[q][m[q]++] = 1;
+      } else {
+         if (f[q] >= 2) c[q][m[q]] = (f[q] >> 1) - 1, d[q][m[q]++] = 2;
+         if ((f[q] >> 1) < nc[q]) c[q][m[q]] = f[q] >> 1, d[q][m[q]++] = 0;
+      }
+   }
+   for (int a = 0; a < m[0]; a++)
+      for (int b = 0; b < m[1]; b++)
+         for (int q = 0; q < m[2]; q++)
+            acc = acc + wl[d[0][a] * 9 + d[1][b] * 3 + d[2][q]] *
+                           e[((long long)c[0][a] * ncy + c[1][b]) * ncx + c[2][q]];
+   return acc;
+}
+
+__global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ e, double *__restrict__ u,
+                                                     const double *__restrict__ wg, int nx, int ny, int nz,
+                                                     long long npairs)
+{
+   __shared__ double wl[27];
+   const int tid = (int)threadIdx.x;
+   if (tid < 27) wl[tid] = wg[tid];
+   __syncthreads();
+   const long long q = (long long)blockIdx.x * 256 + tid;
+   if (q >= npairs) return;
+   const long long i = 2 * q;
+   const int x = (int)(i % nx);
+   const long long yz = i / nx;
+   const int y = (int)(yz % ny), z = (int)(yz / ny);
+   const v2d acc = *reinterpret_cast<const v2du *>(u + i);
+   *reinterpret_cast<v2du *>(u + i) = geo_prolong_pair(acc, e, wl, x, y, z, nx >> 1, ny >> 1, nz >> 1);
 }
 
 void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u)
 {
    const long long np = (long long)g.nx * g.ny * g.nz / 2;
    geo_prolong_k<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, np);
+}
+
+// Prolongation + correction fused with the first post-smoothing sweep of a
+// marched 7-pt level (SMEM_Sync_AMG.cpp:118-134: SMEM_Sync_SpGEMV(P, e, u, 1, 1,
+// u) then the Jacobi / L1 Jacobi sweep of SMEM_Smooth.cpp:35-45 / 122-130):
+// u_out = uc + w (f - A uc) / a_ii with uc = u + P e never stored.  The
+// csr_mz_kernel march over the corrected iterate: every uc operand (the
+// pair's own line of plane k + 2, lines y -+ 1 of plane k, the wave-edge
+// neighbours) is formed in registers from u and the coarse e exactly as
+// geo_prolong_k forms it (same terms, same order), so the output is
+// bit-identical to geo_prolong_k followed by csr_mz_kernel.  One pass over
+// the fine level instead of two (reads f, u and e, writes u_out).
+template <bool UNI, bool L1>
+__global__ __launch_bounds__(256) void mz_prolong_sweep_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
+   const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ u, const double *__restrict__ e,
+   const double *__restrict__ f, const double *__restrict__ l1, const double *__restrict__ wg, double omega,
+   int nx, int ny, int nz, int zc, int npb, int xcd, double *__restrict__ uout)
+{
+   __shared__ unsigned long long mtab[256];
+   __shared__ v2d mval[UNI ? 1 : 256 * 7];
+   __shared__ double wl[27];
+   const int tid = (int)threadIdx.x, lane = tid & 63;
+   if (tid < np) mtab[tid] = mmask_g[tid];
+   if (tid < 27) wl[tid] = wg[tid];
+   if (!UNI)
+      for (int w = tid; w < np * 7; w += 256) mval[w] = mval_g[w];
+   const int S = nx, P = nx * ny;
+   const int ncx = nx >> 1, ncy = ny >> 1, ncz = nz >> 1;
+   const int G = (int)gridDim.x;
+   int lg = (int)blockIdx.x;
+   if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
+   const int pblk = lg % npb, chunk = lg / npb;
+   const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
+   const int pos = pblk * 512 + 2 * tid;
+   const int fx = pos % nx, fy = pos / nx;
+   __syncthreads();
+   // The operands follow csr_mz_kernel's element indices exactly (row -+ S,
+   // row - 1, row + 2 may wrap into the neighbouring line / plane, as they do
+   // for any matrix with this master list); only indices outside [0, N) are
+   // dropped (no row can use them).  Coordinates one step outside a line or
+   // plane carry into the next one.
+   auto norm3 = [&](int &x, int &y, int &z) {
+      if (x < 0) x += nx, y--;
+      if (x >= nx) x -= nx, y++;
+      if (y < 0) y += ny, z--;
+      if (y >= ny) y -= ny, z++;
+   };
+   // corrected pair at (fx, fy + dy, p)
+   auto uc2 = [&](int p, int dy) -> v2d {
+      int x = fx, y = fy + dy, z = p;
+      norm3(x, y, z);
+      if (z < 0 || z >= nz) return v2d{0.0, 0.0};
+      const unsigned i = (unsigned)z * P + (unsigned)(y * S + x);
+      return geo_prolong_pair(ld2u(u, i), e, wl, x, y, z, ncx, ncy, ncz);
+   };
+   // wave-edge neighbour of the own line (lane 0: element - 1, lane 63: + 2)
+   auto edge = [&](int p) -> double {
+      if (lane != 0 && lane != 63) return 0.0;
+      int x = lane == 0 ? fx - 1 : fx + 2, y = fy, z = p;
+      norm3(x, y, z);
+      if (z < 0 || z >= nz) return 0.0;
+      const unsigned i = (unsigned)z * P + (unsigned)(y * S + x);
+      return geo_prolong_point(ld1u(u, i), e, wl, x, y, z, ncx, ncy, ncz);
+   };
+   v2d xm = uc2(k0 - 1, 0);
+   v2d xc = uc2(k0, 0);
+   double ec = edge(k0);
+   v2d xq = uc2(k0 + 1, 0);
+   double eq = edge(k0 + 1);
+   for (int k = k0; k < k1; k++) {
+      const unsigned row = (unsigned)k * P + pos;
+      // prefetch plane k + 2 (this chunk's last iteration needs plane k1)
+      v2d xn{0.0, 0.0};
+      double en = 0.0;
+      if (k + 2 < nz && k + 1 < k1) {
+         xn = uc2(k + 2, 0);
+         en = edge(k + 2);
+      }
+      const int pid = ppat[row >> 1];
+      const v2d fr = ld2u(f, row);
+      const v2d ym = uc2(k, -1);
+      const v2d yp = uc2(k, 1);
+      double lft = __shfl_up(xc.y, 1, 64);
+      double rgt = __shfl_down(xc.x, 1, 64);
+      if (lane == 0) lft = ec;
+      if (lane == 63) rgt = ec;
+      const unsigned long long mk = mtab[pid];
+      v2d xv[7];
+      xv[0] = xc;
+      xv[1] = xm;
+      xv[2] = ym;
+      xv[3] = v2d{lft, xc.x};
+      xv[4] = v2d{xc.y, rgt};
+      xv[5] = yp;
+      xv[6] = xq;
+      const v2d res = mz_acc7<1, UNI>(fr, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
+      v2d o;
+      if (L1) {
+         const v2d l = ld2u(l1, row);
+         o = v2d{xc.x + res.x / l.x, xc.y + res.y / l.y};
+      } else {
+         const v2d a = UNI ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 7];
+         o = v2d{(a.x != 0.0) ? xc.x + omega * res.x / a.x : xc.x, (a.y != 0.0) ? xc.y + omega * res.y / a.y : xc.y};
+      }
+      *reinterpret_cast<v2du *>(uout + row) = o;
+      xm = xc;
+      xc = xq;
+      ec = eq;
+      xq = xn;
+      eq = en;
+   }
+}
+
+void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const double *u, const double *ec,
+                      const GeoT &g, const double *wdev, const double *l1, double omega, double *uout)
+{
+   MpSten S;
+   for (int j = 0; j < AMG_MP_MAXJ; j++) {
+      S.off[j] = A->mp_off[j];
+      S.val[j] = A->mp_val[j];
+   }
+   const int P = A->mz_P, nz = A->nrows / P, zc = mz_chunk(A, nz, P / 512);
+   const int npb = P / 512, nch = (nz + zc - 1) / zc;
+   const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+#define AMG_PS(U, L) \
+   mz_prolong_sweep_kernel<U, L><<<npb * nch, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, ec, f, l1, wdev, \
+                                                           omega, g.nx, g.ny, g.nz, zc, npb, A->ctx->mz_xcd, uout)
+   if (A->mp_uni) {
+      if (l1) AMG_PS(true, true);
+      else AMG_PS(true, false);
+   } else {
+      if (l1) AMG_PS(false, true);
+      else AMG_PS(false, false);
+   }
+#undef AMG_PS
 }
 
 // Geometric restriction f_c = R r (SMEM_Sync_Parfor_Restrict,
@@ -1462,7 +1811,9 @@ template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int rb, int re,
                          const Epi &e, double *partials, int tiles)
 {
-   if (A->mz_P && rb == 0 && re == A->nrows)
+   if (A->mz_P && rb == 0 && re == A->nrows && A->mz27)
+      launch_mz27<NEG, NEED_DIAG>(s, A, x, e, partials);
+   else if (A->mz_P && rb == 0 && re == A->nrows)
       launch_mz<NEG, NEED_DIAG>(s, A, x, e, partials);
    else if (A->mp_J && (rb & 1) == 0)
       launch_mp<NEG, NEED_DIAG>(s, A, x, rb, re, e, partials);

@@ -77,6 +77,9 @@ struct amg_hier {
    std::vector<amgk::GeoT> gl;
    std::vector<double *> d_geo_w;
    bool geo0 = false;
+   // psw[l]: level l's prolongation + correction runs fused into its first
+   // post-smoothing sweep (geometric P_l, 7-pt marched A_l of the same box)
+   std::vector<char> psw;
    std::vector<void *> allocs;
    // profiling
    std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[PROF_NCAT];
@@ -277,6 +280,7 @@ static int detect_geo(amg_hier *H)
    H->gl.assign(H->L, amgk::GeoT{});
    H->d_geo_w.assign(H->L, nullptr);
    H->geo0 = false;
+   H->psw.assign(H->L, 0);
    if (H->L < 2 || !H->ctx->fuse_transfer) return AMG_OK;
    const amg_mat *A = H->lv[0].A;
    if (!A->mz_P || A->mz_P % A->mz_S) return AMG_OK;
@@ -291,7 +295,13 @@ static int detect_geo(amg_hier *H)
       nz /= 2;
    }
    const amgk::GeoT &g = H->gl[0];
-   H->geo0 = H->geo[0] && g.nx >= 64 && g.nx <= 512 && 512 % g.nx == 0 && (g.ny / 2) % (512 / g.nx) == 0;
+   for (int l = 0; l < H->L - 1; l++) {
+      const amg_mat *Al = H->lv[l].A;
+      const amgk::GeoT &gg = H->gl[l];
+      H->psw[l] = H->geo[l] && H->ctx->fuse_prolong && Al->mz_P && !Al->mz27 && Al->mz_S == gg.nx &&
+                  (long long)Al->mz_P == (long long)gg.nx * gg.ny && Al->nrows / Al->mz_P == gg.nz;
+   }
+   H->geo0 = H->geo[0] && !A->mz27 && g.nx >= 64 && g.nx <= 512 && 512 % g.nx == 0 && (g.ny / 2) % (512 / g.nx) == 0;
    return AMG_OK;
 }
 
@@ -301,6 +311,15 @@ extern "C" int amg_hier_fused(const amg_hier *H)
    int m = H->geo0 ? 1 : 0;
    for (int l = 0; l < H->L; l++)
       if (H->geo[l]) m |= 2 << l;
+   return m;
+}
+
+extern "C" int amg_hier_fused_prolong(const amg_hier *H)
+{
+   if (!H) return 0;
+   int m = 0;
+   for (int l = 0; l < (int)H->psw.size(); l++)
+      if (H->psw[l]) m |= 1 << l;
    return m;
 }
 
@@ -574,6 +593,20 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
    for (int l = L - 2; l >= 0; l--) {
       Level &v = H->lv[l];
       v.zero_flag = 0;
+      const double *f_fine = (l == 0 && precond) ? H->r0 : v.f;
+      const bool l1 = o.smoother == AMG_L1_JACOBI;
+      if (H->psw[l] && o.num_post_smooth_sweeps >= 1 && (l1 || o.smoother == AMG_JACOBI)) {
+         // u += P e fused into the first post sweep (the corrected u is never
+         // stored; the sweep's output is the same bits)
+         {
+            ProfScope ps(H, PROF_FINE_SMOOTH, s, l == 0);
+            amgk::mz_prolong_sweep(s, v.A, f_fine, v.u, H->lv[l + 1].u, H->gl[l], H->d_geo_w[l],
+                                   l1 ? v.l1 : nullptr, o.smooth_weight, v.u_alt);
+         }
+         std::swap(v.u, v.u_alt);
+         smooth_one_level(H, s, l, f_fine, o.num_post_smooth_sweeps - 1, false);
+         continue;
+      }
       {
          ProfScope ps(H, PROF_PROLONG0, s, l == 0);
          if (H->geo[l])
@@ -581,7 +614,6 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
          else
             amgk::spgemv(s, v.P, H->lv[l + 1].u, v.u, pro_mode, v.u, 0, v.n, nullptr);
       }
-      const double *f_fine = (l == 0 && precond) ? H->r0 : v.f;
       smooth_one_level(H, s, l, f_fine, o.num_post_smooth_sweeps, false);
    }
 }

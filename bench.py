@@ -78,19 +78,26 @@ def load_traffic(n, kernel):
         return None
 
 
-def fine_kernels(n0, mat_bytes, ms, launches, fused, fmt):
+def fine_kernels(n0, mat_bytes, ms, launches, fused, fmt, fused_prolong=0):
     """Per-launch time (HIP events on the compute stream inside the timed loop)
     and algorithmic bytes of each fine-level kernel of a step.
     Profile categories: 0 level-0 residual (fused with R0 when fused & 1),
-    1 post-smoothing sweep, 2 R0, 3 P0 prolongation + correction, 4 outer
-    residual + norm (fused with the next cycle's first sweep)."""
+    1 post-smoothing sweep (fused with P0 when fused_prolong & 1), 2 R0, 3 P0
+    prolongation + correction, 4 outer residual + norm (fused with the next
+    cycle's first sweep)."""
     def per(c):
         return ms[c] / launches[c] if launches[c] else None
     out = {}
     out["outer_residual_sweep"] = (per(4), mat_bytes + 24 * n0,
                                    "outer residual r = f - A0 u + norm partials, fused with the next "
                                    f"cycle's first Jacobi sweep (reads f, u; writes u_next; {fmt})")
-    out["post_sweep"] = (per(1), mat_bytes + 24 * n0, f"post-smoothing Jacobi sweep (reads f, u; writes u_next; {fmt})")
+    if fused_prolong & 1:
+        out["prolong_sweep"] = (per(1), mat_bytes + 24 * n0 + 8 * (n0 // 8),
+                                "geometric prolongation u + P0 e fused into the post-smoothing Jacobi sweep "
+                                f"(reads f, u, e; writes u_next; {fmt})")
+    else:
+        out["post_sweep"] = (per(1), mat_bytes + 24 * n0,
+                             f"post-smoothing Jacobi sweep (reads f, u; writes u_next; {fmt})")
     if fused & 1:
         out["residual_restrict"] = (per(0), mat_bytes + 16 * n0 + 8 * (n0 // 8),
                                     "level-0 residual fused with the geometric restriction "
@@ -98,7 +105,9 @@ def fine_kernels(n0, mat_bytes, ms, launches, fused, fmt):
     else:
         out["residual"] = (per(0), mat_bytes + 24 * n0, f"level-0 residual ({fmt})")
         out["restrict0"] = (per(2), None, "R0 restriction")
-    if fused & 2:
+    if fused_prolong & 1:
+        pass
+    elif fused & 2:
         out["prolong0"] = (per(3), 16 * n0 + 8 * (n0 // 8),
                            "geometric prolongation + correction u += P0 e (reads u, e; writes u)")
     else:
@@ -233,8 +242,9 @@ def main():
     mat_bytes, fmt = storage(n0, z0, As[0].value_index, As[0].dict_index, As[0].row_pattern,
                              As[0].pair_pattern, As[0].master_pattern)
     fused = H.fused
+    fused_prolong = H.fused_prolong
     plane_march = As[0].plane_march
-    kernels = fine_kernels(n0, mat_bytes, ms, launches, fused, fmt)
+    kernels = fine_kernels(n0, mat_bytes, ms, launches, fused, fmt, fused_prolong)
     # fine-grid SpMV y = A x (matrix + x + y), events on the same stream
     x = ctx.vec(n0)
     x.set(1.0)
@@ -316,7 +326,9 @@ def main():
                                f"{L}-level geometric Galerkin hierarchy, outer residual + norm per step",
                    "n": n, "levels": L, "nnz_A0": z0, "rows": n0,
                    "reuse_outer_residual": args.reuse_outer_residual,
-                   "matrix_format": fmt, "plane_march": plane_march, "geometric_transfers": fused,
+                   "matrix_format": fmt, "plane_march": plane_march,
+                   "march_points": [A.march_points for A in As], "geometric_transfers": fused,
+                   "fused_prolong_sweep": fused_prolong,
                    "parallelism": "single GPU"},
         "fine_spmv": {"gbs": spmv_gbs, "ms": spmv_ms.value, "bytes": spmv_bytes,
                       "frac": spmv_gbs / HBM_PEAK_GBS, "format": fmt},

@@ -188,9 +188,15 @@ int amg_mat_master_pattern(const amg_mat *A);
  * while a workgroup marches through zc planes.  Bit-identical to every other
  * form.  enable applies to matrices registered afterwards; zc (1..64, 0 keeps)
  * and xcd (XCD-contiguous workgroup order, -1 keeps) apply to later launches.
- * amg_mat_plane_march: the plane size P (0: not marched). */
+ * The 27-point form (master list [0, then dz P + dy S + dx ascending]: the
+ * Galerkin coarse operators R A P of the box hierarchy, SMEM_MatVec.cpp:140-258
+ * on them) marches the same way with lines y - 1, y, y + 1 of three planes in
+ * registers.
+ * amg_mat_plane_march: the plane size P (0: not marched);
+ * amg_mat_march_points: the marched stencil, 7 or 27 (0: not marched). */
 int amg_set_plane_march(amg_ctx *ctx, int enable, int zc, int xcd);
 int amg_mat_plane_march(const amg_mat *A);
+int amg_mat_march_points(const amg_mat *A);
 int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz);
 int amg_mat_download(amg_ctx *ctx, const amg_mat *A, int *rowptr, int *col, double *val);
 
@@ -286,6 +292,17 @@ int amg_hier_free(amg_hier *H);
  * for hierarchies created afterwards. */
 int amg_hier_fused(const amg_hier *H);
 int amg_set_fuse_transfer(amg_ctx *ctx, int enable);
+/* Prolongation fused into the post-smoothing sweep: bit l set when level l's
+ * up-phase runs SMEM_Sync_SpGEMV(P_l, e, u, 1, 1, u) and the first Jacobi /
+ * L1 Jacobi post sweep (SMEM_Sync_AMG.cpp:118-134, SMEM_Smooth.cpp:35-45,
+ * 122-130) as one plane-marching pass that forms u + P e in registers (level
+ * l geometric and its A_l 7-pt marched).  Bit-identical to the two kernels.
+ * Off by default (measured 1.79 ms against 0.48 + 0.65 ms for the two kernels
+ * at 512^3: the register-formed operands make it VALU-bound);
+ * amg_set_fuse_prolong(ctx, 1) (env AMG_FUSE_PROLONG=1) turns it on for
+ * hierarchies created afterwards. */
+int amg_hier_fused_prolong(const amg_hier *H);
+int amg_set_fuse_prolong(amg_ctx *ctx, int enable);
 int amg_hier_set_opts(amg_hier *H, const amg_opts *opts);
 /* override level `level`'s hybrid-JGS block partition (thread.A_ns/A_ne) */
 int amg_hier_set_blocks(amg_hier *H, int level, const int *blk, int nblk);

@@ -107,7 +107,7 @@ def test_plane_march_bitwise(ctx, amg, boxes, name, zc, xcd):
         for M in (mz, mp, pl):
             M.free()
     finally:
-        ctx.set_plane_march(1, 16, 1)
+        ctx.set_plane_march(1, -1, 1)
 
 
 @pytest.mark.parametrize("zc", [32, 5])
@@ -142,7 +142,7 @@ def test_plane_march_solve(ctx, amg, oracle, smoother, zc):
                 for M in v:
                     M.free()
     finally:
-        ctx.set_plane_march(1, 16, 1)
+        ctx.set_plane_march(1, -1, 1)
     OH = po.Hier(host["A"], host["P"], host["R"],
                  po.make_opts(smooth_weight=0.8, num_cycles=12, smoother=sm))
     u_cpu, hist_cpu, _ = OH.solve(f)
@@ -170,7 +170,7 @@ def _hier_solve(ctx, amg, host, f, cycles, march, fuse, sm=0, zc=16):
             for M in v:
                 M.free()
     finally:
-        ctx.set_plane_march(1, 16, 1)
+        ctx.set_plane_march(1, -1, 1)
         ctx.set_fuse_transfer(1)
     return fused, out
 
@@ -244,3 +244,174 @@ def test_fused_transfer_detection(ctx, amg, oracle):
 
     assert hier(amg.Gen(64, interp=amg.AMG_INTERP_LINEAR), bump_r) == 0
     assert hier(amg.Gen(64, interp=amg.AMG_INTERP_LINEAR), move_p) == 0
+
+
+def box_27pt(oracle, nx, ny, nz, per_pattern=True):
+    """27-pt operator on an nx*ny*nz box, diagonal-first rows, the other entries
+    ascending (the Galerkin coarse operators' CSR order).  per_pattern: the
+    off-diagonal weights depend on (dz, dy, dx) and the row's boundary class
+    (27 pair patterns, per-pattern values); else the uniform 26 / -1 stencil."""
+    n = nx * ny * nz
+    idx = np.arange(n)
+    x, y, z = idx % nx, (idx // nx) % ny, idx // (nx * ny)
+    cls = ((x == 0) | (x == nx - 1)).astype(int) + 2 * ((y == 0) | (y == ny - 1)) + 4 * ((z == 0) | (z == nz - 1))
+    rows, cols, vals = [idx], [idx], [np.full(n, 26.0)]
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                if dz == dy == dx == 0:
+                    continue
+                ok = (x + dx >= 0) & (x + dx < nx) & (y + dy >= 0) & (y + dy < ny) & (z + dz >= 0) & (z + dz < nz)
+                w = -1.0 if not per_pattern else -(1.0 + 0.125 * abs(dz) + 0.25 * abs(dy) + 0.0625 * dx) * (1.0 + 0.5 * cls)
+                w = np.broadcast_to(w, (n,))
+                rows.append(idx[ok])
+                cols.append((idx + dz * nx * ny + dy * nx + dx)[ok])
+                vals.append(np.asarray(w)[ok])
+    r = np.concatenate(rows)
+    c = np.concatenate(cols)
+    v = np.concatenate(vals)
+    # diagonal first, then ascending columns
+    key = np.where(c == r, -1, c)
+    order = np.lexsort((key, r))
+    r, c, v = r[order], c[order], v[order]
+    rowptr = np.zeros(n + 1, dtype=np.int32)
+    np.add.at(rowptr, r + 1, 1)
+    rowptr = np.cumsum(rowptr).astype(np.int32)
+    return oracle.Csr(n, n, rowptr, c.astype(np.int32), v.astype(np.float64))
+
+
+@pytest.fixture(scope="module")
+def boxes27(oracle, amg):
+    from oracle import pyoracle as po
+    g = amg.Gen(64, interp=amg.AMG_INTERP_LINEAR)
+    return {
+        "galerkin32": po.Csr(*g.host_csr(amg.AMG_GEN_A, 1)),  # R A P of the 64^3 Laplacian
+        "pat32x16x5": box_27pt(oracle, 32, 16, 5),
+        "uni64x8x4": box_27pt(oracle, 64, 8, 4, per_pattern=False),
+        "pat256x2x3": box_27pt(oracle, 256, 2, 3),
+    }
+
+
+def test_plane_march27_selection(ctx, oracle, boxes27):
+    want = {"galerkin32": 1024, "pat32x16x5": 512, "uni64x8x4": 512, "pat256x2x3": 0}
+    # below the pair-coding size (4M rows) a 27-pt operator keeps the pair /
+    # master forms only when it marches; otherwise the row-pattern form
+    for name, A in boxes27.items():
+        M = register(ctx, A)
+        assert abs(M.master_pattern) == (27 if want[name] else 0), (name, M.master_pattern)
+        assert M.plane_march == want[name], (name, M.plane_march)
+        assert M.march_points == (27 if want[name] else 0), name
+        M.free()
+    # planes of 256 rows: not marched
+    M = register(ctx, box_27pt(oracle, 16, 16, 4))
+    assert M.master_pattern == 0 and M.plane_march == 0 and M.row_pattern > 0
+    M.free()
+    # forced pair coding (pair_pattern 2): the master kernel
+    ctx.set_pair_pattern(2)
+    try:
+        M = register(ctx, box_27pt(oracle, 16, 16, 4))
+        assert abs(M.master_pattern) == 27 and M.plane_march == 0
+        M.free()
+    finally:
+        ctx.set_pair_pattern(1)
+
+
+@pytest.mark.parametrize("zc,xcd", [(16, 1), (1, 0), (3, 1), (64, 0)])
+@pytest.mark.parametrize("name", ["galerkin32", "pat32x16x5", "uni64x8x4"])
+def test_plane_march27_bitwise(ctx, amg, oracle, boxes27, name, zc, xcd):
+    """csr_mz27_kernel: SpGEMV in every (alpha, beta) branch, Jacobi sweeps
+    (zero-guess and not), bit-identical to plain CSR and the master kernel."""
+    A = boxes27[name]
+    ctx.set_plane_march(1, zc, xcd)
+    try:
+        mz = register(ctx, A)
+        ctx.set_pair_pattern(2)
+        try:
+            mp = register(ctx, A, march=0)
+        finally:
+            ctx.set_pair_pattern(1)
+        pl = register(ctx, A, plain=True)
+        assert mz.march_points == 27 and mp.plane_march == 0 and abs(mp.master_pattern) == 27
+        assert pl.value_index == 0
+        n = A.nrows
+        l1 = ctx.vec(oracle.l1_norms(A))
+        x = ctx.vec(_vecs(n, 51))
+        b = ctx.vec(_vecs(n, 52))
+        outs = {}
+        for tag, M in (("plain", pl), ("master", mp), ("march", mz)):
+            o = []
+            for ab in ((1.0, 0.0), (-1.0, 1.0), (1.0, 1.0), (2.5, -0.5), (-1.0, 0.7)):
+                y = ctx.vec(n)
+                amg.smem.SMEM_SpGEMV(ctx, M, x, b, ab[0], ab[1], y, 0, n)
+                o.append(y.download())
+            u = ctx.vec(_vecs(n, 54))
+            amg.smem.SMEM_Sync_Parfor_Jacobi(ctx, M, b, u, ctx.vec(n), 3, 0, 0.7)
+            o.append(u.download())
+            u = ctx.vec(_vecs(n, 55))
+            amg.smem.SMEM_Sync_Parfor_L1Jacobi(ctx, M, b, u, ctx.vec(n), l1, 2, 0)
+            o.append(u.download())
+            outs[tag] = o
+        for tag in ("master", "march"):
+            for k, (g, r) in enumerate(zip(outs[tag], outs["plain"])):
+                assert_bitwise(g, r, f"{name} zc={zc} {tag} output {k}")
+        for M in (mz, mp, pl):
+            M.free()
+    finally:
+        ctx.set_plane_march(1, -1, 1)
+
+
+def test_plane_march27_hierarchy(ctx, amg):
+    """The 64^3 linear-interpolation hierarchy marches its level-1 Galerkin
+    operator with the 27-point kernel (test_plane_march_solve checks the solve
+    bit for bit against the oracle with every level's kernels)."""
+    g = amg.Gen(64, interp=amg.AMG_INTERP_LINEAR)
+    A0 = g.register(ctx, amg.AMG_GEN_A, 0)
+    A1 = g.register(ctx, amg.AMG_GEN_A, 1)
+    assert A0.march_points == 7 and A1.march_points == 27
+    A0.free()
+    A1.free()
+
+
+@pytest.mark.parametrize("dims,zc,sm,post", [((64, 64, 64), 16, "jacobi", 1), ((512, 8, 6), 4, "l1", 1),
+                                             ((128, 16, 10), 3, "jacobi", 2), ((64, 32, 14), 64, "l1", 2),
+                                             ((256, 12, 8), 2, "jacobi", 1)])
+def test_fused_prolong_sweep(ctx, amg, oracle, dims, zc, sm, post):
+    """Prolongation + correction fused into the first post-smoothing sweep
+    (mz_prolong_sweep_kernel, SMEM_Sync_AMG.cpp:118-134): iterate and norm
+    history bit-identical to the unfused run (geo_prolong_k + csr_mz_kernel)
+    and the iterate to the oracle after 6 cycles; Jacobi and L1 Jacobi, one
+    and two post sweeps, chunk lengths 2..64, lines of 64..512."""
+    from oracle import pyoracle as po
+    g = amg.Gen(*dims, interp=amg.AMG_INTERP_LINEAR)
+    host = {w: [po.Csr(*g.host_csr(c, l)) for l in range(cnt)]
+            for w, c, cnt in (("A", amg.AMG_GEN_A, g.L), ("P", amg.AMG_GEN_P, g.L - 1),
+                              ("R", amg.AMG_GEN_R, g.L - 1))}
+    n = dims[0] * dims[1] * dims[2]
+    f = amg.rhs_rand(0, n)
+    smoother = amg.AMG_JACOBI if sm == "jacobi" else amg.AMG_L1_JACOBI
+    res = {}
+    ctx.set_plane_march(1, zc, 1)
+    try:
+        for fp in (1, 0):
+            ctx.set_fuse_prolong(fp)
+            dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v] for k, v in host.items()}
+            opts = amg.default_opts(smooth_weight=0.8, num_cycles=6, tol=0.0, reuse_outer_residual=2,
+                                    smoother=smoother, num_post_smooth_sweeps=post)
+            H = amg.Hier(ctx, dev["A"], dev["P"], dev["R"], opts)
+            res[fp] = (H.fused_prolong, H.solve(f))
+            H.free()
+            for v in dev.values():
+                for M in v:
+                    M.free()
+    finally:
+        ctx.set_plane_march(1, -1, 1)
+        ctx.set_fuse_prolong(1)
+    (fp1, (u1, h1, k1)), (fp0, (u0, h0, k0)) = res[1], res[0]
+    assert fp1 & 1 and fp0 == 0, (fp1, fp0)
+    OH = po.Hier(host["A"], host["P"], host["R"],
+                 po.make_opts(smooth_weight=0.8, num_cycles=6, smoother=smoother, num_post=post))
+    u_cpu, hist_cpu, _ = OH.solve(f)
+    assert_bitwise(u1, u0, "fused vs unfused iterate")
+    assert_bitwise(u1, u_cpu, "fused vs oracle iterate")
+    assert_bitwise(h1[:k1 + 1], h0[:k0 + 1], "norm history")
+    np.testing.assert_allclose(h1[:k1 + 1], hist_cpu[:k1 + 1], rtol=1e-12)
