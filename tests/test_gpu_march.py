@@ -405,7 +405,7 @@ def test_fused_prolong_sweep(ctx, amg, oracle, dims, zc, sm, post):
                     M.free()
     finally:
         ctx.set_plane_march(1, -1, 1)
-        ctx.set_fuse_prolong(1)
+        ctx.set_fuse_prolong(0)
     (fp1, (u1, h1, k1)), (fp0, (u0, h0, k0)) = res[1], res[0]
     assert fp1 & 1 and fp0 == 0, (fp1, fp0)
     OH = po.Hier(host["A"], host["P"], host["R"],
