@@ -350,3 +350,4 @@ def build_hierarchy(ctx, gen, opts, levels=None):
 from . import smem  # noqa: E402,F401  (reference-named kernel mirror)
 from . import dist  # noqa: E402,F401  (multi-GPU solve phase)
 from . import classical  # noqa: E402,F401  (in-house BoomerAMG-style setup)
+from . import io  # noqa: E402,F401  (binary triplet matrix files)

@@ -184,6 +184,19 @@ class AmgCsrPart(C.Structure):
     _fields_ = [("nrows", _i), ("nnz", _ll), ("rowptr", _ip), ("col", _ip), ("val", _dp)]
 
 
+class AmgHostCsr(C.Structure):
+    _fields_ = [("nrows", _i), ("ncols", _i), ("nnz", _ll), ("rowptr", _ip), ("col", _ip), ("val", _dp)]
+
+
+PROTOTYPES.update({
+    "amg_triplet_read": (_i, [C.c_char_p, _i, _i, C.POINTER(AmgHostCsr)]),
+    "amg_triplet_read_part": (_i, [C.c_char_p, _i, _ip, C.POINTER(AmgHostCsr)]),
+    "amg_triplet_write": (_i, [C.c_char_p, _i, _i, _ip, _ip, _dp, _i]),
+    "amg_triplet_text_to_bin": (_i, [C.c_char_p, C.c_char_p]),
+    "amg_host_csr_free": (None, [C.POINTER(AmgHostCsr)]),
+})
+
+
 # amg_host_xchg_fn: (user, op, npeers, peers, send, send_bytes, recv, recv_bytes) -> int
 HOST_XCHG_FN = C.CFUNCTYPE(_i, _p, _i, _i, _ip, _pp, _llp, _pp, _llp)
 

@@ -493,6 +493,32 @@ int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, int sweeps, i
  * split); *ms = average device milliseconds over reps */
 int amg_dist_fine_spmv(amg_dist_hier *D, int reps, double *ms);
 
+/* ---- binary triplet matrix files (-problem file) ------------------------------ */
+/* records {int32 i, int32 j, double val} (Triplet_AOS, Main.hpp:433-437), 1-based;
+ * record 0 is the header (i = number of rows).  Rows come back assembled the way
+ * hypre's IJ interface assembles them (a repeated column keeps its first position
+ * and its last value; the diagonal first).  Host arrays owned by the caller:
+ * release them with amg_host_csr_free. */
+typedef struct amg_host_csr {
+   int nrows, ncols;
+   long long nnz;
+   int *rowptr;
+   int *col;
+   double *val;
+} amg_host_csr;
+/* ReadBinary_fread_HypreParCSR (Misc.cpp:800-915; SMEM_Setup.cpp:1645-1653 reads
+ * with symm = 1, remove_disconnected = 0): symm mirrors every off-diagonal record */
+int amg_triplet_read(const char *path, int symm, int remove_disconnected, amg_host_csr *out);
+/* ParReadBinary_fread (DMEM_BuildMatrix.cpp:1488-1560): a rank's file of its own rows
+ * (zero values skipped); *first_row = the first global row (0-based) */
+int amg_triplet_read_part(const char *path, int ncols, int *first_row, amg_host_csr *out);
+/* PrintCSRMatrix (Misc.cpp:753-797): header, then (row, col, value) per entry */
+int amg_triplet_write(const char *path, int nrows, int ncols, const int *rowptr, const int *col,
+                      const double *val, int binary);
+/* TextToBin (TextToBin.cpp:5-39): "row col value" lines to binary records */
+int amg_triplet_text_to_bin(const char *in_path, const char *out_path);
+void amg_host_csr_free(amg_host_csr *M);
+
 #ifdef __cplusplus
 }
 #endif

@@ -100,3 +100,30 @@ def test_elasticity_solve_matches_oracle(amg, oracle, ctx, r, ct):
     M = ctx.csr(*lv["A"][0])
     assert M.value_index > 0 and M.dict_index == 0
     M.free()
+
+
+def test_problem_file(amg, oracle, ctx, tmp_path):
+    """-problem file (SMEM_Setup.cpp:1645-1653): a binary triplet file holding
+    the lower triangle of an anisotropic 7-pt operator, read with symm = 1
+    (ReadBinary_fread_HypreParCSR, Misc.cpp:800-915), classical setup on it and
+    the GPU solve bit-identical to the oracle on the same hierarchy."""
+    from test_io import lower_triangle_entries, records
+    A = oracle.laplace_7pt(14, 12, 10)
+    val = A.val.copy()
+    rows = np.repeat(np.arange(A.nrows), np.diff(A.rowptr))
+    val[np.abs(A.col.astype(np.int64) - rows) == 14] = -0.5  # y-couplings weaker
+    first = A.rowptr[:-1]
+    val[first] = 0.0
+    val[first] = -np.add.reduceat(val, first) + 0.25
+    A = oracle.Csr(A.nrows, A.ncols, A.rowptr, A.col, val)
+    p = tmp_path / "aniso.bin"
+    records(A.nrows, lower_triangle_entries(A)).tofile(p)
+    n, m, rowptr, col, v = amg.io.read(p, symm=1)
+    assert n == m == A.nrows and rowptr[-1] == A.rowptr[-1]
+    H = amg.classical.ClassicalAMG(n, rowptr, col, v, coarsen_type=10, strong_threshold=0.25)
+    lv = host_levels(amg, H)
+    host = {k: [oracle.Csr(*mm) for mm in vv] for k, vv in lv.items()}
+    opts = amg.default_opts(smooth_weight=0.8, num_cycles=10, tol=0.0)
+    f = amg.rhs_rand(0, n)
+    u, hist = compare_solve(amg, oracle, ctx, host, opts, f)
+    assert hist[-1] < 1e-2 * hist[0]
