@@ -49,7 +49,12 @@ class AmgOpts(C.Structure):
                 ("cheby_delta", _d), ("num_threads", _i), ("jgs_block_rows", _i),
                 ("reuse_outer_residual", _i), ("async_type", _i), ("profile", _i),
                 ("accel_type", _i), ("cheby_grid", _i), ("res_compute_type", _i),
-                ("read_type", _i), ("converge_test_type", _i)]
+                ("read_type", _i), ("converge_test_type", _i),
+                ("delay_type", _i), ("delay_usec", _i), ("delay_frac", _d), ("fail_iter", _i),
+                ("delay_rank", _i)]
+
+
+AMG_DELAY_NONE, AMG_DELAY_ONE, AMG_DELAY_SOME, AMG_DELAY_ALL, AMG_FAIL_ONE = 0, 1, 2, 3, 4
 
 
 class AmgClassicalOpts(C.Structure):

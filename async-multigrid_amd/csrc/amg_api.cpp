@@ -47,6 +47,11 @@ extern "C" void amg_opts_default(amg_opts *o)
    o->profile = 0;
    o->accel_type = AMG_NO_ACCEL; // DMEM_Main.cpp:130
    o->cheby_grid = 0;            // DMEM_Main.cpp:142
+   o->delay_type = AMG_DELAY_NONE; // SMEM_Main.cpp:98-101
+   o->delay_usec = 0;
+   o->delay_frac = 0.0;
+   o->fail_iter = 0;
+   o->delay_rank = -1; // DMEM_DelayProc: every rank (DMEM_Misc.cpp:670-676)
 }
 
 // ---------------------------------------------------------------------------
@@ -73,6 +78,8 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    AMG_HIP(hipHostMalloc(&c->h_pinned, 1024 * sizeof(double)));
    hipDeviceProp_t prop;
    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+   if (hipDeviceGetAttribute(&c->wall_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || c->wall_khz <= 0)
+      c->wall_khz = 100000; // gfx9 s_memrealtime: 100 MHz
    if (const char *v = std::getenv("AMG_VALUE_INDEX")) c->value_index = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_DICT_INDEX")) c->dict_index = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_ROW_PATTERN")) c->row_pattern = std::atoi(v) != 0;

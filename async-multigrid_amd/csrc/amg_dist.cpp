@@ -1094,11 +1094,23 @@ extern "C" int amg_dist_solve_start(amg_dist_hier *D, const double *f_local, dou
    return AMG_OK;
 }
 
+// DMEM_DelayProc (DMEM_Misc.cpp:668-684): before every cycle the rank waits
+// delay_usec (every rank; delay_rank >= 0: that rank only, the commented-out
+// delay_id test) -- here a wait on the stream the cycle runs on
+void amgd::dist_delay(amg_dist_hier *D, hipStream_t s)
+{
+   const amg_opts &o = D->o;
+   if (o.delay_type == AMG_DELAY_NONE || o.delay_usec <= 0) return;
+   if (o.delay_rank >= 0 && o.delay_rank != D->ctx->xport->rank) return;
+   amgk::delay(s, (double)o.delay_usec, D->ctx->wall_khz);
+}
+
 extern "C" int amg_dist_solve_iterate(amg_dist_hier *D, int k)
 {
    AMG_ARG(D && D->have_state, "amg_dist_solve_iterate: call amg_dist_solve_start first");
    const bool accel = dist_mult_accel(D);
    for (int i = 0; i < k; i++) {
+      dist_delay(D, D->ctx->stream); // DMEM_Mult.cpp:40
       if (accel) {
          // DMEM_Mult.cpp:40-55: e = 0; e = M r; x += e; ChebyUpdate(d, e); x += d
          DLevel &v = D->lv[0];

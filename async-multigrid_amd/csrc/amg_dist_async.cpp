@@ -325,8 +325,10 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    // issue order cycle-major / level-minor: every rank enqueues the same
    // sequence of RCCL operations on the one comm stream; the GPU runs the
    // level streams' compute freely
-   for (int cyc = 0; cyc < D->o.num_cycles; cyc++)
+   for (int cyc = 0; cyc < D->o.num_cycles; cyc++) {
+      for (int k = 0; k < active; k++) dist_delay(D, D->al[k].s); // DMEM_Add.cpp:106
       for (int k = 0; k < active; k++) AMG_TRY(level_correction(D, k));
+   }
    for (int k = 0; k < active; k++) {
       AMG_HIP(hipEventRecord(ready, D->al[k].s));
       AMG_HIP(hipStreamWaitEvent(c->stream, ready, 0));

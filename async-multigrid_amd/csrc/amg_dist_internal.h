@@ -157,4 +157,6 @@ int dist_outer_residual(amg_dist_hier *D, int slot);
 // the level-0 iterate: x_acc for accelerated MULT (DMEM_Mult), else lv[0].u
 bool dist_mult_accel(const amg_dist_hier *D);
 double *dist_iterate(amg_dist_hier *D);
+// DMEM_DelayProc: the injected per-cycle wait of this rank on stream s
+void dist_delay(amg_dist_hier *D, hipStream_t s);
 } // namespace amgd

@@ -85,6 +85,7 @@ struct amg_ctx {
    double *d_scalars = nullptr;            // device scalars (norms, dots)
    double *h_pinned = nullptr;             // pinned host mirror of scalars
    int num_cus = 256;
+   int wall_khz = 100000;  // device wall clock (wall_clock64) rate, for injected delays
    int value_index = 1; // build value-indexed CSR for matrices with <= 256 distinct values
    int dict_index = 1;  // build dictionary-coded CSR for stencil-like square operators
    int row_pattern = 1; // build row-pattern-coded CSR on top of the dictionary
@@ -253,6 +254,8 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
 void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc);
 // u += P e for the checked geometric P of GeoT g (bit-identical to the SpGEMV)
 void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u);
+// the stream waits usec microseconds (device wall clock at wall_khz)
+void delay(hipStream_t s, double usec, int wall_khz);
 // u_out = first Jacobi (l1 == nullptr) / L1 Jacobi sweep of A on uc = u + P e,
 // P the checked geometric transfer of marched 7-pt level A (uc never stored)
 void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const double *u, const double *ec,

@@ -2732,6 +2732,23 @@ static inline int ew_blocks(int n)
         i += gridDim.x * blockDim.x)
 
 // SMEM_Smooth.cpp:25-29 / SEQ_Smooth.cpp:24-29 / SMEM_Smooth.cpp:114-116 / SEQ_Smooth.cpp:67-72
+// Injected delay (SMEM_Solve.cpp:137-145 usleep, DMEM_DelayProc
+// DMEM_Misc.cpp:668-684) as a wait on the stream: one lane polls the device
+// wall clock (bounded: every launch ends after `ticks`)
+__global__ void delay_k(unsigned long long ticks)
+{
+   if (threadIdx.x != 0) return;
+   const unsigned long long t0 = wall_clock64();
+   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+
+void delay(hipStream_t s, double usec, int wall_khz)
+{
+   if (!(usec > 0.0)) return;
+   usec = std::min(usec, 1e7); // at most 10 s per delay
+   delay_k<<<1, 64, 0, s>>>((unsigned long long)(usec * 1e-3 * wall_khz));
+}
+
 __global__ void jacobi_zero_k(const double *__restrict__ diag, const double *__restrict__ f,
                               const double *__restrict__ l1, double omega, double *__restrict__ u,
                               int rb, int re, int variant)

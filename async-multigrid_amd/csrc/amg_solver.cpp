@@ -80,6 +80,9 @@ struct amg_hier {
    // psw[l]: level l's prolongation + correction runs fused into its first
    // post-smoothing sweep (geometric P_l, 7-pt marched A_l of the same box)
    std::vector<char> psw;
+   // delay / fault injection: one generator per reference thread (srand(tid),
+   // SMEM_Solve.cpp:113), reset by every solve
+   std::vector<unsigned long long> delay_rng;
    std::vector<void *> allocs;
    // profiling
    std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[PROF_NCAT];
@@ -778,6 +781,57 @@ static void init_vectors(amg_hier *H)
    }
 }
 
+// ---- delay / fault injection (SMEM_Solve.cpp:33-43, 112-146) ------------------
+// threads T-1 (DELAY_ONE / FAIL_ONE) or the last ceil(T delay_frac) (DELAY_SOME,
+// DELAY_ALL: frac 1) sleep; in cycle k a sleeping thread sleeps RandDouble(0,
+// 2 delay_usec) microseconds (the per-thread usec_vec draw of :41 is
+// overwritten at :139 and never used).  rand() after srand(tid) is shared,
+// unsynchronised glibc state in the reference; here every thread has its own
+// splitmix64 stream seeded with its id -- the delays only move time.
+static int delay_threads(const amg_opts &o)
+{
+   return std::max(1, o.num_threads);
+}
+
+static bool thread_sleeps(const amg_opts &o, int t, int k)
+{
+   const int T = delay_threads(o);
+   switch (o.delay_type) {
+   case AMG_DELAY_ONE: return t == T - 1;
+   case AMG_FAIL_ONE: return t == T - 1 && k == o.fail_iter;
+   case AMG_DELAY_SOME: return t >= T - (int)std::ceil((double)T * o.delay_frac);
+   case AMG_DELAY_ALL: return true;
+   default: return false;
+   }
+}
+
+static double rand_double(unsigned long long &st, double lo, double hi)
+{
+   unsigned long long z = (st += 0x9E3779B97F4A7C15ULL);
+   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+   z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+   z ^= z >> 31;
+   return lo + (hi - lo) * (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// the longest sleep of threads [t0, t1) in cycle k (0: none sleeps)
+static double delay_usec(amg_hier *H, int t0, int t1, int k)
+{
+   const amg_opts &o = H->o;
+   if (o.delay_type == AMG_DELAY_NONE || o.delay_usec <= 0) return 0.0;
+   double d = 0.0;
+   for (int t = t0; t < t1; t++)
+      if (thread_sleeps(o, t, k)) d = std::max(d, (double)(int)rand_double(H->delay_rng[t], 0.0, 2.0 * o.delay_usec));
+   return d;
+}
+
+static void delay_reset(amg_hier *H)
+{
+   const int T = delay_threads(H->o);
+   H->delay_rng.assign(T, 0);
+   for (int t = 0; t < T; t++) H->delay_rng[t] = 0x5DEECE66DULL * (unsigned long long)(t + 1);
+}
+
 static int solve_begin(amg_hier *H, const amg_vec *f, const amg_vec *u)
 {
    amg_ctx *c = H->ctx;
@@ -793,6 +847,7 @@ static int solve_begin(amg_hier *H, const amg_vec *f, const amg_vec *u)
    H->cheby_omega = 2.0;
    H->iter = 0;
    H->have_state = true;
+   delay_reset(H);
    return AMG_OK;
 }
 
@@ -804,6 +859,8 @@ static int solve_step(amg_hier *H)
    const bool precond = o.cheby_flag == 1;
    const bool one_level = !is_all_levels(o);
    const bool reuse = reuse_applies(H);
+   // the cycle starts when its slowest thread has slept (SMEM_Solve.cpp:137-145)
+   amgk::delay(c->stream, delay_usec(H, 0, delay_threads(o), H->iter + 1), c->wall_khz);
    if (o.solver == AMG_BPX)
       bpx_cycle(H, precond); // SMEM_Solve.cpp:161-163
    else if (one_level)
@@ -1110,6 +1167,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    AMG_HIP(hipStreamWaitEvent(c->comm_stream, ready, 0));
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    hipStream_t us = c->comm_stream; // SEMI_ASYNC update stream
+   std::vector<int> issued(L, 0);
    // one correction of level k, issued on its stream
    auto correction = [&](int k) -> int {
       hipStream_t s = c->level_streams[k];
@@ -1125,6 +1183,12 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          return AMG_OK;
       };
       const int grb = v0.blk[gb[k]], gre = v0.blk[gb[k + 1]];
+      {
+         // injected delay of the threads this level group stands for
+         const int T = delay_threads(o), g = k - k_lo;
+         const int t0 = (int)((long long)T * g / ngrp), t1 = std::max(t0 + 1, (int)((long long)T * (g + 1) / ngrp));
+         amgk::delay(s, delay_usec(H, t0, std::min(t1, T), issued[k] + 1), c->wall_khz);
+      }
       if (global_res) {
          smooth_fine_slice(H, s, k, a.y_fine, gb[k], gb[k + 1]);
          if (!semi) amgk::atomic_add(s, v0.u, a.g_u, grb, gre);
@@ -1170,7 +1234,6 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       AMG_HIP(hipGetLastError());
       return AMG_OK;
    };
-   std::vector<int> issued(L, 0);
    if (!conv_global) {
       for (int cyc = 0; cyc < o.num_cycles; cyc++)
          for (int k = k_lo; k < k_hi; k++) {

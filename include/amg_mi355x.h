@@ -115,7 +115,31 @@ typedef struct {
    int converge_test_type;       /* input.converge_test_type: AMG_LOCAL (every level
                                     num_cycles corrections) / AMG_GLOBAL (levels run
                                     on until every level has done num_cycles)  */
+   /* delay / fault injection (input.delay_type, delay_usec, delay_frac, fail_iter,
+    * SMEM_Main.cpp:572-595; SMEM_Solve.cpp:33-43,112-146; DMEM_DelayProc,
+    * DMEM_Misc.cpp:668-684).  The reference's "threads" are the num_threads row
+    * partitions: thread T-1 is delayed by DELAY_ONE / FAIL_ONE, the last
+    * ceil(T * delay_frac) threads by DELAY_SOME (DELAY_ALL: all), each cycle by
+    * RandDouble(0, 2 usec_t) microseconds (usec_t = delay_usec for ONE / FAIL_ONE,
+    * RandDouble(0, delay_usec) drawn once per thread for SOME / ALL; FAIL_ONE only
+    * in cycle fail_iter).  On the GPU a delay is a device-side wait on the stream
+    * the delayed work runs on: the compute stream before a synchronous cycle (the
+    * cycle waits for its slowest thread), the level stream before a correction of
+    * an async additive level (the group owning the thread -- an extension: the
+    * reference's async loop takes no delays), the rank's stream before every
+    * distributed cycle (delay_usec exactly; delay_rank -1 = every rank, as the
+    * reference, else that rank only, its commented-out delay_id variant). */
+   int delay_type;               /* AMG_DELAY_NONE / _ONE / _SOME / _ALL / AMG_FAIL_ONE */
+   int delay_usec;               /* input.delay_usec                              */
+   double delay_frac;            /* input.delay_frac (DELAY_SOME)                 */
+   int fail_iter;                /* input.fail_iter (FAIL_ONE)                    */
+   int delay_rank;               /* distributed: -1 every rank, else that rank    */
 } amg_opts;
+#define AMG_DELAY_NONE 0
+#define AMG_DELAY_ONE 1
+#define AMG_DELAY_SOME 2
+#define AMG_DELAY_ALL 3
+#define AMG_FAIL_ONE 4
 
 void amg_opts_default(amg_opts *o); /* SMEM_Main.cpp:65-105 defaults */
 

@@ -1,0 +1,95 @@
+"""Delay / fault injection (input.delay_type, delay_usec, delay_frac, fail_iter;
+SMEM_Solve.cpp:33-43,112-146, DMEM_DelayProc DMEM_Misc.cpp:668-684): a delay
+is a device-side wait on the stream the delayed work runs on, so it moves time
+and never values -- synchronous results stay bit-identical, the wall clock
+grows by the injected waits, and an async level group that is slowed down does
+fewer corrections than the others under converge_test GLOBAL."""
+import time
+
+import numpy as np
+import pytest
+
+from test_gpu_dist import distributed
+from test_gpu_kernels import assert_bitwise
+from test_gpu_solve import gpu_hier, hierarchy
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def h24(amg, oracle):
+    _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
+    return L, host, amg.rhs_rand(0, 24 ** 3)
+
+
+def timed_solve(amg, ctx, host, f, **kw):
+    opts = amg.default_opts(smooth_weight=0.8, num_cycles=6, tol=0.0, **kw)
+    H, _ = gpu_hier(amg, ctx, host, opts)
+    H.solve(f)  # warm
+    t0 = time.perf_counter()
+    u, hist, k = H.solve(f)
+    dt = time.perf_counter() - t0
+    H.free()
+    return u, hist, dt
+
+
+@pytest.mark.parametrize("kind", ["one", "some", "all", "fail"])
+def test_sync_delay_moves_time_not_values(amg, ctx, h24, kind):
+    L, host, f = h24
+    u0, h0, t0 = timed_solve(amg, ctx, host, f)
+    dt = {"one": amg.AMG_DELAY_ONE, "some": amg.AMG_DELAY_SOME, "all": amg.AMG_DELAY_ALL,
+          "fail": amg.AMG_FAIL_ONE}[kind]
+    # 16 threads; DELAY_ALL: each cycle waits for the longest of 16 draws in
+    # [0, 40 ms) (expected 37.6 ms); ONE / FAIL_ONE: one draw (expected 20 ms)
+    u1, h1, t1 = timed_solve(amg, ctx, host, f, num_threads=16, delay_type=dt, delay_usec=20000,
+                             delay_frac=0.5, fail_iter=3)
+    assert_bitwise(u1, u0, f"delay {kind} iterate")
+    assert_bitwise(h1, h0, f"delay {kind} norm history")
+    lo = {"one": 0.010, "some": 0.10, "all": 0.15, "fail": 0.0}[kind]
+    assert t1 - t0 >= lo, (kind, t0, t1)
+    assert t1 - t0 < 6 * 0.040 + 1.0, (kind, t0, t1)
+
+
+def test_async_delayed_group_does_fewer_corrections(amg, oracle, ctx):
+    """ASYNC_MULTADD, converge_test GLOBAL: the coarsest group (thread T-1)
+    waits 3 ms before each correction; the others keep correcting meanwhile,
+    and the solve still converges."""
+    _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs = oracle.smooth_transfer(host["A"][lev], host["P"][lev], 0.8)
+        Ps.append(ps)
+        Rs.append(rs)
+    mult = {"A": host["A"], "P": Ps, "R": Rs}
+    f = amg.rhs_rand(0, 24 ** 3)
+    N = 8
+    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=N, tol=0.0,
+                            num_threads=8, converge_test_type=amg.AMG_GLOBAL, delay_type=amg.AMG_DELAY_ONE,
+                            delay_usec=3000)
+    H, _ = gpu_hier(amg, ctx, mult, opts)
+    u, rel, cnt = H.async_solve(f)
+    H.free()
+    k_hi = max(1, L - 1)
+    assert np.all(np.isfinite(u)) and rel < 1.0
+    assert cnt[k_hi - 1] >= N and np.all(cnt[:k_hi] >= N), cnt
+    assert np.max(cnt[:k_hi - 1]) > cnt[k_hi - 1], cnt  # the undelayed groups ran ahead
+
+
+@pytest.mark.parametrize("delay_rank", [-1, 1, 7])
+def test_dist_delay(amg, ctx, delay_rank):
+    """DMEM_DelayProc on the distributed MULT cycle (2 ranks over the host
+    transport): every rank (-1), one rank, or none (rank 7 absent) waits 5 ms
+    per cycle; the iterate is bit-identical in every case."""
+    gen = amg.Gen(24, interp=amg.AMG_INTERP_LINEAR)
+    f = amg.rhs_rand(0, 24 ** 3)
+    base = amg.default_opts(smooth_weight=0.8, num_cycles=4, tol=0.0)
+    u0, h0 = distributed(amg, gen, base, f, 4, 2, 0)
+    opts = amg.default_opts(smooth_weight=0.8, num_cycles=4, tol=0.0, delay_type=amg.AMG_DELAY_ALL,
+                            delay_usec=5000, delay_rank=delay_rank)
+    t0 = time.perf_counter()
+    u1, h1 = distributed(amg, gen, opts, f, 4, 2, 0)
+    dt = time.perf_counter() - t0
+    assert_bitwise(u1, u0, "delayed distributed iterate")
+    np.testing.assert_array_equal(h1, h0)
+    if delay_rank != 7:
+        assert dt >= 4 * 0.005, dt
