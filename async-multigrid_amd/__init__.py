@@ -352,3 +352,4 @@ from . import smem  # noqa: E402,F401  (reference-named kernel mirror)
 from . import dist  # noqa: E402,F401  (multi-GPU solve phase)
 from . import classical  # noqa: E402,F401  (in-house BoomerAMG-style setup)
 from . import io  # noqa: E402,F401  (binary triplet matrix files)
+from . import grid  # noqa: E402,F401  (level-grouped async additive solve)

@@ -51,7 +51,7 @@ class AmgOpts(C.Structure):
                 ("accel_type", _i), ("cheby_grid", _i), ("res_compute_type", _i),
                 ("read_type", _i), ("converge_test_type", _i),
                 ("delay_type", _i), ("delay_usec", _i), ("delay_frac", _d), ("fail_iter", _i),
-                ("delay_rank", _i)]
+                ("delay_rank", _i), ("max_inflight", _i), ("async_comm_save_divisor", _i)]
 
 
 AMG_DELAY_NONE, AMG_DELAY_ONE, AMG_DELAY_SOME, AMG_DELAY_ALL, AMG_FAIL_ONE = 0, 1, 2, 3, 4

@@ -52,6 +52,8 @@ extern "C" void amg_opts_default(amg_opts *o)
    o->delay_frac = 0.0;
    o->fail_iter = 0;
    o->delay_rank = -1; // DMEM_DelayProc: every rank (DMEM_Misc.cpp:670-676)
+   o->max_inflight = 1;            // DMEM_Main.cpp:113
+   o->async_comm_save_divisor = 1; // DMEM_Main.cpp:123
 }
 
 // ---------------------------------------------------------------------------

@@ -33,6 +33,7 @@
 // Termination: each level performs num_cycles corrections (LOCAL convergence,
 // fixed count), then the streams join and the outer residual is formed.
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "amg_dist_internal.h"
@@ -299,6 +300,133 @@ int setup_async(amg_dist_hier *D)
 }
 
 } // namespace
+
+// ---- level-grouped corrections (grid k of the DMEM add solver) ----------------
+// AddCycle (DMEM_Add.cpp:180-329, NUMLEVELS_INTERPOLANTS): the grid's residual
+// F[0] restricted level by level to level k, DMEM_AddSmooth there
+// (DMEM_Smooth.cpp:574-638: u = f ./ s; v = A u; u = 2u + v ./ (-s), s = a_ii / w
+// (1 where a_ii = 0, DMEM_Setup.cpp:471-482) or the L1 row norm) -- or
+// hypre_GaussElimSolve on the coarsest grid, an exact dense solve here --
+// then prolonged back to level 0 (MatvecOutOfPlace(P, U_c, 0, Vtemp, U_f)).
+int amgd::grid_prepare(amg_dist_hier *D, int k)
+{
+   const int L = D->L, Ld = D->Ld;
+   AMG_ARG(k >= 0 && k < L, "amg_grid_add: grid %d outside [0, %d)", k, L);
+   GridState &g = D->grid;
+   if (g.ready && g.k == k) return AMG_OK;
+   AMG_ARG(!g.ready, "amg_grid_add: the hierarchy already serves grid %d", g.k);
+   amg_ctx *c = D->ctx;
+   hipStream_t s = c->stream;
+   g.k = k;
+   // the replicated levels' L1 norms (as setup_async)
+   if (D->cl1.empty())
+      for (int l = Ld; l < L; l++) {
+         double *p;
+         AMG_TRY(dvec(D, std::max(1, level_n(D, l)), &p));
+         amgk::l1_norms(s, D->cA[l - Ld], p);
+         D->cl1.push_back(p);
+      }
+   // the grid's own level vectors F[l], U[l] (l <= k) and smoother scratch
+   AsyncLevel &a = g.al;
+   a.s = s;
+   AMG_HIP(hipEventCreateWithFlags(&a.ev_ready, hipEventDisableTiming));
+   AMG_HIP(hipEventCreateWithFlags(&a.ev_done, hipEventDisableTiming));
+   a.r.assign(k + 1, nullptr);
+   a.e.assign(k + 1, nullptr);
+   for (int l = 0; l <= k; l++) {
+      AMG_TRY(dvec(D, std::max(1, level_cap(D, l)), &a.r[l]));
+      AMG_TRY(dvec(D, std::max(1, level_cap(D, l)), &a.e[l]));
+   }
+   const int ck = std::max(1, level_cap(D, k));
+   AMG_TRY(dvec(D, ck, &a.sy));
+   AMG_TRY(dvec(D, ck, &a.sr));
+   AMG_TRY(dvec(D, ck, &a.u_prev));
+   if (Ld < L) AMG_TRY(dvec(D, (size_t)D->gath_blk * (c->xport->nranks + 1), &a.gath));
+   if (k == L - 1) {
+      // hypre_GaussElimSetup: the coarsest operator gathered and factorised
+      AMG_ARG(k >= Ld, "amg_grid_add: the coarsest level must be replicated "
+                       "(amg_dist_hier_set_replicate_rows)");
+      const amg_mat *Ac = D->cA[k - Ld];
+      const int n = Ac->nrows;
+      AMG_ARG(n <= 4096, "amg_grid_add: coarsest level of %d rows too large for the dense solve", n);
+      std::vector<int> rp(n + 1), cj(std::max<long long>(1, Ac->nnz));
+      std::vector<double> cv(std::max<long long>(1, Ac->nnz));
+      AMG_TRY(amg_mat_download(c, Ac, rp.data(), cj.data(), cv.data()));
+      g.n_c = n;
+      g.lu.assign((size_t)n * n, 0.0);
+      g.piv.assign(n, 0);
+      for (int i = 0; i < n; i++)
+         for (int q = rp[i]; q < rp[i + 1]; q++) g.lu[(size_t)i * n + cj[q]] += cv[q];
+      for (int cc = 0; cc < n; cc++) {
+         int p = cc;
+         for (int i = cc + 1; i < n; i++)
+            if (std::fabs(g.lu[(size_t)i * n + cc]) > std::fabs(g.lu[(size_t)p * n + cc])) p = i;
+         g.piv[cc] = p;
+         if (p != cc)
+            for (int j = 0; j < n; j++) std::swap(g.lu[(size_t)cc * n + j], g.lu[(size_t)p * n + j]);
+         const double d = g.lu[(size_t)cc * n + cc];
+         if (d == 0.0) continue; // singular pivot: that unknown stays 0
+         for (int i = cc + 1; i < n; i++) {
+            const double m = (g.lu[(size_t)i * n + cc] /= d);
+            for (int j = cc + 1; j < n; j++) g.lu[(size_t)i * n + j] -= m * g.lu[(size_t)cc * n + j];
+         }
+      }
+      g.fh.assign(n, 0.0);
+   } else {
+      const int n = level_n(D, k);
+      AMG_TRY(dvec(D, std::max(1, n), &g.sc));
+      AMG_TRY(dvec(D, std::max(1, n), &g.nsc));
+      const bool l1 = D->o.smoother == AMG_L1_JACOBI;
+      amgk::dmem_scale(s, diag_of(D, k), l1 ? l1_of(D, k) : nullptr, D->o.smooth_weight, g.sc, g.nsc, n);
+   }
+   AMG_HIP(hipStreamSynchronize(s));
+   g.ready = true;
+   return AMG_OK;
+}
+
+int amgd::grid_cycle(amg_dist_hier *D, const double *r0, double **u0)
+{
+   GridState &g = D->grid;
+   const int k = g.k, L = D->L;
+   AsyncLevel &a = g.al;
+   hipStream_t s = a.s;
+   amgk::vcopy(s, r0, a.r[0], 0, D->lv[0].n);
+   for (int l = 0; l < k; l++) AMG_TRY(restrict_to(D, a, l));
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   if (k == L - 1) {
+      // hypre_GaussElimSolve: A_c u = f_c on the gathered coarsest level
+      const int n = g.n_c;
+      std::vector<double> &x = g.fh;
+      AMG_TRY(d2h(s, x.data(), a.r[k], (size_t)n * 8));
+      for (int cc = 0; cc < n; cc++)
+         if (g.piv[cc] != cc) std::swap(x[cc], x[g.piv[cc]]);
+      for (int i = 0; i < n; i++)
+         for (int j = 0; j < i; j++) x[i] -= g.lu[(size_t)i * n + j] * x[j];
+      for (int i = n - 1; i >= 0; i--) {
+         for (int j = i + 1; j < n; j++) x[i] -= g.lu[(size_t)i * n + j] * x[j];
+         const double d = g.lu[(size_t)i * n + i];
+         x[i] = d != 0.0 ? x[i] / d : 0.0;
+      }
+      AMG_TRY(h2d(s, a.e[k], x.data(), (size_t)n * 8));
+   } else {
+      // DMEM_AddSmooth with simple_jacobi_flag = -1 (DMEM_Main.cpp:122)
+      const int n = level_n(D, k);
+      amgk::vset(s, a.e[k], 0.0, 0, n);
+      amgk::vivaxpy(s, a.r[k], g.sc, a.e[k], 0, n);
+      AMG_TRY(apply_A(D, a, k, a.e[k], nullptr, mv, a.sy));
+      amgk::vscale(s, 2.0, a.e[k], 0, n);
+      amgk::vivaxpy(s, a.sy, g.nsc, a.e[k], 0, n);
+   }
+   for (int l = k - 1; l >= 0; l--) AMG_TRY(prolong_to(D, a, l, a.e[l + 1], a.e[l]));
+   *u0 = a.e[0];
+   return AMG_OK;
+}
+
+// r = b - A x on the grid's fine level (halo exchange inside the grid)
+int amgd::grid_residual(amg_dist_hier *D, double *x, const double *b, double *r)
+{
+   return a_spgemv(D, D->grid.al, D->lv[0].A, x, b, amgk::gemv_mode(-1.0, 1.0), r);
+}
 
 extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int *level_corrections,
                                     double *relres)

@@ -111,6 +111,19 @@ void launch_sqrt(hipStream_t s, const double *in, double *out);
 
 } // namespace amgd
 
+// one grid of the level-grouped add solver (amg_grid.cpp): level k's
+// restriction / smoothing / prolongation buffers, the DMEM_AddSmooth scale
+// vectors, the coarsest grid's dense LU
+struct GridState {
+   bool ready = false;
+   int k = -1;
+   amgd::AsyncLevel al;
+   double *sc = nullptr, *nsc = nullptr; // s and -s of DMEM_AddSmooth
+   int n_c = 0;
+   std::vector<double> lu, fh;
+   std::vector<int> piv;
+};
+
 struct amg_dist_hier {
    amg_ctx *ctx = nullptr;
    amg_opts o{};
@@ -143,6 +156,7 @@ struct amg_dist_hier {
    // then carries the cycle's correction e) and the ChebyUpdate direction d
    double *x_acc = nullptr, *d_acc = nullptr;
    amgd::AccelState acc;
+   GridState grid;
    double prof_ms[5] = {0, 0, 0, 0, 0};
    long long prof_n[5] = {0, 0, 0, 0, 0};
 };
@@ -159,4 +173,9 @@ bool dist_mult_accel(const amg_dist_hier *D);
 double *dist_iterate(amg_dist_hier *D);
 // DMEM_DelayProc: the injected per-cycle wait of this rank on stream s
 void dist_delay(amg_dist_hier *D, hipStream_t s);
+// grid k of the level-grouped add solver (amg_dist_async.cpp): buffers,
+// AddCycle from the residual r0 (*u0: U[0], on D->ctx->stream), F[0] = b - A x
+int grid_prepare(amg_dist_hier *D, int k);
+int grid_cycle(amg_dist_hier *D, const double *r0, double **u0);
+int grid_residual(amg_dist_hier *D, double *x, const double *b, double *r);
 } // namespace amgd

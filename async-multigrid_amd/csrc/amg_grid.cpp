@@ -1,0 +1,688 @@
+// amg_grid.cpp -- the level-grouped asynchronous additive solver of the
+// distributed reference (DMEM_Add, DMEM_Add.cpp:20-944; message engine
+// DMEM_Comm.cpp:11-382; grid assignment DMEM_Setup.cpp:1638-1735; message
+// classes DMEM_Setup.cpp:990-1140).
+//
+// Ranks (one per GPU) are split into grids, one grid per level k.  Every grid
+// holds the WHOLE fine problem, row-partitioned among its own ranks (an
+// amg_dist_hier over the grid's transport: halo exchange inside the grid), and
+// computes only level k's additive correction (AddCycle).  Between grids the
+// corrections travel as messages between the ranks whose row ranges overlap
+// (gridjToGridk_Correct_outside{Send,Recv}): each message carries the
+// accumulated correction of the overlap, a done flag (0 running, 1 my grid
+// done, 2 all done) and one spare slot, and a sender keeps at most
+// max_inflight messages in flight per destination (data accumulates while
+// every slot is busy).  Termination follows CheckConverge / AddResNorm's
+// InnerProdFlag / AsyncRecvCleanup.  The protocol runs on the host over a
+// non-blocking transport with MPI point-to-point semantics (amg_nb_transport:
+// isend / irecv / test / wait and a sum over the grid's ranks); the numerics of
+// a grid run on its GPU (or, for protocol tests, a host model).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "amg_dist_internal.h"
+
+namespace {
+
+constexpr int GRIDJ_TO_GRIDK_CORRECT_TAG = 7; // one tag for the correction class
+enum Op { ACCUMULATE, WRITE };
+
+// ---- numerics of one grid rank -----------------------------------------------
+// vectors of the grid's local rows: x (iterate), b, r (F[0]), y (outgoing
+// corrections), e (incoming), d (ChebyUpdate direction of the cheby grid)
+struct Backend {
+   virtual ~Backend() {}
+   virtual int n() const = 0;
+   virtual int begin(const double *b, const double *x0) = 0; // y = e = d = 0, r = b - A x
+   virtual int cycle() = 0;                                   // AddCycle: u = M_k r (+ ChebyUpdate)
+   virtual int y_add_u() = 0;                                 // y += u
+   virtual int x_add_u() = 0;                                 // x += u
+   virtual int get_y(double *host) = 0;                       // y -> host, then y = 0
+   virtual int add_e(const double *host, bool to_d) = 0;      // x += e (d += e)
+   virtual int residual(double *rr) = 0;                      // r = b - A x; *rr = local r.r
+   virtual int get_x(double *host) = 0;
+};
+
+// GPU: the grid's distributed hierarchy
+struct DistBackend : Backend {
+   amg_dist_hier *D;
+   double *x = nullptr, *b = nullptr, *r = nullptr, *y = nullptr, *e = nullptr, *d = nullptr;
+   double *u = nullptr; // U[0] of the last cycle
+   double *dot = nullptr;
+   amgd::AccelState acc;
+   bool cheby_mine = false;
+   std::vector<double> tmp;
+   int n0 = 0;
+   explicit DistBackend(amg_dist_hier *D_) : D(D_) {}
+   int n() const override { return n0; }
+   int init(int k)
+   {
+      AMG_TRY(amgd::grid_prepare(D, k));
+      n0 = D->lv[0].n;
+      const size_t cap = std::max(1, D->lv[0].cap);
+      AMG_TRY(amgd::dvec(D, cap, &x));
+      AMG_TRY(amgd::dvec(D, cap, &b));
+      AMG_TRY(amgd::dvec(D, cap, &r));
+      AMG_TRY(amgd::dvec(D, cap, &y));
+      AMG_TRY(amgd::dvec(D, cap, &e));
+      AMG_TRY(amgd::dvec(D, cap, &d));
+      AMG_TRY(amgd::dvec(D, 1, &dot));
+      tmp.assign(std::max(1, n0), 0.0);
+      cheby_mine = k == std::min(D->o.cheby_grid, D->L - 1);
+      return AMG_OK;
+   }
+   hipStream_t st() const { return D->ctx->stream; }
+   int begin(const double *bh, const double *x0) override
+   {
+      AMG_TRY(amgd::h2d(st(), b, bh, (size_t)n0 * 8));
+      AMG_TRY(amgd::h2d(st(), x, x0, (size_t)n0 * 8));
+      amgk::vset(st(), y, 0.0, 0, n0);
+      amgk::vset(st(), e, 0.0, 0, n0);
+      amgk::vset(st(), d, 0.0, 0, n0);
+      acc.reset(D->o);
+      double rr;
+      return residual(&rr);
+   }
+   int cycle() override
+   {
+      AMG_TRY(amgd::grid_cycle(D, r, &u));
+      if (D->o.accel_type != AMG_NO_ACCEL) {
+         // DMEM_Add.cpp:319-324: ChebyUpdate(gridk.d, U_array[0]) (async
+         // branch, DMEM_Misc.cpp:650-663: only cheby_grid keeps d)
+         double om1 = 0.0, omd = 0.0;
+         if (acc.next(D->o, &om1, &omd))
+            amgk::dmem_cheby_update(st(), d, u, n0, cheby_mine ? 1 : 2, om1, omd);
+         else if (cheby_mine)
+            amgk::vcopy(st(), u, d, 0, n0);
+      }
+      AMG_HIP(hipGetLastError());
+      return AMG_OK;
+   }
+   int y_add_u() override
+   {
+      amgk::vaxpy(st(), 1.0, u, y, 0, n0);
+      return AMG_OK;
+   }
+   int x_add_u() override
+   {
+      amgk::vaxpy(st(), 1.0, u, x, 0, n0);
+      return AMG_OK;
+   }
+   int get_y(double *host) override
+   {
+      AMG_TRY(amgd::d2h(st(), host, y, (size_t)n0 * 8));
+      amgk::vset(st(), y, 0.0, 0, n0);
+      return AMG_OK;
+   }
+   int add_e(const double *host, bool to_d) override
+   {
+      AMG_TRY(amgd::h2d(st(), e, host, (size_t)n0 * 8));
+      amgk::vaxpy(st(), 1.0, e, x, 0, n0);
+      if (to_d) amgk::vaxpy(st(), 1.0, e, d, 0, n0);
+      return AMG_OK;
+   }
+   int residual(double *rr) override
+   {
+      AMG_TRY(amgd::grid_residual(D, x, b, r));
+      double *part;
+      AMG_TRY(amg_ctx_partials(D->ctx, 4096 + 1024, &part));
+      int np = 0;
+      amgk::sumsq_partials(st(), r, n0, part, &np);
+      amgk::reduce_partials(st(), part, np, dot, 0, part + 4096);
+      AMG_TRY(amgd::d2h(st(), rr, dot, 8));
+      return AMG_OK;
+   }
+   int get_x(double *host) override { return amgd::d2h(st(), host, x, (size_t)n0 * 8); }
+};
+
+// host model for protocol tests: A = diag(a); grid k corrects its own share of
+// the rows (global row % number of grids == k) by u = w r ./ a -- the grids
+// act on complementary subspaces, as the levels of an additive cycle do
+struct HostBackend : Backend {
+   std::vector<double> a, x, b, r, y, u, d;
+   std::vector<char> mine;
+   double w;
+   explicit HostBackend(const double *diag, int n, double weight) : a(diag, diag + n), w(weight) {}
+   int n() const override { return (int)a.size(); }
+   int begin(const double *bh, const double *x0) override
+   {
+      const int m = n();
+      b.assign(bh, bh + m);
+      x.assign(x0, x0 + m);
+      y.assign(m, 0.0);
+      u.assign(m, 0.0);
+      d.assign(m, 0.0);
+      r.assign(m, 0.0);
+      double rr;
+      return residual(&rr);
+   }
+   int cycle() override
+   {
+      for (int i = 0; i < n(); i++) u[i] = mine[i] ? w * r[i] / a[i] : 0.0;
+      return AMG_OK;
+   }
+   int y_add_u() override
+   {
+      for (int i = 0; i < n(); i++) y[i] += u[i];
+      return AMG_OK;
+   }
+   int x_add_u() override
+   {
+      for (int i = 0; i < n(); i++) x[i] += u[i];
+      return AMG_OK;
+   }
+   int get_y(double *host) override
+   {
+      std::memcpy(host, y.data(), y.size() * 8);
+      std::fill(y.begin(), y.end(), 0.0);
+      return AMG_OK;
+   }
+   int add_e(const double *host, bool to_d) override
+   {
+      for (int i = 0; i < n(); i++) {
+         x[i] += host[i];
+         if (to_d) d[i] += host[i];
+      }
+      return AMG_OK;
+   }
+   int residual(double *rr) override
+   {
+      double s = 0.0;
+      for (int i = 0; i < n(); i++) {
+         r[i] = b[i] - a[i] * x[i];
+         s += r[i] * r[i];
+      }
+      *rr = s;
+      return AMG_OK;
+   }
+   int get_x(double *host) override
+   {
+      std::memcpy(host, x.data(), x.size() * 8);
+      return AMG_OK;
+   }
+};
+
+// ---- one message class (DMEM_CommData) -----------------------------------------
+struct CommClass {
+   bool send = false;
+   std::vector<int> procs, start, len;
+   std::vector<int> done_flags, recv_flags, message_count;
+   std::vector<std::vector<double>> data;    // [i][len + 2]
+   std::vector<long long> requests;          // outstanding receive per peer
+   std::vector<int> max_inflight, num_inflight, next_inflight;
+   std::vector<std::vector<std::vector<double>>> data_inflight; // [i][j][len + 2]
+   std::vector<std::vector<long long>> requests_inflight;
+   std::vector<std::vector<int>> inflight_flags;
+};
+
+} // namespace
+
+struct amg_grid_add {
+   amg_nb_transport t{};
+   amg_opts o{};
+   int my_grid = 0, world = 1, me = 0, grid_size = 1;
+   long long row0 = 0, row1 = 0; // my global rows in my grid's partition
+   std::unique_ptr<Backend> be;
+   CommClass send, recv;
+   // DMEM_AllData iter / comm state
+   int all_done_flag = 0, outside_done_flag = 0, grid_done_flag = 0, converge_flag = 0;
+   int r_local_converge_flag = 0, cycle = 0;
+   double r0_norm2 = 1.0, r_local = 1.0;
+   long long messages_sent = 0, messages_recv = 0;
+   std::vector<double> yh, eh;
+};
+
+namespace {
+
+int xp_err(int st, const char *what)
+{
+   return st == 0 ? AMG_OK : amg_set_error(AMG_ERR_ARG, "amg_grid_add: transport %s failed (%d)", what, st);
+}
+
+// CheckInFlight (DMEM_Comm.cpp:25-63)
+int check_inflight(amg_grid_add *G, CommClass &cd, int i)
+{
+   while (true) {
+      int break_flag = 0;
+      if (G->all_done_flag == 0)
+         break_flag = 1;
+      else if (cd.num_inflight[i] < cd.max_inflight[i])
+         break;
+      for (int j = 0; j < cd.max_inflight[i]; j++) {
+         if (cd.inflight_flags[i][j] == 1) {
+            int flag = 0;
+            AMG_TRY(xp_err(G->t.test(G->t.user, cd.requests_inflight[i][j], &flag), "test"));
+            if (flag) {
+               cd.inflight_flags[i][j] = 0;
+               cd.num_inflight[i]--;
+               if (j < cd.next_inflight[i]) cd.next_inflight[i] = j;
+               if (G->all_done_flag == 1) {
+                  break_flag = 1;
+                  break;
+               }
+            }
+         } else if (G->all_done_flag == 1) {
+            break_flag = 1;
+            break;
+         }
+      }
+      if (break_flag) break;
+   }
+   return AMG_OK;
+}
+
+// SetNextInFlight (DMEM_Comm.cpp:65-75)
+void set_next_inflight(CommClass &cd, int i)
+{
+   for (int j = 0; j < cd.max_inflight[i]; j++)
+      if (cd.inflight_flags[i][j] == 0) {
+         cd.next_inflight[i] = j;
+         return;
+      }
+   cd.next_inflight[i] = cd.max_inflight[i];
+}
+
+// SendRecv, asynchronous outside classes (DMEM_Comm.cpp:77-348); v holds the
+// grid's local rows; returns the recv / send flag
+int send_recv(amg_grid_add *G, CommClass &cd, double *v, Op op, int *ret)
+{
+   const bool local = G->o.converge_test_type != AMG_GLOBAL;
+   int return_flag = 0;
+   for (int i = 0; i < (int)cd.procs.size(); i++) {
+      const int ip = cd.procs[i], vs = cd.start[i], vl = cd.len[i];
+      cd.recv_flags[i] = 0;
+      if (cd.send) {
+         if (cd.done_flags[i] >= 2) continue;
+         if (op == WRITE)
+            std::memcpy(cd.data[i].data(), v + vs, (size_t)vl * 8);
+         else
+            for (int j = 0; j < vl; j++) cd.data[i][j] += v[vs + j];
+         AMG_TRY(check_inflight(G, cd, i));
+         if (cd.num_inflight[i] >= cd.max_inflight[i]) continue;
+         const int nx = cd.next_inflight[i];
+         std::vector<double> &slot = cd.data_inflight[i][nx];
+         std::memcpy(slot.data(), cd.data[i].data(), (size_t)vl * 8);
+         std::fill(cd.data[i].begin(), cd.data[i].begin() + vl, 0.0);
+         if (G->grid_done_flag == 1) {
+            slot[vl] = 1.0;
+            if (local) {
+               cd.done_flags[i] = 2;
+            } else {
+               cd.done_flags[i] = 1;
+               if (G->all_done_flag == 1) {
+                  cd.done_flags[i] = 2;
+                  slot[vl] = 2.0;
+               }
+            }
+         }
+         AMG_TRY(xp_err(G->t.isend(G->t.user, ip, GRIDJ_TO_GRIDK_CORRECT_TAG, slot.data(), vl + 2,
+                                   &cd.requests_inflight[i][nx]),
+                        "isend"));
+         cd.inflight_flags[i][nx] = 1;
+         cd.num_inflight[i]++;
+         set_next_inflight(cd, i);
+         cd.message_count[i]++;
+         G->messages_sent++;
+         return_flag = 1;
+      } else {
+         if (cd.done_flags[i] >= 2) continue;
+         while (true) {
+            int flag = 0;
+            AMG_TRY(xp_err(G->t.test(G->t.user, cd.requests[i], &flag), "test"));
+            if (!flag) break;
+            cd.message_count[i]++;
+            G->messages_recv++;
+            for (int j = 0; j < vl; j++) v[vs + j] += cd.data[i][j];
+            const double fl = cd.data[i][vl];
+            if (local) {
+               if (fl == 1.0) {
+                  cd.done_flags[i] = 2;
+                  break;
+               }
+            } else {
+               if (fl == 1.0) {
+                  cd.done_flags[i] = 1;
+               } else if (fl == 2.0) {
+                  cd.done_flags[i] = 2;
+                  break;
+               }
+            }
+            AMG_TRY(xp_err(G->t.irecv(G->t.user, ip, GRIDJ_TO_GRIDK_CORRECT_TAG, cd.data[i].data(), vl + 2,
+                                      &cd.requests[i]),
+                           "irecv"));
+            cd.recv_flags[i] = 1;
+            return_flag = 1;
+            if (G->o.async_type == AMG_SEMI_ASYNC && G->all_done_flag == 0) break;
+         }
+      }
+   }
+   *ret = return_flag;
+   return AMG_OK;
+}
+
+// DMEM_AddCheckComm (DMEM_Add.cpp:460-528)
+int add_check_comm(amg_grid_add *G)
+{
+   std::fill(G->eh.begin(), G->eh.end(), 0.0);
+   int recv_flag = 0;
+   AMG_TRY(send_recv(G, G->recv, G->eh.data(), ACCUMULATE, &recv_flag));
+   if (recv_flag == 1) {
+      const bool to_d = G->o.accel_type != AMG_NO_ACCEL && G->my_grid == G->o.cheby_grid;
+      AMG_TRY(G->be->add_e(G->eh.data(), to_d));
+   }
+   for (int i = 0; i < (int)G->send.procs.size(); i++) AMG_TRY(check_inflight(G, G->send, i));
+   return AMG_OK;
+}
+
+// DMEM_AddCorrect_LocalRes (DMEM_Add.cpp:391-458)
+int add_correct(amg_grid_add *G)
+{
+   AMG_TRY(G->be->y_add_u());
+   if (G->converge_flag == 1 || G->cycle % std::max(1, G->o.async_comm_save_divisor) == 0) {
+      AMG_TRY(G->be->get_y(G->yh.data()));
+      int f;
+      AMG_TRY(send_recv(G, G->send, G->yh.data(), ACCUMULATE, &f));
+   }
+   AMG_TRY(G->be->x_add_u());
+   return add_check_comm(G);
+}
+
+// DMEM_CheckOutsideDoneFlag (DMEM_Add.cpp:741-749)
+void check_outside_done(amg_grid_add *G)
+{
+   auto none0 = [](const CommClass &cd) {
+      for (int f : cd.done_flags)
+         if (f == 0) return false;
+      return true;
+   };
+   if (none0(G->send) && none0(G->recv)) G->outside_done_flag = 1;
+}
+
+// CheckConverge (DMEM_Add.cpp:905-944)
+int check_converge(amg_grid_add *G)
+{
+   const amg_opts &o = G->o;
+   if (o.converge_test_type == AMG_GLOBAL) {
+      if (G->all_done_flag == 0) {
+         if (G->grid_done_flag == 0 && (G->cycle >= o.num_cycles - 1 || G->r_local_converge_flag == 1))
+            G->grid_done_flag = 1;
+         if (G->grid_done_flag == 1 && G->outside_done_flag == 0) check_outside_done(G);
+         return 0;
+      }
+      return 1;
+   }
+   if (G->cycle >= o.num_cycles - 1 || G->r_local_converge_flag == 1) {
+      G->grid_done_flag = 1;
+      return 1;
+   }
+   return 0;
+}
+
+// AddResNorm, async FULL_ASYNC branch (DMEM_Add.cpp:331-389): InnerProdFlag
+// sums (r.r, outside_done_flag) over the grid's ranks
+int add_res_norm(amg_grid_add *G, double rr)
+{
+   if (G->o.async_type == AMG_SEMI_ASYNC) return AMG_OK; // :346-358: not computed
+   double v[2] = {rr, (double)G->outside_done_flag};
+   AMG_TRY(xp_err(G->t.grid_allreduce(G->t.user, v, 2), "grid_allreduce"));
+   G->r_local = std::sqrt(v[0]) / G->r0_norm2;
+   if (G->r_local < G->o.tol) G->r_local_converge_flag = 1;
+   if ((int)v[1] == G->grid_size) G->all_done_flag = 1;
+   return AMG_OK;
+}
+
+// AsyncRecvCleanup (DMEM_Add.cpp:829-884) + CompleteInFlight (DMEM_Comm.cpp:11-23)
+int async_end(amg_grid_add *G)
+{
+   const bool local = G->o.converge_test_type != AMG_GLOBAL;
+   auto all2 = [](const CommClass &cd) {
+      for (int f : cd.done_flags)
+         if (f != 2) return false;
+      return true;
+   };
+   std::fill(G->eh.begin(), G->eh.end(), 0.0);
+   std::vector<double> zero(G->yh.size(), 0.0);
+   for (long long spin = 0;; spin++) {
+      if (local ? (all2(G->recv) && all2(G->send)) : all2(G->recv)) break;
+      int f;
+      AMG_TRY(send_recv(G, G->recv, G->eh.data(), ACCUMULATE, &f));
+      if (local) AMG_TRY(send_recv(G, G->send, zero.data(), ACCUMULATE, &f));
+      if (spin > (1LL << 34)) return amg_set_error(AMG_ERR_ARG, "amg_grid_add: cleanup never completed");
+   }
+   AMG_TRY(G->be->add_e(G->eh.data(), false));
+   for (int i = 0; i < (int)G->send.procs.size(); i++)
+      for (int j = 0; j < G->send.max_inflight[i]; j++)
+         if (G->send.inflight_flags[i][j] == 1) {
+            AMG_TRY(xp_err(G->t.wait(G->t.user, G->send.requests_inflight[i][j]), "wait"));
+            G->send.inflight_flags[i][j] = 0;
+         }
+   return AMG_OK;
+}
+
+// the outside classes: every rank of another grid whose row range overlaps
+// mine (DMEM_Setup.cpp:996-1047 send, :1106-1140 receive); start / len in my
+// local rows
+int build_classes(amg_grid_add *G, const int *rank_grid, const long long *rank_rows)
+{
+   for (CommClass *cd : {&G->send, &G->recv}) {
+      const bool send = cd == &G->send;
+      cd->send = send;
+      for (int p = 0; p < G->world; p++) {
+         if (rank_grid[p] == G->my_grid) continue;
+         const long long ps = rank_rows[2 * p], pe = rank_rows[2 * p + 1];
+         const long long s = std::max(ps, G->row0), e = std::min(pe, G->row1);
+         if (e <= s) continue;
+         cd->procs.push_back(p);
+         cd->start.push_back((int)(s - G->row0));
+         cd->len.push_back((int)(e - s));
+      }
+      const size_t np = cd->procs.size();
+      cd->done_flags.assign(np, 0);
+      cd->recv_flags.assign(np, 0);
+      cd->message_count.assign(np, 0);
+      cd->data.resize(np);
+      for (size_t i = 0; i < np; i++) cd->data[i].assign(cd->len[i] + 2, 0.0);
+      if (send) {
+         const int mi = std::max(1, G->o.max_inflight);
+         cd->max_inflight.assign(np, mi);
+         cd->num_inflight.assign(np, 0);
+         cd->next_inflight.assign(np, 0);
+         cd->data_inflight.resize(np);
+         cd->requests_inflight.assign(np, std::vector<long long>(mi, 0));
+         cd->inflight_flags.assign(np, std::vector<int>(mi, 0));
+         for (size_t i = 0; i < np; i++)
+            cd->data_inflight[i].assign(mi, std::vector<double>(cd->len[i] + 2, 0.0));
+      } else {
+         cd->requests.assign(np, 0);
+      }
+   }
+   return AMG_OK;
+}
+
+void reset_classes(amg_grid_add *G)
+{
+   for (CommClass *cd : {&G->send, &G->recv}) {
+      std::fill(cd->done_flags.begin(), cd->done_flags.end(), 0);
+      std::fill(cd->recv_flags.begin(), cd->recv_flags.end(), 0);
+      std::fill(cd->message_count.begin(), cd->message_count.end(), 0);
+      for (auto &v : cd->data) std::fill(v.begin(), v.end(), 0.0);
+      for (auto &f : cd->inflight_flags) std::fill(f.begin(), f.end(), 0);
+      std::fill(cd->num_inflight.begin(), cd->num_inflight.end(), 0);
+      std::fill(cd->next_inflight.begin(), cd->next_inflight.end(), 0);
+      for (auto &pool : cd->data_inflight)
+         for (auto &v : pool) std::fill(v.begin(), v.end(), 0.0);
+   }
+}
+
+int create_common(amg_grid_add *G, int my_grid, int world, int me, const int *rank_grid,
+                  const long long *rank_rows, const amg_nb_transport *t)
+{
+   AMG_ARG(t && t->isend && t->irecv && t->test && t->wait && t->grid_allreduce,
+           "amg_grid_add: incomplete transport");
+   AMG_ARG(rank_grid && rank_rows && world >= 1 && me >= 0 && me < world && rank_grid[me] == my_grid,
+           "amg_grid_add: bad rank layout");
+   AMG_ARG(!(G->o.async_type == AMG_SEMI_ASYNC && G->o.converge_test_type == AMG_GLOBAL),
+           "amg_grid_add: SEMI_ASYNC with converge_test GLOBAL never terminates in the reference "
+           "(AddResNorm computes no flags for SEMI_ASYNC, DMEM_Add.cpp:346-358)");
+   G->t = *t;
+   G->my_grid = my_grid;
+   G->world = world;
+   G->me = me;
+   G->grid_size = 0;
+   for (int p = 0; p < world; p++) G->grid_size += rank_grid[p] == my_grid;
+   G->row0 = rank_rows[2 * me];
+   G->row1 = rank_rows[2 * me + 1];
+   AMG_ARG(G->row1 - G->row0 == G->be->n(), "amg_grid_add: row range %lld..%lld vs %d local rows", G->row0,
+           G->row1, G->be->n());
+   G->yh.assign(std::max(1, G->be->n()), 0.0);
+   G->eh.assign(std::max(1, G->be->n()), 0.0);
+   return build_classes(G, rank_grid, rank_rows);
+}
+
+} // namespace
+
+// DMEM_Setup.cpp:1638-1735 (assign_procs_type default): ranks per grid from the
+// levels' work fractions, grids in level order, at least one rank each
+extern "C" int amg_grid_partition(int num_procs, int num_grids, const double *frac_work, int *procs_per_grid)
+{
+   AMG_ARG(num_procs >= num_grids && num_grids >= 1 && frac_work && procs_per_grid,
+           "amg_grid_partition: %d ranks cannot hold %d grids", num_procs, num_grids);
+   int count = num_procs;
+   for (int level = 0; level < num_grids; level++) {
+      int cur;
+      if (level == num_grids - 1 || count == 1) {
+         cur = count;
+      } else if (count == num_grids - level) {
+         cur = 1;
+      } else {
+         cur = std::max((int)std::ceil(frac_work[level] * (double)num_procs), 1);
+         while (true) {
+            const int next = cur - 1;
+            const double next_frac = (double)next / (double)num_procs;
+            const double diff_cur = std::fabs(frac_work[level] - (double)cur / (double)num_procs);
+            const double diff_next = std::fabs(frac_work[level] - next_frac);
+            if (count - cur <= num_grids - level) {
+               cur = count - (num_grids - level) + 1;
+               break;
+            }
+            if (diff_cur <= diff_next || cur == 1) break;
+            cur--;
+         }
+      }
+      procs_per_grid[level] = cur;
+      count -= cur;
+   }
+   return AMG_OK;
+}
+
+extern "C" int amg_grid_add_create(amg_dist_hier *D, int my_grid, int world_nranks, int world_rank,
+                                   const int *rank_grid, const long long *rank_rows, const amg_nb_transport *t,
+                                   amg_grid_add **out)
+{
+   AMG_ARG(D && out, "amg_grid_add_create: null argument");
+   AMG_ARG(D->o.solver == AMG_ASYNC_MULTADD, "amg_grid_add_create: ASYNC_MULTADD hierarchies only");
+   auto G = std::make_unique<amg_grid_add>();
+   G->o = D->o;
+   auto be = std::make_unique<DistBackend>(D);
+   AMG_TRY(be->init(my_grid));
+   G->be = std::move(be);
+   AMG_TRY(create_common(G.get(), my_grid, world_nranks, world_rank, rank_grid, rank_rows, t));
+   *out = G.release();
+   return AMG_OK;
+}
+
+extern "C" int amg_grid_add_create_host(int nrows, const double *diag, double weight, const amg_opts *opts,
+                                        int my_grid, int world_nranks, int world_rank, const int *rank_grid,
+                                        const long long *rank_rows, const amg_nb_transport *t,
+                                        amg_grid_add **out)
+{
+   AMG_ARG(diag && opts && out && nrows >= 0, "amg_grid_add_create_host: bad argument");
+   for (int i = 0; i < nrows; i++) AMG_ARG(diag[i] != 0.0, "amg_grid_add_create_host: zero diagonal at %d", i);
+   auto G = std::make_unique<amg_grid_add>();
+   G->o = *opts;
+   auto hb = std::make_unique<HostBackend>(diag, nrows, weight);
+   AMG_ARG(rank_grid && rank_rows && world_rank >= 0 && world_rank < world_nranks,
+           "amg_grid_add_create_host: bad rank layout");
+   int ngrids = 0;
+   for (int p = 0; p < world_nranks; p++) ngrids = std::max(ngrids, rank_grid[p] + 1);
+   hb->mine.assign(nrows, 0);
+   for (int i = 0; i < nrows; i++) hb->mine[i] = (rank_rows[2 * world_rank] + i) % ngrids == my_grid;
+   G->be = std::move(hb);
+   AMG_TRY(create_common(G.get(), my_grid, world_nranks, world_rank, rank_grid, rank_rows, t));
+   *out = G.release();
+   return AMG_OK;
+}
+
+// DMEM_Add (DMEM_Add.cpp:20-178), asynchronous branch
+extern "C" int amg_grid_add_solve(amg_grid_add *G, const double *b_local, double *x_local, int *cycles,
+                                  double *relres_local, long long *messages)
+{
+   AMG_ARG(G && b_local && x_local, "amg_grid_add_solve: null argument");
+   G->all_done_flag = G->outside_done_flag = G->grid_done_flag = G->converge_flag = 0;
+   G->r_local_converge_flag = 0;
+   G->cycle = 0;
+   G->messages_sent = G->messages_recv = 0;
+   reset_classes(G);
+   // r = b - A x0 and its norm over the grid (the whole problem: every grid
+   // holds all rows) -- output.r0_norm2
+   AMG_TRY(G->be->begin(b_local, x_local));
+   double rr;
+   AMG_TRY(G->be->residual(&rr));
+   double v[1] = {rr};
+   AMG_TRY(xp_err(G->t.grid_allreduce(G->t.user, v, 1), "grid_allreduce"));
+   G->r0_norm2 = std::sqrt(v[0]);
+   if (G->r0_norm2 == 0.0) G->r0_norm2 = 1.0;
+   G->r_local = 1.0;
+   // AsyncStart: post every outside receive
+   for (int i = 0; i < (int)G->recv.procs.size(); i++)
+      AMG_TRY(xp_err(G->t.irecv(G->t.user, G->recv.procs[i], GRIDJ_TO_GRIDK_CORRECT_TAG, G->recv.data[i].data(),
+                                G->recv.len[i] + 2, &G->recv.requests[i]),
+                     "irecv"));
+   const long long cap = 1000LL * std::max(1, G->o.num_cycles) + 1000;
+   while (true) {
+      G->converge_flag = check_converge(G);
+      if (G->o.delay_type != AMG_DELAY_NONE && G->o.delay_usec > 0 &&
+          (G->o.delay_rank < 0 || G->o.delay_rank == G->me)) {
+         // DMEM_DelayProc (DMEM_Misc.cpp:668-684)
+         DistBackend *db = dynamic_cast<DistBackend *>(G->be.get());
+         if (db) amgk::delay(db->st(), (double)G->o.delay_usec, db->D->ctx->wall_khz);
+      }
+      AMG_TRY(G->be->cycle());
+      AMG_TRY(add_correct(G));
+      AMG_TRY(G->be->residual(&rr)); // DMEM_AddResidual_LocalRes
+      if (G->all_done_flag == 0) AMG_TRY(add_res_norm(G, rr));
+      G->cycle++;
+      if (G->converge_flag == 1) break;
+      if (G->cycle > cap) return amg_set_error(AMG_ERR_ARG, "amg_grid_add_solve: no termination after %d cycles",
+                                               G->cycle);
+   }
+   AMG_TRY(async_end(G));
+   AMG_TRY(G->be->residual(&rr));
+   v[0] = rr;
+   AMG_TRY(xp_err(G->t.grid_allreduce(G->t.user, v, 1), "grid_allreduce"));
+   AMG_TRY(G->be->get_x(x_local));
+   if (cycles) *cycles = G->cycle;
+   if (relres_local) *relres_local = std::sqrt(v[0]) / G->r0_norm2;
+   if (messages) {
+      messages[0] = G->messages_sent;
+      messages[1] = G->messages_recv;
+   }
+   return AMG_OK;
+}
+
+extern "C" int amg_grid_add_peers(const amg_grid_add *G, int *nsend, int *nrecv)
+{
+   AMG_ARG(G, "amg_grid_add_peers: null handle");
+   if (nsend) *nsend = (int)G->send.procs.size();
+   if (nrecv) *nrecv = (int)G->recv.procs.size();
+   return AMG_OK;
+}
+
+extern "C" int amg_grid_add_free(amg_grid_add *G)
+{
+   delete G;
+   return AMG_OK;
+}

@@ -254,6 +254,9 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
 void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc);
 // u += P e for the checked geometric P of GeoT g (bit-identical to the SpGEMV)
 void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u);
+// DMEM_AddSmooth scale vectors: s = a_ii / w (1 where a_ii = 0) or the L1 row
+// norm l1 (l1 != nullptr), ns = -s (DMEM_Setup.cpp:423-482)
+void dmem_scale(hipStream_t s, const double *diag, const double *l1, double omega, double *sc, double *nsc, int n);
 // the stream waits usec microseconds (device wall clock at wall_khz)
 void delay(hipStream_t s, double usec, int wall_khz);
 // u_out = first Jacobi (l1 == nullptr) / L1 Jacobi sweep of A on uc = u + P e,

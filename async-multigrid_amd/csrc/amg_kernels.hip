@@ -2977,6 +2977,21 @@ void vivaxpy(hipStream_t s, const double *x, const double *sc, double *y, int rb
    if (re > rb) vivaxpy_k<<<ew_blocks(re - rb), 256, 0, s>>>(x, sc, y, rb, re);
 }
 
+__global__ void dmem_scale_k(const double *__restrict__ diag, const double *__restrict__ l1, double omega,
+                             double *__restrict__ sc, double *__restrict__ nsc, int n)
+{
+   EW_LOOP(i, 0, n)
+   {
+      const double v = l1 ? l1[i] : (diag[i] == 0.0 ? 1.0 : diag[i] / omega);
+      sc[i] = v;
+      nsc[i] = -v;
+   }
+}
+void dmem_scale(hipStream_t s, const double *diag, const double *l1, double omega, double *sc, double *nsc, int n)
+{
+   if (n > 0) dmem_scale_k<<<ew_blocks(n), 256, 0, s>>>(diag, l1, omega, sc, nsc, n);
+}
+
 __global__ void vscale_k(double a, double *__restrict__ y, int rb, int re)
 {
    EW_LOOP(i, rb, re) y[i] = a * y[i];

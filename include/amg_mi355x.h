@@ -134,6 +134,10 @@ typedef struct {
    double delay_frac;            /* input.delay_frac (DELAY_SOME)                 */
    int fail_iter;                /* input.fail_iter (FAIL_ONE)                    */
    int delay_rank;               /* distributed: -1 every rank, else that rank    */
+   int max_inflight;             /* input.max_inflight (DMEM_Main.cpp:113): messages
+                                    in flight per destination (amg_grid_add)   */
+   int async_comm_save_divisor;  /* input.async_comm_save_divisor (:123): send the
+                                    accumulated corrections every this many cycles */
 } amg_opts;
 #define AMG_DELAY_NONE 0
 #define AMG_DELAY_ONE 1
@@ -516,6 +520,58 @@ int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, int sweeps, i
 /* y = A_0 x on the distributed fine operator (halo exchange + interior/boundary
  * split); *ms = average device milliseconds over reps */
 int amg_dist_fine_spmv(amg_dist_hier *D, int reps, double *ms);
+
+/* ---- level-grouped asynchronous additive solve (DMEM_Add) ------------------------ */
+/* Ranks (one per GPU) split into grids, one per level k (DMEM_Add.cpp:20-944).
+ * Every grid holds the whole fine problem row-partitioned among its ranks (an
+ * amg_dist_hier created on a context whose transport spans the grid's ranks) and
+ * computes level k's additive correction: restriction to level k,
+ * DMEM_AddSmooth (u = f./s; v = A u; u = 2u + v./(-s)) or, on the coarsest grid,
+ * an exact dense solve (hypre_GaussElimSolve), prolongation.  Corrections travel
+ * between the ranks of different grids whose row ranges overlap as messages of
+ * len + 2 doubles (data, done flag 0/1/2, spare), at most max_inflight per
+ * destination in flight, accumulated while every slot is busy (SendRecv /
+ * CheckInFlight / CompleteInFlight, DMEM_Comm.cpp:11-382); termination by
+ * CheckConverge, AddResNorm's InnerProdFlag and AsyncRecvCleanup
+ * (DMEM_Add.cpp:331-389, 829-944).  The messages go over a caller-supplied
+ * non-blocking transport with MPI point-to-point semantics: */
+typedef struct amg_nb_transport {
+   void *user;
+   /* post a send of n doubles to world rank peer; buf stays untouched until the
+    * request completes (test / wait) */
+   int (*isend)(void *user, int peer, int tag, const double *buf, long long n, long long *req);
+   /* post a receive of n doubles from world rank peer into buf */
+   int (*irecv)(void *user, int peer, int tag, double *buf, long long n, long long *req);
+   int (*test)(void *user, long long req, int *done); /* MPI_Test: *done = 1 once complete */
+   int (*wait)(void *user, long long req);            /* MPI_Wait */
+   /* in-place sum of n doubles over the ranks of the caller's grid */
+   int (*grid_allreduce)(void *user, double *vals, int n);
+} amg_nb_transport;
+typedef struct amg_grid_add amg_grid_add;
+/* DMEM_Setup.cpp:1638-1735: ranks per grid from the levels' work fractions */
+int amg_grid_partition(int num_procs, int num_grids, const double *frac_work, int *procs_per_grid);
+/* rank_grid[world]: every rank's grid; rank_rows[2 world]: every rank's global fine
+ * rows [start, end) in its own grid's partition.  D: this rank's share of its
+ * grid's hierarchy (opts: solver ASYNC_MULTADD, num_cycles, tol, converge_test_type,
+ * async_type, accel_type / cheby_grid, max_inflight, async_comm_save_divisor,
+ * delay_*). */
+int amg_grid_add_create(amg_dist_hier *D, int my_grid, int world_nranks, int world_rank,
+                        const int *rank_grid, const long long *rank_rows, const amg_nb_transport *t,
+                        amg_grid_add **out);
+/* the same protocol over a host model grid (A = diag(diag); grid k corrects the
+ * rows with global index % number of grids == k by u = weight r ./ diag):
+ * protocol tests without a GPU */
+int amg_grid_add_create_host(int nrows, const double *diag, double weight, const amg_opts *opts, int my_grid,
+                             int world_nranks, int world_rank, const int *rank_grid,
+                             const long long *rank_rows, const amg_nb_transport *t, amg_grid_add **out);
+/* DMEM_Add, asynchronous branch: b / x (in: x0, out: x) are this rank's rows of
+ * its grid's partition; *cycles = cycles run, *relres = ||b - A x|| / ||b - A x0||
+ * over the grid after AsyncRecvCleanup, messages[2] = sent, received */
+int amg_grid_add_solve(amg_grid_add *G, const double *b_local, double *x_local, int *cycles, double *relres,
+                       long long *messages);
+/* number of outside send / receive peers (the overlapping ranks of other grids) */
+int amg_grid_add_peers(const amg_grid_add *G, int *nsend, int *nrecv);
+int amg_grid_add_free(amg_grid_add *G);
 
 /* ---- binary triplet matrix files (-problem file) ------------------------------ */
 /* records {int32 i, int32 j, double val} (Triplet_AOS, Main.hpp:433-437), 1-based;

@@ -1,0 +1,92 @@
+"""Level-grouped asynchronous additive solve (DMEM_Add, csrc/amg_grid.cpp) on the
+GPU: ranks as threads sharing one GPU, split into one grid per level; every
+grid holds the whole 24^3 problem row-partitioned among its ranks (intra-grid
+halo over the host transport), computes its level's AddCycle correction
+(restriction, DMEM_AddSmooth or the coarsest grid's exact solve, prolongation)
+and exchanges corrections with the overlapping ranks of the other grids
+through the message protocol (rendezvous mailboxes: the in-flight pools fill).
+Asynchronous, so checked as a band: every grid converges, every message sent
+is received, and the grids' iterates agree (they all add every correction)."""
+import numpy as np
+import pytest
+
+from test_gpu_dist import run_ranks, split_host
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mult24(amg, oracle):
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs = oracle.smooth_transfer(host["A"][lev], host["P"][lev], 0.8)
+        Ps.append(ps)
+        Rs.append(rs)
+    return L, {"A": host["A"], "P": Ps, "R": Rs}, amg.rhs_rand(0, 24 ** 3)
+
+
+def grid_solve(amg, L, host, f, ppg, **kw):
+    n = host["A"][0].nrows
+    rank_grid, rank_rows = amg.grid.layout(ppg, n)
+    world = len(rank_grid)
+    nb = amg.grid.ThreadNbHub(rank_grid)
+    # per grid: its ranks' row cuts of every level (the fine cuts of layout)
+    parts, hubs, first = {}, {}, {}
+    for g in range(len(ppg)):
+        ranks = [r for r in range(world) if rank_grid[r] == g]
+        first[g] = ranks[0]
+        cuts = tuple(i / len(ranks) for i in range(1, len(ranks)))
+        parts[g] = split_host(host, cuts)
+        hubs[g] = amg.dist.ThreadMailbox(len(ranks))
+    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=0.8, tol=0.0, **kw)
+
+    def rank(r):
+        g = int(rank_grid[r])
+        gr = r - first[g]
+        rs, pr = parts[g]
+        c = amg.Context(0, nstreams=2)
+        tr = amg.dist.HostTransport(hubs[g], gr)
+        amg.dist.init_host(c, int(np.sum(rank_grid == g)), gr, tr)
+        A, P, R = pr[gr]
+        D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
+        assert D.row0 == rank_rows[2 * r] and D.row0 + D.n0 == rank_rows[2 * r + 1]
+        G = amg.grid.GridAdd(nb.transport(r), g, world, r, rank_grid, rank_rows, dist_hier=D)
+        x, cyc, rel, msgs = G.solve(f[D.row0:D.row0 + D.n0])
+        row0 = D.row0
+        G.free()
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        if tr.error is not None:
+            raise tr.error
+        return g, row0, x, cyc, rel, msgs
+
+    return run_ranks(world, rank)
+
+
+@pytest.mark.parametrize("ppg,conv,inflight", [((1, 1, 1, 1), "local", 1), ((2, 1, 1, 1), "global", 2),
+                                               ((2, 2, 1, 1), "local", 3)])
+def test_grid_add_converges(amg, mult24, ppg, conv, inflight):
+    L, host, f = mult24
+    ppg = ppg[:L] if len(ppg) >= L else ppg + (1,) * (L - len(ppg))
+    N = 20
+    res = grid_solve(amg, L, host, f, ppg, num_cycles=N, max_inflight=inflight,
+                     converge_test_type=amg.AMG_GLOBAL if conv == "global" else amg.AMG_LOCAL)
+    n = host["A"][0].nrows
+    xs = {}
+    sent = recv = 0
+    for g, row0, x, cyc, rel, msgs in res:
+        assert np.all(np.isfinite(x))
+        assert cyc >= N
+        assert rel < 0.5, (g, rel)
+        sent += int(msgs[0])
+        recv += int(msgs[1])
+        xs.setdefault(g, np.zeros(n))[row0:row0 + x.size] = x
+    assert sent == recv
+    # every grid ends with (nearly) the same iterate: all corrections reach all
+    # grids, up to the reference's dropped final payloads (test_grid_add.py)
+    x0 = xs[0]
+    for g, x in xs.items():
+        assert np.linalg.norm(x - x0) <= 0.2 * np.linalg.norm(x0), g
