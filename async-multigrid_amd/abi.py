@@ -193,7 +193,26 @@ class AmgHostCsr(C.Structure):
     _fields_ = [("nrows", _i), ("ncols", _i), ("nnz", _ll), ("rowptr", _ip), ("col", _ip), ("val", _dp)]
 
 
+_ISEND = C.CFUNCTYPE(_i, _p, _i, _i, _dp, _ll, _llp)
+_IRECV = _ISEND
+_TEST = C.CFUNCTYPE(_i, _p, _ll, _ip)
+_WAIT = C.CFUNCTYPE(_i, _p, _ll)
+_ALLRED = C.CFUNCTYPE(_i, _p, _dp, _i)
+
+
+class AmgNbTransport(C.Structure):
+    _fields_ = [("user", _p), ("isend", _ISEND), ("irecv", _IRECV), ("test", _TEST), ("wait", _WAIT),
+                ("grid_allreduce", _ALLRED)]
+
+
 PROTOTYPES.update({
+    "amg_grid_partition": (_i, [_i, _i, _dp, _ip]),
+    "amg_grid_add_create": (_i, [_p, _i, _i, _i, _ip, _llp, C.POINTER(AmgNbTransport), _pp]),
+    "amg_grid_add_create_host": (_i, [_i, _dp, _d, C.POINTER(AmgOpts), _i, _i, _i, _ip, _llp,
+                                      C.POINTER(AmgNbTransport), _pp]),
+    "amg_grid_add_solve": (_i, [_p, _dp, _dp, _ip, _dp, _llp]),
+    "amg_grid_add_peers": (_i, [_p, _ip, _ip]),
+    "amg_grid_add_free": (_i, [_p]),
     "amg_triplet_read": (_i, [C.c_char_p, _i, _i, C.POINTER(AmgHostCsr)]),
     "amg_triplet_read_part": (_i, [C.c_char_p, _i, _ip, C.POINTER(AmgHostCsr)]),
     "amg_triplet_write": (_i, [C.c_char_p, _i, _i, _ip, _ip, _dp, _i]),

@@ -18,35 +18,7 @@ import numpy as np
 from . import check, lib
 from .abi import AmgOpts
 
-_ISEND = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double), C.c_longlong,
-                     C.POINTER(C.c_longlong))
-_IRECV = _ISEND
-_TEST = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_longlong, C.POINTER(C.c_int))
-_WAIT = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_longlong)
-_ALLRED = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int)
-
-
-class AmgNbTransport(C.Structure):
-    _fields_ = [("user", C.c_void_p), ("isend", _ISEND), ("irecv", _IRECV), ("test", _TEST),
-                ("wait", _WAIT), ("grid_allreduce", _ALLRED)]
-
-
-lib.amg_grid_partition.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]
-lib.amg_grid_partition.restype = C.c_int
-lib.amg_grid_add_create.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
-                                    C.POINTER(C.c_longlong), C.POINTER(AmgNbTransport), C.POINTER(C.c_void_p)]
-lib.amg_grid_add_create.restype = C.c_int
-lib.amg_grid_add_create_host.argtypes = [C.c_int, C.POINTER(C.c_double), C.c_double, C.POINTER(AmgOpts), C.c_int,
-                                         C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_longlong),
-                                         C.POINTER(AmgNbTransport), C.POINTER(C.c_void_p)]
-lib.amg_grid_add_create_host.restype = C.c_int
-lib.amg_grid_add_solve.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int),
-                                   C.POINTER(C.c_double), C.POINTER(C.c_longlong)]
-lib.amg_grid_add_solve.restype = C.c_int
-lib.amg_grid_add_peers.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
-lib.amg_grid_add_peers.restype = C.c_int
-lib.amg_grid_add_free.argtypes = [C.c_void_p]
-lib.amg_grid_add_free.restype = C.c_int
+from .abi import AmgNbTransport, _ISEND, _IRECV, _TEST, _WAIT, _ALLRED  # noqa: E402
 
 
 def partition(num_procs, frac_work):
