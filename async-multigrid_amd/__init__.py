@@ -100,6 +100,10 @@ class Context:
         """Fused level-0 residual + restriction on geometric hierarchies (default on)."""
         check(lib.amg_set_fuse_transfer(self.h, int(enable)))
 
+    def set_bsr3(self, enable):
+        """3x3 block form of num_functions = 3 operators for matrices registered from now on (default on)."""
+        check(lib.amg_set_bsr3(self.h, int(enable)))
+
     def set_fuse_prolong(self, enable):
         """Prolongation fused into the first post-smoothing sweep of marched geometric levels (default off: VALU-bound, slower)."""
         check(lib.amg_set_fuse_prolong(self.h, int(enable)))
@@ -137,6 +141,7 @@ class Mat:
         self.master_pattern = lib.amg_mat_master_pattern(handle)  # master length J (-J: uniform values), 0 = not coded
         self.plane_march = lib.amg_mat_plane_march(handle)  # plane size P of the marching kernel, 0 = not marched
         self.march_points = lib.amg_mat_march_points(handle)  # 7 / 27-point marching kernel, 0 = not marched
+        self.bsr3 = lib.amg_mat_bsr3(handle)  # 3x3 blocks: 1 value-indexed, 2 fp64, 0 not blocked
 
     @classmethod
     def register(cls, ctx, nrows, ncols, rowptr, col, val, diag_first=1):

@@ -95,6 +95,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_PLANE_MARCH_XCD")) c->mz_xcd = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
    if (const char *v = std::getenv("AMG_RR_OCC")) c->rr_occ = std::atoi(v);
    *out = c;
@@ -798,6 +799,143 @@ int amg_mat_create_device(amg_ctx *c, int nrows, int ncols, long long nnz, amg_m
    return mat_alloc(c, nrows, ncols, nnz, out);
 }
 
+// 3x3 block form of a square, diagonal-first operator with num_functions = 3
+// (dofs byVDIM: rows 3t..3t+2 are the three components of node t, e.g. the
+// DMEM elasticity problem, DMEM_BuildMatrix.cpp:442-719): block row t is
+// blocked when its three rows hold exactly the columns 3j..3j+2 of the same
+// node set {j} -- each row diagonal first, then ascending, so walking the
+// blocks (ascending j, components ascending) with the diagonal taken first
+// adds every row's products in its CSR order (bit-identical).  Other block
+// rows (the identity rows of fixed dofs) keep the CSR form.  Used only when
+// at least 90% of the block rows are blocked.
+static int build_bsr3(amg_mat *A, const int *rowptr, const int *col, const double *val)
+{
+   const int n = A->nrows, nb = n / 3;
+   if (!A->ctx->bsr3 || n % 3 || n != A->ncols || !A->diag_first || n < 3 || A->nnz < 24LL * n) return AMG_OK;
+   std::vector<int> bptr(nb + 1, 0), bdiag(nb, -1), bcol;
+   std::vector<unsigned char> mode(nb, 1);
+   std::vector<long long> src; // CSR position of every block entry (row-major 3x3), -1 unused
+   std::vector<int> js;
+   long long blocked = 0;
+   for (int t = 0; t < nb; t++) {
+      bptr[t + 1] = bptr[t];
+      const int r0 = 3 * t;
+      const int len = rowptr[r0 + 1] - rowptr[r0];
+      if (len < 3 || len % 3) continue;
+      bool ok = true;
+      js.clear();
+      for (int c = 0; c < 3 && ok; c++) {
+         const int r = r0 + c, b = rowptr[r], e = rowptr[r + 1];
+         ok = e - b == len && col[b] == r;
+         // the row minus its diagonal, ascending, with the diagonal reinserted
+         // at its sorted place: 3j, 3j+1, 3j+2 per node j
+         int prev = -1, k = b + 1;
+         std::vector<int> cols;
+         cols.reserve(len);
+         bool ins = false;
+         for (int q = 0; q < len - 1 && ok; q++, k++) {
+            const int cc = col[k];
+            if (!ins && r < cc) cols.push_back(r), ins = true;
+            ok = cc > prev && cc != r;
+            prev = cc;
+            cols.push_back(cc);
+         }
+         if (!ins) cols.push_back(r);
+         for (int q = 0; q < len && ok; q += 3) {
+            ok = cols[q] % 3 == 0 && cols[q + 1] == cols[q] + 1 && cols[q + 2] == cols[q] + 2;
+            if (ok && c == 0) js.push_back(cols[q] / 3);
+            if (ok && c > 0) ok = js[q / 3] == cols[q] / 3;
+         }
+      }
+      if (!ok) continue;
+      mode[t] = 0;
+      blocked++;
+      for (size_t q = 0; q < js.size(); q++) {
+         if (js[q] == t) bdiag[t] = bptr[t + 1];
+         bcol.push_back(js[q]);
+         bptr[t + 1]++;
+      }
+      if (bdiag[t] < 0) return AMG_OK; // unreachable: every row holds its diagonal
+      // CSR positions: row r's entry for column 3j + cc
+      const size_t base = src.size();
+      src.resize(base + js.size() * 9, -1);
+      for (int c = 0; c < 3; c++) {
+         const int r = r0 + c, b = rowptr[r], e = rowptr[r + 1];
+         for (int k = b; k < e; k++) {
+            const int j = col[k] / 3, cc = col[k] % 3;
+            const size_t q = std::lower_bound(js.begin(), js.end(), j) - js.begin();
+            src[base + q * 9 + 3 * c + cc] = k;
+         }
+      }
+   }
+   if (blocked * 10 < 9LL * nb) return AMG_OK;
+   const size_t nbk = bcol.size();
+   hipStream_t s = A->ctx->stream;
+   auto fail = [&](hipError_t e) {
+      hipFree(A->bptr), hipFree(A->bcol), hipFree(A->bdiag), hipFree(A->bmode), hipFree(A->bvi), hipFree(A->bval);
+      A->bptr = A->bcol = A->bdiag = nullptr;
+      A->bmode = nullptr;
+      A->bvi = nullptr;
+      A->bval = nullptr;
+      (void)e;
+      (void)hipGetLastError();
+      return AMG_OK; // not enough room: keep the CSR forms
+   };
+   hipError_t e = hipMalloc(&A->bptr, (nb + 1) * sizeof(int));
+   if (e == hipSuccess) e = hipMalloc(&A->bcol, std::max<size_t>(nbk, 1) * sizeof(int));
+   if (e == hipSuccess) e = hipMalloc(&A->bdiag, nb * sizeof(int));
+   if (e == hipSuccess) e = hipMalloc(&A->bmode, nb);
+   if (e != hipSuccess) return fail(e);
+   if (A->vidx) {
+      // block entries as indices into the value table (3 rows x 4 bytes)
+      std::vector<double> tab(256);
+      AMG_HIP(hipMemcpy(tab.data(), A->vtab, 256 * sizeof(double), hipMemcpyDeviceToHost));
+      std::vector<unsigned long long> keys(A->vi_n);
+      std::memcpy(keys.data(), tab.data(), A->vi_n * 8);
+      std::vector<unsigned int> bvi(std::max<size_t>(nbk * 3, 1), 0);
+      for (size_t q = 0; q < nbk * 9; q++) {
+         if (src[q] < 0) continue;
+         unsigned long long b;
+         std::memcpy(&b, &val[src[q]], 8);
+         const size_t idx = std::lower_bound(keys.begin(), keys.end(), b) - keys.begin();
+         const size_t blk = q / 9, rr = (q % 9) / 3, cc = q % 3;
+         bvi[blk * 3 + rr] |= (unsigned int)idx << (8 * cc);
+      }
+      e = hipMalloc(&A->bvi, bvi.size() * 4);
+      if (e != hipSuccess) return fail(e);
+      AMG_HIP(hipMemcpyAsync(A->bvi, bvi.data(), bvi.size() * 4, hipMemcpyHostToDevice, s));
+      AMG_HIP(hipStreamSynchronize(s));
+      A->bsr3 = 1;
+   } else {
+      std::vector<double> bv(std::max<size_t>(nbk * 9, 1), 0.0);
+      for (size_t q = 0; q < nbk * 9; q++)
+         if (src[q] >= 0) bv[q] = val[src[q]];
+      e = hipMalloc(&A->bval, bv.size() * 8);
+      if (e != hipSuccess) return fail(e);
+      AMG_HIP(hipMemcpyAsync(A->bval, bv.data(), bv.size() * 8, hipMemcpyHostToDevice, s));
+      AMG_HIP(hipStreamSynchronize(s));
+      A->bsr3 = 2;
+   }
+   AMG_HIP(hipMemcpyAsync(A->bptr, bptr.data(), (nb + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+   if (nbk) AMG_HIP(hipMemcpyAsync(A->bcol, bcol.data(), nbk * sizeof(int), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemcpyAsync(A->bdiag, bdiag.data(), nb * sizeof(int), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemcpyAsync(A->bmode, mode.data(), nb, hipMemcpyHostToDevice, s));
+   AMG_HIP(hipStreamSynchronize(s));
+   return AMG_OK;
+}
+
+extern "C" int amg_set_bsr3(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_bsr3: null context");
+   c->bsr3 = enable ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_mat_bsr3(const amg_mat *A)
+{
+   return A ? A->bsr3 : 0;
+}
+
 extern "C" int amg_csr_register(amg_ctx *c, int nrows, int ncols, long long nnz, const int *rowptr,
                                 const int *col, const double *val, int diag_first, amg_mat **out)
 {
@@ -819,6 +957,7 @@ extern "C" int amg_csr_register(amg_ctx *c, int nrows, int ncols, long long nnz,
    }
    AMG_TRY(amg_mat_finish(A));
    AMG_HIP(hipStreamSynchronize(c->stream));
+   AMG_TRY(build_bsr3(A, rowptr, col, val));
    *out = A;
    return AMG_OK;
 }
@@ -843,6 +982,12 @@ extern "C" int amg_mat_free(amg_mat *A)
    hipFree(A->pptab);
    hipFree(A->mpmask);
    hipFree(A->mpval);
+   hipFree(A->bptr);
+   hipFree(A->bcol);
+   hipFree(A->bdiag);
+   hipFree(A->bmode);
+   hipFree(A->bvi);
+   hipFree(A->bval);
    hipFree(A->pbase);
    hipFree(A->pdelta);
    delete A;

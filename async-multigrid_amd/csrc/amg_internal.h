@@ -97,6 +97,7 @@ struct amg_ctx {
    int mz_zc_auto = 1;     // shorten the chunks of small levels to keep >= 2048 workgroups
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies
+   int bsr3 = 1;           // 3x3 block form of num_functions = 3 operators
    int fuse_prolong = 0;   // prolongation fused into the first post sweep (measured slower: off)
    int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)
    int rr_occ = 0;         // 5: the fused residual + restriction compiled for 5 waves / SIMD
@@ -173,6 +174,17 @@ struct amg_mat {
    int mz27 = 0;
    int mz_dom = -1;
    double mz_domval[27] = {};
+   // 3x3 block form (num_functions = 3 operators, byVDIM): block row t = rows
+   // 3t..3t+2 whose three rows hold the same block columns, each block dense;
+   // bmode[t] = 1: the block row keeps the CSR form (identity rows of fixed
+   // dofs, irregular rows).  Block values as value-table indices (bvi: 3 rows
+   // x 4 bytes, the 4th unused) when the matrix is value-indexed, else fp64
+   // (bval: 9 per block, row-major)
+   int bsr3 = 0; // 1: value-indexed blocks, 2: fp64 blocks
+   int *bptr = nullptr, *bcol = nullptr, *bdiag = nullptr;
+   unsigned char *bmode = nullptr;
+   unsigned int *bvi = nullptr;
+   double *bval = nullptr;
 };
 
 struct amg_vec {

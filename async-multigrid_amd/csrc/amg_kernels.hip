@@ -2139,13 +2139,108 @@ Gemv gemv_mode(double alpha, double beta)
    return g;
 }
 
+// 3x3 block kernel (bsr3_kernel) for num_functions = 3 operators (the DMEM
+// elasticity problem, DMEM_BuildMatrix.cpp:442-719): lanes 3q, 3q+1, 3q+2 of
+// a wave own the three rows of block row t (21 block rows per wave) and walk
+// its blocks together -- per block one 4-byte load of the lane's three value
+// indices (or its three fp64 values), the block column, and the node's three
+// x values (shared by the three lanes).  Each row adds its diagonal first,
+// then every other entry in ascending column order: its CSR order
+// (bit-identical to the CSR kernels).  Block rows kept in CSR form (bmode 1:
+// identity rows of fixed dofs) run the CSR row loop.  Per block row the
+// value-indexed form streams 27 x (12 + 4) bytes against 81 x 5 for
+// value-indexed CSR.
+template <int NEG, bool NEED_DIAG, class Epi, bool VI>
+__global__ __launch_bounds__(256) void bsr3_kernel(const int *__restrict__ bptr, const int *__restrict__ bcol,
+                                                   const int *__restrict__ bdiag,
+                                                   const unsigned char *__restrict__ bmode,
+                                                   const unsigned int *__restrict__ bvi,
+                                                   const double *__restrict__ bval, const double *__restrict__ vtab_g,
+                                                   const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                   const double *__restrict__ val, const double *__restrict__ x,
+                                                   int t0, int t1, Epi epi)
+{
+   __shared__ double vtab[VI ? 256 : 1];
+   if (VI) vtab[threadIdx.x] = vtab_g[threadIdx.x];
+   if (VI) __syncthreads();
+   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+   if (lane >= 63) return;
+   const int t = t0 + (int)blockIdx.x * 84 + wave * 21 + lane / 3;
+   if (t >= t1) return;
+   const int c = lane % 3, i = 3 * t + c;
+   double acc = epi.init(i);
+   const double xi = x[i];
+   double a = 0.0;
+   auto madd = [&](double v, double xv) { acc = NEG ? acc - v * xv : acc + v * xv; };
+   if (bmode[t]) {
+      // CSR form: the row's entries in order
+      const int b = rowptr[i], e = rowptr[i + 1];
+      if (NEED_DIAG) a = b < e ? val[b] : 0.0;
+      for (int k = b; k < e; k++) madd(val[k], x[col[k]]);
+   } else {
+      const int k0 = bptr[t], k1 = bptr[t + 1], kd = bdiag[t];
+      auto row3 = [&](int k, double &v0, double &v1, double &v2) {
+         if (VI) {
+            const unsigned int w = bvi[(size_t)k * 3 + c];
+            v0 = vtab[w & 0xff];
+            v1 = vtab[(w >> 8) & 0xff];
+            v2 = vtab[(w >> 16) & 0xff];
+         } else {
+            const double *p = bval + (size_t)k * 9 + 3 * c;
+            v0 = p[0];
+            v1 = p[1];
+            v2 = p[2];
+         }
+      };
+      double d0, d1, d2;
+      row3(kd, d0, d1, d2);
+      a = c == 0 ? d0 : (c == 1 ? d1 : d2);
+      madd(a, xi); // the diagonal first
+      for (int k = k0; k < k1; k++) {
+         double v0, v1, v2;
+         row3(k, v0, v1, v2);
+         const double *xj = x + 3 * (size_t)bcol[k];
+         const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
+         if (k != kd || c != 0) madd(v0, x0);
+         if (k != kd || c != 1) madd(v1, x1);
+         if (k != kd || c != 2) madd(v2, x2);
+      }
+   }
+   epi.finish(i, acc, a, (pf_is_x<Epi>::value && epi_pf_vec(epi) == x) ? xi : epi.pf(i));
+}
+
+template <int NEG, bool NEED_DIAG, class Epi>
+static void launch_bsr3(hipStream_t s, const amg_mat *A, const double *x, int rb, int re, const Epi &e)
+{
+   const int t0 = rb / 3, t1 = re / 3;
+   const int nb = (t1 - t0 + 83) / 84;
+   if (A->bsr3 == 1)
+      bsr3_kernel<NEG, NEED_DIAG, Epi, true><<<nb, 256, 0, s>>>(A->bptr, A->bcol, A->bdiag, A->bmode, A->bvi,
+                                                                 nullptr, A->vtab, A->rowptr, A->col, A->val, x,
+                                                                 t0, t1, e);
+   else
+      bsr3_kernel<NEG, NEED_DIAG, Epi, false><<<nb, 256, 0, s>>>(A->bptr, A->bcol, A->bdiag, A->bmode, nullptr,
+                                                                  A->bval, nullptr, A->rowptr, A->col, A->val, x,
+                                                                  t0, t1, e);
+}
+
+static inline bool use_bsr3(const amg_mat *A, int rb, int re, const double *partials)
+{
+   return A->bsr3 && !partials && rb % 3 == 0 && re % 3 == 0;
+}
+
 void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, const Gemv &g,
             double *y, int rb, int re, double *partials)
 {
    if (re <= rb) return;
    EpiGemv e{b, y, g.init, g.scale, g.alpha, g.temp};
    const int nb = tile_blocks(rb, re);
-   if (A->didx) {
+   if (use_bsr3(A, rb, re, partials)) {
+      if (g.negacc)
+         launch_bsr3<1, false>(s, A, x, rb, re, e);
+      else
+         launch_bsr3<0, false>(s, A, x, rb, re, e);
+   } else if (A->didx) {
       if (g.negacc)
          launch_dc_op<1, false>(s, A, x, rb, re, e, partials, nb);
       else
@@ -2187,7 +2282,12 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
 {
    if (re <= rb) return;
    const int nb = tile_blocks(rb, re);
-   if (A->didx) {
+   if (use_bsr3(A, rb, re, nullptr)) {
+      if (l1)
+         launch_bsr3<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out});
+      else
+         launch_bsr3<1, true>(s, A, x, rb, re, EpiJacobi{f, x, out, omega});
+   } else if (A->didx) {
       if (l1)
          launch_dc_op<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out}, nullptr, nb);
       else
@@ -2226,7 +2326,12 @@ void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const dou
    if (re <= rb) return;
    const int nb = tile_blocks(rb, re);
    EpiResJacobi e{f, x, l1, r, unext, omega};
-   if (A->didx) {
+   if (use_bsr3(A, rb, re, partials)) {
+      if (l1)
+         launch_bsr3<1, false>(s, A, x, rb, re, e);
+      else
+         launch_bsr3<1, true>(s, A, x, rb, re, e);
+   } else if (A->didx) {
       if (l1)
          launch_dc_op<1, false>(s, A, x, rb, re, e, partials, nb);
       else

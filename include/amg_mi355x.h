@@ -223,6 +223,17 @@ int amg_mat_master_pattern(const amg_mat *A);
  * amg_mat_plane_march: the plane size P (0: not marched);
  * amg_mat_march_points: the marched stencil, 7 or 27 (0: not marched). */
 int amg_set_plane_march(amg_ctx *ctx, int enable, int zc, int xcd);
+/* 3x3 block form of num_functions = 3 operators (dofs byVDIM, the DMEM
+ * elasticity problem DMEM_BuildMatrix.cpp:442-719): block rows whose three rows
+ * hold the same dense 3x3 blocks are stored as blocks -- value-table indices
+ * when the matrix is value-indexed, else fp64 -- and the SpMV / Jacobi kernels
+ * walk them three lanes per block row (diagonal first, then ascending: the
+ * CSR order, bit-identical); the identity rows of fixed dofs keep the CSR
+ * form.  Used when >= 90% of the block rows block.  amg_set_bsr3(ctx, 0) (env
+ * AMG_BSR3=0) keeps CSR for matrices registered afterwards;
+ * amg_mat_bsr3: 1 value-indexed blocks, 2 fp64 blocks, 0 not blocked. */
+int amg_set_bsr3(amg_ctx *ctx, int enable);
+int amg_mat_bsr3(const amg_mat *A);
 int amg_mat_plane_march(const amg_mat *A);
 int amg_mat_march_points(const amg_mat *A);
 int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz);
