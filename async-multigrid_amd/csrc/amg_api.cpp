@@ -869,57 +869,86 @@ static int build_bsr3(amg_mat *A, const int *rowptr, const int *col, const doubl
       }
    }
    if (blocked * 10 < 9LL * nb) return AMG_OK;
-   const size_t nbk = bcol.size();
+   // sliced layout (21 block rows per slice, padded to the slice's longest)
+   constexpr int SL = 21;
+   const int ns = (nb + SL - 1) / SL;
+   std::vector<long long> soff(ns + 1, 0);
+   for (int sl = 0; sl < ns; sl++) {
+      int w = 0;
+      for (int t = sl * SL; t < std::min(nb, (sl + 1) * SL); t++) w = std::max(w, bptr[t + 1] - bptr[t]);
+      soff[sl + 1] = soff[sl] + (long long)w * SL;
+   }
+   const size_t nslot = (size_t)soff[ns];
+   std::vector<int> scol(std::max<size_t>(nslot, 1), 0), bdk(nb, 0);
+   std::vector<unsigned char> bcnt(nb, 0);
+   for (int t = 0; t < nb; t++) {
+      const int cnt = bptr[t + 1] - bptr[t];
+      if (cnt > 255) return AMG_OK; // block rows of more than 255 blocks: keep CSR
+      bcnt[t] = (unsigned char)cnt;
+      bdk[t] = mode[t] ? 0 : bdiag[t] - bptr[t];
+      const int sl = t / SL, q = t % SL;
+      const int w = (int)((soff[sl + 1] - soff[sl]) / SL);
+      for (int k = 0; k < w; k++) scol[(size_t)soff[sl] + (size_t)k * SL + q] = k < cnt ? bcol[bptr[t] + k] : t;
+   }
    hipStream_t s = A->ctx->stream;
-   auto fail = [&](hipError_t e) {
-      hipFree(A->bptr), hipFree(A->bcol), hipFree(A->bdiag), hipFree(A->bmode), hipFree(A->bvi), hipFree(A->bval);
-      A->bptr = A->bcol = A->bdiag = nullptr;
+   auto fail = [&]() {
+      hipFree(A->soff), hipFree(A->bcol), hipFree(A->bdiag), hipFree(A->bmode), hipFree(A->bvi), hipFree(A->bval);
+      A->soff = nullptr;
+      A->bcol = A->bdiag = nullptr;
       A->bmode = nullptr;
       A->bvi = nullptr;
       A->bval = nullptr;
-      (void)e;
       (void)hipGetLastError();
       return AMG_OK; // not enough room: keep the CSR forms
    };
-   hipError_t e = hipMalloc(&A->bptr, (nb + 1) * sizeof(int));
-   if (e == hipSuccess) e = hipMalloc(&A->bcol, std::max<size_t>(nbk, 1) * sizeof(int));
+   hipError_t e = hipMalloc(&A->soff, (ns + 1) * sizeof(long long));
+   if (e == hipSuccess) e = hipMalloc(&A->bcol, scol.size() * sizeof(int));
    if (e == hipSuccess) e = hipMalloc(&A->bdiag, nb * sizeof(int));
    if (e == hipSuccess) e = hipMalloc(&A->bmode, nb);
-   if (e != hipSuccess) return fail(e);
+   if (e != hipSuccess) return fail();
+   // slot of block k of block row t
+   auto slot = [&](int t, int k) { return (size_t)soff[t / SL] + (size_t)k * SL + t % SL; };
    if (A->vidx) {
       // block entries as indices into the value table (3 rows x 4 bytes)
       std::vector<double> tab(256);
       AMG_HIP(hipMemcpy(tab.data(), A->vtab, 256 * sizeof(double), hipMemcpyDeviceToHost));
       std::vector<unsigned long long> keys(A->vi_n);
       std::memcpy(keys.data(), tab.data(), A->vi_n * 8);
-      std::vector<unsigned int> bvi(std::max<size_t>(nbk * 3, 1), 0);
-      for (size_t q = 0; q < nbk * 9; q++) {
-         if (src[q] < 0) continue;
-         unsigned long long b;
-         std::memcpy(&b, &val[src[q]], 8);
-         const size_t idx = std::lower_bound(keys.begin(), keys.end(), b) - keys.begin();
-         const size_t blk = q / 9, rr = (q % 9) / 3, cc = q % 3;
-         bvi[blk * 3 + rr] |= (unsigned int)idx << (8 * cc);
-      }
+      std::vector<unsigned int> bvi(std::max<size_t>(nslot * 3, 1), 0);
+      for (int t = 0; t < nb; t++)
+         for (int k = 0; k < bptr[t + 1] - bptr[t]; k++)
+            for (int q = 0; q < 9; q++) {
+               const long long sp = src[(size_t)(bptr[t] + k) * 9 + q];
+               if (sp < 0) continue;
+               unsigned long long b;
+               std::memcpy(&b, &val[sp], 8);
+               const size_t idx = std::lower_bound(keys.begin(), keys.end(), b) - keys.begin();
+               bvi[slot(t, k) * 3 + q / 3] |= (unsigned int)idx << (8 * (q % 3));
+            }
       e = hipMalloc(&A->bvi, bvi.size() * 4);
-      if (e != hipSuccess) return fail(e);
+      if (e != hipSuccess) return fail();
       AMG_HIP(hipMemcpyAsync(A->bvi, bvi.data(), bvi.size() * 4, hipMemcpyHostToDevice, s));
       AMG_HIP(hipStreamSynchronize(s));
       A->bsr3 = 1;
    } else {
-      std::vector<double> bv(std::max<size_t>(nbk * 9, 1), 0.0);
-      for (size_t q = 0; q < nbk * 9; q++)
-         if (src[q] >= 0) bv[q] = val[src[q]];
+      std::vector<double> bv(std::max<size_t>(nslot * 9, 1), 0.0);
+      for (int t = 0; t < nb; t++)
+         for (int k = 0; k < bptr[t + 1] - bptr[t]; k++)
+            for (int q = 0; q < 9; q++) {
+               const long long sp = src[(size_t)(bptr[t] + k) * 9 + q];
+               if (sp >= 0) bv[slot(t, k) * 9 + q] = val[sp];
+            }
       e = hipMalloc(&A->bval, bv.size() * 8);
-      if (e != hipSuccess) return fail(e);
+      if (e != hipSuccess) return fail();
       AMG_HIP(hipMemcpyAsync(A->bval, bv.data(), bv.size() * 8, hipMemcpyHostToDevice, s));
       AMG_HIP(hipStreamSynchronize(s));
       A->bsr3 = 2;
    }
-   AMG_HIP(hipMemcpyAsync(A->bptr, bptr.data(), (nb + 1) * sizeof(int), hipMemcpyHostToDevice, s));
-   if (nbk) AMG_HIP(hipMemcpyAsync(A->bcol, bcol.data(), nbk * sizeof(int), hipMemcpyHostToDevice, s));
-   AMG_HIP(hipMemcpyAsync(A->bdiag, bdiag.data(), nb * sizeof(int), hipMemcpyHostToDevice, s));
-   AMG_HIP(hipMemcpyAsync(A->bmode, mode.data(), nb, hipMemcpyHostToDevice, s));
+   for (int t = 0; t < nb; t++) bcnt[t] = mode[t] ? 0 : bcnt[t];
+   AMG_HIP(hipMemcpyAsync(A->soff, soff.data(), (ns + 1) * sizeof(long long), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemcpyAsync(A->bcol, scol.data(), scol.size() * sizeof(int), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemcpyAsync(A->bdiag, bdk.data(), nb * sizeof(int), hipMemcpyHostToDevice, s));
+   AMG_HIP(hipMemcpyAsync(A->bmode, bcnt.data(), nb, hipMemcpyHostToDevice, s));
    AMG_HIP(hipStreamSynchronize(s));
    return AMG_OK;
 }
@@ -982,7 +1011,7 @@ extern "C" int amg_mat_free(amg_mat *A)
    hipFree(A->pptab);
    hipFree(A->mpmask);
    hipFree(A->mpval);
-   hipFree(A->bptr);
+   hipFree(A->soff);
    hipFree(A->bcol);
    hipFree(A->bdiag);
    hipFree(A->bmode);

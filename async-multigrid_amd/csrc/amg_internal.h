@@ -180,8 +180,14 @@ struct amg_mat {
    // dofs, irregular rows).  Block values as value-table indices (bvi: 3 rows
    // x 4 bytes, the 4th unused) when the matrix is value-indexed, else fp64
    // (bval: 9 per block, row-major)
+   // Sliced layout: slice s = block rows 21s..21s+20 (one wave), padded to
+   // its longest block row; block k of the slice's block row q sits at slot
+   // soff[s] + 21 k + q, so a wave's loads of block k are contiguous.
+   // bcnt[t] = blocks of block row t (0: CSR form), bdiag[t] = its diagonal
+   // block's index k
    int bsr3 = 0; // 1: value-indexed blocks, 2: fp64 blocks
-   int *bptr = nullptr, *bcol = nullptr, *bdiag = nullptr;
+   long long *soff = nullptr;
+   int *bcol = nullptr, *bdiag = nullptr;
    unsigned char *bmode = nullptr;
    unsigned int *bvi = nullptr;
    double *bval = nullptr;

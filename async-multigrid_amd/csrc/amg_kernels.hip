@@ -2151,9 +2151,9 @@ Gemv gemv_mode(double alpha, double beta)
 // value-indexed form streams 27 x (12 + 4) bytes against 81 x 5 for
 // value-indexed CSR.
 template <int NEG, bool NEED_DIAG, class Epi, bool VI>
-__global__ __launch_bounds__(256) void bsr3_kernel(const int *__restrict__ bptr, const int *__restrict__ bcol,
+__global__ __launch_bounds__(256) void bsr3_kernel(const long long *__restrict__ soff, const int *__restrict__ bcol,
                                                    const int *__restrict__ bdiag,
-                                                   const unsigned char *__restrict__ bmode,
+                                                   const unsigned char *__restrict__ bcnt,
                                                    const unsigned int *__restrict__ bvi,
                                                    const double *__restrict__ bval, const double *__restrict__ vtab_g,
                                                    const int *__restrict__ rowptr, const int *__restrict__ col,
@@ -2165,45 +2165,62 @@ __global__ __launch_bounds__(256) void bsr3_kernel(const int *__restrict__ bptr,
    if (VI) __syncthreads();
    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
    if (lane >= 63) return;
-   const int t = t0 + (int)blockIdx.x * 84 + wave * 21 + lane / 3;
-   if (t >= t1) return;
-   const int c = lane % 3, i = 3 * t + c;
+   const int sl = t0 / 21 + (int)blockIdx.x * 4 + wave, q = lane / 3, c = lane % 3;
+   const int t = sl * 21 + q;
+   if (t < t0 || t >= t1) return;
+   const int i = 3 * t + c;
    double acc = epi.init(i);
    const double xi = x[i];
    double a = 0.0;
    auto madd = [&](double v, double xv) { acc = NEG ? acc - v * xv : acc + v * xv; };
-   if (bmode[t]) {
+   const int cnt = bcnt[t];
+   if (cnt == 0) {
       // CSR form: the row's entries in order
       const int b = rowptr[i], e = rowptr[i + 1];
       if (NEED_DIAG) a = b < e ? val[b] : 0.0;
       for (int k = b; k < e; k++) madd(val[k], x[col[k]]);
    } else {
-      const int k0 = bptr[t], k1 = bptr[t + 1], kd = bdiag[t];
-      auto row3 = [&](int k, double &v0, double &v1, double &v2) {
+      const long long base = soff[sl] + q;
+      auto row3 = [&](long long sp, double &v0, double &v1, double &v2) {
          if (VI) {
-            const unsigned int w = bvi[(size_t)k * 3 + c];
+            const unsigned int w = bvi[sp * 3 + c];
             v0 = vtab[w & 0xff];
             v1 = vtab[(w >> 8) & 0xff];
             v2 = vtab[(w >> 16) & 0xff];
          } else {
-            const double *p = bval + (size_t)k * 9 + 3 * c;
+            const double *p = bval + sp * 9 + 3 * c;
             v0 = p[0];
             v1 = p[1];
             v2 = p[2];
          }
       };
+      const int kd = bdiag[t];
       double d0, d1, d2;
-      row3(kd, d0, d1, d2);
+      row3(base + 21LL * kd, d0, d1, d2);
       a = c == 0 ? d0 : (c == 1 ? d1 : d2);
       madd(a, xi); // the diagonal first
-      for (int k = k0; k < k1; k++) {
-         double v0, v1, v2;
-         row3(k, v0, v1, v2);
-         const double *xj = x + 3 * (size_t)bcol[k];
-         const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
-         if (k != kd || c != 0) madd(v0, x0);
-         if (k != kd || c != 1) madd(v1, x1);
-         if (k != kd || c != 2) madd(v2, x2);
+      // blocks in chunks of U, the wave's loads of block k contiguous; every
+      // load of a chunk in flight before its products are added in order
+      constexpr int U = 9;
+      for (int kc = 0; kc < cnt; kc += U) {
+         int jj[U];
+         double vv[U][3];
+#pragma unroll
+         for (int u = 0; u < U; u++) {
+            const long long sp = base + 21LL * min(kc + u, cnt - 1);
+            jj[u] = bcol[sp];
+            row3(sp, vv[u][0], vv[u][1], vv[u][2]);
+         }
+#pragma unroll
+         for (int u = 0; u < U; u++) {
+            const int k = kc + u;
+            if (k >= cnt) break;
+            const double *xj = x + 3 * (size_t)jj[u];
+            const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
+            if (k != kd || c != 0) madd(vv[u][0], x0);
+            if (k != kd || c != 1) madd(vv[u][1], x1);
+            if (k != kd || c != 2) madd(vv[u][2], x2);
+         }
       }
    }
    epi.finish(i, acc, a, (pf_is_x<Epi>::value && epi_pf_vec(epi) == x) ? xi : epi.pf(i));
@@ -2213,20 +2230,23 @@ template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_bsr3(hipStream_t s, const amg_mat *A, const double *x, int rb, int re, const Epi &e)
 {
    const int t0 = rb / 3, t1 = re / 3;
-   const int nb = (t1 - t0 + 83) / 84;
+   const int nsl = (t1 - t0 + 20) / 21;
+   const int nb = (nsl + 3) / 4;
    if (A->bsr3 == 1)
-      bsr3_kernel<NEG, NEED_DIAG, Epi, true><<<nb, 256, 0, s>>>(A->bptr, A->bcol, A->bdiag, A->bmode, A->bvi,
+      bsr3_kernel<NEG, NEED_DIAG, Epi, true><<<nb, 256, 0, s>>>(A->soff, A->bcol, A->bdiag, A->bmode, A->bvi,
                                                                  nullptr, A->vtab, A->rowptr, A->col, A->val, x,
                                                                  t0, t1, e);
    else
-      bsr3_kernel<NEG, NEED_DIAG, Epi, false><<<nb, 256, 0, s>>>(A->bptr, A->bcol, A->bdiag, A->bmode, nullptr,
+      bsr3_kernel<NEG, NEED_DIAG, Epi, false><<<nb, 256, 0, s>>>(A->soff, A->bcol, A->bdiag, A->bmode, nullptr,
                                                                   A->bval, nullptr, A->rowptr, A->col, A->val, x,
                                                                   t0, t1, e);
 }
 
+// the block form serves row ranges that start on a slice (21 block rows) and
+// end on a slice or at the last row
 static inline bool use_bsr3(const amg_mat *A, int rb, int re, const double *partials)
 {
-   return A->bsr3 && !partials && rb % 3 == 0 && re % 3 == 0;
+   return A->bsr3 && !partials && rb % 63 == 0 && (re % 63 == 0 || re == A->nrows) && A->nrows % 3 == 0;
 }
 
 void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, const Gemv &g,

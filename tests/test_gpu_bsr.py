@@ -44,7 +44,8 @@ def test_bsr3_bitwise(amg, oracle, ctx, elast, r, vi):
             y = ctx.vec(n)
             amg.smem.SMEM_SpGEMV(ctx, M, x, f, ab[0], ab[1], y, 0, n)
             o.append(y.download())
-        for rb, re in ((3, n - 6), (1, n - 2)):  # block-aligned slice (blocks) and not (CSR)
+        # slice-aligned row ranges (63 rows: blocks) and others (CSR)
+        for rb, re in ((63, 63 * (n // 63 - 1)), (126, n), (3, n - 6), (1, n - 2)):
             y = ctx.vec(_vecs(n, 63))
             amg.smem.SMEM_SpGEMV(ctx, M, x, f, -1.0, 1.0, y, rb, re)
             o.append(y.download())
