@@ -21,7 +21,8 @@ CAL = 2 << 30  # 2 GiB per calibration stream, far beyond the 256 MiB Infinity C
 for mode in range(5):
     amg.check(lib.amg_pmc_calib(ctx.h, mode, CAL))
 g = amg.Gen(n)
-H = amg.build_hierarchy(ctx, g, amg.default_opts(smooth_weight=0.8, num_cycles=1 << 30, tol=0.0))
+H = amg.build_hierarchy(ctx, g, amg.default_opts(smooth_weight=0.8, num_cycles=1 << 30, tol=0.0,
+                                                  reuse_outer_residual=2))
 f = ctx.vec(amg.rhs_rand(0, n ** 3))
 H.solve_start(f, ctx.vec(n ** 3))
 H.iterate(3)
