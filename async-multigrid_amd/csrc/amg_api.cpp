@@ -96,6 +96,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_MZ_EDGE")) c->mz_edge = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
    if (const char *v = std::getenv("AMG_RR_OCC")) c->rr_occ = std::atoi(v);
    *out = c;
@@ -640,6 +641,35 @@ static int build_master_pattern(amg_mat *A)
          }
          if (dom >= 0)
             for (int j = 0; j < J; j++) A->mz_domval[j] = mv[((size_t)dom * J + j) * 2];
+         // x-edge pair patterns (the waves at both ends of every line)
+         if (dom >= 0) {
+            unsigned long long lo_x = 0, hi_y = 0; // row 2t's mask without dx = -1, row 2t+1's without +1
+            for (int j = 0; j < 27; j++) {
+               const int L = j == 0 ? 13 : (j <= 13 ? j - 1 : j), dx = L % 3 - 1;
+               if (dx != -1) lo_x |= 1ull << (2 * j);
+               if (dx != 1) hi_y |= 2ull << (2 * j);
+            }
+            const unsigned long long even = 0x5555555555555555ull & full, odd = 0xAAAAAAAAAAAAAAAAull & full;
+            long long best_lo = 0, best_hi = 0;
+            for (int t = 0; t < T; t++) {
+               auto same = [&](int j, int r) {
+                  return std::memcmp(&mv[((size_t)t * J + j) * 2 + r], &A->mz_domval[j], 8) == 0;
+               };
+               if (mask[t] == (lo_x | odd) && cnt[t] > best_lo) {
+                  bool ok = true;
+                  for (int j = 0; j < J && ok; j++) ok = same(j, 1) && (!((lo_x >> (2 * j)) & 1) || same(j, 0));
+                  if (ok) A->mz_xlo = t, best_lo = cnt[t];
+               }
+               if (mask[t] == (even | hi_y) && cnt[t] > best_hi) {
+                  bool ok = true;
+                  for (int j = 0; j < J && ok; j++) ok = same(j, 0);
+                  if (ok) {
+                     A->mz_xhi = t, best_hi = cnt[t];
+                     for (int j = 0; j < J; j++) A->mz_hival[j] = mv[((size_t)t * J + j) * 2 + 1];
+                  }
+               }
+            }
+         }
       }
       if (ok) {
          A->mz_P = P;
@@ -666,6 +696,7 @@ static void drop_pair_forms(amg_mat *A)
    A->mp_J = A->mp_uni = 0;
    A->mz_P = A->mz_S = A->mz27 = 0;
    A->mz_dom = -1;
+   A->mz_xlo = A->mz_xhi = -1;
 }
 
 int amg_mat_finish(amg_mat *A)

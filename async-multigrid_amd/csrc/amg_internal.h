@@ -94,6 +94,7 @@ struct amg_ctx {
    int pair_anchor16 = 0;  // slab-compressed anchors of pair-coded P/R (measured slower: off)
    int plane_march = 1;    // plane-marching kernel for 7-pt box-grid masters (csr_mz_kernel)
    int mz_zc = 16;         // planes per workgroup chunk of the plane-marching kernel
+   int mz_edge = 1;        // x-edge pair patterns on the 27-pt march's fast path
    int mz_zc_auto = 1;     // shorten the chunks of small levels to keep >= 2048 workgroups
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies
@@ -174,6 +175,12 @@ struct amg_mat {
    int mz27 = 0;
    int mz_dom = -1;
    double mz_domval[27] = {};
+   // x-edge pair patterns of the fast path: mz_xlo = row 2t at the box's low
+   // x face (its dx = -1 entries unused, values the dominant ones), row 2t+1
+   // dominant; mz_xhi = row 2t dominant, row 2t+1 at the high x face (dx = +1
+   // unused, values mz_hival); -1: none
+   int mz_xlo = -1, mz_xhi = -1;
+   double mz_hival[27] = {};
    // 3x3 block form (num_functions = 3 operators, byVDIM): block row t = rows
    // 3t..3t+2 whose three rows hold the same block columns, each block dense;
    // bmode[t] = 1: the block row keeps the CSR form (identity rows of fixed

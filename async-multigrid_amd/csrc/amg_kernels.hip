@@ -1161,11 +1161,15 @@ __device__ __forceinline__ Ln4 mz27_line(v2d v, double e, int lane)
    return Ln4{l, v.x, v.y, r};
 }
 
+struct Val27 {
+   double v[27];
+};
+
 template <int NEG, bool NEED_DIAG, class Epi, bool UNI>
 __global__ __launch_bounds__(256) void csr_mz27_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
-   const v2d *__restrict__ mval_g, MpSten Sv, int dom, const double *__restrict__ x, int P, int S, int nz,
-   int zc, int npb, int xcd, Epi epi, double *__restrict__ partials)
+   const v2d *__restrict__ mval_g, MpSten Sv, int dom, int xlo, int xhi, Val27 Hv, const double *__restrict__ x,
+   int P, int S, int nz, int zc, int npb, int xcd, Epi epi, double *__restrict__ partials)
 {
    constexpr unsigned long long FULL = (1ull << 54) - 1;
    const bool xc_pf = pf_is_x<Epi>::value && epi_pf_vec(epi) == x;
@@ -1206,9 +1210,14 @@ __global__ __launch_bounds__(256) void csr_mz27_kernel(
          for (int d = 0; d < 3; d++) mz27_load(x, (long long)row + 2LL * P + (d - 1) * S, Nu, lane, nv[d], ne[d]);
       }
       const int pid = ppat[row >> 1];
-      v2d acc = epi.init2((int)row);
+      const v2d acc0 = epi.init2((int)row);
+      v2d acc = acc0;
       const v2d pf = xc_pf ? v2d{X[1][1].a, X[1][1].b} : epi.pf2((int)row);
-      const bool fast = UNI ? __all(mtab[pid] == FULL) : __all(pid == dom);
+      // fast path: every pair of the wave dominant, or an x-edge pair whose
+      // edge row is then recomputed on its own (its entries in master order,
+      // the dx = -1 / +1 ones skipped, its own values) -- the ends of every
+      // line, which otherwise send every wave of a short line to the LDS path
+      const bool fast = UNI ? __all(mtab[pid] == FULL) : __all(pid == dom || pid == xlo || pid == xhi);
       if (fast) {
 #pragma unroll
          for (int j = 0; j < 27; j++) {
@@ -1216,6 +1225,26 @@ __global__ __launch_bounds__(256) void csr_mz27_kernel(
             const double v = Sv.val[j];
             acc.x = NEG ? acc.x - v * o.x : acc.x + v * o.x;
             acc.y = NEG ? acc.y - v * o.y : acc.y + v * o.y;
+         }
+         if (!UNI && pid == xlo) {
+            acc.x = acc0.x;
+#pragma unroll
+            for (int j = 0; j < 27; j++) {
+               const int L = mz27_slot(j);
+               if (L % 3 == 0) continue; // dx = -1
+               const double o = mz27_opnd(X, L).x, v = Sv.val[j];
+               acc.x = NEG ? acc.x - v * o : acc.x + v * o;
+            }
+         }
+         if (!UNI && pid == xhi) {
+            acc.y = acc0.y;
+#pragma unroll
+            for (int j = 0; j < 27; j++) {
+               const int L = mz27_slot(j);
+               if (L % 3 == 2) continue; // dx = +1
+               const double o = mz27_opnd(X, L).y, v = Hv.v[j];
+               acc.y = NEG ? acc.y - v * o : acc.y + v * o;
+            }
          }
       } else {
          const unsigned long long mk = mtab[pid];
@@ -1230,7 +1259,10 @@ __global__ __launch_bounds__(256) void csr_mz27_kernel(
          }
       }
       v2d dg{0.0, 0.0};
-      if (NEED_DIAG) dg = (UNI || fast) ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 27];
+      if (NEED_DIAG) {
+         dg = (UNI || fast) ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 27];
+         if (!UNI && fast && pid == xhi) dg.y = Hv.v[0];
+      }
       const v2d out = epi.finish2((int)row, acc, dg, pf);
       if (partials) {
          double a = out.x * out.x, b = out.y * out.y;
@@ -1269,13 +1301,18 @@ static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const 
    const int P = A->mz_P, nz = A->nrows / P, zc = mz_chunk(A, nz, P / 512);
    const int npb = P / 512, nch = (nz + zc - 1) / zc;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+   Val27 H;
+   for (int j = 0; j < 27; j++) H.v[j] = A->mz_hival[j];
+   // the x-edge fast path needs the dominant pattern (ctx->mz_edge: on)
+   const int xlo = A->ctx->mz_edge ? A->mz_xlo : -1, xhi = A->ctx->mz_edge ? A->mz_xhi : -1;
    if (A->mp_uni)
       csr_mz27_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, -1, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);
+         A->ppat, A->mpmask, A->pp_n, mv, S, -1, -1, -1, H, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e,
+         partials);
    else
       csr_mz27_kernel<NEG, NEED_DIAG, Epi, false><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, A->mz_dom, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e,
-         partials);
+         A->ppat, A->mpmask, A->pp_n, mv, S, A->mz_dom, A->mz_dom >= 0 ? xlo : -1, A->mz_dom >= 0 ? xhi : -1, H,
+         x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);
 }
 
 // ---------------------------------------------------------------------------
