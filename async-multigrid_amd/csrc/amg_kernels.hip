@@ -1403,7 +1403,13 @@ struct Val7 {
    double v[7];
 };
 
-template <bool UNI, int LC, int OCC = 1>
+// RING: the wave-edge residuals travel through an LDS ring of RR planes
+// between adjacent waves, ordered by per-wave produced / consumed plane
+// counters (release fence + flag, acquire spin) instead of a workgroup
+// barrier per plane, so the four waves march loosely coupled
+constexpr int AMG_RR_RING = 4;
+
+template <bool UNI, int LC, int OCC = 1, bool RING = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void mz_res_restrict_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, Val7 Sv7, const double *__restrict__ x, const double *__restrict__ f,
@@ -1416,7 +1422,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
    for (int j = 0; j < 7; j++) Sv.val[j] = Sv7.v[j];
    __shared__ unsigned long long mtab[256];
    __shared__ v2d mval[UNI ? 1 : 256 * 7];
-   __shared__ double xr[2][4][NL];
+   __shared__ double xr[RING ? AMG_RR_RING : 2][4][NL];
+   __shared__ int prod[4], cons[4]; // RING: planes produced by wave w's lane 0, consumed by wave w's lane 63
    __shared__ double wl[27]; // R's weights (uniform LDS reads)
    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
    if (tid < np) mtab[tid] = mmask_g[tid];
@@ -1451,6 +1458,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
    double acc[LC];
 #pragma unroll
    for (int c = 0; c < LC; c++) acc[c] = 0.0;
+   if (RING && tid < 4) prod[tid] = cons[tid] = kf0 - 1;
+   // wave wv reads from wave wv + 1 when both hold the same line group
+   const int wpl = lpl >> 6; // waves per line group (lpl > 64)
+   const bool has_next = lpl > 64 && (wv + 1) % wpl != 0;
+   const bool has_prev = lpl > 64 && wv % wpl != 0;
    __syncthreads();
    for (int k = kf0; k <= kf1; k++) {
       const unsigned base = (unsigned)k * P + pos0;
@@ -1498,7 +1510,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       double r2[NL];
 #pragma unroll
       for (int i = 0; i < NL; i++) r2[i] = __shfl_down(r[i].x, 1, 64);
-      if (lpl > 64) {
+      if (RING && lpl > 64) {
+         volatile int *vp = prod, *vc = cons;
+         const int slot = (k - kf0) % AMG_RR_RING;
+         if (has_prev && lane == 0) {
+            // slot free once wave wv - 1 consumed plane k - RING
+            while (vc[wv - 1] < k - AMG_RR_RING) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int i = 0; i < NL; i++) xr[slot][wv][i] = r[i].x;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            vp[wv] = k;
+         }
+         if (has_next && lane == 63) {
+            while (vp[wv + 1] < k) __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+            for (int i = 0; i < NL; i++) r2[i] = xr[slot][wv + 1][i];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            vc[wv] = k;
+         }
+      } else if (lpl > 64) {
          if (lane == 0)
 #pragma unroll
             for (int i = 0; i < NL; i++) xr[k & 1][wv][i] = r[i].x;
@@ -1558,6 +1589,7 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
    if (A->mp_uni) {
       if (LC == 2) AMG_RR(true, 2);
       else if (A->ctx->rr_occ == 5) AMG_RR(true, 1, 5);
+      else if (A->ctx->rr_ring) AMG_RR(true, 1, 1, true);
       else AMG_RR(true, 1);
    } else {
       if (LC == 2) AMG_RR(false, 2);
