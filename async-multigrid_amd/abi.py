@@ -60,7 +60,7 @@ AMG_DELAY_NONE, AMG_DELAY_ONE, AMG_DELAY_SOME, AMG_DELAY_ALL, AMG_FAIL_ONE = 0, 
 class AmgClassicalOpts(C.Structure):
     _fields_ = [("coarsen_type", _i), ("interp_type", _i), ("strong_threshold", _d),
                 ("max_row_sum", _d), ("max_levels", _i), ("max_coarse_size", _i),
-                ("num_functions", _i), ("seed", C.c_ulonglong)]
+                ("num_functions", _i), ("seed", C.c_ulonglong), ("device", _i)]
 
 
 AMG_COARSEN_PMIS, AMG_COARSEN_PMIS_FIXED, AMG_COARSEN_HMIS = 8, 9, 10

@@ -19,12 +19,21 @@
 // Levels are built until the coarse operator has at most max_coarse_size rows,
 // coarsening stalls, or max_levels is reached.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstdint>
 #include <set>
 #include <vector>
 
 #include "amg_internal.h"
+
+// amg_spgemm.hip: C = A B on a GPU, bit-identical to spgemm() below
+int amg_spgemm_device(int device, int An, const std::vector<int> &arp, const std::vector<int> &acj,
+                      const std::vector<double> &av, int Bn, const std::vector<int> &brp,
+                      const std::vector<int> &bcj, const std::vector<double> &bv, int Bm, std::vector<int> &crp,
+                      std::vector<int> &ccj, std::vector<double> &cv);
 
 namespace {
 
@@ -412,6 +421,7 @@ extern "C" void amg_classical_opts_default(amg_classical_opts *o)
    o->max_coarse_size = 9; // hypre's default
    o->num_functions = 1;
    o->seed = 2747;
+   o->device = -1;
 }
 
 extern "C" int amg_classical_setup(const amg_classical_opts *o, int n, const int *rowptr, const int *col,
@@ -446,21 +456,46 @@ extern "C" int amg_classical_setup(const amg_classical_opts *o, int n, const int
       if (A.n <= o->max_coarse_size) break;
       const int nfun = A.n % o->num_functions == 0 ? o->num_functions : 1;
       HCsr S, ST;
+      const bool tm = std::getenv("AMG_CLASSICAL_TIMING") != nullptr;
+      auto now = [] { return std::chrono::steady_clock::now(); };
+      auto t0 = now();
       strength(A, o->strong_threshold, o->max_row_sum, nfun, S);
       transpose_pattern(S, ST);
+      auto t1 = now();
       std::vector<int> cf;
       if (o->coarsen_type == AMG_COARSEN_HMIS)
          coarsen_rs(S, ST, cf);
       else
          coarsen_pmis(S, ST, seed + (uint64_t)l * 7919ULL, cf);
+      auto t2 = now();
       HCsr P;
       int nc = 0;
       interpolation(A, S, cf, o->interp_type, nfun, P, &nc);
+      auto t3 = now();
       if (nc == 0 || nc == A.n) break; // coarsening stalled
       HCsr R, AP, Ac;
       transpose(P, R);
-      spgemm(A, P, AP);
-      spgemm(R, AP, Ac);
+      if (o->device >= 0) {
+         AP.n = A.n, AP.m = P.m;
+         Ac.n = R.n, Ac.m = AP.m;
+         int st = amg_spgemm_device(o->device, A.n, A.rp, A.cj, A.v, P.n, P.rp, P.cj, P.v, P.m, AP.rp, AP.cj, AP.v);
+         if (st == AMG_OK)
+            st = amg_spgemm_device(o->device, R.n, R.rp, R.cj, R.v, AP.n, AP.rp, AP.cj, AP.v, AP.m, Ac.rp, Ac.cj,
+                                   Ac.v);
+         if (st != AMG_OK) {
+            delete H;
+            return st;
+         }
+      } else {
+         spgemm(A, P, AP);
+         spgemm(R, AP, Ac);
+      }
+      auto t4 = now();
+      if (tm) {
+         auto d = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
+         std::fprintf(stderr, "[classical] level %d n=%d: strength %.2fs coarsen %.2fs interp %.2fs RAP %.2fs\n", l,
+                      A.n, d(t0, t1), d(t1, t2), d(t2, t3), d(t3, t4));
+      }
       H->cf.push_back(std::move(cf));
       H->P.push_back(std::move(P));
       H->R.push_back(std::move(R));

@@ -415,6 +415,9 @@ typedef struct {
    int max_coarse_size;     /* stop when a level has at most this many rows       */
    int num_functions;       /* hypre.num_functions: unknowns per node (dof i % k)  */
    unsigned long long seed; /* PMIS random measure                                */
+   int device;              /* >= 0: the Galerkin products A P and R (A P) run on this
+                               GPU (amg_spgemm.hip: one lane per row, the host's
+                               Gustavson order -- bit-identical); -1: on the host */
 } amg_classical_opts;
 void amg_classical_opts_default(amg_classical_opts *o); /* the SMEM parameters */
 int amg_classical_setup(const amg_classical_opts *o, int n, const int *rowptr, const int *col,

@@ -127,3 +127,27 @@ def test_problem_file(amg, oracle, ctx, tmp_path):
     f = amg.rhs_rand(0, n)
     u, hist = compare_solve(amg, oracle, ctx, host, opts, f)
     assert hist[-1] < 1e-2 * hist[0]
+
+
+@pytest.mark.parametrize("case", ["lap20-hmis", "elast2-pmis", "elast3-pmis"])
+def test_galerkin_on_gpu_bitwise(amg, oracle, case):
+    """The classical setup's Galerkin products R (A P) on the GPU (amg_spgemm.hip,
+    opts.device = 0): every level's A, P, R identical to the host setup's, bit
+    for bit (one lane per row in the host's Gustavson order)."""
+    if case.startswith("lap"):
+        A = oracle.laplace_7pt(20)
+        args = (A.nrows, A.rowptr, A.col, A.val)
+        kw = dict(coarsen_type=10, strong_threshold=0.25)
+    else:
+        n, rp, cj, v, b = amg.classical.elasticity(int(case[5]))
+        args = (n, rp, cj, v)
+        kw = dict(coarsen_type=9, strong_threshold=0.5, num_functions=3)
+    Hh = amg.classical.ClassicalAMG(*args, **kw)
+    Hd = amg.classical.ClassicalAMG(*args, device=0, **kw)
+    lh, ld = host_levels(amg, Hh), host_levels(amg, Hd)
+    assert len(lh["A"]) == len(ld["A"]) >= 3
+    for w in ("A", "P", "R"):
+        for l, (mh, md) in enumerate(zip(lh[w], ld[w])):
+            assert mh[0] == md[0] and mh[1] == md[1], (w, l)
+            for a, b_ in zip(mh[2:], md[2:]):
+                assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b_).view(np.uint8)), (w, l)
