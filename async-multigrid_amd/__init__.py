@@ -25,7 +25,7 @@ from .abi import (AMG_JACOBI, AMG_GAUSS_SEIDEL, AMG_HYBRID_JGS, AMG_SYMM_JACOBI,
                   AMG_ASYNC_GS, AMG_SEMI_ASYNC_GS, AMG_BPX, AMG_NO_ACCEL, AMG_RICHARD_ACCEL,
                   AMG_CHEBY_RECUR_ACCEL, AMG_FULL_ASYNC, AMG_SEMI_ASYNC, AMG_LOCAL, AMG_GLOBAL,
                   AMG_READ_SOL, AMG_READ_RES, AMG_DELAY_NONE, AMG_DELAY_ONE, AMG_DELAY_SOME,
-                  AMG_DELAY_ALL, AMG_FAIL_ONE)
+                  AMG_DELAY_ALL, AMG_FAIL_ONE, AMG_SPS_EXPONENTIAL, AMG_SPS_INVERSE, AMG_SPS_RANDOM)
 
 lib = abi.load()
 
@@ -341,6 +341,13 @@ class Gen:
 def rhs_rand(r0, r1, lo=-1.0, hi=1.0):
     out = np.empty(r1 - r0, dtype=np.float64)
     check(lib.amg_rhs_rand(r0, r1, lo, hi, _dp(out)))
+    return out
+
+
+def rand_double_stream(seed, n, lo=0.0, hi=1.0):
+    """n RandDouble(lo, hi) draws after srand(seed) (glibc rand(), Misc.cpp:282-285)."""
+    out = np.empty(n, dtype=np.float64)
+    check(lib.amg_rand_double_stream(int(seed), int(n), float(lo), float(hi), _dp(out)))
     return out
 
 

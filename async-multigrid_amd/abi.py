@@ -51,10 +51,12 @@ class AmgOpts(C.Structure):
                 ("accel_type", _i), ("cheby_grid", _i), ("res_compute_type", _i),
                 ("read_type", _i), ("converge_test_type", _i),
                 ("delay_type", _i), ("delay_usec", _i), ("delay_frac", _d), ("fail_iter", _i),
-                ("delay_rank", _i), ("max_inflight", _i), ("async_comm_save_divisor", _i)]
+                ("delay_rank", _i), ("max_inflight", _i), ("async_comm_save_divisor", _i),
+                ("sps_probability_type", _i), ("sps_alpha", _d), ("sps_min_prob", _d)]
 
 
 AMG_DELAY_NONE, AMG_DELAY_ONE, AMG_DELAY_SOME, AMG_DELAY_ALL, AMG_FAIL_ONE = 0, 1, 2, 3, 4
+AMG_SPS_EXPONENTIAL, AMG_SPS_INVERSE, AMG_SPS_RANDOM = 0, 1, 2
 
 
 class AmgClassicalOpts(C.Structure):
@@ -181,6 +183,8 @@ PROTOTYPES = {
     "amg_dist_hier_set_replicate_rows": (_i, [_p, _ll]),
     "amg_dist_async_solve": (_i, [_p, _dp, _ip, _dp]),
     "amg_dist_async_jacobi": (_i, [_p, _dp, _i, _i, _dp]),
+    "amg_dist_async_sps": (_i, [_p, _dp, _i, _dp, C.POINTER(C.c_longlong)]),
+    "amg_rand_double_stream": (_i, [C.c_uint, _i, _d, _d, _dp]),
     "amg_dist_structured_row_starts": (_i, [_p, _i, _llp]),
     "amg_dist_hier_create": (_i, [_p, _i, _llp, C.c_void_p, C.c_void_p, C.c_void_p,
                                   C.POINTER(AmgOpts), _pp]),

@@ -54,6 +54,9 @@ extern "C" void amg_opts_default(amg_opts *o)
    o->delay_rank = -1; // DMEM_DelayProc: every rank (DMEM_Misc.cpp:670-676)
    o->max_inflight = 1;            // DMEM_Main.cpp:113
    o->async_comm_save_divisor = 1; // DMEM_Main.cpp:123
+   o->sps_probability_type = AMG_SPS_EXPONENTIAL; // DMEM_Main.cpp:119-121
+   o->sps_alpha = 1.0;
+   o->sps_min_prob = 0.0;
 }
 
 // ---------------------------------------------------------------------------

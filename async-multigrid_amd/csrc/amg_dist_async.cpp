@@ -495,10 +495,15 @@ namespace {
 //   e = 0 + u;  x += e
 // acc: 0 none, 1 first cycle (d = u), 2 recurrence with om1 = w - 1, omd = w delta
 // (this grid is cheby_grid), 3 recurrence on another grid (u = omd u)
+// gate (SPS): the device flag of this sweep; 0 = no relaxation (e = 0, x kept)
 __global__ void ajac_update_k(const double *__restrict__ r, const double *__restrict__ sc,
                               double *__restrict__ e, double *__restrict__ x, double *__restrict__ d,
-                              int n, int acc, double om1, double omd)
+                              int n, int acc, double om1, double omd, const int *__restrict__ gate)
 {
+   if (gate && *gate == 0) {
+      for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) e[i] = 0.0;
+      return;
+   }
    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
       double u = 0.0 + r[i] / sc[i];
       if (acc == 1) {
@@ -531,12 +536,88 @@ __global__ void ajac_scale_k(const double *__restrict__ diag, const double *__re
 
 constexpr int AJ_NBUF = 4;
 
+// StochasticParallelSouthwellUpdateProbability (DMEM_Smooth.cpp:548-572) and the
+// draw that follows it (:286-290), for sweep k >= 1 (sweep 0 always relaxes,
+// update_flag = 1 at :70): x = the neighbours whose latest norm exceeds mine
+// (not counted for RANDOM); p = (1/x)(1/alpha), exp(-x alpha) or alpha; relax
+// when draws[k-1] < p.  One lane; count = the sweeps relaxed in.
+__global__ void sps_decide_k(const double *__restrict__ mynorm, const double *__restrict__ rnorm, int np,
+                             int type, double alpha, const double *__restrict__ draws, int k,
+                             int *__restrict__ gate, long long *__restrict__ count)
+{
+   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+   int up = 1;
+   if (k > 0) {
+      double x = 0.0;
+      if (type != AMG_SPS_RANDOM)
+         for (int i = 0; i < np; i++)
+            if (mynorm[0] < rnorm[i]) x++;
+      double p;
+      if (type == AMG_SPS_INVERSE)
+         p = (1.0 / x) * (1.0 / alpha);
+      else if (type == AMG_SPS_EXPONENTIAL)
+         p = exp(-x * alpha);
+      else
+         p = alpha;
+      up = draws[k - 1] < p ? 1 : 0;
+   }
+   gate[0] = up;
+   count[0] += up;
+}
+
+// glibc random_r TYPE_3 (the default state of rand(), degree 31, separation 3):
+// seeded by the Lehmer generator 16807 r mod (2^31 - 1), 310 outputs discarded,
+// then r_i = r_{i-31} + r_{i-3} (mod 2^32), output r_i >> 1
+std::vector<double> rand_double_stream(unsigned seed, int n, double low, double high)
+{
+   std::vector<unsigned> r(344 + (size_t)std::max(n, 0));
+   int32_t w = seed == 0 ? 1 : (int32_t)seed;
+   r[0] = (unsigned)w;
+   for (int i = 1; i < 31; i++) {
+      const int32_t hi = w / 127773, lo = w % 127773;
+      w = 16807 * lo - 2836 * hi;
+      if (w < 0) w += 2147483647;
+      r[i] = (unsigned)w;
+   }
+   for (int i = 31; i < 34; i++) r[i] = r[i - 31];
+   for (size_t i = 34; i < r.size(); i++) r[i] = r[i - 31] + r[i - 3];
+   std::vector<double> out(std::max(n, 0));
+   for (int k = 0; k < n; k++) out[k] = low + (high - low) * ((double)(r[344 + k] >> 1) / 2147483647.0);
+   return out;
+}
+
+int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1, bool sps, double *relres,
+                     long long *relaxations);
+
 } // namespace
+
+extern "C" int amg_rand_double_stream(unsigned seed, int n, double low, double high, double *out)
+{
+   AMG_ARG(n >= 0 && (n == 0 || out), "amg_rand_double_stream: bad argument");
+   const std::vector<double> v = rand_double_stream(seed, n, low, high);
+   std::copy(v.begin(), v.end(), out);
+   return AMG_OK;
+}
 
 extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, int sweeps, int l1,
                                      double *relres)
 {
+   return async_jacobi_run(D, f_local, sweeps, l1, false, relres, nullptr);
+}
+
+extern "C" int amg_dist_async_sps(amg_dist_hier *D, const double *f_local, int sweeps, double *relres,
+                                  long long *relaxations)
+{
+   return async_jacobi_run(D, f_local, sweeps, 0, true, relres, relaxations);
+}
+
+namespace {
+
+int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1, bool sps, double *relres,
+                     long long *relaxations)
+{
    AMG_ARG(D && f_local && sweeps >= 0, "amg_dist_async_jacobi: bad argument");
+   AMG_ARG(!sps || D->o.accel_type == AMG_NO_ACCEL, "amg_dist_async_sps: no accel_type with SPS gating");
    amg_ctx *c = D->ctx;
    hipStream_t s = c->stream, cs = c->comm_stream;
    DLevel &v = D->lv[0];
@@ -567,6 +648,32 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
       return code;
    };
    if (!wv || !f || !sbuf || !rbuf || !dacc) return fail(amg_set_error(AMG_ERR_OOM, "amg_dist_async_jacobi: workspace"));
+   // SPS: [my norm per slot (NBUF) | neighbour norms per slot (NBUF np) | latest
+   // neighbour norms (np) | draws (sweeps)], gate flag and relaxation count
+   double *part = nullptr, sps_alpha = D->o.sps_alpha;
+   double *snorm = nullptr, *rnorm = nullptr, *lnorm = nullptr, *draws = nullptr;
+   int *gate = nullptr;
+   long long *count = nullptr;
+   if (sps) {
+      double *ws = tmp((size_t)AJ_NBUF * (1 + np) + np + sweeps + 2);
+      if (!ws) return fail(amg_set_error(AMG_ERR_OOM, "amg_dist_async_sps: workspace"));
+      // the reference's RandDouble stream: one draw per sweep after the first
+      const std::vector<double> dr = rand_double_stream(0, sweeps, 0.0, 1.0);
+      double *pp = nullptr;
+      if ((st = amg_ctx_partials(c, 65536, &pp)) != AMG_OK) return fail(st);
+      part = pp;
+      snorm = ws;
+      rnorm = snorm + AJ_NBUF;
+      lnorm = rnorm + (size_t)AJ_NBUF * np;
+      draws = lnorm + np;
+      gate = reinterpret_cast<int *>(draws + sweeps);
+      count = reinterpret_cast<long long *>(draws + sweeps + 1);
+      amgk::vset(s, ws, 0.0, 0, (long long)AJ_NBUF * (1 + np) + np + sweeps + 2);
+      if (sweeps > 0 && (st = h2d(s, draws, dr.data(), (size_t)sweeps * sizeof(double))) != AMG_OK)
+         return fail(st);
+      // sps_min_prob > 0: alpha = -log(min_prob) / num_sends (DMEM_Setup.cpp:1168-1169)
+      if (D->o.sps_min_prob > 0 && np > 0) sps_alpha = -std::log(D->o.sps_min_prob) / (double)np;
+   }
    if ((st = h2d(s, f, f_local, (size_t)n * sizeof(double))) != AMG_OK) return fail(st);
    const int nb = std::max(1, std::min(65536, (n + 255) / 256));
    ajac_scale_k<<<nb, 256, 0, s>>>(M.A->diag, l1 ? v.l1 : nullptr, D->o.smooth_weight, wv, n);
@@ -587,6 +694,9 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
       AMG_HIP(hipStreamWaitEvent(s, arrived[q], 0));
       AMG_HIP(hipMemcpyAsync(gext + no, rbuf + (size_t)q * std::max(1, ng), (size_t)ng * sizeof(double),
                              hipMemcpyDeviceToDevice, s));
+      if (sps && np > 0) // the neighbours' norms that came with these deltas
+         AMG_HIP(hipMemcpyAsync(lnorm, rnorm + (size_t)q * np, (size_t)np * sizeof(double),
+                                hipMemcpyDeviceToDevice, s));
       amgk::spgemv(s, M.A, gext, r, upd, r, 0, n, nullptr); // r -= A_offd g
       return AMG_OK;
    };
@@ -605,7 +715,16 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
       AMG_HIP(hipStreamWaitEvent(s, sent[q], 0));
       double om1 = 0.0, omd = 0.0;
       const int am = !accel ? 0 : !acc.next(D->o, &om1, &omd) ? 1 : D->o.cheby_grid == 0 ? 2 : 3;
-      ajac_update_k<<<nb, 256, 0, s>>>(r, wv, eext, x, dacc, n, am, om1, omd);
+      if (sps) {
+         // my residual L1 norm (DMEM_Smooth.cpp:258-268), sent with this sweep's
+         // deltas; then this sweep's update decision
+         int parts = 0;
+         amgk::abssum_partials(s, r, n, part, &parts);
+         amgk::reduce_partials(s, part, parts, snorm + q, 0, c->d_scalars + 4096);
+         sps_decide_k<<<1, 64, 0, s>>>(snorm + q, lnorm, np, D->o.sps_probability_type, sps_alpha, draws, k, gate,
+                                       count);
+      }
+      ajac_update_k<<<nb, 256, 0, s>>>(r, wv, eext, x, dacc, n, am, om1, omd, gate);
       if (np > 0) {
          launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * std::max<long long>(1, M.nsend), (int)M.nsend);
          AMG_HIP(hipEventRecord(packed[q], s));
@@ -620,6 +739,16 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
          }
          if ((st = xp_p2p(c, cs, np, M.peers.data(), sp.data(), sb.data(), rp.data(), rb.data())) != AMG_OK)
             break;
+         if (sps) { // the norm travels with the deltas (data[vec_len + 1], DMEM_Comm.cpp:216-220)
+            for (int i = 0; i < np; i++) {
+               sp[i] = snorm + q;
+               sb[i] = 8;
+               rp[i] = rnorm + (size_t)q * np + i;
+               rb[i] = 8;
+            }
+            if ((st = xp_p2p(c, cs, np, M.peers.data(), sp.data(), sb.data(), rp.data(), rb.data())) != AMG_OK)
+               break;
+         }
          AMG_HIP(hipEventRecord(sent[q], cs));
          AMG_HIP(hipEventRecord(arrived[q], cs));
          pending.push_back(k);
@@ -644,6 +773,10 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
       hipEventDestroy(arrived[q]);
    }
    if (st != AMG_OK) return fail(st);
+   if (relaxations) {
+      *relaxations = sps ? 0 : sweeps;
+      if (sps && (st = d2h(s, relaxations, count, sizeof(long long))) != AMG_OK) return fail(st);
+   }
    // true residual f - A x with a synchronous exchange, and its global norm
    amgk::vcopy(s, f, v.f, 0, n);
    if ((st = dist_outer_residual(D, 1)) != AMG_OK) return fail(st);
@@ -665,3 +798,5 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
    for (double *q : dtmp) hipFree(q);
    return AMG_OK;
 }
+
+} // namespace

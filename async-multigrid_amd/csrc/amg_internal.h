@@ -359,6 +359,7 @@ void dc_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, 
 
 // deterministic reductions
 void sumsq_partials(hipStream_t s, const double *x, int n, double *partials, int *nparts);
+void abssum_partials(hipStream_t s, const double *x, int n, double *partials, int *nparts);
 void dot_partials(hipStream_t s, const double *x, const double *y, int n, double *partials,
                   int *nparts);
 // out[0] = sum(partials[0..np)) in fixed order; if do_sqrt, out[0] = sqrt(sum)

@@ -3459,7 +3459,8 @@ void atomic_add(hipStream_t s, double *u, const double *x, int rb, int re)
 // ---------------------------------------------------------------------------
 static inline int red_blocks(int n) { return std::max(1, std::min(1024, (n + 2047) / 2048)); }
 
-template <bool DOT>
+// MODE 0: sum x^2, 1: sum x y, 2: sum |x|
+template <int MODE>
 __global__ __launch_bounds__(256) void partials_k(const double *__restrict__ x,
                                                   const double *__restrict__ y, int n,
                                                   double *__restrict__ partials)
@@ -3467,7 +3468,7 @@ __global__ __launch_bounds__(256) void partials_k(const double *__restrict__ x,
    __shared__ double red[4];
    double s = 0.0;
    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
-      s += DOT ? x[i] * y[i] : x[i] * x[i];
+      s += MODE == 1 ? x[i] * y[i] : MODE == 2 ? fabs(x[i]) : x[i] * x[i];
    s = block_sum_256(s, red);
    if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
@@ -3475,7 +3476,14 @@ __global__ __launch_bounds__(256) void partials_k(const double *__restrict__ x,
 void sumsq_partials(hipStream_t s, const double *x, int n, double *partials, int *nparts)
 {
    const int nb = red_blocks(n);
-   partials_k<false><<<nb, 256, 0, s>>>(x, nullptr, n, partials);
+   partials_k<0><<<nb, 256, 0, s>>>(x, nullptr, n, partials);
+   *nparts = nb;
+}
+
+void abssum_partials(hipStream_t s, const double *x, int n, double *partials, int *nparts)
+{
+   const int nb = red_blocks(n);
+   partials_k<2><<<nb, 256, 0, s>>>(x, nullptr, n, partials);
    *nparts = nb;
 }
 
@@ -3483,7 +3491,7 @@ void dot_partials(hipStream_t s, const double *x, const double *y, int n, double
                   int *nparts)
 {
    const int nb = red_blocks(n);
-   partials_k<true><<<nb, 256, 0, s>>>(x, y, n, partials);
+   partials_k<1><<<nb, 256, 0, s>>>(x, y, n, partials);
    *nparts = nb;
 }
 

@@ -303,6 +303,15 @@ class DistHier:
         check(lib.amg_dist_async_jacobi(self.h, _dp(f), int(sweeps), int(l1), C.byref(rel)))
         return rel.value
 
+    def async_sps(self, f_local, sweeps):
+        """-smoother async_sps (stochastic parallel Southwell gating of the
+        asynchronous Jacobi, opts.sps_*): (relres, sweeps this rank relaxed in)."""
+        f = np.ascontiguousarray(f_local, dtype=np.float64)
+        assert f.size == self.n0
+        rel, nrel = C.c_double(), C.c_longlong()
+        check(lib.amg_dist_async_sps(self.h, _dp(f), int(sweeps), C.byref(rel), C.byref(nrel)))
+        return rel.value, nrel.value
+
     def get_u(self):
         u = np.empty(self.n0)
         check(lib.amg_dist_get_u(self.h, _dp(u)))

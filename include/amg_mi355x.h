@@ -138,7 +138,17 @@ typedef struct {
                                     in flight per destination (amg_grid_add)   */
    int async_comm_save_divisor;  /* input.async_comm_save_divisor (:123): send the
                                     accumulated corrections every this many cycles */
+   /* stochastic parallel Southwell gating of the asynchronous Jacobi smoother
+    * (-smoother async_sps, input.sps_*, DMEM_Main.cpp:119-121,448-459;
+    * StochasticParallelSouthwellUpdateProbability, DMEM_Smooth.cpp:548-572) */
+   int sps_probability_type;     /* AMG_SPS_EXPONENTIAL / _INVERSE / _RANDOM       */
+   double sps_alpha;             /* exp(-x alpha) / 1/(x alpha) / alpha (RANDOM)   */
+   double sps_min_prob;          /* > 0: alpha = -log(min_prob) / num_sends
+                                    (DMEM_Setup.cpp:1168-1169)                  */
 } amg_opts;
+#define AMG_SPS_EXPONENTIAL 0 /* Main.hpp:132-134 */
+#define AMG_SPS_INVERSE 1
+#define AMG_SPS_RANDOM 2
 #define AMG_DELAY_NONE 0
 #define AMG_DELAY_ONE 1
 #define AMG_DELAY_SOME 2
@@ -529,6 +539,20 @@ int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int *level_cor
  * stream while the compute stream updates the residual from the owned columns, and
  * applies neighbours' deltas once they have arrived (never waiting for them).  Read x
  * with amg_dist_get_u.  *relres = ||f - A x|| / ||f|| after all deltas are drained. */
+/* -smoother async_sps (ASYNC_STOCHASTIC_PARALLEL_SOUTHWELL_JACOBI,
+ * DMEM_Smooth.cpp:165-291): the asynchronous Jacobi above, where a rank relaxes
+ * in a sweep only when a draw RandDouble(0,1) falls below the update probability
+ * of its local residual L1 norm against the latest norms its neighbours sent
+ * (carried with every delta message, DMEM_Comm.cpp:216-220,286-290): the first
+ * sweep always relaxes.  The draws are the reference's RandDouble stream (glibc
+ * rand() after srand(0), DMEM_Setup.cpp:1426, Misc.cpp:282-285), the same on
+ * every rank; the decision is made on the device, so nothing waits on the host.
+ * *relaxations (optional) = the sweeps this rank relaxed in.  No accel_type. */
+int amg_dist_async_sps(amg_dist_hier *D, const double *f_local, int sweeps, double *relres,
+                       long long *relaxations);
+/* n draws low + (high - low) rand() / RAND_MAX after srand(seed), by the glibc
+ * TYPE_3 additive feedback generator (Misc.cpp:282-285's RandDouble) */
+int amg_rand_double_stream(unsigned seed, int n, double low, double high, double *out);
 int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, int sweeps, int l1,
                           double *relres);
 /* y = A_0 x on the distributed fine operator (halo exchange + interior/boundary
