@@ -137,6 +137,9 @@ def main(args, world, rank):
                                                    "slab, incl. ghost exchange wait)",
                          "achieved": ach0, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach0 / HBM_PEAK_GBS, "traffic": None,
+                         "traffic_note": "PMC FETCH/WRITE passes are single-GPU runs of bench.py "
+                                         "(profiles/traffic.json); the per-rank slab residual is the "
+                                         "same kernel on a z-slab and is not profiled per rank",
                          "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms,
                          "aggregate_gbs": res_gbs},
             "cpu_baseline": cpu,
