@@ -971,6 +971,20 @@ __device__ __forceinline__ double ld1u(const double *b, unsigned i)
    return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(b) + (size_t)(i * 8u));
 }
 
+// 16-byte load; nt bit 1: nontemporal (a streamed right-hand side)
+__device__ __forceinline__ v2d ld2nt(const double *p, int nt)
+{
+   if (nt & 2) return __builtin_nontemporal_load(reinterpret_cast<const v2du *>(p));
+   return *reinterpret_cast<const v2du *>(p);
+}
+
+// streaming hints (st2 / ld2nt bits) for levels whose vectors exceed the
+// Infinity Cache (ctx->mz_nt, AMG_MZ_NT)
+static int stream_hint(const amg_mat *A)
+{
+   return (long long)A->nrows * 8 > (512LL << 20) ? A->ctx->mz_nt : 0;
+}
+
 // the 7 master entries of a row pair in master (= CSR) order; a wave whose
 // pairs all use every entry (the box interior) skips the per-entry use tests
 template <int NEG, bool UNI>
@@ -1426,7 +1440,7 @@ template <bool UNI, int LC, int OCC = 1, bool RING = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void mz_res_restrict_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, Val7 Sv7, const double *__restrict__ x, const double *__restrict__ f,
-   const double *__restrict__ wg, int nx, int ny, int nz, int zcc, int nlb, int xcd,
+   const double *__restrict__ wg, int nx, int ny, int nz, int zcc, int nlb, int xcd, int ntf,
    double *__restrict__ fc)
 {
    constexpr int NL = 2 * LC + 1; // fine lines per lane
@@ -1497,7 +1511,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
          in.e[i] = 0.0;
          if (i == NL - 1 && lastl) continue;
          in.pid[i] = ppat[row >> 1];
-         in.a2[i] = ld2u(f, row);
+         in.a2[i] = ld2nt(f + row, ntf);
          if (lane == 0 && row > 0) in.e[i] = ld1u(x, row - 1);
          if (lane == 63 && row + 2 < Nu) in.e[i] = ld1u(x, row + 2);
       }
@@ -1620,7 +1634,7 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
 #define AMG_RR(U, L, ...) \
    mz_res_restrict_kernel<U, L, ##__VA_ARGS__><<<nb, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, f, wdev, g.nx, g.ny, \
-                                                   g.nz, zcc, nlb, xcd, fc)
+                                                   g.nz, zcc, nlb, xcd, stream_hint(A), fc)
    if (A->mp_uni) {
       if (LC == 2) AMG_RR(true, 2);
       else if (A->ctx->rr_occ == 5) AMG_RR(true, 1, 5);
@@ -2065,11 +2079,12 @@ static inline bool short_rows(const amg_mat *A) { return A->nnz < 12LL * A->nrow
 // row's outputs and returns the value whose square feeds the norm partials.
 
 // y = SpGEMV epilogue (SMEM_MatVec.cpp:140-258)
-// 16-byte store of rows (i, i+1); nt: nontemporal (streamed past the
-// caches, for fine-grid outputs far larger than L2 + Infinity Cache)
+// 16-byte store of rows (i, i+1); nt bit 0: nontemporal (streamed past the
+// caches, for fine-grid outputs far larger than L2 + Infinity Cache); bit 1
+// (ld2nt): the same for the streamed right-hand side loads
 __device__ __forceinline__ void st2(double *p, v2d v, int nt)
 {
-   if (nt)
+   if (nt & 1)
       __builtin_nontemporal_store(v, reinterpret_cast<v2du *>(p));
    else
       *reinterpret_cast<v2du *>(p) = v;
@@ -2135,7 +2150,7 @@ struct EpiJacobi {
       out[i] = v;
       return v;
    }
-   __device__ __forceinline__ v2d init2(int i) const { return *reinterpret_cast<const v2du *>(f + i); }
+   __device__ __forceinline__ v2d init2(int i) const { return ld2nt(f + i, nt); }
    __device__ __forceinline__ v2d pf2(int i) const { return *reinterpret_cast<const v2du *>(x + i); }
    __device__ __forceinline__ v2d finish2(int i, v2d res, v2d a, v2d xi) const
    {
@@ -2192,7 +2207,7 @@ struct EpiResJacobi {
       unext[i] = l1 ? xi + res / l1[i] : ((a != 0.0) ? xi + omega * res / a : xi);
       return res;
    }
-   __device__ __forceinline__ v2d init2(int i) const { return *reinterpret_cast<const v2du *>(f + i); }
+   __device__ __forceinline__ v2d init2(int i) const { return ld2nt(f + i, nt); }
    __device__ __forceinline__ v2d pf2(int i) const { return *reinterpret_cast<const v2du *>(x + i); }
    __device__ __forceinline__ v2d finish2(int i, v2d res, v2d a, v2d xi) const
    {
@@ -2415,7 +2430,7 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
       if (l1)
          launch_dc_op<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out}, nullptr, nb);
       else
-         launch_dc_op<1, true>(s, A, x, rb, re, EpiJacobi{f, x, out, omega}, nullptr, nb);
+         launch_dc_op<1, true>(s, A, x, rb, re, EpiJacobi{f, x, out, omega, stream_hint(A)}, nullptr, nb);
    } else if (long_rows(A)) {
       if (l1)
          launch_long<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out});
@@ -2450,6 +2465,7 @@ void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const dou
    if (re <= rb) return;
    const int nb = tile_blocks(rb, re);
    EpiResJacobi e{f, x, l1, r, unext, omega};
+   if (A->didx) e.nt = stream_hint(A);
    if (use_bsr3(A, rb, re, partials)) {
       if (l1)
          launch_bsr3<1, false>(s, A, x, rb, re, e);
