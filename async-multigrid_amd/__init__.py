@@ -108,6 +108,10 @@ class Context:
         """Prolongation fused into the first post-smoothing sweep of marched geometric levels (default off: VALU-bound, slower)."""
         check(lib.amg_set_fuse_prolong(self.h, int(enable)))
 
+    def set_march_lines(self, lines):
+        """Lines per lane of the 7-pt plane march (1 or 2; bit-identical)."""
+        check(lib.amg_set_march_lines(self.h, int(lines)))
+
     def csr(self, nrows, ncols, rowptr, col, val, diag_first=1):
         return Mat.register(self, nrows, ncols, rowptr, col, val, diag_first)
 

@@ -1010,7 +1010,12 @@ __device__ __forceinline__ v2d mz_acc7(v2d acc, const v2d (&xv)[7], unsigned lon
    return acc;
 }
 
-template <int NEG, bool NEED_DIAG, class Epi, bool UNI>
+// NLN lines per lane (register blocking in y): the workgroup holds NLN
+// adjacent lines of 512 positions, a lane keeps x of its NLN lines for planes
+// k - 1, k, k + 1, so the +-S operands of its inner lines come from registers
+// and only the two halo lines are loaded per plane (2 / NLN line loads per line
+// instead of 2).  NLN > 1 needs S % 512 == 0 and NLN | P / S.
+template <int NEG, bool NEED_DIAG, class Epi, bool UNI, int NLN = 1>
 __global__ __launch_bounds__(256) void csr_mz_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ x, int P, int S, int nz, int zc,
@@ -1019,7 +1024,7 @@ __global__ __launch_bounds__(256) void csr_mz_kernel(
    const bool xc_pf = pf_is_x<Epi>::value && epi_pf_vec(epi) == x;
    __shared__ unsigned long long mtab[256];
    __shared__ v2d mval[UNI ? 1 : 256 * 7];
-   __shared__ double red[AMG_MZ_MAXZC * 8];
+   __shared__ double red[AMG_MZ_MAXZC * 8 * NLN];
    const int tid = (int)threadIdx.x, lane = tid & 63;
    if (tid < np) mtab[tid] = mmask_g[tid];
    if (!UNI)
@@ -1032,75 +1037,100 @@ __global__ __launch_bounds__(256) void csr_mz_kernel(
    if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
    const int pblk = lg % npb, chunk = lg / npb;
    const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
-   const int pos = pblk * 512 + 2 * tid;
+   int blk0 = pblk * 512; // plane offset of the workgroup's first line block
+   if (NLN > 1) {
+      const int nbx = S / 512;
+      blk0 = (pblk / nbx) * NLN * S + (pblk % nbx) * 512;
+   }
+   const int pos = blk0 + 2 * tid;
    const unsigned Nu = (unsigned)((long long)nz * P);
-   v2d xm = k0 > 0 ? ld2u(x, (unsigned)(k0 - 1) * P + pos) : v2d{0.0, 0.0};
-   v2d xc = ld2u(x, (unsigned)k0 * P + pos);
-   v2d xq = k0 + 1 < nz ? ld2u(x, (unsigned)(k0 + 1) * P + pos) : v2d{0.0, 0.0};
+   v2d xm[NLN], xc[NLN], xq[NLN];
+#pragma unroll
+   for (int i = 0; i < NLN; i++) {
+      const unsigned p = (unsigned)(pos + i * S);
+      xm[i] = k0 > 0 ? ld2u(x, (unsigned)(k0 - 1) * P + p) : v2d{0.0, 0.0};
+      xc[i] = ld2u(x, (unsigned)k0 * P + p);
+      xq[i] = k0 + 1 < nz ? ld2u(x, (unsigned)(k0 + 1) * P + p) : v2d{0.0, 0.0};
+   }
    struct PlaneIn {
-      v2d ym, yp;
-      double e;
-      int pid;
+      v2d ym, yp; // halo lines: below the first, above the last
+      double e[NLN];
+      int pid[NLN];
    };
    auto fetch = [&](int k, PlaneIn &in) {
       const unsigned row = (unsigned)k * P + pos;
-      in.pid = ppat[row >> 1];
       in.ym = ld2u(x, row >= (unsigned)S ? row - S : 0u);
-      in.yp = ld2u(x, row + S + 2 <= Nu ? row + S : Nu - 2);
-      in.e = 0.0;
-      if (lane == 0 && row > 0) in.e = ld1u(x, row - 1);
-      if (lane == 63 && row + 2 < Nu) in.e = ld1u(x, row + 2);
+      const unsigned rp = row + (unsigned)(NLN * S);
+      in.yp = ld2u(x, rp + 2 <= Nu ? rp : Nu - 2);
+#pragma unroll
+      for (int i = 0; i < NLN; i++) {
+         const unsigned ri = row + (unsigned)(i * S);
+         in.pid[i] = ppat[ri >> 1];
+         in.e[i] = 0.0;
+         if (lane == 0 && ri > 0) in.e[i] = ld1u(x, ri - 1);
+         if (lane == 63 && ri + 2 < Nu) in.e[i] = ld1u(x, ri + 2);
+      }
    };
    __syncthreads();
    for (int k = k0; k < k1; k++) {
-      const unsigned row = (unsigned)k * P + pos;
+      const unsigned row0 = (unsigned)k * P + pos;
       // prefetch plane k + 2 (this chunk's last iteration needs plane k1)
-      v2d xn{0.0, 0.0};
-      if (k + 2 < nz && k + 1 < k1) xn = ld2u(x, row + 2u * P);
+      v2d xn[NLN];
+#pragma unroll
+      for (int i = 0; i < NLN; i++) {
+         xn[i] = v2d{0.0, 0.0};
+         if (k + 2 < nz && k + 1 < k1) xn[i] = ld2u(x, row0 + (unsigned)(i * S) + 2u * P);
+      }
       PlaneIn cur;
       fetch(k, cur);
-      const int pid = cur.pid;
-      v2d acc = epi.init2((int)row);
-      v2d pf = xc_pf ? xc : epi.pf2((int)row);
-      const v2d ym = cur.ym, yp = cur.yp;
-      const double e = cur.e;
-      double lft = __shfl_up(xc.y, 1, 64);
-      double rgt = __shfl_down(xc.x, 1, 64);
-      if (lane == 0) lft = e;
-      if (lane == 63) rgt = e;
-      const unsigned long long mk = mtab[pid];
-      v2d xv[7];
-      xv[0] = xc;
-      xv[1] = xm;
-      xv[2] = ym;
-      xv[3] = v2d{lft, xc.x};
-      xv[4] = v2d{xc.y, rgt};
-      xv[5] = yp;
-      xv[6] = xq;
-      acc = mz_acc7<NEG, UNI>(acc, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
-      v2d dg{0.0, 0.0};
-      if (NEED_DIAG) dg = UNI ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 7];
-      const v2d out = epi.finish2((int)row, acc, dg, pf);
-      if (partials) {
-         // csr_mp_kernel's 64-row group sums
-         double a = out.x * out.x, b = out.y * out.y;
 #pragma unroll
-         for (int off = 16; off > 0; off >>= 1) {
-            a += __shfl_down(a, off, 32);
-            b += __shfl_down(b, off, 32);
+      for (int i = 0; i < NLN; i++) {
+         const unsigned row = row0 + (unsigned)(i * S);
+         const int pid = cur.pid[i];
+         v2d acc = epi.init2((int)row);
+         v2d pf = xc_pf ? xc[i] : epi.pf2((int)row);
+         const double e = cur.e[i];
+         double lft = __shfl_up(xc[i].y, 1, 64);
+         double rgt = __shfl_down(xc[i].x, 1, 64);
+         if (lane == 0) lft = e;
+         if (lane == 63) rgt = e;
+         const unsigned long long mk = mtab[pid];
+         v2d xv[7];
+         xv[0] = xc[i];
+         xv[1] = xm[i];
+         xv[2] = i == 0 ? cur.ym : xc[i == 0 ? 0 : i - 1];
+         xv[3] = v2d{lft, xc[i].x};
+         xv[4] = v2d{xc[i].y, rgt};
+         xv[5] = i == NLN - 1 ? cur.yp : xc[i == NLN - 1 ? 0 : i + 1];
+         xv[6] = xq[i];
+         acc = mz_acc7<NEG, UNI>(acc, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
+         v2d dg{0.0, 0.0};
+         if (NEED_DIAG) dg = UNI ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 7];
+         const v2d out = epi.finish2((int)row, acc, dg, pf);
+         if (partials) {
+            // csr_mp_kernel's 64-row group sums
+            double a = out.x * out.x, b = out.y * out.y;
+#pragma unroll
+            for (int off = 16; off > 0; off >>= 1) {
+               a += __shfl_down(a, off, 32);
+               b += __shfl_down(b, off, 32);
+            }
+            if ((tid & 31) == 0) red[((k - k0) * NLN + i) * 8 + (tid >> 5)] = a + b;
          }
-         if ((tid & 31) == 0) red[(k - k0) * 8 + (tid >> 5)] = a + b;
       }
-      xm = xc;
-      xc = xq;
-      xq = xn;
+#pragma unroll
+      for (int i = 0; i < NLN; i++) {
+         xm[i] = xc[i];
+         xc[i] = xq[i];
+         xq[i] = xn[i];
+      }
    }
    if (partials) {
       __syncthreads();
-      for (int w = tid; w < 2 * (k1 - k0); w += 256) {
-         const int it = w >> 1, h = w & 1;
-         const double *g = red + it * 8 + 4 * h;
-         partials[((long long)(k0 + it) * P + pblk * 512) / 256 + h] = ((g[0] + g[1]) + g[2]) + g[3];
+      for (int w = tid; w < 2 * NLN * (k1 - k0); w += 256) {
+         const int it = w / (2 * NLN), i = (w >> 1) % NLN, h = w & 1;
+         const double *g = red + (it * NLN + i) * 8 + 4 * h;
+         partials[((long long)(k0 + it) * P + blk0 + i * S) / 256 + h] = ((g[0] + g[1]) + g[2]) + g[3];
       }
    }
 }
@@ -1122,9 +1152,17 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
       S.off[j] = A->mp_off[j];
       S.val[j] = A->mp_val[j];
    }
-   const int P = A->mz_P, nz = A->nrows / P, zc = mz_chunk(A, nz, P / 512);
-   const int npb = P / 512, nch = (nz + zc - 1) / zc;
+   const int P = A->mz_P, nz = A->nrows / P, Sx = A->mz_S;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+   // two lines per lane (ctx->mz_lines) where the plane splits into line pairs
+   if (A->mp_uni && A->ctx->mz_lines == 2 && Sx % 512 == 0 && (P / Sx) % 2 == 0) {
+      const int npb = P / 1024, zc = mz_chunk(A, nz, npb), nch = (nz + zc - 1) / zc;
+      csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 2><<<npb * nch, 256, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials);
+      return;
+   }
+   const int zc = mz_chunk(A, nz, P / 512);
+   const int npb = P / 512, nch = (nz + zc - 1) / zc;
    if (A->mp_uni)
       csr_mz_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
          A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);

@@ -49,12 +49,13 @@ def boxes(oracle):
         "lap32": oracle.laplace_7pt(32),
         "lap64x8x5": oracle.laplace_7pt(64, 8, 5),
         "lap512x2x3": oracle.laplace_7pt(512, 2, 3),
+        "lap512x6x5": oracle.laplace_7pt(512, 6, 5),
         "neu32x16x7": neumann_7pt(oracle, 32, 16, 7),
     }
 
 
 def test_plane_march_selection(ctx, oracle, boxes):
-    want = {"lap32": 1024, "lap64x8x5": 512, "lap512x2x3": 1024, "neu32x16x7": 512}
+    want = {"lap32": 1024, "lap64x8x5": 512, "lap512x2x3": 1024, "lap512x6x5": 3072, "neu32x16x7": 512}
     for name, A in boxes.items():
         M = register(ctx, A)
         assert M.plane_march == want[name], (name, M.plane_march)
@@ -70,11 +71,13 @@ def test_plane_march_selection(ctx, oracle, boxes):
         M.free()
 
 
+@pytest.mark.parametrize("lines", [1, 2])
 @pytest.mark.parametrize("zc,xcd", [(32, 1), (1, 0), (3, 1), (64, 0), (2, 1)])
-@pytest.mark.parametrize("name", ["lap32", "lap64x8x5", "lap512x2x3", "neu32x16x7"])
-def test_plane_march_bitwise(ctx, amg, boxes, name, zc, xcd):
+@pytest.mark.parametrize("name", ["lap32", "lap64x8x5", "lap512x2x3", "lap512x6x5", "neu32x16x7"])
+def test_plane_march_bitwise(ctx, amg, boxes, name, zc, xcd, lines):
     A = boxes[name]
     ctx.set_plane_march(1, zc, xcd)
+    ctx.set_march_lines(lines)
     try:
         mz = register(ctx, A)
         mp = register(ctx, A, march=0)
@@ -108,6 +111,7 @@ def test_plane_march_bitwise(ctx, amg, boxes, name, zc, xcd):
             M.free()
     finally:
         ctx.set_plane_march(1, -1, 1)
+        ctx.set_march_lines(1)
 
 
 @pytest.mark.parametrize("zc", [32, 5])
@@ -199,6 +203,35 @@ def test_fused_residual_restrict(ctx, amg, oracle, dims, zc):
     assert_bitwise(u1, u_cpu, "fused vs oracle iterate")
     assert_bitwise(h1[:k1 + 1], h0[:k0 + 1], "norm history")
     np.testing.assert_allclose(h1[:k1 + 1], hist_cpu[:k1 + 1], rtol=1e-12)
+
+
+@pytest.mark.parametrize("dims,zc", [((512, 8, 6), 4), ((512, 6, 10), 3), ((1024, 4, 6), 64)])
+def test_march_two_lines_solve(ctx, amg, oracle, dims, zc):
+    """Two lines per lane (csr_mz_kernel<..., 2>: +-S operands of the inner
+    lines from registers) through whole solves: the fused outer residual + norm
+    partials + first sweep and the post sweeps on 512- and 1024-wide boxes.
+    Iterate and norm history bit-identical to one line per lane and to the
+    oracle (iterate), 8 cycles."""
+    from oracle import pyoracle as po
+    g = amg.Gen(*dims, interp=amg.AMG_INTERP_LINEAR)
+    host = {w: [po.Csr(*g.host_csr(c, l)) for l in range(cnt)]
+            for w, c, cnt in (("A", amg.AMG_GEN_A, g.L), ("P", amg.AMG_GEN_P, g.L - 1),
+                              ("R", amg.AMG_GEN_R, g.L - 1))}
+    f = amg.rhs_rand(0, dims[0] * dims[1] * dims[2])
+    out = {}
+    for lines in (2, 1):
+        ctx.set_march_lines(lines)
+        try:
+            _, out[lines] = _hier_solve(ctx, amg, host, f, 8, 1, 1, zc=zc)
+        finally:
+            ctx.set_march_lines(1)
+    (u2, h2, k2), (u1, h1, k1) = out[2], out[1]
+    OH = po.Hier(host["A"], host["P"], host["R"], po.make_opts(smooth_weight=0.8, num_cycles=8))
+    u_cpu, hist_cpu, _ = OH.solve(f)
+    assert k2 == k1 == 8
+    assert_bitwise(u2, u1, "two lines vs one line iterate")
+    assert_bitwise(h2[:k2 + 1], h1[:k1 + 1], "two lines vs one line norm history")
+    assert_bitwise(u2, u_cpu, "two lines vs oracle iterate")
 
 
 def test_fused_transfer_detection(ctx, amg, oracle):
