@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdint>
 #include <set>
+#include <thread>
 #include <vector>
 
 #include "amg_internal.h"
@@ -46,6 +47,47 @@ struct HCsr {
 
 constexpr int CF_U = 0, CF_C = 1, CF_F = -1;
 
+// host threads for the row-parallel setup phases (strength, interpolation):
+// AMG_SETUP_THREADS (any level of at least 64 rows), else the hardware's, at
+// most 16, on levels of at least 16384 rows
+int setup_threads(int n)
+{
+   if (const char *v = std::getenv("AMG_SETUP_THREADS"))
+      return n < 64 ? 1 : std::max(1, std::min(64, std::atoi(v)));
+   if (n < 16384) return 1;
+   return (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+// M's rows built in parallel over contiguous row ranges: fn(r0, r1, cnt, cj, v)
+// appends rows r0..r1-1 in order to its own cj / v and sets cnt[r]; the ranges
+// are then concatenated in row order, so M is the same as a sequential build
+template <class Fn>
+void rows_parallel(int n, HCsr &M, Fn fn)
+{
+   const int T = setup_threads(n);
+   std::vector<std::vector<int>> cjs(T);
+   std::vector<std::vector<double>> vs(T);
+   std::vector<int> cnt(n, 0);
+   std::vector<std::thread> th;
+   for (int t = 0; t < T; t++) {
+      const int r0 = (int)((long long)n * t / T), r1 = (int)((long long)n * (t + 1) / T);
+      if (T == 1)
+         fn(r0, r1, cnt, cjs[t], vs[t]);
+      else
+         th.emplace_back([&, t, r0, r1] { fn(r0, r1, cnt, cjs[t], vs[t]); });
+   }
+   for (auto &x : th) x.join();
+   M.rp.assign(n + 1, 0);
+   for (int i = 0; i < n; i++) M.rp[i + 1] = M.rp[i] + cnt[i];
+   M.cj.clear();
+   M.v.clear();
+   M.cj.reserve(M.rp[n]);
+   for (int t = 0; t < T; t++) {
+      M.cj.insert(M.cj.end(), cjs[t].begin(), cjs[t].end());
+      M.v.insert(M.v.end(), vs[t].begin(), vs[t].end());
+   }
+}
+
 // hypre_BoomerAMGCreateS (serial): row scale = most negative off-diagonal for
 // a non-negative diagonal (most positive for a negative one); a_ij is strong
 // when it exceeds theta times that scale in the diagonal's opposite sign.
@@ -55,27 +97,29 @@ void strength(const HCsr &A, double theta, double max_row_sum, int nfun, HCsr &S
 {
    S = HCsr();
    S.n = S.m = A.n;
-   S.rp.assign(A.n + 1, 0);
-   for (int i = 0; i < A.n; i++) {
-      double diag = 0.0, row_scale = 0.0, row_sum = 0.0;
-      for (int k = A.rp[i]; k < A.rp[i + 1]; k++)
-         if (A.cj[k] == i) diag = A.v[k];
-      for (int k = A.rp[i]; k < A.rp[i + 1]; k++) {
-         const int j = A.cj[k];
-         row_sum += A.v[k];
-         if (j == i || j % nfun != i % nfun) continue;
-         row_scale = diag < 0 ? std::max(row_scale, A.v[k]) : std::min(row_scale, A.v[k]);
-      }
-      const bool all_weak = max_row_sum < 1.0 && std::fabs(row_sum) > std::fabs(diag) * max_row_sum;
-      if (!all_weak)
+   rows_parallel(A.n, S, [&](int r0, int r1, std::vector<int> &cnt, std::vector<int> &cj, std::vector<double> &) {
+      for (int i = r0; i < r1; i++) {
+         const size_t before = cj.size();
+         double diag = 0.0, row_scale = 0.0, row_sum = 0.0;
+         for (int k = A.rp[i]; k < A.rp[i + 1]; k++)
+            if (A.cj[k] == i) diag = A.v[k];
          for (int k = A.rp[i]; k < A.rp[i + 1]; k++) {
             const int j = A.cj[k];
+            row_sum += A.v[k];
             if (j == i || j % nfun != i % nfun) continue;
-            const bool strong = diag < 0 ? A.v[k] > theta * row_scale : A.v[k] < theta * row_scale;
-            if (strong) S.cj.push_back(j);
+            row_scale = diag < 0 ? std::max(row_scale, A.v[k]) : std::min(row_scale, A.v[k]);
          }
-      S.rp[i + 1] = (int)S.cj.size();
-   }
+         const bool all_weak = max_row_sum < 1.0 && std::fabs(row_sum) > std::fabs(diag) * max_row_sum;
+         if (!all_weak)
+            for (int k = A.rp[i]; k < A.rp[i + 1]; k++) {
+               const int j = A.cj[k];
+               if (j == i || j % nfun != i % nfun) continue;
+               const bool strong = diag < 0 ? A.v[k] > theta * row_scale : A.v[k] < theta * row_scale;
+               if (strong) cj.push_back(j);
+            }
+         cnt[i] = (int)(cj.size() - before);
+      }
+   });
 }
 
 void transpose_pattern(const HCsr &S, HCsr &T)
@@ -299,20 +343,21 @@ void interpolation(const HCsr &A, const HCsr &S, const std::vector<int> &cf, int
    P = HCsr();
    P.n = n;
    P.m = nc;
-   P.rp.assign(n + 1, 0);
-   std::vector<int> mark(n, -1), smark(n, -1), chat;
-   std::vector<double> num(n, 0.0);
    auto aval = [&](int k, int l) -> double { // a_kl by search (rows are short)
       for (int q = A.rp[k]; q < A.rp[k + 1]; q++)
          if (A.cj[q] == l) return A.v[q];
       return 0.0;
    };
    auto diag_of = [&](int k) { return aval(k, k); };
-   for (int i = 0; i < n; i++) {
+   rows_parallel(n, P, [&](int r0, int r1, std::vector<int> &cnt, std::vector<int> &pcj, std::vector<double> &pv) {
+   std::vector<int> mark(n, -1), smark(n, -1), chat;
+   std::vector<double> num(n, 0.0);
+   for (int i = r0; i < r1; i++) {
+      const size_t before = pcj.size();
       if (cf[i] == CF_C) {
-         P.cj.push_back(cidx[i]);
-         P.v.push_back(1.0);
-         P.rp[i + 1] = (int)P.cj.size();
+         pcj.push_back(cidx[i]);
+         pv.push_back(1.0);
+         cnt[i] = 1;
          continue;
       }
       for (int a = S.rp[i]; a < S.rp[i + 1]; a++) smark[S.cj[a]] = i;
@@ -341,11 +386,11 @@ void interpolation(const HCsr &A, const HCsr &S, const std::vector<int> &cf, int
          if (sum_c != 0.0 && aii != 0.0) {
             const double alpha = sum_all / sum_c;
             for (int j : chat) {
-               P.cj.push_back(cidx[j]);
-               P.v.push_back(-alpha * num[j] / aii);
+               pcj.push_back(cidx[j]);
+               pv.push_back(-alpha * num[j] / aii);
             }
          }
-         P.rp[i + 1] = (int)P.cj.size();
+         cnt[i] = (int)(pcj.size() - before);
          continue;
       }
       // extended+i
@@ -396,11 +441,12 @@ void interpolation(const HCsr &A, const HCsr &S, const std::vector<int> &cf, int
       std::sort(chat.begin(), chat.end());
       if (atil != 0.0)
          for (int j : chat) {
-            P.cj.push_back(cidx[j]);
-            P.v.push_back(-num[j] / atil);
+            pcj.push_back(cidx[j]);
+            pv.push_back(-num[j] / atil);
          }
-      P.rp[i + 1] = (int)P.cj.size();
+      cnt[i] = (int)(pcj.size() - before);
    }
+   });
 }
 
 } // namespace

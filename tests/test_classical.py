@@ -185,3 +185,27 @@ def test_pmis_seed_and_errors(amg, oracle):
         amg.classical.ClassicalAMG(A.nrows, A.rowptr, A.col, A.val, coarsen_type=3)
     with pytest.raises(amg.AmgError, match="num_functions"):
         amg.classical.ClassicalAMG(A.nrows, A.rowptr, A.col, A.val, num_functions=7)
+
+
+@pytest.mark.parametrize("ct,it", [(9, 6), (10, 6), (9, 3)])
+def test_threaded_setup_identical(amg, monkeypatch, ct, it):
+    """Strength and interpolation run over row ranges on host threads
+    (AMG_SETUP_THREADS); the ranges are concatenated in row order, so every
+    level's A, P and R is identical to the single-thread build (elasticity r=3,
+    3 functions; with the variable set every level of >= 64 rows splits)."""
+    n, rp, cj, v, _ = amg.classical.elasticity(3)
+    mats = {}
+    for t in ("1", "5"):
+        monkeypatch.setenv("AMG_SETUP_THREADS", t)
+        H = amg.classical.ClassicalAMG(n, rp, cj, v, coarsen_type=ct, strong_threshold=0.5, num_functions=3,
+                                       interp_type=it)
+        mats[t] = [H.get(w, l) for l in range(H.L) for w in (amg.AMG_GEN_A, amg.AMG_GEN_P, amg.AMG_GEN_R)
+                   if not (w != amg.AMG_GEN_A and l == H.L - 1)]
+        H.free()
+    assert len(mats["1"]) == len(mats["5"]) >= 6
+    for a, b in zip(mats["1"], mats["5"]):
+        assert a[0] == b[0] and a[1] == b[1]
+        for x, y in zip(a[2:], b[2:]):
+            assert np.array_equal(x, y)
+            if x.dtype == np.float64:
+                assert np.array_equal(x.view(np.int64), y.view(np.int64))
