@@ -1713,16 +1713,26 @@ __device__ __forceinline__ v2d geo_prolong_pair(v2d acc, const double *__restric
       if ((y >> 1) < ncy) cy[my] = y >> 1, dy[my++] = 0;
    }
    const bool lo = t >= 1, hi = t < ncx; // row 2t: coarse t - 1 (dx = 2), t (dx = 0)
+   // every (plane, line) candidate's load issued first (absent candidates read
+   // the first one's, unused), then the terms added in P's CSR order
+   if (my < 2) cy[1] = cy[0];
+   if (mz < 2) cz[1] = cz[0];
+   v2d ev[2][2];
+#pragma unroll
+   for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int b = 0; b < 2; b++) {
+         const long long cb = ((long long)cz[a] * ncy + cy[b]) * ncx + t;
+         // e[cb - 1], e[cb]; the first is unused (and clamped) at t = 0
+         ev[a][b] = *reinterpret_cast<const v2du *>(e + (lo ? cb - 1 : cb));
+      }
 #pragma unroll
    for (int a = 0; a < 2; a++) {
       if (a >= mz) break;
 #pragma unroll
       for (int b = 0; b < 2; b++) {
          if (b >= my) break;
-         const long long cb = ((long long)cz[a] * ncy + cy[b]) * ncx + t;
-         // e[cb - 1], e[cb]; the first is unused (and clamped) at t = 0
-         const v2d ev = *reinterpret_cast<const v2du *>(e + (lo ? cb - 1 : cb));
-         const double em = lo ? ev.x : 0.0, ec = lo ? ev.y : ev.x;
+         const double em = lo ? ev[a][b].x : 0.0, ec = lo ? ev[a][b].y : ev[a][b].x;
          const double *w = wl + dz[a] * 9 + dy[b] * 3;
          if (lo) acc.x = acc.x + w[2] * em;
          if (hi) acc.x = acc.x + w[0] * ec;
@@ -1768,9 +1778,18 @@ __global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ 
    const long long q = (long long)blockIdx.x * 256 + tid;
    if (q >= npairs) return;
    const long long i = 2 * q;
-   const int x = (int)(i % nx);
-   const long long yz = i / nx;
-   const int y = (int)(yz % ny), z = (int)(yz / ny);
+   int x, y, z;
+   if (npairs < (1LL << 30)) { // 32-bit index arithmetic (the 64-bit divisions are emulated)
+      const unsigned iu = (unsigned)i, yz = iu / (unsigned)nx;
+      x = (int)(iu - yz * (unsigned)nx);
+      y = (int)(yz % (unsigned)ny);
+      z = (int)(yz / (unsigned)ny);
+   } else {
+      x = (int)(i % nx);
+      const long long yz = i / nx;
+      y = (int)(yz % ny);
+      z = (int)(yz / ny);
+   }
    const v2d acc = *reinterpret_cast<const v2du *>(u + i);
    *reinterpret_cast<v2du *>(u + i) = geo_prolong_pair(acc, e, wl, x, y, z, nx >> 1, ny >> 1, nz >> 1);
 }
@@ -1931,9 +1950,18 @@ __global__ __launch_bounds__(256) void geo_restrict_k(const double *__restrict__
    const long long K = (long long)blockIdx.x * 256 + tid;
    if (K >= nc) return;
    const int ncx = nx >> 1, ncy = ny >> 1;
-   const int Kx = (int)(K % ncx);
-   const long long t = K / ncx;
-   const int Ky = (int)(t % ncy), Kz = (int)(t / ncy);
+   int Kx, Ky, Kz;
+   if (nc < (1LL << 31)) { // 32-bit index arithmetic (the 64-bit divisions are emulated)
+      const unsigned t = (unsigned)K / (unsigned)ncx;
+      Kx = (int)((unsigned)K - t * (unsigned)ncx);
+      Ky = (int)(t % (unsigned)ncy);
+      Kz = (int)(t / (unsigned)ncy);
+   } else {
+      Kx = (int)(K % ncx);
+      const long long t = K / ncx;
+      Ky = (int)(t % ncy);
+      Kz = (int)(t / ncy);
+   }
    const bool dx2 = 2 * Kx + 2 < nx;
    double acc = 0.0;
 #pragma unroll
