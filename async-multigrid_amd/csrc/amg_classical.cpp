@@ -35,6 +35,12 @@ int amg_spgemm_device(int device, int An, const std::vector<int> &arp, const std
                       const std::vector<double> &av, int Bn, const std::vector<int> &brp,
                       const std::vector<int> &bcj, const std::vector<double> &bv, int Bm, std::vector<int> &crp,
                       std::vector<int> &ccj, std::vector<double> &cv);
+// A_c = R (A P) on a GPU with A P kept on the device, bit-identical to two spgemm() calls
+int amg_rap_device(int device, int An, const std::vector<int> &arp, const std::vector<int> &acj,
+                   const std::vector<double> &av, const std::vector<int> &prp, const std::vector<int> &pcj,
+                   const std::vector<double> &pv, int Pm, int Rn, const std::vector<int> &rrp,
+                   const std::vector<int> &rcj, const std::vector<double> &rv, std::vector<int> &crp,
+                   std::vector<int> &ccj, std::vector<double> &cv);
 
 namespace {
 
@@ -522,12 +528,9 @@ extern "C" int amg_classical_setup(const amg_classical_opts *o, int n, const int
       HCsr R, AP, Ac;
       transpose(P, R);
       if (o->device >= 0) {
-         AP.n = A.n, AP.m = P.m;
-         Ac.n = R.n, Ac.m = AP.m;
-         int st = amg_spgemm_device(o->device, A.n, A.rp, A.cj, A.v, P.n, P.rp, P.cj, P.v, P.m, AP.rp, AP.cj, AP.v);
-         if (st == AMG_OK)
-            st = amg_spgemm_device(o->device, R.n, R.rp, R.cj, R.v, AP.n, AP.rp, AP.cj, AP.v, AP.m, Ac.rp, Ac.cj,
-                                   Ac.v);
+         Ac.n = R.n, Ac.m = P.m;
+         const int st = amg_rap_device(o->device, A.n, A.rp, A.cj, A.v, P.rp, P.cj, P.v, P.m, R.n, R.rp, R.cj, R.v,
+                                       Ac.rp, Ac.cj, Ac.v);
          if (st != AMG_OK) {
             delete H;
             return st;
