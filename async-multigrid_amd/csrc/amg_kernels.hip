@@ -1963,6 +1963,19 @@ __global__ __launch_bounds__(256) void geo_restrict_k(const double *__restrict__
       Kz = (int)(t / ncy);
    }
    const bool dx2 = 2 * Kx + 2 < nx;
+   // the nine fine (plane, line) loads issued first (lines outside the box
+   // read the last inside one, unused), then the terms in R's CSR order
+   v2d a[3][3];
+   double c[3][3];
+#pragma unroll
+   for (int dz = 0; dz < 3; dz++)
+#pragma unroll
+      for (int dy = 0; dy < 3; dy++) {
+         const int fz = min(2 * Kz + dz, nz - 1), fy = min(2 * Ky + dy, ny - 1);
+         const double *p = r + ((long long)fz * ny + fy) * nx + 2 * Kx;
+         a[dz][dy] = *reinterpret_cast<const v2du *>(p);
+         c[dz][dy] = dx2 ? p[2] : 0.0;
+      }
    double acc = 0.0;
 #pragma unroll
    for (int dz = 0; dz < 3; dz++) {
@@ -1970,12 +1983,10 @@ __global__ __launch_bounds__(256) void geo_restrict_k(const double *__restrict__
 #pragma unroll
       for (int dy = 0; dy < 3; dy++) {
          if (2 * Ky + dy >= ny) break;
-         const double *p = r + ((long long)(2 * Kz + dz) * ny + 2 * Ky + dy) * nx + 2 * Kx;
-         const v2d a = *reinterpret_cast<const v2du *>(p);
          const double *w = wl + dz * 9 + dy * 3;
-         acc = acc + w[0] * a.x;
-         acc = acc + w[1] * a.y;
-         if (dx2) acc = acc + w[2] * p[2];
+         acc = acc + w[0] * a[dz][dy].x;
+         acc = acc + w[1] * a[dz][dy].y;
+         if (dx2) acc = acc + w[2] * c[dz][dy];
       }
    }
    fc[K] = acc;
