@@ -104,6 +104,10 @@ class Context:
         """3x3 block form of num_functions = 3 operators for matrices registered from now on (default on)."""
         check(lib.amg_set_bsr3(self.h, int(enable)))
 
+    def set_jgs_wave(self, enable):
+        """Hybrid JGS: one wave per block (default) or one lane per block (0); bit-identical."""
+        check(lib.amg_set_jgs_wave(self.h, int(enable)))
+
     def set_fuse_prolong(self, enable):
         """Prolongation fused into the first post-smoothing sweep of marched geometric levels (default off: VALU-bound, slower)."""
         check(lib.amg_set_fuse_prolong(self.h, int(enable)))

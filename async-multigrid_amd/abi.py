@@ -130,6 +130,7 @@ PROTOTYPES = {
     "amg_set_fuse_transfer": (_i, [_p, _i]),
     "amg_hier_fused_prolong": (_i, [_p]),
     "amg_set_fuse_prolong": (_i, [_p, _i]),
+    "amg_set_jgs_wave": (_i, [_p, _i]),
     "amg_set_march_lines": (_i, [_p, _i]),
     "amg_hier_set_opts": (_i, [_p, C.POINTER(AmgOpts)]),
     "amg_hier_set_blocks": (_i, [_p, _i, _ip, _i]),
@@ -170,6 +171,8 @@ PROTOTYPES = {
     "amg_dist_allreduce_sum": (_i, [_p, _dp, _i]),
     "amg_dist_barrier": (_i, [_p]),
     "amg_dist_hier_create_structured": (_i, [_p, _p, C.POINTER(AmgOpts), _pp]),
+    "amg_dist_hier_create_slab": (_i, [_p, _p, C.POINTER(AmgOpts), _pp]),
+    "amg_dist_hier_slab_info": (_i, [_p, _ip, _ip, _ip]),
     "amg_dist_hier_local_rows": (_i, [_p, _i, _ip, _ip]),
     "amg_dist_hier_matrix_info": (_i, [_p, _i, _llp, _ip, _ip, _ip]),
     "amg_dist_hier_pair_pattern": (_i, [_p, _i, _ip]),

@@ -98,6 +98,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_PLANE_MARCH_XCD")) c->mz_xcd = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_JGS_WAVE")) c->jgs_wave = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ_EDGE")) c->mz_edge = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
@@ -709,6 +710,18 @@ int amg_mat_finish(amg_mat *A)
 {
    amgk::extract_diag(A->ctx->stream, A);
    AMG_HIP(hipGetLastError());
+   {
+      int *d = nullptr;
+      AMG_HIP(hipMalloc(&d, sizeof(int)));
+      AMG_HIP(hipMemsetAsync(d, 0, sizeof(int), A->ctx->stream));
+      amgk::row_max(A->ctx->stream, A, d);
+      int h = 0;
+      hipError_t e = hipMemcpyAsync(&h, d, sizeof(int), hipMemcpyDeviceToHost, A->ctx->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(A->ctx->stream);
+      hipFree(d);
+      if (e != hipSuccess) return amg_set_error(AMG_ERR_HIP, "amg_mat_finish: %s", hipGetErrorString(e));
+      A->maxrow = h;
+   }
    if (A->ctx->value_index && A->nnz > 0) AMG_TRY(build_value_index(A));
    if (A->ctx->dict_index && A->vidx) AMG_TRY(build_dict_index(A));
    if (A->ctx->row_pattern && A->didx) AMG_TRY(build_row_pattern(A));
@@ -780,6 +793,13 @@ extern "C" int amg_set_plane_march(amg_ctx *c, int enable, int zc, int xcd)
    if (zc > 0) c->mz_zc = zc, c->mz_zc_auto = 0;
    if (zc == -1) c->mz_zc = 16, c->mz_zc_auto = 1;
    if (xcd >= 0) c->mz_xcd = xcd ? 1 : 0;
+   return AMG_OK;
+}
+
+extern "C" int amg_set_jgs_wave(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_jgs_wave: null context");
+   c->jgs_wave = enable ? 1 : 0;
    return AMG_OK;
 }
 

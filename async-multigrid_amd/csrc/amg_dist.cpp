@@ -280,6 +280,47 @@ int amgd::dvec(amg_dist_hier *D, size_t n, double **p)
    return dalloc(D, n * sizeof(double), (void **)p);
 }
 
+int amgd::lvec(amg_dist_hier *D, int l, double **p) { return lvec2(D, l, l, p); }
+
+int amgd::lvec2(amg_dist_hier *D, int la, int lb, double **p)
+{
+   long long off = 0, tail = 1;
+   for (int l : {la, lb}) {
+      if (l < D->Ld) {
+         const DLevel &v = D->lv[l];
+         if (D->slab) {
+            off = std::max(off, v.sg.off());
+            tail = std::max(tail, v.sg.ext_rows() - v.sg.off());
+         } else {
+            tail = std::max(tail, (long long)std::max(v.cap, v.n));
+         }
+      } else if (l - D->Ld < (int)D->cA.size()) {
+         tail = std::max(tail, (long long)D->cA[l - D->Ld]->nrows);
+      }
+   }
+   double *b = nullptr;
+   AMG_TRY(dvec(D, (size_t)(off + tail), &b));
+   *p = b + off;
+   return AMG_OK;
+}
+
+int amgd::dist_check_opts(const amg_opts *o)
+{
+   AMG_ARG(o->cheby_flag == 0 && (o->smoother == AMG_JACOBI || o->smoother == AMG_L1_JACOBI ||
+                                   o->smoother == AMG_SYMM_JACOBI),
+           "amg_dist: the distributed cycles support the Jacobi / L1 Jacobi / symmetric Jacobi "
+           "smoothers without the SMEM Chebyshev (use accel_type, DMEM_ChebyUpdate)");
+   AMG_ARG(o->accel_type == AMG_NO_ACCEL || o->accel_type == AMG_RICHARD_ACCEL ||
+              o->accel_type == AMG_CHEBY_RECUR_ACCEL,
+           "amg_dist: accel_type %d (AMG_NO_ACCEL / AMG_RICHARD_ACCEL / AMG_CHEBY_RECUR_ACCEL)",
+           o->accel_type);
+   AMG_ARG(o->cheby_grid >= 0, "amg_dist: cheby_grid %d < 0", o->cheby_grid);
+   AMG_ARG(o->solver == AMG_MULT || o->solver == AMG_ASYNC_MULTADD || o->solver == AMG_ASYNC_AFACX,
+           "amg_dist: solver must be MULT (amg_dist_solve_*) or ASYNC_MULTADD / ASYNC_AFACX "
+           "(amg_dist_async_solve)");
+   return AMG_OK;
+}
+
 namespace {
 
 // owner of global column g of a level's column space: the rank r with
@@ -538,22 +579,7 @@ using LocalFn = std::function<int(int which, int level, HostRows &out)>;
 // every row of operator `which` of level l (replicated levels), registered on the device
 using FullFn = std::function<int(int which, int level, amg_mat **out)>;
 
-int check_opts(const amg_opts *o)
-{
-   AMG_ARG(o->cheby_flag == 0 && (o->smoother == AMG_JACOBI || o->smoother == AMG_L1_JACOBI ||
-                                   o->smoother == AMG_SYMM_JACOBI),
-           "amg_dist: the distributed cycles support the Jacobi / L1 Jacobi / symmetric Jacobi "
-           "smoothers without the SMEM Chebyshev (use accel_type, DMEM_ChebyUpdate)");
-   AMG_ARG(o->accel_type == AMG_NO_ACCEL || o->accel_type == AMG_RICHARD_ACCEL ||
-              o->accel_type == AMG_CHEBY_RECUR_ACCEL,
-           "amg_dist: accel_type %d (AMG_NO_ACCEL / AMG_RICHARD_ACCEL / AMG_CHEBY_RECUR_ACCEL)",
-           o->accel_type);
-   AMG_ARG(o->cheby_grid >= 0, "amg_dist: cheby_grid %d < 0", o->cheby_grid);
-   AMG_ARG(o->solver == AMG_MULT || o->solver == AMG_ASYNC_MULTADD || o->solver == AMG_ASYNC_AFACX,
-           "amg_dist: solver must be MULT (amg_dist_solve_*) or ASYNC_MULTADD / ASYNC_AFACX "
-           "(amg_dist_async_solve)");
-   return AMG_OK;
-}
+int check_opts(const amg_opts *o) { return dist_check_opts(o); }
 
 // levels [0, Ld) distributed, [Ld, L) replicated: the first level with fewer
 // rows than replicate_rows, at least level 1, at most L-1 (coarsest replicated)
@@ -573,7 +599,7 @@ int build_hier(amg_ctx *c, int L, Partition part, const amg_opts *opts, const Lo
                const FullFn &full, amg_dist_hier **out)
 {
    amg_transport *t = c->xport;
-   const int R = t->nranks, me = t->rank;
+   const int me = t->rank;
    auto D = std::make_unique<amg_dist_hier>();
    D->ctx = c;
    D->o = *opts;
@@ -624,43 +650,7 @@ int build_hier(amg_ctx *c, int L, Partition part, const amg_opts *opts, const Lo
       AMG_TRY(dvec(D.get(), std::max(1, D->lv[0].n), &D->d_acc));
    }
    // replicated coarse hierarchy (identical on every rank, no communication)
-   if (Ld < L) {
-      const int Lc = L - Ld;
-      std::vector<amg_mat *> As(Lc), Ps(std::max(1, Lc - 1)), Rs(std::max(1, Lc - 1));
-      for (int l = Ld; l < L; l++) {
-         AMG_TRY(full(AMG_GEN_A, l, &As[l - Ld]));
-         D->coarse_mats.push_back(As[l - Ld]);
-         if (l < L - 1) {
-            AMG_TRY(full(AMG_GEN_P, l, &Ps[l - Ld]));
-            D->coarse_mats.push_back(Ps[l - Ld]);
-            AMG_TRY(full(AMG_GEN_R, l, &Rs[l - Ld]));
-            D->coarse_mats.push_back(Rs[l - Ld]);
-         }
-      }
-      D->cA.assign(As.begin(), As.end());
-      D->cP.assign(Ps.begin(), Ps.begin() + (Lc - 1));
-      D->cR.assign(Rs.begin(), Rs.begin() + (Lc - 1));
-      amg_opts co = *opts;
-      co.solver = AMG_MULT; // the replicated levels run the multiplicative sub-cycle
-      co.profile = 0;
-      co.reuse_outer_residual = 0;
-      AMG_TRY(amg_hier_create(c, Lc, As.data(), Ps.data(), Rs.data(), &co, &D->coarse));
-      AMG_TRY(dvec(D.get(), D->part.total(Ld), &D->f_rep));
-      // allgather blocks padded to the largest owned row count at level Ld
-      int blk = 0;
-      std::vector<int> cnt(R), dsp(R);
-      for (int r = 0; r < R; r++) {
-         cnt[r] = (int)(D->part.rows_end(Ld, r) - D->part.rows_begin(Ld, r));
-         dsp[r] = (int)D->part.rows_begin(Ld, r);
-         blk = std::max(blk, cnt[r]);
-      }
-      D->gath_blk = blk;
-      AMG_TRY(dvec(D.get(), (size_t)blk * (R + 1), &D->gath_buf));
-      AMG_TRY(dalloc(D.get(), R * sizeof(int), (void **)&D->d_gcnt));
-      AMG_TRY(dalloc(D.get(), R * sizeof(int), (void **)&D->d_gdsp));
-      AMG_TRY(h2d(c->stream, D->d_gcnt, cnt.data(), R * sizeof(int)));
-      AMG_TRY(h2d(c->stream, D->d_gdsp, dsp.data(), R * sizeof(int)));
-   }
+   if (Ld < L) AMG_TRY(dist_build_replicated(D.get(), full));
    AMG_HIP(hipStreamSynchronize(c->stream));
    *out = D.release();
    return AMG_OK;
@@ -696,11 +686,56 @@ int host_allgatherv(amg_ctx *c, const void *mine, long long bytes, std::vector<c
 
 } // namespace
 
+// the replicated coarse levels [Ld, L): the same sub-hierarchy on every rank
+// (no communication), fed by one allgather of the restricted residual
+int amgd::dist_build_replicated(amg_dist_hier *D, const std::function<int(int, int, amg_mat **)> &full)
+{
+   amg_ctx *c = D->ctx;
+   const int R = c->xport->nranks, L = D->L, Ld = D->Ld;
+   const amg_opts *opts = &D->o;
+   const int Lc = L - Ld;
+   std::vector<amg_mat *> As(Lc), Ps(std::max(1, Lc - 1)), Rs(std::max(1, Lc - 1));
+   for (int l = Ld; l < L; l++) {
+      AMG_TRY(full(AMG_GEN_A, l, &As[l - Ld]));
+      D->coarse_mats.push_back(As[l - Ld]);
+      if (l < L - 1) {
+         AMG_TRY(full(AMG_GEN_P, l, &Ps[l - Ld]));
+         D->coarse_mats.push_back(Ps[l - Ld]);
+         AMG_TRY(full(AMG_GEN_R, l, &Rs[l - Ld]));
+         D->coarse_mats.push_back(Rs[l - Ld]);
+      }
+   }
+   D->cA.assign(As.begin(), As.end());
+   D->cP.assign(Ps.begin(), Ps.begin() + (Lc - 1));
+   D->cR.assign(Rs.begin(), Rs.begin() + (Lc - 1));
+   amg_opts co = *opts;
+   co.solver = AMG_MULT; // the replicated levels run the multiplicative sub-cycle
+   co.profile = 0;
+   co.reuse_outer_residual = 0;
+   AMG_TRY(amg_hier_create(c, Lc, As.data(), Ps.data(), Rs.data(), &co, &D->coarse));
+   AMG_TRY(dvec(D, D->part.total(Ld), &D->f_rep));
+   // allgather blocks padded to the largest owned row count at level Ld
+   int blk = 0;
+   std::vector<int> cnt(R), dsp(R);
+   for (int r = 0; r < R; r++) {
+      cnt[r] = (int)(D->part.rows_end(Ld, r) - D->part.rows_begin(Ld, r));
+      dsp[r] = (int)D->part.rows_begin(Ld, r);
+      blk = std::max(blk, cnt[r]);
+   }
+   D->gath_blk = blk;
+   AMG_TRY(dvec(D, (size_t)blk * (R + 1), &D->gath_buf));
+   AMG_TRY(dalloc(D, R * sizeof(int), (void **)&D->d_gcnt));
+   AMG_TRY(dalloc(D, R * sizeof(int), (void **)&D->d_gdsp));
+   AMG_TRY(h2d(c->stream, D->d_gcnt, cnt.data(), R * sizeof(int)));
+   AMG_TRY(h2d(c->stream, D->d_gdsp, dsp.data(), R * sizeof(int)));
+   return AMG_OK;
+}
+
 // z-plane slabs of the structured problem: level-0 planes split evenly; coarse
 // plane k follows the owner of the fine plane it is injected from (2k+1 under
 // linear interpolation, the aggregate's second plane under aggregation), so
 // restriction and prolongation only touch neighbouring slabs
-static void structured_planes(const amg_gen *g, int R, std::vector<std::vector<int>> &z0)
+void amgd::structured_planes(const amg_gen *g, int R, std::vector<std::vector<int>> &z0)
 {
    const int L = amg_gen_num_levels(g);
    std::vector<int> nz(L);
@@ -947,6 +982,7 @@ int d_smooth(amg_dist_hier *D, int l, const double *f, int sweeps, bool allow_re
 // correction in lv[0].u
 int d_vcycle(amg_dist_hier *D, bool precond)
 {
+   if (D->slab) return slab_vcycle(D, precond);
    amg_ctx *c = D->ctx;
    hipStream_t s = c->stream;
    const int L = D->L, Ld = D->Ld;
@@ -1000,6 +1036,7 @@ int d_vcycle(amg_dist_hier *D, bool precond)
 
 int d_outer_residual(amg_dist_hier *D, int slot)
 {
+   if (D->slab) return slab_outer_residual(D, slot);
    amg_ctx *c = D->ctx;
    hipStream_t s = c->stream;
    DLevel &v = D->lv[0];
@@ -1063,6 +1100,7 @@ bool amgd::AccelState::next(const amg_opts &o, double *om1, double *omd)
 
 int amgd::dist_solve_begin(amg_dist_hier *D, const double *f_local)
 {
+   if (D->slab) return slab_solve_begin(D, f_local);
    amg_ctx *c = D->ctx;
    for (auto &v : D->lv) {
       for (double *p : {v.f, v.u, v.u_alt, v.r_fine}) amgk::vset(c->stream, p, 0.0, 0, v.cap);
@@ -1176,6 +1214,7 @@ extern "C" int amg_dist_profile_read(amg_dist_hier *D, double *ms, long long *la
 extern "C" int amg_dist_fine_spmv(amg_dist_hier *D, int reps, double *ms)
 {
    AMG_ARG(D && ms && reps >= 1, "amg_dist_fine_spmv: bad argument");
+   if (D->slab) return slab_fine_spmv(D, reps, ms);
    amg_ctx *c = D->ctx;
    DLevel &v = D->lv[0];
    hipEvent_t a, b;

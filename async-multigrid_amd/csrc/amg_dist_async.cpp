@@ -54,6 +54,10 @@ int level_cap(const amg_dist_hier *D, int l)
    return l < D->Ld ? D->lv[l].cap : D->cA[l - D->Ld]->nrows;
 }
 
+// the level stream's exchange of a slab vector's ghost planes, through the
+// comm stream (XchgFn of slab_restrict / slab_prolong)
+XchgFn level_xchg(amg_dist_hier *D, AsyncLevel &a);
+
 // hand the level stream's work to the comm stream (and back): the RCCL
 // operation runs on c->comm_stream after everything level k issued before it
 int to_comm(amg_dist_hier *D, AsyncLevel &a)
@@ -74,6 +78,10 @@ int from_comm(amg_dist_hier *D, AsyncLevel &a)
 // the comm stream over the main communicator
 int a_halo(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x)
 {
+   if (M.slab) {
+      if (M.replicated_cols || D->ctx->xport->nranks == 1) return AMG_OK;
+      return level_xchg(D, a)(x, M.ncol_own, M.cP, M.nlo, M.nhi);
+   }
    if (M.replicated_cols || M.peers.empty()) return AMG_OK;
    double *&sb = a.sbuf[&M];
    if (!sb) AMG_TRY(dvec(D, std::max<long long>(1, M.nsend), &sb));
@@ -97,8 +105,20 @@ int a_spgemv(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x, const doubl
              const amgk::Gemv &g, double *y)
 {
    AMG_TRY(a_halo(D, a, M, x));
-   amgk::spgemv(a.s, M.A, x, b, g, y, 0, M.nrows, nullptr);
+   if (M.slab)
+      slab_spgemv(a.s, M, x, b, g, y, 0, M.nrows, nullptr);
+   else
+      amgk::spgemv(a.s, M.A, x, b, g, y, 0, M.nrows, nullptr);
    return AMG_OK;
+}
+
+XchgFn level_xchg(amg_dist_hier *D, AsyncLevel &a)
+{
+   return [D, &a](double *x, long long n, long long cP, const std::vector<int> &lo, const std::vector<int> &hi) {
+      AMG_TRY(to_comm(D, a));
+      AMG_TRY(slab_xchg(D->ctx, D->ctx->comm_stream, x, n, cP, lo, hi));
+      return from_comm(D, a);
+   };
 }
 
 // y = A_l x (+ b per g) on level l
@@ -112,7 +132,8 @@ int apply_A(amg_dist_hier *D, AsyncLevel &a, int l, double *x, const double *b, 
 
 const double *diag_of(const amg_dist_hier *D, int l)
 {
-   return l < D->Ld ? D->lv[l].A.A->diag : D->cA[l - D->Ld]->diag;
+   if (l < D->Ld) return D->slab ? slab_diag(D->lv[l].A) : D->lv[l].A.A->diag;
+   return D->cA[l - D->Ld]->diag;
 }
 
 const double *l1_of(const amg_dist_hier *D, int l)
@@ -125,11 +146,15 @@ int restrict_to(amg_dist_hier *D, AsyncLevel &a, int l)
 {
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    const int Ld = D->Ld;
+   if (D->slab && l + 1 < Ld) return slab_restrict(D, a.s, l, a.r[l], a.r[l + 1], level_xchg(D, a));
    if (l + 1 < Ld) return a_spgemv(D, a, D->lv[l].R, a.r[l], nullptr, mv, a.r[l + 1]);
    if (l + 1 == Ld) {
       const int R = D->ctx->xport->nranks;
       double *slot = a.gath + (size_t)D->gath_blk * R;
-      AMG_TRY(a_spgemv(D, a, D->lv[l].R, a.r[l], nullptr, mv, slot));
+      if (D->slab)
+         AMG_TRY(slab_restrict(D, a.s, l, a.r[l], slot, level_xchg(D, a)));
+      else
+         AMG_TRY(a_spgemv(D, a, D->lv[l].R, a.r[l], nullptr, mv, slot));
       AMG_TRY(to_comm(D, a));
       AMG_TRY(xp_allgather(D->ctx, D->ctx->comm_stream, slot, a.gath, (long long)D->gath_blk * 8));
       AMG_TRY(from_comm(D, a));
@@ -144,6 +169,7 @@ int restrict_to(amg_dist_hier *D, AsyncLevel &a, int l)
 int prolong_to(amg_dist_hier *D, AsyncLevel &a, int l, double *x, double *out)
 {
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   if (D->slab && l < D->Ld) return slab_prolong(D, a.s, l, x, out, false, level_xchg(D, a));
    if (l < D->Ld) return a_spgemv(D, a, D->lv[l].P, x, nullptr, mv, out);
    amgk::spgemv(a.s, D->cP[l - D->Ld], x, nullptr, mv, out, 0, level_n(D, l), nullptr);
    return AMG_OK;
@@ -187,7 +213,10 @@ int a_smooth(amg_dist_hier *D, AsyncLevel &a, int l, const double *f, double *u,
          if (l < D->Ld) {
             DistMat &M = D->lv[l].A;
             AMG_TRY(a_halo(D, a, M, a.u_prev));
-            amgk::jacobi_sweep(s, M.A, f, a.u_prev, l1v, omega, u, 0, n);
+            if (M.slab)
+               slab_jacobi(s, M, f, a.u_prev, l1v, omega, u, 0, n);
+            else
+               amgk::jacobi_sweep(s, M.A, f, a.u_prev, l1v, omega, u, 0, n);
          } else {
             amgk::jacobi_sweep(s, D->cA[l - D->Ld], f, a.u_prev, l1v, omega, u, 0, n);
          }
@@ -277,19 +306,18 @@ int setup_async(amg_dist_hier *D)
       const int coarsest = std::min(L - 1, multadd ? k : k + 1);
       a.r.assign(coarsest + 1, nullptr);
       a.e.assign(k + 1, nullptr);
-      for (int l = 0; l <= coarsest; l++) AMG_TRY(dvec(D, level_cap(D, l), &a.r[l]));
-      for (int l = 0; l <= k; l++) AMG_TRY(dvec(D, level_cap(D, l), &a.e[l]));
-      const int ck = level_cap(D, k), ck1 = level_cap(D, std::min(L - 1, k + 1));
-      const int cm = std::max(ck, ck1);
-      AMG_TRY(dvec(D, D->lv[0].cap, &a.u_priv));
-      AMG_TRY(dvec(D, std::max(cm, D->lv[0].n), &a.y));
-      AMG_TRY(dvec(D, cm, &a.u_prev));
-      AMG_TRY(dvec(D, cm, &a.sy));
-      AMG_TRY(dvec(D, cm, &a.sr));
+      for (int l = 0; l <= coarsest; l++) AMG_TRY(lvec(D, l, &a.r[l]));
+      for (int l = 0; l <= k; l++) AMG_TRY(lvec(D, l, &a.e[l]));
+      const int k1 = std::min(L - 1, k + 1);
+      AMG_TRY(lvec(D, 0, &a.u_priv));
+      AMG_TRY(lvec2(D, 0, k1, &a.y));
+      AMG_TRY(lvec2(D, k, k1, &a.u_prev));
+      AMG_TRY(lvec2(D, k, k1, &a.sy));
+      AMG_TRY(lvec2(D, k, k1, &a.sr));
       if (!multadd) {
-         AMG_TRY(dvec(D, ck, &a.uf));
-         AMG_TRY(dvec(D, ck1, &a.uc));
-         AMG_TRY(dvec(D, ck, &a.rf));
+         AMG_TRY(lvec(D, k, &a.uf));
+         AMG_TRY(lvec(D, k1, &a.uc));
+         AMG_TRY(lvec(D, k, &a.rf));
       }
       if (Ld < L) AMG_TRY(dvec(D, (size_t)D->gath_blk * (t->nranks + 1), &a.gath));
    }
@@ -312,6 +340,8 @@ int amgd::grid_prepare(amg_dist_hier *D, int k)
 {
    const int L = D->L, Ld = D->Ld;
    AMG_ARG(k >= 0 && k < L, "amg_grid_add: grid %d outside [0, %d)", k, L);
+   AMG_ARG(!D->slab, "amg_grid_add: use a row-partitioned hierarchy (amg_dist_hier_create[_structured]), "
+                     "not a z-slab one");
    GridState &g = D->grid;
    if (g.ready && g.k == k) return AMG_OK;
    AMG_ARG(!g.ready, "amg_grid_add: the hierarchy already serves grid %d", g.k);
@@ -617,6 +647,8 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
                      long long *relaxations)
 {
    AMG_ARG(D && f_local && sweeps >= 0, "amg_dist_async_jacobi: bad argument");
+   AMG_ARG(!D->slab, "amg_dist_async_jacobi / _sps: use a row-partitioned hierarchy "
+                     "(amg_dist_hier_create[_structured]), not a z-slab one");
    AMG_ARG(!sps || D->o.accel_type == AMG_NO_ACCEL, "amg_dist_async_sps: no accel_type with SPS gating");
    amg_ctx *c = D->ctx;
    hipStream_t s = c->stream, cs = c->comm_stream;

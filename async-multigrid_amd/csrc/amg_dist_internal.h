@@ -5,6 +5,7 @@
 
 #include <rccl/rccl.h>
 
+#include <functional>
 #include <map>
 #include <vector>
 
@@ -37,6 +38,22 @@ struct Partition {
    long long total(int l) const { return rs[l].back(); }
 };
 
+// z-slab form of a distributed level of the structured problem
+// (amg_dist_hier_create_slab): the rank owns planes [za, zb) of the level's
+// nx * ny * nz box; its vectors hold glo / ghi ghost planes below / above the
+// owned rows (the pointers the cycle passes around point at the first owned
+// row, so the ghost planes sit at negative offsets and past the end)
+struct SlabGeom {
+   int nx = 0, ny = 0, nz = 0;
+   long long P = 0; // rows per plane
+   int za = 0, zb = 0;
+   int glo = 0, ghi = 0;
+   long long off() const { return glo * P; }
+   long long ext_rows() const { return (long long)(zb - za + glo + ghi) * P; }
+   int e0() const { return za - glo; } // global plane of the extended base
+   int nzl() const { return zb - za; }
+};
+
 struct DistMat {
    amg_mat *A = nullptr;        // local rows, remapped columns
    long long row0 = 0;          // first global row
@@ -51,6 +68,15 @@ struct DistMat {
    int *d_send_idx = nullptr;   // owned-column index list of all sends
    long long nsend = 0;
    double *sendbuf = nullptr;
+   // slab form: A is the extended operator (rows / columns of the ghost planes
+   // around the owned ones, amg_gen_register_ext); the owned rows are its rows
+   // [sro, sro + nrows), the column vector's extended base is x - sco.
+   // nlo[r] / nhi[r]: column planes below / above rank r's owned column planes
+   // that rank r's rows read (its ghost planes, received from r -+ 1); cP:
+   // column rows per plane
+   bool slab = false;
+   long long sro = 0, sco = 0, cP = 0;
+   std::vector<int> nlo, nhi;
 };
 
 struct DLevel {
@@ -60,6 +86,12 @@ struct DLevel {
    DistMat A, P, R;            // P: level l -> l+1 (rows = level l), R: rows = level l+1
    double *f = nullptr, *u = nullptr, *u_alt = nullptr, *r_fine = nullptr, *l1 = nullptr;
    int zero_flag = 0;
+   // slab form
+   SlabGeom sg;
+   bool geo = false;   // R_l / P_l are the box's geometric transfers (checked)
+   amgk::GeoT g{};
+   double *d_geo_w = nullptr;
+   int Ka = 0, Kb = 0; // owned planes of level l + 1
 };
 
 
@@ -127,6 +159,13 @@ struct GridState {
 struct amg_dist_hier {
    amg_ctx *ctx = nullptr;
    amg_opts o{};
+   // z-slab hierarchy (amg_dist_hier_create_slab): slab-form distributed
+   // levels, geometric transfers, fused level-0 residual + restriction (geo0)
+   // reading rr_u* / rr_f* ghost planes of u / f (per rank, below / above)
+   bool slab = false;
+   bool geo0 = false;
+   std::vector<int> rr_ulo, rr_uhi, rr_flo, rr_fhi;
+   amgd::SlabGeom sg_rep; // owned planes of the first replicated level (the allgather blocks)
    int L = 0, Ld = 0; // levels [0, Ld) distributed, [Ld, L) replicated
    amgd::Partition part;
    std::vector<amgd::DLevel> lv;
@@ -164,6 +203,42 @@ struct amg_dist_hier {
 namespace amgd {
 int dalloc(amg_dist_hier *D, size_t bytes, void **p);
 int dvec(amg_dist_hier *D, size_t n, double **p);
+// a level vector: slab levels get their ghost planes around the owned rows
+// (the pointer is the first owned row); lvec2: room for the ghost planes of
+// both levels la and lb (scratch used on either)
+int lvec(amg_dist_hier *D, int l, double **p);
+int lvec2(amg_dist_hier *D, int la, int lb, double **p);
+// ---- slab hierarchies (amg_slab.cpp) ----
+// plane exchange of x's ghost planes for an operator with per-rank needs
+// nlo / nhi (planes of cP rows below / above each rank's n_own owned rows)
+int slab_xchg(amg_ctx *c, hipStream_t s, double *x, long long n_own, long long cP, const std::vector<int> &nlo,
+              const std::vector<int> &nhi);
+// y = alpha A x + beta b on owned rows [rb, re) of a slab operator (no exchange)
+void slab_spgemv(hipStream_t s, const DistMat &M, const double *x, const double *b, const amgk::Gemv &g,
+                 double *y, long long rb, long long re, double *partials);
+void slab_jacobi(hipStream_t s, const DistMat &M, const double *f, const double *x, const double *l1,
+                 double omega, double *out, long long rb, long long re);
+// the diagonal of the owned rows
+const double *slab_diag(const DistMat &M);
+// level-l transfers of a slab hierarchy on stream s, ghost planes exchanged
+// by xchg(x, M-like needs); restrict: dst = level l+1 owned rows (or the
+// allgather slot when l + 1 is replicated); prolong: out = P_l x (add = false)
+// or u += P_l x (add = true)
+using XchgFn = std::function<int(double *x, long long n_own, long long cP, const std::vector<int> &nlo,
+                                 const std::vector<int> &nhi)>;
+int slab_restrict(amg_dist_hier *D, hipStream_t s, int l, double *r, double *dst, const XchgFn &xchg);
+int slab_prolong(amg_dist_hier *D, hipStream_t s, int l, double *x, double *out, bool add, const XchgFn &xchg);
+// sync cycle pieces of slab hierarchies (amg_dist.cpp dispatches to them)
+int slab_vcycle(amg_dist_hier *D, bool precond);
+int slab_outer_residual(amg_dist_hier *D, int slot);
+int slab_solve_begin(amg_dist_hier *D, const double *f_local);
+int slab_fine_spmv(amg_dist_hier *D, int reps, double *ms);
+// shared construction pieces (amg_dist.cpp)
+int dist_check_opts(const amg_opts *o);
+void structured_planes(const amg_gen *g, int R, std::vector<std::vector<int>> &z0);
+// the replicated coarse levels [Ld, L): full(which, level, &mat) registers
+// every row of an operator; builds D->coarse and the allgather buffers
+int dist_build_replicated(amg_dist_hier *D, const std::function<int(int, int, amg_mat **)> &full);
 // InitVectors + initial outer residual r0 = f - A u (u = 0) and its norm
 int dist_solve_begin(amg_dist_hier *D, const double *f_local);
 // r0 = f - A x, ||r0|| into d_hist[slot] (all ranks); x = dist_iterate(D)

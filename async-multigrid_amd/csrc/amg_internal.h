@@ -105,6 +105,7 @@ struct amg_ctx {
    int mz_nt = 0;          // streaming hints on > 512 MB levels: 1 NT stores, 2 NT rhs loads
    int rr_ring = 0;        // wave-edge residuals through a flag-ordered LDS ring (measured slower: off)
    int rr_occ = 0;         // 5: the fused residual + restriction compiled for 5 waves / SIMD
+   int jgs_wave = 1;       // hybrid JGS one wave per block (rows <= 32 entries); 0: one lane per block
 };
 
 struct amg_mat {
@@ -116,6 +117,7 @@ struct amg_mat {
    double *val = nullptr;
    double *diag = nullptr; // val[rowptr[i]] (the reference's a_ii; the zero pad after the last row)
    int diag_first = 1;
+   int maxrow = -1;          // longest row (amg_mat_finish)
    amg_mat *trans = nullptr; // lazily built transpose for amg_matvec_t
    // value-indexed form (the hot kernels' format when the matrix has at most
    // 256 distinct values): vidx[k] indexes vtab (256 doubles, sorted by bits)
@@ -258,10 +260,12 @@ void jacobi_zero(hipStream_t s, const double *diag, const double *f, const doubl
 // u_new = u + (omega*r)/a (a != 0): Jacobi sweep from a precomputed residual
 void jacobi_from_residual(hipStream_t s, const double *diag, const double *r, const double *l1,
                           double omega, double *u, int rb, int re);
-// hybrid JGS: one lane per block, blocks d_blk[0..nblk] (device), in place on u
+// hybrid JGS: one wave (rows <= 32 entries) or one lane per block, blocks d_blk[0..nblk] (device), in place on u
 void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
                 const int *d_blk, int nblk, const double *diag_scale, double weight, int zero,
                 int reverse);
+// *d_out = max(*d_out, longest row of A)
+void row_max(hipStream_t s, const amg_mat *A, int *d_out);
 // asynchronous / semi-asynchronous Gauss-Seidel, one lane per block, live u
 void async_gs(hipStream_t s, const amg_mat *A, const double *f, double *u, const int *d_blk, int nblk,
               int sweeps, int semi, int reverse);
@@ -273,15 +277,24 @@ struct GeoT {
 };
 // *bad |= 1 unless every row of M equals the geometric form (mode 0: M = R,
 // coarse rows; mode 1: M = P, fine rows): lengths, columns, value bits
-void geo_check(hipStream_t s, const amg_mat *M, int mode, const GeoT &g, int *bad);
+// z-slab forms (rows / columns of an extended slab operator): local rows [rb, re)
+// are global rows + row_g0, local columns global columns + col_g0 (re < 0: all rows)
+void geo_check(hipStream_t s, const amg_mat *M, int mode, const GeoT &g, int *bad, int rb = 0, int re = -1,
+               long long row_g0 = 0, long long col_g0 = 0);
 // fc = R (f - A u) for a plane-marched A with geometric R, without the fine
-// residual vector (bit-identical to the residual SpGEMV + R SpMV)
+// residual vector (bit-identical to the residual SpGEMV + R SpMV).  Slab form:
+// coarse planes [Kb, Ke) (Ke < 0: all), u / f plane 0 = fine plane fz0 (A's
+// rows are those vectors' planes), fc plane 0 = coarse plane cz0
 void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, const double *u, const GeoT &g,
-                          const double *wdev, double *fc);
-// f_c = R r for the checked geometric R of GeoT g (bit-identical to the SpMV)
-void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc);
-// u += P e for the checked geometric P of GeoT g (bit-identical to the SpGEMV)
-void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u);
+                          const double *wdev, double *fc, int Kb = 0, int Ke = -1, int fz0 = 0, int cz0 = 0);
+// f_c = R r for the checked geometric R of GeoT g (bit-identical to the SpMV);
+// coarse planes [Kb, Ke), r plane 0 = fine plane fz0, fc plane 0 = coarse cz0
+void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc, int Kb = 0,
+                  int Ke = -1, int fz0 = 0, int cz0 = 0);
+// u += P e for the checked geometric P of GeoT g (bit-identical to the SpGEMV);
+// fine planes [zb, ze), u plane 0 = fine plane fz0, e plane 0 = coarse cz0
+void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u, int zb = 0,
+                 int ze = -1, int fz0 = 0, int cz0 = 0);
 // DMEM_AddSmooth scale vectors: s = a_ii / w (1 where a_ii = 0) or the L1 row
 // norm l1 (l1 != nullptr), ns = -s (DMEM_Setup.cpp:423-482)
 void dmem_scale(hipStream_t s, const double *diag, const double *l1, double omega, double *sc, double *nsc, int n);

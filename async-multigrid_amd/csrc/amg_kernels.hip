@@ -1019,7 +1019,7 @@ template <int NEG, bool NEED_DIAG, class Epi, bool UNI, int NLN = 1>
 __global__ __launch_bounds__(256) void csr_mz_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ x, int P, int S, int nz, int zc,
-   int npb, int xcd, Epi epi, double *__restrict__ partials)
+   int npb, int xcd, Epi epi, double *__restrict__ partials, int kb, int ke)
 {
    const bool xc_pf = pf_is_x<Epi>::value && epi_pf_vec(epi) == x;
    __shared__ unsigned long long mtab[256];
@@ -1036,7 +1036,9 @@ __global__ __launch_bounds__(256) void csr_mz_kernel(
    int lg = (int)blockIdx.x;
    if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
    const int pblk = lg % npb, chunk = lg / npb;
-   const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
+   // planes [kb, ke) of the nz-plane operator (a z-slab's owned planes; the
+   // planes outside stay readable as x operands)
+   const int k0 = kb + chunk * zc, k1 = min(k0 + zc, ke);
    int blk0 = pblk * 512; // plane offset of the workgroup's first line block
    if (NLN > 1) {
       const int nbx = S / 512;
@@ -1130,7 +1132,7 @@ __global__ __launch_bounds__(256) void csr_mz_kernel(
       for (int w = tid; w < 2 * NLN * (k1 - k0); w += 256) {
          const int it = w / (2 * NLN), i = (w >> 1) % NLN, h = w & 1;
          const double *g = red + (it * NLN + i) * 8 + 4 * h;
-         partials[((long long)(k0 + it) * P + blk0 + i * S) / 256 + h] = ((g[0] + g[1]) + g[2]) + g[3];
+         partials[((long long)(k0 + it - kb) * P + blk0 + i * S) / 256 + h] = ((g[0] + g[1]) + g[2]) + g[3];
       }
    }
 }
@@ -1145,30 +1147,32 @@ static int mz_chunk(const amg_mat *A, int nz, int npb)
 }
 
 template <int NEG, bool NEED_DIAG, class Epi>
-static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Epi &e, double *partials)
+static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Epi &e, double *partials, int kb,
+                      int ke)
 {
    MpSten S;
    for (int j = 0; j < AMG_MP_MAXJ; j++) {
       S.off[j] = A->mp_off[j];
       S.val[j] = A->mp_val[j];
    }
-   const int P = A->mz_P, nz = A->nrows / P, Sx = A->mz_S;
+   const int P = A->mz_P, nz = A->nrows / P, Sx = A->mz_S, nk = ke - kb;
+   if (nk <= 0) return;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
    // two lines per lane (ctx->mz_lines) where the plane splits into line pairs
    if (A->mp_uni && A->ctx->mz_lines == 2 && Sx % 512 == 0 && (P / Sx) % 2 == 0) {
-      const int npb = P / 1024, zc = mz_chunk(A, nz, npb), nch = (nz + zc - 1) / zc;
+      const int npb = P / 1024, zc = mz_chunk(A, nk, npb), nch = (nk + zc - 1) / zc;
       csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 2><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials);
+         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
       return;
    }
-   const int zc = mz_chunk(A, nz, P / 512);
-   const int npb = P / 512, nch = (nz + zc - 1) / zc;
+   const int zc = mz_chunk(A, nk, P / 512);
+   const int npb = P / 512, nch = (nk + zc - 1) / zc;
    if (A->mp_uni)
       csr_mz_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);
+         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
    else
       csr_mz_kernel<NEG, NEED_DIAG, Epi, false><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);
+         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
 }
 
 // ---------------------------------------------------------------------------
@@ -1234,7 +1238,7 @@ template <int NEG, bool NEED_DIAG, class Epi, bool UNI>
 __global__ __launch_bounds__(256) void csr_mz27_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, int dom, int xlo, int xhi, Val27 Hv, const double *__restrict__ x,
-   int P, int S, int nz, int zc, int npb, int xcd, Epi epi, double *__restrict__ partials)
+   int P, int S, int nz, int zc, int npb, int xcd, Epi epi, double *__restrict__ partials, int kb, int ke)
 {
    constexpr unsigned long long FULL = (1ull << 54) - 1;
    const bool xc_pf = pf_is_x<Epi>::value && epi_pf_vec(epi) == x;
@@ -1249,7 +1253,7 @@ __global__ __launch_bounds__(256) void csr_mz27_kernel(
    int lg = (int)blockIdx.x;
    if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
    const int pblk = lg % npb, chunk = lg / npb;
-   const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
+   const int k0 = kb + chunk * zc, k1 = min(k0 + zc, ke); // planes [kb, ke) (csr_mz_kernel)
    const int pos = pblk * 512 + 2 * tid;
    const unsigned Nu = (unsigned)((long long)nz * P);
    Ln4 X[3][3];
@@ -1350,21 +1354,24 @@ __global__ __launch_bounds__(256) void csr_mz27_kernel(
       for (int w = tid; w < 2 * (k1 - k0); w += 256) {
          const int it = w >> 1, h = w & 1;
          const double *g = red + it * 8 + 4 * h;
-         partials[((long long)(k0 + it) * P + pblk * 512) / 256 + h] = ((g[0] + g[1]) + g[2]) + g[3];
+         partials[((long long)(k0 + it - kb) * P + pblk * 512) / 256 + h] = ((g[0] + g[1]) + g[2]) + g[3];
       }
    }
 }
 
 template <int NEG, bool NEED_DIAG, class Epi>
-static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const Epi &e, double *partials)
+static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const Epi &e, double *partials, int kb,
+                        int ke)
 {
    MpSten S;
    for (int j = 0; j < AMG_MP_MAXJ; j++) {
       S.off[j] = A->mp_off[j];
       S.val[j] = A->mp_uni ? A->mp_val[j] : A->mz_domval[j];
    }
-   const int P = A->mz_P, nz = A->nrows / P, zc = mz_chunk(A, nz, P / 512);
-   const int npb = P / 512, nch = (nz + zc - 1) / zc;
+   const int P = A->mz_P, nz = A->nrows / P, nk = ke - kb;
+   if (nk <= 0) return;
+   const int zc = mz_chunk(A, nk, P / 512);
+   const int npb = P / 512, nch = (nk + zc - 1) / zc;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
    Val27 H;
    for (int j = 0; j < 27; j++) H.v[j] = A->mz_hival[j];
@@ -1373,11 +1380,11 @@ static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const 
    if (A->mp_uni)
       csr_mz27_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
          A->ppat, A->mpmask, A->pp_n, mv, S, -1, -1, -1, H, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e,
-         partials);
+         partials, kb, ke);
    else
       csr_mz27_kernel<NEG, NEED_DIAG, Epi, false><<<npb * nch, 256, 0, s>>>(
          A->ppat, A->mpmask, A->pp_n, mv, S, A->mz_dom, A->mz_dom >= 0 ? xlo : -1, A->mz_dom >= 0 ? xhi : -1, H,
-         x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials);
+         x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
 }
 
 // ---------------------------------------------------------------------------
@@ -1392,30 +1399,33 @@ static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const 
 // every row of R (mode 0, coarse rows) or P (mode 1, fine rows) equals the
 // geometric form: same length, same columns in CSR order, same value bits
 __global__ __launch_bounds__(256) void geo_check_k(const int *__restrict__ rowptr, const int *__restrict__ col,
-                                                   const double *__restrict__ val, int nrows, int mode, GeoT g,
-                                                   int *__restrict__ bad)
+                                                   const double *__restrict__ val, int rb, int re, int mode, GeoT g,
+                                                   long long row_g0, long long col_g0, int *__restrict__ bad)
 {
-   const int i = (int)(blockIdx.x * 256 + threadIdx.x);
-   if (i >= nrows) return;
+   // local rows [rb, re) are global rows + row_g0, local columns global + col_g0
+   // (a z-slab's extended operator); the full operator: 0, nrows, 0, 0
+   const int li = rb + (int)(blockIdx.x * 256 + threadIdx.x);
+   if (li >= re) return;
+   const long long gi = li + row_g0;
    const int cx_n = g.nx / 2, cy_n = g.ny / 2, cz_n = g.nz / 2;
-   int k = rowptr[i];
-   const int e = rowptr[i + 1];
+   int k = rowptr[li];
+   const int e = rowptr[li + 1];
    bool ok = true;
    if (mode == 0) {
-      const int Kx = i % cx_n, Ky = (i / cx_n) % cy_n, Kz = i / (cx_n * cy_n);
+      const int Kx = (int)(gi % cx_n), Ky = (int)((gi / cx_n) % cy_n), Kz = (int)(gi / ((long long)cx_n * cy_n));
       for (int dz = 0; dz < 3; dz++)
          for (int dy = 0; dy < 3; dy++)
             for (int dx = 0; dx < 3; dx++) {
                const int fz = 2 * Kz + dz, fy = 2 * Ky + dy, fx = 2 * Kx + dx;
                if (fz >= g.nz || fy >= g.ny || fx >= g.nx) continue;
-               const int c = (fz * g.ny + fy) * g.nx + fx;
-               if (k >= e || col[k] != c ||
+               const long long c = ((long long)fz * g.ny + fy) * g.nx + fx;
+               if (k >= e || col[k] + col_g0 != c ||
                    __double_as_longlong(val[k]) != __double_as_longlong(g.w[dz * 9 + dy * 3 + dx]))
                   ok = false;
                k++;
             }
    } else {
-      const int fx = i % g.nx, fy = (i / g.nx) % g.ny, fz = i / (g.nx * g.ny);
+      const int fx = (int)(gi % g.nx), fy = (int)((gi / g.nx) % g.ny), fz = (int)(gi / ((long long)g.nx * g.ny));
       // coarse candidates of one axis, ascending: odd f -> (f-1)/2; even f -> f/2-1, f/2
       auto cand = [](int f, int nc, int *c) {
          int m = 0;
@@ -1433,8 +1443,8 @@ __global__ __launch_bounds__(256) void geo_check_k(const int *__restrict__ rowpt
          for (int b = 0; b < my; b++)
             for (int q = 0; q < mx; q++) {
                const int dz = fz - 2 * czs[a], dy = fy - 2 * cys[b], dx = fx - 2 * cxs[q];
-               const int c = (czs[a] * cy_n + cys[b]) * cx_n + cxs[q];
-               if (k >= e || col[k] != c ||
+               const long long c = ((long long)czs[a] * cy_n + cys[b]) * cx_n + cxs[q];
+               if (k >= e || col[k] + col_g0 != c ||
                    __double_as_longlong(val[k]) != __double_as_longlong(g.w[dz * 9 + dy * 3 + dx]))
                   ok = false;
                k++;
@@ -1444,9 +1454,13 @@ __global__ __launch_bounds__(256) void geo_check_k(const int *__restrict__ rowpt
    if (!ok) atomicOr(bad, 1);
 }
 
-void geo_check(hipStream_t s, const amg_mat *M, int mode, const GeoT &g, int *bad)
+void geo_check(hipStream_t s, const amg_mat *M, int mode, const GeoT &g, int *bad, int rb, int re,
+               long long row_g0, long long col_g0)
 {
-   geo_check_k<<<(M->nrows + 255) / 256, 256, 0, s>>>(M->rowptr, M->col, M->val, M->nrows, mode, g, bad);
+   if (re < 0) re = M->nrows;
+   if (re <= rb) return;
+   geo_check_k<<<(re - rb + 255) / 256, 256, 0, s>>>(M->rowptr, M->col, M->val, rb, re, mode, g, row_g0, col_g0,
+                                                      bad);
 }
 
 // Fused level-0 residual + restriction: f_c = R (f - A u) without the fine
@@ -1479,8 +1493,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, Val7 Sv7, const double *__restrict__ x, const double *__restrict__ f,
    const double *__restrict__ wg, int nx, int ny, int nz, int zcc, int nlb, int xcd, int ntf,
-   double *__restrict__ fc)
+   double *__restrict__ fc, int Kb, int Ke, int fz0, int cz0, int nzm)
 {
+   // coarse planes [Kb, Ke) of the nx * ny * nz box; x / f (and the pattern
+   // bytes) hold nzm planes from fine plane fz0, fc's plane 0 is coarse plane
+   // cz0 (a z-slab's extended vectors; the whole box: 0, ncz, 0, 0, nz)
    constexpr int NL = 2 * LC + 1; // fine lines per lane
    MpSten Sv;
 #pragma unroll
@@ -1496,15 +1513,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
    if (!UNI)
       for (int w = tid; w < np * 7; w += 256) mval[w] = mval_g[w];
    const int S = nx, P = nx * ny;
-   const long long N = (long long)nz * P;
+   const long long N = (long long)nzm * P;
    const int lpl = nx >> 1; // lanes per line group
-   const int ncy = ny >> 1, ncz = nz >> 1;
+   const int ncy = ny >> 1;
    const int G = (int)gridDim.x;
    int lg = (int)blockIdx.x;
    if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
    const int lb = lg % nlb, chunk = lg / nlb;
    const int Ky0 = (lb * (256 / lpl) + tid / lpl) * LC, cx = tid % lpl;
-   const int Kc0 = chunk * zcc, Kc1 = min(Kc0 + zcc, ncz);
+   const int Kc0 = Kb + chunk * zcc, Kc1 = min(Kc0 + zcc, Ke);
    const int kf0 = 2 * Kc0, kf1 = min(2 * Kc1, nz - 1); // fine planes, inclusive
    const int y0 = 2 * Ky0;
    const bool lastl = y0 + 2 * LC >= ny; // the group's last line is outside the box
@@ -1516,9 +1533,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
    for (int i = 0; i < NL; i++) {
       const unsigned p = (unsigned)pos0 + (unsigned)i * S;
       const bool ok = i < NL - 1 || !lastl;
-      xm[i] = (ok && kf0 > 0) ? ld2u(x, p + (unsigned)(kf0 - 1) * P) : v2d{0.0, 0.0};
-      xc[i] = ok ? ld2u(x, p + (unsigned)kf0 * P) : v2d{0.0, 0.0};
-      xq[i] = (ok && kf0 + 1 < nz) ? ld2u(x, p + (unsigned)(kf0 + 1) * P) : v2d{0.0, 0.0};
+      xm[i] = (ok && kf0 > 0) ? ld2u(x, p + (unsigned)(kf0 - 1 - fz0) * P) : v2d{0.0, 0.0};
+      xc[i] = ok ? ld2u(x, p + (unsigned)(kf0 - fz0) * P) : v2d{0.0, 0.0};
+      xq[i] = (ok && kf0 + 1 < nz) ? ld2u(x, p + (unsigned)(kf0 + 1 - fz0) * P) : v2d{0.0, 0.0};
    }
    double acc[LC];
 #pragma unroll
@@ -1536,7 +1553,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       int pid[NL];
    };
    auto fetch = [&](int k, PlaneIn &in) {
-      const unsigned base = (unsigned)k * P + pos0;
+      const unsigned base = (unsigned)(k - fz0) * P + pos0;
       // halo lines 2Ky0 - 1 and 2Ky0 + 2 LC + 1 (entries outside the box are unused)
       in.hm = ld2u(x, base >= (unsigned)S ? base - S : 0u);
       const unsigned hp_i = base + (unsigned)NL * S;
@@ -1556,7 +1573,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
    };
    __syncthreads();
    for (int k = kf0; k <= kf1; k++) {
-      const unsigned base = (unsigned)k * P + pos0;
+      const unsigned base = (unsigned)(k - fz0) * P + pos0;
       v2d r[NL];
       PlaneIn cur;
       fetch(k, cur);
@@ -1642,11 +1659,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
          const long long ci = ((long long)(Ky0 + c)) * lpl + cx;
          if (k & 1) {
             add(c, 1);
-            if (k + 1 >= nz) fc[(long long)Kz * ncy * lpl + ci] = acc[c];
+            if (k + 1 >= nz) fc[(long long)(Kz - cz0) * ncy * lpl + ci] = acc[c];
          } else {
             if (k > kf0) {
                add(c, 2);
-               fc[(long long)(Kz - 1) * ncy * lpl + ci] = acc[c];
+               fc[(long long)(Kz - 1 - cz0) * ncy * lpl + ci] = acc[c];
             }
             if (Kz < Kc1) {
                acc[c] = 0.0;
@@ -1658,21 +1675,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 }
 
 void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, const double *u, const GeoT &g,
-                          const double *wdev, double *fc)
+                          const double *wdev, double *fc, int Kb, int Ke, int fz0, int cz0)
 {
+   if (Ke < 0) Ke = g.nz / 2;
+   if (Ke <= Kb) return;
+   const int nzm = A->nrows / (g.nx * g.ny);
    Val7 S;
    for (int j = 0; j < 7; j++) S.v[j] = A->mp_val[j];
    const int lpl = g.nx / 2, groups = 256 / lpl;
    const int LC = ((g.ny / 2) % (2 * groups) == 0 && A->ctx->rr_lines == 2) ? 2 : 1;
    const int nlb = (g.ny / 2) / (groups * LC);
    const int zcc = std::max(1, std::min(A->ctx->mz_zc / 2, 32));
-   const int nch = (g.nz / 2 + zcc - 1) / zcc;
+   const int nch = (Ke - Kb + zcc - 1) / zcc;
    const int nb = nlb * nch;
    const int xcd = A->ctx->mz_xcd;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
 #define AMG_RR(U, L, ...) \
    mz_res_restrict_kernel<U, L, ##__VA_ARGS__><<<nb, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, f, wdev, g.nx, g.ny, \
-                                                   g.nz, zcc, nlb, xcd, stream_hint(A), fc)
+                                                   g.nz, zcc, nlb, xcd, stream_hint(A), fc, Kb, Ke, fz0, cz0, nzm)
    if (A->mp_uni) {
       if (LC == 2) AMG_RR(true, 2);
       else if (A->ctx->rr_occ == 5) AMG_RR(true, 1, 5);
@@ -1694,7 +1714,7 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
 // rows (i, i + 1) = fine (x, y, z), x even: u_i + sum w e_c over the coarse
 // columns of P's rows in CSR order (cz, cy, cx ascending), from the pair's u
 __device__ __forceinline__ v2d geo_prolong_pair(v2d acc, const double *__restrict__ e, const double *wl, int x,
-                                                int y, int z, int ncx, int ncy, int ncz)
+                                                int y, int z, int ncx, int ncy, int ncz, int czoff = 0)
 {
    const int t = x >> 1;
    // coarse candidates of one axis (ascending) and their offsets d = f - 2c
@@ -1722,7 +1742,7 @@ __device__ __forceinline__ v2d geo_prolong_pair(v2d acc, const double *__restric
    for (int a = 0; a < 2; a++)
 #pragma unroll
       for (int b = 0; b < 2; b++) {
-         const long long cb = ((long long)cz[a] * ncy + cy[b]) * ncx + t;
+         const long long cb = ((long long)(cz[a] - czoff) * ncy + cy[b]) * ncx + t; // e plane 0 = coarse czoff
          // e[cb - 1], e[cb]; the first is unused (and clamped) at t = 0
          ev[a][b] = *reinterpret_cast<const v2du *>(e + (lo ? cb - 1 : cb));
       }
@@ -1767,9 +1787,11 @@ __device__ __forceinline__ double geo_prolong_point(double acc, const double *__
    return acc;
 }
 
+// fine planes [zb, zb + npairs / (nx ny / 2)) of the nx * ny * nz box; u's
+// plane 0 is fine plane fz0, e's plane 0 coarse plane cz0 (z-slab vectors)
 __global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ e, double *__restrict__ u,
                                                      const double *__restrict__ wg, int nx, int ny, int nz,
-                                                     long long npairs)
+                                                     long long npairs, int zb, int fz0, int cz0)
 {
    __shared__ double wl[27];
    const int tid = (int)threadIdx.x;
@@ -1790,14 +1812,19 @@ __global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ 
       y = (int)(yz % ny);
       z = (int)(yz / ny);
    }
-   const v2d acc = *reinterpret_cast<const v2du *>(u + i);
-   *reinterpret_cast<v2du *>(u + i) = geo_prolong_pair(acc, e, wl, x, y, z, nx >> 1, ny >> 1, nz >> 1);
+   z += zb;
+   double *ui = u + (long long)(z - fz0) * nx * ny + (i - (long long)(z - zb) * nx * ny);
+   const v2d acc = *reinterpret_cast<const v2du *>(ui);
+   *reinterpret_cast<v2du *>(ui) = geo_prolong_pair(acc, e, wl, x, y, z, nx >> 1, ny >> 1, nz >> 1, cz0);
 }
 
-void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u)
+void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u, int zb, int ze,
+                 int fz0, int cz0)
 {
-   const long long np = (long long)g.nx * g.ny * g.nz / 2;
-   geo_prolong_k<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, np);
+   if (ze < 0) ze = g.nz;
+   const long long np = (long long)g.nx * g.ny * (ze - zb) / 2;
+   if (np <= 0) return;
+   geo_prolong_k<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, np, zb, fz0, cz0);
 }
 
 // Prolongation + correction fused with the first post-smoothing sweep of a
@@ -1939,9 +1966,11 @@ void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const do
 // Geometric restriction f_c = R r (SMEM_Sync_Parfor_Restrict,
 // SMEM_MatVec.cpp:380-392) for a checked geometric R: coarse point K sums
 // w * r over fine 2K + d in R's CSR order (dz, dy, dx), from 0.
+// coarse planes [Kb, Kb + nc / (ncx ncy)); r's plane 0 is fine plane fz0, fc's
+// plane 0 coarse plane cz0 (z-slab vectors)
 __global__ __launch_bounds__(256) void geo_restrict_k(const double *__restrict__ r, double *__restrict__ fc,
                                                       const double *__restrict__ wg, int nx, int ny, int nz,
-                                                      long long nc)
+                                                      long long nc, int Kb, int fz0, int cz0)
 {
    __shared__ double wl[27];
    const int tid = (int)threadIdx.x;
@@ -1962,6 +1991,7 @@ __global__ __launch_bounds__(256) void geo_restrict_k(const double *__restrict__
       Ky = (int)(t % ncy);
       Kz = (int)(t / ncy);
    }
+   Kz += Kb;
    const bool dx2 = 2 * Kx + 2 < nx;
    // the nine fine (plane, line) loads issued first (lines outside the box
    // read the last inside one, unused), then the terms in R's CSR order
@@ -1972,7 +2002,7 @@ __global__ __launch_bounds__(256) void geo_restrict_k(const double *__restrict__
 #pragma unroll
       for (int dy = 0; dy < 3; dy++) {
          const int fz = min(2 * Kz + dz, nz - 1), fy = min(2 * Ky + dy, ny - 1);
-         const double *p = r + ((long long)fz * ny + fy) * nx + 2 * Kx;
+         const double *p = r + ((long long)(fz - fz0) * ny + fy) * nx + 2 * Kx;
          a[dz][dy] = *reinterpret_cast<const v2du *>(p);
          c[dz][dy] = dx2 ? p[2] : 0.0;
       }
@@ -1989,13 +2019,16 @@ __global__ __launch_bounds__(256) void geo_restrict_k(const double *__restrict__
          if (dx2) acc = acc + w[2] * c[dz][dy];
       }
    }
-   fc[K] = acc;
+   fc[((long long)(Kz - cz0) * ncy + Ky) * ncx + Kx] = acc;
 }
 
-void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc)
+void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc, int Kb, int Ke,
+                  int fz0, int cz0)
 {
-   const long long nc = (long long)g.nx * g.ny * g.nz / 8;
-   geo_restrict_k<<<(unsigned)((nc + 255) / 256), 256, 0, s>>>(r, fc, wdev, g.nx, g.ny, g.nz, nc);
+   if (Ke < 0) Ke = g.nz / 2;
+   const long long nc = (long long)(g.nx / 2) * (g.ny / 2) * (Ke - Kb);
+   if (nc <= 0) return;
+   geo_restrict_k<<<(unsigned)((nc + 255) / 256), 256, 0, s>>>(r, fc, wdev, g.nx, g.ny, g.nz, nc, Kb, fz0, cz0);
 }
 
 // dictionary-coded launches: rows of <= 8 entries (7-pt stencil, interpolation)
@@ -2006,10 +2039,12 @@ template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_dc_op(hipStream_t s, const amg_mat *A, const double *x, int rb, int re,
                          const Epi &e, double *partials, int tiles)
 {
-   if (A->mz_P && rb == 0 && re == A->nrows && A->mz27)
-      launch_mz27<NEG, NEED_DIAG>(s, A, x, e, partials);
-   else if (A->mz_P && rb == 0 && re == A->nrows)
-      launch_mz<NEG, NEED_DIAG>(s, A, x, e, partials);
+   // plane-aligned row ranges march over their planes (a z-slab's owned planes)
+   const bool march = A->mz_P && rb % A->mz_P == 0 && re % A->mz_P == 0;
+   if (march && A->mz27)
+      launch_mz27<NEG, NEED_DIAG>(s, A, x, e, partials, rb / A->mz_P, re / A->mz_P);
+   else if (march)
+      launch_mz<NEG, NEED_DIAG>(s, A, x, e, partials, rb / A->mz_P, re / A->mz_P);
    else if (A->mp_J && (rb & 1) == 0)
       launch_mp<NEG, NEED_DIAG>(s, A, x, rb, re, e, partials);
    else if (A->ppat && (rb & 1) == 0)
@@ -3212,11 +3247,169 @@ void async_gs(hipStream_t s, const amg_mat *A, const double *f, double *u, const
       async_gs_k<<<nb, tpb, 0, s>>>(A->rowptr, A->col, A->val, f, u, d_blk, nblk, sweeps, reverse);
 }
 
+// Hybrid Jacobi / Gauss-Seidel, one WAVE per block (SMEM_Smooth.cpp:265-304 /
+// 548-585; the reference's thread-range block, here any block): the block's
+// rows in chunks of 64, lane l owning the chunk's l-th row in sweep order.
+// Every row's sum is res = f_i - sum a_ij x_j over its entries in CSR order,
+// with x_j the operand the reference's sequential loop reads:
+//   * a column outside the block: u_prev (skipped in the zero-guess sweep);
+//   * an in-block column not updated yet this sweep: its old value u_prev
+//     (0 in the zero-guess sweep);
+//   * an in-block column updated in an EARLIER chunk: its new value (loaded,
+//     agent-scope, after the chunk fence);
+//   * an in-block column updated earlier in THIS chunk: a dependency.
+// Phase 1 (all lanes at once, coalesced loads): each lane forms its rounded
+// products and sums the prefix up to its first dependency.  Phase 2 (the
+// chain): step s = 0 .. 63, lane s adds its tail -- the dependent products
+// with the values broadcast (v_readlane) at the earlier steps, the other
+// tail products as precomputed -- in CSR order, divides, and its new value is
+// broadcast to every lane that depends on it.  The operations and their
+// order are the sequential loop's: bit-identical.  Rows of at most RMAX
+// entries (longer rows: hybrid_jgs_k).
+__device__ __forceinline__ double readlane_d(double v, int s)
+{
+   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+   const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, s);
+   const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), s);
+   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+template <int RMAX>
+__global__ __launch_bounds__(256) void hybrid_jgs_wave_k(const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                         const double *__restrict__ val, const double *__restrict__ f,
+                                                         double *u, const double *__restrict__ u_prev,
+                                                         const int *__restrict__ blk, int nblk,
+                                                         const double *__restrict__ ds, double weight, int zero,
+                                                         int reverse)
+{
+   const int lane = (int)threadIdx.x & 63;
+   const int b = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+   if (b >= nblk) return; // whole waves
+   const int ns = blk[b], ne = blk[b + 1];
+   const int nb = ne - ns;
+   for (int c0 = 0; c0 < nb; c0 += 64) {
+      const int cnt = min(64, nb - c0);
+      const bool act = lane < cnt;
+      const int i = reverse ? ne - 1 - (c0 + lane) : ns + c0 + lane;
+      double res = 0.0, a = 0.0, d = 1.0, old = 0.0;
+      double pa[RMAX], xd[RMAX];
+      int dl[RMAX];
+      int len = 0, fd = RMAX;
+#pragma unroll
+      for (int k = 0; k < RMAX; k++) {
+         pa[k] = 0.0;
+         xd[k] = 0.0;
+         dl[k] = -2;
+      }
+      if (act) {
+         const int rs = rowptr[i];
+         len = rowptr[i + 1] - rs;
+         a = val[rs];
+         d = ds ? ds[i] : a;
+         old = zero ? 0.0 : u_prev[i];
+         res = f[i];
+         int jj[RMAX];
+         double vv[RMAX], xx[RMAX];
+#pragma unroll
+         for (int k = 0; k < RMAX; k++) {
+            jj[k] = 0;
+            vv[k] = 0.0;
+            if (k < len) {
+               jj[k] = col[rs + k];
+               vv[k] = val[rs + k];
+            }
+         }
+         // operands (dl: -1 independent product, -2 nothing, >= 0 dependency lane)
+#pragma unroll
+         for (int k = 0; k < RMAX; k++) {
+            xx[k] = 0.0;
+            if (k >= len) continue;
+            const int j = jj[k];
+            if (j >= ns && j < ne) {
+               const bool done = reverse ? j > i : j < i;
+               if (!done) {
+                  xx[k] = zero ? 0.0 : u_prev[j];
+                  dl[k] = -1;
+               } else {
+                  const int pos = reverse ? ne - 1 - j : j - ns; // position in sweep order
+                  if (pos >= c0) {
+                     dl[k] = pos - c0;
+                  } else {
+                     xx[k] = __hip_atomic_load(u + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                     dl[k] = -1;
+                  }
+               }
+            } else if (!zero) {
+               xx[k] = u_prev[j];
+               dl[k] = -1;
+            }
+         }
+#pragma unroll
+         for (int k = 0; k < RMAX; k++) {
+            if (k >= len) break;
+            if (dl[k] >= 0 && fd == RMAX) fd = k;
+            if (dl[k] == -1) pa[k] = vv[k] * xx[k];
+            else if (dl[k] >= 0) pa[k] = vv[k];
+            if (fd == RMAX && dl[k] == -1) res = res - pa[k];
+         }
+      }
+      auto finish = [&](double r) { return (a != 0.0) ? (zero ? weight * r / d : old + weight * r / d) : old; };
+      double v = old;
+      if (act && fd == RMAX) v = finish(res);
+      for (int st = 0; st < cnt; st++) {
+         if (lane == st && fd < RMAX) {
+            double r = res;
+#pragma unroll
+            for (int k = 0; k < RMAX; k++) {
+               if (k < fd || k >= len || dl[k] == -2) continue;
+               r = r - (dl[k] >= 0 ? pa[k] * xd[k] : pa[k]);
+            }
+            v = finish(r);
+         }
+         const double vs = readlane_d(v, st);
+#pragma unroll
+         for (int k = 0; k < RMAX; k++)
+            if (dl[k] == st) xd[k] = vs;
+      }
+      // a_ii == 0: the row keeps its value (0 after the zero-guess reset)
+      if (act && (a != 0.0 || zero)) __hip_atomic_store(u + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the next chunk's loads of these rows see the stores
+      if (c0 + 64 < nb) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+   }
+}
+
+__global__ void row_max_k(const int *__restrict__ rowptr, int n, int *__restrict__ out)
+{
+   int m = 0;
+   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+      m = max(m, rowptr[i + 1] - rowptr[i]);
+   for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_down(m, o, 64));
+   if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+void row_max(hipStream_t s, const amg_mat *A, int *d_out)
+{
+   const int n = A->nrows;
+   if (n <= 0) return;
+   row_max_k<<<std::max(1, std::min(1024, (n + 255) / 256)), 256, 0, s>>>(A->rowptr, n, d_out);
+}
+
 void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
                 const int *d_blk, int nblk, const double *diag_scale, double weight, int zero,
                 int reverse)
 {
    if (nblk <= 0) return;
+   const int mode = A->ctx->jgs_wave;
+   if (mode && A->maxrow >= 0 && A->maxrow <= 32) {
+      const int nwg = (nblk + 3) / 4;
+      if (A->maxrow <= 8)
+         hybrid_jgs_wave_k<8><<<nwg, 256, 0, s>>>(A->rowptr, A->col, A->val, f, u, u_prev, d_blk, nblk, diag_scale,
+                                                  weight, zero, reverse);
+      else
+         hybrid_jgs_wave_k<32><<<nwg, 256, 0, s>>>(A->rowptr, A->col, A->val, f, u, u_prev, d_blk, nblk,
+                                                   diag_scale, weight, zero, reverse);
+      return;
+   }
    const int tpb = 64;
    hybrid_jgs_k<<<(nblk + tpb - 1) / tpb, tpb, 0, s>>>(A->rowptr, A->col, A->val, f, u, u_prev,
                                                        d_blk, nblk, diag_scale, weight, zero,

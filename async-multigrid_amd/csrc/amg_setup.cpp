@@ -370,24 +370,64 @@ extern "C" int amg_rhs_rand(long long r0, long long r1, double lo, double hi, do
 int amg_mat_create_device(amg_ctx *c, int nrows, int ncols, long long nnz, amg_mat **out);
 int amg_mat_finish(amg_mat *A);
 
-extern "C" int amg_gen_register(amg_ctx *ctx, const amg_gen *g, int which, int level, int z0,
-                                int z1, amg_mat **out)
+// Rows of planes [e0, e1) of the operator's row grid (rows of planes outside
+// [o0, o1) are "ghost" rows: A keeps its whole row when every column lies in
+// the column planes -- the fused residual + restriction forms residuals of the
+// first ghost plane -- else only its diagonal entry; P / R keep none),
+// columns shifted to planes [ce0, ce1) of the column grid (every kept column
+// must lie there).  The whole operator: e0 = o0 = 0, e1 = o1 = nz, ce0 = 0,
+// ce1 = nz of the column grid.  A z-slab's extended operator: the owned planes
+// [o0, o1) plus ghost planes around them (amg_dist.cpp, slab hierarchies).
+int amg_gen_register_ext(amg_ctx *ctx, const amg_gen *g, int which, int level, int e0, int e1, int o0, int o1,
+                         int ce0, int ce1, amg_mat **out)
 {
-   AMG_TRY(check_op(g, which, level, z0, z1));
+   AMG_TRY(check_op(g, which, level, e0, e1));
    AMG_ARG(ctx && out, "amg_gen_register: null argument");
+   AMG_ARG(e0 <= o0 && o0 <= o1 && o1 <= e1, "amg_gen_register: owned planes [%d,%d) outside [%d,%d)", o0, o1, e0,
+           e1);
    const auto &d = row_grid(g, which, level);
    const long long plane = (long long)d[0] * d[1];
-   const long long nrows = plane * (z1 - z0);
+   const long long nrows = plane * (e1 - e0);
    const auto &cdim = (which == AMG_GEN_A) ? g->dims[level]
                       : (which == AMG_GEN_P) ? g->dims[level + 1]
                                              : g->dims[level];
-   const long long ncols = (long long)cdim[0] * cdim[1] * cdim[2];
-   const long long nnz = amg_gen_nnz(g, which, level, z0, z1);
+   const long long cplane = (long long)cdim[0] * cdim[1];
+   AMG_ARG(ce0 >= 0 && ce0 <= ce1 && ce1 <= cdim[2], "amg_gen_register: column planes [%d,%d) of %d", ce0, ce1,
+           cdim[2]);
+   const long long ncols = cplane * (ce1 - ce0), cshift = cplane * ce0;
+   // A's ghost rows: the whole row if it fits the column planes, else the diagonal
+   auto ghost_keep = [&](const int *rp, const int *cj, long long r, long long &cnt) {
+      const long long kb = rp[r], ke = rp[r + 1];
+      bool fits = true;
+      for (long long k = kb; k < ke; k++) {
+         const long long c = (long long)cj[k] - cshift;
+         fits = fits && c >= 0 && c < ncols;
+      }
+      cnt = fits ? ke - kb : std::min(ke - kb, 1LL);
+      return fits;
+   };
+   long long ghost_nnz = 0;
+   if (which == AMG_GEN_A) {
+      for (int z = e0; z < e1; z++) {
+         if (z >= o0 && z < o1) continue;
+         const long long pn = amg_gen_nnz(g, which, level, z, z + 1);
+         std::vector<int> rp(plane + 1), cj(std::max(1LL, pn));
+         std::vector<double> cv(std::max(1LL, pn));
+         AMG_TRY(amg_gen_fill(g, which, level, z, z + 1, rp.data(), cj.data(), cv.data(), 0));
+         for (long long q = 0; q < plane; q++) {
+            long long cnt;
+            ghost_keep(rp.data(), cj.data(), q, cnt);
+            ghost_nnz += cnt;
+         }
+      }
+   }
+   const long long nnz = amg_gen_nnz(g, which, level, o0, o1) + ghost_nnz;
    AMG_ARG(nnz >= 0 && nnz < (1LL << 31) - AMG_NNZ_PAD, "amg_gen_register: nnz %lld", nnz);
+   AMG_ARG(nrows < (1LL << 31) && ncols < (1LL << 31), "amg_gen_register: %lld x %lld exceeds int32", nrows, ncols);
    amg_mat *A = nullptr;
-   AMG_TRY(amg_mat_create_device(ctx, (int)nrows, (int)ncols, nnz, &A));
+   AMG_TRY(amg_mat_create_device(ctx, (int)nrows, (int)std::max(1LL, ncols), nnz, &A));
    // batches of planes, double-buffered through pinned host memory
-   const int np = z1 - z0;
+   const int np = e1 - e0;
    // ~16M entries (~190 MB of pinned staging) per batch
    const int batch =
       std::max(1, (int)std::min<long long>(np, (16LL << 20) / 27 / std::max(1LL, plane)));
@@ -405,21 +445,46 @@ extern "C" int amg_gen_register(amg_ctx *ctx, const amg_gen *g, int which, int l
    long long base = 0;
    int buf = 0;
    bool used[2] = {false, false};
+   int bad = 0;
    for (int zb = 0; zb < np; zb += batch) {
       const int nb = std::min(batch, np - zb);
       if (used[buf]) AMG_HIP(hipEventSynchronize(done[buf]));
       std::vector<int> rp(nb * plane + 1);
-      AMG_TRY(amg_gen_fill(g, which, level, z0 + zb, z0 + zb + nb, rp.data(), hcol[buf], hval[buf], 0));
-      const long long bn = rp[nb * plane];
-      for (long long r = 0; r < nb * plane; r++) rp_all[zb * plane + r + 1] = (int)(rp[r + 1] + base);
-      AMG_HIP(hipMemcpyAsync(A->col + base, hcol[buf], bn * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-      AMG_HIP(hipMemcpyAsync(A->val + base, hval[buf], bn * sizeof(double), hipMemcpyHostToDevice,
+      AMG_TRY(amg_gen_fill(g, which, level, e0 + zb, e0 + zb + nb, rp.data(), hcol[buf], hval[buf], 0));
+      // ghost rows and the column shift, compacted in place (k_out <= k_in)
+      long long ko = 0;
+      for (int pz = 0; pz < nb; pz++) {
+         const int z = e0 + zb + pz;
+         const bool ghost = z < o0 || z >= o1;
+         for (long long q = 0; q < plane; q++) {
+            const long long r = (long long)pz * plane + q;
+            const long long kb = rp[r], ke = rp[r + 1];
+            long long keep_to = ke;
+            if (ghost) {
+               long long cnt = 0;
+               if (which == AMG_GEN_A) ghost_keep(rp.data(), hcol[buf], r, cnt);
+               keep_to = kb + cnt;
+            }
+            for (long long k = kb; k < keep_to; k++) {
+               const long long c = (long long)hcol[buf][k] - cshift;
+               if (c < 0 || c >= ncols) bad = 1;
+               hcol[buf][ko] = (int)c;
+               hval[buf][ko] = hval[buf][k];
+               ko++;
+            }
+            rp_all[zb * plane + r + 1] = (int)(base + ko);
+         }
+      }
+      AMG_ARG(!bad, "amg_gen_register: a column of an owned row lies outside column planes [%d,%d)", ce0, ce1);
+      AMG_HIP(hipMemcpyAsync(A->col + base, hcol[buf], ko * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+      AMG_HIP(hipMemcpyAsync(A->val + base, hval[buf], ko * sizeof(double), hipMemcpyHostToDevice,
                              ctx->stream));
       AMG_HIP(hipEventRecord(done[buf], ctx->stream));
       used[buf] = true;
-      base += bn;
+      base += ko;
       buf ^= 1;
    }
+   AMG_ARG(base == nnz, "amg_gen_register: %lld entries written, %lld expected", base, nnz);
    rp_all[0] = 0;
    AMG_HIP(hipMemcpyAsync(A->rowptr, rp_all.data(), (nrows + 1) * sizeof(int), hipMemcpyHostToDevice,
                           ctx->stream));
@@ -432,4 +497,12 @@ extern "C" int amg_gen_register(amg_ctx *ctx, const amg_gen *g, int which, int l
    }
    *out = A;
    return AMG_OK;
+}
+
+extern "C" int amg_gen_register(amg_ctx *ctx, const amg_gen *g, int which, int level, int z0,
+                                int z1, amg_mat **out)
+{
+   AMG_TRY(check_op(g, which, level, z0, z1));
+   const int cl = (which == AMG_GEN_P) ? level + 1 : level;
+   return amg_gen_register_ext(ctx, g, which, level, z0, z1, z0, z1, 0, g->dims[cl][2], out);
 }

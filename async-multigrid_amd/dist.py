@@ -221,14 +221,26 @@ class DistHier:
     ``DistHier.from_parts`` takes this rank's rows of every operator with
     global column ids and the per-level row partition (ParCSR row_starts)."""
 
-    def __init__(self, ctx, gen, opts, _handle=None):
+    def __init__(self, ctx, gen, opts, _handle=None, slab=False):
+        """slab=True: the z-slab form (amg_dist_hier_create_slab: extended slab
+        operators, plane exchange, the single-GPU march / geometric / fused
+        kernels); False: the row-partitioned form with [owned | ghost] columns."""
         self.ctx, self.gen, self.opts = ctx, gen, opts
+        self.slab = bool(slab)
         if _handle is None:
             h = C.c_void_p()
-            check(lib.amg_dist_hier_create_structured(ctx.h, gen.h, C.byref(opts), C.byref(h)))
+            create = lib.amg_dist_hier_create_slab if slab else lib.amg_dist_hier_create_structured
+            check(create(ctx.h, gen.h, C.byref(opts), C.byref(h)))
             _handle = h
         self.h = _handle
         self.row0, self.n0 = self.local_rows(0)
+
+    def slab_info(self):
+        """(distributed levels, bitmask of geometric-transfer levels, fused level-0
+        residual + restriction) of a slab hierarchy ((0, 0, 0) otherwise)"""
+        a, b, c = C.c_int(), C.c_int(), C.c_int()
+        check(lib.amg_dist_hier_slab_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
 
     @classmethod
     def from_parts(cls, ctx, row_starts, A, P, R, opts):

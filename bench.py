@@ -41,6 +41,9 @@ def parse():
     p.add_argument("--spmv-reps", type=int, default=20)
     p.add_argument("--force-dist", type=int, default=0,
                    help="run the distributed (RCCL) path even at one rank")
+    p.add_argument("--dist-form", choices=("slab", "rows"), default="slab",
+                   help="distributed hierarchy: z-slab extended operators (default) or the "
+                        "row-partitioned [owned | ghost] CSR form")
     return p.parse_args()
 
 

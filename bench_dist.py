@@ -30,6 +30,10 @@ def main(args, world, rank):
     from bench import METRIC, HBM_PEAK_GBS, storage
 
     local = int(os.environ.get("LOCAL_RANK", rank))
+    # stdout carries exactly one JSON line: gloo / RCCL banners go to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     amg = load_package()
     n = args.n
@@ -45,9 +49,17 @@ def main(args, world, rank):
     gen = amg.Gen(n, interp=amg.AMG_INTERP_LINEAR)
     opts = amg.default_opts(smooth_weight=args.smooth_weight, num_cycles=1 << 30, tol=0.0,
                             reuse_outer_residual=args.reuse_outer_residual, profile=1)
-    D = amg.dist.DistHier(ctx, gen, opts)
+    slab = getattr(args, "dist_form", "slab") == "slab"
+    D = amg.dist.DistHier(ctx, gen, opts, slab=slab)
     nnz_local, vi, dc, rp = D.matrix_info(0)
-    mat_bytes, fmt = storage(D.n0, nnz_local, vi, dc, rp, D.pair_pattern(0))
+    Ld, geo_mask, fused0 = D.slab_info()
+    if slab:
+        # the extended slab operator streams its owned planes (plane march:
+        # n/2 pattern bytes per pass, as one GPU)
+        mat_bytes, fmt = (D.n0 + 1) // 2, ("7-pt plane march over the owned planes of the extended slab "
+                                            "operator (csr-mp master form, one pattern byte per row pair)")
+    else:
+        mat_bytes, fmt = storage(D.n0, nnz_local, vi, dc, rp, D.pair_pattern(0))
     if rank == 0:
         log(f"[dist] {world} ranks, {gen.L} levels, slab {D.n0} rows / {nnz_local} nnz on rank 0; "
             f"setup {time.time() - t0:.1f}s")
@@ -71,6 +83,15 @@ def main(args, world, rank):
     ms, launches = D.profile(reset=True)
     res_ms = ms[0] / max(launches[0], 1)
     res_bytes = mat_bytes + 24 * D.n0
+    kernels = None
+    if slab:
+        # the fine-level kernels of a step on this rank's slab (bench.fine_kernels,
+        # DESIGN.md Sec.4 byte counts over the owned rows)
+        from bench import fine_kernels
+        fmask = (1 if fused0 else 0) | (2 if geo_mask & 1 else 0)
+        kernels = fine_kernels(D.n0, mat_bytes, ms, launches, fmask, fmt)
+    all_k = [None] * world
+    tdist.all_gather_object(all_k, kernels)
     u_par = None
     if args.cpu_baseline:
         # parity leg (untimed): restart and run exactly the oracle's cpu_cycles
@@ -111,6 +132,27 @@ def main(args, world, rank):
         spmv_gbs = P[:, 0].sum() / (P[:, 1].max() * 1e-3) / 1e9
         res_gbs = P[:, 2].sum() / (P[:, 3].max() * 1e-3) / 1e9
         ach0 = res_bytes / (res_ms * 1e-3) / 1e9
+        if kernels:
+            dom = max(kernels, key=lambda k: kernels[k]["ms"])
+            dk = kernels[dom]
+            agg = sum(k[dom]["bytes"] for k in all_k) / (max(k[dom]["ms"] for k in all_k) * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": f"{dom}: {dk['what']} (rank 0 slab, incl. ghost-plane exchange "
+                                              "waits)",
+                    "achieved": dk["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dk["frac"],
+                    "traffic": None,
+                    "traffic_note": "PMC FETCH/WRITE passes are single-GPU runs of bench.py (profiles/traffic.json)",
+                    "alg_bytes_per_launch": dk["bytes"], "avg_launch_ms": dk["ms"], "aggregate_gbs": agg,
+                    "selection": "the fine-level kernel with the largest time per step on rank 0"}
+        else:
+            roof = {"bound": "hbm", "kernel": f"fine-grid residual SpGEMV r = f - A0 u ({fmt}, rank 0 "
+                                              "slab, incl. ghost exchange wait)",
+                    "achieved": ach0, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach0 / HBM_PEAK_GBS, "traffic": None,
+                    "traffic_note": "PMC FETCH/WRITE passes are single-GPU runs of bench.py "
+                                    "(profiles/traffic.json); the per-rank slab residual is the "
+                                    "same kernel on a z-slab and is not profiled per rank",
+                    "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms,
+                    "aggregate_gbs": res_gbs}
         log(f"[dist] {args.steps} steps in {dt * 1e3:.2f} ms -> {value:.2f} it/s; relres {rn / r0:.3e}; "
             f"fine SpMV aggregate {spmv_gbs:.0f} GB/s")
         out = {
@@ -130,22 +172,21 @@ def main(args, world, rank):
                                    f"w={args.smooth_weight}, {gen.L}-level geometric Galerkin "
                                    f"hierarchy, z-slab partition, RCCL ghost exchange",
                        "n": n, "levels": gen.L, "parallelism": f"slab{world}", "matrix_format": fmt,
+                       "dist_form": "z-slab extended operators (amg_dist_hier_create_slab)" if slab
+                                    else "row-partitioned [owned | ghost] CSR (amg_dist_hier_create_structured)",
+                       "distributed_levels": Ld if slab else None,
+                       "geometric_transfer_levels": geo_mask if slab else None,
+                       "fused_residual_restriction": bool(fused0) if slab else None,
                        "reuse_outer_residual": args.reuse_outer_residual},
             "fine_spmv": {"gbs_aggregate": spmv_gbs, "ms_max": float(P[:, 1].max()),
                           "frac_per_gpu": spmv_gbs / world / HBM_PEAK_GBS},
-            "roofline": {"bound": "hbm", "kernel": f"fine-grid residual SpGEMV r = f - A0 u ({fmt}, rank 0 "
-                                                   "slab, incl. ghost exchange wait)",
-                         "achieved": ach0, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach0 / HBM_PEAK_GBS, "traffic": None,
-                         "traffic_note": "PMC FETCH/WRITE passes are single-GPU runs of bench.py "
-                                         "(profiles/traffic.json); the per-rank slab residual is the "
-                                         "same kernel on a z-slab and is not profiled per rank",
-                         "alg_bytes_per_launch": res_bytes, "avg_launch_ms": res_ms,
-                         "aggregate_gbs": res_gbs},
+            "roofline": roof,
+            "fine_kernels": kernels,
             "cpu_baseline": cpu,
             "parity": parity,
             "final_relres": rn / r0,
         }
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     tdist.barrier()
     tdist.destroy_process_group()

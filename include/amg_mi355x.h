@@ -291,6 +291,11 @@ int amg_l1_jacobi(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, 
  * SMEM_Sync_Parfor_HybridJacobiGaussSeidel[T] SMEM_Smooth.cpp:222-363 (diag_scale =
  * A_diag, weight 1) and SMEM_Sync_HybridJacobiGaussSeidel[T] :533-641
  * (diag_scale NULL = a_ii); reverse selects the [T] variants */
+/* hybrid JGS kernel form: 1 (default, env AMG_JGS_WAVE) one wave per block for
+ * rows of <= 32 entries -- coalesced operand loads, the in-chunk dependency
+ * chain carried lane to lane (v_readlane), bit-identical; 0: one lane walks
+ * each block (the reference's sequential loop as is) */
+int amg_set_jgs_wave(amg_ctx *ctx, int enable);
 int amg_hybrid_jgs(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, amg_vec *u_prev,
                    const int *blk, int nblk, const amg_vec *diag_scale, double weight, int sweeps,
                    int zero_first, int reverse);
@@ -510,6 +515,24 @@ int amg_dist_hier_create(amg_ctx *ctx, int num_levels, const long long *row_star
  * plane 2k+1 */
 int amg_dist_hier_create_structured(amg_ctx *ctx, const amg_gen *gen, const amg_opts *opts,
                                     amg_dist_hier **out);
+/* the z-slab form of the same partition (config 4's path): every distributed
+ * level's operators are the rank's extended slab operators (owned planes plus
+ * up to two ghost planes each side), so the single-GPU kernels run on them --
+ * plane-marched 7-pt / 27-pt sweeps and residuals over the owned planes,
+ * geometric restriction / prolongation, the fused level-0 residual +
+ * restriction -- and the ghost exchange is whole contiguous planes with the
+ * two neighbouring ranks (RCCL send/recv on the communication stream,
+ * overlapped with the planes that read no ghost).  Rows keep their global
+ * entry order: iterates are bit-identical to one GPU.  Needs >= 2 level-0
+ * planes per rank; levels where a rank would own < 2 planes (or below the
+ * replication threshold) are replicated.  Serves amg_dist_solve_* and
+ * amg_dist_async_solve (replaces the ParCSR halo of hypre_ParCSRMatrixMatvec,
+ * DMEM_Add.cpp:230-308, and the finestIntra exchange, DMEM_Comm.cpp:81-348);
+ * amg_dist_async_jacobi / _sps and amg_grid_add_* need the row-partitioned forms. */
+int amg_dist_hier_create_slab(amg_ctx *ctx, const amg_gen *gen, const amg_opts *opts, amg_dist_hier **out);
+/* slab hierarchy facts: distributed levels, bitmask of levels whose transfers run
+ * the geometric kernels, 1 if level 0 runs the fused residual + restriction */
+int amg_dist_hier_slab_info(const amg_dist_hier *D, int *distributed_levels, int *geometric, int *fused);
 /* that partition (host only, no device): row_starts[l * (nranks + 1) + r] */
 int amg_dist_structured_row_starts(const amg_gen *gen, int nranks, long long *row_starts);
 /* levels with fewer rows than this are replicated on every rank (default 2^18) */

@@ -394,17 +394,24 @@ def test_l1_jacobi(mats, ctx, oracle, amg, name, zero):
         assert_bitwise(du.download(), ru, f"{name} {variant}")
 
 
-@pytest.mark.parametrize("name", ["lap16", "A1", "rand_sq"])
-@pytest.mark.parametrize("T", [1, 4, 8, "perf64"])
+@pytest.mark.parametrize("name", ["lap16", "A1", "rand_sq", "lap_hole"])
+@pytest.mark.parametrize("T", [1, 4, 8, "perf64", "ragged"])
 @pytest.mark.parametrize("zero", [0, 1])
-def test_hybrid_jgs(mats, ctx, oracle, amg, name, T, zero):
+@pytest.mark.parametrize("wave", [1, 0])
+def test_hybrid_jgs(mats, ctx, oracle, amg, name, T, zero, wave):
     """Hybrid Jacobi/GS is partition dependent: the same blocks must give the
-    same bits -- the reference's thread ranges (T) and the device partition."""
+    same bits -- the reference's thread ranges (T) and the device partition --
+    with one wave per block (the in-chunk chain carried lane to lane, blocks
+    spanning many 64-row chunks) and with one lane per block."""
     host, dev = mats
+    ctx.set_jgs_wave(wave)
     A, dA = host[name], dev[name]
     if T == "perf64":
         blk = np.minimum(np.arange(0, A.nrows + 64, 64), A.nrows).astype(np.int32)
         blk = np.unique(blk)
+    elif T == "ragged":  # blocks of 1 .. 200 rows, some empty
+        cuts = np.cumsum(rng(5).integers(0, 200, size=A.nrows // 50))
+        blk = np.concatenate([[0], cuts[cuts < A.nrows], [A.nrows]]).astype(np.int32)
     else:
         blk = oracle.partition_equal(A.nrows, T)
     f, u = _vecs(A.nrows, 22), _vecs(A.nrows, 23)
@@ -424,7 +431,8 @@ def test_hybrid_jgs(mats, ctx, oracle, amg, name, T, zero):
             else:
                 amg.smem.SMEM_Sync_HybridJacobiGaussSeidel(ctx, dA, ctx.vec(f), du, dp, 2, zero,
                                                           blk, reverse)
-            assert_bitwise(du.download(), ru, f"{name} T={T} rev={reverse} parfor={parfor}")
+            assert_bitwise(du.download(), ru, f"{name} T={T} rev={reverse} parfor={parfor} wave={wave}")
+    ctx.set_jgs_wave(1)
 
 
 def test_gauss_seidel(mats, ctx, oracle, amg):
