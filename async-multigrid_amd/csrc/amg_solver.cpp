@@ -1252,17 +1252,30 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       int st = AMG_OK;
       for (;;) {
          bool all = true;
-         for (int k = k_lo; k < k_hi; k++) {
-            while (completed[k] < issued[k] && hipEventQuery(done[k][completed[k] % DEPTH]) == hipSuccess)
+         for (int k = k_lo; k < k_hi && st == AMG_OK; k++) {
+            while (completed[k] < issued[k]) {
+               // not ready: still pending; any other status is a device error
+               const hipError_t q = hipEventQuery(done[k][completed[k] % DEPTH]);
+               if (q == hipErrorNotReady) break;
+               if (q != hipSuccess) {
+                  st = amg_set_error(AMG_ERR_HIP, "amg_async_solve: level %d correction: %s", k,
+                                     hipGetErrorString(q));
+                  break;
+               }
                completed[k]++;
+            }
             if (completed[k] < o.num_cycles) all = false;
          }
-         if (all) break;
+         if (st != AMG_OK || all) break;
          bool progressed = false;
          for (int k = k_lo; k < k_hi && st == AMG_OK; k++) {
             if (issued[k] - completed[k] < DEPTH && issued[k] < cap) {
                if ((st = correction(k)) != AMG_OK) break;
-               hipEventRecord(done[k][issued[k] % DEPTH], c->level_streams[k]);
+               const hipError_t er = hipEventRecord(done[k][issued[k] % DEPTH], c->level_streams[k]);
+               if (er != hipSuccess) {
+                  st = amg_set_error(AMG_ERR_HIP, "amg_async_solve: hipEventRecord: %s", hipGetErrorString(er));
+                  break;
+               }
                issued[k]++;
                progressed = true;
             }

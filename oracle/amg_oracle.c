@@ -21,6 +21,7 @@
 #include <stdio.h>
 #ifdef _OPENMP
 #include <omp.h>
+#include <sched.h>
 #endif
 
 #define OMP_MIN_ROWS 32768
@@ -271,9 +272,44 @@ void or_seq_gauss_seidel(const or_csr *A, const double *f, double *u, int sweeps
  * in place reading the live u of every row.  The restatement runs the blocks
  * one after another -- one admissible interleaving of the racy reference, and
  * THE result for a single block.  No zero-guess case, no weight. */
+static int g_async_gs_threads = 0;
+void or_set_async_gs_threads(int on) { g_async_gs_threads = on; }
+
+/* the same on one OpenMP thread per block, every u access a relaxed atomic:
+ * the reference's race itself (or_set_async_gs_threads(1)), so repeated
+ * solves give its spread of results */
+static inline double ld_relaxed(const double *p)
+{
+   double v;
+   __atomic_load(p, &v, __ATOMIC_RELAXED);
+   return v;
+}
+static inline void st_relaxed(double *p, double v) { __atomic_store(p, &v, __ATOMIC_RELAXED); }
+
+static void async_gs_threaded(const or_csr *A, const double *f, double *u, const int *blk, int nblk, int sweeps,
+                              int reverse)
+{
+#pragma omp parallel num_threads(nblk)
+   {
+      const int b = omp_get_thread_num();
+      for (int k = 0; k < sweeps; k++)
+         for (int c = 0; c < blk[b + 1] - blk[b]; c++) {
+            const int i = reverse ? blk[b + 1] - 1 - c : blk[b] + c;
+            if (A->data[A->i[i]] == 0.0) continue;
+            double res = f[i];
+            for (int jj = A->i[i]; jj < A->i[i + 1]; jj++) res -= A->data[jj] * ld_relaxed(&u[A->j[jj]]);
+            st_relaxed(&u[i], ld_relaxed(&u[i]) + res / A->data[A->i[i]]);
+         }
+   }
+}
+
 void or_async_gs(const or_csr *A, const double *f, double *u, const int *blk, int nblk, int sweeps,
                  int reverse)
 {
+   if (g_async_gs_threads && nblk > 1) {
+      async_gs_threaded(A, f, u, blk, nblk, sweeps, reverse);
+      return;
+   }
    for (int k = 0; k < sweeps; k++)
       for (int b = 0; b < nblk; b++)
          for (int c = 0; c < blk[b + 1] - blk[b]; c++) {
@@ -969,6 +1005,352 @@ int or_solve(or_hier *H, const double *f, double *u, double *reshist)
 #endif
    memcpy(u, H->u[0], (size_t)n0 * sizeof(double));
    return done;
+}
+
+/* ------------------------------------------------------------------------- */
+/* SMEM_Async_Add_AMG (SMEM_Async_AMG.cpp:7-437) on real OpenMP threads        */
+/* ------------------------------------------------------------------------- */
+/* The reference's asynchronous additive cycle restated on T threads, so its
+ * nondeterminism is the reference's own: nt[k] threads own level k (every
+ * level at least one: the thread-to-level map PartitionLevels computes,
+ * SMEM_Setup.cpp:590-868, given here as input); each group loops restrict ->
+ * smooth -> prolong -> update of the shared fine iterate with no
+ * synchronisation between groups; inside a group the threads split each
+ * level's rows nnz-balanced (PartitionGrids, SMEM_Setup.cpp:945-978) and meet at
+ * the group barrier (SMEM_LevelBarrier, Misc.cpp:485-533).  FULL_ASYNC adds
+ * with `omp atomic` (:284-301; the private copy takes the value after this
+ * thread's add), SEMI_ASYNC under one lock held by the group root (:238-283).
+ * READ_SOL or READ_RES (:227-236, 270-295: the groups subtract A e from the
+ * shared residual and keep private correction sums, joined at the end,
+ * :416-426), res_compute LOCAL, converge LOCAL (:317-322: a group stops after
+ * num_cycles corrections) or GLOBAL (:323-337: the finest group's root sets
+ * the converge flag once every level has num_cycles corrections -- CheckConverge,
+ * Misc.cpp:418-442 -- and each group barrier hands it to the group).  The
+ * smoothers are the ALL_LEVELS ones of the dispatcher (SMEM_Solve.cpp:277-321):
+ * hybrid JGS (:533-586), Jacobi / L1 (:365-443), symmetric Jacobi / L1
+ * (:643-762) with their barriers.  Test infrastructure: relres bands. */
+typedef struct {
+   int n, count, gen, flag;
+} or_gbar;
+
+static int gbar_wait(or_gbar *b, const int *conv)
+{
+   int g = __atomic_load_n(&b->gen, __ATOMIC_ACQUIRE);
+   if (__atomic_add_fetch(&b->count, 1, __ATOMIC_ACQ_REL) == b->n) {
+      __atomic_store_n(&b->count, 0, __ATOMIC_RELAXED);
+      __atomic_store_n(&b->flag, conv ? __atomic_load_n(conv, __ATOMIC_ACQUIRE) : 0, __ATOMIC_RELAXED);
+      __atomic_store_n(&b->gen, g + 1, __ATOMIC_RELEASE);
+   } else {
+      while (__atomic_load_n(&b->gen, __ATOMIC_ACQUIRE) == g) sched_yield();
+   }
+   return __atomic_load_n(&b->flag, __ATOMIC_RELAXED);
+}
+
+/* the ALL_LEVELS smoother of level `level` on A = A[Alevel], this thread's rows
+ * [ns, ne) (SMEM_Smooth's argument order: f, u, y (u_prev), r (y)) */
+static void async_smooth(or_hier *H, int Alevel, const double *f, double *u, double *up, double *yy,
+                         int sweeps, int level, int ns, int ne, or_gbar *b)
+{
+   const or_csr *A = &H->A[Alevel];
+   const or_opts *o = &H->o;
+   const int *Ai = A->i, *Aj = A->j;
+   const double *Ad = A->data;
+   const double w = o->smooth_weight;
+   const int zf = H->zero_flags[level];
+   const int multadd = (o->solver == OR_MULTADD || o->solver == OR_ASYNC_MULTADD);
+   const int sym = multadd && o->num_post > 0 && o->num_pre > 0;
+   /* the smoothed operator's L1 norms.  The reference reads
+    * L1_row_norm[level] with the GROUP's level (SMEM_Smooth.cpp:426,438), which
+    * for AFACx's coarse-grid smoothing (SMEM_Async_AMG.cpp:164-173) are the
+    * fine level's norms -- a quirk that makes AFACx + L1 diverge; the sync
+    * additive restatement (smooth() above) and the device use A[Alevel]'s */
+   const double *l1 = H->L1[Alevel];
+   if (o->smoother == OR_HYBRID_JACOBI_GAUSS_SEIDEL) {
+      /* SMEM_Sync_HybridJacobiGaussSeidel :533-586 (weight 1, divisor a_ii): the
+       * GS block is the thread's rows [ns, ne); a hierarchy with an explicit
+       * block partition of this level (or_hier_set_blocks: the device's 64-row
+       * blocks) runs every block whose first row is in [ns, ne) -- the
+       * reference with one thread per block, each block's rows in order */
+      const int *hb = H->blk[Alevel];
+      const int nhb = H->nblk[Alevel];
+      const int many = nhb > 1;
+      int b0 = 0, b1 = 1, one[2] = {ns, ne};
+      if (many) {
+         while (b0 < nhb && hb[b0] < ns) b0++;
+         b1 = b0;
+         while (b1 < nhb && hb[b1] < ne) b1++;
+      }
+      for (int k = 0; k < sweeps; k++) {
+         const int zero = (k == 0 && zf == 1);
+         if (!zero) {
+            for (int i = ns; i < ne; i++) up[i] = u[i];
+            gbar_wait(b, NULL);
+         }
+         for (int q = b0; q < b1; q++) {
+            const int bs = many ? hb[q] : one[0], be = many ? hb[q + 1] : one[1];
+            if (zero)
+               for (int i = bs; i < be; i++) u[i] = 0.0;
+            for (int i = bs; i < be; i++) {
+               if (Ad[Ai[i]] == 0.0) continue;
+               double res = f[i];
+               for (int jj = Ai[i]; jj < Ai[i + 1]; jj++) {
+                  int ii = Aj[jj];
+                  if (ii >= bs && ii < be) res -= Ad[jj] * u[ii];
+                  else if (!zero) res -= Ad[jj] * up[ii];
+               }
+               if (zero) u[i] = 1.0 * res / Ad[Ai[i]];
+               else u[i] += 1.0 * res / Ad[Ai[i]];
+            }
+         }
+         gbar_wait(b, NULL);
+      }
+      return;
+   }
+   const int use_l1 = o->smoother == OR_L1_JACOBI;
+   if (sym) {
+      /* SMEM_Sync_Symmetric[L1]Jacobi :643-762 (res_compute LOCAL); r = yy, y = up */
+      double *r = yy, *y = up;
+      int k = 0;
+      if (zf == 1) for (int i = ns; i < ne; i++) r[i] = f[i];
+      else or_smem_residual(A, f, u, y, r, ns, ne);
+      while (1) {
+         for (int i = ns; i < ne; i++) {
+            if (use_l1) r[i] /= l1[i];
+            else r[i] *= w / Ad[Ai[i]];
+         }
+         gbar_wait(b, NULL);
+         or_smem_matvec(A, r, y, ns, ne);
+         gbar_wait(b, NULL);
+         for (int i = ns; i < ne; i++) {
+            if (use_l1) {
+               r[i] = (2.0 * l1[i] * r[i]) - y[i];
+               r[i] /= l1[i];
+            } else {
+               r[i] = (2.0 * Ad[Ai[i]] * r[i] / w) - y[i];
+               r[i] *= w / Ad[Ai[i]];
+            }
+         }
+         if (zf == 1) for (int i = ns; i < ne; i++) u[i] = r[i];
+         else for (int i = ns; i < ne; i++) u[i] += r[i];
+         gbar_wait(b, NULL);
+         if (++k == sweeps) break;
+         or_smem_residual(A, f, u, y, r, ns, ne);
+      }
+      return;
+   }
+   /* SMEM_Sync_[L1]Jacobi :365-443 */
+   for (int k = 0; k < sweeps; k++) {
+      if (k == 0 && zf == 1) {
+         for (int i = ns; i < ne; i++) {
+            if (use_l1) u[i] = f[i] / l1[i];
+            else if (Ad[Ai[i]] != 0.0) u[i] = w * f[i] / Ad[Ai[i]];
+         }
+      } else {
+         for (int i = ns; i < ne; i++) up[i] = u[i];
+         gbar_wait(b, NULL);
+         for (int i = ns; i < ne; i++) {
+            if (!use_l1 && Ad[Ai[i]] == 0.0) continue;
+            double res = f[i];
+            for (int jj = Ai[i]; jj < Ai[i + 1]; jj++) res -= Ad[jj] * up[Aj[jj]];
+            if (use_l1) u[i] += res / l1[i];
+            else u[i] += w * res / Ad[Ai[i]];
+         }
+      }
+      gbar_wait(b, NULL);
+   }
+}
+
+int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int async_type, int read_type,
+                 int converge_type, int *corrections, double *relres)
+{
+   const or_opts *o = &H->o;
+   const int L = H->L, n0 = H->n[0];
+   const int multadd = (o->solver == OR_MULTADD || o->solver == OR_ASYNC_MULTADD);
+   int T = 0;
+   for (int k = 0; k < L; k++) {
+      if (nt[k] < 1) return -1;
+      T += nt[k];
+   }
+   init_vectors(H);
+   memcpy(H->f[0], f, (size_t)n0 * sizeof(double));
+   memcpy(H->u[0], u, (size_t)n0 * sizeof(double));
+   /* SMEM_Solve: r = f - A u, its norm (SMEM_Solve.cpp:60-70) */
+   or_smem_spgemv(&H->A[0], H->u[0], H->f[0], -1.0, 1.0, H->r[0], 0, n0);
+   const double r0 = or_norm2(H->r[0], n0);
+   for (int k = 0; k < L; k++) {
+      H->zero_flags[k] = 1;
+      memcpy(H->lv_r[k][0], H->r[0], (size_t)n0 * sizeof(double)); /* :10-15 */
+   }
+   /* groups: thread -> level, rank inside the group; row ranges per level */
+   int *lev = (int *)malloc(T * sizeof(int)), *gi = (int *)malloc(T * sizeof(int));
+   int *root = (int *)malloc(L * sizeof(int));
+   for (int k = 0, t = 0; k < L; k++) {
+      root[k] = t;
+      for (int g = 0; g < nt[k]; g++, t++) {
+         lev[t] = k;
+         gi[t] = g;
+      }
+   }
+   /* blkA[k][l]: level-l row partition among group k (nt[k] + 1 entries); P / R likewise */
+   int ***blk = (int ***)malloc(3 * sizeof(int **));
+   for (int m = 0; m < 3; m++) {
+      blk[m] = (int **)malloc((size_t)L * L * sizeof(int *));
+      for (int k = 0; k < L; k++)
+         for (int l = 0; l < L; l++) {
+            int *b = (int *)malloc((nt[k] + 1) * sizeof(int));
+            const or_csr *M = m == 0 ? &H->A[l] : (l < L - 1 ? (m == 1 ? &H->P[l] : &H->R[l]) : NULL);
+            if (M) or_partition_nnz(M, nt[k], b);
+            else for (int g = 0; g <= nt[k]; g++) b[g] = 0;
+            blk[m][k * L + l] = b;
+         }
+   }
+   or_gbar *bar = (or_gbar *)calloc(L, sizeof(or_gbar));
+   int *count = (int *)calloc(L, sizeof(int));
+   double **uk = (double **)malloc(L * sizeof(double *)), **facc = (double **)malloc(L * sizeof(double *));
+   for (int k = 0; k < L; k++) {
+      bar[k].n = nt[k];
+      uk[k] = dvec(n0);
+      facc[k] = dvec(n0);
+   }
+   int conv_flag = 0;
+   omp_lock_t lock;
+   omp_init_lock(&lock);
+   double *U = H->u[0];
+   const double *F = H->f[0];
+#pragma omp parallel num_threads(T)
+   {
+      const int tid = omp_get_thread_num();
+      const int k = lev[tid], g = gi[tid];
+      or_gbar *b = &bar[k];
+#define RNG(m, l, s, e) const int s = blk[m][k * L + (l)][g], e = blk[m][k * L + (l)][g + 1]
+      int tid_converge = 0;
+      const int coarsest = multadd ? k : k + 1;
+      while (1) {
+         /* restriction :93-108 */
+         for (int l = 0; l < coarsest; l++) {
+            if (l >= L - 1) continue;
+            RNG(2, l, rs, re);
+            or_smem_matvec(&H->R[l], H->lv_r[k][l], H->lv_r[k][l + 1], rs, re);
+            gbar_wait(b, NULL);
+         }
+         if (k == L - 1) {
+            gbar_wait(b, NULL); /* :112-132: the coarsest solve is commented out */
+         } else if (multadd) {
+            RNG(0, k, ns, ne);
+            for (int i = ns; i < ne; i++) H->lv_e[k][k][i] = 0.0;
+            gbar_wait(b, NULL);
+            async_smooth(H, k, H->lv_r[k][k], H->lv_e[k][k], H->lv_u_prev[k][k], H->lv_y[k][k], o->num_fine, k,
+                         ns, ne, b);
+         } else {
+            const int fg = k, cg = k + 1;
+            {
+               RNG(0, fg, ns, ne);
+               for (int i = ns; i < ne; i++) H->lv_u_fine[k][fg][i] = 0.0;
+            }
+            {
+               RNG(0, cg, ns, ne);
+               for (int i = ns; i < ne; i++) H->lv_u_coarse[k][cg][i] = 0.0;
+               gbar_wait(b, NULL);
+               async_smooth(H, cg, H->lv_r[k][cg], H->lv_u_coarse[k][cg], H->lv_u_coarse_prev[k][cg],
+                            H->lv_y[k][cg], o->num_coarse, k, ns, ne, b);
+            }
+            RNG(0, fg, ns, ne);
+            or_smem_matvec(&H->P[fg], H->lv_u_coarse[k][cg], H->lv_e[k][fg], ns, ne);
+            gbar_wait(b, NULL);
+            or_smem_residual(&H->A[fg], H->lv_r[k][fg], H->lv_e[k][fg], H->lv_y[k][fg], H->lv_r_fine[k][fg], ns,
+                             ne);
+            gbar_wait(b, NULL);
+            async_smooth(H, fg, H->lv_r_fine[k][fg], H->lv_u_fine[k][fg], H->lv_u_fine_prev[k][fg],
+                         H->lv_y[k][fg], o->num_fine, k, ns, ne, b);
+            for (int i = ns; i < ne; i++) H->lv_e[k][k][i] = H->lv_u_fine[k][k][i];
+            gbar_wait(b, NULL);
+         }
+         /* prolongation :211-224 */
+         for (int l = k - 1; l > -1; l--) {
+            RNG(1, l, ps, pe);
+            or_smem_matvec(&H->P[l], H->lv_e[k][l + 1], H->lv_e[k][l], ps, pe);
+            gbar_wait(b, NULL);
+         }
+         RNG(0, 0, ns, ne);
+         const double *e0 = H->lv_e[k][0];
+         double *ukk = uk[k];
+         const int rres = read_type == OR_READ_RES;
+         /* READ_RES: y = A e on the group's rows (:227-236) */
+         if (rres) or_smem_matvec(&H->A[0], e0, H->lv_y[k][0], ns, ne);
+         const double *y0 = H->lv_y[k][0];
+         double *R0 = H->r[0], *rk = H->lv_r[k][0], *fk = facc[k];
+         /* update of the shared iterate (READ_SOL) or residual (READ_RES) :238-301 */
+         if (async_type == OR_SEMI_ASYNC) {
+            if (tid == root[k]) omp_set_lock(&lock);
+            gbar_wait(b, NULL);
+         }
+         for (int i = ns; i < ne; i++) {
+            double v;
+            if (rres) {
+               if (async_type != OR_SEMI_ASYNC) fk[i] += e0[i];
+               else {
+#pragma omp atomic
+                  U[i] += e0[i];
+               }
+#pragma omp atomic capture
+               {
+                  R0[i] -= y0[i];
+                  v = R0[i];
+               }
+               rk[i] = v;
+            } else {
+#pragma omp atomic capture
+               {
+                  U[i] += e0[i];
+                  v = U[i];
+               }
+               ukk[i] = v;
+            }
+         }
+         if (async_type == OR_SEMI_ASYNC && tid == root[k]) omp_unset_lock(&lock);
+         if (tid == root[k]) __atomic_add_fetch(&count[k], 1, __ATOMIC_ACQ_REL);
+         if (converge_type == OR_CONVERGE_LOCAL) {
+            gbar_wait(b, NULL);
+            if (__atomic_load_n(&count[k], __ATOMIC_ACQUIRE) == o->num_cycles) tid_converge = 1;
+         } else {
+            if (tid == root[0] && __atomic_load_n(&conv_flag, __ATOMIC_ACQUIRE) == 0) {
+               int all = 1;
+               for (int l = 0; l < L; l++)
+                  if (__atomic_load_n(&count[l], __ATOMIC_ACQUIRE) < o->num_cycles) all = 0;
+               if (all) __atomic_store_n(&conv_flag, 1, __ATOMIC_RELEASE);
+            }
+            if (gbar_wait(b, &conv_flag) == 1) tid_converge = 1;
+         }
+         /* LOCAL residual, READ_SOL :338-351 */
+         if (!rres) or_smem_residual(&H->A[0], F, ukk, H->lv_y[k][0], H->lv_r[k][0], ns, ne);
+         gbar_wait(b, NULL);
+         if (tid_converge == 1) break;
+      }
+#undef RNG
+   }
+   omp_destroy_lock(&lock);
+   /* FULL_ASYNC READ_RES: the private correction sums join u (:416-426) */
+   if (read_type == OR_READ_RES && async_type != OR_SEMI_ASYNC)
+      for (int k = 0; k < L; k++)
+         for (int i = 0; i < n0; i++) H->u[0][i] += facc[k][i];
+   /* SMEM_Solve.cpp:82-91: the final residual */
+   or_smem_spgemv(&H->A[0], H->u[0], H->f[0], -1.0, 1.0, H->r[0], 0, n0);
+   if (relres) *relres = r0 > 0 ? or_norm2(H->r[0], n0) / r0 : 0.0;
+   if (corrections)
+      for (int k = 0; k < L; k++) corrections[k] = count[k];
+   memcpy(u, H->u[0], (size_t)n0 * sizeof(double));
+   for (int m = 0; m < 3; m++) {
+      for (int q = 0; q < L * L; q++) free(blk[m][q]);
+      free(blk[m]);
+   }
+   free(blk);
+   for (int k = 0; k < L; k++) {
+      free(uk[k]);
+      free(facc[k]);
+   }
+   free(uk);
+   free(facc); free(bar); free(count); free(lev); free(gi); free(root);
+   return 0;
 }
 
 /* M^{-1} = one V-cycle in preconditioner mode from a zero state (the

@@ -85,6 +85,9 @@ void or_seq_jacobi(const or_csr *A, const double *f, double *u, double *u_prev, 
 void or_seq_l1jacobi(const or_csr *A, const double *f, double *u, double *u_prev, const double *l1,
                      int sweeps, int zero_flag);
 void or_seq_gauss_seidel(const or_csr *A, const double *f, double *u, int sweeps);
+/* 1: or_async_gs runs one OpenMP thread per block on the live u (the reference's
+ * race; nondeterministic), 0 (default): the blocks one after another */
+void or_set_async_gs_threads(int on);
 void or_async_gs(const or_csr *A, const double *f, double *u, const int *blk, int nblk, int sweeps,
                  int reverse);
 void or_hybrid_jgs(const or_csr *A, const double *f, double *u, double *u_prev, const int *blk,
@@ -183,6 +186,23 @@ int or_dmem_mult_solve(or_hier *H, const double *b, double *x, double *reshist, 
  * x = 0 and r = b on entry.  Returns ||b - A x||. */
 double or_dmem_async_jacobi(const or_csr *A, const double *b, double *x, int sweeps, double omega,
                             const double *l1, int accel, double mu, double delta);
+
+/* SMEM_Async_Add_AMG (SMEM_Async_AMG.cpp:7-437) on real OpenMP threads: nt[k]
+ * threads own level k (sum = T threads, each >= 1); async_type FULL / SEMI,
+ * READ_SOL / READ_RES, res_compute LOCAL, converge LOCAL or GLOBAL; the hierarchy's opts
+ * give solver (ASYNC_MULTADD / ASYNC_AFACX), smoother (Jacobi, L1, hybrid JGS;
+ * symmetric forms for multadd with pre and post sweeps), num_fine /
+ * num_coarse sweeps, num_cycles.  u: initial guess in, iterate out;
+ * corrections[k] = level k's correction count; *relres = ||f - A u|| / ||f - A u0||.
+ * Nondeterministic, as the reference: run it repeatedly for a band. */
+#define OR_FULL_ASYNC 0
+#define OR_SEMI_ASYNC 1
+#define OR_CONVERGE_LOCAL 0
+#define OR_CONVERGE_GLOBAL 1
+#define OR_READ_SOL 0
+#define OR_READ_RES 1
+int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int async_type, int read_type,
+                 int converge_type, int *corrections, double *relres);
 
 /* access the hierarchy's level vectors (u, f) for tests */
 double *or_hier_vec(or_hier *H, const char *name, int level);

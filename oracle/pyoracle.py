@@ -15,6 +15,10 @@ _LIB = None
 OR_JACOBI, OR_GAUSS_SEIDEL, OR_HYBRID_JGS, OR_SYMM_JACOBI = 0, 1, 2, 3
 OR_L1_JACOBI, OR_L1_HYBRID_JGS = 6, 12
 OR_MULT, OR_AFACX, OR_MULTADD = 0, 1, 2
+OR_ASYNC_AFACX, OR_ASYNC_MULTADD = 5, 6
+OR_FULL_ASYNC, OR_SEMI_ASYNC = 0, 1
+OR_CONVERGE_LOCAL, OR_CONVERGE_GLOBAL = 0, 1
+OR_READ_SOL, OR_READ_RES = 0, 1
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int)
@@ -72,6 +76,10 @@ def lib():
                                            C.c_double, _dp]
         L.or_dmem_mult_solve.restype = C.c_int
         L.or_dmem_mult_solve.argtypes = [C.c_void_p, _dp, _dp, _dp, C.c_int, C.c_double, C.c_double]
+        L.or_set_async_gs_threads.argtypes = [C.c_int]
+        L.or_async_add.restype = C.c_int
+        L.or_async_add.argtypes = [C.c_void_p, _dp, _dp, _ip, C.c_int, C.c_int, C.c_int, _ip,
+                                   C.POINTER(C.c_double)]
         L.or_dmem_async_jacobi.restype = C.c_double
         L.or_dmem_async_jacobi.argtypes = [C.POINTER(OrCsr), _dp, _dp, C.c_int, C.c_double, _dp,
                                            C.c_int, C.c_double, C.c_double]
@@ -369,6 +377,20 @@ class Hier:
         k = lib().or_dmem_mult_solve(self.h, dptr(np.ascontiguousarray(b, dtype=np.float64)), dptr(x),
                                      dptr(hist), accel, mu, delta)
         return x, hist[:k + 1], k
+
+    def async_add(self, f, nt, async_type=0, converge_type=0, u0=None, read_type=0):
+        """SMEM_Async_Add_AMG on sum(nt) OpenMP threads (nt[k] threads own level k):
+        (u, relres, per-level correction counts).  Nondeterministic."""
+        n0 = self._keep[0][0].nrows
+        u = np.zeros(n0) if u0 is None else np.array(u0, dtype=np.float64)
+        ntv = np.ascontiguousarray(nt, dtype=np.int32)
+        assert ntv.size == self.L and np.all(ntv >= 1)
+        cnt = np.zeros(self.L, dtype=np.int32)
+        rel = C.c_double()
+        st = lib().or_async_add(self.h, dptr(np.ascontiguousarray(f, dtype=np.float64)), dptr(u), iptr(ntv),
+                                int(async_type), int(read_type), int(converge_type), iptr(cnt), C.byref(rel))
+        assert st == 0, st
+        return u, rel.value, cnt
 
     def eigs_power(self, iters):
         emax, emin = C.c_double(), C.c_double()

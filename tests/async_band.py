@@ -1,0 +1,47 @@
+"""The oracle's asynchronous additive band (test infrastructure).
+
+oracle/amg_oracle.c or_async_add restates SMEM_Async_Add_AMG
+(SMEM_Async_AMG.cpp:7-437) on real OpenMP threads: thread groups own levels and
+race on the shared iterate exactly as the reference does, so repeated runs
+give the reference's own spread of final relative residuals.  The GPU's
+asynchronous solves must land in [0.5 x min, 2 x max] of that band
+(SURVEY.md Sec.8(d)).  Thread sets: one and two threads per level (T = L and
+2L; every level needs a group); the band is taken over all runs of both."""
+import numpy as np
+
+from test_gpu_solve import oracle_opts
+
+
+def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blocks=None):
+    """(lo, hi, rels, counts) of `reps` runs per thread set; opts: the GPU run's
+    amg_opts (solver ASYNC_MULTADD / ASYNC_AFACX, smoother, sweeps, num_cycles,
+    async_type, read_type, converge_test_type)."""
+    L = len(host["A"])
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    if blocks is not None:
+        for lev, blk in blocks.items():
+            OH.set_blocks(lev, blk)
+    at = oracle.OR_SEMI_ASYNC if opts.async_type == amg.AMG_SEMI_ASYNC else oracle.OR_FULL_ASYNC
+    rt = oracle.OR_READ_RES if opts.read_type == amg.AMG_READ_RES else oracle.OR_READ_SOL
+    ct = oracle.OR_CONVERGE_GLOBAL if opts.converge_test_type == amg.AMG_GLOBAL else oracle.OR_CONVERGE_LOCAL
+    rels, counts = [], []
+    for nt in thread_sets or ([1] * L, [2] * L):
+        for _ in range(reps):
+            u, rel, cnt = OH.async_add(f, nt, async_type=at, converge_type=ct, read_type=rt)
+            assert np.all(np.isfinite(u))
+            rels.append(rel)
+            counts.append(cnt)
+    return min(rels), max(rels), rels, counts
+
+
+def blocks64(host):
+    """the device's default hybrid JGS blocks (jgs_block_rows = 64) per level"""
+    out = {}
+    for lev, A in enumerate(host["A"]):
+        n = A.nrows
+        out[lev] = np.unique(np.minimum(np.arange(0, n + 64, 64), n)).astype(np.int32)
+    return out
+
+
+def in_band(rel, lo, hi):
+    return 0.5 * lo <= rel <= 2.0 * hi

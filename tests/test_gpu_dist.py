@@ -279,10 +279,10 @@ def split_host(host, cuts):
                                              ("afacx", (0.45,), 0), ("multadd", (), 0),
                                              ("afacx", (), 1000)])
 def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
-    """Distributed asynchronous additive AMG (level streams x ranks, per-level
-    communicators): nondeterministic; its relres after N corrections per level
-    sits in the same band around the oracle's synchronous additive cycle as the
-    single-GPU async solver (test_gpu_solve.py::test_async_multadd_band)."""
+    """Distributed asynchronous additive AMG (level streams x ranks, one comm
+    stream): nondeterministic; its relres after N corrections per level lies in
+    [0.5 x min, 2 x max] of the oracle's asynchronous band (SMEM_Async_Add_AMG
+    on OpenMP threads, tests/async_band.py), as the single-GPU async solver."""
     from test_gpu_solve import hierarchy, oracle_opts
     _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
     w = 0.8
@@ -306,7 +306,7 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
 
     def rank(r):
         c = amg.Context(0, nstreams=L)
-        if nranks == 1:  # one rank: the RCCL transport itself (ncclCommSplit per level)
+        if nranks == 1:  # one rank: the RCCL transport itself
             amg.dist.init_rccl(c, 1, 0, lambda b: b)
         else:
             amg.dist.init_host(c, nranks, r, amg.dist.HostTransport(hub, r))
@@ -327,7 +327,11 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
     assert np.all(np.isfinite(u))
     assert list(res[0][2][:L - 1]) == [N] * (L - 1)
     assert rels[0] < 1.0
-    assert sync_rel / 50 <= rels[0] <= sync_rel * 50, (rels[0], sync_rel)
+    from async_band import in_band, oracle_async_band
+    lo, hi, orels, _ = oracle_async_band(amg, oracle, host, f, opts)
+    print(f"dist async {solver} {nranks} ranks: oracle band [{lo:.4e}, {hi:.4e}] ({len(orels)} runs), "
+          f"sync {sync_rel:.4e}, device {rels[0]:.4e}")
+    assert in_band(rels[0], lo, hi), (rels[0], lo, hi, sync_rel)
 
 
 @pytest.mark.parametrize("nranks,l1", [(1, 0), (2, 0), (3, 1)])

@@ -121,8 +121,10 @@ def test_bpx_cycle(amg, oracle, ctx, smoother, extra):
 
 @pytest.mark.parametrize("sm", ["asyncgs", "semiasyncgs"])
 def test_mult_vcycle_async_gs_band(amg, oracle, ctx, sm):
-    """Asynchronous Gauss-Seidel smoother with many thread blocks: racy, so
-    the V-cycle is checked for convergence against the single-block run."""
+    """Asynchronous Gauss-Seidel smoother with many thread blocks: racy, so the
+    V-cycle's final relative residual is checked against the oracle's band: the
+    same solve with the smoother's 32 blocks on 32 OpenMP threads racing on the
+    live iterate (the reference's own race), 10 runs, [0.5 x min, 2 x max]."""
     _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
     code = amg.AMG_ASYNC_GS if sm == "asyncgs" else amg.AMG_SEMI_ASYNC_GS
     f = amg.rhs_rand(0, 24 ** 3)
@@ -131,10 +133,18 @@ def test_mult_vcycle_async_gs_band(amg, oracle, ctx, sm):
     u, h, k = H.solve(f)
     H.free()
     rel = h[-1] / h[0]
-    # the oracle runs the 32 blocks one after another: one admissible interleaving
-    _, h_c, _ = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts)).solve(f)
-    rel_c = h_c[-1] / h_c[0]
-    assert np.all(np.isfinite(u)) and rel < 1e-4 and rel_c / 100 <= rel <= rel_c * 1000, (rel, rel_c)
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    oracle.lib().or_set_async_gs_threads(1)
+    try:
+        band = []
+        for _ in range(10):
+            _, h_c, _ = OH.solve(f)
+            band.append(h_c[-1] / h_c[0])
+    finally:
+        oracle.lib().or_set_async_gs_threads(0)
+    lo, hi = min(band), max(band)
+    print(f"{sm}: oracle band [{lo:.4e}, {hi:.4e}], device {rel:.4e}")
+    assert np.all(np.isfinite(u)) and rel < 1e-4 and 0.5 * lo <= rel <= 2.0 * hi, (rel, lo, hi)
 
 
 def test_reuse_outer_residual_is_bit_identical(amg, oracle, ctx):
@@ -224,9 +234,10 @@ def test_sync_additive(amg, oracle, ctx, solver, smoother):
 
 def test_async_multadd_band(amg, oracle, ctx):
     """Asynchronous additive AMG: nondeterministic; its final relative residual
-    after N corrections per level must sit in a band around the synchronous
-    additive result of the oracle ([0.5x, 2x] of the CPU band,
-    widened here because the CPU band itself is a single deterministic run)."""
+    after N corrections per level must sit in [0.5 x min, 2 x max] of the
+    oracle's asynchronous band (SMEM_Async_Add_AMG on OpenMP threads, 10 runs
+    with one and two threads per level)."""
+    from async_band import in_band, oracle_async_band
     _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
     w = 0.8
     Ps, Rs = [], []
@@ -249,6 +260,9 @@ def test_async_multadd_band(amg, oracle, ctx):
         rels.append(rel)
         assert np.all(np.isfinite(u))
     H.free()
+    lo, hi, orels, _ = oracle_async_band(amg, oracle, host, f, opts)
+    print(f"async multadd: oracle band [{lo:.4e}, {hi:.4e}] ({len(orels)} runs), sync {sync_rel:.4e}, "
+          f"device {rels}")
     assert max(rels) < 1.0
     for rel in rels:
-        assert sync_rel / 50 <= rel <= sync_rel * 50, (rels, sync_rel)
+        assert in_band(rel, lo, hi), (rels, lo, hi)

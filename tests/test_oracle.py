@@ -155,3 +155,52 @@ def test_dmem_async_jacobi_one_rank(oracle):
     np.testing.assert_allclose(x, u, rtol=1e-10, atol=1e-13)
     r = b - A.to_scipy() @ x
     np.testing.assert_allclose(rn, np.linalg.norm(r), rtol=1e-10)
+
+
+def test_async_add_oracle(oracle, amg):
+    """or_async_add (SMEM_Async_Add_AMG on OpenMP threads): every level group does
+    num_cycles corrections (LOCAL) or at least that many (GLOBAL), the solve
+    converges for MULTADD / AFACx with Jacobi, L1 and hybrid JGS, FULL / SEMI,
+    READ_SOL / READ_RES; with two levels only the fine group changes u (the
+    coarsest correction is zero: the reference's coarsest solve is commented
+    out), so the run is deterministic and equals the synchronous additive
+    cycle up to the residual's two-pass rounding."""
+    g = amg.Gen(16, interp=amg.AMG_INTERP_LINEAR)
+    L = g.L
+    A = [oracle.Csr(*g.host_csr(amg.AMG_GEN_A, l)) for l in range(L)]
+    P = [oracle.Csr(*g.host_csr(amg.AMG_GEN_P, l)) for l in range(L - 1)]
+    Ps, Rs = [], []
+    for l in range(L - 1):
+        p, r = oracle.smooth_transfer(A[l], P[l], 0.8)
+        Ps.append(p)
+        Rs.append(r)
+    f = amg.rhs_rand(0, 16 ** 3)
+    N = 12
+    for solver, host_p, host_r in ((oracle.OR_ASYNC_MULTADD, Ps, Rs), (oracle.OR_ASYNC_AFACX, P, [
+            oracle.Csr(*g.host_csr(amg.AMG_GEN_R, l)) for l in range(L - 1)])):
+        for sm in (oracle.OR_JACOBI, oracle.OR_L1_JACOBI, oracle.OR_HYBRID_JGS):
+            H = oracle.Hier(A, host_p, host_r, oracle.make_opts(solver=solver, smoother=sm, smooth_weight=0.8,
+                                                                num_cycles=N))
+            for at in (oracle.OR_FULL_ASYNC, oracle.OR_SEMI_ASYNC):
+                for rt in (oracle.OR_READ_SOL, oracle.OR_READ_RES):
+                    for ct in (oracle.OR_CONVERGE_LOCAL, oracle.OR_CONVERGE_GLOBAL):
+                        u, rel, cnt = H.async_add(f, [1] * L, async_type=at, read_type=rt, converge_type=ct)
+                        assert np.all(np.isfinite(u))
+                        # AFACx on the plain transfers contracts slowly; with GLOBAL
+                        # convergence its fast coarse groups run many stale corrections
+                        if solver == oracle.OR_ASYNC_MULTADD:
+                            assert rel < 0.05, (solver, sm, at, rt, ct, rel)
+                        elif ct == oracle.OR_CONVERGE_LOCAL:
+                            assert rel < 1.0, (solver, sm, at, rt, ct, rel)
+                        if ct == oracle.OR_CONVERGE_LOCAL:
+                            assert list(cnt) == [N] * L, cnt
+                        else:
+                            assert min(cnt) >= N, cnt
+    # two levels: deterministic, equal to the synchronous additive cycle
+    A2, P2, R2 = A[:2], Ps[:1], Rs[:1]
+    o = dict(smoother=oracle.OR_JACOBI, smooth_weight=0.8, num_cycles=N)
+    _, h, _ = oracle.Hier(A2, P2, R2, oracle.make_opts(solver=oracle.OR_MULTADD, **o)).solve(f)
+    Ha = oracle.Hier(A2, P2, R2, oracle.make_opts(solver=oracle.OR_ASYNC_MULTADD, **o))
+    rels = [Ha.async_add(f, [2, 1])[1] for _ in range(3)]
+    assert max(rels) == min(rels)
+    assert abs(rels[0] - h[-1] / h[0]) <= 1e-9 * h[-1] / h[0], (rels, h[-1] / h[0])

@@ -1,8 +1,17 @@
-# hybrid JGS kernel change: kernel / solve / config tests, then config-3 bench
-set -o pipefail
-cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_solve.py tests/test_gpu_async.py tests/test_gpu_configs.py tests/test_gpu_dist.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_jgs.log 2>&1
-st=$?; tail -3 gpurun_out/pytest_jgs.log; [ $st -eq 0 ] || exit $st
-timeout -k 10 600 python tools/bench_async.py > gpurun_out/bench_async.json 2> gpurun_out/bench_async.log
-st=$?; cat gpurun_out/bench_async.log; exit $st
+#!/bin/bash
+# hybrid JGS wave kernel: bitwise kernel tests, async solves, config-3 throughput (wave vs lane), kernel stats
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R=$PWD
+P=$R/gpurun_out/jgs
+mkdir -p $P
+timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py -k "hybrid or gauss" tests/test_gpu_solve.py tests/test_gpu_async.py tests/test_gpu_configs.py -q --timeout 400 --timeout-method thread > $P/pytest.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -4 $P/pytest.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+AMG_JGS_WAVE=0 timeout -k 10 600 python tools/bench_async.py --reps 2 > $P/bench_async_lane.json 2> $P/bench_async_lane.log || exit $?
+timeout -k 10 600 python tools/bench_async.py --reps 3 > $P/bench_async.json 2> $P/bench_async.log || exit $?
+tail -3 $P/bench_async_lane.log; tail -3 $P/bench_async.log
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace -o run \
+   -- python3 $R/tools/bench_async.py --reps 1 --cycles 10 > $P/trace_async.json 2> $P/trace_async.err || exit $?
+head -12 $P/trace/run_kernel_stats.csv
