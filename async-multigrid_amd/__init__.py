@@ -105,7 +105,8 @@ class Context:
         check(lib.amg_set_bsr3(self.h, int(enable)))
 
     def set_jgs_wave(self, enable):
-        """Hybrid JGS: one wave per block (default) or one lane per block (0); bit-identical."""
+        """Hybrid JGS kernel form, all bit-identical: 1 (default) 8 lanes per block,
+        8 blocks per wave; 2 one wave per block; 0 one lane per block."""
         check(lib.amg_set_jgs_wave(self.h, int(enable)))
 
     def set_fuse_prolong(self, enable):

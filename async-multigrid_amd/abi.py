@@ -52,7 +52,8 @@ class AmgOpts(C.Structure):
                 ("read_type", _i), ("converge_test_type", _i),
                 ("delay_type", _i), ("delay_usec", _i), ("delay_frac", _d), ("fail_iter", _i),
                 ("delay_rank", _i), ("max_inflight", _i), ("async_comm_save_divisor", _i),
-                ("sps_probability_type", _i), ("sps_alpha", _d), ("sps_min_prob", _d)]
+                ("sps_probability_type", _i), ("sps_alpha", _d), ("sps_min_prob", _d),
+                ("delay_level", _i)]
 
 
 AMG_DELAY_NONE, AMG_DELAY_ONE, AMG_DELAY_SOME, AMG_DELAY_ALL, AMG_FAIL_ONE = 0, 1, 2, 3, 4
@@ -186,6 +187,7 @@ PROTOTYPES = {
     "amg_dist_init_host": (_i, [_p, _i, _i, C.c_void_p, _p]),
     "amg_dist_hier_set_replicate_rows": (_i, [_p, _ll]),
     "amg_dist_async_solve": (_i, [_p, _dp, _ip, _dp]),
+    "amg_dist_async_level_ms": (_i, [_p, _dp]),
     "amg_dist_async_jacobi": (_i, [_p, _dp, _i, _i, _dp]),
     "amg_dist_async_sps": (_i, [_p, _dp, _i, _dp, C.POINTER(C.c_longlong)]),
     "amg_rand_double_stream": (_i, [C.c_uint, _i, _d, _d, _dp]),

@@ -57,6 +57,7 @@ extern "C" void amg_opts_default(amg_opts *o)
    o->sps_probability_type = AMG_SPS_EXPONENTIAL; // DMEM_Main.cpp:119-121
    o->sps_alpha = 1.0;
    o->sps_min_prob = 0.0;
+   o->delay_level = -1;
 }
 
 // ---------------------------------------------------------------------------
@@ -98,7 +99,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_PLANE_MARCH_XCD")) c->mz_xcd = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::atoi(v) != 0;
-   if (const char *v = std::getenv("AMG_JGS_WAVE")) c->jgs_wave = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_JGS_WAVE")) c->jgs_wave = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ_EDGE")) c->mz_edge = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
@@ -799,7 +800,7 @@ extern "C" int amg_set_plane_march(amg_ctx *c, int enable, int zc, int xcd)
 extern "C" int amg_set_jgs_wave(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_jgs_wave: null context");
-   c->jgs_wave = enable ? 1 : 0;
+   c->jgs_wave = std::max(0, std::min(2, enable));
    return AMG_OK;
 }
 

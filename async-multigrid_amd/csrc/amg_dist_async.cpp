@@ -471,9 +471,13 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    AMG_TRY(dist_solve_begin(D, f_local));
    const int active = (int)D->al.size();
    const int n0 = D->lv[0].n;
-   hipEvent_t ready;
+   hipEvent_t ready, t_start;
+   std::vector<hipEvent_t> t_end(active);
    AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+   AMG_HIP(hipEventCreate(&t_start));
+   for (auto &e : t_end) AMG_HIP(hipEventCreate(&e));
    AMG_HIP(hipEventRecord(ready, c->stream));
+   AMG_HIP(hipEventRecord(t_start, c->stream));
    for (int k = 0; k < active; k++) {
       AMG_HIP(hipStreamWaitEvent(D->al[k].s, ready, 0));
       // level_vector[k].r[0] = vector.r[0] (SMEM_Async_AMG.cpp:10-15)
@@ -484,12 +488,13 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    // sequence of RCCL operations on the one comm stream; the GPU runs the
    // level streams' compute freely
    for (int cyc = 0; cyc < D->o.num_cycles; cyc++) {
-      for (int k = 0; k < active; k++) dist_delay(D, D->al[k].s); // DMEM_Add.cpp:106
+      for (int k = 0; k < active; k++)
+         if (D->o.delay_level < 0 || D->o.delay_level == k) dist_delay(D, D->al[k].s); // DMEM_Add.cpp:106
       for (int k = 0; k < active; k++) AMG_TRY(level_correction(D, k));
    }
    for (int k = 0; k < active; k++) {
-      AMG_HIP(hipEventRecord(ready, D->al[k].s));
-      AMG_HIP(hipStreamWaitEvent(c->stream, ready, 0));
+      AMG_HIP(hipEventRecord(t_end[k], D->al[k].s));
+      AMG_HIP(hipStreamWaitEvent(c->stream, t_end[k], 0));
    }
    AMG_HIP(hipEventDestroy(ready));
    D->pre_ready = false;
@@ -499,6 +504,22 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    if (relres) *relres = c->h_pinned[0] / D->r0norm;
    if (level_corrections)
       for (int k = 0; k < D->L; k++) level_corrections[k] = k < active ? D->o.num_cycles : 0;
+   D->level_ms.assign(D->L, 0.0);
+   for (int k = 0; k < active; k++) {
+      float ms = 0.f;
+      AMG_HIP(hipEventElapsedTime(&ms, t_start, t_end[k]));
+      D->level_ms[k] = ms;
+      AMG_HIP(hipEventDestroy(t_end[k]));
+   }
+   AMG_HIP(hipEventDestroy(t_start));
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_async_level_ms(const amg_dist_hier *D, double *ms)
+{
+   AMG_ARG(D && ms, "amg_dist_async_level_ms: null argument");
+   AMG_ARG(!D->level_ms.empty(), "amg_dist_async_level_ms: no asynchronous solve yet");
+   for (int k = 0; k < D->L; k++) ms[k] = D->level_ms[k];
    return AMG_OK;
 }
 
@@ -565,6 +586,37 @@ __global__ void ajac_scale_k(const double *__restrict__ diag, const double *__re
 }
 
 constexpr int AJ_NBUF = 4;
+
+// SPS messages carry the sender's residual norm after each peer's deltas
+// (data[vec_len + 1], DMEM_Comm.cpp:216-220): peer i's segment of the slot is
+// [scnt[i] deltas | norm] at soff[i] + i.  One thread per slot entry.
+__device__ __forceinline__ int seg_of(const long long *__restrict__ off, int np, long long p)
+{
+   int lo = 0, hi = np - 1; // last segment with off[seg] <= p
+   while (lo < hi) {
+      const int mid = (lo + hi + 1) / 2;
+      if (off[mid] <= p) lo = mid;
+      else hi = mid - 1;
+   }
+   return lo;
+}
+
+__global__ void sps_pack_k(const double *__restrict__ e, const int *__restrict__ idx, long long nsend,
+                           const long long *__restrict__ soff, int np, const double *__restrict__ norm,
+                           double *__restrict__ out)
+{
+   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (p < nsend) out[p + seg_of(soff, np, p)] = e[idx[p]];
+   if (p < np) out[soff[p + 1] + p] = norm[0];
+}
+
+__global__ void sps_unpack_k(const double *__restrict__ in, long long ng, const long long *__restrict__ roff, int np,
+                             double *__restrict__ g, double *__restrict__ rnorm)
+{
+   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (p < ng) g[p] = in[p + seg_of(roff, np, p)];
+   if (p < np) rnorm[p] = in[roff[p + 1] + p];
+}
 
 // StochasticParallelSouthwellUpdateProbability (DMEM_Smooth.cpp:548-572) and the
 // draw that follows it (:286-290), for sweep k >= 1 (sweep 0 always relaxes,
@@ -666,8 +718,10 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
       dtmp.push_back(p);
       return p;
    };
-   double *wv = tmp(n), *f = tmp(n), *sbuf = tmp((size_t)std::max<long long>(1, M.nsend) * AJ_NBUF),
-          *rbuf = tmp((size_t)std::max(1, ng) * AJ_NBUF), *dacc = tmp(n);
+   // slot sizes: SPS appends the sender's norm to every peer's deltas
+   const long long SS = std::max<long long>(1, M.nsend + (sps ? np : 0)), RS = std::max<long long>(1, ng + (sps ? np : 0));
+   double *wv = tmp(n), *f = tmp(n), *sbuf = tmp((size_t)SS * AJ_NBUF), *rbuf = tmp((size_t)RS * AJ_NBUF),
+          *dacc = tmp(n);
    AccelState acc;
    acc.reset(D->o);
    const bool accel = D->o.accel_type != AMG_NO_ACCEL;
@@ -680,14 +734,14 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
       return code;
    };
    if (!wv || !f || !sbuf || !rbuf || !dacc) return fail(amg_set_error(AMG_ERR_OOM, "amg_dist_async_jacobi: workspace"));
-   // SPS: [my norm per slot (NBUF) | neighbour norms per slot (NBUF np) | latest
-   // neighbour norms (np) | draws (sweeps)], gate flag and relaxation count
+   // SPS: [my norm per slot (NBUF) | latest neighbour norms (np) | draws
+   // (sweeps)], gate flag, relaxation count, the segment offsets soff / roff
    double *part = nullptr, sps_alpha = D->o.sps_alpha;
-   double *snorm = nullptr, *rnorm = nullptr, *lnorm = nullptr, *draws = nullptr;
+   double *snorm = nullptr, *lnorm = nullptr, *draws = nullptr;
    int *gate = nullptr;
-   long long *count = nullptr;
+   long long *count = nullptr, *d_soff = nullptr, *d_roff = nullptr;
    if (sps) {
-      double *ws = tmp((size_t)AJ_NBUF * (1 + np) + np + sweeps + 2);
+      double *ws = tmp((size_t)AJ_NBUF + np + sweeps + 2 + 2 * (np + 1));
       if (!ws) return fail(amg_set_error(AMG_ERR_OOM, "amg_dist_async_sps: workspace"));
       // the reference's RandDouble stream: one draw per sweep after the first
       const std::vector<double> dr = rand_double_stream(0, sweeps, 0.0, 1.0);
@@ -695,13 +749,22 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
       if ((st = amg_ctx_partials(c, 65536, &pp)) != AMG_OK) return fail(st);
       part = pp;
       snorm = ws;
-      rnorm = snorm + AJ_NBUF;
-      lnorm = rnorm + (size_t)AJ_NBUF * np;
+      lnorm = snorm + AJ_NBUF;
       draws = lnorm + np;
       gate = reinterpret_cast<int *>(draws + sweeps);
       count = reinterpret_cast<long long *>(draws + sweeps + 1);
-      amgk::vset(s, ws, 0.0, 0, (long long)AJ_NBUF * (1 + np) + np + sweeps + 2);
+      d_soff = reinterpret_cast<long long *>(draws + sweeps + 2);
+      d_roff = d_soff + np + 1;
+      amgk::vset(s, ws, 0.0, 0, (long long)AJ_NBUF + np + sweeps + 2);
       if (sweeps > 0 && (st = h2d(s, draws, dr.data(), (size_t)sweeps * sizeof(double))) != AMG_OK)
+         return fail(st);
+      std::vector<long long> so(M.soff), ro(M.roff);
+      so.resize(np + 1);
+      ro.resize(np + 1);
+      so[np] = M.nsend;
+      ro[np] = ng;
+      if (np > 0 && ((st = h2d(s, d_soff, so.data(), (size_t)(np + 1) * 8)) != AMG_OK ||
+                     (st = h2d(s, d_roff, ro.data(), (size_t)(np + 1) * 8)) != AMG_OK))
          return fail(st);
       // sps_min_prob > 0: alpha = -log(min_prob) / num_sends (DMEM_Setup.cpp:1168-1169)
       if (D->o.sps_min_prob > 0 && np > 0) sps_alpha = -std::log(D->o.sps_min_prob) / (double)np;
@@ -724,11 +787,14 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
    auto apply = [&](int k) -> int {
       const int q = k % AJ_NBUF;
       AMG_HIP(hipStreamWaitEvent(s, arrived[q], 0));
-      AMG_HIP(hipMemcpyAsync(gext + no, rbuf + (size_t)q * std::max(1, ng), (size_t)ng * sizeof(double),
-                             hipMemcpyDeviceToDevice, s));
-      if (sps && np > 0) // the neighbours' norms that came with these deltas
-         AMG_HIP(hipMemcpyAsync(lnorm, rnorm + (size_t)q * np, (size_t)np * sizeof(double),
+      if (sps) { // the deltas, and the neighbours' norms that came with them
+         const long long m = std::max<long long>(ng, np);
+         sps_unpack_k<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(rbuf + (size_t)q * RS, ng, d_roff, np, gext + no,
+                                                                   lnorm);
+      } else {
+         AMG_HIP(hipMemcpyAsync(gext + no, rbuf + (size_t)q * RS, (size_t)ng * sizeof(double),
                                 hipMemcpyDeviceToDevice, s));
+      }
       amgk::spgemv(s, M.A, gext, r, upd, r, 0, n, nullptr); // r -= A_offd g
       return AMG_OK;
    };
@@ -758,29 +824,26 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
       }
       ajac_update_k<<<nb, 256, 0, s>>>(r, wv, eext, x, dacc, n, am, om1, omd, gate);
       if (np > 0) {
-         launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * std::max<long long>(1, M.nsend), (int)M.nsend);
+         if (sps) { // the norm travels with the deltas (data[vec_len + 1], DMEM_Comm.cpp:216-220)
+            const long long m = std::max<long long>(M.nsend, np);
+            sps_pack_k<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(eext, M.d_send_idx, M.nsend, d_soff, np, snorm + q,
+                                                                    sbuf + (size_t)q * SS);
+         } else {
+            launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * SS, (int)M.nsend);
+         }
          AMG_HIP(hipEventRecord(packed[q], s));
          AMG_HIP(hipStreamWaitEvent(cs, packed[q], 0));
          std::vector<void *> sp(np), rp(np);
          std::vector<long long> sb(np), rb(np);
+         const int g = sps ? 1 : 0;
          for (int i = 0; i < np; i++) {
-            sp[i] = sbuf + (size_t)q * std::max<long long>(1, M.nsend) + M.soff[i];
-            sb[i] = M.scnt[i] * 8;
-            rp[i] = rbuf + (size_t)q * std::max(1, ng) + M.roff[i];
-            rb[i] = M.rcnt[i] * 8;
+            sp[i] = sbuf + (size_t)q * SS + M.soff[i] + g * i;
+            sb[i] = (M.scnt[i] + g) * 8;
+            rp[i] = rbuf + (size_t)q * RS + M.roff[i] + g * i;
+            rb[i] = (M.rcnt[i] + g) * 8;
          }
          if ((st = xp_p2p(c, cs, np, M.peers.data(), sp.data(), sb.data(), rp.data(), rb.data())) != AMG_OK)
             break;
-         if (sps) { // the norm travels with the deltas (data[vec_len + 1], DMEM_Comm.cpp:216-220)
-            for (int i = 0; i < np; i++) {
-               sp[i] = snorm + q;
-               sb[i] = 8;
-               rp[i] = rnorm + (size_t)q * np + i;
-               rb[i] = 8;
-            }
-            if ((st = xp_p2p(c, cs, np, M.peers.data(), sp.data(), sb.data(), rp.data(), rb.data())) != AMG_OK)
-               break;
-         }
          AMG_HIP(hipEventRecord(sent[q], cs));
          AMG_HIP(hipEventRecord(arrived[q], cs));
          pending.push_back(k);

@@ -196,6 +196,7 @@ struct amg_dist_hier {
    double *x_acc = nullptr, *d_acc = nullptr;
    amgd::AccelState acc;
    GridState grid;
+   std::vector<double> level_ms; // amg_dist_async_level_ms
    double prof_ms[5] = {0, 0, 0, 0, 0};
    long long prof_n[5] = {0, 0, 0, 0, 0};
 };

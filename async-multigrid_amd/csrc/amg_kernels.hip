@@ -3266,6 +3266,12 @@ void async_gs(hipStream_t s, const amg_mat *A, const double *f, double *u, const
 // broadcast to every lane that depends on it.  The operations and their
 // order are the sequential loop's: bit-identical.  Rows of at most RMAX
 // entries (longer rows: hybrid_jgs_k).
+// rows of older chunks were stored by THIS wave with write-through (sc1,
+// agent-scope relaxed) stores and are re-read with L1-bypassing (sc1) loads:
+// only the stores' completion is needed -- no cache write-back / invalidate
+// (an agent-scope fence costs several microseconds per chunk)
+__device__ __forceinline__ void wait_own_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ double readlane_d(double v, int s)
 {
    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -3374,7 +3380,189 @@ __global__ __launch_bounds__(256) void hybrid_jgs_wave_k(const int *__restrict__
       // a_ii == 0: the row keeps its value (0 after the zero-guess reset)
       if (act && (a != 0.0 || zero)) __hip_atomic_store(u + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // the next chunk's loads of these rows see the stores
-      if (c0 + 64 < nb) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+      if (c0 + 64 < nb) wait_own_stores();
+   }
+}
+
+// Hybrid Jacobi / Gauss-Seidel with C lanes per block and 64 / C blocks per
+// wave (one wave per workgroup): the blocks advance side by side, so every
+// wave instruction of the dependency chain serves 64 / C rows.  A block runs
+// in chunks of C rows; lane sl of a block's lane group owns the chunk's sl-th
+// row in sweep order.  Phase 1 (all lanes, branch-free batches of 8 entries:
+// every column / value load of a batch, then every operand load, in flight
+// together): the row's operands as in hybrid_jgs_wave_k, its prefix up to the
+// first in-chunk dependency, and its tail -- every entry from there on, in CSR
+// order -- as (tag, value): a product, or a coefficient whose operand is the
+// previous row (DPP row shift), an earlier row of this chunk (the group's LDS
+// value row) or the previous chunk's last row (carried in a register).  Tails
+// live in registers indexed by entry (RMAX <= 8) or in LDS.  Phase 2: step
+// s = 0 .. C - 1, lane s of every group adds its tail and divides.  The
+// operations and their order are the reference's sequential loop's:
+// bit-identical.  Rows of older chunks are loaded (agent scope) after this
+// wave's stores have completed.  VI: values through the value index.
+constexpr int JG_NONE = -2, JG_PROD = -1, JG_PREV = -3, JG_CARRY = -4, JG_FAR = -5, JG_PLAIN = -6;
+
+__device__ __forceinline__ double dpp_shr1(double v)
+{
+   // lane l <- lane l - 1 within each row of 16 lanes (row_shr:1)
+   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+   const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, 0x111, 0xf, 0xf, false);
+   const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), 0x111, 0xf, 0xf, false);
+   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+template <int C, int RMAX, bool VI>
+__global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                       const double *__restrict__ val,
+                                                       const unsigned char *__restrict__ vidx,
+                                                       const double *__restrict__ vtab, const double *__restrict__ f,
+                                                       double *u, const double *__restrict__ u_prev,
+                                                       const int *__restrict__ blk, int nblk,
+                                                       const double *__restrict__ ds, double weight, int zero,
+                                                       int reverse)
+{
+   static_assert(C == 8 || C == 16, "lane groups inside DPP rows");
+   constexpr int B = 64 / C;
+   constexpr int KB = 8;              // entries per batch
+   constexpr bool REG = RMAX <= KB;   // tails in registers
+   constexpr int TL = REG ? 1 : RMAX; // LDS tail slots
+   __shared__ double tv[TL][64];
+   __shared__ int tg[TL][64];
+   __shared__ double cv[64]; // the chunk's values (generic in-chunk dependencies)
+   const int lane = (int)threadIdx.x, q = lane / C, sl = lane % C;
+   const int b = (int)blockIdx.x * B + q;
+   const bool has = b < nblk;
+   const int ns = has ? blk[b] : 0, ne = has ? blk[b + 1] : 0, nb = ne - ns;
+   int nmax = nb; // the wave runs the longest block's chunks
+   for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
+   double carry = 0.0;
+   volatile double *cvv = cv;
+   for (int c0 = 0; c0 < nmax; c0 += C) {
+      const bool act = has && c0 + sl < nb;
+      const int i = act ? (reverse ? ne - 1 - (c0 + sl) : ns + c0 + sl) : 0;
+      double res = 0.0, a = 0.0, d = 1.0, old = 0.0;
+      int rs = 0, len = 0, tl = 0;
+      if (act) {
+         rs = rowptr[i];
+         len = rowptr[i + 1] - rs;
+         d = ds ? ds[i] : 0.0;
+         old = zero ? 0.0 : u_prev[i];
+         res = f[i];
+      }
+      double pa[REG ? RMAX : 1];
+      int pt[REG ? RMAX : 1];
+      bool dep = false;
+#pragma unroll
+      for (int k = 0; k < (REG ? RMAX : 1); k++) pt[k] = JG_NONE;
+      for (int kb = 0; kb < RMAX; kb += KB) {
+         if (!__any(kb < len)) break;
+         int jk[KB], tk[KB];
+         double vk[KB], xk[KB];
+#pragma unroll
+         for (int k = 0; k < KB; k++) { // column / value loads (clamped: always in range)
+            const int e = rs + max(0, min(kb + k, len - 1));
+            jk[k] = col[e];
+            vk[k] = VI ? vtab[vidx[e]] : val[e];
+         }
+         if (kb == 0) a = vk[0];
+         bool far = false;
+#pragma unroll
+         for (int k = 0; k < KB; k++) { // operand kinds
+            const int j = jk[k];
+            int t = JG_NONE;
+            if (act && kb + k < len) {
+               if (j >= ns && j < ne) {
+                  const bool done = reverse ? j > i : j < i;
+                  if (!done) {
+                     t = zero ? JG_PROD : JG_PLAIN; // not yet updated: u_prev (0 in the zero sweep)
+                  } else {
+                     const int pos = reverse ? ne - 1 - j : j - ns;
+                     t = pos >= c0 ? (pos - c0 == sl - 1 ? JG_PREV : pos - c0) : pos == c0 - 1 ? JG_CARRY : JG_FAR;
+                  }
+               } else {
+                  t = zero ? JG_NONE : JG_PLAIN; // the zero sweep skips out-of-block columns
+               }
+            }
+            far = far || t == JG_FAR;
+            tk[k] = t;
+         }
+#pragma unroll
+         for (int k = 0; k < KB; k++) { // operand loads (own row when unused)
+            const double xv = u_prev[tk[k] == JG_PLAIN ? jk[k] : i];
+            xk[k] = tk[k] == JG_PLAIN ? xv : 0.0;
+         }
+         if (__any(far)) {
+            wait_own_stores(); // older chunks' stores (this wave's) have reached memory
+#pragma unroll
+            for (int k = 0; k < KB; k++)
+               if (tk[k] == JG_FAR) xk[k] = __hip_atomic_load(u + jk[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+         }
+#pragma unroll
+         for (int k = 0; k < KB; k++) { // CSR order: prefix, then tail
+            int t = tk[k];
+            if (t == JG_NONE) continue;
+            const bool prod = t == JG_PLAIN || t == JG_PROD || t == JG_FAR;
+            if (prod) t = JG_PROD;
+            dep = dep || !prod;
+            const double w = prod ? vk[k] * xk[k] : vk[k];
+            if (!dep) {
+               res = res - w;
+            } else if (REG) {
+               pa[kb + k < (REG ? RMAX : 1) ? kb + k : 0] = w;
+               pt[kb + k < (REG ? RMAX : 1) ? kb + k : 0] = t;
+               tl = 1;
+            } else {
+               tv[tl][lane] = w;
+               tg[tl][lane] = t;
+               tl++;
+            }
+         }
+      }
+      if (!ds) d = a;
+      auto finish = [&](double r) { return (a != 0.0) ? (zero ? weight * r / d : old + weight * r / d) : old; };
+      double v = old;
+      if (act && tl == 0) v = finish(res);
+      double vprev = 0.0;
+      for (int st = 0; st < C; st++) {
+         if (act && sl == st && tl > 0) {
+            double r = res;
+            if (REG) {
+#pragma unroll
+               for (int k = 0; k < (REG ? RMAX : 1); k++) {
+                  const int t = pt[k];
+                  if (t == JG_NONE) continue;
+                  const double cw = cvv[q * C + max(t, 0)];
+                  const double x = t == JG_PREV ? vprev : t == JG_CARRY ? carry : cw;
+                  r = r - (t == JG_PROD ? pa[k] : pa[k] * x);
+               }
+            } else {
+               for (int t0 = 0; t0 < tl; t0 += 4) {
+                  int tt[4];
+                  double ww[4], cw[4];
+#pragma unroll
+                  for (int m = 0; m < 4; m++) {
+                     const int slot = min(t0 + m, TL - 1);
+                     tt[m] = t0 + m < tl ? tg[slot][lane] : JG_NONE;
+                     ww[m] = tv[slot][lane];
+                     cw[m] = cvv[q * C + max(tt[m], 0)];
+                  }
+#pragma unroll
+                  for (int m = 0; m < 4; m++) {
+                     const int t = tt[m];
+                     if (t == JG_NONE) continue;
+                     const double x = t == JG_PREV ? vprev : t == JG_CARRY ? carry : cw[m];
+                     r = r - (t == JG_PROD ? ww[m] : ww[m] * x);
+                  }
+               }
+            }
+            v = finish(r);
+         }
+         if (sl == st) cvv[lane] = v;
+         vprev = dpp_shr1(v);
+      }
+      carry = __shfl(v, q * C + C - 1, 64);
+      // a_ii == 0: the row keeps its value (0 after the zero-guess reset)
+      if (act && (a != 0.0 || zero)) __hip_atomic_store(u + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
    }
 }
 
@@ -3400,7 +3588,24 @@ void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
 {
    if (nblk <= 0) return;
    const int mode = A->ctx->jgs_wave;
-   if (mode && A->maxrow >= 0 && A->maxrow <= 32) {
+   if (mode == 1 && A->maxrow >= 1 && A->maxrow <= 32) {
+      // 8 lanes per block, 8 blocks per wave
+      const int nwg = (nblk + 7) / 8;
+      const bool vi = A->vidx != nullptr;
+#define JGS_GRP(R, V)                                                                                               \
+   hybrid_jgs_grp_k<8, R, V><<<nwg, 64, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u, u_prev, d_blk, \
+                                                nblk, diag_scale, weight, zero, reverse)
+      if (A->maxrow <= 8) {
+         if (vi) JGS_GRP(8, true);
+         else JGS_GRP(8, false);
+      } else {
+         if (vi) JGS_GRP(32, true);
+         else JGS_GRP(32, false);
+      }
+#undef JGS_GRP
+      return;
+   }
+   if (mode == 2 && A->maxrow >= 0 && A->maxrow <= 32) {
       const int nwg = (nblk + 3) / 4;
       if (A->maxrow <= 8)
          hybrid_jgs_wave_k<8><<<nwg, 256, 0, s>>>(A->rowptr, A->col, A->val, f, u, u_prev, d_blk, nblk, diag_scale,

@@ -307,6 +307,13 @@ class DistHier:
         check(lib.amg_dist_async_solve(self.h, _dp(f), _ip(cnt), C.byref(rel)))
         return rel.value, cnt
 
+    def async_level_ms(self):
+        """per level: ms from the last async_solve's start to the level's last correction"""
+        L = self.gen.L if self.gen is not None else 64
+        ms = np.zeros(max(L, 64), dtype=np.float64)
+        check(lib.amg_dist_async_level_ms(self.h, _dp(ms)))
+        return ms[:L]
+
     def async_jacobi(self, f_local, sweeps, l1=False):
         """DMEM_AsyncSmooth (ASYNC_JACOBI / ASYNC_L1_JACOBI) on the fine level: relres."""
         f = np.ascontiguousarray(f_local, dtype=np.float64)

@@ -145,6 +145,9 @@ typedef struct {
    double sps_alpha;             /* exp(-x alpha) / 1/(x alpha) / alpha (RANDOM)   */
    double sps_min_prob;          /* > 0: alpha = -log(min_prob) / num_sends
                                     (DMEM_Setup.cpp:1168-1169)                  */
+   int delay_level;              /* distributed async additive: -1 every level's
+                                    stream takes the delay (DMEM_Add.cpp:106), else
+                                    that level's only (a probe of level coupling) */
 } amg_opts;
 #define AMG_SPS_EXPONENTIAL 0 /* Main.hpp:132-134 */
 #define AMG_SPS_INVERSE 1
@@ -291,10 +294,11 @@ int amg_l1_jacobi(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, 
  * SMEM_Sync_Parfor_HybridJacobiGaussSeidel[T] SMEM_Smooth.cpp:222-363 (diag_scale =
  * A_diag, weight 1) and SMEM_Sync_HybridJacobiGaussSeidel[T] :533-641
  * (diag_scale NULL = a_ii); reverse selects the [T] variants */
-/* hybrid JGS kernel form: 1 (default, env AMG_JGS_WAVE) one wave per block for
- * rows of <= 32 entries -- coalesced operand loads, the in-chunk dependency
- * chain carried lane to lane (v_readlane), bit-identical; 0: one lane walks
- * each block (the reference's sequential loop as is) */
+/* hybrid JGS kernel form (rows of <= 32 entries; env AMG_JGS_WAVE), all
+ * bit-identical: 1 (default) 8 lanes per block, 8 blocks per wave -- each
+ * chunk's rows loaded coalesced, the dependency chain advancing eight blocks
+ * per wave instruction; 2: one wave per block (the chain carried lane to lane
+ * by v_readlane); 0: one lane walks each block (the reference's loop as is) */
 int amg_set_jgs_wave(amg_ctx *ctx, int enable);
 int amg_hybrid_jgs(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, amg_vec *u_prev,
                    const int *blk, int nblk, const amg_vec *diag_scale, double weight, int sweeps,
@@ -555,12 +559,23 @@ int amg_dist_profile_read(amg_dist_hier *D, double *ms, long long *launches, int
 /* asynchronous additive AMG across GPUs (DMEM_Add DMEM_Add.cpp:20-178, AddCycle
  * :180-329, DMEM_AddCorrect_LocalRes :391-458; SMEM_Async_Add_AMG semantics):
  * hierarchy created with solver ASYNC_MULTADD or ASYNC_AFACX.  Every level runs
- * num_cycles corrections on its own HIP stream with its own RCCL communicator
- * (ghost rows per operator, never waiting for other levels), adding into the
- * shared slab of u with fp64 atomics.  u starts at zero; read it with
+ * num_cycles corrections on its own HIP stream, adding into the shared slab of u
+ * with fp64 atomics; the levels' compute overlaps, but their ghost exchanges and
+ * the allgather to the replicated levels all run, in one cycle-major order, on
+ * the rank's single communication stream over one communicator (RCCL requires
+ * the same operation order on every rank, and per-level communicators on
+ * streams sharing hardware queues can deadlock across ranks).  A level's
+ * exchange in cycle c therefore waits for every exchange issued before it, each
+ * waiting for its own level's compute: a slow level holds the others back at
+ * their next exchange (head-of-line coupling; measured by
+ * amg_dist_async_level_ms with delay_level).  u starts at zero; read it with
  * amg_dist_get_u.  *relres = ||f - A u|| / ||f|| after the levels joined. */
 int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int *level_corrections,
                          double *relres);
+/* per level of the last amg_dist_async_solve: milliseconds from the solve's
+ * start to the level's last correction (HIP events; 0 for levels without a
+ * correction group); ms holds L entries */
+int amg_dist_async_level_ms(const amg_dist_hier *D, double *ms);
 /* DMEM_AsyncSmooth (DMEM_Smooth.cpp:16-313) with ASYNC_JACOBI (l1 = 0: u = r ./ (a_ii/omega))
  * or ASYNC_L1_JACOBI (l1 = 1): `sweeps` relaxations of the fine level in residual-update
  * form from x = 0; every relaxation sends its boundary deltas on the communication

@@ -273,7 +273,7 @@ void or_seq_gauss_seidel(const or_csr *A, const double *f, double *u, int sweeps
  * one after another -- one admissible interleaving of the racy reference, and
  * THE result for a single block.  No zero-guess case, no weight. */
 static int g_async_gs_threads = 0;
-void or_set_async_gs_threads(int on) { g_async_gs_threads = on; }
+void or_set_async_gs_threads(int mode) { g_async_gs_threads = mode; }
 
 /* the same on one OpenMP thread per block, every u access a relaxed atomic:
  * the reference's race itself (or_set_async_gs_threads(1)), so repeated
@@ -303,9 +303,42 @@ static void async_gs_threaded(const or_csr *A, const double *f, double *u, const
    }
 }
 
+/* the equal-speed interleaving (or_set_async_gs_threads(2)): every block at
+ * the same row step c, all reading u before any stores of step c -- the
+ * schedule of threads running in lockstep, which an 8-core host cannot
+ * produce with 32 OS threads; also one admissible interleaving of the race */
+static void async_gs_lockstep(const or_csr *A, const double *f, double *u, const int *blk, int nblk, int sweeps,
+                              int reverse)
+{
+   int lmax = 0;
+   for (int b = 0; b < nblk; b++) lmax = blk[b + 1] - blk[b] > lmax ? blk[b + 1] - blk[b] : lmax;
+   double *nv = (double *)malloc(sizeof(double) * (size_t)(nblk > 0 ? nblk : 1));
+   for (int k = 0; k < sweeps; k++)
+      for (int c = 0; c < lmax; c++) {
+         for (int b = 0; b < nblk; b++) {
+            if (c >= blk[b + 1] - blk[b]) continue;
+            const int i = reverse ? blk[b + 1] - 1 - c : blk[b] + c;
+            if (A->data[A->i[i]] == 0.0) continue;
+            double res = f[i];
+            for (int jj = A->i[i]; jj < A->i[i + 1]; jj++) res -= A->data[jj] * u[A->j[jj]];
+            nv[b] = u[i] + res / A->data[A->i[i]];
+         }
+         for (int b = 0; b < nblk; b++) {
+            if (c >= blk[b + 1] - blk[b]) continue;
+            const int i = reverse ? blk[b + 1] - 1 - c : blk[b] + c;
+            if (A->data[A->i[i]] != 0.0) u[i] = nv[b];
+         }
+      }
+   free(nv);
+}
+
 void or_async_gs(const or_csr *A, const double *f, double *u, const int *blk, int nblk, int sweeps,
                  int reverse)
 {
+   if (g_async_gs_threads == 2 && nblk > 1) {
+      async_gs_lockstep(A, f, u, blk, nblk, sweeps, reverse);
+      return;
+   }
    if (g_async_gs_threads && nblk > 1) {
       async_gs_threaded(A, f, u, blk, nblk, sweeps, reverse);
       return;

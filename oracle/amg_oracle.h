@@ -85,9 +85,9 @@ void or_seq_jacobi(const or_csr *A, const double *f, double *u, double *u_prev, 
 void or_seq_l1jacobi(const or_csr *A, const double *f, double *u, double *u_prev, const double *l1,
                      int sweeps, int zero_flag);
 void or_seq_gauss_seidel(const or_csr *A, const double *f, double *u, int sweeps);
-/* 1: or_async_gs runs one OpenMP thread per block on the live u (the reference's
- * race; nondeterministic), 0 (default): the blocks one after another */
-void or_set_async_gs_threads(int on);
+/* async GS interleaving: 0 blocks one after another, 1 one OpenMP thread per
+ * block racing (the reference), 2 all blocks in lockstep (equal speed) */
+void or_set_async_gs_threads(int mode);
 void or_async_gs(const or_csr *A, const double *f, double *u, const int *blk, int nblk, int sweeps,
                  int reverse);
 void or_hybrid_jgs(const or_csr *A, const double *f, double *u, double *u_prev, const int *blk,

