@@ -79,6 +79,10 @@ class Context:
         """Row-pattern-coded CSR on top of the dictionary (default on)."""
         check(lib.amg_set_row_pattern(self.h, int(enable)))
 
+    def set_long_dict(self, enable):
+        """Long-row dictionary form (rows of >= 64 entries, e.g. smoothed restrictions; default on)."""
+        check(lib.amg_set_long_dict(self.h, int(enable)))
+
     def set_pair_pattern(self, enable):
         """Paired-row-pattern CSR on top of the row patterns (default on)."""
         check(lib.amg_set_pair_pattern(self.h, int(enable)))
@@ -145,6 +149,7 @@ class Mat:
         self.value_index = lib.amg_mat_value_index(handle)  # table size, 0 = plain CSR
         self.dict_index = lib.amg_mat_dict_index(handle)    # dictionary size, 0 = not coded
         self.row_pattern = lib.amg_mat_row_pattern(handle)  # distinct row patterns, 0 = not coded
+        self.long_dict = lib.amg_mat_long_dict(handle)  # long-row dictionary size, 0 = not coded
         self.pair_pattern = lib.amg_mat_pair_pattern(handle)  # distinct row-pair patterns, 0 = not coded
         self.pair_anchor16 = lib.amg_mat_pair_anchor16(handle)  # slab-compressed anchors
         self.master_pattern = lib.amg_mat_master_pattern(handle)  # master length J (-J: uniform values), 0 = not coded

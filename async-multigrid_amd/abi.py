@@ -85,6 +85,8 @@ PROTOTYPES = {
     "amg_mat_dict_index": (_i, [_p]),
     "amg_set_row_pattern": (_i, [_p, _i]),
     "amg_mat_row_pattern": (_i, [_p]),
+    "amg_set_long_dict": (_i, [_p, _i]),
+    "amg_mat_long_dict": (_i, [_p]),
     "amg_set_pair_pattern": (_i, [_p, _i]),
     "amg_mat_pair_pattern": (_i, [_p]),
     "amg_set_pair_anchor16": (_i, [_p, _i]),

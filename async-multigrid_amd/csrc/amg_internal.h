@@ -88,6 +88,7 @@ struct amg_ctx {
    int wall_khz = 100000;  // device wall clock (wall_clock64) rate, for injected delays
    int value_index = 1; // build value-indexed CSR for matrices with <= 256 distinct values
    int dict_index = 1;  // build dictionary-coded CSR for stencil-like square operators
+   int long_dict = 1;   // long-row dictionary form (ldidx) for rows of > AMG_DC_MAXROW entries
    int row_pattern = 1; // build row-pattern-coded CSR on top of the dictionary
    int pair_pattern = 1; // paired-row-pattern CSR: 0 off, 1 size-gated for long rows, 2 always
    int master_pattern = 1; // master-pattern form of square pair-coded operators
@@ -134,6 +135,15 @@ struct amg_mat {
    int *danch = nullptr;
    int dc_n = 0;
    int dc_maxrow = 0; // longest row (selects the LDS staging size)
+   // long-row dictionary form (rows of more than AMG_DC_MAXROW entries, the
+   // smoothed restrictions): each row anchored at its largest-magnitude entry's
+   // column, col = ldanch[i] + ldoff[ldidx[k]], a_ik = ldval[ldidx[k]] -- one
+   // byte per entry for csr_long_dc_kernel; nothing else reads it
+   unsigned char *ldidx = nullptr;
+   int *ldoff = nullptr;
+   double *ldval = nullptr;
+   int *ldanch = nullptr;
+   int ldc_n = 0;
    // row-pattern-coded form (dictionary-coded operators with <= 256 distinct
    // rows, none empty): rpat[i] names row i's dictionary sequence in ptab
    // (AMG_RP_STRIDE bytes per pattern: length, then the entries)
@@ -242,6 +252,10 @@ Gemv gemv_mode(double alpha, double beta);
 // sum of y_i^2 to partials[0..nblocks) (fixed order)
 void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, const Gemv &g,
             double *y, int rb, int re, double *partials);
+// r = b - (A x) over [0, n): SMEM_Residual's y = A x; r = b - y (the sum
+// rounded first, then subtracted) in one pass without y where A is
+// dictionary-coded, else the two passes through y (bit-identical either way)
+void residual_fsub(hipStream_t s, const amg_mat *A, const double *x, const double *b, double *y, double *r, int n);
 int tile_blocks(int rb, int re);
 
 // Jacobi sweep out[i] = x[i] + (omega*(f_i - sum a_ij x_j))/a_ii  (a_ii != 0)
@@ -367,10 +381,11 @@ void pp_encode(hipStream_t s, const amg_mat *A, const unsigned char *map, unsign
                unsigned long long *counts);
 
 // dictionary-coded CSR construction (needs the value index)
+// centre: anchor each row at its largest-magnitude entry (the long-row form)
 void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,
-                int *maxlen);
+                int *maxlen, bool centre = false);
 void dc_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
-               unsigned char *didx, int *anch);
+               unsigned char *didx, int *anch, bool centre = false);
 
 // deterministic reductions
 void sumsq_partials(hipStream_t s, const double *x, int n, double *partials, int *nparts);

@@ -1939,6 +1939,128 @@ __global__ __launch_bounds__(256) void mz_prolong_sweep_kernel(
    }
 }
 
+// The same fused sweep with NL lines per workgroup (lines of nx % 512 == 0
+// points; lane t owns the pair (xs + 2t, xs + 2t + 1) of NL consecutive lines
+// y0 .. y0 + NL - 1): the corrected iterate of the workgroup's own lines is
+// formed ONCE per point (plane k + 2, carried through k + 1, k, k - 1 in
+// registers, as csr_mz_kernel's NLN lines), and only the two halo lines
+// y0 - 1, y0 + NL of plane k and the wave-edge points are formed on the side:
+// (NL + 2) / NL prolongations per point instead of 3.  Same terms, same order:
+// bit-identical to geo_prolong_k + csr_mz_kernel.
+template <bool UNI, bool L1, int NL>
+__global__ __launch_bounds__(256) void mz_prolong_sweep_nl_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
+   const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ u, const double *__restrict__ e,
+   const double *__restrict__ f, const double *__restrict__ l1, const double *__restrict__ wg, double omega,
+   int nx, int ny, int nz, int zc, int npb, int xcd, double *__restrict__ uout)
+{
+   __shared__ unsigned long long mtab[256];
+   __shared__ v2d mval[UNI ? 1 : 256 * 7];
+   __shared__ double wl[27];
+   const int tid = (int)threadIdx.x, lane = tid & 63;
+   if (tid < np) mtab[tid] = mmask_g[tid];
+   if (tid < 27) wl[tid] = wg[tid];
+   if (!UNI)
+      for (int w = tid; w < np * 7; w += 256) mval[w] = mval_g[w];
+   const int S = nx, P = nx * ny;
+   const int ncx = nx >> 1, ncy = ny >> 1, ncz = nz >> 1;
+   const int G = (int)gridDim.x;
+   int lg = (int)blockIdx.x;
+   if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
+   const int pblk = lg % npb, chunk = lg / npb;
+   const int nsx = nx / 512;                          // 512-point segments per line
+   const int y0 = (pblk / nsx) * NL, fx = (pblk % nsx) * 512 + 2 * tid;
+   const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
+   __syncthreads();
+   // operands as csr_mz_kernel's element indices (coordinates one step
+   // outside a line / plane carry into the next one; outside [0, N) dropped)
+   auto norm3 = [&](int &x, int &y, int &z) {
+      if (x < 0) x += nx, y--;
+      if (x >= nx) x -= nx, y++;
+      if (y < 0) y += ny, z--;
+      if (y >= ny) y -= ny, z++;
+   };
+   auto uc2 = [&](int p, int yy) -> v2d {
+      int x = fx, y = yy, z = p;
+      norm3(x, y, z);
+      if (z < 0 || z >= nz) return v2d{0.0, 0.0};
+      const unsigned i = (unsigned)z * P + (unsigned)(y * S + x);
+      return geo_prolong_pair(ld2u(u, i), e, wl, x, y, z, ncx, ncy, ncz);
+   };
+   auto edge = [&](int p, int yy) -> double {
+      if (lane != 0 && lane != 63) return 0.0;
+      int x = lane == 0 ? fx - 1 : fx + 2, y = yy, z = p;
+      norm3(x, y, z);
+      if (z < 0 || z >= nz) return 0.0;
+      const unsigned i = (unsigned)z * P + (unsigned)(y * S + x);
+      return geo_prolong_point(ld1u(u, i), e, wl, x, y, z, ncx, ncy, ncz);
+   };
+   v2d xm[NL], xc[NL], xq[NL];
+   double ec[NL], eq[NL];
+#pragma unroll
+   for (int i = 0; i < NL; i++) {
+      xm[i] = uc2(k0 - 1, y0 + i);
+      xc[i] = uc2(k0, y0 + i);
+      ec[i] = edge(k0, y0 + i);
+      xq[i] = uc2(k0 + 1, y0 + i);
+      eq[i] = edge(k0 + 1, y0 + i);
+   }
+   for (int k = k0; k < k1; k++) {
+      // plane k + 2 of the own lines (this chunk's last iteration needs k1)
+      v2d xn[NL];
+      double en[NL];
+      const bool nxt = k + 2 < nz && k + 1 < k1;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+         xn[i] = v2d{0.0, 0.0};
+         en[i] = 0.0;
+         if (nxt) {
+            xn[i] = uc2(k + 2, y0 + i);
+            en[i] = edge(k + 2, y0 + i);
+         }
+      }
+      const v2d ym = uc2(k, y0 - 1), yp = uc2(k, y0 + NL); // halo lines of plane k
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+         const unsigned row = (unsigned)k * P + (unsigned)((y0 + i) * S + fx);
+         const int pid = ppat[row >> 1];
+         const v2d fr = ld2u(f, row);
+         double lft = __shfl_up(xc[i].y, 1, 64);
+         double rgt = __shfl_down(xc[i].x, 1, 64);
+         if (lane == 0) lft = ec[i];
+         if (lane == 63) rgt = ec[i];
+         const unsigned long long mk = mtab[pid];
+         v2d xv[7];
+         xv[0] = xc[i];
+         xv[1] = xm[i];
+         xv[2] = i == 0 ? ym : xc[i == 0 ? 0 : i - 1];
+         xv[3] = v2d{lft, xc[i].x};
+         xv[4] = v2d{xc[i].y, rgt};
+         xv[5] = i == NL - 1 ? yp : xc[i == NL - 1 ? 0 : i + 1];
+         xv[6] = xq[i];
+         const v2d res = mz_acc7<1, UNI>(fr, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
+         v2d o;
+         if (L1) {
+            const v2d l = ld2u(l1, row);
+            o = v2d{xc[i].x + res.x / l.x, xc[i].y + res.y / l.y};
+         } else {
+            const v2d a = UNI ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 7];
+            o = v2d{(a.x != 0.0) ? xc[i].x + omega * res.x / a.x : xc[i].x,
+                    (a.y != 0.0) ? xc[i].y + omega * res.y / a.y : xc[i].y};
+         }
+         *reinterpret_cast<v2du *>(uout + row) = o;
+      }
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+         xm[i] = xc[i];
+         xc[i] = xq[i];
+         ec[i] = eq[i];
+         xq[i] = xn[i];
+         eq[i] = en[i];
+      }
+   }
+}
+
 void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const double *u, const double *ec,
                       const GeoT &g, const double *wdev, const double *l1, double omega, double *uout)
 {
@@ -1947,9 +2069,34 @@ void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const do
       S.off[j] = A->mp_off[j];
       S.val[j] = A->mp_val[j];
    }
-   const int P = A->mz_P, nz = A->nrows / P, zc = mz_chunk(A, nz, P / 512);
-   const int npb = P / 512, nch = (nz + zc - 1) / zc;
+   const int P = A->mz_P, nz = A->nrows / P;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+   // fuse_prolong 1: four lines per workgroup, 3: two, 2: one (mz_prolong_sweep_kernel)
+   const int NL = A->ctx->fuse_prolong == 3 ? 2 : 4;
+   if (A->ctx->fuse_prolong != 2 && g.nx % 512 == 0 && g.ny % NL == 0) {
+      const int npb = P / (512 * NL), zc = mz_chunk(A, nz, npb), nch = (nz + zc - 1) / zc;
+#define AMG_PSN(U, L, N)                                                                                              \
+   mz_prolong_sweep_nl_kernel<U, L, N><<<npb * nch, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, ec, f, l1, wdev, \
+                                                                 omega, g.nx, g.ny, g.nz, zc, npb, A->ctx->mz_xcd, uout)
+#define AMG_PSN2(N)                           \
+   if (A->mp_uni) {                           \
+      if (l1) AMG_PSN(true, true, N);         \
+      else AMG_PSN(true, false, N);           \
+   } else {                                   \
+      if (l1) AMG_PSN(false, true, N);        \
+      else AMG_PSN(false, false, N);          \
+   }
+      if (NL == 2) {
+         AMG_PSN2(2)
+      } else {
+         AMG_PSN2(4)
+      }
+#undef AMG_PSN2
+#undef AMG_PSN
+      return;
+   }
+   const int zc = mz_chunk(A, nz, P / 512);
+   const int npb = P / 512, nch = (nz + zc - 1) / zc;
 #define AMG_PS(U, L) \
    mz_prolong_sweep_kernel<U, L><<<npb * nch, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, ec, f, l1, wdev, \
                                                            omega, g.nx, g.ny, g.nz, zc, npb, A->ctx->mz_xcd, uout)
@@ -2143,6 +2290,62 @@ __global__ __launch_bounds__(TB) void csr_long_kernel(
    }
 }
 
+// Long-row dictionary form (amg_mat::ldidx): one lane per row walks its row
+// in CSR order -- col = anchor + off[d], a = val[d] from one byte per entry
+// (the tables in LDS), eight entries' loads in flight, then their products
+// added in order.  The same products in the same order as csr_long_kernel:
+// bit-identical.  Norm partials per 256-row tile (block_sum_256's order).
+template <int NEG, bool NEED_DIAG, class Epi>
+__global__ __launch_bounds__(256) void csr_ldc_kernel(const int *__restrict__ rowptr,
+                                                      const unsigned char *__restrict__ didx,
+                                                      const int *__restrict__ doff_g,
+                                                      const double *__restrict__ dval_g,
+                                                      const int *__restrict__ anch, int T,
+                                                      const double *__restrict__ x, int rb, int re, Epi epi,
+                                                      double *__restrict__ partials)
+{
+   __shared__ double vtab[256];
+   __shared__ int otab[256];
+   __shared__ double red[4];
+   const int tid = (int)threadIdx.x;
+   if (tid < T) {
+      vtab[tid] = dval_g[tid];
+      otab[tid] = doff_g[tid];
+   }
+   __syncthreads();
+   const int row = rb + (int)blockIdx.x * 256 + tid;
+   double out = 0.0;
+   if (row < re) {
+      const int rs = rowptr[row], rend = rowptr[row + 1];
+      const int an = anch[row];
+      double acc = epi.init(row);
+      const double pf = epi.pf(row);
+      const double dg = NEED_DIAG ? vtab[didx[rs]] : 0.0; // no empty rows in this form
+      for (int k = rs; k < rend; k += 8) {
+         const int m = rend - k;
+         double p[8];
+#pragma unroll
+         for (int j = 0; j < 8; j++) {
+            const int d = didx[k + min(j, m - 1)];
+            p[j] = vtab[d] * x[an + otab[d]];
+         }
+#pragma unroll
+         for (int j = 0; j < 8; j++)
+            if (j < m) {
+               if (NEG)
+                  acc -= p[j];
+               else
+                  acc += p[j];
+            }
+      }
+      out = epi.finish(row, acc, dg, pf);
+   }
+   if (partials) {
+      const double sblk = block_sum_256(out * out, red);
+      if (tid == 0) partials[blockIdx.x] = sblk;
+   }
+}
+
 // long rows: at least 64 entries per row on average
 static inline bool long_rows(const amg_mat *A) { return A->nnz >= 64LL * A->nrows; }
 
@@ -2165,6 +2368,11 @@ template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_long(hipStream_t s, const amg_mat *A, const double *x, int rb, int re, const Epi &e,
                         double *partials = nullptr)
 {
+   if (A->ldidx && A->ctx->long_dict) { // one lane per row over the one-byte entries
+      csr_ldc_kernel<NEG, NEED_DIAG, Epi><<<(re - rb + 255) / 256, 256, 0, s>>>(
+         A->rowptr, A->ldidx, A->ldoff, A->ldval, A->ldanch, A->ldc_n, x, rb, re, e, partials);
+      return;
+   }
    const int n = re - rb;
    if (partials)
       launch_long_cfg<NEG, NEED_DIAG, 256, 256>(s, A, x, rb, re, e, partials);
@@ -2243,6 +2451,29 @@ struct EpiGemv {
    {
       const v2d v = scale ? v2d{alpha * acc.x, alpha * acc.y} : acc;
       st2(y + i, v, nt);
+      return v;
+   }
+};
+
+// r = b - sum (SMEM_Residual's y = A x then r = b - y, y not stored)
+struct EpiFsub {
+   const double *b;
+   double *r;
+   int nt = 0;
+   __device__ __forceinline__ double init(int) const { return 0.0; }
+   __device__ __forceinline__ double pf(int i) const { return b[i]; }
+   __device__ __forceinline__ double finish(int i, double acc, double, double bi) const
+   {
+      const double v = bi - acc;
+      r[i] = v;
+      return v;
+   }
+   __device__ __forceinline__ v2d init2(int) const { return v2d{0.0, 0.0}; }
+   __device__ __forceinline__ v2d pf2(int i) const { return *reinterpret_cast<const v2du *>(b + i); }
+   __device__ __forceinline__ v2d finish2(int i, v2d acc, v2d, v2d bi) const
+   {
+      const v2d v{bi.x - acc.x, bi.y - acc.y};
+      st2(r + i, v, nt);
       return v;
    }
 };
@@ -2478,6 +2709,17 @@ static void launch_bsr3(hipStream_t s, const amg_mat *A, const double *x, int rb
 static inline bool use_bsr3(const amg_mat *A, int rb, int re, const double *partials)
 {
    return A->bsr3 && !partials && rb % 63 == 0 && (re % 63 == 0 || re == A->nrows) && A->nrows % 3 == 0;
+}
+
+void residual_fsub(hipStream_t s, const amg_mat *A, const double *x, const double *b, double *y, double *r, int n)
+{
+   if (n <= 0) return;
+   if (A->didx && !use_bsr3(A, 0, n, nullptr)) {
+      launch_dc_op<0, false>(s, A, x, 0, n, EpiFsub{b, r}, nullptr, tile_blocks(0, n));
+      return;
+   }
+   spgemv(s, A, x, nullptr, gemv_mode(1.0, 0.0), y, 0, n, nullptr);
+   vsub(s, b, y, r, 0, n);
 }
 
 void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, const Gemv &g,
@@ -3425,9 +3667,9 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
    constexpr int B = 64 / C;
    constexpr int KB = 8;              // entries per batch
    constexpr bool REG = RMAX <= KB;   // tails in registers
-   constexpr int TL = REG ? 1 : RMAX; // LDS tail slots
+   constexpr int TL = REG ? 1 : 16;   // LDS tail slots (longer tails: re-read at the step)
    __shared__ double tv[TL][64];
-   __shared__ int tg[TL][64];
+   __shared__ signed char tg[TL][64];
    __shared__ double cv[64]; // the chunk's values (generic in-chunk dependencies)
    const int lane = (int)threadIdx.x, q = lane / C, sl = lane % C;
    const int b = (int)blockIdx.x * B + q;
@@ -3437,18 +3679,41 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
    for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
    double carry = 0.0;
    volatile double *cvv = cv;
+   // the row pointers run one chunk ahead (their latency hides behind a chunk)
+   auto row_of = [&](int c) { return reverse ? ne - 1 - (c + sl) : ns + c + sl; };
+   int rs_n = 0, re_n = 0;
+   if (has && sl < nb) {
+      rs_n = rowptr[row_of(0)];
+      re_n = rowptr[row_of(0) + 1];
+   }
    for (int c0 = 0; c0 < nmax; c0 += C) {
       const bool act = has && c0 + sl < nb;
-      const int i = act ? (reverse ? ne - 1 - (c0 + sl) : ns + c0 + sl) : 0;
+      const int i = act ? row_of(c0) : 0;
       double res = 0.0, a = 0.0, d = 1.0, old = 0.0;
-      int rs = 0, len = 0, tl = 0;
+      const int rs = act ? rs_n : 0, len = act ? re_n - rs_n : 0;
+      int tl = 0;
       if (act) {
-         rs = rowptr[i];
-         len = rowptr[i + 1] - rs;
          d = ds ? ds[i] : 0.0;
          old = zero ? 0.0 : u_prev[i];
          res = f[i];
       }
+      if (has && c0 + C + sl < nb) {
+         rs_n = rowptr[row_of(c0 + C)];
+         re_n = rowptr[row_of(c0 + C) + 1];
+      }
+      // the operand of column j: JG_PLAIN (u_prev), JG_PROD (a ready product:
+      // 0 in the zero sweep), JG_FAR (an older chunk's row, re-read), a
+      // dependency (JG_PREV, JG_CARRY, >= 0: this chunk's row), JG_NONE
+      auto kind = [&](int j) -> int {
+         if (j >= ns && j < ne) {
+            const bool done = reverse ? j > i : j < i;
+            if (!done) return zero ? JG_PROD : JG_PLAIN; // not yet updated: u_prev (0 in the zero sweep)
+            const int pos = reverse ? ne - 1 - j : j - ns;
+            return pos >= c0 ? (pos - c0 == sl - 1 ? JG_PREV : pos - c0) : pos == c0 - 1 ? JG_CARRY : JG_FAR;
+         }
+         return zero ? JG_NONE : JG_PLAIN; // the zero sweep skips out-of-block columns
+      };
+      int kov = 0; // entry where the tail leaves the LDS slots
       double pa[REG ? RMAX : 1];
       int pt[REG ? RMAX : 1];
       bool dep = false;
@@ -3468,21 +3733,7 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
          bool far = false;
 #pragma unroll
          for (int k = 0; k < KB; k++) { // operand kinds
-            const int j = jk[k];
-            int t = JG_NONE;
-            if (act && kb + k < len) {
-               if (j >= ns && j < ne) {
-                  const bool done = reverse ? j > i : j < i;
-                  if (!done) {
-                     t = zero ? JG_PROD : JG_PLAIN; // not yet updated: u_prev (0 in the zero sweep)
-                  } else {
-                     const int pos = reverse ? ne - 1 - j : j - ns;
-                     t = pos >= c0 ? (pos - c0 == sl - 1 ? JG_PREV : pos - c0) : pos == c0 - 1 ? JG_CARRY : JG_FAR;
-                  }
-               } else {
-                  t = zero ? JG_NONE : JG_PLAIN; // the zero sweep skips out-of-block columns
-               }
-            }
+            const int t = (act && kb + k < len) ? kind(jk[k]) : JG_NONE;
             far = far || t == JG_FAR;
             tk[k] = t;
          }
@@ -3512,8 +3763,12 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
                pt[kb + k < (REG ? RMAX : 1) ? kb + k : 0] = t;
                tl = 1;
             } else {
-               tv[tl][lane] = w;
-               tg[tl][lane] = t;
+               if (tl < TL) {
+                  tv[tl][lane] = w;
+                  tg[tl][lane] = (signed char)t;
+               } else if (tl == TL) {
+                  kov = kb + k;
+               }
                tl++;
             }
          }
@@ -3536,13 +3791,14 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
                   r = r - (t == JG_PROD ? pa[k] : pa[k] * x);
                }
             } else {
-               for (int t0 = 0; t0 < tl; t0 += 4) {
+               const int tn = min(tl, TL);
+               for (int t0 = 0; t0 < tn; t0 += 4) {
                   int tt[4];
                   double ww[4], cw[4];
 #pragma unroll
                   for (int m = 0; m < 4; m++) {
                      const int slot = min(t0 + m, TL - 1);
-                     tt[m] = t0 + m < tl ? tg[slot][lane] : JG_NONE;
+                     tt[m] = t0 + m < tn ? (int)tg[slot][lane] : JG_NONE;
                      ww[m] = tv[slot][lane];
                      cw[m] = cvv[q * C + max(tt[m], 0)];
                   }
@@ -3552,6 +3808,23 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
                      if (t == JG_NONE) continue;
                      const double x = t == JG_PREV ? vprev : t == JG_CARRY ? carry : cw[m];
                      r = r - (t == JG_PROD ? ww[m] : ww[m] * x);
+                  }
+               }
+               // the tail past the slots (long rows with an early dependency):
+               // its entries again from memory, in CSR order
+               for (int k = kov; tl > TL && k < len; k++) {
+                  const int j = col[rs + k];
+                  const double vk = VI ? vtab[vidx[rs + k]] : val[rs + k];
+                  const int t = kind(j);
+                  if (t == JG_NONE) continue;
+                  if (t == JG_PLAIN || t == JG_PROD || t == JG_FAR) {
+                     const double x = t == JG_PLAIN  ? u_prev[j]
+                                      : t == JG_FAR ? __hip_atomic_load(u + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                    : 0.0;
+                     r = r - vk * x;
+                  } else {
+                     const double x = t == JG_PREV ? vprev : t == JG_CARRY ? carry : cvv[q * C + t];
+                     r = r - vk * x;
                   }
                }
             }
@@ -4094,16 +4367,36 @@ __device__ __forceinline__ unsigned long long dc_key(int off, unsigned char b)
 
 // anchor of row i: its first column (the diagonal for diag-first square
 // operators, the parent coarse point for interpolation rows)
+// centre (vtab given): the column of the row's first largest-magnitude entry
+__device__ __forceinline__ int dc_anchor(const int *__restrict__ col, const unsigned char *__restrict__ vidx,
+                                         const double *__restrict__ vtab, int rs, int re, int i)
+{
+   if (rs >= re) return i;
+   if (!vtab) return col[rs];
+   int best = rs;
+   double bv = fabs(vtab[vidx[rs]]);
+   for (int k = rs + 1; k < re; k++) {
+      const double a = fabs(vtab[vidx[k]]);
+      if (a > bv) {
+         bv = a;
+         best = k;
+      }
+   }
+   return col[best];
+}
+
 __global__ void dc_collect_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                              const unsigned char *__restrict__ vidx, int n,
-                             unsigned long long *slots, int nslots, int *count, int *maxlen)
+                             unsigned long long *slots, int nslots, int *count, int *maxlen,
+                             const double *__restrict__ vtab)
 {
    unsigned long long last0 = VI_EMPTY, last1 = VI_EMPTY;
-   int ml = 0, offrow = 0;
+   int ml = 0, offrow = 0, mn = 1;
    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
       const int rs = rowptr[i], re = rowptr[i + 1];
       ml = max(ml, re - rs);
-      const int anc = rs < re ? col[rs] : i;
+      if (re == rs) mn = 0;
+      const int anc = dc_anchor(col, vidx, vtab, rs, re, i);
       offrow |= (anc != i);
       for (int k = rs; k < re; k++) {
          const unsigned long long key = dc_key(col[k] - anc, vidx[k]);
@@ -4115,19 +4408,21 @@ __global__ void dc_collect_k(const int *__restrict__ rowptr, const int *__restri
    }
    atomicMax(maxlen, ml);
    if (offrow) atomicOr(maxlen + 1, 1); // some row's anchor is not its own index
+   if (mn == 0) atomicOr(maxlen + 2, 1); // some row is empty
 }
 
 __global__ void dc_encode_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                             const unsigned char *__restrict__ vidx, int n,
                             const unsigned long long *__restrict__ keys, int T,
-                            unsigned char *__restrict__ didx, int *__restrict__ anch)
+                            unsigned char *__restrict__ didx, int *__restrict__ anch,
+                            const double *__restrict__ vtab)
 {
    __shared__ unsigned long long tk[256];
    if (threadIdx.x < 256) tk[threadIdx.x] = threadIdx.x < T ? keys[threadIdx.x] : VI_EMPTY;
    __syncthreads();
    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
       const int rs = rowptr[i], re = rowptr[i + 1];
-      const int anc = rs < re ? col[rs] : i;
+      const int anc = dc_anchor(col, vidx, vtab, rs, re, i);
       if (anch) anch[i] = anc;
       for (int k = rs; k < re; k++) {
          const unsigned long long key = dc_key(col[k] - anc, vidx[k]);
@@ -4355,19 +4650,19 @@ void rp_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, 
 }
 
 void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,
-                int *maxlen)
+                int *maxlen, bool centre)
 {
    if (A->nrows <= 0) return;
    dc_collect_k<<<std::min(8192, (A->nrows + 255) / 256), 256, 0, s>>>(
-      A->rowptr, A->col, A->vidx, A->nrows, slots, nslots, count, maxlen);
+      A->rowptr, A->col, A->vidx, A->nrows, slots, nslots, count, maxlen, centre ? A->vtab : nullptr);
 }
 
 void dc_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
-               unsigned char *didx, int *anch)
+               unsigned char *didx, int *anch, bool centre)
 {
    if (A->nrows <= 0) return;
-   dc_encode_k<<<std::min(8192, (A->nrows + 255) / 256), 256, 0, s>>>(A->rowptr, A->col, A->vidx,
-                                                                        A->nrows, keys, T, didx, anch);
+   dc_encode_k<<<std::min(8192, (A->nrows + 255) / 256), 256, 0, s>>>(
+      A->rowptr, A->col, A->vidx, A->nrows, keys, T, didx, anch, centre ? A->vtab : nullptr);
 }
 
 __global__ void vi_collect_k(const double *__restrict__ val, long long nnz,

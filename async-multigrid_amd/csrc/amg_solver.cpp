@@ -381,7 +381,7 @@ extern "C" int amg_hier_create(amg_ctx *c, int L, amg_mat *const *A, amg_mat *co
          a.r.assign(L, nullptr);
          a.e.assign(L, nullptr);
          for (int l = 0; l <= top; l++) {
-            AMG_TRY(dalloc(H, H->lv[l].n, &a.r[l]));
+            if (l > 0) AMG_TRY(dalloc(H, H->lv[l].n, &a.r[l])); // r[0]: the caller's fine residual
             AMG_TRY(dalloc(H, H->lv[l].n, &a.e[l]));
          }
          const int nk = H->lv[k].n;
@@ -674,26 +674,28 @@ static void add_level_correction(amg_hier *H, hipStream_t s, int k, const double
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    H->lv[k].zero_flag = 1;
    const int coarsest = multadd ? k : k + 1;
-   amgk::vcopy(s, r_fine0, a.r[0], 0, H->lv[0].n);
+   // r[0] = the fine residual (level_vector[k].r[0], SMEM_Sync_AMG.cpp:418-421):
+   // only ever read, so the caller's vector stands in for the copy
+   auto rl = [&](int l) -> const double * { return l == 0 ? r_fine0 : a.r[l]; };
    for (int l = 0; l < coarsest; l++)
       if (l < L - 1)
-         amgk::spgemv(s, H->lv[l].R, a.r[l], nullptr, mv, a.r[l + 1], 0, H->lv[l + 1].n, nullptr);
+         amgk::spgemv(s, H->lv[l].R, rl(l), nullptr, mv, a.r[l + 1], 0, H->lv[l + 1].n, nullptr);
    if (k == L - 1) {
       // hypre_GaussElimSolve writes hypre's U_array, never read back by the
       // reference's cycle: the coarsest correction e[k] keeps its zero value
    } else if (multadd) {
       amgk::vset(s, a.e[k], 0.0, 0, H->lv[k].n);
-      smooth_all_levels(H, s, k, a.r[k], a.e[k], a.u_prev, a.y, a.scratch, o.num_fine_smooth_sweeps, k);
+      smooth_all_levels(H, s, k, rl(k), a.e[k], a.u_prev, a.y, a.scratch, o.num_fine_smooth_sweeps, k);
    } else {
       const int fg = k, cg = k + 1;
       amgk::vset(s, a.u_fine, 0.0, 0, H->lv[fg].n);
       amgk::vset(s, a.u_coarse, 0.0, 0, H->lv[cg].n);
-      smooth_all_levels(H, s, cg, a.r[cg], a.u_coarse, a.u_coarse_prev, a.y, a.scratch,
+      smooth_all_levels(H, s, cg, rl(cg), a.u_coarse, a.u_coarse_prev, a.y, a.scratch,
                         o.num_coarse_smooth_sweeps, k);
       amgk::spgemv(s, H->lv[fg].P, a.u_coarse, nullptr, mv, a.e[fg], 0, H->lv[fg].n, nullptr);
       // SMEM_Residual: y = A e; r_fine = r - y
       amgk::spgemv(s, H->lv[fg].A, a.e[fg], nullptr, mv, a.y, 0, H->lv[fg].n, nullptr);
-      amgk::vsub(s, a.r[fg], a.y, a.r_fine, 0, H->lv[fg].n);
+      amgk::vsub(s, rl(fg), a.y, a.r_fine, 0, H->lv[fg].n);
       smooth_all_levels(H, s, fg, a.r_fine, a.u_fine, a.u_fine_prev, a.y, a.scratch,
                         o.num_fine_smooth_sweeps, k);
       amgk::vcopy(s, a.u_fine, a.e[k], 0, H->lv[k].n);
@@ -767,11 +769,10 @@ static void init_vectors(amg_hier *H)
       v.zero_flag = 0;
    }
    for (auto &a : H->al) {
-      for (size_t l = 0; l < a.r.size(); l++)
-         if (a.r[l]) {
-            amgk::vset(s, a.r[l], 0.0, 0, H->lv[l].n);
-            amgk::vset(s, a.e[l], 0.0, 0, H->lv[l].n);
-         }
+      for (size_t l = 0; l < a.r.size(); l++) {
+         if (a.r[l]) amgk::vset(s, a.r[l], 0.0, 0, H->lv[l].n);
+         if (a.e[l]) amgk::vset(s, a.e[l], 0.0, 0, H->lv[l].n);
+      }
    }
    amgk::vset(s, H->u_outer, 0.0, 0, H->lv[0].n);
    amgk::vset(s, H->y_outer, 0.0, 0, H->lv[0].n);
@@ -1215,9 +1216,8 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
             amgk::atomic_correct(s, v0.u, a.e[0], a.u_priv, n0);
          }
          if (!global_res) {
-            // SMEM_Residual(A0, f, u_k, y, r_k): y = A u_k; r = f - y
-            amgk::spgemv(s, v0.A, a.u_priv, nullptr, mv, a.y, 0, n0, nullptr);
-            amgk::vsub(s, v0.f, a.y, a.y_fine, 0, n0);
+            // SMEM_Residual(A0, f, u_k, y, r_k): y = A u_k; r = f - y (one pass, y unused)
+            amgk::residual_fsub(s, v0.A, a.u_priv, v0.f, a.y, a.y_fine, n0);
          }
       }
       if (global_res) {

@@ -194,6 +194,14 @@ int amg_mat_dict_index(const amg_mat *A);
 int amg_set_row_pattern(amg_ctx *ctx, int enable);
 /* number of distinct row patterns of A (0: not row-pattern-coded) */
 int amg_mat_row_pattern(const amg_mat *A);
+/* long-row dictionary form for matrices registered from now on: 1 (default; env
+ * AMG_LONG_DICT=0 turns it off) = a value-indexed matrix of >= 64 entries per row
+ * (the smoothed restrictions) whose (column - anchor, value) pairs take at most
+ * 256 forms, each row anchored at its largest-magnitude entry, and no empty row:
+ * one byte per entry for the long-row kernel (bit-identical results) */
+int amg_set_long_dict(amg_ctx *ctx, int enable);
+/* dictionary size of A's long-row form (0: not coded) */
+int amg_mat_long_dict(const amg_mat *A);
 /* paired-row-pattern storage (default on; env AMG_PAIR_PATTERN=0 disables),
  * built at registration on top of the row patterns for square operators whose
  * rows hold <= 32 entries: rows 2t and 2t+1 share one byte naming their merged

@@ -50,6 +50,10 @@ def matrices(oracle, amg):
         for lev in (0, 1) if which != amg.AMG_GEN_A else (1, 2):
             nr, nc, rp, cj, cv = g.host_csr(which, lev)
             out[f"{name}{lev}"] = oracle.Csr(nr, nc, rp, cj, cv)
+    # smoothed restriction (R (I - w D^-1 A), ~77 entries per row): the long-row
+    # dictionary form (rows anchored at their largest entry)
+    A0 = oracle.Csr(*g.host_csr(amg.AMG_GEN_A, 0))
+    _, out["Rs0"] = oracle.smooth_transfer(A0, out["P0"], 0.8)
     out["rand_sq"] = random_csr(oracle, 3000, 3000, 9, seed=1, with_zero_diag=True)
     out["rand_nz"] = random_csr(oracle, 2500, 2500, 9, seed=4)
     out["rand_rect"] = random_csr(oracle, 1777, 901, 5, seed=2, diag_first=False)
@@ -99,7 +103,7 @@ def mats(oracle, amg, ctx):
 
 SQUARE = ["lap16", "A1", "A2", "rand_sq", "longrows", "rand_q", "longrows_q", "rand_q257", "lap_hole",
           "dense", "dense_q"]
-ALL = SQUARE + ["lap_rect", "P0", "P1", "R0", "R1", "rand_rect"]
+ALL = SQUARE + ["lap_rect", "P0", "P1", "R0", "R1", "rand_rect", "Rs0"]
 
 
 def _vecs(n, seed):
@@ -299,7 +303,7 @@ def test_matvec(mats, ctx, oracle, amg, name):
     assert_bitwise(y.download(), ref, name)
 
 
-@pytest.mark.parametrize("name", ["lap16", "rand_rect", "longrows", "P0"])
+@pytest.mark.parametrize("name", ["lap16", "rand_rect", "longrows", "P0", "Rs0"])
 @pytest.mark.parametrize("ab", [(1, 0), (-1, 0), (2.5, 0), (1, -1), (-1, 1), (0.5, -0.5),
                                 (1, 1), (-1, -1), (3, 3), (1, 0.3), (-1, 0.7), (1.7, -0.4)])
 def test_spgemv_branches(mats, ctx, oracle, amg, name, ab):
@@ -325,6 +329,35 @@ def test_spgemv_row_range_and_inplace(mats, ctx, oracle, amg):
     du = ctx.vec(u)
     amg.smem.SMEM_SpGEMV(ctx, dA, ctx.vec(x), du, 1.0, 1.0, du, 37, A.nrows - 101)
     assert_bitwise(du.download(), ref)
+
+
+def test_long_dict(mats, ctx, oracle, amg):
+    """Long-row dictionary form: the smoothed restriction (>= 64 entries per
+    row, <= 256 (column - anchor, value) pairs with each row anchored at its
+    largest entry) is coded, random long rows are not; the coded kernel is
+    bit-identical to the value-indexed one and to the oracle."""
+    host, dev = mats
+    assert dev["Rs0"].long_dict > 0 and dev["Rs0"].dict_index == 0
+    for name in ("dense", "dense_q", "longrows", "lap16", "P0"):
+        assert dev[name].long_dict == 0, name
+    A = host["Rs0"]
+    ctx.set_long_dict(0)
+    try:
+        plain = ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val)
+    finally:
+        ctx.set_long_dict(1)
+    assert plain.long_dict == 0 and plain.value_index > 0
+    x, b = _vecs(A.ncols, 17), _vecs(A.nrows, 18)
+    for alpha, beta in ((1, 0), (-1, 1), (0.5, -0.5)):
+        outs = []
+        for M in (dev["Rs0"], plain):
+            y = ctx.vec(A.nrows)
+            amg.smem.SMEM_SpGEMV(ctx, M, ctx.vec(x), ctx.vec(b), alpha, beta, y, 0, A.nrows)
+            outs.append(y.download())
+        ref = oracle.smem_spgemv(A, x, b, alpha, beta, np.zeros(A.nrows))
+        assert_bitwise(outs[0], outs[1], f"long dict vs value index {alpha, beta}")
+        assert_bitwise(outs[0], ref, f"long dict vs oracle {alpha, beta}")
+    plain.free()
 
 
 @pytest.mark.parametrize("name", ["lap16", "A1", "rand_sq"])

@@ -405,15 +405,20 @@ def test_plane_march27_hierarchy(ctx, amg):
     A1.free()
 
 
-@pytest.mark.parametrize("dims,zc,sm,post", [((64, 64, 64), 16, "jacobi", 1), ((512, 8, 6), 4, "l1", 1),
-                                             ((128, 16, 10), 3, "jacobi", 2), ((64, 32, 14), 64, "l1", 2),
-                                             ((256, 12, 8), 2, "jacobi", 1)])
-def test_fused_prolong_sweep(ctx, amg, oracle, dims, zc, sm, post):
+@pytest.mark.parametrize("dims,zc,sm,post,form", [((64, 64, 64), 16, "jacobi", 1, 2), ((512, 8, 6), 4, "l1", 1, 2),
+                                                  ((128, 16, 10), 3, "jacobi", 2, 2), ((64, 32, 14), 64, "l1", 2, 2),
+                                                  ((256, 12, 8), 2, "jacobi", 1, 2),
+                                                  ((512, 8, 6), 4, "l1", 1, 1), ((512, 16, 12), 5, "jacobi", 1, 1),
+                                                  ((512, 12, 10), 3, "l1", 2, 1), ((1024, 8, 6), 2, "jacobi", 1, 1),
+                                                  ((512, 16, 12), 64, "jacobi", 2, 3), ((512, 6, 10), 3, "l1", 1, 3)])
+def test_fused_prolong_sweep(ctx, amg, oracle, dims, zc, sm, post, form):
     """Prolongation + correction fused into the first post-smoothing sweep
-    (mz_prolong_sweep_kernel, SMEM_Sync_AMG.cpp:118-134): iterate and norm
-    history bit-identical to the unfused run (geo_prolong_k + csr_mz_kernel)
-    and the iterate to the oracle after 6 cycles; Jacobi and L1 Jacobi, one
-    and two post sweeps, chunk lengths 2..64, lines of 64..512."""
+    (SMEM_Sync_AMG.cpp:118-134): iterate and norm history bit-identical to the
+    unfused run (geo_prolong_k + csr_mz_kernel) and the iterate to the oracle
+    after 6 cycles; Jacobi and L1 Jacobi, one and two post sweeps, chunk
+    lengths 2..64.  form 2: one line per lane (mz_prolong_sweep_kernel, lines
+    of 64..512); 1 / 3: four / two lines per workgroup, each corrected value
+    formed once (mz_prolong_sweep_nl_kernel, lines of 512 and 1024)."""
     from oracle import pyoracle as po
     g = amg.Gen(*dims, interp=amg.AMG_INTERP_LINEAR)
     host = {w: [po.Csr(*g.host_csr(c, l)) for l in range(cnt)]
@@ -426,7 +431,7 @@ def test_fused_prolong_sweep(ctx, amg, oracle, dims, zc, sm, post):
     ctx.set_plane_march(1, zc, 1)
     try:
         for fp in (1, 0):
-            ctx.set_fuse_prolong(fp)
+            ctx.set_fuse_prolong(form if fp else 0)
             dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v] for k, v in host.items()}
             opts = amg.default_opts(smooth_weight=0.8, num_cycles=6, tol=0.0, reuse_outer_residual=2,
                                     smoother=smoother, num_post_smooth_sweeps=post)

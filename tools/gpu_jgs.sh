@@ -4,7 +4,9 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD
 P=$R/gpurun_out/jgs
 mkdir -p $P
-timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py -k "hybrid or gauss" tests/test_gpu_solve.py tests/test_gpu_async.py tests/test_gpu_configs.py -q --timeout 400 --timeout-method thread > $P/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py -k "hybrid or gauss" -q --timeout 400 --timeout-method thread > $P/pytest_kernels.log 2>&1 || exit $?
+tail -2 $P/pytest_kernels.log
+timeout -k 10 900 python -u -m pytest tests/test_gpu_solve.py tests/test_gpu_async.py tests/test_gpu_configs.py tests/test_gpu_sps.py tests/test_gpu_delay.py -q -s --timeout 400 --timeout-method thread > $P/pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -4 $P/pytest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
