@@ -79,10 +79,6 @@ class Context:
         """Row-pattern-coded CSR on top of the dictionary (default on)."""
         check(lib.amg_set_row_pattern(self.h, int(enable)))
 
-    def set_long_dict(self, enable):
-        """Long-row dictionary form (rows of >= 64 entries, e.g. smoothed restrictions; default on)."""
-        check(lib.amg_set_long_dict(self.h, int(enable)))
-
     def set_pair_pattern(self, enable):
         """Paired-row-pattern CSR on top of the row patterns (default on)."""
         check(lib.amg_set_pair_pattern(self.h, int(enable)))
@@ -107,6 +103,10 @@ class Context:
     def set_bsr3(self, enable):
         """3x3 block form of num_functions = 3 operators for matrices registered from now on (default on)."""
         check(lib.amg_set_bsr3(self.h, int(enable)))
+
+    def set_jgs_small(self, form):
+        """Small-level hybrid JGS form (bit-identical): 2 one batch per row (default), 1 wave per block, 0 as large."""
+        check(lib.amg_set_jgs_small(self.h, int(form)))
 
     def set_jgs_wave(self, enable):
         """Hybrid JGS kernel form, all bit-identical: 1 (default) 8 lanes per block,
@@ -149,7 +149,6 @@ class Mat:
         self.value_index = lib.amg_mat_value_index(handle)  # table size, 0 = plain CSR
         self.dict_index = lib.amg_mat_dict_index(handle)    # dictionary size, 0 = not coded
         self.row_pattern = lib.amg_mat_row_pattern(handle)  # distinct row patterns, 0 = not coded
-        self.long_dict = lib.amg_mat_long_dict(handle)  # long-row dictionary size, 0 = not coded
         self.pair_pattern = lib.amg_mat_pair_pattern(handle)  # distinct row-pair patterns, 0 = not coded
         self.pair_anchor16 = lib.amg_mat_pair_anchor16(handle)  # slab-compressed anchors
         self.master_pattern = lib.amg_mat_master_pattern(handle)  # master length J (-J: uniform values), 0 = not coded

@@ -85,8 +85,6 @@ PROTOTYPES = {
     "amg_mat_dict_index": (_i, [_p]),
     "amg_set_row_pattern": (_i, [_p, _i]),
     "amg_mat_row_pattern": (_i, [_p]),
-    "amg_set_long_dict": (_i, [_p, _i]),
-    "amg_mat_long_dict": (_i, [_p]),
     "amg_set_pair_pattern": (_i, [_p, _i]),
     "amg_mat_pair_pattern": (_i, [_p]),
     "amg_set_pair_anchor16": (_i, [_p, _i]),
@@ -134,6 +132,7 @@ PROTOTYPES = {
     "amg_hier_fused_prolong": (_i, [_p]),
     "amg_set_fuse_prolong": (_i, [_p, _i]),
     "amg_set_jgs_wave": (_i, [_p, _i]),
+    "amg_set_jgs_small": (_i, [_p, _i]),
     "amg_set_march_lines": (_i, [_p, _i]),
     "amg_hier_set_opts": (_i, [_p, C.POINTER(AmgOpts)]),
     "amg_hier_set_blocks": (_i, [_p, _i, _ip, _i]),

@@ -98,8 +98,8 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    }
    if (const char *v = std::getenv("AMG_PLANE_MARCH_XCD")) c->mz_xcd = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
-   if (const char *v = std::getenv("AMG_LONG_DICT")) c->long_dict = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::max(0, std::min(3, std::atoi(v)));
+   if (const char *v = std::getenv("AMG_JGS_SMALL")) c->jgs_small = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_WAVE")) c->jgs_wave = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ_EDGE")) c->mz_edge = std::atoi(v) != 0;
@@ -245,7 +245,7 @@ static int build_dict_index(amg_mat *A)
    AMG_HIP(hipMalloc(&slots, NS * sizeof(unsigned long long) + 64));
    int *count = reinterpret_cast<int *>(slots + NS);
    AMG_HIP(hipMemsetAsync(slots, 0xff, NS * sizeof(unsigned long long), s));
-   AMG_HIP(hipMemsetAsync(count, 0, 4 * sizeof(int), s));
+   AMG_HIP(hipMemsetAsync(count, 0, 3 * sizeof(int), s));
    amgk::dc_collect(s, A, slots, NS, count, count + 1);
    std::vector<unsigned long long> h(NS);
    int cm[3] = {0, 0, 0}; // distinct pairs, longest row, some anchor != row
@@ -298,72 +298,6 @@ static int build_dict_index(amg_mat *A)
    hipFree(slots);
    A->dc_n = T;
    A->dc_maxrow = cm[1];
-   return AMG_OK;
-}
-
-// long-row dictionary form: operators whose rows are too long for CSR-DC
-// (the smoothed restrictions, ~80-125 entries) but whose (col - anchor,
-// value) pairs still fit 256 entries when each row is anchored at its
-// largest-magnitude entry (the coarse point's own fine point); no empty rows.
-// csr_long_dc_kernel then streams one byte per entry instead of five.
-static int build_long_dict(amg_mat *A)
-{
-   amg_ctx *c = A->ctx;
-   hipStream_t s = c->stream;
-   constexpr int NS = 4096;
-   unsigned long long *slots = nullptr;
-   AMG_HIP(hipMalloc(&slots, NS * sizeof(unsigned long long) + 64));
-   int *count = reinterpret_cast<int *>(slots + NS);
-   AMG_HIP(hipMemsetAsync(slots, 0xff, NS * sizeof(unsigned long long), s));
-   AMG_HIP(hipMemsetAsync(count, 0, 4 * sizeof(int), s));
-   amgk::dc_collect(s, A, slots, NS, count, count + 1, true);
-   std::vector<unsigned long long> h(NS);
-   int cm[4] = {0, 0, 0, 0}; // distinct pairs, longest row, some anchor != row, some row empty
-   AMG_HIP(hipMemcpyAsync(h.data(), slots, NS * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-   AMG_HIP(hipMemcpyAsync(cm, count, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
-   AMG_HIP(hipStreamSynchronize(s));
-   if (cm[0] < 1 || cm[0] > 256 || cm[3] != 0) {
-      hipFree(slots);
-      return AMG_OK;
-   }
-   std::vector<unsigned long long> keys;
-   for (auto k : h)
-      if (k != ~0ULL) keys.push_back(k);
-   std::sort(keys.begin(), keys.end());
-   const int T = (int)keys.size();
-   std::vector<double> vt(256, 0.0);
-   AMG_HIP(hipMemcpy(vt.data(), A->vtab, 256 * sizeof(double), hipMemcpyDeviceToHost));
-   std::vector<int> off(256, 0);
-   std::vector<double> dv(256, 0.0);
-   for (int t = 0; t < T; t++) {
-      off[t] = (int)(unsigned int)(keys[t] >> 8);
-      dv[t] = vt[keys[t] & 0xff];
-   }
-   hipError_t e = hipMalloc(&A->ldidx, (size_t)A->nnz + 64);
-   if (e == hipSuccess) e = hipMalloc(&A->ldoff, 256 * sizeof(int));
-   if (e == hipSuccess) e = hipMalloc(&A->ldval, 256 * sizeof(double));
-   if (e == hipSuccess) e = hipMalloc(&A->ldanch, std::max(1, A->nrows) * sizeof(int));
-   if (e != hipSuccess) {
-      hipFree(A->ldidx);
-      hipFree(A->ldoff);
-      hipFree(A->ldval);
-      hipFree(A->ldanch);
-      A->ldidx = nullptr;
-      A->ldoff = nullptr;
-      A->ldval = nullptr;
-      A->ldanch = nullptr;
-      hipFree(slots);
-      (void)hipGetLastError();
-      return AMG_OK;
-   }
-   AMG_HIP(hipMemcpyAsync(slots, keys.data(), T * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
-   AMG_HIP(hipMemcpyAsync(A->ldoff, off.data(), 256 * sizeof(int), hipMemcpyHostToDevice, s));
-   AMG_HIP(hipMemcpyAsync(A->ldval, dv.data(), 256 * sizeof(double), hipMemcpyHostToDevice, s));
-   AMG_HIP(hipMemsetAsync(A->ldidx + A->nnz, 0, 64, s));
-   amgk::dc_encode(s, A, slots, T, A->ldidx, A->ldanch, true);
-   AMG_HIP(hipStreamSynchronize(s));
-   hipFree(slots);
-   A->ldc_n = T;
    return AMG_OK;
 }
 
@@ -792,8 +726,6 @@ int amg_mat_finish(amg_mat *A)
    }
    if (A->ctx->value_index && A->nnz > 0) AMG_TRY(build_value_index(A));
    if (A->ctx->dict_index && A->vidx) AMG_TRY(build_dict_index(A));
-   // long rows (csr_long_kernel's operators): the long-row dictionary form
-   if (A->ctx->long_dict && A->vidx && !A->didx && A->nnz >= 64LL * A->nrows) AMG_TRY(build_long_dict(A));
    if (A->ctx->row_pattern && A->didx) AMG_TRY(build_row_pattern(A));
    const bool pp = A->dc_maxrow <= 8 || A->nrows >= AMG_PP_LONG_MIN_ROWS || A->ctx->pair_pattern == 2;
    // long-row operators below the pair-coding size still try the 27-pt march
@@ -816,18 +748,6 @@ extern "C" int amg_set_row_pattern(amg_ctx *c, int enable)
 extern "C" int amg_mat_row_pattern(const amg_mat *A)
 {
    return A ? A->rp_n : 0;
-}
-
-extern "C" int amg_mat_long_dict(const amg_mat *A)
-{
-   return A && A->ldidx ? A->ldc_n : 0;
-}
-
-extern "C" int amg_set_long_dict(amg_ctx *c, int enable)
-{
-   AMG_ARG(c, "amg_set_long_dict: null context");
-   c->long_dict = enable ? 1 : 0;
-   return AMG_OK;
 }
 
 extern "C" int amg_set_pair_pattern(amg_ctx *c, int enable)
@@ -882,6 +802,13 @@ extern "C" int amg_set_jgs_wave(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_jgs_wave: null context");
    c->jgs_wave = std::max(0, std::min(2, enable));
+   return AMG_OK;
+}
+
+extern "C" int amg_set_jgs_small(amg_ctx *c, int form)
+{
+   AMG_ARG(c, "amg_set_jgs_small: null context");
+   c->jgs_small = std::max(0, std::min(2, form));
    return AMG_OK;
 }
 
@@ -1151,10 +1078,6 @@ extern "C" int amg_mat_free(amg_mat *A)
    hipFree(A->doff);
    hipFree(A->dval);
    hipFree(A->danch);
-   hipFree(A->ldidx);
-   hipFree(A->ldoff);
-   hipFree(A->ldval);
-   hipFree(A->ldanch);
    hipFree(A->rpat);
    hipFree(A->ptab);
    hipFree(A->ppat);

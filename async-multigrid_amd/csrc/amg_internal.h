@@ -88,7 +88,6 @@ struct amg_ctx {
    int wall_khz = 100000;  // device wall clock (wall_clock64) rate, for injected delays
    int value_index = 1; // build value-indexed CSR for matrices with <= 256 distinct values
    int dict_index = 1;  // build dictionary-coded CSR for stencil-like square operators
-   int long_dict = 1;   // long-row dictionary form (ldidx) for rows of > AMG_DC_MAXROW entries
    int row_pattern = 1; // build row-pattern-coded CSR on top of the dictionary
    int pair_pattern = 1; // paired-row-pattern CSR: 0 off, 1 size-gated for long rows, 2 always
    int master_pattern = 1; // master-pattern form of square pair-coded operators
@@ -106,7 +105,8 @@ struct amg_ctx {
    int mz_nt = 0;          // streaming hints on > 512 MB levels: 1 NT stores, 2 NT rhs loads
    int rr_ring = 0;        // wave-edge residuals through a flag-ordered LDS ring (measured slower: off)
    int rr_occ = 0;         // 5: the fused residual + restriction compiled for 5 waves / SIMD
-   int jgs_wave = 1;       // hybrid JGS one wave per block (rows <= 32 entries); 0: one lane per block
+   int jgs_wave = 1;
+   int jgs_small = 2; // small levels' hybrid JGS form (amg_set_jgs_small)       // hybrid JGS one wave per block (rows <= 32 entries); 0: one lane per block
 };
 
 struct amg_mat {
@@ -135,15 +135,6 @@ struct amg_mat {
    int *danch = nullptr;
    int dc_n = 0;
    int dc_maxrow = 0; // longest row (selects the LDS staging size)
-   // long-row dictionary form (rows of more than AMG_DC_MAXROW entries, the
-   // smoothed restrictions): each row anchored at its largest-magnitude entry's
-   // column, col = ldanch[i] + ldoff[ldidx[k]], a_ik = ldval[ldidx[k]] -- one
-   // byte per entry for csr_long_dc_kernel; nothing else reads it
-   unsigned char *ldidx = nullptr;
-   int *ldoff = nullptr;
-   double *ldval = nullptr;
-   int *ldanch = nullptr;
-   int ldc_n = 0;
    // row-pattern-coded form (dictionary-coded operators with <= 256 distinct
    // rows, none empty): rpat[i] names row i's dictionary sequence in ptab
    // (AMG_RP_STRIDE bytes per pattern: length, then the entries)
@@ -381,11 +372,10 @@ void pp_encode(hipStream_t s, const amg_mat *A, const unsigned char *map, unsign
                unsigned long long *counts);
 
 // dictionary-coded CSR construction (needs the value index)
-// centre: anchor each row at its largest-magnitude entry (the long-row form)
 void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,
-                int *maxlen, bool centre = false);
+                int *maxlen);
 void dc_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
-               unsigned char *didx, int *anch, bool centre = false);
+               unsigned char *didx, int *anch);
 
 // deterministic reductions
 void sumsq_partials(hipStream_t s, const double *x, int n, double *partials, int *nparts);

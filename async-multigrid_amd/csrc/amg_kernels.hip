@@ -2290,62 +2290,6 @@ __global__ __launch_bounds__(TB) void csr_long_kernel(
    }
 }
 
-// Long-row dictionary form (amg_mat::ldidx): one lane per row walks its row
-// in CSR order -- col = anchor + off[d], a = val[d] from one byte per entry
-// (the tables in LDS), eight entries' loads in flight, then their products
-// added in order.  The same products in the same order as csr_long_kernel:
-// bit-identical.  Norm partials per 256-row tile (block_sum_256's order).
-template <int NEG, bool NEED_DIAG, class Epi>
-__global__ __launch_bounds__(256) void csr_ldc_kernel(const int *__restrict__ rowptr,
-                                                      const unsigned char *__restrict__ didx,
-                                                      const int *__restrict__ doff_g,
-                                                      const double *__restrict__ dval_g,
-                                                      const int *__restrict__ anch, int T,
-                                                      const double *__restrict__ x, int rb, int re, Epi epi,
-                                                      double *__restrict__ partials)
-{
-   __shared__ double vtab[256];
-   __shared__ int otab[256];
-   __shared__ double red[4];
-   const int tid = (int)threadIdx.x;
-   if (tid < T) {
-      vtab[tid] = dval_g[tid];
-      otab[tid] = doff_g[tid];
-   }
-   __syncthreads();
-   const int row = rb + (int)blockIdx.x * 256 + tid;
-   double out = 0.0;
-   if (row < re) {
-      const int rs = rowptr[row], rend = rowptr[row + 1];
-      const int an = anch[row];
-      double acc = epi.init(row);
-      const double pf = epi.pf(row);
-      const double dg = NEED_DIAG ? vtab[didx[rs]] : 0.0; // no empty rows in this form
-      for (int k = rs; k < rend; k += 8) {
-         const int m = rend - k;
-         double p[8];
-#pragma unroll
-         for (int j = 0; j < 8; j++) {
-            const int d = didx[k + min(j, m - 1)];
-            p[j] = vtab[d] * x[an + otab[d]];
-         }
-#pragma unroll
-         for (int j = 0; j < 8; j++)
-            if (j < m) {
-               if (NEG)
-                  acc -= p[j];
-               else
-                  acc += p[j];
-            }
-      }
-      out = epi.finish(row, acc, dg, pf);
-   }
-   if (partials) {
-      const double sblk = block_sum_256(out * out, red);
-      if (tid == 0) partials[blockIdx.x] = sblk;
-   }
-}
-
 // long rows: at least 64 entries per row on average
 static inline bool long_rows(const amg_mat *A) { return A->nnz >= 64LL * A->nrows; }
 
@@ -2368,11 +2312,6 @@ template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_long(hipStream_t s, const amg_mat *A, const double *x, int rb, int re, const Epi &e,
                         double *partials = nullptr)
 {
-   if (A->ldidx && A->ctx->long_dict) { // one lane per row over the one-byte entries
-      csr_ldc_kernel<NEG, NEED_DIAG, Epi><<<(re - rb + 255) / 256, 256, 0, s>>>(
-         A->rowptr, A->ldidx, A->ldoff, A->ldval, A->ldanch, A->ldc_n, x, rb, re, e, partials);
-      return;
-   }
    const int n = re - rb;
    if (partials)
       launch_long_cfg<NEG, NEED_DIAG, 256, 256>(s, A, x, rb, re, e, partials);
@@ -3653,7 +3592,7 @@ __device__ __forceinline__ double dpp_shr1(double v)
    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-template <int C, int RMAX, bool VI>
+template <int C, int RMAX, bool VI, bool UNR = false>
 __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                        const double *__restrict__ val,
                                                        const unsigned char *__restrict__ vidx,
@@ -3665,9 +3604,12 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
 {
    static_assert(C == 8 || C == 16, "lane groups inside DPP rows");
    constexpr int B = 64 / C;
-   constexpr int KB = 8;              // entries per batch
-   constexpr bool REG = RMAX <= KB;   // tails in registers
-   constexpr int TL = REG ? 1 : 16;   // LDS tail slots (longer tails: re-read at the step)
+   // UNR (small levels, latency-bound): the whole row's loads in one batch and
+   // every tail in LDS (occupancy does not matter there; the re-read of long
+   // tails costs two dependent loads per entry at every step)
+   constexpr int KB = UNR ? RMAX : 8;                // entries per batch
+   constexpr bool REG = RMAX <= 8;                   // tails in registers
+   constexpr int TL = REG ? 1 : UNR ? RMAX - 1 : 16; // LDS tail slots (longer tails: re-read at the step)
    __shared__ double tv[TL][64];
    __shared__ signed char tg[TL][64];
    __shared__ double cv[64]; // the chunk's values (generic in-chunk dependencies)
@@ -3860,7 +3802,23 @@ void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
                 int reverse)
 {
    if (nblk <= 0) return;
-   const int mode = A->ctx->jgs_wave;
+   int mode = A->ctx->jgs_wave;
+   // small levels (fewer workgroups than CUs) are latency-bound: jgs_small 1
+   // runs them one wave per block, 2 with the whole row's loads in one batch
+   const int small_form = A->ctx->jgs_small;
+   const bool small = (nblk + 7) / 8 < 1024 && A->maxrow > 8 && A->maxrow <= 32;
+   if (mode == 1 && small && small_form == 1) mode = 2;
+   if (mode == 1 && small && small_form == 2) {
+      const int nwg = (nblk + 7) / 8;
+      if (A->vidx)
+         hybrid_jgs_grp_k<8, 32, true, true><<<nwg, 64, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u,
+                                                                 u_prev, d_blk, nblk, diag_scale, weight, zero, reverse);
+      else
+         hybrid_jgs_grp_k<8, 32, false, true><<<nwg, 64, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u,
+                                                                  u_prev, d_blk, nblk, diag_scale, weight, zero,
+                                                                  reverse);
+      return;
+   }
    if (mode == 1 && A->maxrow >= 1 && A->maxrow <= 32) {
       // 8 lanes per block, 8 blocks per wave
       const int nwg = (nblk + 7) / 8;
@@ -4367,36 +4325,16 @@ __device__ __forceinline__ unsigned long long dc_key(int off, unsigned char b)
 
 // anchor of row i: its first column (the diagonal for diag-first square
 // operators, the parent coarse point for interpolation rows)
-// centre (vtab given): the column of the row's first largest-magnitude entry
-__device__ __forceinline__ int dc_anchor(const int *__restrict__ col, const unsigned char *__restrict__ vidx,
-                                         const double *__restrict__ vtab, int rs, int re, int i)
-{
-   if (rs >= re) return i;
-   if (!vtab) return col[rs];
-   int best = rs;
-   double bv = fabs(vtab[vidx[rs]]);
-   for (int k = rs + 1; k < re; k++) {
-      const double a = fabs(vtab[vidx[k]]);
-      if (a > bv) {
-         bv = a;
-         best = k;
-      }
-   }
-   return col[best];
-}
-
 __global__ void dc_collect_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                              const unsigned char *__restrict__ vidx, int n,
-                             unsigned long long *slots, int nslots, int *count, int *maxlen,
-                             const double *__restrict__ vtab)
+                             unsigned long long *slots, int nslots, int *count, int *maxlen)
 {
    unsigned long long last0 = VI_EMPTY, last1 = VI_EMPTY;
-   int ml = 0, offrow = 0, mn = 1;
+   int ml = 0, offrow = 0;
    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
       const int rs = rowptr[i], re = rowptr[i + 1];
       ml = max(ml, re - rs);
-      if (re == rs) mn = 0;
-      const int anc = dc_anchor(col, vidx, vtab, rs, re, i);
+      const int anc = rs < re ? col[rs] : i;
       offrow |= (anc != i);
       for (int k = rs; k < re; k++) {
          const unsigned long long key = dc_key(col[k] - anc, vidx[k]);
@@ -4408,21 +4346,19 @@ __global__ void dc_collect_k(const int *__restrict__ rowptr, const int *__restri
    }
    atomicMax(maxlen, ml);
    if (offrow) atomicOr(maxlen + 1, 1); // some row's anchor is not its own index
-   if (mn == 0) atomicOr(maxlen + 2, 1); // some row is empty
 }
 
 __global__ void dc_encode_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                             const unsigned char *__restrict__ vidx, int n,
                             const unsigned long long *__restrict__ keys, int T,
-                            unsigned char *__restrict__ didx, int *__restrict__ anch,
-                            const double *__restrict__ vtab)
+                            unsigned char *__restrict__ didx, int *__restrict__ anch)
 {
    __shared__ unsigned long long tk[256];
    if (threadIdx.x < 256) tk[threadIdx.x] = threadIdx.x < T ? keys[threadIdx.x] : VI_EMPTY;
    __syncthreads();
    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
       const int rs = rowptr[i], re = rowptr[i + 1];
-      const int anc = dc_anchor(col, vidx, vtab, rs, re, i);
+      const int anc = rs < re ? col[rs] : i;
       if (anch) anch[i] = anc;
       for (int k = rs; k < re; k++) {
          const unsigned long long key = dc_key(col[k] - anc, vidx[k]);
@@ -4650,19 +4586,19 @@ void rp_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, 
 }
 
 void dc_collect(hipStream_t s, const amg_mat *A, unsigned long long *slots, int nslots, int *count,
-                int *maxlen, bool centre)
+                int *maxlen)
 {
    if (A->nrows <= 0) return;
    dc_collect_k<<<std::min(8192, (A->nrows + 255) / 256), 256, 0, s>>>(
-      A->rowptr, A->col, A->vidx, A->nrows, slots, nslots, count, maxlen, centre ? A->vtab : nullptr);
+      A->rowptr, A->col, A->vidx, A->nrows, slots, nslots, count, maxlen);
 }
 
 void dc_encode(hipStream_t s, const amg_mat *A, const unsigned long long *keys, int T,
-               unsigned char *didx, int *anch, bool centre)
+               unsigned char *didx, int *anch)
 {
    if (A->nrows <= 0) return;
-   dc_encode_k<<<std::min(8192, (A->nrows + 255) / 256), 256, 0, s>>>(
-      A->rowptr, A->col, A->vidx, A->nrows, keys, T, didx, anch, centre ? A->vtab : nullptr);
+   dc_encode_k<<<std::min(8192, (A->nrows + 255) / 256), 256, 0, s>>>(A->rowptr, A->col, A->vidx,
+                                                                        A->nrows, keys, T, didx, anch);
 }
 
 __global__ void vi_collect_k(const double *__restrict__ val, long long nnz,

@@ -194,14 +194,6 @@ int amg_mat_dict_index(const amg_mat *A);
 int amg_set_row_pattern(amg_ctx *ctx, int enable);
 /* number of distinct row patterns of A (0: not row-pattern-coded) */
 int amg_mat_row_pattern(const amg_mat *A);
-/* long-row dictionary form for matrices registered from now on: 1 (default; env
- * AMG_LONG_DICT=0 turns it off) = a value-indexed matrix of >= 64 entries per row
- * (the smoothed restrictions) whose (column - anchor, value) pairs take at most
- * 256 forms, each row anchored at its largest-magnitude entry, and no empty row:
- * one byte per entry for the long-row kernel (bit-identical results) */
-int amg_set_long_dict(amg_ctx *ctx, int enable);
-/* dictionary size of A's long-row form (0: not coded) */
-int amg_mat_long_dict(const amg_mat *A);
 /* paired-row-pattern storage (default on; env AMG_PAIR_PATTERN=0 disables),
  * built at registration on top of the row patterns for square operators whose
  * rows hold <= 32 entries: rows 2t and 2t+1 share one byte naming their merged
@@ -308,6 +300,10 @@ int amg_l1_jacobi(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, 
  * per wave instruction; 2: one wave per block (the chain carried lane to lane
  * by v_readlane); 0: one lane walks each block (the reference's loop as is) */
 int amg_set_jgs_wave(amg_ctx *ctx, int enable);
+/* form 1's small levels (fewer than 8192 blocks of rows of 9..32 entries; env
+ * AMG_JGS_SMALL), all bit-identical: 2 (default) the whole row's loads in one
+ * batch, 1 one wave per block, 0 as the large levels */
+int amg_set_jgs_small(amg_ctx *ctx, int form);
 int amg_hybrid_jgs(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, amg_vec *u_prev,
                    const int *blk, int nblk, const amg_vec *diag_scale, double weight, int sweeps,
                    int zero_first, int reverse);

@@ -50,8 +50,8 @@ def matrices(oracle, amg):
         for lev in (0, 1) if which != amg.AMG_GEN_A else (1, 2):
             nr, nc, rp, cj, cv = g.host_csr(which, lev)
             out[f"{name}{lev}"] = oracle.Csr(nr, nc, rp, cj, cv)
-    # smoothed restriction (R (I - w D^-1 A), ~77 entries per row): the long-row
-    # dictionary form (rows anchored at their largest entry)
+    # smoothed restriction (R (I - w D^-1 A), ~77 entries per row): the
+    # long-row kernel on the async additive cycle's transfers
     A0 = oracle.Csr(*g.host_csr(amg.AMG_GEN_A, 0))
     _, out["Rs0"] = oracle.smooth_transfer(A0, out["P0"], 0.8)
     out["rand_sq"] = random_csr(oracle, 3000, 3000, 9, seed=1, with_zero_diag=True)
@@ -331,35 +331,6 @@ def test_spgemv_row_range_and_inplace(mats, ctx, oracle, amg):
     assert_bitwise(du.download(), ref)
 
 
-def test_long_dict(mats, ctx, oracle, amg):
-    """Long-row dictionary form: the smoothed restriction (>= 64 entries per
-    row, <= 256 (column - anchor, value) pairs with each row anchored at its
-    largest entry) is coded, random long rows are not; the coded kernel is
-    bit-identical to the value-indexed one and to the oracle."""
-    host, dev = mats
-    assert dev["Rs0"].long_dict > 0 and dev["Rs0"].dict_index == 0
-    for name in ("dense", "dense_q", "longrows", "lap16", "P0"):
-        assert dev[name].long_dict == 0, name
-    A = host["Rs0"]
-    ctx.set_long_dict(0)
-    try:
-        plain = ctx.csr(A.nrows, A.ncols, A.rowptr, A.col, A.val)
-    finally:
-        ctx.set_long_dict(1)
-    assert plain.long_dict == 0 and plain.value_index > 0
-    x, b = _vecs(A.ncols, 17), _vecs(A.nrows, 18)
-    for alpha, beta in ((1, 0), (-1, 1), (0.5, -0.5)):
-        outs = []
-        for M in (dev["Rs0"], plain):
-            y = ctx.vec(A.nrows)
-            amg.smem.SMEM_SpGEMV(ctx, M, ctx.vec(x), ctx.vec(b), alpha, beta, y, 0, A.nrows)
-            outs.append(y.download())
-        ref = oracle.smem_spgemv(A, x, b, alpha, beta, np.zeros(A.nrows))
-        assert_bitwise(outs[0], outs[1], f"long dict vs value index {alpha, beta}")
-        assert_bitwise(outs[0], ref, f"long dict vs oracle {alpha, beta}")
-    plain.free()
-
-
 @pytest.mark.parametrize("name", ["lap16", "A1", "rand_sq"])
 def test_residual_two_pass(mats, ctx, oracle, amg, name):
     host, dev = mats
@@ -430,7 +401,7 @@ def test_l1_jacobi(mats, ctx, oracle, amg, name, zero):
 @pytest.mark.parametrize("name", ["lap16", "A1", "rand_sq", "lap_hole"])
 @pytest.mark.parametrize("T", [1, 4, 8, "perf64", "ragged"])
 @pytest.mark.parametrize("zero", [0, 1])
-@pytest.mark.parametrize("wave", [1, 2, 0])
+@pytest.mark.parametrize("wave", [1, 2, 0, "1s0", "1s1"])
 def test_hybrid_jgs(mats, ctx, oracle, amg, name, T, zero, wave):
     """Hybrid Jacobi/GS is partition dependent: the same blocks must give the
     same bits -- the reference's thread ranges (T) and the device partition --
@@ -438,7 +409,11 @@ def test_hybrid_jgs(mats, ctx, oracle, amg, name, T, zero, wave):
     wave per block (2; the chain carried lane to lane, blocks spanning many
     64-row chunks), one lane per block (0)."""
     host, dev = mats
+    small = 2
+    if isinstance(wave, str):  # form 1 with the small levels' form 0 / 1
+        wave, small = 1, int(wave[2])
     ctx.set_jgs_wave(wave)
+    ctx.set_jgs_small(small)
     A, dA = host[name], dev[name]
     if T == "perf64":
         blk = np.minimum(np.arange(0, A.nrows + 64, 64), A.nrows).astype(np.int32)
@@ -467,6 +442,7 @@ def test_hybrid_jgs(mats, ctx, oracle, amg, name, T, zero, wave):
                                                           blk, reverse)
             assert_bitwise(du.download(), ru, f"{name} T={T} rev={reverse} parfor={parfor} wave={wave}")
     ctx.set_jgs_wave(1)
+    ctx.set_jgs_small(2)
 
 
 def test_gauss_seidel(mats, ctx, oracle, amg):

@@ -13,6 +13,10 @@ echo "pytest rc=$rc"; tail -4 $P/pytest.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 600 python tools/bench_async.py --reps 3 > $P/bench_async.json 2> $P/bench_async.log || exit $?
 tail -2 $P/bench_async.log
+for sm in 0 1; do
+  AMG_JGS_SMALL=$sm timeout -k 10 600 python tools/bench_async.py --reps 2 > $P/bench_async_s$sm.json 2> $P/bench_async_s$sm.log || exit $?
+  echo "small=$sm"; tail -2 $P/bench_async_s$sm.log
+done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace -o run \
    -- python3 $R/tools/bench_async.py --reps 1 --cycles 10 > $P/trace_async.json 2> $P/trace_async.err || exit $?
