@@ -106,7 +106,8 @@ struct amg_ctx {
    int rr_ring = 0;        // wave-edge residuals through a flag-ordered LDS ring (measured slower: off)
    int rr_occ = 0;         // 5: the fused residual + restriction compiled for 5 waves / SIMD
    int jgs_wave = 1;
-   int jgs_small = 2; // small levels' hybrid JGS form (amg_set_jgs_small)       // hybrid JGS one wave per block (rows <= 32 entries); 0: one lane per block
+   int jgs_small = 2; // small levels' hybrid JGS form (amg_set_jgs_small)
+   int mz27_occ = 1;  // waves per SIMD the 27-pt march is compiled for (1: the compiler's choice; env AMG_MZ27_OCC=4)       // hybrid JGS one wave per block (rows <= 32 entries); 0: one lane per block
 };
 
 struct amg_mat {

@@ -102,6 +102,28 @@ def test_elasticity_solve_matches_oracle(amg, oracle, ctx, r, ct):
     M.free()
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("r,cycles", [(5, 3), (6, 2)])
+def test_elasticity_at_size(amg, oracle, ctx, r, cycles):
+    """Config 5's problem at the largest refinements one GPU's setup builds
+    here (r = 5: 0.84 M dofs, 65 M nnz; r = 6: 6.5 M dofs, 514 M nnz; config 5
+    itself is r = 7 over 8 GPUs): the DMEM classical hierarchy (coarsen 9,
+    ext+i, theta 0.5, three functions, Galerkin products on the GPU), the fine
+    operator in 3x3 blocks, the V-cycle iterate bit-identical to the oracle's
+    on the same hierarchy."""
+    n, rp, cj, v, b = amg.classical.elasticity(r)
+    H = amg.classical.ClassicalAMG(n, rp, cj, v, coarsen_type=9, strong_threshold=0.5, num_functions=3, device=0)
+    lv = host_levels(amg, H)
+    del H
+    host = {k: [oracle.Csr(*m) for m in lv_] for k, lv_ in lv.items()}
+    opts = amg.default_opts(smooth_weight=0.6, num_cycles=cycles, tol=0.0)
+    M = ctx.csr(*lv["A"][0])
+    assert M.bsr3 > 0
+    M.free()
+    u, hist = compare_solve(amg, oracle, ctx, host, opts, b)
+    assert np.all(np.diff(hist) < 0)
+
+
 def test_problem_file(amg, oracle, ctx, tmp_path):
     """-problem file (SMEM_Setup.cpp:1645-1653): a binary triplet file holding
     the lower triangle of an anisotropic 7-pt operator, read with symm = 1

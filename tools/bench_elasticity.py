@@ -84,6 +84,10 @@ def main():
                          "frac": spmv_bytes / (ms.value * 1e-3) / 1e9 / HBM_PEAK_GBS},
            "fine_spmv_csr": {"ms": ms_csr.value, "bytes": csr_bytes,
                              "gbs": csr_bytes / (ms_csr.value * 1e-3) / 1e9},
+           "roofline": {"bound": "hbm", "kernel": f"fine SpMV y = A0 x ({fmt})",
+                        "achieved": spmv_bytes / (ms.value * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": spmv_bytes / (ms.value * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                        "alg_bytes_per_launch": spmv_bytes, "avg_launch_ms": ms.value},
            "relres_after": rn / r0, "cycles": a.warmup + a.steps,
            "setup_s": {"generate": t1 - t0, "classical": t2 - t1,
                        "galerkin_on": "gpu" if a.gpu_setup else "host"}}
