@@ -1234,8 +1234,8 @@ struct Val27 {
    double v[27];
 };
 
-template <int NEG, bool NEED_DIAG, class Epi, bool UNI, int OCC = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void csr_mz27_kernel(
+template <int NEG, bool NEED_DIAG, class Epi, bool UNI>
+__global__ __launch_bounds__(256) void csr_mz27_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, int dom, int xlo, int xhi, Val27 Hv, const double *__restrict__ x,
    int P, int S, int nz, int zc, int npb, int xcd, Epi epi, double *__restrict__ partials, int kb, int ke)
@@ -1381,10 +1381,6 @@ static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const 
       csr_mz27_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
          A->ppat, A->mpmask, A->pp_n, mv, S, -1, -1, -1, H, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e,
          partials, kb, ke);
-   else if (A->ctx->mz27_occ == 4)
-      csr_mz27_kernel<NEG, NEED_DIAG, Epi, false, 4><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, A->mz_dom, A->mz_dom >= 0 ? xlo : -1, A->mz_dom >= 0 ? xhi : -1, H,
-         x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
    else
       csr_mz27_kernel<NEG, NEED_DIAG, Epi, false><<<npb * nch, 256, 0, s>>>(
          A->ppat, A->mpmask, A->pp_n, mv, S, A->mz_dom, A->mz_dom >= 0 ? xlo : -1, A->mz_dom >= 0 ? xhi : -1, H,
