@@ -105,9 +105,8 @@ struct amg_ctx {
    int mz_nt = 0;          // streaming hints on > 512 MB levels: 1 NT stores, 2 NT rhs loads
    int rr_ring = 0;        // wave-edge residuals through a flag-ordered LDS ring (measured slower: off)
    int rr_occ = 0;         // 5: the fused residual + restriction compiled for 5 waves / SIMD
-   int jgs_wave = 1;
-   int jgs_small = 2; // small levels' hybrid JGS form (amg_set_jgs_small)
-   int mz27_occ = 1;  // waves per SIMD the 27-pt march is compiled for (1: the compiler's choice; env AMG_MZ27_OCC=4)       // hybrid JGS one wave per block (rows <= 32 entries); 0: one lane per block
+   int jgs_wave = 1;       // hybrid JGS form: 1 8 blocks per wave, 2 one wave per block, 0 one lane per block
+   int jgs_small = 2;      // small levels' hybrid JGS form (amg_set_jgs_small)
 };
 
 struct amg_mat {
