@@ -1066,6 +1066,12 @@ typedef struct {
    int n, count, gen, flag;
 } or_gbar;
 
+/* schedule of the groups (converge LOCAL only): 0 free (the OS's), 1 / 2 the
+ * groups one after another, finest / coarsest first -- the extreme speed
+ * ratios of the race, for the band's ends */
+static int g_async_schedule = 0;
+void or_set_async_schedule(int s) { g_async_schedule = s; }
+
 static int gbar_wait(or_gbar *b, const int *conv)
 {
    int g = __atomic_load_n(&b->gen, __ATOMIC_ACQUIRE);
@@ -1258,6 +1264,11 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
 #define RNG(m, l, s, e) const int s = blk[m][k * L + (l)][g], e = blk[m][k * L + (l)][g + 1]
       int tid_converge = 0;
       const int coarsest = multadd ? k : k + 1;
+      if (g_async_schedule && converge_type == OR_CONVERGE_LOCAL) {
+         const int prev = g_async_schedule == 1 ? k - 1 : k + 1; /* the group that runs before this one */
+         if (prev >= 0 && prev < L)
+            while (__atomic_load_n(&count[prev], __ATOMIC_ACQUIRE) < o->num_cycles) sched_yield();
+      }
       while (1) {
          /* restriction :93-108 */
          for (int l = 0; l < coarsest; l++) {

@@ -201,6 +201,9 @@ double or_dmem_async_jacobi(const or_csr *A, const double *b, double *x, int swe
 #define OR_CONVERGE_GLOBAL 1
 #define OR_READ_SOL 0
 #define OR_READ_RES 1
+/* group schedule of or_async_add (converge LOCAL): 0 free, 1 / 2 one group
+ * after another, finest / coarsest first */
+void or_set_async_schedule(int s);
 int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int async_type, int read_type,
                  int converge_type, int *corrections, double *relres);
 

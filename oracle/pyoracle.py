@@ -77,6 +77,7 @@ def lib():
         L.or_dmem_mult_solve.restype = C.c_int
         L.or_dmem_mult_solve.argtypes = [C.c_void_p, _dp, _dp, _dp, C.c_int, C.c_double, C.c_double]
         L.or_set_async_gs_threads.argtypes = [C.c_int]
+        L.or_set_async_schedule.argtypes = [C.c_int]
         L.or_async_add.restype = C.c_int
         L.or_async_add.argtypes = [C.c_void_p, _dp, _dp, _ip, C.c_int, C.c_int, C.c_int, _ip,
                                    C.POINTER(C.c_double)]

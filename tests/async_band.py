@@ -8,7 +8,9 @@ asynchronous solves must land in [0.5 x min, 2 x max] of that band
 (SURVEY.md Sec.8(d)).  Thread sets: one and two threads per level (T = L and
 2L; every level needs a group); the band is taken over all runs of both and
 the equal-speed schedule: every level correcting from the same state each
-cycle, which is the synchronous additive cycle (MULTADD / AFACX).  How fast
+cycle, which is the synchronous additive cycle (MULTADD / AFACX).  With
+sequential=True (converge LOCAL) also the two extreme speed ratios: the groups
+one after another, finest first and coarsest first.  How fast
 the groups run relative to one another sets where a run lands, and that
 differs between this container's 8 cores, the GPU box's host share and the
 device's level streams; equal speed is the schedule the device's concurrent
@@ -20,7 +22,8 @@ import numpy as np
 from test_gpu_solve import oracle_opts
 
 
-def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blocks=None, lockstep=True):
+def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blocks=None, lockstep=True,
+                      sequential=False):
     """(lo, hi, rels, counts) of `reps` runs per thread set (rels[-1]: the
     synchronous schedule when lockstep); opts: the GPU run's
     amg_opts (solver ASYNC_MULTADD / ASYNC_AFACX, smoother, sweeps, num_cycles,
@@ -38,6 +41,17 @@ def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blo
         for _ in range(reps):
             u, rel, cnt = OH.async_add(f, nt, async_type=at, converge_type=ct, read_type=rt)
             assert np.all(np.isfinite(u))
+            rels.append(rel)
+            counts.append(cnt)
+    if sequential and ct == oracle.OR_CONVERGE_LOCAL:
+        # the extreme speed ratios: the groups one after another, finest /
+        # coarsest first (admissible schedules of the same race)
+        for sched in (1, 2):
+            oracle.lib().or_set_async_schedule(sched)
+            try:
+                u, rel, cnt = OH.async_add(f, [1] * L, async_type=at, converge_type=ct, read_type=rt)
+            finally:
+                oracle.lib().or_set_async_schedule(0)
             rels.append(rel)
             counts.append(cnt)
     if lockstep:

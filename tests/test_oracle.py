@@ -204,3 +204,31 @@ def test_async_add_oracle(oracle, amg):
     rels = [Ha.async_add(f, [2, 1])[1] for _ in range(3)]
     assert max(rels) == min(rels)
     assert abs(rels[0] - h[-1] / h[0]) <= 1e-9 * h[-1] / h[0], (rels, h[-1] / h[0])
+
+
+def test_async_add_sequential_schedules(amg, oracle):
+    """or_set_async_schedule: the groups one after another (finest / coarsest
+    first) -- every level still runs num_cycles corrections and the iterate
+    converges, slower than the free race."""
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, 16, amg.AMG_INTERP_LINEAR)
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs = oracle.smooth_transfer(host["A"][lev], host["P"][lev], 0.8)
+        Ps.append(ps)
+        Rs.append(rs)
+    o = oracle.make_opts(solver=oracle.OR_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=12, tol=0.0)
+    OH = oracle.Hier(host["A"], Ps, Rs, o)
+    f = amg.rhs_rand(0, 16 ** 3)
+    rels = {}
+    for sched in (0, 1, 2):
+        oracle.lib().or_set_async_schedule(sched)
+        try:
+            u, rel, cnt = OH.async_add(f, [1] * L, async_type=oracle.OR_FULL_ASYNC,
+                                       converge_type=oracle.OR_CONVERGE_LOCAL)
+        finally:
+            oracle.lib().or_set_async_schedule(0)
+        assert np.all(np.isfinite(u)) and list(cnt[:L]) == [12] * L
+        rels[sched] = rel
+    assert rels[0] < 1e-2 and rels[1] < 1.0 and rels[2] < 1.0
+    assert rels[0] < rels[1] and rels[0] < rels[2], rels
