@@ -117,9 +117,12 @@ class Context:
         """Prolongation fused into the first post-smoothing sweep of marched geometric levels (default off: VALU-bound, slower)."""
         check(lib.amg_set_fuse_prolong(self.h, int(enable)))
 
-    def set_march_lines(self, lines):
-        """Lines per lane of the 7-pt plane march (1 or 2; bit-identical)."""
+    def set_march_lines(self, lines, gemv=None):
+        """Lines per lane of the 7-pt plane march (1, 2 or 4; bit-identical);
+        gemv: a different count for SpMV / SpGEMV (default: the same)."""
         check(lib.amg_set_march_lines(self.h, int(lines)))
+        if gemv is not None:
+            check(lib.amg_set_march_lines_gemv(self.h, int(gemv)))
 
     def csr(self, nrows, ncols, rowptr, col, val, diag_first=1):
         return Mat.register(self, nrows, ncols, rowptr, col, val, diag_first)

@@ -107,7 +107,9 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_RR_OCC")) c->rr_occ = std::atoi(v);
    if (const char *v = std::getenv("AMG_RR_RING")) c->rr_ring = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ_NT")) c->mz_nt = std::atoi(v) & 3;
-   if (const char *v = std::getenv("AMG_MZ_LINES")) c->mz_lines = std::atoi(v) == 2 ? 2 : 1;
+   if (const char *v = std::getenv("AMG_MZ_LINES")) c->mz_lines = std::atoi(v) == 4 ? 4 : std::atoi(v) == 2 ? 2 : 1;
+   if (const char *v = std::getenv("AMG_MZ_LINES_GEMV"))
+      c->mz_lines_gemv = std::atoi(v) == 4 ? 4 : std::atoi(v) == 2 ? 2 : 1;
    *out = c;
    return AMG_OK;
 }
@@ -821,8 +823,16 @@ extern "C" int amg_set_fuse_prolong(amg_ctx *c, int enable)
 
 extern "C" int amg_set_march_lines(amg_ctx *c, int lines)
 {
-   AMG_ARG(c && (lines == 1 || lines == 2), "amg_set_march_lines: lines must be 1 or 2");
+   AMG_ARG(c && (lines == 1 || lines == 2 || lines == 4), "amg_set_march_lines: lines must be 1, 2 or 4");
    c->mz_lines = lines;
+   c->mz_lines_gemv = lines;
+   return AMG_OK;
+}
+
+extern "C" int amg_set_march_lines_gemv(amg_ctx *c, int lines)
+{
+   AMG_ARG(c && (lines == 1 || lines == 2 || lines == 4), "amg_set_march_lines_gemv: lines must be 1, 2 or 4");
+   c->mz_lines_gemv = lines;
    return AMG_OK;
 }
 

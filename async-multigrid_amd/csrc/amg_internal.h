@@ -101,7 +101,8 @@ struct amg_ctx {
    int bsr3 = 1;           // 3x3 block form of num_functions = 3 operators
    int fuse_prolong = 0;   // prolongation fused into the first post sweep (measured slower: off)
    int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)
-   int mz_lines = 1;       // 7-pt plane march: lines per lane (1 or 2, AMG_MZ_LINES)
+   int mz_lines = 1;       // 7-pt plane march: lines per lane (1, 2 or 4, AMG_MZ_LINES)
+   int mz_lines_gemv = 2;  // the same for SpMV / SpGEMV (AMG_MZ_LINES_GEMV; 2: -8 % on the 512^3 SpMV)
    int mz_nt = 0;          // streaming hints on > 512 MB levels: 1 NT stores, 2 NT rhs loads
    int rr_ring = 0;        // wave-edge residuals through a flag-ordered LDS ring (measured slower: off)
    int rr_occ = 0;         // 5: the fused residual + restriction compiled for 5 waves / SIMD

@@ -17,6 +17,7 @@
 #include "amg_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace amgk {
 
@@ -1146,6 +1147,8 @@ static int mz_chunk(const amg_mat *A, int nz, int npb)
    return zc;
 }
 
+struct EpiGemv; // below
+
 template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Epi &e, double *partials, int kb,
                       int ke)
@@ -1158,11 +1161,17 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
    const int P = A->mz_P, nz = A->nrows / P, Sx = A->mz_S, nk = ke - kb;
    if (nk <= 0) return;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
-   // two lines per lane (ctx->mz_lines) where the plane splits into line pairs
-   if (A->mp_uni && A->ctx->mz_lines == 2 && Sx % 512 == 0 && (P / Sx) % 2 == 0) {
-      const int npb = P / 1024, zc = mz_chunk(A, nk, npb), nch = (nk + zc - 1) / zc;
-      csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 2><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
+   // two or four lines per lane (ctx->mz_lines; SpMV / SpGEMV: ctx->mz_lines_gemv)
+   // where the plane splits into line groups
+   const int lines = std::is_same<Epi, EpiGemv>::value ? A->ctx->mz_lines_gemv : A->ctx->mz_lines;
+   if (A->mp_uni && lines > 1 && Sx % 512 == 0 && (P / Sx) % lines == 0) {
+      const int npb = P / (512 * lines), zc = mz_chunk(A, nk, npb), nch = (nk + zc - 1) / zc;
+      if (lines == 4)
+         csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 4><<<npb * nch, 256, 0, s>>>(
+            A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
+      else
+         csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 2><<<npb * nch, 256, 0, s>>>(
+            A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
       return;
    }
    const int zc = mz_chunk(A, nk, P / 512);

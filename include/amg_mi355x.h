@@ -365,11 +365,14 @@ int amg_set_fuse_transfer(amg_ctx *ctx, int enable);
  * hierarchies created afterwards. */
 int amg_hier_fused_prolong(const amg_hier *H);
 int amg_set_fuse_prolong(amg_ctx *ctx, int enable);
-/* lines per lane of the 7-pt plane march (1 or 2; env AMG_MZ_LINES): with 2 a
- * lane keeps two adjacent lines, their +-S operands from registers (planes whose
- * line length is a multiple of 512 and line count even).  Bit-identical;
- * takes effect on the next launch. */
+/* lines per lane of the 7-pt plane march (1, 2 or 4; env AMG_MZ_LINES for the
+ * sweeps and residuals, AMG_MZ_LINES_GEMV for SpMV / SpGEMV; defaults 1 and 2):
+ * a lane keeps adjacent lines, their +-S operands from registers (planes whose
+ * line length is a multiple of 512 and line count a multiple of the lines).
+ * Bit-identical; takes effect on the next launch; sets both. */
 int amg_set_march_lines(amg_ctx *ctx, int lines);
+/* the SpMV / SpGEMV lines alone */
+int amg_set_march_lines_gemv(amg_ctx *ctx, int lines);
 int amg_hier_set_opts(amg_hier *H, const amg_opts *opts);
 /* override level `level`'s hybrid-JGS block partition (thread.A_ns/A_ne) */
 int amg_hier_set_blocks(amg_hier *H, int level, const int *blk, int nblk);

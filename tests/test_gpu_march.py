@@ -50,12 +50,14 @@ def boxes(oracle):
         "lap64x8x5": oracle.laplace_7pt(64, 8, 5),
         "lap512x2x3": oracle.laplace_7pt(512, 2, 3),
         "lap512x6x5": oracle.laplace_7pt(512, 6, 5),
+        "lap512x8x4": oracle.laplace_7pt(512, 8, 4),
         "neu32x16x7": neumann_7pt(oracle, 32, 16, 7),
     }
 
 
 def test_plane_march_selection(ctx, oracle, boxes):
-    want = {"lap32": 1024, "lap64x8x5": 512, "lap512x2x3": 1024, "lap512x6x5": 3072, "neu32x16x7": 512}
+    want = {"lap32": 1024, "lap64x8x5": 512, "lap512x2x3": 1024, "lap512x6x5": 3072, "lap512x8x4": 4096,
+            "neu32x16x7": 512}
     for name, A in boxes.items():
         M = register(ctx, A)
         assert M.plane_march == want[name], (name, M.plane_march)
@@ -71,9 +73,9 @@ def test_plane_march_selection(ctx, oracle, boxes):
         M.free()
 
 
-@pytest.mark.parametrize("lines", [1, 2])
+@pytest.mark.parametrize("lines", [1, 2, 4])
 @pytest.mark.parametrize("zc,xcd", [(32, 1), (1, 0), (3, 1), (64, 0), (2, 1)])
-@pytest.mark.parametrize("name", ["lap32", "lap64x8x5", "lap512x2x3", "lap512x6x5", "neu32x16x7"])
+@pytest.mark.parametrize("name", ["lap32", "lap64x8x5", "lap512x2x3", "lap512x6x5", "lap512x8x4", "neu32x16x7"])
 def test_plane_march_bitwise(ctx, amg, boxes, name, zc, xcd, lines):
     A = boxes[name]
     ctx.set_plane_march(1, zc, xcd)
@@ -111,7 +113,7 @@ def test_plane_march_bitwise(ctx, amg, boxes, name, zc, xcd, lines):
             M.free()
     finally:
         ctx.set_plane_march(1, -1, 1)
-        ctx.set_march_lines(1)
+        ctx.set_march_lines(1, gemv=2)
 
 
 @pytest.mark.parametrize("zc", [32, 5])
@@ -224,7 +226,7 @@ def test_march_two_lines_solve(ctx, amg, oracle, dims, zc):
         try:
             _, out[lines] = _hier_solve(ctx, amg, host, f, 8, 1, 1, zc=zc)
         finally:
-            ctx.set_march_lines(1)
+            ctx.set_march_lines(1, gemv=2)
     (u2, h2, k2), (u1, h1, k1) = out[2], out[1]
     OH = po.Hier(host["A"], host["P"], host["R"], po.make_opts(smooth_weight=0.8, num_cycles=8))
     u_cpu, hist_cpu, _ = OH.solve(f)
