@@ -68,6 +68,9 @@ CASES = [
     ((64, 64, 64), "linear", 2, 1 << 12, {"reuse_outer_residual": 0}, (True, True)),
     ((64, 64, 64), "linear", 3, 1 << 12, {"num_pre_smooth_sweeps": 2, "num_post_smooth_sweeps": 3},
      (True, True)),
+    # the bench's N = 8 decomposition: 8 ranks (level 3 and below replicated at 64^3)
+    ((64, 64, 64), "linear", 8, 0, {"smooth_weight": 0.8}, (True, True)),
+    ((128, 128, 128), "linear", 8, 1 << 12, {"smooth_weight": 0.8}, (True, True)),
 ]
 
 
@@ -239,6 +242,25 @@ def test_slab_512(amg, ctx):
         assert_bitwise(ud, u1, f"512^3 slab iterate, {nranks} rank(s)")
         np.testing.assert_allclose(hd, h1, rtol=1e-12, atol=0)
         del ud
+    gen.free()
+
+
+@pytest.mark.slow
+def test_slab_512_eight_ranks(amg, ctx):
+    """The N = 8 decomposition of config 4 (64 planes per rank, levels down to
+    2^18 rows distributed) as eight ranks over the host transport on this GPU:
+    bit-identical to one GPU after 3 cycles -- the plan, ghost needs and
+    replicated tail bench.py --gpus 8 runs over RCCL."""
+    n = 512
+    gen = amg.Gen(n)
+    opts = amg.default_opts(num_cycles=3, tol=0.0, smooth_weight=0.8, reuse_outer_residual=2)
+    f = amg.rhs_rand(0, n ** 3)
+    u1, h1 = single_gpu(amg, ctx, gen, opts, f, 3)
+    info = []
+    ud, hd = slab_ranks(amg, gen, opts, f, 3, 8, 1 << 18, info=info)
+    assert info[0][2] == 1, info
+    assert_bitwise(ud, u1, "512^3 slab iterate, 8 ranks")
+    np.testing.assert_allclose(hd, h1, rtol=1e-12, atol=0)
     gen.free()
 
 
