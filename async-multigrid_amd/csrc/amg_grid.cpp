@@ -17,10 +17,25 @@
 // non-blocking transport with MPI point-to-point semantics (amg_nb_transport:
 // isend / irecv / test / wait and a sum over the grid's ranks); the numerics of
 // a grid run on its GPU (or, for protocol tests, a host model).
+//
+// Device-resident messages (amg_devhub, amg_grid_add_create_devhub): the
+// correction accumulators and the in-flight send slots live in device memory,
+// and a receiver's accumulate kernel reads a message straight from the sender's
+// slot (peer-mapped: ranks are threads of one process sharing the device(s)).
+// Completion is by events -- the slot written on the sender's stream, the slot
+// read on the receiver's -- polled by test(); the done flag travels as a host
+// word of the match.  No payload passes through host memory and no copy is
+// made.  The host transport remains the path across processes.
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <map>
 #include <memory>
+#include <mutex>
+#include <thread>
+#include <tuple>
 #include <vector>
 
 #include "amg_dist_internal.h"
@@ -44,6 +59,10 @@ struct Backend {
    virtual int add_e(const double *host, bool to_d) = 0;      // x += e (d += e)
    virtual int residual(double *rr) = 0;                      // r = b - A x; *rr = local r.r
    virtual int get_x(double *host) = 0;
+   // device-resident messages (DistBackend only)
+   virtual double *y_dev() { return nullptr; }
+   virtual int add_e_dev(const double *, bool) { return AMG_ERR_ARG; }
+   virtual hipStream_t dstream() const { return nullptr; }
 };
 
 // GPU: the grid's distributed hierarchy
@@ -136,6 +155,14 @@ struct DistBackend : Backend {
       return AMG_OK;
    }
    int get_x(double *host) override { return amgd::d2h(st(), host, x, (size_t)n0 * 8); }
+   double *y_dev() override { return y; }
+   int add_e_dev(const double *ed, bool to_d) override
+   {
+      amgk::vaxpy(st(), 1.0, ed, x, 0, n0);
+      if (to_d) amgk::vaxpy(st(), 1.0, ed, d, 0, n0);
+      return AMG_OK;
+   }
+   hipStream_t dstream() const override { return st(); }
 };
 
 // host model for protocol tests: A = diag(a); grid k corrects its own share of
@@ -216,12 +243,214 @@ struct CommClass {
    std::vector<std::vector<std::vector<double>>> data_inflight; // [i][j][len + 2]
    std::vector<std::vector<long long>> requests_inflight;
    std::vector<std::vector<int>> inflight_flags;
+   // device-resident messages: accumulators / receive buffers and send slots
+   std::vector<double *> dd;
+   std::vector<std::vector<double *>> dslot;
+   std::vector<std::vector<double>> dflag; // the slots' done flags (host words of the messages)
 };
 
 } // namespace
 
+// ---- device message hub (ranks as threads of one process) -------------------
+// A message is the sender's in-flight slot itself: the receiver's accumulate
+// kernel reads the payload straight from it (no copy), and two events order the
+// slot's life -- `written` (recorded on the sender's stream after the slot is
+// filled) is waited for on the receiver's stream before the read, `consumed`
+// (recorded on the receiver's stream after the read) completes the send, so the
+// slot is refilled only after it was read.  A receive completes at its match.  Posted sends and receives match per (destination,
+// source, tag) in order, as MPI's do; the done flag rides in the match.
+struct amg_devhub {
+   struct Msg {
+      const double *src = nullptr;
+      long long n = 0;
+      double flag = 0.0;
+      hipEvent_t written = nullptr, consumed = nullptr;
+      bool matched = false;
+      ~Msg()
+      {
+         for (hipEvent_t e : {written, consumed})
+            if (e) hipEventDestroy(e);
+      }
+   };
+   using Key = std::tuple<int, int, int>; // (dst, src, tag)
+   struct Grid {
+      int n = 0, arrived = 0, readers = 0;
+      long long gen = 0;
+      std::vector<double> acc, out;
+   };
+   int world = 0;
+   std::vector<int> rank_grid;
+   std::mutex mu;
+   std::condition_variable cv;
+   std::map<Key, std::deque<std::shared_ptr<Msg>>> sends, recvs;
+   std::map<long long, std::shared_ptr<Msg>> sreq, rreq;
+   long long next = 1;
+   std::map<int, Grid> grids;
+
+   static int mark(hipStream_t s, hipEvent_t *e)
+   {
+      AMG_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+      AMG_HIP(hipEventRecord(*e, s));
+      return AMG_OK;
+   }
+   static int ready(hipEvent_t e, bool *ok) // non-blocking completion of e
+   {
+      *ok = false;
+      if (!e) return AMG_OK;
+      const hipError_t r = hipEventQuery(e);
+      if (r == hipErrorNotReady) return AMG_OK;
+      AMG_HIP(r);
+      *ok = true;
+      return AMG_OK;
+   }
+   // post a send of src[0:n) (filled by work already queued on stream s) with
+   // the message's done flag
+   int isend(int me, int peer, int tag, const double *src, long long n, double flag, hipStream_t s,
+             long long *req)
+   {
+      auto m = std::make_shared<Msg>();
+      m->src = src;
+      m->n = n;
+      m->flag = flag;
+      AMG_TRY(mark(s, &m->written));
+      std::lock_guard<std::mutex> lk(mu);
+      auto &q = recvs[Key(peer, me, tag)];
+      if (!q.empty()) {
+         // hand the payload to the receiver's posted request
+         auto r = q.front();
+         q.pop_front();
+         r->src = m->src;
+         r->n = std::min(r->n, n);
+         r->flag = flag;
+         r->written = m->written;
+         m->written = nullptr;
+         r->matched = true;
+         m = r;
+      } else {
+         sends[Key(peer, me, tag)].push_back(m);
+      }
+      *req = next++;
+      sreq[*req] = m;
+      return AMG_OK;
+   }
+   int irecv(int me, int peer, int tag, long long n, long long *req)
+   {
+      std::lock_guard<std::mutex> lk(mu);
+      auto &q = sends[Key(me, peer, tag)];
+      std::shared_ptr<Msg> m;
+      if (!q.empty()) {
+         m = q.front();
+         q.pop_front();
+         m->n = std::min(m->n, n);
+         m->matched = true;
+      } else {
+         m = std::make_shared<Msg>();
+         m->n = n;
+         recvs[Key(me, peer, tag)].push_back(m);
+      }
+      *req = next++;
+      rreq[*req] = m;
+      return AMG_OK;
+   }
+   // MPI_Test of a receive: done once a send has matched it (the sender's
+   // slot write is queued on its stream).  The receiver's stream then waits for
+   // that write (in stream order: the event was recorded before this wait is
+   // queued, so waits never form a cycle) and reads *src until consume()
+   int test_recv(long long req, hipStream_t s, int *done, double *flag, const double **src, long long *n)
+   {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = rreq.find(req);
+      AMG_ARG(it != rreq.end(), "amg_devhub: unknown receive %lld", req);
+      const auto &m = it->second;
+      *done = m->matched;
+      if (m->matched) {
+         AMG_HIP(hipStreamWaitEvent(s, m->written, 0));
+         *flag = m->flag;
+         *src = m->src;
+         *n = m->n;
+      }
+      return AMG_OK;
+   }
+   // the receiver's kernels reading the slot are queued on s: the send completes
+   // when they have run
+   int consume(long long req, hipStream_t s)
+   {
+      hipEvent_t e;
+      AMG_TRY(mark(s, &e));
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = rreq.find(req);
+      AMG_ARG(it != rreq.end(), "amg_devhub: unknown receive %lld", req);
+      it->second->consumed = e;
+      rreq.erase(it);
+      return AMG_OK;
+   }
+   // MPI_Test of a send
+   int test_send(long long req, int *done)
+   {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = sreq.find(req);
+      AMG_ARG(it != sreq.end(), "amg_devhub: unknown send %lld", req);
+      bool ok = false;
+      AMG_TRY(ready(it->second->consumed, &ok));
+      *done = ok;
+      if (ok) sreq.erase(it); // the record (and its events) goes with the last side
+      return AMG_OK;
+   }
+   int wait_send(long long req)
+   {
+      for (;;) {
+         int done = 0;
+         AMG_TRY(test_send(req, &done));
+         if (done) return AMG_OK;
+         std::this_thread::yield();
+      }
+   }
+   // InnerProdFlag over the caller's grid
+   int grid_sum(int me, double *vals, int n)
+   {
+      std::unique_lock<std::mutex> lk(mu);
+      Grid &g = grids[rank_grid[me]];
+      cv.wait(lk, [&] { return g.readers == 0; }); // the previous sum fully read
+      if (g.arrived == 0) g.acc.assign(n, 0.0);
+      for (int i = 0; i < n; i++) g.acc[i] += vals[i];
+      const long long gen = g.gen;
+      if (++g.arrived == g.n) {
+         g.out = g.acc;
+         g.arrived = 0;
+         g.readers = g.n;
+         g.gen++;
+         cv.notify_all();
+      } else {
+         cv.wait(lk, [&] { return g.gen != gen; });
+      }
+      for (int i = 0; i < n; i++) vals[i] = g.out[i];
+      if (--g.readers == 0) cv.notify_all();
+      return AMG_OK;
+   }
+};
+
+extern "C" int amg_devhub_create(int world, const int *rank_grid, amg_devhub **out)
+{
+   AMG_ARG(world >= 1 && rank_grid && out, "amg_devhub_create: bad argument");
+   auto h = std::make_unique<amg_devhub>();
+   h->world = world;
+   h->rank_grid.assign(rank_grid, rank_grid + world);
+   for (int r = 0; r < world; r++) h->grids[rank_grid[r]].n++;
+   *out = h.release();
+   return AMG_OK;
+}
+
+extern "C" int amg_devhub_free(amg_devhub *h)
+{
+   delete h;
+   return AMG_OK;
+}
+
 struct amg_grid_add {
    amg_nb_transport t{};
+   amg_devhub *hub = nullptr; // device-resident messages (else the host transport t)
+   bool dev = false;
+   double *ehd = nullptr, *zd = nullptr; // incoming corrections / zeros (device)
    amg_opts o{};
    int my_grid = 0, world = 1, me = 0, grid_size = 1;
    long long row0 = 0, row1 = 0; // my global rows in my grid's partition
@@ -242,6 +471,27 @@ int xp_err(int st, const char *what)
    return st == 0 ? AMG_OK : amg_set_error(AMG_ERR_ARG, "amg_grid_add: transport %s failed (%d)", what, st);
 }
 
+// the message transport: the device hub or the caller's host transport
+int tp_test(amg_grid_add *G, long long req, int *done)
+{
+   if (G->dev) return G->hub->test_send(req, done);
+   return xp_err(G->t.test(G->t.user, req, done), "test");
+}
+
+int tp_sum(amg_grid_add *G, double *v, int n)
+{
+   if (G->dev) return G->hub->grid_sum(G->me, v, n);
+   return xp_err(G->t.grid_allreduce(G->t.user, v, n), "grid_allreduce");
+}
+
+int tp_irecv(amg_grid_add *G, CommClass &cd, int i)
+{
+   if (G->dev) return G->hub->irecv(G->me, cd.procs[i], GRIDJ_TO_GRIDK_CORRECT_TAG, cd.len[i], &cd.requests[i]);
+   return xp_err(G->t.irecv(G->t.user, cd.procs[i], GRIDJ_TO_GRIDK_CORRECT_TAG, cd.data[i].data(), cd.len[i] + 2,
+                            &cd.requests[i]),
+                 "irecv");
+}
+
 // CheckInFlight (DMEM_Comm.cpp:25-63)
 int check_inflight(amg_grid_add *G, CommClass &cd, int i)
 {
@@ -254,7 +504,7 @@ int check_inflight(amg_grid_add *G, CommClass &cd, int i)
       for (int j = 0; j < cd.max_inflight[i]; j++) {
          if (cd.inflight_flags[i][j] == 1) {
             int flag = 0;
-            AMG_TRY(xp_err(G->t.test(G->t.user, cd.requests_inflight[i][j], &flag), "test"));
+            AMG_TRY(tp_test(G, cd.requests_inflight[i][j], &flag));
             if (flag) {
                cd.inflight_flags[i][j] = 0;
                cd.num_inflight[i]--;
@@ -286,41 +536,63 @@ void set_next_inflight(CommClass &cd, int i)
 }
 
 // SendRecv, asynchronous outside classes (DMEM_Comm.cpp:77-348); v holds the
-// grid's local rows; returns the recv / send flag
+// grid's local rows (device memory in device mode); returns the recv / send flag
 int send_recv(amg_grid_add *G, CommClass &cd, double *v, Op op, int *ret)
 {
    const bool local = G->o.converge_test_type != AMG_GLOBAL;
+   const bool dev = G->dev;
+   const hipStream_t s = dev ? G->be->dstream() : nullptr;
    int return_flag = 0;
    for (int i = 0; i < (int)cd.procs.size(); i++) {
       const int ip = cd.procs[i], vs = cd.start[i], vl = cd.len[i];
       cd.recv_flags[i] = 0;
       if (cd.send) {
          if (cd.done_flags[i] >= 2) continue;
-         if (op == WRITE)
+         if (dev) {
+            // the accumulator of what could not be sent yet, on the grid's stream
+            // (adding the cleanup's zeros is skipped: it changes nothing)
+            if (op == WRITE)
+               amgk::vcopy(s, v + vs, cd.dd[i], 0, vl);
+            else if (v != G->zd)
+               amgk::vaxpy(s, 1.0, v + vs, cd.dd[i], 0, vl);
+         } else if (op == WRITE) {
             std::memcpy(cd.data[i].data(), v + vs, (size_t)vl * 8);
-         else
+         } else {
             for (int j = 0; j < vl; j++) cd.data[i][j] += v[vs + j];
+         }
          AMG_TRY(check_inflight(G, cd, i));
          if (cd.num_inflight[i] >= cd.max_inflight[i]) continue;
          const int nx = cd.next_inflight[i];
-         std::vector<double> &slot = cd.data_inflight[i][nx];
-         std::memcpy(slot.data(), cd.data[i].data(), (size_t)vl * 8);
-         std::fill(cd.data[i].begin(), cd.data[i].begin() + vl, 0.0);
+         double *flw;
+         if (dev) {
+            amgk::vcopy(s, cd.dd[i], cd.dslot[i][nx], 0, vl);
+            amgk::vset(s, cd.dd[i], 0.0, 0, vl);
+            flw = &cd.dflag[i][nx];
+         } else {
+            std::vector<double> &slot = cd.data_inflight[i][nx];
+            std::memcpy(slot.data(), cd.data[i].data(), (size_t)vl * 8);
+            std::fill(cd.data[i].begin(), cd.data[i].begin() + vl, 0.0);
+            flw = &slot[vl];
+         }
          if (G->grid_done_flag == 1) {
-            slot[vl] = 1.0;
+            *flw = 1.0;
             if (local) {
                cd.done_flags[i] = 2;
             } else {
                cd.done_flags[i] = 1;
                if (G->all_done_flag == 1) {
                   cd.done_flags[i] = 2;
-                  slot[vl] = 2.0;
+                  *flw = 2.0;
                }
             }
          }
-         AMG_TRY(xp_err(G->t.isend(G->t.user, ip, GRIDJ_TO_GRIDK_CORRECT_TAG, slot.data(), vl + 2,
-                                   &cd.requests_inflight[i][nx]),
-                        "isend"));
+         if (dev)
+            AMG_TRY(G->hub->isend(G->me, ip, GRIDJ_TO_GRIDK_CORRECT_TAG, cd.dslot[i][nx], vl, *flw, s,
+                                  &cd.requests_inflight[i][nx]));
+         else
+            AMG_TRY(xp_err(G->t.isend(G->t.user, ip, GRIDJ_TO_GRIDK_CORRECT_TAG, cd.data_inflight[i][nx].data(),
+                                      vl + 2, &cd.requests_inflight[i][nx]),
+                           "isend"));
          cd.inflight_flags[i][nx] = 1;
          cd.num_inflight[i]++;
          set_next_inflight(cd, i);
@@ -331,12 +603,24 @@ int send_recv(amg_grid_add *G, CommClass &cd, double *v, Op op, int *ret)
          if (cd.done_flags[i] >= 2) continue;
          while (true) {
             int flag = 0;
-            AMG_TRY(xp_err(G->t.test(G->t.user, cd.requests[i], &flag), "test"));
+            double fl = 0.0;
+            const double *src = nullptr;
+            long long got = 0;
+            if (dev)
+               AMG_TRY(G->hub->test_recv(cd.requests[i], s, &flag, &fl, &src, &got));
+            else
+               AMG_TRY(tp_test(G, cd.requests[i], &flag));
             if (!flag) break;
             cd.message_count[i]++;
             G->messages_recv++;
-            for (int j = 0; j < vl; j++) v[vs + j] += cd.data[i][j];
-            const double fl = cd.data[i][vl];
+            if (dev) {
+               // read the payload from the sender's slot, then release it
+               amgk::vaxpy(s, 1.0, src, v + vs, 0, (int)std::min<long long>(got, vl));
+               AMG_TRY(G->hub->consume(cd.requests[i], s));
+            } else {
+               for (int j = 0; j < vl; j++) v[vs + j] += cd.data[i][j];
+               fl = cd.data[i][vl];
+            }
             if (local) {
                if (fl == 1.0) {
                   cd.done_flags[i] = 2;
@@ -350,9 +634,7 @@ int send_recv(amg_grid_add *G, CommClass &cd, double *v, Op op, int *ret)
                   break;
                }
             }
-            AMG_TRY(xp_err(G->t.irecv(G->t.user, ip, GRIDJ_TO_GRIDK_CORRECT_TAG, cd.data[i].data(), vl + 2,
-                                      &cd.requests[i]),
-                           "irecv"));
+            AMG_TRY(tp_irecv(G, cd, i));
             cd.recv_flags[i] = 1;
             return_flag = 1;
             if (G->o.async_type == AMG_SEMI_ASYNC && G->all_done_flag == 0) break;
@@ -366,12 +648,16 @@ int send_recv(amg_grid_add *G, CommClass &cd, double *v, Op op, int *ret)
 // DMEM_AddCheckComm (DMEM_Add.cpp:460-528)
 int add_check_comm(amg_grid_add *G)
 {
-   std::fill(G->eh.begin(), G->eh.end(), 0.0);
+   const bool to_d = G->o.accel_type != AMG_NO_ACCEL && G->my_grid == G->o.cheby_grid;
    int recv_flag = 0;
-   AMG_TRY(send_recv(G, G->recv, G->eh.data(), ACCUMULATE, &recv_flag));
-   if (recv_flag == 1) {
-      const bool to_d = G->o.accel_type != AMG_NO_ACCEL && G->my_grid == G->o.cheby_grid;
-      AMG_TRY(G->be->add_e(G->eh.data(), to_d));
+   if (G->dev) {
+      amgk::vset(G->be->dstream(), G->ehd, 0.0, 0, G->be->n());
+      AMG_TRY(send_recv(G, G->recv, G->ehd, ACCUMULATE, &recv_flag));
+      if (recv_flag == 1) AMG_TRY(G->be->add_e_dev(G->ehd, to_d));
+   } else {
+      std::fill(G->eh.begin(), G->eh.end(), 0.0);
+      AMG_TRY(send_recv(G, G->recv, G->eh.data(), ACCUMULATE, &recv_flag));
+      if (recv_flag == 1) AMG_TRY(G->be->add_e(G->eh.data(), to_d));
    }
    for (int i = 0; i < (int)G->send.procs.size(); i++) AMG_TRY(check_inflight(G, G->send, i));
    return AMG_OK;
@@ -382,9 +668,15 @@ int add_correct(amg_grid_add *G)
 {
    AMG_TRY(G->be->y_add_u());
    if (G->converge_flag == 1 || G->cycle % std::max(1, G->o.async_comm_save_divisor) == 0) {
-      AMG_TRY(G->be->get_y(G->yh.data()));
       int f;
-      AMG_TRY(send_recv(G, G->send, G->yh.data(), ACCUMULATE, &f));
+      if (G->dev) {
+         double *y = G->be->y_dev();
+         AMG_TRY(send_recv(G, G->send, y, ACCUMULATE, &f));
+         amgk::vset(G->be->dstream(), y, 0.0, 0, G->be->n());
+      } else {
+         AMG_TRY(G->be->get_y(G->yh.data()));
+         AMG_TRY(send_recv(G, G->send, G->yh.data(), ACCUMULATE, &f));
+      }
    }
    AMG_TRY(G->be->x_add_u());
    return add_check_comm(G);
@@ -427,7 +719,7 @@ int add_res_norm(amg_grid_add *G, double rr)
 {
    if (G->o.async_type == AMG_SEMI_ASYNC) return AMG_OK; // :346-358: not computed
    double v[2] = {rr, (double)G->outside_done_flag};
-   AMG_TRY(xp_err(G->t.grid_allreduce(G->t.user, v, 2), "grid_allreduce"));
+   AMG_TRY(tp_sum(G, v, 2));
    G->r_local = std::sqrt(v[0]) / G->r0_norm2;
    if (G->r_local < G->o.tol) G->r_local_converge_flag = 1;
    if ((int)v[1] == G->grid_size) G->all_done_flag = 1;
@@ -443,20 +735,34 @@ int async_end(amg_grid_add *G)
          if (f != 2) return false;
       return true;
    };
-   std::fill(G->eh.begin(), G->eh.end(), 0.0);
-   std::vector<double> zero(G->yh.size(), 0.0);
+   std::vector<double> zero;
+   double *eh = G->ehd, *z = G->zd;
+   if (G->dev) {
+      amgk::vset(G->be->dstream(), G->ehd, 0.0, 0, G->be->n());
+   } else {
+      std::fill(G->eh.begin(), G->eh.end(), 0.0);
+      zero.assign(G->yh.size(), 0.0);
+      eh = G->eh.data();
+      z = zero.data();
+   }
    for (long long spin = 0;; spin++) {
       if (local ? (all2(G->recv) && all2(G->send)) : all2(G->recv)) break;
       int f;
-      AMG_TRY(send_recv(G, G->recv, G->eh.data(), ACCUMULATE, &f));
-      if (local) AMG_TRY(send_recv(G, G->send, zero.data(), ACCUMULATE, &f));
+      AMG_TRY(send_recv(G, G->recv, eh, ACCUMULATE, &f));
+      if (local) AMG_TRY(send_recv(G, G->send, z, ACCUMULATE, &f));
       if (spin > (1LL << 34)) return amg_set_error(AMG_ERR_ARG, "amg_grid_add: cleanup never completed");
    }
-   AMG_TRY(G->be->add_e(G->eh.data(), false));
+   if (G->dev)
+      AMG_TRY(G->be->add_e_dev(G->ehd, false));
+   else
+      AMG_TRY(G->be->add_e(G->eh.data(), false));
    for (int i = 0; i < (int)G->send.procs.size(); i++)
       for (int j = 0; j < G->send.max_inflight[i]; j++)
          if (G->send.inflight_flags[i][j] == 1) {
-            AMG_TRY(xp_err(G->t.wait(G->t.user, G->send.requests_inflight[i][j]), "wait"));
+            if (G->dev)
+               AMG_TRY(G->hub->wait_send(G->send.requests_inflight[i][j]));
+            else
+               AMG_TRY(xp_err(G->t.wait(G->t.user, G->send.requests_inflight[i][j]), "wait"));
             G->send.inflight_flags[i][j] = 0;
          }
    return AMG_OK;
@@ -483,8 +789,10 @@ int build_classes(amg_grid_add *G, const int *rank_grid, const long long *rank_r
       cd->done_flags.assign(np, 0);
       cd->recv_flags.assign(np, 0);
       cd->message_count.assign(np, 0);
+      // host payload buffers (device mode: in device memory, alloc_dev)
+      const auto hl = [&](size_t i) { return G->dev ? (size_t)2 : (size_t)cd->len[i] + 2; };
       cd->data.resize(np);
-      for (size_t i = 0; i < np; i++) cd->data[i].assign(cd->len[i] + 2, 0.0);
+      for (size_t i = 0; i < np; i++) cd->data[i].assign(hl(i), 0.0);
       if (send) {
          const int mi = std::max(1, G->o.max_inflight);
          cd->max_inflight.assign(np, mi);
@@ -493,8 +801,8 @@ int build_classes(amg_grid_add *G, const int *rank_grid, const long long *rank_r
          cd->data_inflight.resize(np);
          cd->requests_inflight.assign(np, std::vector<long long>(mi, 0));
          cd->inflight_flags.assign(np, std::vector<int>(mi, 0));
-         for (size_t i = 0; i < np; i++)
-            cd->data_inflight[i].assign(mi, std::vector<double>(cd->len[i] + 2, 0.0));
+         for (size_t i = 0; i < np; i++) cd->data_inflight[i].assign(mi, std::vector<double>(hl(i), 0.0));
+         cd->dflag.assign(np, std::vector<double>(mi, 0.0));
       } else {
          cd->requests.assign(np, 0);
       }
@@ -514,20 +822,47 @@ void reset_classes(amg_grid_add *G)
       std::fill(cd->next_inflight.begin(), cd->next_inflight.end(), 0);
       for (auto &pool : cd->data_inflight)
          for (auto &v : pool) std::fill(v.begin(), v.end(), 0.0);
+      for (auto &f : cd->dflag) std::fill(f.begin(), f.end(), 0.0);
    }
+   if (G->dev) {
+      // the device accumulators / receive buffers start from zero
+      const hipStream_t s = G->be->dstream();
+      for (CommClass *cd : {&G->send, &G->recv})
+         for (size_t i = 0; i < cd->dd.size(); i++) amgk::vset(s, cd->dd[i], 0.0, 0, cd->len[i]);
+   }
+}
+
+// device-mode buffers, from the grid's hierarchy's pool (freed with it)
+int alloc_dev(amg_grid_add *G, amg_dist_hier *D)
+{
+   const int n = std::max(1, G->be->n());
+   AMG_TRY(amgd::dvec(D, n, &G->ehd));
+   AMG_TRY(amgd::dvec(D, n, &G->zd));
+   amgk::vset(G->be->dstream(), G->zd, 0.0, 0, n);
+   // send side only: the receiver reads the sender's slots
+   CommClass &cd = G->send;
+   const size_t np = cd.procs.size();
+   cd.dd.assign(np, nullptr);
+   cd.dslot.assign(np, {});
+   for (size_t i = 0; i < np; i++) {
+      AMG_TRY(amgd::dvec(D, std::max(1, cd.len[i]), &cd.dd[i]));
+      cd.dslot[i].assign(cd.max_inflight[i], nullptr);
+      for (auto &p : cd.dslot[i]) AMG_TRY(amgd::dvec(D, std::max(1, cd.len[i]), &p));
+   }
+   return AMG_OK;
 }
 
 int create_common(amg_grid_add *G, int my_grid, int world, int me, const int *rank_grid,
                   const long long *rank_rows, const amg_nb_transport *t)
 {
-   AMG_ARG(t && t->isend && t->irecv && t->test && t->wait && t->grid_allreduce,
+   AMG_ARG(G->dev || (t && t->isend && t->irecv && t->test && t->wait && t->grid_allreduce),
            "amg_grid_add: incomplete transport");
    AMG_ARG(rank_grid && rank_rows && world >= 1 && me >= 0 && me < world && rank_grid[me] == my_grid,
            "amg_grid_add: bad rank layout");
    AMG_ARG(!(G->o.async_type == AMG_SEMI_ASYNC && G->o.converge_test_type == AMG_GLOBAL),
            "amg_grid_add: SEMI_ASYNC with converge_test GLOBAL never terminates in the reference "
            "(AddResNorm computes no flags for SEMI_ASYNC, DMEM_Add.cpp:346-358)");
-   G->t = *t;
+   if (t) G->t = *t;
    G->my_grid = my_grid;
    G->world = world;
    G->me = me;
@@ -594,6 +929,31 @@ extern "C" int amg_grid_add_create(amg_dist_hier *D, int my_grid, int world_nran
    return AMG_OK;
 }
 
+// the same, with device-resident correction messages over an in-process hub
+extern "C" int amg_grid_add_create_devhub(amg_dist_hier *D, int my_grid, int world_nranks, int world_rank,
+                                          const int *rank_grid, const long long *rank_rows, amg_devhub *hub,
+                                          amg_grid_add **out)
+{
+   AMG_ARG(D && hub && out, "amg_grid_add_create_devhub: null argument");
+   AMG_ARG(D->o.solver == AMG_ASYNC_MULTADD, "amg_grid_add_create_devhub: ASYNC_MULTADD hierarchies only");
+   AMG_ARG(world_nranks == hub->world && rank_grid && world_rank >= 0 && world_rank < world_nranks,
+           "amg_grid_add_create_devhub: rank layout does not match the hub's %d ranks", hub->world);
+   for (int p = 0; p < world_nranks; p++)
+      AMG_ARG(rank_grid[p] == hub->rank_grid[p], "amg_grid_add_create_devhub: rank %d's grid differs from the hub's",
+              p);
+   auto G = std::make_unique<amg_grid_add>();
+   G->o = D->o;
+   G->hub = hub;
+   G->dev = true;
+   auto be = std::make_unique<DistBackend>(D);
+   AMG_TRY(be->init(my_grid));
+   G->be = std::move(be);
+   AMG_TRY(create_common(G.get(), my_grid, world_nranks, world_rank, rank_grid, rank_rows, nullptr));
+   AMG_TRY(alloc_dev(G.get(), D));
+   *out = G.release();
+   return AMG_OK;
+}
+
 extern "C" int amg_grid_add_create_host(int nrows, const double *diag, double weight, const amg_opts *opts,
                                         int my_grid, int world_nranks, int world_rank, const int *rank_grid,
                                         const long long *rank_rows, const amg_nb_transport *t,
@@ -632,15 +992,12 @@ extern "C" int amg_grid_add_solve(amg_grid_add *G, const double *b_local, double
    double rr;
    AMG_TRY(G->be->residual(&rr));
    double v[1] = {rr};
-   AMG_TRY(xp_err(G->t.grid_allreduce(G->t.user, v, 1), "grid_allreduce"));
+   AMG_TRY(tp_sum(G, v, 1));
    G->r0_norm2 = std::sqrt(v[0]);
    if (G->r0_norm2 == 0.0) G->r0_norm2 = 1.0;
    G->r_local = 1.0;
    // AsyncStart: post every outside receive
-   for (int i = 0; i < (int)G->recv.procs.size(); i++)
-      AMG_TRY(xp_err(G->t.irecv(G->t.user, G->recv.procs[i], GRIDJ_TO_GRIDK_CORRECT_TAG, G->recv.data[i].data(),
-                                G->recv.len[i] + 2, &G->recv.requests[i]),
-                     "irecv"));
+   for (int i = 0; i < (int)G->recv.procs.size(); i++) AMG_TRY(tp_irecv(G, G->recv, i));
    const long long cap = 1000LL * std::max(1, G->o.num_cycles) + 1000;
    while (true) {
       G->converge_flag = check_converge(G);
@@ -662,7 +1019,7 @@ extern "C" int amg_grid_add_solve(amg_grid_add *G, const double *b_local, double
    AMG_TRY(async_end(G));
    AMG_TRY(G->be->residual(&rr));
    v[0] = rr;
-   AMG_TRY(xp_err(G->t.grid_allreduce(G->t.user, v, 1), "grid_allreduce"));
+   AMG_TRY(tp_sum(G, v, 1));
    AMG_TRY(G->be->get_x(x_local));
    if (cycles) *cycles = G->cycle;
    if (relres_local) *relres_local = std::sqrt(v[0]) / G->r0_norm2;

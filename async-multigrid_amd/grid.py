@@ -8,6 +8,8 @@ The protocol needs a non-blocking transport with MPI point-to-point semantics
     in-flight pools of DMEM_Comm.cpp really fill up);
   * TorchNbTransport -- ranks as processes over torch.distributed (gloo on the
     host: isend / irecv / Work.is_completed, all_reduce over the grid's group).
+DevHub (amg_devhub) replaces the transport for ranks as threads of one
+process: the correction payloads stay in device memory end to end.
 """
 import ctypes as C
 import threading
@@ -198,6 +200,25 @@ class TorchNbTransport(_Transport):
         return t.numpy()
 
 
+class DevHub:
+    """Device-resident correction messages between ranks running as threads of
+    one process (amg_devhub, csrc/amg_grid.cpp): payloads move device to
+    device, done flags and InnerProdFlag sums on the hub."""
+
+    def __init__(self, rank_grid):
+        self.rank_grid = np.ascontiguousarray(rank_grid, dtype=np.int32)
+        h = C.c_void_p()
+        check(lib.amg_devhub_create(int(self.rank_grid.size), self.rank_grid.ctypes.data_as(C.POINTER(C.c_int)),
+                                    C.byref(h)))
+        self.h = h
+        self.error = None  # the GridAdd transport interface
+
+    def free(self):
+        if getattr(self, "h", None):
+            lib.amg_devhub_free(self.h)
+            self.h = None
+
+
 class GridAdd:
     """One rank of the level-grouped solve: over its grid's distributed
     hierarchy (`dist_hier`) or, with `diag` / `weight`, over the host model."""
@@ -210,7 +231,10 @@ class GridAdd:
         h = C.c_void_p()
         rg = self.rank_grid.ctypes.data_as(C.POINTER(C.c_int))
         rr = self.rank_rows.ctypes.data_as(C.POINTER(C.c_longlong))
-        if dist_hier is not None:
+        if dist_hier is not None and isinstance(transport, DevHub):
+            st = lib.amg_grid_add_create_devhub(dist_hier.h, my_grid, world, rank, rg, rr, transport.h, C.byref(h))
+            self.n = dist_hier.n0
+        elif dist_hier is not None:
             st = lib.amg_grid_add_create(dist_hier.h, my_grid, world, rank, rg, rr, C.byref(transport.c), C.byref(h))
             self.n = dist_hier.n0
         else:

@@ -652,6 +652,25 @@ int amg_grid_add_create(amg_dist_hier *D, int my_grid, int world_nranks, int wor
 int amg_grid_add_create_host(int nrows, const double *diag, double weight, const amg_opts *opts, int my_grid,
                              int world_nranks, int world_rank, const int *rank_grid,
                              const long long *rank_rows, const amg_nb_transport *t, amg_grid_add **out);
+/* Device-resident correction messages (replaces the host transport's payload
+ * path, DMEM_Comm.cpp:77-348's MPI_Isend / MPI_Irecv / MPI_Test of the correction
+ * vectors): ranks are threads of one process; a hub matches every rank's posted
+ * sends and receives per (source, destination) in order.  A message is the
+ * sender's device slot: the receiver's accumulate kernel reads it in place
+ * (peer access between the ranks' devices is the caller's) after its stream
+ * waits for the slot's write on the sender's stream; a receive completes once
+ * matched, a send once the receiver's read has run (events; no host staging,
+ * no copy).  The message's done flag (0/1/2) travels as a host
+ * word of the match.  rank_grid[world]: every rank's grid (InnerProdFlag sums
+ * over a grid's ranks run on the hub as well). */
+typedef struct amg_devhub amg_devhub;
+int amg_devhub_create(int world_nranks, const int *rank_grid, amg_devhub **out);
+int amg_devhub_free(amg_devhub *hub); /* after every grid_add using it is freed */
+/* amg_grid_add_create with the hub as the messages' transport: accumulators,
+ * in-flight slots and receive buffers in D's device pool */
+int amg_grid_add_create_devhub(amg_dist_hier *D, int my_grid, int world_nranks, int world_rank,
+                               const int *rank_grid, const long long *rank_rows, amg_devhub *hub,
+                               amg_grid_add **out);
 /* DMEM_Add, asynchronous branch: b / x (in: x0, out: x) are this rank's rows of
  * its grid's partition; *cycles = cycles run, *relres = ||b - A x|| / ||b - A x0||
  * over the grid after AsyncRecvCleanup, messages[2] = sent, received */
