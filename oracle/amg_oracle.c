@@ -1055,7 +1055,7 @@ int or_solve(or_hier *H, const double *f, double *u, double *reshist)
  * thread's add), SEMI_ASYNC under one lock held by the group root (:238-283).
  * READ_SOL or READ_RES (:227-236, 270-295: the groups subtract A e from the
  * shared residual and keep private correction sums, joined at the end,
- * :416-426), res_compute LOCAL, converge LOCAL (:317-322: a group stops after
+ * :416-426), res_compute LOCAL or GLOBAL (below), converge LOCAL (:317-322: a group stops after
  * num_cycles corrections) or GLOBAL (:323-337: the finest group's root sets
  * the converge flag once every level has num_cycles corrections -- CheckConverge,
  * Misc.cpp:418-442 -- and each group barrier hands it to the group).  The
@@ -1071,6 +1071,17 @@ typedef struct {
  * ratios of the race, for the band's ends */
 static int g_async_schedule = 0;
 void or_set_async_schedule(int s) { g_async_schedule = s; }
+
+/* res_compute_type GLOBAL (ASYNC_MULTADD, SMEM_Main.cpp:650-660): no group owns
+ * level 0 (PartitionLevels' finest_level = 1, SMEM_Setup.cpp:609-615); every
+ * thread first smooths its global slice of the fine grid (A_ns_global: equal
+ * row splits over all threads, SMEM_Setup.cpp:923-937) from its group's
+ * residual and adds that into u (:35-77, SEMI_ASYNC under the lock :258-265),
+ * and each iteration ends with the thread's slice of the global residual
+ * f - A u_k written into the shared r and the group's rows of r read back
+ * (:356-414) */
+static int g_async_res_global = 0;
+void or_set_async_res_global(int on) { g_async_res_global = on; }
 
 static int gbar_wait(or_gbar *b, const int *conv)
 {
@@ -1205,9 +1216,12 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
    const or_opts *o = &H->o;
    const int L = H->L, n0 = H->n[0];
    const int multadd = (o->solver == OR_MULTADD || o->solver == OR_ASYNC_MULTADD);
+   const int gres = g_async_res_global && multadd;
+   const int k_lo = gres ? 1 : 0; /* the finest level with a group */
+   if (gres && (L < 2 || read_type != OR_READ_SOL)) return -1; /* READ_RES needs LOCAL residuals (:227, 270, 288) */
    int T = 0;
    for (int k = 0; k < L; k++) {
-      if (nt[k] < 1) return -1;
+      if (k < k_lo ? nt[k] != 0 : nt[k] < 1) return -1;
       T += nt[k];
    }
    init_vectors(H);
@@ -1230,6 +1244,12 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
          gi[t] = g;
       }
    }
+   /* GLOBAL residuals: thread t's global fine slice [gs[t], gs[t + 1]) */
+   int *gs = (int *)malloc((T + 1) * sizeof(int));
+   {
+      const int size = n0 / T, rest = n0 - size * T;
+      for (int t = 0; t <= T; t++) gs[t] = t * size + (t < rest ? t : rest);
+   }
    /* blkA[k][l]: level-l row partition among group k (nt[k] + 1 entries); P / R likewise */
    int ***blk = (int ***)malloc(3 * sizeof(int **));
    for (int m = 0; m < 3; m++) {
@@ -1238,7 +1258,7 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
          for (int l = 0; l < L; l++) {
             int *b = (int *)malloc((nt[k] + 1) * sizeof(int));
             const or_csr *M = m == 0 ? &H->A[l] : (l < L - 1 ? (m == 1 ? &H->P[l] : &H->R[l]) : NULL);
-            if (M) or_partition_nnz(M, nt[k], b);
+            if (M && nt[k] > 0) or_partition_nnz(M, nt[k], b);
             else for (int g = 0; g <= nt[k]; g++) b[g] = 0;
             blk[m][k * L + l] = b;
          }
@@ -1266,10 +1286,21 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
       const int coarsest = multadd ? k : k + 1;
       if (g_async_schedule && converge_type == OR_CONVERGE_LOCAL) {
          const int prev = g_async_schedule == 1 ? k - 1 : k + 1; /* the group that runs before this one */
-         if (prev >= 0 && prev < L)
+         if (prev >= k_lo && prev < L)
             while (__atomic_load_n(&count[prev], __ATOMIC_ACQUIRE) < o->num_cycles) sched_yield();
       }
+      const int gns = gs[tid], gne = gs[tid + 1];
       while (1) {
+         if (gres) {
+            /* :35-77: smooth the global slice of A_0 u = r_k from zero */
+            async_smooth(H, 0, H->lv_r[k][0], H->lv_u_fine[k][0], H->lv_u_prev[k][0], H->lv_y[k][0], o->num_fine,
+                         k, gns, gne, b);
+            if (async_type != OR_SEMI_ASYNC)
+               for (int i = gns; i < gne; i++) {
+#pragma omp atomic
+                  U[i] += H->lv_u_fine[k][0][i];
+               }
+         }
          /* restriction :93-108 */
          for (int l = 0; l < coarsest; l++) {
             if (l >= L - 1) continue;
@@ -1327,6 +1358,8 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
          if (async_type == OR_SEMI_ASYNC) {
             if (tid == root[k]) omp_set_lock(&lock);
             gbar_wait(b, NULL);
+            if (gres) /* :258-265 */
+               for (int i = gns; i < gne; i++) U[i] += H->lv_u_fine[k][0][i];
          }
          for (int i = ns; i < ne; i++) {
             double v;
@@ -1357,18 +1390,45 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
             gbar_wait(b, NULL);
             if (__atomic_load_n(&count[k], __ATOMIC_ACQUIRE) == o->num_cycles) tid_converge = 1;
          } else {
-            if (tid == root[0] && __atomic_load_n(&conv_flag, __ATOMIC_ACQUIRE) == 0) {
+            if (tid == root[k_lo] && __atomic_load_n(&conv_flag, __ATOMIC_ACQUIRE) == 0) {
                int all = 1;
-               for (int l = 0; l < L; l++)
+               for (int l = k_lo; l < L; l++)
                   if (__atomic_load_n(&count[l], __ATOMIC_ACQUIRE) < o->num_cycles) all = 0;
                if (all) __atomic_store_n(&conv_flag, 1, __ATOMIC_RELEASE);
             }
             if (gbar_wait(b, &conv_flag) == 1) tid_converge = 1;
          }
-         /* LOCAL residual, READ_SOL :338-351 */
-         if (!rres) or_smem_residual(&H->A[0], F, ukk, H->lv_y[k][0], H->lv_r[k][0], ns, ne);
-         gbar_wait(b, NULL);
+         if (!gres) {
+            /* LOCAL residual, READ_SOL :338-351 */
+            if (!rres) or_smem_residual(&H->A[0], F, ukk, H->lv_y[k][0], H->lv_r[k][0], ns, ne);
+            gbar_wait(b, NULL);
+         }
          if (tid_converge == 1) break;
+         if (gres) {
+            /* :356-414: u_k = u on the group's rows; the slice's residual
+             * into the shared r; the group's rows of r back into r_k */
+            for (int i = ns; i < ne; i++) {
+               double v;
+#pragma omp atomic read
+               v = U[i];
+               ukk[i] = v;
+            }
+            gbar_wait(b, NULL);
+            or_smem_residual(&H->A[0], F, ukk, H->lv_y[k][0], H->lv_r[k][0], gns, gne);
+            if (async_type == OR_SEMI_ASYNC && tid == root[k]) omp_set_lock(&lock);
+            gbar_wait(b, NULL);
+            for (int i = gns; i < gne; i++) {
+#pragma omp atomic write
+               R0[i] = rk[i];
+            }
+            for (int i = ns; i < ne; i++) {
+               double v;
+#pragma omp atomic read
+               v = R0[i];
+               rk[i] = v;
+            }
+            if (async_type == OR_SEMI_ASYNC && tid == root[k]) omp_unset_lock(&lock);
+         }
       }
 #undef RNG
    }
@@ -1393,7 +1453,7 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
       free(facc[k]);
    }
    free(uk);
-   free(facc); free(bar); free(count); free(lev); free(gi); free(root);
+   free(facc); free(bar); free(count); free(lev); free(gi); free(root); free(gs);
    return 0;
 }
 

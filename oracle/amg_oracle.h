@@ -189,7 +189,7 @@ double or_dmem_async_jacobi(const or_csr *A, const double *b, double *x, int swe
 
 /* SMEM_Async_Add_AMG (SMEM_Async_AMG.cpp:7-437) on real OpenMP threads: nt[k]
  * threads own level k (sum = T threads, each >= 1); async_type FULL / SEMI,
- * READ_SOL / READ_RES, res_compute LOCAL, converge LOCAL or GLOBAL; the hierarchy's opts
+ * READ_SOL / READ_RES, res_compute LOCAL (GLOBAL: or_set_async_res_global), converge LOCAL or GLOBAL; the hierarchy's opts
  * give solver (ASYNC_MULTADD / ASYNC_AFACX), smoother (Jacobi, L1, hybrid JGS;
  * symmetric forms for multadd with pre and post sweeps), num_fine /
  * num_coarse sweeps, num_cycles.  u: initial guess in, iterate out;
@@ -204,6 +204,9 @@ double or_dmem_async_jacobi(const or_csr *A, const double *b, double *x, int swe
 /* group schedule of or_async_add (converge LOCAL): 0 free, 1 / 2 one group
  * after another, finest / coarsest first */
 void or_set_async_schedule(int s);
+/* res_compute_type GLOBAL for or_async_add (ASYNC_MULTADD, READ_SOL): nt[0] = 0
+ * (no level-0 group), each thread smooths its global fine slice (:35-77, 356-414) */
+void or_set_async_res_global(int on);
 int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int async_type, int read_type,
                  int converge_type, int *corrections, double *relres);
 

@@ -24,6 +24,9 @@ from test_gpu_solve import oracle_opts
 
 def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blocks=None, lockstep=True,
                       sequential=False):
+    """res_compute_type GLOBAL (ASYNC_MULTADD): no level-0 group (thread sets
+    [0, 1, ..] / [0, 2, ..]) and no synchronous equivalent, so no lockstep
+    member; the sequential schedules are added instead."""
     """(lo, hi, rels, counts) of `reps` runs per thread set (rels[-1]: the
     synchronous schedule when lockstep); opts: the GPU run's
     amg_opts (solver ASYNC_MULTADD / ASYNC_AFACX, smoother, sweeps, num_cycles,
@@ -36,10 +39,14 @@ def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blo
     at = oracle.OR_SEMI_ASYNC if opts.async_type == amg.AMG_SEMI_ASYNC else oracle.OR_FULL_ASYNC
     rt = oracle.OR_READ_RES if opts.read_type == amg.AMG_READ_RES else oracle.OR_READ_SOL
     ct = oracle.OR_CONVERGE_GLOBAL if opts.converge_test_type == amg.AMG_GLOBAL else oracle.OR_CONVERGE_LOCAL
+    gres = opts.res_compute_type == amg.AMG_GLOBAL and opts.solver == amg.AMG_ASYNC_MULTADD
+    if gres:
+        thread_sets = thread_sets or ([0] + [1] * (L - 1), [0] + [2] * (L - 1))
+        lockstep, sequential = False, True
     rels, counts = [], []
     for nt in thread_sets or ([1] * L, [2] * L):
         for _ in range(reps):
-            u, rel, cnt = OH.async_add(f, nt, async_type=at, converge_type=ct, read_type=rt)
+            u, rel, cnt = OH.async_add(f, nt, async_type=at, converge_type=ct, read_type=rt, res_global=gres)
             assert np.all(np.isfinite(u))
             rels.append(rel)
             counts.append(cnt)
@@ -49,7 +56,8 @@ def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blo
         for sched in (1, 2):
             oracle.lib().or_set_async_schedule(sched)
             try:
-                u, rel, cnt = OH.async_add(f, [1] * L, async_type=at, converge_type=ct, read_type=rt)
+                u, rel, cnt = OH.async_add(f, [0 if gres else 1] + [1] * (L - 1), async_type=at, converge_type=ct,
+                                           read_type=rt, res_global=gres)
             finally:
                 oracle.lib().or_set_async_schedule(0)
             rels.append(rel)

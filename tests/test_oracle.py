@@ -232,3 +232,37 @@ def test_async_add_sequential_schedules(amg, oracle):
         rels[sched] = rel
     assert rels[0] < 1e-2 and rels[1] < 1.0 and rels[2] < 1.0
     assert rels[0] < rels[1] and rels[0] < rels[2], rels
+
+
+def test_async_add_res_global(amg, oracle):
+    """or_set_async_res_global (res_compute_type GLOBAL, SMEM_Async_AMG.cpp:35-77,
+    356-414): no level-0 group; every level group runs num_cycles corrections,
+    the free race converges, and with one thread per group run one after
+    another the result is deterministic."""
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, 16, amg.AMG_INTERP_LINEAR)
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs = oracle.smooth_transfer(host["A"][lev], host["P"][lev], 0.8)
+        Ps.append(ps)
+        Rs.append(rs)
+    o = oracle.make_opts(solver=oracle.OR_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=12, tol=0.0)
+    OH = oracle.Hier(host["A"], Ps, Rs, o)
+    f = amg.rhs_rand(0, 16 ** 3)
+    nt = [0] + [1] * (L - 1)
+    for at in (oracle.OR_FULL_ASYNC, oracle.OR_SEMI_ASYNC):
+        u, rel, cnt = OH.async_add(f, nt, async_type=at, res_global=True)
+        assert np.all(np.isfinite(u)) and list(cnt[:L]) == [0] + [12] * (L - 1)
+        assert rel < 0.5, rel
+        seq = []
+        for _ in range(2):
+            oracle.lib().or_set_async_schedule(1)
+            try:
+                seq.append(OH.async_add(f, nt, async_type=at, res_global=True))
+            finally:
+                oracle.lib().or_set_async_schedule(0)
+        assert np.array_equal(seq[0][0].view(np.uint64), seq[1][0].view(np.uint64))
+        assert rel < seq[0][1] < 1.0, (rel, seq[0][1])
+    # a level-0 group is refused with GLOBAL residuals
+    with pytest.raises(AssertionError):
+        OH.async_add(f, [1] * L, res_global=True)
