@@ -1083,6 +1083,22 @@ void or_set_async_schedule(int s) { g_async_schedule = s; }
 static int g_async_res_global = 0;
 void or_set_async_res_global(int on) { g_async_res_global = on; }
 
+/* DMEM acceleration of the asynchronous additive cycle (DMEM_Add.cpp:319-324):
+ * ChebyUpdate(gridk.d, U_array[0]) on each level's prolonged fine correction
+ * before it is added, async branch (DMEM_Misc.cpp:650-663): level `grid` (the
+ * cheby_grid) carries d, the others scale their correction by omega * delta;
+ * each level counts its own cycles.  Restated here per level group on the
+ * group's rows, so the distributed solve's acceleration gets a band too. */
+static int g_acc_type = 0, g_acc_grid = 0;
+static double g_acc_mu = 0.0, g_acc_delta = 0.0;
+void or_set_async_accel(int accel, int grid, double mu, double delta)
+{
+   g_acc_type = accel;
+   g_acc_grid = grid;
+   g_acc_mu = mu;
+   g_acc_delta = delta;
+}
+
 static int gbar_wait(or_gbar *b, const int *conv)
 {
    int g = __atomic_load_n(&b->gen, __ATOMIC_ACQUIRE);
@@ -1266,10 +1282,12 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
    or_gbar *bar = (or_gbar *)calloc(L, sizeof(or_gbar));
    int *count = (int *)calloc(L, sizeof(int));
    double **uk = (double **)malloc(L * sizeof(double *)), **facc = (double **)malloc(L * sizeof(double *));
+   double **dacc = (double **)malloc(L * sizeof(double *));
    for (int k = 0; k < L; k++) {
       bar[k].n = nt[k];
       uk[k] = dvec(n0);
       facc[k] = dvec(n0);
+      dacc[k] = dvec(n0);
    }
    int conv_flag = 0;
    omp_lock_t lock;
@@ -1290,6 +1308,8 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
             while (__atomic_load_n(&count[prev], __ATOMIC_ACQUIRE) < o->num_cycles) sched_yield();
       }
       const int gns = gs[tid], gne = gs[tid + 1];
+      int acc_cycle = 0;
+      double acc_state[2] = {g_acc_mu, 1.0}; /* every thread of the group advances it alike */
       while (1) {
          if (gres) {
             /* :35-77: smooth the global slice of A_0 u = r_k from zero */
@@ -1347,6 +1367,11 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
             gbar_wait(b, NULL);
          }
          RNG(0, 0, ns, ne);
+         if (g_acc_type != OR_NO_ACCEL) {
+            or_dmem_cheby_update(dacc[k] + ns, H->lv_e[k][0] + ns, ne - ns, acc_cycle, g_acc_type,
+                                 k == g_acc_grid ? OR_CHEBY_GRID : OR_CHEBY_OTHER, g_acc_mu, g_acc_delta, acc_state);
+            acc_cycle++;
+         }
          const double *e0 = H->lv_e[k][0];
          double *ukk = uk[k];
          const int rres = read_type == OR_READ_RES;
@@ -1451,8 +1476,10 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
    for (int k = 0; k < L; k++) {
       free(uk[k]);
       free(facc[k]);
+      free(dacc[k]);
    }
    free(uk);
+   free(dacc);
    free(facc); free(bar); free(count); free(lev); free(gi); free(root); free(gs);
    return 0;
 }

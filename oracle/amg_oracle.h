@@ -207,6 +207,9 @@ void or_set_async_schedule(int s);
 /* res_compute_type GLOBAL for or_async_add (ASYNC_MULTADD, READ_SOL): nt[0] = 0
  * (no level-0 group), each thread smooths its global fine slice (:35-77, 356-414) */
 void or_set_async_res_global(int on);
+/* DMEM ChebyUpdate on each level's fine correction in or_async_add (accel 0: off;
+ * grid: the clamped cheby_grid level) -- DMEM_Add.cpp:319-324 */
+void or_set_async_accel(int accel, int grid, double mu, double delta);
 int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int async_type, int read_type,
                  int converge_type, int *corrections, double *relres);
 

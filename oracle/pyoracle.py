@@ -79,6 +79,7 @@ def lib():
         L.or_set_async_gs_threads.argtypes = [C.c_int]
         L.or_set_async_schedule.argtypes = [C.c_int]
         L.or_set_async_res_global.argtypes = [C.c_int]
+        L.or_set_async_accel.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double]
         L.or_async_add.restype = C.c_int
         L.or_async_add.argtypes = [C.c_void_p, _dp, _dp, _ip, C.c_int, C.c_int, C.c_int, _ip,
                                    C.POINTER(C.c_double)]
@@ -380,10 +381,12 @@ class Hier:
                                      dptr(hist), accel, mu, delta)
         return x, hist[:k + 1], k
 
-    def async_add(self, f, nt, async_type=0, converge_type=0, u0=None, read_type=0, res_global=False):
+    def async_add(self, f, nt, async_type=0, converge_type=0, u0=None, read_type=0, res_global=False,
+                  accel=None):
         """SMEM_Async_Add_AMG on sum(nt) OpenMP threads (nt[k] threads own level k):
         (u, relres, per-level correction counts).  Nondeterministic.
-        res_global: res_compute_type GLOBAL (nt[0] must be 0: no level-0 group)."""
+        res_global: res_compute_type GLOBAL (nt[0] must be 0: no level-0 group).
+        accel: (accel_type, cheby level, mu, delta) -- DMEM ChebyUpdate per level."""
         n0 = self._keep[0][0].nrows
         u = np.zeros(n0) if u0 is None else np.array(u0, dtype=np.float64)
         ntv = np.ascontiguousarray(nt, dtype=np.int32)
@@ -392,11 +395,14 @@ class Hier:
         cnt = np.zeros(self.L, dtype=np.int32)
         rel = C.c_double()
         lib().or_set_async_res_global(1 if res_global else 0)
+        if accel is not None:
+            lib().or_set_async_accel(int(accel[0]), int(accel[1]), float(accel[2]), float(accel[3]))
         try:
             st = lib().or_async_add(self.h, dptr(np.ascontiguousarray(f, dtype=np.float64)), dptr(u), iptr(ntv),
                                     int(async_type), int(read_type), int(converge_type), iptr(cnt), C.byref(rel))
         finally:
             lib().or_set_async_res_global(0)
+            lib().or_set_async_accel(0, 0, 0.0, 0.0)
         assert st == 0, st
         return u, rel.value, cnt
 

@@ -26,7 +26,9 @@ def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blo
                       sequential=False):
     """res_compute_type GLOBAL (ASYNC_MULTADD): no level-0 group (thread sets
     [0, 1, ..] / [0, 2, ..]) and no synchronous equivalent, so no lockstep
-    member; the sequential schedules are added instead."""
+    member; the sequential schedules are added instead.  accel_type (the
+    distributed solve's ChebyUpdate per level, DMEM_Add.cpp:319-324) likewise
+    has no synchronous equivalent: sequential schedules, no lockstep."""
     """(lo, hi, rels, counts) of `reps` runs per thread set (rels[-1]: the
     synchronous schedule when lockstep); opts: the GPU run's
     amg_opts (solver ASYNC_MULTADD / ASYNC_AFACX, smoother, sweeps, num_cycles,
@@ -43,10 +45,16 @@ def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blo
     if gres:
         thread_sets = thread_sets or ([0] + [1] * (L - 1), [0] + [2] * (L - 1))
         lockstep, sequential = False, True
+    accel = None
+    if opts.accel_type != amg.AMG_NO_ACCEL:
+        # the device's cheby_grid is clamped to its last correcting level, L - 2
+        accel = (opts.accel_type, min(opts.cheby_grid, L - 2), opts.cheby_mu, opts.cheby_delta)
+        lockstep, sequential = False, True
     rels, counts = [], []
     for nt in thread_sets or ([1] * L, [2] * L):
         for _ in range(reps):
-            u, rel, cnt = OH.async_add(f, nt, async_type=at, converge_type=ct, read_type=rt, res_global=gres)
+            u, rel, cnt = OH.async_add(f, nt, async_type=at, converge_type=ct, read_type=rt, res_global=gres,
+                                       accel=accel)
             assert np.all(np.isfinite(u))
             rels.append(rel)
             counts.append(cnt)
@@ -57,7 +65,7 @@ def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blo
             oracle.lib().or_set_async_schedule(sched)
             try:
                 u, rel, cnt = OH.async_add(f, [0 if gres else 1] + [1] * (L - 1), async_type=at, converge_type=ct,
-                                           read_type=rt, res_global=gres)
+                                           read_type=rt, res_global=gres, accel=accel)
             finally:
                 oracle.lib().or_set_async_schedule(0)
             rels.append(rel)
