@@ -473,20 +473,32 @@ def test_async_gauss_seidel_single_block(mats, ctx, oracle, amg, name, semi, rev
 
 @pytest.mark.parametrize("semi", [0, 1])
 def test_async_gauss_seidel_many_blocks(mats, ctx, oracle, amg, semi):
-    """Many blocks: racy across blocks like the reference; the sweeps still
-    reduce the residual about as much as the serialised restatement."""
+    """Many blocks: racy across blocks like the reference, so the residual after
+    the sweeps must lie in [0.5 x min, 2 x max] of the oracle's band: the
+    blocks one after another, 10 runs with one OpenMP thread per block on the
+    live iterate (SMEM_Async_GaussSeidel's race) and all blocks in lockstep."""
     host, dev = mats
     A, dA = host["A1"], dev["A1"]
     f = _vecs(A.nrows, 42)
     blk = np.linspace(0, A.nrows, 65).astype(np.int32)
-    ru = np.zeros(A.nrows)
-    oracle.async_gs(A, f, ru, blk, 4, 0)
+    res = lambda x: np.linalg.norm(f - oracle.smem_matvec(A, x, np.zeros(A.nrows)))
+    band = []
+    try:
+        for mode, reps in ((0, 1), (1, 10), (2, 1)):
+            oracle.lib().or_set_async_gs_threads(mode)
+            for _ in range(reps):
+                ru = np.zeros(A.nrows)
+                oracle.async_gs(A, f, ru, blk, 4, 0)
+                band.append(res(ru))
+    finally:
+        oracle.lib().or_set_async_gs_threads(0)
     du = ctx.vec(np.zeros(A.nrows))
     amg.smem.SMEM_Async_Parfor_GaussSeidel(ctx, dA, ctx.vec(f), du, 4, blk, semi, 0)
-    u = du.download()
-    res = lambda x: np.linalg.norm(f - oracle.smem_matvec(A, x, np.zeros(A.nrows)))
-    r0, rg, rc = np.linalg.norm(f), res(u), res(ru)
-    assert rg < 0.5 * r0 and rg < 2.0 * rc, (r0, rg, rc)
+    rg = res(du.download())
+    lo, hi = min(band), max(band)
+    print(f"async GS {semi}: oracle band [{lo:.4e}, {hi:.4e}], device {rg:.4e}")
+    assert rg < 0.5 * np.linalg.norm(f)
+    assert 0.5 * lo <= rg <= 2.0 * hi, (rg, lo, hi)
 
 
 @pytest.mark.parametrize("name", ["lap16", "A1", "rand_nz"])
