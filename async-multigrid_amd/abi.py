@@ -225,6 +225,7 @@ PROTOTYPES.update({
     "amg_devhub_create": (_i, [_i, _ip, _pp]),
     "amg_devhub_free": (_i, [_p]),
     "amg_grid_add_create_devhub": (_i, [_p, _i, _i, _i, _ip, _llp, _p, _pp]),
+    "amg_grid_add_create_ipc": (_i, [_p, _i, _i, _i, _ip, _llp, C.POINTER(AmgNbTransport), _pp]),
     "amg_grid_add_create_host": (_i, [_i, _dp, _d, C.POINTER(AmgOpts), _i, _i, _i, _ip, _llp,
                                       C.POINTER(AmgNbTransport), _pp]),
     "amg_grid_add_solve": (_i, [_p, _dp, _dp, _ip, _dp, _llp]),

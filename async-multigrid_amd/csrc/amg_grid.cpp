@@ -246,6 +246,7 @@ struct CommClass {
    // device-resident messages: accumulators / receive buffers and send slots
    std::vector<double *> dd;
    std::vector<std::vector<double *>> dslot;
+   std::vector<double *> dpool; // one allocation per peer holding its slots (IPC-mappable)
    std::vector<std::vector<double>> dflag; // the slots' done flags (host words of the messages)
 };
 
@@ -446,9 +447,216 @@ extern "C" int amg_devhub_free(amg_devhub *h)
    return AMG_OK;
 }
 
+namespace {
+
+constexpr int IPC_ACK_TAG = GRIDJ_TO_GRIDK_CORRECT_TAG + 1;    // receiver -> sender: slot read
+constexpr int IPC_HANDLE_TAG = GRIDJ_TO_GRIDK_CORRECT_TAG + 2; // the slot pools' IPC handles
+
+// the payload path of device-resident messages: a message is sender slot
+// `slot` (device memory), read in place by the receiver's kernel
+struct MsgLink {
+   virtual ~MsgLink() = default;
+   virtual int isend(int peer, const double *src, int slot, long long n, double flag, hipStream_t s,
+                     long long *req) = 0;
+   virtual int irecv(int peer, long long n, long long *req) = 0;
+   // done: *src may be read by work queued on s from now on, until consume()
+   virtual int test_recv(long long req, hipStream_t s, int *done, double *flag, const double **src,
+                         long long *n) = 0;
+   virtual int consume(long long req, hipStream_t s) = 0;
+   virtual int test_send(long long req, int *done) = 0;
+   virtual int grid_sum(double *v, int n) = 0;
+   virtual int flush() { return AMG_OK; } // outstanding acknowledgements, at the end of a solve
+   int wait_send(long long req)
+   {
+      for (;;) {
+         int done = 0;
+         AMG_TRY(test_send(req, &done));
+         if (done) return AMG_OK;
+         std::this_thread::yield();
+      }
+   }
+};
+
+// ranks as threads of one process: the hub
+struct HubLink : MsgLink {
+   amg_devhub *h;
+   int me;
+   HubLink(amg_devhub *h_, int me_) : h(h_), me(me_) {}
+   int isend(int peer, const double *src, int, long long n, double flag, hipStream_t s, long long *req) override
+   {
+      return h->isend(me, peer, GRIDJ_TO_GRIDK_CORRECT_TAG, src, n, flag, s, req);
+   }
+   int irecv(int peer, long long n, long long *req) override
+   {
+      return h->irecv(me, peer, GRIDJ_TO_GRIDK_CORRECT_TAG, n, req);
+   }
+   int test_recv(long long req, hipStream_t s, int *done, double *flag, const double **src, long long *n) override
+   {
+      return h->test_recv(req, s, done, flag, src, n);
+   }
+   int consume(long long req, hipStream_t s) override { return h->consume(req, s); }
+   int test_send(long long req, int *done) override { return h->test_send(req, done); }
+   int grid_sum(double *v, int n) override { return h->grid_sum(me, v, n); }
+};
+
+int xp(int st, const char *what)
+{
+   return st == 0 ? AMG_OK : amg_set_error(AMG_ERR_ARG, "amg_grid_add: transport %s failed (%d)", what, st);
+}
+
+// ranks as processes: every send slot pool is mapped into its receiver's
+// address space once (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles
+// exchanged over the host transport at creation).  Per message the host
+// transport carries only a control word pair (slot, done flag) -- sent once
+// the slot's write has run on the sender's stream -- and an acknowledgement
+// back once the receiver's read of the slot has run on its stream; the send
+// completes with the acknowledgement, so the slot is refilled only after it
+// was read.  The payload never leaves device memory.
+struct IpcLink : MsgLink {
+   amg_nb_transport t;
+   struct Peer {
+      const double *base = nullptr; // the sender's slot pool, mapped here
+      long long len = 0;            // doubles per slot
+   };
+   std::map<int, Peer> peers; // receive peers
+   struct SendRec {
+      long long ctl_req = 0, ack_req = 0;
+      double ctl[2] = {0.0, 0.0}, ack = 0.0;
+      bool ctl_done = false, ack_done = false;
+   };
+   struct RecvRec {
+      long long req = 0;
+      int peer = 0;
+      double ctl[2] = {0.0, 0.0};
+   };
+   struct AckRec {
+      int peer = 0;
+      hipEvent_t ev = nullptr;
+      bool sent = false;
+      long long req = 0;
+      double buf = 1.0;
+   };
+   std::map<long long, std::unique_ptr<SendRec>> sends;
+   std::map<long long, std::unique_ptr<RecvRec>> recvs;
+   std::deque<std::unique_ptr<AckRec>> acks;
+   std::vector<void *> opened;
+   long long next = 1;
+   explicit IpcLink(const amg_nb_transport &t_) : t(t_) {}
+   ~IpcLink() override
+   {
+      for (auto &a : acks)
+         if (a->ev) hipEventDestroy(a->ev);
+      for (void *p : opened) hipIpcCloseMemHandle(p);
+   }
+   // acknowledge every read that has run; retire sent acknowledgements
+   int progress()
+   {
+      for (auto it = acks.begin(); it != acks.end();) {
+         AckRec &a = **it;
+         if (!a.sent) {
+            const hipError_t q = hipEventQuery(a.ev);
+            if (q == hipErrorNotReady) {
+               ++it;
+               continue;
+            }
+            AMG_HIP(q);
+            AMG_TRY(xp(t.isend(t.user, a.peer, IPC_ACK_TAG, &a.buf, 1, &a.req), "isend"));
+            a.sent = true;
+         }
+         int done = 0;
+         AMG_TRY(xp(t.test(t.user, a.req, &done), "test"));
+         if (done) {
+            hipEventDestroy(a.ev);
+            it = acks.erase(it);
+         } else {
+            ++it;
+         }
+      }
+      return AMG_OK;
+   }
+   int isend(int peer, const double *, int slot, long long, double flag, hipStream_t s, long long *req) override
+   {
+      AMG_HIP(hipStreamSynchronize(s)); // the slot is written
+      auto r = std::make_unique<SendRec>();
+      r->ctl[0] = (double)slot;
+      r->ctl[1] = flag;
+      AMG_TRY(xp(t.irecv(t.user, peer, IPC_ACK_TAG, &r->ack, 1, &r->ack_req), "irecv"));
+      AMG_TRY(xp(t.isend(t.user, peer, GRIDJ_TO_GRIDK_CORRECT_TAG, r->ctl, 2, &r->ctl_req), "isend"));
+      *req = next++;
+      sends[*req] = std::move(r);
+      return progress();
+   }
+   int irecv(int peer, long long, long long *req) override
+   {
+      auto r = std::make_unique<RecvRec>();
+      r->peer = peer;
+      AMG_TRY(xp(t.irecv(t.user, peer, GRIDJ_TO_GRIDK_CORRECT_TAG, r->ctl, 2, &r->req), "irecv"));
+      *req = next++;
+      recvs[*req] = std::move(r);
+      return AMG_OK;
+   }
+   int test_recv(long long req, hipStream_t, int *done, double *flag, const double **src, long long *n) override
+   {
+      AMG_TRY(progress());
+      auto it = recvs.find(req);
+      AMG_ARG(it != recvs.end(), "amg_grid_add: unknown receive %lld", req);
+      RecvRec &r = *it->second;
+      AMG_TRY(xp(t.test(t.user, r.req, done), "test"));
+      if (*done) {
+         const Peer &p = peers.at(r.peer);
+         *flag = r.ctl[1];
+         *src = p.base + (long long)r.ctl[0] * p.len;
+         *n = p.len;
+      }
+      return AMG_OK;
+   }
+   int consume(long long req, hipStream_t s) override
+   {
+      auto it = recvs.find(req);
+      AMG_ARG(it != recvs.end(), "amg_grid_add: unknown receive %lld", req);
+      auto a = std::make_unique<AckRec>();
+      a->peer = it->second->peer;
+      AMG_HIP(hipEventCreateWithFlags(&a->ev, hipEventDisableTiming));
+      AMG_HIP(hipEventRecord(a->ev, s));
+      acks.push_back(std::move(a));
+      recvs.erase(it);
+      return progress();
+   }
+   int test_send(long long req, int *done) override
+   {
+      AMG_TRY(progress());
+      auto it = sends.find(req);
+      AMG_ARG(it != sends.end(), "amg_grid_add: unknown send %lld", req);
+      SendRec &r = *it->second;
+      int d = 0;
+      if (!r.ctl_done) {
+         AMG_TRY(xp(t.test(t.user, r.ctl_req, &d), "test"));
+         r.ctl_done = d;
+      }
+      if (!r.ack_done) {
+         AMG_TRY(xp(t.test(t.user, r.ack_req, &d), "test"));
+         r.ack_done = d;
+      }
+      *done = r.ctl_done && r.ack_done;
+      if (*done) sends.erase(it);
+      return AMG_OK;
+   }
+   int grid_sum(double *v, int n) override { return xp(t.grid_allreduce(t.user, v, n), "grid_allreduce"); }
+   int flush() override
+   {
+      while (!acks.empty()) {
+         AMG_TRY(progress());
+         if (!acks.empty()) std::this_thread::yield();
+      }
+      return AMG_OK;
+   }
+};
+
+} // namespace
+
 struct amg_grid_add {
    amg_nb_transport t{};
-   amg_devhub *hub = nullptr; // device-resident messages (else the host transport t)
+   std::unique_ptr<MsgLink> link; // device-resident messages (else the host transport t)
    bool dev = false;
    double *ehd = nullptr, *zd = nullptr; // incoming corrections / zeros (device)
    amg_opts o{};
@@ -474,19 +682,19 @@ int xp_err(int st, const char *what)
 // the message transport: the device hub or the caller's host transport
 int tp_test(amg_grid_add *G, long long req, int *done)
 {
-   if (G->dev) return G->hub->test_send(req, done);
+   if (G->dev) return G->link->test_send(req, done);
    return xp_err(G->t.test(G->t.user, req, done), "test");
 }
 
 int tp_sum(amg_grid_add *G, double *v, int n)
 {
-   if (G->dev) return G->hub->grid_sum(G->me, v, n);
+   if (G->dev) return G->link->grid_sum(v, n);
    return xp_err(G->t.grid_allreduce(G->t.user, v, n), "grid_allreduce");
 }
 
 int tp_irecv(amg_grid_add *G, CommClass &cd, int i)
 {
-   if (G->dev) return G->hub->irecv(G->me, cd.procs[i], GRIDJ_TO_GRIDK_CORRECT_TAG, cd.len[i], &cd.requests[i]);
+   if (G->dev) return G->link->irecv(cd.procs[i], cd.len[i], &cd.requests[i]);
    return xp_err(G->t.irecv(G->t.user, cd.procs[i], GRIDJ_TO_GRIDK_CORRECT_TAG, cd.data[i].data(), cd.len[i] + 2,
                             &cd.requests[i]),
                  "irecv");
@@ -587,8 +795,7 @@ int send_recv(amg_grid_add *G, CommClass &cd, double *v, Op op, int *ret)
             }
          }
          if (dev)
-            AMG_TRY(G->hub->isend(G->me, ip, GRIDJ_TO_GRIDK_CORRECT_TAG, cd.dslot[i][nx], vl, *flw, s,
-                                  &cd.requests_inflight[i][nx]));
+            AMG_TRY(G->link->isend(ip, cd.dslot[i][nx], nx, vl, *flw, s, &cd.requests_inflight[i][nx]));
          else
             AMG_TRY(xp_err(G->t.isend(G->t.user, ip, GRIDJ_TO_GRIDK_CORRECT_TAG, cd.data_inflight[i][nx].data(),
                                       vl + 2, &cd.requests_inflight[i][nx]),
@@ -607,7 +814,7 @@ int send_recv(amg_grid_add *G, CommClass &cd, double *v, Op op, int *ret)
             const double *src = nullptr;
             long long got = 0;
             if (dev)
-               AMG_TRY(G->hub->test_recv(cd.requests[i], s, &flag, &fl, &src, &got));
+               AMG_TRY(G->link->test_recv(cd.requests[i], s, &flag, &fl, &src, &got));
             else
                AMG_TRY(tp_test(G, cd.requests[i], &flag));
             if (!flag) break;
@@ -616,7 +823,7 @@ int send_recv(amg_grid_add *G, CommClass &cd, double *v, Op op, int *ret)
             if (dev) {
                // read the payload from the sender's slot, then release it
                amgk::vaxpy(s, 1.0, src, v + vs, 0, (int)std::min<long long>(got, vl));
-               AMG_TRY(G->hub->consume(cd.requests[i], s));
+               AMG_TRY(G->link->consume(cd.requests[i], s));
             } else {
                for (int j = 0; j < vl; j++) v[vs + j] += cd.data[i][j];
                fl = cd.data[i][vl];
@@ -760,11 +967,12 @@ int async_end(amg_grid_add *G)
       for (int j = 0; j < G->send.max_inflight[i]; j++)
          if (G->send.inflight_flags[i][j] == 1) {
             if (G->dev)
-               AMG_TRY(G->hub->wait_send(G->send.requests_inflight[i][j]));
+               AMG_TRY(G->link->wait_send(G->send.requests_inflight[i][j]));
             else
                AMG_TRY(xp_err(G->t.wait(G->t.user, G->send.requests_inflight[i][j]), "wait"));
             G->send.inflight_flags[i][j] = 0;
          }
+   if (G->dev) AMG_TRY(G->link->flush()); // acknowledge the last reads
    return AMG_OK;
 }
 
@@ -844,10 +1052,13 @@ int alloc_dev(amg_grid_add *G, amg_dist_hier *D)
    const size_t np = cd.procs.size();
    cd.dd.assign(np, nullptr);
    cd.dslot.assign(np, {});
+   cd.dpool.assign(np, nullptr);
    for (size_t i = 0; i < np; i++) {
-      AMG_TRY(amgd::dvec(D, std::max(1, cd.len[i]), &cd.dd[i]));
-      cd.dslot[i].assign(cd.max_inflight[i], nullptr);
-      for (auto &p : cd.dslot[i]) AMG_TRY(amgd::dvec(D, std::max(1, cd.len[i]), &p));
+      const int len = std::max(1, cd.len[i]), mi = cd.max_inflight[i];
+      AMG_TRY(amgd::dvec(D, len, &cd.dd[i]));
+      AMG_TRY(amgd::dvec(D, (size_t)len * mi, &cd.dpool[i]));
+      cd.dslot[i].assign(mi, nullptr);
+      for (int j = 0; j < mi; j++) cd.dslot[i][j] = cd.dpool[i] + (size_t)j * len;
    }
    return AMG_OK;
 }
@@ -943,13 +1154,69 @@ extern "C" int amg_grid_add_create_devhub(amg_dist_hier *D, int my_grid, int wor
               p);
    auto G = std::make_unique<amg_grid_add>();
    G->o = D->o;
-   G->hub = hub;
+   G->link = std::make_unique<HubLink>(hub, world_rank);
    G->dev = true;
    auto be = std::make_unique<DistBackend>(D);
    AMG_TRY(be->init(my_grid));
    G->be = std::move(be);
    AMG_TRY(create_common(G.get(), my_grid, world_nranks, world_rank, rank_grid, rank_rows, nullptr));
    AMG_TRY(alloc_dev(G.get(), D));
+   *out = G.release();
+   return AMG_OK;
+}
+
+// the same across processes: slot pools mapped into their receivers by IPC
+// handles exchanged over t at creation (every rank of the world calls this
+// together); t then carries only control words, acknowledgements and the grid
+// sums
+extern "C" int amg_grid_add_create_ipc(amg_dist_hier *D, int my_grid, int world_nranks, int world_rank,
+                                       const int *rank_grid, const long long *rank_rows, const amg_nb_transport *t,
+                                       amg_grid_add **out)
+{
+   AMG_ARG(D && t && out, "amg_grid_add_create_ipc: null argument");
+   AMG_ARG(D->o.solver == AMG_ASYNC_MULTADD, "amg_grid_add_create_ipc: ASYNC_MULTADD hierarchies only");
+   AMG_ARG(t->isend && t->irecv && t->test && t->wait && t->grid_allreduce,
+           "amg_grid_add_create_ipc: incomplete transport");
+   auto G = std::make_unique<amg_grid_add>();
+   G->o = D->o;
+   G->dev = true;
+   auto be = std::make_unique<DistBackend>(D);
+   AMG_TRY(be->init(my_grid));
+   G->be = std::move(be);
+   AMG_TRY(create_common(G.get(), my_grid, world_nranks, world_rank, rank_grid, rank_rows, t));
+   AMG_TRY(alloc_dev(G.get(), D));
+   AMG_HIP(hipStreamSynchronize(G->be->dstream()));
+   auto link = std::make_unique<IpcLink>(*t);
+   // exchange the slot pools' handles with every outside peer
+   constexpr int HW = 8; // doubles per handle
+   static_assert(sizeof(hipIpcMemHandle_t) <= HW * sizeof(double), "IPC handle size");
+   const CommClass &sd = G->send, &rd = G->recv;
+   std::vector<std::vector<double>> sb(sd.procs.size(), std::vector<double>(HW, 0.0)),
+      rb(rd.procs.size(), std::vector<double>(HW, 0.0));
+   std::vector<long long> reqs;
+   for (size_t i = 0; i < rd.procs.size(); i++) {
+      long long q;
+      AMG_TRY(xp(t->irecv(t->user, rd.procs[i], IPC_HANDLE_TAG, rb[i].data(), HW, &q), "irecv"));
+      reqs.push_back(q);
+   }
+   for (size_t i = 0; i < sd.procs.size(); i++) {
+      hipIpcMemHandle_t h;
+      AMG_HIP(hipIpcGetMemHandle(&h, sd.dpool[i]));
+      std::memcpy(sb[i].data(), &h, sizeof h);
+      long long q;
+      AMG_TRY(xp(t->isend(t->user, sd.procs[i], IPC_HANDLE_TAG, sb[i].data(), HW, &q), "isend"));
+      reqs.push_back(q);
+   }
+   for (long long q : reqs) AMG_TRY(xp(t->wait(t->user, q), "wait"));
+   for (size_t i = 0; i < rd.procs.size(); i++) {
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, rb[i].data(), sizeof h);
+      void *p = nullptr;
+      AMG_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+      link->opened.push_back(p);
+      link->peers[rd.procs[i]] = IpcLink::Peer{(const double *)p, (long long)std::max(1, rd.len[i])};
+   }
+   G->link = std::move(link);
    *out = G.release();
    return AMG_OK;
 }

@@ -9,7 +9,9 @@ The protocol needs a non-blocking transport with MPI point-to-point semantics
   * TorchNbTransport -- ranks as processes over torch.distributed (gloo on the
     host: isend / irecv / Work.is_completed, all_reduce over the grid's group).
 DevHub (amg_devhub) replaces the transport for ranks as threads of one
-process: the correction payloads stay in device memory end to end.
+process, and GridAdd(..., ipc=True) keeps the payloads on the device across
+processes (IPC-mapped slots; the transport carries control words only): the
+correction payloads stay in device memory end to end.
 """
 import ctypes as C
 import threading
@@ -224,7 +226,7 @@ class GridAdd:
     hierarchy (`dist_hier`) or, with `diag` / `weight`, over the host model."""
 
     def __init__(self, transport, my_grid, world, rank, rank_grid, rank_rows, dist_hier=None, diag=None,
-                 weight=1.0, opts=None):
+                 weight=1.0, opts=None, ipc=False):
         self.t = transport
         self.rank_grid = np.ascontiguousarray(rank_grid, dtype=np.int32)
         self.rank_rows = np.ascontiguousarray(rank_rows, dtype=np.int64)
@@ -233,6 +235,12 @@ class GridAdd:
         rr = self.rank_rows.ctypes.data_as(C.POINTER(C.c_longlong))
         if dist_hier is not None and isinstance(transport, DevHub):
             st = lib.amg_grid_add_create_devhub(dist_hier.h, my_grid, world, rank, rg, rr, transport.h, C.byref(h))
+            self.n = dist_hier.n0
+        elif dist_hier is not None and ipc:
+            # device-resident payloads across processes: the transport carries
+            # the IPC handles (here, collectively), control words and acks
+            st = lib.amg_grid_add_create_ipc(dist_hier.h, my_grid, world, rank, rg, rr, C.byref(transport.c),
+                                             C.byref(h))
             self.n = dist_hier.n0
         elif dist_hier is not None:
             st = lib.amg_grid_add_create(dist_hier.h, my_grid, world, rank, rg, rr, C.byref(transport.c), C.byref(h))

@@ -671,6 +671,16 @@ int amg_devhub_free(amg_devhub *hub); /* after every grid_add using it is freed 
 int amg_grid_add_create_devhub(amg_dist_hier *D, int my_grid, int world_nranks, int world_rank,
                                const int *rank_grid, const long long *rank_rows, amg_devhub *hub,
                                amg_grid_add **out);
+/* Device-resident messages across processes (one per GPU, or several on one GPU):
+ * every send slot pool is mapped into its receiver once (hipIpcGetMemHandle /
+ * hipIpcOpenMemHandle, the handles exchanged over t here -- all ranks call this
+ * together).  Per message t carries a control pair (slot index, done flag), sent
+ * once the slot's write has run, and an acknowledgement back once the
+ * receiver's kernel has read the slot in place; the send completes with the
+ * acknowledgement.  The payload never leaves device memory. */
+int amg_grid_add_create_ipc(amg_dist_hier *D, int my_grid, int world_nranks, int world_rank,
+                            const int *rank_grid, const long long *rank_rows, const amg_nb_transport *t,
+                            amg_grid_add **out);
 /* DMEM_Add, asynchronous branch: b / x (in: x0, out: x) are this rank's rows of
  * its grid's partition; *cycles = cycles run, *relres = ||b - A x|| / ||b - A x0||
  * over the grid after AsyncRecvCleanup, messages[2] = sent, received */

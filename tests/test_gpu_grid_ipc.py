@@ -1,0 +1,115 @@
+"""Level-grouped asynchronous additive solve (DMEM_Add, csrc/amg_grid.cpp) with
+its ranks as PROCESSES on one GPU: the correction payloads stay in device
+memory across processes (amg_grid_add_create_ipc: every send slot pool is
+mapped into its receiver by hipIpcGetMemHandle / hipIpcOpenMemHandle; gloo
+carries only the handles, the (slot, done flag) control words and the
+acknowledgements), against the same solve with the payloads over gloo
+(amg_grid_add_create: D2H / H2D per message).  One grid per level, one rank
+per grid; asynchronous, so checked as the oracle's async band (tests/async_band.py):
+every grid's final relative residual in [0.5 x min, 2 x max], every message
+sent received."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N = 20
+
+
+NX = 24  # the full 24^3 hierarchy (5 levels, 5 grids): its coarsest grid's exact
+# solve is small, as in the oracle band's SMEM_Async_Add_AMG, where the coarsest
+# level does not correct (its solve is commented out, SMEM_Async_AMG.cpp:112-132)
+
+
+def _host(amg, oracle):
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, NX, amg.AMG_INTERP_LINEAR)
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs = oracle.smooth_transfer(host["A"][lev], host["P"][lev], 0.8)
+        Ps.append(ps)
+        Rs.append(rs)
+    return L, {"A": host["A"], "P": Ps, "R": Rs}, amg.rhs_rand(0, NX ** 3)
+
+
+def _opts(amg):
+    return amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=0.8, tol=0.0, num_cycles=N,
+                            max_inflight=2, converge_test_type=amg.AMG_LOCAL)
+
+
+def _rank(rank, world, port, ipc, q):
+    try:
+        import sys
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path.insert(0, here)
+        from conftest import load_package
+        from oracle import pyoracle as oracle
+        from test_gpu_dist import split_host
+        amg = load_package()
+        L, host, f = _host(amg, oracle)
+        assert L == world
+        rank_grid, rank_rows = amg.grid.layout((1,) * L, NX ** 3)
+        groups = {g: dist.new_group([r for r in range(world) if rank_grid[r] == g]) for g in range(L)}
+        my = int(rank_grid[rank])
+        rs, parts = split_host(host, ())
+        c = amg.Context(0, nstreams=2)
+        amg.dist.init_host(c, 1, 0, amg.dist.HostTransport(amg.dist.ThreadMailbox(1), 0))
+        A, P, R = parts[0]
+        D = amg.dist.DistHier.from_parts(c, rs, A, P, R, _opts(amg))
+        T = amg.grid.TorchNbTransport(groups[my])
+        G = amg.grid.GridAdd(T, my, world, rank, rank_grid, rank_rows, dist_hier=D, ipc=ipc)
+        dist.barrier()  # the ranks enter DMEM_Add together
+        x, cyc, rel, msgs = G.solve(f)
+        G.free()
+        dist.barrier()  # no rank unmaps a pool another still reads
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        dist.destroy_process_group()
+        q.put((rank, bool(np.all(np.isfinite(x))), cyc, rel, int(msgs[0]), int(msgs[1])))
+    except BaseException as ex:  # noqa: BLE001
+        q.put((rank, repr(ex)))
+
+
+@pytest.mark.parametrize("transport", ["ipc", "host"])
+def test_grid_add_processes(amg, oracle, transport):
+    import multiprocessing as mp
+    from async_band import in_band, oracle_async_band
+    L, host, f = _host(amg, oracle)
+    world = L
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank, args=(r, world, port, transport == "ipc", q), daemon=True)
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            item = q.get(timeout=150)
+            out[item[0]] = item
+    finally:
+        for p in ps:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    lo, hi, _, _ = oracle_async_band(amg, oracle, host, f, _opts(amg))
+    print(f"grid add processes {transport} L={L}: oracle band [{lo:.4e}, {hi:.4e}], "
+          f"ranks (finite, cycles, rel, sent, received) {[out[r][1:] for r in sorted(out)]}")
+    for r in range(world):
+        item = out[r]
+        assert len(item) == 6, item
+        _, finite, cyc, rel, sent, recv = item
+        assert finite and cyc >= N, item
+        assert in_band(rel, lo, hi), (item, lo, hi)
+    assert sum(out[r][4] for r in range(world)) == sum(out[r][5] for r in range(world))
