@@ -23,12 +23,15 @@ from test_gpu_solve import oracle_opts
 
 
 def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blocks=None, lockstep=True,
-                      sequential=False):
+                      sequential=False, lockstep_cycles=()):
     """res_compute_type GLOBAL (ASYNC_MULTADD): no level-0 group (thread sets
     [0, 1, ..] / [0, 2, ..]) and no synchronous equivalent, so no lockstep
     member; the sequential schedules are added instead.  accel_type (the
     distributed solve's ChebyUpdate per level, DMEM_Add.cpp:319-324) likewise
-    has no synchronous equivalent: sequential schedules, no lockstep."""
+    has no synchronous equivalent: sequential schedules, no lockstep.
+    lockstep_cycles: further equal-speed members with these cycle counts
+    (converge GLOBAL: the device's grids keep correcting until the slowest is
+    done, so the fastest may run many more than num_cycles corrections)."""
     """(lo, hi, rels, counts) of `reps` runs per thread set (rels[-1]: the
     synchronous schedule when lockstep); opts: the GPU run's
     amg_opts (solver ASYNC_MULTADD / ASYNC_AFACX, smoother, sweeps, num_cycles,
@@ -80,6 +83,14 @@ def oracle_async_band(amg, oracle, host, f, opts, reps=10, thread_sets=None, blo
                 SH.set_blocks(lev, blk)
         _, h, _ = SH.solve(f)
         rels.append(h[-1] / h[0])
+        for nc in lockstep_cycles:
+            so.num_cycles = int(nc)
+            XH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, so))
+            if blocks is not None:
+                for lev, blk in blocks.items():
+                    XH.set_blocks(lev, blk)
+            _, h, _ = XH.solve(f)
+            rels.append(h[-1] / h[0])
     return min(rels), max(rels), rels, counts
 
 
