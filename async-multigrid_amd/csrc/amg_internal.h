@@ -291,12 +291,20 @@ void geo_check(hipStream_t s, const amg_mat *M, int mode, const GeoT &g, int *ba
 // residual vector (bit-identical to the residual SpGEMV + R SpMV).  Slab form:
 // coarse planes [Kb, Ke) (Ke < 0: all), u / f plane 0 = fine plane fz0 (A's
 // rows are those vectors' planes), fc plane 0 = coarse plane cz0
+// the coarse level's zero-guess Jacobi sweep folded into a restriction: where
+// u != null, u[i] = w fc[i] / d[i] for d[i] != 0 (jacobi_zero variant 0, no L1)
+struct ZeroGuess {
+   const double *d = nullptr;
+   double w = 0.0;
+   double *u = nullptr;
+};
 void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, const double *u, const GeoT &g,
-                          const double *wdev, double *fc, int Kb = 0, int Ke = -1, int fz0 = 0, int cz0 = 0);
+                          const double *wdev, double *fc, int Kb = 0, int Ke = -1, int fz0 = 0, int cz0 = 0,
+                          ZeroGuess zg = ZeroGuess());
 // f_c = R r for the checked geometric R of GeoT g (bit-identical to the SpMV);
 // coarse planes [Kb, Ke), r plane 0 = fine plane fz0, fc plane 0 = coarse cz0
 void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc, int Kb = 0,
-                  int Ke = -1, int fz0 = 0, int cz0 = 0);
+                  int Ke = -1, int fz0 = 0, int cz0 = 0, ZeroGuess zg = ZeroGuess());
 // u += P e for the checked geometric P of GeoT g (bit-identical to the SpGEMV);
 // fine planes [zb, ze), u plane 0 = fine plane fz0, e plane 0 = coarse cz0
 void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u, int zb = 0,

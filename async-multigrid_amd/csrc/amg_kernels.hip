@@ -1497,12 +1497,23 @@ struct Val7 {
 // barrier per plane, so the four waves march loosely coupled
 constexpr int AMG_RR_RING = 4;
 
+// ZeroGuess epilogue of a restriction: the coarse level's first pre-smoothing
+// sweep from a zero guess, u = w f / a (jacobi_zero_k variant 0, same
+// expression, a == 0 rows untouched), from the restricted value in registers
+__device__ __forceinline__ void zg_apply(const ZeroGuess &zg, long long i, double fv)
+{
+   if (zg.u) {
+      const double a = zg.d[i];
+      if (a != 0.0) zg.u[i] = zg.w * fv / a;
+   }
+}
+
 template <bool UNI, int LC, int OCC = 1, bool RING = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void mz_res_restrict_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, Val7 Sv7, const double *__restrict__ x, const double *__restrict__ f,
    const double *__restrict__ wg, int nx, int ny, int nz, int zcc, int nlb, int xcd, int ntf,
-   double *__restrict__ fc, int Kb, int Ke, int fz0, int cz0, int nzm)
+   double *__restrict__ fc, int Kb, int Ke, int fz0, int cz0, int nzm, ZeroGuess zg)
 {
    // coarse planes [Kb, Ke) of the nx * ny * nz box; x / f (and the pattern
    // bytes) hold nzm planes from fine plane fz0, fc's plane 0 is coarse plane
@@ -1668,11 +1679,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
          const long long ci = ((long long)(Ky0 + c)) * lpl + cx;
          if (k & 1) {
             add(c, 1);
-            if (k + 1 >= nz) fc[(long long)(Kz - cz0) * ncy * lpl + ci] = acc[c];
+            if (k + 1 >= nz) {
+               fc[(long long)(Kz - cz0) * ncy * lpl + ci] = acc[c];
+               zg_apply(zg, (long long)(Kz - cz0) * ncy * lpl + ci, acc[c]);
+            }
          } else {
             if (k > kf0) {
                add(c, 2);
                fc[(long long)(Kz - 1 - cz0) * ncy * lpl + ci] = acc[c];
+               zg_apply(zg, (long long)(Kz - 1 - cz0) * ncy * lpl + ci, acc[c]);
             }
             if (Kz < Kc1) {
                acc[c] = 0.0;
@@ -1684,7 +1699,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 }
 
 void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, const double *u, const GeoT &g,
-                          const double *wdev, double *fc, int Kb, int Ke, int fz0, int cz0)
+                          const double *wdev, double *fc, int Kb, int Ke, int fz0, int cz0, ZeroGuess zg)
 {
    if (Ke < 0) Ke = g.nz / 2;
    if (Ke <= Kb) return;
@@ -1701,7 +1716,7 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
 #define AMG_RR(U, L, ...) \
    mz_res_restrict_kernel<U, L, ##__VA_ARGS__><<<nb, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, f, wdev, g.nx, g.ny, \
-                                                   g.nz, zcc, nlb, xcd, stream_hint(A), fc, Kb, Ke, fz0, cz0, nzm)
+                                                   g.nz, zcc, nlb, xcd, stream_hint(A), fc, Kb, Ke, fz0, cz0, nzm, zg)
    if (A->mp_uni) {
       if (LC == 2) AMG_RR(true, 2);
       else if (A->ctx->rr_occ == 5) AMG_RR(true, 1, 5);
@@ -1827,12 +1842,125 @@ __global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ 
    *reinterpret_cast<v2du *>(ui) = geo_prolong_pair(acc, e, wl, x, y, z, nx >> 1, ny >> 1, nz >> 1, cz0);
 }
 
+// coarse candidates of fine coordinate y on an axis of nc coarse points, in
+// ascending order: (y - 1) / 2 (d 1) when odd; y / 2 - 1 (d 2) and y / 2 (d 0)
+// when even, inside [0, nc).  Constant-index stores only (a runtime-indexed
+// store would put the arrays in scratch); an absent second candidate repeats
+// the first
+__device__ __forceinline__ void line_cands(int y, int nc, int &m, int (&c)[2], int (&d)[2])
+{
+   if (y & 1) {
+      m = 1, c[0] = c[1] = (y - 1) >> 1, d[0] = d[1] = 1;
+   } else if (y >= 2) {
+      c[0] = (y >> 1) - 1, d[0] = 2;
+      const bool h = (y >> 1) < nc;
+      m = h ? 2 : 1, c[1] = h ? y >> 1 : c[0], d[1] = h ? 0 : 2;
+   } else {
+      m = (y >> 1) < nc ? 1 : 0, c[0] = c[1] = y >> 1, d[0] = d[1] = 0;
+   }
+}
+
+// The same prolongation as a plane march: a lane owns one fine pair (x = 2t,
+// 2t + 1, y) and walks fine planes [z0, z1) of its chunk.  Fine planes 2c and
+// 2c + 1 read coarse plane c (and 2c plane c - 1 too), so a lane loads each
+// coarse plane's e[t - 1], e[t] of its (one or two) coarse lines once, at the
+// even plane, and keeps the last two in registers: <= 1 coarse 16-byte load
+// per fine pair and plane instead of geo_prolong_k's 4.  u of plane z + 1 is
+// loaded before plane z is stored.  Terms and order as geo_prolong_pair
+// (bit-identical).  Workgroups are mapped XCD-contiguously (csr_mz_kernel).
+__global__ __launch_bounds__(256) void geo_prolong_march_k(const double *__restrict__ e, double *__restrict__ u,
+                                                           const double *__restrict__ wg, int nx, int ny, int nz,
+                                                           int zb, int ze, int fz0, int cz0, int zc, int nseg,
+                                                           int xcd)
+{
+   __shared__ double wl[27];
+   const int tid = (int)threadIdx.x;
+   if (tid < 27) wl[tid] = wg[tid];
+   __syncthreads();
+   const int G = (int)gridDim.x;
+   int lg = (int)blockIdx.x;
+   if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
+   const int seg = lg % nseg, chunk = lg / nseg;
+   const unsigned ph = (unsigned)nx >> 1, npp = ph * (unsigned)ny; // pairs per line / plane
+   const unsigned pp = (unsigned)seg * 256u + (unsigned)tid;
+   const int z0 = zb + chunk * zc, z1 = min(z0 + zc, ze);
+   if (pp >= npp || z0 >= z1) return;
+   const int t = (int)(pp % ph), y = (int)(pp / ph);
+   const int ncx = nx >> 1, ncy = ny >> 1, ncz = nz >> 1;
+   int cy[2], dy[2], my;
+   line_cands(y, ncy, my, cy, dy);
+   const bool lo = t >= 1, hi = t < ncx;
+   const long long fpl = (long long)nx * ny, cpl = (long long)ncx * ncy;
+   // this lane's e[t - 1] (clamped to e[t] at t = 0) on coarse lines cy[0], cy[1] of plane 0
+   const double *eb0 = e + (long long)cy[0] * ncx + (lo ? t - 1 : t);
+   const double *eb1 = e + (long long)cy[1] * ncx + (lo ? t - 1 : t);
+   auto load_c = [&](int c, v2d (&ev)[2]) {
+      const long long o = (long long)(c - cz0) * cpl;
+      ev[0] = *reinterpret_cast<const v2du *>(eb0 + o);
+      ev[1] = *reinterpret_cast<const v2du *>(eb1 + o);
+   };
+   auto add_plane = [&](v2d acc, const v2d (&ev)[2], int d) {
+#pragma unroll
+      for (int b = 0; b < 2; b++) {
+         if (b >= my) break;
+         const double em = lo ? ev[b].x : 0.0, ec = lo ? ev[b].y : ev[b].x;
+         const double *w = wl + d * 9 + dy[b] * 3;
+         if (lo) acc.x = acc.x + w[2] * em;
+         if (hi) acc.x = acc.x + w[0] * ec;
+         acc.y = acc.y + w[1] * ec;
+      }
+      return acc;
+   };
+   v2d eprev[2], ecur[2];
+   // coarse planes held on entry: z0 odd -> (z0 - 1) / 2; z0 even -> z0 / 2 - 1 (as
+   // the "current" plane; the loop's even step shifts it to "previous")
+   if (z0 & 1) {
+      load_c((z0 - 1) >> 1, ecur);
+   } else if (z0 >= 2) {
+      load_c((z0 >> 1) - 1, ecur);
+   }
+   double *up = u + (long long)(z0 - fz0) * fpl + (long long)y * nx + 2 * t;
+   v2d uc = *reinterpret_cast<const v2du *>(up);
+   for (int z = z0; z < z1; z++, up += fpl) {
+      v2d un{0.0, 0.0};
+      if (z + 1 < z1) un = *reinterpret_cast<const v2du *>(up + fpl);
+      v2d acc = uc;
+      if (z & 1) {
+         acc = add_plane(acc, ecur, 1);
+      } else {
+         eprev[0] = ecur[0], eprev[1] = ecur[1];
+         const bool has_lo = z >= 2, has_hi = (z >> 1) < ncz;
+         if (has_hi) load_c(z >> 1, ecur);
+         if (has_lo) acc = add_plane(acc, eprev, 2);
+         if (has_hi) acc = add_plane(acc, ecur, 0);
+      }
+      *reinterpret_cast<v2du *>(up) = acc;
+      uc = un;
+   }
+}
+
 void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u, int zb, int ze,
                  int fz0, int cz0)
 {
    if (ze < 0) ze = g.nz;
    const long long np = (long long)g.nx * g.ny * (ze - zb) / 2;
    if (np <= 0) return;
+   static const int march = [] {
+      const char *v = std::getenv("AMG_PROLONG_MARCH");
+      return v ? std::atoi(v) : 1;
+   }();
+   const long long npp = (long long)g.nx * g.ny / 2;
+   if (march && (g.nx & 1) == 0 && npp >= 256 && npp < (1LL << 31)) {
+      // fine planes per chunk: 16, fewer when the launch would have < 2048 workgroups
+      const int nseg = (int)((npp + 255) / 256);
+      const int nzl = ze - zb;
+      int zc = 16;
+      while (zc > 2 && (long long)nseg * ((nzl + zc - 1) / zc) < 2048) zc >>= 1;
+      const long long G = (long long)nseg * ((nzl + zc - 1) / zc);
+      geo_prolong_march_k<<<(unsigned)G, 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, zb, ze, fz0, cz0, zc, nseg,
+                                                        1);
+      return;
+   }
    geo_prolong_k<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, np, zb, fz0, cz0);
 }
 
@@ -2126,7 +2254,7 @@ void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const do
 // plane 0 coarse plane cz0 (z-slab vectors)
 __global__ __launch_bounds__(256) void geo_restrict_k(const double *__restrict__ r, double *__restrict__ fc,
                                                       const double *__restrict__ wg, int nx, int ny, int nz,
-                                                      long long nc, int Kb, int fz0, int cz0)
+                                                      long long nc, int Kb, int fz0, int cz0, ZeroGuess zg)
 {
    __shared__ double wl[27];
    const int tid = (int)threadIdx.x;
@@ -2175,16 +2303,18 @@ __global__ __launch_bounds__(256) void geo_restrict_k(const double *__restrict__
          if (dx2) acc = acc + w[2] * c[dz][dy];
       }
    }
-   fc[((long long)(Kz - cz0) * ncy + Ky) * ncx + Kx] = acc;
+   const long long ci = ((long long)(Kz - cz0) * ncy + Ky) * ncx + Kx;
+   fc[ci] = acc;
+   zg_apply(zg, ci, acc);
 }
 
 void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc, int Kb, int Ke,
-                  int fz0, int cz0)
+                  int fz0, int cz0, ZeroGuess zg)
 {
    if (Ke < 0) Ke = g.nz / 2;
    const long long nc = (long long)(g.nx / 2) * (g.ny / 2) * (Ke - Kb);
    if (nc <= 0) return;
-   geo_restrict_k<<<(unsigned)((nc + 255) / 256), 256, 0, s>>>(r, fc, wdev, g.nx, g.ny, g.nz, nc, Kb, fz0, cz0);
+   geo_restrict_k<<<(unsigned)((nc + 255) / 256), 256, 0, s>>>(r, fc, wdev, g.nx, g.ny, g.nz, nc, Kb, fz0, cz0, zg);
 }
 
 // dictionary-coded launches: rows of <= 8 entries (7-pt stencil, interpolation)

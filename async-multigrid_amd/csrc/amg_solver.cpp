@@ -37,6 +37,7 @@ struct Level {
    std::vector<int> blk;
    int *d_blk = nullptr;
    int zero_flag = 0;
+   bool zero_done = false; // the zero-guess sweep already written by the restriction into this level
 };
 
 // per-level private vectors of the additive cycles (level_vector[k], SMEM_Setup.cpp:292-341)
@@ -491,7 +492,10 @@ static void smooth_one_level(amg_hier *H, hipStream_t s, int l, const double *f,
    const bool l1 = (o.smoother == AMG_L1_JACOBI);
    for (int k = 0; k < sweeps; k++) {
       if (k == 0 && zf == 1) {
-         amgk::jacobi_zero(s, v.A->diag, f, l1 ? v.l1 : nullptr, o.smooth_weight, v.u, 0, v.n, 0);
+         if (v.zero_done)
+            v.zero_done = false; // folded into the restriction that produced f (same bits)
+         else
+            amgk::jacobi_zero(s, v.A->diag, f, l1 ? v.l1 : nullptr, o.smooth_weight, v.u, 0, v.n, 0);
       } else if (k == 0 && from_outer_residual && H->pre_ready) {
          // the outer-residual kernel already produced u + w r / a_ii from this
          // very u and r = f - A u (same summation order): take it
@@ -566,16 +570,31 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
    const amgk::Gemv res_mode = amgk::gemv_mode(-1.0, 1.0);
    const amgk::Gemv mv_mode = amgk::gemv_mode(1.0, 0.0);
    const amgk::Gemv pro_mode = amgk::gemv_mode(1.0, 1.0);
+   static const bool zg_fold = [] {
+      const char *e = std::getenv("AMG_ZG_FOLD");
+      return e ? std::atoi(e) != 0 : true;
+   }();
    for (int l = 0; l < L - 1; l++) {
       Level &v = H->lv[l];
       v.zero_flag = 1;
       if (l == 0 && !precond) v.zero_flag = 0;
       const double *f_fine = (l == 0 && precond) ? H->r0 : v.f;
       smooth_one_level(H, s, l, f_fine, o.num_pre_smooth_sweeps, l == 0 && reuse_r0);
+      // level l + 1 (not the coarsest) starts its pre-smoothing with the
+      // zero-guess Jacobi sweep u = w f / a: a geometric restriction writes it
+      // together with f (one pass over the coarse level fewer)
+      Level &nx = H->lv[l + 1];
+      amgk::ZeroGuess zg;
+      if (zg_fold && l + 1 < L - 1 && o.smoother == AMG_JACOBI && o.num_pre_smooth_sweeps >= 1) {
+         zg.d = nx.A->diag;
+         zg.w = o.smooth_weight;
+         zg.u = nx.u;
+      }
       if (l == 0 && H->geo0) {
          // level-0 residual and restriction in one pass (no r_fine vector)
          ProfScope ps(H, PROF_FINE_SPMV, s);
-         amgk::mz_residual_restrict(s, v.A, f_fine, v.u, H->gl[0], H->d_geo_w[0], H->lv[1].f);
+         amgk::mz_residual_restrict(s, v.A, f_fine, v.u, H->gl[0], H->d_geo_w[0], nx.f, 0, -1, 0, 0, zg);
+         nx.zero_done = zg.u != nullptr;
          continue;
       }
       {
@@ -584,8 +603,10 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
       }
       {
          ProfScope ps(H, PROF_RESTRICT0, s, l == 0);
-         if (H->geo[l])
-            amgk::geo_restrict(s, H->gl[l], H->d_geo_w[l], v.r_fine, H->lv[l + 1].f);
+         if (H->geo[l]) {
+            amgk::geo_restrict(s, H->gl[l], H->d_geo_w[l], v.r_fine, nx.f, 0, -1, 0, 0, zg);
+            nx.zero_done = zg.u != nullptr;
+         }
          else
             amgk::spgemv(s, v.R, v.r_fine, nullptr, mv_mode, H->lv[l + 1].f, 0, H->lv[l + 1].n,
                          nullptr);
