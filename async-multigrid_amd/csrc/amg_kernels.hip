@@ -1868,6 +1868,7 @@ __device__ __forceinline__ void line_cands(int y, int nc, int &m, int (&c)[2], i
 // per fine pair and plane instead of geo_prolong_k's 4.  u of plane z + 1 is
 // loaded before plane z is stored.  Terms and order as geo_prolong_pair
 // (bit-identical).  Workgroups are mapped XCD-contiguously (csr_mz_kernel).
+template <int PF>
 __global__ __launch_bounds__(256) void geo_prolong_march_k(const double *__restrict__ e, double *__restrict__ u,
                                                            const double *__restrict__ wg, int nx, int ny, int nz,
                                                            int zb, int ze, int fz0, int cz0, int zc, int nseg,
@@ -1920,11 +1921,14 @@ __global__ __launch_bounds__(256) void geo_prolong_march_k(const double *__restr
       load_c((z0 >> 1) - 1, ecur);
    }
    double *up = u + (long long)(z0 - fz0) * fpl + (long long)y * nx + 2 * t;
-   v2d uc = *reinterpret_cast<const v2du *>(up);
+   // PF u pairs in flight ahead of the plane being stored
+   v2d uq[PF];
+#pragma unroll
+   for (int i = 0; i < PF; i++) uq[i] = z0 + i < z1 ? *reinterpret_cast<const v2du *>(up + i * fpl) : v2d{0.0, 0.0};
    for (int z = z0; z < z1; z++, up += fpl) {
       v2d un{0.0, 0.0};
-      if (z + 1 < z1) un = *reinterpret_cast<const v2du *>(up + fpl);
-      v2d acc = uc;
+      if (z + PF < z1) un = *reinterpret_cast<const v2du *>(up + PF * fpl);
+      v2d acc = uq[0];
       if (z & 1) {
          acc = add_plane(acc, ecur, 1);
       } else {
@@ -1935,7 +1939,9 @@ __global__ __launch_bounds__(256) void geo_prolong_march_k(const double *__restr
          if (has_hi) acc = add_plane(acc, ecur, 0);
       }
       *reinterpret_cast<v2du *>(up) = acc;
-      uc = un;
+#pragma unroll
+      for (int i = 0; i + 1 < PF; i++) uq[i] = uq[i + 1];
+      uq[PF - 1] = un;
    }
 }
 
@@ -1949,16 +1955,29 @@ void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double 
       const char *v = std::getenv("AMG_PROLONG_MARCH");
       return v ? std::atoi(v) : 1;
    }();
+   // tuning switches: planes per chunk (16) and u pairs in flight (1)
+   static const int zc0 = [] {
+      const char *v = std::getenv("AMG_PROLONG_ZC");
+      return v ? std::max(2, std::min(64, std::atoi(v))) : 16;
+   }();
+   static const int pf = [] {
+      const char *v = std::getenv("AMG_PROLONG_PF");
+      return v && std::atoi(v) == 2 ? 2 : 1;
+   }();
    const long long npp = (long long)g.nx * g.ny / 2;
    if (march && (g.nx & 1) == 0 && npp >= 256 && npp < (1LL << 31)) {
       // fine planes per chunk: 16, fewer when the launch would have < 2048 workgroups
       const int nseg = (int)((npp + 255) / 256);
       const int nzl = ze - zb;
-      int zc = 16;
+      int zc = zc0;
       while (zc > 2 && (long long)nseg * ((nzl + zc - 1) / zc) < 2048) zc >>= 1;
       const long long G = (long long)nseg * ((nzl + zc - 1) / zc);
-      geo_prolong_march_k<<<(unsigned)G, 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, zb, ze, fz0, cz0, zc, nseg,
-                                                        1);
+      if (pf == 2)
+         geo_prolong_march_k<2><<<(unsigned)G, 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, zb, ze, fz0, cz0, zc, nseg,
+                                                            1);
+      else
+         geo_prolong_march_k<1><<<(unsigned)G, 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, zb, ze, fz0, cz0, zc, nseg,
+                                                            1);
       return;
    }
    geo_prolong_k<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, np, zb, fz0, cz0);
