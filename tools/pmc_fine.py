@@ -17,7 +17,7 @@ KERNELS = {
     "outer_residual_sweep": (r"csr_mz_kernel<1, true, amgk::EpiResJacobi", lambda r: (r + 1) // 2 + 24 * r),
     "post_sweep": (r"csr_mz_kernel<1, true, amgk::EpiJacobi,", lambda r: (r + 1) // 2 + 24 * r),
     "residual_restrict": (r"mz_res_restrict_kernel", lambda r: (r + 1) // 2 + 16 * r + r),
-    "prolong0": (r"geo_prolong_k", lambda r: 16 * r + r),
+    "prolong0": (r"geo_prolong_(march_)?k", lambda r: 16 * r + r),
 }
 
 
