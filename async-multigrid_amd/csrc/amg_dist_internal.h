@@ -86,7 +86,6 @@ struct DLevel {
    DistMat A, P, R;            // P: level l -> l+1 (rows = level l), R: rows = level l+1
    double *f = nullptr, *u = nullptr, *u_alt = nullptr, *r_fine = nullptr, *l1 = nullptr;
    int zero_flag = 0;
-   bool zero_done = false; // slab V-cycle: the zero-guess sweep already written by the restriction
    // slab form
    SlabGeom sg;
    bool geo = false;   // R_l / P_l are the box's geometric transfers (checked)
@@ -228,8 +227,7 @@ const double *slab_diag(const DistMat &M);
 // or u += P_l x (add = true)
 using XchgFn = std::function<int(double *x, long long n_own, long long cP, const std::vector<int> &nlo,
                                  const std::vector<int> &nhi)>;
-int slab_restrict(amg_dist_hier *D, hipStream_t s, int l, double *r, double *dst, const XchgFn &xchg,
-                  amgk::ZeroGuess zg = amgk::ZeroGuess());
+int slab_restrict(amg_dist_hier *D, hipStream_t s, int l, double *r, double *dst, const XchgFn &xchg);
 int slab_prolong(amg_dist_hier *D, hipStream_t s, int l, double *x, double *out, bool add, const XchgFn &xchg);
 // sync cycle pieces of slab hierarchies (amg_dist.cpp dispatches to them)
 int slab_vcycle(amg_dist_hier *D, bool precond);
