@@ -25,7 +25,8 @@ from .abi import (AMG_JACOBI, AMG_GAUSS_SEIDEL, AMG_HYBRID_JGS, AMG_SYMM_JACOBI,
                   AMG_ASYNC_GS, AMG_SEMI_ASYNC_GS, AMG_BPX, AMG_NO_ACCEL, AMG_RICHARD_ACCEL,
                   AMG_CHEBY_RECUR_ACCEL, AMG_FULL_ASYNC, AMG_SEMI_ASYNC, AMG_LOCAL, AMG_GLOBAL,
                   AMG_READ_SOL, AMG_READ_RES, AMG_DELAY_NONE, AMG_DELAY_ONE, AMG_DELAY_SOME,
-                  AMG_DELAY_ALL, AMG_FAIL_ONE, AMG_SPS_EXPONENTIAL, AMG_SPS_INVERSE, AMG_SPS_RANDOM)
+                  AMG_DELAY_ALL, AMG_FAIL_ONE, AMG_SPS_EXPONENTIAL, AMG_SPS_INVERSE, AMG_SPS_RANDOM,
+                  AMG_SCHED_FREE, AMG_SCHED_FINEST_FIRST, AMG_SCHED_COARSEST_FIRST, AMG_SCHED_ROUND_ROBIN)
 
 lib = abi.load()
 

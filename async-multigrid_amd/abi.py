@@ -53,9 +53,11 @@ class AmgOpts(C.Structure):
                 ("delay_type", _i), ("delay_usec", _i), ("delay_frac", _d), ("fail_iter", _i),
                 ("delay_rank", _i), ("max_inflight", _i), ("async_comm_save_divisor", _i),
                 ("sps_probability_type", _i), ("sps_alpha", _d), ("sps_min_prob", _d),
-                ("delay_level", _i)]
+                ("delay_level", _i), ("async_schedule", _i),
+                ("smooth_transfer", _i)]
 
 
+AMG_SCHED_FREE, AMG_SCHED_FINEST_FIRST, AMG_SCHED_COARSEST_FIRST, AMG_SCHED_ROUND_ROBIN = 0, 1, 2, 3
 AMG_DELAY_NONE, AMG_DELAY_ONE, AMG_DELAY_SOME, AMG_DELAY_ALL, AMG_FAIL_ONE = 0, 1, 2, 3, 4
 AMG_SPS_EXPONENTIAL, AMG_SPS_INVERSE, AMG_SPS_RANDOM = 0, 1, 2
 

@@ -119,6 +119,7 @@ extern "C" int amg_finalize(amg_ctx *c)
    if (!c) return AMG_OK;
    hipSetDevice(c->device);
    hipStreamSynchronize(c->stream);
+   if (c->comm_stream) hipStreamSynchronize(c->comm_stream);
    for (auto s : c->level_streams) {
       hipStreamSynchronize(s);
       hipStreamDestroy(s);

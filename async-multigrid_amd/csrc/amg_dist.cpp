@@ -883,6 +883,7 @@ extern "C" int amg_dist_hier_free(amg_dist_hier *D)
    hipStreamSynchronize(D->ctx->stream);
    hipStreamSynchronize(D->ctx->comm_stream);
    for (auto s : D->ctx->level_streams) hipStreamSynchronize(s);
+   if (D->links) link_free(D->links); // collective (a barrier between unmapping and freeing)
    for (auto *a : {&D->grid.al}) {
       if (a->ev_ready) hipEventDestroy(a->ev_ready);
       if (a->ev_done) hipEventDestroy(a->ev_done);

@@ -17,23 +17,31 @@
 //   * it then recomputes its private residual f - A u_k from the value of u it
 //     observed at its own update (LOCAL residual, SMEM_Async_AMG.cpp:284-301);
 //   * every operator application of level k exchanges its ghost rows with the
-//     neighbouring slabs over RCCL point-to-point.  All exchanges of all levels
-//     go through ONE communicator on ONE communication stream, in the host's
-//     issue order (cycle-major, level-minor, the same on every rank): level
-//     k's stream packs its send buffer and records an event, the comm stream
-//     waits on it, runs the grouped send/recv and records completion, level
-//     k's stream waits on that.  Every RCCL operation thus has the same
-//     position in one sequence on every rank, so no cross-rank ordering of
-//     concurrent communicators (nor the multiplexing of level streams onto
-//     the 4 hardware queues) can deadlock; the compute of the levels still
-//     overlaps freely (DMEM_Comm.cpp:81-348 likewise drives every message
-//     class through one MPI communicator);
+//     neighbouring ranks through level k's OWN device-resident channels
+//     (amg_link.cpp: the sender's copy kernel writes the ghost rows straight
+//     into a slot of the receiver's memory, sequence words in host memory,
+//     polled by the receiving level's host thread -- the MPI_Test analogue of
+//     DMEM_Comm.cpp:81-348), and each level group runs its correction loop on
+//     its own host thread: level k on rank r waits only for level k on the
+//     ranks it exchanges with, as each DMEM grid does within its own
+//     communicator, never for another level (no shared comm stream, no
+//     head-of-line coupling; DMEM_Smooth.cpp:165-269 likewise moves ghost data
+//     independently of the other message classes);
 //   * levels below the replication threshold are computed redundantly on every
-//     rank after one allgather of the restricted residual.
+//     rank after an allgather of the restricted residual, also over level k's
+//     channels.
+// ASYNC_MULTADD may use the reference's smoothed transfers (smooth_transfer:
+// P~ = (I - w D^-1 A) P, R~ = P~^T, SmoothTransfer SMEM_Setup.cpp:1173-1254),
+// composed on the fly from the slab operators (R~ r = R (r - w A D^-1 r)).
 // Termination: each level performs num_cycles corrections (LOCAL convergence,
-// fixed count), then the streams join and the outer residual is formed.
+// fixed count), then the threads join and the outer residual is formed.  A
+// deterministic schedule (async_schedule) runs the level corrections on one
+// host thread and one stream, in the oracle's order (bit-identical to
+// or_async_add under or_set_async_schedule).
 #include <algorithm>
 #include <cmath>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "amg_dist_internal.h"
@@ -74,8 +82,9 @@ int from_comm(amg_dist_hier *D, AsyncLevel &a)
    return AMG_OK;
 }
 
-// ghost exchange of x for M: packed on the level stream, sent / received on
-// the comm stream over the main communicator
+// ghost exchange of x for M: packed on the level stream; through the level's
+// device-resident channels (D->links, the asynchronous solve) or, for the
+// level-grouped solve's grid, sent / received on the comm stream
 int a_halo(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x)
 {
    if (M.slab) {
@@ -87,6 +96,14 @@ int a_halo(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x)
    if (!sb) AMG_TRY(dvec(D, std::max<long long>(1, M.nsend), &sb));
    launch_gather(a.s, x, M.d_send_idx, sb, (int)M.nsend);
    const int np = (int)M.peers.size();
+   if (D->links && a.k >= 0) {
+      for (int i = 0; i < np; i++)
+         if (M.scnt[i] > 0) AMG_TRY(link_send(D->links, a.k, M.peers[i], sb + M.soff[i], M.scnt[i], a.s));
+      for (int i = 0; i < np; i++)
+         if (M.rcnt[i] > 0)
+            AMG_TRY(link_recv(D->links, a.k, M.peers[i], x + M.ncol_own + M.roff[i], M.rcnt[i], a.s));
+      return AMG_OK;
+   }
    std::vector<void *> sp(np), rp(np);
    std::vector<long long> sbytes(np), rbytes(np);
    for (int i = 0; i < np; i++) {
@@ -115,6 +132,7 @@ int a_spgemv(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x, const doubl
 XchgFn level_xchg(amg_dist_hier *D, AsyncLevel &a)
 {
    return [D, &a](double *x, long long n, long long cP, const std::vector<int> &lo, const std::vector<int> &hi) {
+      if (D->links && a.k >= 0) return link_xchg_planes(D->links, a.k, a.s, x, n, cP, lo, hi);
       AMG_TRY(to_comm(D, a));
       AMG_TRY(slab_xchg(D->ctx, D->ctx->comm_stream, x, n, cP, lo, hi));
       return from_comm(D, a);
@@ -141,37 +159,69 @@ const double *l1_of(const amg_dist_hier *D, int l)
    return l < D->Ld ? D->lv[l].l1 : D->cl1[l - D->Ld];
 }
 
-// r[l+1] = R_l r[l] (SMEM_Sync_Parfor_Restrict / hypre MatvecT in AddCycle)
+// the MULTADD transfers are the smoothed ones, composed (smooth_transfer)
+bool composed(const amg_dist_hier *D)
+{
+   return D->o.smooth_transfer == 1 && (D->o.solver == AMG_ASYNC_MULTADD || D->o.solver == AMG_MULTADD);
+}
+
+// r[l+1] = R_l r[l] (SMEM_Sync_Parfor_Restrict / hypre MatvecT in AddCycle); with
+// composed smoothed transfers R~_l r = R_l (r - w A_l D_l^-1 r): t = r ./ a;
+// y = A t; t = r + (-w) y (the oracle's or_hier_set_composed_transfers order)
 int restrict_to(amg_dist_hier *D, AsyncLevel &a, int l)
 {
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    const int Ld = D->Ld;
-   if (D->slab && l + 1 < Ld) return slab_restrict(D, a.s, l, a.r[l], a.r[l + 1], level_xchg(D, a));
-   if (l + 1 < Ld) return a_spgemv(D, a, D->lv[l].R, a.r[l], nullptr, mv, a.r[l + 1]);
+   double *r = a.r[l];
+   if (composed(D)) {
+      const int n = level_n(D, l);
+      amgk::xfer_div(a.s, diag_of(D, l), r, a.xt, 0, n);
+      AMG_TRY(apply_A(D, a, l, a.xt, nullptr, mv, a.xy));
+      amgk::xfer_sub(a.s, D->o.smooth_weight, r, a.xy, a.xt, 0, n);
+      r = a.xt;
+   }
+   if (D->slab && l + 1 < Ld) return slab_restrict(D, a.s, l, r, a.r[l + 1], level_xchg(D, a));
+   if (l + 1 < Ld) return a_spgemv(D, a, D->lv[l].R, r, nullptr, mv, a.r[l + 1]);
    if (l + 1 == Ld) {
       const int R = D->ctx->xport->nranks;
       double *slot = a.gath + (size_t)D->gath_blk * R;
       if (D->slab)
-         AMG_TRY(slab_restrict(D, a.s, l, a.r[l], slot, level_xchg(D, a)));
+         AMG_TRY(slab_restrict(D, a.s, l, r, slot, level_xchg(D, a)));
       else
-         AMG_TRY(a_spgemv(D, a, D->lv[l].R, a.r[l], nullptr, mv, slot));
-      AMG_TRY(to_comm(D, a));
-      AMG_TRY(xp_allgather(D->ctx, D->ctx->comm_stream, slot, a.gath, (long long)D->gath_blk * 8));
-      AMG_TRY(from_comm(D, a));
+         AMG_TRY(a_spgemv(D, a, D->lv[l].R, r, nullptr, mv, slot));
+      if (R == 1 && a.k >= 0) {
+         // one rank: the allgather is a copy (no transport: the level threads
+         // must not share the communicator)
+         amgk::vcopy(a.s, slot, a.gath, 0, D->gath_blk);
+      } else if (D->links && a.k >= 0) {
+         AMG_TRY(link_allgather(D->links, a.k, a.s, slot, a.gath, D->gath_blk));
+      } else {
+         AMG_TRY(to_comm(D, a));
+         AMG_TRY(xp_allgather(D->ctx, D->ctx->comm_stream, slot, a.gath, (long long)D->gath_blk * 8));
+         AMG_TRY(from_comm(D, a));
+      }
       launch_scatter_blocks(a.s, a.gath, D->gath_blk, D->d_gcnt, D->d_gdsp, R, a.r[l + 1]);
       return AMG_OK;
    }
-   amgk::spgemv(a.s, D->cR[l - Ld], a.r[l], nullptr, mv, a.r[l + 1], 0, level_n(D, l + 1), nullptr);
+   amgk::spgemv(a.s, D->cR[l - Ld], r, nullptr, mv, a.r[l + 1], 0, level_n(D, l + 1), nullptr);
    return AMG_OK;
 }
 
-// out = P_l x (x on level l+1, out on level l)
+// out = P_l x (x on level l+1, out on level l); composed smoothed transfers:
+// out = P x;  y = A out;  out = out + (-w) (y ./ a)
 int prolong_to(amg_dist_hier *D, AsyncLevel &a, int l, double *x, double *out)
 {
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
-   if (D->slab && l < D->Ld) return slab_prolong(D, a.s, l, x, out, false, level_xchg(D, a));
-   if (l < D->Ld) return a_spgemv(D, a, D->lv[l].P, x, nullptr, mv, out);
-   amgk::spgemv(a.s, D->cP[l - D->Ld], x, nullptr, mv, out, 0, level_n(D, l), nullptr);
+   if (D->slab && l < D->Ld)
+      AMG_TRY(slab_prolong(D, a.s, l, x, out, false, level_xchg(D, a)));
+   else if (l < D->Ld)
+      AMG_TRY(a_spgemv(D, a, D->lv[l].P, x, nullptr, mv, out));
+   else
+      amgk::spgemv(a.s, D->cP[l - D->Ld], x, nullptr, mv, out, 0, level_n(D, l), nullptr);
+   if (composed(D)) {
+      AMG_TRY(apply_A(D, a, l, out, nullptr, mv, a.xy));
+      amgk::xfer_corr(a.s, D->o.smooth_weight, a.xy, diag_of(D, l), out, 0, level_n(D, l));
+   }
    return AMG_OK;
 }
 
@@ -320,10 +370,48 @@ int setup_async(amg_dist_hier *D)
          AMG_TRY(lvec(D, k, &a.rf));
       }
       if (Ld < L) AMG_TRY(dvec(D, (size_t)D->gath_blk * (t->nranks + 1), &a.gath));
+      a.k = k;
    }
    if (D->o.accel_type != AMG_NO_ACCEL)
       AMG_TRY(dvec(D, std::max(1, D->lv[0].n), &D->al[cheby_grid_of(D)].d_acc));
    AMG_HIP(hipStreamSynchronize(c->stream));
+   // the level groups' channels (amg_link.cpp): the largest message a peer
+   // sends me in any exchange of a level correction -- the ghost rows of every
+   // distributed operator, and the allgather block into the replicated levels
+   if (t->nranks > 1) {
+      const int R = t->nranks, me = t->rank;
+      std::vector<long long> cap1(R, 0);
+      for (int l = 0; l < Ld; l++)
+         for (const DistMat *M : {&D->lv[l].A, &D->lv[l].P, &D->lv[l].R}) {
+            if (!M->A || M->replicated_cols) continue;
+            if (M->slab) {
+               if (me > 0) cap1[me - 1] = std::max(cap1[me - 1], (long long)M->nlo[me] * M->cP);
+               if (me < R - 1) cap1[me + 1] = std::max(cap1[me + 1], (long long)M->nhi[me] * M->cP);
+            } else {
+               for (size_t i = 0; i < M->peers.size(); i++)
+                  cap1[M->peers[i]] = std::max(cap1[M->peers[i]], M->rcnt[i]);
+            }
+         }
+      if (Ld < L)
+         for (int p = 0; p < R; p++)
+            if (p != me) cap1[p] = std::max(cap1[p], (long long)D->gath_blk);
+      std::vector<long long> caps((size_t)active * R, 0);
+      for (int k = 0; k < active; k++)
+         for (int p = 0; p < R; p++) caps[(size_t)k * R + p] = cap1[p];
+      AMG_TRY(link_create(D, active, caps, &D->links));
+   }
+   return AMG_OK;
+}
+
+// the composed smoothed transfers' scratch (first solve that asks for them)
+int setup_composed(amg_dist_hier *D)
+{
+   if (!composed(D)) return AMG_OK;
+   for (auto &a : D->al)
+      if (!a.xt) {
+         AMG_TRY(lvec(D, 0, &a.xt));
+         AMG_TRY(lvec(D, 0, &a.xy));
+      }
    return AMG_OK;
 }
 
@@ -466,11 +554,19 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
            "amg_dist_async_solve: ASYNC_MULTADD / ASYNC_AFACX hierarchies only");
    AMG_ARG(D->o.async_type == AMG_FULL_ASYNC, "amg_dist_async_solve: SEMI_ASYNC not supported");
    AMG_ARG(D->L >= 2, "amg_dist_async_solve: needs at least two levels");
+   const int sched = D->o.async_schedule;
+   AMG_ARG(sched >= AMG_SCHED_FREE && sched <= AMG_SCHED_ROUND_ROBIN, "amg_dist_async_solve: async_schedule %d",
+           sched);
    amg_ctx *c = D->ctx;
    AMG_TRY(setup_async(D));
+   AMG_TRY(setup_composed(D));
    AMG_TRY(dist_solve_begin(D, f_local));
+   if (D->links) AMG_TRY(link_reset(D->links));
    const int active = (int)D->al.size();
    const int n0 = D->lv[0].n;
+   // a deterministic schedule runs every level on one stream and one host
+   // thread, in the schedule's order; free: a stream and a host thread per level
+   for (int k = 0; k < active; k++) D->al[k].s = c->level_streams[sched != AMG_SCHED_FREE ? 0 : k];
    hipEvent_t ready, t_start;
    std::vector<hipEvent_t> t_end(active);
    AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
@@ -484,26 +580,61 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
       amgk::vcopy(D->al[k].s, D->r0, D->al[k].r[0], 0, n0);
       D->al[k].acc.reset(D->o);
    }
-   // issue order cycle-major / level-minor: every rank enqueues the same
-   // sequence of RCCL operations on the one comm stream; the GPU runs the
-   // level streams' compute freely
-   for (int cyc = 0; cyc < D->o.num_cycles; cyc++) {
+   // one correction of level k (DMEM_DelayProc before AddCycle, DMEM_Add.cpp:106)
+   auto correct = [&](int k) -> int {
+      if (D->o.delay_level < 0 || D->o.delay_level == k) dist_delay(D, D->al[k].s);
+      return level_correction(D, k);
+   };
+   const int N = D->o.num_cycles;
+   std::vector<int> st(active, AMG_OK);
+   std::vector<std::string> msg(active);
+   if (sched == AMG_SCHED_FREE) {
+      // every level group on its own host thread: it blocks only on its own
+      // channels (the MPI_Test loop of amg_link.cpp)
+      std::vector<std::thread> th;
       for (int k = 0; k < active; k++)
-         if (D->o.delay_level < 0 || D->o.delay_level == k) dist_delay(D, D->al[k].s); // DMEM_Add.cpp:106
-      for (int k = 0; k < active; k++) AMG_TRY(level_correction(D, k));
+         th.emplace_back([&, k] {
+            hipSetDevice(c->device);
+            for (int cyc = 0; cyc < N && st[k] == AMG_OK; cyc++) st[k] = correct(k);
+            if (st[k] == AMG_OK && D->links) st[k] = link_drain(D->links, k);
+            if (st[k] != AMG_OK) {
+               msg[k] = amg_last_error(); // thread-local: handed to the caller's thread
+               if (D->links) link_abort(D->links);
+            }
+         });
+      for (auto &t : th) t.join();
+   } else {
+      // the oracle's or_set_async_schedule order: 1 / 2 level after level, 3
+      // cycle-major round robin; every rank issues the same sequence
+      for (int q = 0; q < active * N && st[0] == AMG_OK; q++) {
+         int k;
+         if (sched == AMG_SCHED_ROUND_ROBIN) k = q % active;
+         else k = sched == AMG_SCHED_FINEST_FIRST ? q / N : active - 1 - q / N;
+         st[0] = correct(k);
+      }
+      for (int k = 0; k < active && st[0] == AMG_OK && D->links; k++) st[0] = link_drain(D->links, k);
+      if (st[0] != AMG_OK && D->links) link_abort(D->links);
    }
    for (int k = 0; k < active; k++) {
       AMG_HIP(hipEventRecord(t_end[k], D->al[k].s));
       AMG_HIP(hipStreamWaitEvent(c->stream, t_end[k], 0));
    }
    AMG_HIP(hipEventDestroy(ready));
+   for (int k = 0; k < active; k++)
+      if (st[k] != AMG_OK) {
+         for (auto &e : t_end) hipEventDestroy(e);
+         hipEventDestroy(t_start);
+         for (auto &a : D->al) hipStreamSynchronize(a.s);
+         if (sched == AMG_SCHED_FREE) return amg_set_error(st[k], "level %d: %s", k, msg[k].c_str());
+         return st[k];
+      }
    D->pre_ready = false;
    AMG_TRY(dist_outer_residual(D, 1));
    D->iter = 1;
    AMG_TRY(d2h(c->stream, c->h_pinned, D->d_hist + 1, sizeof(double)));
    if (relres) *relres = c->h_pinned[0] / D->r0norm;
    if (level_corrections)
-      for (int k = 0; k < D->L; k++) level_corrections[k] = k < active ? D->o.num_cycles : 0;
+      for (int k = 0; k < D->L; k++) level_corrections[k] = k < active ? N : 0;
    D->level_ms.assign(D->L, 0.0);
    for (int k = 0; k < active; k++) {
       float ms = 0.f;

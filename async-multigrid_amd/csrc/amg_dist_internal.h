@@ -86,6 +86,7 @@ struct DLevel {
    DistMat A, P, R;            // P: level l -> l+1 (rows = level l), R: rows = level l+1
    double *f = nullptr, *u = nullptr, *u_alt = nullptr, *r_fine = nullptr, *l1 = nullptr;
    int zero_flag = 0;
+   bool zero_done = false; // slab V-cycle: the zero-guess sweep already written by the restriction
    // slab form
    SlabGeom sg;
    bool geo = false;   // R_l / P_l are the box's geometric transfers (checked)
@@ -123,8 +124,25 @@ struct AsyncLevel {
    double *uf = nullptr, *uc = nullptr, *rf = nullptr; // AFACx fine / coarse iterates, fine residual
    double *gath = nullptr;                   // allgather staging at the replication level
    double *d_acc = nullptr;                  // ChebyUpdate d of the cheby_grid level
+   double *xt = nullptr, *xy = nullptr;      // composed smoothed transfers' scratch (level-0 room)
+   int k = -1;                               // the level group (its link channels)
    AccelState acc;
 };
+
+// per-level device-resident mailboxes of the asynchronous distributed solve
+// (amg_link.cpp).  caps[k * R + src]: largest message (doubles) src sends me
+// in level group k, 0 = no channel (the sets are symmetric by construction)
+struct LinkSet;
+int link_create(amg_dist_hier *D, int K, const std::vector<long long> &caps, LinkSet **out);
+int link_reset(LinkSet *L); // collective: sequence numbers back to 0 before a solve
+int link_send(LinkSet *L, int k, int peer, const double *src, long long n, hipStream_t s);
+int link_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipStream_t s);
+int link_drain(LinkSet *L, int k); // publish everything level group k has in flight
+void link_abort(LinkSet *L);       // tell every peer to give up waiting on this rank
+void link_free(LinkSet *L);
+int link_xchg_planes(LinkSet *L, int k, hipStream_t s, double *x, long long n_own, long long cP,
+                     const std::vector<int> &nlo, const std::vector<int> &nhi);
+int link_allgather(LinkSet *L, int k, hipStream_t s, const double *mine, double *gath, long long blk);
 
 // host <-> device copies ordered on stream s and complete on return
 int h2d(hipStream_t s, void *dst, const void *src, size_t bytes);
@@ -187,8 +205,10 @@ struct amg_dist_hier {
    std::vector<void *> allocs;
    // profiling: [0] fine residual, [1] fine smoother, [2] R0, [3] P0, [4] outer residual
    std::vector<std::pair<hipEvent_t, hipEvent_t>> pend[5];
-   // asynchronous additive cycle (built on first use)
+   // asynchronous additive cycle (built on first use): per-level state and
+   // the per-level device-resident channels between ranks
    std::vector<amgd::AsyncLevel> al;
+   amgd::LinkSet *links = nullptr;
    std::vector<amg_mat *> cA, cP, cR; // replicated levels' operators (level Ld + i)
    std::vector<double *> cl1;         // and their l1 norms
    // DMEM_Mult with acceleration (accel_type != 0): x (the iterate; lv[0].u
@@ -227,7 +247,8 @@ const double *slab_diag(const DistMat &M);
 // or u += P_l x (add = true)
 using XchgFn = std::function<int(double *x, long long n_own, long long cP, const std::vector<int> &nlo,
                                  const std::vector<int> &nhi)>;
-int slab_restrict(amg_dist_hier *D, hipStream_t s, int l, double *r, double *dst, const XchgFn &xchg);
+int slab_restrict(amg_dist_hier *D, hipStream_t s, int l, double *r, double *dst, const XchgFn &xchg,
+                  amgk::ZeroGuess zg = amgk::ZeroGuess());
 int slab_prolong(amg_dist_hier *D, hipStream_t s, int l, double *x, double *out, bool add, const XchgFn &xchg);
 // sync cycle pieces of slab hierarchies (amg_dist.cpp dispatches to them)
 int slab_vcycle(amg_dist_hier *D, bool precond);

@@ -283,6 +283,34 @@ struct amg_devhub {
    std::vector<int> rank_grid;
    std::mutex mu;
    std::condition_variable cv;
+   // round-robin schedule (async_schedule = AMG_SCHED_ROUND_ROBIN): the rank
+   // holding the token runs; it passes the token at the oracle's points
+   int token = 0;
+   std::vector<char> finished;
+   void wait_turn(int me)
+   {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return token == me; });
+   }
+   void pass_turn(int me, bool fin)
+   {
+      std::lock_guard<std::mutex> lk(mu);
+      if (fin) finished[me] = 1;
+      int nx = -1;
+      for (int q = 1; q <= world; q++) {
+         const int c = (me + q) % world;
+         if (!finished[c]) {
+            nx = c;
+            break;
+         }
+      }
+      if (nx < 0) { // every rank is through: ready for the next solve
+         std::fill(finished.begin(), finished.end(), 0);
+         nx = 0;
+      }
+      token = nx;
+      cv.notify_all();
+   }
    std::map<Key, std::deque<std::shared_ptr<Msg>>> sends, recvs;
    std::map<long long, std::shared_ptr<Msg>> sreq, rreq;
    long long next = 1;
@@ -436,6 +464,7 @@ extern "C" int amg_devhub_create(int world, const int *rank_grid, amg_devhub **o
    auto h = std::make_unique<amg_devhub>();
    h->world = world;
    h->rank_grid.assign(rank_grid, rank_grid + world);
+   h->finished.assign(world, 0);
    for (int r = 0; r < world; r++) h->grids[rank_grid[r]].n++;
    *out = h.release();
    return AMG_OK;
@@ -657,6 +686,8 @@ struct IpcLink : MsgLink {
 struct amg_grid_add {
    amg_nb_transport t{};
    std::unique_ptr<MsgLink> link; // device-resident messages (else the host transport t)
+   amg_devhub *hub = nullptr;     // the in-process hub (round-robin schedule)
+   bool rr = false;               // async_schedule = AMG_SCHED_ROUND_ROBIN
    bool dev = false;
    double *ehd = nullptr, *zd = nullptr; // incoming corrections / zeros (device)
    amg_opts o{};
@@ -673,6 +704,18 @@ struct amg_grid_add {
 };
 
 namespace {
+
+// round robin (the oracle's or_dmem_add sched 1): at each of the oracle's
+// yield points the rank finishes its queued work (so every event a peer may
+// test has completed), hands the token on and waits for it to come back
+int rr_yield(amg_grid_add *G)
+{
+   if (!G->rr) return AMG_OK;
+   AMG_HIP(hipStreamSynchronize(G->be->dstream()));
+   G->hub->pass_turn(G->me, false);
+   G->hub->wait_turn(G->me);
+   return AMG_OK;
+}
 
 int xp_err(int st, const char *what)
 {
@@ -728,6 +771,7 @@ int check_inflight(amg_grid_add *G, CommClass &cd, int i)
          }
       }
       if (break_flag) break;
+      AMG_TRY(rr_yield(G));
    }
    return AMG_OK;
 }
@@ -957,6 +1001,7 @@ int async_end(amg_grid_add *G)
       int f;
       AMG_TRY(send_recv(G, G->recv, eh, ACCUMULATE, &f));
       if (local) AMG_TRY(send_recv(G, G->send, z, ACCUMULATE, &f));
+      AMG_TRY(rr_yield(G));
       if (spin > (1LL << 34)) return amg_set_error(AMG_ERR_ARG, "amg_grid_add: cleanup never completed");
    }
    if (G->dev)
@@ -966,7 +1011,14 @@ int async_end(amg_grid_add *G)
    for (int i = 0; i < (int)G->send.procs.size(); i++)
       for (int j = 0; j < G->send.max_inflight[i]; j++)
          if (G->send.inflight_flags[i][j] == 1) {
-            if (G->dev)
+            if (G->rr) {
+               for (;;) {
+                  int done = 0;
+                  AMG_TRY(G->link->test_send(G->send.requests_inflight[i][j], &done));
+                  if (done) break;
+                  AMG_TRY(rr_yield(G));
+               }
+            } else if (G->dev)
                AMG_TRY(G->link->wait_send(G->send.requests_inflight[i][j]));
             else
                AMG_TRY(xp_err(G->t.wait(G->t.user, G->send.requests_inflight[i][j]), "wait"));
@@ -1155,6 +1207,7 @@ extern "C" int amg_grid_add_create_devhub(amg_dist_hier *D, int my_grid, int wor
    auto G = std::make_unique<amg_grid_add>();
    G->o = D->o;
    G->link = std::make_unique<HubLink>(hub, world_rank);
+   G->hub = hub;
    G->dev = true;
    auto be = std::make_unique<DistBackend>(D);
    AMG_TRY(be->init(my_grid));
@@ -1248,6 +1301,11 @@ extern "C" int amg_grid_add_solve(amg_grid_add *G, const double *b_local, double
                                   double *relres_local, long long *messages)
 {
    AMG_ARG(G && b_local && x_local, "amg_grid_add_solve: null argument");
+   G->rr = G->o.async_schedule == AMG_SCHED_ROUND_ROBIN;
+   AMG_ARG(!G->rr || (G->hub && G->grid_size == 1),
+           "amg_grid_add_solve: the round-robin schedule needs the device hub and one rank per grid");
+   AMG_ARG(G->o.async_schedule == AMG_SCHED_FREE || G->rr, "amg_grid_add_solve: async_schedule %d (free or "
+                                                          "round robin)", G->o.async_schedule);
    G->all_done_flag = G->outside_done_flag = G->grid_done_flag = G->converge_flag = 0;
    G->r_local_converge_flag = 0;
    G->cycle = 0;
@@ -1266,6 +1324,7 @@ extern "C" int amg_grid_add_solve(amg_grid_add *G, const double *b_local, double
    // AsyncStart: post every outside receive
    for (int i = 0; i < (int)G->recv.procs.size(); i++) AMG_TRY(tp_irecv(G, G->recv, i));
    const long long cap = 1000LL * std::max(1, G->o.num_cycles) + 1000;
+   if (G->rr) G->hub->wait_turn(G->me);
    while (true) {
       G->converge_flag = check_converge(G);
       if (G->o.delay_type != AMG_DELAY_NONE && G->o.delay_usec > 0 &&
@@ -1279,11 +1338,16 @@ extern "C" int amg_grid_add_solve(amg_grid_add *G, const double *b_local, double
       AMG_TRY(G->be->residual(&rr)); // DMEM_AddResidual_LocalRes
       if (G->all_done_flag == 0) AMG_TRY(add_res_norm(G, rr));
       G->cycle++;
+      AMG_TRY(rr_yield(G));
       if (G->converge_flag == 1) break;
       if (G->cycle > cap) return amg_set_error(AMG_ERR_ARG, "amg_grid_add_solve: no termination after %d cycles",
                                                G->cycle);
    }
    AMG_TRY(async_end(G));
+   if (G->rr) {
+      AMG_HIP(hipStreamSynchronize(G->be->dstream()));
+      G->hub->pass_turn(G->me, true);
+   }
    AMG_TRY(G->be->residual(&rr));
    v[0] = rr;
    AMG_TRY(tp_sum(G, v, 1));

@@ -329,6 +329,10 @@ void vaxpy(hipStream_t s, double a, const double *x, double *y, int rb, int re);
 void vivaxpy(hipStream_t s, const double *x, const double *sc, double *y, int rb, int re);
 void vscale(hipStream_t s, double a, double *y, int rb, int re);
 void vsub(hipStream_t s, const double *b, const double *y, double *r, int rb, int re); // r = b - y
+// composed smoothed transfers: out = x ./ diag;  z = r + (-w) y;  e = e + (-w) (y ./ diag)
+void xfer_div(hipStream_t s, const double *diag, const double *x, double *out, int rb, int re);
+void xfer_sub(hipStream_t s, double w, const double *r, const double *y, double *z, int rb, int re);
+void xfer_corr(hipStream_t s, double w, const double *y, const double *diag, double *e, int rb, int re);
 void vadd_into(hipStream_t s, const double *r, double *u, int rb, int re, int overwrite);
 void l1_norms(hipStream_t s, const amg_mat *A, double *out);
 void a_diag(hipStream_t s, const double *diag, double omega, double *out, int n);

@@ -4075,6 +4075,41 @@ void vaxpy(hipStream_t s, double a, const double *x, double *y, int rb, int re)
    if (re > rb) vaxpy_k<<<ew_blocks(re - rb), 256, 0, s>>>(a, x, y, rb, re);
 }
 
+// composed smoothed transfers (SmoothTransfer, SMEM_Setup.cpp:1173-1254, applied
+// as R~ r = R (r - w A D^-1 r), P~ e = P e - w D^-1 A P e; the oracle's
+// or_hier_set_composed_transfers order of operations)
+__global__ void xfer_div_k(const double *__restrict__ diag, const double *__restrict__ x,
+                           double *__restrict__ out, int rb, int re)
+{
+   EW_LOOP(i, rb, re) out[i] = x[i] / diag[i];
+}
+void xfer_div(hipStream_t s, const double *diag, const double *x, double *out, int rb, int re)
+{
+   if (re > rb) xfer_div_k<<<ew_blocks(re - rb), 256, 0, s>>>(diag, x, out, rb, re);
+}
+__global__ void xfer_sub_k(double mw, const double *__restrict__ r, const double *__restrict__ y,
+                           double *__restrict__ z, int rb, int re)
+{
+   EW_LOOP(i, rb, re) z[i] = r[i] + mw * y[i];
+}
+void xfer_sub(hipStream_t s, double w, const double *r, const double *y, double *z, int rb, int re)
+{
+   if (re > rb) xfer_sub_k<<<ew_blocks(re - rb), 256, 0, s>>>(-w, r, y, z, rb, re);
+}
+__global__ void xfer_corr_k(double mw, const double *__restrict__ y, const double *__restrict__ diag,
+                            double *__restrict__ e, int rb, int re)
+{
+   EW_LOOP(i, rb, re)
+   {
+      const double t = y[i] / diag[i];
+      e[i] = e[i] + mw * t;
+   }
+}
+void xfer_corr(hipStream_t s, double w, const double *y, const double *diag, double *e, int rb, int re)
+{
+   if (re > rb) xfer_corr_k<<<ew_blocks(re - rb), 256, 0, s>>>(-w, y, diag, e, rb, re);
+}
+
 // DMEM_HypreParVector_Ivaxpy DMEM_Misc.cpp:462-478: y += x ./ s
 __global__ void vivaxpy_k(const double *__restrict__ x, const double *__restrict__ sc,
                           double *__restrict__ y, int rb, int re)

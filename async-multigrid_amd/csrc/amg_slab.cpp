@@ -265,6 +265,17 @@ bool s_reuse(const amg_dist_hier *D)
    return D->o.reuse_outer_residual && D->o.num_pre_smooth_sweeps > 0 && !dist_mult_accel(D);
 }
 
+// the slab levels' zero-guess sweeps folded into their restrictions (as the
+// single-GPU V-cycle does; AMG_ZG_FOLD_SLAB=0 turns it off)
+bool zg_fold_on()
+{
+   static const bool on = [] {
+      const char *e = std::getenv("AMG_ZG_FOLD_SLAB");
+      return e ? std::atoi(e) != 0 : true;
+   }();
+   return on;
+}
+
 int s_smooth(amg_dist_hier *D, int l, const double *f, int sweeps, bool allow_reuse)
 {
    DLevel &v = D->lv[l];
@@ -272,7 +283,10 @@ int s_smooth(amg_dist_hier *D, int l, const double *f, int sweeps, bool allow_re
    const bool l1 = D->o.smoother == AMG_L1_JACOBI;
    for (int k = 0; k < sweeps; k++) {
       if (k == 0 && v.zero_flag == 1) {
-         amgk::jacobi_zero(s, slab_diag(v.A), f, l1 ? v.l1 : nullptr, D->o.smooth_weight, v.u, 0, v.n, 0);
+         if (v.zero_done)
+            v.zero_done = false; // folded into the restriction that produced f (same bits)
+         else
+            amgk::jacobi_zero(s, slab_diag(v.A), f, l1 ? v.l1 : nullptr, D->o.smooth_weight, v.u, 0, v.n, 0);
       } else if (k == 0 && allow_reuse && D->pre_ready) {
          std::swap(v.u, v.u_alt);
          D->pre_ready = false;
@@ -303,7 +317,8 @@ void rr_interior(const amg_dist_hier *D, int &k0, int &k1)
 // fused level-0 residual + restriction f_1 = R_0 (f - A_0 u) on the owned
 // coarse planes (dst: level 1's owned rows, or the allgather slot; dcz0 its
 // first coarse plane), overlapping u's exchange with the interior planes
-int s_res_restrict(amg_dist_hier *D, const double *f, double *u, double *dst, int dcz0)
+int s_res_restrict(amg_dist_hier *D, const double *f, double *u, double *dst, int dcz0,
+                   amgk::ZeroGuess zg = amgk::ZeroGuess())
 {
    amg_ctx *c = D->ctx;
    hipStream_t s = c->stream;
@@ -313,7 +328,7 @@ int s_res_restrict(amg_dist_hier *D, const double *f, double *u, double *dst, in
    auto run = [&](int K0, int K1) {
       if (K1 > K0)
          amgk::mz_residual_restrict(s, v.A.A, f - sg.off(), u - sg.off(), v.g, v.d_geo_w, dst, K0, K1, sg.e0(),
-                                    dcz0);
+                                    dcz0, zg);
    };
    if (D->rr_ulo[me] == 0 && D->rr_uhi[me] == 0 && c->xport->nranks == 1) {
       run(v.Ka, v.Kb);
@@ -360,7 +375,8 @@ int s_gather(amg_dist_hier *D, hipStream_t s, double *slot, double *gath, double
 // ---------------------------------------------------------------------------
 // transfers (sync and async paths)
 // ---------------------------------------------------------------------------
-int amgd::slab_restrict(amg_dist_hier *D, hipStream_t s, int l, double *r, double *dst, const XchgFn &xchg)
+int amgd::slab_restrict(amg_dist_hier *D, hipStream_t s, int l, double *r, double *dst, const XchgFn &xchg,
+                        amgk::ZeroGuess zg)
 {
    DLevel &v = D->lv[l];
    DistMat &M = v.R;
@@ -369,7 +385,11 @@ int amgd::slab_restrict(amg_dist_hier *D, hipStream_t s, int l, double *r, doubl
    if (v.geo) {
       const long long coff = to_rep ? 0 : D->lv[l + 1].sg.off();
       const int cz0 = to_rep ? v.Ka : D->lv[l + 1].sg.e0();
-      amgk::geo_restrict(s, v.g, v.d_geo_w, r - v.sg.off(), dst - coff, v.Ka, v.Kb, v.sg.e0(), cz0);
+      if (zg.u) { // the ZeroGuess vectors are indexed like dst (level l + 1's owned rows)
+         zg.d -= coff;
+         zg.u -= coff;
+      }
+      amgk::geo_restrict(s, v.g, v.d_geo_w, r - v.sg.off(), dst - coff, v.Ka, v.Kb, v.sg.e0(), cz0, zg);
    } else {
       slab_spgemv(s, M, r, nullptr, amgk::gemv_mode(1.0, 0.0), dst, 0, M.nrows, nullptr);
    }
@@ -416,12 +436,32 @@ int amgd::slab_vcycle(amg_dist_hier *D, bool precond)
       AMG_TRY(s_smooth(D, l, fl, D->o.num_pre_smooth_sweeps, l == 0 && s_reuse(D)));
       const bool to_rep = l + 1 == Ld;
       double *dst = to_rep ? slot : D->lv[l + 1].f;
+      // a slab level l + 1 (not the coarsest) starts its pre-smoothing with the
+      // zero-guess sweep u = w f / a: a geometric restriction writes it with f
+      // (as the single-GPU V-cycle does, amg_solver.cpp vcycle)
+      amgk::ZeroGuess zg;
+      if (!to_rep && l + 1 < L - 1 && D->o.smoother == AMG_JACOBI && D->o.num_pre_smooth_sweeps >= 1 &&
+          zg_fold_on()) {
+         // the fold writes u_{l+1} / reads a_ii on the coarse rows both
+         // restrictions write: owned coarse planes [Ka, Kb) of level l + 1,
+         // indexed from its first owned row -- the level's own rows exactly
+         const DLevel &nx = D->lv[l + 1];
+         AMG_ARG(nx.sg.za == v.Ka && nx.sg.zb == v.Kb && (long long)nx.n == (long long)(v.Kb - v.Ka) * nx.sg.P &&
+                    nx.A.sro >= 0 && nx.A.sro + nx.n <= (long long)nx.A.A->nrows,
+                 "slab zero-guess fold: level %d owns planes [%d, %d) (%d rows, diag rows [%lld, +%d) of %d), "
+                 "the restriction writes [%d, %d)",
+                 l + 1, nx.sg.za, nx.sg.zb, nx.n, nx.A.sro, nx.n, nx.A.A->nrows, v.Ka, v.Kb);
+         zg.d = slab_diag(nx.A);
+         zg.w = D->o.smooth_weight;
+         zg.u = nx.u;
+      }
       if (l == 0 && D->geo0) {
          SProf pr(D, 0, true);
          // the right-hand side's ghost planes: f's were exchanged at the solve's
          // start; the outer residual (preconditioner mode) changes every cycle
          if (precond) AMG_TRY(slab_xchg(c, s, fl, v.n, v.sg.P, D->rr_flo, D->rr_fhi));
-         AMG_TRY(s_res_restrict(D, fl, v.u, dst, v.Ka)); // dst: coarse plane Ka first
+         AMG_TRY(s_res_restrict(D, fl, v.u, dst, v.Ka, zg)); // dst: coarse plane Ka first
+         D->lv[l + 1].zero_done = zg.u != nullptr;
       } else {
          {
             SProf pr(D, 0, l == 0);
@@ -430,7 +470,8 @@ int amgd::slab_vcycle(amg_dist_hier *D, bool precond)
             }));
          }
          SProf pr(D, 2, l == 0);
-         AMG_TRY(slab_restrict(D, s, l, v.r_fine, dst, xchg));
+         AMG_TRY(slab_restrict(D, s, l, v.r_fine, dst, xchg, v.geo ? zg : amgk::ZeroGuess()));
+         D->lv[l + 1].zero_done = v.geo && zg.u != nullptr;
       }
       if (to_rep) AMG_TRY(s_gather(D, s, slot, D->gath_buf, D->f_rep));
    }

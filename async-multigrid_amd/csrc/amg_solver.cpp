@@ -50,6 +50,7 @@ struct AddLevel {
    // GLOBAL residual phase's fine smoothing correction and scratch (n0 each)
    double *f_acc = nullptr, *g_u = nullptr, *g_prev = nullptr, *g_y = nullptr, *g_r = nullptr;
    hipEvent_t ev_a = nullptr, ev_b = nullptr; // level stream <-> update stream (SEMI_ASYNC)
+   double *xt = nullptr, *xy = nullptr;       // composed smoothed transfers' scratch (n0 each)
 };
 
 } // namespace
@@ -686,6 +687,46 @@ static void bpx_cycle(amg_hier *H, bool precond)
 
 // ---- SMEM_Sync_Add_Vcycle (SMEM_Sync_AMG.cpp:408-621), res_compute LOCAL ------
 // The level corrections are accumulated into u in level order.
+// MULTADD with smooth_transfer: the reference's smoothed transfers
+// (SmoothTransfer, SMEM_Setup.cpp:1173-1254) composed from the plain P, R, A
+static bool composed_transfers(const amg_hier *H) { return H->o.smooth_transfer == 1 && is_multadd(H->o); }
+
+// rc = R~_l r (composed) or R_l r; t / y: scratch of level l's size
+static void xfer_restrict(amg_hier *H, hipStream_t s, int l, const double *r, double *rc, double *t, double *y)
+{
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   const Level &v = H->lv[l];
+   if (composed_transfers(H)) {
+      // t = r ./ a;  y = A t;  t = r + (-w) y;  rc = R t
+      amgk::xfer_div(s, v.A->diag, r, t, 0, v.n);
+      amgk::spgemv(s, v.A, t, nullptr, mv, y, 0, v.n, nullptr);
+      amgk::xfer_sub(s, H->o.smooth_weight, r, y, t, 0, v.n);
+      r = t;
+   }
+   amgk::spgemv(s, v.R, r, nullptr, mv, rc, 0, H->lv[l + 1].n, nullptr);
+}
+
+// ef = P~_l ec (composed) or P_l ec; y: scratch of level l's size
+static void xfer_prolong(amg_hier *H, hipStream_t s, int l, const double *ec, double *ef, double *y)
+{
+   const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   const Level &v = H->lv[l];
+   amgk::spgemv(s, v.P, ec, nullptr, mv, ef, 0, v.n, nullptr);
+   if (composed_transfers(H)) {
+      // y = A ef;  ef = ef + (-w) (y ./ a)
+      amgk::spgemv(s, v.A, ef, nullptr, mv, y, 0, v.n, nullptr);
+      amgk::xfer_corr(s, H->o.smooth_weight, y, v.A->diag, ef, 0, v.n);
+   }
+}
+
+static int ensure_xfer_scratch(amg_hier *H, AddLevel &a)
+{
+   if (!composed_transfers(H) || a.xt) return AMG_OK;
+   AMG_TRY(dalloc(H, H->lv[0].n, &a.xt));
+   AMG_TRY(dalloc(H, H->lv[0].n, &a.xy));
+   return AMG_OK;
+}
+
 static void add_level_correction(amg_hier *H, hipStream_t s, int k, const double *r_fine0)
 {
    const int L = H->L;
@@ -699,8 +740,7 @@ static void add_level_correction(amg_hier *H, hipStream_t s, int k, const double
    // only ever read, so the caller's vector stands in for the copy
    auto rl = [&](int l) -> const double * { return l == 0 ? r_fine0 : a.r[l]; };
    for (int l = 0; l < coarsest; l++)
-      if (l < L - 1)
-         amgk::spgemv(s, H->lv[l].R, rl(l), nullptr, mv, a.r[l + 1], 0, H->lv[l + 1].n, nullptr);
+      if (l < L - 1) xfer_restrict(H, s, l, rl(l), a.r[l + 1], a.xt, a.xy);
    if (k == L - 1) {
       // hypre_GaussElimSolve writes hypre's U_array, never read back by the
       // reference's cycle: the coarsest correction e[k] keeps its zero value
@@ -721,8 +761,7 @@ static void add_level_correction(amg_hier *H, hipStream_t s, int k, const double
                         o.num_fine_smooth_sweeps, k);
       amgk::vcopy(s, a.u_fine, a.e[k], 0, H->lv[k].n);
    }
-   for (int l = k - 1; l >= 0; l--)
-      amgk::spgemv(s, H->lv[l].P, a.e[l + 1], nullptr, mv, a.e[l], 0, H->lv[l].n, nullptr);
+   for (int l = k - 1; l >= 0; l--) xfer_prolong(H, s, l, a.e[l + 1], a.e[l], a.xy);
 }
 
 static void sync_add_vcycle(amg_hier *H)
@@ -859,6 +898,7 @@ static int solve_begin(amg_hier *H, const amg_vec *f, const amg_vec *u)
    amg_ctx *c = H->ctx;
    Level &v = H->lv[0];
    AMG_ARG(f->n == v.n && u->n == v.n, "amg_solve: vector size %d/%d vs %d", f->n, u->n, v.n);
+   for (auto &a : H->al) AMG_TRY(ensure_xfer_scratch(H, a));
    init_vectors(H);
    amgk::vcopy(c->stream, f->d, v.f, 0, v.n);
    amgk::vcopy(c->stream, u->d, v.u, 0, v.n);
@@ -986,6 +1026,7 @@ int amg_hier_reset(amg_hier *H)
 extern "C" int amg_vcycle(amg_hier *H)
 {
    AMG_ARG(H, "amg_vcycle: null hierarchy");
+   for (auto &a : H->al) AMG_TRY(ensure_xfer_scratch(H, a));
    H->pre_ready = false;
    if (is_all_levels(H->o))
       sync_add_vcycle(H);
@@ -1068,12 +1109,14 @@ extern "C" int amg_eigs_power(amg_hier *H, int iters, double *eig_max, double *e
 // the GLOBAL residual phase's fine smoothing of level k's A_ns_global slice
 // (SMEM_Async_AMG.cpp:46-59), with level k's residual r.  Block-aligned slices
 // (the hybrid / asynchronous GS smoothers work on whole blocks).
-static void smooth_fine_slice(amg_hier *H, hipStream_t s, int k, const double *r, int b0, int b1)
+// Slice rows [rb, re); the block smoothers take blocks [b0, b1) (rb = blk[b0],
+// re = blk[b1]).
+static void smooth_fine_slice(amg_hier *H, hipStream_t s, int k, const double *r, int b0, int b1, int rb,
+                              int re)
 {
    Level &v = H->lv[0];
    AddLevel &a = H->al[k];
    const amg_opts &o = H->o;
-   const int rb = v.blk[b0], re = v.blk[b1];
    const int sweeps = o.num_fine_smooth_sweeps;
    if (re <= rb || sweeps <= 0) return;
    const bool sym = is_multadd(o) && o.num_post_smooth_sweeps > 0 && o.num_pre_smooth_sweeps > 0;
@@ -1145,22 +1188,40 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    const bool global_res = o.res_compute_type == AMG_GLOBAL && o.solver == AMG_ASYNC_MULTADD;
    const bool read_res = o.read_type == AMG_READ_RES && !global_res;
    const bool conv_global = o.converge_test_type == AMG_GLOBAL;
+   const int sched = o.async_schedule;
+   AMG_ARG(sched >= AMG_SCHED_FREE && sched <= AMG_SCHED_ROUND_ROBIN, "amg_async_solve: async_schedule %d", sched);
+   AMG_ARG(!conv_global || sched == AMG_SCHED_FREE || sched == AMG_SCHED_ROUND_ROBIN,
+           "amg_async_solve: a sequential schedule needs converge_test_type LOCAL");
    AMG_TRY(solve_begin(H, f, u));
    Level &v0 = H->lv[0];
    const int n0 = v0.n;
    // levels with a correction loop: [k_lo, k_hi).  The finest level whose
    // correction is nonzero is L-2 (see add_level_correction); with GLOBAL
    // residuals no group runs level 0 -- the sliced fine-grid smoothing takes
-   // its place (PartitionLevels' finest_level = 1, SMEM_Setup.cpp:609-615)
+   // its place (PartitionLevels' finest_level = 1, SMEM_Setup.cpp:609-615) --
+   // and the coarsest level's group runs too: its correction is zero, but it
+   // smooths its slice of the fine grid and forms its slice of the residual
    const int k_lo = global_res ? 1 : 0;
-   const int k_hi = std::max(k_lo + 1, L - 1);
+   const int k_hi = global_res ? L : std::max(k_lo + 1, L - 1);
    const int ngrp = k_hi - k_lo;
-   // global slices: equal splits of level 0's blocks (A_ns_global, SMEM_Setup.cpp:924-936)
-   std::vector<int> gb(L + 1, 0);
+   // global slices (A_ns_global, SMEM_Setup.cpp:924-936): equal row splits of
+   // the fine grid over the groups; the block smoothers split level 0's blocks
+   // instead (no GS block straddles two slices)
+   const bool blk_smoother = o.smoother == AMG_HYBRID_JACOBI_GAUSS_SEIDEL ||
+                             o.smoother == AMG_L1_HYBRID_JACOBI_GAUSS_SEIDEL ||
+                             o.smoother == AMG_ASYNC_GAUSS_SEIDEL || o.smoother == AMG_SEMI_ASYNC_GAUSS_SEIDEL;
+   std::vector<int> gb(L + 1, 0), gr(L + 1, 0);
    {
       const int nb = (int)v0.blk.size() - 1;
-      for (int q = 0; q <= ngrp; q++) gb[k_lo + q] = (int)((long long)nb * q / ngrp);
+      const int size = n0 / ngrp, rest = n0 - size * ngrp;
+      for (int q = 0; q <= ngrp; q++) {
+         gb[k_lo + q] = (int)((long long)nb * q / ngrp);
+         gr[k_lo + q] = blk_smoother ? v0.blk[gb[k_lo + q]] : q * size + std::min(q, rest);
+      }
    }
+   // a deterministic schedule runs every level on one stream in the
+   // schedule's order (the oracle's or_set_async_schedule 1 / 2 / 3)
+   auto lstream = [&](int k) { return sched != AMG_SCHED_FREE ? c->level_streams[k_lo] : c->level_streams[k]; };
    for (int k = k_lo; k < k_hi; k++) {
       AddLevel &a = H->al[k];
       if (read_res && !a.f_acc) AMG_TRY(dalloc(H, n0, &a.f_acc));
@@ -1179,20 +1240,24 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
    AMG_HIP(hipEventRecord(ready, c->stream));
    for (int k = k_lo; k < k_hi; k++) {
-      hipStream_t s = c->level_streams[k];
+      hipStream_t s = lstream(k);
       AMG_HIP(hipStreamWaitEvent(s, ready, 0));
       // level_vector[k].r[0] = vector.r[0] (SMEM_Async_AMG.cpp:10-15)
       amgk::vcopy(s, H->r0, H->al[k].y_fine, 0, n0);
       if (read_res) amgk::vset(s, H->al[k].f_acc, 0.0, 0, n0);
-      if (global_res) amgk::vset(s, H->al[k].g_u, 0.0, 0, n0);
+      if (global_res) {
+         amgk::vset(s, H->al[k].g_u, 0.0, 0, n0);
+         amgk::vset(s, H->al[k].g_prev, 0.0, 0, n0);
+      }
    }
    AMG_HIP(hipStreamWaitEvent(c->comm_stream, ready, 0));
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
-   hipStream_t us = c->comm_stream; // SEMI_ASYNC update stream
+   // SEMI_ASYNC update stream (the lock of :238-283)
+   hipStream_t us = sched != AMG_SCHED_FREE ? lstream(k_lo) : c->comm_stream;
    std::vector<int> issued(L, 0);
    // one correction of level k, issued on its stream
    auto correction = [&](int k) -> int {
-      hipStream_t s = c->level_streams[k];
+      hipStream_t s = lstream(k);
       AddLevel &a = H->al[k];
       auto to_update = [&]() -> int {
          AMG_HIP(hipEventRecord(a.ev_a, s));
@@ -1204,7 +1269,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          AMG_HIP(hipStreamWaitEvent(s, a.ev_b, 0));
          return AMG_OK;
       };
-      const int grb = v0.blk[gb[k]], gre = v0.blk[gb[k + 1]];
+      const int grb = gr[k], gre = gr[k + 1];
       {
          // injected delay of the threads this level group stands for
          const int T = delay_threads(o), g = k - k_lo;
@@ -1212,7 +1277,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          amgk::delay(s, delay_usec(H, t0, std::min(t1, T), issued[k] + 1), c->wall_khz);
       }
       if (global_res) {
-         smooth_fine_slice(H, s, k, a.y_fine, gb[k], gb[k + 1]);
+         smooth_fine_slice(H, s, k, a.y_fine, gb[k], gb[k + 1], grb, gre);
          if (!semi) amgk::atomic_add(s, v0.u, a.g_u, grb, gre);
       }
       add_level_correction(H, s, k, a.y_fine);
@@ -1255,7 +1320,45 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       AMG_HIP(hipGetLastError());
       return AMG_OK;
    };
-   if (!conv_global) {
+   if (sched == AMG_SCHED_FINEST_FIRST || sched == AMG_SCHED_COARSEST_FIRST) {
+      // the level groups one after another (or_set_async_schedule 1 / 2)
+      for (int q = 0; q < ngrp; q++) {
+         const int k = sched == AMG_SCHED_FINEST_FIRST ? k_lo + q : k_hi - 1 - q;
+         for (int cyc = 0; cyc < o.num_cycles; cyc++) {
+            AMG_TRY(correction(k));
+            issued[k]++;
+         }
+      }
+   } else if (sched == AMG_SCHED_ROUND_ROBIN && conv_global) {
+      // round robin under converge GLOBAL (or_set_async_schedule 3): the
+      // finest group's root raises the converge flag after its update once
+      // every group (the idle coarsest group of the reference too, which
+      // keeps the same count) has num_cycles corrections; a group stops at
+      // the first of its own updates that sees the flag (Misc.cpp:418-441)
+      std::vector<int> stopped(L, 0);
+      bool flag = false;
+      for (int left = ngrp; left > 0;)
+         for (int k = k_lo; k < k_hi; k++) {
+            if (stopped[k]) continue;
+            AMG_TRY(correction(k));
+            issued[k]++;
+            if (k == k_lo && !flag) {
+               bool all = true;
+               for (int l = k_lo; l < k_hi; l++)
+                  if (issued[l] < o.num_cycles) all = false;
+               // the reference's idle coarsest group runs its turn after the
+               // last correcting level, so in round r it has r - 1 when k_lo checks
+               if (k_hi < L && issued[k_lo] - 1 < o.num_cycles) all = false;
+               flag = all;
+            }
+            if (flag) {
+               stopped[k] = 1;
+               left--;
+            }
+         }
+   } else if (!conv_global) {
+      // free race, or round robin under converge LOCAL (one stream: the
+      // cycle-major, level-minor issue order is the turn order)
       for (int cyc = 0; cyc < o.num_cycles; cyc++)
          for (int k = k_lo; k < k_hi; k++) {
             AMG_TRY(correction(k));

@@ -148,7 +148,30 @@ typedef struct {
    int delay_level;              /* distributed async additive: -1 every level's
                                     stream takes the delay (DMEM_Add.cpp:106), else
                                     that level's only (a probe of level coupling) */
+   int async_schedule;           /* asynchronous additive solves (amg_async_solve,
+                                    amg_dist_async_solve): AMG_SCHED_FREE (the race)
+                                    or a deterministic admissible schedule of the
+                                    race -- the level corrections one level after
+                                    another (AMG_SCHED_FINEST_FIRST /
+                                    AMG_SCHED_COARSEST_FIRST, converge LOCAL only)
+                                    or taking turns, one whole correction each
+                                    (AMG_SCHED_ROUND_ROBIN) -- bit-identical to the
+                                    oracle's or_set_async_schedule 1 / 2 / 3 */
+   int smooth_transfer;          /* 1: the MULTADD / ASYNC_MULTADD transfers are the
+                                    reference's smoothed P~ = (I - w D^-1 A) P and
+                                    R~ = P~^T (SmoothTransfer, SMEM_Setup.cpp:
+                                    1173-1254, w = smooth_weight), applied composed
+                                    from the registered plain P, R and A (symmetric):
+                                    R~ r = R (r - w A D^-1 r), P~ e = P e - w D^-1 A P e
+                                    -- two stencil passes instead of streaming the
+                                    long rows of the explicit products; the order of
+                                    operations is the oracle's
+                                    or_hier_set_composed_transfers.  0: as registered */
 } amg_opts;
+#define AMG_SCHED_FREE 0
+#define AMG_SCHED_FINEST_FIRST 1
+#define AMG_SCHED_COARSEST_FIRST 2
+#define AMG_SCHED_ROUND_ROBIN 3
 #define AMG_SPS_EXPONENTIAL 0 /* Main.hpp:132-134 */
 #define AMG_SPS_INVERSE 1
 #define AMG_SPS_RANDOM 2

@@ -722,6 +722,8 @@ struct or_hier {
    int *zero_flags;
    int **blk; int *nblk;
    double *u_outer, *y_outer;
+   int composed;        /* or_hier_set_composed_transfers */
+   double **xt, **xy;   /* composed transfers: scratch per level group (n[0] each) */
 };
 
 static double *dvec(int n) { return (double *)calloc((size_t)(n > 0 ? n : 1), sizeof(double)); }
@@ -796,7 +798,65 @@ void or_hier_free(or_hier *H)
    }
    free(H->A); free(H->P); free(H->R); free(H->n); free(H->A_diag); free(H->L1);
    free(H->zero_flags); free(H->blk); free(H->nblk); free(H->u_outer); free(H->y_outer);
+   if (H->xt) {
+      for (int k = 0; k < L; k++) {
+         free(H->xt[k]);
+         free(H->xy[k]);
+      }
+      free(H->xt);
+      free(H->xy);
+   }
    free(H);
+}
+
+void or_hier_set_composed_transfers(or_hier *H, int on)
+{
+   H->composed = on;
+   if (on && !H->xt) {
+      H->xt = (double **)malloc(H->L * sizeof(double *));
+      H->xy = (double **)malloc(H->L * sizeof(double *));
+      for (int k = 0; k < H->L; k++) {
+         H->xt[k] = dvec(H->n[0]);
+         H->xy[k] = dvec(H->n[0]);
+      }
+   }
+}
+
+/* does level transfer use the composed smoothed operators? (MULTADD only,
+ * SMEM_Setup.cpp:244-261) */
+static int composed_of(const or_hier *H)
+{
+   return H->composed && (H->o.solver == OR_MULTADD || H->o.solver == OR_ASYNC_MULTADD);
+}
+
+/* rc = R~_l r (composed, see or_hier_set_composed_transfers) or R_l r; t / y:
+ * scratch of level l's size */
+static void xfer_restrict(or_hier *H, int l, const double *r, double *rc, double *t, double *y)
+{
+   if (!composed_of(H)) {
+      or_smem_matvec(&H->R[l], r, rc, 0, H->n[l + 1]);
+      return;
+   }
+   const or_csr *A = &H->A[l];
+   const int n = H->n[l];
+   const double w = H->o.smooth_weight;
+   for (int i = 0; i < n; i++) t[i] = r[i] / A->data[A->i[i]];
+   or_smem_matvec(A, t, y, 0, n);
+   for (int i = 0; i < n; i++) t[i] = r[i] + (-w) * y[i];
+   or_smem_matvec(&H->R[l], t, rc, 0, H->n[l + 1]);
+}
+
+/* ef = P~_l ec (composed) or P_l ec; y: scratch of level l's size */
+static void xfer_prolong(or_hier *H, int l, const double *ec, double *ef, double *y)
+{
+   or_smem_matvec(&H->P[l], ec, ef, 0, H->n[l]);
+   if (!composed_of(H)) return;
+   const or_csr *A = &H->A[l];
+   const int n = H->n[l];
+   const double w = H->o.smooth_weight;
+   or_smem_matvec(A, ef, y, 0, n);
+   for (int i = 0; i < n; i++) y[i] = y[i] / A->data[A->i[i]];
+   for (int i = 0; i < n; i++) ef[i] = ef[i] + (-w) * y[i];
 }
 
 void or_hier_set_blocks(or_hier *H, int level, const int *blk, int nblk)
@@ -935,7 +995,8 @@ void or_sync_add_vcycle(or_hier *H)
       memcpy(H->lv_r[k][0], H->r[0], (size_t)H->n[0] * sizeof(double));
       for (int level = 0; level < coarsest; level++) {
          if (level < L - 1)
-            or_smem_matvec(&H->R[level], H->lv_r[k][level], H->lv_r[k][level + 1], 0, H->n[level + 1]);
+            xfer_restrict(H, level, H->lv_r[k][level], H->lv_r[k][level + 1], H->xt ? H->xt[k] : NULL,
+                          H->xy ? H->xy[k] : NULL);
       }
       if (k == L - 1) {
          /* hypre_GaussElimSolve writes hypre's own U_array, which the cycle
@@ -958,7 +1019,7 @@ void or_sync_add_vcycle(or_hier *H)
          memcpy(H->lv_e[k][k], H->lv_u_fine[k][k], (size_t)H->n[k] * sizeof(double));
       }
       for (int level = k - 1; level > -1; level--)
-         or_smem_matvec(&H->P[level], H->lv_e[k][level + 1], H->lv_e[k][level], 0, H->n[level]);
+         xfer_prolong(H, level, H->lv_e[k][level + 1], H->lv_e[k][level], H->xy ? H->xy[k] : NULL);
       for (int i = 0; i < H->n[0]; i++) H->u[0][i] += H->lv_e[k][0][i];
    }
 }
@@ -1066,9 +1127,12 @@ typedef struct {
    int n, count, gen, flag;
 } or_gbar;
 
-/* schedule of the groups (converge LOCAL only): 0 free (the OS's), 1 / 2 the
+/* schedule of the groups: 0 free (the OS's); 1 / 2 (converge LOCAL only) the
  * groups one after another, finest / coarsest first -- the extreme speed
- * ratios of the race, for the band's ends */
+ * ratios of the race, for the band's ends; 3 round robin: a token passes
+ * from group to group (ascending level, cyclic, skipping groups that have
+ * stopped), each holding it for one whole correction -- the equal-speed
+ * schedule with a fixed update order.  1-3 make the race deterministic. */
 static int g_async_schedule = 0;
 void or_set_async_schedule(int s) { g_async_schedule = s; }
 
@@ -1235,6 +1299,9 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
    const int gres = g_async_res_global && multadd;
    const int k_lo = gres ? 1 : 0; /* the finest level with a group */
    if (gres && (L < 2 || read_type != OR_READ_SOL)) return -1; /* READ_RES needs LOCAL residuals (:227, 270, 288) */
+   /* a sequential schedule never ends under converge GLOBAL (the first group
+    * would wait for the others' counts forever) */
+   if ((g_async_schedule == 1 || g_async_schedule == 2) && converge_type != OR_CONVERGE_LOCAL) return -1;
    int T = 0;
    for (int k = 0; k < L; k++) {
       if (k < k_lo ? nt[k] != 0 : nt[k] < 1) return -1;
@@ -1262,7 +1329,13 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
    }
    /* GLOBAL residuals: thread t's global fine slice [gs[t], gs[t + 1]) */
    int *gs = (int *)malloc((T + 1) * sizeof(int));
-   {
+   if (H->nblk[0] > 1) {
+      /* an explicit block partition of level 0 (the device's GS blocks): the
+       * slices are equal splits of the blocks, so no block straddles two
+       * threads' slices (the reference's GS block is the thread's slice) */
+      const int nb = H->nblk[0];
+      for (int t = 0; t <= T; t++) gs[t] = H->blk[0][(int)((long long)nb * t / T)];
+   } else {
       const int size = n0 / T, rest = n0 - size * T;
       for (int t = 0; t <= T; t++) gs[t] = t * size + (t < rest ? t : rest);
    }
@@ -1294,6 +1367,9 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
    omp_init_lock(&lock);
    double *U = H->u[0];
    const double *F = H->f[0];
+   const int rr = g_async_schedule == 3;
+   int turn = k_lo;                       /* round robin: the group holding the token */
+   int *gdone = (int *)calloc(L, sizeof(int)); /* round robin: groups that have stopped */
 #pragma omp parallel num_threads(T)
    {
       const int tid = omp_get_thread_num();
@@ -1302,15 +1378,36 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
 #define RNG(m, l, s, e) const int s = blk[m][k * L + (l)][g], e = blk[m][k * L + (l)][g + 1]
       int tid_converge = 0;
       const int coarsest = multadd ? k : k + 1;
-      if (g_async_schedule && converge_type == OR_CONVERGE_LOCAL) {
+      if (g_async_schedule == 1 || g_async_schedule == 2) {
          const int prev = g_async_schedule == 1 ? k - 1 : k + 1; /* the group that runs before this one */
          if (prev >= k_lo && prev < L)
             while (__atomic_load_n(&count[prev], __ATOMIC_ACQUIRE) < o->num_cycles) sched_yield();
       }
+      /* round robin: the group's whole correction runs while it holds the
+       * token; the root hands it on (next group up, cyclic, skipping stopped
+       * groups) after the group's last barrier of the correction */
+#define RR_PASS(stop)                                                                 \
+      do {                                                                           \
+         if (rr) {                                                                   \
+            gbar_wait(b, NULL);                                                      \
+            if (tid == root[k]) {                                                    \
+               if (stop) gdone[k] = 1;                                               \
+               int nx = k;                                                           \
+               for (int q = 1; q <= L - k_lo; q++) {                                 \
+                  const int c = k_lo + (k - k_lo + q) % (L - k_lo);                  \
+                  if (!gdone[c]) { nx = c; break; }                                  \
+               }                                                                     \
+               __atomic_store_n(&turn, nx, __ATOMIC_RELEASE);                        \
+            }                                                                        \
+            gbar_wait(b, NULL); /* no thread of the group re-tests turn before */    \
+         }                                                                           \
+      } while (0)
       const int gns = gs[tid], gne = gs[tid + 1];
       int acc_cycle = 0;
       double acc_state[2] = {g_acc_mu, 1.0}; /* every thread of the group advances it alike */
       while (1) {
+         if (rr)
+            while (__atomic_load_n(&turn, __ATOMIC_ACQUIRE) != k) sched_yield();
          if (gres) {
             /* :35-77: smooth the global slice of A_0 u = r_k from zero */
             async_smooth(H, 0, H->lv_r[k][0], H->lv_u_fine[k][0], H->lv_u_prev[k][0], H->lv_y[k][0], o->num_fine,
@@ -1324,8 +1421,12 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
          /* restriction :93-108 */
          for (int l = 0; l < coarsest; l++) {
             if (l >= L - 1) continue;
-            RNG(2, l, rs, re);
-            or_smem_matvec(&H->R[l], H->lv_r[k][l], H->lv_r[k][l + 1], rs, re);
+            if (composed_of(H)) { /* the group's first thread applies R~ (composed) */
+               if (g == 0) xfer_restrict(H, l, H->lv_r[k][l], H->lv_r[k][l + 1], H->xt[k], H->xy[k]);
+            } else {
+               RNG(2, l, rs, re);
+               or_smem_matvec(&H->R[l], H->lv_r[k][l], H->lv_r[k][l + 1], rs, re);
+            }
             gbar_wait(b, NULL);
          }
          if (k == L - 1) {
@@ -1362,8 +1463,12 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
          }
          /* prolongation :211-224 */
          for (int l = k - 1; l > -1; l--) {
-            RNG(1, l, ps, pe);
-            or_smem_matvec(&H->P[l], H->lv_e[k][l + 1], H->lv_e[k][l], ps, pe);
+            if (composed_of(H)) {
+               if (g == 0) xfer_prolong(H, l, H->lv_e[k][l + 1], H->lv_e[k][l], H->xy[k]);
+            } else {
+               RNG(1, l, ps, pe);
+               or_smem_matvec(&H->P[l], H->lv_e[k][l + 1], H->lv_e[k][l], ps, pe);
+            }
             gbar_wait(b, NULL);
          }
          RNG(0, 0, ns, ne);
@@ -1428,7 +1533,10 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
             if (!rres) or_smem_residual(&H->A[0], F, ukk, H->lv_y[k][0], H->lv_r[k][0], ns, ne);
             gbar_wait(b, NULL);
          }
-         if (tid_converge == 1) break;
+         if (tid_converge == 1) {
+            RR_PASS(1);
+            break;
+         }
          if (gres) {
             /* :356-414: u_k = u on the group's rows; the slice's residual
              * into the shared r; the group's rows of r back into r_k */
@@ -1454,10 +1562,13 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
             }
             if (async_type == OR_SEMI_ASYNC && tid == root[k]) omp_unset_lock(&lock);
          }
+         RR_PASS(0);
       }
 #undef RNG
+#undef RR_PASS
    }
    omp_destroy_lock(&lock);
+   free(gdone);
    /* FULL_ASYNC READ_RES: the private correction sums join u (:416-426) */
    if (read_type == OR_READ_RES && async_type != OR_SEMI_ASYNC)
       for (int k = 0; k < L; k++)
@@ -1647,4 +1758,646 @@ double or_dmem_async_jacobi(const or_csr *A, const double *b, double *x, int swe
    double rn = or_norm2(r, n);
    free(s); free(u); free(e); free(r); free(d);
    return rn;
+}
+
+/* ------------------------------------------------------------------------- */
+/* DMEM_Add (DMEM_Add.cpp:20-944) with its message engine (DMEM_Comm.cpp:11-382) */
+/* ------------------------------------------------------------------------- */
+/* The reference's level-grouped asynchronous additive solver restated with
+ * OpenMP threads standing in for the MPI ranks, one rank per grid (grid k
+ * computes level k's correction): every grid holds the whole fine problem,
+ * AddCycle (:180-329) restricts its residual F[0] to level k with R,
+ * DMEM_AddSmooth's 2-step symmetric Jacobi there (DMEM_Smooth.cpp:574-638, s =
+ * a_ii / w or 1 where a_ii = 0, DMEM_Setup.cpp:471-482) -- or, on the coarsest
+ * grid, the exact solve of hypre_GaussElimSolve (:263; dense LU with partial
+ * pivoting here) -- and prolongs with P; DMEM_AddCorrect_LocalRes / AddCheckComm
+ * (:391-528) send the accumulated correction y to every other grid
+ * (gridjToGridk_Correct_outsideSend, ACCUMULATE, every async_comm_save_divisor
+ * cycles and on convergence) and add what arrived into x (payloads of
+ * messages received alone with a done flag are dropped, as in the reference:
+ * SendRecv breaks before raising the receive flag, DMEM_Comm.cpp:292-305);
+ * CheckInFlight / SetNextInFlight keep max_inflight sends per destination;
+ * CheckConverge LOCAL / GLOBAL (:906-944), AddResNorm's InnerProdFlag (one rank
+ * per grid: local), AsyncRecvCleanup + CompleteInFlight (:827-890).
+ *
+ * Messages: an in-process mailbox with MPI point-to-point matching (per source,
+ * destination, in order); a receive completes when matched, a send when the
+ * receiver has taken its payload (the device hub's completion: the slot is
+ * released by the receiver's read).
+ *
+ * sched 0: the free race (the OS schedules the grid threads).  sched 1: round
+ * robin -- a token passes from grid to grid (ascending, cyclic, skipping
+ * finished grids) at fixed points: the end of every main-loop iteration, every
+ * pass of CheckInFlight's wait, every iteration of AsyncRecvCleanup, every
+ * failed test of the final waits.  The device's amg_grid_add_solve with
+ * async_schedule = AMG_SCHED_ROUND_ROBIN yields at the same points. */
+typedef struct or_rec {
+   double *pay;          /* payload copy (send) */
+   int n;
+   double flag;          /* the done flag slot data[len] */
+   int matched, consumed;
+   struct or_rec *peer;  /* receive: the matched send */
+   struct or_rec *qnext; /* mailbox queue */
+   struct or_rec *all;   /* every record (freed at the end) */
+} or_rec;
+
+typedef struct {
+   int G;
+   or_rec **sendq, **recvq; /* [src * G + dst] unmatched sends / posted receives */
+   or_rec *all;
+   omp_lock_t lock;
+   /* round robin */
+   int sched, token;
+   int *finished;
+} or_mbox;
+
+static or_rec *mb_new(or_mbox *M)
+{
+   or_rec *r = (or_rec *)calloc(1, sizeof(or_rec));
+   r->all = M->all;
+   M->all = r;
+   return r;
+}
+
+static void q_push(or_rec **q, or_rec *r)
+{
+   r->qnext = NULL;
+   while (*q) q = &(*q)->qnext;
+   *q = r;
+}
+
+static or_rec *q_pop(or_rec **q)
+{
+   or_rec *r = *q;
+   if (r) *q = r->qnext;
+   return r;
+}
+
+static or_rec *mb_isend(or_mbox *M, int src, int dst, const double *data, int n, double flag)
+{
+   omp_set_lock(&M->lock);
+   or_rec *s = mb_new(M);
+   s->pay = (double *)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+   memcpy(s->pay, data, (size_t)n * sizeof(double));
+   s->n = n;
+   s->flag = flag;
+   or_rec *r = q_pop(&M->recvq[src * M->G + dst]);
+   if (r) {
+      r->matched = s->matched = 1;
+      r->peer = s;
+   } else {
+      q_push(&M->sendq[src * M->G + dst], s);
+   }
+   omp_unset_lock(&M->lock);
+   return s;
+}
+
+static or_rec *mb_irecv(or_mbox *M, int dst, int src)
+{
+   omp_set_lock(&M->lock);
+   or_rec *r = mb_new(M);
+   or_rec *s = q_pop(&M->sendq[src * M->G + dst]);
+   if (s) {
+      r->matched = s->matched = 1;
+      r->peer = s;
+   } else {
+      q_push(&M->recvq[src * M->G + dst], r);
+   }
+   omp_unset_lock(&M->lock);
+   return r;
+}
+
+static int mb_matched(or_mbox *M, or_rec *r)
+{
+   omp_set_lock(&M->lock);
+   const int m = r->matched;
+   omp_unset_lock(&M->lock);
+   return m;
+}
+
+static void mb_consume(or_mbox *M, or_rec *r)
+{
+   omp_set_lock(&M->lock);
+   r->peer->consumed = 1;
+   omp_unset_lock(&M->lock);
+}
+
+static int mb_sent(or_mbox *M, or_rec *s)
+{
+   omp_set_lock(&M->lock);
+   const int c = s->consumed;
+   omp_unset_lock(&M->lock);
+   return c;
+}
+
+/* round robin: hand the token to the next unfinished grid and wait for it */
+static void rr_wait(or_mbox *M, int g)
+{
+   if (!M->sched) return;
+   while (__atomic_load_n(&M->token, __ATOMIC_ACQUIRE) != g) sched_yield();
+}
+
+static void rr_pass(or_mbox *M, int g, int finished)
+{
+   if (!M->sched) return;
+   if (finished) M->finished[g] = 1;
+   int nx = -1;
+   for (int q = 1; q <= M->G; q++) {
+      const int c = (g + q) % M->G;
+      if (!M->finished[c]) {
+         nx = c;
+         break;
+      }
+   }
+   __atomic_store_n(&M->token, nx, __ATOMIC_RELEASE);
+}
+
+static void rr_yield(or_mbox *M, int g)
+{
+   if (!M->sched) return;
+   rr_pass(M, g, 0);
+   rr_wait(M, g);
+}
+
+enum { OR_MSG_ACCUMULATE = 0, OR_MSG_WRITE = 1 };
+
+/* DMEM_CommData of one grid: the other grids, all rows overlapping */
+typedef struct {
+   int send, np, len, max_inflight;
+   int *procs, *done_flags, *recv_flags, *message_count;
+   double **data;
+   or_rec **requests;
+   int *num_inflight, *next_inflight;
+   double ***data_inflight;
+   or_rec ***requests_inflight;
+   int **inflight_flags;
+} or_cls;
+
+typedef struct {
+   or_hier *H;
+   or_mbox *M;
+   int k, L, n0;
+   int converge_local, semi, save, accel, cheby_mine;
+   double tol, mu, delta;
+   int num_cycles;
+   or_cls send, recv;
+   /* iter / comm flags (DMEM_AllData) */
+   int all_done_flag, outside_done_flag, grid_done_flag, converge_flag, r_local_converge_flag, cycle;
+   double r0_norm2, r_local;
+   long long sent, rcvd;
+   /* numerics */
+   double *x, *b, *r, *y, *e, *d, *z, *vt;
+   double **F, **U;
+   double *sc, *nsc; /* DMEM_AddSmooth scales of level k */
+   double *lu;
+   int *piv, nc;
+   double acc_state[2];
+   int acc_cycle;
+} or_grid;
+
+static void cls_init(or_cls *c, int send, int G, int me, int n0, int mi)
+{
+   memset(c, 0, sizeof(*c));
+   c->send = send;
+   c->np = G - 1;
+   c->len = n0;
+   c->max_inflight = mi;
+   c->procs = (int *)malloc(G * sizeof(int));
+   for (int p = 0, i = 0; p < G; p++)
+      if (p != me) c->procs[i++] = p;
+   c->done_flags = (int *)calloc(G, sizeof(int));
+   c->recv_flags = (int *)calloc(G, sizeof(int));
+   c->message_count = (int *)calloc(G, sizeof(int));
+   c->data = (double **)malloc(G * sizeof(double *));
+   for (int i = 0; i < c->np; i++) c->data[i] = dvec(n0 + 2);
+   c->requests = (or_rec **)calloc(G, sizeof(or_rec *));
+   if (send) {
+      c->num_inflight = (int *)calloc(G, sizeof(int));
+      c->next_inflight = (int *)calloc(G, sizeof(int));
+      c->data_inflight = (double ***)malloc(G * sizeof(double **));
+      c->requests_inflight = (or_rec ***)malloc(G * sizeof(or_rec **));
+      c->inflight_flags = (int **)malloc(G * sizeof(int *));
+      for (int i = 0; i < c->np; i++) {
+         c->data_inflight[i] = (double **)malloc(mi * sizeof(double *));
+         for (int j = 0; j < mi; j++) c->data_inflight[i][j] = dvec(n0 + 2);
+         c->requests_inflight[i] = (or_rec **)calloc(mi, sizeof(or_rec *));
+         c->inflight_flags[i] = (int *)calloc(mi, sizeof(int));
+      }
+   }
+}
+
+static void cls_free(or_cls *c)
+{
+   for (int i = 0; i < c->np; i++) {
+      free(c->data[i]);
+      if (c->send) {
+         for (int j = 0; j < c->max_inflight; j++) free(c->data_inflight[i][j]);
+         free(c->data_inflight[i]);
+         free(c->requests_inflight[i]);
+         free(c->inflight_flags[i]);
+      }
+   }
+   free(c->procs); free(c->done_flags); free(c->recv_flags); free(c->message_count); free(c->data);
+   free(c->requests);
+   if (c->send) {
+      free(c->num_inflight); free(c->next_inflight); free(c->data_inflight); free(c->requests_inflight);
+      free(c->inflight_flags);
+   }
+}
+
+/* CheckInFlight (DMEM_Comm.cpp:25-67) */
+static void check_inflight(or_grid *g, or_cls *c, int i)
+{
+   while (1) {
+      int break_flag = 0;
+      if (g->all_done_flag == 0)
+         break_flag = 1;
+      else if (c->num_inflight[i] < c->max_inflight)
+         break;
+      for (int j = 0; j < c->max_inflight; j++) {
+         if (c->inflight_flags[i][j] == 1) {
+            if (mb_sent(g->M, c->requests_inflight[i][j])) {
+               c->inflight_flags[i][j] = 0;
+               c->num_inflight[i]--;
+               if (j < c->next_inflight[i]) c->next_inflight[i] = j;
+               if (g->all_done_flag == 1) {
+                  break_flag = 1;
+                  break;
+               }
+            }
+         } else if (g->all_done_flag == 1) {
+            break_flag = 1;
+            break;
+         }
+      }
+      if (break_flag) break;
+      rr_yield(g->M, g->k);
+   }
+}
+
+/* SetNextInFlight (DMEM_Comm.cpp:69-79) */
+static void set_next_inflight(or_cls *c, int i)
+{
+   for (int j = 0; j < c->max_inflight; j++)
+      if (c->inflight_flags[i][j] == 0) {
+         c->next_inflight[i] = j;
+         return;
+      }
+   c->next_inflight[i] = c->max_inflight;
+}
+
+/* SendRecv, asynchronous outside classes (DMEM_Comm.cpp:81-348) */
+static int send_recv(or_grid *g, or_cls *c, double *v, int op)
+{
+   int return_flag = 0;
+   const int len = c->len;
+   for (int i = 0; i < c->np; i++) {
+      const int ip = c->procs[i];
+      c->recv_flags[i] = 0;
+      if (c->send) {
+         if (c->done_flags[i] >= 2) continue;
+         if (op == OR_MSG_WRITE)
+            memcpy(c->data[i], v, (size_t)len * sizeof(double));
+         else
+            for (int j = 0; j < len; j++) c->data[i][j] += 1.0 * v[j];
+         check_inflight(g, c, i);
+         if (c->num_inflight[i] >= c->max_inflight) continue;
+         const int nx = c->next_inflight[i];
+         double *slot = c->data_inflight[i][nx];
+         memcpy(slot, c->data[i], (size_t)len * sizeof(double));
+         for (int j = 0; j < len; j++) c->data[i][j] = 0.0;
+         slot[len] = 0.0;
+         if (g->grid_done_flag == 1) {
+            slot[len] = 1.0;
+            if (g->converge_local) {
+               c->done_flags[i] = 2;
+            } else {
+               c->done_flags[i] = 1;
+               if (g->all_done_flag == 1) {
+                  c->done_flags[i] = 2;
+                  slot[len] = 2.0;
+               }
+            }
+         }
+         c->requests_inflight[i][nx] = mb_isend(g->M, g->k, ip, slot, len, slot[len]);
+         c->inflight_flags[i][nx] = 1;
+         c->num_inflight[i]++;
+         set_next_inflight(c, i);
+         c->message_count[i]++;
+         g->sent++;
+         return_flag = 1;
+      } else {
+         if (c->done_flags[i] >= 2) continue;
+         while (1) {
+            or_rec *rq = c->requests[i];
+            if (!mb_matched(g->M, rq)) break;
+            c->message_count[i]++;
+            g->rcvd++;
+            const or_rec *s = rq->peer;
+            for (int j = 0; j < len; j++) v[j] += 1.0 * s->pay[j];
+            const double fl = s->flag;
+            mb_consume(g->M, rq);
+            if (g->converge_local) {
+               if (fl == 1.0) {
+                  c->done_flags[i] = 2;
+                  break;
+               }
+            } else {
+               if (fl == 1.0) {
+                  c->done_flags[i] = 1;
+               } else if (fl == 2.0) {
+                  c->done_flags[i] = 2;
+                  break;
+               }
+            }
+            c->requests[i] = mb_irecv(g->M, g->k, ip);
+            c->recv_flags[i] = 1;
+            return_flag = 1;
+            if (g->semi && g->all_done_flag == 0) break;
+         }
+      }
+   }
+   return return_flag;
+}
+
+/* AddCycle (DMEM_Add.cpp:180-329), NUMLEVELS_INTERPOLANTS, grid k; u = U[0] */
+static void add_cycle(or_grid *g)
+{
+   or_hier *H = g->H;
+   const int k = g->k, L = g->L;
+   memcpy(g->F[0], g->r, (size_t)g->n0 * sizeof(double));
+   for (int l = 0; l < k; l++) or_smem_matvec(&H->R[l], g->F[l], g->F[l + 1], 0, H->n[l + 1]);
+   if (k == L - 1) {
+      /* hypre_GaussElimSolve: A_c u = f_c, dense LU with partial pivoting */
+      const int n = g->nc;
+      double *x = g->U[k];
+      memcpy(x, g->F[k], (size_t)n * sizeof(double));
+      for (int c = 0; c < n; c++)
+         if (g->piv[c] != c) {
+            double t = x[c];
+            x[c] = x[g->piv[c]];
+            x[g->piv[c]] = t;
+         }
+      for (int i = 0; i < n; i++)
+         for (int j = 0; j < i; j++) x[i] -= g->lu[(size_t)i * n + j] * x[j];
+      for (int i = n - 1; i >= 0; i--) {
+         for (int j = i + 1; j < n; j++) x[i] -= g->lu[(size_t)i * n + j] * x[j];
+         const double dd = g->lu[(size_t)i * n + i];
+         x[i] = dd != 0.0 ? x[i] / dd : 0.0;
+      }
+   } else {
+      /* DMEM_AddSmooth (DMEM_Smooth.cpp:574-638), simple_jacobi_flag = -1:
+       * u = 0 + f ./ s;  v = A u;  u = 2 u;  u = u + v ./ (-s) */
+      const int n = H->n[k];
+      double *u = g->U[k];
+      for (int i = 0; i < n; i++) u[i] = 0.0;
+      for (int i = 0; i < n; i++) u[i] += g->F[k][i] / g->sc[i];
+      or_smem_matvec(&H->A[k], u, g->vt, 0, n);
+      for (int i = 0; i < n; i++) u[i] = 2.0 * u[i];
+      for (int i = 0; i < n; i++) u[i] += g->vt[i] / g->nsc[i];
+   }
+   for (int l = k - 1; l >= 0; l--) or_smem_matvec(&H->P[l], g->U[l + 1], g->U[l], 0, H->n[l]);
+   if (g->accel != OR_NO_ACCEL) {
+      /* :320-324 DMEM_ChebyUpdate(gridk.d, U_array[0]), async branch */
+      or_dmem_cheby_update(g->d, g->U[0], g->n0, g->acc_cycle, g->accel, g->cheby_mine ? OR_CHEBY_GRID : OR_CHEBY_OTHER,
+                           g->mu, g->delta, g->acc_state);
+      g->acc_cycle++;
+   }
+}
+
+/* r = b - A x (DMEM_AddResidual_LocalRes, :530-556); returns r.r */
+static double add_residual(or_grid *g)
+{
+   or_smem_spgemv(&g->H->A[0], g->x, g->b, -1.0, 1.0, g->r, 0, g->n0);
+   double s = 0.0;
+   for (int i = 0; i < g->n0; i++) s += g->r[i] * g->r[i];
+   return s;
+}
+
+/* DMEM_AddCheckComm (:460-528) */
+static void add_check_comm(or_grid *g)
+{
+   for (int i = 0; i < g->n0; i++) g->e[i] = 0.0;
+   const int recv_flag = send_recv(g, &g->recv, g->e, OR_MSG_ACCUMULATE);
+   if (recv_flag == 1) {
+      for (int i = 0; i < g->n0; i++) g->x[i] += 1.0 * g->e[i];
+      if (g->accel != OR_NO_ACCEL && g->cheby_mine)
+         for (int i = 0; i < g->n0; i++) g->d[i] += 1.0 * g->e[i];
+   }
+   for (int i = 0; i < g->send.np; i++) check_inflight(g, &g->send, i);
+}
+
+/* DMEM_AddCorrect_LocalRes (:391-458) */
+static void add_correct(or_grid *g)
+{
+   double *u = g->U[0];
+   for (int i = 0; i < g->n0; i++) g->y[i] += 1.0 * u[i];
+   if (g->converge_flag == 1 || g->cycle % g->save == 0) {
+      send_recv(g, &g->send, g->y, OR_MSG_ACCUMULATE);
+      for (int i = 0; i < g->n0; i++) g->y[i] = 0.0;
+   }
+   for (int i = 0; i < g->n0; i++) g->x[i] += 1.0 * u[i];
+   add_check_comm(g);
+}
+
+static int all_flags(const or_cls *c, int v)
+{
+   for (int i = 0; i < c->np; i++)
+      if (c->done_flags[i] != v) return 0;
+   return 1;
+}
+
+/* CheckConverge (:906-944) with DMEM_CheckOutsideDoneFlag (:795-803) */
+static int check_converge(or_grid *g)
+{
+   if (!g->converge_local) {
+      if (g->all_done_flag == 0) {
+         if (g->grid_done_flag == 0 && (g->cycle >= g->num_cycles - 1 || g->r_local_converge_flag == 1))
+            g->grid_done_flag = 1;
+         if (g->grid_done_flag == 1 && g->outside_done_flag == 0) {
+            int ok = 1;
+            for (int i = 0; i < g->send.np; i++)
+               if (g->send.done_flags[i] == 0) ok = 0;
+            for (int i = 0; i < g->recv.np; i++)
+               if (g->recv.done_flags[i] == 0) ok = 0;
+            if (ok) g->outside_done_flag = 1;
+         }
+         return 0;
+      }
+      return 1;
+   }
+   if (g->cycle >= g->num_cycles - 1 || g->r_local_converge_flag == 1) {
+      g->grid_done_flag = 1;
+      return 1;
+   }
+   return 0;
+}
+
+/* the grid's solve: DMEM_Add's asynchronous branch (:20-178) */
+static void grid_run(or_grid *g)
+{
+   or_mbox *M = g->M;
+   for (int i = 0; i < g->n0; i++) g->y[i] = g->e[i] = g->d[i] = 0.0;
+   g->r0_norm2 = sqrt(add_residual(g));
+   if (g->r0_norm2 == 0.0) g->r0_norm2 = 1.0;
+   g->r_local = 1.0;
+   for (int i = 0; i < g->recv.np; i++) g->recv.requests[i] = mb_irecv(M, g->k, g->recv.procs[i]); /* AsyncStart */
+   rr_wait(M, g->k);
+   while (1) {
+      g->converge_flag = check_converge(g);
+      add_cycle(g);
+      add_correct(g);
+      const double rr = add_residual(g);
+      if (g->all_done_flag == 0 && !g->semi) {
+         /* AddResNorm: InnerProdFlag over the grid (one rank: local) */
+         g->r_local = sqrt(rr) / g->r0_norm2;
+         if (g->r_local < g->tol) g->r_local_converge_flag = 1;
+         if (g->outside_done_flag == 1) g->all_done_flag = 1;
+      }
+      g->cycle++;
+      rr_yield(M, g->k);
+      if (g->converge_flag == 1) break;
+   }
+   /* AsyncEnd: AsyncRecvCleanup (:827-890) */
+   for (int i = 0; i < g->n0; i++) g->e[i] = 0.0;
+   double *zero = dvec(g->n0);
+   while (1) {
+      if (g->converge_local ? (all_flags(&g->recv, 2) && all_flags(&g->send, 2)) : all_flags(&g->recv, 2)) break;
+      send_recv(g, &g->recv, g->e, OR_MSG_ACCUMULATE);
+      if (g->converge_local) send_recv(g, &g->send, zero, OR_MSG_ACCUMULATE);
+      rr_yield(M, g->k);
+   }
+   free(zero);
+   for (int i = 0; i < g->n0; i++) g->x[i] += 1.0 * g->e[i];
+   /* CompleteInFlight (DMEM_Comm.cpp:11-23) */
+   for (int i = 0; i < g->send.np; i++)
+      for (int j = 0; j < g->send.max_inflight; j++)
+         if (g->send.inflight_flags[i][j] == 1) {
+            while (!mb_sent(M, g->send.requests_inflight[i][j])) {
+               if (M->sched)
+                  rr_yield(M, g->k);
+               else
+                  sched_yield();
+            }
+            g->send.inflight_flags[i][j] = 0;
+         }
+   rr_pass(M, g->k, 1);
+}
+
+int or_dmem_add(or_hier *H, const double *b, double *x_out, int sched, int converge_type, int async_type,
+                int max_inflight, int save_divisor, double tol, int accel, int cheby_grid, double mu, double delta,
+                int *cycles, double *relres, long long *messages)
+{
+   const int L = H->L, n0 = H->n[0], G = L;
+   if (G < 2 || max_inflight < 1) return -1;
+   if (async_type == OR_SEMI_ASYNC && converge_type == OR_CONVERGE_GLOBAL) return -1; /* :346-358 */
+   or_mbox M;
+   memset(&M, 0, sizeof(M));
+   M.G = G;
+   M.sendq = (or_rec **)calloc((size_t)G * G, sizeof(or_rec *));
+   M.recvq = (or_rec **)calloc((size_t)G * G, sizeof(or_rec *));
+   omp_init_lock(&M.lock);
+   M.sched = sched;
+   M.finished = (int *)calloc(G, sizeof(int));
+   or_grid *gs = (or_grid *)calloc(G, sizeof(or_grid));
+   const int cg = cheby_grid < L - 1 ? cheby_grid : L - 1; /* DMEM_Setup.cpp:1911-1913 */
+   for (int k = 0; k < G; k++) {
+      or_grid *g = &gs[k];
+      g->H = H;
+      g->M = &M;
+      g->k = k;
+      g->L = L;
+      g->n0 = n0;
+      g->converge_local = converge_type == OR_CONVERGE_LOCAL;
+      g->semi = async_type == OR_SEMI_ASYNC;
+      g->save = save_divisor > 0 ? save_divisor : 1;
+      g->tol = tol;
+      g->num_cycles = H->o.num_cycles;
+      g->accel = accel;
+      g->cheby_mine = k == cg;
+      g->mu = mu;
+      g->delta = delta;
+      g->acc_state[0] = mu;
+      g->acc_state[1] = 1.0;
+      cls_init(&g->send, 1, G, k, n0, max_inflight);
+      cls_init(&g->recv, 0, G, k, n0, max_inflight);
+      g->x = dvec(n0); g->b = dvec(n0); g->r = dvec(n0); g->y = dvec(n0); g->e = dvec(n0); g->d = dvec(n0);
+      memcpy(g->b, b, (size_t)n0 * sizeof(double));
+      g->F = (double **)malloc((k + 1) * sizeof(double *));
+      g->U = (double **)malloc((k + 1) * sizeof(double *));
+      for (int l = 0; l <= k; l++) {
+         g->F[l] = dvec(H->n[l]);
+         g->U[l] = dvec(H->n[l]);
+      }
+      g->vt = dvec(H->n[k]);
+      if (k == L - 1) {
+         /* hypre_GaussElimSetup: the coarsest operator dense, LU with partial pivoting */
+         const or_csr *A = &H->A[k];
+         const int n = A->nrows;
+         g->nc = n;
+         g->lu = (double *)calloc((size_t)n * n, sizeof(double));
+         g->piv = (int *)calloc(n, sizeof(int));
+         for (int i = 0; i < n; i++)
+            for (int q = A->i[i]; q < A->i[i + 1]; q++) g->lu[(size_t)i * n + A->j[q]] += A->data[q];
+         for (int c = 0; c < n; c++) {
+            int p = c;
+            for (int i = c + 1; i < n; i++)
+               if (fabs(g->lu[(size_t)i * n + c]) > fabs(g->lu[(size_t)p * n + c])) p = i;
+            g->piv[c] = p;
+            if (p != c)
+               for (int j = 0; j < n; j++) {
+                  double t = g->lu[(size_t)c * n + j];
+                  g->lu[(size_t)c * n + j] = g->lu[(size_t)p * n + j];
+                  g->lu[(size_t)p * n + j] = t;
+               }
+            const double dd = g->lu[(size_t)c * n + c];
+            if (dd == 0.0) continue;
+            for (int i = c + 1; i < n; i++) {
+               const double m = (g->lu[(size_t)i * n + c] /= dd);
+               for (int j = c + 1; j < n; j++) g->lu[(size_t)i * n + j] -= m * g->lu[(size_t)c * n + j];
+            }
+         }
+      } else {
+         /* wJacobi_scale_gridk / symmwJacobi_scale_gridk (DMEM_Setup.cpp:471-482) */
+         const or_csr *A = &H->A[k];
+         const int n = A->nrows;
+         g->sc = dvec(n);
+         g->nsc = dvec(n);
+         for (int i = 0; i < n; i++) {
+            const double a = A->data[A->i[i]];
+            g->sc[i] = a == 0.0 ? 1.0 : a / H->o.smooth_weight;
+            g->nsc[i] = -g->sc[i];
+         }
+      }
+   }
+#pragma omp parallel num_threads(G)
+   grid_run(&gs[omp_get_thread_num()]);
+   for (int k = 0; k < G; k++) {
+      or_grid *g = &gs[k];
+      const double rr = add_residual(g);
+      memcpy(x_out + (size_t)k * n0, g->x, (size_t)n0 * sizeof(double));
+      if (cycles) cycles[k] = g->cycle;
+      if (relres) relres[k] = sqrt(rr) / g->r0_norm2;
+      if (messages) {
+         messages[2 * k] = g->sent;
+         messages[2 * k + 1] = g->rcvd;
+      }
+      cls_free(&g->send);
+      cls_free(&g->recv);
+      free(g->x); free(g->b); free(g->r); free(g->y); free(g->e); free(g->d); free(g->vt);
+      for (int l = 0; l <= k; l++) {
+         free(g->F[l]);
+         free(g->U[l]);
+      }
+      free(g->F); free(g->U); free(g->sc); free(g->nsc); free(g->lu); free(g->piv);
+   }
+   while (M.all) {
+      or_rec *r = M.all;
+      M.all = r->all;
+      free(r->pay);
+      free(r);
+   }
+   omp_destroy_lock(&M.lock);
+   free(M.sendq); free(M.recvq); free(M.finished); free(gs);
+   return 0;
 }

@@ -144,6 +144,16 @@ or_hier *or_hier_create(int num_levels, const or_csr *A, const or_csr *P, const 
 void or_hier_free(or_hier *H);
 /* override a level's hybrid-JGS block partition (blk[nblk+1]) */
 void or_hier_set_blocks(or_hier *H, int level, const int *blk, int nblk);
+/* on = 1: the MULTADD solvers' transfers are the reference's smoothed ones,
+ * P~ = (I - w D^-1 A) P and R~ = P~^T (SmoothTransfer, SMEM_Setup.cpp:1173-1254,
+ * w = smooth_weight, JACOBI smooth_interp_type), applied COMPOSED from the
+ * hierarchy's plain P, R and A (A symmetric, R = P^T):
+ *    R~ r = R (r - w A (D^-1 r)):  t = r / a;  y = A t;  z = r + (-w) y;  R z
+ *    P~ e = P e - w D^-1 A P e:    p = P e;  y = A p;  t = y / a;  p + (-w) t
+ * in exactly this order of operations (the device's composed transfers, on
+ * one GPU and on z-slabs, follow it bit for bit); the hierarchy's P / R stay
+ * the plain ones. */
+void or_hier_set_composed_transfers(or_hier *H, int on);
 /* SMEM_Solve sync branch; f/u are level-0 vectors (u is the initial guess and
  * receives the result).  reshist[k] = ||r_k||_2 for k = 0..cycles done.
  * Returns the number of cycles performed. */
@@ -201,8 +211,12 @@ double or_dmem_async_jacobi(const or_csr *A, const double *b, double *x, int swe
 #define OR_CONVERGE_GLOBAL 1
 #define OR_READ_SOL 0
 #define OR_READ_RES 1
-/* group schedule of or_async_add (converge LOCAL): 0 free, 1 / 2 one group
- * after another, finest / coarsest first */
+/* group schedule of or_async_add: 0 free (the OS's); 1 / 2 one group after
+ * another, finest / coarsest first (converge LOCAL only); 3 round robin: the
+ * groups take turns, one whole correction each, finest first (LOCAL or
+ * GLOBAL).  1-3 are deterministic admissible schedules of the race: the
+ * device's deterministic-schedule mode (amg_opts.async_schedule) is checked
+ * against them bit for bit. */
 void or_set_async_schedule(int s);
 /* res_compute_type GLOBAL for or_async_add (ASYNC_MULTADD, READ_SOL): nt[0] = 0
  * (no level-0 group), each thread smooths its global fine slice (:35-77, 356-414) */
@@ -212,6 +226,21 @@ void or_set_async_res_global(int on);
 void or_set_async_accel(int accel, int grid, double mu, double delta);
 int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int async_type, int read_type,
                  int converge_type, int *corrections, double *relres);
+
+/* DMEM_Add (DMEM_Add.cpp:20-944, DMEM_Comm.cpp:11-382): the level-grouped
+ * asynchronous additive solver on L OpenMP threads standing in for the ranks,
+ * one rank per grid (grid k = level k's correction, the coarsest grid an exact
+ * dense LU solve), correction messages through an in-process mailbox with MPI
+ * matching (a send completes once its receiver took the payload).  sched 0:
+ * the free race; 1: round robin (a token passes between the grids at fixed
+ * points -- bit-identical to the device's amg_grid_add_solve with
+ * async_schedule = AMG_SCHED_ROUND_ROBIN).  The hierarchy's opts give
+ * smooth_weight and num_cycles.  x_out[k * n0 ...]: grid k's iterate (all
+ * rows); cycles[k], relres[k] (||b - A x_k|| / ||b||), messages[2k, 2k + 1]
+ * (sent, received).  b: right-hand side, x0 = 0. */
+int or_dmem_add(or_hier *H, const double *b, double *x_out, int sched, int converge_type, int async_type,
+                int max_inflight, int save_divisor, double tol, int accel, int cheby_grid, double mu, double delta,
+                int *cycles, double *relres, long long *messages);
 
 /* access the hierarchy's level vectors (u, f) for tests */
 double *or_hier_vec(or_hier *H, const char *name, int level);

@@ -63,6 +63,7 @@ def lib():
                                      C.POINTER(OrCsr), C.POINTER(OrOpts)]
         L.or_hier_free.argtypes = [C.c_void_p]
         L.or_hier_set_blocks.argtypes = [C.c_void_p, C.c_int, _ip, C.c_int]
+        L.or_hier_set_composed_transfers.argtypes = [C.c_void_p, C.c_int]
         L.or_solve.argtypes = [C.c_void_p, _dp, _dp, _dp]
         L.or_solve.restype = C.c_int
         L.or_vcycle.argtypes = [C.c_void_p]
@@ -80,6 +81,9 @@ def lib():
         L.or_set_async_schedule.argtypes = [C.c_int]
         L.or_set_async_res_global.argtypes = [C.c_int]
         L.or_set_async_accel.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double]
+        L.or_dmem_add.restype = C.c_int
+        L.or_dmem_add.argtypes = [C.c_void_p, _dp, _dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
+                                  C.c_int, C.c_int, C.c_double, C.c_double, _ip, _dp, C.POINTER(C.c_longlong)]
         L.or_async_add.restype = C.c_int
         L.or_async_add.argtypes = [C.c_void_p, _dp, _dp, _ip, C.c_int, C.c_int, C.c_int, _ip,
                                    C.POINTER(C.c_double)]
@@ -361,6 +365,12 @@ class Hier:
         self.opts = opts
         self.h = lib().or_hier_create(self.L, self.Ac, self.Pc, self.Rc, C.byref(self.opts))
 
+    def set_composed_transfers(self, on=True):
+        """MULTADD transfers = the smoothed P~ = (I - w D^-1 A) P, R~ = P~^T
+        (SmoothTransfer, SMEM_Setup.cpp:1173-1254) applied composed from the
+        plain P / R (or_hier_set_composed_transfers)"""
+        lib().or_hier_set_composed_transfers(self.h, 1 if on else 0)
+
     def set_blocks(self, level, blk):
         blk = np.ascontiguousarray(blk, dtype=np.int32)
         lib().or_hier_set_blocks(self.h, level, iptr(blk), len(blk) - 1)
@@ -380,6 +390,24 @@ class Hier:
         k = lib().or_dmem_mult_solve(self.h, dptr(np.ascontiguousarray(b, dtype=np.float64)), dptr(x),
                                      dptr(hist), accel, mu, delta)
         return x, hist[:k + 1], k
+
+    def dmem_add(self, b, sched=0, converge_type=0, async_type=0, max_inflight=1, save_divisor=1, tol=0.0,
+                 accel=None):
+        """DMEM_Add (DMEM_Add.cpp:20-944) on L threads, one rank per grid:
+        (x per grid [L, n0], cycles[L], relres[L], messages[L, 2] (sent, received)).
+        sched 0: the free race (nondeterministic); 1: round robin."""
+        n0 = self._keep[0][0].nrows
+        x = np.zeros(self.L * n0)
+        cyc = np.zeros(self.L, dtype=np.int32)
+        rel = np.zeros(self.L)
+        msg = np.zeros(2 * self.L, dtype=np.int64)
+        acc = accel if accel is not None else (0, 0, 0.0, 0.0)
+        st = lib().or_dmem_add(self.h, dptr(np.ascontiguousarray(b, dtype=np.float64)), dptr(x), int(sched),
+                               int(converge_type), int(async_type), int(max_inflight), int(save_divisor),
+                               float(tol), int(acc[0]), int(acc[1]), float(acc[2]), float(acc[3]), iptr(cyc),
+                               dptr(rel), msg.ctypes.data_as(C.POINTER(C.c_longlong)))
+        assert st == 0, st
+        return x.reshape(self.L, n0), cyc, rel, msg.reshape(self.L, 2)
 
     def async_add(self, f, nt, async_type=0, converge_type=0, u0=None, read_type=0, res_global=False,
                   accel=None):

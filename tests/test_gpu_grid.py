@@ -5,12 +5,13 @@ halo over the host transport), computes its level's AddCycle correction
 (restriction, DMEM_AddSmooth or the coarsest grid's exact solve, prolongation)
 and exchanges corrections with the overlapping ranks of the other grids
 through the message protocol: over the host transport (rendezvous mailboxes:
-the in-flight pools fill) or the device hub (amg_devhub: payloads copied
-device to device, never staged through host memory).  Asynchronous, so checked
-as a band: every grid's final relative residual lies in [0.5 x min, 2 x max]
-of the oracle's asynchronous additive band (SMEM_Async_Add_AMG on threads,
-the same level corrections racing on one iterate), every message sent is
-received, and the grids' iterates agree (they all add every correction)."""
+the in-flight pools fill) or the device hub (amg_devhub: payloads read device
+to device, never staged through host memory).  The arithmetic and protocol are
+pinned bit for bit against the oracle's DMEM_Add restatement (or_dmem_add)
+under the round-robin schedule; the free race is checked as a band of that
+restatement: every grid's final relative residual lies in [0.5 x min, 2 x max]
+of or_dmem_add's free races and round robin, every message sent is received,
+and the grids' iterates agree (they all add every correction)."""
 import threading
 
 import numpy as np
@@ -86,23 +87,73 @@ def grid_solve(amg, L, host, f, ppg, transport="host", **kw):
 _bands = {}
 
 
+def dmem_band(oracle, host, f, opts, reps=10):
+    """the band of the DMEM_Add restatement (oracle or_dmem_add: grids as
+    threads, one rank per grid, the same AddCycle / message protocol /
+    termination): `reps` free races and the round-robin schedule; every grid's
+    final relative residual of every run"""
+    o = oracle.make_opts(solver=oracle.OR_ASYNC_MULTADD, smooth_weight=opts.smooth_weight,
+                         num_cycles=opts.num_cycles, tol=opts.tol)
+    OH = oracle.Hier(host["A"], host["P"], host["R"], o)
+    kw = dict(converge_type=oracle.OR_CONVERGE_GLOBAL if opts.converge_test_type == 1 else oracle.OR_CONVERGE_LOCAL,
+              async_type=opts.async_type, max_inflight=opts.max_inflight,
+              save_divisor=opts.async_comm_save_divisor, tol=opts.tol)
+    rels = []
+    for sched in [0] * reps + [1]:
+        _, _, rel, _ = OH.dmem_add(f, sched=sched, **kw)
+        rels += rel.tolist()
+    return min(rels), max(rels), rels, None
+
+
+@pytest.mark.parametrize("conv,at,inflight,save", [("local", 0, 1, 1), ("global", 0, 2, 1), ("local", 1, 1, 1),
+                                                    ("local", 0, 2, 2)])
+def test_grid_add_round_robin_bitwise(amg, oracle, mult24, conv, at, inflight, save):
+    """The level-grouped solve's arithmetic and protocol pinned bit for bit:
+    one rank per grid over the device hub with async_schedule = ROUND_ROBIN
+    (a token passes between the grids at the oracle's yield points) against
+    the oracle's DMEM_Add restatement (or_dmem_add, DMEM_Add.cpp:20-944,
+    DMEM_Comm.cpp:11-382) under the same schedule: every grid's iterate is the
+    same bits, with the same cycle and message counts -- AddCycle with the
+    coarsest grid's exact solve, AddCorrect / AddCheckComm including the
+    dropped final payload, CheckInFlight with max_inflight, the save divisor,
+    CheckConverge LOCAL / GLOBAL and AsyncRecvCleanup."""
+    L, host, f = mult24
+    N = 12
+    res, opts = grid_solve(amg, L, host, f, (1,) * L, transport="device", num_cycles=N, max_inflight=inflight,
+                           async_comm_save_divisor=save, async_type=at,
+                           converge_test_type=amg.AMG_GLOBAL if conv == "global" else amg.AMG_LOCAL,
+                           async_schedule=amg.AMG_SCHED_ROUND_ROBIN)
+    o = oracle.make_opts(solver=oracle.OR_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=N, tol=0.0)
+    OH = oracle.Hier(host["A"], host["P"], host["R"], o)
+    xo, co, ro, mo = OH.dmem_add(f, sched=1, converge_type=oracle.OR_CONVERGE_GLOBAL if conv == "global"
+                                 else oracle.OR_CONVERGE_LOCAL, async_type=at, max_inflight=inflight,
+                                 save_divisor=save)
+    for g, row0, x, cyc, rel, msgs in res:
+        nd = int(np.count_nonzero(x.view(np.uint64) != xo[g].view(np.uint64)))
+        print(f"grid {g}: device relres {rel:.6e} oracle {ro[g]:.6e}, cycles {cyc}/{co[g]}, "
+              f"messages {list(msgs)}/{list(mo[g])}, differing entries {nd}")
+        assert cyc == co[g]
+        assert list(msgs) == list(mo[g])
+        assert nd == 0, g
+        assert abs(rel - ro[g]) <= 1e-10 * ro[g]
+
+
 @pytest.mark.parametrize("transport", ["host", "device"])
 @pytest.mark.parametrize("ppg,conv,inflight", [((1, 1, 1, 1), "local", 1), ((2, 1, 1, 1), "global", 2),
                                                ((2, 2, 1, 1), "local", 3)])
 def test_grid_add_converges(amg, oracle, mult24, ppg, conv, inflight, transport):
-    from async_band import in_band, oracle_async_band
+    from async_band import in_band
     L, host, f = mult24
     ppg = ppg[:L] if len(ppg) >= L else ppg + (1,) * (L - len(ppg))
     N = 20
     res, opts = grid_solve(amg, L, host, f, ppg, transport=transport, num_cycles=N, max_inflight=inflight,
                            converge_test_type=amg.AMG_GLOBAL if conv == "global" else amg.AMG_LOCAL)
-    # converge GLOBAL: every grid keeps correcting until all are done, so the
-    # fast grids run more than N cycles -- the band adds the equal-speed
-    # schedule at the device's largest cycle count
-    extra = (max(r[3] for r in res),) if conv == "global" else ()
-    key = (conv, extra)
+    # the band of the DMEM_Add restatement itself (or_dmem_add free races and
+    # its round robin; one rank per grid there -- multi-rank device grids
+    # exchange the same corrections in row pieces)
+    key = (conv, inflight)
     if key not in _bands:
-        _bands[key] = oracle_async_band(amg, oracle, host, f, opts, lockstep_cycles=extra)
+        _bands[key] = dmem_band(oracle, host, f, opts)
     lo, hi, _, _ = _bands[key]
     n = host["A"][0].nrows
     xs = {}

@@ -5,9 +5,9 @@ mapped into its receiver by hipIpcGetMemHandle / hipIpcOpenMemHandle; gloo
 carries only the handles, the (slot, done flag) control words and the
 acknowledgements), against the same solve with the payloads over gloo
 (amg_grid_add_create: D2H / H2D per message).  One grid per level, one rank
-per grid; asynchronous, so checked as the oracle's async band (tests/async_band.py):
-every grid's final relative residual in [0.5 x min, 2 x max], every message
-sent received."""
+per grid; asynchronous, so checked against the band of the oracle's DMEM_Add
+restatement (or_dmem_add, tests/test_gpu_grid.py dmem_band): every grid's final
+relative residual in [0.5 x min, 2 x max], every message sent received."""
 import os
 import socket
 
@@ -19,9 +19,8 @@ pytestmark = pytest.mark.gpu
 N = 20
 
 
-NX = 24  # the full 24^3 hierarchy (5 levels, 5 grids): its coarsest grid's exact
-# solve is small, as in the oracle band's SMEM_Async_Add_AMG, where the coarsest
-# level does not correct (its solve is commented out, SMEM_Async_AMG.cpp:112-132)
+NX = 24  # the full 24^3 hierarchy (5 levels, 5 grids; the coarsest grid's exact solve
+# is restated by the oracle's DMEM_Add, or_dmem_add)
 
 
 def _host(amg, oracle):
@@ -81,7 +80,7 @@ def _rank(rank, world, port, ipc, q):
 @pytest.mark.parametrize("transport", ["ipc", "host"])
 def test_grid_add_processes(amg, oracle, transport):
     import multiprocessing as mp
-    from async_band import in_band, oracle_async_band
+    from async_band import in_band
     L, host, f = _host(amg, oracle)
     world = L
     with socket.socket() as s:
@@ -103,11 +102,11 @@ def test_grid_add_processes(amg, oracle, transport):
             p.join(30)
             if p.is_alive():
                 p.kill()
-    # five processes share one GPU and (host transport) a gloo mailbox, so the
-    # grids run at very uneven speeds: the band also holds the extreme speed
-    # ratios (the groups one after another, finest / coarsest first), the
-    # admissible schedules of the same race (tests/async_band.py)
-    lo, hi, _, _ = oracle_async_band(amg, oracle, host, f, _opts(amg), sequential=True)
+    # the band of the DMEM_Add restatement itself (oracle or_dmem_add: the same
+    # grids, AddCycle, messages and termination on threads; free races plus
+    # its round robin)
+    from test_gpu_grid import dmem_band
+    lo, hi, _, _ = dmem_band(oracle, host, f, _opts(amg))
     print(f"grid add processes {transport} L={L}: oracle band [{lo:.4e}, {hi:.4e}], "
           f"ranks (finite, cycles, rel, sent, received) {[out[r][1:] for r in sorted(out)]}")
     for r in range(world):

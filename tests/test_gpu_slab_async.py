@@ -1,0 +1,181 @@
+"""The asynchronous additive solve on z-slab hierarchies (config 4's path):
+amg_dist_async_solve with per-level device-resident channels between ranks
+(csrc/amg_link.cpp) and the reference's smoothed transfers composed on the fly
+(smooth_transfer = 1: P~ = (I - w D^-1 A) P, R~ = P~^T, SmoothTransfer,
+SMEM_Setup.cpp:1173-1254; DMEM_Add.cpp:20-178 / SMEM_Async_AMG.cpp:7-437).
+
+* Deterministic schedules (async_schedule 1 / 2 / 3) pin the arithmetic: the
+  assembled iterate of 1-3 ranks is bit-identical to the oracle's
+  or_async_add under the same schedule with composed transfers
+  (or_hier_set_composed_transfers), one thread per level group.
+* The free race converges and lands in the oracle's asynchronous band.
+* At 512^3 the free race converges (relres < 0.5 after N corrections per
+  level) at 1 rank (RCCL) and 2 / 8 ranks (the host transport for setup, the
+  device-resident channels for every exchange).
+
+Ranks run as threads of this process on cuda:0 (RCCL refuses two ranks per
+device); each rank's level groups run on their own host threads."""
+import numpy as np
+import pytest
+
+from async_band import in_band, oracle_async_band
+from test_gpu_dist import run_ranks
+from test_gpu_kernels import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+W = 0.8
+
+
+def slab_async(amg, gen, opts, f, nranks, rep=1 << 12, rccl1=True, runs=1):
+    hub = amg.dist.ThreadMailbox(nranks, timeout=900.0)
+
+    def rank(r):
+        c = amg.Context(0, nstreams=gen.L + 2)
+        tr = None
+        if nranks == 1 and rccl1:
+            amg.dist.init_rccl(c, 1, 0, lambda b: b)
+        else:
+            tr = amg.dist.HostTransport(hub, r)
+            amg.dist.init_host(c, nranks, r, tr)
+        amg.dist.set_replicate_rows(c, rep)
+        D = amg.dist.DistHier(c, gen, opts, slab=True)
+        out = []
+        for _ in range(runs):
+            rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
+            out.append((rel, cnt.copy(), D.get_u(), D.async_level_ms()))
+        row0 = D.row0
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        if tr is not None and tr.error is not None:
+            raise tr.error
+        return row0, out
+
+    res = run_ranks(nranks, rank)
+    res.sort(key=lambda t: t[0])
+    runs_out = []
+    for q in range(runs):
+        rel = res[0][1][q][0]
+        assert all(t[1][q][0] == rel for t in res)  # one allreduced norm
+        u = np.concatenate([t[1][q][2] for t in res])
+        runs_out.append((rel, res[0][1][q][1], u, [t[1][q][3] for t in res]))
+    return runs_out
+
+
+def host_hier(amg, oracle, gen):
+    L = gen.L
+    host = {}
+    for which, tag, cnt in ((amg.AMG_GEN_A, "A", L), (amg.AMG_GEN_P, "P", L - 1), (amg.AMG_GEN_R, "R", L - 1)):
+        host[tag] = [oracle.Csr(*gen.host_csr(which, l)) for l in range(cnt)]
+    return host
+
+
+def oracle_opts_of(oracle, o):
+    return oracle.make_opts(solver=o.solver, smoother=o.smoother, num_pre=o.num_pre_smooth_sweeps,
+                            num_post=o.num_post_smooth_sweeps, num_fine=o.num_fine_smooth_sweeps,
+                            num_coarse=o.num_coarse_smooth_sweeps, smooth_weight=o.smooth_weight,
+                            num_cycles=o.num_cycles, tol=o.tol)
+
+
+SCHED = [
+    # (solver, composed transfers, nranks, schedule)
+    ("multadd", True, 1, 3),
+    ("multadd", True, 2, 3),
+    ("multadd", True, 3, 1),
+    ("multadd", True, 2, 2),
+    ("afacx", False, 2, 3),
+    ("afacx", False, 3, 2),
+]
+
+
+@pytest.mark.parametrize("solver,comp,nranks,sched", SCHED, ids=[f"{s}-{n}r-s{q}" for s, _, n, q in SCHED])
+def test_slab_async_schedule_bitwise(amg, oracle, ctx, solver, comp, nranks, sched):
+    """deterministic schedules of the slab-distributed asynchronous additive
+    solve against the oracle's or_async_add (SMEM_Async_Add_AMG restated) under
+    the same schedule: the assembled iterate is the same bits"""
+    n, N = 32, 8
+    gen = amg.Gen(n)
+    f = amg.rhs_rand(0, n ** 3)
+    sv = amg.AMG_ASYNC_MULTADD if solver == "multadd" else amg.AMG_ASYNC_AFACX
+    opts = amg.default_opts(solver=sv, smooth_weight=W, num_cycles=N, tol=0.0, async_schedule=sched,
+                            smooth_transfer=1 if comp else 0)
+    ((rel, cnt, u, _),) = slab_async(amg, gen, opts, f, nranks, rep=1 << 10, rccl1=False)
+    host = host_hier(amg, oracle, gen)
+    L = gen.L
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts_of(oracle, opts))
+    if comp:
+        OH.set_composed_transfers()
+    oracle.lib().or_set_async_schedule(sched)
+    try:
+        uo, relo, cnto = OH.async_add(f, [1] * L)
+    finally:
+        oracle.lib().or_set_async_schedule(0)
+    assert list(cnt[:L - 1]) == list(cnto[:L - 1]) == [N] * (L - 1)
+    nd = int(np.count_nonzero(u.view(np.uint64) != uo.view(np.uint64)))
+    print(f"slab async {solver} composed={comp} {nranks} ranks schedule {sched}: device {rel:.13e} "
+          f"oracle {relo:.13e}, differing entries {nd}")
+    assert_bitwise(u, uo, "slab async iterate vs oracle")
+    assert abs(rel - relo) <= 1e-12 * relo
+    gen.free()
+
+
+def test_slab_async_band(amg, oracle, ctx):
+    """the free race (a host thread and a stream per level group, per-level
+    channels) of ASYNC_MULTADD with composed smoothed transfers at 48^3 on 1-3
+    ranks: every level runs num_cycles corrections and the relative residual
+    lies in the oracle's asynchronous band (or_async_add free runs with one and
+    two threads per level, composed transfers, plus the sync additive cycle)"""
+    n, N = 48, 12
+    gen = amg.Gen(n)
+    f = amg.rhs_rand(0, n ** 3)
+    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=W, num_cycles=N, tol=0.0, smooth_transfer=1)
+    host = host_hier(amg, oracle, gen)
+
+    class Composed:
+        """oracle.Hier with composed transfers for oracle_async_band"""
+
+        def __init__(self, A, P, R, o):
+            self.h = oracle.Hier(A, P, R, o)
+            self.h.set_composed_transfers()
+
+        def __getattr__(self, k):
+            return getattr(self.h, k)
+
+    class OracleShim:
+        def __getattr__(self, k):
+            return Composed if k == "Hier" else getattr(oracle, k)
+
+    lo, hi, orels, _ = oracle_async_band(amg, OracleShim(), host, f, opts)
+    print(f"oracle async band (composed MULTADD, 48^3) [{lo:.4e}, {hi:.4e}] width {hi / lo:.1f}x over {len(orels)}")
+    for nranks in (1, 2, 3):
+        ((rel, cnt, u, _),) = slab_async(amg, gen, opts, f, nranks, rccl1=True)
+        assert list(cnt[:gen.L - 1]) == [N] * (gen.L - 1)
+        print(f"  {nranks} rank(s): device relres {rel:.4e}")
+        assert np.all(np.isfinite(u))
+        assert in_band(rel, lo, hi), (nranks, rel, (lo, hi))
+    gen.free()
+
+
+@pytest.mark.slow
+def test_slab_512_async(amg, ctx):
+    """config 4 at size: ASYNC_MULTADD with the smoothed transfers on the 512^3
+    slab hierarchy, the free race, at 1 rank (RCCL), 2 and 8 ranks (the
+    device-resident per-level channels): every level does N corrections and
+    the relative residual falls below 0.5 (it contracts; the plain-transfer
+    AFACx run of round 3 sat at 1.41)"""
+    n, N = 512, 8
+    gen = amg.Gen(n)
+    f = amg.rhs_rand(0, n ** 3)
+    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=W, num_cycles=N, tol=0.0, smooth_transfer=1)
+    rels = {}
+    for nranks in (1, 2, 8):
+        ((rel, cnt, u, ms),) = slab_async(amg, gen, opts, f, nranks, rep=1 << 18)
+        assert list(cnt[:gen.L - 1]) == [N] * (gen.L - 1)
+        assert np.all(np.isfinite(u))
+        rels[nranks] = rel
+        print(f"512^3 async MULTADD (smoothed transfers) {nranks} rank(s): relres {rel:.4e}, "
+              f"level finish ms (rank 0) {np.round(ms[0][:gen.L - 1], 1).tolist()}")
+        del u
+    assert all(r < 0.5 for r in rels.values()), rels
+    gen.free()
