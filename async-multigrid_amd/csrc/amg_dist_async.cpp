@@ -561,7 +561,7 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    AMG_TRY(setup_async(D));
    AMG_TRY(setup_composed(D));
    AMG_TRY(dist_solve_begin(D, f_local));
-   if (D->links) AMG_TRY(link_reset(D->links));
+   if (D->links) AMG_TRY(link_reset(D->links, sched != AMG_SCHED_FREE));
    const int active = (int)D->al.size();
    const int n0 = D->lv[0].n;
    // a deterministic schedule runs every level on one stream and one host

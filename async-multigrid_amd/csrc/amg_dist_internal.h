@@ -134,7 +134,9 @@ struct AsyncLevel {
 // in level group k, 0 = no channel (the sets are symmetric by construction)
 struct LinkSet;
 int link_create(amg_dist_hier *D, int K, const std::vector<long long> &caps, LinkSet **out);
-int link_reset(LinkSet *L); // collective: sequence numbers back to 0 before a solve
+// collective: sequence numbers back to 0 before a solve; one_thread: every
+// level group driven by the calling thread (a deterministic schedule)
+int link_reset(LinkSet *L, bool one_thread);
 int link_send(LinkSet *L, int k, int peer, const double *src, long long n, hipStream_t s);
 int link_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipStream_t s);
 int link_drain(LinkSet *L, int k); // publish everything level group k has in flight

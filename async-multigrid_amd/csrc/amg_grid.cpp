@@ -263,6 +263,7 @@ struct CommClass {
 struct amg_devhub {
    struct Msg {
       const double *src = nullptr;
+      int src_rank = -1;
       long long n = 0;
       double flag = 0.0;
       hipEvent_t written = nullptr, consumed = nullptr;
@@ -281,6 +282,7 @@ struct amg_devhub {
    };
    int world = 0;
    std::vector<int> rank_grid;
+   std::vector<int> device;   // each rank's device (registered at create)
    std::mutex mu;
    std::condition_variable cv;
    // round-robin schedule (async_schedule = AMG_SCHED_ROUND_ROBIN): the rank
@@ -339,6 +341,7 @@ struct amg_devhub {
    {
       auto m = std::make_shared<Msg>();
       m->src = src;
+      m->src_rank = me;
       m->n = n;
       m->flag = flag;
       AMG_TRY(mark(s, &m->written));
@@ -349,6 +352,7 @@ struct amg_devhub {
          auto r = q.front();
          q.pop_front();
          r->src = m->src;
+         r->src_rank = me;
          r->n = std::min(r->n, n);
          r->flag = flag;
          r->written = m->written;
@@ -393,6 +397,21 @@ struct amg_devhub {
       const auto &m = it->second;
       *done = m->matched;
       if (m->matched) {
+         // the receiver's kernel reads the sender's slot in place: a sender on
+         // another device must be peer-accessible from this one
+         const int sd = m->src_rank >= 0 ? device[m->src_rank] : -1;
+         int cur = -1;
+         AMG_HIP(hipGetDevice(&cur));
+         if (sd >= 0 && sd != cur) {
+            int can = 0;
+            AMG_HIP(hipDeviceCanAccessPeer(&can, cur, sd));
+            AMG_ARG(can, "amg_devhub: device %d cannot read device %d's message slots", cur, sd);
+            const hipError_t e = hipDeviceEnablePeerAccess(sd, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+               return amg_set_error(AMG_ERR_HIP, "amg_devhub: hipDeviceEnablePeerAccess(%d): %s", sd,
+                                    hipGetErrorString(e));
+            (void)hipGetLastError();
+         }
          AMG_HIP(hipStreamWaitEvent(s, m->written, 0));
          *flag = m->flag;
          *src = m->src;
@@ -465,6 +484,7 @@ extern "C" int amg_devhub_create(int world, const int *rank_grid, amg_devhub **o
    h->world = world;
    h->rank_grid.assign(rank_grid, rank_grid + world);
    h->finished.assign(world, 0);
+   h->device.assign(world, -1);
    for (int r = 0; r < world; r++) h->grids[rank_grid[r]].n++;
    *out = h.release();
    return AMG_OK;
@@ -549,6 +569,9 @@ struct IpcLink : MsgLink {
    };
    std::map<int, Peer> peers; // receive peers
    struct SendRec {
+      int peer = 0;
+      hipEvent_t written = nullptr; // the slot's write, on the sender's stream
+      bool ctl_sent = false;        // the control word goes out once `written` has run
       long long ctl_req = 0, ack_req = 0;
       double ctl[2] = {0.0, 0.0}, ack = 0.0;
       bool ctl_done = false, ack_done = false;
@@ -575,11 +598,26 @@ struct IpcLink : MsgLink {
    {
       for (auto &a : acks)
          if (a->ev) hipEventDestroy(a->ev);
+      for (auto &sr : sends)
+         if (sr.second->written) hipEventDestroy(sr.second->written);
       for (void *p : opened) hipIpcCloseMemHandle(p);
    }
-   // acknowledge every read that has run; retire sent acknowledgements
+   // send the control word of every slot whose write has run (in issue order:
+   // the writes are on one stream, so they complete in order); acknowledge
+   // every read that has run; retire sent acknowledgements
    int progress()
    {
+      for (auto &kv : sends) {
+         SendRec &r = *kv.second;
+         if (r.ctl_sent) continue;
+         const hipError_t q = hipEventQuery(r.written);
+         if (q == hipErrorNotReady) break;
+         AMG_HIP(q);
+         AMG_TRY(xp(t.isend(t.user, r.peer, GRIDJ_TO_GRIDK_CORRECT_TAG, r.ctl, 2, &r.ctl_req), "isend"));
+         r.ctl_sent = true;
+         hipEventDestroy(r.written);
+         r.written = nullptr;
+      }
       for (auto it = acks.begin(); it != acks.end();) {
          AckRec &a = **it;
          if (!a.sent) {
@@ -605,12 +643,15 @@ struct IpcLink : MsgLink {
    }
    int isend(int peer, const double *, int slot, long long, double flag, hipStream_t s, long long *req) override
    {
-      AMG_HIP(hipStreamSynchronize(s)); // the slot is written
+      // the control word waits for the slot's write (an event, polled by
+      // progress()) -- the host never blocks on the grid's stream here
       auto r = std::make_unique<SendRec>();
+      r->peer = peer;
       r->ctl[0] = (double)slot;
       r->ctl[1] = flag;
+      AMG_HIP(hipEventCreateWithFlags(&r->written, hipEventDisableTiming));
+      AMG_HIP(hipEventRecord(r->written, s));
       AMG_TRY(xp(t.irecv(t.user, peer, IPC_ACK_TAG, &r->ack, 1, &r->ack_req), "irecv"));
-      AMG_TRY(xp(t.isend(t.user, peer, GRIDJ_TO_GRIDK_CORRECT_TAG, r->ctl, 2, &r->ctl_req), "isend"));
       *req = next++;
       sends[*req] = std::move(r);
       return progress();
@@ -658,6 +699,10 @@ struct IpcLink : MsgLink {
       AMG_ARG(it != sends.end(), "amg_grid_add: unknown send %lld", req);
       SendRec &r = *it->second;
       int d = 0;
+      if (!r.ctl_sent) {
+         *done = 0;
+         return AMG_OK;
+      }
       if (!r.ctl_done) {
          AMG_TRY(xp(t.test(t.user, r.ctl_req, &d), "test"));
          r.ctl_done = d;
@@ -673,9 +718,14 @@ struct IpcLink : MsgLink {
    int grid_sum(double *v, int n) override { return xp(t.grid_allreduce(t.user, v, n), "grid_allreduce"); }
    int flush() override
    {
-      while (!acks.empty()) {
+      auto unsent = [&] {
+         for (auto &kv : sends)
+            if (!kv.second->ctl_sent) return true;
+         return false;
+      };
+      while (!acks.empty() || unsent()) {
          AMG_TRY(progress());
-         if (!acks.empty()) std::this_thread::yield();
+         if (!acks.empty() || unsent()) std::this_thread::yield();
       }
       return AMG_OK;
    }
@@ -1208,6 +1258,10 @@ extern "C" int amg_grid_add_create_devhub(amg_dist_hier *D, int my_grid, int wor
    G->o = D->o;
    G->link = std::make_unique<HubLink>(hub, world_rank);
    G->hub = hub;
+   {
+      std::lock_guard<std::mutex> lk(hub->mu);
+      hub->device[world_rank] = D->ctx->device;
+   }
    G->dev = true;
    auto be = std::make_unique<DistBackend>(D);
    AMG_TRY(be->init(my_grid));

@@ -96,6 +96,11 @@ struct amg_ctx {
    int mz_zc = 16;         // planes per workgroup chunk of the plane-marching kernel
    int mz_edge = 1;        // x-edge pair patterns on the 27-pt march's fast path
    int mz_zc_auto = 1;     // shorten the chunks of small levels to keep >= 2048 workgroups
+   // 27-pt march: chunks sized so the grid is one round of resident
+   // workgroups (mz27_occ > 0: workgroups per CU; 0: mz_chunk's rule) and the
+   // prefetch distance in planes (1 or 2)
+   int mz27_occ = 3;
+   int mz27_pf = 2;
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies
    int bsr3 = 1;           // 3x3 block form of num_functions = 3 operators

@@ -1243,7 +1243,7 @@ struct Val27 {
    double v[27];
 };
 
-template <int NEG, bool NEED_DIAG, class Epi, bool UNI>
+template <int NEG, bool NEED_DIAG, class Epi, bool UNI, int PF = 1>
 __global__ __launch_bounds__(256) void csr_mz27_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, int dom, int xlo, int xhi, Val27 Hv, const double *__restrict__ x,
@@ -1277,15 +1277,25 @@ __global__ __launch_bounds__(256) void csr_mz27_kernel(
          X[m][d] = mz27_line(v, e, lane);
       }
    }
+   // PF = 2: plane k + 2 arrives one iteration early (qv / qe), plane k + 3 is
+   // in flight while plane k is computed
+   v2d qv[3] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+   double qe[3] = {0.0, 0.0, 0.0};
+   if (PF == 2 && k0 + 2 < nz && k0 + 1 < k1) {
+#pragma unroll
+      for (int d = 0; d < 3; d++)
+         mz27_load(x, (long long)(k0 + 2) * P + pos + (d - 1) * S, Nu, lane, qv[d], qe[d]);
+   }
    __syncthreads();
    for (int k = k0; k < k1; k++) {
       const unsigned row = (unsigned)k * P + pos;
-      // prefetch plane k + 2 (the chunk's last iteration needs plane k1)
+      // prefetch plane k + PF + 1 (the chunk's last iteration needs plane k1)
       v2d nv[3] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
       double ne[3] = {0.0, 0.0, 0.0};
-      if (k + 2 < nz && k + 1 < k1) {
+      if (k + PF + 1 < nz && k + PF < k1) {
 #pragma unroll
-         for (int d = 0; d < 3; d++) mz27_load(x, (long long)row + 2LL * P + (d - 1) * S, Nu, lane, nv[d], ne[d]);
+         for (int d = 0; d < 3; d++)
+            mz27_load(x, (long long)row + (PF + 1LL) * P + (d - 1) * S, Nu, lane, nv[d], ne[d]);
       }
       const int pid = ppat[row >> 1];
       const v2d acc0 = epi.init2((int)row);
@@ -1355,7 +1365,13 @@ __global__ __launch_bounds__(256) void csr_mz27_kernel(
       for (int d = 0; d < 3; d++) {
          X[0][d] = X[1][d];
          X[1][d] = X[2][d];
-         X[2][d] = mz27_line(nv[d], ne[d], lane);
+         if (PF == 2) {
+            X[2][d] = mz27_line(qv[d], qe[d], lane);
+            qv[d] = nv[d];
+            qe[d] = ne[d];
+         } else {
+            X[2][d] = mz27_line(nv[d], ne[d], lane);
+         }
       }
    }
    if (partials) {
@@ -1379,21 +1395,34 @@ static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const 
    }
    const int P = A->mz_P, nz = A->nrows / P, nk = ke - kb;
    if (nk <= 0) return;
-   const int zc = mz_chunk(A, nk, P / 512);
-   const int npb = P / 512, nch = (nk + zc - 1) / zc;
+   const int npb = P / 512;
+   int zc = mz_chunk(A, nk, npb);
+   // one round of resident workgroups (mz27_occ per CU, the VGPR-limited
+   // occupancy of this kernel) when the level is large enough to fill it
+   const int slots = A->ctx->mz27_occ * A->ctx->num_cus;
+   if (A->ctx->mz_zc_auto && slots > 0 && (long long)nk * npb >= slots)
+      zc = std::min(AMG_MZ_MAXZC, (int)(((long long)nk * npb + slots - 1) / slots));
+   const int nch = (nk + zc - 1) / zc;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
    Val27 H;
    for (int j = 0; j < 27; j++) H.v[j] = A->mz_hival[j];
    // the x-edge fast path needs the dominant pattern (ctx->mz_edge: on)
    const int xlo = A->ctx->mz_edge ? A->mz_xlo : -1, xhi = A->ctx->mz_edge ? A->mz_xhi : -1;
-   if (A->mp_uni)
-      csr_mz27_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, -1, -1, -1, H, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e,
-         partials, kb, ke);
+   auto go = [&](auto pf) {
+      constexpr int PF = decltype(pf)::value;
+      if (A->mp_uni)
+         csr_mz27_kernel<NEG, NEED_DIAG, Epi, true, PF><<<npb * nch, 256, 0, s>>>(
+            A->ppat, A->mpmask, A->pp_n, mv, S, -1, -1, -1, H, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e,
+            partials, kb, ke);
+      else
+         csr_mz27_kernel<NEG, NEED_DIAG, Epi, false, PF><<<npb * nch, 256, 0, s>>>(
+            A->ppat, A->mpmask, A->pp_n, mv, S, A->mz_dom, A->mz_dom >= 0 ? xlo : -1, A->mz_dom >= 0 ? xhi : -1,
+            H, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
+   };
+   if (A->ctx->mz27_pf == 2)
+      go(std::integral_constant<int, 2>{});
    else
-      csr_mz27_kernel<NEG, NEED_DIAG, Epi, false><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, A->mz_dom, A->mz_dom >= 0 ? xlo : -1, A->mz_dom >= 0 ? xhi : -1, H,
-         x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
+      go(std::integral_constant<int, 1>{});
 }
 
 // ---------------------------------------------------------------------------

@@ -129,6 +129,7 @@ struct amgd::LinkSet {
    bool own_ctrl_malloc = false;
    double *slots = nullptr;        // my receive slot region
    std::vector<double *> ipc_open; // opened peer regions (closed at free)
+   bool one_thread = false;        // every level group on one host thread: progress serves them all
    Chan &c(int k, int p) { return ch[(size_t)k * R + p]; }
    Word *abort_word(int r) { return ctrl[r] + ctrl_words(K, R) - 1; }
 };
@@ -141,8 +142,18 @@ bool aborted(LinkSet *L, int peer)
    return peer >= 0 && L->abort_word(peer)->v.load(std::memory_order_acquire);
 }
 
-// publish this level group's completed sends (arrived) and unpacks (acked)
+// publish this level group's completed sends (arrived) and unpacks (acked);
+// with one host thread for every group, all groups' (a group whose thread has
+// moved on to another level must still publish: its peer may be waiting)
+int progress_one(LinkSet *L, int k);
 int progress(LinkSet *L, int k)
+{
+   if (!L->one_thread) return progress_one(L, k);
+   for (int q = 0; q < L->K; q++) AMG_TRY(progress_one(L, q));
+   return AMG_OK;
+}
+
+int progress_one(LinkSet *L, int k)
 {
    for (int p = 0; p < L->R; p++) {
       Chan &c = L->c(k, p);
@@ -381,9 +392,11 @@ int amgd::link_create(amg_dist_hier *D, int K, const std::vector<long long> &cap
 }
 
 // reset the sequence numbers before a solve (every rank calls it, then a
-// barrier through the transport, so no peer still reads the old words)
-int amgd::link_reset(LinkSet *L)
+// barrier through the transport, so no peer still reads the old words);
+// one_thread: every level group is driven by the calling thread
+int amgd::link_reset(LinkSet *L, bool one_thread)
 {
+   L->one_thread = one_thread;
    for (auto &c : L->ch) {
       c.rseq = c.r_pub = c.sseq = c.s_pub = 0;
    }

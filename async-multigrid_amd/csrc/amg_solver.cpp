@@ -1307,13 +1307,14 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          }
       }
       if (global_res) {
-         // :356-414: u_k = u; the level's slice of r = f - A u_k into the shared
-         // r; then r_k = r (under the update stream for SEMI_ASYNC)
+         // :356-414: u_k = u; the level's slice of r = f - A u_k (SMEM_Residual:
+         // y = A u_k, then r = f - y) into the shared r; then r_k = r (under the
+         // update stream for SEMI_ASYNC)
          amgk::vcopy(s, v0.u, a.u_priv, 0, n0);
-         amgk::spgemv(s, v0.A, a.u_priv, v0.f, amgk::gemv_mode(-1.0, 1.0), a.y, grb, gre, nullptr);
+         amgk::spgemv(s, v0.A, a.u_priv, nullptr, mv, a.y, grb, gre, nullptr);
          if (semi) AMG_TRY(to_update());
          hipStream_t ws = semi ? us : s;
-         amgk::vcopy(ws, a.y, H->r0, grb, gre);
+         amgk::vsub(ws, v0.f, a.y, H->r0, grb, gre);
          amgk::vcopy(ws, H->r0, a.y_fine, 0, n0);
          if (semi) AMG_TRY(from_update());
       }

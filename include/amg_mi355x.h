@@ -711,6 +711,12 @@ int amg_grid_add_solve(amg_grid_add *G, const double *b_local, double *x_local, 
                        long long *messages);
 /* number of outside send / receive peers (the overlapping ranks of other grids) */
 int amg_grid_add_peers(const amg_grid_add *G, int *nsend, int *nrecv);
+/* IPC mode: a rank's slot pools live in its hierarchy D's allocations and are
+ * mapped by its receivers -- every rank must free its grid_add (which closes the
+ * handles it opened) before ANY rank frees its amg_dist_hier (a barrier between
+ * the two, as tests/test_gpu_grid_ipc.py does).  amg_opts.async_schedule =
+ * AMG_SCHED_ROUND_ROBIN (device hub, one rank per grid): the grids take turns at
+ * the oracle's or_dmem_add points -- bit-identical to it. */
 int amg_grid_add_free(amg_grid_add *G);
 
 /* ---- binary triplet matrix files (-problem file) ------------------------------ */

@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--block", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--smoother", default="hybrid")
+    ap.add_argument("--transfers", default="explicit", choices=("explicit", "composed"),
+                    help="smoothed transfers as explicit products (host SpGEMM) or composed on the device "
+                         "(smooth_transfer = 1: R~ r = R (r - w A D^-1 r))")
     a = ap.parse_args()
     amg = load_package()
     from oracle import pyoracle as po
@@ -43,10 +46,14 @@ def main():
     A = [po.Csr(*g.host_csr(amg.AMG_GEN_A, l)) for l in range(L)]
     P = [po.Csr(*g.host_csr(amg.AMG_GEN_P, l)) for l in range(L - 1)]
     Ps, Rs = [], []
-    for l in range(L - 1):
-        p, r = po.smooth_transfer(A[l], P[l], w)
-        Ps.append(p)
-        Rs.append(r)
+    if a.transfers == "composed":
+        Ps = P
+        Rs = [po.Csr(*g.host_csr(amg.AMG_GEN_R, l)) for l in range(L - 1)]
+    else:
+        for l in range(L - 1):
+            p, r = po.smooth_transfer(A[l], P[l], w)
+            Ps.append(p)
+            Rs.append(r)
     print(f"[async] {L}-level smoothed hierarchy built in {time.time() - t0:.1f}s", file=sys.stderr)
     ctx = amg.Context(0, nstreams=16)
     dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v]
@@ -56,11 +63,12 @@ def main():
     fv = ctx.vec(f)
     out = {"config": {"workload": f"{n}^3 7-pt Laplacian, ASYNC_MULTADD {a.smoother} "
                                   f"(blocks of {a.block} rows), FULL_ASYNC, LOCAL residual / convergence, "
-                                  f"{a.cycles} corrections per level, smoothed linear transfers",
+                                  f"{a.cycles} corrections per level, smoothed linear transfers ({a.transfers})",
                       "levels": L, "n": n}}
     for tag, solver in (("async", amg.AMG_ASYNC_MULTADD), ("sync", amg.AMG_MULTADD)):
         opts = amg.default_opts(solver=solver, smoother=sm, smooth_weight=w, num_cycles=a.cycles, tol=0.0,
-                                num_threads=0, jgs_block_rows=a.block)
+                                num_threads=0, jgs_block_rows=a.block,
+                                smooth_transfer=1 if a.transfers == "composed" else 0)
         H = amg.Hier(ctx, dev["A"], dev["P"], dev["R"], opts)
         times, rels = [], []
         for rep in range(a.reps + 1):
