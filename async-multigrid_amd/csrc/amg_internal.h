@@ -104,6 +104,7 @@ struct amg_ctx {
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies
    int bsr3 = 1;           // 3x3 block form of num_functions = 3 operators
+   int fuse_xfer = 1;      // composed smoothed transfers of marched 7-pt levels in one pass each
    int fuse_prolong = 0;   // prolongation fused into the first post sweep (measured slower: off)
    int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)
    int mz_lines = 1;       // 7-pt plane march: lines per lane (1, 2 or 4, AMG_MZ_LINES)
@@ -311,9 +312,10 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
 void geo_restrict(hipStream_t s, const GeoT &g, const double *wdev, const double *r, double *fc, int Kb = 0,
                   int Ke = -1, int fz0 = 0, int cz0 = 0, ZeroGuess zg = ZeroGuess());
 // u += P e for the checked geometric P of GeoT g (bit-identical to the SpGEMV);
-// fine planes [zb, ze), u plane 0 = fine plane fz0, e plane 0 = coarse cz0
+// fine planes [zb, ze), u plane 0 = fine plane fz0, e plane 0 = coarse cz0;
+// assign: u = P e (the SpMV, alpha 1 beta 0)
 void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u, int zb = 0,
-                 int ze = -1, int fz0 = 0, int cz0 = 0);
+                 int ze = -1, int fz0 = 0, int cz0 = 0, int assign = 0);
 // DMEM_AddSmooth scale vectors: s = a_ii / w (1 where a_ii = 0) or the L1 row
 // norm l1 (l1 != nullptr), ns = -s (DMEM_Setup.cpp:423-482)
 void dmem_scale(hipStream_t s, const double *diag, const double *l1, double omega, double *sc, double *nsc, int n);
@@ -323,6 +325,15 @@ void delay(hipStream_t s, double usec, int wall_khz);
 // P the checked geometric transfer of marched 7-pt level A (uc never stored)
 void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const double *u, const double *ec,
                       const GeoT &g, const double *wdev, const double *l1, double omega, double *uout);
+// composed smoothed transfers of a marched 7-pt level with geometric R / P in
+// one pass each (bit-identical to xfer_div + SpMV + xfer_sub + R, and to
+// P + SpMV + xfer_corr): rc = R (r + (-w) A (r ./ a)) (uniform operators only);
+// ef = P ec + (-w) (A P ec) ./ a, then mode 0: out = ef; 1: atomic_correct(out =
+// u, ef, u_priv); 2: out = u + ef
+void mz_xfer_restrict(hipStream_t s, const amg_mat *A, const double *r, const GeoT &g, const double *wdev,
+                      double omega, double *rc);
+void mz_xfer_prolong(hipStream_t s, const amg_mat *A, const double *ec, const GeoT &g, const double *wdev,
+                     double omega, int mode, double *out, double *u_priv);
 // transpose-product with the expansion-buffer order of T static chunks
 void matvec_t_chunked(hipStream_t s, const amg_mat *AT, const double *x, double *y, int n_src,
                       int T);

@@ -1537,12 +1537,17 @@ __device__ __forceinline__ void zg_apply(const ZeroGuess &zg, long long i, doubl
    }
 }
 
-template <bool UNI, int LC, int OCC = 1, bool RING = false>
+// XF: the composed smoothed restriction instead of the residual (UNI operators,
+// xfer_restrict of the solver): x is the fine residual r, the operands are
+// t = r ./ a (a = the uniform diagonal, divided once per loaded element), the
+// fine value is z = r + (-w) (A t) (xfer_div, SpMV, xfer_sub: same operations,
+// same order) and f_c = R z; f is not read
+template <bool UNI, int LC, int OCC = 1, bool RING = false, bool XF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void mz_res_restrict_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, Val7 Sv7, const double *__restrict__ x, const double *__restrict__ f,
    const double *__restrict__ wg, int nx, int ny, int nz, int zcc, int nlb, int xcd, int ntf,
-   double *__restrict__ fc, int Kb, int Ke, int fz0, int cz0, int nzm, ZeroGuess zg)
+   double *__restrict__ fc, int Kb, int Ke, int fz0, int cz0, int nzm, ZeroGuess zg, double mw = 0.0)
 {
    // coarse planes [Kb, Ke) of the nx * ny * nz box; x / f (and the pattern
    // bytes) hold nzm planes from fine plane fz0, fc's plane 0 is coarse plane
@@ -1577,7 +1582,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
    const bool d2x = 2 * cx + 2 < nx;     // dx = 2 inside
    const int pos0 = y0 * S + 2 * cx;      // line 0 offset in the plane
    const unsigned Nu = (unsigned)N;
+   const double d0 = Sv.val[0];
+   auto sc = [&](v2d v) { return XF ? v2d{v.x / d0, v.y / d0} : v; };
    v2d xm[NL], xc[NL], xq[NL];
+   v2d xcr[XF ? NL : 1], xqr[XF ? NL : 1]; // XF: the unscaled r of planes k, k + 1
 #pragma unroll
    for (int i = 0; i < NL; i++) {
       const unsigned p = (unsigned)pos0 + (unsigned)i * S;
@@ -1585,6 +1593,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       xm[i] = (ok && kf0 > 0) ? ld2u(x, p + (unsigned)(kf0 - 1 - fz0) * P) : v2d{0.0, 0.0};
       xc[i] = ok ? ld2u(x, p + (unsigned)(kf0 - fz0) * P) : v2d{0.0, 0.0};
       xq[i] = (ok && kf0 + 1 < nz) ? ld2u(x, p + (unsigned)(kf0 + 1 - fz0) * P) : v2d{0.0, 0.0};
+      if (XF) {
+         xcr[i] = xc[i];
+         xqr[i] = xq[i];
+         xm[i] = sc(xm[i]);
+         xc[i] = sc(xc[i]);
+         xq[i] = sc(xq[i]);
+      }
    }
    double acc[LC];
 #pragma unroll
@@ -1615,7 +1630,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
          in.e[i] = 0.0;
          if (i == NL - 1 && lastl) continue;
          in.pid[i] = ppat[row >> 1];
-         in.a2[i] = ld2nt(f + row, ntf);
+         if (!XF) in.a2[i] = ld2nt(f + row, ntf);
          if (lane == 0 && row > 0) in.e[i] = ld1u(x, row - 1);
          if (lane == 63 && row + 2 < Nu) in.e[i] = ld1u(x, row + 2);
       }
@@ -1626,14 +1641,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       v2d r[NL];
       PlaneIn cur;
       fetch(k, cur);
-      const v2d hm = cur.hm, hp = cur.hp;
+      const v2d hm = sc(cur.hm), hp = sc(cur.hp);
 #pragma unroll
       for (int i = 0; i < NL; i++) {
          r[i] = v2d{0.0, 0.0};
          if (i == NL - 1 && lastl) continue;
          const int pid = cur.pid[i];
          v2d a2 = cur.a2[i];
-         const double e = cur.e[i];
+         const double e = XF ? cur.e[i] / d0 : cur.e[i];
          double lft = __shfl_up(xc[i].y, 1, 64);
          double rgt = __shfl_down(xc[i].x, 1, 64);
          if (lane == 0) lft = e;
@@ -1647,16 +1662,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
          xv[4] = v2d{xc[i].y, rgt};
          xv[5] = i == NL - 1 ? hp : xc[i == NL - 1 ? NL - 1 : i + 1];
          xv[6] = xq[i];
-         r[i] = mz_acc7<1, UNI>(a2, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
+         if (XF) {
+            const v2d y = mz_acc7<0, UNI>(v2d{0.0, 0.0}, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
+            r[i] = v2d{xcr[i].x + mw * y.x, xcr[i].y + mw * y.y};
+         } else {
+            r[i] = mz_acc7<1, UNI>(a2, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
+         }
       }
       // next plane's operands: load plane k + 2 while the restriction runs
 #pragma unroll
       for (int i = 0; i < NL; i++) {
          xm[i] = xc[i];
          xc[i] = xq[i];
-         xq[i] = v2d{0.0, 0.0};
+         v2d raw{0.0, 0.0};
          if ((i < NL - 1 || !lastl) && k + 2 < nz && k + 1 <= kf1)
-            xq[i] = ld2u(x, base + (unsigned)i * S + 2u * P);
+            raw = ld2u(x, base + (unsigned)i * S + 2u * P);
+         if (XF) {
+            xcr[i] = xqr[i];
+            xqr[i] = raw;
+         }
+         xq[i] = sc(raw);
       }
       // r at fine column 2cx + 2: lane t + 1 (LDS across waves for line groups
       // of more than 64 lanes)
@@ -1758,6 +1783,32 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
 #undef AMG_RR
 }
 
+// rc = R (r + (-w) A (r ./ a)) for a marched uniform 7-pt level with geometric
+// R (the composed smoothed restriction of xfer_restrict in one pass)
+void mz_xfer_restrict(hipStream_t s, const amg_mat *A, const double *r, const GeoT &g, const double *wdev,
+                      double omega, double *rc)
+{
+   const int Ke = g.nz / 2;
+   if (Ke <= 0) return;
+   const int nzm = A->nrows / (g.nx * g.ny);
+   Val7 S;
+   for (int j = 0; j < 7; j++) S.v[j] = A->mp_val[j];
+   const int lpl = g.nx / 2, groups = 256 / lpl;
+   const int LC = ((g.ny / 2) % (2 * groups) == 0 && A->ctx->rr_lines == 2) ? 2 : 1;
+   const int nlb = (g.ny / 2) / (groups * LC);
+   const int zcc = std::max(1, std::min(A->ctx->mz_zc / 2, 32));
+   const int nb = nlb * ((Ke + zcc - 1) / zcc);
+   const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+   if (LC == 2)
+      mz_res_restrict_kernel<true, 2, 1, false, true><<<nb, 256, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, mv, S, r, nullptr, wdev, g.nx, g.ny, g.nz, zcc, nlb, A->ctx->mz_xcd, 0, rc, 0,
+         Ke, 0, 0, nzm, ZeroGuess(), -omega);
+   else
+      mz_res_restrict_kernel<true, 1, 1, false, true><<<nb, 256, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, mv, S, r, nullptr, wdev, g.nx, g.ny, g.nz, zcc, nlb, A->ctx->mz_xcd, 0, rc, 0,
+         Ke, 0, 0, nzm, ZeroGuess(), -omega);
+}
+
 // Geometric prolongation + correction u += P e (SMEM_Sync_SpGEMV(P, e, u, 1, 1,
 // u), SMEM_Sync_AMG.cpp:118-123) for the checked geometric P_0 of a marched
 // level: lane t owns fine rows (2t, 2t + 1) of a line; per coarse (plane, line)
@@ -1844,7 +1895,7 @@ __device__ __forceinline__ double geo_prolong_point(double acc, const double *__
 // plane 0 is fine plane fz0, e's plane 0 coarse plane cz0 (z-slab vectors)
 __global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ e, double *__restrict__ u,
                                                      const double *__restrict__ wg, int nx, int ny, int nz,
-                                                     long long npairs, int zb, int fz0, int cz0)
+                                                     long long npairs, int zb, int fz0, int cz0, int asg)
 {
    __shared__ double wl[27];
    const int tid = (int)threadIdx.x;
@@ -1867,7 +1918,8 @@ __global__ __launch_bounds__(256) void geo_prolong_k(const double *__restrict__ 
    }
    z += zb;
    double *ui = u + (long long)(z - fz0) * nx * ny + (i - (long long)(z - zb) * nx * ny);
-   const v2d acc = *reinterpret_cast<const v2du *>(ui);
+   // asg: u = P e (from 0.0, the SpMV's start) instead of u += P e
+   const v2d acc = asg ? v2d{0.0, 0.0} : *reinterpret_cast<const v2du *>(ui);
    *reinterpret_cast<v2du *>(ui) = geo_prolong_pair(acc, e, wl, x, y, z, nx >> 1, ny >> 1, nz >> 1, cz0);
 }
 
@@ -1901,7 +1953,7 @@ template <int PF>
 __global__ __launch_bounds__(256) void geo_prolong_march_k(const double *__restrict__ e, double *__restrict__ u,
                                                            const double *__restrict__ wg, int nx, int ny, int nz,
                                                            int zb, int ze, int fz0, int cz0, int zc, int nseg,
-                                                           int xcd)
+                                                           int xcd, int asg)
 {
    __shared__ double wl[27];
    const int tid = (int)threadIdx.x;
@@ -1953,10 +2005,11 @@ __global__ __launch_bounds__(256) void geo_prolong_march_k(const double *__restr
    // PF u pairs in flight ahead of the plane being stored
    v2d uq[PF];
 #pragma unroll
-   for (int i = 0; i < PF; i++) uq[i] = z0 + i < z1 ? *reinterpret_cast<const v2du *>(up + i * fpl) : v2d{0.0, 0.0};
+   for (int i = 0; i < PF; i++)
+      uq[i] = (!asg && z0 + i < z1) ? *reinterpret_cast<const v2du *>(up + i * fpl) : v2d{0.0, 0.0};
    for (int z = z0; z < z1; z++, up += fpl) {
       v2d un{0.0, 0.0};
-      if (z + PF < z1) un = *reinterpret_cast<const v2du *>(up + PF * fpl);
+      if (!asg && z + PF < z1) un = *reinterpret_cast<const v2du *>(up + PF * fpl);
       v2d acc = uq[0];
       if (z & 1) {
          acc = add_plane(acc, ecur, 1);
@@ -1975,7 +2028,7 @@ __global__ __launch_bounds__(256) void geo_prolong_march_k(const double *__restr
 }
 
 void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double *e, double *u, int zb, int ze,
-                 int fz0, int cz0)
+                 int fz0, int cz0, int assign)
 {
    if (ze < 0) ze = g.nz;
    const long long np = (long long)g.nx * g.ny * (ze - zb) / 2;
@@ -2003,13 +2056,13 @@ void geo_prolong(hipStream_t s, const GeoT &g, const double *wdev, const double 
       const long long G = (long long)nseg * ((nzl + zc - 1) / zc);
       if (pf == 2)
          geo_prolong_march_k<2><<<(unsigned)G, 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, zb, ze, fz0, cz0, zc, nseg,
-                                                            1);
+                                                            1, assign);
       else
          geo_prolong_march_k<1><<<(unsigned)G, 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, zb, ze, fz0, cz0, zc, nseg,
-                                                            1);
+                                                            1, assign);
       return;
    }
-   geo_prolong_k<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, np, zb, fz0, cz0);
+   geo_prolong_k<<<(unsigned)((np + 255) / 256), 256, 0, s>>>(e, u, wdev, g.nx, g.ny, g.nz, np, zb, fz0, cz0, assign);
 }
 
 // Prolongation + correction fused with the first post-smoothing sweep of a
@@ -2122,6 +2175,138 @@ __global__ __launch_bounds__(256) void mz_prolong_sweep_kernel(
       xq = xn;
       eq = en;
    }
+}
+
+// The composed smoothed prolongation of a marched 7-pt level with geometric P
+// (xfer_prolong of the solver: ef = P ec; y = A ef; ef = ef + (-w) (y ./ a))
+// in one pass, mz_prolong_sweep_kernel's march over ef = P ec formed in
+// registers (from 0.0, the SpMV's start; same terms, same order), then
+//   OUT 0: ef stored;
+//   OUT 1: atomic_correct: u += ef by device-scope fp64 atomics, u_priv = the
+//          value after this level's update (old + ef);
+//   OUT 2: u = u + ef (the synchronous cycle's vaxpy with a = 1).
+// a_ii := master entry 0 (the diagonal-first rows' first value, = diag).
+template <bool UNI, int OUT>
+__global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
+   const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ e, const double *__restrict__ wg,
+   double mw, int nx, int ny, int nz, int zc, int npb, int xcd, double *__restrict__ out, double *__restrict__ u_priv)
+{
+   __shared__ unsigned long long mtab[256];
+   __shared__ v2d mval[UNI ? 1 : 256 * 7];
+   __shared__ double wl[27];
+   const int tid = (int)threadIdx.x, lane = tid & 63;
+   if (tid < np) mtab[tid] = mmask_g[tid];
+   if (tid < 27) wl[tid] = wg[tid];
+   if (!UNI)
+      for (int w = tid; w < np * 7; w += 256) mval[w] = mval_g[w];
+   const int P = nx * ny;
+   const int ncx = nx >> 1, ncy = ny >> 1, ncz = nz >> 1;
+   const int G = (int)gridDim.x;
+   int lg = (int)blockIdx.x;
+   if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
+   const int pblk = lg % npb, chunk = lg / npb;
+   const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
+   const int pos = pblk * 512 + 2 * tid;
+   const int fx = pos % nx, fy = pos / nx;
+   __syncthreads();
+   auto norm3 = [&](int &x, int &y, int &z) {
+      if (x < 0) x += nx, y--;
+      if (x >= nx) x -= nx, y++;
+      if (y < 0) y += ny, z--;
+      if (y >= ny) y -= ny, z++;
+   };
+   auto ef2 = [&](int p, int dy) -> v2d {
+      int x = fx, y = fy + dy, z = p;
+      norm3(x, y, z);
+      if (z < 0 || z >= nz) return v2d{0.0, 0.0};
+      return geo_prolong_pair(v2d{0.0, 0.0}, e, wl, x, y, z, ncx, ncy, ncz);
+   };
+   auto edge = [&](int p) -> double {
+      if (lane != 0 && lane != 63) return 0.0;
+      int x = lane == 0 ? fx - 1 : fx + 2, y = fy, z = p;
+      norm3(x, y, z);
+      if (z < 0 || z >= nz) return 0.0;
+      return geo_prolong_point(0.0, e, wl, x, y, z, ncx, ncy, ncz);
+   };
+   v2d xm = ef2(k0 - 1, 0);
+   v2d xc = ef2(k0, 0);
+   double ec = edge(k0);
+   v2d xq = ef2(k0 + 1, 0);
+   double eq = edge(k0 + 1);
+   for (int k = k0; k < k1; k++) {
+      const unsigned row = (unsigned)k * P + pos;
+      v2d xn{0.0, 0.0};
+      double en = 0.0;
+      if (k + 2 < nz && k + 1 < k1) {
+         xn = ef2(k + 2, 0);
+         en = edge(k + 2);
+      }
+      const int pid = ppat[row >> 1];
+      v2d uo{0.0, 0.0};
+      if (OUT == 2) uo = ld2u(out, row);
+      const v2d ym = ef2(k, -1);
+      const v2d yp = ef2(k, 1);
+      double lft = __shfl_up(xc.y, 1, 64);
+      double rgt = __shfl_down(xc.x, 1, 64);
+      if (lane == 0) lft = ec;
+      if (lane == 63) rgt = ec;
+      const unsigned long long mk = mtab[pid];
+      v2d xv[7];
+      xv[0] = xc;
+      xv[1] = xm;
+      xv[2] = ym;
+      xv[3] = v2d{lft, xc.x};
+      xv[4] = v2d{xc.y, rgt};
+      xv[5] = yp;
+      xv[6] = xq;
+      const v2d y = mz_acc7<0, UNI>(v2d{0.0, 0.0}, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
+      const v2d a = UNI ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 7];
+      const double t0 = y.x / a.x, t1 = y.y / a.y;
+      const v2d o{xc.x + mw * t0, xc.y + mw * t1};
+      if (OUT == 0) {
+         *reinterpret_cast<v2du *>(out + row) = o;
+      } else if (OUT == 1) {
+         const double q0 = atomicAdd(out + row, o.x);
+         const double q1 = atomicAdd(out + row + 1, o.y);
+         *reinterpret_cast<v2du *>(u_priv + row) = v2d{q0 + o.x, q1 + o.y};
+      } else {
+         *reinterpret_cast<v2du *>(out + row) = v2d{uo.x + 1.0 * o.x, uo.y + 1.0 * o.y};
+      }
+      xm = xc;
+      xc = xq;
+      ec = eq;
+      xq = xn;
+      eq = en;
+   }
+}
+
+void mz_xfer_prolong(hipStream_t s, const amg_mat *A, const double *ec, const GeoT &g, const double *wdev,
+                     double omega, int mode, double *out, double *u_priv)
+{
+   MpSten S;
+   for (int j = 0; j < AMG_MP_MAXJ; j++) {
+      S.off[j] = A->mp_off[j];
+      S.val[j] = A->mp_val[j];
+   }
+   const int P = A->mz_P, nz = A->nrows / P;
+   const int zc = mz_chunk(A, nz, P / 512);
+   const int npb = P / 512, nch = (nz + zc - 1) / zc;
+   const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
+#define AMG_XP(U, O)                                                                                           \
+   mz_xfer_prolong_kernel<U, O><<<npb * nch, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, ec, wdev, -omega, \
+                                                          g.nx, g.ny, g.nz, zc, npb, A->ctx->mz_xcd, out, u_priv)
+#define AMG_XP2(U)                 \
+   if (mode == 1) AMG_XP(U, 1);    \
+   else if (mode == 2) AMG_XP(U, 2); \
+   else AMG_XP(U, 0);
+   if (A->mp_uni) {
+      AMG_XP2(true)
+   } else {
+      AMG_XP2(false)
+   }
+#undef AMG_XP2
+#undef AMG_XP
 }
 
 // The same fused sweep with NL lines per workgroup (lines of nx % 512 == 0

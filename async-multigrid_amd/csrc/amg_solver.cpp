@@ -82,6 +82,10 @@ struct amg_hier {
    // psw[l]: level l's prolongation + correction runs fused into its first
    // post-smoothing sweep (geometric P_l, 7-pt marched A_l of the same box)
    std::vector<char> psw;
+   // xfr[l] / xfp[l]: level l's composed smoothed restriction / prolongation
+   // runs as one fused pass (mz_xfer_restrict / mz_xfer_prolong: geometric
+   // R_l / P_l, marched 7-pt A_l; the restriction needs uniform values)
+   std::vector<char> xfr, xfp;
    // delay / fault injection: one generator per reference thread (srand(tid),
    // SMEM_Solve.cpp:113), reset by every solve
    std::vector<unsigned long long> delay_rng;
@@ -286,6 +290,8 @@ static int detect_geo(amg_hier *H)
    H->d_geo_w.assign(H->L, nullptr);
    H->geo0 = false;
    H->psw.assign(H->L, 0);
+   H->xfr.assign(H->L, 0);
+   H->xfp.assign(H->L, 0);
    if (H->L < 2 || !H->ctx->fuse_transfer) return AMG_OK;
    const amg_mat *A = H->lv[0].A;
    if (!A->mz_P || A->mz_P % A->mz_S) return AMG_OK;
@@ -303,8 +309,12 @@ static int detect_geo(amg_hier *H)
    for (int l = 0; l < H->L - 1; l++) {
       const amg_mat *Al = H->lv[l].A;
       const amgk::GeoT &gg = H->gl[l];
-      H->psw[l] = H->geo[l] && H->ctx->fuse_prolong && Al->mz_P && !Al->mz27 && Al->mz_S == gg.nx &&
-                  (long long)Al->mz_P == (long long)gg.nx * gg.ny && Al->nrows / Al->mz_P == gg.nz;
+      const bool box7 = H->geo[l] && Al->mz_P && !Al->mz27 && Al->mz_S == gg.nx &&
+                        (long long)Al->mz_P == (long long)gg.nx * gg.ny && Al->nrows / Al->mz_P == gg.nz;
+      H->psw[l] = box7 && H->ctx->fuse_prolong;
+      H->xfp[l] = box7 && H->ctx->fuse_xfer;
+      H->xfr[l] = box7 && H->ctx->fuse_xfer && Al->mp_uni && gg.nx >= 64 && gg.nx <= 512 && 512 % gg.nx == 0 &&
+                  (gg.ny / 2) % (512 / gg.nx) == 0;
    }
    H->geo0 = H->geo[0] && !A->mz27 && g.nx >= 64 && g.nx <= 512 && 512 % g.nx == 0 && (g.ny / 2) % (512 / g.nx) == 0;
    return AMG_OK;
@@ -696,6 +706,10 @@ static void xfer_restrict(amg_hier *H, hipStream_t s, int l, const double *r, do
 {
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    const Level &v = H->lv[l];
+   if (composed_transfers(H) && H->xfr[l]) {
+      amgk::mz_xfer_restrict(s, v.A, r, H->gl[l], H->d_geo_w[l], H->o.smooth_weight, rc);
+      return;
+   }
    if (composed_transfers(H)) {
       // t = r ./ a;  y = A t;  t = r + (-w) y;  rc = R t
       amgk::xfer_div(s, v.A->diag, r, t, 0, v.n);
@@ -703,20 +717,38 @@ static void xfer_restrict(amg_hier *H, hipStream_t s, int l, const double *r, do
       amgk::xfer_sub(s, H->o.smooth_weight, r, y, t, 0, v.n);
       r = t;
    }
-   amgk::spgemv(s, v.R, r, nullptr, mv, rc, 0, H->lv[l + 1].n, nullptr);
+   if (H->geo[l]) // the checked geometric R (bit-identical to its SpMV)
+      amgk::geo_restrict(s, H->gl[l], H->d_geo_w[l], r, rc);
+   else
+      amgk::spgemv(s, v.R, r, nullptr, mv, rc, 0, H->lv[l + 1].n, nullptr);
 }
 
-// ef = P~_l ec (composed) or P_l ec; y: scratch of level l's size
-static void xfer_prolong(amg_hier *H, hipStream_t s, int l, const double *ec, double *ef, double *y)
+// ef = P~_l ec (composed) or P_l ec; y: scratch of level l's size.  apply
+// (level 0, composed, fused form only): 1 = the FULL_ASYNC atomic correction
+// u += ef, u_priv = u after it; 2 = u += ef -- ef itself is then not stored;
+// returns whether the correction was applied
+static bool xfer_prolong(amg_hier *H, hipStream_t s, int l, const double *ec, double *ef, double *y, int apply = 0,
+                         double *u = nullptr, double *u_priv = nullptr)
 {
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    const Level &v = H->lv[l];
-   amgk::spgemv(s, v.P, ec, nullptr, mv, ef, 0, v.n, nullptr);
+   if (composed_transfers(H) && H->xfp[l]) {
+      if (apply)
+         amgk::mz_xfer_prolong(s, v.A, ec, H->gl[l], H->d_geo_w[l], H->o.smooth_weight, apply, u, u_priv);
+      else
+         amgk::mz_xfer_prolong(s, v.A, ec, H->gl[l], H->d_geo_w[l], H->o.smooth_weight, 0, ef, nullptr);
+      return apply != 0;
+   }
+   if (H->geo[l]) // u = P e from 0.0 (the SpMV's alpha 1, beta 0 start)
+      amgk::geo_prolong(s, H->gl[l], H->d_geo_w[l], ec, ef, 0, -1, 0, 0, 1);
+   else
+      amgk::spgemv(s, v.P, ec, nullptr, mv, ef, 0, v.n, nullptr);
    if (composed_transfers(H)) {
       // y = A ef;  ef = ef + (-w) (y ./ a)
       amgk::spgemv(s, v.A, ef, nullptr, mv, y, 0, v.n, nullptr);
       amgk::xfer_corr(s, H->o.smooth_weight, y, v.A->diag, ef, 0, v.n);
    }
+   return false;
 }
 
 static int ensure_xfer_scratch(amg_hier *H, AddLevel &a)
@@ -727,7 +759,10 @@ static int ensure_xfer_scratch(amg_hier *H, AddLevel &a)
    return AMG_OK;
 }
 
-static void add_level_correction(amg_hier *H, hipStream_t s, int k, const double *r_fine0)
+// apply / u / u_priv: the level-0 correction fused into the last prolongation
+// where it can be (xfer_prolong); returns whether it was (e[0] not written)
+static bool add_level_correction(amg_hier *H, hipStream_t s, int k, const double *r_fine0, int apply = 0,
+                                 double *u = nullptr, double *u_priv = nullptr)
 {
    const int L = H->L;
    const amg_opts &o = H->o;
@@ -761,15 +796,18 @@ static void add_level_correction(amg_hier *H, hipStream_t s, int k, const double
                         o.num_fine_smooth_sweeps, k);
       amgk::vcopy(s, a.u_fine, a.e[k], 0, H->lv[k].n);
    }
-   for (int l = k - 1; l >= 0; l--) xfer_prolong(H, s, l, a.e[l + 1], a.e[l], a.xy);
+   bool applied = false;
+   for (int l = k - 1; l >= 0; l--)
+      applied = xfer_prolong(H, s, l, a.e[l + 1], a.e[l], a.xy, l == 0 ? apply : 0, u, u_priv);
+   return applied;
 }
 
 static void sync_add_vcycle(amg_hier *H)
 {
    hipStream_t s = H->ctx->stream;
    for (int k = 0; k < H->L; k++) {
-      add_level_correction(H, s, k, H->r0);
-      if (k < H->L - 1) amgk::vaxpy(s, 1.0, H->al[k].e[0], H->lv[0].u, 0, H->lv[0].n);
+      const bool done = add_level_correction(H, s, k, H->r0, k < H->L - 1 ? 2 : 0, H->lv[0].u);
+      if (k < H->L - 1 && !done) amgk::vaxpy(s, 1.0, H->al[k].e[0], H->lv[0].u, 0, H->lv[0].n);
    }
 }
 
@@ -1280,7 +1318,9 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          smooth_fine_slice(H, s, k, a.y_fine, gb[k], gb[k + 1], grb, gre);
          if (!semi) amgk::atomic_add(s, v0.u, a.g_u, grb, gre);
       }
-      add_level_correction(H, s, k, a.y_fine);
+      // FULL_ASYNC / READ_SOL: the atomic correction fused into the level-0
+      // prolongation where the transfers allow it
+      const bool fused = add_level_correction(H, s, k, a.y_fine, (!read_res && !semi) ? 1 : 0, v0.u, a.u_priv);
       if (read_res) {
          amgk::spgemv(s, v0.A, a.e[0], nullptr, mv, a.y, 0, n0, nullptr);
          if (semi) {
@@ -1298,7 +1338,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
             if (global_res) amgk::semi_correct(us, v0.u, a.g_u, nullptr, n0); // :258-265 (g_u is 0 off the slice)
             amgk::semi_correct(us, v0.u, a.e[0], a.u_priv, n0);
             AMG_TRY(from_update());
-         } else {
+         } else if (!fused) {
             amgk::atomic_correct(s, v0.u, a.e[0], a.u_priv, n0);
          }
          if (!global_res) {

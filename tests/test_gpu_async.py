@@ -266,3 +266,49 @@ def test_composed_transfers_sync_bitwise(amg, oracle, ctx, setup):
     assert np.array_equal(u.view(np.uint64), uo.view(np.uint64))
     np.testing.assert_allclose(hist, ho, rtol=1e-12, atol=0)
     assert hist[-1] / hist[0] < 0.05
+
+
+@pytest.mark.parametrize("mode", ["sync", "async-jacobi-s3", "async-hybrid-s1"])
+def test_composed_transfers_geometric_bitwise(amg, oracle, ctx, mode):
+    """composed smoothed transfers on a plane-marched 64^3 hierarchy whose plain
+    P / R are the checked geometric transfers (amg_hier_fused bit l + 1): the
+    transfers run as the geometric restriction / prolongation kernels (and the
+    fused level-0 forms), and the iterate is bit-identical to the oracle's
+    composed restatement -- synchronous MULTADD after every cycle, the
+    asynchronous cycle under a deterministic schedule"""
+    n = 64
+    _, L, host = hierarchy(amg, oracle, n, amg.AMG_INTERP_LINEAR)
+    f = amg.rhs_rand(0, n ** 3)
+    hybrid = "hybrid" in mode
+    sm = amg.AMG_HYBRID_JGS if hybrid else amg.AMG_JACOBI
+    sched = int(mode[-1]) if mode != "sync" else 0
+    opts = amg.default_opts(solver=amg.AMG_MULTADD if mode == "sync" else amg.AMG_ASYNC_MULTADD, smoother=sm,
+                            smooth_weight=W, num_cycles=8, tol=0.0, num_threads=0, jgs_block_rows=64,
+                            async_schedule=sched, smooth_transfer=1)
+    H, _ = gpu_hier(amg, ctx, host, opts)
+    assert H.fused & 2, "level 0's transfers not detected as geometric"
+    if mode == "sync":
+        u, hist, k = H.solve(f)
+    else:
+        u, rel, cnt = H.async_solve(f)
+    H.free()
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    OH.set_composed_transfers()
+    if hybrid:
+        for lev, blk in blocks64(host).items():
+            OH.set_blocks(lev, blk)
+    if mode == "sync":
+        uo, ho, _ = OH.solve(f)
+        assert k == 8
+        np.testing.assert_allclose(hist, ho, rtol=1e-12, atol=0)
+    else:
+        oracle.lib().or_set_async_schedule(sched)
+        try:
+            uo, relo, cnto = OH.async_add(f, [1] * L)
+        finally:
+            oracle.lib().or_set_async_schedule(0)
+        assert list(cnt[:L - 1]) == list(cnto[:L - 1])
+        assert abs(rel - relo) <= 1e-12 * relo
+    nd = int(np.count_nonzero(u.view(np.uint64) != uo.view(np.uint64)))
+    print(f"composed geometric {mode}: differing entries {nd}")
+    assert nd == 0
