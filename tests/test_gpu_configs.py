@@ -8,9 +8,10 @@
   (master-pattern CSR for the square operators) and once with every compressed form
   off (plain CSR through the general tile kernel).
 * config 3 -- 256^3 SMEM_Async_AMG ASYNC_MULTADD with hybrid Jacobi-Gauss-Seidel:
-  nondeterministic like the reference (SMEM_Async_AMG.cpp:7-437), so the final
-  relative residual after N corrections per level must sit inside a band around
-  the oracle's synchronous additive cycle (SMEM_Sync_AMG.cpp:408-621) on the same
+  nondeterministic like the reference (SMEM_Async_AMG.cpp:7-437).  Under the
+  round-robin schedule the iterate is bit-identical to the oracle's
+  or_async_add; the free race's final relative residual must sit inside the
+  band of 20 committed oracle runs (tests/golden/config3_band.json) on the same
   hierarchy, smoother and block partition.  The reference applies Chebyshev only on
   its synchronous path (SMEM_Solve.cpp:169-188), so the async
   solve runs without it; the Chebyshev-accelerated sync solve is checked bitwise at
@@ -115,8 +116,7 @@ def test_config3_256cube_cheby_sync(amg, oracle, ctx):
     run_sync(amg, oracle, ctx, 256, 8, "default", cheby_flag=1, cheby_mu=mu, cheby_delta=delta)
 
 
-def test_config3_256cube_async_multadd_hybrid_jgs(amg, oracle, ctx):
-    n, w, N, B = 256, 0.8, 8, 64
+def config3_setup(amg, oracle, n=256, w=0.8, B=64):
     g = amg.Gen(n, interp=amg.AMG_INTERP_LINEAR)
     host = host_levels(amg, oracle, g)
     L = g.L
@@ -131,14 +131,26 @@ def test_config3_256cube_async_multadd_hybrid_jgs(amg, oracle, ctx):
     blocks = {lev: np.unique(np.minimum(np.arange(0, host["A"][lev].nrows + B, B),
                                         host["A"][lev].nrows)).astype(np.int32)
               for lev in range(L)}
-    sync_opts = amg.default_opts(solver=amg.AMG_MULTADD, smoother=amg.AMG_HYBRID_JGS,
-                                 smooth_weight=w, num_cycles=N, tol=0.0, num_threads=0,
-                                 jgs_block_rows=B)
-    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, sync_opts))
-    for lev, blk in blocks.items():
-        OH.set_blocks(lev, blk)
-    _, h_c, _ = OH.solve(f)
-    sync_rel = h_c[-1] / h_c[0]
+    return g, L, host, f, blocks
+
+
+def test_config3_256cube_async_multadd_hybrid_jgs(amg, oracle, ctx):
+    """config 3's race against a committed oracle band: tests/golden/config3_band.json
+    holds 10 or_async_add runs with one thread per level and 10 with two (the
+    reference's SMEM_Async_Add_AMG restated on OpenMP thread groups, generated by
+    tools/gen_config3_band.py on this container's 8 cores).  The device's median
+    run must lie in [0.5 min, 2 max] of those 20 oracle runs and no run beyond
+    4 max (round 3 saw one run at 2.3x the others when a level stream queued
+    behind the shared hardware queues); no band member comes from the device."""
+    import json
+    import os
+    n, w, N, B = 256, 0.8, 8, 64
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "config3_band.json")))
+    assert (fx["n"], fx["num_cycles"], fx["jgs_block_rows"]) == (n, N, B)
+    orels = [x for v in fx["threads_per_level_runs"].values() for x in v]
+    assert len(orels) >= 20
+    lo, hi = min(orels), max(orels)
+    g, L, host, f, blocks = config3_setup(amg, oracle, n, w, B)
     dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v] for k, v in host.items()}
     opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smoother=amg.AMG_HYBRID_JGS,
                             smooth_weight=w, num_cycles=N, tol=0.0, num_threads=0, jgs_block_rows=B)
@@ -147,21 +159,39 @@ def test_config3_256cube_async_multadd_hybrid_jgs(amg, oracle, ctx):
     for _ in range(3):
         u, rel, cnt = H.async_solve(f)
         assert np.all(np.isfinite(u))
+        assert list(cnt[:L - 1]) == [N] * (L - 1)
         rels.append(rel)
     free_hier(H)
     g.free()
-    assert sync_rel < 1.0
-    # the oracle's asynchronous band (SMEM_Async_Add_AMG on OpenMP threads, one
-    # thread per level: ~13 s a run at this size, so 3 runs + the equal-speed
-    # schedule), SURVEY.md Sec.8(d).  Both sides are samples of a race whose
-    # outcome depends on the levels' relative speeds; with this few oracle
-    # samples the device's median run must lie in [0.5 min, 2 max] and no run
-    # beyond 4 max (device runs here: 0.0080-0.0095, once 0.0184 when a level
-    # stream lagged behind the shared hardware queues)
-    from async_band import in_band, oracle_async_band
-    lo, hi, orels, _ = oracle_async_band(amg, oracle, host, f, opts, reps=3, thread_sets=([1] * L,),
-                                         blocks=blocks)
-    print(f"config 3 async: oracle band [{lo:.4e}, {hi:.4e}] ({len(orels)} runs), sync {sync_rel:.4e}, "
-          f"device {rels}")
-    assert in_band(sorted(rels)[1], lo, hi), (rels, lo, hi, sync_rel)
+    from async_band import in_band
+    print(f"config 3 async: oracle band [{lo:.4e}, {hi:.4e}] width {hi / lo:.2f}x ({len(orels)} runs), "
+          f"sync {fx['sync_multadd_relres']:.4e}, device {rels}")
+    assert in_band(sorted(rels)[1], lo, hi), (rels, lo, hi)
     assert max(rels) <= 4.0 * hi, (rels, lo, hi)
+
+
+def test_config3_256cube_round_robin_bitwise(amg, oracle, ctx):
+    """config 3 with the arithmetic pinned: under the round-robin schedule
+    (async_schedule 3: level corrections in turn, k_lo first) the device's
+    ASYNC_MULTADD / hybrid JGS iterate at 256^3 is bit-identical to or_async_add
+    under or_set_async_schedule(3)"""
+    n, w, N, B = 256, 0.8, 4, 64
+    g, L, host, f, blocks = config3_setup(amg, oracle, n, w, B)
+    dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v] for k, v in host.items()}
+    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smoother=amg.AMG_HYBRID_JGS, smooth_weight=w,
+                            num_cycles=N, tol=0.0, num_threads=0, jgs_block_rows=B, async_schedule=3)
+    H = amg.Hier(ctx, dev["A"], dev["P"], dev["R"], opts)
+    u, rel, cnt = H.async_solve(f)
+    free_hier(H)
+    g.free()
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    for lev, blk in blocks.items():
+        OH.set_blocks(lev, blk)
+    oracle.lib().or_set_async_schedule(3)
+    try:
+        uo, relo, cnto = OH.async_add(f, [1] * L)
+    finally:
+        oracle.lib().or_set_async_schedule(0)
+    assert list(cnt[:L - 1]) == list(cnto[:L - 1]) == [N] * (L - 1)
+    assert_bitwise(u, uo, "config 3 round-robin iterate")
+    assert abs(rel - relo) <= 1e-12 * relo
