@@ -9,6 +9,37 @@
 
 #include "amg_internal.h"
 
+#include <csignal>
+#include <execinfo.h>
+#include <unistd.h>
+
+// AMG_SEGV_TRACE=1: a host SIGSEGV / SIGBUS prints the native backtrace
+// (frames as libamg_mi355x.so(+offset), for addr2line) before the default
+// action -- the diagnostic for teardown faults of multi-rank tests
+namespace {
+void amg_fault_trace(int sig, siginfo_t *si, void *)
+{
+   char msg[96];
+   const int m = snprintf(msg, sizeof(msg), "[amg] signal %d at address %p, native backtrace:\n", sig, si->si_addr);
+   if (m > 0) (void)!write(2, msg, (size_t)m);
+   void *buf[64];
+   const int n = backtrace(buf, 64);
+   backtrace_symbols_fd(buf, n, 2);
+   raise(sig); // SA_RESETHAND: the default action now
+}
+__attribute__((constructor)) void amg_fault_trace_init()
+{
+   const char *e = std::getenv("AMG_SEGV_TRACE");
+   if (!e || std::atoi(e) == 0) return;
+   struct sigaction sa;
+   std::memset(&sa, 0, sizeof(sa));
+   sa.sa_sigaction = amg_fault_trace;
+   sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+   sigaction(SIGSEGV, &sa, nullptr);
+   sigaction(SIGBUS, &sa, nullptr);
+}
+} // namespace
+
 static thread_local std::string g_last_error;
 
 int amg_set_error(int code, const char *fmt, ...)
@@ -105,6 +136,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ_EDGE")) c->mz_edge = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ27_OCC")) c->mz27_occ = std::max(0, std::min(8, std::atoi(v)));
+   if (const char *v = std::getenv("AMG_MZ_OCC")) c->mz_occ = std::max(0, std::min(8, std::atoi(v)));
    if (const char *v = std::getenv("AMG_MZ27_PF")) c->mz27_pf = std::atoi(v) == 1 ? 1 : 2;
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
    if (const char *v = std::getenv("AMG_RR_OCC")) c->rr_occ = std::atoi(v);

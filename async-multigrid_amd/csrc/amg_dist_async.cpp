@@ -596,6 +596,11 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
          th.emplace_back([&, k] {
             hipSetDevice(c->device);
             for (int cyc = 0; cyc < N && st[k] == AMG_OK; cyc++) st[k] = correct(k);
+            // the level's finish: its stream reaches this marker after its last
+            // correction (recorded here, not after the join, so a level that is
+            // done early is not stamped with the slowest level's time)
+            if (st[k] == AMG_OK && hipEventRecord(t_end[k], D->al[k].s) != hipSuccess)
+               st[k] = amg_set_error(AMG_ERR_HIP, "level %d: hipEventRecord", k);
             if (st[k] == AMG_OK && D->links) st[k] = link_drain(D->links, k);
             if (st[k] != AMG_OK) {
                msg[k] = amg_last_error(); // thread-local: handed to the caller's thread
@@ -611,13 +616,20 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
          if (sched == AMG_SCHED_ROUND_ROBIN) k = q % active;
          else k = sched == AMG_SCHED_FINEST_FIRST ? q / N : active - 1 - q / N;
          st[0] = correct(k);
+         const bool last = sched == AMG_SCHED_ROUND_ROBIN ? q / active == N - 1 : q % N == N - 1;
+         if (st[0] == AMG_OK && last && hipEventRecord(t_end[k], D->al[k].s) != hipSuccess)
+            st[0] = amg_set_error(AMG_ERR_HIP, "level %d: hipEventRecord", k);
       }
       for (int k = 0; k < active && st[0] == AMG_OK && D->links; k++) st[0] = link_drain(D->links, k);
       if (st[0] != AMG_OK && D->links) link_abort(D->links);
    }
    for (int k = 0; k < active; k++) {
-      AMG_HIP(hipEventRecord(t_end[k], D->al[k].s));
-      AMG_HIP(hipStreamWaitEvent(c->stream, t_end[k], 0));
+      if (st[k] == AMG_OK && N <= 0) AMG_HIP(hipEventRecord(t_end[k], D->al[k].s));
+      hipEvent_t done;
+      AMG_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+      AMG_HIP(hipEventRecord(done, D->al[k].s)); // everything level k issued (drains included)
+      AMG_HIP(hipStreamWaitEvent(c->stream, done, 0));
+      AMG_HIP(hipEventDestroy(done));
    }
    AMG_HIP(hipEventDestroy(ready));
    for (int k = 0; k < active; k++)

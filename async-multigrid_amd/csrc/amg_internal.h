@@ -100,6 +100,7 @@ struct amg_ctx {
    // workgroups (mz27_occ > 0: workgroups per CU; 0: mz_chunk's rule) and the
    // prefetch distance in planes (1 or 2)
    int mz27_occ = 3;
+   int mz_occ = 0; // the same for the 7-pt march (AMG_MZ_OCC; 0: mz_chunk's rule)
    int mz27_pf = 2;
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies

@@ -1147,6 +1147,19 @@ static int mz_chunk(const amg_mat *A, int nz, int npb)
    return zc;
 }
 
+// planes per chunk sized so the launch is a whole number of rounds of `occ`
+// resident workgroups per CU (occ: the kernel's VGPR-limited occupancy; 0: off,
+// mz_chunk's rule), each chunk at most AMG_MZ_MAXZC planes
+static int occ_chunk(const amg_mat *A, int nk, int npb, int occ)
+{
+   int zc = mz_chunk(A, nk, npb);
+   const long long slots = (long long)occ * A->ctx->num_cus, work = (long long)nk * npb;
+   if (!A->ctx->mz_zc_auto || occ <= 0 || work < slots) return zc;
+   const long long rounds = (work + slots * AMG_MZ_MAXZC - 1) / (slots * AMG_MZ_MAXZC);
+   zc = (int)((work + slots * rounds - 1) / (slots * rounds));
+   return std::max(1, std::min(zc, AMG_MZ_MAXZC));
+}
+
 struct EpiGemv; // below
 
 template <int NEG, bool NEED_DIAG, class Epi>
@@ -1165,7 +1178,7 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
    // where the plane splits into line groups
    const int lines = std::is_same<Epi, EpiGemv>::value ? A->ctx->mz_lines_gemv : A->ctx->mz_lines;
    if (A->mp_uni && lines > 1 && Sx % 512 == 0 && (P / Sx) % lines == 0) {
-      const int npb = P / (512 * lines), zc = mz_chunk(A, nk, npb), nch = (nk + zc - 1) / zc;
+      const int npb = P / (512 * lines), zc = occ_chunk(A, nk, npb, A->ctx->mz_occ), nch = (nk + zc - 1) / zc;
       if (lines == 4)
          csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 4><<<npb * nch, 256, 0, s>>>(
             A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
@@ -1174,7 +1187,7 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
             A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
       return;
    }
-   const int zc = mz_chunk(A, nk, P / 512);
+   const int zc = occ_chunk(A, nk, P / 512, A->ctx->mz_occ);
    const int npb = P / 512, nch = (nk + zc - 1) / zc;
    if (A->mp_uni)
       csr_mz_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
@@ -1396,12 +1409,9 @@ static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const 
    const int P = A->mz_P, nz = A->nrows / P, nk = ke - kb;
    if (nk <= 0) return;
    const int npb = P / 512;
-   int zc = mz_chunk(A, nk, npb);
-   // one round of resident workgroups (mz27_occ per CU, the VGPR-limited
-   // occupancy of this kernel) when the level is large enough to fill it
-   const int slots = A->ctx->mz27_occ * A->ctx->num_cus;
-   if (A->ctx->mz_zc_auto && slots > 0 && (long long)nk * npb >= slots)
-      zc = std::min(AMG_MZ_MAXZC, (int)(((long long)nk * npb + slots - 1) / slots));
+   // whole rounds of resident workgroups (mz27_occ per CU, the VGPR-limited
+   // occupancy of this kernel)
+   const int zc = occ_chunk(A, nk, npb, A->ctx->mz27_occ);
    const int nch = (nk + zc - 1) / zc;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
    Val27 H;

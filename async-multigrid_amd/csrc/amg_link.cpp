@@ -157,15 +157,16 @@ int progress_one(LinkSet *L, int k)
 {
    for (int p = 0; p < L->R; p++) {
       Chan &c = L->c(k, p);
+      // message seq's event is ev[seq % MAX_EV]: the next to publish is s_pub + 1
       while (c.s_pub < c.sseq) {
-         const hipError_t q = hipEventQuery(c.sev[c.s_pub % MAX_EV]);
+         const hipError_t q = hipEventQuery(c.sev[(c.s_pub + 1) % MAX_EV]);
          if (q == hipErrorNotReady) break;
          if (q != hipSuccess) return amg_set_error(AMG_ERR_HIP, "link send event: %s", hipGetErrorString(q));
          c.s_pub++;
          c.s_arrived->v.store(c.s_pub, std::memory_order_release);
       }
       while (c.r_pub < c.rseq) {
-         const hipError_t q = hipEventQuery(c.rev[c.r_pub % MAX_EV]);
+         const hipError_t q = hipEventQuery(c.rev[(c.r_pub + 1) % MAX_EV]);
          if (q == hipErrorNotReady) break;
          if (q != hipSuccess) return amg_set_error(AMG_ERR_HIP, "link unpack event: %s", hipGetErrorString(q));
          c.r_pub++;

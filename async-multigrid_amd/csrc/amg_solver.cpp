@@ -1346,7 +1346,11 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
             amgk::residual_fsub(s, v0.A, a.u_priv, v0.f, a.y, a.y_fine, n0);
          }
       }
-      if (global_res) {
+      // the reference leaves its loop after the converged correction BEFORE the
+      // GLOBAL residual update (SMEM_Async_AMG.cpp:353-356): converge LOCAL's
+      // N-th correction does not touch the shared residual
+      const bool last_local = !conv_global && issued[k] + 1 >= o.num_cycles;
+      if (global_res && !last_local) {
          // :356-414: u_k = u; the level's slice of r = f - A u_k (SMEM_Residual:
          // y = A u_k, then r = f - y) into the shared r; then r_k = r (under the
          // update stream for SEMI_ASYNC)
