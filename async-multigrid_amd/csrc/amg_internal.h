@@ -99,7 +99,8 @@ struct amg_ctx {
    // 27-pt march: chunks sized so the grid is one round of resident
    // workgroups (mz27_occ > 0: workgroups per CU; 0: mz_chunk's rule) and the
    // prefetch distance in planes (1 or 2)
-   int mz27_occ = 3;
+   // (> 0: that many per CU; < 0: the kernel's own occupancy from the runtime)
+   int mz27_occ = -1;
    int mz_occ = 0; // the same for the 7-pt march (AMG_MZ_OCC; 0: mz_chunk's rule)
    int mz27_pf = 2;
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel

@@ -16,6 +16,9 @@
 // The kernels are HBM-bound (≈0.17 flop/byte); no MFMA.
 #include "amg_internal.h"
 
+#include <mutex>
+#include <unordered_map>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -1150,8 +1153,28 @@ static int mz_chunk(const amg_mat *A, int nz, int npb)
 // planes per chunk sized so the launch is a whole number of rounds of `occ`
 // resident workgroups per CU (occ: the kernel's VGPR-limited occupancy; 0: off,
 // mz_chunk's rule), each chunk at most AMG_MZ_MAXZC planes
-static int occ_chunk(const amg_mat *A, int nk, int npb, int occ)
+// resident 256-thread workgroups per CU of a kernel (its VGPR / LDS limits),
+// from the runtime's occupancy calculator, cached per kernel
+static int kernel_occ(const void *fn)
 {
+   static std::mutex mu;
+   static std::unordered_map<const void *, int> cache;
+   std::lock_guard<std::mutex> g(mu);
+   auto it = cache.find(fn);
+   if (it != cache.end()) return it->second;
+   int nb = 0;
+   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      nb = 0;
+   }
+   cache[fn] = nb;
+   return nb;
+}
+
+// occ < 0: the kernel's own occupancy (kernel_occ)
+static int occ_chunk(const amg_mat *A, int nk, int npb, int occ, const void *fn)
+{
+   if (occ < 0) occ = fn ? kernel_occ(fn) : 0;
    int zc = mz_chunk(A, nk, npb);
    const long long slots = (long long)occ * A->ctx->num_cus, work = (long long)nk * npb;
    if (!A->ctx->mz_zc_auto || occ <= 0 || work < slots) return zc;
@@ -1178,7 +1201,9 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
    // where the plane splits into line groups
    const int lines = std::is_same<Epi, EpiGemv>::value ? A->ctx->mz_lines_gemv : A->ctx->mz_lines;
    if (A->mp_uni && lines > 1 && Sx % 512 == 0 && (P / Sx) % lines == 0) {
-      const int npb = P / (512 * lines), zc = occ_chunk(A, nk, npb, A->ctx->mz_occ), nch = (nk + zc - 1) / zc;
+      const void *fn = lines == 4 ? (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 4>
+                                  : (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 2>;
+      const int npb = P / (512 * lines), zc = occ_chunk(A, nk, npb, A->ctx->mz_occ, fn), nch = (nk + zc - 1) / zc;
       if (lines == 4)
          csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 4><<<npb * nch, 256, 0, s>>>(
             A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
@@ -1187,7 +1212,9 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
             A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
       return;
    }
-   const int zc = occ_chunk(A, nk, P / 512, A->ctx->mz_occ);
+   const void *fn = A->mp_uni ? (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, true>
+                              : (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, false>;
+   const int zc = occ_chunk(A, nk, P / 512, A->ctx->mz_occ, fn);
    const int npb = P / 512, nch = (nk + zc - 1) / zc;
    if (A->mp_uni)
       csr_mz_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
@@ -1411,7 +1438,14 @@ static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const 
    const int npb = P / 512;
    // whole rounds of resident workgroups (mz27_occ per CU, the VGPR-limited
    // occupancy of this kernel)
-   const int zc = occ_chunk(A, nk, npb, A->ctx->mz27_occ);
+   const void *fn;
+   if (A->ctx->mz27_pf == 2)
+      fn = A->mp_uni ? (const void *)csr_mz27_kernel<NEG, NEED_DIAG, Epi, true, 2>
+                     : (const void *)csr_mz27_kernel<NEG, NEED_DIAG, Epi, false, 2>;
+   else
+      fn = A->mp_uni ? (const void *)csr_mz27_kernel<NEG, NEED_DIAG, Epi, true, 1>
+                     : (const void *)csr_mz27_kernel<NEG, NEED_DIAG, Epi, false, 1>;
+   const int zc = occ_chunk(A, nk, npb, A->ctx->mz27_occ, fn);
    const int nch = (nk + zc - 1) / zc;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
    Val27 H;
