@@ -165,6 +165,32 @@ bool composed(const amg_dist_hier *D)
    return D->o.smooth_transfer == 1 && (D->o.solver == AMG_ASYNC_MULTADD || D->o.solver == AMG_MULTADD);
 }
 
+// the level-0 composed restriction as one fused pass: slab hierarchies whose
+// level 0 runs the fused residual + restriction (geo0) with uniform values
+bool fused_xfer0(const amg_dist_hier *D)
+{
+   return composed(D) && D->slab && D->geo0 && D->ctx->fuse_xfer && D->lv[0].A.A && D->lv[0].A.A->mp_uni;
+}
+
+// every rank's restricted rows (slot) into the replicated level's full vector
+int gather_restricted(amg_dist_hier *D, AsyncLevel &a, double *slot, double *full)
+{
+   const int R = D->ctx->xport->nranks;
+   if (R == 1 && a.k >= 0) {
+      // one rank: the allgather is a copy (no transport: the level threads
+      // must not share the communicator)
+      amgk::vcopy(a.s, slot, a.gath, 0, D->gath_blk);
+   } else if (D->links && a.k >= 0) {
+      AMG_TRY(link_allgather(D->links, a.k, a.s, slot, a.gath, D->gath_blk));
+   } else {
+      AMG_TRY(to_comm(D, a));
+      AMG_TRY(xp_allgather(D->ctx, D->ctx->comm_stream, slot, a.gath, (long long)D->gath_blk * 8));
+      AMG_TRY(from_comm(D, a));
+   }
+   launch_scatter_blocks(a.s, a.gath, D->gath_blk, D->d_gcnt, D->d_gdsp, R, full);
+   return AMG_OK;
+}
+
 // r[l+1] = R_l r[l] (SMEM_Sync_Parfor_Restrict / hypre MatvecT in AddCycle); with
 // composed smoothed transfers R~_l r = R_l (r - w A_l D_l^-1 r): t = r ./ a;
 // y = A t; t = r + (-w) y (the oracle's or_hier_set_composed_transfers order)
@@ -173,6 +199,19 @@ int restrict_to(amg_dist_hier *D, AsyncLevel &a, int l)
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    const int Ld = D->Ld;
    double *r = a.r[l];
+   const int R = D->ctx->xport->nranks;
+   double *slot = (l + 1 == Ld) ? a.gath + (size_t)D->gath_blk * R : nullptr;
+   if (fused_xfer0(D) && l == 0) {
+      // the composed restriction of the slab's level 0 in one pass (the fused
+      // residual + restriction kernel's composed mode): r's ghost planes as
+      // that kernel reads them, then coarse planes [Ka, Kb)
+      DLevel &v = D->lv[0];
+      if (R > 1) AMG_TRY(level_xchg(D, a)(r, v.n, v.sg.P, D->rr_ulo, D->rr_uhi));
+      amgk::mz_xfer_restrict(a.s, v.A.A, r - v.sg.off(), v.g, v.d_geo_w, D->o.smooth_weight,
+                             l + 1 < Ld ? a.r[1] : slot, v.Ka, v.Kb, v.sg.e0(), v.Ka);
+      if (l + 1 < Ld) return AMG_OK;
+      return gather_restricted(D, a, slot, a.r[l + 1]);
+   }
    if (composed(D)) {
       const int n = level_n(D, l);
       amgk::xfer_div(a.s, diag_of(D, l), r, a.xt, 0, n);
@@ -183,25 +222,11 @@ int restrict_to(amg_dist_hier *D, AsyncLevel &a, int l)
    if (D->slab && l + 1 < Ld) return slab_restrict(D, a.s, l, r, a.r[l + 1], level_xchg(D, a));
    if (l + 1 < Ld) return a_spgemv(D, a, D->lv[l].R, r, nullptr, mv, a.r[l + 1]);
    if (l + 1 == Ld) {
-      const int R = D->ctx->xport->nranks;
-      double *slot = a.gath + (size_t)D->gath_blk * R;
       if (D->slab)
          AMG_TRY(slab_restrict(D, a.s, l, r, slot, level_xchg(D, a)));
       else
          AMG_TRY(a_spgemv(D, a, D->lv[l].R, r, nullptr, mv, slot));
-      if (R == 1 && a.k >= 0) {
-         // one rank: the allgather is a copy (no transport: the level threads
-         // must not share the communicator)
-         amgk::vcopy(a.s, slot, a.gath, 0, D->gath_blk);
-      } else if (D->links && a.k >= 0) {
-         AMG_TRY(link_allgather(D->links, a.k, a.s, slot, a.gath, D->gath_blk));
-      } else {
-         AMG_TRY(to_comm(D, a));
-         AMG_TRY(xp_allgather(D->ctx, D->ctx->comm_stream, slot, a.gath, (long long)D->gath_blk * 8));
-         AMG_TRY(from_comm(D, a));
-      }
-      launch_scatter_blocks(a.s, a.gath, D->gath_blk, D->d_gcnt, D->d_gdsp, R, a.r[l + 1]);
-      return AMG_OK;
+      return gather_restricted(D, a, slot, a.r[l + 1]);
    }
    amgk::spgemv(a.s, D->cR[l - Ld], r, nullptr, mv, a.r[l + 1], 0, level_n(D, l + 1), nullptr);
    return AMG_OK;
@@ -392,6 +417,11 @@ int setup_async(amg_dist_hier *D)
                   cap1[M->peers[i]] = std::max(cap1[M->peers[i]], M->rcnt[i]);
             }
          }
+      if (fused_xfer0(D)) {
+         const long long P0 = D->lv[0].sg.P;
+         if (me > 0) cap1[me - 1] = std::max(cap1[me - 1], (long long)D->rr_ulo[me] * P0);
+         if (me < R - 1) cap1[me + 1] = std::max(cap1[me + 1], (long long)D->rr_uhi[me] * P0);
+      }
       if (Ld < L)
          for (int p = 0; p < R; p++)
             if (p != me) cap1[p] = std::max(cap1[p], (long long)D->gath_blk);

@@ -333,7 +333,7 @@ void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const do
 // ef = P ec + (-w) (A P ec) ./ a, then mode 0: out = ef; 1: atomic_correct(out =
 // u, ef, u_priv); 2: out = u + ef
 void mz_xfer_restrict(hipStream_t s, const amg_mat *A, const double *r, const GeoT &g, const double *wdev,
-                      double omega, double *rc);
+                      double omega, double *rc, int Kb = 0, int Ke = -1, int fz0 = 0, int cz0 = 0);
 void mz_xfer_prolong(hipStream_t s, const amg_mat *A, const double *ec, const GeoT &g, const double *wdev,
                      double omega, int mode, double *out, double *u_priv);
 // transpose-product with the expansion-buffer order of T static chunks

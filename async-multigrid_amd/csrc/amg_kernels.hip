@@ -1830,10 +1830,10 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
 // rc = R (r + (-w) A (r ./ a)) for a marched uniform 7-pt level with geometric
 // R (the composed smoothed restriction of xfer_restrict in one pass)
 void mz_xfer_restrict(hipStream_t s, const amg_mat *A, const double *r, const GeoT &g, const double *wdev,
-                      double omega, double *rc)
+                      double omega, double *rc, int Kb, int Ke, int fz0, int cz0)
 {
-   const int Ke = g.nz / 2;
-   if (Ke <= 0) return;
+   if (Ke < 0) Ke = g.nz / 2;
+   if (Ke <= Kb) return;
    const int nzm = A->nrows / (g.nx * g.ny);
    Val7 S;
    for (int j = 0; j < 7; j++) S.v[j] = A->mp_val[j];
@@ -1841,16 +1841,16 @@ void mz_xfer_restrict(hipStream_t s, const amg_mat *A, const double *r, const Ge
    const int LC = ((g.ny / 2) % (2 * groups) == 0 && A->ctx->rr_lines == 2) ? 2 : 1;
    const int nlb = (g.ny / 2) / (groups * LC);
    const int zcc = std::max(1, std::min(A->ctx->mz_zc / 2, 32));
-   const int nb = nlb * ((Ke + zcc - 1) / zcc);
+   const int nb = nlb * ((Ke - Kb + zcc - 1) / zcc);
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
    if (LC == 2)
       mz_res_restrict_kernel<true, 2, 1, false, true><<<nb, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, r, nullptr, wdev, g.nx, g.ny, g.nz, zcc, nlb, A->ctx->mz_xcd, 0, rc, 0,
-         Ke, 0, 0, nzm, ZeroGuess(), -omega);
+         A->ppat, A->mpmask, A->pp_n, mv, S, r, nullptr, wdev, g.nx, g.ny, g.nz, zcc, nlb, A->ctx->mz_xcd, 0, rc, Kb,
+         Ke, fz0, cz0, nzm, ZeroGuess(), -omega);
    else
       mz_res_restrict_kernel<true, 1, 1, false, true><<<nb, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, r, nullptr, wdev, g.nx, g.ny, g.nz, zcc, nlb, A->ctx->mz_xcd, 0, rc, 0,
-         Ke, 0, 0, nzm, ZeroGuess(), -omega);
+         A->ppat, A->mpmask, A->pp_n, mv, S, r, nullptr, wdev, g.nx, g.ny, g.nz, zcc, nlb, A->ctx->mz_xcd, 0, rc, Kb,
+         Ke, fz0, cz0, nzm, ZeroGuess(), -omega);
 }
 
 // Geometric prolongation + correction u += P e (SMEM_Sync_SpGEMV(P, e, u, 1, 1,

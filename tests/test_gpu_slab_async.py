@@ -79,22 +79,27 @@ def oracle_opts_of(oracle, o):
 
 
 SCHED = [
-    # (solver, composed transfers, nranks, schedule)
-    ("multadd", True, 1, 3),
-    ("multadd", True, 2, 3),
-    ("multadd", True, 3, 1),
-    ("multadd", True, 2, 2),
-    ("afacx", False, 2, 3),
-    ("afacx", False, 3, 2),
+    # (solver, composed transfers, nranks, schedule, n)
+    ("multadd", True, 1, 3, 32),
+    ("multadd", True, 2, 3, 32),
+    ("multadd", True, 3, 1, 32),
+    ("multadd", True, 2, 2, 32),
+    ("afacx", False, 2, 3, 32),
+    ("afacx", False, 3, 2, 32),
+    # 64^3: level 0 runs the fused residual + restriction form, so the composed
+    # restriction of level 0 is the one-pass kernel (ghost planes over the channels)
+    ("multadd", True, 2, 3, 64),
+    ("multadd", True, 1, 1, 64),
 ]
 
 
-@pytest.mark.parametrize("solver,comp,nranks,sched", SCHED, ids=[f"{s}-{n}r-s{q}" for s, _, n, q in SCHED])
-def test_slab_async_schedule_bitwise(amg, oracle, ctx, solver, comp, nranks, sched):
+@pytest.mark.parametrize("solver,comp,nranks,sched,n", SCHED,
+                         ids=[f"{s}-{n}r-s{q}-{m}" for s, _, n, q, m in SCHED])
+def test_slab_async_schedule_bitwise(amg, oracle, ctx, solver, comp, nranks, sched, n):
     """deterministic schedules of the slab-distributed asynchronous additive
     solve against the oracle's or_async_add (SMEM_Async_Add_AMG restated) under
     the same schedule: the assembled iterate is the same bits"""
-    n, N = 32, 8
+    N = 8
     gen = amg.Gen(n)
     f = amg.rhs_rand(0, n ** 3)
     sv = amg.AMG_ASYNC_MULTADD if solver == "multadd" else amg.AMG_ASYNC_AFACX
