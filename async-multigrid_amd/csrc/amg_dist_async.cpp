@@ -132,6 +132,9 @@ int a_spgemv(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x, const doubl
 XchgFn level_xchg(amg_dist_hier *D, AsyncLevel &a)
 {
    return [D, &a](double *x, long long n, long long cP, const std::vector<int> &lo, const std::vector<int> &hi) {
+      // one rank: no neighbour, nothing to exchange -- and no hop through the
+      // shared comm stream, which would serialise the level streams
+      if (D->ctx->xport->nranks == 1) return (int)AMG_OK;
       if (D->links && a.k >= 0) return link_xchg_planes(D->links, a.k, a.s, x, n, cP, lo, hi);
       AMG_TRY(to_comm(D, a));
       AMG_TRY(slab_xchg(D->ctx, D->ctx->comm_stream, x, n, cP, lo, hi));
