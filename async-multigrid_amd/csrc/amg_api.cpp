@@ -14,10 +14,14 @@
 #include <unistd.h>
 
 // AMG_SEGV_TRACE=1: a host SIGSEGV / SIGBUS prints the native backtrace
-// (frames as libamg_mi355x.so(+offset), for addr2line) before the default
-// action -- the diagnostic for teardown faults of multi-rank tests
+// (frames as libamg_mi355x.so(+offset), for addr2line), then hands the signal
+// to the handler that was installed before (Python's faulthandler prints the
+// threads' Python stacks) -- the diagnostic for teardown faults of multi-rank
+// tests.  backtrace() is called once at install so that libgcc is loaded
+// before any fault (loading it inside the handler would allocate).
 namespace {
-void amg_fault_trace(int sig, siginfo_t *si, void *)
+struct sigaction g_prev_segv, g_prev_bus;
+void amg_fault_trace(int sig, siginfo_t *si, void *uc)
 {
    char msg[96];
    const int m = snprintf(msg, sizeof(msg), "[amg] signal %d at address %p, native backtrace:\n", sig, si->si_addr);
@@ -25,18 +29,27 @@ void amg_fault_trace(int sig, siginfo_t *si, void *)
    void *buf[64];
    const int n = backtrace(buf, 64);
    backtrace_symbols_fd(buf, n, 2);
-   raise(sig); // SA_RESETHAND: the default action now
+   const struct sigaction &prev = sig == SIGSEGV ? g_prev_segv : g_prev_bus;
+   if ((prev.sa_flags & SA_SIGINFO) && prev.sa_sigaction) {
+      prev.sa_sigaction(sig, si, uc);
+   } else if (prev.sa_handler != SIG_DFL && prev.sa_handler != SIG_IGN && prev.sa_handler) {
+      prev.sa_handler(sig);
+   }
+   signal(sig, SIG_DFL);
+   raise(sig);
 }
 __attribute__((constructor)) void amg_fault_trace_init()
 {
    const char *e = std::getenv("AMG_SEGV_TRACE");
    if (!e || std::atoi(e) == 0) return;
+   void *warm[4];
+   (void)backtrace(warm, 4);
    struct sigaction sa;
    std::memset(&sa, 0, sizeof(sa));
    sa.sa_sigaction = amg_fault_trace;
-   sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
-   sigaction(SIGSEGV, &sa, nullptr);
-   sigaction(SIGBUS, &sa, nullptr);
+   sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+   sigaction(SIGSEGV, &sa, &g_prev_segv);
+   sigaction(SIGBUS, &sa, &g_prev_bus);
 }
 } // namespace
 

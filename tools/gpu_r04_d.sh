@@ -4,9 +4,9 @@
 set -o pipefail
 mkdir -p gpurun_out/r04d
 export AMG_LINK_TIMEOUT_S=120 AMG_SEGV_TRACE=1
-timeout -k 10 780 python -u -m pytest tests -m "gpu and not slow" -q --timeout 170 --timeout-method thread \
+timeout -k 10 780 python -u -m pytest tests -m "gpu and not slow" -v -rf --timeout 170 --timeout-method thread \
    -p no:cacheprovider > gpurun_out/r04d/pytest_gpu.log 2>&1
-rc=$?; echo "pytest exit $rc"; tail -3 gpurun_out/r04d/pytest_gpu.log
+rc=$?; echo "pytest exit $rc"; tail -12 gpurun_out/r04d/pytest_gpu.log | cut -c1-200
 case $rc in 124|134|137|139) exit $rc;; esac
 timeout -k 10 380 python -u -m pytest tests/test_gpu_slab_async.py -k 512 -v -s --timeout 360 --timeout-method thread \
    > gpurun_out/r04d/slab512.log 2>&1
