@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "amg_internal.h"
@@ -162,9 +163,19 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    return AMG_OK;
 }
 
+// one process-wide lock around teardown (contexts, hierarchies, matrices):
+// ranks that are threads of one process free concurrently, and the runtime's
+// free / destroy paths are kept out of each other's way
+std::recursive_mutex &amg_teardown_mutex()
+{
+   static std::recursive_mutex m;
+   return m;
+}
+
 extern "C" int amg_finalize(amg_ctx *c)
 {
    if (!c) return AMG_OK;
+   std::lock_guard<std::recursive_mutex> td(amg_teardown_mutex());
    hipSetDevice(c->device);
    hipStreamSynchronize(c->stream);
    if (c->comm_stream) hipStreamSynchronize(c->comm_stream);
@@ -1125,6 +1136,7 @@ extern "C" int amg_csr_register(amg_ctx *c, int nrows, int ncols, long long nnz,
 
 extern "C" int amg_mat_free(amg_mat *A)
 {
+   std::lock_guard<std::recursive_mutex> td(amg_teardown_mutex());
    if (!A) return AMG_OK;
    if (A->trans) amg_mat_free(A->trans);
    hipFree(A->rowptr);

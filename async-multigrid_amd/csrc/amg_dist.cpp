@@ -79,6 +79,7 @@ extern "C" int amg_dist_init_host(amg_ctx *c, int nranks, int rank, amg_host_xch
 extern "C" int amg_dist_finalize(amg_ctx *c)
 {
    if (!c || !c->xport) return AMG_OK;
+   std::lock_guard<std::recursive_mutex> td(amg_teardown_mutex());
    // nothing may be in flight on any stream when the communicator goes
    // (an async solve that returned early can leave level-stream work queued)
    hipStreamSynchronize(c->stream);
@@ -884,6 +885,9 @@ extern "C" int amg_dist_hier_free(amg_dist_hier *D)
    hipStreamSynchronize(D->ctx->comm_stream);
    for (auto s : D->ctx->level_streams) hipStreamSynchronize(s);
    if (D->links) link_free(D->links); // collective (a barrier between unmapping and freeing)
+   // the rest under the process-wide teardown lock (not link_free: a peer
+   // blocked in its barrier would hold it)
+   std::lock_guard<std::recursive_mutex> td(amg_teardown_mutex());
    for (auto *a : {&D->grid.al}) {
       if (a->ev_ready) hipEventDestroy(a->ev_ready);
       if (a->ev_done) hipEventDestroy(a->ev_done);

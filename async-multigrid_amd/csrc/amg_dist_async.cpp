@@ -93,7 +93,14 @@ int a_halo(amg_dist_hier *D, AsyncLevel &a, DistMat &M, double *x)
    }
    if (M.replicated_cols || M.peers.empty()) return AMG_OK;
    double *&sb = a.sbuf[&M];
-   if (!sb) AMG_TRY(dvec(D, std::max<long long>(1, M.nsend), &sb));
+   if (!sb) {
+      // the level groups' buffers are made by setup_async (a level thread must
+      // not allocate: dvec appends to the hierarchy's list and zeroes on the
+      // main stream); the grid's on first use, ordered before this stream
+      AMG_ARG(a.k < 0, "a_halo: level %d has no send buffer for this operator", a.k);
+      AMG_TRY(dvec(D, std::max<long long>(1, M.nsend), &sb));
+      AMG_HIP(hipStreamSynchronize(D->ctx->stream));
+   }
    launch_gather(a.s, x, M.d_send_idx, sb, (int)M.nsend);
    const int np = (int)M.peers.size();
    if (D->links && a.k >= 0) {
@@ -398,6 +405,13 @@ int setup_async(amg_dist_hier *D)
          AMG_TRY(lvec(D, k, &a.rf));
       }
       if (Ld < L) AMG_TRY(dvec(D, (size_t)D->gath_blk * (t->nranks + 1), &a.gath));
+      // the row form's packed send buffers, one per operator with peers
+      for (int l = 0; l < Ld; l++)
+         for (DistMat *M : {&D->lv[l].A, &D->lv[l].P, &D->lv[l].R}) {
+            if (!M->A || M->slab || M->replicated_cols || M->peers.empty()) continue;
+            double *&sb = a.sbuf[M];
+            if (!sb) AMG_TRY(dvec(D, std::max<long long>(1, M->nsend), &sb));
+         }
       a.k = k;
    }
    if (D->o.accel_type != AMG_NO_ACCEL)

@@ -418,3 +418,7 @@ void reduce_partials(hipStream_t s, const double *partials, int np, double *out,
                      double *scratch);
 
 } // namespace amgk
+
+// process-wide lock held by the teardown entry points (amg_api.cpp)
+#include <mutex>
+std::recursive_mutex &amg_teardown_mutex();

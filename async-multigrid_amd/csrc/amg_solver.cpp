@@ -420,6 +420,7 @@ extern "C" int amg_hier_create(amg_ctx *c, int L, amg_mat *const *A, amg_mat *co
 extern "C" int amg_hier_free(amg_hier *H)
 {
    if (!H) return AMG_OK;
+   std::lock_guard<std::recursive_mutex> td(amg_teardown_mutex());
    hipStreamSynchronize(H->ctx->stream);
    for (auto s : H->ctx->level_streams) hipStreamSynchronize(s);
    prof_drain(H);
