@@ -151,6 +151,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_MZ_EDGE")) c->mz_edge = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ27_OCC")) c->mz27_occ = std::max(-1, std::min(8, std::atoi(v)));
    if (const char *v = std::getenv("AMG_MZ_OCC")) c->mz_occ = std::max(-1, std::min(8, std::atoi(v)));
+   if (const char *v = std::getenv("AMG_MZ_PF")) c->mz_pf = std::atoi(v) == 2 ? 2 : 1;
    if (const char *v = std::getenv("AMG_MZ27_PF")) c->mz27_pf = std::atoi(v) == 1 ? 1 : 2;
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
    if (const char *v = std::getenv("AMG_RR_OCC")) c->rr_occ = std::atoi(v);

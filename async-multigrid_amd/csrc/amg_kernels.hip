@@ -1019,7 +1019,7 @@ __device__ __forceinline__ v2d mz_acc7(v2d acc, const v2d (&xv)[7], unsigned lon
 // k - 1, k, k + 1, so the +-S operands of its inner lines come from registers
 // and only the two halo lines are loaded per plane (2 / NLN line loads per line
 // instead of 2).  NLN > 1 needs S % 512 == 0 and NLN | P / S.
-template <int NEG, bool NEED_DIAG, class Epi, bool UNI, int NLN = 1>
+template <int NEG, bool NEED_DIAG, class Epi, bool UNI, int NLN = 1, int PF = 1>
 __global__ __launch_bounds__(256) void csr_mz_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ x, int P, int S, int nz, int zc,
@@ -1058,6 +1058,14 @@ __global__ __launch_bounds__(256) void csr_mz_kernel(
       xc[i] = ld2u(x, (unsigned)k0 * P + p);
       xq[i] = k0 + 1 < nz ? ld2u(x, (unsigned)(k0 + 1) * P + p) : v2d{0.0, 0.0};
    }
+   // PF = 2: plane k + 2 arrives one iteration early (q2), plane k + 3 is in
+   // flight while plane k is computed
+   v2d q2[PF == 2 ? NLN : 1];
+#pragma unroll
+   for (int i = 0; i < (PF == 2 ? NLN : 1); i++) {
+      q2[i] = v2d{0.0, 0.0};
+      if (PF == 2 && k0 + 2 < nz && k0 + 1 < k1) q2[i] = ld2u(x, (unsigned)(k0 + 2) * P + (unsigned)(pos + i * S));
+   }
    struct PlaneIn {
       v2d ym, yp; // halo lines: below the first, above the last
       double e[NLN];
@@ -1080,12 +1088,12 @@ __global__ __launch_bounds__(256) void csr_mz_kernel(
    __syncthreads();
    for (int k = k0; k < k1; k++) {
       const unsigned row0 = (unsigned)k * P + pos;
-      // prefetch plane k + 2 (this chunk's last iteration needs plane k1)
+      // prefetch plane k + PF + 1 (this chunk's last iteration needs plane k1)
       v2d xn[NLN];
 #pragma unroll
       for (int i = 0; i < NLN; i++) {
          xn[i] = v2d{0.0, 0.0};
-         if (k + 2 < nz && k + 1 < k1) xn[i] = ld2u(x, row0 + (unsigned)(i * S) + 2u * P);
+         if (k + PF + 1 < nz && k + PF < k1) xn[i] = ld2u(x, row0 + (unsigned)(i * S) + (PF + 1u) * P);
       }
       PlaneIn cur;
       fetch(k, cur);
@@ -1128,7 +1136,12 @@ __global__ __launch_bounds__(256) void csr_mz_kernel(
       for (int i = 0; i < NLN; i++) {
          xm[i] = xc[i];
          xc[i] = xq[i];
-         xq[i] = xn[i];
+         if (PF == 2) {
+            xq[i] = q2[i];
+            q2[i] = xn[i];
+         } else {
+            xq[i] = xn[i];
+         }
       }
    }
    if (partials) {
@@ -1198,30 +1211,39 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
    if (nk <= 0) return;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
    // two or four lines per lane (ctx->mz_lines; SpMV / SpGEMV: ctx->mz_lines_gemv)
-   // where the plane splits into line groups
+   // where the plane splits into line groups; ctx->mz_pf: prefetch distance
    const int lines = std::is_same<Epi, EpiGemv>::value ? A->ctx->mz_lines_gemv : A->ctx->mz_lines;
+   const bool pf2 = A->ctx->mz_pf == 2;
+   auto go = [&](auto uni, auto nln, auto pf) {
+      constexpr bool U = decltype(uni)::value;
+      constexpr int N = decltype(nln)::value, F = decltype(pf)::value;
+      const void *fn = (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F>;
+      const int npb = P / (512 * N), zc = occ_chunk(A, nk, npb, A->ctx->mz_occ, fn), nch = (nk + zc - 1) / zc;
+      csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F><<<npb * nch, 256, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
+   };
+   using T = std::true_type;
+   using F = std::false_type;
+   using I1 = std::integral_constant<int, 1>;
+   using I2 = std::integral_constant<int, 2>;
+   using I4 = std::integral_constant<int, 4>;
    if (A->mp_uni && lines > 1 && Sx % 512 == 0 && (P / Sx) % lines == 0) {
-      const void *fn = lines == 4 ? (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 4>
-                                  : (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 2>;
-      const int npb = P / (512 * lines), zc = occ_chunk(A, nk, npb, A->ctx->mz_occ, fn), nch = (nk + zc - 1) / zc;
-      if (lines == 4)
-         csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 4><<<npb * nch, 256, 0, s>>>(
-            A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
-      else
-         csr_mz_kernel<NEG, NEED_DIAG, Epi, true, 2><<<npb * nch, 256, 0, s>>>(
-            A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
+      if (lines == 4) {
+         if (pf2) go(T{}, I4{}, I2{});
+         else go(T{}, I4{}, I1{});
+      } else {
+         if (pf2) go(T{}, I2{}, I2{});
+         else go(T{}, I2{}, I1{});
+      }
       return;
    }
-   const void *fn = A->mp_uni ? (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, true>
-                              : (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, false>;
-   const int zc = occ_chunk(A, nk, P / 512, A->ctx->mz_occ, fn);
-   const int npb = P / 512, nch = (nk + zc - 1) / zc;
-   if (A->mp_uni)
-      csr_mz_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
-   else
-      csr_mz_kernel<NEG, NEED_DIAG, Epi, false><<<npb * nch, 256, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, mv, S, x, P, A->mz_S, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
+   if (A->mp_uni) {
+      if (pf2) go(T{}, I1{}, I2{});
+      else go(T{}, I1{}, I1{});
+   } else {
+      if (pf2) go(F{}, I1{}, I2{});
+      else go(F{}, I1{}, I1{});
+   }
 }
 
 // ---------------------------------------------------------------------------
