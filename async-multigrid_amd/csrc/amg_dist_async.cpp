@@ -182,6 +182,14 @@ bool fused_xfer0(const amg_dist_hier *D)
    return composed(D) && D->slab && D->geo0 && D->ctx->fuse_xfer && D->lv[0].A.A && D->lv[0].A.A->mp_uni;
 }
 
+// the level-0 composed prolongation as one fused pass (and, when asked, the
+// FULL_ASYNC atomic correction with it): slab hierarchies whose level 0 runs
+// the fused kernels and whose level-1 ghost needs fit (xfp0)
+bool fused_xfp0(const amg_dist_hier *D)
+{
+   return composed(D) && D->slab && D->xfp0 && D->ctx->fuse_xfer && D->lv[0].A.A;
+}
+
 // every rank's restricted rows (slot) into the replicated level's full vector
 int gather_restricted(amg_dist_hier *D, AsyncLevel &a, double *slot, double *full)
 {
@@ -244,9 +252,34 @@ int restrict_to(amg_dist_hier *D, AsyncLevel &a, int l)
 
 // out = P_l x (x on level l+1, out on level l); composed smoothed transfers:
 // out = P x;  y = A out;  out = out + (-w) (y ./ a)
-int prolong_to(amg_dist_hier *D, AsyncLevel &a, int l, double *x, double *out)
+int prolong_to(amg_dist_hier *D, AsyncLevel &a, int l, double *x, double *out, int apply = 0,
+               double *u = nullptr, double *u_priv = nullptr)
 {
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
+   if (l == 0 && fused_xfp0(D)) {
+      // P~ e = P e - w (A P e) ./ a over the owned fine planes in one march
+      // (mz_xfer_prolong): the coarse ghost planes it reads, then the kernel;
+      // apply 1: the atomic correction of u (u_priv = the value after it)
+      DLevel &v = D->lv[0];
+      const bool from_rep = D->Ld < 2;
+      long long coff = 0;
+      int cz0 = 0;
+      if (!from_rep) {
+         const DLevel &c1 = D->lv[1];
+         coff = c1.sg.off();
+         cz0 = c1.sg.e0();
+         if (D->ctx->xport->nranks > 1)
+            AMG_TRY(level_xchg(D, a)(x, c1.n, c1.sg.P, D->xp_lo, D->xp_hi));
+      }
+      const long long off = v.sg.off();
+      if (apply == 1)
+         amgk::mz_xfer_prolong(a.s, v.A.A, x - coff, v.g, v.d_geo_w, D->o.smooth_weight, 1, u - off, u_priv - off,
+                               v.sg.za, v.sg.zb, v.sg.e0(), cz0);
+      else
+         amgk::mz_xfer_prolong(a.s, v.A.A, x - coff, v.g, v.d_geo_w, D->o.smooth_weight, 0, out - off, nullptr,
+                               v.sg.za, v.sg.zb, v.sg.e0(), cz0);
+      return AMG_OK;
+   }
    if (D->slab && l < D->Ld)
       AMG_TRY(slab_prolong(D, a.s, l, x, out, false, level_xchg(D, a)));
    else if (l < D->Ld)
@@ -343,7 +376,11 @@ int level_correction(amg_dist_hier *D, int k)
       AMG_TRY(a_smooth(D, a, fg, a.rf, a.uf, o.num_fine_smooth_sweeps));
       amgk::vcopy(s, a.uf, a.e[k], 0, nf);
    }
-   for (int l = k - 1; l >= 0; l--) AMG_TRY(prolong_to(D, a, l, a.e[l + 1], a.e[l]));
+   // the atomic correction rides on the fused level-0 prolongation where it
+   // can (no acceleration step between them)
+   const bool fuse_corr = k > 0 && o.accel_type == AMG_NO_ACCEL && fused_xfp0(D);
+   for (int l = k - 1; l >= 0; l--)
+      AMG_TRY(prolong_to(D, a, l, a.e[l + 1], a.e[l], (l == 0 && fuse_corr) ? 1 : 0, D->lv[0].u, a.u_priv));
    const int n0 = D->lv[0].n;
    if (o.accel_type != AMG_NO_ACCEL) {
       // DMEM_Add.cpp:319-324: ChebyUpdate(gridk.d, U_array[0]) on the level's
@@ -357,7 +394,7 @@ int level_correction(amg_dist_hier *D, int k)
          amgk::vcopy(s, a.e[0], a.d_acc, 0, n0);
    }
    // correction into the shared slab; u_priv = the value each row saw
-   amgk::atomic_correct(s, D->lv[0].u, a.e[0], a.u_priv, n0);
+   if (!fuse_corr) amgk::atomic_correct(s, D->lv[0].u, a.e[0], a.u_priv, n0);
    // private residual r_k = f - A u_k  (SMEM_Residual on u_k)
    AMG_TRY(a_spgemv(D, a, D->lv[0].A, a.u_priv, nullptr, amgk::gemv_mode(1.0, 0.0), a.y));
    amgk::vsub(s, D->lv[0].f, a.y, a.r[0], 0, n0);
@@ -434,6 +471,11 @@ int setup_async(amg_dist_hier *D)
                   cap1[M->peers[i]] = std::max(cap1[M->peers[i]], M->rcnt[i]);
             }
          }
+      if (fused_xfp0(D) && Ld >= 2) {
+         const long long P1 = D->lv[1].sg.P;
+         if (me > 0) cap1[me - 1] = std::max(cap1[me - 1], (long long)D->xp_lo[me] * P1);
+         if (me < R - 1) cap1[me + 1] = std::max(cap1[me + 1], (long long)D->xp_hi[me] * P1);
+      }
       if (fused_xfer0(D)) {
          const long long P0 = D->lv[0].sg.P;
          if (me > 0) cap1[me - 1] = std::max(cap1[me - 1], (long long)D->rr_ulo[me] * P0);

@@ -185,6 +185,11 @@ struct amg_dist_hier {
    bool slab = false;
    bool geo0 = false;
    std::vector<int> rr_ulo, rr_uhi, rr_flo, rr_fhi;
+   // the fused composed prolongation of level 0 (mz_xfer_prolong over the
+   // owned fine planes): level-1 ghost planes it reads per rank, and whether
+   // they fit the ghost room (xfp0)
+   std::vector<int> xp_lo, xp_hi;
+   bool xfp0 = false;
    amgd::SlabGeom sg_rep; // owned planes of the first replicated level (the allgather blocks)
    int L = 0, Ld = 0; // levels [0, Ld) distributed, [Ld, L) replicated
    amgd::Partition part;

@@ -336,7 +336,8 @@ void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const do
 void mz_xfer_restrict(hipStream_t s, const amg_mat *A, const double *r, const GeoT &g, const double *wdev,
                       double omega, double *rc, int Kb = 0, int Ke = -1, int fz0 = 0, int cz0 = 0);
 void mz_xfer_prolong(hipStream_t s, const amg_mat *A, const double *ec, const GeoT &g, const double *wdev,
-                     double omega, int mode, double *out, double *u_priv);
+                     double omega, int mode, double *out, double *u_priv, int zlo = 0, int zhi = -1, int fz0 = 0,
+                     int cz0 = 0);
 // transpose-product with the expansion-buffer order of T static chunks
 void matvec_t_chunked(hipStream_t s, const amg_mat *AT, const double *x, double *y, int n_src,
                       int T);

@@ -2256,8 +2256,12 @@ template <bool UNI, int OUT>
 __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ e, const double *__restrict__ wg,
-   double mw, int nx, int ny, int nz, int zc, int npb, int xcd, double *__restrict__ out, double *__restrict__ u_priv)
+   double mw, int nx, int ny, int nz, int zc, int npb, int xcd, double *__restrict__ out, double *__restrict__ u_priv,
+   int zlo, int zhi, int fz0, int cz0)
 {
+   // fine planes [zlo, zhi) of the nx * ny * nz box; out / u_priv / the
+   // operator's rows (pattern bytes) have plane 0 = fine plane fz0, e plane 0
+   // = coarse plane cz0 (a z-slab's extended vectors; the whole box: 0, nz, 0, 0)
    __shared__ unsigned long long mtab[256];
    __shared__ v2d mval[UNI ? 1 : 256 * 7];
    __shared__ double wl[27];
@@ -2272,7 +2276,7 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
    int lg = (int)blockIdx.x;
    if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
    const int pblk = lg % npb, chunk = lg / npb;
-   const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
+   const int k0 = zlo + chunk * zc, k1 = min(k0 + zc, zhi);
    const int pos = pblk * 512 + 2 * tid;
    const int fx = pos % nx, fy = pos / nx;
    __syncthreads();
@@ -2286,14 +2290,14 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
       int x = fx, y = fy + dy, z = p;
       norm3(x, y, z);
       if (z < 0 || z >= nz) return v2d{0.0, 0.0};
-      return geo_prolong_pair(v2d{0.0, 0.0}, e, wl, x, y, z, ncx, ncy, ncz);
+      return geo_prolong_pair(v2d{0.0, 0.0}, e, wl, x, y, z, ncx, ncy, ncz, cz0);
    };
    auto edge = [&](int p) -> double {
       if (lane != 0 && lane != 63) return 0.0;
       int x = lane == 0 ? fx - 1 : fx + 2, y = fy, z = p;
       norm3(x, y, z);
       if (z < 0 || z >= nz) return 0.0;
-      return geo_prolong_point(0.0, e, wl, x, y, z, ncx, ncy, ncz);
+      return geo_prolong_point(0.0, e - (long long)cz0 * ncx * ncy, wl, x, y, z, ncx, ncy, ncz);
    };
    v2d xm = ef2(k0 - 1, 0);
    v2d xc = ef2(k0, 0);
@@ -2301,7 +2305,7 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
    v2d xq = ef2(k0 + 1, 0);
    double eq = edge(k0 + 1);
    for (int k = k0; k < k1; k++) {
-      const unsigned row = (unsigned)k * P + pos;
+      const unsigned row = (unsigned)(k - fz0) * P + pos;
       v2d xn{0.0, 0.0};
       double en = 0.0;
       if (k + 2 < nz && k + 1 < k1) {
@@ -2348,20 +2352,24 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
 }
 
 void mz_xfer_prolong(hipStream_t s, const amg_mat *A, const double *ec, const GeoT &g, const double *wdev,
-                     double omega, int mode, double *out, double *u_priv)
+                     double omega, int mode, double *out, double *u_priv, int zlo, int zhi, int fz0, int cz0)
 {
    MpSten S;
    for (int j = 0; j < AMG_MP_MAXJ; j++) {
       S.off[j] = A->mp_off[j];
       S.val[j] = A->mp_val[j];
    }
-   const int P = A->mz_P, nz = A->nrows / P;
-   const int zc = mz_chunk(A, nz, P / 512);
-   const int npb = P / 512, nch = (nz + zc - 1) / zc;
+   const int P = A->mz_P;
+   if (zhi < 0) zhi = g.nz;
+   const int nk = zhi - zlo;
+   if (nk <= 0) return;
+   const int zc = mz_chunk(A, nk, P / 512);
+   const int npb = P / 512, nch = (nk + zc - 1) / zc;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
 #define AMG_XP(U, O)                                                                                           \
    mz_xfer_prolong_kernel<U, O><<<npb * nch, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, ec, wdev, -omega, \
-                                                          g.nx, g.ny, g.nz, zc, npb, A->ctx->mz_xcd, out, u_priv)
+                                                          g.nx, g.ny, g.nz, zc, npb, A->ctx->mz_xcd, out, u_priv, \
+                                                          zlo, zhi, fz0, cz0)
 #define AMG_XP2(U)                 \
    if (mode == 1) AMG_XP(U, 1);    \
    else if (mode == 2) AMG_XP(U, 2); \

@@ -737,6 +737,34 @@ extern "C" int amg_dist_hier_create_slab(amg_ctx *c, const amg_gen *g, const amg
                D->geo0 = false;
          }
       }
+      // the fused composed prolongation reads P e on fine planes za - 1 .. zb
+      // (the 7-pt stencil around the owned planes): coarse planes of level 1
+      // from the first candidate of za - 1 to the last of zb
+      D->xfp0 = D->geo0;
+      if (D->xfp0 && Ld >= 2) {
+         D->xp_lo.assign(R, 0);
+         D->xp_hi.assign(R, 0);
+         const int nz = gg.nz, ncz = nz / 2;
+         for (int r = 0; r < R; r++) {
+            const int za = zp[0][r], zb = zp[0][r + 1], Ka = zp[1][r], Kb = zp[1][r + 1];
+            if (zb <= za) continue;
+            int cmin = ncz, cmax = -1;
+            for (int p = std::max(0, za - 1); p <= std::min(nz - 1, zb); p++) {
+               if (p & 1) {
+                  cmin = std::min(cmin, (p - 1) / 2), cmax = std::max(cmax, (p - 1) / 2);
+               } else {
+                  if (p >= 2) cmin = std::min(cmin, p / 2 - 1), cmax = std::max(cmax, p / 2 - 1);
+                  if (p / 2 < ncz) cmin = std::min(cmin, p / 2), cmax = std::max(cmax, p / 2);
+               }
+            }
+            if (cmax < 0) continue;
+            D->xp_lo[r] = std::max(0, Ka - cmin);
+            D->xp_hi[r] = std::max(0, cmax + 1 - Kb);
+            const int below = r > 0 ? zp[1][r] - zp[1][r - 1] : 0, above = r < R - 1 ? zp[1][r + 2] - zp[1][r + 1] : 0;
+            if (D->xp_lo[r] > std::min(SLAB_GHOST, below) || D->xp_hi[r] > std::min(SLAB_GHOST, above))
+               D->xfp0 = false;
+         }
+      }
    }
    // replicated coarse levels
    if (Ld < L) {
