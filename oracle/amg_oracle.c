@@ -1790,7 +1790,12 @@ double or_dmem_async_jacobi(const or_csr *A, const double *b, double *x, int swe
  * finished grids) at fixed points: the end of every main-loop iteration, every
  * pass of CheckInFlight's wait, every iteration of AsyncRecvCleanup, every
  * failed test of the final waits.  The device's amg_grid_add_solve with
- * async_schedule = AMG_SCHED_ROUND_ROBIN yields at the same points. */
+ * async_schedule = AMG_SCHED_ROUND_ROBIN yields at the same points.
+ * sched 2 / 3 (converge LOCAL): the race's extreme speed ratios -- the token
+ * starts at the finest (2) / coarsest (3) grid and a grid keeps it through its
+ * main loop, handing it on (ascending / descending) only where a reference rank
+ * would block (CheckInFlight's wait, AsyncRecvCleanup, the final waits): each
+ * grid runs its cycles as if the others were stalled. */
 typedef struct or_rec {
    double *pay;          /* payload copy (send) */
    int n;
@@ -1903,7 +1908,7 @@ static void rr_pass(or_mbox *M, int g, int finished)
    if (finished) M->finished[g] = 1;
    int nx = -1;
    for (int q = 1; q <= M->G; q++) {
-      const int c = (g + q) % M->G;
+      const int c = M->sched == 3 ? ((g - q) % M->G + M->G) % M->G : (g + q) % M->G;
       if (!M->finished[c]) {
          nx = c;
          break;
@@ -1917,6 +1922,13 @@ static void rr_yield(or_mbox *M, int g)
    if (!M->sched) return;
    rr_pass(M, g, 0);
    rr_wait(M, g);
+}
+
+/* the end of a main-loop iteration: round robin hands the token on, the
+ * sequential schedules keep it */
+static void rr_yield_main(or_mbox *M, int g)
+{
+   if (M->sched == 1) rr_yield(M, g);
 }
 
 enum { OR_MSG_ACCUMULATE = 0, OR_MSG_WRITE = 1 };
@@ -2255,7 +2267,7 @@ static void grid_run(or_grid *g)
          if (g->outside_done_flag == 1) g->all_done_flag = 1;
       }
       g->cycle++;
-      rr_yield(M, g->k);
+      rr_yield_main(M, g->k);
       if (g->converge_flag == 1) break;
    }
    /* AsyncEnd: AsyncRecvCleanup (:827-890) */
@@ -2291,6 +2303,7 @@ int or_dmem_add(or_hier *H, const double *b, double *x_out, int sched, int conve
    const int L = H->L, n0 = H->n[0], G = L;
    if (G < 2 || max_inflight < 1) return -1;
    if (async_type == OR_SEMI_ASYNC && converge_type == OR_CONVERGE_GLOBAL) return -1; /* :346-358 */
+   if (sched < 0 || sched > 3 || (sched >= 2 && converge_type != OR_CONVERGE_LOCAL)) return -1;
    or_mbox M;
    memset(&M, 0, sizeof(M));
    M.G = G;
@@ -2298,6 +2311,7 @@ int or_dmem_add(or_hier *H, const double *b, double *x_out, int sched, int conve
    M.recvq = (or_rec **)calloc((size_t)G * G, sizeof(or_rec *));
    omp_init_lock(&M.lock);
    M.sched = sched;
+   M.token = sched == 3 ? G - 1 : 0;
    M.finished = (int *)calloc(G, sizeof(int));
    or_grid *gs = (or_grid *)calloc(G, sizeof(or_grid));
    const int cg = cheby_grid < L - 1 ? cheby_grid : L - 1; /* DMEM_Setup.cpp:1911-1913 */

@@ -395,7 +395,8 @@ class Hier:
                  accel=None):
         """DMEM_Add (DMEM_Add.cpp:20-944) on L threads, one rank per grid:
         (x per grid [L, n0], cycles[L], relres[L], messages[L, 2] (sent, received)).
-        sched 0: the free race (nondeterministic); 1: round robin."""
+        sched 0: the free race (nondeterministic); 1: round robin; 2 / 3 (converge LOCAL):
+        finest- / coarsest-first sequential (the race's extreme speed ratios)."""
         n0 = self._keep[0][0].nrows
         x = np.zeros(self.L * n0)
         cyc = np.zeros(self.L, dtype=np.int32)

@@ -87,11 +87,13 @@ def grid_solve(amg, L, host, f, ppg, transport="host", **kw):
 _bands = {}
 
 
-def dmem_band(oracle, host, f, opts, reps=10):
+def dmem_band(oracle, host, f, opts, reps=10, sequential=False):
     """the band of the DMEM_Add restatement (oracle or_dmem_add: grids as
     threads, one rank per grid, the same AddCycle / message protocol /
     termination): `reps` free races and the round-robin schedule; every grid's
-    final relative residual of every run"""
+    final relative residual of every run.  sequential (converge LOCAL): also
+    the finest- / coarsest-first sequential schedules, the race's extreme speed
+    ratios -- for runs whose grids are known to run at very uneven speeds"""
     o = oracle.make_opts(solver=oracle.OR_ASYNC_MULTADD, smooth_weight=opts.smooth_weight,
                          num_cycles=opts.num_cycles, tol=opts.tol)
     OH = oracle.Hier(host["A"], host["P"], host["R"], o)
@@ -99,7 +101,8 @@ def dmem_band(oracle, host, f, opts, reps=10):
               async_type=opts.async_type, max_inflight=opts.max_inflight,
               save_divisor=opts.async_comm_save_divisor, tol=opts.tol)
     rels = []
-    for sched in [0] * reps + [1]:
+    extra = [2, 3] if sequential and kw["converge_type"] == oracle.OR_CONVERGE_LOCAL else []
+    for sched in [0] * reps + [1] + extra:
         _, _, rel, _ = OH.dmem_add(f, sched=sched, **kw)
         rels += rel.tolist()
     return min(rels), max(rels), rels, None

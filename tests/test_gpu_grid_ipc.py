@@ -106,7 +106,11 @@ def test_grid_add_processes(amg, oracle, transport):
     # grids, AddCycle, messages and termination on threads; free races plus
     # its round robin)
     from test_gpu_grid import dmem_band
-    lo, hi, _, _ = dmem_band(oracle, host, f, _opts(amg))
+    # five processes sharing one GPU and a gloo control plane run their grids
+    # at very uneven speeds (round 3: 1.4-2.1e-4 against a free-race band
+    # maximum of 7.1e-6), so the band also holds the DMEM restatement's
+    # sequential schedules
+    lo, hi, _, _ = dmem_band(oracle, host, f, _opts(amg), sequential=True)
     print(f"grid add processes {transport} L={L}: oracle band [{lo:.4e}, {hi:.4e}], "
           f"ranks (finite, cycles, rel, sent, received) {[out[r][1:] for r in sorted(out)]}")
     for r in range(world):

@@ -387,3 +387,32 @@ def test_dmem_add_oracle(amg, oracle, conv, at, inflight, save):
         assert np.all(rel < ((1e-3 if save == 1 else 1e-2) if q < 2 else 1.0)), (q, rel)
     print(f"dmem_add {conv} async_type {at} inflight {inflight} save {save}: round robin relres {runs[0][2]}, "
           f"cycles {runs[0][1]}; free {[r[2].max() for r in runs[2:]]}")
+
+
+@pytest.mark.parametrize("sched", [2, 3])
+def test_dmem_add_sequential_schedules(amg, oracle, sched):
+    """or_dmem_add's sequential schedules (converge LOCAL): the finest / coarsest
+    grid keeps the token through its main loop and hands it on only where a
+    reference rank would block -- the race's extreme speed ratios, members of
+    the grid tests' band.  Deterministic (two runs, the same bits), every grid
+    runs num_cycles, every message sent is received; GLOBAL is refused."""
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, 16, amg.AMG_INTERP_LINEAR)
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs = oracle.smooth_transfer(host["A"][lev], host["P"][lev], 0.8)
+        Ps.append(ps)
+        Rs.append(rs)
+    N = 12
+    o = oracle.make_opts(solver=oracle.OR_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=N, tol=0.0)
+    OH = oracle.Hier(host["A"], Ps, Rs, o)
+    f = amg.rhs_rand(0, 16 ** 3)
+    runs = [OH.dmem_add(f, sched=sched, max_inflight=2) for _ in range(2)]
+    assert np.array_equal(runs[0][0].view(np.uint64), runs[1][0].view(np.uint64))
+    x, cyc, rel, msg = runs[0]
+    assert np.all(np.isfinite(x)) and np.all(cyc == N), cyc
+    assert msg[:, 0].sum() == msg[:, 1].sum(), msg
+    rr = OH.dmem_add(f, sched=1, max_inflight=2)
+    print(f"dmem_add sequential {sched}: relres {rel}; round robin {rr[2]}")
+    with pytest.raises(Exception):
+        OH.dmem_add(f, sched=sched, converge_type=oracle.OR_CONVERGE_GLOBAL)
