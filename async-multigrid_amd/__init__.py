@@ -118,6 +118,13 @@ class Context:
         """Prolongation fused into the first post-smoothing sweep of marched geometric levels (default off: VALU-bound, slower)."""
         check(lib.amg_set_fuse_prolong(self.h, int(enable)))
 
+    def set_march_tuning(self, mz_pf=None, mz27_pf=None, mz_occ=None, mz27_occ=None):
+        """Plane-march scheduling (bit-identical): prefetch distance (1 / 2) of the
+        7-pt / 27-pt march, occupancy-sized chunks (-1 the kernel's own, 0 off,
+        > 0 workgroups per CU); None keeps a value."""
+        k = lambda v: -2 if v is None else int(v)  # noqa: E731
+        check(lib.amg_set_march_tuning(self.h, k(mz_pf), k(mz27_pf), k(mz_occ), k(mz27_occ)))
+
     def set_march_lines(self, lines, gemv=None):
         """Lines per lane of the 7-pt plane march (1, 2 or 4; bit-identical);
         gemv: a different count for SpMV / SpGEMV (default: the same)."""

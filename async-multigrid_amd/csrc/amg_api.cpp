@@ -897,6 +897,21 @@ extern "C" int amg_set_march_lines_gemv(amg_ctx *c, int lines)
    return AMG_OK;
 }
 
+extern "C" int amg_set_march_tuning(amg_ctx *c, int mz_pf, int mz27_pf, int mz_occ, int mz27_occ)
+{
+   AMG_ARG(c, "amg_set_march_tuning: null context");
+   AMG_ARG(mz_pf == -2 || mz_pf == 1 || mz_pf == 2, "amg_set_march_tuning: 7-pt prefetch distance %d", mz_pf);
+   AMG_ARG(mz27_pf == -2 || mz27_pf == 1 || mz27_pf == 2, "amg_set_march_tuning: 27-pt prefetch distance %d",
+           mz27_pf);
+   AMG_ARG(mz_occ >= -2 && mz_occ <= 8 && mz27_occ >= -2 && mz27_occ <= 8,
+           "amg_set_march_tuning: occupancy %d / %d outside [-1, 8]", mz_occ, mz27_occ);
+   if (mz_pf != -2) c->mz_pf = mz_pf;
+   if (mz27_pf != -2) c->mz27_pf = mz27_pf;
+   if (mz_occ != -2) c->mz_occ = mz_occ;
+   if (mz27_occ != -2) c->mz27_occ = mz27_occ;
+   return AMG_OK;
+}
+
 extern "C" int amg_set_fuse_transfer(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_fuse_transfer: null context");
