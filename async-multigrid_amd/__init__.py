@@ -118,6 +118,10 @@ class Context:
         """Prolongation fused into the first post-smoothing sweep of marched geometric levels (default off: VALU-bound, slower)."""
         check(lib.amg_set_fuse_prolong(self.h, int(enable)))
 
+    def set_graphs(self, enable):
+        """hipGraphs of the additive cycles' launch-bound loops (bit-identical)."""
+        check(lib.amg_set_graphs(self.h, int(bool(enable))))
+
     def set_march_tuning(self, mz_pf=None, mz27_pf=None, mz_occ=None, mz27_occ=None):
         """Plane-march scheduling (bit-identical): prefetch distance (1 / 2) of the
         7-pt / 27-pt march, occupancy-sized chunks (-1 the kernel's own, 0 off,

@@ -144,6 +144,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_PLANE_MARCH_XCD")) c->mz_xcd = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_XFER")) c->fuse_xfer = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_GRAPHS")) c->graphs = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::max(0, std::min(3, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_SMALL")) c->jgs_small = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_WAVE")) c->jgs_wave = std::max(0, std::min(2, std::atoi(v)));
@@ -894,6 +895,13 @@ extern "C" int amg_set_march_lines_gemv(amg_ctx *c, int lines)
 {
    AMG_ARG(c && (lines == 1 || lines == 2 || lines == 4), "amg_set_march_lines_gemv: lines must be 1, 2 or 4");
    c->mz_lines_gemv = lines;
+   return AMG_OK;
+}
+
+extern "C" int amg_set_graphs(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_graphs: null context");
+   c->graphs = enable != 0;
    return AMG_OK;
 }
 

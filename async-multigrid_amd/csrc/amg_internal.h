@@ -107,6 +107,7 @@ struct amg_ctx {
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies
    int bsr3 = 1;           // 3x3 block form of num_functions = 3 operators
+   int graphs = 0;         // hipGraphs of the additive cycles' launch-bound loops (AMG_GRAPHS)
    int fuse_xfer = 1;      // composed smoothed transfers of marched 7-pt levels in one pass each
    int fuse_prolong = 0;   // prolongation fused into the first post sweep (measured slower: off)
    int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)

@@ -86,6 +86,15 @@ struct amg_hier {
    // runs as one fused pass (mz_xfer_restrict / mz_xfer_prolong: geometric
    // R_l / P_l, marched 7-pt A_l; the restriction needs uniform values)
    std::vector<char> xfr, xfp;
+   // hipGraphs of launch-bound loops (ctx->graphs): the synchronous additive
+   // cycle (g_add, on ctx->stream) and each asynchronous level's correction
+   // (g_lev[k] on stream g_lev_s[k]); captured after one eager run (lazy
+   // allocations), dropped when the options or blocks change
+   hipGraphExec_t g_add = nullptr;
+   bool g_add_warm = false;
+   std::vector<hipGraphExec_t> g_lev;
+   std::vector<hipStream_t> g_lev_s;
+   std::vector<char> g_lev_warm;
    // delay / fault injection: one generator per reference thread (srand(tid),
    // SMEM_Solve.cpp:113), reset by every solve
    std::vector<unsigned long long> delay_rng;
@@ -214,6 +223,8 @@ static int default_blocks(amg_hier *H, Level &l)
    return upload_blocks(H, l);
 }
 
+static void graphs_reset(amg_hier *H);
+
 extern "C" int amg_hier_set_blocks(amg_hier *H, int level, const int *blk, int nblk)
 {
    AMG_ARG(H && blk && level >= 0 && level < H->L && nblk > 0, "amg_hier_set_blocks: bad argument");
@@ -221,6 +232,7 @@ extern "C" int amg_hier_set_blocks(amg_hier *H, int level, const int *blk, int n
    AMG_ARG(blk[0] == 0 && blk[nblk] == l.n, "amg_hier_set_blocks: blocks must cover [0,%d)", l.n);
    for (int b = 0; b < nblk; b++) AMG_ARG(blk[b] <= blk[b + 1], "amg_hier_set_blocks: unsorted");
    l.blk.assign(blk, blk + nblk + 1);
+   graphs_reset(H);
    return upload_blocks(H, l);
 }
 
@@ -417,6 +429,54 @@ extern "C" int amg_hier_create(amg_ctx *c, int L, amg_mat *const *A, amg_mat *co
    return AMG_OK;
 }
 
+static void graphs_reset(amg_hier *H)
+{
+   if (H->g_add) hipGraphExecDestroy(H->g_add);
+   H->g_add = nullptr;
+   H->g_add_warm = false;
+   for (auto &g : H->g_lev)
+      if (g) hipGraphExecDestroy(g);
+   H->g_lev.assign(H->L, nullptr);
+   H->g_lev_s.assign(H->L, nullptr);
+   H->g_lev_warm.assign(H->L, 0);
+}
+
+// issue `body` on stream s through a cached graph: the first call runs it
+// eagerly (allocations, scratch growth), the second captures and instantiates,
+// every call from then on launches the graph
+template <class F>
+static int graph_issue(hipGraphExec_t &gx, bool &warm, hipStream_t s, F body)
+{
+   if (!warm) {
+      warm = true;
+      AMG_TRY(body());
+      AMG_HIP(hipGetLastError());
+      return AMG_OK;
+   }
+   if (!gx) {
+      AMG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      const int st = body();
+      hipGraph_t g = nullptr;
+      const hipError_t e = hipStreamEndCapture(s, &g);
+      if (st != AMG_OK) {
+         if (g) hipGraphDestroy(g);
+         return st;
+      }
+      if (e != hipSuccess) {
+         if (g) hipGraphDestroy(g);
+         return amg_set_error(AMG_ERR_HIP, "graph capture: %s", hipGetErrorString(e));
+      }
+      const hipError_t ei = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
+      hipGraphDestroy(g);
+      if (ei != hipSuccess) {
+         gx = nullptr;
+         return amg_set_error(AMG_ERR_HIP, "graph instantiate: %s", hipGetErrorString(ei));
+      }
+   }
+   AMG_HIP(hipGraphLaunch(gx, s));
+   return AMG_OK;
+}
+
 extern "C" int amg_hier_free(amg_hier *H)
 {
    if (!H) return AMG_OK;
@@ -424,6 +484,7 @@ extern "C" int amg_hier_free(amg_hier *H)
    hipStreamSynchronize(H->ctx->stream);
    for (auto s : H->ctx->level_streams) hipStreamSynchronize(s);
    prof_drain(H);
+   graphs_reset(H);
    for (auto &a : H->al) {
       if (a.ev_a) hipEventDestroy(a.ev_a);
       if (a.ev_b) hipEventDestroy(a.ev_b);
@@ -442,6 +503,7 @@ extern "C" int amg_hier_set_opts(amg_hier *H, const amg_opts *opts)
    const bool w = opts->smooth_weight != H->o.smooth_weight;
    const bool t = opts->num_threads != H->o.num_threads || opts->jgs_block_rows != H->o.jgs_block_rows;
    H->o = *opts;
+   graphs_reset(H);
    if (w) AMG_TRY(hier_prepare_smoother_arrays(H));
    if (t)
       for (auto &l : H->lv) AMG_TRY(default_blocks(H, l));
@@ -966,6 +1028,11 @@ static int solve_step(amg_hier *H)
       bpx_cycle(H, precond); // SMEM_Solve.cpp:161-163
    else if (one_level)
       vcycle(H, precond, reuse);
+   else if (c->graphs && !H->o.profile)
+      AMG_TRY(graph_issue(H->g_add, H->g_add_warm, c->stream, [&] {
+         sync_add_vcycle(H);
+         return (int)AMG_OK;
+      }));
    else
       sync_add_vcycle(H);
    if (o.cheby_flag == 1) {
@@ -1366,12 +1433,32 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       AMG_HIP(hipGetLastError());
       return AMG_OK;
    };
+   // graphs of the level corrections (ctx->graphs): the FULL_ASYNC / READ_SOL /
+   // LOCAL-residual correction issues the same kernels with the same
+   // arguments every time (no delays, no profiling events), so each level's
+   // is captured once per stream and replayed
+   const bool graphs = c->graphs && !semi && !read_res && !global_res && !H->o.profile &&
+                       (o.delay_type == AMG_DELAY_NONE || o.delay_usec <= 0);
+   if (graphs && (int)H->g_lev.size() != L) graphs_reset(H);
+   auto run = [&](int k) -> int {
+      if (!graphs) return correction(k);
+      hipStream_t s = lstream(k);
+      if (H->g_lev_s[k] != s) {
+         if (H->g_lev[k]) hipGraphExecDestroy(H->g_lev[k]);
+         H->g_lev[k] = nullptr;
+         H->g_lev_s[k] = s;
+      }
+      bool warm = H->g_lev_warm[k] != 0;
+      const int st = graph_issue(H->g_lev[k], warm, s, [&] { return correction(k); });
+      H->g_lev_warm[k] = warm ? 1 : 0;
+      return st;
+   };
    if (sched == AMG_SCHED_FINEST_FIRST || sched == AMG_SCHED_COARSEST_FIRST) {
       // the level groups one after another (or_set_async_schedule 1 / 2)
       for (int q = 0; q < ngrp; q++) {
          const int k = sched == AMG_SCHED_FINEST_FIRST ? k_lo + q : k_hi - 1 - q;
          for (int cyc = 0; cyc < o.num_cycles; cyc++) {
-            AMG_TRY(correction(k));
+            AMG_TRY(run(k));
             issued[k]++;
          }
       }
@@ -1386,7 +1473,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       for (int left = ngrp; left > 0;)
          for (int k = k_lo; k < k_hi; k++) {
             if (stopped[k]) continue;
-            AMG_TRY(correction(k));
+            AMG_TRY(run(k));
             issued[k]++;
             if (k == k_lo && !flag) {
                bool all = true;
@@ -1407,7 +1494,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       // cycle-major, level-minor issue order is the turn order)
       for (int cyc = 0; cyc < o.num_cycles; cyc++)
          for (int k = k_lo; k < k_hi; k++) {
-            AMG_TRY(correction(k));
+            AMG_TRY(run(k));
             issued[k]++;
          }
    } else {
@@ -1440,7 +1527,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          bool progressed = false;
          for (int k = k_lo; k < k_hi && st == AMG_OK; k++) {
             if (issued[k] - completed[k] < DEPTH && issued[k] < cap) {
-               if ((st = correction(k)) != AMG_OK) break;
+               if ((st = run(k)) != AMG_OK) break;
                const hipError_t er = hipEventRecord(done[k][issued[k] % DEPTH], c->level_streams[k]);
                if (er != hipSuccess) {
                   st = amg_set_error(AMG_ERR_HIP, "amg_async_solve: hipEventRecord: %s", hipGetErrorString(er));

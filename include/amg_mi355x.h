@@ -404,6 +404,13 @@ int amg_set_march_lines_gemv(amg_ctx *ctx, int lines);
  * -1, automatic chunking only).  Bit-identical in every setting; -2 keeps a
  * value. */
 int amg_set_march_tuning(amg_ctx *ctx, int mz_pf, int mz27_pf, int mz_occ, int mz27_occ);
+/* hipGraphs of the additive cycles' launch-bound loops (MI355X, no reference
+ * counterpart; env AMG_GRAPHS): the synchronous additive cycle of amg_solve and
+ * each level's correction of amg_async_solve (FULL_ASYNC, READ_SOL, LOCAL
+ * residuals, no delays, no profiling) are captured after one eager run and
+ * replayed; the same kernels with the same arguments, bit-identical.  Off by
+ * default; the graphs are dropped when the hierarchy's options or blocks change. */
+int amg_set_graphs(amg_ctx *ctx, int enable);
 int amg_hier_set_opts(amg_hier *H, const amg_opts *opts);
 /* override level `level`'s hybrid-JGS block partition (thread.A_ns/A_ne) */
 int amg_hier_set_blocks(amg_hier *H, int level, const int *blk, int nblk);
