@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--transfers", default="explicit", choices=("explicit", "composed"),
                     help="smoothed transfers as explicit products (host SpGEMM) or composed on the device "
                          "(smooth_transfer = 1: R~ r = R (r - w A D^-1 r))")
+    ap.add_argument("--graphs", type=int, default=0,
+                    help="hipGraph replay of the level corrections / the sync cycle (amg_set_graphs)")
     a = ap.parse_args()
     amg = load_package()
     from oracle import pyoracle as po
@@ -56,6 +58,7 @@ def main():
             Rs.append(r)
     print(f"[async] {L}-level smoothed hierarchy built in {time.time() - t0:.1f}s", file=sys.stderr)
     ctx = amg.Context(0, nstreams=16)
+    ctx.set_graphs(a.graphs)
     dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v]
            for k, v in (("A", A), ("P", Ps), ("R", Rs))}
     sm = amg.AMG_HYBRID_JGS if a.smoother == "hybrid" else amg.AMG_JACOBI
@@ -63,7 +66,8 @@ def main():
     fv = ctx.vec(f)
     out = {"config": {"workload": f"{n}^3 7-pt Laplacian, ASYNC_MULTADD {a.smoother} "
                                   f"(blocks of {a.block} rows), FULL_ASYNC, LOCAL residual / convergence, "
-                                  f"{a.cycles} corrections per level, smoothed linear transfers ({a.transfers})",
+                                  f"{a.cycles} corrections per level, smoothed linear transfers ({a.transfers})"
+                                  f"{', hipGraph replay' if a.graphs else ''}",
                       "levels": L, "n": n}}
     for tag, solver in (("async", amg.AMG_ASYNC_MULTADD), ("sync", amg.AMG_MULTADD)):
         opts = amg.default_opts(solver=solver, smoother=sm, smooth_weight=w, num_cycles=a.cycles, tol=0.0,

@@ -16,6 +16,7 @@ step() { # name timeout cmd...
 }
 step bench 420 python -u bench.py
 step async3_composed 240 python -u tools/bench_async.py --transfers composed
+step async3_composed_graphs 240 python -u tools/bench_async.py --transfers composed --graphs 1
 step async_dist1 300 python -u tools/bench_dist_async.py --ranks 1 --cycles 8
 step async_dist8 420 python -u tools/bench_dist_async.py --ranks 8 --cycles 8
 step async3_explicit 300 python -u tools/bench_async.py --transfers explicit
