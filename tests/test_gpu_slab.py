@@ -170,60 +170,6 @@ def test_slab_refuses_row_partitioned_solvers(amg):
     gen.free()
 
 
-def _async_run(amg, gen, opts, f, nranks, slab, rep=1 << 12):
-    hub = amg.dist.ThreadMailbox(nranks, timeout=600.0)
-
-    def rank(r):
-        c = amg.Context(0, nstreams=gen.L + 2)
-        tr = None
-        if nranks == 1:
-            amg.dist.init_rccl(c, 1, 0, lambda b: b)
-        else:
-            tr = amg.dist.HostTransport(hub, r)
-            amg.dist.init_host(c, nranks, r, tr)
-        amg.dist.set_replicate_rows(c, rep)
-        D = amg.dist.DistHier(c, gen, opts, slab=slab)
-        rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-        u = D.get_u()
-        D.free()
-        amg.dist.finalize(c)
-        c.close()
-        if tr is not None and tr.error is not None:
-            raise tr.error
-        return rel, cnt, u
-
-    out = run_ranks(nranks, rank)
-    assert all(o[0] == out[0][0] for o in out)  # one allreduced norm
-    assert all(np.all(np.isfinite(o[2])) for o in out)
-    return out[0][0], out[0][1]
-
-
-def test_slab_async_additive_band(amg, ctx):
-    """amg_dist_async_solve (ASYNC_AFACX) on slab hierarchies, 1 rank over RCCL
-    and 2 / 3 ranks over the host transport, against the row-partitioned
-    hierarchies of the same problem: every level does num_cycles corrections
-    and the (nondeterministic) relative residuals agree within [0.5x, 2x].
-    The generator's transfers are the plain geometric ones, with which the
-    additive cycle does not contract (the reference runs MULTADD / AFACx on
-    smoothed transfers, SMEM_Setup.cpp:244-261 -- test_gpu_dist.py's async
-    tests use those): this test pins the slab form to the row form, not the
-    method's convergence."""
-    gen = amg.Gen(64)
-    f = amg.rhs_rand(0, 64 ** 3)
-    N = 10
-    opts = amg.default_opts(solver=amg.AMG_ASYNC_AFACX, num_cycles=N, tol=0.0, smooth_weight=0.8)
-    rels = {}
-    for nranks, slab in ((1, True), (2, True), (3, True), (1, False), (2, False)):
-        rel, cnt = _async_run(amg, gen, opts, f, nranks, slab)
-        assert list(cnt[:gen.L - 1]) == [N] * (gen.L - 1)
-        rels[(nranks, slab)] = rel
-    print("async AFACx relres", rels)
-    ref = rels[(1, False)]
-    for k, v in rels.items():
-        assert np.isfinite(v) and 0.5 * ref <= v <= 2.0 * ref, (k, rels)
-    gen.free()
-
-
 @pytest.mark.slow
 def test_slab_512(amg, ctx):
     """Config 4's problem at size: the 512^3 slab hierarchy over RCCL at one rank
@@ -264,22 +210,7 @@ def test_slab_512_eight_ranks(amg, ctx):
     gen.free()
 
 
-@pytest.mark.slow
-def test_slab_512_async(amg, ctx):
-    """amg_dist_async_solve at 512^3 on the slab hierarchy (one rank over RCCL,
-    two over the host transport): every level does its corrections, the
-    iterate stays finite and the two runs' relative residuals agree within
-    [0.5x, 2x] (plain geometric transfers: see test_slab_async_additive_band)."""
-    n = 512
-    gen = amg.Gen(n)
-    f = amg.rhs_rand(0, n ** 3)
-    N = 6
-    opts = amg.default_opts(solver=amg.AMG_ASYNC_AFACX, num_cycles=N, tol=0.0, smooth_weight=0.8)
-    rels = []
-    for nranks in (1, 2):
-        rel, cnt = _async_run(amg, gen, opts, f, nranks, True, rep=1 << 18)
-        assert list(cnt[:gen.L - 1]) == [N] * (gen.L - 1)
-        rels.append(rel)
-    print("512^3 async AFACx relres", rels)
-    assert all(np.isfinite(rels)) and max(rels) <= 2.0 * min(rels), rels
-    gen.free()
+# The asynchronous additive solve on slabs (schedules bitwise against the
+# oracle, the race in the oracle's band, 512^3 converging at 1 / 2 / 8 ranks)
+# is tests/test_gpu_slab_async.py; round 3's AFACx-on-plain-transfers checks
+# (a diverging method compared only with itself) are gone.
