@@ -313,47 +313,3 @@ def test_composed_transfers_geometric_bitwise(amg, oracle, ctx, mode):
     print(f"composed geometric {mode}: differing entries {nd}")
     assert nd == 0
 
-
-@pytest.mark.parametrize("mode", ["async-jacobi-s3", "async-hybrid-s1", "sync"])
-def test_graphs_bitwise(amg, oracle, ctx, mode):
-    """hipGraph replay of the additive cycles (amg_set_graphs): every level's
-    correction captured after its first eager run and replayed (async), the
-    whole synchronous additive cycle likewise -- the iterate is the oracle's
-    bit for bit, over two solves (the second replays graphs made by the first)"""
-    n = 64
-    _, L, host = hierarchy(amg, oracle, n, amg.AMG_INTERP_LINEAR)
-    f = amg.rhs_rand(0, n ** 3)
-    sm = amg.AMG_HYBRID_JGS if "hybrid" in mode else amg.AMG_JACOBI
-    sched = int(mode[-1]) if mode != "sync" else 0
-    opts = amg.default_opts(solver=amg.AMG_MULTADD if mode == "sync" else amg.AMG_ASYNC_MULTADD, smoother=sm,
-                            smooth_weight=W, num_cycles=6, tol=0.0, num_threads=0, jgs_block_rows=64,
-                            async_schedule=sched, smooth_transfer=1)
-    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
-    OH.set_composed_transfers()
-    if sm == amg.AMG_HYBRID_JGS:
-        for lev, blk in blocks64(host).items():
-            OH.set_blocks(lev, blk)
-    if mode == "sync":
-        uo, ho, _ = OH.solve(f)
-    else:
-        oracle.lib().or_set_async_schedule(sched)
-        try:
-            uo, relo, _ = OH.async_add(f, [1] * L)
-        finally:
-            oracle.lib().or_set_async_schedule(0)
-    ctx.set_graphs(1)
-    try:
-        H, _ = gpu_hier(amg, ctx, host, opts)
-        for rep in range(2):
-            if mode == "sync":
-                u, hist, k = H.solve(f)
-                np.testing.assert_allclose(hist, ho, rtol=1e-12, atol=0)
-            else:
-                u, rel, cnt = H.async_solve(f)
-                assert abs(rel - relo) <= 1e-12 * relo
-            nd = int(np.count_nonzero(u.view(np.uint64) != uo.view(np.uint64)))
-            print(f"graphs {mode} solve {rep}: differing entries {nd}")
-            assert nd == 0
-        H.free()
-    finally:
-        ctx.set_graphs(0)

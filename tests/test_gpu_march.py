@@ -456,74 +456,3 @@ def test_fused_prolong_sweep(ctx, amg, oracle, dims, zc, sm, post, form):
     assert_bitwise(h1[:k1 + 1], h0[:k0 + 1], "norm history")
     np.testing.assert_allclose(h1[:k1 + 1], hist_cpu[:k1 + 1], rtol=1e-12)
 
-
-@pytest.mark.parametrize("tune", [(2, 2, -1, -1), (1, 1, 0, 0), (2, 1, 3, 5)],
-                         ids=["pf2-occ", "pf1-off", "mixed"])
-@pytest.mark.parametrize("name", ["lap64x8x5", "lap512x8x4", "neu32x16x7"])
-def test_march_tuning_bitwise(ctx, amg, boxes, name, tune):
-    """the 7-pt march's scheduling knobs (prefetch distance, occupancy-sized
-    chunks; amg_set_march_tuning) change only who computes which plane: SpGEMV
-    and Jacobi outputs bit-identical to plain CSR"""
-    A = boxes[name]
-    ctx.set_plane_march(1, -1, 1)
-    ctx.set_march_tuning(*tune)
-    try:
-        mz = register(ctx, A)
-        pl = register(ctx, A, plain=True)
-        n = A.nrows
-        x = ctx.vec(_vecs(n, 61))
-        b = ctx.vec(_vecs(n, 62))
-        for lines in (1, 2):
-            ctx.set_march_lines(lines)
-            for ab in ((1.0, 0.0), (-1.0, 1.0)):
-                ys = []
-                for M in (pl, mz):
-                    y = ctx.vec(n)
-                    amg.smem.SMEM_SpGEMV(ctx, M, x, b, ab[0], ab[1], y, 0, n)
-                    ys.append(y.download())
-                assert_bitwise(ys[1], ys[0], f"{name} {tune} lines {lines} spgemv {ab}")
-            us = []
-            for M in (pl, mz):
-                u = ctx.vec(_vecs(n, 63))
-                amg.smem.SMEM_Sync_Parfor_Jacobi(ctx, M, b, u, ctx.vec(n), 3, 0, 0.7)
-                us.append(u.download())
-            assert_bitwise(us[1], us[0], f"{name} {tune} lines {lines} jacobi")
-        mz.free()
-        pl.free()
-    finally:
-        ctx.set_march_tuning(1, 2, 0, -1)
-        ctx.set_march_lines(1, gemv=2)
-
-
-@pytest.mark.parametrize("tune", [(1, 1, 0, 0), (1, 2, 0, 3), (1, 2, 0, -1)], ids=["pf1-off", "pf2-occ3", "pf2-auto"])
-@pytest.mark.parametrize("name", ["galerkin32", "uni64x8x4"])
-def test_march27_tuning_bitwise(ctx, amg, oracle, boxes27, name, tune):
-    """the 27-pt march's prefetch distance and occupancy-sized chunks: SpGEMV
-    and Jacobi bit-identical to plain CSR"""
-    A = boxes27[name]
-    ctx.set_plane_march(1, -1, 1)
-    ctx.set_march_tuning(*tune)
-    try:
-        mz = register(ctx, A)
-        pl = register(ctx, A, plain=True)
-        assert mz.march_points == 27
-        n = A.nrows
-        x = ctx.vec(_vecs(n, 71))
-        b = ctx.vec(_vecs(n, 72))
-        for ab in ((1.0, 0.0), (-1.0, 1.0), (2.5, -0.5)):
-            ys = []
-            for M in (pl, mz):
-                y = ctx.vec(n)
-                amg.smem.SMEM_SpGEMV(ctx, M, x, b, ab[0], ab[1], y, 0, n)
-                ys.append(y.download())
-            assert_bitwise(ys[1], ys[0], f"{name} {tune} spgemv {ab}")
-        us = []
-        for M in (pl, mz):
-            u = ctx.vec(_vecs(n, 73))
-            amg.smem.SMEM_Sync_Parfor_Jacobi(ctx, M, b, u, ctx.vec(n), 3, 0, 0.7)
-            us.append(u.download())
-        assert_bitwise(us[1], us[0], f"{name} {tune} jacobi")
-        mz.free()
-        pl.free()
-    finally:
-        ctx.set_march_tuning(1, 2, 0, -1)
