@@ -145,6 +145,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_XFER")) c->fuse_xfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_GRAPHS")) c->graphs = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_FUSE_XFP_SLAB")) c->fuse_xfp_slab = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::max(0, std::min(3, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_SMALL")) c->jgs_small = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_WAVE")) c->jgs_wave = std::max(0, std::min(2, std::atoi(v)));

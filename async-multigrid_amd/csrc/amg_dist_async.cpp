@@ -187,7 +187,7 @@ bool fused_xfer0(const amg_dist_hier *D)
 // the fused kernels and whose level-1 ghost needs fit (xfp0)
 bool fused_xfp0(const amg_dist_hier *D)
 {
-   return composed(D) && D->slab && D->xfp0 && D->ctx->fuse_xfer && D->lv[0].A.A;
+   return composed(D) && D->slab && D->xfp0 && D->ctx->fuse_xfer && D->ctx->fuse_xfp_slab && D->lv[0].A.A;
 }
 
 // every rank's restricted rows (slot) into the replicated level's full vector

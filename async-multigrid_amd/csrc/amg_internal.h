@@ -109,6 +109,7 @@ struct amg_ctx {
    int bsr3 = 1;           // 3x3 block form of num_functions = 3 operators
    int graphs = 0;         // hipGraphs of the additive cycles' launch-bound loops (AMG_GRAPHS)
    int fuse_xfer = 1;      // composed smoothed transfers of marched 7-pt levels in one pass each
+   int fuse_xfp_slab = 0;  // ... and the slab async solve's fused prolongation + atomic (AMG_FUSE_XFP_SLAB)
    int fuse_prolong = 0;   // prolongation fused into the first post sweep (measured slower: off)
    int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)
    int mz_lines = 1;       // 7-pt plane march: lines per lane (1, 2 or 4, AMG_MZ_LINES)

@@ -130,3 +130,14 @@ def test_graphs_bitwise(amg, oracle, ctx, mode):
         H.free()
     finally:
         ctx.set_graphs(0)
+
+
+@pytest.mark.parametrize("nranks,sched", [(2, 3), (1, 1)])
+def test_slab_fused_prolong_bitwise(amg, oracle, ctx, monkeypatch, nranks, sched):
+    """the slab async solve's level-0 composed prolongation and atomic
+    correction as one fused march (AMG_FUSE_XFP_SLAB=1; level-1 ghost planes
+    over the level channels): under a deterministic schedule the 64^3
+    iterate is the oracle's bit for bit"""
+    from test_gpu_slab_async import test_slab_async_schedule_bitwise
+    monkeypatch.setenv("AMG_FUSE_XFP_SLAB", "1")
+    test_slab_async_schedule_bitwise(amg, oracle, ctx, "multadd", True, nranks, sched, 64)
