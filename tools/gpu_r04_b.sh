@@ -19,6 +19,7 @@ step async3_composed 240 python -u tools/bench_async.py --transfers composed
 step async3_composed_graphs 240 python -u tools/bench_async.py --transfers composed --graphs 1
 step async_dist1 300 python -u tools/bench_dist_async.py --ranks 1 --cycles 8
 step async_dist8 420 python -u tools/bench_dist_async.py --ranks 8 --cycles 8
+step async_dist8_xfp 420 env AMG_FUSE_XFP_SLAB=1 python -u tools/bench_dist_async.py --ranks 8 --cycles 8
 step async3_explicit 300 python -u tools/bench_async.py --transfers explicit
 step bench_mzpf2 300 env AMG_MZ_PF=2 python -u bench.py --cpu-baseline 0
 step bench_again 300 python -u bench.py --cpu-baseline 0
