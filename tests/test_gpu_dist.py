@@ -328,10 +328,74 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
     assert list(res[0][2][:L - 1]) == [N] * (L - 1)
     assert rels[0] < 1.0
     from async_band import in_band, oracle_async_band
-    lo, hi, orels, _ = oracle_async_band(amg, oracle, host, f, opts)
-    print(f"dist async {solver} {nranks} ranks: oracle band [{lo:.4e}, {hi:.4e}] ({len(orels)} runs), "
+    # the free runs of the oracle's race plus its extreme speed ratios (the
+    # level groups one after another, finest / coarsest first): the device's
+    # level streams run the coarse groups far ahead of the fine one, a ratio
+    # no OpenMP run on the host reaches (the arithmetic itself is pinned by
+    # test_dist_async_schedule_bitwise)
+    lo, hi, orels, _ = oracle_async_band(amg, oracle, host, f, opts, sequential=True)
+    print(f"dist async {solver} {nranks} ranks: oracle band [{lo:.4e}, {hi:.4e}] ({len(orels)} runs, "
+          f"sequential finest / coarsest first {orels[-3]:.4e} / {orels[-2]:.4e}), "
           f"sync {sync_rel:.4e}, device {rels[0]:.4e}")
     assert in_band(rels[0], lo, hi), (rels[0], lo, hi, sync_rel)
+
+
+@pytest.mark.parametrize("solver,cuts,rep,sched", [("multadd", (0.5,), 0, 3), ("multadd", (0.3, 0.7), 1000, 1),
+                                                   ("afacx", (0.45,), 0, 2), ("multadd", (), 0, 2),
+                                                   ("afacx", (0.5,), 1000, 3)])
+def test_dist_async_schedule_bitwise(amg, oracle, ctx, solver, cuts, rep, sched):
+    """The row-partitioned asynchronous additive solve (from_parts, explicit
+    smoothed transfers) under a deterministic schedule (async_schedule 1 / 2 /
+    3: finest first, coarsest first, round robin) against the oracle's
+    or_async_add under the same schedule, one thread per level group: the
+    assembled iterate is the same bits at 1-3 ranks."""
+    from test_gpu_solve import hierarchy, oracle_opts
+    _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
+    w, N = 0.8, 10
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs_ = oracle.smooth_transfer(host["A"][lev], host["P"][lev], w)
+        Ps.append(ps)
+        Rs.append(rs_)
+    host = {"A": host["A"], "P": Ps, "R": Rs}
+    f = amg.rhs_rand(0, 24 ** 3)
+    a_solver = amg.AMG_ASYNC_MULTADD if solver == "multadd" else amg.AMG_ASYNC_AFACX
+    opts = amg.default_opts(solver=a_solver, smooth_weight=w, num_cycles=N, tol=0.0, async_schedule=sched)
+    rs, parts = split_host(host, cuts)
+    nranks = len(cuts) + 1
+    hub = amg.dist.ThreadMailbox(nranks)
+
+    def rank(r):
+        c = amg.Context(0, nstreams=L)
+        if nranks == 1:
+            amg.dist.init_rccl(c, 1, 0, lambda b: b)
+        else:
+            amg.dist.init_host(c, nranks, r, amg.dist.HostTransport(hub, r))
+        amg.dist.set_replicate_rows(c, rep)
+        A, P, R = parts[r]
+        D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
+        rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
+        out = (D.row0, rel, cnt.copy(), D.get_u())
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        return out
+
+    res = sorted(run_ranks(nranks, rank), key=lambda t: t[0])
+    u = np.concatenate([t[3] for t in res])
+    rel, cnt = res[0][1], res[0][2]
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    oracle.lib().or_set_async_schedule(sched)
+    try:
+        uo, relo, cnto = OH.async_add(f, [1] * L)
+    finally:
+        oracle.lib().or_set_async_schedule(0)
+    nd = int(np.count_nonzero(u.view(np.uint64) != uo.view(np.uint64)))
+    print(f"dist async {solver} {nranks} ranks schedule {sched}: device {rel:.13e} oracle {relo:.13e}, "
+          f"differing entries {nd}")
+    assert list(cnt[:L - 1]) == list(cnto[:L - 1]) == [N] * (L - 1)
+    assert_bitwise(u, uo, "row-partitioned async iterate vs oracle")
+    assert abs(rel - relo) <= 1e-12 * relo
 
 
 @pytest.mark.parametrize("nranks,l1", [(1, 0), (2, 0), (3, 1)])
