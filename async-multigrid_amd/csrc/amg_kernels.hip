@@ -1818,6 +1818,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
    }
 }
 
+// coarse planes per chunk: ctx->rr_zc (AMG_RR_ZC), else half the march chunk;
+// a chunk re-reads fine planes 2 Kc0 - 1 and 2 Kc1 + 1 of its neighbours
+static int rr_chunk(const amg_mat *A)
+{
+   const int z = A->ctx->rr_zc > 0 ? A->ctx->rr_zc : A->ctx->mz_zc / 2;
+   return std::max(1, std::min(z, 32));
+}
+
 void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, const double *u, const GeoT &g,
                           const double *wdev, double *fc, int Kb, int Ke, int fz0, int cz0, ZeroGuess zg)
 {
@@ -1829,7 +1837,7 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
    const int lpl = g.nx / 2, groups = 256 / lpl;
    const int LC = ((g.ny / 2) % (2 * groups) == 0 && A->ctx->rr_lines == 2) ? 2 : 1;
    const int nlb = (g.ny / 2) / (groups * LC);
-   const int zcc = std::max(1, std::min(A->ctx->mz_zc / 2, 32));
+   const int zcc = rr_chunk(A);
    const int nch = (Ke - Kb + zcc - 1) / zcc;
    const int nb = nlb * nch;
    const int xcd = A->ctx->mz_xcd;
@@ -1862,7 +1870,7 @@ void mz_xfer_restrict(hipStream_t s, const amg_mat *A, const double *r, const Ge
    const int lpl = g.nx / 2, groups = 256 / lpl;
    const int LC = ((g.ny / 2) % (2 * groups) == 0 && A->ctx->rr_lines == 2) ? 2 : 1;
    const int nlb = (g.ny / 2) / (groups * LC);
-   const int zcc = std::max(1, std::min(A->ctx->mz_zc / 2, 32));
+   const int zcc = rr_chunk(A);
    const int nb = nlb * ((Ke - Kb + zcc - 1) / zcc);
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
    if (LC == 2)
