@@ -2513,6 +2513,222 @@ __global__ __launch_bounds__(256) void mz_prolong_sweep_nl_kernel(
    }
 }
 
+// The fused sweep with the coarse correction read from LDS (fuse_prolong 4 /
+// 5: NL = 2 / 4 lines per workgroup): the workgroup's coarse lines of the
+// coarse planes in use sit in a 4-slot LDS ring (coarse lines y0 / 2 - 1 ..
+// y0 / 2 + NL / 2 of the 512-point segment plus one coarse point either side),
+// so every corrected operand -- the own lines' plane k + 2, the halo lines
+// y0 - 1 / y0 + NL of plane k, the wave-edge points -- is u plus LDS terms, no
+// coarse gathers from memory and no coarse values held in registers.  A
+// coarse plane enters the ring every second fine plane (one workgroup barrier
+// per two planes).  Terms and order as geo_prolong_march_k / geo_prolong_pair:
+// bit-identical to geo_prolong + csr_mz_kernel.
+template <bool UNI, bool L1, int NL>
+__global__ __launch_bounds__(256) void mz_prolong_sweep_lds_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
+   const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ u, const double *__restrict__ e,
+   const double *__restrict__ f, const double *__restrict__ l1, const double *__restrict__ wg, double omega,
+   int nx, int ny, int nz, int zc, int npb, int xcd, double *__restrict__ uout)
+{
+   constexpr int NCL = NL / 2 + 2; // coarse lines per ring slot
+   constexpr int CW = 258;         // coarse points per line: t0 - 1 .. t0 + 256
+   constexpr int NLD = (NCL * CW + 255) / 256;
+   __shared__ unsigned long long mtab[256];
+   __shared__ v2d mval[UNI ? 1 : 256 * 7];
+   __shared__ double wl[27];
+   __shared__ double ring[4][NCL][CW];
+   const int tid = (int)threadIdx.x, lane = tid & 63;
+   if (tid < np) mtab[tid] = mmask_g[tid];
+   if (tid < 27) wl[tid] = wg[tid];
+   if (!UNI)
+      for (int w = tid; w < np * 7; w += 256) mval[w] = mval_g[w];
+   const int S = nx, P = nx * ny;
+   const int ncx = nx >> 1, ncy = ny >> 1, ncz = nz >> 1;
+   const int G = (int)gridDim.x;
+   int lg = (int)blockIdx.x;
+   if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
+   const int pblk = lg % npb, chunk = lg / npb;
+   const int nsx = nx / 512;
+   const int y0 = (pblk / nsx) * NL, seg = pblk % nsx, fx = seg * 512 + 2 * tid;
+   const int t = fx >> 1;                   // the pair's coarse x
+   const int ct0 = seg * 256 - 1, cy0 = (y0 >> 1) - 1; // ring[.][0][0] = coarse (cy0, ct0)
+   const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
+   const bool lo = t >= 1, hi = t < ncx;
+   // coarse plane c (its NCL lines of CW points; outside the box 0.0) into registers / a slot
+   auto fetch_c = [&](int c, double (&v)[NLD]) {
+#pragma unroll
+      for (int j = 0; j < NLD; j++) {
+         const int idx = tid + 256 * j, li = idx / CW, xi = idx - li * CW;
+         const int cy = cy0 + li, cx = ct0 + xi;
+         v[j] = (idx < NCL * CW && c >= 0 && c < ncz && cy >= 0 && cy < ncy && cx >= 0 && cx < ncx)
+                   ? e[((long long)c * ncy + cy) * ncx + cx]
+                   : 0.0;
+      }
+   };
+   auto store_c = [&](int c, const double (&v)[NLD]) {
+      double *sl = &ring[c & 3][0][0];
+#pragma unroll
+      for (int j = 0; j < NLD; j++) {
+         const int idx = tid + 256 * j;
+         if (idx < NCL * CW) sl[idx] = v[j];
+      }
+   };
+   // line candidates of fine line y (line_cands; ring line indices)
+   struct LC {
+      int m, c[2], d[2];
+   };
+   auto cands = [&](int y) {
+      LC r;
+      line_cands(y, ncy, r.m, r.c, r.d);
+      r.c[0] -= cy0;
+      r.c[1] -= cy0;
+      return r;
+   };
+   // coarse terms of fine plane z for the pair (acc.x: coarse t - 1, t; acc.y: t)
+   auto add_pair = [&](v2d acc, int z, const LC &lc) {
+      auto plane = [&](int c, int d) {
+#pragma unroll
+         for (int b = 0; b < 2; b++) {
+            if (b >= lc.m) break;
+            const double *E = &ring[c & 3][lc.c[b]][0];
+            const double em = lo ? E[tid] : 0.0, ec = E[tid + 1];
+            const double *w = wl + d * 9 + lc.d[b] * 3;
+            if (lo) acc.x = acc.x + w[2] * em;
+            if (hi) acc.x = acc.x + w[0] * ec;
+            acc.y = acc.y + w[1] * ec;
+         }
+      };
+      if (z & 1) {
+         plane((z - 1) >> 1, 1);
+      } else {
+         if (z >= 2) plane((z >> 1) - 1, 2);
+         if ((z >> 1) < ncz) plane(z >> 1, 0);
+      }
+      return acc;
+   };
+   // corrected pair of line y, plane z (outside the box: 0.0, no row uses it)
+   auto uc2 = [&](int z, int y, const LC &lc) -> v2d {
+      if (z < 0 || z >= nz || y < 0 || y >= ny) return v2d{0.0, 0.0};
+      return add_pair(ld2u(u, (unsigned)z * P + (unsigned)(y * S + fx)), z, lc);
+   };
+   // wave-edge neighbour of the own line: lane 0 the point fx - 1 (the .y of
+   // pair t - 1), lane 63 the point fx + 2 (the .x of pair t + 1)
+   auto edge = [&](int z, int y, const LC &lc) -> double {
+      if (lane != 0 && lane != 63) return 0.0;
+      if (z < 0 || z >= nz) return 0.0;
+      const bool left = lane == 0;
+      if (left ? fx == 0 : fx + 2 >= nx) return 0.0;
+      double acc = ld1u(u, (unsigned)z * P + (unsigned)(y * S + (left ? fx - 1 : fx + 2)));
+      const int q = left ? tid : tid + 1; // ring index of coarse t - 1 / t
+      const bool hi2 = t + 1 < ncx;
+      auto plane = [&](int c, int d) {
+#pragma unroll
+         for (int b = 0; b < 2; b++) {
+            if (b >= lc.m) break;
+            const double *E = &ring[c & 3][lc.c[b]][0];
+            const double *w = wl + d * 9 + lc.d[b] * 3;
+            if (left) {
+               acc = acc + w[1] * E[q];
+            } else {
+               acc = acc + w[2] * E[q];
+               if (hi2) acc = acc + w[0] * E[q + 1];
+            }
+         }
+      };
+      if (z & 1) {
+         plane((z - 1) >> 1, 1);
+      } else {
+         if (z >= 2) plane((z >> 1) - 1, 2);
+         if ((z >> 1) < ncz) plane(z >> 1, 0);
+      }
+      return acc;
+   };
+   LC lcs[NL];
+#pragma unroll
+   for (int i = 0; i < NL; i++) lcs[i] = cands(y0 + i);
+   const LC lcm = cands(y0 - 1), lcp = cands(y0 + NL);
+   // the ring holds coarse planes (k >> 1) - 1 .. (k >> 1) + 1 at step k, and
+   // (k >> 1) + 2 from the barrier of the even step before it is needed
+   {
+      const int cb = (k0 >> 1) - 1, ce = (k0 >> 1) + 1 + (k0 & 1);
+      double v[NLD];
+      for (int c = cb; c <= ce; c++) {
+         fetch_c(c, v);
+         store_c(c, v);
+      }
+   }
+   __syncthreads();
+   v2d xm[NL], xc[NL], xq[NL];
+   double ec[NL], eq[NL];
+#pragma unroll
+   for (int i = 0; i < NL; i++) {
+      xm[i] = uc2(k0 - 1, y0 + i, lcs[i]);
+      xc[i] = uc2(k0, y0 + i, lcs[i]);
+      ec[i] = edge(k0, y0 + i, lcs[i]);
+      xq[i] = uc2(k0 + 1, y0 + i, lcs[i]);
+      eq[i] = edge(k0 + 1, y0 + i, lcs[i]);
+   }
+   for (int k = k0; k < k1; k++) {
+      double cv[NLD];
+      if ((k & 1) == 0) {
+         if (k != k0) __syncthreads(); // slot (k >> 1) - 2 free, plane (k >> 1) + 1 visible
+         fetch_c((k >> 1) + 2, cv);
+      }
+      v2d xn[NL];
+      double en[NL];
+      const bool nxt = k + 2 < nz && k + 1 < k1;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+         xn[i] = v2d{0.0, 0.0};
+         en[i] = 0.0;
+         if (nxt) {
+            xn[i] = uc2(k + 2, y0 + i, lcs[i]);
+            en[i] = edge(k + 2, y0 + i, lcs[i]);
+         }
+      }
+      const v2d ym = uc2(k, y0 - 1, lcm), yp = uc2(k, y0 + NL, lcp); // halo lines of plane k
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+         const unsigned row = (unsigned)k * P + (unsigned)((y0 + i) * S + fx);
+         const int pid = ppat[row >> 1];
+         const v2d fr = ld2u(f, row);
+         double lft = __shfl_up(xc[i].y, 1, 64);
+         double rgt = __shfl_down(xc[i].x, 1, 64);
+         if (lane == 0) lft = ec[i];
+         if (lane == 63) rgt = ec[i];
+         const unsigned long long mk = mtab[pid];
+         v2d xv[7];
+         xv[0] = xc[i];
+         xv[1] = xm[i];
+         xv[2] = i == 0 ? ym : xc[i == 0 ? 0 : i - 1];
+         xv[3] = v2d{lft, xc[i].x};
+         xv[4] = v2d{xc[i].y, rgt};
+         xv[5] = i == NL - 1 ? yp : xc[i == NL - 1 ? 0 : i + 1];
+         xv[6] = xq[i];
+         const v2d res = mz_acc7<1, UNI>(fr, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
+         v2d o;
+         if (L1) {
+            const v2d l = ld2u(l1, row);
+            o = v2d{xc[i].x + res.x / l.x, xc[i].y + res.y / l.y};
+         } else {
+            const v2d a = UNI ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 7];
+            o = v2d{(a.x != 0.0) ? xc[i].x + omega * res.x / a.x : xc[i].x,
+                    (a.y != 0.0) ? xc[i].y + omega * res.y / a.y : xc[i].y};
+         }
+         *reinterpret_cast<v2du *>(uout + row) = o;
+      }
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+         xm[i] = xc[i];
+         xc[i] = xq[i];
+         ec[i] = eq[i];
+         xq[i] = xn[i];
+         eq[i] = en[i];
+      }
+      if ((k & 1) == 0) store_c((k >> 1) + 2, cv);
+   }
+}
+
 void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const double *u, const double *ec,
                       const GeoT &g, const double *wdev, const double *l1, double omega, double *uout)
 {
@@ -2523,9 +2739,34 @@ void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const do
    }
    const int P = A->mz_P, nz = A->nrows / P;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
-   // fuse_prolong 1: four lines per workgroup, 3: two, 2: one (mz_prolong_sweep_kernel)
-   const int NL = A->ctx->fuse_prolong == 3 ? 2 : 4;
-   if (A->ctx->fuse_prolong != 2 && g.nx % 512 == 0 && g.ny % NL == 0) {
+   // fuse_prolong 1: four lines per workgroup, 3: two, 2: one (mz_prolong_sweep_kernel);
+   // 4 / 5: two / four lines, the coarse correction from an LDS ring (mz_prolong_sweep_lds_kernel)
+   const int fp = A->ctx->fuse_prolong;
+   if ((fp == 4 || fp == 5) && g.nx % 512 == 0 && g.ny % (fp == 4 ? 2 : 4) == 0) {
+      const int NLs = fp == 4 ? 2 : 4;
+      const int npb = P / (512 * NLs), zc = mz_chunk(A, nz, npb), nch = (nz + zc - 1) / zc;
+#define AMG_PSL(U, L, N)                                                                                               \
+   mz_prolong_sweep_lds_kernel<U, L, N><<<npb * nch, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, ec, f, l1, wdev, \
+                                                                  omega, g.nx, g.ny, g.nz, zc, npb, A->ctx->mz_xcd, uout)
+#define AMG_PSL2(N)                           \
+   if (A->mp_uni) {                           \
+      if (l1) AMG_PSL(true, true, N);         \
+      else AMG_PSL(true, false, N);           \
+   } else {                                   \
+      if (l1) AMG_PSL(false, true, N);        \
+      else AMG_PSL(false, false, N);          \
+   }
+      if (NLs == 2) {
+         AMG_PSL2(2)
+      } else {
+         AMG_PSL2(4)
+      }
+#undef AMG_PSL2
+#undef AMG_PSL
+      return;
+   }
+   const int NL = fp == 3 ? 2 : 4;
+   if (fp != 2 && g.nx % 512 == 0 && g.ny % NL == 0) {
       const int npb = P / (512 * NL), zc = mz_chunk(A, nz, npb), nch = (nz + zc - 1) / zc;
 #define AMG_PSN(U, L, N)                                                                                              \
    mz_prolong_sweep_nl_kernel<U, L, N><<<npb * nch, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, ec, f, l1, wdev, \

@@ -323,7 +323,10 @@ static int detect_geo(amg_hier *H)
       const amgk::GeoT &gg = H->gl[l];
       const bool box7 = H->geo[l] && Al->mz_P && !Al->mz27 && Al->mz_S == gg.nx &&
                         (long long)Al->mz_P == (long long)gg.nx * gg.ny && Al->nrows / Al->mz_P == gg.nz;
-      H->psw[l] = box7 && H->ctx->fuse_prolong;
+      // the LDS-ring forms (4 / 5) fuse only the levels they tile (lines of
+      // 512k points, 2 / 4 lines per workgroup); the others stay unfused
+      const int fp = H->ctx->fuse_prolong;
+      H->psw[l] = box7 && fp && (fp < 4 || (gg.nx % 512 == 0 && gg.ny % (fp == 4 ? 2 : 4) == 0));
       H->xfp[l] = box7 && H->ctx->fuse_xfer;
       H->xfr[l] = box7 && H->ctx->fuse_xfer && Al->mp_uni && gg.nx >= 64 && gg.nx <= 512 && 512 % gg.nx == 0 &&
                   (gg.ny / 2) % (512 / gg.nx) == 0;

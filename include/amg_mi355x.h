@@ -384,8 +384,11 @@ int amg_set_fuse_transfer(amg_ctx *ctx, int enable);
  * l geometric and its A_l 7-pt marched).  Bit-identical to the two kernels.
  * Off by default (measured 1.79 ms against 0.48 + 0.65 ms for the two kernels
  * at 512^3: the register-formed operands make it VALU-bound);
- * amg_set_fuse_prolong(ctx, 1) (env AMG_FUSE_PROLONG=1) turns it on for
- * hierarchies created afterwards. */
+ * amg_set_fuse_prolong(ctx, form) (env AMG_FUSE_PROLONG) turns it on for
+ * hierarchies created afterwards: 1 four lines per workgroup, 3 two, 2 one
+ * (coarse values gathered per operand); 4 / 5 two / four lines with the
+ * coarse correction read from an LDS ring of coarse planes (levels whose
+ * lines are multiples of 512 points only). */
 int amg_hier_fused_prolong(const amg_hier *H);
 int amg_set_fuse_prolong(amg_ctx *ctx, int enable);
 /* lines per lane of the 7-pt plane march (1, 2 or 4; env AMG_MZ_LINES for the
