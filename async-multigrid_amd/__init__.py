@@ -68,6 +68,13 @@ class Context:
     def sync(self):
         check(lib.amg_sync(self.h))
 
+    def device_errors(self):
+        """Device-side range-check flags raised since the last call (bit 0: a
+        zero-guess fold write outside the coarse level's rows, dropped)."""
+        v = C.c_int(0)
+        check(lib.amg_device_errors(self.h, C.byref(v)))
+        return v.value
+
     def set_value_index(self, enable):
         """Value-indexed CSR for matrices registered from now on (default on)."""
         check(lib.amg_set_value_index(self.h, int(enable)))

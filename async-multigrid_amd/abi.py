@@ -77,6 +77,7 @@ PROTOTYPES = {
     "amg_init": (_i, [_pp, _i, _i]),
     "amg_finalize": (_i, [_p]),
     "amg_sync": (_i, [_p]),
+    "amg_device_errors": (_i, [_p, _ip]),
     "amg_last_error": (C.c_char_p, []),
     "amg_version": (_i, []),
     "amg_csr_register": (_i, [_p, _i, _i, _ll, _ip, _ip, _dp, _i, _pp]),

@@ -126,6 +126,8 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    }
    AMG_HIP(hipMalloc(&c->d_scalars, 8192 * sizeof(double)));
    AMG_HIP(hipMemset(c->d_scalars, 0, 8192 * sizeof(double)));
+   AMG_HIP(hipMalloc(&c->d_err, 64));
+   AMG_HIP(hipMemset(c->d_err, 0, 64));
    AMG_HIP(hipHostMalloc(&c->h_pinned, 1024 * sizeof(double)));
    hipDeviceProp_t prop;
    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
@@ -191,8 +193,22 @@ extern "C" int amg_finalize(amg_ctx *c)
    hipStreamDestroy(c->stream);
    hipFree(c->d_partials);
    hipFree(c->d_scalars);
+   hipFree(c->d_err);
    hipHostFree(c->h_pinned);
    delete c;
+   return AMG_OK;
+}
+
+// device-side range-check flags since the last call (bit 0: a zero-guess fold
+// write outside the coarse level's rows, dropped), cleared on read
+extern "C" int amg_device_errors(amg_ctx *c, int *flags)
+{
+   AMG_ARG(c && flags, "amg_device_errors: null argument");
+   int h[16];
+   AMG_HIP(hipStreamSynchronize(c->stream));
+   AMG_HIP(hipMemcpy(h, c->d_err, sizeof(h), hipMemcpyDeviceToHost));
+   AMG_HIP(hipMemset(c->d_err, 0, sizeof(h)));
+   *flags = h[0];
    return AMG_OK;
 }
 

@@ -83,6 +83,7 @@ struct amg_ctx {
    double *d_partials = nullptr;           // per-workgroup partial sums
    size_t partials_cap = 0;
    double *d_scalars = nullptr;            // device scalars (norms, dots)
+   int *d_err = nullptr;                   // device-side range-check flags (amg_device_errors)
    double *h_pinned = nullptr;             // pinned host mirror of scalars
    int num_cus = 256;
    int wall_khz = 100000;  // device wall clock (wall_clock64) rate, for injected delays
@@ -309,6 +310,10 @@ struct ZeroGuess {
    const double *d = nullptr;
    double w = 0.0;
    double *u = nullptr;
+   // indices the fold may write: [lo, hi) (hi < 0: unchecked); a write outside
+   // is dropped and flagged in *err (amg_device_errors)
+   long long lo = 0, hi = -1;
+   int *err = nullptr;
 };
 void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, const double *u, const GeoT &g,
                           const double *wdev, double *fc, int Kb = 0, int Ke = -1, int fz0 = 0, int cz0 = 0,

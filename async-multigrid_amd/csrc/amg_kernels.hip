@@ -1598,6 +1598,10 @@ constexpr int AMG_RR_RING = 4;
 __device__ __forceinline__ void zg_apply(const ZeroGuess &zg, long long i, double fv)
 {
    if (zg.u) {
+      if (zg.hi >= 0 && (i < zg.lo || i >= zg.hi)) {
+         if (zg.err) *zg.err = 1;
+         return;
+      }
       const double a = zg.d[i];
       if (a != 0.0) zg.u[i] = zg.w * fv / a;
    }

@@ -388,6 +388,8 @@ int amgd::slab_restrict(amg_dist_hier *D, hipStream_t s, int l, double *r, doubl
       if (zg.u) { // the ZeroGuess vectors are indexed like dst (level l + 1's owned rows)
          zg.d -= coff;
          zg.u -= coff;
+         zg.lo += coff;
+         if (zg.hi >= 0) zg.hi += coff;
       }
       amgk::geo_restrict(s, v.g, v.d_geo_w, r - v.sg.off(), dst - coff, v.Ka, v.Kb, v.sg.e0(), cz0, zg);
    } else {
@@ -454,6 +456,8 @@ int amgd::slab_vcycle(amg_dist_hier *D, bool precond)
          zg.d = slab_diag(nx.A);
          zg.w = D->o.smooth_weight;
          zg.u = nx.u;
+         zg.hi = nx.n;
+         zg.err = c->d_err;
       }
       if (l == 0 && D->geo0) {
          SProf pr(D, 0, true);

@@ -666,6 +666,8 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
          zg.d = nx.A->diag;
          zg.w = o.smooth_weight;
          zg.u = nx.u;
+         zg.hi = nx.n;
+         zg.err = H->ctx->d_err;
       }
       if (l == 0 && H->geo0) {
          // level-0 residual and restriction in one pass (no r_fine vector)

@@ -187,6 +187,10 @@ void amg_opts_default(amg_opts *o); /* SMEM_Main.cpp:65-105 defaults */
 int amg_init(amg_ctx **ctx, int device, int nstreams);
 int amg_finalize(amg_ctx *ctx);
 int amg_sync(amg_ctx *ctx);
+/* Device-side range-check flags raised since the last call (bit 0: a
+ * zero-guess fold write outside the coarse level's rows, dropped instead of
+ * written), cleared on read; synchronises the context's stream. */
+int amg_device_errors(amg_ctx *ctx, int *flags);
 const char *amg_last_error(void);
 int amg_version(void);
 

@@ -42,10 +42,12 @@ def slab_ranks(amg, gen, opts, f, cycles, nranks, replicate_rows, rccl=False, in
         u = D.get_u()
         row0 = D.row0
         D.free()
+        errs = ctx.device_errors()  # the zero-guess fold's range checks
         amg.dist.finalize(ctx)
         ctx.close()
         if tr is not None and tr.error is not None:
             raise tr.error
+        assert errs == 0, f"rank {r}: device range-check flags {errs:#x}"
         return row0, u, np.array(hist)
 
     res = run_ranks(nranks, rank)

@@ -5,7 +5,7 @@
 # post-sweep with the coarse correction from an LDS ring (AMG_FUSE_PROLONG 4 /
 # 5); first the LDS form's bitwise tests
 set -o pipefail
-R=$GRAFT_REPO_ROOT
+R=${GRAFT_REPO_ROOT:-$(pwd)}
 P=$R/gpurun_out/r04h
 mkdir -p $P
 timeout -k 10 300 python -u -m pytest tests/test_gpu_march.py -k fused_prolong -v -rf --timeout 120 \
