@@ -102,9 +102,10 @@ def fine_kernels(n0, mat_bytes, ms, launches, fused, fmt, fused_prolong=0):
         out["post_sweep"] = (per(1), mat_bytes + 24 * n0,
                              f"post-smoothing Jacobi sweep (reads f, u; writes u_next; {fmt})")
     if fused & 1:
-        out["residual_restrict"] = (per(0), mat_bytes + 16 * n0 + 8 * (n0 // 8),
-                                    "level-0 residual fused with the geometric restriction "
-                                    "(reads f, u; writes f_1)")
+        # the coarse level's zero-guess sweep rides on it (reads a_1, writes u_1)
+        out["residual_restrict"] = (per(0), mat_bytes + 16 * n0 + 24 * (n0 // 8),
+                                    "level-0 residual fused with the geometric restriction and level 1's "
+                                    "zero-guess sweep (reads f, u, a_1; writes f_1, u_1)")
     else:
         out["residual"] = (per(0), mat_bytes + 24 * n0, f"level-0 residual ({fmt})")
         out["restrict0"] = (per(2), None, "R0 restriction")

@@ -16,7 +16,9 @@ KERNELS = {
     # name in bench.fine_kernels: (kernel pattern, algorithmic bytes per launch as f(n))
     "outer_residual_sweep": (r"csr_mz_kernel<1, true, amgk::EpiResJacobi", lambda r: (r + 1) // 2 + 24 * r),
     "post_sweep": (r"csr_mz_kernel<1, true, amgk::EpiJacobi,", lambda r: (r + 1) // 2 + 24 * r),
-    "residual_restrict": (r"mz_res_restrict_kernel", lambda r: (r + 1) // 2 + 16 * r + r),
+    # + level 1's zero-guess sweep folded in: f_1, u_1 written, a_1 read (r / 8 rows each)
+    "residual_restrict": (r"mz_res_restrict_kernel", lambda r: (r + 1) // 2 + 16 * r + 3 * r),
+    "prolong_sweep": (r"mz_prolong_sweep", lambda r: (r + 1) // 2 + 24 * r + r),
     "prolong0": (r"geo_prolong_(march_)?k", lambda r: 16 * r + r),
 }
 
