@@ -148,7 +148,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_FUSE_XFER")) c->fuse_xfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_GRAPHS")) c->graphs = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_XFP_SLAB")) c->fuse_xfp_slab = std::atoi(v) != 0;
-   if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::max(0, std::min(5, std::atoi(v)));
+   if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::max(0, std::min(7, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_SMALL")) c->jgs_small = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_WAVE")) c->jgs_wave = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::atoi(v) != 0;
@@ -897,7 +897,7 @@ extern "C" int amg_set_jgs_small(amg_ctx *c, int form)
 extern "C" int amg_set_fuse_prolong(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_fuse_prolong: null context");
-   c->fuse_prolong = std::max(0, std::min(5, enable));
+   c->fuse_prolong = std::max(0, std::min(7, enable));
    return AMG_OK;
 }
 

@@ -2527,8 +2527,8 @@ __global__ __launch_bounds__(256) void mz_prolong_sweep_nl_kernel(
 // coarse plane enters the ring every second fine plane (one workgroup barrier
 // per two planes).  Terms and order as geo_prolong_march_k / geo_prolong_pair:
 // bit-identical to geo_prolong + csr_mz_kernel.
-template <bool UNI, bool L1, int NL>
-__global__ __launch_bounds__(256) void mz_prolong_sweep_lds_kernel(
+template <bool UNI, bool L1, int NL, int OCC = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void mz_prolong_sweep_lds_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ u, const double *__restrict__ e,
    const double *__restrict__ f, const double *__restrict__ l1, const double *__restrict__ wg, double omega,
@@ -2746,6 +2746,20 @@ void mz_prolong_sweep(hipStream_t s, const amg_mat *A, const double *f, const do
    // fuse_prolong 1: four lines per workgroup, 3: two, 2: one (mz_prolong_sweep_kernel);
    // 4 / 5: two / four lines, the coarse correction from an LDS ring (mz_prolong_sweep_lds_kernel)
    const int fp = A->ctx->fuse_prolong;
+   if (fp >= 6 && g.nx % 512 == 0 && g.ny % 2 == 0) {
+      // two lines, the kernel held to 5 / 6 waves per SIMD (register budget)
+      const int npb = P / 1024, zc = mz_chunk(A, nz, npb), nch = (nz + zc - 1) / zc;
+#define AMG_PSO(U, L, O)                                                                                           \
+   mz_prolong_sweep_lds_kernel<U, L, 2, O><<<npb * nch, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, u, ec, f, l1, \
+                                                                     wdev, omega, g.nx, g.ny, g.nz, zc, npb,           \
+                                                                     A->ctx->mz_xcd, uout)
+      if (A->mp_uni && !l1) {
+         if (fp == 6) AMG_PSO(true, false, 5);
+         else AMG_PSO(true, false, 6);
+         return;
+      }
+#undef AMG_PSO
+   }
    if ((fp == 4 || fp == 5) && g.nx % 512 == 0 && g.ny % (fp == 4 ? 2 : 4) == 0) {
       const int NLs = fp == 4 ? 2 : 4;
       const int npb = P / (512 * NLs), zc = mz_chunk(A, nz, npb), nch = (nz + zc - 1) / zc;

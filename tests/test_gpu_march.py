@@ -416,7 +416,8 @@ def test_plane_march27_hierarchy(ctx, amg):
                                                   ((512, 8, 6), 4, "l1", 1, 4), ((512, 16, 12), 5, "jacobi", 1, 4),
                                                   ((512, 12, 10), 3, "jacobi", 2, 4), ((1024, 8, 6), 2, "jacobi", 1, 4),
                                                   ((512, 16, 12), 64, "l1", 2, 5), ((512, 8, 14), 3, "jacobi", 1, 5),
-                                                  ((1024, 16, 6), 5, "l1", 1, 5)])
+                                                  ((1024, 16, 6), 5, "l1", 1, 5), ((512, 16, 12), 5, "jacobi", 1, 6),
+                                                  ((512, 8, 10), 3, "jacobi", 2, 7)])
 def test_fused_prolong_sweep(ctx, amg, oracle, dims, zc, sm, post, form):
     """Prolongation + correction fused into the first post-smoothing sweep
     (SMEM_Sync_AMG.cpp:118-134): iterate and norm history bit-identical to the
@@ -426,7 +427,8 @@ def test_fused_prolong_sweep(ctx, amg, oracle, dims, zc, sm, post, form):
     of 64..512); 1 / 3: four / two lines per workgroup, each corrected value
     formed once (mz_prolong_sweep_nl_kernel, lines of 512 and 1024); 4 / 5: two /
     four lines per workgroup with the coarse correction from an LDS ring of
-    coarse planes (mz_prolong_sweep_lds_kernel; odd chunk starts at zc 3 / 5)."""
+    coarse planes (mz_prolong_sweep_lds_kernel; odd chunk starts at zc 3 / 5);
+    6 / 7: the two-line LDS form held to 5 / 6 waves per SIMD."""
     from oracle import pyoracle as po
     g = amg.Gen(*dims, interp=amg.AMG_INTERP_LINEAR)
     host = {w: [po.Csr(*g.host_csr(c, l)) for l in range(cnt)]

@@ -14,7 +14,7 @@ st=$?; echo "fused_prolong tests exit $st"; tail -3 $P/fused_prolong.log
 case $st in 0|1) ;; *) exit $st;; esac
 grep -q "illegal memory access\|Memory access fault" $P/fused_prolong.log && exit 3
 cd /tmp && export TMPDIR=/tmp
-for v in "AMG_RR_ZC=0" "AMG_FUSE_PROLONG=4" "AMG_FUSE_PROLONG=5" "AMG_RR_ZC=16" "AMG_RR_ZC=32"; do
+for v in "AMG_RR_ZC=0" "AMG_FUSE_PROLONG=4" "AMG_FUSE_PROLONG=6" "AMG_FUSE_PROLONG=5" "AMG_FUSE_PROLONG=7" "AMG_RR_ZC=16" "AMG_RR_ZC=32"; do
   name=${v//=/_}
   env $v timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
      -d $P/$name -o run -- python3 $R/bench.py --steps 6 --warmup 2 --cpu-baseline 0 --spmv-reps 2 \
