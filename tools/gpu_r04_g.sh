@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4: row-form async schedules bitwise + the widened bands; the sync slab
-# file with the zero-guess fold off; the LDS-ring fused prolongation tests and
+# file (zero-guess fold off, the default); the LDS-ring fused prolongation tests and
 # the level-0 variants under a kernel trace (tools/gpu_r04_h.sh); last (fold
 # on) the first two slab cases with kernels serialised so a fault names its launch
 set -o pipefail
@@ -17,7 +17,7 @@ run() { # name timeout args...
 }
 run dist 400 tests/test_gpu_dist.py -k "async_band or schedule_bitwise"
 run grid 300 tests/test_gpu_grid.py -k converges
-AMG_ZG_FOLD_SLAB=0 run slab_nofold 420 -p no:faulthandler tests/test_gpu_slab.py -k "not 512"
+run slab_nofold 420 -p no:faulthandler tests/test_gpu_slab.py -k "not 512"
 ./tools/gpu_r04_h.sh || exit $?
-AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3 run slab_serial 300 -p no:faulthandler tests/test_gpu_slab.py -k "dims0 or dims1" -x
+AMG_ZG_FOLD_SLAB=1 AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3 run slab_serial 300 -p no:faulthandler tests/test_gpu_slab.py -k "dims0 or dims1" -x
 echo done
