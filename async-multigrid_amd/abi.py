@@ -14,6 +14,10 @@ LIB_PATH = os.path.join(_HERE, "lib", "libamg_mi355x.so")
 # tools/ tuning scripts select it, by setting AMG_DEV_LIB=1 before import
 if os.environ.get("AMG_DEV_LIB") == "1":
     LIB_PATH = os.path.join(_HERE, "lib", "libamg_mi355x_dev.so")
+# host-checked build (make -C csrc chk: bounds-checked containers, host debug
+# info) for diagnosing host faults; selected by AMG_CHK_LIB=1
+if os.environ.get("AMG_CHK_LIB") == "1":
+    LIB_PATH = os.path.join(_HERE, "lib", "libamg_mi355x_chk.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "amg_mi355x.h")
 
 _p = C.c_void_p

@@ -14,14 +14,14 @@
 #include <execinfo.h>
 #include <unistd.h>
 
-// AMG_SEGV_TRACE=1: a host SIGSEGV / SIGBUS prints the native backtrace
+// AMG_SEGV_TRACE=1: a host SIGSEGV / SIGBUS / SIGABRT prints the native backtrace
 // (frames as libamg_mi355x.so(+offset), for addr2line), then hands the signal
 // to the handler that was installed before (Python's faulthandler prints the
 // threads' Python stacks) -- the diagnostic for teardown faults of multi-rank
 // tests.  backtrace() is called once at install so that libgcc is loaded
 // before any fault (loading it inside the handler would allocate).
 namespace {
-struct sigaction g_prev_segv, g_prev_bus;
+struct sigaction g_prev_segv, g_prev_bus, g_prev_abrt;
 void amg_fault_trace(int sig, siginfo_t *si, void *uc)
 {
    char msg[96];
@@ -30,7 +30,7 @@ void amg_fault_trace(int sig, siginfo_t *si, void *uc)
    void *buf[64];
    const int n = backtrace(buf, 64);
    backtrace_symbols_fd(buf, n, 2);
-   const struct sigaction &prev = sig == SIGSEGV ? g_prev_segv : g_prev_bus;
+   const struct sigaction &prev = sig == SIGSEGV ? g_prev_segv : sig == SIGBUS ? g_prev_bus : g_prev_abrt;
    if ((prev.sa_flags & SA_SIGINFO) && prev.sa_sigaction) {
       prev.sa_sigaction(sig, si, uc);
    } else if (prev.sa_handler != SIG_DFL && prev.sa_handler != SIG_IGN && prev.sa_handler) {
@@ -51,6 +51,7 @@ __attribute__((constructor)) void amg_fault_trace_init()
    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
    sigaction(SIGSEGV, &sa, &g_prev_segv);
    sigaction(SIGBUS, &sa, &g_prev_bus);
+   sigaction(SIGABRT, &sa, &g_prev_abrt); // heap-check / assertion aborts
 }
 } // namespace
 
