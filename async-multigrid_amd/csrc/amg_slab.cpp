@@ -467,7 +467,9 @@ int amgd::slab_vcycle(amg_dist_hier *D, bool precond)
          // start; the outer residual (preconditioner mode) changes every cycle
          if (precond) AMG_TRY(slab_xchg(c, s, fl, v.n, v.sg.P, D->rr_flo, D->rr_fhi));
          AMG_TRY(s_res_restrict(D, fl, v.u, dst, v.Ka, zg)); // dst: coarse plane Ka first
-         D->lv[l + 1].zero_done = zg.u != nullptr;
+         // level l + 1 is a slab level only below Ld (to_rep: the replicated
+         // tail, which has no DLevel -- D->lv holds Ld entries)
+         if (!to_rep) D->lv[l + 1].zero_done = zg.u != nullptr;
       } else {
          {
             SProf pr(D, 0, l == 0);
@@ -477,7 +479,7 @@ int amgd::slab_vcycle(amg_dist_hier *D, bool precond)
          }
          SProf pr(D, 2, l == 0);
          AMG_TRY(slab_restrict(D, s, l, v.r_fine, dst, xchg, v.geo ? zg : amgk::ZeroGuess()));
-         D->lv[l + 1].zero_done = v.geo && zg.u != nullptr;
+         if (!to_rep) D->lv[l + 1].zero_done = v.geo && zg.u != nullptr;
       }
       if (to_rep) AMG_TRY(s_gather(D, s, slot, D->gath_buf, D->f_rep));
    }
