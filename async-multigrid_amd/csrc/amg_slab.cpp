@@ -266,14 +266,12 @@ bool s_reuse(const amg_dist_hier *D)
 }
 
 // the slab levels' zero-guess sweeps folded into their restrictions (as the
-// single-GPU V-cycle does): opt-in (AMG_ZG_FOLD_SLAB=1) while the sync slab
-// tests' device fault of this round is open -- the runs that
-// faulted all had it on, the round-3 runs without it passed
+// single-GPU V-cycle does; AMG_ZG_FOLD_SLAB=0 turns it off)
 bool zg_fold_on()
 {
    static const bool on = [] {
       const char *e = std::getenv("AMG_ZG_FOLD_SLAB");
-      return e ? std::atoi(e) != 0 : false;
+      return e ? std::atoi(e) != 0 : true;
    }();
    return on;
 }
