@@ -102,8 +102,8 @@ struct amg_ctx {
    // prefetch distance in planes (1 or 2)
    // (> 0: that many per CU; < 0: the kernel's own occupancy from the runtime)
    int mz27_occ = -1;
-   int mz_occ = -1; // the same for the 7-pt march (AMG_MZ_OCC; 0: mz_chunk's rule; -1 measured best with mz_pf 2)
-   int mz_pf = 2;  // 7-pt march prefetch distance in planes (AMG_MZ_PF: 1 or 2)
+   int mz_occ = 0; // the same for the 7-pt march (AMG_MZ_OCC; 0: mz_chunk's rule)
+   int mz_pf = 1;  // 7-pt march prefetch distance in planes (AMG_MZ_PF: 1 or 2)
    int mz27_pf = 2;
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies

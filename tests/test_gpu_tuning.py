@@ -49,7 +49,7 @@ def test_march_tuning_bitwise(ctx, amg, boxes, name, tune):
         mz.free()
         pl.free()
     finally:
-        ctx.set_march_tuning(2, 2, -1, -1)  # the defaults
+        ctx.set_march_tuning(1, 2, 0, -1)  # the defaults
         ctx.set_march_lines(1, gemv=2)
 
 
@@ -84,7 +84,7 @@ def test_march27_tuning_bitwise(ctx, amg, oracle, boxes27, name, tune):
         mz.free()
         pl.free()
     finally:
-        ctx.set_march_tuning(2, 2, -1, -1)  # the defaults
+        ctx.set_march_tuning(1, 2, 0, -1)  # the defaults
 
 
 @pytest.mark.parametrize("mode", ["async-jacobi-s3", "async-hybrid-s1", "sync"])
