@@ -824,6 +824,7 @@ int amg_mat_finish(amg_mat *A)
 extern "C" int amg_set_row_pattern(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_row_pattern: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->row_pattern = enable ? 1 : 0;
    return AMG_OK;
 }
@@ -836,6 +837,7 @@ extern "C" int amg_mat_row_pattern(const amg_mat *A)
 extern "C" int amg_set_pair_pattern(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_pair_pattern: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->pair_pattern = enable < 0 ? 0 : enable > 2 ? 2 : enable;
    return AMG_OK;
 }
@@ -848,6 +850,7 @@ extern "C" int amg_mat_pair_pattern(const amg_mat *A)
 extern "C" int amg_set_pair_anchor16(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_pair_anchor16: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->pair_anchor16 = enable ? 1 : 0;
    return AMG_OK;
 }
@@ -860,6 +863,7 @@ extern "C" int amg_mat_pair_anchor16(const amg_mat *A)
 extern "C" int amg_set_master_pattern(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_master_pattern: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->master_pattern = enable ? 1 : 0;
    return AMG_OK;
 }
@@ -874,6 +878,7 @@ extern "C" int amg_set_plane_march(amg_ctx *c, int enable, int zc, int xcd)
    AMG_ARG(c, "amg_set_plane_march: null context");
    AMG_ARG(zc >= -1 && zc <= 64, "amg_set_plane_march: planes per chunk %d outside [1, 64] (0: keep, -1: auto)",
            zc);
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->plane_march = enable ? 1 : 0;
    if (zc > 0) c->mz_zc = zc, c->mz_zc_auto = 0;
    if (zc == -1) c->mz_zc = 16, c->mz_zc_auto = 1;
@@ -884,6 +889,7 @@ extern "C" int amg_set_plane_march(amg_ctx *c, int enable, int zc, int xcd)
 extern "C" int amg_set_jgs_wave(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_jgs_wave: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->jgs_wave = std::max(0, std::min(2, enable));
    return AMG_OK;
 }
@@ -891,6 +897,7 @@ extern "C" int amg_set_jgs_wave(amg_ctx *c, int enable)
 extern "C" int amg_set_jgs_small(amg_ctx *c, int form)
 {
    AMG_ARG(c, "amg_set_jgs_small: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->jgs_small = std::max(0, std::min(2, form));
    return AMG_OK;
 }
@@ -898,6 +905,7 @@ extern "C" int amg_set_jgs_small(amg_ctx *c, int form)
 extern "C" int amg_set_fuse_prolong(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_fuse_prolong: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->fuse_prolong = std::max(0, std::min(7, enable));
    return AMG_OK;
 }
@@ -905,6 +913,7 @@ extern "C" int amg_set_fuse_prolong(amg_ctx *c, int enable)
 extern "C" int amg_set_march_lines(amg_ctx *c, int lines)
 {
    AMG_ARG(c && (lines == 1 || lines == 2 || lines == 4), "amg_set_march_lines: lines must be 1, 2 or 4");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->mz_lines = lines;
    c->mz_lines_gemv = lines;
    return AMG_OK;
@@ -913,6 +922,7 @@ extern "C" int amg_set_march_lines(amg_ctx *c, int lines)
 extern "C" int amg_set_march_lines_gemv(amg_ctx *c, int lines)
 {
    AMG_ARG(c && (lines == 1 || lines == 2 || lines == 4), "amg_set_march_lines_gemv: lines must be 1, 2 or 4");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->mz_lines_gemv = lines;
    return AMG_OK;
 }
@@ -920,6 +930,7 @@ extern "C" int amg_set_march_lines_gemv(amg_ctx *c, int lines)
 extern "C" int amg_set_graphs(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_graphs: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->graphs = enable != 0;
    return AMG_OK;
 }
@@ -932,6 +943,7 @@ extern "C" int amg_set_march_tuning(amg_ctx *c, int mz_pf, int mz27_pf, int mz_o
            mz27_pf);
    AMG_ARG(mz_occ >= -2 && mz_occ <= 8 && mz27_occ >= -2 && mz27_occ <= 8,
            "amg_set_march_tuning: occupancy %d / %d outside [-1, 8]", mz_occ, mz27_occ);
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    if (mz_pf != -2) c->mz_pf = mz_pf;
    if (mz27_pf != -2) c->mz27_pf = mz27_pf;
    if (mz_occ != -2) c->mz_occ = mz_occ;
@@ -942,6 +954,7 @@ extern "C" int amg_set_march_tuning(amg_ctx *c, int mz_pf, int mz27_pf, int mz_o
 extern "C" int amg_set_fuse_transfer(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_fuse_transfer: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->fuse_transfer = enable ? 1 : 0;
    return AMG_OK;
 }
@@ -959,6 +972,7 @@ extern "C" int amg_mat_march_points(const amg_mat *A)
 extern "C" int amg_set_dict_index(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_dict_index: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->dict_index = enable ? 1 : 0;
    return AMG_OK;
 }
@@ -971,6 +985,7 @@ extern "C" int amg_mat_dict_index(const amg_mat *A)
 extern "C" int amg_set_value_index(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_value_index: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->value_index = enable ? 1 : 0;
    return AMG_OK;
 }
@@ -1142,6 +1157,7 @@ static int build_bsr3(amg_mat *A, const int *rowptr, const int *col, const doubl
 extern "C" int amg_set_bsr3(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_bsr3: null context");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->bsr3 = enable ? 1 : 0;
    return AMG_OK;
 }

@@ -170,16 +170,21 @@ const double *l1_of(const amg_dist_hier *D, int l)
 }
 
 // the MULTADD transfers are the smoothed ones, composed (smooth_transfer)
+// (P~ only with post-smoothing, R~ only with pre-smoothing: SmoothTransfer,
+// SMEM_Setup.cpp:1176-1180,1245-1250)
 bool composed(const amg_dist_hier *D)
 {
-   return D->o.smooth_transfer == 1 && (D->o.solver == AMG_ASYNC_MULTADD || D->o.solver == AMG_MULTADD);
+   return D->o.smooth_transfer == 1 && (D->o.solver == AMG_ASYNC_MULTADD || D->o.solver == AMG_MULTADD) &&
+          (D->o.num_pre_smooth_sweeps > 0 || D->o.num_post_smooth_sweeps > 0);
 }
+static bool composed_r(const amg_dist_hier *D) { return composed(D) && D->o.num_pre_smooth_sweeps > 0; }
+static bool composed_p(const amg_dist_hier *D) { return composed(D) && D->o.num_post_smooth_sweeps > 0; }
 
 // the level-0 composed restriction as one fused pass: slab hierarchies whose
 // level 0 runs the fused residual + restriction (geo0) with uniform values
 bool fused_xfer0(const amg_dist_hier *D)
 {
-   return composed(D) && D->slab && D->geo0 && D->ctx->fuse_xfer && D->lv[0].A.A && D->lv[0].A.A->mp_uni;
+   return composed_r(D) && D->slab && D->geo0 && D->ctx->fuse_xfer && D->lv[0].A.A && D->lv[0].A.A->mp_uni;
 }
 
 // the level-0 composed prolongation as one fused pass (and, when asked, the
@@ -187,7 +192,7 @@ bool fused_xfer0(const amg_dist_hier *D)
 // the fused kernels and whose level-1 ghost needs fit (xfp0)
 bool fused_xfp0(const amg_dist_hier *D)
 {
-   return composed(D) && D->slab && D->xfp0 && D->ctx->fuse_xfer && D->ctx->fuse_xfp_slab && D->lv[0].A.A;
+   return composed_p(D) && D->slab && D->xfp0 && D->ctx->fuse_xfer && D->ctx->fuse_xfp_slab && D->lv[0].A.A;
 }
 
 // every rank's restricted rows (slot) into the replicated level's full vector
@@ -230,7 +235,7 @@ int restrict_to(amg_dist_hier *D, AsyncLevel &a, int l)
       if (l + 1 < Ld) return AMG_OK;
       return gather_restricted(D, a, slot, a.r[l + 1]);
    }
-   if (composed(D)) {
+   if (composed_r(D)) {
       const int n = level_n(D, l);
       amgk::xfer_div(a.s, diag_of(D, l), r, a.xt, 0, n);
       AMG_TRY(apply_A(D, a, l, a.xt, nullptr, mv, a.xy));
@@ -286,7 +291,7 @@ int prolong_to(amg_dist_hier *D, AsyncLevel &a, int l, double *x, double *out, i
       AMG_TRY(a_spgemv(D, a, D->lv[l].P, x, nullptr, mv, out));
    else
       amgk::spgemv(a.s, D->cP[l - D->Ld], x, nullptr, mv, out, 0, level_n(D, l), nullptr);
-   if (composed(D)) {
+   if (composed_p(D)) {
       AMG_TRY(apply_A(D, a, l, out, nullptr, mv, a.xy));
       amgk::xfer_corr(a.s, D->o.smooth_weight, a.xy, diag_of(D, l), out, 0, level_n(D, l));
    }

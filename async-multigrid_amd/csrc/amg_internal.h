@@ -108,6 +108,7 @@ struct amg_ctx {
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies
    int bsr3 = 1;           // 3x3 block form of num_functions = 3 operators
+   unsigned knob_gen = 0;  // bumped by every amg_set_* knob: captured hipGraphs older than it are dropped
    int graphs = 0;         // hipGraphs of the additive cycles' launch-bound loops (AMG_GRAPHS)
    int fuse_xfer = 1;      // composed smoothed transfers of marched 7-pt levels in one pass each
    int fuse_xfp_slab = 0;  // ... and the slab async solve's fused prolongation + atomic (AMG_FUSE_XFP_SLAB)

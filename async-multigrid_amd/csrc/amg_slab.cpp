@@ -431,6 +431,9 @@ int amgd::slab_vcycle(amg_dist_hier *D, bool precond)
                      const std::vector<int> &hi) { return slab_xchg(c, s, x, n, cP, lo, hi); };
    const int R = c->xport->nranks;
    double *slot = D->gath_buf ? D->gath_buf + (size_t)D->gath_blk * R : nullptr;
+   // a fold flag set by an earlier cycle that returned early (an error between
+   // the restriction and the level's smoothing) must not skip this cycle's sweep
+   for (auto &lv : D->lv) lv.zero_done = false;
    for (int l = 0; l < Ld && l < L - 1; l++) {
       DLevel &v = D->lv[l];
       double *fl = (l == 0 && precond) ? D->r0 : v.f;

@@ -90,6 +90,7 @@ struct amg_hier {
    // cycle (g_add, on ctx->stream) and each asynchronous level's correction
    // (g_lev[k] on stream g_lev_s[k]); captured after one eager run (lazy
    // allocations), dropped when the options or blocks change
+   unsigned g_gen = 0; // ctx->knob_gen the cached graphs were captured under
    hipGraphExec_t g_add = nullptr;
    bool g_add_warm = false;
    std::vector<hipGraphExec_t> g_lev;
@@ -444,6 +445,16 @@ static void graphs_reset(amg_hier *H)
    H->g_lev_warm.assign(H->L, 0);
 }
 
+// a context knob changed since the cached graphs were captured: drop them
+// (kernel knobs are read at launch, so a replayed graph keeps the old setting)
+static void graphs_check(amg_hier *H)
+{
+   if (H->g_gen != H->ctx->knob_gen) {
+      graphs_reset(H);
+      H->g_gen = H->ctx->knob_gen;
+   }
+}
+
 // issue `body` on stream s through a cached graph: the first call runs it
 // eagerly (allocations, scratch growth), the second captures and instantiates,
 // every call from then on launches the graph
@@ -651,6 +662,7 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
       const char *e = std::getenv("AMG_ZG_FOLD");
       return e ? std::atoi(e) != 0 : true;
    }();
+   for (auto &lv : H->lv) lv.zero_done = false;
    for (int l = 0; l < L - 1; l++) {
       Level &v = H->lv[l];
       v.zero_flag = 1;
@@ -767,18 +779,25 @@ static void bpx_cycle(amg_hier *H, bool precond)
 // The level corrections are accumulated into u in level order.
 // MULTADD with smooth_transfer: the reference's smoothed transfers
 // (SmoothTransfer, SMEM_Setup.cpp:1173-1254) composed from the plain P, R, A
-static bool composed_transfers(const amg_hier *H) { return H->o.smooth_transfer == 1 && is_multadd(H->o); }
+// forms P~ only with post-smoothing and R~ only with pre-smoothing (SMEM_Setup.cpp:1176-1180,1245-1250)
+static bool composed_transfers(const amg_hier *H)
+{
+   return H->o.smooth_transfer == 1 && is_multadd(H->o) &&
+          (H->o.num_pre_smooth_sweeps > 0 || H->o.num_post_smooth_sweeps > 0);
+}
+static bool composed_r(const amg_hier *H) { return composed_transfers(H) && H->o.num_pre_smooth_sweeps > 0; }
+static bool composed_p(const amg_hier *H) { return composed_transfers(H) && H->o.num_post_smooth_sweeps > 0; }
 
 // rc = R~_l r (composed) or R_l r; t / y: scratch of level l's size
 static void xfer_restrict(amg_hier *H, hipStream_t s, int l, const double *r, double *rc, double *t, double *y)
 {
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    const Level &v = H->lv[l];
-   if (composed_transfers(H) && H->xfr[l]) {
+   if (composed_r(H) && H->xfr[l]) {
       amgk::mz_xfer_restrict(s, v.A, r, H->gl[l], H->d_geo_w[l], H->o.smooth_weight, rc);
       return;
    }
-   if (composed_transfers(H)) {
+   if (composed_r(H)) {
       // t = r ./ a;  y = A t;  t = r + (-w) y;  rc = R t
       amgk::xfer_div(s, v.A->diag, r, t, 0, v.n);
       amgk::spgemv(s, v.A, t, nullptr, mv, y, 0, v.n, nullptr);
@@ -800,7 +819,7 @@ static bool xfer_prolong(amg_hier *H, hipStream_t s, int l, const double *ec, do
 {
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    const Level &v = H->lv[l];
-   if (composed_transfers(H) && H->xfp[l]) {
+   if (composed_p(H) && H->xfp[l]) {
       if (apply)
          amgk::mz_xfer_prolong(s, v.A, ec, H->gl[l], H->d_geo_w[l], H->o.smooth_weight, apply, u, u_priv);
       else
@@ -811,7 +830,7 @@ static bool xfer_prolong(amg_hier *H, hipStream_t s, int l, const double *ec, do
       amgk::geo_prolong(s, H->gl[l], H->d_geo_w[l], ec, ef, 0, -1, 0, 0, 1);
    else
       amgk::spgemv(s, v.P, ec, nullptr, mv, ef, 0, v.n, nullptr);
-   if (composed_transfers(H)) {
+   if (composed_p(H)) {
       // y = A ef;  ef = ef + (-w) (y ./ a)
       amgk::spgemv(s, v.A, ef, nullptr, mv, y, 0, v.n, nullptr);
       amgk::xfer_corr(s, H->o.smooth_weight, y, v.A->diag, ef, 0, v.n);
@@ -1033,7 +1052,7 @@ static int solve_step(amg_hier *H)
       bpx_cycle(H, precond); // SMEM_Solve.cpp:161-163
    else if (one_level)
       vcycle(H, precond, reuse);
-   else if (c->graphs && !H->o.profile)
+   else if (c->graphs && !H->o.profile && (graphs_check(H), true))
       AMG_TRY(graph_issue(H->g_add, H->g_add_warm, c->stream, [&] {
          sync_add_vcycle(H);
          return (int)AMG_OK;
@@ -1366,6 +1385,9 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    // SEMI_ASYNC update stream (the lock of :238-283)
    hipStream_t us = sched != AMG_SCHED_FREE ? lstream(k_lo) : c->comm_stream;
    std::vector<int> issued(L, 0);
+   // converge GLOBAL under round robin: the correction about to run is the
+   // group's last (it sees the converge flag at its barrier)
+   bool rr_last = false;
    // one correction of level k, issued on its stream
    auto correction = [&](int k) -> int {
       hipStream_t s = lstream(k);
@@ -1422,8 +1444,10 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       // the reference leaves its loop after the converged correction BEFORE the
       // GLOBAL residual update (SMEM_Async_AMG.cpp:353-356): converge LOCAL's
       // N-th correction does not touch the shared residual
-      const bool last_local = !conv_global && issued[k] + 1 >= o.num_cycles;
-      if (global_res && !last_local) {
+      // (converge GLOBAL: the correction whose barrier sees the flag, known
+      // only under the round-robin schedule)
+      const bool last = conv_global ? rr_last : issued[k] + 1 >= o.num_cycles;
+      if (global_res && !last) {
          // :356-414: u_k = u; the level's slice of r = f - A u_k (SMEM_Residual:
          // y = A u_k, then r = f - y) into the shared r; then r_k = r (under the
          // update stream for SEMI_ASYNC)
@@ -1444,6 +1468,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    // is captured once per stream and replayed
    const bool graphs = c->graphs && !semi && !read_res && !global_res && !H->o.profile &&
                        (o.delay_type == AMG_DELAY_NONE || o.delay_usec <= 0);
+   if (graphs) graphs_check(H);
    if (graphs && (int)H->g_lev.size() != L) graphs_reset(H);
    auto run = [&](int k) -> int {
       if (!graphs) return correction(k);
@@ -1478,17 +1503,23 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       for (int left = ngrp; left > 0;)
          for (int k = k_lo; k < k_hi; k++) {
             if (stopped[k]) continue;
-            AMG_TRY(run(k));
-            issued[k]++;
+            // k_lo raises the flag after its update (counted with this
+            // correction); the correction that sees it is the group's last
+            bool raise = false;
             if (k == k_lo && !flag) {
                bool all = true;
                for (int l = k_lo; l < k_hi; l++)
-                  if (issued[l] < o.num_cycles) all = false;
+                  if (issued[l] + (l == k ? 1 : 0) < o.num_cycles) all = false;
                // the reference's idle coarsest group runs its turn after the
                // last correcting level, so in round r it has r - 1 when k_lo checks
-               if (k_hi < L && issued[k_lo] - 1 < o.num_cycles) all = false;
-               flag = all;
+               if (k_hi < L && issued[k_lo] < o.num_cycles) all = false;
+               raise = all;
             }
+            rr_last = flag || raise;
+            AMG_TRY(run(k));
+            rr_last = false;
+            issued[k]++;
+            if (raise) flag = true;
             if (flag) {
                stopped[k] = 1;
                left--;

@@ -829,11 +829,16 @@ static int composed_of(const or_hier *H)
    return H->composed && (H->o.solver == OR_MULTADD || H->o.solver == OR_ASYNC_MULTADD);
 }
 
+/* SmoothTransfer forms P~ only when num_post_smooth_sweeps > 0 and R~ only when
+ * num_pre_smooth_sweeps > 0 (SMEM_Setup.cpp:1176-1180, 1245-1250) */
+static int composed_r(const or_hier *H) { return composed_of(H) && H->o.num_pre > 0; }
+static int composed_p(const or_hier *H) { return composed_of(H) && H->o.num_post > 0; }
+
 /* rc = R~_l r (composed, see or_hier_set_composed_transfers) or R_l r; t / y:
  * scratch of level l's size */
 static void xfer_restrict(or_hier *H, int l, const double *r, double *rc, double *t, double *y)
 {
-   if (!composed_of(H)) {
+   if (!composed_r(H)) {
       or_smem_matvec(&H->R[l], r, rc, 0, H->n[l + 1]);
       return;
    }
@@ -850,7 +855,7 @@ static void xfer_restrict(or_hier *H, int l, const double *r, double *rc, double
 static void xfer_prolong(or_hier *H, int l, const double *ec, double *ef, double *y)
 {
    or_smem_matvec(&H->P[l], ec, ef, 0, H->n[l]);
-   if (!composed_of(H)) return;
+   if (!composed_p(H)) return;
    const or_csr *A = &H->A[l];
    const int n = H->n[l];
    const double w = H->o.smooth_weight;
@@ -1421,7 +1426,7 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
          /* restriction :93-108 */
          for (int l = 0; l < coarsest; l++) {
             if (l >= L - 1) continue;
-            if (composed_of(H)) { /* the group's first thread applies R~ (composed) */
+            if (composed_r(H)) { /* the group's first thread applies R~ (composed) */
                if (g == 0) xfer_restrict(H, l, H->lv_r[k][l], H->lv_r[k][l + 1], H->xt[k], H->xy[k]);
             } else {
                RNG(2, l, rs, re);
@@ -1463,7 +1468,7 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
          }
          /* prolongation :211-224 */
          for (int l = k - 1; l > -1; l--) {
-            if (composed_of(H)) {
+            if (composed_p(H)) {
                if (g == 0) xfer_prolong(H, l, H->lv_e[k][l + 1], H->lv_e[k][l], H->xy[k]);
             } else {
                RNG(1, l, ps, pe);

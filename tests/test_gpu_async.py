@@ -65,6 +65,9 @@ CASES = [
     ("multadd", "hybrid", "full", "sol", "global", "local"),
     ("multadd", "jacobi", "full", "sol", "local", "global"),
     ("multadd", "jacobi", "semi", "res", "local", "global"),
+    # res_compute GLOBAL with converge GLOBAL: the correction that sees the
+    # converge flag leaves before the GLOBAL residual update (:353-356)
+    ("multadd", "jacobi", "full", "sol", "global", "global"),
     ("afacx", "jacobi", "semi", "sol", "local", "local"),
     ("afacx", "jacobi", "full", "res", "local", "local"),
 ]
@@ -313,3 +316,52 @@ def test_composed_transfers_geometric_bitwise(amg, oracle, ctx, mode):
     print(f"composed geometric {mode}: differing entries {nd}")
     assert nd == 0
 
+
+
+ZERO_SWEEPS = [(0, 1), (1, 0), (0, 0)]
+
+
+@pytest.mark.parametrize("pre,post", ZERO_SWEEPS, ids=[f"pre{a}-post{b}" for a, b in ZERO_SWEEPS])
+@pytest.mark.parametrize("mode", ["sync", "async-s3", "geo-sync", "geo-async-s1"])
+def test_composed_transfers_zero_sweeps_bitwise(amg, oracle, ctx, setup, pre, post, mode):
+    """SmoothTransfer (SMEM_Setup.cpp:1173-1254) forms P~ only when
+    num_post_smooth_sweeps > 0 and R~ only when num_pre_smooth_sweeps > 0:
+    with a zero sweep count the corresponding transfer stays the plain one.
+    The device (the generic composed chain on 24^3 and the fused geometric
+    forms on a marched 64^3 hierarchy) is bit-identical to the oracle's
+    composed restatement with the same gating, synchronous MULTADD after every
+    cycle and the asynchronous cycle under a deterministic schedule."""
+    geo = mode.startswith("geo")
+    if geo:
+        n = 64
+        _, L, host = hierarchy(amg, oracle, n, amg.AMG_INTERP_LINEAR)
+        f = amg.rhs_rand(0, n ** 3)
+    else:
+        L, _, host, f = setup
+    sched = int(mode[-1]) if "async" in mode else 0
+    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD if sched else amg.AMG_MULTADD, smooth_weight=W,
+                            num_cycles=6, tol=0.0, async_schedule=sched, smooth_transfer=1,
+                            num_pre_smooth_sweeps=pre, num_post_smooth_sweeps=post)
+    H, _ = gpu_hier(amg, ctx, host, opts)
+    if geo:
+        assert H.fused & 2, "level 0's transfers not detected as geometric"
+    if sched:
+        u, rel, cnt = H.async_solve(f)
+    else:
+        u, hist, k = H.solve(f)
+    H.free()
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    OH.set_composed_transfers()
+    if sched:
+        oracle.lib().or_set_async_schedule(sched)
+        try:
+            uo, relo, cnto = OH.async_add(f, [1] * L)
+        finally:
+            oracle.lib().or_set_async_schedule(0)
+        assert list(cnt[:L - 1]) == list(cnto[:L - 1])
+    else:
+        uo, ho, _ = OH.solve(f)
+        np.testing.assert_allclose(hist, ho, rtol=1e-12, atol=0)
+    nd = int(np.count_nonzero(u.view(np.uint64) != uo.view(np.uint64)))
+    print(f"composed pre {pre} post {post} {mode}: differing entries {nd}")
+    assert nd == 0
