@@ -26,7 +26,8 @@ from .abi import (AMG_JACOBI, AMG_GAUSS_SEIDEL, AMG_HYBRID_JGS, AMG_SYMM_JACOBI,
                   AMG_CHEBY_RECUR_ACCEL, AMG_FULL_ASYNC, AMG_SEMI_ASYNC, AMG_LOCAL, AMG_GLOBAL,
                   AMG_READ_SOL, AMG_READ_RES, AMG_DELAY_NONE, AMG_DELAY_ONE, AMG_DELAY_SOME,
                   AMG_DELAY_ALL, AMG_FAIL_ONE, AMG_SPS_EXPONENTIAL, AMG_SPS_INVERSE, AMG_SPS_RANDOM,
-                  AMG_SCHED_FREE, AMG_SCHED_FINEST_FIRST, AMG_SCHED_COARSEST_FIRST, AMG_SCHED_ROUND_ROBIN)
+                  AMG_SCHED_FREE, AMG_SCHED_FINEST_FIRST, AMG_SCHED_COARSEST_FIRST, AMG_SCHED_ROUND_ROBIN,
+                  AMG_SCHED_TIMED)
 
 lib = abi.load()
 
@@ -305,6 +306,17 @@ class Hier:
         rel = C.c_double()
         check(lib.amg_async_solve(self.h, fv.h, uv.h, _ip(cnt), C.byref(rel)))
         return uv.download(), rel.value, cnt
+
+    def async_level_ms(self):
+        """per level: ms from the last async_solve's start to the level's last correction (free race)"""
+        ms = np.zeros(self.L, dtype=np.float64)
+        check(lib.amg_async_level_ms(self.h, _dp(ms)))
+        return ms
+
+    def set_async_durations(self, ms):
+        """AMG_SCHED_TIMED: level k's time per correction"""
+        d = np.ascontiguousarray(ms, dtype=np.float64)
+        check(lib.amg_hier_set_async_durations(self.h, _dp(d), int(d.size)))
 
     def eigs_power(self, iters):
         emax, emin = C.c_double(), C.c_double()

@@ -61,7 +61,7 @@ class AmgOpts(C.Structure):
                 ("smooth_transfer", _i)]
 
 
-AMG_SCHED_FREE, AMG_SCHED_FINEST_FIRST, AMG_SCHED_COARSEST_FIRST, AMG_SCHED_ROUND_ROBIN = 0, 1, 2, 3
+AMG_SCHED_FREE, AMG_SCHED_FINEST_FIRST, AMG_SCHED_COARSEST_FIRST, AMG_SCHED_ROUND_ROBIN, AMG_SCHED_TIMED = 0, 1, 2, 3, 4
 AMG_DELAY_NONE, AMG_DELAY_ONE, AMG_DELAY_SOME, AMG_DELAY_ALL, AMG_FAIL_ONE = 0, 1, 2, 3, 4
 AMG_SPS_EXPONENTIAL, AMG_SPS_INVERSE, AMG_SPS_RANDOM = 0, 1, 2
 
@@ -154,6 +154,8 @@ PROTOTYPES = {
     "amg_solve_get_u": (_i, [_p, _p]),
     "amg_vcycle": (_i, [_p]),
     "amg_async_solve": (_i, [_p, _p, _p, _ip, _dp]),
+    "amg_async_level_ms": (_i, [_p, _dp]),
+    "amg_hier_set_async_durations": (_i, [_p, _dp, _i]),
     "amg_eigs_power": (_i, [_p, _i, _dp, _dp]),
     "amg_hier_profile_read": (_i, [_p, _dp, _llp, _i]),
     "amg_gen_create": (_i, [_i, _i, _i, _i, _i, _i, _pp]),
@@ -199,6 +201,7 @@ PROTOTYPES = {
     "amg_dist_hier_set_replicate_rows": (_i, [_p, _ll]),
     "amg_dist_async_solve": (_i, [_p, _dp, _ip, _dp]),
     "amg_dist_async_level_ms": (_i, [_p, _dp]),
+    "amg_dist_hier_set_async_durations": (_i, [_p, _dp, _i]),
     "amg_dist_async_jacobi": (_i, [_p, _dp, _i, _i, _dp]),
     "amg_dist_async_sps": (_i, [_p, _dp, _i, _dp, C.POINTER(C.c_longlong)]),
     "amg_rand_double_stream": (_i, [C.c_uint, _i, _d, _d, _dp]),

@@ -649,8 +649,9 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    AMG_ARG(D->o.async_type == AMG_FULL_ASYNC, "amg_dist_async_solve: SEMI_ASYNC not supported");
    AMG_ARG(D->L >= 2, "amg_dist_async_solve: needs at least two levels");
    const int sched = D->o.async_schedule;
-   AMG_ARG(sched >= AMG_SCHED_FREE && sched <= AMG_SCHED_ROUND_ROBIN, "amg_dist_async_solve: async_schedule %d",
-           sched);
+   AMG_ARG(sched >= AMG_SCHED_FREE && sched <= AMG_SCHED_TIMED, "amg_dist_async_solve: async_schedule %d", sched);
+   AMG_ARG(sched != AMG_SCHED_TIMED || (int)D->async_dur.size() >= D->L,
+           "amg_dist_async_solve: AMG_SCHED_TIMED needs amg_dist_hier_set_async_durations");
    amg_ctx *c = D->ctx;
    AMG_TRY(setup_async(D));
    AMG_TRY(setup_composed(D));
@@ -704,13 +705,26 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
       for (auto &t : th) t.join();
    } else {
       // the oracle's or_set_async_schedule order: 1 / 2 level after level, 3
-      // cycle-major round robin; every rank issues the same sequence
+      // cycle-major round robin, 4 timed (end times (j+1) dur[k], ties to the
+      // finer level); every rank issues the same sequence
+      std::vector<int> done_k(active, 0);
       for (int q = 0; q < active * N && st[0] == AMG_OK; q++) {
          int k;
-         if (sched == AMG_SCHED_ROUND_ROBIN) k = q % active;
-         else k = sched == AMG_SCHED_FINEST_FIRST ? q / N : active - 1 - q / N;
+         if (sched == AMG_SCHED_ROUND_ROBIN) {
+            k = q % active;
+         } else if (sched == AMG_SCHED_TIMED) {
+            k = -1;
+            double tb = 0.0;
+            for (int j = 0; j < active; j++) {
+               if (done_k[j] >= N) continue;
+               const double t = (double)(done_k[j] + 1) * D->async_dur[j];
+               if (k < 0 || t < tb) k = j, tb = t;
+            }
+         } else {
+            k = sched == AMG_SCHED_FINEST_FIRST ? q / N : active - 1 - q / N;
+         }
          st[0] = correct(k);
-         const bool last = sched == AMG_SCHED_ROUND_ROBIN ? q / active == N - 1 : q % N == N - 1;
+         const bool last = ++done_k[k] == N;
          if (st[0] == AMG_OK && last && hipEventRecord(t_end[k], D->al[k].s) != hipSuccess)
             st[0] = amg_set_error(AMG_ERR_HIP, "level %d: hipEventRecord", k);
       }
@@ -749,6 +763,15 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
       AMG_HIP(hipEventDestroy(t_end[k]));
    }
    AMG_HIP(hipEventDestroy(t_start));
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_hier_set_async_durations(amg_dist_hier *D, const double *ms, int n)
+{
+   AMG_ARG(D && ms && n >= D->L, "amg_dist_hier_set_async_durations: need %d levels", D ? D->L : 0);
+   for (int k = 0; k < D->L; k++)
+      AMG_ARG(ms[k] > 0.0, "amg_dist_hier_set_async_durations: level %d: %g", k, ms[k]);
+   D->async_dur.assign(ms, ms + D->L);
    return AMG_OK;
 }
 

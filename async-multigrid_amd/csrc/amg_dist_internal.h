@@ -224,6 +224,7 @@ struct amg_dist_hier {
    amgd::AccelState acc;
    GridState grid;
    std::vector<double> level_ms; // amg_dist_async_level_ms
+   std::vector<double> async_dur; // AMG_SCHED_TIMED: per-level correction time
    double prof_ms[5] = {0, 0, 0, 0, 0};
    long long prof_n[5] = {0, 0, 0, 0, 0};
 };

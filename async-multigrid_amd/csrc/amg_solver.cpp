@@ -96,6 +96,11 @@ struct amg_hier {
    std::vector<hipGraphExec_t> g_lev;
    std::vector<hipStream_t> g_lev_s;
    std::vector<char> g_lev_warm;
+   // AMG_SCHED_TIMED: per-level correction time (amg_hier_set_async_durations)
+   std::vector<double> async_dur;
+   // per level of the last amg_async_solve: ms from its start to the level's
+   // last correction (amg_async_level_ms)
+   std::vector<double> level_ms;
    // delay / fault injection: one generator per reference thread (srand(tid),
    // SMEM_Solve.cpp:113), reset by every solve
    std::vector<unsigned long long> delay_rng;
@@ -1319,9 +1324,11 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    const bool read_res = o.read_type == AMG_READ_RES && !global_res;
    const bool conv_global = o.converge_test_type == AMG_GLOBAL;
    const int sched = o.async_schedule;
-   AMG_ARG(sched >= AMG_SCHED_FREE && sched <= AMG_SCHED_ROUND_ROBIN, "amg_async_solve: async_schedule %d", sched);
-   AMG_ARG(!conv_global || sched == AMG_SCHED_FREE || sched == AMG_SCHED_ROUND_ROBIN,
+   AMG_ARG(sched >= AMG_SCHED_FREE && sched <= AMG_SCHED_TIMED, "amg_async_solve: async_schedule %d", sched);
+   AMG_ARG(!conv_global || sched == AMG_SCHED_FREE || sched == AMG_SCHED_ROUND_ROBIN || sched == AMG_SCHED_TIMED,
            "amg_async_solve: a sequential schedule needs converge_test_type LOCAL");
+   AMG_ARG(sched != AMG_SCHED_TIMED || (int)H->async_dur.size() >= L,
+           "amg_async_solve: AMG_SCHED_TIMED needs amg_hier_set_async_durations");
    AMG_TRY(solve_begin(H, f, u));
    Level &v0 = H->lv[0];
    const int n0 = v0.n;
@@ -1366,9 +1373,11 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          AMG_HIP(hipEventCreateWithFlags(&a.ev_b, hipEventDisableTiming));
       }
    }
-   hipEvent_t ready;
+   hipEvent_t ready, t_start;
    AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+   AMG_HIP(hipEventCreate(&t_start));
    AMG_HIP(hipEventRecord(ready, c->stream));
+   AMG_HIP(hipEventRecord(t_start, c->stream));
    for (int k = k_lo; k < k_hi; k++) {
       hipStream_t s = lstream(k);
       AMG_HIP(hipStreamWaitEvent(s, ready, 0));
@@ -1525,6 +1534,44 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
                left--;
             }
          }
+   } else if (sched == AMG_SCHED_TIMED) {
+      // the race at fixed level speeds (or_set_async_schedule 4): level k's
+      // j-th correction ends at j * dur[k]; whole corrections in the order of
+      // their end times, ties to the finer level.  The reference's idle
+      // coarsest group (LOCAL residuals: its correction is zero) takes its
+      // turns too, as a group that issues nothing -- under converge GLOBAL its
+      // count is part of the flag (the oracle's group L - 1).  Converge LOCAL:
+      // a group stops after num_cycles; GLOBAL: k_lo raises the flag after an
+      // update once every group has num_cycles, and each group stops at the
+      // first of its corrections that sees the flag (as under round robin)
+      const int kv = std::max(k_hi, L); // groups [k_lo, kv); k >= k_hi: idle
+      std::vector<int> cnt(kv, 0), stopped(kv, 0);
+      bool flag = false;
+      for (;;) {
+         int best = -1;
+         double tb = 0.0;
+         for (int k = k_lo; k < kv; k++) {
+            if (stopped[k]) continue;
+            const double t = (double)(cnt[k] + 1) * H->async_dur[k];
+            if (best < 0 || t < tb) best = k, tb = t;
+         }
+         if (best < 0) break;
+         bool raise = false;
+         if (conv_global && best == k_lo && !flag) {
+            raise = true;
+            for (int l = k_lo; l < kv; l++)
+               if (cnt[l] + (l == best ? 1 : 0) < o.num_cycles) raise = false;
+         }
+         if (best < k_hi) {
+            rr_last = flag || raise;
+            AMG_TRY(run(best));
+            rr_last = false;
+            issued[best]++;
+         }
+         cnt[best]++;
+         if (raise) flag = true;
+         if (conv_global ? flag : cnt[best] >= o.num_cycles) stopped[best] = 1;
+      }
    } else if (!conv_global) {
       // free race, or round robin under converge LOCAL (one stream: the
       // cycle-major, level-minor issue order is the turn order)
@@ -1581,9 +1628,12 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          for (auto &e : d) hipEventDestroy(e);
       if (st != AMG_OK) return st;
    }
+   // each level's finish (its stream after its last correction)
+   std::vector<hipEvent_t> t_end(L, nullptr);
    for (int k = k_lo; k < k_hi; k++) {
-      AMG_HIP(hipEventRecord(ready, c->level_streams[k]));
-      AMG_HIP(hipStreamWaitEvent(c->stream, ready, 0));
+      AMG_HIP(hipEventCreate(&t_end[k]));
+      AMG_HIP(hipEventRecord(t_end[k], c->level_streams[k]));
+      AMG_HIP(hipStreamWaitEvent(c->stream, t_end[k], 0));
    }
    AMG_HIP(hipEventRecord(ready, us));
    AMG_HIP(hipStreamWaitEvent(c->stream, ready, 0));
@@ -1597,5 +1647,31 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    if (relres) *relres = c->h_pinned[0] / H->r0norm;
    if (level_corrections)
       for (int k = 0; k < L; k++) level_corrections[k] = issued[k];
+   H->level_ms.assign(L, 0.0);
+   for (int k = k_lo; k < k_hi; k++) {
+      float ms = 0.f;
+      // one stream under a deterministic schedule: a level's last correction
+      // is not its stream's last work, so only the free race is timed
+      if (sched == AMG_SCHED_FREE) AMG_HIP(hipEventElapsedTime(&ms, t_start, t_end[k]));
+      H->level_ms[k] = ms;
+      AMG_HIP(hipEventDestroy(t_end[k]));
+   }
+   AMG_HIP(hipEventDestroy(t_start));
+   return AMG_OK;
+}
+
+extern "C" int amg_hier_set_async_durations(amg_hier *H, const double *ms, int n)
+{
+   AMG_ARG(H && ms && n >= H->L, "amg_hier_set_async_durations: need %d levels", H ? H->L : 0);
+   for (int k = 0; k < H->L; k++) AMG_ARG(ms[k] > 0.0, "amg_hier_set_async_durations: level %d: %g", k, ms[k]);
+   H->async_dur.assign(ms, ms + H->L);
+   return AMG_OK;
+}
+
+extern "C" int amg_async_level_ms(const amg_hier *H, double *ms)
+{
+   AMG_ARG(H && ms, "amg_async_level_ms: null argument");
+   AMG_ARG(!H->level_ms.empty(), "amg_async_level_ms: no asynchronous solve yet");
+   for (int k = 0; k < H->L; k++) ms[k] = H->level_ms[k];
    return AMG_OK;
 }

@@ -307,6 +307,11 @@ class DistHier:
         check(lib.amg_dist_async_solve(self.h, _dp(f), _ip(cnt), C.byref(rel)))
         return rel.value, cnt
 
+    def set_async_durations(self, ms):
+        """AMG_SCHED_TIMED: level k's time per correction (the same on every rank)"""
+        d = np.ascontiguousarray(ms, dtype=np.float64)
+        check(lib.amg_dist_hier_set_async_durations(self.h, _dp(d), int(d.size)))
+
     def async_level_ms(self):
         """per level: ms from the last async_solve's start to the level's last correction"""
         L = self.gen.L if self.gen is not None else 64

@@ -172,6 +172,12 @@ typedef struct {
 #define AMG_SCHED_FINEST_FIRST 1
 #define AMG_SCHED_COARSEST_FIRST 2
 #define AMG_SCHED_ROUND_ROBIN 3
+#define AMG_SCHED_TIMED 4 /* converge LOCAL: level k takes dur[k] per correction
+                             (amg_hier_set_async_durations /
+                             amg_dist_hier_set_async_durations); whole corrections
+                             in the order of their end times (j+1) dur[k], ties to
+                             the finer level -- the race at fixed level speeds,
+                             the oracle's or_set_async_schedule 4 */
 #define AMG_SPS_EXPONENTIAL 0 /* Main.hpp:132-134 */
 #define AMG_SPS_INVERSE 1
 #define AMG_SPS_RANDOM 2
@@ -443,6 +449,14 @@ int amg_solve_resnorm(amg_hier *H, double *out);
  * num_cycles corrections on its own stream).  level_corrections[L] out. */
 int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *level_corrections,
                     double *relres);
+/* per level of the last amg_async_solve (free race): milliseconds from the
+ * solve's start to the level's last correction (HIP events on the level
+ * streams; 0 for levels without a group or under a deterministic schedule);
+ * ms holds L entries.  ms[k] / corrections[k] is the level's measured
+ * correction time, the input of AMG_SCHED_TIMED. */
+int amg_async_level_ms(const amg_hier *H, double *ms);
+/* AMG_SCHED_TIMED: level k's time per correction (ms[0..L-1], > 0) */
+int amg_hier_set_async_durations(amg_hier *H, const double *ms, int n);
 /* EigsPower SMEM_Cheby.cpp:410-518 with this hierarchy's V-cycle as M^{-1} */
 int amg_eigs_power(amg_hier *H, int iters, double *eig_max, double *eig_min);
 /* profile: accumulated device milliseconds and launch counts of the fine-level
@@ -628,6 +642,9 @@ int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int *level_cor
  * start to the level's last correction (HIP events; 0 for levels without a
  * correction group); ms holds L entries */
 int amg_dist_async_level_ms(const amg_dist_hier *D, double *ms);
+/* AMG_SCHED_TIMED on the distributed solve: level k's time per correction
+ * (every rank passes the same values, so every rank issues the same order) */
+int amg_dist_hier_set_async_durations(amg_dist_hier *D, const double *ms, int n);
 /* DMEM_AsyncSmooth (DMEM_Smooth.cpp:16-313) with ASYNC_JACOBI (l1 = 0: u = r ./ (a_ii/omega))
  * or ASYNC_L1_JACOBI (l1 = 1): `sweeps` relaxations of the fine level in residual-update
  * form from x = 0; every relaxation sends its boundary deltas on the communication

@@ -1141,6 +1141,37 @@ typedef struct {
 static int g_async_schedule = 0;
 void or_set_async_schedule(int s) { g_async_schedule = s; }
 
+/* schedule 4 (timed): the race with fixed level speeds.  Group k
+ * takes d[k] per correction; its j-th correction ends (and updates the shared
+ * vectors) at j * d[k]; the corrections run whole, in the order of those end
+ * times (ties: the finer group first) -- the race of level groups running
+ * concurrently at those speeds, each update applied at its end.  Fed with
+ * the device's measured per-level correction times, it is the oracle's model
+ * of the device's free race. */
+#define OR_MAX_LEVELS 64
+static double g_async_dur[OR_MAX_LEVELS];
+void or_set_async_durations(const double *d, int n)
+{
+   for (int k = 0; k < OR_MAX_LEVELS; k++) g_async_dur[k] = k < n ? d[k] : 1.0;
+}
+
+/* the next group of the timed schedule: the smallest end time of its next
+ * correction among the groups that have not stopped (-1: none) */
+static int timed_next(const int *count, const int *done, int k_lo, int k_hi)
+{
+   int best = -1;
+   double tb = 0.0;
+   for (int c = k_lo; c < k_hi; c++) {
+      if (done[c]) continue;
+      const double t = (double)(__atomic_load_n(&count[c], __ATOMIC_ACQUIRE) + 1) * g_async_dur[c];
+      if (best < 0 || t < tb) {
+         best = c;
+         tb = t;
+      }
+   }
+   return best;
+}
+
 /* res_compute_type GLOBAL (ASYNC_MULTADD, SMEM_Main.cpp:650-660): no group owns
  * level 0 (PartitionLevels' finest_level = 1, SMEM_Setup.cpp:609-615); every
  * thread first smooths its global slice of the fine grid (A_ns_global: equal
@@ -1307,6 +1338,7 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
    /* a sequential schedule never ends under converge GLOBAL (the first group
     * would wait for the others' counts forever) */
    if ((g_async_schedule == 1 || g_async_schedule == 2) && converge_type != OR_CONVERGE_LOCAL) return -1;
+   if (L > OR_MAX_LEVELS) return -1;
    int T = 0;
    for (int k = 0; k < L; k++) {
       if (k < k_lo ? nt[k] != 0 : nt[k] < 1) return -1;
@@ -1372,9 +1404,11 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
    omp_init_lock(&lock);
    double *U = H->u[0];
    const double *F = H->f[0];
-   const int rr = g_async_schedule == 3;
-   int turn = k_lo;                       /* round robin: the group holding the token */
+   const int rr = g_async_schedule == 3 || g_async_schedule == 4;
+   const int timed = g_async_schedule == 4;
    int *gdone = (int *)calloc(L, sizeof(int)); /* round robin: groups that have stopped */
+   /* round robin / timed: the group holding the token */
+   int turn = timed ? timed_next(count, gdone, k_lo, L) : k_lo;
 #pragma omp parallel num_threads(T)
    {
       const int tid = omp_get_thread_num();
@@ -1398,9 +1432,14 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
             if (tid == root[k]) {                                                    \
                if (stop) gdone[k] = 1;                                               \
                int nx = k;                                                           \
-               for (int q = 1; q <= L - k_lo; q++) {                                 \
-                  const int c = k_lo + (k - k_lo + q) % (L - k_lo);                  \
-                  if (!gdone[c]) { nx = c; break; }                                  \
+               if (timed) {                                                          \
+                  const int c = timed_next(count, gdone, k_lo, L);                   \
+                  if (c >= 0) nx = c;                                                \
+               } else {                                                              \
+                  for (int q = 1; q <= L - k_lo; q++) {                              \
+                     const int c = k_lo + (k - k_lo + q) % (L - k_lo);               \
+                     if (!gdone[c]) { nx = c; break; }                               \
+                  }                                                                  \
                }                                                                     \
                __atomic_store_n(&turn, nx, __ATOMIC_RELEASE);                        \
             }                                                                        \

@@ -218,6 +218,10 @@ double or_dmem_async_jacobi(const or_csr *A, const double *b, double *x, int swe
  * device's deterministic-schedule mode (amg_opts.async_schedule) is checked
  * against them bit for bit. */
 void or_set_async_schedule(int s);
+/* schedule 4 (timed, converge LOCAL or GLOBAL): group k takes d[k] per correction; the
+ * corrections run whole, in the order of their end times (j+1) d[k] (ties:
+ * the finer group first) -- the race at fixed level speeds */
+void or_set_async_durations(const double *d, int n);
 /* res_compute_type GLOBAL for or_async_add (ASYNC_MULTADD, READ_SOL): nt[0] = 0
  * (no level-0 group), each thread smooths its global fine slice (:35-77, 356-414) */
 void or_set_async_res_global(int on);

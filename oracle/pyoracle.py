@@ -79,6 +79,7 @@ def lib():
         L.or_dmem_mult_solve.argtypes = [C.c_void_p, _dp, _dp, _dp, C.c_int, C.c_double, C.c_double]
         L.or_set_async_gs_threads.argtypes = [C.c_int]
         L.or_set_async_schedule.argtypes = [C.c_int]
+        L.or_set_async_durations.argtypes = [_dp, C.c_int]
         L.or_set_async_res_global.argtypes = [C.c_int]
         L.or_set_async_accel.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double]
         L.or_dmem_add.restype = C.c_int
@@ -344,6 +345,12 @@ def dmem_async_jacobi(A, b, sweeps, omega, l1=None, accel=0, mu=0.0, delta=0.0):
 
 
 # ---- hierarchy / solve -------------------------------------------------------
+def set_async_durations(d):
+    """or_set_async_durations: per-level correction times of schedule 4 (timed)"""
+    d = np.ascontiguousarray(d, dtype=np.float64)
+    lib().or_set_async_durations(dptr(d), int(d.size))
+
+
 def make_opts(solver=OR_MULT, smoother=OR_JACOBI, num_pre=1, num_post=1, num_fine=1,
               num_coarse=1, smooth_weight=1.0, num_cycles=20, tol=0.0, check_resnorm=1,
               cheby_flag=0, cheby_mu=0.0, cheby_delta=0.0, num_threads=1):

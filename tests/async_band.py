@@ -105,3 +105,55 @@ def blocks64(host):
 
 def in_band(rel, lo, hi):
     return 0.5 * lo <= rel <= 2.0 * hi
+
+
+def durations_of(level_ms, counts, L):
+    """per-level correction times of a device free race: finish time / corrections
+    for the levels that corrected; the reference's idle coarsest group (no
+    device group under LOCAL residuals) runs at the coarsest correcting level's
+    speed; levels without a group take 1 (unused)"""
+    d = np.ones(L)
+    last = None
+    for k in range(L):
+        if counts[k] > 0 and level_ms[k] > 0:
+            d[k] = level_ms[k] / counts[k]
+            last = d[k]
+    if counts[L - 1] == 0 and last is not None:
+        d[L - 1] = last
+    return d
+
+
+def timed_band(amg, oracle, host, f, opts, durations, blocks=None, composed=False, nt=None):
+    """The oracle's model of a device free race: or_async_add under the timed
+    schedule (or_set_async_schedule 4: whole corrections in the order of their
+    end times at fixed per-level speeds) with each duration set the device
+    measured (durations_of of its runs).  Returns (lo, hi, rels): the device's
+    free race must lie in [0.5 lo, 2 hi] (in_band) -- the window of the race's
+    jitter around its model, instead of the band of every speed ratio."""
+    L = len(host["A"])
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    if composed:
+        OH.set_composed_transfers()
+    if blocks is not None:
+        for lev, blk in blocks.items():
+            OH.set_blocks(lev, blk)
+    at = oracle.OR_SEMI_ASYNC if opts.async_type == amg.AMG_SEMI_ASYNC else oracle.OR_FULL_ASYNC
+    rt = oracle.OR_READ_RES if opts.read_type == amg.AMG_READ_RES else oracle.OR_READ_SOL
+    ct = oracle.OR_CONVERGE_GLOBAL if opts.converge_test_type == amg.AMG_GLOBAL else oracle.OR_CONVERGE_LOCAL
+    gres = opts.res_compute_type == amg.AMG_GLOBAL and opts.solver == amg.AMG_ASYNC_MULTADD
+    accel = None
+    if opts.accel_type != amg.AMG_NO_ACCEL:
+        accel = (opts.accel_type, min(opts.cheby_grid, L - 2), opts.cheby_mu, opts.cheby_delta)
+    rels = []
+    for d in durations:
+        d = np.ascontiguousarray(d, dtype=np.float64)
+        oracle.lib().or_set_async_durations(d.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), int(d.size))
+        oracle.lib().or_set_async_schedule(4)
+        try:
+            u, rel, cnt = OH.async_add(f, nt or ([0 if gres else 1] + [1] * (L - 1)), async_type=at,
+                                       converge_type=ct, read_type=rt, res_global=gres, accel=accel)
+        finally:
+            oracle.lib().or_set_async_schedule(0)
+        assert np.all(np.isfinite(u))
+        rels.append(rel)
+    return min(rels), max(rels), rels

@@ -313,31 +313,37 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
         amg.dist.set_replicate_rows(c, rep)
         A, P, R = parts[r]
         D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
-        rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-        u = D.get_u()
+        out = []
+        for _ in range(2):
+            rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
+            out.append((rel, D.get_u(), cnt.copy(), D.async_level_ms()))
         D.free()
         amg.dist.finalize(c)
         c.close()
-        return rel, u, cnt
+        return out
 
     res = run_ranks(nranks, rank)
-    rels = [t[0] for t in res]
-    assert all(r == rels[0] for r in rels)  # one allreduced norm
-    u = np.concatenate([t[1] for t in res])
-    assert np.all(np.isfinite(u))
-    assert list(res[0][2][:L - 1]) == [N] * (L - 1)
-    assert rels[0] < 1.0
-    from async_band import in_band, oracle_async_band
-    # the free runs of the oracle's race plus its extreme speed ratios (the
-    # level groups one after another, finest / coarsest first): the device's
-    # level streams run the coarse groups far ahead of the fine one, a ratio
-    # no OpenMP run on the host reaches (the arithmetic itself is pinned by
-    # test_dist_async_schedule_bitwise)
-    lo, hi, orels, _ = oracle_async_band(amg, oracle, host, f, opts, sequential=True)
-    print(f"dist async {solver} {nranks} ranks: oracle band [{lo:.4e}, {hi:.4e}] ({len(orels)} runs, "
-          f"sequential finest / coarsest first {orels[-3]:.4e} / {orels[-2]:.4e}), "
-          f"sync {sync_rel:.4e}, device {rels[0]:.4e}")
-    assert in_band(rels[0], lo, hi), (rels[0], lo, hi, sync_rel)
+    from async_band import durations_of, in_band, timed_band
+    rels, durs = [], []
+    for q in range(2):
+        rq = [t[q][0] for t in res]
+        assert all(r == rq[0] for r in rq)  # one allreduced norm
+        u = np.concatenate([t[q][1] for t in res])
+        assert np.all(np.isfinite(u))
+        cnt = res[0][q][2]
+        assert list(cnt[:L - 1]) == [N] * (L - 1)
+        assert rq[0] < 1.0
+        rels.append(rq[0])
+        durs.append(durations_of(np.max(np.array([t[q][3] for t in res]), axis=0), cnt, L))
+    # the oracle's model of each run: the race at the level speeds the device
+    # measured (slowest rank per level), or_async_add under the timed schedule
+    # (the arithmetic itself is pinned by test_dist_async_schedule_bitwise)
+    lo, hi, _ = timed_band(amg, oracle, host, f, opts, durs)
+    print(f"dist async {solver} {nranks} ranks: timed-model band [{lo:.4e}, {hi:.4e}] (width {hi / lo:.2f}x), "
+          f"sync {sync_rel:.4e}, device {rels}, durations {[np.round(d, 3).tolist() for d in durs]}")
+    assert hi / lo <= 20.0
+    for rel in rels:
+        assert in_band(rel, lo, hi), (rel, lo, hi, sync_rel)
 
 
 @pytest.mark.parametrize("solver,cuts,rep,sched", [("multadd", (0.5,), 0, 3), ("multadd", (0.3, 0.7), 1000, 1),
@@ -601,24 +607,27 @@ def test_dist_async_additive_accel(amg, oracle, solver, accel, cuts, grid, bound
                 amg.dist.init_host(c, nranks, r, amg.dist.HostTransport(hub, r))
             A, P, R = parts[r]
             D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
-            rel, _ = D.async_solve(f[D.row0:D.row0 + D.n0])
+            rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
             u = D.get_u()
+            ms = D.async_level_ms()
             D.free()
             amg.dist.finalize(c)
             c.close()
-            return rel, u
+            return rel, u, cnt.copy(), ms
 
         res = run_ranks(nranks, rank)
         assert all(t[0] == res[0][0] for t in res)
         assert all(np.all(np.isfinite(t[1])) for t in res)
-        return res[0][0]
+        return res[0][0], durations_of(np.max(np.array([t[3] for t in res]), axis=0), res[0][2], L)
 
-    rel_acc, rel_plain = solve(acc), solve(amg.AMG_NO_ACCEL)
+    from async_band import durations_of, in_band, timed_band
+    (rel_acc, d_acc), (rel_plain, _) = solve(acc), solve(amg.AMG_NO_ACCEL)
     assert rel_acc < 1.0
-    from async_band import in_band, oracle_async_band
     opts = amg.default_opts(solver=a_solver, smooth_weight=w, num_cycles=N, tol=0.0, accel_type=acc,
                             cheby_mu=mu, cheby_delta=delta, cheby_grid=grid)
-    lo, hi, orels, _ = oracle_async_band(amg, oracle, host, f, opts)
-    print(f"dist async {solver} {accel} grid {grid}: oracle band [{lo:.4e}, {hi:.4e}] ({len(orels)} runs), "
-          f"device {rel_acc:.4e} (no accel {rel_plain:.4e})")
+    # the oracle's model of the run: the race at the level speeds the device
+    # measured, with the same ChebyUpdate per level group (timed schedule)
+    lo, hi, _ = timed_band(amg, oracle, host, f, opts, [d_acc])
+    print(f"dist async {solver} {accel} grid {grid}: timed-model {lo:.4e}, device {rel_acc:.4e} "
+          f"(no accel {rel_plain:.4e}), durations {np.round(d_acc, 3).tolist()}")
     assert in_band(rel_acc, lo, hi), (rel_acc, lo, hi, rel_plain)

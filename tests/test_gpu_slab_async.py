@@ -18,7 +18,7 @@ device); each rank's level groups run on their own host threads."""
 import numpy as np
 import pytest
 
-from async_band import in_band, oracle_async_band
+from async_band import durations_of, in_band, oracle_async_band, timed_band
 from test_gpu_dist import run_ranks
 from test_gpu_kernels import assert_bitwise
 
@@ -27,7 +27,7 @@ pytestmark = pytest.mark.gpu
 W = 0.8
 
 
-def slab_async(amg, gen, opts, f, nranks, rep=1 << 12, rccl1=True, runs=1):
+def slab_async(amg, gen, opts, f, nranks, rep=1 << 12, rccl1=True, runs=1, dur=None):
     hub = amg.dist.ThreadMailbox(nranks, timeout=900.0)
 
     def rank(r):
@@ -40,6 +40,8 @@ def slab_async(amg, gen, opts, f, nranks, rep=1 << 12, rccl1=True, runs=1):
             amg.dist.init_host(c, nranks, r, tr)
         amg.dist.set_replicate_rows(c, rep)
         D = amg.dist.DistHier(c, gen, opts, slab=True)
+        if dur is not None:
+            D.set_async_durations(dur)
         out = []
         for _ in range(runs):
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
@@ -90,6 +92,9 @@ SCHED = [
     # restriction of level 0 is the one-pass kernel (ghost planes over the channels)
     ("multadd", True, 2, 3, 64),
     ("multadd", True, 1, 1, 64),
+    # AMG_SCHED_TIMED (the race at fixed level speeds)
+    ("multadd", True, 2, 4, 32),
+    ("multadd", True, 3, 4, 64),
 ]
 
 
@@ -105,12 +110,15 @@ def test_slab_async_schedule_bitwise(amg, oracle, ctx, solver, comp, nranks, sch
     sv = amg.AMG_ASYNC_MULTADD if solver == "multadd" else amg.AMG_ASYNC_AFACX
     opts = amg.default_opts(solver=sv, smooth_weight=W, num_cycles=N, tol=0.0, async_schedule=sched,
                             smooth_transfer=1 if comp else 0)
-    ((rel, cnt, u, _),) = slab_async(amg, gen, opts, f, nranks, rep=1 << 10, rccl1=False)
-    host = host_hier(amg, oracle, gen)
     L = gen.L
+    dur = np.array([3.0 / (1.9 ** k) + 0.05 for k in range(L)]) if sched == 4 else None
+    ((rel, cnt, u, _),) = slab_async(amg, gen, opts, f, nranks, rep=1 << 10, rccl1=False, dur=dur)
+    host = host_hier(amg, oracle, gen)
     OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts_of(oracle, opts))
     if comp:
         OH.set_composed_transfers()
+    if dur is not None:
+        oracle.set_async_durations(dur)
     oracle.lib().or_set_async_schedule(sched)
     try:
         uo, relo, cnto = OH.async_add(f, [1] * L)
@@ -129,42 +137,29 @@ def test_slab_async_band(amg, oracle, ctx):
     """the free race (a host thread and a stream per level group, per-level
     channels) of ASYNC_MULTADD with composed smoothed transfers at 48^3 on 1-3
     ranks: every level runs num_cycles corrections and the relative residual
-    lies in the oracle's asynchronous band (or_async_add free runs with one and
-    two threads per level, composed transfers, the sequential schedules and the
-    sync additive cycle)"""
+    lies within [0.5x, 2x] of the oracle's model of that very race -- or_async_add
+    under the timed schedule at the per-level correction times the device
+    measured (slowest rank per level), composed transfers"""
     n, N = 48, 12
     gen = amg.Gen(n)
     f = amg.rhs_rand(0, n ** 3)
     opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=W, num_cycles=N, tol=0.0, smooth_transfer=1)
     host = host_hier(amg, oracle, gen)
-
-    class Composed:
-        """oracle.Hier with composed transfers for oracle_async_band"""
-
-        def __init__(self, A, P, R, o):
-            self.h = oracle.Hier(A, P, R, o)
-            self.h.set_composed_transfers()
-
-        def __getattr__(self, k):
-            return getattr(self.h, k)
-
-    class OracleShim:
-        def __getattr__(self, k):
-            return Composed if k == "Hier" else getattr(oracle, k)
-
-    # the free runs plus the race's extreme speed ratios (sequential schedules):
-    # each level group has its own host thread and stream, so the coarse groups
-    # can finish far ahead of the fine one (as in test_dist_async_band); the
-    # arithmetic is pinned by test_slab_async_schedule_bitwise
-    lo, hi, orels, _ = oracle_async_band(amg, OracleShim(), host, f, opts, sequential=True)
-    print(f"oracle async band (composed MULTADD, 48^3) [{lo:.4e}, {hi:.4e}] width {hi / lo:.1f}x over {len(orels)}, "
-          f"sequential finest / coarsest first {orels[-3]:.4e} / {orels[-2]:.4e}")
+    L = gen.L
     for nranks in (1, 2, 3):
-        ((rel, cnt, u, _),) = slab_async(amg, gen, opts, f, nranks, rccl1=True)
-        assert list(cnt[:gen.L - 1]) == [N] * (gen.L - 1)
-        print(f"  {nranks} rank(s): device relres {rel:.4e}")
-        assert np.all(np.isfinite(u))
-        assert in_band(rel, lo, hi), (nranks, rel, (lo, hi))
+        runs = slab_async(amg, gen, opts, f, nranks, rccl1=True, runs=2)
+        durs = []
+        for rel, cnt, u, ms in runs:
+            assert list(cnt[:L - 1]) == [N] * (L - 1)
+            assert np.all(np.isfinite(u))
+            durs.append(durations_of(np.max(np.array(ms), axis=0), cnt, L))
+        lo, hi, trels = timed_band(amg, oracle, host, f, opts, durs, composed=True)
+        rels = [r[0] for r in runs]
+        print(f"  {nranks} rank(s): device relres {[f'{r:.4e}' for r in rels]}; timed-model band "
+              f"[{lo:.4e}, {hi:.4e}] (width {hi / lo:.2f}x), durations {[np.round(d, 3).tolist() for d in durs]}")
+        assert hi / lo <= 20.0
+        for rel in rels:
+            assert in_band(rel, lo, hi), (nranks, rel, (lo, hi))
     gen.free()
 
 

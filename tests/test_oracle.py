@@ -311,6 +311,51 @@ def test_async_add_round_robin_schedule(amg, oracle, ct):
         oracle.lib().or_set_async_schedule(0)
 
 
+@pytest.mark.parametrize("ct", ["local", "global"])
+def test_async_add_timed_schedule(amg, oracle, ct):
+    """or_set_async_schedule(4), the race at fixed level speeds: with equal
+    durations it is the round robin (end times tie, the finer group first);
+    under converge LOCAL, durations growing 1000x per level give the groups
+    finest first and durations falling 1000x per level coarsest first (every
+    group's corrections end before the next group's first); uneven durations
+    are deterministic and converge."""
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, 16, amg.AMG_INTERP_LINEAR)
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs = oracle.smooth_transfer(host["A"][lev], host["P"][lev], 0.8)
+        Ps.append(ps)
+        Rs.append(rs)
+    N = 10
+    o = oracle.make_opts(solver=oracle.OR_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=N, tol=0.0)
+    OH = oracle.Hier(host["A"], Ps, Rs, o)
+    f = amg.rhs_rand(0, 16 ** 3)
+    conv = oracle.OR_CONVERGE_GLOBAL if ct == "global" else oracle.OR_CONVERGE_LOCAL
+
+    def run(sched, d=None):
+        if d is not None:
+            oracle.set_async_durations(d)
+        oracle.lib().or_set_async_schedule(sched)
+        try:
+            return OH.async_add(f, [1] * L, async_type=oracle.OR_FULL_ASYNC, converge_type=conv)
+        finally:
+            oracle.lib().or_set_async_schedule(0)
+
+    def same(a, b):
+        return np.array_equal(a[0].view(np.uint64), b[0].view(np.uint64)) and list(a[2]) == list(b[2])
+
+    assert same(run(4, np.ones(L)), run(3))
+    if ct == "local":
+        assert same(run(4, 1000.0 ** np.arange(L)), run(1))
+        assert same(run(4, 1000.0 ** -np.arange(L)), run(2))
+    d = np.array([3.0 / (1.9 ** k) + 0.05 for k in range(L)])
+    a, b = run(4, d), run(4, d)
+    assert same(a, b)
+    assert a[1] < 0.1, a[1]
+    if ct == "local":
+        assert list(a[2][:L]) == [N] * L
+
+
 def test_composed_transfers_match_explicit(amg, oracle):
     """or_hier_set_composed_transfers: the smoothed transfers applied composed
     from the plain P / R (R~ r = R (r - w A D^-1 r), P~ e = P e - w D^-1 A P e)
