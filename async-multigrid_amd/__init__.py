@@ -57,6 +57,23 @@ def default_opts(**kw):
     return o
 
 
+
+def _times_flat(times):
+    n = np.array([len(t) for t in times], dtype=np.int32)
+    flat = np.ascontiguousarray(np.concatenate([np.asarray(t, dtype=np.float64) for t in times] + [np.zeros(1)]))
+    return flat, n
+
+
+def _corr_ms(fn, h, L):
+    out = []
+    for k in range(L):
+        cnt = np.zeros(1, dtype=np.int32)
+        check(fn(h, k, None, 0, _ip(cnt)))
+        ms = np.zeros(max(1, int(cnt[0])))
+        check(fn(h, k, _dp(ms), int(cnt[0]), _ip(cnt)))
+        out.append(ms[:int(cnt[0])])
+    return out
+
 class Context:
     """Device, compute stream and level streams (amg_init)."""
 
@@ -317,6 +334,15 @@ class Hier:
         """AMG_SCHED_TIMED: level k's time per correction"""
         d = np.ascontiguousarray(ms, dtype=np.float64)
         check(lib.amg_hier_set_async_durations(self.h, _dp(d), int(d.size)))
+
+    def set_async_times(self, times):
+        """AMG_SCHED_TIMED replaying recorded end times: times[k] = level k's correction end times"""
+        flat, n = _times_flat(times)
+        check(lib.amg_hier_set_async_times(self.h, _dp(flat), _ip(n), int(n.size)))
+
+    def async_correction_ms(self):
+        """per level: end times (ms) of its corrections in the last free-race async_solve"""
+        return _corr_ms(lib.amg_async_correction_ms, self.h, self.L)
 
     def eigs_power(self, iters):
         emax, emin = C.c_double(), C.c_double()

@@ -650,8 +650,8 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    AMG_ARG(D->L >= 2, "amg_dist_async_solve: needs at least two levels");
    const int sched = D->o.async_schedule;
    AMG_ARG(sched >= AMG_SCHED_FREE && sched <= AMG_SCHED_TIMED, "amg_dist_async_solve: async_schedule %d", sched);
-   AMG_ARG(sched != AMG_SCHED_TIMED || (int)D->async_dur.size() >= D->L,
-           "amg_dist_async_solve: AMG_SCHED_TIMED needs amg_dist_hier_set_async_durations");
+   AMG_ARG(sched != AMG_SCHED_TIMED || ((int)D->async_dur.size() >= D->L && (int)D->async_t.size() >= D->L),
+           "amg_dist_async_solve: AMG_SCHED_TIMED needs amg_dist_hier_set_async_durations / _times");
    amg_ctx *c = D->ctx;
    AMG_TRY(setup_async(D));
    AMG_TRY(setup_composed(D));
@@ -669,6 +669,7 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    for (auto &e : t_end) AMG_HIP(hipEventCreate(&e));
    AMG_HIP(hipEventRecord(ready, c->stream));
    AMG_HIP(hipEventRecord(t_start, c->stream));
+   D->corr.reset(D->L);
    for (int k = 0; k < active; k++) {
       AMG_HIP(hipStreamWaitEvent(D->al[k].s, ready, 0));
       // level_vector[k].r[0] = vector.r[0] (SMEM_Async_AMG.cpp:10-15)
@@ -690,7 +691,11 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
       for (int k = 0; k < active; k++)
          th.emplace_back([&, k] {
             hipSetDevice(c->device);
-            for (int cyc = 0; cyc < N && st[k] == AMG_OK; cyc++) st[k] = correct(k);
+            for (int cyc = 0; cyc < N && st[k] == AMG_OK; cyc++) {
+               st[k] = correct(k);
+               if (st[k] == AMG_OK && D->corr.record(k, cyc, D->al[k].s))
+                  st[k] = amg_set_error(AMG_ERR_HIP, "level %d: correction event", k);
+            }
             // the level's finish: its stream reaches this marker after its last
             // correction (recorded here, not after the join, so a level that is
             // done early is not stamped with the slowest level's time)
@@ -717,7 +722,7 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
             double tb = 0.0;
             for (int j = 0; j < active; j++) {
                if (done_k[j] >= N) continue;
-               const double t = (double)(done_k[j] + 1) * D->async_dur[j];
+               const double t = amg_timed_end(D->async_t[j], D->async_dur[j], done_k[j]);
                if (k < 0 || t < tb) k = j, tb = t;
             }
          } else {
@@ -755,6 +760,11 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    if (relres) *relres = c->h_pinned[0] / D->r0norm;
    if (level_corrections)
       for (int k = 0; k < D->L; k++) level_corrections[k] = k < active ? N : 0;
+   if (sched == AMG_SCHED_FREE) {
+      std::vector<int> cnt(D->L, 0);
+      for (int k = 0; k < active; k++) cnt[k] = N;
+      if (D->corr.collect(t_start, cnt)) return amg_set_error(AMG_ERR_HIP, "amg_dist_async_solve: correction times");
+   }
    D->level_ms.assign(D->L, 0.0);
    for (int k = 0; k < active; k++) {
       float ms = 0.f;
@@ -772,6 +782,28 @@ extern "C" int amg_dist_hier_set_async_durations(amg_dist_hier *D, const double 
    for (int k = 0; k < D->L; k++)
       AMG_ARG(ms[k] > 0.0, "amg_dist_hier_set_async_durations: level %d: %g", k, ms[k]);
    D->async_dur.assign(ms, ms + D->L);
+   D->async_t.assign(D->L, {});
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_hier_set_async_times(amg_dist_hier *D, const double *t, const int *n, int nlev)
+{
+   AMG_ARG(D && t && n && nlev >= D->L, "amg_dist_hier_set_async_times: need %d levels", D ? D->L : 0);
+   D->async_t.assign(D->L, {});
+   D->async_dur.assign(D->L, 1.0);
+   for (int k = 0, off = 0; k < D->L; off += n[k], k++) {
+      AMG_ARG(n[k] >= 0, "amg_dist_hier_set_async_times: level %d: %d entries", k, n[k]);
+      D->async_t[k].assign(t + off, t + off + n[k]);
+   }
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_async_correction_ms(const amg_dist_hier *D, int level, double *ms, int cap, int *count)
+{
+   AMG_ARG(D && count && level >= 0 && level < D->L, "amg_dist_async_correction_ms: bad argument");
+   const auto &v = level < (int)D->corr.ms.size() ? D->corr.ms[level] : std::vector<double>();
+   *count = (int)v.size();
+   for (int j = 0; j < (int)v.size() && j < cap && ms; j++) ms[j] = v[j];
    return AMG_OK;
 }
 

@@ -225,6 +225,8 @@ struct amg_dist_hier {
    GridState grid;
    std::vector<double> level_ms; // amg_dist_async_level_ms
    std::vector<double> async_dur; // AMG_SCHED_TIMED: per-level correction time
+   std::vector<std::vector<double>> async_t; // AMG_SCHED_TIMED: recorded end times (replay)
+   AmgCorrTimes corr;             // per-correction end times of the last free race
    double prof_ms[5] = {0, 0, 0, 0, 0};
    long long prof_n[5] = {0, 0, 0, 0, 0};
 };

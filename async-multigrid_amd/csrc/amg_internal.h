@@ -55,6 +55,57 @@ constexpr int AMG_PP_LDS = 32 * 1024;
 // twice the entries: latency-bound grids below it run faster one row per lane)
 constexpr int AMG_PP_LONG_MIN_ROWS = 1 << 22;
 inline int amg_pp_stride(int maxrow) { return 1 + 2 * (maxrow <= 8 ? 8 : AMG_PP_MAXROW); }
+
+// AMG_SCHED_TIMED: the end time of a level's correction j (0-based) -- its
+// recorded end times t (the replay of a measured race; past the table the
+// last interval repeats) or, without a table, (j + 1) dur.  The oracle's
+// timed_end (or_set_async_durations / or_set_async_times), the same doubles.
+inline double amg_timed_end(const std::vector<double> &t, double dur, int j)
+{
+   const int n = (int)t.size();
+   if (n == 0) return (double)(j + 1) * dur;
+   if (j < n) return t[j];
+   const double dt = n > 1 ? t[n - 1] - t[n - 2] : t[0];
+   return t[n - 1] + (double)(j - n + 1) * dt;
+}
+
+// per-correction end events of a free race (one pool per level, grown on use)
+struct AmgCorrTimes {
+   std::vector<std::vector<hipEvent_t>> ev; // [level][correction]
+   std::vector<std::vector<double>> ms;     // [level][correction], after the solve
+   int record(int k, int j, hipStream_t s)
+   {
+      auto &v = ev[k];
+      while ((int)v.size() <= j) {
+         hipEvent_t e;
+         if (hipEventCreate(&e) != hipSuccess) return -1;
+         v.push_back(e);
+      }
+      return hipEventRecord(v[j], s) == hipSuccess ? 0 : -1;
+   }
+   void reset(int L)
+   {
+      ev.resize(L);
+      ms.assign(L, {});
+   }
+   // elapsed ms of the first cnt[k] events of every level from t0
+   int collect(hipEvent_t t0, const std::vector<int> &cnt)
+   {
+      ms.assign(ev.size(), {});
+      for (size_t k = 0; k < ev.size() && k < cnt.size(); k++)
+         for (int j = 0; j < cnt[k] && j < (int)ev[k].size(); j++) {
+            float m = 0.f;
+            if (hipEventElapsedTime(&m, t0, ev[k][j]) != hipSuccess) return -1;
+            ms[k].push_back(m);
+         }
+      return 0;
+   }
+   ~AmgCorrTimes()
+   {
+      for (auto &v : ev)
+         for (auto e : v) hipEventDestroy(e);
+   }
+};
 // anchored operators (interpolation, restriction): row 2t+1's anchor minus
 // row 2t's, + AMG_PP_DA0, must lie in [0, AMG_PP_NDA)
 constexpr int AMG_PP_NDA = 16;

@@ -97,7 +97,11 @@ struct amg_hier {
    std::vector<hipStream_t> g_lev_s;
    std::vector<char> g_lev_warm;
    // AMG_SCHED_TIMED: per-level correction time (amg_hier_set_async_durations)
+   // or recorded end times (amg_hier_set_async_times)
    std::vector<double> async_dur;
+   std::vector<std::vector<double>> async_t;
+   // per-correction end times of the last free race (amg_async_correction_ms)
+   AmgCorrTimes corr;
    // per level of the last amg_async_solve: ms from its start to the level's
    // last correction (amg_async_level_ms)
    std::vector<double> level_ms;
@@ -1327,8 +1331,8 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    AMG_ARG(sched >= AMG_SCHED_FREE && sched <= AMG_SCHED_TIMED, "amg_async_solve: async_schedule %d", sched);
    AMG_ARG(!conv_global || sched == AMG_SCHED_FREE || sched == AMG_SCHED_ROUND_ROBIN || sched == AMG_SCHED_TIMED,
            "amg_async_solve: a sequential schedule needs converge_test_type LOCAL");
-   AMG_ARG(sched != AMG_SCHED_TIMED || (int)H->async_dur.size() >= L,
-           "amg_async_solve: AMG_SCHED_TIMED needs amg_hier_set_async_durations");
+   AMG_ARG(sched != AMG_SCHED_TIMED || ((int)H->async_dur.size() >= L && (int)H->async_t.size() >= L),
+           "amg_async_solve: AMG_SCHED_TIMED needs amg_hier_set_async_durations / _times");
    AMG_TRY(solve_begin(H, f, u));
    Level &v0 = H->lv[0];
    const int n0 = v0.n;
@@ -1376,6 +1380,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    hipEvent_t ready, t_start;
    AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
    AMG_HIP(hipEventCreate(&t_start));
+   H->corr.reset(L);
    AMG_HIP(hipEventRecord(ready, c->stream));
    AMG_HIP(hipEventRecord(t_start, c->stream));
    for (int k = k_lo; k < k_hi; k++) {
@@ -1552,7 +1557,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          double tb = 0.0;
          for (int k = k_lo; k < kv; k++) {
             if (stopped[k]) continue;
-            const double t = (double)(cnt[k] + 1) * H->async_dur[k];
+            const double t = amg_timed_end(H->async_t[k], H->async_dur[k], cnt[k]);
             if (best < 0 || t < tb) best = k, tb = t;
          }
          if (best < 0) break;
@@ -1578,6 +1583,8 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       for (int cyc = 0; cyc < o.num_cycles; cyc++)
          for (int k = k_lo; k < k_hi; k++) {
             AMG_TRY(run(k));
+            if (sched == AMG_SCHED_FREE && H->corr.record(k, issued[k], lstream(k)))
+               return amg_set_error(AMG_ERR_HIP, "amg_async_solve: correction event");
             issued[k]++;
          }
    } else {
@@ -1611,6 +1618,10 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          for (int k = k_lo; k < k_hi && st == AMG_OK; k++) {
             if (issued[k] - completed[k] < DEPTH && issued[k] < cap) {
                if ((st = run(k)) != AMG_OK) break;
+               if (H->corr.record(k, issued[k], c->level_streams[k])) {
+                  st = amg_set_error(AMG_ERR_HIP, "amg_async_solve: correction event");
+                  break;
+               }
                const hipError_t er = hipEventRecord(done[k][issued[k] % DEPTH], c->level_streams[k]);
                if (er != hipSuccess) {
                   st = amg_set_error(AMG_ERR_HIP, "amg_async_solve: hipEventRecord: %s", hipGetErrorString(er));
@@ -1647,6 +1658,8 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    if (relres) *relres = c->h_pinned[0] / H->r0norm;
    if (level_corrections)
       for (int k = 0; k < L; k++) level_corrections[k] = issued[k];
+   if (sched == AMG_SCHED_FREE && H->corr.collect(t_start, issued))
+      return amg_set_error(AMG_ERR_HIP, "amg_async_solve: correction times");
    H->level_ms.assign(L, 0.0);
    for (int k = k_lo; k < k_hi; k++) {
       float ms = 0.f;
@@ -1665,6 +1678,28 @@ extern "C" int amg_hier_set_async_durations(amg_hier *H, const double *ms, int n
    AMG_ARG(H && ms && n >= H->L, "amg_hier_set_async_durations: need %d levels", H ? H->L : 0);
    for (int k = 0; k < H->L; k++) AMG_ARG(ms[k] > 0.0, "amg_hier_set_async_durations: level %d: %g", k, ms[k]);
    H->async_dur.assign(ms, ms + H->L);
+   H->async_t.assign(H->L, {});
+   return AMG_OK;
+}
+
+extern "C" int amg_hier_set_async_times(amg_hier *H, const double *t, const int *n, int nlev)
+{
+   AMG_ARG(H && t && n && nlev >= H->L, "amg_hier_set_async_times: need %d levels", H ? H->L : 0);
+   H->async_t.assign(H->L, {});
+   H->async_dur.assign(H->L, 1.0);
+   for (int k = 0, off = 0; k < H->L; off += n[k], k++) {
+      AMG_ARG(n[k] >= 0, "amg_hier_set_async_times: level %d: %d entries", k, n[k]);
+      H->async_t[k].assign(t + off, t + off + n[k]);
+   }
+   return AMG_OK;
+}
+
+extern "C" int amg_async_correction_ms(const amg_hier *H, int level, double *ms, int cap, int *count)
+{
+   AMG_ARG(H && count && level >= 0 && level < H->L, "amg_async_correction_ms: bad argument");
+   const auto &v = level < (int)H->corr.ms.size() ? H->corr.ms[level] : std::vector<double>();
+   *count = (int)v.size();
+   for (int j = 0; j < (int)v.size() && j < cap && ms; j++) ms[j] = v[j];
    return AMG_OK;
 }
 

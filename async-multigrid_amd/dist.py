@@ -312,6 +312,18 @@ class DistHier:
         d = np.ascontiguousarray(ms, dtype=np.float64)
         check(lib.amg_dist_hier_set_async_durations(self.h, _dp(d), int(d.size)))
 
+    def set_async_times(self, times):
+        """AMG_SCHED_TIMED replaying recorded end times (the same on every rank)"""
+        from . import _times_flat
+        flat, n = _times_flat(times)
+        check(lib.amg_dist_hier_set_async_times(self.h, _dp(flat), _ip(n), int(n.size)))
+
+    def async_correction_ms(self):
+        """per level: end times (ms) of this rank's corrections in the last free-race async_solve"""
+        from . import _corr_ms
+        L = self.gen.L if self.gen is not None else len(self.async_level_ms())
+        return _corr_ms(lib.amg_dist_async_correction_ms, self.h, L)
+
     def async_level_ms(self):
         """per level: ms from the last async_solve's start to the level's last correction"""
         L = self.gen.L if self.gen is not None else 64

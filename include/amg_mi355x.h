@@ -457,6 +457,14 @@ int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *level_correc
 int amg_async_level_ms(const amg_hier *H, double *ms);
 /* AMG_SCHED_TIMED: level k's time per correction (ms[0..L-1], > 0) */
 int amg_hier_set_async_durations(amg_hier *H, const double *ms, int n);
+/* AMG_SCHED_TIMED replaying recorded end times: level k's j-th correction ends
+ * at t[n[0] + .. + n[k-1] + j] (past n[k] entries its last interval repeats);
+ * nlev >= L */
+int amg_hier_set_async_times(amg_hier *H, const double *t, const int *n, int nlev);
+/* end times (ms from the solve's start, HIP events on the level streams) of
+ * level `level`'s corrections in the last free-race amg_async_solve: *count
+ * corrections, the first min(count, cap) written to ms */
+int amg_async_correction_ms(const amg_hier *H, int level, double *ms, int cap, int *count);
 /* EigsPower SMEM_Cheby.cpp:410-518 with this hierarchy's V-cycle as M^{-1} */
 int amg_eigs_power(amg_hier *H, int iters, double *eig_max, double *eig_min);
 /* profile: accumulated device milliseconds and launch counts of the fine-level
@@ -645,6 +653,10 @@ int amg_dist_async_level_ms(const amg_dist_hier *D, double *ms);
 /* AMG_SCHED_TIMED on the distributed solve: level k's time per correction
  * (every rank passes the same values, so every rank issues the same order) */
 int amg_dist_hier_set_async_durations(amg_dist_hier *D, const double *ms, int n);
+/* amg_hier_set_async_times / amg_async_correction_ms for the distributed solve
+ * (this rank's level streams) */
+int amg_dist_hier_set_async_times(amg_dist_hier *D, const double *t, const int *n, int nlev);
+int amg_dist_async_correction_ms(const amg_dist_hier *D, int level, double *ms, int cap, int *count);
 /* DMEM_AsyncSmooth (DMEM_Smooth.cpp:16-313) with ASYNC_JACOBI (l1 = 0: u = r ./ (a_ii/omega))
  * or ASYNC_L1_JACOBI (l1 = 1): `sweeps` relaxations of the fine level in residual-update
  * form from x = 0; every relaxation sends its boundary deltas on the communication

@@ -1150,9 +1150,41 @@ void or_set_async_schedule(int s) { g_async_schedule = s; }
  * of the device's free race. */
 #define OR_MAX_LEVELS 64
 static double g_async_dur[OR_MAX_LEVELS];
+static double *g_async_t[OR_MAX_LEVELS]; /* or_set_async_times: end time of every correction */
+static int g_async_tn[OR_MAX_LEVELS];
 void or_set_async_durations(const double *d, int n)
 {
-   for (int k = 0; k < OR_MAX_LEVELS; k++) g_async_dur[k] = k < n ? d[k] : 1.0;
+   for (int k = 0; k < OR_MAX_LEVELS; k++) {
+      g_async_dur[k] = k < n ? d[k] : 1.0;
+      free(g_async_t[k]);
+      g_async_t[k] = NULL;
+      g_async_tn[k] = 0;
+   }
+}
+
+/* schedule 4 with recorded end times: group k's j-th correction ends at
+ * t[off_k + j] (j < n[k]; past the table the last interval repeats) -- the
+ * replay of a measured race's update order */
+void or_set_async_times(const double *t, const int *n, int L)
+{
+   or_set_async_durations(NULL, 0);
+   for (int k = 0, off = 0; k < L && k < OR_MAX_LEVELS; off += n[k], k++) {
+      if (n[k] <= 0) continue;
+      g_async_t[k] = (double *)malloc((size_t)n[k] * sizeof(double));
+      memcpy(g_async_t[k], t + off, (size_t)n[k] * sizeof(double));
+      g_async_tn[k] = n[k];
+   }
+}
+
+/* end time of group c's correction j (0-based) */
+static double timed_end(int c, int j)
+{
+   const int n = g_async_tn[c];
+   if (n == 0) return (double)(j + 1) * g_async_dur[c];
+   const double *t = g_async_t[c];
+   if (j < n) return t[j];
+   const double dt = n > 1 ? t[n - 1] - t[n - 2] : t[0];
+   return t[n - 1] + (double)(j - n + 1) * dt;
 }
 
 /* the next group of the timed schedule: the smallest end time of its next
@@ -1163,7 +1195,7 @@ static int timed_next(const int *count, const int *done, int k_lo, int k_hi)
    double tb = 0.0;
    for (int c = k_lo; c < k_hi; c++) {
       if (done[c]) continue;
-      const double t = (double)(__atomic_load_n(&count[c], __ATOMIC_ACQUIRE) + 1) * g_async_dur[c];
+      const double t = timed_end(c, __atomic_load_n(&count[c], __ATOMIC_ACQUIRE));
       if (best < 0 || t < tb) {
          best = c;
          tb = t;

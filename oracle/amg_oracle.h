@@ -222,6 +222,10 @@ void or_set_async_schedule(int s);
  * corrections run whole, in the order of their end times (j+1) d[k] (ties:
  * the finer group first) -- the race at fixed level speeds */
 void or_set_async_durations(const double *d, int n);
+/* schedule 4 with recorded end times (the replay of a measured race): group
+ * k's j-th correction ends at t[sum(n[0..k-1]) + j]; past n[k] entries its
+ * last interval repeats */
+void or_set_async_times(const double *t, const int *n, int L);
 /* res_compute_type GLOBAL for or_async_add (ASYNC_MULTADD, READ_SOL): nt[0] = 0
  * (no level-0 group), each thread smooths its global fine slice (:35-77, 356-414) */
 void or_set_async_res_global(int on);

@@ -80,6 +80,7 @@ def lib():
         L.or_set_async_gs_threads.argtypes = [C.c_int]
         L.or_set_async_schedule.argtypes = [C.c_int]
         L.or_set_async_durations.argtypes = [_dp, C.c_int]
+        L.or_set_async_times.argtypes = [_dp, _ip, C.c_int]
         L.or_set_async_res_global.argtypes = [C.c_int]
         L.or_set_async_accel.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double]
         L.or_dmem_add.restype = C.c_int
@@ -349,6 +350,13 @@ def set_async_durations(d):
     """or_set_async_durations: per-level correction times of schedule 4 (timed)"""
     d = np.ascontiguousarray(d, dtype=np.float64)
     lib().or_set_async_durations(dptr(d), int(d.size))
+
+
+def set_async_times(times):
+    """or_set_async_times: times[k] = end times of level k's corrections (schedule 4 replay)"""
+    n = np.array([len(t) for t in times], dtype=np.int32)
+    flat = np.ascontiguousarray(np.concatenate([np.asarray(t, dtype=np.float64) for t in times] + [np.zeros(1)]))
+    lib().or_set_async_times(dptr(flat), iptr(n), int(n.size))
 
 
 def make_opts(solver=OR_MULT, smoother=OR_JACOBI, num_pre=1, num_post=1, num_fine=1,

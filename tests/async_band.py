@@ -123,11 +123,32 @@ def durations_of(level_ms, counts, L):
     return d
 
 
+def times_of(corr_ms, L, ranks=None):
+    """the recorded end times of a device free race's corrections, per level
+    (corr_ms: async_correction_ms() of one hierarchy, or a list of them, one
+    per rank -- a distributed correction ends on its slowest rank); the
+    reference's idle coarsest group (no device group under LOCAL residuals)
+    takes the coarsest correcting level's times"""
+    per = corr_ms if isinstance(corr_ms[0], (list, tuple)) else [corr_ms]
+    out = []
+    for k in range(L):
+        rows = [np.asarray(r[k], dtype=np.float64) for r in per]
+        n = min(len(x) for x in rows)
+        out.append(np.max(np.array([x[:n] for x in rows]), axis=0) if n else np.zeros(0))
+    if len(out[L - 1]) == 0:
+        for k in range(L - 2, -1, -1):
+            if len(out[k]):
+                out[L - 1] = out[k].copy()
+                break
+    return out
+
+
 def timed_band(amg, oracle, host, f, opts, durations, blocks=None, composed=False, nt=None):
     """The oracle's model of a device free race: or_async_add under the timed
     schedule (or_set_async_schedule 4: whole corrections in the order of their
-    end times at fixed per-level speeds) with each duration set the device
-    measured (durations_of of its runs).  Returns (lo, hi, rels): the device's
+    end times) -- the replay of the update order each device run recorded
+    (times_of: every correction's end event), or the race at the fixed
+    per-level speeds it measured (durations_of).  Returns (lo, hi, rels): the device's
     free race must lie in [0.5 lo, 2 hi] (in_band) -- the window of the race's
     jitter around its model, instead of the band of every speed ratio."""
     L = len(host["A"])
@@ -146,8 +167,10 @@ def timed_band(amg, oracle, host, f, opts, durations, blocks=None, composed=Fals
         accel = (opts.accel_type, min(opts.cheby_grid, L - 2), opts.cheby_mu, opts.cheby_delta)
     rels = []
     for d in durations:
-        d = np.ascontiguousarray(d, dtype=np.float64)
-        oracle.lib().or_set_async_durations(d.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), int(d.size))
+        if isinstance(d, list):  # recorded end times per level (times_of): the replay
+            oracle.set_async_times(d)
+        else:  # per-level correction times (durations_of)
+            oracle.set_async_durations(d)
         oracle.lib().or_set_async_schedule(4)
         try:
             u, rel, cnt = OH.async_add(f, nt or ([0 if gres else 1] + [1] * (L - 1)), async_type=at,

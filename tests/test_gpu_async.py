@@ -19,7 +19,7 @@ converge GLOBAL also checks the per-level correction counts."""
 import numpy as np
 import pytest
 
-from async_band import blocks64, durations_of, in_band, oracle_async_band, timed_band
+from async_band import blocks64, in_band, oracle_async_band, timed_band, times_of
 from test_gpu_solve import hierarchy, gpu_hier, oracle_opts
 
 pytestmark = pytest.mark.gpu
@@ -94,7 +94,7 @@ def test_async_options_band(amg, oracle, ctx, setup, case):
         u, rel, cnt = H.async_solve(f)
         assert np.all(np.isfinite(u))
         rels.append(rel)
-        durs.append(durations_of(H.async_level_ms(), cnt, L))
+        durs.append(times_of(H.async_correction_ms(), L))
         # correcting levels: [k_lo, k_hi); GLOBAL residuals replace level 0's
         # group by the sliced fine smoothing (SMEM_Setup.cpp:609-615)
         # (and the coarsest level's group runs: it smooths its slice)
@@ -111,14 +111,15 @@ def test_async_options_band(amg, oracle, ctx, setup, case):
             assert np.all(cnt[k_lo:k_hi] == N), cnt
     H.free()
     blocks = blocks64(host) if sm == amg.AMG_HYBRID_JGS else None
-    # the oracle's model of each device run: the race at the level speeds the
-    # device measured (or_async_add under the timed schedule)
+    # the oracle's model of each device run: the replay of the order in which
+    # its corrections ended (or_async_add under the timed schedule with the
+    # recorded end times)
     lo, hi, trels = timed_band(amg, oracle, host, f, opts, durs, blocks=blocks)
     # for the record: the oracle's own free races on this container's threads
     # (every speed ratio the OS happens to give; not the acceptance window)
     flo, fhi, orels, _ = oracle_async_band(amg, oracle, host, f, opts, reps=4, blocks=blocks)
-    print(f"{'-'.join(case)}: timed-model band [{lo:.4e}, {hi:.4e}] (width {hi / lo:.2f}x) from device "
-          f"durations {[np.round(d, 4).tolist() for d in durs]}; device relres {rels}, max corrections {cmax}; "
+    print(f"{'-'.join(case)}: replay band [{lo:.4e}, {hi:.4e}] (width {hi / lo:.2f}x) of the recorded "
+          f"update orders; device relres {rels}, max corrections {cmax}; "
           f"oracle free races [{flo:.3e}, {fhi:.3e}] ({fhi / flo:.1f}x)")
     assert sync_rel < 1.0
     assert hi / lo <= 20.0, (lo, hi)
@@ -373,3 +374,52 @@ def test_composed_transfers_zero_sweeps_bitwise(amg, oracle, ctx, setup, pre, po
     nd = int(np.count_nonzero(u.view(np.uint64) != uo.view(np.uint64)))
     print(f"composed pre {pre} post {post} {mode}: differing entries {nd}")
     assert nd == 0
+
+
+@pytest.mark.parametrize("case", [CASES[1], CASES[4], CASES[7]], ids=["jacobi-full-res", "jacobi-semi-gres",
+                                                                      "jacobi-convglobal"])
+def test_async_replay_bitwise(amg, oracle, ctx, setup, case):
+    """the replay of a free race: the device records the end of every
+    correction (async_correction_ms); AMG_SCHED_TIMED with those end times
+    (amg_hier_set_async_times) re-runs the corrections in that order on one
+    stream, bit-identical to the oracle's or_async_add under schedule 4 with
+    the same times (or_set_async_times) -- the model the free-race checks
+    compare against"""
+    solver, smoother, at, rt, rc, ct = case
+    L, mult, afacx, f = setup
+    host = mult
+    kw = dict(solver=amg.AMG_ASYNC_MULTADD, smoother=amg.AMG_JACOBI, smooth_weight=W, num_cycles=N, tol=0.0,
+              async_type=amg.AMG_SEMI_ASYNC if at == "semi" else amg.AMG_FULL_ASYNC,
+              read_type=amg.AMG_READ_RES if rt == "res" else amg.AMG_READ_SOL,
+              res_compute_type=amg.AMG_GLOBAL if rc == "global" else amg.AMG_LOCAL,
+              converge_test_type=amg.AMG_GLOBAL if ct == "global" else amg.AMG_LOCAL)
+    opts = amg.default_opts(**kw)
+    H, _ = gpu_hier(amg, ctx, host, opts)
+    _, rel_free, cnt_free = H.async_solve(f)
+    times = times_of(H.async_correction_ms(), L)
+    H.free()
+    opts = amg.default_opts(async_schedule=4, **kw)
+    H, _ = gpu_hier(amg, ctx, host, opts)
+    H.set_async_times(times)
+    u, rel, cnt = H.async_solve(f)
+    H.free()
+    gres = rc == "global"
+    oracle.set_async_times(times)
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    oracle.lib().or_set_async_schedule(4)
+    try:
+        uo, relo, cnto = OH.async_add(
+            f, [0 if gres else 1] + [1] * (L - 1),
+            async_type=oracle.OR_SEMI_ASYNC if at == "semi" else oracle.OR_FULL_ASYNC,
+            converge_type=oracle.OR_CONVERGE_GLOBAL if ct == "global" else oracle.OR_CONVERGE_LOCAL,
+            read_type=oracle.OR_READ_RES if rt == "res" else oracle.OR_READ_SOL, res_global=gres)
+    finally:
+        oracle.lib().or_set_async_schedule(0)
+    k_lo = 1 if gres else 0
+    k_hi = L if gres else L - 1
+    nd = int(np.count_nonzero(u.view(np.uint64) != uo.view(np.uint64)))
+    print(f"replay {'-'.join(case)}: free race {rel_free:.6e} (counts {list(cnt_free)}), device replay {rel:.13e}, "
+          f"oracle {relo:.13e}, counts {list(cnt[k_lo:k_hi])} / {list(cnto[k_lo:k_hi])}, differing {nd}")
+    assert list(cnt[k_lo:k_hi]) == list(cnto[k_lo:k_hi])
+    assert nd == 0
+    assert in_band(rel_free, relo, relo)

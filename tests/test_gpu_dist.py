@@ -316,14 +316,14 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
         out = []
         for _ in range(2):
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-            out.append((rel, D.get_u(), cnt.copy(), D.async_level_ms()))
+            out.append((rel, D.get_u(), cnt.copy(), D.async_correction_ms()))
         D.free()
         amg.dist.finalize(c)
         c.close()
         return out
 
     res = run_ranks(nranks, rank)
-    from async_band import durations_of, in_band, timed_band
+    from async_band import in_band, timed_band, times_of
     rels, durs = [], []
     for q in range(2):
         rq = [t[q][0] for t in res]
@@ -334,13 +334,13 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
         assert list(cnt[:L - 1]) == [N] * (L - 1)
         assert rq[0] < 1.0
         rels.append(rq[0])
-        durs.append(durations_of(np.max(np.array([t[q][3] for t in res]), axis=0), cnt, L))
-    # the oracle's model of each run: the race at the level speeds the device
-    # measured (slowest rank per level), or_async_add under the timed schedule
+        durs.append(times_of([t[q][3] for t in res], L))
+    # the oracle's model of each run: the replay of its recorded update order
+    # (every correction's end, slowest rank), or_async_add under the timed schedule
     # (the arithmetic itself is pinned by test_dist_async_schedule_bitwise)
     lo, hi, _ = timed_band(amg, oracle, host, f, opts, durs)
-    print(f"dist async {solver} {nranks} ranks: timed-model band [{lo:.4e}, {hi:.4e}] (width {hi / lo:.2f}x), "
-          f"sync {sync_rel:.4e}, device {rels}, durations {[np.round(d, 3).tolist() for d in durs]}")
+    print(f"dist async {solver} {nranks} ranks: replay band [{lo:.4e}, {hi:.4e}] (width {hi / lo:.2f}x), "
+          f"sync {sync_rel:.4e}, device {rels}, level finish ms {[[round(float(t[-1]), 3) for t in d] for d in durs]}")
     assert hi / lo <= 20.0
     for rel in rels:
         assert in_band(rel, lo, hi), (rel, lo, hi, sync_rel)
@@ -609,7 +609,7 @@ def test_dist_async_additive_accel(amg, oracle, solver, accel, cuts, grid, bound
             D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
             u = D.get_u()
-            ms = D.async_level_ms()
+            ms = D.async_correction_ms()
             D.free()
             amg.dist.finalize(c)
             c.close()
@@ -618,16 +618,16 @@ def test_dist_async_additive_accel(amg, oracle, solver, accel, cuts, grid, bound
         res = run_ranks(nranks, rank)
         assert all(t[0] == res[0][0] for t in res)
         assert all(np.all(np.isfinite(t[1])) for t in res)
-        return res[0][0], durations_of(np.max(np.array([t[3] for t in res]), axis=0), res[0][2], L)
+        return res[0][0], times_of([t[3] for t in res], L)
 
-    from async_band import durations_of, in_band, timed_band
+    from async_band import in_band, timed_band, times_of
     (rel_acc, d_acc), (rel_plain, _) = solve(acc), solve(amg.AMG_NO_ACCEL)
     assert rel_acc < 1.0
     opts = amg.default_opts(solver=a_solver, smooth_weight=w, num_cycles=N, tol=0.0, accel_type=acc,
                             cheby_mu=mu, cheby_delta=delta, cheby_grid=grid)
-    # the oracle's model of the run: the race at the level speeds the device
-    # measured, with the same ChebyUpdate per level group (timed schedule)
+    # the oracle's model of the run: the replay of its recorded update order,
+    # with the same ChebyUpdate per level group (timed schedule)
     lo, hi, _ = timed_band(amg, oracle, host, f, opts, [d_acc])
-    print(f"dist async {solver} {accel} grid {grid}: timed-model {lo:.4e}, device {rel_acc:.4e} "
-          f"(no accel {rel_plain:.4e}), durations {np.round(d_acc, 3).tolist()}")
+    print(f"dist async {solver} {accel} grid {grid}: replay {lo:.4e}, device {rel_acc:.4e} "
+          f"(no accel {rel_plain:.4e})")
     assert in_band(rel_acc, lo, hi), (rel_acc, lo, hi, rel_plain)

@@ -13,7 +13,8 @@ Setup exchanges (plans, handles, the final norm) go over gloo (TorchGroupHub).
   bit-identical to the oracle's or_async_add under the same schedule (and so
   to the thread-rank run of tests/test_gpu_slab_async.py), for two solves in a
   row on the same channels (the slots are reused: a stale read would show).
-* The free race converges into the oracle's asynchronous band.
+* The free race lands within [0.5x, 2x] of the oracle's replay of its recorded
+  update order.
 """
 import os
 import socket
@@ -51,7 +52,7 @@ def _rank(rank, world, port, n, optd, rep, runs, q):
         for _ in range(runs):
             dist.barrier()  # the ranks enter the solve together
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-            out.append((float(rel), [int(x) for x in cnt], D.get_u(), [float(x) for x in D.async_level_ms()]))
+            out.append((float(rel), [int(x) for x in cnt], D.get_u(), [t.tolist() for t in D.async_correction_ms()]))
         row0 = D.row0
         D.free()
         amg.dist.finalize(c)
@@ -96,8 +97,7 @@ def slab_async_procs(n, optd, world, rep=1 << 10, runs=1):
         rel = got[0][2][k][0]
         assert all(got[r][2][k][0] == rel for r in range(world))  # one allreduced norm
         u = np.concatenate([got[r][2][k][2] for r in order])
-        ms = np.max(np.array([got[r][2][k][3] for r in range(world)]), axis=0)  # slowest rank per level
-        out.append((rel, got[0][2][k][1], u, ms))
+        out.append((rel, got[0][2][k][1], u, [got[r][2][k][3] for r in range(world)]))  # per rank
     return out
 
 
@@ -154,9 +154,9 @@ def test_slab_async_processes_free_race(amg, oracle):
     """the free race with one process per rank (2 and 3 processes, 48^3,
     composed MULTADD): every level runs num_cycles corrections, the iterate is
     finite and the relative residual lies within [0.5x, 2x] of the oracle's
-    model of the race at the level speeds the processes measured (or_async_add
-    under the timed schedule, slowest rank per level)"""
-    from async_band import durations_of, in_band, timed_band
+    replay of the update order the processes recorded (or_async_add under the
+    timed schedule with every correction's end time, slowest rank)"""
+    from async_band import in_band, timed_band, times_of
     from test_gpu_slab_async import host_hier
     n, N = 48, 12
     optd = _optd(amg, "multadd", True, N, 0)
@@ -172,11 +172,12 @@ def test_slab_async_processes_free_race(amg, oracle):
         for rel, cnt, u, ms in runs:
             assert list(cnt[:L - 1]) == [N] * (L - 1)
             assert np.all(np.isfinite(u))
-            durs.append(durations_of(ms, cnt, L))
+            durs.append(times_of(ms, L))
         lo, hi, _ = timed_band(amg, oracle, host, f, opts, durs, composed=True)
         rels = [r[0] for r in runs]
-        print(f"  {world} processes: device relres {[f'{r:.4e}' for r in rels]}; timed-model band "
-              f"[{lo:.4e}, {hi:.4e}] (width {hi / lo:.2f}x), durations {[np.round(d, 3).tolist() for d in durs]}")
+        print(f"  {world} processes: device relres {[f'{r:.4e}' for r in rels]}; replay band "
+              f"[{lo:.4e}, {hi:.4e}] (width {hi / lo:.2f}x), level finish ms "
+              f"{[[round(float(t[-1]), 2) for t in d] for d in durs]}")
         assert hi / lo <= 20.0
         for rel in rels:
             assert in_band(rel, lo, hi), (world, rel, (lo, hi))

@@ -351,6 +351,16 @@ def test_async_add_timed_schedule(amg, oracle, ct):
     d = np.array([3.0 / (1.9 ** k) + 0.05 for k in range(L)])
     a, b = run(4, d), run(4, d)
     assert same(a, b)
+    # the recorded-times form (or_set_async_times) of the same end times, also
+    # through the repeated last interval past a short table
+    for m in (N + 2, 3):
+        oracle.set_async_times([d[k] * np.arange(1, m + 1) for k in range(L)])
+        oracle.lib().or_set_async_schedule(4)
+        try:
+            c = OH.async_add(f, [1] * L, async_type=oracle.OR_FULL_ASYNC, converge_type=conv)
+        finally:
+            oracle.lib().or_set_async_schedule(0)
+        assert same(a, c)
     assert a[1] < 0.1, a[1]
     if ct == "local":
         assert list(a[2][:L]) == [N] * L
