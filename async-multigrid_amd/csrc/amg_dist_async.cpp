@@ -355,7 +355,10 @@ int cheby_grid_of(const amg_dist_hier *D)
 }
 
 // one correction of level k (SMEM_Async_Add_AMG inner body / DMEM AddCycle)
-int level_correction(amg_dist_hier *D, int k)
+// j >= 0 (free race): record the correction's update point -- the atomic add
+// into the shared slab, where it reads and writes the shared iterate -- as
+// its end event (amg_dist_async_correction_ms)
+int level_correction(amg_dist_hier *D, int k, int j = -1)
 {
    AsyncLevel &a = D->al[k];
    const amg_opts &o = D->o;
@@ -400,6 +403,7 @@ int level_correction(amg_dist_hier *D, int k)
    }
    // correction into the shared slab; u_priv = the value each row saw
    if (!fuse_corr) amgk::atomic_correct(s, D->lv[0].u, a.e[0], a.u_priv, n0);
+   if (j >= 0 && D->corr.record(k, j, s)) return amg_set_error(AMG_ERR_HIP, "level %d: correction event", k);
    // private residual r_k = f - A u_k  (SMEM_Residual on u_k)
    AMG_TRY(a_spgemv(D, a, D->lv[0].A, a.u_priv, nullptr, amgk::gemv_mode(1.0, 0.0), a.y));
    amgk::vsub(s, D->lv[0].f, a.y, a.r[0], 0, n0);
@@ -677,9 +681,9 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
       D->al[k].acc.reset(D->o);
    }
    // one correction of level k (DMEM_DelayProc before AddCycle, DMEM_Add.cpp:106)
-   auto correct = [&](int k) -> int {
+   auto correct = [&](int k, int j = -1) -> int {
       if (D->o.delay_level < 0 || D->o.delay_level == k) dist_delay(D, D->al[k].s);
-      return level_correction(D, k);
+      return level_correction(D, k, j);
    };
    const int N = D->o.num_cycles;
    std::vector<int> st(active, AMG_OK);
@@ -691,11 +695,7 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
       for (int k = 0; k < active; k++)
          th.emplace_back([&, k] {
             hipSetDevice(c->device);
-            for (int cyc = 0; cyc < N && st[k] == AMG_OK; cyc++) {
-               st[k] = correct(k);
-               if (st[k] == AMG_OK && D->corr.record(k, cyc, D->al[k].s))
-                  st[k] = amg_set_error(AMG_ERR_HIP, "level %d: correction event", k);
-            }
+            for (int cyc = 0; cyc < N && st[k] == AMG_OK; cyc++) st[k] = correct(k, cyc);
             // the level's finish: its stream reaches this marker after its last
             // correction (recorded here, not after the join, so a level that is
             // done early is not stamped with the slowest level's time)

@@ -1402,6 +1402,15 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    // converge GLOBAL under round robin: the correction about to run is the
    // group's last (it sees the converge flag at its barrier)
    bool rr_last = false;
+   // graphs of the level corrections (ctx->graphs): the FULL_ASYNC / READ_SOL /
+   // LOCAL-residual correction issues the same kernels with the same
+   // arguments every time (no delays, no profiling events), so each level's
+   // is captured once per stream and replayed
+   const bool graphs = c->graphs && !semi && !read_res && !global_res && !H->o.profile &&
+                       (o.delay_type == AMG_DELAY_NONE || o.delay_usec <= 0);
+   // free race without graphs: record each correction's update point (the
+   // atomic add / the exclusive update of the shared vectors) as its end event
+   const bool rec = sched == AMG_SCHED_FREE && !graphs;
    // one correction of level k, issued on its stream
    auto correction = [&](int k) -> int {
       hipStream_t s = lstream(k);
@@ -1441,6 +1450,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
             amgk::vaxpy(s, 1.0, a.e[0], a.f_acc, 0, n0);
             amgk::res_update(s, H->r0, a.y, a.y_fine, n0, 1);
          }
+         if (rec && H->corr.record(k, issued[k], s)) return amg_set_error(AMG_ERR_HIP, "correction event");
       } else {
          if (semi) {
             AMG_TRY(to_update());
@@ -1450,6 +1460,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          } else if (!fused) {
             amgk::atomic_correct(s, v0.u, a.e[0], a.u_priv, n0);
          }
+         if (rec && H->corr.record(k, issued[k], s)) return amg_set_error(AMG_ERR_HIP, "correction event");
          if (!global_res) {
             // SMEM_Residual(A0, f, u_k, y, r_k): y = A u_k; r = f - y (one pass, y unused)
             amgk::residual_fsub(s, v0.A, a.u_priv, v0.f, a.y, a.y_fine, n0);
@@ -1476,12 +1487,6 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       AMG_HIP(hipGetLastError());
       return AMG_OK;
    };
-   // graphs of the level corrections (ctx->graphs): the FULL_ASYNC / READ_SOL /
-   // LOCAL-residual correction issues the same kernels with the same
-   // arguments every time (no delays, no profiling events), so each level's
-   // is captured once per stream and replayed
-   const bool graphs = c->graphs && !semi && !read_res && !global_res && !H->o.profile &&
-                       (o.delay_type == AMG_DELAY_NONE || o.delay_usec <= 0);
    if (graphs) graphs_check(H);
    if (graphs && (int)H->g_lev.size() != L) graphs_reset(H);
    auto run = [&](int k) -> int {
@@ -1583,8 +1588,6 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       for (int cyc = 0; cyc < o.num_cycles; cyc++)
          for (int k = k_lo; k < k_hi; k++) {
             AMG_TRY(run(k));
-            if (sched == AMG_SCHED_FREE && H->corr.record(k, issued[k], lstream(k)))
-               return amg_set_error(AMG_ERR_HIP, "amg_async_solve: correction event");
             issued[k]++;
          }
    } else {
@@ -1618,10 +1621,6 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          for (int k = k_lo; k < k_hi && st == AMG_OK; k++) {
             if (issued[k] - completed[k] < DEPTH && issued[k] < cap) {
                if ((st = run(k)) != AMG_OK) break;
-               if (H->corr.record(k, issued[k], c->level_streams[k])) {
-                  st = amg_set_error(AMG_ERR_HIP, "amg_async_solve: correction event");
-                  break;
-               }
                const hipError_t er = hipEventRecord(done[k][issued[k] % DEPTH], c->level_streams[k]);
                if (er != hipSuccess) {
                   st = amg_set_error(AMG_ERR_HIP, "amg_async_solve: hipEventRecord: %s", hipGetErrorString(er));

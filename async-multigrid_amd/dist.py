@@ -233,6 +233,7 @@ class DistHier:
             check(create(ctx.h, gen.h, C.byref(opts), C.byref(h)))
             _handle = h
         self.h = _handle
+        self.L = gen.L if gen is not None else None
         self.row0, self.n0 = self.local_rows(0)
 
     def slab_info(self):
@@ -260,7 +261,9 @@ class DistHier:
         check(lib.amg_dist_hier_create(ctx.h, L, rs.ctypes.data_as(C.POINTER(C.c_longlong)),
                                        C.cast(a, C.c_void_p), C.cast(p, C.c_void_p),
                                        C.cast(r, C.c_void_p), C.byref(opts), C.byref(h)))
-        return cls(ctx, None, opts, _handle=h)
+        D = cls(ctx, None, opts, _handle=h)
+        D.L = L
+        return D
 
     def matrix_info(self, level):
         """(local nnz, value-index table size, dictionary size, row patterns) of
@@ -321,8 +324,7 @@ class DistHier:
     def async_correction_ms(self):
         """per level: end times (ms) of this rank's corrections in the last free-race async_solve"""
         from . import _corr_ms
-        L = self.gen.L if self.gen is not None else len(self.async_level_ms())
-        return _corr_ms(lib.amg_dist_async_correction_ms, self.h, L)
+        return _corr_ms(lib.amg_dist_async_correction_ms, self.h, self.L)
 
     def async_level_ms(self):
         """per level: ms from the last async_solve's start to the level's last correction"""

@@ -143,6 +143,34 @@ def times_of(corr_ms, L, ranks=None):
     return out
 
 
+def replay_tables(corr_ms, L):
+    """the replay tables of one device free race: the update order of the
+    slowest rank (times_of over every rank) and, with several ranks, each
+    rank's own order -- every rank's rows receive the corrections in that
+    rank's order, so a distributed race lies between these replays"""
+    per = corr_ms if isinstance(corr_ms[0], (list, tuple)) else [corr_ms]
+    out = [times_of(per, L)]
+    if len(per) > 1:
+        out += [times_of([r], L) for r in per]
+    return out
+
+
+def replay_check(amg, oracle, host, f, opts, runs, blocks=None, composed=False, what=""):
+    """every device free run (rel, corr_ms) against the oracle's replays of its
+    own recorded update order(s): rel in [0.5 min, 2 max] of those replays.
+    Prints each run's replay range and ratio; returns the widest replay range."""
+    L = len(host["A"])
+    widest = 1.0
+    for i, (rel, corr_ms) in enumerate(runs):
+        lo, hi, rr = timed_band(amg, oracle, host, f, opts, replay_tables(corr_ms, L), blocks=blocks,
+                                composed=composed)
+        widest = max(widest, hi / lo)
+        print(f"  {what} run {i}: device {rel:.4e}, replay [{lo:.4e}, {hi:.4e}] ({len(rr)} order(s), width "
+              f"{hi / lo:.2f}x), device / replay {rel / lo:.2f}-{rel / hi:.2f}")
+        assert in_band(rel, lo, hi), (what, i, rel, lo, hi)
+    return widest
+
+
 def timed_band(amg, oracle, host, f, opts, durations, blocks=None, composed=False, nt=None):
     """The oracle's model of a device free race: or_async_add under the timed
     schedule (or_set_async_schedule 4: whole corrections in the order of their

@@ -18,7 +18,7 @@ device); each rank's level groups run on their own host threads."""
 import numpy as np
 import pytest
 
-from async_band import in_band, oracle_async_band, timed_band, times_of
+from async_band import replay_check
 from test_gpu_dist import run_ranks
 from test_gpu_kernels import assert_bitwise
 
@@ -148,19 +148,12 @@ def test_slab_async_band(amg, oracle, ctx):
     L = gen.L
     for nranks in (1, 2, 3):
         runs = slab_async(amg, gen, opts, f, nranks, rccl1=True, runs=2)
-        durs = []
         for rel, cnt, u, ms in runs:
             assert list(cnt[:L - 1]) == [N] * (L - 1)
             assert np.all(np.isfinite(u))
-            durs.append(times_of(ms, L))
-        lo, hi, trels = timed_band(amg, oracle, host, f, opts, durs, composed=True)
-        rels = [r[0] for r in runs]
-        print(f"  {nranks} rank(s): device relres {[f'{r:.4e}' for r in rels]}; replay band "
-              f"[{lo:.4e}, {hi:.4e}] (width {hi / lo:.2f}x), level finish ms "
-              f"{[[round(float(t[-1]), 2) for t in d] for d in durs]}")
-        assert hi / lo <= 20.0
-        for rel in rels:
-            assert in_band(rel, lo, hi), (nranks, rel, (lo, hi))
+        widest = replay_check(amg, oracle, host, f, opts, [(r[0], r[3]) for r in runs], composed=True,
+                              what=f"slab async {nranks} rank(s)")
+        assert widest <= 20.0
     gen.free()
 
 

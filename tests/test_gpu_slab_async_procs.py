@@ -156,7 +156,7 @@ def test_slab_async_processes_free_race(amg, oracle):
     finite and the relative residual lies within [0.5x, 2x] of the oracle's
     replay of the update order the processes recorded (or_async_add under the
     timed schedule with every correction's end time, slowest rank)"""
-    from async_band import in_band, timed_band, times_of
+    from async_band import replay_check
     from test_gpu_slab_async import host_hier
     n, N = 48, 12
     optd = _optd(amg, "multadd", True, N, 0)
@@ -168,16 +168,9 @@ def test_slab_async_processes_free_race(amg, oracle):
     opts = amg.default_opts(**optd)
     for world in (2, 3):
         runs = slab_async_procs(n, optd, world, rep=1 << 12, runs=2)
-        durs = []
         for rel, cnt, u, ms in runs:
             assert list(cnt[:L - 1]) == [N] * (L - 1)
             assert np.all(np.isfinite(u))
-            durs.append(times_of(ms, L))
-        lo, hi, _ = timed_band(amg, oracle, host, f, opts, durs, composed=True)
-        rels = [r[0] for r in runs]
-        print(f"  {world} processes: device relres {[f'{r:.4e}' for r in rels]}; replay band "
-              f"[{lo:.4e}, {hi:.4e}] (width {hi / lo:.2f}x), level finish ms "
-              f"{[[round(float(t[-1]), 2) for t in d] for d in durs]}")
-        assert hi / lo <= 20.0
-        for rel in rels:
-            assert in_band(rel, lo, hi), (world, rel, (lo, hi))
+        widest = replay_check(amg, oracle, host, f, opts, [(r[0], r[3]) for r in runs], composed=True,
+                              what=f"slab async {world} processes")
+        assert widest <= 20.0
