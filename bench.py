@@ -38,6 +38,10 @@ def parse():
     p.add_argument("--reuse-outer-residual", type=int, default=2)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-cycles", type=int, default=20)
+    p.add_argument("--general", type=int, default=1,
+                   help="also time the general (plain-CSR, CSR-transfer) V-cycle on the same 512^3 solve")
+    p.add_argument("--seq-cycles", type=int, default=200,
+                   help="outer iterations of the config-1 (64^3) SEQ leg on one core, and of its GPU rate")
     p.add_argument("--spmv-reps", type=int, default=20)
     p.add_argument("--force-dist", type=int, default=0,
                    help="run the distributed (RCCL) path even at one rank")
@@ -125,6 +129,157 @@ def fine_kernels(n0, mat_bytes, ms, launches, fused, fmt, fused_prolong=0):
     return res
 
 
+def host_info():
+    """the host CPU the baseline ran on (model, cores, binding)"""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count()
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": avail,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"),
+            "OMP_PLACES": os.environ.get("OMP_PLACES")}
+
+
+def seq_baseline(amg, args):
+    """Config 1 (SEQ_AMG 64^3, sync Jacobi V-cycle on CPU): the oracle's loops on
+    ONE thread (or_set_threads(1): the SEQ configuration of BASELINE.md Sec.3)
+    for args.seq_cycles outer iterations, beside the GPU's rate on the same
+    64^3 solve (HIP path, same hierarchy / RHS / options)."""
+    from oracle import pyoracle as po
+    n = 64
+    gen = amg.Gen(n, interp=amg.AMG_INTERP_LINEAR)
+    L = gen.L
+    host = {tag: [po.Csr(*gen.host_csr(code, l)) for l in range(cnt)]
+            for tag, code, cnt in (("A", amg.AMG_GEN_A, L), ("P", amg.AMG_GEN_P, L - 1), ("R", amg.AMG_GEN_R, L - 1))}
+    f = amg.rhs_rand(0, n ** 3)
+    po.lib().or_set_threads(1)
+    try:
+        opts = po.make_opts(smooth_weight=args.smooth_weight, num_cycles=args.seq_cycles, tol=0.0, num_threads=1)
+        u, hist, k = po.Hier(host["A"], host["P"], host["R"], opts).solve(f)
+        secs = po.lib().or_last_loop_seconds()
+    finally:
+        po.lib().or_set_threads(max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    gen.free()
+    return {"value": k / secs, "unit": "V-cycle iters/s", "cores": 1, "kind": "port",
+            "sample": f"config 1: {k} outer iterations (V(1,1) Jacobi w={args.smooth_weight} + residual + norm) "
+                      f"of the {n}^3 7-pt solve ({L}-level geometric Galerkin hierarchy), oracle/amg_oracle.c "
+                      "loops on one thread", "seconds": secs, "relres": float(hist[-1] / hist[0])}
+
+
+def gpu_config1(amg, args):
+    """the GPU's rate on config 1's 64^3 solve (the SEQ leg's workload)"""
+    n = 64
+    ctx = amg.Context(device=0, nstreams=4)
+    gen = amg.Gen(n, interp=amg.AMG_INTERP_LINEAR)
+    L = gen.L
+    As = [gen.register(ctx, amg.AMG_GEN_A, l) for l in range(L)]
+    Ps = [gen.register(ctx, amg.AMG_GEN_P, l) for l in range(L - 1)]
+    Rs = [gen.register(ctx, amg.AMG_GEN_R, l) for l in range(L - 1)]
+    opts = amg.default_opts(smooth_weight=args.smooth_weight, num_cycles=1 << 30, tol=0.0,
+                            reuse_outer_residual=args.reuse_outer_residual)
+    H = amg.Hier(ctx, As, Ps, Rs, opts)
+    f = ctx.vec(amg.rhs_rand(0, n ** 3))
+    u0 = ctx.vec(n ** 3)
+    r0 = H.solve_start(f, u0)
+    H.iterate(20)
+    ctx.sync()
+    t1 = time.perf_counter()
+    H.iterate(args.seq_cycles)
+    ctx.sync()
+    dt = time.perf_counter() - t1
+    rel = H.resnorm() / r0
+    H.free()
+    for M in As + Ps + Rs:
+        M.free()
+    gen.free()
+    ctx.close()
+    return {"value": args.seq_cycles / dt, "unit": "V-cycle iters/s", "steps": args.seq_cycles,
+            "relres_after_warmup_and_steps": rel, "workload": f"config 1 ({n}^3) on the GPU"}
+
+
+def general_csr_vcycle(amg, gen, f_host, args):
+    """The same 512^3 solve on the GENERAL path -- the one a BoomerAMG or
+    elasticity hierarchy takes: every operator in plain CSR (no value index,
+    dictionary, row / pair / master patterns, no plane march) and the transfers
+    as CSR SpMVs (no geometric kernels, no fused residual + restriction):
+    csr_tile_kernel for every SpMV / residual / sweep (SMEM_MatVec.cpp:95-259,
+    SMEM_Smooth.cpp:6-49).  Timed like the headline (HIP events per fine
+    kernel on the compute stream), with its own dominant-kernel roofline on the
+    CSR bytes of SURVEY.md Sec.8(d) (12 nnz + 28 n for a residual / sweep)."""
+    n = args.n
+    ctx = amg.Context(device=0, nstreams=4)
+    for fn in (ctx.set_value_index, ctx.set_dict_index, ctx.set_row_pattern, ctx.set_pair_pattern,
+               ctx.set_master_pattern, ctx.set_fuse_transfer):
+        fn(0)
+    ctx.set_plane_march(0)
+    t0 = time.time()
+    L = gen.L
+    As = [gen.register(ctx, amg.AMG_GEN_A, l) for l in range(L)]
+    Ps = [gen.register(ctx, amg.AMG_GEN_P, l) for l in range(L - 1)]
+    Rs = [gen.register(ctx, amg.AMG_GEN_R, l) for l in range(L - 1)]
+    assert As[0].value_index == 0 and As[0].plane_march == 0
+    opts = amg.default_opts(smooth_weight=args.smooth_weight, num_cycles=1 << 30, tol=0.0,
+                            reuse_outer_residual=args.reuse_outer_residual, profile=1)
+    H = amg.Hier(ctx, As, Ps, Rs, opts)
+    assert H.fused == 0
+    f = ctx.vec(f_host)
+    u0 = ctx.vec(n ** 3)
+    r0 = H.solve_start(f, u0)
+    H.iterate(args.warmup)
+    ctx.sync()
+    H.profile(reset=True)
+    t1 = time.perf_counter()
+    H.iterate(args.steps)
+    ctx.sync()
+    dt = time.perf_counter() - t1
+    rel = H.resnorm() / r0
+    ms, launches = H.profile(reset=True)
+    n0, z0 = As[0].nrows, As[0].nnz
+    zP, zR, nc = Ps[0].nnz, Rs[0].nnz, As[1].nrows
+    def per(c):
+        return ms[c] / launches[c] if launches[c] else None
+    # algorithmic CSR bytes per launch (DESIGN.md Sec.4 table, b = 12)
+    kern = {"outer_residual_sweep": (per(4), 12 * z0 + 36 * n0, "outer residual + norm fused with the next "
+                                     "first Jacobi sweep, plain CSR (reads f, u; writes r... u_next)"),
+            "post_sweep": (per(1), 12 * z0 + 28 * n0, "post-smoothing Jacobi sweep, plain CSR"),
+            "residual": (per(0), 12 * z0 + 28 * n0, "level-0 residual r = f - A u, plain CSR"),
+            "restrict0": (per(2), 12 * zR + 4 * nc + 8 * n0 + 8 * nc, "R0 restriction SpMV, plain CSR"),
+            "prolong0": (per(3), 12 * zP + 28 * n0 + 8 * nc, "P0 prolongation + correction u += P0 e, plain CSR")}
+    if args.reuse_outer_residual >= 2:
+        kern["outer_residual_sweep"] = (per(4), 12 * z0 + 28 * n0, kern["outer_residual_sweep"][2]
+                                        .replace("r... ", ""))
+    res = {}
+    for k, (t, b, what) in kern.items():
+        if t is None:
+            continue
+        gbs = b / (t * 1e-3) / 1e9
+        res[k] = {"ms": t, "bytes": b, "gbs": gbs, "frac": gbs / HBM_PEAK_GBS, "what": what}
+    dom = max(res, key=lambda k: res[k]["ms"])
+    out = {"value": args.steps / dt, "unit": "V-cycle iters/s", "ms_per_step": dt * 1e3 / args.steps,
+           "steps": args.steps, "relres": rel, "setup_s": time.time() - t0 - dt,
+           "workload": f"{n}^3 7-pt, the headline's solve with every operator plain CSR and CSR transfers "
+                       "(compressed forms, plane march and geometric / fused transfers off)",
+           "fine_kernels": res,
+           "roofline": {"bound": "hbm", "kernel": f"{dom}: {res[dom]['what']}", "achieved": res[dom]["gbs"],
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": res[dom]["frac"],
+                        "alg_bytes_per_launch": res[dom]["bytes"], "avg_launch_ms": res[dom]["ms"]}}
+    log(f"[general] plain-CSR V-cycle {out['value']:.1f} it/s ({out['ms_per_step']:.2f} ms/step); dominant "
+        f"{dom} {res[dom]['ms']:.3f} ms = {res[dom]['frac']:.3f} of peak")
+    H.free()
+    for M in As + Ps + Rs:
+        M.free()
+    ctx.close()
+    return out
+
+
 def cpu_baseline(gen, amg, f, args):
     """The oracle (C restatement of SMEM_Solve, OpenMP) on the host cores, on a
     bounded sample of the same workload: args.cpu_cycles outer iterations of
@@ -146,7 +301,7 @@ def cpu_baseline(gen, amg, f, args):
     return ({"value": k / secs, "unit": "V-cycle iters/s", "cores": threads, "kind": "port",
              "sample": f"{k} outer iterations (V(1,1) Jacobi + residual + norm) of the same "
                        f"{args.n}^3 solve, oracle/amg_oracle.c OpenMP, {threads} threads",
-             "seconds": secs}, u, hist[-1] / hist[0])
+             "seconds": secs, "host": host_info()}, u, hist[-1] / hist[0])
 
 
 def check_parity(u_par, u_cpu, rel_cpu, cycles):
@@ -304,8 +459,23 @@ def main():
         M.free()
     ctx.close()
 
-    cpu, parity = None, None
+    vgen = None
+    if args.general:
+        try:
+            vgen = general_csr_vcycle(amg, gen, f_host, args)
+        except Exception as e:  # noqa: BLE001
+            log(f"[general] failed: {e!r}")
+    cpu, parity, seq = None, None, None
     if args.cpu_baseline:
+        # OMP_PROC_BIND=close for the SMEM leg; read by
+        # libgomp when the oracle library loads, which happens below
+        os.environ.setdefault("OMP_PROC_BIND", "close")
+        try:
+            seq = {"cpu": seq_baseline(amg, args), "gpu": gpu_config1(amg, args)}
+            seq["gpu_over_cpu"] = seq["gpu"]["value"] / seq["cpu"]["value"]
+            log(f"[seq] config 1 (64^3): CPU 1 core {seq['cpu']['value']:.2f} it/s, GPU {seq['gpu']['value']:.1f} it/s")
+        except Exception as e:  # noqa: BLE001
+            log(f"[seq] config-1 leg failed: {e!r}")
         try:
             cpu, u_cpu, rel_cpu = cpu_baseline(gen, amg, f_host, args)
             log(f"[cpu] {cpu['value']:.4f} it/s on {cpu['cores']} threads")
@@ -346,6 +516,8 @@ def main():
         "roofline": roofline,
         "fine_kernels": kernels,
         "cpu_baseline": cpu,
+        "cpu_baseline_seq": seq,
+        "vcycle_general_csr": vgen,
         "parity": parity,
         "final_relres": rn / r0,
     }

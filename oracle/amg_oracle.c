@@ -26,6 +26,17 @@
 
 #define OMP_MIN_ROWS 32768
 
+/* OpenMP threads of the parallel loops (omp_set_num_threads; the CPU
+ * baseline's SEQ leg runs the same loops on one thread) */
+void or_set_threads(int t)
+{
+#ifdef _OPENMP
+   if (t > 0) omp_set_num_threads(t);
+#else
+   (void)t;
+#endif
+}
+
 int or_num_threads(void)
 {
 #ifdef _OPENMP

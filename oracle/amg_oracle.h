@@ -258,6 +258,7 @@ int or_hier_levels(or_hier *H);
 double or_last_loop_seconds(void);
 /* number of OpenMP threads the oracle loops use (cpu_baseline "cores") */
 int or_num_threads(void);
+void or_set_threads(int t);
 
 #ifdef __cplusplus
 }

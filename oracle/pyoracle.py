@@ -72,6 +72,7 @@ def lib():
         L.or_hier_vec.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
         L.or_eigs_power.argtypes = [C.c_void_p, C.c_int, _dp, _dp]
         L.or_num_threads.restype = C.c_int
+        L.or_set_threads.argtypes = [C.c_int]
         L.or_last_loop_seconds.restype = C.c_double
         L.or_dmem_cheby_update.argtypes = [_dp, _dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
                                            C.c_double, _dp]
