@@ -1682,6 +1682,175 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
    return 0;
 }
 
+/* Replay of a DISTRIBUTED free race (the row-sliced event model of
+ * amg_dist_async_solve, FULL_ASYNC / READ_SOL / LOCAL residuals, converge
+ * LOCAL).  Every rank holds slice [rs[r], rs[r+1]) of the fine rows; level k's
+ * correction j is one collective computation (its restrictions, smoothing and
+ * prolongations exchange halos inside level k only), but its update of the
+ * shared iterate -- u += e on the slice, the private copy u_k = u there -- runs
+ * on every rank at that rank's own time t[k][j][r], in between the other
+ * levels' updates of the same slice, and the level's next residual
+ * r_k = f - A u_k takes each slice from its own rank's copy.  The replay
+ * applies the slice updates in the order of the recorded times (ties: lower
+ * level, then lower rank) and forms e_{k,j} from r_k as left by every slice of
+ * correction j - 1 -- so it reproduces the blend of per-rank update orders a
+ * single global order cannot.  t: for each level k in 0..L-1, nc[k] * R times
+ * (correction-major); levels with nc[k] = 0 do not correct.  One thread; the
+ * arithmetic of each correction is or_async_add's group body with one thread
+ * per group. */
+int or_async_add_replay(or_hier *H, const double *f, double *u, int R, const int *rs, const double *t,
+                        const int *nc, int *corrections, double *relres)
+{
+   const or_opts *o = &H->o;
+   const int L = H->L, n0 = H->n[0];
+   const int multadd = (o->solver == OR_MULTADD || o->solver == OR_ASYNC_MULTADD);
+   if (R < 1 || rs[0] != 0 || rs[R] != n0 || L > OR_MAX_LEVELS) return -1;
+   init_vectors(H);
+   memcpy(H->f[0], f, (size_t)n0 * sizeof(double));
+   memcpy(H->u[0], u, (size_t)n0 * sizeof(double));
+   or_smem_spgemv(&H->A[0], H->u[0], H->f[0], -1.0, 1.0, H->r[0], 0, n0);
+   const double r0 = or_norm2(H->r[0], n0);
+   for (int k = 0; k < L; k++) {
+      H->zero_flags[k] = 1;
+      memcpy(H->lv_r[k][0], H->r[0], (size_t)n0 * sizeof(double));
+   }
+   double *U = H->u[0];
+   const double *F = H->f[0];
+   /* the event list (k, j, r) sorted by time */
+   int ne = 0, off[OR_MAX_LEVELS + 1];
+   for (int k = 0; k < L; k++) {
+      off[k] = ne;
+      ne += nc[k] * R;
+   }
+   off[L] = ne;
+   int *ev = (int *)malloc((size_t)(ne > 0 ? ne : 1) * sizeof(int));
+   for (int q = 0; q < ne; q++) ev[q] = q;
+   /* insertion sort by (time, k, r): small event counts */
+   for (int a = 1; a < ne; a++) {
+      const int x = ev[a];
+      int b = a - 1;
+      while (b >= 0) {
+         const int y = ev[b];
+         const double tx = t[x], ty = t[y];
+         int ky = 0, kx = 0;
+         while (ky < L && off[ky + 1] <= y) ky++;
+         while (kx < L && off[kx + 1] <= x) kx++;
+         const int later = ty > tx || (ty == tx && (ky > kx || (ky == kx && (y - off[ky]) % R > (x - off[kx]) % R)));
+         if (!later) break;
+         ev[b + 1] = y;
+         b--;
+      }
+      ev[b + 1] = x;
+   }
+   double **E = (double **)malloc(L * sizeof(double *)), **uk = (double **)malloc(L * sizeof(double *));
+   double **dacc = (double **)malloc(L * sizeof(double *));
+   int *jc = (int *)calloc(L, sizeof(int));    /* corrections whose e is formed */
+   int *nup = (int *)calloc(L, sizeof(int));   /* slices updated of the current correction */
+   int *done = (int *)calloc((size_t)(ne > 0 ? ne : 1), sizeof(int));
+   int *acc_cycle = (int *)calloc(L, sizeof(int));
+   double (*acc_state)[2] = malloc((size_t)L * sizeof(*acc_state));
+   for (int k = 0; k < L; k++) {
+      E[k] = dvec(n0);
+      uk[k] = dvec(n0);
+      dacc[k] = dvec(n0);
+      acc_state[k][0] = g_acc_mu;
+      acc_state[k][1] = 1.0;
+   }
+   or_gbar one = {1, 0, 0, 0};
+   or_gbar *b = &one;
+   /* e_{k, jc[k]}: or_async_add's group body, one thread */
+   #define FORM_E(k)                                                                                          \
+   do {                                                                                                      \
+      const int coarsest = multadd ? (k) : (k) + 1;                                                          \
+      for (int l = 0; l < coarsest; l++) {                                                                   \
+         if (l >= L - 1) continue;                                                                           \
+         if (composed_r(H)) xfer_restrict(H, l, H->lv_r[k][l], H->lv_r[k][l + 1], H->xt[k], H->xy[k]);      \
+         else or_smem_matvec(&H->R[l], H->lv_r[k][l], H->lv_r[k][l + 1], 0, H->n[l + 1]);                     \
+      }                                                                                                      \
+      if ((k) == L - 1) {                                                                                    \
+      } else if (multadd) {                                                                                  \
+         memset(H->lv_e[k][k], 0, (size_t)H->n[k] * sizeof(double));                                         \
+         async_smooth(H, k, H->lv_r[k][k], H->lv_e[k][k], H->lv_u_prev[k][k], H->lv_y[k][k], o->num_fine, k, \
+                      0, H->n[k], b);                                                                       \
+      } else {                                                                                               \
+         const int fg = (k), cg = (k) + 1;                                                                   \
+         memset(H->lv_u_fine[k][fg], 0, (size_t)H->n[fg] * sizeof(double));                                 \
+         memset(H->lv_u_coarse[k][cg], 0, (size_t)H->n[cg] * sizeof(double));                               \
+         async_smooth(H, cg, H->lv_r[k][cg], H->lv_u_coarse[k][cg], H->lv_u_coarse_prev[k][cg],             \
+                      H->lv_y[k][cg], o->num_coarse, k, 0, H->n[cg], b);                                     \
+         or_smem_matvec(&H->P[fg], H->lv_u_coarse[k][cg], H->lv_e[k][fg], 0, H->n[fg]);                      \
+         or_smem_residual(&H->A[fg], H->lv_r[k][fg], H->lv_e[k][fg], H->lv_y[k][fg], H->lv_r_fine[k][fg], 0, \
+                          H->n[fg]);                                                                        \
+         async_smooth(H, fg, H->lv_r_fine[k][fg], H->lv_u_fine[k][fg], H->lv_u_fine_prev[k][fg],            \
+                      H->lv_y[k][fg], o->num_fine, k, 0, H->n[fg], b);                                       \
+         memcpy(H->lv_e[k][k], H->lv_u_fine[k][k], (size_t)H->n[k] * sizeof(double));                        \
+      }                                                                                                      \
+      for (int l = (k) - 1; l > -1; l--) {                                                                   \
+         if (composed_p(H)) xfer_prolong(H, l, H->lv_e[k][l + 1], H->lv_e[k][l], H->xy[k]);                 \
+         else or_smem_matvec(&H->P[l], H->lv_e[k][l + 1], H->lv_e[k][l], 0, H->n[l]);                         \
+      }                                                                                                      \
+      if (g_acc_type != OR_NO_ACCEL) {                                                                       \
+         or_dmem_cheby_update(dacc[k], H->lv_e[k][0], n0, acc_cycle[k], g_acc_type,                          \
+                              (k) == g_acc_grid ? OR_CHEBY_GRID : OR_CHEBY_OTHER, g_acc_mu, g_acc_delta,     \
+                              acc_state[k]);                                                                 \
+         acc_cycle[k]++;                                                                                     \
+      }                                                                                                      \
+      memcpy(E[k], H->lv_e[k][0], (size_t)n0 * sizeof(double));                                              \
+      jc[k]++;                                                                                               \
+   } while (0)
+   for (int q = 0; q < ne; q++) {
+      const int x = ev[q];
+      if (done[x]) continue;
+      int k = 0;
+      while (k < L && off[k + 1] <= x) k++;
+      const int j = (x - off[k]) / R;
+      /* a slice of correction j before correction j - 1 finished on every
+       * rank (timer skew): the earlier correction's remaining slices first */
+      while (jc[k] < j + 1) {
+         if (jc[k] > 0 && nup[k] > 0) {
+            const int jp = jc[k] - 1;
+            for (int r = 0; r < R; r++) {
+               const int y = off[k] + jp * R + r;
+               if (done[y]) continue;
+               for (int i = rs[r]; i < rs[r + 1]; i++) {
+                  U[i] += E[k][i];
+                  uk[k][i] = U[i];
+               }
+               done[y] = 1;
+               nup[k]++;
+            }
+            or_smem_residual(&H->A[0], F, uk[k], H->lv_y[k][0], H->lv_r[k][0], 0, n0);
+            nup[k] = 0;
+         }
+         FORM_E(k);
+      }
+      const int r = (x - off[k]) % R;
+      for (int i = rs[r]; i < rs[r + 1]; i++) {
+         U[i] += E[k][i];
+         uk[k][i] = U[i];
+      }
+      done[x] = 1;
+      if (++nup[k] == R) {
+         /* SMEM_Residual on every slice's own copy: the level's next residual */
+         or_smem_residual(&H->A[0], F, uk[k], H->lv_y[k][0], H->lv_r[k][0], 0, n0);
+         nup[k] = 0;
+      }
+   }
+   #undef FORM_E
+   or_smem_spgemv(&H->A[0], H->u[0], H->f[0], -1.0, 1.0, H->r[0], 0, n0);
+   if (relres) *relres = r0 > 0 ? or_norm2(H->r[0], n0) / r0 : 0.0;
+   if (corrections)
+      for (int k = 0; k < L; k++) corrections[k] = jc[k];
+   memcpy(u, H->u[0], (size_t)n0 * sizeof(double));
+   for (int k = 0; k < L; k++) {
+      free(E[k]);
+      free(uk[k]);
+      free(dacc[k]);
+   }
+   free(E); free(uk); free(dacc); free(jc); free(nup); free(done); free(acc_cycle); free(acc_state); free(ev);
+   return 0;
+}
+
 /* M^{-1} = one V-cycle in preconditioner mode from a zero state (the
  * reference uses HYPRE_BoomerAMGSolve here, SMEM_Cheby.cpp:458-459). */
 static void precond_apply(or_hier *H, const double *fin, double *out)

@@ -226,6 +226,14 @@ void or_set_async_durations(const double *d, int n);
  * k's j-th correction ends at t[sum(n[0..k-1]) + j]; past n[k] entries its
  * last interval repeats */
 void or_set_async_times(const double *t, const int *n, int L);
+/* replay of a distributed free race (FULL_ASYNC, READ_SOL, LOCAL residuals and
+ * convergence): rank r owns fine rows [rs[r], rs[r+1]); level k's correction j
+ * updates slice r at t[off_k + j R + r] (off_k = R (nc[0] + .. + nc[k-1]));
+ * the slice updates are applied in time order, each level's residual taken
+ * from every slice's own copy -- amg_dist_async_solve's blend of per-rank
+ * update orders.  One thread, deterministic. */
+int or_async_add_replay(or_hier *H, const double *f, double *u, int R, const int *rs, const double *t,
+                        const int *nc, int *corrections, double *relres);
 /* res_compute_type GLOBAL for or_async_add (ASYNC_MULTADD, READ_SOL): nt[0] = 0
  * (no level-0 group), each thread smooths its global fine slice (:35-77, 356-414) */
 void or_set_async_res_global(int on);

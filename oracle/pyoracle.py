@@ -88,6 +88,8 @@ def lib():
         L.or_dmem_add.argtypes = [C.c_void_p, _dp, _dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
                                   C.c_int, C.c_int, C.c_double, C.c_double, _ip, _dp, C.POINTER(C.c_longlong)]
         L.or_async_add.restype = C.c_int
+        L.or_async_add_replay.restype = C.c_int
+        L.or_async_add_replay.argtypes = [C.c_void_p, _dp, _dp, C.c_int, _ip, _dp, _ip, _ip, C.POINTER(C.c_double)]
         L.or_async_add.argtypes = [C.c_void_p, _dp, _dp, _ip, C.c_int, C.c_int, C.c_int, _ip,
                                    C.POINTER(C.c_double)]
         L.or_dmem_async_jacobi.restype = C.c_double
@@ -447,6 +449,28 @@ class Hier:
                                     int(async_type), int(read_type), int(converge_type), iptr(cnt), C.byref(rel))
         finally:
             lib().or_set_async_res_global(0)
+            lib().or_set_async_accel(0, 0, 0.0, 0.0)
+        assert st == 0, st
+        return u, rel.value, cnt
+
+    def async_add_replay(self, f, rs, times, accel=None):
+        """or_async_add_replay: times[k] = (corrections, R) update times of level k's
+        slices (rank r: fine rows [rs[r], rs[r+1])); (u, relres, corrections)"""
+        n0 = self._keep[0][0].nrows
+        R = len(rs) - 1
+        u = np.zeros(n0)
+        nc = np.array([np.asarray(t).reshape(-1, R).shape[0] if np.size(t) else 0 for t in times], dtype=np.int32)
+        flat = np.ascontiguousarray(np.concatenate([np.asarray(t, dtype=np.float64).reshape(-1) for t in times]
+                                                   + [np.zeros(1)]))
+        rsv = np.ascontiguousarray(rs, dtype=np.int32)
+        cnt = np.zeros(self.L, dtype=np.int32)
+        rel = C.c_double()
+        if accel is not None:
+            lib().or_set_async_accel(int(accel[0]), int(accel[1]), float(accel[2]), float(accel[3]))
+        try:
+            st = lib().or_async_add_replay(self.h, dptr(np.ascontiguousarray(f, dtype=np.float64)), dptr(u), R,
+                                           iptr(rsv), dptr(flat), iptr(nc), iptr(cnt), C.byref(rel))
+        finally:
             lib().or_set_async_accel(0, 0, 0.0, 0.0)
         assert st == 0, st
         return u, rel.value, cnt

@@ -155,15 +155,46 @@ def replay_tables(corr_ms, L):
     return out
 
 
+def sliced_replay(amg, oracle, host, f, opts, corr_ms, rs, composed=False):
+    """the oracle's replay of a DISTRIBUTED free race (or_async_add_replay):
+    rank r's slice [rs[r], rs[r+1]) of the fine rows receives every level's
+    corrections at that rank's recorded update times"""
+    L = len(host["A"])
+    R = len(rs) - 1
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    if composed:
+        OH.set_composed_transfers()
+    accel = None
+    if opts.accel_type != amg.AMG_NO_ACCEL:
+        accel = (opts.accel_type, min(opts.cheby_grid, L - 2), opts.cheby_mu, opts.cheby_delta)
+    times = []
+    for k in range(L):
+        n = min(len(corr_ms[r][k]) for r in range(R))
+        times.append(np.stack([np.asarray(corr_ms[r][k][:n], dtype=np.float64) for r in range(R)], axis=1)
+                     if n else np.zeros((0, R)))
+    u, rel, _ = OH.async_add_replay(f, rs, times, accel=accel)
+    assert np.all(np.isfinite(u))
+    return rel
+
+
 def replay_check(amg, oracle, host, f, opts, runs, blocks=None, composed=False, what=""):
-    """every device free run (rel, corr_ms) against the oracle's replays of its
-    own recorded update order(s): rel in [0.5 min, 2 max] of those replays.
-    Prints each run's replay range and ratio; returns the widest replay range."""
+    """every device free run (rel, corr_ms[, rs]) against the oracle's replay of
+    its own recorded update order: rel in [0.5 lo, 2 hi] of the replay(s).
+    One hierarchy (or rank): the timed schedule with its recorded end times.
+    Several ranks with their fine-row partition rs: the sliced replay
+    (or_async_add_replay, every slice in its own rank's order).  Prints each
+    run's replay and ratio; returns the widest replay range."""
     L = len(host["A"])
     widest = 1.0
-    for i, (rel, corr_ms) in enumerate(runs):
-        lo, hi, rr = timed_band(amg, oracle, host, f, opts, replay_tables(corr_ms, L), blocks=blocks,
-                                composed=composed)
+    for i, run in enumerate(runs):
+        rel, corr_ms = run[0], run[1]
+        rs = run[2] if len(run) > 2 else None
+        if rs is not None and len(rs) > 2:
+            lo = hi = sliced_replay(amg, oracle, host, f, opts, corr_ms, rs, composed=composed)
+            rr = [lo]
+        else:
+            lo, hi, rr = timed_band(amg, oracle, host, f, opts, replay_tables(corr_ms, L), blocks=blocks,
+                                    composed=composed)
         widest = max(widest, hi / lo)
         print(f"  {what} run {i}: device {rel:.4e}, replay [{lo:.4e}, {hi:.4e}] ({len(rr)} order(s), width "
               f"{hi / lo:.2f}x), device / replay {rel / lo:.2f}-{rel / hi:.2f}")

@@ -334,7 +334,7 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
         assert list(cnt[:L - 1]) == [N] * (L - 1)
         assert rq[0] < 1.0
         rels.append(rq[0])
-        runs.append((rq[0], [t[q][3] for t in res]))
+        runs.append((rq[0], [t[q][3] for t in res], [int(x) for x in rs[0]]))
     # the oracle's model of each run: the replay of its recorded update orders
     # (every correction's update point; the slowest rank's and each rank's),
     # or_async_add under the timed schedule (the arithmetic itself is pinned by
@@ -620,10 +620,11 @@ def test_dist_async_additive_accel(amg, oracle, solver, accel, cuts, grid, bound
 
     from async_band import replay_check
     (rel_acc, d_acc), (rel_plain, _) = solve(acc), solve(amg.AMG_NO_ACCEL)
+    d_acc = (d_acc, [int(x) for x in rs[0]])
     assert rel_acc < 1.0
     opts = amg.default_opts(solver=a_solver, smooth_weight=w, num_cycles=N, tol=0.0, accel_type=acc,
                             cheby_mu=mu, cheby_delta=delta, cheby_grid=grid)
     # the oracle's model of the run: the replay of its recorded update order,
     # with the same ChebyUpdate per level group (timed schedule)
     print(f"dist async {solver} {accel} grid {grid}: device {rel_acc:.4e} (no accel {rel_plain:.4e})")
-    replay_check(amg, oracle, host, f, opts, [(rel_acc, d_acc)], what=f"dist async {solver} {accel}")
+    replay_check(amg, oracle, host, f, opts, [(rel_acc,) + d_acc], what=f"dist async {solver} {accel}")

@@ -366,6 +366,45 @@ def test_async_add_timed_schedule(amg, oracle, ct):
         assert list(a[2][:L]) == [N] * L
 
 
+def test_async_add_replay(amg, oracle):
+    """or_async_add_replay (the row-sliced replay of a distributed free race):
+    with one slice it is the timed schedule with the same end times, bit for
+    bit; with two slices updated at the same times it is the one-slice replay;
+    with slices updated in different orders it differs from both single-order
+    replays and still converges."""
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, 16, amg.AMG_INTERP_LINEAR)
+    Ps, Rs = [], []
+    for lev in range(L - 1):
+        ps, rs = oracle.smooth_transfer(host["A"][lev], host["P"][lev], 0.8)
+        Ps.append(ps)
+        Rs.append(rs)
+    N = 10
+    o = oracle.make_opts(solver=oracle.OR_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=N, tol=0.0)
+    OH = oracle.Hier(host["A"], Ps, Rs, o)
+    f = amg.rhs_rand(0, 16 ** 3)
+    n0 = 16 ** 3
+    d = np.array([3.0 / (1.9 ** k) + 0.05 for k in range(L)])
+    times = [d[k] * np.arange(1, N + 1) for k in range(L - 1)] + [np.zeros(0)]
+    oracle.set_async_times(times[:-1] + [times[-2]])
+    oracle.lib().or_set_async_schedule(4)
+    try:
+        ut, relt, _ = OH.async_add(f, [1] * L)
+    finally:
+        oracle.lib().or_set_async_schedule(0)
+    u1, rel1, c1 = OH.async_add_replay(f, [0, n0], [t[:, None] for t in times])
+    assert np.array_equal(u1.view(np.uint64), ut.view(np.uint64)) and rel1 == relt
+    assert list(c1[:L - 1]) == [N] * (L - 1)
+    half = [0, n0 // 2, n0]
+    u2, rel2, _ = OH.async_add_replay(f, half, [np.stack([t, t], axis=1) for t in times])
+    assert np.array_equal(u2.view(np.uint64), u1.view(np.uint64))
+    # slice 1 runs the fine level late: a blend of two orders
+    skew = [np.stack([t, t + (1.7 if k == 0 else 0.0)], axis=1) for k, t in enumerate(times)]
+    u3, rel3, _ = OH.async_add_replay(f, half, skew)
+    assert not np.array_equal(u3.view(np.uint64), u1.view(np.uint64))
+    assert rel3 < 0.1, rel3
+
+
 def test_composed_transfers_match_explicit(amg, oracle):
     """or_hier_set_composed_transfers: the smoothed transfers applied composed
     from the plain P / R (R~ r = R (r - w A D^-1 r), P~ e = P e - w D^-1 A P e)
