@@ -143,6 +143,11 @@ class Context:
         """Prolongation fused into the first post-smoothing sweep of marched geometric levels (default off: VALU-bound, slower)."""
         check(lib.amg_set_fuse_prolong(self.h, int(enable)))
 
+    def set_fuse_outer(self, mode):
+        """level 0's last post sweep + the outer residual as one march (0 off, 1 on, 2 on with u'
+        stored only at the end of an iterate batch; bit-identical)"""
+        check(lib.amg_set_fuse_outer(self.h, int(mode)))
+
     def set_graphs(self, enable):
         """hipGraphs of the additive cycles' launch-bound loops (bit-identical)."""
         check(lib.amg_set_graphs(self.h, int(bool(enable))))
@@ -272,6 +277,7 @@ class Hier:
         self.n0 = As[0].nrows
         self.fused = lib.amg_hier_fused(h)  # bit 0: level-0 residual + restriction fused; bit l+1: level l geometric transfers
         self.fused_prolong = lib.amg_hier_fused_prolong(h)  # bit l: level l's prolongation fused into its post sweep
+        self.fused_outer = lib.amg_hier_fused_outer(h)  # level 0's last post sweep fused with the outer residual
 
     def set_opts(self, opts):
         check(lib.amg_hier_set_opts(self.h, C.byref(opts)))

@@ -148,6 +148,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_XFER")) c->fuse_xfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_GRAPHS")) c->graphs = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_FUSE_OUTER")) c->fuse_outer = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_FUSE_XFP_SLAB")) c->fuse_xfp_slab = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::max(0, std::min(7, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_SMALL")) c->jgs_small = std::max(0, std::min(2, std::atoi(v)));
@@ -924,6 +925,14 @@ extern "C" int amg_set_march_lines_gemv(amg_ctx *c, int lines)
    AMG_ARG(c && (lines == 1 || lines == 2 || lines == 4), "amg_set_march_lines_gemv: lines must be 1, 2 or 4");
    c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->mz_lines_gemv = lines;
+   return AMG_OK;
+}
+
+extern "C" int amg_set_fuse_outer(amg_ctx *c, int mode)
+{
+   AMG_ARG(c && mode >= 0 && mode <= 2, "amg_set_fuse_outer: mode 0, 1 or 2");
+   c->knob_gen++; // cached hipGraphs were captured with the old setting
+   c->fuse_outer = mode;
    return AMG_OK;
 }
 

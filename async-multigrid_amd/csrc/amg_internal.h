@@ -164,6 +164,8 @@ struct amg_ctx {
    int fuse_xfer = 1;      // composed smoothed transfers of marched 7-pt levels in one pass each
    int fuse_xfp_slab = 0;  // ... and the slab async solve's fused prolongation + atomic (AMG_FUSE_XFP_SLAB)
    int fuse_prolong = 0;   // prolongation fused into the first post sweep (measured slower: off)
+   int fuse_outer = 0;     // level 0's last post sweep + the outer residual as one march (AMG_FUSE_OUTER;
+                           // 1: u' stored every step, 2: only at the end of an iterate batch)
    int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)
    int mz_lines = 1;       // 7-pt plane march: lines per lane (1, 2 or 4, AMG_MZ_LINES)
    int mz_lines_gemv = 2;  // the same for SpMV / SpGEMV (AMG_MZ_LINES_GEMV; 2: -8 % on the 512^3 SpMV)
@@ -324,6 +326,12 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
 void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const double *x,
                      const double *l1, double omega, double *r, double *unext, int rb, int re,
                      double *partials);
+// level 0's last post-smoothing sweep and the outer residual + next first
+// sweep as ONE plane march (7-pt master form, S = 512): u1out = u' (null: not
+// stored), rout = r (null: not stored), unext = u'', partials of sum r_i^2
+bool mz_sweep_outer_ok(const amg_mat *A);
+void mz_sweep_outer(hipStream_t s, const amg_mat *A, const double *f, const double *u, double *u1out,
+                    double *rout, double *unext, double omega, double *partials);
 // zero-guess sweep: variant 0 (SMEM) u = omega*f/a (a != 0) | u = f/l1
 //                   variant 1 (SEQ)  u += omega*f/a (a != 0) | u += f/l1 (a != 0)
 void jacobi_zero(hipStream_t s, const double *diag, const double *f, const double *l1,

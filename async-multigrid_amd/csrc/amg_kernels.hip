@@ -3220,6 +3220,205 @@ struct EpiResJacobi {
    }
 };
 
+// ---------------------------------------------------------------------------
+// Temporally fused pair of 7-pt marches (mz_sweep_outer_kernel).  A V-cycle
+// ends with level 0's last post-smoothing sweep u' = u + w (f - A u) ./ a
+// (csr_mz_kernel<EpiJacobi>); SMEM_Solve then forms the outer residual
+// r = f - A u' with its norm, fused with the next cycle's first sweep
+// u'' = u' + w r ./ a (csr_mz_kernel<EpiResJacobi>).  Here both run in ONE
+// march, so u' never round-trips through HBM between them (f and u are read
+// once, u' and u'' written once):
+//   * a workgroup is NT = NL + 2 teams of 256 lanes; team t owns line
+//     y = NL * group - 1 + t of the plane (512 positions; lane: rows 2l, 2l+1
+//     as in csr_mz_kernel); teams 0 and NL + 1 carry the halo lines sweep 2
+//     needs and store nothing;
+//   * plane step k: every team computes u'(k) of its line exactly as
+//     csr_mz_kernel<EpiJacobi> does (u of planes k-1, k, k+1 in registers, the
+//     +-S lines loaded, +-1 from the neighbour lanes and one two-lane edge
+//     load) and writes it to an LDS ring (2 planes); the inner teams then
+//     compute sweep 2 at plane k - 1: u' of planes k-2, k-1, k of their own
+//     pair from registers, the +-S and +-1 operands of plane k - 1 from the
+//     ring; one barrier per plane step (the ring's RAW and WAR hazards both
+//     fall on it);
+//   * a chunk of ZC planes runs sweep 1 over k0-1 .. k1 (the z halo) and
+//     sweep 2 over k0 .. k1-1;
+//   * the next plane's operands (the +-S lines, f, the pattern byte, the edge)
+//     are loaded before the barrier, so they are in flight across it.
+// Every row adds its used entries in master (= CSR) order from the same
+// operand values as the two separate marches, and the partials are
+// csr_mz_kernel's (one per 256-row tile, the same operand order): u', u'' and
+// every partial are bit-identical to the two launches.  Needs S = 512 (a team
+// is one line) and NL | P / S.
+// ---------------------------------------------------------------------------
+constexpr int AMG_MZF_NL = 2;
+constexpr int AMG_MZF_NT = AMG_MZF_NL + 2;
+
+template <bool STORE_U>
+__global__ __launch_bounds__(256 * AMG_MZF_NT) void mz_sweep_outer_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np, MpSten Sv,
+   const double *__restrict__ f, const double *__restrict__ u, double *__restrict__ u1out,
+   double *__restrict__ rout, double *__restrict__ unext, double omega, int P, int nz, int zc, int npb, int xcd,
+   double *__restrict__ partials)
+{
+   constexpr int NL = AMG_MZF_NL, NT = AMG_MZF_NT, S = 512;
+   __shared__ unsigned long long mtab[256];
+   __shared__ v2d ring[2][NT][256];
+   __shared__ double red[AMG_MZ_MAXZC * NL * 8];
+   const int tid = (int)threadIdx.x, team = tid >> 8, lt = tid & 255, lane = tid & 63;
+   if (tid < np) mtab[tid] = mmask_g[tid];
+   const int G = (int)gridDim.x;
+   int lg = (int)blockIdx.x;
+   if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
+   const int pblk = lg % npb, chunk = lg / npb;
+   const int k0 = chunk * zc, k1 = min(k0 + zc, nz);
+   const int ny = P / S;
+   const int y = pblk * NL - 1 + team;
+   const bool inner = team >= 1 && team <= NL;
+   const int ly = y < 0 ? 0 : (y >= ny ? ny - 1 : y); // halo teams past the box: a valid line, never used
+   const unsigned pos = (unsigned)(ly * S + 2 * lt);
+   const unsigned Nu = (unsigned)((long long)nz * P);
+   const double a0 = Sv.val[0];
+   auto ldp = [&](int k) { return (k >= 0 && k < nz) ? ld2u(u, (unsigned)k * P + pos) : v2d{0.0, 0.0}; };
+   // u of planes k-1, k, k+1 (sweep 1 at plane k)
+   v2d xm = ldp(k0 - 2), xc = ldp(k0 - 1), xq = ldp(k0);
+   struct PlaneIn {
+      v2d ym, yp, fv;
+      double e;
+      int pid;
+   };
+   auto fetch = [&](int k, PlaneIn &in) {
+      const int kk = k < 0 ? 0 : (k >= nz ? nz - 1 : k);
+      const unsigned row = (unsigned)kk * P + pos;
+      in.ym = ld2u(u, row >= (unsigned)S ? row - S : 0u);
+      const unsigned rp = row + (unsigned)S;
+      in.yp = ld2u(u, rp + 2 <= Nu ? rp : Nu - 2);
+      in.fv = ld2u(f, row);
+      in.pid = ppat[row >> 1];
+      in.e = 0.0;
+      if (lane == 0 && row > 0) in.e = ld1u(u, row - 1);
+      if (lane == 63 && row + 2 < Nu) in.e = ld1u(u, row + 2);
+   };
+   PlaneIn cur;
+   fetch(k0 - 1, cur);
+   // sweep-2 state: u' of planes k-2, k-1 of the own pair; f and pattern of plane k-1
+   v2d wm{0.0, 0.0}, wc{0.0, 0.0}, fm{0.0, 0.0};
+   int pidm = 0;
+   __syncthreads();
+   for (int k = k0 - 1; k <= k1; k++) {
+      const bool s1 = k >= 0 && k < nz;  // workgroup-uniform
+      v2d xn = ldp(k + 2);               // u of plane k + 2, one step ahead
+      // ---- sweep 1 at plane k: u' = u + w (f - A u) ./ a (EpiJacobi) ----
+      v2d w1{0.0, 0.0};
+      if (s1) {
+         double lft = __shfl_up(xc.y, 1, 64);
+         double rgt = __shfl_down(xc.x, 1, 64);
+         if (lane == 0) lft = cur.e;
+         if (lane == 63) rgt = cur.e;
+         const unsigned long long mk = mtab[cur.pid];
+         v2d xv[7];
+         xv[0] = xc;
+         xv[1] = xm;
+         xv[2] = cur.ym;
+         xv[3] = v2d{lft, xc.x};
+         xv[4] = v2d{xc.y, rgt};
+         xv[5] = cur.yp;
+         xv[6] = xq;
+         const v2d acc = mz_acc7<1, true>(cur.fv, xv, mk, Sv, nullptr);
+         w1 = v2d{(a0 != 0.0) ? xc.x + omega * acc.x / a0 : xc.x, (a0 != 0.0) ? xc.y + omega * acc.y / a0 : xc.y};
+         if (STORE_U && inner && y < ny && k >= k0 && k < k1)
+            *reinterpret_cast<v2du *>(u1out + (size_t)((unsigned)k * P + pos)) = w1;
+      }
+      ring[k & 1][team][lt] = w1;
+      const v2d fk = cur.fv;
+      const int pidk = cur.pid;
+      // the next plane's operands, in flight across the barrier below
+      if (k + 1 <= k1) fetch(k + 1, cur);
+      // ---- sweep 2 at plane k - 1 (inner teams): r = f - A u', u'' = u' + w r ./ a ----
+      const int km = k - 1;
+      if (km >= k0 && km < k1) {
+         if (inner && y < ny) {
+            const v2d *rg = ring[km & 1][0];
+            // +-1 of the pair from the ring (line ends: clamped, masked out)
+            const double *rl = reinterpret_cast<const double *>(ring[km & 1][team]);
+            const double lft = rl[lt > 0 ? 2 * lt - 1 : 0];
+            const double rgt = rl[lt < 255 ? 2 * lt + 2 : 511];
+            const unsigned long long mk = mtab[pidm];
+            v2d xv[7];
+            xv[0] = wc;
+            xv[1] = wm;
+            xv[2] = rg[(team - 1) * 256 + lt];
+            xv[3] = v2d{lft, wc.x};
+            xv[4] = v2d{wc.y, rgt};
+            xv[5] = rg[(team + 1) * 256 + lt];
+            xv[6] = s1 ? w1 : v2d{0.0, 0.0};
+            const v2d res = mz_acc7<1, true>(fm, xv, mk, Sv, nullptr);
+            const unsigned row = (unsigned)km * P + pos;
+            if (rout) *reinterpret_cast<v2du *>(rout + (size_t)row) = res;
+            const v2d v{(a0 != 0.0) ? wc.x + omega * res.x / a0 : wc.x,
+                        (a0 != 0.0) ? wc.y + omega * res.y / a0 : wc.y};
+            *reinterpret_cast<v2du *>(unext + (size_t)row) = v;
+            if (partials) {
+               double a = res.x * res.x, b = res.y * res.y;
+#pragma unroll
+               for (int off = 16; off > 0; off >>= 1) {
+                  a += __shfl_down(a, off, 32);
+                  b += __shfl_down(b, off, 32);
+               }
+               if ((lt & 31) == 0) red[((km - k0) * NL + (team - 1)) * 8 + (lt >> 5)] = a + b;
+            }
+         }
+      }
+      __syncthreads();
+      wm = wc;
+      wc = w1;
+      fm = fk;
+      pidm = pidk;
+      xm = xc;
+      xc = xq;
+      xq = xn;
+   }
+   if (partials) {
+      for (int w = tid; w < 2 * NL * (k1 - k0); w += 256 * NT) {
+         const int it = w / (2 * NL), i = (w >> 1) % NL, h = w & 1;
+         const int yl = pblk * NL + i;
+         const double *g = red + (it * NL + i) * 8 + 4 * h;
+         partials[((long long)(k0 + it) * P + (long long)yl * S) / 256 + h] = ((g[0] + g[1]) + g[2]) + g[3];
+      }
+   }
+}
+
+// can level 0's last post-sweep and the outer residual run as one march?
+bool mz_sweep_outer_ok(const amg_mat *A)
+{
+   return A->mz_P && !A->mz27 && A->mp_uni && A->mz_S == 512 && A->mz_P % 512 == 0 &&
+          (A->mz_P / 512) % AMG_MZF_NL == 0 && A->ppat && A->mpmask;
+}
+
+// the fused pair (see mz_sweep_outer_kernel): u1out = u' (when non-null),
+// rout = r (when non-null), unext = u'', partials: the outer residual's
+void mz_sweep_outer(hipStream_t s, const amg_mat *A, const double *f, const double *u, double *u1out,
+                    double *rout, double *unext, double omega, double *partials)
+{
+   MpSten Sv;
+   for (int j = 0; j < AMG_MP_MAXJ; j++) {
+      Sv.off[j] = A->mp_off[j];
+      Sv.val[j] = A->mp_val[j];
+   }
+   const int P = A->mz_P, nz = A->nrows / P;
+   const int npb = P / (512 * AMG_MZF_NL);
+   int zc = std::max(1, std::min(A->ctx->mz_zc, AMG_MZ_MAXZC));
+   if (A->ctx->mz_zc_auto) zc = (int)std::max(1LL, std::min((long long)zc, (long long)nz * npb / 1024));
+   const int nch = (nz + zc - 1) / zc;
+   if (u1out)
+      mz_sweep_outer_kernel<true><<<npb * nch, 256 * AMG_MZF_NT, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, Sv, f, u, u1out, rout, unext, omega, P, nz, zc, npb, A->ctx->mz_xcd,
+         partials);
+   else
+      mz_sweep_outer_kernel<false><<<npb * nch, 256 * AMG_MZF_NT, 0, s>>>(
+         A->ppat, A->mpmask, A->pp_n, Sv, f, u, nullptr, rout, unext, omega, P, nz, zc, npb, A->ctx->mz_xcd,
+         partials);
+}
+
 __device__ __forceinline__ const double *epi_pf_vec(const EpiJacobi &e) { return e.x; }
 __device__ __forceinline__ const double *epi_pf_vec(const EpiL1Jacobi &e) { return e.x; }
 __device__ __forceinline__ const double *epi_pf_vec(const EpiResJacobi &e) { return e.x; }

@@ -96,6 +96,12 @@ struct amg_hier {
    std::vector<hipGraphExec_t> g_lev;
    std::vector<hipStream_t> g_lev_s;
    std::vector<char> g_lev_warm;
+   // fused level-0 last post sweep + outer residual (ctx->fuse_outer): the
+   // V-cycle left its last post sweep to outer_residual; u2: u'' buffer;
+   // store_u1: write u' (always in mode 1; mode 2: the last step of a batch)
+   bool post_deferred = false;
+   bool store_u1 = true;
+   double *u2 = nullptr;
    // AMG_SCHED_TIMED: per-level correction time (amg_hier_set_async_durations)
    // or recorded end times (amg_hier_set_async_times)
    std::vector<double> async_dur;
@@ -659,7 +665,9 @@ static void smooth_all_levels(amg_hier *H, hipStream_t s, int Alevel, const doub
 }
 
 // ---- SMEM_Sync_Parfor_Vcycle (SMEM_Sync_AMG.cpp:8-145) -------------------------
-static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
+// defer_post: leave level 0's last post-smoothing sweep to outer_residual,
+// which runs it fused with the outer residual (mz_sweep_outer)
+static void vcycle(amg_hier *H, bool precond, bool reuse_r0, bool defer_post = false)
 {
    hipStream_t s = H->ctx->stream;
    const amg_opts &o = H->o;
@@ -737,6 +745,11 @@ static void vcycle(amg_hier *H, bool precond, bool reuse_r0)
             amgk::geo_prolong(s, H->gl[l], H->d_geo_w[l], H->lv[l + 1].u, v.u);
          else
             amgk::spgemv(s, v.P, H->lv[l + 1].u, v.u, pro_mode, v.u, 0, v.n, nullptr);
+      }
+      if (l == 0 && defer_post) {
+         smooth_one_level(H, s, l, f_fine, o.num_post_smooth_sweeps - 1, false);
+         H->post_deferred = true;
+         continue;
       }
       smooth_one_level(H, s, l, f_fine, o.num_post_smooth_sweeps, false);
    }
@@ -919,8 +932,27 @@ static bool reuse_applies(const amg_hier *H)
           o.num_pre_smooth_sweeps > 0 && H->L > 1;
 }
 
+// can level 0's last post sweep run fused with the outer residual
+// (mz_sweep_outer: plain weighted Jacobi, the 7-pt master form with S = 512)?
+static bool fused_outer_applies(const amg_hier *H)
+{
+   const amg_opts &o = H->o;
+   return H->ctx->fuse_outer && reuse_applies(H) && o.smoother == AMG_JACOBI && o.num_post_smooth_sweeps >= 1 &&
+          (H->psw.empty() || !H->psw[0]) && amgk::mz_sweep_outer_ok(H->lv[0].A);
+}
+
+extern "C" int amg_hier_fused_outer(const amg_hier *H)
+{
+   return (H && fused_outer_applies(H)) ? H->ctx->fuse_outer : 0;
+}
+
 // r = f - A u and ||r|| into d_hist[slot].  With reuse, the same kernel also
-// emits the next cycle's first Jacobi sweep u_alt = u + w r / a_ii.
+// emits the next cycle's first Jacobi sweep u_alt = u + w r / a_ii.  After a
+// V-cycle that deferred level 0's last post sweep (post_deferred), that sweep
+// runs in the same march (mz_sweep_outer): u' = u + w (f - A u) ./ a into
+// u_alt (swapped in as u), r = f - A u', and u'' = u' + w r ./ a into u2
+// (swapped in as u_alt, the next cycle's first sweep) -- the same bits as the
+// sweep followed by the fused outer residual.
 static int outer_residual(amg_hier *H, int slot)
 {
    amg_ctx *c = H->ctx;
@@ -928,6 +960,23 @@ static int outer_residual(amg_hier *H, int slot)
    double *p;
    const int nb = amgk::tile_blocks(0, v.n);
    AMG_TRY(amg_ctx_partials(c, nb, &p));
+   if (H->post_deferred) {
+      if (!H->u2) AMG_TRY(dalloc(H, v.n, &H->u2));
+      const bool skip_r = H->o.reuse_outer_residual >= 2;
+      {
+         ProfScope ps(H, PROF_OUTER, c->stream);
+         amgk::mz_sweep_outer(c->stream, v.A, v.f, v.u, H->store_u1 ? v.u_alt : nullptr, skip_r ? nullptr : H->r0,
+                              H->u2, H->o.smooth_weight, p);
+      }
+      std::swap(v.u, v.u_alt);  // u = u' (when stored)
+      std::swap(v.u_alt, H->u2); // u_alt = u''
+      H->post_deferred = false;
+      H->pre_ready = true;
+      H->r0_stale = skip_r;
+      amgk::reduce_partials(c->stream, p, nb, H->d_hist + slot, 1, c->d_scalars + 4096);
+      AMG_HIP(hipGetLastError());
+      return AMG_OK;
+   }
    {
       ProfScope ps(H, PROF_OUTER, c->stream);
       if (reuse_applies(H)) {
@@ -1060,7 +1109,7 @@ static int solve_step(amg_hier *H)
    if (o.solver == AMG_BPX)
       bpx_cycle(H, precond); // SMEM_Solve.cpp:161-163
    else if (one_level)
-      vcycle(H, precond, reuse);
+      vcycle(H, precond, reuse, fused_outer_applies(H));
    else if (c->graphs && !H->o.profile && (graphs_check(H), true))
       AMG_TRY(graph_issue(H->g_add, H->g_add_warm, c->stream, [&] {
          sync_add_vcycle(H);
@@ -1107,7 +1156,15 @@ extern "C" int amg_solve(amg_hier *H, const amg_vec *f, amg_vec *u, double *resh
 extern "C" int amg_solve_iterate(amg_hier *H, int k)
 {
    AMG_ARG(H && H->have_state, "amg_solve_iterate: call amg_solve (or amg_solve_start) first");
-   for (int i = 0; i < k; i++) AMG_TRY(solve_step(H));
+   for (int i = 0; i < k; i++) {
+      // fuse_outer 2: the fused post sweep writes u' only in the batch's last
+      // step (the iterate the caller can observe); the steps before consume it
+      // in registers
+      H->store_u1 = H->ctx->fuse_outer != 2 || i == k - 1;
+      const int st = solve_step(H);
+      H->store_u1 = true;
+      AMG_TRY(st);
+   }
    return AMG_OK;
 }
 

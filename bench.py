@@ -38,6 +38,9 @@ def parse():
     p.add_argument("--reuse-outer-residual", type=int, default=2)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-cycles", type=int, default=20)
+    p.add_argument("--fuse-outer", type=int, default=-1,
+                   help="level 0's last post sweep fused with the outer residual (0 off, 1, 2; -1: the library "
+                        "default / AMG_FUSE_OUTER)")
     p.add_argument("--general", type=int, default=1,
                    help="also time the general (plain-CSR, CSR-transfer) V-cycle on the same 512^3 solve")
     p.add_argument("--seq-cycles", type=int, default=200,
@@ -85,7 +88,7 @@ def load_traffic(n, kernel):
         return None
 
 
-def fine_kernels(n0, mat_bytes, ms, launches, fused, fmt, fused_prolong=0):
+def fine_kernels(n0, mat_bytes, ms, launches, fused, fmt, fused_prolong=0, fused_outer=0):
     """Per-launch time (HIP events on the compute stream inside the timed loop)
     and algorithmic bytes of each fine-level kernel of a step.
     Profile categories: 0 level-0 residual (fused with R0 when fused & 1),
@@ -95,10 +98,21 @@ def fine_kernels(n0, mat_bytes, ms, launches, fused, fmt, fused_prolong=0):
     def per(c):
         return ms[c] / launches[c] if launches[c] else None
     out = {}
-    out["outer_residual_sweep"] = (per(4), mat_bytes + 24 * n0,
-                                   "outer residual r = f - A0 u + norm partials, fused with the next "
-                                   f"cycle's first Jacobi sweep (reads f, u; writes u_next; {fmt})")
-    if fused_prolong & 1:
+    if fused_outer:
+        # one march: the last post sweep u' = u + w (f - A u)./a and the outer
+        # residual of u' + norm + the next first sweep u'' (mz_sweep_outer_kernel)
+        out["post_sweep_outer_residual"] = (
+            per(4), mat_bytes + (32 if fused_outer == 1 else 24) * n0,
+            "level-0 post-smoothing sweep fused with the outer residual r = f - A0 u' + norm partials and the "
+            f"next cycle's first Jacobi sweep in one plane march (reads f, u; writes {'u, ' if fused_outer == 1 else ''}"
+            f"u_next; {fmt}" + ("" if fused_outer == 1 else "; u' itself written only in a batch's last step") + ")")
+    else:
+        out["outer_residual_sweep"] = (per(4), mat_bytes + 24 * n0,
+                                       "outer residual r = f - A0 u + norm partials, fused with the next "
+                                       f"cycle's first Jacobi sweep (reads f, u; writes u_next; {fmt})")
+    if fused_outer:
+        pass
+    elif fused_prolong & 1:
         out["prolong_sweep"] = (per(1), mat_bytes + 24 * n0 + 8 * (n0 // 8),
                                 "geometric prolongation u + P0 e fused into the post-smoothing Jacobi sweep "
                                 f"(reads f, u, e; writes u_next; {fmt})")
@@ -178,6 +192,8 @@ def gpu_config1(amg, args):
     """the GPU's rate on config 1's 64^3 solve (the SEQ leg's workload)"""
     n = 64
     ctx = amg.Context(device=0, nstreams=4)
+    if args.fuse_outer >= 0:
+        ctx.set_fuse_outer(args.fuse_outer)
     gen = amg.Gen(n, interp=amg.AMG_INTERP_LINEAR)
     L = gen.L
     As = [gen.register(ctx, amg.AMG_GEN_A, l) for l in range(L)]
@@ -358,6 +374,8 @@ def main():
     n = args.n
     t0 = time.time()
     ctx = amg.Context(device=0, nstreams=4)
+    if args.fuse_outer >= 0:
+        ctx.set_fuse_outer(args.fuse_outer)
     gen = amg.Gen(n, interp=amg.AMG_INTERP_LINEAR)
     L = gen.L
     As = [gen.register(ctx, amg.AMG_GEN_A, l) for l in range(L)]
@@ -402,8 +420,9 @@ def main():
                              As[0].pair_pattern, As[0].master_pattern)
     fused = H.fused
     fused_prolong = H.fused_prolong
+    fused_outer = H.fused_outer
     plane_march = As[0].plane_march
-    kernels = fine_kernels(n0, mat_bytes, ms, launches, fused, fmt, fused_prolong)
+    kernels = fine_kernels(n0, mat_bytes, ms, launches, fused, fmt, fused_prolong, fused_outer)
     # fine-grid SpMV y = A x (matrix + x + y), events on the same stream
     x = ctx.vec(n0)
     x.set(1.0)
@@ -503,6 +522,7 @@ def main():
                    "matrix_format": fmt, "plane_march": plane_march,
                    "march_points": [A.march_points for A in As], "geometric_transfers": fused,
                    "fused_prolong_sweep": fused_prolong,
+                   "fused_post_sweep_outer_residual": fused_outer,
                    "parallelism": "single GPU"},
         "fine_spmv": {"gbs": spmv_gbs, "ms": spmv_ms.value, "bytes": spmv_bytes,
                       "frac": spmv_gbs / HBM_PEAK_GBS, "format": fmt},

@@ -400,6 +400,15 @@ int amg_set_fuse_transfer(amg_ctx *ctx, int enable);
  * coarse correction read from an LDS ring of coarse planes (levels whose
  * lines are multiples of 512 points only). */
 int amg_hier_fused_prolong(const amg_hier *H);
+/* level 0's last post-smoothing sweep and the outer residual + the next
+ * cycle's first sweep as ONE plane march (weighted Jacobi MULT solves with
+ * reuse_outer_residual on a 7-pt master-form A0 whose lines are 512 long):
+ * mode 0 off, 1 on (u' written every step), 2 on with u' written only in the
+ * last step of each amg_solve_iterate batch (the steps before consume it in
+ * registers); bit-identical to the two marches.  AMG_FUSE_OUTER sets it too. */
+int amg_set_fuse_outer(amg_ctx *ctx, int mode);
+/* the fused post sweep + outer residual mode this hierarchy runs (0: not fused) */
+int amg_hier_fused_outer(const amg_hier *H);
 int amg_set_fuse_prolong(amg_ctx *ctx, int enable);
 /* lines per lane of the 7-pt plane march (1, 2 or 4; env AMG_MZ_LINES for the
  * sweeps and residuals, AMG_MZ_LINES_GEMV for SpMV / SpGEMV; defaults 1 and 2):

@@ -47,7 +47,8 @@ def grid_solve(amg, L, host, f, ppg, transport="host", **kw):
         cuts = tuple(i / len(ranks) for i in range(1, len(ranks)))
         parts[g] = split_host(host, cuts)
         hubs[g] = amg.dist.ThreadMailbox(len(ranks))
-    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=0.8, tol=0.0, **kw)
+    w = kw.pop("smooth_weight", 0.8)
+    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=w, tol=0.0, **kw)
     dh = amg.grid.DevHub(rank_grid) if transport == "device" else None
     # every rank starts its solve once all hierarchies are built (the
     # reference's ranks start DMEM_Add together): otherwise a fast grid runs
