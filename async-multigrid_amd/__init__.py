@@ -64,13 +64,14 @@ def _times_flat(times):
     return flat, n
 
 
-def _corr_ms(fn, h, L):
+def _corr_ms(fn, h, L, start=False):
+    """per level: the end (start=False) or start times of its update windows"""
     out = []
     for k in range(L):
         cnt = np.zeros(1, dtype=np.int32)
-        check(fn(h, k, None, 0, _ip(cnt)))
+        check(fn(h, k, None, -1 if start else 0, _ip(cnt)))
         ms = np.zeros(max(1, int(cnt[0])))
-        check(fn(h, k, _dp(ms), int(cnt[0]), _ip(cnt)))
+        check(fn(h, k, _dp(ms), -max(1, int(cnt[0])) if start else int(cnt[0]), _ip(cnt)))
         out.append(ms[:int(cnt[0])])
     return out
 
@@ -346,9 +347,10 @@ class Hier:
         flat, n = _times_flat(times)
         check(lib.amg_hier_set_async_times(self.h, _dp(flat), _ip(n), int(n.size)))
 
-    def async_correction_ms(self):
-        """per level: end times (ms) of its corrections in the last free-race async_solve"""
-        return _corr_ms(lib.amg_async_correction_ms, self.h, self.L)
+    def async_correction_ms(self, start=False):
+        """per level: end times (ms) of its corrections' update windows in the last free-race
+        async_solve (start=True: the windows' start times, where recorded)"""
+        return _corr_ms(lib.amg_async_correction_ms, self.h, self.L, start)
 
     def eigs_power(self, iters):
         emax, emin = C.c_double(), C.c_double()

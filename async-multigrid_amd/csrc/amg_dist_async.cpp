@@ -387,6 +387,9 @@ int level_correction(amg_dist_hier *D, int k, int j = -1)
    // the atomic correction rides on the fused level-0 prolongation where it
    // can (no acceleration step between them)
    const bool fuse_corr = k > 0 && o.accel_type == AMG_NO_ACCEL && fused_xfp0(D);
+   // (the fused prolongation + atomic correction: its whole launch is the window)
+   if (j >= 0 && fuse_corr && D->corr.record_start(k, j, s))
+      return amg_set_error(AMG_ERR_HIP, "level %d: correction event", k);
    for (int l = k - 1; l >= 0; l--)
       AMG_TRY(prolong_to(D, a, l, a.e[l + 1], a.e[l], (l == 0 && fuse_corr) ? 1 : 0, D->lv[0].u, a.u_priv));
    const int n0 = D->lv[0].n;
@@ -402,6 +405,8 @@ int level_correction(amg_dist_hier *D, int k, int j = -1)
          amgk::vcopy(s, a.e[0], a.d_acc, 0, n0);
    }
    // correction into the shared slab; u_priv = the value each row saw
+   if (j >= 0 && !fuse_corr && D->corr.record_start(k, j, s))
+      return amg_set_error(AMG_ERR_HIP, "level %d: correction event", k);
    if (!fuse_corr) amgk::atomic_correct(s, D->lv[0].u, a.e[0], a.u_priv, n0);
    if (j >= 0 && D->corr.record(k, j, s)) return amg_set_error(AMG_ERR_HIP, "level %d: correction event", k);
    // private residual r_k = f - A u_k  (SMEM_Residual on u_k)
@@ -801,7 +806,10 @@ extern "C" int amg_dist_hier_set_async_times(amg_dist_hier *D, const double *t, 
 extern "C" int amg_dist_async_correction_ms(const amg_dist_hier *D, int level, double *ms, int cap, int *count)
 {
    AMG_ARG(D && count && level >= 0 && level < D->L, "amg_dist_async_correction_ms: bad argument");
-   const auto &v = level < (int)D->corr.ms.size() ? D->corr.ms[level] : std::vector<double>();
+   const bool start = cap < 0; // cap < 0: the update windows' start times, -cap entries
+   if (start) cap = -cap;
+   const auto &vv = start ? D->corr.ms0 : D->corr.ms;
+   const auto &v = level < (int)vv.size() ? vv[level] : std::vector<double>();
    *count = (int)v.size();
    for (int j = 0; j < (int)v.size() && j < cap && ms; j++) ms[j] = v[j];
    return AMG_OK;

@@ -70,12 +70,14 @@ inline double amg_timed_end(const std::vector<double> &t, double dur, int j)
 }
 
 // per-correction end events of a free race (one pool per level, grown on use)
+// (the update point of correction j: its start event `record_start`, before
+// the kernel that adds it into the shared iterate, and its end event `record`,
+// after it -- a window in which other levels' updates may interleave row by row)
 struct AmgCorrTimes {
-   std::vector<std::vector<hipEvent_t>> ev; // [level][correction]
-   std::vector<std::vector<double>> ms;     // [level][correction], after the solve
-   int record(int k, int j, hipStream_t s)
+   std::vector<std::vector<hipEvent_t>> ev, ev0; // [level][correction]: update end / start
+   std::vector<std::vector<double>> ms, ms0;     // [level][correction], after the solve
+   static int rec(std::vector<hipEvent_t> &v, int j, hipStream_t s)
    {
-      auto &v = ev[k];
       while ((int)v.size() <= j) {
          hipEvent_t e;
          if (hipEventCreate(&e) != hipSuccess) return -1;
@@ -83,27 +85,37 @@ struct AmgCorrTimes {
       }
       return hipEventRecord(v[j], s) == hipSuccess ? 0 : -1;
    }
+   int record(int k, int j, hipStream_t s) { return rec(ev[k], j, s); }
+   int record_start(int k, int j, hipStream_t s) { return rec(ev0[k], j, s); }
    void reset(int L)
    {
       ev.resize(L);
+      ev0.resize(L);
       ms.assign(L, {});
+      ms0.assign(L, {});
    }
    // elapsed ms of the first cnt[k] events of every level from t0
    int collect(hipEvent_t t0, const std::vector<int> &cnt)
    {
       ms.assign(ev.size(), {});
+      ms0.assign(ev.size(), {});
       for (size_t k = 0; k < ev.size() && k < cnt.size(); k++)
          for (int j = 0; j < cnt[k] && j < (int)ev[k].size(); j++) {
             float m = 0.f;
             if (hipEventElapsedTime(&m, t0, ev[k][j]) != hipSuccess) return -1;
             ms[k].push_back(m);
+            if (j < (int)ev0[k].size()) {
+               if (hipEventElapsedTime(&m, t0, ev0[k][j]) != hipSuccess) return -1;
+               ms0[k].push_back(m);
+            }
          }
       return 0;
    }
    ~AmgCorrTimes()
    {
-      for (auto &v : ev)
-         for (auto e : v) hipEventDestroy(e);
+      for (auto *vv : {&ev, &ev0})
+         for (auto &v : *vv)
+            for (auto e : v) hipEventDestroy(e);
    }
 };
 // anchored operators (interpolation, restriction): row 2t+1's anchor minus

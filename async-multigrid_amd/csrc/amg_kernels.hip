@@ -3253,8 +3253,9 @@ struct EpiResJacobi {
 constexpr int AMG_MZF_NL = 2;
 constexpr int AMG_MZF_NT = AMG_MZF_NL + 2;
 
-template <bool STORE_U>
-__global__ __launch_bounds__(256 * AMG_MZF_NT) void mz_sweep_outer_kernel(
+template <bool STORE_U, int MINB>
+__global__ __launch_bounds__(256 * AMG_MZF_NT) __attribute__((amdgpu_waves_per_eu(MINB * 4))) void
+mz_sweep_outer_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np, MpSten Sv,
    const double *__restrict__ f, const double *__restrict__ u, double *__restrict__ u1out,
    double *__restrict__ rout, double *__restrict__ unext, double omega, int P, int nz, int zc, int npb, int xcd,
@@ -3409,14 +3410,29 @@ void mz_sweep_outer(hipStream_t s, const amg_mat *A, const double *f, const doub
    int zc = std::max(1, std::min(A->ctx->mz_zc, AMG_MZ_MAXZC));
    if (A->ctx->mz_zc_auto) zc = (int)std::max(1LL, std::min((long long)zc, (long long)nz * npb / 1024));
    const int nch = (nz + zc - 1) / zc;
-   if (u1out)
-      mz_sweep_outer_kernel<true><<<npb * nch, 256 * AMG_MZF_NT, 0, s>>>(
+   // AMG_FUSE_OUTER_OCC=2: two workgroups per CU (<= 64 VGPRs; the compiler may spill)
+   static const int occ2 = [] {
+      const char *e = std::getenv("AMG_FUSE_OUTER_OCC");
+      return e && std::atoi(e) == 2;
+   }();
+   auto go = [&](auto store, auto minb) {
+      constexpr bool ST = decltype(store)::value;
+      constexpr int MB = decltype(minb)::value;
+      mz_sweep_outer_kernel<ST, MB><<<npb * nch, 256 * AMG_MZF_NT, 0, s>>>(
          A->ppat, A->mpmask, A->pp_n, Sv, f, u, u1out, rout, unext, omega, P, nz, zc, npb, A->ctx->mz_xcd,
          partials);
-   else
-      mz_sweep_outer_kernel<false><<<npb * nch, 256 * AMG_MZF_NT, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, Sv, f, u, nullptr, rout, unext, omega, P, nz, zc, npb, A->ctx->mz_xcd,
-         partials);
+   };
+   using T = std::true_type;
+   using F = std::false_type;
+   using M1 = std::integral_constant<int, 1>;
+   using M2 = std::integral_constant<int, 2>;
+   if (u1out) {
+      if (occ2) go(T{}, M2{});
+      else go(T{}, M1{});
+   } else {
+      if (occ2) go(F{}, M2{});
+      else go(F{}, M1{});
+   }
 }
 
 __device__ __forceinline__ const double *epi_pf_vec(const EpiJacobi &e) { return e.x; }

@@ -1504,6 +1504,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
             amgk::res_update(us, H->r0, a.y, a.y_fine, n0, 0);
             AMG_TRY(from_update());
          } else {
+            if (rec && H->corr.record_start(k, issued[k], s)) return amg_set_error(AMG_ERR_HIP, "correction event");
             amgk::vaxpy(s, 1.0, a.e[0], a.f_acc, 0, n0);
             amgk::res_update(s, H->r0, a.y, a.y_fine, n0, 1);
          }
@@ -1515,6 +1516,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
             amgk::semi_correct(us, v0.u, a.e[0], a.u_priv, n0);
             AMG_TRY(from_update());
          } else if (!fused) {
+            if (rec && H->corr.record_start(k, issued[k], s)) return amg_set_error(AMG_ERR_HIP, "correction event");
             amgk::atomic_correct(s, v0.u, a.e[0], a.u_priv, n0);
          }
          if (rec && H->corr.record(k, issued[k], s)) return amg_set_error(AMG_ERR_HIP, "correction event");
@@ -1753,7 +1755,10 @@ extern "C" int amg_hier_set_async_times(amg_hier *H, const double *t, const int 
 extern "C" int amg_async_correction_ms(const amg_hier *H, int level, double *ms, int cap, int *count)
 {
    AMG_ARG(H && count && level >= 0 && level < H->L, "amg_async_correction_ms: bad argument");
-   const auto &v = level < (int)H->corr.ms.size() ? H->corr.ms[level] : std::vector<double>();
+   const bool start = cap < 0; // cap < 0: the update windows' start times, -cap entries
+   if (start) cap = -cap;
+   const auto &vv = start ? H->corr.ms0 : H->corr.ms;
+   const auto &v = level < (int)vv.size() ? vv[level] : std::vector<double>();
    *count = (int)v.size();
    for (int j = 0; j < (int)v.size() && j < cap && ms; j++) ms[j] = v[j];
    return AMG_OK;

@@ -321,10 +321,11 @@ class DistHier:
         flat, n = _times_flat(times)
         check(lib.amg_dist_hier_set_async_times(self.h, _dp(flat), _ip(n), int(n.size)))
 
-    def async_correction_ms(self):
-        """per level: end times (ms) of this rank's corrections in the last free-race async_solve"""
+    def async_correction_ms(self, start=False):
+        """per level: end (start=True: start) times (ms) of this rank's update windows in the last
+        free-race async_solve"""
         from . import _corr_ms
-        return _corr_ms(lib.amg_dist_async_correction_ms, self.h, self.L)
+        return _corr_ms(lib.amg_dist_async_correction_ms, self.h, self.L, start)
 
     def async_level_ms(self):
         """per level: ms from the last async_solve's start to the level's last correction"""

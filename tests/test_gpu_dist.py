@@ -314,9 +314,9 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
         A, P, R = parts[r]
         D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
         out = []
-        for _ in range(2):
+        for _ in range(3):
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-            out.append((rel, D.get_u(), cnt.copy(), D.async_correction_ms()))
+            out.append((rel, D.get_u(), cnt.copy(), D.async_correction_ms(), D.async_correction_ms(start=True)))
         D.free()
         amg.dist.finalize(c)
         c.close()
@@ -325,7 +325,7 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
     res = run_ranks(nranks, rank)
     from async_band import replay_check
     rels, runs = [], []
-    for q in range(2):
+    for q in range(3):
         rq = [t[q][0] for t in res]
         assert all(r == rq[0] for r in rq)  # one allreduced norm
         u = np.concatenate([t[q][1] for t in res])
@@ -334,7 +334,7 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
         assert list(cnt[:L - 1]) == [N] * (L - 1)
         assert rq[0] < 1.0
         rels.append(rq[0])
-        runs.append((rq[0], [t[q][3] for t in res], [int(x) for x in rs[0]]))
+        runs.append((rq[0], [t[q][3] for t in res], [int(x) for x in rs[0]], [t[q][4] for t in res]))
     # the oracle's model of each run: the replay of its recorded update orders
     # (every correction's update point; the slowest rank's and each rank's),
     # or_async_add under the timed schedule (the arithmetic itself is pinned by
@@ -607,7 +607,7 @@ def test_dist_async_additive_accel(amg, oracle, solver, accel, cuts, grid, bound
             D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
             u = D.get_u()
-            ms = D.async_correction_ms()
+            ms = (D.async_correction_ms(), D.async_correction_ms(start=True))
             D.free()
             amg.dist.finalize(c)
             c.close()
@@ -616,11 +616,11 @@ def test_dist_async_additive_accel(amg, oracle, solver, accel, cuts, grid, bound
         res = run_ranks(nranks, rank)
         assert all(t[0] == res[0][0] for t in res)
         assert all(np.all(np.isfinite(t[1])) for t in res)
-        return res[0][0], [t[3] for t in res]
+        return res[0][0], [t[3][0] for t in res], [t[3][1] for t in res]
 
     from async_band import replay_check
-    (rel_acc, d_acc), (rel_plain, _) = solve(acc), solve(amg.AMG_NO_ACCEL)
-    d_acc = (d_acc, [int(x) for x in rs[0]])
+    (rel_acc, d_acc, s_acc), (rel_plain, _, _) = solve(acc), solve(amg.AMG_NO_ACCEL)
+    d_acc = (d_acc, [int(x) for x in rs[0]], s_acc)
     assert rel_acc < 1.0
     opts = amg.default_opts(solver=a_solver, smooth_weight=w, num_cycles=N, tol=0.0, accel_type=acc,
                             cheby_mu=mu, cheby_delta=delta, cheby_grid=grid)

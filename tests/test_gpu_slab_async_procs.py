@@ -52,7 +52,8 @@ def _rank(rank, world, port, n, optd, rep, runs, q):
         for _ in range(runs):
             dist.barrier()  # the ranks enter the solve together
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-            out.append((float(rel), [int(x) for x in cnt], D.get_u(), [t.tolist() for t in D.async_correction_ms()]))
+            out.append((float(rel), [int(x) for x in cnt], D.get_u(), [t.tolist() for t in D.async_correction_ms()],
+                        [t.tolist() for t in D.async_correction_ms(start=True)]))
         row0 = D.row0
         D.free()
         amg.dist.finalize(c)
@@ -98,7 +99,8 @@ def slab_async_procs(n, optd, world, rep=1 << 10, runs=1):
         assert all(got[r][2][k][0] == rel for r in range(world))  # one allreduced norm
         u = np.concatenate([got[r][2][k][2] for r in order])
         rs = [got[r][1] for r in order] + [got[order[-1]][1] + got[order[-1]][2][k][2].size]
-        out.append((rel, got[0][2][k][1], u, [got[r][2][k][3] for r in order], rs))  # per rank
+        out.append((rel, got[0][2][k][1], u, [got[r][2][k][3] for r in order], rs,
+                    [got[r][2][k][4] for r in order]))  # per rank
     return out
 
 
@@ -142,7 +144,7 @@ def test_slab_async_processes_schedule_bitwise(amg, oracle, solver, comp, world,
     finally:
         oracle.lib().or_set_async_schedule(0)
     gen.free()
-    for k, (rel, cnt, u, _, _) in enumerate(runs):
+    for k, (rel, cnt, u, _, _, _) in enumerate(runs):
         nd = int(np.count_nonzero(u.view(np.uint64) != uo.view(np.uint64)))
         print(f"slab async processes {solver} composed={comp} {world} processes schedule {sched} n={n} "
               f"solve {k}: device {rel:.13e} oracle {relo:.13e}, differing entries {nd}")
@@ -168,10 +170,11 @@ def test_slab_async_processes_free_race(amg, oracle):
     gen.free()
     opts = amg.default_opts(**optd)
     for world in (2, 3):
-        runs = slab_async_procs(n, optd, world, rep=1 << 12, runs=2)
-        for rel, cnt, u, ms, _ in runs:
+        runs = slab_async_procs(n, optd, world, rep=1 << 12, runs=3)
+        for rel, cnt, u, ms, _, _ in runs:
             assert list(cnt[:L - 1]) == [N] * (L - 1)
             assert np.all(np.isfinite(u))
-        widest = replay_check(amg, oracle, host, f, opts, [(r[0], r[3], r[4]) for r in runs], composed=True,
+            assert rel < 1.0
+        widest = replay_check(amg, oracle, host, f, opts, [(r[0], r[3], r[4], r[5]) for r in runs], composed=True,
                               what=f"slab async {world} processes")
         assert widest <= 20.0

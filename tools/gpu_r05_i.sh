@@ -1,0 +1,25 @@
+#!/bin/bash
+# round 5 (i): the replay checks with torn-update detection (slab threads and
+# processes, row-partitioned, elasticity), and the fused post-sweep +
+# outer-residual march at 1 and 2 workgroups per CU
+set -o pipefail
+O=gpurun_out/r05i
+mkdir -p $O
+export AMG_SEGV_TRACE=1
+run() { # name timeout files...
+   local name=$1 t=$2; shift 2
+   timeout -k 10 $t python -u -m pytest "$@" -m "gpu and not slow" -v -s -rf --timeout 240 --timeout-method thread \
+      > $O/$name.log 2>&1
+   local rc=$?; echo "$name exit $rc"; grep -E "passed|failed" $O/$name.log | tail -2
+   return $rc
+}
+run slab_async 400 tests/test_gpu_slab_async.py
+run procs 400 tests/test_gpu_slab_async_procs.py
+run dist_band 400 tests/test_gpu_dist.py -k "band or accel"
+run elast 400 tests/test_gpu_elast_async.py
+grep -hE "run [0-9]: device" $O/*.log | sed 's/^ *//' > $O/replay_summary.txt
+for occ in 1 2; do
+  AMG_FUSE_OUTER_OCC=$occ timeout -k 10 200 python -u bench.py --fuse-outer 2 --cpu-baseline 0 --general 0 \
+     > $O/fo2_occ$occ.json 2> $O/fo2_occ$occ.err
+  echo "fuse_outer 2 occ $occ exit $?: $(grep -o '"ms_per_step": [0-9.]*' $O/fo2_occ$occ.json)"; grep -E "post_sweep_outer" $O/fo2_occ$occ.err
+done

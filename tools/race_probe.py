@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--runs", type=int, default=6)
     ap.add_argument("--ranks", type=int, default=1)
     ap.add_argument("--cycles", type=int, default=12)
+    ap.add_argument("--form", choices=("slab", "single"), default="slab")
     a = ap.parse_args()
     from conftest import load_package
     from oracle import pyoracle as oracle
@@ -31,7 +32,17 @@ def main():
                             smooth_transfer=1)
     host = host_hier(amg, oracle, gen)
     L = gen.L
-    runs = slab_async(amg, gen, opts, f, a.ranks, rccl1=True, runs=a.runs)
+    if a.form == "single":
+        ctx = amg.Context(0, nstreams=L + 2)
+        dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v] for k, v in host.items()}
+        H = amg.Hier(ctx, dev["A"], dev["P"], dev["R"], opts)
+        runs = []
+        for _ in range(a.runs):
+            u, rel, cnt = H.async_solve(f)
+            runs.append((rel, cnt, u, [H.async_correction_ms()], [0, a.n ** 3]))
+        H.free()
+    else:
+        runs = slab_async(amg, gen, opts, f, a.ranks, rccl1=True, runs=a.runs)
     for i, (rel, cnt, u, ms, rs) in enumerate(runs):
         if a.ranks > 1:
             rep = sliced_replay(amg, oracle, host, f, opts, ms, rs, composed=True)
