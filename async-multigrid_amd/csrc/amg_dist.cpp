@@ -885,6 +885,7 @@ extern "C" int amg_dist_hier_free(amg_dist_hier *D)
    hipStreamSynchronize(D->ctx->comm_stream);
    for (auto s : D->ctx->level_streams) hipStreamSynchronize(s);
    if (D->links) link_free(D->links); // collective (a barrier between unmapping and freeing)
+   if (D->ajac_links) link_free(D->ajac_links);
    // the rest under the process-wide teardown lock (not link_free: a peer
    // blocked in its barrier would hold it)
    std::lock_guard<std::recursive_mutex> td(amg_teardown_mutex());

@@ -987,6 +987,14 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
    return async_jacobi_run(D, f_local, sweeps, l1, false, relres, nullptr);
 }
 
+extern "C" int amg_dist_async_jacobi_stats(const amg_dist_hier *D, double *stats, int n)
+{
+   AMG_ARG(D && stats && n >= 0, "amg_dist_async_jacobi_stats: bad argument");
+   AMG_ARG(!D->ajac_stats.empty(), "amg_dist_async_jacobi_stats: no asynchronous Jacobi run yet");
+   for (int i = 0; i < n && i < (int)D->ajac_stats.size(); i++) stats[i] = D->ajac_stats[i];
+   return AMG_OK;
+}
+
 extern "C" int amg_dist_async_sps(amg_dist_hier *D, const double *f_local, int sweeps, double *relres,
                                   long long *relaxations)
 {
@@ -1083,6 +1091,62 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
       hipEventCreateWithFlags(&sent[q], hipEventDisableTiming);
       hipEventCreateWithFlags(&arrived[q], hipEventDisableTiming);
    }
+   // the overlap record: per sweep the exchange window on the comm stream and
+   // the interior product's window on the compute stream (timing events)
+   std::vector<hipEvent_t> tev((size_t)sweeps * 4, nullptr);
+   for (auto &e : tev) hipEventCreate(&e);
+   auto tx0 = [&](int k) { return tev[(size_t)k * 4]; };
+   auto tx1 = [&](int k) { return tev[(size_t)k * 4 + 1]; };
+   auto ti0 = [&](int k) { return tev[(size_t)k * 4 + 2]; };
+   auto ti1 = [&](int k) { return tev[(size_t)k * 4 + 3]; };
+   // the deltas through device-resident channels (amg_link.cpp) where the
+   // ranks share a node: a send is a copy kernel on the comm stream straight
+   // into the neighbour's slot (overlapping the interior product on the
+   // compute stream), a receive an MPI_Test-like poll; SPS (norms ride with
+   // the deltas) and AMG_AJAC_LINKS=0 keep the transport's grouped send/recv
+   static const bool links_env = [] {
+      const char *e = std::getenv("AMG_AJAC_LINKS");
+      return e ? std::atoi(e) != 0 : true;
+   }();
+   const bool use_links = !sps && links_env && c->xport->nranks > 1;
+   if (use_links && !D->ajac_links) {
+      std::vector<long long> caps(c->xport->nranks, 0);
+      for (int i = 0; i < np; i++) caps[M.peers[i]] = M.rcnt[i];
+      if ((st = link_create(D, 1, caps, &D->ajac_links)) != AMG_OK) return fail(st);
+   }
+   if (use_links && (st = link_reset(D->ajac_links, true)) != AMG_OK) return fail(st);
+   std::vector<long long> got_cnt(np, 0);
+   long long on_time = 0, late = 0;
+   // r -= A_offd g on the rows that have ghost columns (outside the interior [b0, b1))
+   auto apply_offd = [&]() {
+      amgk::spgemv(s, M.A, gext, r, upd, r, 0, M.b0, nullptr);
+      amgk::spgemv(s, M.A, gext, r, upd, r, M.b1, n, nullptr);
+   };
+   // every delta that has arrived from peer i, each applied on its own, then
+   // the ghost region cleared (so no delta is applied twice)
+   auto poll_links = [&](int k, bool block) -> int {
+      for (int i = 0; i < np; i++) {
+         if (M.rcnt[i] <= 0) continue;
+         for (;;) {
+            int got = 0;
+            double *dst = gext + no + M.roff[i];
+            if (block) {
+               if (got_cnt[i] >= sweeps) break;
+               AMG_TRY(link_recv(D->ajac_links, 0, M.peers[i], dst, M.rcnt[i], s));
+               got = 1;
+            } else {
+               AMG_TRY(link_try_recv(D->ajac_links, 0, M.peers[i], dst, M.rcnt[i], s, &got));
+            }
+            if (!got) break;
+            if (got_cnt[i] == k) on_time++;
+            else late++;
+            got_cnt[i]++;
+            apply_offd();
+            amgk::vset(s, gext + no + M.roff[i], 0.0, 0, M.rcnt[i]);
+         }
+      }
+      return AMG_OK;
+   };
    std::vector<int> pending; // relaxations whose ghost deltas are not applied yet
    auto apply = [&](int k) -> int {
       const int q = k % AJ_NBUF;
@@ -1123,6 +1187,27 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
                                        count);
       }
       ajac_update_k<<<nb, 256, 0, s>>>(r, wv, eext, x, dacc, n, am, om1, omd, gate);
+      if (use_links) {
+         if (np > 0) {
+            launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * SS, (int)M.nsend);
+            AMG_HIP(hipEventRecord(packed[q], s));
+            AMG_HIP(hipStreamWaitEvent(cs, packed[q], 0));
+         }
+         AMG_HIP(hipEventRecord(tx0(k), cs));
+         for (int i = 0; i < np && st == AMG_OK; i++)
+            if (M.scnt[i] > 0)
+               st = link_send(D->ajac_links, 0, M.peers[i], sbuf + (size_t)q * SS + M.soff[i], M.scnt[i], cs);
+         if (st != AMG_OK) break;
+         AMG_HIP(hipEventRecord(tx1(k), cs));
+         AMG_HIP(hipEventRecord(sent[q], cs));
+         // r -= A_diag e (ghost region of e_ext stays zero), overlapping the sends
+         AMG_HIP(hipEventRecord(ti0(k), s));
+         amgk::spgemv(s, M.A, eext, r, upd, r, 0, n, nullptr);
+         AMG_HIP(hipEventRecord(ti1(k), s));
+         if ((st = poll_links(k, false)) != AMG_OK) break;
+         D->iter = k + 1;
+         continue;
+      }
       if (np > 0) {
          if (sps) { // the norm travels with the deltas (data[vec_len + 1], DMEM_Comm.cpp:216-220)
             const long long m = std::max<long long>(M.nsend, np);
@@ -1133,6 +1218,7 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
          }
          AMG_HIP(hipEventRecord(packed[q], s));
          AMG_HIP(hipStreamWaitEvent(cs, packed[q], 0));
+         AMG_HIP(hipEventRecord(tx0(k), cs));
          std::vector<void *> sp(np), rp(np);
          std::vector<long long> sb(np), rb(np);
          const int g = sps ? 1 : 0;
@@ -1148,8 +1234,11 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
          AMG_HIP(hipEventRecord(arrived[q], cs));
          pending.push_back(k);
       }
+      AMG_HIP(hipEventRecord(tx1(k), cs));
       // r -= A_diag e (ghost region of e_ext stays zero), overlapping the exchange
+      AMG_HIP(hipEventRecord(ti0(k), s));
       amgk::spgemv(s, M.A, eext, r, upd, r, 0, n, nullptr);
+      AMG_HIP(hipEventRecord(ti1(k), s));
       // deltas that have already arrived (host poll: never blocks)
       for (size_t i = 0; i < pending.size();) {
          if (hipEventQuery(arrived[pending[i] % AJ_NBUF]) == hipSuccess) {
@@ -1162,12 +1251,71 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
       D->iter = k + 1;
    }
    for (size_t i = 0; st == AMG_OK && i < pending.size(); i++) st = apply(pending[i]); // drain
+   if (use_links && st == AMG_OK) {
+      st = poll_links(sweeps, true); // the deltas still in flight, each applied once
+      if (st == AMG_OK) st = link_drain(D->ajac_links, 0);
+      for (int i = 0; i < np && st == AMG_OK; i++)
+         if (M.rcnt[i] > 0 && got_cnt[i] != sweeps)
+            st = amg_set_error(AMG_ERR_RCCL, "amg_dist_async_jacobi: %lld deltas from rank %d, expected %d",
+                               got_cnt[i], M.peers[i], sweeps);
+      if (st != AMG_OK) link_abort(D->ajac_links);
+   }
    for (int q = 0; q < AJ_NBUF; q++) {
       hipEventDestroy(packed[q]);
       hipEventDestroy(sent[q]);
       hipEventDestroy(arrived[q]);
    }
-   if (st != AMG_OK) return fail(st);
+   if (st != AMG_OK) {
+      for (auto e : tev) hipEventDestroy(e);
+      return fail(st);
+   }
+   // the overlap record: the fraction of each sweep's exchange window that the
+   // interior product covers, the windows' lengths
+   {
+      AMG_HIP(hipStreamSynchronize(cs));
+      AMG_HIP(hipStreamSynchronize(s));
+      double hid = 0.0, xs = 0.0, is = 0.0;
+      int cntk = 0;
+      for (int k = 0; k < sweeps && np > 0; k++) {
+         float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
+         if (hipEventElapsedTime(&a0, tx0(0), tx0(k)) != hipSuccess ||
+             hipEventElapsedTime(&a1, tx0(0), tx1(k)) != hipSuccess ||
+             hipEventElapsedTime(&b0, tx0(0), ti0(k)) != hipSuccess ||
+             hipEventElapsedTime(&b1, tx0(0), ti1(k)) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+         }
+         const double xd = a1 - a0, ov = std::max(0.0, (double)std::min(a1, b1) - (double)std::max(a0, b0));
+         hid += xd > 0 ? std::min(1.0, ov / xd) : 1.0;
+         xs += xd;
+         is += b1 - b0;
+         cntk++;
+      }
+      long long nrecv = 0;
+      for (int i = 0; i < np; i++) nrecv += M.rcnt[i] > 0 ? 1 : 0;
+      D->ajac_stats.assign(8, 0.0);
+      D->ajac_stats[0] = cntk ? hid / cntk : 0.0;  // hidden fraction of the exchange
+      D->ajac_stats[1] = cntk ? xs / cntk : 0.0;   // exchange window, ms per sweep
+      D->ajac_stats[2] = cntk ? is / cntk : 0.0;   // interior product, ms per sweep
+      D->ajac_stats[3] = use_links && nrecv * sweeps > 0 ? (double)on_time / (double)(nrecv * sweeps) : -1.0;
+      D->ajac_stats[4] = use_links ? (double)late : -1.0;
+      D->ajac_stats[7] = use_links ? 1.0 : 0.0;
+   }
+   for (auto e : tev) hipEventDestroy(e);
+   // every delta applied once <=> the incrementally kept r equals f - A x (to
+   // rounding): its global norm, beside the true residual's below
+   {
+      double *pp;
+      if ((st = amg_ctx_partials(c, 65536, &pp)) != AMG_OK) return fail(st);
+      int parts = 0;
+      amgk::sumsq_partials(s, r, n, pp, &parts);
+      amgk::reduce_partials(s, pp, parts, D->d_hist + 3, 0, c->d_scalars + 4096);
+      if ((st = xp_allreduce(c, s, D->d_hist + 3, 1)) != AMG_OK) return fail(st);
+      launch_sqrt(s, D->d_hist + 3, D->d_hist + 3);
+      double rn = 0.0;
+      if ((st = d2h(s, &rn, D->d_hist + 3, sizeof(double))) != AMG_OK) return fail(st);
+      D->ajac_stats[5] = rn;
+   }
    if (relaxations) {
       *relaxations = sps ? 0 : sweeps;
       if (sps && (st = d2h(s, relaxations, count, sizeof(long long))) != AMG_OK) return fail(st);
@@ -1189,6 +1337,7 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
    if ((st = d2h(s, hn + 1, D->d_hist + 2, sizeof(double))) != AMG_OK) return fail(st);
    D->r0norm = hn[1];
    D->have_state = true;
+   D->ajac_stats[6] = hn[0]; // the true residual norm
    if (relres) *relres = hn[1] > 0 ? hn[0] / hn[1] : 0.0;
    for (double *q : dtmp) hipFree(q);
    return AMG_OK;

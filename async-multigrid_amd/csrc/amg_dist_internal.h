@@ -139,6 +139,9 @@ int link_create(amg_dist_hier *D, int K, const std::vector<long long> &caps, Lin
 int link_reset(LinkSet *L, bool one_thread);
 int link_send(LinkSet *L, int k, int peer, const double *src, long long n, hipStream_t s);
 int link_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipStream_t s);
+// MPI_Test + receive: if the next message from peer has arrived, launch its
+// unpack on s and set *got = 1; else *got = 0 and return at once
+int link_try_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipStream_t s, int *got);
 int link_drain(LinkSet *L, int k); // publish everything level group k has in flight
 void link_abort(LinkSet *L);       // tell every peer to give up waiting on this rank
 void link_free(LinkSet *L);
@@ -216,6 +219,10 @@ struct amg_dist_hier {
    // the per-level device-resident channels between ranks
    std::vector<amgd::AsyncLevel> al;
    amgd::LinkSet *links = nullptr;
+   amgd::LinkSet *ajac_links = nullptr; // DMEM_AsyncSmooth's delta channels (one group)
+   // amg_dist_async_jacobi_stats: the last asynchronous Jacobi run's overlap
+   // and delta accounting
+   std::vector<double> ajac_stats;
    std::vector<amg_mat *> cA, cP, cR; // replicated levels' operators (level Ld + i)
    std::vector<double *> cl1;         // and their l1 norms
    // DMEM_Mult with acceleration (accel_type != 0): x (the iterate; lv[0].u

@@ -442,6 +442,26 @@ int amgd::link_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipSt
    return AMG_OK;
 }
 
+int amgd::link_try_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipStream_t s, int *got)
+{
+   Chan &c = L->c(k, peer);
+   AMG_ARG(n <= c.rcap, "link_try_recv: %lld doubles from rank %d on level %d (capacity %lld)", n, peer, k, c.rcap);
+   *got = 0;
+   AMG_TRY(progress(L, k));
+   const unsigned long long seq = c.rseq + 1;
+   if (c.r_arrived->v.load(std::memory_order_acquire) < seq || c.rseq - c.r_pub >= MAX_EV) {
+      if (aborted(L, peer)) return amg_set_error(AMG_ERR_RCCL, "link: receive (level %d, rank %d <-> %d): aborted", k,
+                                                 L->me, peer);
+      return AMG_OK;
+   }
+   launch_copy(s, c.rslot + (long long)(seq % NS) * c.rcap, dst, n);
+   AMG_HIP(hipGetLastError());
+   AMG_HIP(hipEventRecord(c.rev[seq % MAX_EV], s));
+   c.rseq = seq;
+   *got = 1;
+   return AMG_OK;
+}
+
 int amgd::link_drain(LinkSet *L, int k)
 {
    for (int p = 0; p < L->R; p++) {

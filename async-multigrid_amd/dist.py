@@ -342,6 +342,14 @@ class DistHier:
         check(lib.amg_dist_async_jacobi(self.h, _dp(f), int(sweeps), int(l1), C.byref(rel)))
         return rel.value
 
+    def async_jacobi_stats(self):
+        """the last async_jacobi run: dict of the exchange overlap and delta accounting"""
+        st = np.zeros(8)
+        check(lib.amg_dist_async_jacobi_stats(self.h, _dp(st), 8))
+        keys = ("hidden_fraction", "exchange_ms_per_sweep", "interior_ms_per_sweep", "on_time_fraction",
+                "late_deltas", "incremental_resnorm", "true_resnorm", "device_links")
+        return dict(zip(keys, st.tolist()))
+
     def async_sps(self, f_local, sweeps):
         """-smoother async_sps (stochastic parallel Southwell gating of the
         asynchronous Jacobi, opts.sps_*): (relres, sweeps this rank relaxed in)."""

@@ -659,6 +659,16 @@ int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int *level_cor
  * start to the level's last correction (HIP events; 0 for levels without a
  * correction group); ms holds L entries */
 int amg_dist_async_level_ms(const amg_dist_hier *D, double *ms);
+/* the last amg_dist_async_jacobi run of this rank: [0] the fraction of each
+ * sweep's ghost-delta exchange window (comm stream) covered by the interior
+ * product r -= A_diag e (compute stream), averaged over the sweeps; [1] the
+ * exchange window, ms per sweep; [2] the interior product, ms per sweep;
+ * [3] the fraction of the received deltas applied in the sweep they were sent
+ * (device-resident channels; -1 otherwise); [4] deltas applied in a later
+ * sweep; [5] ||r|| as kept incrementally (global); [6] ||f - A x|| (global):
+ * equal to rounding when every delta was applied exactly once; [7] 1 when the
+ * deltas went through the device-resident channels (amg_link.cpp) */
+int amg_dist_async_jacobi_stats(const amg_dist_hier *D, double *stats, int n);
 /* AMG_SCHED_TIMED on the distributed solve: level k's time per correction
  * (every rank passes the same values, so every rank issues the same order) */
 int amg_dist_hier_set_async_durations(amg_dist_hier *D, const double *ms, int n);

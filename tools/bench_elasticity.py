@@ -26,6 +26,12 @@ def main():
     p.add_argument("--theta", type=float, default=0.5)
     p.add_argument("--omega", type=float, default=0.6)
     p.add_argument("--gpu-setup", type=int, default=1, help="Galerkin products on the GPU (classical opts.device)")
+    p.add_argument("--async-ranks", type=int, default=0,
+                   help="also run config 5's asynchronous additive cycle (DMEM_Add: ASYNC_MULTADD, smoothed "
+                        "transfers composed) on this hierarchy as R row-partitioned ranks (threads on this GPU)")
+    p.add_argument("--async-cycles", type=int, default=10)
+    p.add_argument("--async-omega", type=float, default=None, help="smooth weight of the async cycle (default --omega)")
+    p.add_argument("--async-runs", type=int, default=2)
     a = p.parse_args()
     amg = load_package()
     t0 = time.time()
@@ -91,9 +97,79 @@ def main():
            "relres_after": rn / r0, "cycles": a.warmup + a.steps,
            "setup_s": {"generate": t1 - t0, "classical": t2 - t1,
                        "galerkin_on": "gpu" if a.gpu_setup else "host"}}
-    print(json.dumps(out), flush=True)
     Hd.free()
     ctx.close()
+    if a.async_ranks:
+        out["async_additive"] = async_leg(amg, H, b, a)
+    print(json.dumps(out), flush=True)
+
+
+def async_leg(amg, H, b, a):
+    """DMEM_Add's asynchronous additive cycle (DMEM_Add.cpp:20-178) on the
+    elasticity hierarchy: R ranks (threads, one GPU, per-level device-resident
+    channels), every level group on its own host thread and stream, N
+    corrections per level with the reference's smoothed transfers composed
+    (smooth_transfer = 1).  Additive cycles/s = N over the slowest level's
+    finish; relres after the race; the level finish times."""
+    import numpy as np
+    from test_gpu_classical import host_levels
+    from test_gpu_dist import run_ranks, split_host
+    lv = host_levels(amg, H)
+    L = len(lv["A"])
+    R, N = a.async_ranks, a.async_cycles
+    w = a.async_omega if a.async_omega is not None else a.omega
+    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=w, num_cycles=N, tol=0.0, smooth_transfer=1)
+    host = {k: [tuple(m) for m in v] for k, v in lv.items()}
+
+    class _M:  # split_host wants .nrows / .ncols / .rowptr / .col / .val
+        def __init__(self, t):
+            self.nrows, self.ncols, self.rowptr, self.col, self.val = t
+    host = {k: [_M(t) for t in v] for k, v in host.items()}
+    cuts = tuple((i + 1) / R for i in range(R - 1))
+    rs, parts = split_host(host, cuts)
+    del host, lv
+    hub = amg.dist.ThreadMailbox(R, timeout=1200.0)
+    fb = np.ascontiguousarray(b, dtype=np.float64)
+
+    def rank(r):
+        c = amg.Context(0, nstreams=L + 2)
+        if R == 1:
+            amg.dist.init_rccl(c, 1, 0, lambda x: x)
+        else:
+            amg.dist.init_host(c, R, r, amg.dist.HostTransport(hub, r))
+        A, P, Rm = parts[r]
+        D = amg.dist.DistHier.from_parts(c, rs, A, P, Rm, opts)
+        res = []
+        for q in range(a.async_runs + 1):  # the first solve sets up the level groups and channels
+            amg.dist.barrier(c)
+            t1 = time.perf_counter()
+            rel, cnt = D.async_solve(fb[D.row0:D.row0 + D.n0])
+            dt = time.perf_counter() - t1
+            if q:
+                res.append((rel, [int(x) for x in cnt], [float(x) for x in D.async_level_ms()], dt))
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        return res
+
+    t0 = time.time()
+    out = run_ranks(R, rank)
+    runs = []
+    for q in range(a.async_runs):
+        lvms = np.max(np.array([out[r][q][2] for r in range(R)]), axis=0)
+        active = int(np.count_nonzero(out[0][q][1]))
+        slowest = float(np.max(lvms[:active]))
+        runs.append({"relres": out[0][q][0], "corrections": out[0][q][1][:active],
+                     "level_finish_ms": [round(x, 2) for x in lvms[:active].tolist()],
+                     "wall_s": max(out[r][q][3] for r in range(R)), "cycles_per_s": N / (slowest * 1e-3)})
+        print(f"[elast async] {R} ranks run {q}: relres {runs[-1]['relres']:.4e}, slowest level {slowest:.1f} ms",
+              file=sys.stderr, flush=True)
+    best = max(runs, key=lambda r: r["cycles_per_s"])
+    return {"metric": "asynchronous additive cycles/s (every level N corrections)", "value": best["cycles_per_s"],
+            "ranks": R, "num_cycles": N, "smooth_weight": w, "levels": L, "runs": runs,
+            "workload": f"DMEM_Add ASYNC_MULTADD, smoothed transfers composed, {R} row-partitioned ranks "
+                        "(threads) on one GPU, per-level device-resident channels",
+            "setup_and_runs_s": time.time() - t0}
 
 
 if __name__ == "__main__":

@@ -23,3 +23,6 @@ for occ in 1 2; do
      > $O/fo2_occ$occ.json 2> $O/fo2_occ$occ.err
   echo "fuse_outer 2 occ $occ exit $?: $(grep -o '"ms_per_step": [0-9.]*' $O/fo2_occ$occ.json)"; grep -E "post_sweep_outer" $O/fo2_occ$occ.err
 done
+run ajac 300 tests/test_gpu_dist.py -k "async_jacobi or sps"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_dist.py -k "async_jacobi_512" -m slow -v -s -rf --timeout 560 \
+   --timeout-method thread > $O/ajac512.log 2>&1; echo "ajac512 exit $?"; grep -E "512\^3 async|passed|failed" $O/ajac512.log | tail -10
