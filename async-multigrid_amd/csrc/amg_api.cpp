@@ -154,6 +154,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_JGS_SMALL")) c->jgs_small = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_WAVE")) c->jgs_wave = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_BSR3_XS")) c->bsr3_xs = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ_EDGE")) c->mz_edge = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ27_OCC")) c->mz27_occ = std::max(-1, std::min(8, std::atoi(v)));
    if (const char *v = std::getenv("AMG_MZ_OCC")) c->mz_occ = std::max(-1, std::min(8, std::atoi(v)));

@@ -176,6 +176,7 @@ struct amg_ctx {
    int fuse_xfer = 1;      // composed smoothed transfers of marched 7-pt levels in one pass each
    int fuse_xfp_slab = 0;  // ... and the slab async solve's fused prolongation + atomic (AMG_FUSE_XFP_SLAB)
    int fuse_prolong = 0;   // prolongation fused into the first post sweep (measured slower: off)
+   int bsr3_xs = 1;        // 3x3 block kernel: one x load per lane, shared over the triplet (AMG_BSR3_XS)
    int fuse_outer = 0;     // level 0's last post sweep + the outer residual as one march (AMG_FUSE_OUTER;
                            // 1: u' stored every step, 2: only at the end of an iterate batch)
    int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)

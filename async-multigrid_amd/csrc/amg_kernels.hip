@@ -3479,7 +3479,7 @@ Gemv gemv_mode(double alpha, double beta)
 // identity rows of fixed dofs) run the CSR row loop.  Per block row the
 // value-indexed form streams 27 x (12 + 4) bytes against 81 x 5 for
 // value-indexed CSR.
-template <int NEG, bool NEED_DIAG, class Epi, bool VI>
+template <int NEG, bool NEED_DIAG, class Epi, bool VI, bool XS = false>
 __global__ __launch_bounds__(256) void bsr3_kernel(const long long *__restrict__ soff, const int *__restrict__ bcol,
                                                    const int *__restrict__ bdiag,
                                                    const unsigned char *__restrict__ bcnt,
@@ -3540,6 +3540,26 @@ __global__ __launch_bounds__(256) void bsr3_kernel(const long long *__restrict__
             jj[u] = bcol[sp];
             row3(sp, vv[u][0], vv[u][1], vv[u][2]);
          }
+         if (XS) {
+            // XS: lane c of the triplet loads the node's component c (one
+            // 8-byte load per lane and block instead of three), the other two
+            // come from the triplet's lanes (ds_bpermute)
+            double xl[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) xl[u] = x[3 * (size_t)jj[u] + c];
+            const int l0 = lane - c;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+               const int k = kc + u;
+               const double x0 = __shfl(xl[u], l0, 64), x1 = __shfl(xl[u], l0 + 1, 64),
+                            x2 = __shfl(xl[u], l0 + 2, 64);
+               if (k >= cnt) continue; // (every lane takes part in the shuffles)
+               if (k != kd || c != 0) madd(vv[u][0], x0);
+               if (k != kd || c != 1) madd(vv[u][1], x1);
+               if (k != kd || c != 2) madd(vv[u][2], x2);
+            }
+            continue;
+         }
 #pragma unroll
          for (int u = 0; u < U; u++) {
             const int k = kc + u;
@@ -3561,14 +3581,25 @@ static void launch_bsr3(hipStream_t s, const amg_mat *A, const double *x, int rb
    const int t0 = rb / 3, t1 = re / 3;
    const int nsl = (t1 - t0 + 20) / 21;
    const int nb = (nsl + 3) / 4;
-   if (A->bsr3 == 1)
-      bsr3_kernel<NEG, NEED_DIAG, Epi, true><<<nb, 256, 0, s>>>(A->soff, A->bcol, A->bdiag, A->bmode, A->bvi,
-                                                                 nullptr, A->vtab, A->rowptr, A->col, A->val, x,
-                                                                 t0, t1, e);
-   else
-      bsr3_kernel<NEG, NEED_DIAG, Epi, false><<<nb, 256, 0, s>>>(A->soff, A->bcol, A->bdiag, A->bmode, nullptr,
-                                                                  A->bval, nullptr, A->rowptr, A->col, A->val, x,
-                                                                  t0, t1, e);
+   // ctx->bsr3_xs: the node's x shared across the block row's three lanes
+   const bool xs = A->ctx->bsr3_xs != 0;
+   if (A->bsr3 == 1) {
+      if (xs)
+         bsr3_kernel<NEG, NEED_DIAG, Epi, true, true><<<nb, 256, 0, s>>>(
+            A->soff, A->bcol, A->bdiag, A->bmode, A->bvi, nullptr, A->vtab, A->rowptr, A->col, A->val, x, t0, t1, e);
+      else
+         bsr3_kernel<NEG, NEED_DIAG, Epi, true><<<nb, 256, 0, s>>>(A->soff, A->bcol, A->bdiag, A->bmode, A->bvi,
+                                                                    nullptr, A->vtab, A->rowptr, A->col, A->val, x,
+                                                                    t0, t1, e);
+   } else {
+      if (xs)
+         bsr3_kernel<NEG, NEED_DIAG, Epi, false, true><<<nb, 256, 0, s>>>(
+            A->soff, A->bcol, A->bdiag, A->bmode, nullptr, A->bval, nullptr, A->rowptr, A->col, A->val, x, t0, t1, e);
+      else
+         bsr3_kernel<NEG, NEED_DIAG, Epi, false><<<nb, 256, 0, s>>>(A->soff, A->bcol, A->bdiag, A->bmode, nullptr,
+                                                                     A->bval, nullptr, A->rowptr, A->col, A->val, x,
+                                                                     t0, t1, e);
+   }
 }
 
 // the block form serves row ranges that start on a slice (21 block rows) and

@@ -26,3 +26,8 @@ done
 run ajac 300 tests/test_gpu_dist.py -k "async_jacobi or sps"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_dist.py -k "async_jacobi_512" -m slow -v -s -rf --timeout 560 \
    --timeout-method thread > $O/ajac512.log 2>&1; echo "ajac512 exit $?"; grep -E "512\^3 async|passed|failed" $O/ajac512.log | tail -10
+run bsr 200 tests/test_gpu_bsr.py tests/test_gpu_classical.py -k "bsr or elasticity_solve"
+for xs in 1 0; do
+  AMG_BSR3_XS=$xs timeout -k 10 300 python -u tools/bench_elasticity.py --refine 5 > $O/elast5_xs$xs.json 2> $O/elast5_xs$xs.err
+  echo "elast r5 xs=$xs exit $?: $(python3 -c "import json,sys; d=json.load(open('$O/elast5_xs$xs.json')); print(d['it_per_s'], d['fine_spmv'])" 2>&1 | tail -1)"
+done
