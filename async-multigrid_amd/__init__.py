@@ -137,7 +137,8 @@ class Context:
 
     def set_jgs_wave(self, enable):
         """Hybrid JGS kernel form, all bit-identical: 1 (default) 8 lanes per block,
-        8 blocks per wave; 2 one wave per block; 0 one lane per block."""
+        8 blocks per wave; 2 one wave per block; 0 one lane per block; 3 an LDS tile of 64
+        blocks (rows staged coalesced, the chains walked one lane per block)."""
         check(lib.amg_set_jgs_wave(self.h, int(enable)))
 
     def set_fuse_prolong(self, enable):

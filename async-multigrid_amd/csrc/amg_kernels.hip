@@ -4740,6 +4740,195 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
    }
 }
 
+// Hybrid Jacobi / Gauss-Seidel, LDS tile form (jgs_wave 3): a workgroup of
+// 256 lanes owns NB consecutive blocks and walks them in passes of CH rows per
+// block (in sweep order).  Phase 1 (all lanes, one lane per row, consecutive
+// lanes on consecutive rows of a block: coalesced CH-row segments) forms each
+// row's prefix -- f_i minus its products up to the first in-pass dependency,
+// in CSR order -- and its tail as (tag, value) slots: a ready product, or the
+// coefficient of an earlier row of this pass; rows of earlier passes are
+// products of the values this workgroup stored (re-read at agent scope after
+// the stores completed).  Phase 2 (one wave, lane q = block q): the CH steps
+// of every block's chain side by side, operands from LDS ([step][block]
+// layout: the lanes' reads are consecutive), each new value into the pass's
+// value row.  Tails past TMAX slots are re-read from memory at the step.  The
+// operations and their order are the reference's sequential loop's
+// (SMEM_Smooth.cpp:265-304 / 548-585): bit-identical.  Any row length.
+template <int NB, int CH, int TMAX, bool VI>
+__global__ __launch_bounds__(256) void hybrid_jgs_tile_k(const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                         const double *__restrict__ val,
+                                                         const unsigned char *__restrict__ vidx,
+                                                         const double *__restrict__ vtab, const double *__restrict__ f,
+                                                         double *u, const double *__restrict__ u_prev,
+                                                         const int *__restrict__ blk, int nblk,
+                                                         const double *__restrict__ ds, double weight, int zero,
+                                                         int reverse)
+{
+   constexpr int NT = 256, SP = NB + 1, NS = CH * SP, RPT = NB * CH / NT;
+   static_assert(NB == 64 && (NB * CH) % NT == 0, "one phase-2 wave, whole rows per lane");
+   __shared__ double sP[NS], sOld[NS], sD[NS], sV[NS];
+   __shared__ double sW[TMAX][NS];
+   __shared__ signed char sT[TMAX][NS];
+   __shared__ int sM[NS]; // bit 0: a_ii != 0, bits 1-15: tail length, bits 16-31: entry past the slots
+   __shared__ int sBlk[NB + 1];
+   const int t = (int)threadIdx.x;
+   const int b0 = (int)blockIdx.x * NB;
+   if (t <= NB) sBlk[t] = blk[min(b0 + t, nblk)];
+   __syncthreads();
+   int nmax = 0; // the longest block's passes (every wave computes it)
+   {
+      const int q = t & 63;
+      nmax = sBlk[q + 1] - sBlk[q];
+      for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
+   }
+   auto ld_u = [u](int k) { return __hip_atomic_load(u + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+   // operand kinds (as hybrid_jgs_grp_k): JG_PLAIN u_prev, JG_PROD a ready
+   // product (0 in the zero sweep), JG_FAR an earlier pass's row (re-read),
+   // >= 0 an earlier row of this pass, JG_NONE skipped
+   auto kind = [&](int j, int i, int ns, int ne, int c0) -> int {
+      if (j >= ns && j < ne) {
+         const bool done = reverse ? j > i : j < i;
+         if (!done) return zero ? JG_PROD : JG_PLAIN;
+         const int pos = reverse ? ne - 1 - j : j - ns;
+         return pos >= c0 ? pos - c0 : JG_FAR;
+      }
+      return zero ? JG_NONE : JG_PLAIN;
+   };
+   int rs_n[RPT], re_n[RPT]; // row pointers one pass ahead
+#pragma unroll
+   for (int it = 0; it < RPT; it++) {
+      const int r = it * NT + t, q = r / CH, sl = r % CH;
+      const int ns = sBlk[q], ne = sBlk[q + 1];
+      rs_n[it] = re_n[it] = 0;
+      if (sl < ne - ns) {
+         const int i = reverse ? ne - 1 - sl : ns + sl;
+         rs_n[it] = rowptr[i];
+         re_n[it] = rowptr[i + 1];
+      }
+   }
+   for (int c0 = 0; c0 < nmax; c0 += CH) {
+      // phase 1
+#pragma unroll
+      for (int it = 0; it < RPT; it++) {
+         const int r = it * NT + t, q = r / CH, sl = r % CH, slot = sl * SP + q;
+         const int ns = sBlk[q], ne = sBlk[q + 1], pos = c0 + sl;
+         const bool act = pos < ne - ns;
+         const int i = act ? (reverse ? ne - 1 - pos : ns + pos) : 0;
+         const int rs = rs_n[it], len = act ? re_n[it] - rs_n[it] : 0;
+         if (pos + CH < ne - ns) {
+            const int in = reverse ? ne - 1 - (pos + CH) : ns + pos + CH;
+            rs_n[it] = rowptr[in];
+            re_n[it] = rowptr[in + 1];
+         }
+         double P = 0.0, old = 0.0, a = 0.0, dd = 1.0;
+         int tl = 0, kov = 0;
+         bool dep = false;
+         if (act) {
+            P = f[i];
+            old = zero ? 0.0 : u_prev[i];
+            if (ds) dd = ds[i];
+         }
+         for (int kb = 0; kb < len; kb += 8) {
+            int jk[8], tk[8];
+            double vk[8], xk[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) { // column / value loads (clamped: always in range)
+               const int e = rs + min(kb + k, len - 1);
+               jk[k] = col[e];
+               vk[k] = VI ? vtab[vidx[e]] : val[e];
+            }
+            if (kb == 0) a = vk[0];
+            bool far = false;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+               tk[k] = kb + k < len ? kind(jk[k], i, ns, ne, c0) : JG_NONE;
+               far = far || tk[k] == JG_FAR;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) { // operand loads (own row when unused)
+               const double xv = u_prev[tk[k] == JG_PLAIN ? jk[k] : i];
+               xk[k] = tk[k] == JG_PLAIN ? xv : 0.0;
+            }
+            if (far) {
+#pragma unroll
+               for (int k = 0; k < 8; k++)
+                  if (tk[k] == JG_FAR) xk[k] = ld_u(jk[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) { // CSR order: prefix, then tail
+               const int tg = tk[k];
+               if (tg == JG_NONE) continue;
+               const bool prod = tg == JG_PLAIN || tg == JG_PROD || tg == JG_FAR;
+               dep = dep || !prod;
+               const double w = prod ? vk[k] * xk[k] : vk[k];
+               if (!dep) {
+                  P = P - w;
+               } else {
+                  if (tl < TMAX) {
+                     sW[tl][slot] = w;
+                     sT[tl][slot] = (signed char)(prod ? JG_PROD : tg);
+                  } else if (tl == TMAX) {
+                     kov = kb + k;
+                  }
+                  tl++;
+               }
+            }
+         }
+         if (!ds) dd = a;
+         sP[slot] = P;
+         sOld[slot] = old;
+         sD[slot] = dd;
+         sM[slot] = (a != 0.0 ? 1 : 0) | (min(tl, 0x7fff) << 1) | (kov << 16);
+      }
+      __syncthreads();
+      // phase 2: lane q walks block q's CH steps
+      if (t < NB) {
+         const int q = t, ns = sBlk[q], ne = sBlk[q + 1];
+         const int cnt = min(CH, ne - ns - c0);
+         for (int s = 0; s < cnt; s++) {
+            const int slot = s * SP + q;
+            const int m = sM[slot], tl = (m >> 1) & 0x7fff;
+            double r = sP[slot];
+            const int tn = min(tl, TMAX);
+            for (int k = 0; k < tn; k++) {
+               const int tg = sT[k][slot];
+               const double w = sW[k][slot];
+               r = r - (tg == JG_PROD ? w : w * sV[max(tg, 0) * SP + q]);
+            }
+            if (tl > TMAX) { // the tail past the slots, again from memory in CSR order
+               const int pos = c0 + s, i = reverse ? ne - 1 - pos : ns + pos;
+               const int rs = rowptr[i], len = rowptr[i + 1] - rs;
+               for (int k = m >> 16; k < len; k++) {
+                  const int j = col[rs + k];
+                  const double vk = VI ? vtab[vidx[rs + k]] : val[rs + k];
+                  const int tg = kind(j, i, ns, ne, c0);
+                  if (tg == JG_NONE) continue;
+                  const double x = tg == JG_PLAIN ? u_prev[j] : tg == JG_FAR ? ld_u(j) : tg == JG_PROD ? 0.0
+                                                                                                       : sV[tg * SP + q];
+                  r = r - vk * x;
+               }
+            }
+            const double old = sOld[slot], d = sD[slot];
+            sV[slot] = (m & 1) ? (zero ? weight * r / d : old + weight * r / d) : old;
+         }
+      }
+      __syncthreads();
+      // write-out (coalesced): a_ii == 0 keeps the row's value (0 after the zero-guess reset)
+#pragma unroll
+      for (int it = 0; it < RPT; it++) {
+         const int r = it * NT + t, q = r / CH, sl = r % CH, slot = sl * SP + q;
+         const int ns = sBlk[q], ne = sBlk[q + 1], pos = c0 + sl;
+         if (pos < ne - ns && ((sM[slot] & 1) || zero))
+            __hip_atomic_store(u + (reverse ? ne - 1 - pos : ns + pos), sV[slot], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (c0 + CH < nmax) {
+         wait_own_stores(); // the next pass's loads of these rows see the stores
+         __syncthreads();
+      }
+   }
+}
+
 __global__ void row_max_k(const int *__restrict__ rowptr, int n, int *__restrict__ out)
 {
    int m = 0;
@@ -4762,6 +4951,17 @@ void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
 {
    if (nblk <= 0) return;
    int mode = A->ctx->jgs_wave;
+   if (mode == 3) {
+      const int nwg = (nblk + 63) / 64;
+      if (A->vidx)
+         hybrid_jgs_tile_k<64, 16, 4, true><<<nwg, 256, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u,
+                                                                u_prev, d_blk, nblk, diag_scale, weight, zero, reverse);
+      else
+         hybrid_jgs_tile_k<64, 16, 4, false><<<nwg, 256, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u,
+                                                                 u_prev, d_blk, nblk, diag_scale, weight, zero,
+                                                                 reverse);
+      return;
+   }
    // small levels (fewer workgroups than CUs) are latency-bound: jgs_small 1
    // runs them one wave per block, 2 with the whole row's loads in one batch
    const int small_form = A->ctx->jgs_small;

@@ -331,7 +331,9 @@ int amg_l1_jacobi(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, 
  * bit-identical: 1 (default) 8 lanes per block, 8 blocks per wave -- each
  * chunk's rows loaded coalesced, the dependency chain advancing eight blocks
  * per wave instruction; 2: one wave per block (the chain carried lane to lane
- * by v_readlane); 0: one lane walks each block (the reference's loop as is) */
+ * by v_readlane); 0: one lane walks each block (the reference's loop as is);
+ * 3: an LDS tile of 64 blocks -- each pass's rows staged coalesced (prefix and
+ * tail slots per row), the chains walked one lane per block from LDS */
 int amg_set_jgs_wave(amg_ctx *ctx, int enable);
 /* form 1's small levels (fewer than 8192 blocks of rows of 9..32 entries; env
  * AMG_JGS_SMALL), all bit-identical: 2 (default) the whole row's loads in one

@@ -401,13 +401,13 @@ def test_l1_jacobi(mats, ctx, oracle, amg, name, zero):
 @pytest.mark.parametrize("name", ["lap16", "A1", "rand_sq", "lap_hole"])
 @pytest.mark.parametrize("T", [1, 4, 8, "perf64", "ragged"])
 @pytest.mark.parametrize("zero", [0, 1])
-@pytest.mark.parametrize("wave", [1, 2, 0, "1s0", "1s1"])
+@pytest.mark.parametrize("wave", [1, 2, 0, 3, "1s0", "1s1"])
 def test_hybrid_jgs(mats, ctx, oracle, amg, name, T, zero, wave):
     """Hybrid Jacobi/GS is partition dependent: the same blocks must give the
     same bits -- the reference's thread ranges (T) and the device partition --
     in every kernel form: 8 lanes per block and 8 blocks per wave (1), one
     wave per block (2; the chain carried lane to lane, blocks spanning many
-    64-row chunks), one lane per block (0)."""
+    64-row chunks), one lane per block (0), the LDS tile of 64 blocks (3)."""
     host, dev = mats
     small = 2
     if isinstance(wave, str):  # form 1 with the small levels' form 0 / 1
