@@ -1601,13 +1601,18 @@ extern "C" int amg_l1_jacobi(amg_ctx *c, const amg_mat *A, const amg_vec *f, amg
 int amg_hybrid_jgs_dev(amg_ctx *c, hipStream_t s, const amg_mat *A, const double *f, double *u,
                        double *u_prev, int n_vec, const int *d_blk, int nblk, int blk_lo,
                        int blk_hi, const double *ds, double weight, int sweeps, int zero_first,
-                       int reverse)
+                       int reverse, double *apply_u = nullptr, double *apply_priv = nullptr,
+                       bool *applied = nullptr)
 {
+   bool ap = false;
    for (int k = 0; k < sweeps; k++) {
       const int zero = (k == 0 && zero_first == 1);
       if (!zero) amgk::vcopy(s, u, u_prev, blk_lo, blk_hi);
-      amgk::hybrid_jgs(s, A, f, u, u_prev, d_blk, nblk, ds, weight, zero, reverse);
+      const bool last = k == sweeps - 1;
+      ap = amgk::hybrid_jgs(s, A, f, u, u_prev, d_blk, nblk, ds, weight, zero, reverse, last ? apply_u : nullptr,
+                            last ? apply_priv : nullptr);
    }
+   if (applied) *applied = ap;
    (void)n_vec;
    (void)c;
    AMG_HIP(hipGetLastError());

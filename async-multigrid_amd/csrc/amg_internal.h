@@ -352,10 +352,13 @@ void jacobi_zero(hipStream_t s, const double *diag, const double *f, const doubl
 // u_new = u + (omega*r)/a (a != 0): Jacobi sweep from a precomputed residual
 void jacobi_from_residual(hipStream_t s, const double *diag, const double *r, const double *l1,
                           double omega, double *u, int rb, int re);
-// hybrid JGS: one wave (rows <= 32 entries) or one lane per block, blocks d_blk[0..nblk] (device), in place on u
-void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
+// hybrid JGS: one wave (rows <= 32 entries) or one lane per block, blocks d_blk[0..nblk] (device), in place on u.
+// apply_u (the LDS tile form only): the FULL_ASYNC correction of the sweep's result folded into its
+// write-out -- apply_u += u by device-scope atomics, apply_priv = the value after it (atomic_correct);
+// returns whether it was applied
+bool hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
                 const int *d_blk, int nblk, const double *diag_scale, double weight, int zero,
-                int reverse);
+                int reverse, double *apply_u = nullptr, double *apply_priv = nullptr);
 // *d_out = max(*d_out, longest row of A)
 void row_max(hipStream_t s, const amg_mat *A, int *d_out);
 // asynchronous / semi-asynchronous Gauss-Seidel, one lane per block, live u

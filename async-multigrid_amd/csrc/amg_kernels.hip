@@ -4762,7 +4762,7 @@ __global__ __launch_bounds__(256) void hybrid_jgs_tile_k(const int *__restrict__
                                                          double *u, const double *__restrict__ u_prev,
                                                          const int *__restrict__ blk, int nblk,
                                                          const double *__restrict__ ds, double weight, int zero,
-                                                         int reverse)
+                                                         int reverse, double *apply_u, double *__restrict__ apply_priv)
 {
    constexpr int NT = 256, SP = NB + 1, NS = CH * SP, RPT = NB * CH / NT;
    static_assert(NB == 64 && (NB * CH) % NT == 0, "one phase-2 wave, whole rows per lane");
@@ -4913,14 +4913,21 @@ __global__ __launch_bounds__(256) void hybrid_jgs_tile_k(const int *__restrict__
          }
       }
       __syncthreads();
-      // write-out (coalesced): a_ii == 0 keeps the row's value (0 after the zero-guess reset)
+      // write-out (coalesced): a_ii == 0 keeps the row's value (0 after the zero-guess reset);
+      // apply_u: the correction u_shared += v (atomic_correct_k's operations)
 #pragma unroll
       for (int it = 0; it < RPT; it++) {
          const int r = it * NT + t, q = r / CH, sl = r % CH, slot = sl * SP + q;
          const int ns = sBlk[q], ne = sBlk[q + 1], pos = c0 + sl;
-         if (pos < ne - ns && ((sM[slot] & 1) || zero))
-            __hip_atomic_store(u + (reverse ? ne - 1 - pos : ns + pos), sV[slot], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+         if (pos < ne - ns) {
+            const int i = reverse ? ne - 1 - pos : ns + pos;
+            const double v = sV[slot];
+            if ((sM[slot] & 1) || zero) __hip_atomic_store(u + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (apply_u) {
+               const double o = atomicAdd(apply_u + i, v);
+               apply_priv[i] = o + v;
+            }
+         }
       }
       if (c0 + CH < nmax) {
          wait_own_stores(); // the next pass's loads of these rows see the stores
@@ -4945,22 +4952,30 @@ void row_max(hipStream_t s, const amg_mat *A, int *d_out)
    row_max_k<<<std::max(1, std::min(1024, (n + 255) / 256)), 256, 0, s>>>(A->rowptr, n, d_out);
 }
 
-void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
+bool hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
                 const int *d_blk, int nblk, const double *diag_scale, double weight, int zero,
-                int reverse)
+                int reverse, double *apply_u, double *apply_priv)
 {
-   if (nblk <= 0) return;
+   if (nblk <= 0) return false;
    int mode = A->ctx->jgs_wave;
    if (mode == 3) {
+      // short rows: passes of 16 rows per block, 4 tail slots; longer rows
+      // (27-pt, classical): passes of 4 rows, 16 slots
       const int nwg = (nblk + 63) / 64;
-      if (A->vidx)
-         hybrid_jgs_tile_k<64, 16, 4, true><<<nwg, 256, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u,
-                                                                u_prev, d_blk, nblk, diag_scale, weight, zero, reverse);
-      else
-         hybrid_jgs_tile_k<64, 16, 4, false><<<nwg, 256, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u,
-                                                                 u_prev, d_blk, nblk, diag_scale, weight, zero,
-                                                                 reverse);
-      return;
+#define JGS_TILE(CH, TM, V)                                                                                          \
+   hybrid_jgs_tile_k<64, CH, TM, V><<<nwg, 256, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u, u_prev, \
+                                                        d_blk, nblk, diag_scale, weight, zero, reverse, apply_u,  \
+                                                        apply_priv)
+      const bool vi = A->vidx != nullptr;
+      if (A->maxrow >= 0 && A->maxrow <= 8) {
+         if (vi) JGS_TILE(16, 4, true);
+         else JGS_TILE(16, 4, false);
+      } else {
+         if (vi) JGS_TILE(4, 16, true);
+         else JGS_TILE(4, 16, false);
+      }
+#undef JGS_TILE
+      return apply_u != nullptr;
    }
    // small levels (fewer workgroups than CUs) are latency-bound: jgs_small 1
    // runs them one wave per block, 2 with the whole row's loads in one batch
@@ -4976,7 +4991,7 @@ void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
          hybrid_jgs_grp_k<8, 32, false, true><<<nwg, 64, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u,
                                                                   u_prev, d_blk, nblk, diag_scale, weight, zero,
                                                                   reverse);
-      return;
+      return false;
    }
    if (mode == 1 && A->maxrow >= 1 && A->maxrow <= 32) {
       // 8 lanes per block, 8 blocks per wave
@@ -4993,7 +5008,7 @@ void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
          else JGS_GRP(32, false);
       }
 #undef JGS_GRP
-      return;
+      return false;
    }
    if (mode == 2 && A->maxrow >= 0 && A->maxrow <= 32) {
       const int nwg = (nblk + 3) / 4;
@@ -5003,12 +5018,13 @@ void hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
       else
          hybrid_jgs_wave_k<32><<<nwg, 256, 0, s>>>(A->rowptr, A->col, A->val, f, u, u_prev, d_blk, nblk,
                                                    diag_scale, weight, zero, reverse);
-      return;
+      return false;
    }
    const int tpb = 64;
    hybrid_jgs_k<<<(nblk + tpb - 1) / tpb, tpb, 0, s>>>(A->rowptr, A->col, A->val, f, u, u_prev,
                                                        d_blk, nblk, diag_scale, weight, zero,
                                                        reverse);
+   return false;
 }
 
 // y = A^T x in SMEM_Sync_Parfor_MatVecT order (SMEM_MatVec.cpp:42-57): for each

@@ -17,7 +17,8 @@ int amg_reduce_to_host(amg_ctx *c, const double *partials, int np, int do_sqrt, 
 int amg_hybrid_jgs_dev(amg_ctx *c, hipStream_t s, const amg_mat *A, const double *f, double *u,
                        double *u_prev, int n_vec, const int *d_blk, int nblk, int blk_lo,
                        int blk_hi, const double *ds, double weight, int sweeps, int zero_first,
-                       int reverse);
+                       int reverse, double *apply_u = nullptr, double *apply_priv = nullptr,
+                       bool *applied = nullptr);
 int amg_sym_jacobi_dev(hipStream_t s, const amg_mat *A, const double *f, double *u, double *y,
                        double *r, double omega, const double *l1, int sweeps, int zero_first,
                        int rb, int re, int variant);
@@ -108,6 +109,9 @@ struct amg_hier {
    std::vector<std::vector<double>> async_t;
    // per-correction end times of the last free race (amg_async_correction_ms)
    AmgCorrTimes corr;
+   // the correction whose update-window start a fused update kernel records
+   // (mark_update_start; -1: none)
+   int mark_k = -1, mark_j = 0;
    // per level of the last amg_async_solve: ms from its start to the level's
    // last correction (amg_async_level_ms)
    std::vector<double> level_ms;
@@ -619,18 +623,40 @@ static void smooth_one_level(amg_hier *H, hipStream_t s, int l, const double *f,
    }
 }
 
+// the free race's update-window start of the correction in H->mark_k, right
+// before the kernel that adds it into the shared iterate
+static void mark_update_start(amg_hier *H, hipStream_t s)
+{
+   if (H->mark_k < 0) return;
+   H->corr.record_start(H->mark_k, H->mark_j, s);
+   H->mark_k = -1;
+}
+
 // ALL_LEVELS smoothing of A[Alevel] with f -> u (row range version of the
-// smoothers), zero flag of `flag_level`
-static void smooth_all_levels(amg_hier *H, hipStream_t s, int Alevel, const double *f, double *u,
-                              double *u_prev, double *y, double *r, int sweeps, int flag_level)
+// smoothers), zero flag of `flag_level`.  apply_u (hybrid JGS, the LDS tile
+// form): the FULL_ASYNC correction apply_u += u, apply_priv = the value after
+// it, folded into the last sweep; returns whether it was
+static bool smooth_all_levels(amg_hier *H, hipStream_t s, int Alevel, const double *f, double *u,
+                              double *u_prev, double *y, double *r, int sweeps, int flag_level,
+                              double *apply_u = nullptr, double *apply_priv = nullptr)
 {
    Level &v = H->lv[Alevel];
    const amg_opts &o = H->o;
    const int zf = H->lv[flag_level].zero_flag;
    const bool sym = is_multadd(o) && o.num_post_smooth_sweeps > 0 && o.num_pre_smooth_sweeps > 0;
    if (o.smoother == AMG_HYBRID_JACOBI_GAUSS_SEIDEL) {
-      amg_hybrid_jgs_dev(H->ctx, s, v.A, f, u, u_prev, v.n, v.d_blk, (int)v.blk.size() - 1, 0, v.n,
-                         nullptr, 1.0, sweeps, zf, 0);
+      const int nb = (int)v.blk.size() - 1;
+      if (!apply_u || sweeps <= 0) {
+         amg_hybrid_jgs_dev(H->ctx, s, v.A, f, u, u_prev, v.n, v.d_blk, nb, 0, v.n, nullptr, 1.0, sweeps, zf, 0);
+         return false;
+      }
+      if (sweeps > 1)
+         amg_hybrid_jgs_dev(H->ctx, s, v.A, f, u, u_prev, v.n, v.d_blk, nb, 0, v.n, nullptr, 1.0, sweeps - 1, zf, 0);
+      mark_update_start(H, s);
+      bool applied = false;
+      amg_hybrid_jgs_dev(H->ctx, s, v.A, f, u, u_prev, v.n, v.d_blk, nb, 0, v.n, nullptr, 1.0, 1,
+                         sweeps > 1 ? 0 : zf, 0, apply_u, apply_priv, &applied);
+      return applied;
    } else if (o.smoother == AMG_ASYNC_GAUSS_SEIDEL || o.smoother == AMG_SEMI_ASYNC_GAUSS_SEIDEL) {
       // SMEM_Async_GaussSeidel / SMEM_SemiAsync_GaussSeidel (SMEM_Solve.cpp:281-286)
       amgk::async_gs(s, v.A, f, u, v.d_blk, (int)v.blk.size() - 1, sweeps,
@@ -662,6 +688,7 @@ static void smooth_all_levels(amg_hier *H, hipStream_t s, int Alevel, const doub
          }
       }
    }
+   return false;
 }
 
 // ---- SMEM_Sync_Parfor_Vcycle (SMEM_Sync_AMG.cpp:8-145) -------------------------
@@ -842,6 +869,7 @@ static bool xfer_prolong(amg_hier *H, hipStream_t s, int l, const double *ec, do
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    const Level &v = H->lv[l];
    if (composed_p(H) && H->xfp[l]) {
+      if (apply) mark_update_start(H, s);
       if (apply)
          amgk::mz_xfer_prolong(s, v.A, ec, H->gl[l], H->d_geo_w[l], H->o.smooth_weight, apply, u, u_priv);
       else
@@ -890,7 +918,12 @@ static bool add_level_correction(amg_hier *H, hipStream_t s, int k, const double
       // reference's cycle: the coarsest correction e[k] keeps its zero value
    } else if (multadd) {
       amgk::vset(s, a.e[k], 0.0, 0, H->lv[k].n);
-      smooth_all_levels(H, s, k, rl(k), a.e[k], a.u_prev, a.y, a.scratch, o.num_fine_smooth_sweeps, k);
+      // level 0's correction is its own smoothing: the FULL_ASYNC update
+      // folded into the last sweep where the smoother's kernel allows it
+      const bool ap = k == 0 && apply == 1;
+      if (smooth_all_levels(H, s, k, rl(k), a.e[k], a.u_prev, a.y, a.scratch, o.num_fine_smooth_sweeps, k,
+                            ap ? u : nullptr, ap ? u_priv : nullptr))
+         return true;
    } else {
       const int fg = k, cg = k + 1;
       amgk::vset(s, a.u_fine, 0.0, 0, H->lv[fg].n);
@@ -1494,8 +1527,14 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          if (!semi) amgk::atomic_add(s, v0.u, a.g_u, grb, gre);
       }
       // FULL_ASYNC / READ_SOL: the atomic correction fused into the level-0
-      // prolongation where the transfers allow it
+      // prolongation (or level 0's last smoothing sweep) where the kernels
+      // allow it; that kernel records the update-window start
+      if (rec && !read_res && !semi) {
+         H->mark_k = k;
+         H->mark_j = issued[k];
+      }
       const bool fused = add_level_correction(H, s, k, a.y_fine, (!read_res && !semi) ? 1 : 0, v0.u, a.u_priv);
+      H->mark_k = -1;
       if (read_res) {
          amgk::spgemv(s, v0.A, a.e[0], nullptr, mv, a.y, 0, n0, nullptr);
          if (semi) {
