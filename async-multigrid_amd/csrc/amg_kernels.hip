@@ -4827,6 +4827,9 @@ __global__ __launch_bounds__(256) void hybrid_jgs_tile_k(const int *__restrict__
             P = f[i];
             old = zero ? 0.0 : u_prev[i];
             if (ds) dd = ds[i];
+            // a_ii = val[rowptr[i]] as the reference reads it: an empty row's is the
+            // next row's first value (as hybrid_jgs_grp_k's clamped first load)
+            if (len == 0) a = VI ? vtab[vidx[rs]] : val[rs];
          }
          for (int kb = 0; kb < len; kb += 8) {
             int jk[8], tk[8];

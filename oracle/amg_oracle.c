@@ -1163,6 +1163,8 @@ void or_set_async_schedule(int s) { g_async_schedule = s; }
 static double g_async_dur[OR_MAX_LEVELS];
 static double *g_async_t[OR_MAX_LEVELS]; /* or_set_async_times: end time of every correction */
 static int g_async_tn[OR_MAX_LEVELS];
+static int g_async_exact = 0; /* or_set_async_exact: a replay runs exactly the table's corrections */
+void or_set_async_exact(int on) { g_async_exact = on; }
 void or_set_async_durations(const double *d, int n)
 {
    for (int k = 0; k < OR_MAX_LEVELS; k++) {
@@ -1603,7 +1605,13 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
          }
          if (async_type == OR_SEMI_ASYNC && tid == root[k]) omp_unset_lock(&lock);
          if (tid == root[k]) __atomic_add_fetch(&count[k], 1, __ATOMIC_ACQ_REL);
-         if (converge_type == OR_CONVERGE_LOCAL) {
+         if (timed && g_async_exact && g_async_tn[k] > 0) {
+            /* a replay (or_set_async_times + or_set_async_exact) runs exactly the
+             * recorded corrections: under converge GLOBAL the race's stopping
+             * point is in the table */
+            gbar_wait(b, NULL);
+            if (__atomic_load_n(&count[k], __ATOMIC_ACQUIRE) >= g_async_tn[k]) tid_converge = 1;
+         } else if (converge_type == OR_CONVERGE_LOCAL) {
             gbar_wait(b, NULL);
             if (__atomic_load_n(&count[k], __ATOMIC_ACQUIRE) == o->num_cycles) tid_converge = 1;
          } else {

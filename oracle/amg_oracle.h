@@ -226,6 +226,10 @@ void or_set_async_durations(const double *d, int n);
  * k's j-th correction ends at t[sum(n[0..k-1]) + j]; past n[k] entries its
  * last interval repeats */
 void or_set_async_times(const double *t, const int *n, int L);
+/* schedule 4 with tables: 1 = every group runs exactly its table's corrections
+ * (the replay of a recorded race, whatever converge_test_type), 0 = the
+ * converge rule decides (default) */
+void or_set_async_exact(int on);
 /* replay of a distributed free race (FULL_ASYNC, READ_SOL, LOCAL residuals and
  * convergence): rank r owns fine rows [rs[r], rs[r+1]); level k's correction j
  * updates slice r at t[off_k + j R + r] (off_k = R (nc[0] + .. + nc[k-1]));

@@ -353,13 +353,16 @@ def set_async_durations(d):
     """or_set_async_durations: per-level correction times of schedule 4 (timed)"""
     d = np.ascontiguousarray(d, dtype=np.float64)
     lib().or_set_async_durations(dptr(d), int(d.size))
+    lib().or_set_async_exact(0)
 
 
-def set_async_times(times):
-    """or_set_async_times: times[k] = end times of level k's corrections (schedule 4 replay)"""
+def set_async_times(times, exact=False):
+    """or_set_async_times: times[k] = end times of level k's corrections (schedule 4 replay);
+    exact: every level runs exactly len(times[k]) corrections (or_set_async_exact)"""
     n = np.array([len(t) for t in times], dtype=np.int32)
     flat = np.ascontiguousarray(np.concatenate([np.asarray(t, dtype=np.float64) for t in times] + [np.zeros(1)]))
     lib().or_set_async_times(dptr(flat), iptr(n), int(n.size))
+    lib().or_set_async_exact(1 if exact else 0)
 
 
 def make_opts(solver=OR_MULT, smoother=OR_JACOBI, num_pre=1, num_post=1, num_fine=1,

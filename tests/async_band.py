@@ -103,6 +103,15 @@ def blocks64(host):
     return out
 
 
+def _per_rank(x):
+    """per-rank lists of per-level time arrays: one hierarchy's tables (a list
+    of per-level arrays) or a list of them, one per rank"""
+    for lev in x:
+        if len(lev):
+            return list(x) if hasattr(lev[0], "__len__") else [x]
+    return [x]
+
+
 def in_band(rel, lo, hi):
     return 0.5 * lo <= rel <= 2.0 * hi
 
@@ -129,7 +138,7 @@ def times_of(corr_ms, L, ranks=None):
     per rank -- a distributed correction ends on its slowest rank); the
     reference's idle coarsest group (no device group under LOCAL residuals)
     takes the coarsest correcting level's times"""
-    per = corr_ms if isinstance(corr_ms[0], (list, tuple)) else [corr_ms]
+    per = _per_rank(corr_ms)
     out = []
     for k in range(L):
         rows = [np.asarray(r[k], dtype=np.float64) for r in per]
@@ -148,33 +157,75 @@ def replay_tables(corr_ms, L):
     slowest rank (times_of over every rank) and, with several ranks, each
     rank's own order -- every rank's rows receive the corrections in that
     rank's order, so a distributed race lies between these replays"""
-    per = corr_ms if isinstance(corr_ms[0], (list, tuple)) else [corr_ms]
+    per = _per_rank(corr_ms)
     out = [times_of(per, L)]
     if len(per) > 1:
         out += [times_of([r], L) for r in per]
     return out
 
 
-def sliced_replay(amg, oracle, host, f, opts, corr_ms, rs, composed=False):
-    """the oracle's replay of a DISTRIBUTED free race (or_async_add_replay):
-    rank r's slice [rs[r], rs[r+1]) of the fine rows receives every level's
-    corrections at that rank's recorded update times"""
+def _replay_slices(amg, oracle, host, f, opts, rs, per_slice, composed=False, blocks=None):
+    """or_async_add_replay: slice s = [rs[s], rs[s+1]) of the fine rows receives
+    every level's corrections at the times per_slice[s][k] (a correction's
+    update is formed once, at its first slice's time)"""
     L = len(host["A"])
-    R = len(rs) - 1
+    S = len(rs) - 1
     OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
     if composed:
         OH.set_composed_transfers()
+    if blocks is not None:
+        for lev, blk in blocks.items():
+            OH.set_blocks(lev, blk)
     accel = None
     if opts.accel_type != amg.AMG_NO_ACCEL:
         accel = (opts.accel_type, min(opts.cheby_grid, L - 2), opts.cheby_mu, opts.cheby_delta)
     times = []
     for k in range(L):
-        n = min(len(corr_ms[r][k]) for r in range(R))
-        times.append(np.stack([np.asarray(corr_ms[r][k][:n], dtype=np.float64) for r in range(R)], axis=1)
-                     if n else np.zeros((0, R)))
+        n = min(len(per_slice[q][k]) for q in range(S))
+        times.append(np.stack([np.asarray(per_slice[q][k][:n], dtype=np.float64) for q in range(S)], axis=1)
+                     if n else np.zeros((0, S)))
     u, rel, _ = OH.async_add_replay(f, rs, times, accel=accel)
     assert np.all(np.isfinite(u))
     return rel
+
+
+def sliced_replay(amg, oracle, host, f, opts, corr_ms, rs, composed=False, blocks=None):
+    """the oracle's replay of a DISTRIBUTED free race (or_async_add_replay):
+    rank r's slice [rs[r], rs[r+1]) of the fine rows receives every level's
+    corrections at that rank's recorded update times"""
+    return _replay_slices(amg, oracle, host, f, opts, rs, corr_ms, composed=composed, blocks=blocks)
+
+
+def torn_replay(amg, oracle, host, f, opts, ends, starts, rs=None, slices=16, composed=False, blocks=None):
+    """the row-time model of a torn race: a correction's update pass, recorded
+    as the window [start, end] on its rank, reaches the rank's rows in order --
+    row position x in [0, 1) of the rank's rows at start + (end - start) x --
+    so inside overlapping windows the levels' updates interleave by rows.  The
+    rank's rows are cut into `slices` pieces, each receiving every correction
+    at its interpolated time (or_async_add_replay)"""
+    per_e = _per_rank(ends)
+    per_s = _per_rank(starts)
+    L = len(host["A"])
+    n0 = host["A"][0].nrows
+    rs = list(rs) if rs is not None else [0, n0]
+    cuts, tabs = [0], []
+    for r in range(len(per_e)):
+        a, b = rs[r], rs[r + 1]
+        for q in range(slices):
+            lo_, hi_ = a + (b - a) * q // slices, a + (b - a) * (q + 1) // slices
+            if hi_ <= lo_:
+                continue
+            x = (q + 0.5) / slices
+            tab = []
+            for k in range(L):
+                e = np.asarray(per_e[r][k], dtype=np.float64)
+                st = np.asarray(per_s[r][k], dtype=np.float64) if k < len(per_s[r]) else e
+                n = len(e)
+                st = st[:n] if len(st) >= n else np.concatenate([st, e[len(st):]])
+                tab.append(st + (e - st) * x)
+            tabs.append(tab)
+            cuts.append(hi_)
+    return _replay_slices(amg, oracle, host, f, opts, cuts, tabs, composed=composed, blocks=blocks)
 
 
 def torn_updates(ends, starts):
@@ -185,8 +236,8 @@ def torn_updates(ends, starts):
     rows only: a torn update, which the FULL_ASYNC race allows (the
     reference's omp atomic loops of two groups can interleave the same way)
     and no order of whole corrections reproduces."""
-    per_e = ends if isinstance(ends[0], (list, tuple)) else [ends]
-    per_s = starts if isinstance(starts[0], (list, tuple)) else [starts]
+    per_e = _per_rank(ends)
+    per_s = _per_rank(starts)
     torn = 0
     for e_r, s_r in zip(per_e, per_s):
         win = []
@@ -203,35 +254,82 @@ def torn_updates(ends, starts):
     return torn
 
 
-def replay_check(amg, oracle, host, f, opts, runs, blocks=None, composed=False, what="", min_clean=1):
+def replay_check(amg, oracle, host, f, opts, runs, blocks=None, composed=False, what=""):
     """Every free run (rel, ends[, rs[, starts]]) against the oracle's replay of
-    its own recorded update order; with `starts`, a run whose update windows of
-    different levels overlapped (torn_updates > 0) is reported, checked only
-    for a finite relres below 1, and at least `min_clean` runs must be untorn.
-    Untorn runs must lie in [0.5 lo, 2 hi] of their replay(s)."""
+    its own recorded update order: whole corrections in the order of their
+    update points (rows of rank r in rank r's order).  A run whose update
+    windows of different levels overlapped (torn_updates > 0) is also replayed
+    under the row-time model (torn_replay), and its band spans both replays.
+    Every run must lie in [0.5 lo, 2 hi] of its replays."""
     L = len(host["A"])
     widest = 1.0
-    clean = 0
     for i, run in enumerate(runs):
         rel, corr_ms = run[0], run[1]
         rs = run[2] if len(run) > 2 else None
-        torn = torn_updates(corr_ms, run[3]) if len(run) > 3 and run[3] is not None else 0
+        starts = run[3] if len(run) > 3 else None
+        torn = torn_updates(corr_ms, starts) if starts is not None else 0
         if rs is not None and len(rs) > 2:
-            lo = hi = sliced_replay(amg, oracle, host, f, opts, corr_ms, rs, composed=composed)
+            lo = hi = sliced_replay(amg, oracle, host, f, opts, corr_ms, rs, composed=composed, blocks=blocks)
             rr = [lo]
         else:
             lo, hi, rr = timed_band(amg, oracle, host, f, opts, replay_tables(corr_ms, L), blocks=blocks,
                                     composed=composed)
+        tm = None
+        if torn:
+            tm = torn_replay(amg, oracle, host, f, opts, corr_ms, starts, rs=rs, composed=composed, blocks=blocks)
+            lo, hi = min(lo, tm), max(hi, tm)
+            rr = list(rr) + [tm]
         widest = max(widest, hi / lo)
         print(f"  {what} run {i}: device {rel:.4e}, replay [{lo:.4e}, {hi:.4e}] ({len(rr)} order(s), width "
-              f"{hi / lo:.2f}x), device / replay {rel / lo:.2f}-{rel / hi:.2f}, torn updates {torn}")
+              f"{hi / lo:.2f}x), device / replay {rel / lo:.2f}-{rel / hi:.2f}, torn updates {torn}"
+              + (f", row-time model {tm:.4e}" if tm is not None else ""))
+        _dump(what, i, host, f, opts, run, composed, blocks)
         assert np.isfinite(rel), (what, i, rel)
-        if torn:
-            continue
-        clean += 1
         assert in_band(rel, lo, hi), (what, i, rel, lo, hi)
-    assert clean >= min(min_clean, len(runs)), (what, "every run had torn updates", clean)
     return widest
+
+
+def _dump(what, i, host, f, opts, run, composed, blocks):
+    """AMG_REPLAY_DUMP=dir: the run's recorded tables (JSON) and, once per
+    case, the hierarchy and right-hand side (npz) -- for studying the replay
+    models off the GPU"""
+    import json
+    import os
+    d = os.environ.get("AMG_REPLAY_DUMP")
+    if not d:
+        return
+    os.makedirs(d, exist_ok=True)
+    tag = "".join(c if c.isalnum() else "_" for c in what)
+    arr = os.path.join(d, f"{tag}.npz")
+    if not os.path.exists(arr):
+        mats = {}
+        for key in ("A", "P", "R"):
+            for lev, M in enumerate(host[key]):
+                mats[f"{key}{lev}_shape"] = np.array([M.nrows, M.ncols])
+                mats[f"{key}{lev}_rowptr"] = np.asarray(M.rowptr)
+                mats[f"{key}{lev}_col"] = np.asarray(M.col)
+                mats[f"{key}{lev}_val"] = np.asarray(M.val)
+        import ctypes
+        mats["opts"] = np.frombuffer(ctypes.string_at(ctypes.addressof(opts), ctypes.sizeof(opts)), dtype=np.uint8)
+        mats["f"] = np.asarray(f)
+        if blocks is not None:
+            for lev, blk in blocks.items():
+                mats[f"blk{lev}"] = np.asarray(blk)
+        np.savez_compressed(arr, **mats)
+    def lst(x):
+        if x is None:
+            return None
+        if hasattr(x, "tolist"):
+            return x.tolist()
+        if isinstance(x, (list, tuple)):
+            return [lst(v) for v in x]
+        return float(x)
+
+    rec = {"what": what, "run": i, "rel": float(run[0]), "composed": bool(composed),
+           "ends": lst(run[1]), "rs": None if len(run) < 3 or run[2] is None else [int(x) for x in run[2]],
+           "starts": lst(run[3]) if len(run) > 3 else None}
+    with open(os.path.join(d, f"{tag}_run{i}.json"), "w") as fh:
+        json.dump(rec, fh)
 
 
 def timed_band(amg, oracle, host, f, opts, durations, blocks=None, composed=False, nt=None):
@@ -259,7 +357,7 @@ def timed_band(amg, oracle, host, f, opts, durations, blocks=None, composed=Fals
     rels = []
     for d in durations:
         if isinstance(d, list):  # recorded end times per level (times_of): the replay
-            oracle.set_async_times(d)
+            oracle.set_async_times(d, exact=True)
         else:  # per-level correction times (durations_of)
             oracle.set_async_durations(d)
         oracle.lib().or_set_async_schedule(4)

@@ -94,7 +94,7 @@ def test_async_options_band(amg, oracle, ctx, setup, case):
         u, rel, cnt = H.async_solve(f)
         assert np.all(np.isfinite(u))
         rels.append(rel)
-        durs.append((rel, H.async_correction_ms()))
+        durs.append((rel, H.async_correction_ms(), None, H.async_correction_ms(start=True)))
         # correcting levels: [k_lo, k_hi); GLOBAL residuals replace level 0's
         # group by the sliced fine smoothing (SMEM_Setup.cpp:609-615)
         # (and the coarsest level's group runs: it smooths its slice)

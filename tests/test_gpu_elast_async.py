@@ -194,7 +194,7 @@ def test_elast_async_free_race_replay(amg, oracle, ctx, elast):
     for _ in range(2):
         u, rel, cnt = H.async_solve(f)
         assert np.all(np.isfinite(u)) and list(cnt[:L - 1]) == [N] * (L - 1)
-        runs.append((rel, H.async_correction_ms()))
+        runs.append((rel, H.async_correction_ms(), None, H.async_correction_ms(start=True)))
     H.free()
     replay_check(amg, oracle, smoothed, f, opts, runs, what="elasticity one GPU")
     druns = dist_async(amg, smoothed, f, opts, (0.5,), L, runs=3)

@@ -264,7 +264,7 @@ def test_async_multadd_band(amg, oracle, ctx):
     for _ in range(3):
         u, rel, cnt = H.async_solve(f)
         rels.append(rel)
-        durs.append((rel, H.async_correction_ms()))
+        durs.append((rel, H.async_correction_ms(), None, H.async_correction_ms(start=True)))
         assert np.all(np.isfinite(u))
     H.free()
     # the oracle's model of each run (the replay of its recorded update order,

@@ -405,6 +405,41 @@ def test_async_add_replay(amg, oracle):
     assert rel3 < 0.1, rel3
 
 
+def test_torn_replay_model(amg, oracle):
+    """async_band.torn_replay (the row-time model of overlapping update windows):
+    zero-length windows give the plain replay of the end order, bit for bit;
+    windows of two levels that overlap interleave their updates by rows (a
+    different iterate, still converging).  Under converge GLOBAL a replay runs
+    exactly the recorded corrections per level (the race's stopping point)."""
+    from async_band import torn_replay
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, 16, amg.AMG_INTERP_LINEAR)
+    N = 6
+    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=N, tol=0.0)
+    f = amg.rhs_rand(0, 16 ** 3)
+    n0 = 16 ** 3
+    d = np.array([3.0 / (1.9 ** k) + 0.05 for k in range(L)])
+    ends = [list(d[k] * np.arange(1, N + 1)) for k in range(L - 1)] + [[]]
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle.make_opts(
+        solver=oracle.OR_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=N, tol=0.0))
+    _, rel1, _ = OH.async_add_replay(f, [0, n0], [np.asarray(t)[:, None] for t in ends])
+    rel0 = torn_replay(amg, oracle, host, f, opts, ends, ends, slices=8)
+    assert rel0 == rel1
+    # level 0's windows span the previous half interval: they overlap level 1's
+    starts = [list(np.asarray(e) - (0.5 * d[0] if k == 0 else 0.0)) for k, e in enumerate(ends)]
+    relt = torn_replay(amg, oracle, host, f, opts, ends, starts, slices=8)
+    assert relt != rel1 and relt < 0.5, (relt, rel1)
+    # converge GLOBAL replay: exactly the table's counts
+    cnt = [N + 3] + [N] * (L - 2) + [N]
+    oracle.set_async_times([d[k] * np.arange(1, cnt[k] + 1) for k in range(L)], exact=True)
+    oracle.lib().or_set_async_schedule(4)
+    try:
+        _, _, c = OH.async_add(f, [1] * L, converge_type=oracle.OR_CONVERGE_GLOBAL)
+    finally:
+        oracle.lib().or_set_async_schedule(0)
+    assert list(c[:L - 1]) == cnt[:L - 1], c
+
+
 def test_composed_transfers_match_explicit(amg, oracle):
     """or_hier_set_composed_transfers: the smoothed transfers applied composed
     from the plain P / R (R~ r = R (r - w A D^-1 r), P~ e = P e - w D^-1 A P e)
