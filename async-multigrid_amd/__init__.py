@@ -353,6 +353,12 @@ class Hier:
         async_solve (start=True: the windows' start times, where recorded)"""
         return _corr_ms(lib.amg_async_correction_ms, self.h, self.L, start)
 
+    def async_update_windows(self):
+        """per level: (starts, ends) in ms of the device wall clock of its corrections' update
+        kernels in the last free-race async_solve (their actual execution windows)"""
+        return (_corr_ms(lib.amg_async_update_windows, self.h, self.L, True),
+                _corr_ms(lib.amg_async_update_windows, self.h, self.L, False))
+
     def eigs_power(self, iters):
         emax, emin = C.c_double(), C.c_double()
         check(lib.amg_eigs_power(self.h, iters, C.byref(emax), C.byref(emin)))

@@ -1602,7 +1602,7 @@ int amg_hybrid_jgs_dev(amg_ctx *c, hipStream_t s, const amg_mat *A, const double
                        double *u_prev, int n_vec, const int *d_blk, int nblk, int blk_lo,
                        int blk_hi, const double *ds, double weight, int sweeps, int zero_first,
                        int reverse, double *apply_u = nullptr, double *apply_priv = nullptr,
-                       bool *applied = nullptr)
+                       bool *applied = nullptr, unsigned long long *stamp = nullptr)
 {
    bool ap = false;
    for (int k = 0; k < sweeps; k++) {
@@ -1610,7 +1610,7 @@ int amg_hybrid_jgs_dev(amg_ctx *c, hipStream_t s, const amg_mat *A, const double
       if (!zero) amgk::vcopy(s, u, u_prev, blk_lo, blk_hi);
       const bool last = k == sweeps - 1;
       ap = amgk::hybrid_jgs(s, A, f, u, u_prev, d_blk, nblk, ds, weight, zero, reverse, last ? apply_u : nullptr,
-                            last ? apply_priv : nullptr);
+                            last ? apply_priv : nullptr, last ? stamp : nullptr);
    }
    if (applied) *applied = ap;
    (void)n_vec;

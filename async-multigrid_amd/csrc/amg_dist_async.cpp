@@ -258,7 +258,7 @@ int restrict_to(amg_dist_hier *D, AsyncLevel &a, int l)
 // out = P_l x (x on level l+1, out on level l); composed smoothed transfers:
 // out = P x;  y = A out;  out = out + (-w) (y ./ a)
 int prolong_to(amg_dist_hier *D, AsyncLevel &a, int l, double *x, double *out, int apply = 0,
-               double *u = nullptr, double *u_priv = nullptr)
+               double *u = nullptr, double *u_priv = nullptr, unsigned long long *stamp = nullptr)
 {
    const amgk::Gemv mv = amgk::gemv_mode(1.0, 0.0);
    if (l == 0 && fused_xfp0(D)) {
@@ -279,7 +279,7 @@ int prolong_to(amg_dist_hier *D, AsyncLevel &a, int l, double *x, double *out, i
       const long long off = v.sg.off();
       if (apply == 1)
          amgk::mz_xfer_prolong(a.s, v.A.A, x - coff, v.g, v.d_geo_w, D->o.smooth_weight, 1, u - off, u_priv - off,
-                               v.sg.za, v.sg.zb, v.sg.e0(), cz0);
+                               v.sg.za, v.sg.zb, v.sg.e0(), cz0, stamp);
       else
          amgk::mz_xfer_prolong(a.s, v.A.A, x - coff, v.g, v.d_geo_w, D->o.smooth_weight, 0, out - off, nullptr,
                                v.sg.za, v.sg.zb, v.sg.e0(), cz0);
@@ -390,8 +390,10 @@ int level_correction(amg_dist_hier *D, int k, int j = -1)
    // (the fused prolongation + atomic correction: its whole launch is the window)
    if (j >= 0 && fuse_corr && D->corr.record_start(k, j, s))
       return amg_set_error(AMG_ERR_HIP, "level %d: correction event", k);
+   unsigned long long *stp = j >= 0 ? D->corr.stamp(k, j) : nullptr;
    for (int l = k - 1; l >= 0; l--)
-      AMG_TRY(prolong_to(D, a, l, a.e[l + 1], a.e[l], (l == 0 && fuse_corr) ? 1 : 0, D->lv[0].u, a.u_priv));
+      AMG_TRY(prolong_to(D, a, l, a.e[l + 1], a.e[l], (l == 0 && fuse_corr) ? 1 : 0, D->lv[0].u, a.u_priv,
+                         (l == 0 && fuse_corr) ? stp : nullptr));
    const int n0 = D->lv[0].n;
    if (o.accel_type != AMG_NO_ACCEL) {
       // DMEM_Add.cpp:319-324: ChebyUpdate(gridk.d, U_array[0]) on the level's
@@ -407,7 +409,7 @@ int level_correction(amg_dist_hier *D, int k, int j = -1)
    // correction into the shared slab; u_priv = the value each row saw
    if (j >= 0 && !fuse_corr && D->corr.record_start(k, j, s))
       return amg_set_error(AMG_ERR_HIP, "level %d: correction event", k);
-   if (!fuse_corr) amgk::atomic_correct(s, D->lv[0].u, a.e[0], a.u_priv, n0);
+   if (!fuse_corr) amgk::atomic_correct(s, D->lv[0].u, a.e[0], a.u_priv, n0, stp);
    if (j >= 0 && D->corr.record(k, j, s)) return amg_set_error(AMG_ERR_HIP, "level %d: correction event", k);
    // private residual r_k = f - A u_k  (SMEM_Residual on u_k)
    AMG_TRY(a_spgemv(D, a, D->lv[0].A, a.u_priv, nullptr, amgk::gemv_mode(1.0, 0.0), a.y));
@@ -676,6 +678,9 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
    AMG_HIP(hipEventCreate(&t_start));
    for (auto &e : t_end) AMG_HIP(hipEventCreate(&e));
+   // the free race's update windows on the device clock (amg_dist_async_update_windows)
+   if (sched == AMG_SCHED_FREE && D->corr.stamps_begin(c->stream, D->L, std::max(1, D->o.num_cycles)))
+      return amg_set_error(AMG_ERR_OOM, "amg_dist_async_solve: update-window stamps");
    AMG_HIP(hipEventRecord(ready, c->stream));
    AMG_HIP(hipEventRecord(t_start, c->stream));
    D->corr.reset(D->L);
@@ -769,6 +774,8 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
       std::vector<int> cnt(D->L, 0);
       for (int k = 0; k < active; k++) cnt[k] = N;
       if (D->corr.collect(t_start, cnt)) return amg_set_error(AMG_ERR_HIP, "amg_dist_async_solve: correction times");
+      if (D->corr.stamps_collect(cnt, c->wall_khz))
+         return amg_set_error(AMG_ERR_HIP, "amg_dist_async_solve: update-window stamps");
    }
    D->level_ms.assign(D->L, 0.0);
    for (int k = 0; k < active; k++) {
@@ -800,6 +807,18 @@ extern "C" int amg_dist_hier_set_async_times(amg_dist_hier *D, const double *t, 
       AMG_ARG(n[k] >= 0, "amg_dist_hier_set_async_times: level %d: %d entries", k, n[k]);
       D->async_t[k].assign(t + off, t + off + n[k]);
    }
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_async_update_windows(const amg_dist_hier *D, int level, double *ms, int cap, int *count)
+{
+   AMG_ARG(D && count && level >= 0 && level < D->L, "amg_dist_async_update_windows: bad argument");
+   const bool start = cap < 0;
+   if (start) cap = -cap;
+   const auto &vv = start ? D->corr.w0 : D->corr.w1;
+   const auto &v = level < (int)vv.size() ? vv[level] : std::vector<double>();
+   *count = (int)v.size();
+   for (int j = 0; j < (int)v.size() && j < cap && ms; j++) ms[j] = v[j];
    return AMG_OK;
 }
 

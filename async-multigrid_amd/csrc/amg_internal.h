@@ -6,6 +6,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
+#include <limits>
 #include <vector>
 
 #include "amg_mi355x.h"
@@ -69,6 +70,10 @@ inline double amg_timed_end(const std::vector<double> &t, double dur, int j)
    return t[n - 1] + (double)(j - n + 1) * dt;
 }
 
+namespace amgk {
+void stamp_init(hipStream_t s, unsigned long long *stamps, int n);
+}
+
 // per-correction end events of a free race (one pool per level, grown on use)
 // (the update point of correction j: its start event `record_start`, before
 // the kernel that adds it into the shared iterate, and its end event `record`,
@@ -111,11 +116,55 @@ struct AmgCorrTimes {
          }
       return 0;
    }
+   // device execution windows of the update kernels (stamp_begin / stamp_end
+   // in the kernel that adds correction j of level k into the shared vector):
+   // [k][j] start / end in ms of the device wall clock (an arbitrary origin
+   // common to every stream and process on the device); NaN: not stamped
+   unsigned long long *d_st = nullptr;
+   int st_cap = 0, st_L = 0;
+   std::vector<std::vector<double>> w0, w1;
+   int stamps_begin(hipStream_t s, int L, int cap)
+   {
+      if (!d_st || L * cap > st_L * st_cap) {
+         if (d_st) hipFree(d_st);
+         d_st = nullptr;
+         if (hipMalloc((void **)&d_st, (size_t)2 * L * cap * sizeof(unsigned long long)) != hipSuccess) return -1;
+      }
+      st_L = L;
+      st_cap = cap;
+      amgk::stamp_init(s, d_st, L * cap);
+      return 0;
+   }
+   unsigned long long *stamp(int k, int j) const
+   {
+      return (d_st && k >= 0 && k < st_L && j >= 0 && j < st_cap) ? d_st + 2 * ((size_t)k * st_cap + j) : nullptr;
+   }
+   // after the solve (the stream has finished): windows of the first cnt[k]
+   // corrections of every level
+   int stamps_collect(const std::vector<int> &cnt, int wall_khz)
+   {
+      w0.assign(st_L, {});
+      w1.assign(st_L, {});
+      if (!d_st) return 0;
+      std::vector<unsigned long long> h((size_t)2 * st_L * st_cap);
+      if (hipMemcpy(h.data(), d_st, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+         return -1;
+      const double tpm = wall_khz > 0 ? (double)wall_khz : 1e5; // ticks per ms
+      for (int k = 0; k < st_L && k < (int)cnt.size(); k++)
+         for (int j = 0; j < cnt[k] && j < st_cap; j++) {
+            const unsigned long long a = h[2 * ((size_t)k * st_cap + j)], b = h[2 * ((size_t)k * st_cap + j) + 1];
+            const bool ok = a != ~0ull && b != 0ull;
+            w0[k].push_back(ok ? (double)a / tpm : std::numeric_limits<double>::quiet_NaN());
+            w1[k].push_back(ok ? (double)b / tpm : std::numeric_limits<double>::quiet_NaN());
+         }
+      return 0;
+   }
    ~AmgCorrTimes()
    {
       for (auto *vv : {&ev, &ev0})
          for (auto &v : *vv)
             for (auto e : v) hipEventDestroy(e);
+      if (d_st) hipFree(d_st);
    }
 };
 // anchored operators (interpolation, restriction): row 2t+1's anchor minus
@@ -358,7 +407,8 @@ void jacobi_from_residual(hipStream_t s, const double *diag, const double *r, co
 // returns whether it was applied
 bool hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
                 const int *d_blk, int nblk, const double *diag_scale, double weight, int zero,
-                int reverse, double *apply_u = nullptr, double *apply_priv = nullptr);
+                int reverse, double *apply_u = nullptr, double *apply_priv = nullptr,
+                unsigned long long *stamp = nullptr);
 // *d_out = max(*d_out, longest row of A)
 void row_max(hipStream_t s, const amg_mat *A, int *d_out);
 // asynchronous / semi-asynchronous Gauss-Seidel, one lane per block, live u
@@ -421,7 +471,7 @@ void mz_xfer_restrict(hipStream_t s, const amg_mat *A, const double *r, const Ge
                       double omega, double *rc, int Kb = 0, int Ke = -1, int fz0 = 0, int cz0 = 0);
 void mz_xfer_prolong(hipStream_t s, const amg_mat *A, const double *ec, const GeoT &g, const double *wdev,
                      double omega, int mode, double *out, double *u_priv, int zlo = 0, int zhi = -1, int fz0 = 0,
-                     int cz0 = 0);
+                     int cz0 = 0, unsigned long long *stamp = nullptr);
 // transpose-product with the expansion-buffer order of T static chunks
 void matvec_t_chunked(hipStream_t s, const amg_mat *AT, const double *x, double *y, int n_src,
                       int T);
@@ -456,11 +506,17 @@ void dmem_cheby_update(hipStream_t s, double *d, double *u, int n, int branch, d
 void dmem_mult_accel(hipStream_t s, double *x, const double *e, double *d, int n, int first, double om1,
                      double omd);
 // atomic correction: u += e (device-scope fp64 atomics), u_priv = value after the add
-void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n);
+// stamp (nullable, every update kernel of a free race): stamp[0] = min, stamp[1] = max of the
+// device wall clock over the kernel's workgroups -- its actual execution window (stamp_init)
+void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n,
+                    unsigned long long *stamp = nullptr);
+// stamps[0 .. 2n): starts ~0, ends 0
+void stamp_init(hipStream_t s, unsigned long long *stamps, int n);
 // serialised (SEMI_ASYNC) form: u += e; u_priv = u (u_priv may be null)
 void semi_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n);
 // READ_RES: r -= y (atomic or serialised), r_priv = the updated value
-void res_update(hipStream_t s, double *r, const double *y, double *r_priv, int n, int atomic);
+void res_update(hipStream_t s, double *r, const double *y, double *r_priv, int n, int atomic,
+                unsigned long long *stamp = nullptr);
 // u[rb, re) += x[rb, re), device-scope atomics
 void atomic_add(hipStream_t s, double *u, const double *x, int rb, int re);
 

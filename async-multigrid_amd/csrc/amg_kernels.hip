@@ -1592,6 +1592,20 @@ struct Val7 {
 // barrier per plane, so the four waves march loosely coupled
 constexpr int AMG_RR_RING = 4;
 
+// execution window of an update kernel (a free race's replay checks): the
+// workgroups' first start and last end on the device wall clock (vector atomics)
+__device__ __forceinline__ void stamp_begin(unsigned long long *st)
+{
+   if (st && threadIdx.x == 0) atomicMin(st, (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void stamp_end(unsigned long long *st)
+{
+   if (st) {
+      __syncthreads();
+      if (threadIdx.x == 0) atomicMax(st + 1, (unsigned long long)wall_clock64());
+   }
+}
+
 // ZeroGuess epilogue of a restriction: the coarse level's first pre-smoothing
 // sweep from a zero guess, u = w f / a (jacobi_zero_k variant 0, same
 // expression, a == 0 rows untouched), from the restricted value in registers
@@ -2269,8 +2283,9 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ e, const double *__restrict__ wg,
    double mw, int nx, int ny, int nz, int zc, int npb, int xcd, double *__restrict__ out, double *__restrict__ u_priv,
-   int zlo, int zhi, int fz0, int cz0)
+   int zlo, int zhi, int fz0, int cz0, unsigned long long *stamp)
 {
+   stamp_begin(stamp);
    // fine planes [zlo, zhi) of the nx * ny * nz box; out / u_priv / the
    // operator's rows (pattern bytes) have plane 0 = fine plane fz0, e plane 0
    // = coarse plane cz0 (a z-slab's extended vectors; the whole box: 0, nz, 0, 0)
@@ -2361,10 +2376,12 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
       xq = xn;
       eq = en;
    }
+   stamp_end(stamp);
 }
 
 void mz_xfer_prolong(hipStream_t s, const amg_mat *A, const double *ec, const GeoT &g, const double *wdev,
-                     double omega, int mode, double *out, double *u_priv, int zlo, int zhi, int fz0, int cz0)
+                     double omega, int mode, double *out, double *u_priv, int zlo, int zhi, int fz0, int cz0,
+                     unsigned long long *stamp)
 {
    MpSten S;
    for (int j = 0; j < AMG_MP_MAXJ; j++) {
@@ -2381,7 +2398,7 @@ void mz_xfer_prolong(hipStream_t s, const amg_mat *A, const double *ec, const Ge
 #define AMG_XP(U, O)                                                                                           \
    mz_xfer_prolong_kernel<U, O><<<npb * nch, 256, 0, s>>>(A->ppat, A->mpmask, A->pp_n, mv, S, ec, wdev, -omega, \
                                                           g.nx, g.ny, g.nz, zc, npb, A->ctx->mz_xcd, out, u_priv, \
-                                                          zlo, zhi, fz0, cz0)
+                                                          zlo, zhi, fz0, cz0, mode == 1 ? stamp : nullptr)
 #define AMG_XP2(U)                 \
    if (mode == 1) AMG_XP(U, 1);    \
    else if (mode == 2) AMG_XP(U, 2); \
@@ -4754,17 +4771,19 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
 // value row.  Tails past TMAX slots are re-read from memory at the step.  The
 // operations and their order are the reference's sequential loop's
 // (SMEM_Smooth.cpp:265-304 / 548-585): bit-identical.  Any row length.
-template <int NB, int CH, int TMAX, bool VI>
-__global__ __launch_bounds__(256) void hybrid_jgs_tile_k(const int *__restrict__ rowptr, const int *__restrict__ col,
+template <int NB, int CH, int TMAX, bool VI, bool SHORT = false, int NT = 256, int OCC = 1>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(OCC))) void hybrid_jgs_tile_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                          const double *__restrict__ val,
                                                          const unsigned char *__restrict__ vidx,
                                                          const double *__restrict__ vtab, const double *__restrict__ f,
                                                          double *u, const double *__restrict__ u_prev,
                                                          const int *__restrict__ blk, int nblk,
                                                          const double *__restrict__ ds, double weight, int zero,
-                                                         int reverse, double *apply_u, double *__restrict__ apply_priv)
+                                                         int reverse, double *apply_u, double *__restrict__ apply_priv,
+                                                         unsigned long long *stamp)
 {
-   constexpr int NT = 256, SP = NB + 1, NS = CH * SP, RPT = NB * CH / NT;
+   stamp_begin(stamp);
+   constexpr int SP = NB + 1, NS = CH * SP, RPT = NB * CH / NT;
    static_assert(NB == 64 && (NB * CH) % NT == 0, "one phase-2 wave, whole rows per lane");
    __shared__ double sP[NS], sOld[NS], sD[NS], sV[NS];
    __shared__ double sW[TMAX][NS];
@@ -4808,80 +4827,176 @@ __global__ __launch_bounds__(256) void hybrid_jgs_tile_k(const int *__restrict__
    }
    for (int c0 = 0; c0 < nmax; c0 += CH) {
       // phase 1
+      if constexpr (SHORT) {
+         // rows of at most 8 entries: every load of the lane's RPT rows in flight
+         // together (columns / values, then operands), no per-row loop
+         int iv[RPT], nsv[RPT], nev[RPT], lenv[RPT], slotv[RPT];
+         double Pv[RPT], oldv[RPT], ddv[RPT], av[RPT];
+         int jk[RPT][8];
+         double vk[RPT][8], xk[RPT][8];
 #pragma unroll
-      for (int it = 0; it < RPT; it++) {
-         const int r = it * NT + t, q = r / CH, sl = r % CH, slot = sl * SP + q;
-         const int ns = sBlk[q], ne = sBlk[q + 1], pos = c0 + sl;
-         const bool act = pos < ne - ns;
-         const int i = act ? (reverse ? ne - 1 - pos : ns + pos) : 0;
-         const int rs = rs_n[it], len = act ? re_n[it] - rs_n[it] : 0;
-         if (pos + CH < ne - ns) {
-            const int in = reverse ? ne - 1 - (pos + CH) : ns + pos + CH;
-            rs_n[it] = rowptr[in];
-            re_n[it] = rowptr[in + 1];
-         }
-         double P = 0.0, old = 0.0, a = 0.0, dd = 1.0;
-         int tl = 0, kov = 0;
-         bool dep = false;
-         if (act) {
-            P = f[i];
-            old = zero ? 0.0 : u_prev[i];
-            if (ds) dd = ds[i];
-            // a_ii = val[rowptr[i]] as the reference reads it: an empty row's is the
-            // next row's first value (as hybrid_jgs_grp_k's clamped first load)
-            if (len == 0) a = VI ? vtab[vidx[rs]] : val[rs];
-         }
-         for (int kb = 0; kb < len; kb += 8) {
-            int jk[8], tk[8];
-            double vk[8], xk[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) { // column / value loads (clamped: always in range)
-               const int e = rs + min(kb + k, len - 1);
-               jk[k] = col[e];
-               vk[k] = VI ? vtab[vidx[e]] : val[e];
+         for (int it = 0; it < RPT; it++) {
+            const int r = it * NT + t, q = r / CH, sl = r % CH;
+            slotv[it] = sl * SP + q;
+            const int ns = sBlk[q], ne = sBlk[q + 1], pos = c0 + sl;
+            nsv[it] = ns;
+            nev[it] = ne;
+            const bool act = pos < ne - ns;
+            const int i = act ? (reverse ? ne - 1 - pos : ns + pos) : 0;
+            iv[it] = i;
+            const int rs = rs_n[it], len = act ? re_n[it] - rs_n[it] : 0;
+            lenv[it] = act ? len : -1;
+            if (pos + CH < ne - ns) {
+               const int in = reverse ? ne - 1 - (pos + CH) : ns + pos + CH;
+               rs_n[it] = rowptr[in];
+               re_n[it] = rowptr[in + 1];
             }
-            if (kb == 0) a = vk[0];
-            bool far = false;
+            Pv[it] = act ? f[i] : 0.0;
+            oldv[it] = (act && !zero) ? u_prev[i] : 0.0;
+            ddv[it] = (act && ds) ? ds[i] : 1.0;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-               tk[k] = kb + k < len ? kind(jk[k], i, ns, ne, c0) : JG_NONE;
-               far = far || tk[k] == JG_FAR;
+            for (int k = 0; k < 8; k++) { // clamped: an empty row reads its a_ii slot (the next row's first)
+               const int e = rs + max(0, min(k, len - 1));
+               jk[it][k] = col[e];
+               vk[it][k] = VI ? vtab[vidx[e]] : val[e];
             }
+            av[it] = act ? vk[it][0] : 0.0;
+         }
+         bool far = false;
+#pragma unroll
+         for (int it = 0; it < RPT; it++)
 #pragma unroll
             for (int k = 0; k < 8; k++) { // operand loads (own row when unused)
-               const double xv = u_prev[tk[k] == JG_PLAIN ? jk[k] : i];
-               xk[k] = tk[k] == JG_PLAIN ? xv : 0.0;
+               const int tg = k < lenv[it] ? kind(jk[it][k], iv[it], nsv[it], nev[it], c0) : JG_NONE;
+               far = far || tg == JG_FAR;
+               const double xv = u_prev[tg == JG_PLAIN ? jk[it][k] : iv[it]];
+               xk[it][k] = tg == JG_PLAIN ? xv : 0.0;
             }
-            if (far) {
+         if (far) {
+#pragma unroll
+            for (int it = 0; it < RPT; it++)
 #pragma unroll
                for (int k = 0; k < 8; k++)
-                  if (tk[k] == JG_FAR) xk[k] = ld_u(jk[k]);
-            }
+                  if (k < lenv[it] && kind(jk[it][k], iv[it], nsv[it], nev[it], c0) == JG_FAR)
+                     xk[it][k] = ld_u(jk[it][k]);
+         }
+#pragma unroll
+         for (int it = 0; it < RPT; it++) {
+            const int slot = slotv[it];
+            double P = Pv[it];
+            int tl = 0;
+            bool dep = false;
 #pragma unroll
             for (int k = 0; k < 8; k++) { // CSR order: prefix, then tail
-               const int tg = tk[k];
+               const int tg = k < lenv[it] ? kind(jk[it][k], iv[it], nsv[it], nev[it], c0) : JG_NONE;
                if (tg == JG_NONE) continue;
                const bool prod = tg == JG_PLAIN || tg == JG_PROD || tg == JG_FAR;
                dep = dep || !prod;
-               const double w = prod ? vk[k] * xk[k] : vk[k];
+               const double w = prod ? vk[it][k] * xk[it][k] : vk[it][k];
                if (!dep) {
                   P = P - w;
                } else {
                   if (tl < TMAX) {
                      sW[tl][slot] = w;
                      sT[tl][slot] = (signed char)(prod ? JG_PROD : tg);
-                  } else if (tl == TMAX) {
-                     kov = kb + k;
                   }
                   tl++;
                }
             }
+            // (tails past TMAX re-read from entry TMAX slots after the first dependency)
+            int kov = 0;
+            if (tl > TMAX) {
+               int seen = 0;
+#pragma unroll
+               for (int k = 0; k < 8; k++) {
+                  const int tg = k < lenv[it] ? kind(jk[it][k], iv[it], nsv[it], nev[it], c0) : JG_NONE;
+                  if (tg == JG_NONE) continue;
+                  const bool prod = tg == JG_PLAIN || tg == JG_PROD || tg == JG_FAR;
+                  if (!prod || seen > 0) seen++;
+                  if (seen == TMAX + 1 && kov == 0) kov = k;
+               }
+            }
+            sP[slot] = P;
+            sOld[slot] = oldv[it];
+            sD[slot] = ds ? ddv[it] : av[it];
+            sM[slot] = (av[it] != 0.0 ? 1 : 0) | (min(tl, 0x7fff) << 1) | (kov << 16);
          }
-         if (!ds) dd = a;
-         sP[slot] = P;
-         sOld[slot] = old;
-         sD[slot] = dd;
-         sM[slot] = (a != 0.0 ? 1 : 0) | (min(tl, 0x7fff) << 1) | (kov << 16);
+      } else {
+#pragma unroll
+         for (int it = 0; it < RPT; it++) {
+            const int r = it * NT + t, q = r / CH, sl = r % CH, slot = sl * SP + q;
+            const int ns = sBlk[q], ne = sBlk[q + 1], pos = c0 + sl;
+            const bool act = pos < ne - ns;
+            const int i = act ? (reverse ? ne - 1 - pos : ns + pos) : 0;
+            const int rs = rs_n[it], len = act ? re_n[it] - rs_n[it] : 0;
+            if (pos + CH < ne - ns) {
+               const int in = reverse ? ne - 1 - (pos + CH) : ns + pos + CH;
+               rs_n[it] = rowptr[in];
+               re_n[it] = rowptr[in + 1];
+            }
+            double P = 0.0, old = 0.0, a = 0.0, dd = 1.0;
+            int tl = 0, kov = 0;
+            bool dep = false;
+            if (act) {
+               P = f[i];
+               old = zero ? 0.0 : u_prev[i];
+               if (ds) dd = ds[i];
+               // a_ii = val[rowptr[i]] as the reference reads it: an empty row's is the
+               // next row's first value (as hybrid_jgs_grp_k's clamped first load)
+               if (len == 0) a = VI ? vtab[vidx[rs]] : val[rs];
+            }
+            for (int kb = 0; kb < len; kb += 8) {
+               int jk[8], tk[8];
+               double vk[8], xk[8];
+   #pragma unroll
+               for (int k = 0; k < 8; k++) { // column / value loads (clamped: always in range)
+                  const int e = rs + min(kb + k, len - 1);
+                  jk[k] = col[e];
+                  vk[k] = VI ? vtab[vidx[e]] : val[e];
+               }
+               if (kb == 0) a = vk[0];
+               bool far = false;
+   #pragma unroll
+               for (int k = 0; k < 8; k++) {
+                  tk[k] = kb + k < len ? kind(jk[k], i, ns, ne, c0) : JG_NONE;
+                  far = far || tk[k] == JG_FAR;
+               }
+   #pragma unroll
+               for (int k = 0; k < 8; k++) { // operand loads (own row when unused)
+                  const double xv = u_prev[tk[k] == JG_PLAIN ? jk[k] : i];
+                  xk[k] = tk[k] == JG_PLAIN ? xv : 0.0;
+               }
+               if (far) {
+   #pragma unroll
+                  for (int k = 0; k < 8; k++)
+                     if (tk[k] == JG_FAR) xk[k] = ld_u(jk[k]);
+               }
+   #pragma unroll
+               for (int k = 0; k < 8; k++) { // CSR order: prefix, then tail
+                  const int tg = tk[k];
+                  if (tg == JG_NONE) continue;
+                  const bool prod = tg == JG_PLAIN || tg == JG_PROD || tg == JG_FAR;
+                  dep = dep || !prod;
+                  const double w = prod ? vk[k] * xk[k] : vk[k];
+                  if (!dep) {
+                     P = P - w;
+                  } else {
+                     if (tl < TMAX) {
+                        sW[tl][slot] = w;
+                        sT[tl][slot] = (signed char)(prod ? JG_PROD : tg);
+                     } else if (tl == TMAX) {
+                        kov = kb + k;
+                     }
+                     tl++;
+                  }
+               }
+            }
+            if (!ds) dd = a;
+            sP[slot] = P;
+            sOld[slot] = old;
+            sD[slot] = dd;
+            sM[slot] = (a != 0.0 ? 1 : 0) | (min(tl, 0x7fff) << 1) | (kov << 16);
+         }
       }
       __syncthreads();
       // phase 2: lane q walks block q's CH steps
@@ -4937,6 +5052,7 @@ __global__ __launch_bounds__(256) void hybrid_jgs_tile_k(const int *__restrict__
          __syncthreads();
       }
    }
+   stamp_end(stamp);
 }
 
 __global__ void row_max_k(const int *__restrict__ rowptr, int n, int *__restrict__ out)
@@ -4957,7 +5073,7 @@ void row_max(hipStream_t s, const amg_mat *A, int *d_out)
 
 bool hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, const double *u_prev,
                 const int *d_blk, int nblk, const double *diag_scale, double weight, int zero,
-                int reverse, double *apply_u, double *apply_priv)
+                int reverse, double *apply_u, double *apply_priv, unsigned long long *stamp)
 {
    if (nblk <= 0) return false;
    int mode = A->ctx->jgs_wave;
@@ -4965,17 +5081,27 @@ bool hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
       // short rows: passes of 16 rows per block, 4 tail slots; longer rows
       // (27-pt, classical): passes of 4 rows, 16 slots
       const int nwg = (nblk + 63) / 64;
-#define JGS_TILE(CH, TM, V)                                                                                          \
-   hybrid_jgs_tile_k<64, CH, TM, V><<<nwg, 256, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u, u_prev, \
+#define JGS_TILE(CH, TM, V, SH, OC)                                                                                  \
+   hybrid_jgs_tile_k<64, CH, TM, V, SH, SH ? 512 : 256, OC><<<nwg, SH ? 512 : 256, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u, u_prev, \
                                                         d_blk, nblk, diag_scale, weight, zero, reverse, apply_u,  \
-                                                        apply_priv)
+                                                        apply_priv, apply_u ? stamp : nullptr)
       const bool vi = A->vidx != nullptr;
       if (A->maxrow >= 0 && A->maxrow <= 8) {
-         if (vi) JGS_TILE(16, 4, true);
-         else JGS_TILE(16, 4, false);
+         // AMG_JGS_TILE_OCC=4: registers capped for two workgroups per CU
+         static const int occ = [] {
+            const char *v = std::getenv("AMG_JGS_TILE_OCC");
+            return v ? std::atoi(v) : 1;
+         }();
+         if (occ == 4) {
+            if (vi) JGS_TILE(16, 4, true, true, 4);
+            else JGS_TILE(16, 4, false, true, 4);
+         } else {
+            if (vi) JGS_TILE(16, 4, true, true, 1);
+            else JGS_TILE(16, 4, false, true, 1);
+         }
       } else {
-         if (vi) JGS_TILE(4, 16, true);
-         else JGS_TILE(4, 16, false);
+         if (vi) JGS_TILE(4, 16, true, false, 1);
+         else JGS_TILE(4, 16, false, false, 1);
       }
 #undef JGS_TILE
       return apply_u != nullptr;
@@ -5356,18 +5482,33 @@ void dmem_mult_accel(hipStream_t s, double *x, const double *e, double *d, int n
 
 // SMEM_Async_AMG.cpp:296-299 (FULL_ASYNC): omp atomic u[i] += e[i]; u_k[i] = u[i]
 __global__ void atomic_correct_k(double *u, const double *__restrict__ e,
-                                 double *__restrict__ u_priv, int n)
+                                 double *__restrict__ u_priv, int n, unsigned long long *stamp)
 {
+   stamp_begin(stamp);
    EW_LOOP(i, 0, n)
    {
       const double ei = e[i];
       const double old = atomicAdd(u + i, ei);
       u_priv[i] = old + ei;
    }
+   stamp_end(stamp);
 }
-void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n)
+void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n, unsigned long long *stamp)
 {
-   if (n > 0) atomic_correct_k<<<ew_blocks(n), 256, 0, s>>>(u, e, u_priv, n);
+   if (n > 0) atomic_correct_k<<<ew_blocks(n), 256, 0, s>>>(u, e, u_priv, n, stamp);
+}
+
+__global__ void stamp_init_k(unsigned long long *st, int n)
+{
+   EW_LOOP(i, 0, n)
+   {
+      st[2 * i] = ~0ull;
+      st[2 * i + 1] = 0ull;
+   }
+}
+void stamp_init(hipStream_t s, unsigned long long *stamps, int n)
+{
+   if (n > 0) stamp_init_k<<<ew_blocks(n), 256, 0, s>>>(stamps, n);
 }
 
 // SEMI_ASYNC update (SMEM_Async_AMG.cpp:238-283, under the reference's lock;
@@ -5393,8 +5534,9 @@ void semi_correct(hipStream_t s, double *u, const double *e, double *u_priv, int
 // residual = the value after its update.  atomic: FULL_ASYNC (device-scope fp64
 // atomics); otherwise the serialised SEMI_ASYNC form.
 __global__ void res_update_k(double *r, const double *__restrict__ y, double *__restrict__ r_priv, int n,
-                             int atomic)
+                             int atomic, unsigned long long *stamp)
 {
+   stamp_begin(stamp);
    EW_LOOP(i, 0, n)
    {
       const double yi = y[i];
@@ -5407,10 +5549,12 @@ __global__ void res_update_k(double *r, const double *__restrict__ y, double *__
       }
       r_priv[i] = v;
    }
+   stamp_end(stamp);
 }
-void res_update(hipStream_t s, double *r, const double *y, double *r_priv, int n, int atomic)
+void res_update(hipStream_t s, double *r, const double *y, double *r_priv, int n, int atomic,
+                unsigned long long *stamp)
 {
-   if (n > 0) res_update_k<<<ew_blocks(n), 256, 0, s>>>(r, y, r_priv, n, atomic);
+   if (n > 0) res_update_k<<<ew_blocks(n), 256, 0, s>>>(r, y, r_priv, n, atomic, stamp);
 }
 
 // u[rb, re) += x[rb, re) with device-scope atomics (the GLOBAL residual

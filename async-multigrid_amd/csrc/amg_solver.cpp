@@ -18,7 +18,7 @@ int amg_hybrid_jgs_dev(amg_ctx *c, hipStream_t s, const amg_mat *A, const double
                        double *u_prev, int n_vec, const int *d_blk, int nblk, int blk_lo,
                        int blk_hi, const double *ds, double weight, int sweeps, int zero_first,
                        int reverse, double *apply_u = nullptr, double *apply_priv = nullptr,
-                       bool *applied = nullptr);
+                       bool *applied = nullptr, unsigned long long *stamp = nullptr);
 int amg_sym_jacobi_dev(hipStream_t s, const amg_mat *A, const double *f, double *u, double *y,
                        double *r, double omega, const double *l1, int sweeps, int zero_first,
                        int rb, int re, int variant);
@@ -112,6 +112,7 @@ struct amg_hier {
    // the correction whose update-window start a fused update kernel records
    // (mark_update_start; -1: none)
    int mark_k = -1, mark_j = 0;
+   unsigned long long *mark_stamp = nullptr; // its execution-window stamp
    // per level of the last amg_async_solve: ms from its start to the level's
    // last correction (amg_async_level_ms)
    std::vector<double> level_ms;
@@ -655,7 +656,7 @@ static bool smooth_all_levels(amg_hier *H, hipStream_t s, int Alevel, const doub
       mark_update_start(H, s);
       bool applied = false;
       amg_hybrid_jgs_dev(H->ctx, s, v.A, f, u, u_prev, v.n, v.d_blk, nb, 0, v.n, nullptr, 1.0, 1,
-                         sweeps > 1 ? 0 : zf, 0, apply_u, apply_priv, &applied);
+                         sweeps > 1 ? 0 : zf, 0, apply_u, apply_priv, &applied, H->mark_stamp);
       return applied;
    } else if (o.smoother == AMG_ASYNC_GAUSS_SEIDEL || o.smoother == AMG_SEMI_ASYNC_GAUSS_SEIDEL) {
       // SMEM_Async_GaussSeidel / SMEM_SemiAsync_GaussSeidel (SMEM_Solve.cpp:281-286)
@@ -871,7 +872,8 @@ static bool xfer_prolong(amg_hier *H, hipStream_t s, int l, const double *ec, do
    if (composed_p(H) && H->xfp[l]) {
       if (apply) mark_update_start(H, s);
       if (apply)
-         amgk::mz_xfer_prolong(s, v.A, ec, H->gl[l], H->d_geo_w[l], H->o.smooth_weight, apply, u, u_priv);
+         amgk::mz_xfer_prolong(s, v.A, ec, H->gl[l], H->d_geo_w[l], H->o.smooth_weight, apply, u, u_priv, 0, -1, 0,
+                               0, H->mark_stamp);
       else
          amgk::mz_xfer_prolong(s, v.A, ec, H->gl[l], H->d_geo_w[l], H->o.smooth_weight, 0, ef, nullptr);
       return apply != 0;
@@ -1471,6 +1473,11 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
    AMG_HIP(hipEventCreate(&t_start));
    H->corr.reset(L);
+   // the free race's update windows on the device clock (amg_async_update_windows)
+   const bool rec0 = sched == AMG_SCHED_FREE && !(c->graphs && !semi && !read_res && !global_res && !H->o.profile &&
+                                                   (o.delay_type == AMG_DELAY_NONE || o.delay_usec <= 0));
+   if (rec0 && H->corr.stamps_begin(c->stream, L, std::max(1, o.num_cycles) * (conv_global ? 16 : 1) + 1))
+      return amg_set_error(AMG_ERR_OOM, "amg_async_solve: update-window stamps");
    AMG_HIP(hipEventRecord(ready, c->stream));
    AMG_HIP(hipEventRecord(t_start, c->stream));
    for (int k = k_lo; k < k_hi; k++) {
@@ -1516,6 +1523,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          return AMG_OK;
       };
       const int grb = gr[k], gre = gr[k + 1];
+      unsigned long long *stp = rec ? H->corr.stamp(k, issued[k]) : nullptr;
       {
          // injected delay of the threads this level group stands for
          const int T = delay_threads(o), g = k - k_lo;
@@ -1532,9 +1540,11 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       if (rec && !read_res && !semi) {
          H->mark_k = k;
          H->mark_j = issued[k];
+         H->mark_stamp = stp;
       }
       const bool fused = add_level_correction(H, s, k, a.y_fine, (!read_res && !semi) ? 1 : 0, v0.u, a.u_priv);
       H->mark_k = -1;
+      H->mark_stamp = nullptr;
       if (read_res) {
          amgk::spgemv(s, v0.A, a.e[0], nullptr, mv, a.y, 0, n0, nullptr);
          if (semi) {
@@ -1545,7 +1555,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
          } else {
             if (rec && H->corr.record_start(k, issued[k], s)) return amg_set_error(AMG_ERR_HIP, "correction event");
             amgk::vaxpy(s, 1.0, a.e[0], a.f_acc, 0, n0);
-            amgk::res_update(s, H->r0, a.y, a.y_fine, n0, 1);
+            amgk::res_update(s, H->r0, a.y, a.y_fine, n0, 1, stp);
          }
          if (rec && H->corr.record(k, issued[k], s)) return amg_set_error(AMG_ERR_HIP, "correction event");
       } else {
@@ -1556,7 +1566,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
             AMG_TRY(from_update());
          } else if (!fused) {
             if (rec && H->corr.record_start(k, issued[k], s)) return amg_set_error(AMG_ERR_HIP, "correction event");
-            amgk::atomic_correct(s, v0.u, a.e[0], a.u_priv, n0);
+            amgk::atomic_correct(s, v0.u, a.e[0], a.u_priv, n0, stp);
          }
          if (rec && H->corr.record(k, issued[k], s)) return amg_set_error(AMG_ERR_HIP, "correction event");
          if (!global_res) {
@@ -1757,6 +1767,8 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
       for (int k = 0; k < L; k++) level_corrections[k] = issued[k];
    if (sched == AMG_SCHED_FREE && H->corr.collect(t_start, issued))
       return amg_set_error(AMG_ERR_HIP, "amg_async_solve: correction times");
+   if (rec0 && H->corr.stamps_collect(issued, c->wall_khz))
+      return amg_set_error(AMG_ERR_HIP, "amg_async_solve: update-window stamps");
    H->level_ms.assign(L, 0.0);
    for (int k = k_lo; k < k_hi; k++) {
       float ms = 0.f;
@@ -1797,6 +1809,18 @@ extern "C" int amg_async_correction_ms(const amg_hier *H, int level, double *ms,
    const bool start = cap < 0; // cap < 0: the update windows' start times, -cap entries
    if (start) cap = -cap;
    const auto &vv = start ? H->corr.ms0 : H->corr.ms;
+   const auto &v = level < (int)vv.size() ? vv[level] : std::vector<double>();
+   *count = (int)v.size();
+   for (int j = 0; j < (int)v.size() && j < cap && ms; j++) ms[j] = v[j];
+   return AMG_OK;
+}
+
+extern "C" int amg_async_update_windows(const amg_hier *H, int level, double *ms, int cap, int *count)
+{
+   AMG_ARG(H && count && level >= 0 && level < H->L, "amg_async_update_windows: bad argument");
+   const bool start = cap < 0; // cap < 0: the windows' starts, -cap entries
+   if (start) cap = -cap;
+   const auto &vv = start ? H->corr.w0 : H->corr.w1;
    const auto &v = level < (int)vv.size() ? vv[level] : std::vector<double>();
    *count = (int)v.size();
    for (int j = 0; j < (int)v.size() && j < cap && ms; j++) ms[j] = v[j];

@@ -327,6 +327,12 @@ class DistHier:
         from . import _corr_ms
         return _corr_ms(lib.amg_dist_async_correction_ms, self.h, self.L, start)
 
+    def async_update_windows(self):
+        """(starts, ends) per level: device-clock execution windows (ms) of this rank's update
+        kernels in the last free race (amg_dist_async_update_windows)"""
+        return (_corr_ms(lib.amg_dist_async_update_windows, self.h, self.L, True),
+                _corr_ms(lib.amg_dist_async_update_windows, self.h, self.L, False))
+
     def async_level_ms(self):
         """per level: ms from the last async_solve's start to the level's last correction"""
         L = self.gen.L if self.gen is not None else 64

@@ -476,6 +476,12 @@ int amg_hier_set_async_times(amg_hier *H, const double *t, const int *n, int nle
  * level `level`'s corrections in the last free-race amg_async_solve: *count
  * corrections, the first min(count, cap) written to ms */
 int amg_async_correction_ms(const amg_hier *H, int level, double *ms, int cap, int *count);
+/* the actual execution windows of the same corrections' update kernels (the
+ * kernel that adds the correction into the shared iterate / residual stamps
+ * its workgroups' first start and last end on the device wall clock): end
+ * (cap >= 0) or start (cap < 0, -cap entries) in ms of that clock, an origin
+ * common to every stream and process on the device; NaN where not stamped */
+int amg_async_update_windows(const amg_hier *H, int level, double *ms, int cap, int *count);
 /* EigsPower SMEM_Cheby.cpp:410-518 with this hierarchy's V-cycle as M^{-1} */
 int amg_eigs_power(amg_hier *H, int iters, double *eig_max, double *eig_min);
 /* profile: accumulated device milliseconds and launch counts of the fine-level
@@ -678,6 +684,7 @@ int amg_dist_hier_set_async_durations(amg_dist_hier *D, const double *ms, int n)
  * (this rank's level streams) */
 int amg_dist_hier_set_async_times(amg_dist_hier *D, const double *t, const int *n, int nlev);
 int amg_dist_async_correction_ms(const amg_dist_hier *D, int level, double *ms, int cap, int *count);
+int amg_dist_async_update_windows(const amg_dist_hier *D, int level, double *ms, int cap, int *count);
 /* DMEM_AsyncSmooth (DMEM_Smooth.cpp:16-313) with ASYNC_JACOBI (l1 = 0: u = r ./ (a_ii/omega))
  * or ASYNC_L1_JACOBI (l1 = 1): `sweeps` relaxations of the fine level in residual-update
  * form from x = 0; every relaxation sends its boundary deltas on the communication

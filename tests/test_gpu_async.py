@@ -19,7 +19,7 @@ converge GLOBAL also checks the per-level correction counts."""
 import numpy as np
 import pytest
 
-from async_band import blocks64, in_band, oracle_async_band, replay_check, times_of
+from async_band import blocks64, in_band, oracle_async_band, race_tables, replay_check, times_of
 from test_gpu_solve import hierarchy, gpu_hier, oracle_opts
 
 pytestmark = pytest.mark.gpu
@@ -94,7 +94,8 @@ def test_async_options_band(amg, oracle, ctx, setup, case):
         u, rel, cnt = H.async_solve(f)
         assert np.all(np.isfinite(u))
         rels.append(rel)
-        durs.append((rel, H.async_correction_ms(), None, H.async_correction_ms(start=True)))
+        e_, s_ = race_tables(H)
+        durs.append((rel, e_, None, s_))
         # correcting levels: [k_lo, k_hi); GLOBAL residuals replace level 0's
         # group by the sliced fine smoothing (SMEM_Setup.cpp:609-615)
         # (and the coarsest level's group runs: it smooths its slice)

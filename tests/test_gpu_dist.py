@@ -14,6 +14,8 @@ import threading
 import numpy as np
 import pytest
 
+from async_band import race_tables
+
 from test_gpu_kernels import assert_bitwise
 
 pytestmark = pytest.mark.gpu
@@ -316,7 +318,8 @@ def test_dist_async_band(amg, oracle, ctx, solver, cuts, rep):
         out = []
         for _ in range(3):
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-            out.append((rel, D.get_u(), cnt.copy(), D.async_correction_ms(), D.async_correction_ms(start=True)))
+            e_, s_ = race_tables(D)
+            out.append((rel, D.get_u(), cnt.copy(), e_, s_))
         D.free()
         amg.dist.finalize(c)
         c.close()
@@ -614,7 +617,7 @@ def test_dist_async_additive_accel(amg, oracle, solver, accel, cuts, grid, bound
             D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
             u = D.get_u()
-            ms = (D.async_correction_ms(), D.async_correction_ms(start=True))
+            ms = race_tables(D)
             D.free()
             amg.dist.finalize(c)
             c.close()

@@ -19,6 +19,8 @@ functions) driven through DMEM_Add's asynchronous additive cycle
 import numpy as np
 import pytest
 
+from async_band import race_tables
+
 from test_gpu_dist import run_ranks, split_host
 from test_gpu_kernels import assert_bitwise
 from test_gpu_solve import gpu_hier, oracle_opts
@@ -111,7 +113,8 @@ def dist_async(amg, host, f, opts, cuts, L, dur=None, runs=1):
         out = []
         for _ in range(runs):
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-            out.append((rel, cnt.copy(), D.get_u(), D.async_correction_ms(), D.async_correction_ms(start=True)))
+            e_, s_ = race_tables(D)
+            out.append((rel, cnt.copy(), D.get_u(), e_, s_))
         row0 = D.row0
         D.free()
         amg.dist.finalize(c)
@@ -194,7 +197,8 @@ def test_elast_async_free_race_replay(amg, oracle, ctx, elast):
     for _ in range(2):
         u, rel, cnt = H.async_solve(f)
         assert np.all(np.isfinite(u)) and list(cnt[:L - 1]) == [N] * (L - 1)
-        runs.append((rel, H.async_correction_ms(), None, H.async_correction_ms(start=True)))
+        e_, s_ = race_tables(H)
+        runs.append((rel, e_, None, s_))
     H.free()
     replay_check(amg, oracle, smoothed, f, opts, runs, what="elasticity one GPU")
     druns = dist_async(amg, smoothed, f, opts, (0.5,), L, runs=3)

@@ -18,7 +18,7 @@ device); each rank's level groups run on their own host threads."""
 import numpy as np
 import pytest
 
-from async_band import replay_check
+from async_band import race_tables, replay_check
 from test_gpu_dist import run_ranks
 from test_gpu_kernels import assert_bitwise
 
@@ -45,7 +45,8 @@ def slab_async(amg, gen, opts, f, nranks, rep=1 << 12, rccl1=True, runs=1, dur=N
         out = []
         for _ in range(runs):
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-            out.append((rel, cnt.copy(), D.get_u(), D.async_correction_ms(), D.async_correction_ms(start=True)))
+            e_, s_ = race_tables(D)
+            out.append((rel, cnt.copy(), D.get_u(), e_, s_))
         row0, n0 = D.row0, D.n0
         D.free()
         amg.dist.finalize(c)

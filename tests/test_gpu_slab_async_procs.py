@@ -52,8 +52,10 @@ def _rank(rank, world, port, n, optd, rep, runs, q):
         for _ in range(runs):
             dist.barrier()  # the ranks enter the solve together
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
-            out.append((float(rel), [int(x) for x in cnt], D.get_u(), [t.tolist() for t in D.async_correction_ms()],
-                        [t.tolist() for t in D.async_correction_ms(start=True)]))
+            from async_band import race_tables
+            e_, s_ = race_tables(D)
+            out.append((float(rel), [int(x) for x in cnt], D.get_u(), [list(map(float, t)) for t in e_],
+                        [list(map(float, t)) for t in s_]))
         row0 = D.row0
         D.free()
         amg.dist.finalize(c)

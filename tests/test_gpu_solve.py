@@ -243,7 +243,7 @@ def test_async_multadd_band(amg, oracle, ctx):
     after N corrections per level must sit in [0.5 x min, 2 x max] of the
     oracle's asynchronous band (SMEM_Async_Add_AMG on OpenMP threads, 10 runs
     with one and two threads per level)."""
-    from async_band import oracle_async_band, replay_check
+    from async_band import oracle_async_band, race_tables, replay_check
     _, L, host = hierarchy(amg, oracle, 24, amg.AMG_INTERP_LINEAR)
     w = 0.8
     Ps, Rs = [], []
@@ -264,7 +264,8 @@ def test_async_multadd_band(amg, oracle, ctx):
     for _ in range(3):
         u, rel, cnt = H.async_solve(f)
         rels.append(rel)
-        durs.append((rel, H.async_correction_ms(), None, H.async_correction_ms(start=True)))
+        e_, s_ = race_tables(H)
+        durs.append((rel, e_, None, s_))
         assert np.all(np.isfinite(u))
     H.free()
     # the oracle's model of each run (the replay of its recorded update order,
