@@ -1606,6 +1606,31 @@ __device__ __forceinline__ void stamp_end(unsigned long long *st)
    }
 }
 
+// The FULL_ASYNC update u_i += e_i with the level's copy of the updated row.
+// The reference's form (SMEM_Async_AMG.cpp:296-299): an atomic add, then a
+// read of u_i -- here a no-return device-scope add, the wave's wait for it,
+// and an L1-bypassing read (AMG_ATOMIC_NORET=1, default); the capture form
+// takes the returned value + e_i (AMG_ATOMIC_NORET=0).  Alone (one stream)
+// both give the same bits.
+static int atomic_noret_mode()
+{
+   static const int m = [] {
+      const char *v = std::getenv("AMG_ATOMIC_NORET");
+      return v ? std::atoi(v) : 1;
+   }();
+   return m;
+}
+__device__ __forceinline__ void add_noret(double *p, double v)
+{
+   (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every vector-memory operation this wave issued (stores and no-return atomics too) has completed
+__device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ double read_agent(const double *p)
+{
+   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ZeroGuess epilogue of a restriction: the coarse level's first pre-smoothing
 // sweep from a zero guess, u = w f / a (jacobi_zero_k variant 0, same
 // expression, a == 0 rows untouched), from the restricted value in registers
@@ -2285,6 +2310,8 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
    double mw, int nx, int ny, int nz, int zc, int npb, int xcd, double *__restrict__ out, double *__restrict__ u_priv,
    int zlo, int zhi, int fz0, int cz0, unsigned long long *stamp)
 {
+   // OUT 3: OUT 1 in the reference's add-then-read form
+   constexpr bool noret = OUT == 3;
    stamp_begin(stamp);
    // fine planes [zlo, zhi) of the nx * ny * nz box; out / u_priv / the
    // operator's rows (pattern bytes) have plane 0 = fine plane fz0, e plane 0
@@ -2363,10 +2390,17 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
       const v2d o{xc.x + mw * t0, xc.y + mw * t1};
       if (OUT == 0) {
          *reinterpret_cast<v2du *>(out + row) = o;
-      } else if (OUT == 1) {
-         const double q0 = atomicAdd(out + row, o.x);
-         const double q1 = atomicAdd(out + row + 1, o.y);
-         *reinterpret_cast<v2du *>(u_priv + row) = v2d{q0 + o.x, q1 + o.y};
+      } else if (OUT == 1 || OUT == 3) {
+         if (noret) {
+            add_noret(out + row, o.x);
+            add_noret(out + row + 1, o.y);
+            wait_vm_all();
+            *reinterpret_cast<v2du *>(u_priv + row) = v2d{read_agent(out + row), read_agent(out + row + 1)};
+         } else {
+            const double q0 = atomicAdd(out + row, o.x);
+            const double q1 = atomicAdd(out + row + 1, o.y);
+            *reinterpret_cast<v2du *>(u_priv + row) = v2d{q0 + o.x, q1 + o.y};
+         }
       } else {
          *reinterpret_cast<v2du *>(out + row) = v2d{uo.x + 1.0 * o.x, uo.y + 1.0 * o.y};
       }
@@ -2400,7 +2434,8 @@ void mz_xfer_prolong(hipStream_t s, const amg_mat *A, const double *ec, const Ge
                                                           g.nx, g.ny, g.nz, zc, npb, A->ctx->mz_xcd, out, u_priv, \
                                                           zlo, zhi, fz0, cz0, mode == 1 ? stamp : nullptr)
 #define AMG_XP2(U)                 \
-   if (mode == 1) AMG_XP(U, 1);    \
+   if (mode == 1 && atomic_noret_mode()) AMG_XP(U, 3); \
+   else if (mode == 1) AMG_XP(U, 1); \
    else if (mode == 2) AMG_XP(U, 2); \
    else AMG_XP(U, 0);
    if (A->mp_uni) {
@@ -4576,8 +4611,11 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
                                                        double *u, const double *__restrict__ u_prev,
                                                        const int *__restrict__ blk, int nblk,
                                                        const double *__restrict__ ds, double weight, int zero,
-                                                       int reverse)
+                                                       int reverse, double *apply_u = nullptr,
+                                                       double *__restrict__ apply_priv = nullptr,
+                                                       unsigned long long *stamp = nullptr)
 {
+   stamp_begin(stamp);
    static_assert(C == 8 || C == 16, "lane groups inside DPP rows");
    constexpr int B = 64 / C;
    // UNR (small levels, latency-bound): the whole row's loads in one batch and
@@ -4754,7 +4792,14 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
       carry = __shfl(v, q * C + C - 1, 64);
       // a_ii == 0: the row keeps its value (0 after the zero-guess reset)
       if (act && (a != 0.0 || zero)) __hip_atomic_store(u + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // apply_u: the FULL_ASYNC correction folded in (the reference's add, then read)
+      if (apply_u && act) add_noret(apply_u + i, v);
+      if (apply_u) {
+         wait_vm_all();
+         if (act) apply_priv[i] = read_agent(apply_u + i);
+      }
    }
+   stamp_end(stamp);
 }
 
 // Hybrid Jacobi / Gauss-Seidel, LDS tile form (jgs_wave 3): a workgroup of
@@ -4771,7 +4816,7 @@ __global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ r
 // value row.  Tails past TMAX slots are re-read from memory at the step.  The
 // operations and their order are the reference's sequential loop's
 // (SMEM_Smooth.cpp:265-304 / 548-585): bit-identical.  Any row length.
-template <int NB, int CH, int TMAX, bool VI, bool SHORT = false, int NT = 256, int OCC = 1>
+template <int NB, int CH, int TMAX, bool VI, bool SHORT = false, int NT = 256, int OCC = 1, bool NORET = true>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(OCC))) void hybrid_jgs_tile_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                          const double *__restrict__ val,
                                                          const unsigned char *__restrict__ vidx,
@@ -4782,6 +4827,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(OCC))) void 
                                                          int reverse, double *apply_u, double *__restrict__ apply_priv,
                                                          unsigned long long *stamp)
 {
+   constexpr bool noret = NORET;
    stamp_begin(stamp);
    constexpr int SP = NB + 1, NS = CH * SP, RPT = NB * CH / NT;
    static_assert(NB == 64 && (NB * CH) % NT == 0, "one phase-2 wave, whole rows per lane");
@@ -5041,9 +5087,23 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(OCC))) void 
             const int i = reverse ? ne - 1 - pos : ns + pos;
             const double v = sV[slot];
             if ((sM[slot] & 1) || zero) __hip_atomic_store(u + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (apply_u) {
+            if (apply_u && noret) {
+               add_noret(apply_u + i, v);
+            } else if (apply_u) {
                const double o = atomicAdd(apply_u + i, v);
                apply_priv[i] = o + v;
+            }
+         }
+      }
+      if (apply_u && noret) { // the reference's read of u after its add
+         wait_vm_all();
+#pragma unroll
+         for (int it = 0; it < RPT; it++) {
+            const int r = it * NT + t, q = r / CH, sl = r % CH;
+            const int ns = sBlk[q], ne = sBlk[q + 1], pos = c0 + sl;
+            if (pos < ne - ns) {
+               const int i = reverse ? ne - 1 - pos : ns + pos;
+               apply_priv[i] = read_agent(apply_u + i);
             }
          }
       }
@@ -5128,7 +5188,8 @@ bool hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
       const bool vi = A->vidx != nullptr;
 #define JGS_GRP(R, V)                                                                                               \
    hybrid_jgs_grp_k<8, R, V><<<nwg, 64, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u, u_prev, d_blk, \
-                                                nblk, diag_scale, weight, zero, reverse)
+                                                nblk, diag_scale, weight, zero, reverse, apply_u, apply_priv,     \
+                                                apply_u ? stamp : nullptr)
       if (A->maxrow <= 8) {
          if (vi) JGS_GRP(8, true);
          else JGS_GRP(8, false);
@@ -5137,7 +5198,7 @@ bool hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
          else JGS_GRP(32, false);
       }
 #undef JGS_GRP
-      return false;
+      return apply_u != nullptr;
    }
    if (mode == 2 && A->maxrow >= 0 && A->maxrow <= 32) {
       const int nwg = (nblk + 3) / 4;
@@ -5481,21 +5542,31 @@ void dmem_mult_accel(hipStream_t s, double *x, const double *e, double *d, int n
 }
 
 // SMEM_Async_AMG.cpp:296-299 (FULL_ASYNC): omp atomic u[i] += e[i]; u_k[i] = u[i]
+template <bool NORET>
 __global__ void atomic_correct_k(double *u, const double *__restrict__ e,
                                  double *__restrict__ u_priv, int n, unsigned long long *stamp)
 {
+   constexpr bool noret = NORET;
    stamp_begin(stamp);
    EW_LOOP(i, 0, n)
    {
       const double ei = e[i];
-      const double old = atomicAdd(u + i, ei);
-      u_priv[i] = old + ei;
+      if (noret) {
+         add_noret(u + i, ei);
+         wait_vm_all();
+         u_priv[i] = read_agent(u + i);
+      } else {
+         const double old = atomicAdd(u + i, ei);
+         u_priv[i] = old + ei;
+      }
    }
    stamp_end(stamp);
 }
 void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, int n, unsigned long long *stamp)
 {
-   if (n > 0) atomic_correct_k<<<ew_blocks(n), 256, 0, s>>>(u, e, u_priv, n, stamp);
+   if (n <= 0) return;
+   if (atomic_noret_mode()) atomic_correct_k<true><<<ew_blocks(n), 256, 0, s>>>(u, e, u_priv, n, stamp);
+   else atomic_correct_k<false><<<ew_blocks(n), 256, 0, s>>>(u, e, u_priv, n, stamp);
 }
 
 __global__ void stamp_init_k(unsigned long long *st, int n)

@@ -330,6 +330,7 @@ class DistHier:
     def async_update_windows(self):
         """(starts, ends) per level: device-clock execution windows (ms) of this rank's update
         kernels in the last free race (amg_dist_async_update_windows)"""
+        from . import _corr_ms
         return (_corr_ms(lib.amg_dist_async_update_windows, self.h, self.L, True),
                 _corr_ms(lib.amg_dist_async_update_windows, self.h, self.L, False))
 

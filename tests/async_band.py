@@ -290,7 +290,10 @@ def replay_check(amg, oracle, host, f, opts, runs, blocks=None, composed=False, 
             lo, hi, rr = timed_band(amg, oracle, host, f, opts, replay_tables(corr_ms, L), blocks=blocks,
                                     composed=composed)
         tm = None
-        if torn:
+        # (or_async_add_replay restates FULL_ASYNC / READ_SOL / LOCAL residuals only)
+        sliceable = (opts.async_type != amg.AMG_SEMI_ASYNC and opts.read_type != amg.AMG_READ_RES and
+                     not (opts.res_compute_type == amg.AMG_GLOBAL and opts.solver == amg.AMG_ASYNC_MULTADD))
+        if torn and sliceable:
             tm = torn_replay(amg, oracle, host, f, opts, corr_ms, starts, rs=rs, composed=composed, blocks=blocks)
             lo, hi = min(lo, tm), max(hi, tm)
             rr = list(rr) + [tm]
