@@ -41,6 +41,7 @@
 #include <algorithm>
 #include <cmath>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -1213,9 +1214,24 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
             AMG_HIP(hipStreamWaitEvent(cs, packed[q], 0));
          }
          AMG_HIP(hipEventRecord(tx0(k), cs));
-         for (int i = 0; i < np && st == AMG_OK; i++)
-            if (M.scnt[i] > 0)
+         for (int i = 0; i < np && st == AMG_OK; i++) {
+            if (M.scnt[i] <= 0) continue;
+            // a full slot ring: keep receiving (and acknowledging) while waiting,
+            // or two ranks that both wait to send would wait on each other
+            const auto t0 = std::chrono::steady_clock::now();
+            for (;;) {
+               int ok = 0;
+               if ((st = link_can_send(D->ajac_links, 0, M.peers[i], &ok)) != AMG_OK || ok) break;
+               if ((st = poll_links(k, false)) != AMG_OK) break;
+               if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 300.0) {
+                  st = amg_set_error(AMG_ERR_RCCL, "amg_dist_async_jacobi: send to rank %d timed out", M.peers[i]);
+                  break;
+               }
+               std::this_thread::yield();
+            }
+            if (st == AMG_OK)
                st = link_send(D->ajac_links, 0, M.peers[i], sbuf + (size_t)q * SS + M.soff[i], M.scnt[i], cs);
+         }
          if (st != AMG_OK) break;
          AMG_HIP(hipEventRecord(tx1(k), cs));
          AMG_HIP(hipEventRecord(sent[q], cs));

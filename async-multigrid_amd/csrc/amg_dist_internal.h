@@ -142,6 +142,9 @@ int link_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipStream_t
 // MPI_Test + receive: if the next message from peer has arrived, launch its
 // unpack on s and set *got = 1; else *got = 0 and return at once
 int link_try_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipStream_t s, int *got);
+// would link_send to peer go through without waiting (its slot acknowledged)?
+// (publishes this thread's completed copies first); *ok
+int link_can_send(LinkSet *L, int k, int peer, int *ok);
 int link_drain(LinkSet *L, int k); // publish everything level group k has in flight
 void link_abort(LinkSet *L);       // tell every peer to give up waiting on this rank
 void link_free(LinkSet *L);

@@ -1593,14 +1593,18 @@ struct Val7 {
 constexpr int AMG_RR_RING = 4;
 
 // execution window of an update kernel (a free race's replay checks): the
-// workgroups' first start and last end on the device wall clock (vector atomics)
+// first start and last end on the device wall clock over a sample of its
+// workgroups -- every 64th and the last (workgroups dispatch in index order;
+// a stamp from every workgroup would queue tens of thousands of atomics on one
+// word and slow the kernel it measures several-fold); vector atomics
+__device__ __forceinline__ bool stamp_wg() { return (blockIdx.x & 63) == 0 || blockIdx.x == gridDim.x - 1; }
 __device__ __forceinline__ void stamp_begin(unsigned long long *st)
 {
-   if (st && threadIdx.x == 0) atomicMin(st, (unsigned long long)wall_clock64());
+   if (st && threadIdx.x == 0 && stamp_wg()) atomicMin(st, (unsigned long long)wall_clock64());
 }
 __device__ __forceinline__ void stamp_end(unsigned long long *st)
 {
-   if (st) {
+   if (st && stamp_wg()) {
       __syncthreads();
       if (threadIdx.x == 0) atomicMax(st + 1, (unsigned long long)wall_clock64());
    }

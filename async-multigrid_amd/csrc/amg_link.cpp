@@ -462,6 +462,17 @@ int amgd::link_try_recv(LinkSet *L, int k, int peer, double *dst, long long n, h
    return AMG_OK;
 }
 
+int amgd::link_can_send(LinkSet *L, int k, int peer, int *ok)
+{
+   Chan &c = L->c(k, peer);
+   AMG_TRY(progress(L, k));
+   const unsigned long long seq = c.sseq + 1;
+   *ok = (seq <= NS || c.s_acked->v.load(std::memory_order_acquire) >= seq - NS) && c.sseq - c.s_pub < MAX_EV;
+   if (!*ok && aborted(L, peer))
+      return amg_set_error(AMG_ERR_RCCL, "link: send (level %d, rank %d <-> %d): aborted", k, L->me, peer);
+   return AMG_OK;
+}
+
 int amgd::link_drain(LinkSet *L, int k)
 {
    for (int p = 0; p < L->R; p++) {
