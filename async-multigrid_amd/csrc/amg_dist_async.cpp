@@ -1132,11 +1132,13 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
    if (use_links && !D->ajac_links) {
       std::vector<long long> caps(c->xport->nranks, 0);
       for (int i = 0; i < np; i++) caps[M.peers[i]] = M.rcnt[i];
-      if ((st = link_create(D, 1, caps, &D->ajac_links)) != AMG_OK) return fail(st);
+      // 8 slots per channel: a sender runs up to 8 sweeps ahead of a peer's receipts
+      if ((st = link_create(D, 1, caps, &D->ajac_links, 8)) != AMG_OK) return fail(st);
    }
    if (use_links && (st = link_reset(D->ajac_links, true)) != AMG_OK) return fail(st);
    std::vector<long long> got_cnt(np, 0);
    long long on_time = 0, late = 0;
+   double send_wait_ms = 0.0; // host time a send waited for its slot (flow control)
    // r -= A_offd g on the rows that have ghost columns (outside the interior [b0, b1))
    auto apply_offd = [&]() {
       amgk::spgemv(s, M.A, gext, r, upd, r, 0, M.b0, nullptr);
@@ -1213,7 +1215,7 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
             AMG_HIP(hipEventRecord(packed[q], s));
             AMG_HIP(hipStreamWaitEvent(cs, packed[q], 0));
          }
-         AMG_HIP(hipEventRecord(tx0(k), cs));
+         bool first = true;
          for (int i = 0; i < np && st == AMG_OK; i++) {
             if (M.scnt[i] <= 0) continue;
             // a full slot ring: keep receiving (and acknowledging) while waiting,
@@ -1229,9 +1231,15 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
                }
                std::this_thread::yield();
             }
+            send_wait_ms += 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            // the exchange window: from the first copy's issue (after any wait)
+            if (st == AMG_OK && first && hipEventRecord(tx0(k), cs) != hipSuccess)
+               st = amg_set_error(AMG_ERR_HIP, "amg_dist_async_jacobi: event");
+            first = false;
             if (st == AMG_OK)
                st = link_send(D->ajac_links, 0, M.peers[i], sbuf + (size_t)q * SS + M.soff[i], M.scnt[i], cs);
          }
+         if (st == AMG_OK && first) AMG_HIP(hipEventRecord(tx0(k), cs));
          if (st != AMG_OK) break;
          AMG_HIP(hipEventRecord(tx1(k), cs));
          AMG_HIP(hipEventRecord(sent[q], cs));
@@ -1328,7 +1336,8 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
       }
       long long nrecv = 0;
       for (int i = 0; i < np; i++) nrecv += M.rcnt[i] > 0 ? 1 : 0;
-      D->ajac_stats.assign(8, 0.0);
+      D->ajac_stats.assign(9, 0.0);
+      D->ajac_stats[8] = sweeps > 0 ? send_wait_ms / sweeps : 0.0; // host flow-control wait per sweep
       D->ajac_stats[0] = cntk ? hid / cntk : 0.0;  // hidden fraction of the exchange
       D->ajac_stats[1] = cntk ? xs / cntk : 0.0;   // exchange window, ms per sweep
       D->ajac_stats[2] = cntk ? is / cntk : 0.0;   // interior product, ms per sweep

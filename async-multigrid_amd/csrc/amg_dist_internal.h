@@ -133,7 +133,7 @@ struct AsyncLevel {
 // (amg_link.cpp).  caps[k * R + src]: largest message (doubles) src sends me
 // in level group k, 0 = no channel (the sets are symmetric by construction)
 struct LinkSet;
-int link_create(amg_dist_hier *D, int K, const std::vector<long long> &caps, LinkSet **out);
+int link_create(amg_dist_hier *D, int K, const std::vector<long long> &caps, LinkSet **out, int nslots = 2);
 // collective: sequence numbers back to 0 before a solve; one_thread: every
 // level group driven by the calling thread (a deterministic schedule)
 int link_reset(LinkSet *L, bool one_thread);

@@ -54,9 +54,10 @@ using namespace amgd;
 
 namespace {
 
-constexpr int NS = 2;           // slots per channel
-constexpr size_t LINE = 64;     // one sequence word per cache line
-constexpr int MAX_EV = 2 * NS;  // events per channel direction in flight
+constexpr int NS_DEFAULT = 2;      // slots per channel (link_create's nslots)
+constexpr int NS_MAX = 8;
+constexpr size_t LINE = 64;        // one sequence word per cache line
+constexpr int MAX_EV = 2 * NS_MAX; // event ring per channel direction (at most 2 ns in flight)
 
 struct alignas(64) Word {
    std::atomic<unsigned long long> v;
@@ -130,6 +131,7 @@ struct amgd::LinkSet {
    double *slots = nullptr;        // my receive slot region
    std::vector<double *> ipc_open; // opened peer regions (closed at free)
    bool one_thread = false;        // every level group on one host thread: progress serves them all
+   int ns = NS_DEFAULT;            // slots per channel
    Chan &c(int k, int p) { return ch[(size_t)k * R + p]; }
    Word *abort_word(int r) { return ctrl[r] + ctrl_words(K, R) - 1; }
 };
@@ -228,11 +230,14 @@ long long host_id()
 
 // caps[k * R + src]: doubles of the largest message src sends me in level
 // group k (0: no channel); identical on the sending side by construction
-int amgd::link_create(amg_dist_hier *D, int K, const std::vector<long long> &caps, LinkSet **out)
+int amgd::link_create(amg_dist_hier *D, int K, const std::vector<long long> &caps, LinkSet **out, int nslots)
 {
    amg_ctx *c = D->ctx;
    const int R = c->xport->nranks, me = c->xport->rank;
+   AMG_ARG(nslots >= 1 && nslots <= NS_MAX, "link_create: %d slots per channel (1 .. %d)", nslots, NS_MAX);
+   const int NS = nslots;
    auto *L = new LinkSet();
+   L->ns = NS;
    L->D = D;
    L->K = K;
    L->R = R;
@@ -412,13 +417,14 @@ int amgd::link_reset(LinkSet *L, bool one_thread)
 int amgd::link_send(LinkSet *L, int k, int peer, const double *src, long long n, hipStream_t s)
 {
    Chan &c = L->c(k, peer);
+   const unsigned long long NS = (unsigned long long)L->ns, EV = 2 * NS;
    AMG_ARG(n <= c.scap && c.sslot, "link_send: %lld doubles to rank %d on level %d (capacity %lld)", n, peer, k,
            c.scap);
    const unsigned long long seq = c.sseq + 1;
    // the slot seq % NS is free once the peer acknowledged message seq - NS;
    // the event ring holds at most MAX_EV unpublished sends
    AMG_TRY(wait_for(L, k, peer, "send slot", [&] {
-      return (seq <= NS || c.s_acked->v.load(std::memory_order_acquire) >= seq - NS) && c.sseq - c.s_pub < MAX_EV;
+      return (seq <= NS || c.s_acked->v.load(std::memory_order_acquire) >= seq - NS) && c.sseq - c.s_pub < EV;
    }));
    launch_copy(s, src, c.sslot + (long long)(seq % NS) * c.scap, n);
    AMG_HIP(hipGetLastError());
@@ -430,10 +436,11 @@ int amgd::link_send(LinkSet *L, int k, int peer, const double *src, long long n,
 int amgd::link_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipStream_t s)
 {
    Chan &c = L->c(k, peer);
+   const unsigned long long NS = (unsigned long long)L->ns, EV = 2 * NS;
    AMG_ARG(n <= c.rcap, "link_recv: %lld doubles from rank %d on level %d (capacity %lld)", n, peer, k, c.rcap);
    const unsigned long long seq = c.rseq + 1;
    AMG_TRY(wait_for(L, k, peer, "receive", [&] {
-      return c.r_arrived->v.load(std::memory_order_acquire) >= seq && c.rseq - c.r_pub < MAX_EV;
+      return c.r_arrived->v.load(std::memory_order_acquire) >= seq && c.rseq - c.r_pub < EV;
    }));
    launch_copy(s, c.rslot + (long long)(seq % NS) * c.rcap, dst, n);
    AMG_HIP(hipGetLastError());
@@ -445,11 +452,12 @@ int amgd::link_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipSt
 int amgd::link_try_recv(LinkSet *L, int k, int peer, double *dst, long long n, hipStream_t s, int *got)
 {
    Chan &c = L->c(k, peer);
+   const unsigned long long NS = (unsigned long long)L->ns, EV = 2 * NS;
    AMG_ARG(n <= c.rcap, "link_try_recv: %lld doubles from rank %d on level %d (capacity %lld)", n, peer, k, c.rcap);
    *got = 0;
    AMG_TRY(progress(L, k));
    const unsigned long long seq = c.rseq + 1;
-   if (c.r_arrived->v.load(std::memory_order_acquire) < seq || c.rseq - c.r_pub >= MAX_EV) {
+   if (c.r_arrived->v.load(std::memory_order_acquire) < seq || c.rseq - c.r_pub >= EV) {
       if (aborted(L, peer)) return amg_set_error(AMG_ERR_RCCL, "link: receive (level %d, rank %d <-> %d): aborted", k,
                                                  L->me, peer);
       return AMG_OK;
@@ -465,9 +473,10 @@ int amgd::link_try_recv(LinkSet *L, int k, int peer, double *dst, long long n, h
 int amgd::link_can_send(LinkSet *L, int k, int peer, int *ok)
 {
    Chan &c = L->c(k, peer);
+   const unsigned long long NS = (unsigned long long)L->ns, EV = 2 * NS;
    AMG_TRY(progress(L, k));
    const unsigned long long seq = c.sseq + 1;
-   *ok = (seq <= NS || c.s_acked->v.load(std::memory_order_acquire) >= seq - NS) && c.sseq - c.s_pub < MAX_EV;
+   *ok = (seq <= NS || c.s_acked->v.load(std::memory_order_acquire) >= seq - NS) && c.sseq - c.s_pub < EV;
    if (!*ok && aborted(L, peer))
       return amg_set_error(AMG_ERR_RCCL, "link: send (level %d, rank %d <-> %d): aborted", k, L->me, peer);
    return AMG_OK;

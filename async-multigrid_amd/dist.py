@@ -351,10 +351,10 @@ class DistHier:
 
     def async_jacobi_stats(self):
         """the last async_jacobi run: dict of the exchange overlap and delta accounting"""
-        st = np.zeros(8)
-        check(lib.amg_dist_async_jacobi_stats(self.h, _dp(st), 8))
+        st = np.zeros(9)
+        check(lib.amg_dist_async_jacobi_stats(self.h, _dp(st), 9))
         keys = ("hidden_fraction", "exchange_ms_per_sweep", "interior_ms_per_sweep", "on_time_fraction",
-                "late_deltas", "incremental_resnorm", "true_resnorm", "device_links")
+                "late_deltas", "incremental_resnorm", "true_resnorm", "device_links", "send_wait_ms_per_sweep")
         return dict(zip(keys, st.tolist()))
 
     def async_sps(self, f_local, sweeps):

@@ -675,7 +675,9 @@ int amg_dist_async_level_ms(const amg_dist_hier *D, double *ms);
  * (device-resident channels; -1 otherwise); [4] deltas applied in a later
  * sweep; [5] ||r|| as kept incrementally (global); [6] ||f - A x|| (global):
  * equal to rounding when every delta was applied exactly once; [7] 1 when the
- * deltas went through the device-resident channels (amg_link.cpp) */
+ * deltas went through the device-resident channels (amg_link.cpp); [8] host
+ * ms per sweep a send waited for its channel slot (flow control; the
+ * exchange window [1] starts at the first copy's issue, after that wait) */
 int amg_dist_async_jacobi_stats(const amg_dist_hier *D, double *stats, int n);
 /* AMG_SCHED_TIMED on the distributed solve: level k's time per correction
  * (every rank passes the same values, so every rank issues the same order) */

@@ -675,7 +675,8 @@ def test_dist_async_jacobi_512(amg, ctx):
     for q, (rel, st) in enumerate(res):
         print(f"512^3 async Jacobi rank {q}: relres {rel:.6e}, hidden {st['hidden_fraction']:.3f}, exchange "
               f"{st['exchange_ms_per_sweep']:.3f} ms, interior {st['interior_ms_per_sweep']:.3f} ms, on time "
-              f"{st['on_time_fraction']:.3f}, late {st['late_deltas']:.0f}")
+              f"{st['on_time_fraction']:.3f}, late {st['late_deltas']:.0f}, send wait "
+              f"{st['send_wait_ms_per_sweep']:.3f} ms/sweep")
         assert st["device_links"] == 1.0
         assert abs(st["incremental_resnorm"] - st["true_resnorm"]) <= 1e-9 * st["true_resnorm"], st
     # Jacobi on the 7-pt Laplacian: the smooth residual decays slowly, but it decays
