@@ -3186,13 +3186,40 @@ struct EpiFsub {
    }
 };
 
+// Division by a uniform diagonal d with its reciprocal y = RN(1/d) known:
+// q0 = RN(x y), the exact remainder r = x - q0 d (fma), q1 = RN(q0 + r y) --
+// the correctly rounded x / d, the same bits as the division, for x in the
+// normal range (Markstein's correction step; host-checked divisor: fast_div_of;
+// brute-forced against x / d over 10^9 operands incl. near-midpoint ones).
+// A wave takes it only when every lane's divisor is d and operand in range
+// (+0 included, -0 not: q1 would be +0), else the division itself.
+__device__ __forceinline__ double div_rcp(double x, double d, double y)
+{
+   const double q0 = x * y;
+   const double r = __builtin_fma(-q0, d, x);
+   return __builtin_fma(r, y, q0);
+}
+__device__ __forceinline__ bool div_rcp_ok(double x)
+{
+   const double ax = fabs(x);
+   return (ax >= 0x1p-960 && ax < 0x1p+1000) || __double_as_longlong(x) == 0;
+}
+__device__ __forceinline__ v2d jac_div2(v2d num, v2d a, double dq, double rq)
+{
+   const bool ok = a.x == dq && a.y == dq && div_rcp_ok(num.x) && div_rcp_ok(num.y);
+   if (dq != 0.0 && __all(ok)) return v2d{div_rcp(num.x, dq, rq), div_rcp(num.y, dq, rq)};
+   return v2d{num.x / a.x, num.y / a.y};
+}
+
 // Jacobi sweep epilogue (SMEM_Smooth.cpp:35-45): res = f - sum; u_new = u + w*res/a
+// (dq, rq: a uniform diagonal and its reciprocal, jac_div2; dq = 0: off)
 struct EpiJacobi {
    const double *f;
    const double *x;
    double *out;
    double omega;
    int nt = 0;
+   double dq = 0.0, rq = 0.0;
    __device__ __forceinline__ double init(int i) const { return f[i]; }
    __device__ __forceinline__ double pf(int i) const { return x[i]; }
    __device__ __forceinline__ double finish(int i, double res, double a, double xi) const
@@ -3205,8 +3232,8 @@ struct EpiJacobi {
    __device__ __forceinline__ v2d pf2(int i) const { return *reinterpret_cast<const v2du *>(x + i); }
    __device__ __forceinline__ v2d finish2(int i, v2d res, v2d a, v2d xi) const
    {
-      const v2d v{(a.x != 0.0) ? xi.x + omega * res.x / a.x : xi.x,
-                  (a.y != 0.0) ? xi.y + omega * res.y / a.y : xi.y};
+      const v2d q = jac_div2(v2d{omega * res.x, omega * res.y}, a, dq, rq);
+      const v2d v{(a.x != 0.0) ? xi.x + q.x : xi.x, (a.y != 0.0) ? xi.y + q.y : xi.y};
       st2(out + i, v, nt);
       return v;
    }
@@ -3250,6 +3277,7 @@ struct EpiResJacobi {
    double *unext;
    double omega;
    int nt = 0;
+   double dq = 0.0, rq = 0.0;
    __device__ __forceinline__ double init(int i) const { return f[i]; }
    __device__ __forceinline__ double pf(int i) const { return x[i]; }
    __device__ __forceinline__ double finish(int i, double res, double a, double xi) const
@@ -3268,8 +3296,8 @@ struct EpiResJacobi {
          const v2d l = *reinterpret_cast<const v2du *>(l1 + i);
          v = v2d{xi.x + res.x / l.x, xi.y + res.y / l.y};
       } else {
-         v = v2d{(a.x != 0.0) ? xi.x + omega * res.x / a.x : xi.x,
-                 (a.y != 0.0) ? xi.y + omega * res.y / a.y : xi.y};
+         const v2d q = jac_div2(v2d{omega * res.x, omega * res.y}, a, dq, rq);
+         v = v2d{(a.x != 0.0) ? xi.x + q.x : xi.x, (a.y != 0.0) ? xi.y + q.y : xi.y};
       }
       st2(unext + i, v, nt);
       return res;
@@ -3724,6 +3752,29 @@ void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, c
          <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, partials);
 }
 
+// a marched operator's uniform diagonal d whose reciprocal divides exactly
+// (div_rcp): normal, finite, the odd part of its significand below 2^30 (the
+// distance of x / d from a rounding midpoint then dwarfs the correction's
+// error); AMG_FAST_DIV=0: off
+static bool fast_div_of(const amg_mat *A, double *d, double *y)
+{
+   static const bool on = [] {
+      const char *v = std::getenv("AMG_FAST_DIV");
+      return !v || std::atoi(v) != 0;
+   }();
+   if (!on || !A->mp_uni) return false;
+   const double a = A->mp_val[0];
+   if (!std::isnormal(a)) return false;
+   int e = 0;
+   const double m = std::frexp(std::fabs(a), &e); // [0.5, 1)
+   unsigned long long sig = (unsigned long long)std::ldexp(m, 53);
+   while (sig && !(sig & 1)) sig >>= 1;
+   if (sig >= (1ull << 30)) return false;
+   *d = a;
+   *y = 1.0 / a;
+   return true;
+}
+
 void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double *x,
                   const double *l1, double omega, double *out, int rb, int re)
 {
@@ -3737,8 +3788,11 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
    } else if (A->didx) {
       if (l1)
          launch_dc_op<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out}, nullptr, nb);
-      else
-         launch_dc_op<1, true>(s, A, x, rb, re, EpiJacobi{f, x, out, omega, stream_hint(A)}, nullptr, nb);
+      else {
+         EpiJacobi e{f, x, out, omega, stream_hint(A)};
+         fast_div_of(A, &e.dq, &e.rq);
+         launch_dc_op<1, true>(s, A, x, rb, re, e, nullptr, nb);
+      }
    } else if (long_rows(A)) {
       if (l1)
          launch_long<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out});
@@ -3774,6 +3828,7 @@ void residual_jacobi(hipStream_t s, const amg_mat *A, const double *f, const dou
    const int nb = tile_blocks(rb, re);
    EpiResJacobi e{f, x, l1, r, unext, omega};
    if (A->didx) e.nt = stream_hint(A);
+   fast_div_of(A, &e.dq, &e.rq);
    if (use_bsr3(A, rb, re, partials)) {
       if (l1)
          launch_bsr3<1, false>(s, A, x, rb, re, e);
