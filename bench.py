@@ -162,6 +162,10 @@ def host_info():
             "OMP_PLACES": os.environ.get("OMP_PLACES")}
 
 
+# taken at import, before the oracle's OpenMP runtime binds this thread (OMP_PROC_BIND)
+HOST_INFO = host_info()
+
+
 def seq_baseline(amg, args):
     """Config 1 (SEQ_AMG 64^3, sync Jacobi V-cycle on CPU): the oracle's loops on
     ONE thread (or_set_threads(1): the SEQ configuration of BASELINE.md Sec.3)
@@ -317,7 +321,7 @@ def cpu_baseline(gen, amg, f, args):
     return ({"value": k / secs, "unit": "V-cycle iters/s", "cores": threads, "kind": "port",
              "sample": f"{k} outer iterations (V(1,1) Jacobi + residual + norm) of the same "
                        f"{args.n}^3 solve, oracle/amg_oracle.c OpenMP, {threads} threads",
-             "seconds": secs, "host": host_info()}, u, hist[-1] / hist[0])
+             "seconds": secs, "host": HOST_INFO}, u, hist[-1] / hist[0])
 
 
 def check_parity(u_par, u_cpu, rel_cpu, cycles):
