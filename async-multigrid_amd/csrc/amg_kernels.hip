@@ -3762,8 +3762,10 @@ static bool fast_div_of(const amg_mat *A, double *d, double *y)
       const char *v = std::getenv("AMG_FAST_DIV");
       return !v || std::atoi(v) != 0;
    }();
-   if (!on || !A->mp_uni) return false;
-   const double a = A->mp_val[0];
+   // the uniform diagonal, or the 27-pt march's dominant pattern's (the
+   // epilogue checks every wave's divisors against it)
+   if (!on || !(A->mp_uni || (A->mz27 && A->mz_dom >= 0))) return false;
+   const double a = A->mp_uni ? A->mp_val[0] : A->mz_domval[0];
    if (!std::isnormal(a)) return false;
    int e = 0;
    const double m = std::frexp(std::fabs(a), &e); // [0.5, 1)
