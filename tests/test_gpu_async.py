@@ -20,6 +20,7 @@ import numpy as np
 import pytest
 
 from async_band import blocks64, in_band, oracle_async_band, race_tables, replay_check, times_of
+from test_gpu_kernels import assert_bitwise
 from test_gpu_solve import hierarchy, gpu_hier, oracle_opts
 
 pytestmark = pytest.mark.gpu
@@ -373,6 +374,53 @@ def test_composed_transfers_zero_sweeps_bitwise(amg, oracle, ctx, setup, pre, po
     nd = int(np.count_nonzero(u.view(np.uint64) != uo.view(np.uint64)))
     print(f"composed pre {pre} post {post} {mode}: differing entries {nd}")
     assert nd == 0
+
+
+@pytest.mark.parametrize("hybrid", [0, 1], ids=["jacobi", "hybrid-fold"])
+def test_update_windows(amg, oracle, ctx, setup, hybrid):
+    """the device-clock execution windows of a free race's update kernels
+    (amg_async_update_windows; the hybrid case's level 0 folds its correction
+    into the last JGS sweep, which stamps it): one per correction, start <
+    end, a level's windows in order without overlap (its stream runs them one
+    after another), every window inside the solve; replayed in their end order
+    (AMG_SCHED_TIMED with the ends) the device's iterate is the oracle's
+    replay's bit for bit"""
+    L, mult, afacx, f = setup
+    host = mult
+    kw = dict(solver=amg.AMG_ASYNC_MULTADD, smoother=amg.AMG_HYBRID_JGS if hybrid else amg.AMG_JACOBI,
+              smooth_weight=W, num_cycles=N, tol=0.0)
+    opts = amg.default_opts(**kw)
+    blocks = blocks64(host) if hybrid else None
+    H, _ = gpu_hier(amg, ctx, host, opts)
+    _, rel, cnt = H.async_solve(f)
+    w0, w1 = H.async_update_windows()
+    H.free()
+    lo = min(float(x[0]) for x in w0 if len(x))
+    for k in range(L - 1):
+        s_, e_ = np.asarray(w0[k]), np.asarray(w1[k])
+        assert len(s_) == len(e_) == cnt[k] == N, (k, len(s_), len(e_), cnt[k])
+        assert np.all(np.isfinite(s_)) and np.all(np.isfinite(e_)), k
+        assert np.all(s_ < e_), k
+        assert np.all(s_[1:] >= e_[:-1]), k
+        print(f"level {k}: windows {1e3 * np.mean(e_ - s_):.1f} us on average, first at {1e3 * (s_[0] - lo):.1f} us")
+    times = [np.asarray(w1[k]) - lo for k in range(L - 1)]
+    times.append(times[-1].copy())  # the reference's idle coarsest group
+    opts = amg.default_opts(async_schedule=4, **kw)
+    H, _ = gpu_hier(amg, ctx, host, opts)
+    H.set_async_times(times)
+    u, rel, cnt = H.async_solve(f)
+    H.free()
+    oracle.set_async_times(times)
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
+    if blocks is not None:
+        for lev, blk in blocks.items():
+            OH.set_blocks(lev, blk)
+    oracle.lib().or_set_async_schedule(4)
+    try:
+        uo, relo, cnto = OH.async_add(f, [1] * L)
+    finally:
+        oracle.lib().or_set_async_schedule(0)
+    assert_bitwise(u, uo, "windows replay")
 
 
 @pytest.mark.parametrize("case", [CASES[1], CASES[4], CASES[7]], ids=["jacobi-full-res", "jacobi-semi-gres",
