@@ -388,7 +388,7 @@ def test_update_windows(amg, oracle, ctx, setup, hybrid):
     L, mult, afacx, f = setup
     host = mult
     kw = dict(solver=amg.AMG_ASYNC_MULTADD, smoother=amg.AMG_HYBRID_JGS if hybrid else amg.AMG_JACOBI,
-              smooth_weight=W, num_cycles=N, tol=0.0)
+              smooth_weight=W, num_cycles=N, tol=0.0, num_threads=0, jgs_block_rows=64)
     opts = amg.default_opts(**kw)
     blocks = blocks64(host) if hybrid else None
     H, _ = gpu_hier(amg, ctx, host, opts)
