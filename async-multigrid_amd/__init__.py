@@ -135,6 +135,10 @@ class Context:
         """Small-level hybrid JGS form (bit-identical): 2 one batch per row (default), 1 wave per block, 0 as large."""
         check(lib.amg_set_jgs_small(self.h, int(form)))
 
+    def set_jgs_fold(self, enable):
+        """FULL_ASYNC: level 0's correction folded into the last hybrid-JGS sweep (bit-identical; off)."""
+        check(lib.amg_set_jgs_fold(self.h, int(enable)))
+
     def set_jgs_wave(self, enable):
         """Hybrid JGS kernel form, all bit-identical: 1 (default) 8 lanes per block,
         8 blocks per wave; 2 one wave per block; 0 one lane per block; 3 an LDS tile of 64

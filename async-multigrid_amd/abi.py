@@ -140,6 +140,7 @@ PROTOTYPES = {
     "amg_set_fuse_prolong": (_i, [_p, _i]),
     "amg_set_jgs_wave": (_i, [_p, _i]),
     "amg_set_jgs_small": (_i, [_p, _i]),
+    "amg_set_jgs_fold": (_i, [_p, _i]),
     "amg_set_march_lines": (_i, [_p, _i]),
     "amg_set_march_lines_gemv": (_i, [_p, _i]),
     "amg_set_march_tuning": (_i, [_p, _i, _i, _i, _i]),

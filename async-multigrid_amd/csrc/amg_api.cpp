@@ -153,6 +153,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::max(0, std::min(7, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_SMALL")) c->jgs_small = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_WAVE")) c->jgs_wave = std::max(0, std::min(3, std::atoi(v)));
+   if (const char *v = std::getenv("AMG_JGS_FOLD")) c->jgs_fold = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_BSR3_XS")) c->bsr3_xs = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ_EDGE")) c->mz_edge = std::atoi(v) != 0;
@@ -901,6 +902,14 @@ extern "C" int amg_set_jgs_small(amg_ctx *c, int form)
    AMG_ARG(c, "amg_set_jgs_small: null context");
    c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->jgs_small = std::max(0, std::min(2, form));
+   return AMG_OK;
+}
+
+extern "C" int amg_set_jgs_fold(amg_ctx *c, int enable)
+{
+   AMG_ARG(c, "amg_set_jgs_fold: null context");
+   c->knob_gen++;
+   c->jgs_fold = enable != 0;
    return AMG_OK;
 }
 

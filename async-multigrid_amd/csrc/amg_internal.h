@@ -237,6 +237,7 @@ struct amg_ctx {
    int rr_zc = 0;          // coarse planes per chunk of the fused residual + restriction (0: mz_zc / 2)
    int jgs_wave = 1;       // hybrid JGS form: 1 8 blocks per wave, 2 one wave per block, 0 one lane per block, 3 LDS tile
    int jgs_small = 2;      // small levels' hybrid JGS form (amg_set_jgs_small)
+   int jgs_fold = 0;       // FULL_ASYNC level-0 correction folded into the last JGS sweep (amg_set_jgs_fold)
 };
 
 struct amg_mat {

@@ -922,11 +922,7 @@ static bool add_level_correction(amg_hier *H, hipStream_t s, int k, const double
       amgk::vset(s, a.e[k], 0.0, 0, H->lv[k].n);
       // level 0's correction is its own smoothing: the FULL_ASYNC update
       // folded into the last sweep where the smoother's kernel allows it
-      static const bool fold = [] {
-         const char *v = std::getenv("AMG_JGS_FOLD");
-         return !v || std::atoi(v) != 0;
-      }();
-      const bool ap = k == 0 && apply == 1 && fold;
+      const bool ap = k == 0 && apply == 1 && H->ctx->jgs_fold;
       if (smooth_all_levels(H, s, k, rl(k), a.e[k], a.u_prev, a.y, a.scratch, o.num_fine_smooth_sweeps, k,
                             ap ? u : nullptr, ap ? u_priv : nullptr))
          return true;

@@ -339,6 +339,12 @@ int amg_set_jgs_wave(amg_ctx *ctx, int enable);
  * AMG_JGS_SMALL), all bit-identical: 2 (default) the whole row's loads in one
  * batch, 1 one wave per block, 0 as the large levels */
 int amg_set_jgs_small(amg_ctx *ctx, int form);
+/* FULL_ASYNC / READ_SOL: level 0's correction added into the shared iterate by
+ * the last hybrid-JGS sweep's write-out itself (jgs forms 1 and 3; env
+ * AMG_JGS_FOLD), in place of the separate update pass after the smoothing
+ * (SMEM_Async_AMG.cpp:284-301); bit-identical under a schedule, measured
+ * neutral; default off */
+int amg_set_jgs_fold(amg_ctx *ctx, int enable);
 int amg_hybrid_jgs(amg_ctx *ctx, const amg_mat *A, const amg_vec *f, amg_vec *u, amg_vec *u_prev,
                    const int *blk, int nblk, const amg_vec *diag_scale, double weight, int sweeps,
                    int zero_first, int reverse);

@@ -391,6 +391,7 @@ def test_update_windows(amg, oracle, ctx, setup, hybrid):
               smooth_weight=W, num_cycles=N, tol=0.0, num_threads=0, jgs_block_rows=64)
     opts = amg.default_opts(**kw)
     blocks = blocks64(host) if hybrid else None
+    ctx.set_jgs_fold(hybrid)
     H, _ = gpu_hier(amg, ctx, host, opts)
     _, rel, cnt = H.async_solve(f)
     w0, w1 = H.async_update_windows()
@@ -410,6 +411,7 @@ def test_update_windows(amg, oracle, ctx, setup, hybrid):
     H.set_async_times(times)
     u, rel, cnt = H.async_solve(f)
     H.free()
+    ctx.set_jgs_fold(0)
     oracle.set_async_times(times)
     OH = oracle.Hier(host["A"], host["P"], host["R"], oracle_opts(oracle, opts))
     if blocks is not None:
