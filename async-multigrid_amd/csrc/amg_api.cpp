@@ -800,15 +800,21 @@ int amg_mat_finish(amg_mat *A)
    AMG_HIP(hipGetLastError());
    {
       int *d = nullptr;
-      AMG_HIP(hipMalloc(&d, sizeof(int)));
-      AMG_HIP(hipMemsetAsync(d, 0, sizeof(int), A->ctx->stream));
+      AMG_HIP(hipMalloc(&d, 2 * sizeof(int)));
+      AMG_HIP(hipMemsetAsync(d, 0, 2 * sizeof(int), A->ctx->stream));
       amgk::row_max(A->ctx->stream, A, d);
-      int h = 0;
-      hipError_t e = hipMemcpyAsync(&h, d, sizeof(int), hipMemcpyDeviceToHost, A->ctx->stream);
+      amgk::diag_uniform(A->ctx->stream, A, d + 1);
+      int h[2] = {0, 0};
+      double d0 = 0.0;
+      hipError_t e = hipMemcpyAsync(h, d, 2 * sizeof(int), hipMemcpyDeviceToHost, A->ctx->stream);
+      if (e == hipSuccess && A->nrows > 0)
+         e = hipMemcpyAsync(&d0, A->diag, sizeof(double), hipMemcpyDeviceToHost, A->ctx->stream);
       if (e == hipSuccess) e = hipStreamSynchronize(A->ctx->stream);
       hipFree(d);
       if (e != hipSuccess) return amg_set_error(AMG_ERR_HIP, "amg_mat_finish: %s", hipGetErrorString(e));
-      A->maxrow = h;
+      A->maxrow = h[0];
+      A->diag_uni = A->nrows > 0 && h[1] == 0;
+      A->diag_u = d0;
    }
    if (A->ctx->value_index && A->nnz > 0) AMG_TRY(build_value_index(A));
    if (A->ctx->dict_index && A->vidx) AMG_TRY(build_dict_index(A));

@@ -298,6 +298,9 @@ struct amg_mat {
    unsigned short *pdelta = nullptr;
    int mp_J = 0; // master length (0: not master-coded)
    int mp_uni = 0;
+   // every row's diagonal (A->diag) is the same value diag_u (amg_mat_finish)
+   int diag_uni = 0;
+   double diag_u = 0.0;
    int mp_off[AMG_MP_MAXJ] = {};
    double mp_val[AMG_MP_MAXJ] = {};
    unsigned long long *mpmask = nullptr;
@@ -492,6 +495,8 @@ void vadd_into(hipStream_t s, const double *r, double *u, int rb, int re, int ov
 void l1_norms(hipStream_t s, const amg_mat *A, double *out);
 void a_diag(hipStream_t s, const double *diag, double omega, double *out, int n);
 void extract_diag(hipStream_t s, const amg_mat *A);
+// *d_flag = 1 unless every diag[i] has diag[0]'s bits
+void diag_uniform(hipStream_t s, const amg_mat *A, int *d_flag);
 // symmetric Jacobi pieces (SMEM_Smooth.cpp:665,682-683 / SEQ_Smooth.cpp:136,144-145)
 void sym_scale(hipStream_t s, const double *diag, const double *l1, double omega, double *r,
                int rb, int re, int seq);

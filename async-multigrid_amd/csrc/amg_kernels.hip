@@ -3211,6 +3211,13 @@ __device__ __forceinline__ v2d jac_div2(v2d num, v2d a, double dq, double rq)
    return v2d{num.x / a.x, num.y / a.y};
 }
 
+__device__ __forceinline__ double jac_div1(double num, double a, double dq, double rq)
+{
+   const bool ok = a == dq && div_rcp_ok(num);
+   if (dq != 0.0 && __all(ok)) return div_rcp(num, dq, rq);
+   return num / a;
+}
+
 // Jacobi sweep epilogue (SMEM_Smooth.cpp:35-45): res = f - sum; u_new = u + w*res/a
 // (dq, rq: a uniform diagonal and its reciprocal, jac_div2; dq = 0: off)
 struct EpiJacobi {
@@ -3224,7 +3231,8 @@ struct EpiJacobi {
    __device__ __forceinline__ double pf(int i) const { return x[i]; }
    __device__ __forceinline__ double finish(int i, double res, double a, double xi) const
    {
-      const double v = (a != 0.0) ? xi + omega * res / a : xi;
+      const double q = jac_div1(omega * res, a, dq, rq);
+      const double v = (a != 0.0) ? xi + q : xi;
       out[i] = v;
       return v;
    }
@@ -3283,7 +3291,12 @@ struct EpiResJacobi {
    __device__ __forceinline__ double finish(int i, double res, double a, double xi) const
    {
       if (r) r[i] = res;
-      unext[i] = l1 ? xi + res / l1[i] : ((a != 0.0) ? xi + omega * res / a : xi);
+      if (l1) {
+         unext[i] = xi + res / l1[i];
+      } else {
+         const double q = jac_div1(omega * res, a, dq, rq);
+         unext[i] = (a != 0.0) ? xi + q : xi;
+      }
       return res;
    }
    __device__ __forceinline__ v2d init2(int i) const { return ld2nt(f + i, nt); }
@@ -3764,8 +3777,8 @@ static bool fast_div_of(const amg_mat *A, double *d, double *y)
    }();
    // the uniform diagonal, or the 27-pt march's dominant pattern's (the
    // epilogue checks every wave's divisors against it)
-   if (!on || !(A->mp_uni || (A->mz27 && A->mz_dom >= 0))) return false;
-   const double a = A->mp_uni ? A->mp_val[0] : A->mz_domval[0];
+   if (!on || !(A->mp_uni || A->diag_uni || (A->mz27 && A->mz_dom >= 0))) return false;
+   const double a = A->mp_uni ? A->mp_val[0] : A->diag_uni ? A->diag_u : A->mz_domval[0];
    if (!std::isnormal(a)) return false;
    int e = 0;
    const double m = std::frexp(std::fabs(a), &e); // [0.5, 1)
@@ -3785,8 +3798,11 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
    if (use_bsr3(A, rb, re, nullptr)) {
       if (l1)
          launch_bsr3<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out});
-      else
-         launch_bsr3<1, true>(s, A, x, rb, re, EpiJacobi{f, x, out, omega});
+      else {
+         EpiJacobi e{f, x, out, omega};
+         fast_div_of(A, &e.dq, &e.rq);
+         launch_bsr3<1, true>(s, A, x, rb, re, e);
+      }
    } else if (A->didx) {
       if (l1)
          launch_dc_op<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out}, nullptr, nb);
@@ -3798,8 +3814,11 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
    } else if (long_rows(A)) {
       if (l1)
          launch_long<1, false>(s, A, x, rb, re, EpiL1Jacobi{f, x, l1, out});
-      else
-         launch_long<1, true>(s, A, x, rb, re, EpiJacobi{f, x, out, omega});
+      else {
+         EpiJacobi e{f, x, out, omega};
+         fast_div_of(A, &e.dq, &e.rq);
+         launch_long<1, true>(s, A, x, rb, re, e);
+      }
    } else if (l1) {
       EpiL1Jacobi e{f, x, l1, out};
       if (A->vidx)
@@ -3810,6 +3829,7 @@ void jacobi_sweep(hipStream_t s, const amg_mat *A, const double *f, const double
             <<<nb, 256, 0, s>>>(A->rowptr, A->col, A->val, x, rb, re, e, nullptr);
    } else {
       EpiJacobi e{f, x, out, omega};
+      fast_div_of(A, &e.dq, &e.rq);
       if (A->vidx && short_rows(A))
          csr_tile_kernel<ShortCfg, 1, true, EpiJacobi, true><<<nb, 256, 0, s>>>(
             A->rowptr, A->col, A->val, x, rb, re, e, nullptr, A->vidx, A->vtab);
@@ -5481,6 +5501,19 @@ void extract_diag(hipStream_t s, const amg_mat *A)
 {
    if (A->nrows > 0)
       extract_diag_k<<<ew_blocks(A->nrows), 256, 0, s>>>(A->rowptr, A->val, A->diag, A->nrows);
+}
+
+// *flag = 1 when some diag[i] differs from diag[0] in its bits (the writers
+// all store 1)
+__global__ void diag_uniform_k(const double *__restrict__ diag, int n, int *flag)
+{
+   const long long d0 = __double_as_longlong(diag[0]);
+   EW_LOOP(i, 1, n)
+   if (__double_as_longlong(diag[i]) != d0) *flag = 1;
+}
+void diag_uniform(hipStream_t s, const amg_mat *A, int *d_flag)
+{
+   if (A->nrows > 1) diag_uniform_k<<<ew_blocks(A->nrows), 256, 0, s>>>(A->diag, A->nrows, d_flag);
 }
 
 // symmetric Jacobi scale step: SMEM r *= w/a (SMEM_Smooth.cpp:665); SEQ adds the
