@@ -321,7 +321,8 @@ def cpu_baseline(gen, amg, f, args):
     return ({"value": k / secs, "unit": "V-cycle iters/s", "cores": threads, "kind": "port",
              "sample": f"{k} outer iterations (V(1,1) Jacobi + residual + norm) of the same "
                        f"{args.n}^3 solve, oracle/amg_oracle.c OpenMP, {threads} threads",
-             "seconds": secs, "host": HOST_INFO}, u, hist[-1] / hist[0])
+             "seconds": secs, "host": dict(HOST_INFO, **{k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND",
+                                                                                 "OMP_PLACES")})}, u, hist[-1] / hist[0])
 
 
 def check_parity(u_par, u_cpu, rel_cpu, cycles):
