@@ -3576,7 +3576,7 @@ Gemv gemv_mode(double alpha, double beta)
 // identity rows of fixed dofs) run the CSR row loop.  Per block row the
 // value-indexed form streams 27 x (12 + 4) bytes against 81 x 5 for
 // value-indexed CSR.
-template <int NEG, bool NEED_DIAG, class Epi, bool VI, bool XS = false>
+template <int NEG, bool NEED_DIAG, class Epi, bool VI, bool XS = false, int U = 9>
 __global__ __launch_bounds__(256) void bsr3_kernel(const long long *__restrict__ soff, const int *__restrict__ bcol,
                                                    const int *__restrict__ bdiag,
                                                    const unsigned char *__restrict__ bcnt,
@@ -3627,7 +3627,6 @@ __global__ __launch_bounds__(256) void bsr3_kernel(const long long *__restrict__
       madd(a, xi); // the diagonal first
       // blocks in chunks of U, the wave's loads of block k contiguous; every
       // load of a chunk in flight before its products are added in order
-      constexpr int U = 9;
       for (int kc = 0; kc < cnt; kc += U) {
          int jj[U];
          double vv[U][3];
@@ -3678,10 +3677,21 @@ static void launch_bsr3(hipStream_t s, const amg_mat *A, const double *x, int rb
    const int t0 = rb / 3, t1 = re / 3;
    const int nsl = (t1 - t0 + 20) / 21;
    const int nb = (nsl + 3) / 4;
-   // ctx->bsr3_xs: the node's x shared across the block row's three lanes
+   // ctx->bsr3_xs: the node's x shared across the block row's three lanes;
+   // AMG_BSR3_U: blocks per batch of in-flight loads (9, 14 or 27)
    const bool xs = A->ctx->bsr3_xs != 0;
+   static const int ub = [] {
+      const char *v = std::getenv("AMG_BSR3_U");
+      return v ? std::atoi(v) : 9;
+   }();
    if (A->bsr3 == 1) {
-      if (xs)
+      if (xs && ub == 27)
+         bsr3_kernel<NEG, NEED_DIAG, Epi, true, true, 27><<<nb, 256, 0, s>>>(
+            A->soff, A->bcol, A->bdiag, A->bmode, A->bvi, nullptr, A->vtab, A->rowptr, A->col, A->val, x, t0, t1, e);
+      else if (xs && ub == 14)
+         bsr3_kernel<NEG, NEED_DIAG, Epi, true, true, 14><<<nb, 256, 0, s>>>(
+            A->soff, A->bcol, A->bdiag, A->bmode, A->bvi, nullptr, A->vtab, A->rowptr, A->col, A->val, x, t0, t1, e);
+      else if (xs)
          bsr3_kernel<NEG, NEED_DIAG, Epi, true, true><<<nb, 256, 0, s>>>(
             A->soff, A->bcol, A->bdiag, A->bmode, A->bvi, nullptr, A->vtab, A->rowptr, A->col, A->val, x, t0, t1, e);
       else
