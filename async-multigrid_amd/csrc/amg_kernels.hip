@@ -3678,14 +3678,20 @@ static void launch_bsr3(hipStream_t s, const amg_mat *A, const double *x, int rb
    const int nsl = (t1 - t0 + 20) / 21;
    const int nb = (nsl + 3) / 4;
    // ctx->bsr3_xs: the node's x shared across the block row's three lanes;
-   // AMG_BSR3_U: blocks per batch of in-flight loads (4, 6, 9, 14 or 27)
+   // AMG_BSR3_U: blocks per batch of in-flight loads (2, 3, 4, 6, 9, 14 or 27)
    const bool xs = A->ctx->bsr3_xs != 0;
    static const int ub = [] {
       const char *v = std::getenv("AMG_BSR3_U");
       return v ? std::atoi(v) : 9;
    }();
    if (A->bsr3 == 1) {
-      if (xs && ub == 6)
+      if (xs && ub == 3)
+         bsr3_kernel<NEG, NEED_DIAG, Epi, true, true, 3><<<nb, 256, 0, s>>>(
+            A->soff, A->bcol, A->bdiag, A->bmode, A->bvi, nullptr, A->vtab, A->rowptr, A->col, A->val, x, t0, t1, e);
+      else if (xs && ub == 2)
+         bsr3_kernel<NEG, NEED_DIAG, Epi, true, true, 2><<<nb, 256, 0, s>>>(
+            A->soff, A->bcol, A->bdiag, A->bmode, A->bvi, nullptr, A->vtab, A->rowptr, A->col, A->val, x, t0, t1, e);
+      else if (xs && ub == 6)
          bsr3_kernel<NEG, NEED_DIAG, Epi, true, true, 6><<<nb, 256, 0, s>>>(
             A->soff, A->bcol, A->bdiag, A->bmode, A->bvi, nullptr, A->vtab, A->rowptr, A->col, A->val, x, t0, t1, e);
       else if (xs && ub == 4)
