@@ -1019,8 +1019,8 @@ __device__ __forceinline__ v2d mz_acc7(v2d acc, const v2d (&xv)[7], unsigned lon
 // k - 1, k, k + 1, so the +-S operands of its inner lines come from registers
 // and only the two halo lines are loaded per plane (2 / NLN line loads per line
 // instead of 2).  NLN > 1 needs S % 512 == 0 and NLN | P / S.
-template <int NEG, bool NEED_DIAG, class Epi, bool UNI, int NLN = 1, int PF = 1>
-__global__ __launch_bounds__(256) void csr_mz_kernel(
+template <int NEG, bool NEED_DIAG, class Epi, bool UNI, int NLN = 1, int PF = 1, int WPE = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) void csr_mz_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ x, int P, int S, int nz, int zc,
    int npb, int xcd, Epi epi, double *__restrict__ partials, int kb, int ke)
@@ -1214,9 +1214,23 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
    // where the plane splits into line groups; ctx->mz_pf: prefetch distance
    const int lines = std::is_same<Epi, EpiGemv>::value ? A->ctx->mz_lines_gemv : A->ctx->mz_lines;
    const bool pf2 = A->ctx->mz_pf == 2;
+   // AMG_MZ_WPE=8: registers capped for 8 waves per SIMD (one line, prefetch 1)
+   static const int wpe = [] {
+      const char *v = std::getenv("AMG_MZ_WPE");
+      return v ? std::atoi(v) : 0;
+   }();
    auto go = [&](auto uni, auto nln, auto pf) {
       constexpr bool U = decltype(uni)::value;
       constexpr int N = decltype(nln)::value, F = decltype(pf)::value;
+      if constexpr (N == 1 && F == 1) {
+         if (wpe == 8) {
+            const void *fn8 = (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F, 8>;
+            const int npb = P / 512, zc = occ_chunk(A, nk, npb, A->ctx->mz_occ, fn8), nch = (nk + zc - 1) / zc;
+            csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F, 8><<<npb * nch, 256, 0, s>>>(
+               A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
+            return;
+         }
+      }
       const void *fn = (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F>;
       const int npb = P / (512 * N), zc = occ_chunk(A, nk, npb, A->ctx->mz_occ, fn), nch = (nk + zc - 1) / zc;
       csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F><<<npb * nch, 256, 0, s>>>(
