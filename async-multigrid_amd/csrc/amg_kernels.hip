@@ -1233,7 +1233,13 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
       }
       const void *fn = (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F>;
       const int npb = P / (512 * N), zc = occ_chunk(A, nk, npb, A->ctx->mz_occ, fn), nch = (nk + zc - 1) / zc;
-      csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F><<<npb * nch, 256, 0, s>>>(
+      // AMG_MZ_LDSPAD: dynamic LDS bytes per workgroup that cap the resident
+      // workgroups per CU (an occupancy experiment; the kernel does not use them)
+      static const int ldspad = [] {
+         const char *v = std::getenv("AMG_MZ_LDSPAD");
+         return v ? std::atoi(v) : 0;
+      }();
+      csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F><<<npb * nch, 256, (size_t)ldspad, s>>>(
          A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
    };
    using T = std::true_type;
