@@ -4726,8 +4726,8 @@ __device__ __forceinline__ double dpp_shr1(double v)
    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-template <int C, int RMAX, bool VI, bool UNR = false>
-__global__ __launch_bounds__(64) void hybrid_jgs_grp_k(const int *__restrict__ rowptr, const int *__restrict__ col,
+template <int C, int RMAX, bool VI, bool UNR = false, int WPE = 0>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) void hybrid_jgs_grp_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                        const double *__restrict__ val,
                                                        const unsigned char *__restrict__ vidx,
                                                        const double *__restrict__ vtab, const double *__restrict__ f,
@@ -5313,7 +5313,20 @@ bool hybrid_jgs(hipStream_t s, const amg_mat *A, const double *f, double *u, con
    hybrid_jgs_grp_k<8, R, V><<<nwg, 64, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u, u_prev, d_blk, \
                                                 nblk, diag_scale, weight, zero, reverse, apply_u, apply_priv,     \
                                                 apply_u ? stamp : nullptr)
-      if (A->maxrow <= 8) {
+      // AMG_JGS_WPE=6 / 8: registers capped for 6 / 8 waves per SIMD (rows of <= 8 entries)
+      static const int jwpe = [] {
+         const char *v = std::getenv("AMG_JGS_WPE");
+         return v ? std::atoi(v) : 0;
+      }();
+      if (A->maxrow <= 8 && vi && jwpe == 8) {
+         hybrid_jgs_grp_k<8, 8, true, false, 8><<<nwg, 64, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u, u_prev,
+                                                                  d_blk, nblk, diag_scale, weight, zero, reverse, apply_u,
+                                                                  apply_priv, apply_u ? stamp : nullptr);
+      } else if (A->maxrow <= 8 && vi && jwpe == 6) {
+         hybrid_jgs_grp_k<8, 8, true, false, 6><<<nwg, 64, 0, s>>>(A->rowptr, A->col, A->val, A->vidx, A->vtab, f, u, u_prev,
+                                                                  d_blk, nblk, diag_scale, weight, zero, reverse, apply_u,
+                                                                  apply_priv, apply_u ? stamp : nullptr);
+      } else if (A->maxrow <= 8) {
          if (vi) JGS_GRP(8, true);
          else JGS_GRP(8, false);
       } else {
