@@ -674,14 +674,14 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    // a deterministic schedule runs every level on one stream and one host
    // thread, in the schedule's order; free: a stream and a host thread per level
    for (int k = 0; k < active; k++) D->al[k].s = c->level_streams[sched != AMG_SCHED_FREE ? 0 : k];
+   // the free race's update windows on the device clock (amg_dist_async_update_windows)
+   if (sched == AMG_SCHED_FREE && D->corr.stamps_begin(c->stream, D->L, std::max(1, D->o.num_cycles)))
+      return amg_set_error(AMG_ERR_OOM, "amg_dist_async_solve: update-window stamps");
    hipEvent_t ready, t_start;
    std::vector<hipEvent_t> t_end(active);
    AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
    AMG_HIP(hipEventCreate(&t_start));
    for (auto &e : t_end) AMG_HIP(hipEventCreate(&e));
-   // the free race's update windows on the device clock (amg_dist_async_update_windows)
-   if (sched == AMG_SCHED_FREE && D->corr.stamps_begin(c->stream, D->L, std::max(1, D->o.num_cycles)))
-      return amg_set_error(AMG_ERR_OOM, "amg_dist_async_solve: update-window stamps");
    AMG_HIP(hipEventRecord(ready, c->stream));
    AMG_HIP(hipEventRecord(t_start, c->stream));
    D->corr.reset(D->L);
