@@ -641,7 +641,8 @@ def test_dist_async_additive_accel(amg, oracle, solver, accel, cuts, grid, bound
 
 
 @pytest.mark.slow
-def test_dist_async_jacobi_512(amg, ctx):
+@pytest.mark.parametrize("R", [8, 2])
+def test_dist_async_jacobi_512(amg, ctx, R):
     """DMEM_AsyncSmooth at config 4's size: the 512^3 fine operator (A0 of
     11.8 GB) as 8 row-partitioned ranks (threads) on one GPU, the ghost deltas
     through the device-resident channels (a send is a copy kernel on the comm
@@ -651,7 +652,7 @@ def test_dist_async_jacobi_512(amg, ctx):
     rank received `sweeps` messages from each neighbour), the residual
     contracts like Jacobi, and the fraction of the exchange hidden behind the
     interior product is reported per rank."""
-    n, R, K, w = 512, 8, 12, 0.8
+    n, K, w = 512, 12, 0.8
     gen = amg.Gen(n)
     f = amg.rhs_rand(0, n ** 3)
     opts = amg.default_opts(smooth_weight=w)
@@ -673,7 +674,7 @@ def test_dist_async_jacobi_512(amg, ctx):
     rels = [t[0] for t in res]
     assert all(r == rels[0] for r in rels)
     for q, (rel, st) in enumerate(res):
-        print(f"512^3 async Jacobi rank {q}: relres {rel:.6e}, hidden {st['hidden_fraction']:.3f}, exchange "
+        print(f"512^3 async Jacobi {R} ranks, rank {q}: relres {rel:.6e}, hidden {st['hidden_fraction']:.3f}, exchange "
               f"{st['exchange_ms_per_sweep']:.3f} ms, interior {st['interior_ms_per_sweep']:.3f} ms, on time "
               f"{st['on_time_fraction']:.3f}, late {st['late_deltas']:.0f}, send wait "
               f"{st['send_wait_ms_per_sweep']:.3f} ms/sweep")
