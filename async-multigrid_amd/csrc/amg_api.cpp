@@ -159,7 +159,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_MZ_EDGE")) c->mz_edge = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ27_OCC")) c->mz27_occ = std::max(-1, std::min(8, std::atoi(v)));
    if (const char *v = std::getenv("AMG_MZ_OCC")) c->mz_occ = std::max(-1, std::min(8, std::atoi(v)));
-   if (const char *v = std::getenv("AMG_MZ_PF")) c->mz_pf = std::atoi(v) == 2 ? 2 : 1;
+   if (const char *v = std::getenv("AMG_MZ_PF")) c->mz_pf = std::atoi(v) == 2 ? 2 : (std::atoi(v) == 1 ? 1 : 3);
    if (const char *v = std::getenv("AMG_MZ27_PF")) c->mz27_pf = std::atoi(v) == 1 ? 1 : 2;
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
    if (const char *v = std::getenv("AMG_RR_OCC")) c->rr_occ = std::atoi(v);
@@ -963,7 +963,7 @@ extern "C" int amg_set_graphs(amg_ctx *c, int enable)
 extern "C" int amg_set_march_tuning(amg_ctx *c, int mz_pf, int mz27_pf, int mz_occ, int mz27_occ)
 {
    AMG_ARG(c, "amg_set_march_tuning: null context");
-   AMG_ARG(mz_pf == -2 || mz_pf == 1 || mz_pf == 2, "amg_set_march_tuning: 7-pt prefetch distance %d", mz_pf);
+   AMG_ARG(mz_pf == -2 || (mz_pf >= 1 && mz_pf <= 3), "amg_set_march_tuning: 7-pt prefetch distance %d", mz_pf);
    AMG_ARG(mz27_pf == -2 || mz27_pf == 1 || mz27_pf == 2, "amg_set_march_tuning: 27-pt prefetch distance %d",
            mz27_pf);
    AMG_ARG(mz_occ >= -2 && mz_occ <= 8 && mz27_occ >= -2 && mz27_occ <= 8,

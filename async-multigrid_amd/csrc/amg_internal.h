@@ -215,7 +215,7 @@ struct amg_ctx {
    // (> 0: that many per CU; < 0: the kernel's own occupancy from the runtime)
    int mz27_occ = -1;
    int mz_occ = 0; // the same for the 7-pt march (AMG_MZ_OCC; 0: mz_chunk's rule)
-   int mz_pf = 1;  // 7-pt march prefetch distance in planes (AMG_MZ_PF: 1 or 2)
+   int mz_pf = 3;  // 7-pt march prefetch distance in planes (AMG_MZ_PF: 1 or 2; 3: 1 + halo operands and rhs ahead)
    int mz27_pf = 2;
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies

@@ -1019,7 +1019,15 @@ __device__ __forceinline__ v2d mz_acc7(v2d acc, const v2d (&xv)[7], unsigned lon
 // k - 1, k, k + 1, so the +-S operands of its inner lines come from registers
 // and only the two halo lines are loaded per plane (2 / NLN line loads per line
 // instead of 2).  NLN > 1 needs S % 512 == 0 and NLN | P / S.
-template <int NEG, bool NEED_DIAG, class Epi, bool UNI, int NLN = 1, int PF = 1, int WPE = 0>
+//
+// HPF (halo prefetch, ctx->mz_pf == 3): the +-S lines, wave-edge elements and
+// pattern bytes of plane k + 2 are loaded in iteration k, together with the
+// workgroup's own line of that plane -- the three workgroups that read a line
+// of x (as their own line and as the +-S operands of the lines beside it) then
+// read it in the same iteration instead of two iterations apart, when the
+// 2.3 MB per iteration that an XCD's resident workgroups stream has evicted
+// it from the 4 MB L2 (two PlaneIn sets held: planes k and k + 1)
+template <int NEG, bool NEED_DIAG, class Epi, bool UNI, int NLN = 1, int PF = 1, int WPE = 0, int HPF = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) void csr_mz_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ x, int P, int S, int nz, int zc,
@@ -1066,13 +1074,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
       q2[i] = v2d{0.0, 0.0};
       if (PF == 2 && k0 + 2 < nz && k0 + 1 < k1) q2[i] = ld2u(x, (unsigned)(k0 + 2) * P + (unsigned)(pos + i * S));
    }
+   // HPF 1 / 2: halo operands one / two planes ahead; 3 / 4: the same with the
+   // epilogue's first operand (the right-hand side) too
+   constexpr int HD = HPF > 2 ? HPF - 2 : HPF;
+   constexpr bool HF = HPF > 2;
    struct PlaneIn {
       v2d ym, yp; // halo lines: below the first, above the last
       double e[NLN];
       int pid[NLN];
+      v2d a0[NLN]; // HF: epi.init2
    };
    auto fetch = [&](int k, PlaneIn &in) {
       const unsigned row = (unsigned)k * P + pos;
+      if (HF)
+#pragma unroll
+         for (int i = 0; i < NLN; i++) in.a0[i] = epi.init2((int)(row + (unsigned)(i * S)));
       in.ym = ld2u(x, row >= (unsigned)S ? row - S : 0u);
       const unsigned rp = row + (unsigned)(NLN * S);
       in.yp = ld2u(x, rp + 2 <= Nu ? rp : Nu - 2);
@@ -1085,6 +1101,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
          if (lane == 63 && ri + 2 < Nu) in.e[i] = ld1u(x, ri + 2);
       }
    };
+   PlaneIn h0{}, h1{}; // HD 2: planes k, k + 1; HD 1: plane k in h0
+   if (HD) fetch(k0, h0);
+   if (HD == 2 && k0 + 1 < k1) fetch(k0 + 1, h1);
    __syncthreads();
    for (int k = k0; k < k1; k++) {
       const unsigned row0 = (unsigned)k * P + pos;
@@ -1096,12 +1115,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
          if (k + PF + 1 < nz && k + PF < k1) xn[i] = ld2u(x, row0 + (unsigned)(i * S) + (PF + 1u) * P);
       }
       PlaneIn cur;
-      fetch(k, cur);
+      if (HD == 2) {
+         cur = h0;
+         h0 = h1;
+         if (k + 2 < k1) fetch(k + 2, h1);
+      } else if (HD == 1) {
+         cur = h0;
+         if (k + 1 < k1) fetch(k + 1, h0);
+      } else {
+         fetch(k, cur);
+      }
 #pragma unroll
       for (int i = 0; i < NLN; i++) {
          const unsigned row = row0 + (unsigned)(i * S);
          const int pid = cur.pid[i];
-         v2d acc = epi.init2((int)row);
+         v2d acc = HF ? cur.a0[i] : epi.init2((int)row);
          v2d pf = xc_pf ? xc[i] : epi.pf2((int)row);
          const double e = cur.e[i];
          double lft = __shfl_up(xc[i].y, 1, 64);
@@ -1219,9 +1247,43 @@ static void launch_mz(hipStream_t s, const amg_mat *A, const double *x, const Ep
       const char *v = std::getenv("AMG_MZ_WPE");
       return v ? std::atoi(v) : 0;
    }();
+   // ctx->mz_pf == 3: prefetch 1 with the halo operands two planes ahead (HPF, one line per lane)
+   const int pfk = A->ctx->mz_pf == 3 && lines == 1 ? 3 : (pf2 ? 2 : 1);
    auto go = [&](auto uni, auto nln, auto pf) {
       constexpr bool U = decltype(uni)::value;
       constexpr int N = decltype(nln)::value, F = decltype(pf)::value;
+      if constexpr (N == 1 && F == 1) {
+         if (pfk == 3) {
+            auto hpf = [&](auto wv, auto dv) {
+               constexpr int W = decltype(wv)::value, D = decltype(dv)::value;
+               const void *fnh = (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F, W, D>;
+               const int npb = P / 512, zc = occ_chunk(A, nk, npb, A->ctx->mz_occ, fnh), nch = (nk + zc - 1) / zc;
+               csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F, W, D><<<npb * nch, 256, 0, s>>>(
+                  A->ppat, A->mpmask, A->pp_n, mv, S, x, P, Sx, nz, zc, npb, A->ctx->mz_xcd, e, partials, kb, ke);
+            };
+            using W0 = std::integral_constant<int, 0>;
+            using W5 = std::integral_constant<int, 5>;
+            // AMG_MZ_HPF: 1 / 2 the halo operands one / two planes ahead, 3 / 4
+            // with the right-hand side too (default 3: 90 VGPRs, 5 waves per
+            // SIMD; profiles/r05/hpf/); AMG_MZ_WPE=5: held to 5 waves per SIMD
+            static const int hd = [] {
+               const char *v = std::getenv("AMG_MZ_HPF");
+               const int d = v ? std::atoi(v) : 3;
+               return d >= 1 && d <= 4 ? d : 3;
+            }();
+            switch (hd * 2 + (wpe == 5)) {
+            case 2: hpf(W0{}, std::integral_constant<int, 1>{}); break;
+            case 3: hpf(W5{}, std::integral_constant<int, 1>{}); break;
+            case 5: hpf(W5{}, std::integral_constant<int, 2>{}); break;
+            case 6: hpf(W0{}, std::integral_constant<int, 3>{}); break;
+            case 7: hpf(W5{}, std::integral_constant<int, 3>{}); break;
+            case 8: hpf(W0{}, std::integral_constant<int, 4>{}); break;
+            case 9: hpf(W5{}, std::integral_constant<int, 4>{}); break;
+            default: hpf(W0{}, std::integral_constant<int, 2>{}); break;
+            }
+            return;
+         }
+      }
       if constexpr (N == 1 && F == 1) {
          if (wpe == 8) {
             const void *fn8 = (const void *)csr_mz_kernel<NEG, NEED_DIAG, Epi, U, N, F, 8>;

@@ -428,7 +428,9 @@ int amg_set_march_lines(amg_ctx *ctx, int lines);
 int amg_set_march_lines_gemv(amg_ctx *ctx, int lines);
 /* plane-march scheduling (MI355X tuning, no reference counterpart; env
  * AMG_MZ_PF, AMG_MZ27_PF, AMG_MZ_OCC, AMG_MZ27_OCC): prefetch distance in planes
- * of the 7-pt / 27-pt march (1 or 2; defaults 1 / 2) and chunking by occupancy
+ * of the 7-pt / 27-pt march (1 or 2; 7-pt 3: distance 1 with the +-S /
+ * wave-edge / pattern / right-hand-side operands loaded a plane ahead, AMG_MZ_HPF;
+ * defaults 3 / 2) and chunking by occupancy
  * (-1: whole rounds of the kernel's resident workgroups, 0: the planes-per-chunk
  * rule of amg_set_plane_march, > 0: that many workgroups per CU; defaults 0 /
  * -1, automatic chunking only).  Bit-identical in every setting; -2 keeps a

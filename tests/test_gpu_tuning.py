@@ -15,12 +15,13 @@ pytestmark = pytest.mark.gpu
 W = 0.8
 
 
-@pytest.mark.parametrize("tune", [(2, 2, -1, -1), (1, 1, 0, 0), (2, 1, 3, 5)],
-                         ids=["pf2-occ", "pf1-off", "mixed"])
+@pytest.mark.parametrize("tune", [(2, 2, -1, -1), (1, 1, 0, 0), (2, 1, 3, 5), (3, 2, -1, -1)],
+                         ids=["pf2-occ", "pf1-off", "mixed", "halo-pf"])
 @pytest.mark.parametrize("name", ["lap64x8x5", "lap512x8x4", "neu32x16x7"])
 def test_march_tuning_bitwise(ctx, amg, boxes, name, tune):
-    """the 7-pt march's scheduling knobs (prefetch distance, occupancy-sized
-    chunks; amg_set_march_tuning) change only who computes which plane: SpGEMV
+    """the 7-pt march's scheduling knobs (prefetch distance, halo operands two
+    planes ahead, occupancy-sized chunks; amg_set_march_tuning) change only who
+    computes which plane: SpGEMV
     and Jacobi outputs bit-identical to plain CSR"""
     A = boxes[name]
     ctx.set_plane_march(1, -1, 1)
@@ -49,7 +50,7 @@ def test_march_tuning_bitwise(ctx, amg, boxes, name, tune):
         mz.free()
         pl.free()
     finally:
-        ctx.set_march_tuning(1, 2, 0, -1)  # the defaults
+        ctx.set_march_tuning(3, 2, 0, -1)  # the defaults
         ctx.set_march_lines(1, gemv=2)
 
 
@@ -84,7 +85,7 @@ def test_march27_tuning_bitwise(ctx, amg, oracle, boxes27, name, tune):
         mz.free()
         pl.free()
     finally:
-        ctx.set_march_tuning(1, 2, 0, -1)  # the defaults
+        ctx.set_march_tuning(3, 2, 0, -1)  # the defaults
 
 
 @pytest.mark.parametrize("mode", ["async-jacobi-s3", "async-hybrid-s1", "sync"])
