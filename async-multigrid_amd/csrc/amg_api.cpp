@@ -163,6 +163,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_MZ27_PF")) c->mz27_pf = std::atoi(v) == 1 ? 1 : 2;
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
    if (const char *v = std::getenv("AMG_RR_OCC")) c->rr_occ = std::atoi(v);
+   if (const char *v = std::getenv("AMG_RR_FPF")) c->rr_fpf = std::atoi(v);
    if (const char *v = std::getenv("AMG_RR_ZC")) c->rr_zc = std::max(0, std::min(std::atoi(v), 32));
    if (const char *v = std::getenv("AMG_RR_RING")) c->rr_ring = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ_NT")) c->mz_nt = std::atoi(v) & 3;

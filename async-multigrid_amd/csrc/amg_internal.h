@@ -234,6 +234,7 @@ struct amg_ctx {
    int mz_nt = 0;          // streaming hints on > 512 MB levels: 1 NT stores, 2 NT rhs loads
    int rr_ring = 0;        // wave-edge residuals through a flag-ordered LDS ring (measured slower: off)
    int rr_occ = 0;         // 5: the fused residual + restriction compiled for 5 waves / SIMD
+   int rr_fpf = 0;         // 1: its right-hand side a fine plane ahead (AMG_RR_FPF)
    int rr_zc = 0;          // coarse planes per chunk of the fused residual + restriction (0: mz_zc / 2)
    int jgs_wave = 1;       // hybrid JGS form: 1 8 blocks per wave, 2 one wave per block, 0 one lane per block, 3 LDS tile
    int jgs_small = 2;      // small levels' hybrid JGS form (amg_set_jgs_small)

@@ -1737,7 +1737,9 @@ __device__ __forceinline__ void zg_apply(const ZeroGuess &zg, long long i, doubl
 // t = r ./ a (a = the uniform diagonal, divided once per loaded element), the
 // fine value is z = r + (-w) (A t) (xfer_div, SpMV, xfer_sub: same operations,
 // same order) and f_c = R z; f is not read
-template <bool UNI, int LC, int OCC = 1, bool RING = false, bool XF = false>
+// FPF: the right-hand side of fine plane k + 1 loaded in iteration k (12 more
+// VGPRs, still 4 waves per SIMD)
+template <bool UNI, int LC, int OCC = 1, bool RING = false, bool XF = false, bool FPF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void mz_res_restrict_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, Val7 Sv7, const double *__restrict__ x, const double *__restrict__ f,
@@ -1825,17 +1827,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
          in.e[i] = 0.0;
          if (i == NL - 1 && lastl) continue;
          in.pid[i] = ppat[row >> 1];
-         if (!XF) in.a2[i] = ld2nt(f + row, ntf);
+         if (!XF && !FPF) in.a2[i] = ld2nt(f + row, ntf);
          if (lane == 0 && row > 0) in.e[i] = ld1u(x, row - 1);
          if (lane == 63 && row + 2 < Nu) in.e[i] = ld1u(x, row + 2);
       }
    };
+   // FPF: f of the next fine plane (lines outside the box stay zero)
+   auto fetch_f = [&](int k, v2d (&fa)[NL]) {
+      const unsigned base = (unsigned)(k - fz0) * P + pos0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) {
+         fa[i] = v2d{0.0, 0.0};
+         if (i == NL - 1 && lastl) continue;
+         fa[i] = ld2nt(f + base + (unsigned)i * S, ntf);
+      }
+   };
+   v2d fcur[FPF ? NL : 1];
+   if constexpr (FPF) fetch_f(kf0, fcur);
    __syncthreads();
    for (int k = kf0; k <= kf1; k++) {
       const unsigned base = (unsigned)(k - fz0) * P + pos0;
       v2d r[NL];
       PlaneIn cur;
       fetch(k, cur);
+      v2d fnx[FPF ? NL : 1];
+      if constexpr (FPF) {
+#pragma unroll
+         for (int i = 0; i < NL; i++) {
+            cur.a2[i] = fcur[i];
+            fnx[i] = v2d{0.0, 0.0};
+         }
+         if (k + 1 <= kf1) fetch_f(k + 1, fnx);
+      }
       const v2d hm = sc(cur.hm), hp = sc(cur.hp);
 #pragma unroll
       for (int i = 0; i < NL; i++) {
@@ -1864,6 +1887,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
             r[i] = mz_acc7<1, UNI>(a2, xv, mk, Sv, UNI ? nullptr : mval + pid * 7);
          }
       }
+      if constexpr (FPF)
+#pragma unroll
+         for (int i = 0; i < NL; i++) fcur[i] = fnx[i];
       // next plane's operands: load plane k + 2 while the restriction runs
 #pragma unroll
       for (int i = 0; i < NL; i++) {
@@ -1976,6 +2002,8 @@ void mz_residual_restrict(hipStream_t s, const amg_mat *A, const double *f, cons
                                                    g.nz, zcc, nlb, xcd, stream_hint(A), fc, Kb, Ke, fz0, cz0, nzm, zg)
    if (A->mp_uni) {
       if (LC == 2) AMG_RR(true, 2);
+      else if (A->ctx->rr_fpf == 3) AMG_RR(true, 1, 1, false, false, true); // 136 VGPRs, 3 waves / SIMD
+      else if (A->ctx->rr_fpf) AMG_RR(true, 1, 4, false, false, true);      // held to 4 waves (128, 5 spilled)
       else if (A->ctx->rr_occ == 5) AMG_RR(true, 1, 5);
       else if (A->ctx->rr_ring) AMG_RR(true, 1, 1, true);
       else AMG_RR(true, 1);
