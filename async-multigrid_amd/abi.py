@@ -103,6 +103,7 @@ PROTOTYPES = {
     "amg_mat_march_points": (_i, [_p]),
     "amg_set_bsr3": (_i, [_p, _i]),
     "amg_mat_bsr3": (_i, [_p]),
+    "amg_mat_bsr3_slice": (_i, [_p]),
     "amg_mat_info": (_i, [_p, _ip, _ip, _llp]),
     "amg_mat_download": (_i, [_p, _p, _ip, _ip, _dp]),
     "amg_vec_create": (_i, [_p, _i, _pp]),

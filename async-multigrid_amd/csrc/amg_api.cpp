@@ -154,7 +154,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_JGS_SMALL")) c->jgs_small = std::max(0, std::min(2, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_WAVE")) c->jgs_wave = std::max(0, std::min(3, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_FOLD")) c->jgs_fold = std::atoi(v) != 0;
-   if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_BSR3")) c->bsr3 = std::max(0, std::min(std::atoi(v), 2));
    if (const char *v = std::getenv("AMG_BSR3_XS")) c->bsr3_xs = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ_EDGE")) c->mz_edge = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_MZ27_OCC")) c->mz27_occ = std::max(-1, std::min(8, std::atoi(v)));
@@ -1096,8 +1096,10 @@ static int build_bsr3(amg_mat *A, const int *rowptr, const int *col, const doubl
       }
    }
    if (blocked * 10 < 9LL * nb) return AMG_OK;
-   // sliced layout (21 block rows per slice, padded to the slice's longest)
-   constexpr int SL = 21;
+   // sliced layout (21 block rows per slice -- a lane per row -- or, value-indexed
+   // with ctx->bsr3 == 2, 64 -- a lane per block row; padded to the slice's longest)
+   const int SL = A->ctx->bsr3 == 2 && A->vidx ? 64 : 21;
+   A->bsl = SL;
    const int ns = (nb + SL - 1) / SL;
    std::vector<long long> soff(ns + 1, 0);
    for (int sl = 0; sl < ns; sl++) {
@@ -1184,13 +1186,18 @@ extern "C" int amg_set_bsr3(amg_ctx *c, int enable)
 {
    AMG_ARG(c, "amg_set_bsr3: null context");
    c->knob_gen++; // cached hipGraphs were captured with the old setting
-   c->bsr3 = enable ? 1 : 0;
+   c->bsr3 = enable == 2 ? 2 : (enable ? 1 : 0);
    return AMG_OK;
 }
 
 extern "C" int amg_mat_bsr3(const amg_mat *A)
 {
    return A ? A->bsr3 : 0;
+}
+
+extern "C" int amg_mat_bsr3_slice(const amg_mat *A)
+{
+   return A && A->bsr3 ? A->bsl : 0;
 }
 
 extern "C" int amg_csr_register(amg_ctx *c, int nrows, int ncols, long long nnz, const int *rowptr,

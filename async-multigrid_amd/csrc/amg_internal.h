@@ -219,7 +219,7 @@ struct amg_ctx {
    int mz27_pf = 2;
    int mz_xcd = 1;         // XCD-contiguous workgroup order of the plane-marching kernel
    int fuse_transfer = 1;  // fused level-0 residual + restriction on geometric hierarchies
-   int bsr3 = 1;           // 3x3 block form of num_functions = 3 operators
+   int bsr3 = 2;           // 3x3 block form of num_functions = 3 operators (1: lane per row; 2: lane per block row when value-indexed)
    unsigned knob_gen = 0;  // bumped by every amg_set_* knob: captured hipGraphs older than it are dropped
    int graphs = 0;         // hipGraphs of the additive cycles' launch-bound loops (AMG_GRAPHS)
    int fuse_xfer = 1;      // composed smoothed transfers of marched 7-pt levels in one pass each
@@ -334,6 +334,7 @@ struct amg_mat {
    // bcnt[t] = blocks of block row t (0: CSR form), bdiag[t] = its diagonal
    // block's index k
    int bsr3 = 0; // 1: value-indexed blocks, 2: fp64 blocks
+   int bsl = 21; // block rows per slice: 21 (lane per row, bsr3_kernel) or 64 (lane per block row, bsr3_row_kernel)
    long long *soff = nullptr;
    int *bcol = nullptr, *bdiag = nullptr;
    unsigned char *bmode = nullptr;

@@ -3686,6 +3686,90 @@ Gemv gemv_mode(double alpha, double beta)
 // identity rows of fixed dofs) run the CSR row loop.  Per block row the
 // value-indexed form streams 27 x (12 + 4) bytes against 81 x 5 for
 // value-indexed CSR.
+// Lane-per-block-row form (bsr3_row_kernel, ctx->bsr3 == 2, value-indexed):
+// lane q of a wave owns block row t = 64 sl + q -- all three of its rows, three
+// independent accumulators -- and walks its blocks: per block one 12-byte load of
+// the three rows' value indices (a wave's 64 contiguous), one 4-byte block
+// column (contiguous) and the node's three x values, no cross-lane shuffles.
+// Each row adds its diagonal first, then its entries block by block in
+// ascending column order (bsr3_kernel's order: bit-identical).
+template <int NEG, bool NEED_DIAG, class Epi, int U = 4>
+__global__ __launch_bounds__(256) void bsr3_row_kernel(const long long *__restrict__ soff,
+                                                       const int *__restrict__ bcol, const int *__restrict__ bdiag,
+                                                       const unsigned char *__restrict__ bcnt,
+                                                       const unsigned int *__restrict__ bvi,
+                                                       const double *__restrict__ vtab_g,
+                                                       const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                       const double *__restrict__ val, const double *__restrict__ x,
+                                                       int t0, int t1, Epi epi)
+{
+   __shared__ double vtab[256];
+   vtab[threadIdx.x] = vtab_g[threadIdx.x];
+   __syncthreads();
+   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+   const int sl = t0 / 64 + (int)blockIdx.x * 4 + wave;
+   const int t = sl * 64 + lane;
+   if (t < t0 || t >= t1) return;
+   double acc[3], xi[3], a[3];
+   auto madd = [&](double &ac, double v, double xv) { ac = NEG ? ac - v * xv : ac + v * xv; };
+#pragma unroll
+   for (int c = 0; c < 3; c++) {
+      acc[c] = epi.init(3 * t + c);
+      xi[c] = x[3 * t + c];
+      a[c] = 0.0;
+   }
+   const int cnt = bcnt[t];
+   if (cnt == 0) {
+      // CSR form: each row's entries in order
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+         const int i = 3 * t + c, b = rowptr[i], e = rowptr[i + 1];
+         if (NEED_DIAG) a[c] = b < e ? val[b] : 0.0;
+         for (int k = b; k < e; k++) madd(acc[c], val[k], x[col[k]]);
+      }
+   } else {
+      const long long base = soff[sl] + lane;
+      const int kd = bdiag[t];
+      {
+         const unsigned int *w = bvi + (base + 64LL * kd) * 3;
+#pragma unroll
+         for (int c = 0; c < 3; c++) {
+            a[c] = vtab[(w[c] >> (8 * c)) & 0xff];
+            madd(acc[c], a[c], xi[c]); // the diagonal first
+         }
+      }
+      for (int kc = 0; kc < cnt; kc += U) {
+         int jj[U];
+         unsigned int wv[U][3];
+#pragma unroll
+         for (int u = 0; u < U; u++) {
+            const long long sp = base + 64LL * min(kc + u, cnt - 1);
+            jj[u] = bcol[sp];
+#pragma unroll
+            for (int c = 0; c < 3; c++) wv[u][c] = bvi[sp * 3 + c];
+         }
+         double xv[U][3];
+#pragma unroll
+         for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++) xv[u][cc] = x[3 * (size_t)jj[u] + cc];
+#pragma unroll
+         for (int u = 0; u < U; u++) {
+            const int k = kc + u;
+            if (k >= cnt) break;
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+#pragma unroll
+               for (int cc = 0; cc < 3; cc++)
+                  if (k != kd || c != cc) madd(acc[c], vtab[(wv[u][c] >> (8 * cc)) & 0xff], xv[u][cc]);
+         }
+      }
+   }
+#pragma unroll
+   for (int c = 0; c < 3; c++)
+      epi.finish(3 * t + c, acc[c], a[c], (pf_is_x<Epi>::value && epi_pf_vec(epi) == x) ? xi[c] : epi.pf(3 * t + c));
+}
+
 template <int NEG, bool NEED_DIAG, class Epi, bool VI, bool XS = false, int U = 9>
 __global__ __launch_bounds__(256) void bsr3_kernel(const long long *__restrict__ soff, const int *__restrict__ bcol,
                                                    const int *__restrict__ bdiag,
@@ -3785,6 +3869,13 @@ template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_bsr3(hipStream_t s, const amg_mat *A, const double *x, int rb, int re, const Epi &e)
 {
    const int t0 = rb / 3, t1 = re / 3;
+   if (A->bsl == 64) {
+      // a lane per block row (value-indexed 64-row slices)
+      const int nsl = (t1 - t0 + 63) / 64;
+      bsr3_row_kernel<NEG, NEED_DIAG, Epi><<<(nsl + 3) / 4, 256, 0, s>>>(
+         A->soff, A->bcol, A->bdiag, A->bmode, A->bvi, A->vtab, A->rowptr, A->col, A->val, x, t0, t1, e);
+      return;
+   }
    const int nsl = (t1 - t0 + 20) / 21;
    const int nb = (nsl + 3) / 4;
    // ctx->bsr3_xs: the node's x shared across the block row's three lanes;
@@ -3831,11 +3922,12 @@ static void launch_bsr3(hipStream_t s, const amg_mat *A, const double *x, int rb
    }
 }
 
-// the block form serves row ranges that start on a slice (21 block rows) and
-// end on a slice or at the last row
+// the block form serves row ranges that start on a slice (21 or 64 block rows)
+// and end on a slice or at the last row
 static inline bool use_bsr3(const amg_mat *A, int rb, int re, const double *partials)
 {
-   return A->bsr3 && !partials && rb % 63 == 0 && (re % 63 == 0 || re == A->nrows) && A->nrows % 3 == 0;
+   const int sr = 3 * A->bsl;
+   return A->bsr3 && !partials && rb % sr == 0 && (re % sr == 0 || re == A->nrows) && A->nrows % 3 == 0;
 }
 
 void residual_fsub(hipStream_t s, const amg_mat *A, const double *x, const double *b, double *y, double *r, int n)

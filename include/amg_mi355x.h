@@ -276,10 +276,16 @@ int amg_set_plane_march(amg_ctx *ctx, int enable, int zc, int xcd);
  * walk them three lanes per block row (diagonal first, then ascending: the
  * CSR order, bit-identical); the identity rows of fixed dofs keep the CSR
  * form.  Used when >= 90% of the block rows block.  amg_set_bsr3(ctx, 0) (env
- * AMG_BSR3=0) keeps CSR for matrices registered afterwards;
+ * AMG_BSR3=0) keeps CSR for matrices registered afterwards; value-indexed
+ * blocks are walked one lane per block row (64 block rows per slice: the
+ * default, 2) or three lanes per block row (21 per slice: amg_set_bsr3(ctx, 1),
+ * AMG_BSR3=1), the same bits;
  * amg_mat_bsr3: 1 value-indexed blocks, 2 fp64 blocks, 0 not blocked. */
 int amg_set_bsr3(amg_ctx *ctx, int enable);
 int amg_mat_bsr3(const amg_mat *A);
+/* block rows per slice of a blocked matrix: 64 (a lane per block row) or 21
+ * (a lane per row); 0 when not blocked */
+int amg_mat_bsr3_slice(const amg_mat *A);
 int amg_mat_plane_march(const amg_mat *A);
 int amg_mat_march_points(const amg_mat *A);
 int amg_mat_info(const amg_mat *A, int *nrows, int *ncols, long long *nnz);

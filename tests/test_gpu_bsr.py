@@ -22,17 +22,21 @@ def reg(ctx, n, rp, cj, v, bsr=1, vi=1):
     try:
         return ctx.csr(n, n, rp, cj, v)
     finally:
-        ctx.set_bsr3(1)
+        ctx.set_bsr3(2)
         ctx.set_value_index(1)
 
 
+@pytest.mark.parametrize("form", [1, 2], ids=["lane-per-row", "lane-per-block-row"])
 @pytest.mark.parametrize("r", [2, 3])
 @pytest.mark.parametrize("vi", [1, 0])
-def test_bsr3_bitwise(amg, oracle, ctx, elast, r, vi):
+def test_bsr3_bitwise(amg, oracle, ctx, elast, r, vi, form):
+    """form 2 (amg_set_bsr3(ctx, 2)): value-indexed blocks walked one lane per
+    block row (64-row slices); fp64 blocks keep form 1"""
     n, rp, cj, v, b = elast[r]
-    Mb = reg(ctx, n, rp, cj, v, 1, vi)
+    Mb = reg(ctx, n, rp, cj, v, form, vi)
     Mp = reg(ctx, n, rp, cj, v, 0, 0)
     assert Mb.bsr3 == (1 if vi else 2) and Mp.bsr3 == 0
+    assert amg.lib.amg_mat_bsr3_slice(Mb.h) == (64 if vi and form == 2 else 21)
     A = oracle.Csr(n, n, rp, cj, v)
     l1 = ctx.vec(oracle.l1_norms(A))
     x = ctx.vec(_vecs(n, 61))
@@ -44,8 +48,9 @@ def test_bsr3_bitwise(amg, oracle, ctx, elast, r, vi):
             y = ctx.vec(n)
             amg.smem.SMEM_SpGEMV(ctx, M, x, f, ab[0], ab[1], y, 0, n)
             o.append(y.download())
-        # slice-aligned row ranges (63 rows: blocks) and others (CSR)
-        for rb, re in ((63, 63 * (n // 63 - 1)), (126, n), (3, n - 6), (1, n - 2)):
+        # slice-aligned row ranges (63 / 192 rows: blocks) and others (CSR)
+        for rb, re in ((63, 63 * (n // 63 - 1)), (126, n), (192, 192 * (n // 192 - 1)), (384, n), (3, n - 6),
+                       (1, n - 2)):
             y = ctx.vec(_vecs(n, 63))
             amg.smem.SMEM_SpGEMV(ctx, M, x, f, -1.0, 1.0, y, rb, re)
             o.append(y.download())

@@ -68,14 +68,15 @@ def main():
         # diagonal position and mode (9 bytes); blocks ~ nnz / 9
         per = 16 if A0.bsr3 == 1 else 76
         mat_bytes = per * (A0.nnz // 9) + 9 * (n // 3)
-        fmt = f"bsr3 ({'value-indexed' if A0.bsr3 == 1 else 'fp64'} 3x3 blocks)"
+        fmt = (f"bsr3 ({'value-indexed' if A0.bsr3 == 1 else 'fp64'} 3x3 blocks, "
+               f"{amg.lib.amg_mat_bsr3_slice(A0.h)} block rows per slice)")
     else:
         mat_bytes, fmt = storage(A0.nrows, A0.nnz, A0.value_index, A0.dict_index, A0.row_pattern)
     spmv_bytes = mat_bytes + 16 * n
     # the same operator in value-indexed CSR (blocks off): the kernel it replaces
     ctx.set_bsr3(0)
     Ac = ctx.csr(n, n, rp, cj, v)
-    ctx.set_bsr3(1)
+    ctx.set_bsr3(2)  # the default
     ms_csr = C.c_double()
     amg.check(amg.lib.amg_matvec_timed(ctx.h, Ac.h, x.h, y.h, 20, C.byref(ms_csr)))
     csr_bytes = storage(Ac.nrows, Ac.nnz, Ac.value_index, Ac.dict_index, Ac.row_pattern)[0] + 16 * n
