@@ -2424,8 +2424,12 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
    double mw, int nx, int ny, int nz, int zc, int npb, int xcd, double *__restrict__ out, double *__restrict__ u_priv,
    int zlo, int zhi, int fz0, int cz0, unsigned long long *stamp)
 {
-   // OUT 3: OUT 1 in the reference's add-then-read form
-   constexpr bool noret = OUT == 3;
+   // OUT 3: OUT 1 in the reference's add-then-read form; OUT 4: the same with
+   // the reads batched per workgroup -- every plane's no-return adds issued
+   // as the march goes, one wait, then the chunk's rows read back (a wave
+   // stalls once per chunk instead of twice per plane; another level's adds
+   // may land between a row's add and its read, as in the per-row form)
+   constexpr bool noret = OUT == 3 || OUT == 4;
    stamp_begin(stamp);
    // fine planes [zlo, zhi) of the nx * ny * nz box; out / u_priv / the
    // operator's rows (pattern bytes) have plane 0 = fine plane fz0, e plane 0
@@ -2504,12 +2508,14 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
       const v2d o{xc.x + mw * t0, xc.y + mw * t1};
       if (OUT == 0) {
          *reinterpret_cast<v2du *>(out + row) = o;
-      } else if (OUT == 1 || OUT == 3) {
+      } else if (OUT == 1 || OUT == 3 || OUT == 4) {
          if (noret) {
             add_noret(out + row, o.x);
             add_noret(out + row + 1, o.y);
-            wait_vm_all();
-            *reinterpret_cast<v2du *>(u_priv + row) = v2d{read_agent(out + row), read_agent(out + row + 1)};
+            if (OUT == 3) {
+               wait_vm_all();
+               *reinterpret_cast<v2du *>(u_priv + row) = v2d{read_agent(out + row), read_agent(out + row + 1)};
+            }
          } else {
             const double q0 = atomicAdd(out + row, o.x);
             const double q1 = atomicAdd(out + row + 1, o.y);
@@ -2523,6 +2529,14 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
       ec = eq;
       xq = xn;
       eq = en;
+   }
+   if (OUT == 4) {
+      wait_vm_all();
+#pragma unroll 4
+      for (int k = k0; k < k1; k++) {
+         const unsigned row = (unsigned)(k - fz0) * P + pos;
+         *reinterpret_cast<v2du *>(u_priv + row) = v2d{read_agent(out + row), read_agent(out + row + 1)};
+      }
    }
    stamp_end(stamp);
 }
@@ -2548,7 +2562,8 @@ void mz_xfer_prolong(hipStream_t s, const amg_mat *A, const double *ec, const Ge
                                                           g.nx, g.ny, g.nz, zc, npb, A->ctx->mz_xcd, out, u_priv, \
                                                           zlo, zhi, fz0, cz0, mode == 1 ? stamp : nullptr)
 #define AMG_XP2(U)                 \
-   if (mode == 1 && atomic_noret_mode()) AMG_XP(U, 3); \
+   if (mode == 1 && atomic_noret_mode() == 2) AMG_XP(U, 4); \
+   else if (mode == 1 && atomic_noret_mode()) AMG_XP(U, 3); \
    else if (mode == 1) AMG_XP(U, 1); \
    else if (mode == 2) AMG_XP(U, 2); \
    else AMG_XP(U, 0);
