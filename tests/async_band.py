@@ -127,6 +127,19 @@ def in_band(rel, lo, hi):
     return 0.5 * lo <= rel <= 2.0 * hi
 
 
+def in_rate_band(rel, cyc, rels, cycs, margin=0.03):
+    """per-cycle contraction rel^(1/cycles) inside the band runs' [min, max] (+-margin):
+    under GLOBAL convergence every grid runs a race-dependent number of cycles and its
+    final residual falls geometrically with them, so a grid that ran more cycles than
+    the band's runs ends below their residuals at the same rate (a 3 % margin on the
+    rate is the 0.5x / 2x of in_band over ~25 cycles)"""
+    rates = [r ** (1.0 / c) for r, c in zip(rels, cycs) if r > 0 and c > 0]
+    if not rates or rel <= 0 or cyc <= 0:
+        return False
+    rate = rel ** (1.0 / cyc)
+    return min(rates) * (1 - margin) <= rate <= min(1.0, max(rates) * (1 + margin))
+
+
 def durations_of(level_ms, counts, L):
     """per-level correction times of a device free race: finish time / corrections
     for the levels that corrected; the reference's idle coarsest group (no

@@ -545,3 +545,16 @@ def test_dmem_add_sequential_schedules(amg, oracle, sched):
     print(f"dmem_add sequential {sched}: relres {rel}; round robin {rr[2]}")
     with pytest.raises(Exception):
         OH.dmem_add(f, sched=sched, converge_type=oracle.OR_CONVERGE_GLOBAL)
+
+
+def test_rate_band():
+    """async_band.in_rate_band: a residual below every band run's, reached in more
+    cycles at the band's per-cycle contraction, is in the rate band; the same
+    residual reached in as few cycles as the band's runs, or a stalled one, is not"""
+    from async_band import in_band, in_rate_band
+    rels = [1.2e-8, 3.24e-9, 2.4e-8, 1.2e-8]
+    cycs = [23, 25, 22, 23]
+    assert not in_band(1.0e-9, min(rels), max(rels))
+    assert in_rate_band(1.0e-9, 26, rels, cycs)       # one more cycle at the band's rate
+    assert not in_rate_band(1.0e-9, 20, rels, cycs)   # too fast for its cycles
+    assert not in_rate_band(1.0e-3, 25, rels, cycs)   # stalled
