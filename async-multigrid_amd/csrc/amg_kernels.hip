@@ -3207,8 +3207,18 @@ static void launch_long(hipStream_t s, const amg_mat *A, const double *x, int rb
                         double *partials = nullptr)
 {
    const int n = re - rb;
+   // AMG_LONG_RW=128 / 256: rows per workgroup on the largest levels (the rows'
+   // sequential sums then spread over 2 / 4 waves instead of one)
+   static const int lrw = [] {
+      const char *v = std::getenv("AMG_LONG_RW");
+      return v ? std::atoi(v) : 0;
+   }();
    if (partials)
       launch_long_cfg<NEG, NEED_DIAG, 256, 256>(s, A, x, rb, re, e, partials);
+   else if (lrw == 256 && n >= 256 * 2048)
+      launch_long_cfg<NEG, NEED_DIAG, 256, 256>(s, A, x, rb, re, e);
+   else if (lrw == 128 && n >= 128 * 2048)
+      launch_long_cfg<NEG, NEED_DIAG, 256, 128>(s, A, x, rb, re, e);
    else if (n >= 64 * 4096)
       launch_long_cfg<NEG, NEED_DIAG, 256, 64>(s, A, x, rb, re, e);
    else if (n >= 32 * 4096)
