@@ -3896,10 +3896,11 @@ static void launch_bsr3(hipStream_t s, const amg_mat *A, const double *x, int rb
    const int t0 = rb / 3, t1 = re / 3;
    if (A->bsl == 64) {
       // a lane per block row (value-indexed 64-row slices); AMG_BSR3_RU: blocks
-      // per batch of in-flight loads (2, 4 (default), 6 or 8)
+      // per batch of in-flight loads (2, 4, 6 (default: 212 against 219 us for 4
+      // at r = 6, profiles/r05/bsr3/ru/) or 8)
       static const int ru = [] {
          const char *v = std::getenv("AMG_BSR3_RU");
-         return v ? std::atoi(v) : 4;
+         return v ? std::atoi(v) : 6;
       }();
       const int nsl = (t1 - t0 + 63) / 64;
 #define AMG_BR(UU)                                                                                            \
@@ -3907,9 +3908,9 @@ static void launch_bsr3(hipStream_t s, const amg_mat *A, const double *x, int rb
                                                                           A->bvi, A->vtab, A->rowptr, A->col,    \
                                                                           A->val, x, t0, t1, e)
       if (ru == 2) AMG_BR(2);
-      else if (ru == 6) AMG_BR(6);
+      else if (ru == 4) AMG_BR(4);
       else if (ru == 8) AMG_BR(8);
-      else AMG_BR(4);
+      else AMG_BR(6);
 #undef AMG_BR
       return;
    }
