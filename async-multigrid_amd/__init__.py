@@ -75,6 +75,24 @@ def _corr_ms(fn, h, L, start=False):
         out.append(ms[:int(cnt[0])])
     return out
 
+def _update_rows(fn, h, counts, n):
+    """per level: (corrections, n) per-row update times (ms) of its first recorded
+    corrections in the last free race (rows stamped by the update kernels), or None
+    for a level whose corrections were not all row-stamped"""
+    out = []
+    buf = np.zeros(max(1, n))
+    cnt = np.zeros(1, dtype=np.int32)
+    for k, m in enumerate(counts):
+        rows = []
+        for j in range(int(m)):
+            check(fn(h, k, j, _dp(buf), n, _ip(cnt)))
+            if int(cnt[0]) != n:
+                break
+            rows.append(buf[:n].copy())
+        out.append(np.array(rows).reshape(len(rows), n) if len(rows) == int(m) else None)
+    return out
+
+
 class Context:
     """Device, compute stream and level streams (amg_init)."""
 
@@ -362,6 +380,12 @@ class Hier:
         kernels in the last free-race async_solve (their actual execution windows)"""
         return (_corr_ms(lib.amg_async_update_windows, self.h, self.L, True),
                 _corr_ms(lib.amg_async_update_windows, self.h, self.L, False))
+
+    def async_update_rows(self, n0):
+        """per level: (corrections, n0) per-row update times (ms, the windows' clock) of
+        the last free race, or None where not recorded (amg_async_update_rows)"""
+        counts = [len(w) for w in self.async_update_windows()[1]]
+        return _update_rows(lib.amg_async_update_rows, self.h, counts, n0)
 
     def eigs_power(self, iters):
         emax, emin = C.c_double(), C.c_double()

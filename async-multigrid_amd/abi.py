@@ -163,6 +163,7 @@ PROTOTYPES = {
     "amg_hier_set_async_times": (_i, [_p, _dp, _ip, _i]),
     "amg_async_correction_ms": (_i, [_p, _i, _dp, _i, _ip]),
     "amg_async_update_windows": (_i, [_p, _i, _dp, _i, _ip]),
+    "amg_async_update_rows": (_i, [_p, _i, _i, _dp, _i, _ip]),
     "amg_eigs_power": (_i, [_p, _i, _dp, _dp]),
     "amg_hier_profile_read": (_i, [_p, _dp, _llp, _i]),
     "amg_gen_create": (_i, [_i, _i, _i, _i, _i, _i, _pp]),
@@ -212,6 +213,7 @@ PROTOTYPES = {
     "amg_dist_hier_set_async_times": (_i, [_p, _dp, _ip, _i]),
     "amg_dist_async_correction_ms": (_i, [_p, _i, _dp, _i, _ip]),
     "amg_dist_async_update_windows": (_i, [_p, _i, _dp, _i, _ip]),
+    "amg_dist_async_update_rows": (_i, [_p, _i, _i, _dp, _i, _ip]),
     "amg_dist_async_jacobi": (_i, [_p, _dp, _i, _i, _dp]),
     "amg_dist_async_jacobi_stats": (_i, [_p, _dp, _i]),
     "amg_dist_async_sps": (_i, [_p, _dp, _i, _dp, C.POINTER(C.c_longlong)]),

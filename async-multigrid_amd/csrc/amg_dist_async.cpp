@@ -504,7 +504,10 @@ int setup_async(amg_dist_hier *D)
       std::vector<long long> caps((size_t)active * R, 0);
       for (int k = 0; k < active; k++)
          for (int p = 0; p < R; p++) caps[(size_t)k * R + p] = cap1[p];
-      AMG_TRY(link_create(D, active, caps, &D->links));
+      // ranks on several nodes: the transport's send / recv (D->links stays null)
+      bool one = false;
+      AMG_TRY(link_single_node(D, &one));
+      if (one) AMG_TRY(link_create(D, active, caps, &D->links));
    }
    return AMG_OK;
 }
@@ -675,8 +678,16 @@ extern "C" int amg_dist_async_solve(amg_dist_hier *D, const double *f_local, int
    // thread, in the schedule's order; free: a stream and a host thread per level
    for (int k = 0; k < active; k++) D->al[k].s = c->level_streams[sched != AMG_SCHED_FREE ? 0 : k];
    // the free race's update windows on the device clock (amg_dist_async_update_windows)
-   if (sched == AMG_SCHED_FREE && D->corr.stamps_begin(c->stream, D->L, std::max(1, D->o.num_cycles)))
-      return amg_set_error(AMG_ERR_OOM, "amg_dist_async_solve: update-window stamps");
+   // and every row's update time (amg_dist_async_update_rows); the fused
+   // level-0 prolongation + correction indexes the slab vector from its ghost
+   // planes' start
+   if (sched == AMG_SCHED_FREE) {
+      std::vector<long long> koff(D->L, 0);
+      for (int k = 1; k < active; k++)
+         if (D->o.accel_type == AMG_NO_ACCEL && fused_xfp0(D)) koff[k] = D->lv[0].sg.off();
+      if (D->corr.stamps_begin(c->stream, D->L, std::max(1, D->o.num_cycles), n0, koff))
+         return amg_set_error(AMG_ERR_OOM, "amg_dist_async_solve: update-window stamps");
+   }
    hipEvent_t ready, t_start;
    std::vector<hipEvent_t> t_end(active);
    AMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
@@ -820,6 +831,15 @@ extern "C" int amg_dist_async_update_windows(const amg_dist_hier *D, int level, 
    const auto &v = level < (int)vv.size() ? vv[level] : std::vector<double>();
    *count = (int)v.size();
    for (int j = 0; j < (int)v.size() && j < cap && ms; j++) ms[j] = v[j];
+   return AMG_OK;
+}
+
+extern "C" int amg_dist_async_update_rows(const amg_dist_hier *D, int level, int corr, double *ms, int cap,
+                                          int *count)
+{
+   AMG_ARG(D && count && level >= 0 && level < D->L && corr >= 0 && cap >= 0,
+           "amg_dist_async_update_rows: bad argument");
+   *count = D->corr.rows_of(level, corr, ms, cap);
    return AMG_OK;
 }
 
@@ -1128,10 +1148,19 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
       const char *e = std::getenv("AMG_AJAC_LINKS");
       return e ? std::atoi(e) != 0 : true;
    }();
-   const bool use_links = !sps && links_env && c->xport->nranks > 1;
+   bool use_links = !sps && links_env && c->xport->nranks > 1;
    if (use_links && !D->ajac_links) {
+      // ranks on several nodes: the transport's grouped send / recv
+      bool one = false;
+      if ((st = link_single_node(D, &one)) != AMG_OK) return fail(st);
+      use_links = one;
+   }
+   if (use_links && !D->ajac_links) {
+      // channels carry both directions (link_create maps a peer's slots only
+      // where caps > 0): a peer I only send to (a pattern-nonsymmetric
+      // operator: scnt > 0, rcnt = 0) needs its channel too
       std::vector<long long> caps(c->xport->nranks, 0);
-      for (int i = 0; i < np; i++) caps[M.peers[i]] = M.rcnt[i];
+      for (int i = 0; i < np; i++) caps[M.peers[i]] = std::max(M.rcnt[i], M.scnt[i]);
       // 8 slots per channel: a sender runs up to 8 sweeps ahead of a peer's receipts
       if ((st = link_create(D, 1, caps, &D->ajac_links, 8)) != AMG_OK) return fail(st);
    }
@@ -1184,125 +1213,132 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
       amgk::spgemv(s, M.A, gext, r, upd, r, 0, n, nullptr); // r -= A_offd g
       return AMG_OK;
    };
-   for (int k = 0; k < sweeps && st == AMG_OK; k++) {
-      const int q = k % AJ_NBUF;
-      // the slot's previous delta must be applied and its send finished
-      for (size_t i = 0; i < pending.size();) {
-         if (pending[i] <= k - AJ_NBUF) {
-            if ((st = apply(pending[i])) != AMG_OK) break;
-            pending.erase(pending.begin() + i);
-         } else {
-            i++;
+   // the sweeps, the drain and the final checks; every failure after this point
+   // (a send timeout, an aborted peer, a HIP error) leaves through one path:
+   // the peers are told (link_abort), the events destroyed, the workspace freed
+   auto sweep_all = [&]() -> int {
+      for (int k = 0; k < sweeps && st == AMG_OK; k++) {
+         const int q = k % AJ_NBUF;
+         // the slot's previous delta must be applied and its send finished
+         for (size_t i = 0; i < pending.size();) {
+            if (pending[i] <= k - AJ_NBUF) {
+               if ((st = apply(pending[i])) != AMG_OK) break;
+               pending.erase(pending.begin() + i);
+            } else {
+               i++;
+            }
          }
-      }
-      if (st != AMG_OK) break;
-      AMG_HIP(hipStreamWaitEvent(s, sent[q], 0));
-      double om1 = 0.0, omd = 0.0;
-      const int am = !accel ? 0 : !acc.next(D->o, &om1, &omd) ? 1 : D->o.cheby_grid == 0 ? 2 : 3;
-      if (sps) {
-         // my residual L1 norm (DMEM_Smooth.cpp:258-268), sent with this sweep's
-         // deltas; then this sweep's update decision
-         int parts = 0;
-         amgk::abssum_partials(s, r, n, part, &parts);
-         amgk::reduce_partials(s, part, parts, snorm + q, 0, c->d_scalars + 4096);
-         sps_decide_k<<<1, 64, 0, s>>>(snorm + q, lnorm, np, D->o.sps_probability_type, sps_alpha, draws, k, gate,
-                                       count);
-      }
-      ajac_update_k<<<nb, 256, 0, s>>>(r, wv, eext, x, dacc, n, am, om1, omd, gate);
-      if (use_links) {
+         if (st != AMG_OK) break;
+         AMG_HIP(hipStreamWaitEvent(s, sent[q], 0));
+         double om1 = 0.0, omd = 0.0;
+         const int am = !accel ? 0 : !acc.next(D->o, &om1, &omd) ? 1 : D->o.cheby_grid == 0 ? 2 : 3;
+         if (sps) {
+            // my residual L1 norm (DMEM_Smooth.cpp:258-268), sent with this sweep's
+            // deltas; then this sweep's update decision
+            int parts = 0;
+            amgk::abssum_partials(s, r, n, part, &parts);
+            amgk::reduce_partials(s, part, parts, snorm + q, 0, c->d_scalars + 4096);
+            sps_decide_k<<<1, 64, 0, s>>>(snorm + q, lnorm, np, D->o.sps_probability_type, sps_alpha, draws, k, gate,
+                                          count);
+         }
+         ajac_update_k<<<nb, 256, 0, s>>>(r, wv, eext, x, dacc, n, am, om1, omd, gate);
+         if (use_links) {
+            if (np > 0) {
+               launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * SS, (int)M.nsend);
+               AMG_HIP(hipEventRecord(packed[q], s));
+               AMG_HIP(hipStreamWaitEvent(cs, packed[q], 0));
+            }
+            bool first = true;
+            for (int i = 0; i < np && st == AMG_OK; i++) {
+               if (M.scnt[i] <= 0) continue;
+               // a full slot ring: keep receiving (and acknowledging) while waiting,
+               // or two ranks that both wait to send would wait on each other
+               const auto t0 = std::chrono::steady_clock::now();
+               for (;;) {
+                  int ok = 0;
+                  if ((st = link_can_send(D->ajac_links, 0, M.peers[i], &ok)) != AMG_OK || ok) break;
+                  if ((st = poll_links(k, false)) != AMG_OK) break;
+                  if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > link_timeout_s()) {
+                     st = amg_set_error(AMG_ERR_RCCL, "amg_dist_async_jacobi: send to rank %d timed out", M.peers[i]);
+                     break;
+                  }
+                  std::this_thread::yield();
+               }
+               send_wait_ms += 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+               // the exchange window: from the first copy's issue (after any wait)
+               if (st == AMG_OK && first && hipEventRecord(tx0(k), cs) != hipSuccess)
+                  st = amg_set_error(AMG_ERR_HIP, "amg_dist_async_jacobi: event");
+               first = false;
+               if (st == AMG_OK)
+                  st = link_send(D->ajac_links, 0, M.peers[i], sbuf + (size_t)q * SS + M.soff[i], M.scnt[i], cs);
+            }
+            if (st == AMG_OK && first) AMG_HIP(hipEventRecord(tx0(k), cs));
+            if (st != AMG_OK) break;
+            AMG_HIP(hipEventRecord(tx1(k), cs));
+            AMG_HIP(hipEventRecord(sent[q], cs));
+            // r -= A_diag e (ghost region of e_ext stays zero), overlapping the sends
+            AMG_HIP(hipEventRecord(ti0(k), s));
+            amgk::spgemv(s, M.A, eext, r, upd, r, 0, n, nullptr);
+            AMG_HIP(hipEventRecord(ti1(k), s));
+            if ((st = poll_links(k, false)) != AMG_OK) break;
+            D->iter = k + 1;
+            continue;
+         }
          if (np > 0) {
-            launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * SS, (int)M.nsend);
+            if (sps) { // the norm travels with the deltas (data[vec_len + 1], DMEM_Comm.cpp:216-220)
+               const long long m = std::max<long long>(M.nsend, np);
+               sps_pack_k<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(eext, M.d_send_idx, M.nsend, d_soff, np, snorm + q,
+                                                                       sbuf + (size_t)q * SS);
+            } else {
+               launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * SS, (int)M.nsend);
+            }
             AMG_HIP(hipEventRecord(packed[q], s));
             AMG_HIP(hipStreamWaitEvent(cs, packed[q], 0));
-         }
-         bool first = true;
-         for (int i = 0; i < np && st == AMG_OK; i++) {
-            if (M.scnt[i] <= 0) continue;
-            // a full slot ring: keep receiving (and acknowledging) while waiting,
-            // or two ranks that both wait to send would wait on each other
-            const auto t0 = std::chrono::steady_clock::now();
-            for (;;) {
-               int ok = 0;
-               if ((st = link_can_send(D->ajac_links, 0, M.peers[i], &ok)) != AMG_OK || ok) break;
-               if ((st = poll_links(k, false)) != AMG_OK) break;
-               if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 300.0) {
-                  st = amg_set_error(AMG_ERR_RCCL, "amg_dist_async_jacobi: send to rank %d timed out", M.peers[i]);
-                  break;
-               }
-               std::this_thread::yield();
+            AMG_HIP(hipEventRecord(tx0(k), cs));
+            std::vector<void *> sp(np), rp(np);
+            std::vector<long long> sb(np), rb(np);
+            const int g = sps ? 1 : 0;
+            for (int i = 0; i < np; i++) {
+               sp[i] = sbuf + (size_t)q * SS + M.soff[i] + g * i;
+               sb[i] = (M.scnt[i] + g) * 8;
+               rp[i] = rbuf + (size_t)q * RS + M.roff[i] + g * i;
+               rb[i] = (M.rcnt[i] + g) * 8;
             }
-            send_wait_ms += 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            // the exchange window: from the first copy's issue (after any wait)
-            if (st == AMG_OK && first && hipEventRecord(tx0(k), cs) != hipSuccess)
-               st = amg_set_error(AMG_ERR_HIP, "amg_dist_async_jacobi: event");
-            first = false;
-            if (st == AMG_OK)
-               st = link_send(D->ajac_links, 0, M.peers[i], sbuf + (size_t)q * SS + M.soff[i], M.scnt[i], cs);
+            if ((st = xp_p2p(c, cs, np, M.peers.data(), sp.data(), sb.data(), rp.data(), rb.data())) != AMG_OK)
+               break;
+            AMG_HIP(hipEventRecord(sent[q], cs));
+            AMG_HIP(hipEventRecord(arrived[q], cs));
+            pending.push_back(k);
          }
-         if (st == AMG_OK && first) AMG_HIP(hipEventRecord(tx0(k), cs));
-         if (st != AMG_OK) break;
          AMG_HIP(hipEventRecord(tx1(k), cs));
-         AMG_HIP(hipEventRecord(sent[q], cs));
-         // r -= A_diag e (ghost region of e_ext stays zero), overlapping the sends
+         // r -= A_diag e (ghost region of e_ext stays zero), overlapping the exchange
          AMG_HIP(hipEventRecord(ti0(k), s));
          amgk::spgemv(s, M.A, eext, r, upd, r, 0, n, nullptr);
          AMG_HIP(hipEventRecord(ti1(k), s));
-         if ((st = poll_links(k, false)) != AMG_OK) break;
+         // deltas that have already arrived (host poll: never blocks)
+         for (size_t i = 0; i < pending.size();) {
+            if (hipEventQuery(arrived[pending[i] % AJ_NBUF]) == hipSuccess) {
+               if ((st = apply(pending[i])) != AMG_OK) break;
+               pending.erase(pending.begin() + i);
+            } else {
+               break; // in order: later slots cannot have arrived first
+            }
+         }
          D->iter = k + 1;
-         continue;
       }
-      if (np > 0) {
-         if (sps) { // the norm travels with the deltas (data[vec_len + 1], DMEM_Comm.cpp:216-220)
-            const long long m = std::max<long long>(M.nsend, np);
-            sps_pack_k<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(eext, M.d_send_idx, M.nsend, d_soff, np, snorm + q,
-                                                                    sbuf + (size_t)q * SS);
-         } else {
-            launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * SS, (int)M.nsend);
-         }
-         AMG_HIP(hipEventRecord(packed[q], s));
-         AMG_HIP(hipStreamWaitEvent(cs, packed[q], 0));
-         AMG_HIP(hipEventRecord(tx0(k), cs));
-         std::vector<void *> sp(np), rp(np);
-         std::vector<long long> sb(np), rb(np);
-         const int g = sps ? 1 : 0;
-         for (int i = 0; i < np; i++) {
-            sp[i] = sbuf + (size_t)q * SS + M.soff[i] + g * i;
-            sb[i] = (M.scnt[i] + g) * 8;
-            rp[i] = rbuf + (size_t)q * RS + M.roff[i] + g * i;
-            rb[i] = (M.rcnt[i] + g) * 8;
-         }
-         if ((st = xp_p2p(c, cs, np, M.peers.data(), sp.data(), sb.data(), rp.data(), rb.data())) != AMG_OK)
-            break;
-         AMG_HIP(hipEventRecord(sent[q], cs));
-         AMG_HIP(hipEventRecord(arrived[q], cs));
-         pending.push_back(k);
+      for (size_t i = 0; st == AMG_OK && i < pending.size(); i++) st = apply(pending[i]); // drain
+      if (use_links && st == AMG_OK) {
+         st = poll_links(sweeps, true); // the deltas still in flight, each applied once
+         if (st == AMG_OK) st = link_drain(D->ajac_links, 0);
+         for (int i = 0; i < np && st == AMG_OK; i++)
+            if (M.rcnt[i] > 0 && got_cnt[i] != sweeps)
+               st = amg_set_error(AMG_ERR_RCCL, "amg_dist_async_jacobi: %lld deltas from rank %d, expected %d",
+                                  got_cnt[i], M.peers[i], sweeps);
       }
-      AMG_HIP(hipEventRecord(tx1(k), cs));
-      // r -= A_diag e (ghost region of e_ext stays zero), overlapping the exchange
-      AMG_HIP(hipEventRecord(ti0(k), s));
-      amgk::spgemv(s, M.A, eext, r, upd, r, 0, n, nullptr);
-      AMG_HIP(hipEventRecord(ti1(k), s));
-      // deltas that have already arrived (host poll: never blocks)
-      for (size_t i = 0; i < pending.size();) {
-         if (hipEventQuery(arrived[pending[i] % AJ_NBUF]) == hipSuccess) {
-            if ((st = apply(pending[i])) != AMG_OK) break;
-            pending.erase(pending.begin() + i);
-         } else {
-            break; // in order: later slots cannot have arrived first
-         }
-      }
-      D->iter = k + 1;
-   }
-   for (size_t i = 0; st == AMG_OK && i < pending.size(); i++) st = apply(pending[i]); // drain
-   if (use_links && st == AMG_OK) {
-      st = poll_links(sweeps, true); // the deltas still in flight, each applied once
-      if (st == AMG_OK) st = link_drain(D->ajac_links, 0);
-      for (int i = 0; i < np && st == AMG_OK; i++)
-         if (M.rcnt[i] > 0 && got_cnt[i] != sweeps)
-            st = amg_set_error(AMG_ERR_RCCL, "amg_dist_async_jacobi: %lld deltas from rank %d, expected %d",
-                               got_cnt[i], M.peers[i], sweeps);
-      if (st != AMG_OK) link_abort(D->ajac_links);
-   }
+      return st;
+   };
+   st = sweep_all();
+   if (st != AMG_OK && use_links) link_abort(D->ajac_links);
    for (int q = 0; q < AJ_NBUF; q++) {
       hipEventDestroy(packed[q]);
       hipEventDestroy(sent[q]);

@@ -134,6 +134,8 @@ struct AsyncLevel {
 // in level group k, 0 = no channel (the sets are symmetric by construction)
 struct LinkSet;
 int link_create(amg_dist_hier *D, int K, const std::vector<long long> &caps, LinkSet **out, int nslots = 2);
+int link_single_node(amg_dist_hier *D, bool *one);
+double link_timeout_s(); // AMG_LINK_TIMEOUT_S, default 300
 // collective: sequence numbers back to 0 before a solve; one_thread: every
 // level group driven by the calling thread (a deterministic schedule)
 int link_reset(LinkSet *L, bool one_thread);

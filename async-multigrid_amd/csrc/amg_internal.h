@@ -119,45 +119,108 @@ struct AmgCorrTimes {
    // device execution windows of the update kernels (stamp_begin / stamp_end
    // in the kernel that adds correction j of level k into the shared vector):
    // [k][j] start / end in ms of the device wall clock (an arbitrary origin
-   // common to every stream and process on the device); NaN: not stamped
+   // common to every stream and process on the device); NaN: not stamped.
+   // Record of correction (k, j): 4 words -- window start, window end, the
+   // device address of its per-row stamp array (0: none), unused.
    unsigned long long *d_st = nullptr;
    int st_cap = 0, st_L = 0;
    std::vector<std::vector<double>> w0, w1;
-   int stamps_begin(hipStream_t s, int L, int cap)
+   // per-row update times (stamp_row: the low 32 bits of the device wall clock
+   // at which row i's add + read of the shared vector completed) of the first
+   // rows_j corrections of every level; rows_ms[k][j]: nrow times in ms, on the
+   // window clock (empty: not recorded)
+   unsigned *d_rows = nullptr;
+   size_t rows_alloc = 0;
+   int nrow = 0, rows_j = 0;
+   std::vector<std::vector<std::vector<double>>> rows_ms;
+   std::vector<unsigned long long> h_init;
+   // row stamps are taken while nrow * L * rows_j * 4 B stays within this
+   static constexpr size_t kRowBudget = (size_t)256 << 20;
+   // koff[k]: the index of owned row 0 in the vector the update kernel of
+   // level k indexes (a slab level-0 vector with its ghost planes in front)
+   int stamps_begin(hipStream_t s, int L, int cap, int n_rows = 0, const std::vector<long long> &koff = {})
    {
       if (!d_st || L * cap > st_L * st_cap) {
          if (d_st) hipFree(d_st);
          d_st = nullptr;
-         if (hipMalloc((void **)&d_st, (size_t)2 * L * cap * sizeof(unsigned long long)) != hipSuccess) return -1;
+         if (hipMalloc((void **)&d_st, (size_t)4 * L * cap * sizeof(unsigned long long)) != hipSuccess) return -1;
       }
       st_L = L;
       st_cap = cap;
-      amgk::stamp_init(s, d_st, L * cap);
+      nrow = n_rows > 0 ? n_rows : 0;
+      rows_j = nrow > 0 ? (int)std::min<size_t>(cap, kRowBudget / ((size_t)nrow * L * 4)) : 0;
+      const size_t need = (size_t)nrow * L * rows_j;
+      if (need > rows_alloc) {
+         if (d_rows) hipFree(d_rows);
+         d_rows = nullptr;
+         rows_alloc = 0;
+         if (hipMalloc((void **)&d_rows, need * sizeof(unsigned)) != hipSuccess) {
+            rows_j = 0;
+         } else {
+            rows_alloc = need;
+         }
+      }
+      h_init.assign((size_t)4 * L * cap, 0ull);
+      for (int k = 0; k < L; k++)
+         for (int j = 0; j < cap; j++) {
+            unsigned long long *w = &h_init[4 * ((size_t)k * cap + j)];
+            w[0] = ~0ull;
+            if (j < rows_j) {
+               const long long o = k < (int)koff.size() ? koff[k] : 0;
+               w[2] = (unsigned long long)(uintptr_t)(d_rows + ((size_t)k * rows_j + j) * nrow - o);
+            }
+         }
+      if (hipMemcpyAsync(d_st, h_init.data(), h_init.size() * sizeof(unsigned long long), hipMemcpyHostToDevice,
+                         s) != hipSuccess)
+         return -1;
+      if (rows_j > 0 && hipMemsetAsync(d_rows, 0, need * sizeof(unsigned), s) != hipSuccess) return -1;
       return 0;
    }
    unsigned long long *stamp(int k, int j) const
    {
-      return (d_st && k >= 0 && k < st_L && j >= 0 && j < st_cap) ? d_st + 2 * ((size_t)k * st_cap + j) : nullptr;
+      return (d_st && k >= 0 && k < st_L && j >= 0 && j < st_cap) ? d_st + 4 * ((size_t)k * st_cap + j) : nullptr;
    }
    // after the solve (the stream has finished): windows of the first cnt[k]
-   // corrections of every level
+   // corrections of every level, and their row times where recorded
    int stamps_collect(const std::vector<int> &cnt, int wall_khz)
    {
       w0.assign(st_L, {});
       w1.assign(st_L, {});
+      rows_ms.assign(st_L, {});
       if (!d_st) return 0;
-      std::vector<unsigned long long> h((size_t)2 * st_L * st_cap);
+      std::vector<unsigned long long> h((size_t)4 * st_L * st_cap);
       if (hipMemcpy(h.data(), d_st, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
          return -1;
       const double tpm = wall_khz > 0 ? (double)wall_khz : 1e5; // ticks per ms
+      std::vector<unsigned> hr((size_t)nrow);
       for (int k = 0; k < st_L && k < (int)cnt.size(); k++)
          for (int j = 0; j < cnt[k] && j < st_cap; j++) {
-            const unsigned long long a = h[2 * ((size_t)k * st_cap + j)], b = h[2 * ((size_t)k * st_cap + j) + 1];
+            const unsigned long long a = h[4 * ((size_t)k * st_cap + j)], b = h[4 * ((size_t)k * st_cap + j) + 1];
             const bool ok = a != ~0ull && b != 0ull;
             w0[k].push_back(ok ? (double)a / tpm : std::numeric_limits<double>::quiet_NaN());
             w1[k].push_back(ok ? (double)b / tpm : std::numeric_limits<double>::quiet_NaN());
+            if (!ok || j >= rows_j || nrow == 0) continue;
+            if (hipMemcpy(hr.data(), d_rows + ((size_t)k * rows_j + j) * nrow, (size_t)nrow * sizeof(unsigned),
+                          hipMemcpyDeviceToHost) != hipSuccess)
+               return -1;
+            // unwrap the low 32 bits around the window start (|dt| < 21 s)
+            if ((int)rows_ms[k].size() != j) continue;
+            std::vector<double> t((size_t)nrow);
+            for (int i = 0; i < nrow; i++) {
+               const int d = (int)(hr[i] - (unsigned)a);
+               t[i] = ((double)a + (double)d) / tpm;
+            }
+            rows_ms[k].push_back(std::move(t));
          }
       return 0;
+   }
+   // per-row times of correction j of level k: nrow values, or 0 if not recorded
+   int rows_of(int k, int j, double *out, int cap) const
+   {
+      if (k < 0 || k >= (int)rows_ms.size() || j < 0 || j >= (int)rows_ms[k].size()) return 0;
+      const int n = std::min(cap, (int)rows_ms[k][j].size());
+      if (out) std::copy(rows_ms[k][j].begin(), rows_ms[k][j].begin() + n, out);
+      return n;
    }
    ~AmgCorrTimes()
    {
@@ -165,6 +228,7 @@ struct AmgCorrTimes {
          for (auto &v : *vv)
             for (auto e : v) hipEventDestroy(e);
       if (d_st) hipFree(d_st);
+      if (d_rows) hipFree(d_rows);
    }
 };
 // anchored operators (interpolation, restriction): row 2t+1's anchor minus

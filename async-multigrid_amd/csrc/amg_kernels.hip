@@ -1691,18 +1691,38 @@ __device__ __forceinline__ void stamp_end(unsigned long long *st)
       if (threadIdx.x == 0) atomicMax(st + 1, (unsigned long long)wall_clock64());
    }
 }
+// per-row update times (AmgCorrTimes::stamps_begin: word 2 of the record is the
+// row array, indexed like the updated vector, or 0): the low 32 bits of the
+// device wall clock when the row's add + read of the shared vector completed,
+// so a free race's replay can order every row's updates exactly
+__device__ __forceinline__ unsigned *stamp_rows(const unsigned long long *st)
+{
+   return st ? reinterpret_cast<unsigned *>(static_cast<uintptr_t>(st[2])) : nullptr;
+}
+__device__ __forceinline__ void stamp_row(unsigned *rs, long long i)
+{
+   if (rs) rs[i] = (unsigned)wall_clock64();
+}
 
 // The FULL_ASYNC update u_i += e_i with the level's copy of the updated row.
 // The reference's form (SMEM_Async_AMG.cpp:296-299): an atomic add, then a
-// read of u_i -- here a no-return device-scope add, the wave's wait for it,
-// and an L1-bypassing read (AMG_ATOMIC_NORET=1, default); the capture form
-// takes the returned value + e_i (AMG_ATOMIC_NORET=0).  Alone (one stream)
-// both give the same bits.
+// read of u_i.  Default (AMG_ATOMIC_NORET=0): the capture form -- the
+// device-scope add returns the value it replaced, and the level's copy is
+// that value + e_i, i.e. u_i right after this add: the interleaving of the
+// reference's race in which no other group's add falls between a thread's
+// add and its read.  Every row's copy then matches one order of whole adds,
+// which the per-row stamps record, so a free race replays exactly
+// (tests/async_band.py row_replay).  AMG_ATOMIC_NORET=1 keeps the literal
+// form: a no-return add, the wave's wait for it, an L1-bypassing read.  On
+// gfx950 that read is not ordered after the add's completion at the memory
+// side (the wait covers its acknowledgement): one-rank races with the read
+// form ended 0.02-3.95x their exact replay, the capture form 0.91-1.00
+// (profiles/r06/races).  Alone (one stream) both give the same bits.
 static int atomic_noret_mode()
 {
    static const int m = [] {
       const char *v = std::getenv("AMG_ATOMIC_NORET");
-      return v ? std::atoi(v) : 1;
+      return v ? std::atoi(v) : 0;
    }();
    return m;
 }
@@ -2431,6 +2451,7 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
    // may land between a row's add and its read, as in the per-row form)
    constexpr bool noret = OUT == 3 || OUT == 4;
    stamp_begin(stamp);
+   unsigned *rst = stamp_rows(stamp);
    // fine planes [zlo, zhi) of the nx * ny * nz box; out / u_priv / the
    // operator's rows (pattern bytes) have plane 0 = fine plane fz0, e plane 0
    // = coarse plane cz0 (a z-slab's extended vectors; the whole box: 0, nz, 0, 0)
@@ -2515,11 +2536,15 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
             if (OUT == 3) {
                wait_vm_all();
                *reinterpret_cast<v2du *>(u_priv + row) = v2d{read_agent(out + row), read_agent(out + row + 1)};
+               stamp_row(rst, row);
+               stamp_row(rst, row + 1);
             }
          } else {
             const double q0 = atomicAdd(out + row, o.x);
             const double q1 = atomicAdd(out + row + 1, o.y);
             *reinterpret_cast<v2du *>(u_priv + row) = v2d{q0 + o.x, q1 + o.y};
+            stamp_row(rst, row);
+            stamp_row(rst, row + 1);
          }
       } else {
          *reinterpret_cast<v2du *>(out + row) = v2d{uo.x + 1.0 * o.x, uo.y + 1.0 * o.y};
@@ -2536,6 +2561,8 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
       for (int k = k0; k < k1; k++) {
          const unsigned row = (unsigned)(k - fz0) * P + pos;
          *reinterpret_cast<v2du *>(u_priv + row) = v2d{read_agent(out + row), read_agent(out + row + 1)};
+         stamp_row(rst, row);
+         stamp_row(rst, row + 1);
       }
    }
    stamp_end(stamp);
@@ -3337,7 +3364,7 @@ __device__ __forceinline__ double div_rcp(double x, double d, double y)
 __device__ __forceinline__ bool div_rcp_ok(double x)
 {
    const double ax = fabs(x);
-   return (ax >= 0x1p-960 && ax < 0x1p+1000) || __double_as_longlong(x) == 0;
+   return (ax >= 0x1p-960 && ax < 0x1p+960) || __double_as_longlong(x) == 0;
 }
 __device__ __forceinline__ v2d jac_div2(v2d num, v2d a, double dq, double rq)
 {
@@ -4028,7 +4055,7 @@ void spgemv(hipStream_t s, const amg_mat *A, const double *x, const double *b, c
 }
 
 // a marched operator's uniform diagonal d whose reciprocal divides exactly
-// (div_rcp): normal, finite, the odd part of its significand below 2^30 (the
+// (div_rcp): normal, finite, 2^-40 <= |d| <= 2^40, the odd part of its significand below 2^30 (the
 // distance of x / d from a rounding midpoint then dwarfs the correction's
 // error); AMG_FAST_DIV=0: off
 static bool fast_div_of(const amg_mat *A, double *d, double *y)
@@ -4044,6 +4071,9 @@ static bool fast_div_of(const amg_mat *A, double *d, double *y)
    if (!std::isnormal(a)) return false;
    int e = 0;
    const double m = std::frexp(std::fabs(a), &e); // [0.5, 1)
+   // |d| in [2^-40, 2^40]: with div_rcp_ok's |x| in [2^-960, 2^960) every
+   // quotient x / d and product x * (1/d) stays normal and finite
+   if (e < -39 || e > 40) return false;
    unsigned long long sig = (unsigned long long)std::ldexp(m, 53);
    while (sig && !(sig & 1)) sig >>= 1;
    if (sig >= (1ull << 30)) return false;
@@ -4959,6 +4989,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WP
                                                        unsigned long long *stamp = nullptr)
 {
    stamp_begin(stamp);
+   unsigned *rst = stamp_rows(stamp);
    static_assert(C == 8 || C == 16, "lane groups inside DPP rows");
    constexpr int B = 64 / C;
    // UNR (small levels, latency-bound): the whole row's loads in one batch and
@@ -5135,11 +5166,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WP
       carry = __shfl(v, q * C + C - 1, 64);
       // a_ii == 0: the row keeps its value (0 after the zero-guess reset)
       if (act && (a != 0.0 || zero)) __hip_atomic_store(u + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // apply_u: the FULL_ASYNC correction folded in (the reference's add, then read)
-      if (apply_u && act) add_noret(apply_u + i, v);
-      if (apply_u) {
-         wait_vm_all();
-         if (act) apply_priv[i] = read_agent(apply_u + i);
+      // apply_u: the FULL_ASYNC correction folded in (the reference's add, then
+      // read, in the capture form: atomic_noret_mode)
+      if (apply_u && act) {
+         const double o = atomicAdd(apply_u + i, v);
+         apply_priv[i] = o + v;
+         stamp_row(rst, i);
       }
    }
    stamp_end(stamp);
@@ -5159,7 +5191,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WP
 // value row.  Tails past TMAX slots are re-read from memory at the step.  The
 // operations and their order are the reference's sequential loop's
 // (SMEM_Smooth.cpp:265-304 / 548-585): bit-identical.  Any row length.
-template <int NB, int CH, int TMAX, bool VI, bool SHORT = false, int NT = 256, int OCC = 1, bool NORET = true>
+template <int NB, int CH, int TMAX, bool VI, bool SHORT = false, int NT = 256, int OCC = 1, bool NORET = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(OCC))) void hybrid_jgs_tile_k(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                          const double *__restrict__ val,
                                                          const unsigned char *__restrict__ vidx,
@@ -5172,6 +5204,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(OCC))) void 
 {
    constexpr bool noret = NORET;
    stamp_begin(stamp);
+   unsigned *rst = stamp_rows(stamp);
    constexpr int SP = NB + 1, NS = CH * SP, RPT = NB * CH / NT;
    static_assert(NB == 64 && (NB * CH) % NT == 0, "one phase-2 wave, whole rows per lane");
    __shared__ double sP[NS], sOld[NS], sD[NS], sV[NS];
@@ -5435,6 +5468,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(OCC))) void 
             } else if (apply_u) {
                const double o = atomicAdd(apply_u + i, v);
                apply_priv[i] = o + v;
+               stamp_row(rst, i);
             }
          }
       }
@@ -5447,6 +5481,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(OCC))) void 
             if (pos < ne - ns) {
                const int i = reverse ? ne - 1 - pos : ns + pos;
                apply_priv[i] = read_agent(apply_u + i);
+               stamp_row(rst, i);
             }
          }
       }
@@ -5917,6 +5952,7 @@ __global__ void atomic_correct_k(double *u, const double *__restrict__ e,
 {
    constexpr bool noret = NORET;
    stamp_begin(stamp);
+   unsigned *rst = stamp_rows(stamp);
    EW_LOOP(i, 0, n)
    {
       const double ei = e[i];
@@ -5928,6 +5964,7 @@ __global__ void atomic_correct_k(double *u, const double *__restrict__ e,
          const double old = atomicAdd(u + i, ei);
          u_priv[i] = old + ei;
       }
+      stamp_row(rst, i);
    }
    stamp_end(stamp);
 }
@@ -5977,6 +6014,7 @@ __global__ void res_update_k(double *r, const double *__restrict__ y, double *__
                              int atomic, unsigned long long *stamp)
 {
    stamp_begin(stamp);
+   unsigned *rst = stamp_rows(stamp);
    EW_LOOP(i, 0, n)
    {
       const double yi = y[i];
@@ -5988,6 +6026,7 @@ __global__ void res_update_k(double *r, const double *__restrict__ y, double *__
          r[i] = v;
       }
       r_priv[i] = v;
+      stamp_row(rst, i);
    }
    stamp_end(stamp);
 }

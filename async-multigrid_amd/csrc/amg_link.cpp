@@ -82,7 +82,9 @@ void launch_copy(hipStream_t s, const double *src, double *dst, long long n)
    link_copy_k<<<(unsigned)nb, 256, 0, s>>>(src, dst, n);
 }
 
-double link_timeout_s()
+} // namespace
+
+double amgd::link_timeout_s()
 {
    static const double t = [] {
       const char *e = std::getenv("AMG_LINK_TIMEOUT_S");
@@ -90,6 +92,8 @@ double link_timeout_s()
    }();
    return t;
 }
+
+namespace {
 
 struct RankInfo {
    long long pid;
@@ -230,20 +234,53 @@ long long host_id()
 
 // caps[k * R + src]: doubles of the largest message src sends me in level
 // group k (0: no channel); identical on the sending side by construction
+// every rank of the job on this node (collective): the device-resident links
+// need it; callers fall back to the transport's send / recv otherwise
+int amgd::link_single_node(amg_dist_hier *D, bool *one)
+{
+   const long long me = host_id();
+   std::vector<char> all;
+   AMG_TRY(allgather_bytes(D, &me, sizeof(me), all));
+   const int R = D->ctx->xport->nranks;
+   *one = true;
+   for (int r = 0; r < R; r++) {
+      long long h = 0;
+      std::memcpy(&h, all.data() + (size_t)r * sizeof(h), sizeof(h));
+      if (h != me) *one = false;
+   }
+   return AMG_OK;
+}
+
+static int link_create_into(amg_dist_hier *D, int K, const std::vector<long long> &caps, LinkSet *L, int nslots);
+
+// *out is set only on success; a failed creation is torn down (collectively,
+// as link_free) and leaves *out null
 int amgd::link_create(amg_dist_hier *D, int K, const std::vector<long long> &caps, LinkSet **out, int nslots)
+{
+   *out = nullptr;
+   AMG_ARG(nslots >= 1 && nslots <= NS_MAX, "link_create: %d slots per channel (1 .. %d)", nslots, NS_MAX);
+   auto *L = new LinkSet();
+   L->D = D;
+   const int st = link_create_into(D, K, caps, L, nslots);
+   if (st != AMG_OK) {
+      const std::string msg = amg_last_error();
+      link_free(L);
+      return amg_set_error(st, "%s", msg.c_str());
+   }
+   *out = L;
+   return AMG_OK;
+}
+
+static int link_create_into(amg_dist_hier *D, int K, const std::vector<long long> &caps, LinkSet *L, int nslots)
 {
    amg_ctx *c = D->ctx;
    const int R = c->xport->nranks, me = c->xport->rank;
-   AMG_ARG(nslots >= 1 && nslots <= NS_MAX, "link_create: %d slots per channel (1 .. %d)", nslots, NS_MAX);
    const int NS = nslots;
-   auto *L = new LinkSet();
    L->ns = NS;
-   L->D = D;
    L->K = K;
    L->R = R;
    L->me = me;
    L->ch.resize((size_t)K * R);
-   *out = L;
    // who shares my process (the control block's home and the slots' kind)
    RankInfo mine{};
    mine.pid = (long long)getpid();

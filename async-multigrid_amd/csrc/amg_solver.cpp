@@ -1476,7 +1476,7 @@ extern "C" int amg_async_solve(amg_hier *H, const amg_vec *f, amg_vec *u, int *l
    // the free race's update windows on the device clock (amg_async_update_windows)
    const bool rec0 = sched == AMG_SCHED_FREE && !(c->graphs && !semi && !read_res && !global_res && !H->o.profile &&
                                                    (o.delay_type == AMG_DELAY_NONE || o.delay_usec <= 0));
-   if (rec0 && H->corr.stamps_begin(c->stream, L, std::max(1, o.num_cycles) * (conv_global ? 16 : 1) + 1))
+   if (rec0 && H->corr.stamps_begin(c->stream, L, std::max(1, o.num_cycles) * (conv_global ? 16 : 1) + 1, n0))
       return amg_set_error(AMG_ERR_OOM, "amg_async_solve: update-window stamps");
    AMG_HIP(hipEventRecord(ready, c->stream));
    AMG_HIP(hipEventRecord(t_start, c->stream));
@@ -1824,6 +1824,14 @@ extern "C" int amg_async_update_windows(const amg_hier *H, int level, double *ms
    const auto &v = level < (int)vv.size() ? vv[level] : std::vector<double>();
    *count = (int)v.size();
    for (int j = 0; j < (int)v.size() && j < cap && ms; j++) ms[j] = v[j];
+   return AMG_OK;
+}
+
+extern "C" int amg_async_update_rows(const amg_hier *H, int level, int corr, double *ms, int cap, int *count)
+{
+   AMG_ARG(H && count && level >= 0 && level < H->L && corr >= 0 && cap >= 0,
+           "amg_async_update_rows: bad argument");
+   *count = H->corr.rows_of(level, corr, ms, cap);
    return AMG_OK;
 }
 

@@ -334,6 +334,14 @@ class DistHier:
         return (_corr_ms(lib.amg_dist_async_update_windows, self.h, self.L, True),
                 _corr_ms(lib.amg_dist_async_update_windows, self.h, self.L, False))
 
+    def async_update_rows(self):
+        """per level: (corrections, n0) per-row update times (ms, the windows' clock) of
+        this rank's rows in the last free race, or None where not recorded
+        (amg_dist_async_update_rows)"""
+        from . import _update_rows
+        counts = [len(w) for w in self.async_update_windows()[1]]
+        return _update_rows(lib.amg_dist_async_update_rows, self.h, counts, self.n0)
+
     def async_level_ms(self):
         """per level: ms from the last async_solve's start to the level's last correction"""
         L = self.gen.L if self.gen is not None else 64

@@ -496,6 +496,11 @@ int amg_async_correction_ms(const amg_hier *H, int level, double *ms, int cap, i
  * (cap >= 0) or start (cap < 0, -cap entries) in ms of that clock, an origin
  * common to every stream and process on the device; NaN where not stamped */
 int amg_async_update_windows(const amg_hier *H, int level, double *ms, int cap, int *count);
+/* the per-row update times of correction `corr` of level `level` in the same race (ms on
+ * the windows' clock: when row i's add into the shared vector and its read-back
+ * completed); *count = the fine rows written (at most cap), 0 where not recorded (rows are
+ * stamped while rows x levels x corrections x 4 B stays within 256 MiB) */
+int amg_async_update_rows(const amg_hier *H, int level, int corr, double *ms, int cap, int *count);
 /* EigsPower SMEM_Cheby.cpp:410-518 with this hierarchy's V-cycle as M^{-1} */
 int amg_eigs_power(amg_hier *H, int iters, double *eig_max, double *eig_min);
 /* profile: accumulated device milliseconds and launch counts of the fine-level
@@ -701,6 +706,7 @@ int amg_dist_hier_set_async_durations(amg_dist_hier *D, const double *ms, int n)
 int amg_dist_hier_set_async_times(amg_dist_hier *D, const double *t, const int *n, int nlev);
 int amg_dist_async_correction_ms(const amg_dist_hier *D, int level, double *ms, int cap, int *count);
 int amg_dist_async_update_windows(const amg_dist_hier *D, int level, double *ms, int cap, int *count);
+int amg_dist_async_update_rows(const amg_dist_hier *D, int level, int corr, double *ms, int cap, int *count);
 /* DMEM_AsyncSmooth (DMEM_Smooth.cpp:16-313) with ASYNC_JACOBI (l1 = 0: u = r ./ (a_ii/omega))
  * or ASYNC_L1_JACOBI (l1 = 1): `sweeps` relaxations of the fine level in residual-update
  * form from x = 0; every relaxation sends its boundary deltas on the communication

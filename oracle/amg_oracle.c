@@ -1706,6 +1706,20 @@ int or_async_add(or_hier *H, const double *f, double *u, const int *nt, int asyn
  * (correction-major); levels with nc[k] = 0 do not correct.  One thread; the
  * arithmetic of each correction is or_async_add's group body with one thread
  * per group. */
+typedef struct {
+   double t;
+   int k, r, x;
+} replay_ev;
+
+static int replay_ev_cmp(const void *pa, const void *pb)
+{
+   const replay_ev *a = (const replay_ev *)pa, *b = (const replay_ev *)pb;
+   if (a->t != b->t) return a->t < b->t ? -1 : 1;
+   if (a->k != b->k) return a->k < b->k ? -1 : 1;
+   if (a->r != b->r) return a->r < b->r ? -1 : 1;
+   return a->x < b->x ? -1 : a->x > b->x;
+}
+
 int or_async_add_replay(or_hier *H, const double *f, double *u, int R, const int *rs, const double *t,
                         const int *nc, int *corrections, double *relres)
 {
@@ -1732,24 +1746,18 @@ int or_async_add_replay(or_hier *H, const double *f, double *u, int R, const int
    }
    off[L] = ne;
    int *ev = (int *)malloc((size_t)(ne > 0 ? ne : 1) * sizeof(int));
-   for (int q = 0; q < ne; q++) ev[q] = q;
-   /* insertion sort by (time, k, r): small event counts */
-   for (int a = 1; a < ne; a++) {
-      const int x = ev[a];
-      int b = a - 1;
-      while (b >= 0) {
-         const int y = ev[b];
-         const double tx = t[x], ty = t[y];
-         int ky = 0, kx = 0;
-         while (ky < L && off[ky + 1] <= y) ky++;
-         while (kx < L && off[kx + 1] <= x) kx++;
-         const int later = ty > tx || (ty == tx && (ky > kx || (ky == kx && (y - off[ky]) % R > (x - off[kx]) % R)));
-         if (!later) break;
-         ev[b + 1] = y;
-         b--;
+   /* sorted by (time, k, r, j) */
+   replay_ev *key = (replay_ev *)malloc((size_t)(ne > 0 ? ne : 1) * sizeof(replay_ev));
+   for (int k = 0; k < L; k++)
+      for (int q = off[k]; q < off[k + 1]; q++) {
+         key[q].t = t[q];
+         key[q].k = k;
+         key[q].r = (q - off[k]) % R;
+         key[q].x = q;
       }
-      ev[b + 1] = x;
-   }
+   qsort(key, (size_t)ne, sizeof(replay_ev), replay_ev_cmp);
+   for (int q = 0; q < ne; q++) ev[q] = key[q].x;
+   free(key);
    double **E = (double **)malloc(L * sizeof(double *)), **uk = (double **)malloc(L * sizeof(double *));
    double **dacc = (double **)malloc(L * sizeof(double *));
    int *jc = (int *)calloc(L, sizeof(int));    /* corrections whose e is formed */

@@ -122,6 +122,8 @@ def test_async_options_band(amg, oracle, ctx, setup, case):
     flo, fhi, orels, _ = oracle_async_band(amg, oracle, host, f, opts, reps=4, blocks=blocks)
     print(f"{'-'.join(case)}: device relres {rels}, max corrections {cmax}; "
           f"oracle free races [{flo:.3e}, {fhi:.3e}] ({fhi / flo:.1f}x)")
+    from async_band import free_band_check
+    free_band_check(amg, opts, rels, flo, fhi, what="-".join(case))
     assert sync_rel < 1.0
     assert widest <= 20.0
     for rel in rels:

@@ -88,6 +88,24 @@ def grid_solve(amg, L, host, f, ppg, transport="host", **kw):
 _bands = {}
 
 
+def dmem_cycle_members(oracle, host, f, opts, cycles):
+    """further band members for grids that ran other cycle counts than the band's
+    runs (converge GLOBAL: every grid keeps correcting until the slowest is done):
+    the DMEM_Add restatement under round robin with converge LOCAL and
+    num_cycles = c for every device cycle count c -- each grid's relres after
+    exactly c cycles of the same protocol"""
+    out = []
+    for c in sorted(set(int(x) for x in cycles)):
+        o = oracle.make_opts(solver=oracle.OR_ASYNC_MULTADD, smooth_weight=opts.smooth_weight, num_cycles=c,
+                             tol=opts.tol)
+        OH = oracle.Hier(host["A"], host["P"], host["R"], o)
+        _, _, rel, _ = OH.dmem_add(f, sched=1, converge_type=oracle.OR_CONVERGE_LOCAL, async_type=opts.async_type,
+                                   max_inflight=opts.max_inflight, save_divisor=opts.async_comm_save_divisor,
+                                   tol=opts.tol)
+        out += rel.tolist()
+    return out
+
+
 def dmem_band(oracle, host, f, opts, reps=10, sequential=False):
     """the band of the DMEM_Add restatement (oracle or_dmem_add: grids as
     threads, one rank per grid, the same AddCycle / message protocol /
@@ -147,7 +165,7 @@ def test_grid_add_round_robin_bitwise(amg, oracle, mult24, conv, at, inflight, s
 @pytest.mark.parametrize("ppg,conv,inflight", [((1, 1, 1, 1), "local", 1), ((2, 1, 1, 1), "global", 2),
                                                ((2, 2, 1, 1), "local", 3)])
 def test_grid_add_converges(amg, oracle, mult24, ppg, conv, inflight, transport):
-    from async_band import in_band, in_rate_band
+    from async_band import in_band
     L, host, f = mult24
     ppg = ppg[:L] if len(ppg) >= L else ppg + (1,) * (L - len(ppg))
     N = 20
@@ -164,6 +182,11 @@ def test_grid_add_converges(amg, oracle, mult24, ppg, conv, inflight, transport)
     if key not in _bands:
         _bands[key] = dmem_band(oracle, host, f, opts, sequential=True)
     lo, hi, brels, bcycs = _bands[key]
+    # grids that ran other cycle counts than the band's runs: the restatement's
+    # relres after exactly that many cycles joins the band
+    extra = dmem_cycle_members(oracle, host, f, opts, [cyc for _, _, _, cyc, _, _ in res if cyc not in bcycs])
+    if extra:
+        lo, hi = min([lo] + extra), max([hi] + extra)
     n = host["A"][0].nrows
     xs = {}
     sent = recv = 0
@@ -173,9 +196,7 @@ def test_grid_add_converges(amg, oracle, mult24, ppg, conv, inflight, transport)
     for g, row0, x, cyc, rel, msgs in res:
         assert np.all(np.isfinite(x))
         assert cyc >= N
-        # the residual band, or (a grid that ran more / fewer cycles than the
-        # band's runs) the band of per-cycle contraction rates
-        assert in_band(rel, lo, hi) or in_rate_band(rel, cyc, brels, bcycs), (g, rel, cyc, lo, hi)
+        assert in_band(rel, lo, hi), (g, rel, cyc, lo, hi)
         sent += int(msgs[0])
         recv += int(msgs[1])
         xs.setdefault(g, np.zeros(n))[row0:row0 + x.size] = x

@@ -275,4 +275,6 @@ def test_async_multadd_band(amg, oracle, ctx):
     print(f"async multadd: oracle free races [{flo:.4e}, {fhi:.4e}] ({len(orels)} runs), sync {sync_rel:.4e}, "
           f"device {rels}")
     replay_check(amg, oracle, host, f, opts, durs, what="async multadd")
+    from async_band import free_band_check
+    free_band_check(amg, opts, rels, flo, fhi, what="async multadd")
     assert max(rels) < 1.0

@@ -440,6 +440,49 @@ def test_torn_replay_model(amg, oracle):
     assert list(c[:L - 1]) == cnt[:L - 1], c
 
 
+def test_row_replay_model(amg, oracle):
+    """async_band.row_replay (the exact replay of a row-stamped free race): rows
+    that saw the same update order are merged into one slice, which changes
+    nothing -- the merged replay is bit-identical to the replay with one slice
+    per row; untorn tables (every row updated at its correction's time) give one
+    slice and the whole-correction replay; torn tables (two levels' update
+    kernels overlapping, their 64-row waves interleaved in random order) give
+    a different iterate that still converges."""
+    from async_band import row_order_slices, row_replay, _replay_slices
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, 12, amg.AMG_INTERP_LINEAR)
+    N = 6
+    opts = amg.default_opts(solver=amg.AMG_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=N, tol=0.0)
+    n0 = 12 ** 3
+    f = amg.rhs_rand(0, n0)
+    d = np.array([3.0 / (1.9 ** k) + 0.05 for k in range(L)])
+    ends = [d[k] * np.arange(1, N + 1) for k in range(L - 1)] + [np.zeros(0)]
+    flat = [[np.repeat(e[:, None], n0, axis=1) for e in ends]]
+    cuts, tabs = row_order_slices(flat, L)
+    assert cuts == [0, n0] and len(tabs) == 1
+    OH = oracle.Hier(host["A"], host["P"], host["R"], oracle.make_opts(
+        solver=oracle.OR_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=N, tol=0.0))
+    _, rel1, _ = OH.async_add_replay(f, [0, n0], [e[:, None] for e in ends])
+    relf, nsl = row_replay(amg, oracle, host, f, opts, flat)
+    assert nsl == 1 and relf == rel1
+    # torn: level 0's update j = 2 (9.15) overlaps level 1's update j = 5
+    # (9.78); waves of 64 rows of each run at random times inside the overlap
+    g = np.random.default_rng(5)
+    torn = [[t.copy() for t in flat[0]]]
+    mid = 0.5 * (ends[0][2] + ends[1][5])
+    assert ends[0][1] < mid - 0.01 and ends[0][3] > mid + 0.01 and ends[1][4] < mid - 0.01
+    for w in range(0, n0, 64):
+        torn[0][0][2, w:w + 64] = mid + g.uniform(-0.01, 0.01)
+        torn[0][1][5, w:w + 64] = mid + g.uniform(-0.01, 0.01)
+    cuts, tabs = row_order_slices(torn, L)
+    assert 2 < len(tabs) <= n0 // 64
+    relm, _ = row_replay(amg, oracle, host, f, opts, torn)
+    per_row = [[torn[0][k][:, i] for k in range(L)] for i in range(n0)]
+    relr = _replay_slices(amg, oracle, host, f, opts, list(range(n0 + 1)), per_row)
+    assert relm == relr
+    assert relm != rel1 and relm < 0.5, (relm, rel1)
+
+
 def test_composed_transfers_match_explicit(amg, oracle):
     """or_hier_set_composed_transfers: the smoothed transfers applied composed
     from the plain P / R (R~ r = R (r - w A D^-1 r), P~ e = P e - w D^-1 A P e)
@@ -545,16 +588,3 @@ def test_dmem_add_sequential_schedules(amg, oracle, sched):
     print(f"dmem_add sequential {sched}: relres {rel}; round robin {rr[2]}")
     with pytest.raises(Exception):
         OH.dmem_add(f, sched=sched, converge_type=oracle.OR_CONVERGE_GLOBAL)
-
-
-def test_rate_band():
-    """async_band.in_rate_band: a residual below every band run's, reached in more
-    cycles at the band's per-cycle contraction, is in the rate band; the same
-    residual reached in as few cycles as the band's runs, or a stalled one, is not"""
-    from async_band import in_band, in_rate_band
-    rels = [1.2e-8, 3.24e-9, 2.4e-8, 1.2e-8]
-    cycs = [23, 25, 22, 23]
-    assert not in_band(1.0e-9, min(rels), max(rels))
-    assert in_rate_band(1.0e-9, 26, rels, cycs)       # one more cycle at the band's rate
-    assert not in_rate_band(1.0e-9, 20, rels, cycs)   # too fast for its cycles
-    assert not in_rate_band(1.0e-3, 25, rels, cycs)   # stalled
