@@ -75,21 +75,24 @@ def _corr_ms(fn, h, L, start=False):
         out.append(ms[:int(cnt[0])])
     return out
 
-def _update_rows(fn, h, counts, n):
+def _update_rows(fn, h, counts, n, vals=False):
     """per level: (corrections, n) per-row update times (ms) of its first recorded
     corrections in the last free race (rows stamped by the update kernels), or None
-    for a level whose corrections were not all row-stamped"""
+    for a level whose corrections were not all row-stamped; vals: (corrections, n, 2)
+    -- every row's (old, new) value of each add"""
     out = []
-    buf = np.zeros(max(1, n))
+    w = 2 * n if vals else n
+    buf = np.zeros(max(1, w))
     cnt = np.zeros(1, dtype=np.int32)
     for k, m in enumerate(counts):
         rows = []
         for j in range(int(m)):
-            check(fn(h, k, j, _dp(buf), n, _ip(cnt)))
-            if int(cnt[0]) != n:
+            check(fn(h, k, j, _dp(buf), -w if vals else w, _ip(cnt)))
+            if int(cnt[0]) != w:
                 break
-            rows.append(buf[:n].copy())
-        out.append(np.array(rows).reshape(len(rows), n) if len(rows) == int(m) else None)
+            rows.append(buf[:w].copy())
+        shape = (len(rows), n, 2) if vals else (len(rows), n)
+        out.append(np.array(rows).reshape(shape) if len(rows) == int(m) else None)
     return out
 
 
@@ -381,11 +384,17 @@ class Hier:
         return (_corr_ms(lib.amg_async_update_windows, self.h, self.L, True),
                 _corr_ms(lib.amg_async_update_windows, self.h, self.L, False))
 
-    def async_update_rows(self, n0):
+    def async_update_rows(self):
         """per level: (corrections, n0) per-row update times (ms, the windows' clock) of
         the last free race, or None where not recorded (amg_async_update_rows)"""
         counts = [len(w) for w in self.async_update_windows()[1]]
-        return _update_rows(lib.amg_async_update_rows, self.h, counts, n0)
+        return _update_rows(lib.amg_async_update_rows, self.h, counts, self.n0)
+
+    def async_update_vals(self):
+        """per level: (corrections, n0, 2) -- every row's (old, new) value of each add in
+        the last free race (NaN: not recorded), or None (amg_async_update_rows, cap < 0)"""
+        counts = [len(w) for w in self.async_update_windows()[1]]
+        return _update_rows(lib.amg_async_update_rows, self.h, counts, self.n0, vals=True)
 
     def eigs_power(self, iters):
         emax, emin = C.c_double(), C.c_double()

@@ -837,9 +837,9 @@ extern "C" int amg_dist_async_update_windows(const amg_dist_hier *D, int level, 
 extern "C" int amg_dist_async_update_rows(const amg_dist_hier *D, int level, int corr, double *ms, int cap,
                                           int *count)
 {
-   AMG_ARG(D && count && level >= 0 && level < D->L && corr >= 0 && cap >= 0,
+   AMG_ARG(D && count && level >= 0 && level < D->L && corr >= 0,
            "amg_dist_async_update_rows: bad argument");
-   *count = D->corr.rows_of(level, corr, ms, cap);
+   *count = D->corr.rows_of(level, corr, ms, cap < 0 ? -cap : cap, cap < 0);
    return AMG_OK;
 }
 

@@ -130,12 +130,13 @@ struct AmgCorrTimes {
    // rows_j corrections of every level; rows_ms[k][j]: nrow times in ms, on the
    // window clock (empty: not recorded)
    unsigned *d_rows = nullptr;
+   double *d_vals = nullptr; // per row: the value each add replaced and the value it left
    size_t rows_alloc = 0;
    int nrow = 0, rows_j = 0;
-   std::vector<std::vector<std::vector<double>>> rows_ms;
+   std::vector<std::vector<std::vector<double>>> rows_ms, rows_vals;
    std::vector<unsigned long long> h_init;
-   // row stamps are taken while nrow * L * rows_j * 4 B stays within this
-   static constexpr size_t kRowBudget = (size_t)256 << 20;
+   // row stamps are taken while nrow * L * rows_j * 20 B stays within this
+   static constexpr size_t kRowBudget = (size_t)512 << 20;
    // koff[k]: the index of owned row 0 in the vector the update kernel of
    // level k indexes (a slab level-0 vector with its ghost planes in front)
    int stamps_begin(hipStream_t s, int L, int cap, int n_rows = 0, const std::vector<long long> &koff = {})
@@ -148,13 +149,17 @@ struct AmgCorrTimes {
       st_L = L;
       st_cap = cap;
       nrow = n_rows > 0 ? n_rows : 0;
-      rows_j = nrow > 0 ? (int)std::min<size_t>(cap, kRowBudget / ((size_t)nrow * L * 4)) : 0;
+      rows_j = nrow > 0 ? (int)std::min<size_t>(cap, kRowBudget / ((size_t)nrow * L * 20)) : 0;
       const size_t need = (size_t)nrow * L * rows_j;
       if (need > rows_alloc) {
          if (d_rows) hipFree(d_rows);
+         if (d_vals) hipFree(d_vals);
          d_rows = nullptr;
+         d_vals = nullptr;
          rows_alloc = 0;
-         if (hipMalloc((void **)&d_rows, need * sizeof(unsigned)) != hipSuccess) {
+         if (hipMalloc((void **)&d_rows, need * sizeof(unsigned)) != hipSuccess ||
+             hipMalloc((void **)&d_vals, 2 * need * sizeof(double)) != hipSuccess) {
+            (void)hipGetLastError();
             rows_j = 0;
          } else {
             rows_alloc = need;
@@ -168,12 +173,15 @@ struct AmgCorrTimes {
             if (j < rows_j) {
                const long long o = k < (int)koff.size() ? koff[k] : 0;
                w[2] = (unsigned long long)(uintptr_t)(d_rows + ((size_t)k * rows_j + j) * nrow - o);
+               w[3] = (unsigned long long)(uintptr_t)(d_vals + 2 * (((size_t)k * rows_j + j) * nrow - o));
             }
          }
       if (hipMemcpyAsync(d_st, h_init.data(), h_init.size() * sizeof(unsigned long long), hipMemcpyHostToDevice,
                          s) != hipSuccess)
          return -1;
       if (rows_j > 0 && hipMemsetAsync(d_rows, 0, need * sizeof(unsigned), s) != hipSuccess) return -1;
+      // NaN: a row whose update recorded no values (the no-return form)
+      if (rows_j > 0 && hipMemsetAsync(d_vals, 0xff, 2 * need * sizeof(double), s) != hipSuccess) return -1;
       return 0;
    }
    unsigned long long *stamp(int k, int j) const
@@ -187,6 +195,7 @@ struct AmgCorrTimes {
       w0.assign(st_L, {});
       w1.assign(st_L, {});
       rows_ms.assign(st_L, {});
+      rows_vals.assign(st_L, {});
       if (!d_st) return 0;
       std::vector<unsigned long long> h((size_t)4 * st_L * st_cap);
       if (hipMemcpy(h.data(), d_st, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
@@ -211,15 +220,22 @@ struct AmgCorrTimes {
                t[i] = ((double)a + (double)d) / tpm;
             }
             rows_ms[k].push_back(std::move(t));
+            std::vector<double> v((size_t)2 * nrow);
+            if (hipMemcpy(v.data(), d_vals + 2 * ((size_t)k * rows_j + j) * nrow, v.size() * sizeof(double),
+                          hipMemcpyDeviceToHost) != hipSuccess)
+               return -1;
+            rows_vals[k].push_back(std::move(v));
          }
       return 0;
    }
-   // per-row times of correction j of level k: nrow values, or 0 if not recorded
-   int rows_of(int k, int j, double *out, int cap) const
+   // per-row times of correction j of level k: nrow values, or 0 if not
+   // recorded; vals: the 2 nrow (old, new) values instead
+   int rows_of(int k, int j, double *out, int cap, bool vals = false) const
    {
-      if (k < 0 || k >= (int)rows_ms.size() || j < 0 || j >= (int)rows_ms[k].size()) return 0;
-      const int n = std::min(cap, (int)rows_ms[k][j].size());
-      if (out) std::copy(rows_ms[k][j].begin(), rows_ms[k][j].begin() + n, out);
+      const auto &src = vals ? rows_vals : rows_ms;
+      if (k < 0 || k >= (int)src.size() || j < 0 || j >= (int)src[k].size()) return 0;
+      const int n = std::min(cap, (int)src[k][j].size());
+      if (out) std::copy(src[k][j].begin(), src[k][j].begin() + n, out);
       return n;
    }
    ~AmgCorrTimes()
@@ -229,6 +245,7 @@ struct AmgCorrTimes {
             for (auto e : v) hipEventDestroy(e);
       if (d_st) hipFree(d_st);
       if (d_rows) hipFree(d_rows);
+      if (d_vals) hipFree(d_vals);
    }
 };
 // anchored operators (interpolation, restriction): row 2t+1's anchor minus

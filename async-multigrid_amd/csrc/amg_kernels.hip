@@ -1695,13 +1695,29 @@ __device__ __forceinline__ void stamp_end(unsigned long long *st)
 // row array, indexed like the updated vector, or 0): the low 32 bits of the
 // device wall clock when the row's add + read of the shared vector completed,
 // so a free race's replay can order every row's updates exactly
-__device__ __forceinline__ unsigned *stamp_rows(const unsigned long long *st)
+// Word 3: the row values array -- [2i] the value the add replaced, [2i + 1]
+// the value it left (the capture form's returned value and that + e_i): per
+// row they chain the updates of all levels in their actual order (each add's
+// old value is the previous add's new value), which the replay follows
+// where two levels' updates of one row came too close for the clock
+struct RowRec {
+   unsigned *t;
+   double *v;
+};
+__device__ __forceinline__ RowRec stamp_rows(const unsigned long long *st)
 {
-   return st ? reinterpret_cast<unsigned *>(static_cast<uintptr_t>(st[2])) : nullptr;
+   if (!st) return RowRec{nullptr, nullptr};
+   return RowRec{reinterpret_cast<unsigned *>(static_cast<uintptr_t>(st[2])),
+                 reinterpret_cast<double *>(static_cast<uintptr_t>(st[3]))};
 }
-__device__ __forceinline__ void stamp_row(unsigned *rs, long long i)
+__device__ __forceinline__ void stamp_row(const RowRec &r, long long i)
 {
-   if (rs) rs[i] = (unsigned)wall_clock64();
+   if (r.t) r.t[i] = (unsigned)wall_clock64();
+}
+__device__ __forceinline__ void stamp_row(const RowRec &r, long long i, double old, double nw)
+{
+   if (r.t) r.t[i] = (unsigned)wall_clock64();
+   if (r.v) *reinterpret_cast<v2du *>(r.v + 2 * i) = v2d{old, nw};
 }
 
 // The FULL_ASYNC update u_i += e_i with the level's copy of the updated row.
@@ -2451,7 +2467,7 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
    // may land between a row's add and its read, as in the per-row form)
    constexpr bool noret = OUT == 3 || OUT == 4;
    stamp_begin(stamp);
-   unsigned *rst = stamp_rows(stamp);
+   const RowRec rst = stamp_rows(stamp);
    // fine planes [zlo, zhi) of the nx * ny * nz box; out / u_priv / the
    // operator's rows (pattern bytes) have plane 0 = fine plane fz0, e plane 0
    // = coarse plane cz0 (a z-slab's extended vectors; the whole box: 0, nz, 0, 0)
@@ -2543,8 +2559,8 @@ __global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
             const double q0 = atomicAdd(out + row, o.x);
             const double q1 = atomicAdd(out + row + 1, o.y);
             *reinterpret_cast<v2du *>(u_priv + row) = v2d{q0 + o.x, q1 + o.y};
-            stamp_row(rst, row);
-            stamp_row(rst, row + 1);
+            stamp_row(rst, row, q0, q0 + o.x);
+            stamp_row(rst, row + 1, q1, q1 + o.y);
          }
       } else {
          *reinterpret_cast<v2du *>(out + row) = v2d{uo.x + 1.0 * o.x, uo.y + 1.0 * o.y};
@@ -4989,7 +5005,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WP
                                                        unsigned long long *stamp = nullptr)
 {
    stamp_begin(stamp);
-   unsigned *rst = stamp_rows(stamp);
+   const RowRec rst = stamp_rows(stamp);
    static_assert(C == 8 || C == 16, "lane groups inside DPP rows");
    constexpr int B = 64 / C;
    // UNR (small levels, latency-bound): the whole row's loads in one batch and
@@ -5171,7 +5187,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WP
       if (apply_u && act) {
          const double o = atomicAdd(apply_u + i, v);
          apply_priv[i] = o + v;
-         stamp_row(rst, i);
+         stamp_row(rst, i, o, o + v);
       }
    }
    stamp_end(stamp);
@@ -5204,7 +5220,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(OCC))) void 
 {
    constexpr bool noret = NORET;
    stamp_begin(stamp);
-   unsigned *rst = stamp_rows(stamp);
+   const RowRec rst = stamp_rows(stamp);
    constexpr int SP = NB + 1, NS = CH * SP, RPT = NB * CH / NT;
    static_assert(NB == 64 && (NB * CH) % NT == 0, "one phase-2 wave, whole rows per lane");
    __shared__ double sP[NS], sOld[NS], sD[NS], sV[NS];
@@ -5468,7 +5484,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(OCC))) void 
             } else if (apply_u) {
                const double o = atomicAdd(apply_u + i, v);
                apply_priv[i] = o + v;
-               stamp_row(rst, i);
+               stamp_row(rst, i, o, o + v);
             }
          }
       }
@@ -5952,7 +5968,7 @@ __global__ void atomic_correct_k(double *u, const double *__restrict__ e,
 {
    constexpr bool noret = NORET;
    stamp_begin(stamp);
-   unsigned *rst = stamp_rows(stamp);
+   const RowRec rst = stamp_rows(stamp);
    EW_LOOP(i, 0, n)
    {
       const double ei = e[i];
@@ -5960,11 +5976,12 @@ __global__ void atomic_correct_k(double *u, const double *__restrict__ e,
          add_noret(u + i, ei);
          wait_vm_all();
          u_priv[i] = read_agent(u + i);
+         stamp_row(rst, i);
       } else {
          const double old = atomicAdd(u + i, ei);
          u_priv[i] = old + ei;
+         stamp_row(rst, i, old, old + ei);
       }
-      stamp_row(rst, i);
    }
    stamp_end(stamp);
 }
@@ -6014,19 +6031,22 @@ __global__ void res_update_k(double *r, const double *__restrict__ y, double *__
                              int atomic, unsigned long long *stamp)
 {
    stamp_begin(stamp);
-   unsigned *rst = stamp_rows(stamp);
+   const RowRec rst = stamp_rows(stamp);
    EW_LOOP(i, 0, n)
    {
       const double yi = y[i];
       double v;
+      double o;
       if (atomic) {
-         v = atomicAdd(r + i, -yi) - yi;
+         o = atomicAdd(r + i, -yi);
+         v = o - yi;
       } else {
-         v = r[i] - yi;
+         o = r[i];
+         v = o - yi;
          r[i] = v;
       }
       r_priv[i] = v;
-      stamp_row(rst, i);
+      stamp_row(rst, i, o, v);
    }
    stamp_end(stamp);
 }

@@ -1829,9 +1829,9 @@ extern "C" int amg_async_update_windows(const amg_hier *H, int level, double *ms
 
 extern "C" int amg_async_update_rows(const amg_hier *H, int level, int corr, double *ms, int cap, int *count)
 {
-   AMG_ARG(H && count && level >= 0 && level < H->L && corr >= 0 && cap >= 0,
+   AMG_ARG(H && count && level >= 0 && level < H->L && corr >= 0,
            "amg_async_update_rows: bad argument");
-   *count = H->corr.rows_of(level, corr, ms, cap);
+   *count = H->corr.rows_of(level, corr, ms, cap < 0 ? -cap : cap, cap < 0);
    return AMG_OK;
 }
 

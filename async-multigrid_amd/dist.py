@@ -342,6 +342,13 @@ class DistHier:
         counts = [len(w) for w in self.async_update_windows()[1]]
         return _update_rows(lib.amg_dist_async_update_rows, self.h, counts, self.n0)
 
+    def async_update_vals(self):
+        """per level: (corrections, n0, 2) -- every row's (old, new) value of each add in
+        the last free race on this rank (NaN: not recorded), or None"""
+        from . import _update_rows
+        counts = [len(w) for w in self.async_update_windows()[1]]
+        return _update_rows(lib.amg_dist_async_update_rows, self.h, counts, self.n0, vals=True)
+
     def async_level_ms(self):
         """per level: ms from the last async_solve's start to the level's last correction"""
         L = self.gen.L if self.gen is not None else 64

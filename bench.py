@@ -38,6 +38,8 @@ def parse():
     p.add_argument("--reuse-outer-residual", type=int, default=2)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-cycles", type=int, default=20)
+    p.add_argument("--cpu-all-cores", type=int, default=1,
+                   help="also time the CPU sample on every host core (os.cpu_count() threads)")
     p.add_argument("--fuse-outer", type=int, default=-1,
                    help="level 0's last post sweep fused with the outer residual (0 off, 1, 2; -1: the library "
                         "default / AMG_FUSE_OUTER)")
@@ -317,12 +319,32 @@ def cpu_baseline(gen, amg, f, args):
     u, hist, k = H.solve(f)
     secs = po.lib().or_last_loop_seconds()
     threads = po.lib().or_num_threads()
+    # OMP_NUM_THREADS=$(nproc), OMP_PROC_BIND=close -- the
+    # same sample again on every host core (os.cpu_count(): the whole machine,
+    # beyond this process's share of it where the box gives it one)
+    allc = None
+    ncpu = os.cpu_count() or 1
+    if args.cpu_all_cores and ncpu > threads:
+        po.lib().or_set_threads(ncpu)
+        try:
+            ua, ha, ka = H.solve(f)
+            sa = po.lib().or_last_loop_seconds()
+            ta = po.lib().or_num_threads()
+            same = bool(np.array_equal(ua.view(np.uint64), u.view(np.uint64)))
+            allc = {"value": ka / sa, "unit": "V-cycle iters/s", "cores": ta, "seconds": sa,
+                    "iterate_same_bits": same,
+                    "sample": f"the same {ka} outer iterations on {ta} threads (OMP_PROC_BIND "
+                              f"{os.environ.get('OMP_PROC_BIND')})"}
+            log(f"[cpu] all cores: {allc['value']:.4f} it/s on {ta} threads")
+        finally:
+            po.lib().or_set_threads(threads)
     del H, host
     return ({"value": k / secs, "unit": "V-cycle iters/s", "cores": threads, "kind": "port",
              "sample": f"{k} outer iterations (V(1,1) Jacobi + residual + norm) of the same "
                        f"{args.n}^3 solve, oracle/amg_oracle.c OpenMP, {threads} threads",
-             "seconds": secs, "host": dict(HOST_INFO, **{k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND",
-                                                                                 "OMP_PLACES")})}, u, hist[-1] / hist[0])
+             "seconds": secs, "all_cores": allc,
+             "host": dict(HOST_INFO, **{k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND",
+                                                                      "OMP_PLACES")})}, u, hist[-1] / hist[0])
 
 
 def check_parity(u_par, u_cpu, rel_cpu, cycles):

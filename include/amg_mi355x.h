@@ -499,7 +499,8 @@ int amg_async_update_windows(const amg_hier *H, int level, double *ms, int cap, 
 /* the per-row update times of correction `corr` of level `level` in the same race (ms on
  * the windows' clock: when row i's add into the shared vector and its read-back
  * completed); *count = the fine rows written (at most cap), 0 where not recorded (rows are
- * stamped while rows x levels x corrections x 4 B stays within 256 MiB) */
+ * stamped while rows x levels x corrections x 20 B stays within 512 MiB); cap < 0: the
+ * 2 n values (old, new) of every row's add instead, -cap entries (NaN where not recorded) */
 int amg_async_update_rows(const amg_hier *H, int level, int corr, double *ms, int cap, int *count);
 /* EigsPower SMEM_Cheby.cpp:410-518 with this hierarchy's V-cycle as M^{-1} */
 int amg_eigs_power(amg_hier *H, int iters, double *eig_max, double *eig_min);

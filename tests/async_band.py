@@ -108,6 +108,7 @@ class Ends(list):
     update times (async_update_rows: per level a (corrections, rows) array, or
     None where the update kernels did not stamp every row)"""
     rows = None
+    vals = None
 
 
 def race_tables(h):
@@ -120,6 +121,7 @@ def race_tables(h):
     if sum(len(x) for x in w1) and all(np.all(np.isfinite(x)) for x in list(w0) + list(w1)):
         e = Ends(w1)
         e.rows = h.async_update_rows()
+        e.vals = h.async_update_vals()
         return e, w0
     return h.async_correction_ms(), h.async_correction_ms(start=True)
 
@@ -139,38 +141,114 @@ def _rows_of(ends, L):
     return out
 
 
-def row_order_slices(rows, L):
+def _vals_of(ends, L):
+    """the per-rank per-row (old, new) value tables of a run's ends, or None"""
+    per = _per_rank(ends)
+    out = []
+    for e in per:
+        v = getattr(e, "vals", None)
+        if v is None or len(v) < L or any(x is None for x in v[:L]):
+            return None
+        out.append(v)
+    return out
+
+
+def chain_order(order, vold, vnew, u0=0.0, window=16):
+    """repair per-row update orders with the values the adds returned: in the
+    true order of a row's adds each add's old value is the previous add's new
+    value (the first's: the initial u0), bit for bit -- the clock orders two
+    levels' adds of one row only to within the adds' latency.  order: (n, E)
+    event indices by time; vold / vnew: (n, E) values by event index.  Rows whose
+    time order already chains are kept; in the others the next add is the one,
+    among the next `window` by time, whose old value is the running value.
+    Returns (order, repaired rows, rows left unchained)"""
+    n, E = order.shape
+    if E == 0:
+        return order, 0, 0
+    so = np.take_along_axis(vold, order, axis=1)
+    sn = np.take_along_axis(vnew, order, axis=1)
+    ok = np.all(so[:, 1:].view(np.uint64) == sn[:, :-1].view(np.uint64), axis=1)
+    ok &= so[:, 0] == u0
+    bad = np.nonzero(~ok)[0]
+    left = 0
+    order = order.copy()
+    for i in bad:
+        rem = list(order[i])
+        cur = np.float64(u0)
+        out = []
+        broken = False
+        while rem:
+            pick = 0
+            for q in range(min(window, len(rem))):
+                if vold[i, rem[q]] == cur and np.float64(vold[i, rem[q]]).tobytes() == cur.tobytes():
+                    pick = q
+                    break
+            else:
+                broken = True
+            x = rem.pop(pick)
+            out.append(x)
+            cur = np.float64(vnew[i, x])
+        order[i] = out
+        left += broken
+    return order, len(bad), left
+
+
+def row_order_slices(rows, L, vals=None, u0=0.0):
     """cut the fine rows into the fewest slices inside which every row received
     the corrections of all levels in the same order (rows: per rank, per level a
-    (corrections, rank rows) array of update times; ranks' rows in order).
-    Returns (cuts, per-slice per-level time arrays): the times of a slice are its
-    first row's, so or_async_add_replay applies every slice's updates in exactly
-    the order its rows saw them"""
+    (corrections, rank rows) array of update times; ranks' rows in order; vals:
+    the same layout of (old, new) values, which repair the time order where the
+    clock cannot tell two adds apart, chain_order).  Returns (cuts, per-slice
+    per-level time arrays, (repaired rows, unchained rows)): a slice's times are
+    its first row's, reassigned so that sorting them gives that row's order --
+    or_async_add_replay applies every slice's updates in exactly the order its
+    rows saw them"""
     nc = [min(r[k].shape[0] for r in rows) for k in range(L)]
-    T = []
+    T, VO, VN = [], [], []
     for k in range(L):
         T.append(np.concatenate([np.asarray(r[k], dtype=np.float64)[:nc[k]] for r in rows], axis=1)
                  if nc[k] else None)
+        if vals is not None and nc[k]:
+            v = np.concatenate([np.asarray(r[k], dtype=np.float64)[:nc[k]] for r in vals], axis=1)
+            VO.append(v[:, :, 0])
+            VN.append(v[:, :, 1])
     n = sum(np.asarray(r[0]).shape[1] for r in rows)
     cols = [T[k].T for k in range(L) if T[k] is not None]
     M = np.concatenate(cols, axis=1) if cols else np.zeros((n, 0))
     order = np.argsort(M, axis=1, kind="stable")
+    stats = (0, 0)
+    if vals is not None and VO:
+        vo = np.concatenate([x.T for x in VO], axis=1)
+        vn = np.concatenate([x.T for x in VN], axis=1)
+        if np.all(np.isfinite(vo)) and np.all(np.isfinite(vn)):
+            order, nrep, nleft = chain_order(order, vo, vn, u0)
+            stats = (nrep, nleft)
     change = np.any(order[1:] != order[:-1], axis=1) if len(order) > 1 else np.zeros(0, dtype=bool)
     starts = [0] + [int(i) + 1 for i in np.nonzero(change)[0]]
     cuts = starts + [n]
+    # event index -> (level, correction)
+    ev = [(k, j) for k in range(L) if T[k] is not None for j in range(nc[k])]
     tabs = []
     for a in starts:
-        tabs.append([T[k][:, a] if T[k] is not None else np.zeros(0) for k in range(L)])
-    return cuts, tabs
+        ts = np.sort(M[a])
+        tab = [np.zeros(nc[k]) if T[k] is not None else np.zeros(0) for k in range(L)]
+        for m, x in enumerate(order[a]):
+            k, j = ev[x]
+            tab[k][j] = ts[m]
+        tabs.append(tab)
+    return cuts, tabs, stats
 
 
-def row_replay(amg, oracle, host, f, opts, rows, composed=False, blocks=None):
+def row_replay(amg, oracle, host, f, opts, rows, composed=False, blocks=None, vals=None):
     """the oracle's exact replay of a free race whose update kernels stamped every
     row: or_async_add_replay with one slice per run of rows that saw the same
-    update order (row_order_slices).  Returns (relres, slices)"""
+    update order (row_order_slices; vals: the adds' values, which fix the order
+    of adds the clock cannot separate).  Returns (relres, slices, (repaired rows,
+    unchained rows))"""
     L = len(host["A"])
-    cuts, tabs = row_order_slices(rows, L)
-    return _replay_slices(amg, oracle, host, f, opts, cuts, tabs, composed=composed, blocks=blocks), len(tabs)
+    cuts, tabs, stats = row_order_slices(rows, L, vals=vals)
+    rel = _replay_slices(amg, oracle, host, f, opts, cuts, tabs, composed=composed, blocks=blocks)
+    return rel, len(tabs), stats
 
 
 def _per_rank(x):
@@ -365,9 +443,10 @@ def replay_check(amg, oracle, host, f, opts, runs, blocks=None, composed=False, 
         rows = _rows_of(corr_ms, L) if sliceable else None
         tm = None
         if rows is not None:
-            lo, nsl = row_replay(amg, oracle, host, f, opts, rows, composed=composed, blocks=blocks)
+            lo, nsl, (nrep, nleft) = row_replay(amg, oracle, host, f, opts, rows, composed=composed, blocks=blocks,
+                                                vals=_vals_of(corr_ms, L))
             hi, rr = lo, [lo]
-            model = f"row replay, {nsl} slice(s)"
+            model = f"row replay, {nsl} slice(s), {nrep} row(s) reordered by value, {nleft} unchained"
         else:
             if rs is not None and len(rs) > 2:
                 lo = hi = sliced_replay(amg, oracle, host, f, opts, corr_ms, rs, composed=composed, blocks=blocks)

@@ -444,10 +444,11 @@ def test_async_replay_bitwise(amg, oracle, ctx, setup, case):
               read_type=amg.AMG_READ_RES if rt == "res" else amg.AMG_READ_SOL,
               res_compute_type=amg.AMG_GLOBAL if rc == "global" else amg.AMG_LOCAL,
               converge_test_type=amg.AMG_GLOBAL if ct == "global" else amg.AMG_LOCAL)
-    opts = amg.default_opts(**kw)
-    H, _ = gpu_hier(amg, ctx, host, opts)
+    opts_free = amg.default_opts(**kw)
+    H, _ = gpu_hier(amg, ctx, host, opts_free)
     _, rel_free, cnt_free = H.async_solve(f)
     times = times_of(H.async_correction_ms(), L)
+    race = race_tables(H)
     H.free()
     opts = amg.default_opts(async_schedule=4, **kw)
     H, _ = gpu_hier(amg, ctx, host, opts)
@@ -473,4 +474,7 @@ def test_async_replay_bitwise(amg, oracle, ctx, setup, case):
           f"oracle {relo:.13e}, counts {list(cnt[k_lo:k_hi])} / {list(cnto[k_lo:k_hi])}, differing {nd}")
     assert list(cnt[k_lo:k_hi]) == list(cnto[k_lo:k_hi])
     assert nd == 0
-    assert in_band(rel_free, relo, relo)
+    # the free race itself against the replay of its own update order (the
+    # update kernels' row stamps where the options allow the exact replay)
+    replay_check(amg, oracle, host, f, opts_free, [(rel_free, race[0], None, race[1])],
+                 what=f"free race {'-'.join(case)}")

@@ -465,6 +465,63 @@ def test_dist_async_jacobi(amg, oracle, ctx, nranks, l1):
     gen.free()
 
 
+def test_dist_async_jacobi_one_way_peers(amg, oracle, ctx):
+    """DMEM_AsyncSmooth on a pattern-nonsymmetric operator (upwind: the 7-pt
+    Laplacian's lower triangle, a_ij = 0 for j > i): rank 0's rows read no
+    ghost column, rank 1's read rank 0's -- rank 0 only sends, rank 1 only
+    receives.  The device-resident channels carry both directions (every delta
+    applied once: the incrementally kept residual is f - A x); rank 0's rows
+    depend on rank 0's alone, so they are synchronous Jacobi's (rounding aside:
+    residual-update form); rank 1's see rank 0's deltas late, and the whole
+    iterate still contracts."""
+    from test_gpu_solve import hierarchy
+    _, L, host = hierarchy(amg, oracle, 16, amg.AMG_INTERP_LINEAR)
+    A0 = host["A"][0]
+    rp, cj, cv = [0], [], []
+    for i in range(A0.nrows):
+        for q in range(A0.rowptr[i], A0.rowptr[i + 1]):
+            if A0.col[q] <= i:
+                cj.append(A0.col[q])
+                cv.append(A0.val[q])
+        rp.append(len(cj))
+    up = oracle.Csr(A0.nrows, A0.ncols, np.array(rp), np.array(cj, dtype=np.int32), np.array(cv))
+    host = {"A": [up] + host["A"][1:], "P": host["P"], "R": host["R"]}
+    n = up.nrows
+    f = amg.rhs_rand(0, n)
+    K, w = 12, 0.7
+    u = np.zeros(n)
+    for _ in range(K):
+        oracle.smem_jacobi(up, f, u, np.zeros(n), w, 1, 0, 0, n)
+    ref_rel = np.linalg.norm(f - oracle.smem_matvec(up, u, np.zeros(n))) / np.linalg.norm(f)
+    rs, parts = split_host(host, (0.5,))
+    hub = amg.dist.ThreadMailbox(2)
+    opts = amg.default_opts(smooth_weight=w)
+
+    def rank(q):
+        c = amg.Context(0, nstreams=2)
+        amg.dist.init_host(c, 2, q, amg.dist.HostTransport(hub, q))
+        A, P, R = parts[q]
+        D = amg.dist.DistHier.from_parts(c, rs, A, P, R, opts)
+        rel = D.async_jacobi(f[D.row0:D.row0 + D.n0], K)
+        st = D.async_jacobi_stats()
+        x = D.get_u()
+        row0 = D.row0
+        D.free()
+        amg.dist.finalize(c)
+        c.close()
+        return rel, st, x, row0
+
+    res = sorted(run_ranks(2, rank), key=lambda t: t[3])
+    for rel, st, x, row0 in res:
+        print(f"one-way peers: rank at row {row0}: relres {rel:.6e} (sync {ref_rel:.6e}), {st}")
+        assert np.all(np.isfinite(x))
+        assert st["device_links"] == 1.0, st
+        assert abs(st["incremental_resnorm"] - st["true_resnorm"]) <= 1e-9 * st["true_resnorm"], st
+        assert rel < 0.1, rel
+    x0 = res[0][2]
+    np.testing.assert_allclose(x0, u[:x0.size], rtol=1e-9, atol=1e-12 * np.abs(u).max())
+
+
 # ---------------------------------------------------------------------------
 # DMEM outer acceleration (DMEM_ChebyUpdate, DMEM_Misc.cpp:612-666)
 # ---------------------------------------------------------------------------

@@ -458,12 +458,12 @@ def test_row_replay_model(amg, oracle):
     d = np.array([3.0 / (1.9 ** k) + 0.05 for k in range(L)])
     ends = [d[k] * np.arange(1, N + 1) for k in range(L - 1)] + [np.zeros(0)]
     flat = [[np.repeat(e[:, None], n0, axis=1) for e in ends]]
-    cuts, tabs = row_order_slices(flat, L)
+    cuts, tabs, _ = row_order_slices(flat, L)
     assert cuts == [0, n0] and len(tabs) == 1
     OH = oracle.Hier(host["A"], host["P"], host["R"], oracle.make_opts(
         solver=oracle.OR_ASYNC_MULTADD, smooth_weight=0.8, num_cycles=N, tol=0.0))
     _, rel1, _ = OH.async_add_replay(f, [0, n0], [e[:, None] for e in ends])
-    relf, nsl = row_replay(amg, oracle, host, f, opts, flat)
+    relf, nsl, _ = row_replay(amg, oracle, host, f, opts, flat)
     assert nsl == 1 and relf == rel1
     # torn: level 0's update j = 2 (9.15) overlaps level 1's update j = 5
     # (9.78); waves of 64 rows of each run at random times inside the overlap
@@ -474,13 +474,34 @@ def test_row_replay_model(amg, oracle):
     for w in range(0, n0, 64):
         torn[0][0][2, w:w + 64] = mid + g.uniform(-0.01, 0.01)
         torn[0][1][5, w:w + 64] = mid + g.uniform(-0.01, 0.01)
-    cuts, tabs = row_order_slices(torn, L)
+    cuts, tabs, _ = row_order_slices(torn, L)
     assert 2 < len(tabs) <= n0 // 64
-    relm, _ = row_replay(amg, oracle, host, f, opts, torn)
+    relm, _, _ = row_replay(amg, oracle, host, f, opts, torn)
     per_row = [[torn[0][k][:, i] for k in range(L)] for i in range(n0)]
     relr = _replay_slices(amg, oracle, host, f, opts, list(range(n0 + 1)), per_row)
     assert relm == relr
     assert relm != rel1 and relm < 0.5, (relm, rel1)
+
+
+def test_chain_order():
+    """async_band.chain_order: a row whose adds the clock put in the wrong order
+    is put back in the order its adds' values chain in (each add's old value the
+    previous add's new value); rows that already chain are left alone."""
+    from async_band import chain_order
+    e = np.array([1.0, 2.0, 0.5])
+    # true order 2, 0, 1 from u0 = 0
+    old = np.zeros(3)
+    new = np.zeros(3)
+    cur = 0.0
+    for x in (2, 0, 1):
+        old[x], new[x] = cur, cur + e[x]
+        cur = new[x]
+    vo = np.stack([old, np.array([0.0, 1.0, 3.0])])
+    vn = np.stack([new, np.array([1.0, 3.0, 3.5])])
+    order = np.array([[0, 1, 2], [0, 1, 2]])
+    got, nrep, nleft = chain_order(order, vo, vn)
+    assert got[0].tolist() == [2, 0, 1] and got[1].tolist() == [0, 1, 2]
+    assert (nrep, nleft) == (1, 0)
 
 
 def test_composed_transfers_match_explicit(amg, oracle):
