@@ -38,8 +38,9 @@ def parse():
     p.add_argument("--reuse-outer-residual", type=int, default=2)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-cycles", type=int, default=20)
-    p.add_argument("--cpu-all-cores", type=int, default=1,
-                   help="also time the CPU sample on every host core (os.cpu_count() threads)")
+    p.add_argument("--cpu-all-cores", type=int, default=3,
+                   help="outer iterations of the CPU sample also timed on every host core "
+                        "(os.cpu_count() threads); 0: off")
     p.add_argument("--fuse-outer", type=int, default=-1,
                    help="level 0's last post sweep fused with the outer residual (0 off, 1, 2; -1: the library "
                         "default / AMG_FUSE_OUTER)")
@@ -324,20 +325,25 @@ def cpu_baseline(gen, amg, f, args):
     # beyond this process's share of it where the box gives it one)
     allc = None
     ncpu = os.cpu_count() or 1
-    if args.cpu_all_cores and ncpu > threads:
+    if args.cpu_all_cores > 0 and ncpu > threads:
+        # a shorter sample: where the process's CPU share is smaller than the
+        # machine (a GPU box's slice) these threads oversubscribe it
+        HA = po.Hier(host["A"], host["P"], host["R"],
+                     po.make_opts(smooth_weight=args.smooth_weight, num_cycles=args.cpu_all_cores, tol=0.0))
         po.lib().or_set_threads(ncpu)
         try:
-            ua, ha, ka = H.solve(f)
+            ua, ha, ka = HA.solve(f)
             sa = po.lib().or_last_loop_seconds()
             ta = po.lib().or_num_threads()
-            same = bool(np.array_equal(ua.view(np.uint64), u.view(np.uint64)))
             allc = {"value": ka / sa, "unit": "V-cycle iters/s", "cores": ta, "seconds": sa,
-                    "iterate_same_bits": same,
-                    "sample": f"the same {ka} outer iterations on {ta} threads (OMP_PROC_BIND "
-                              f"{os.environ.get('OMP_PROC_BIND')})"}
+                    "affinity_cpus": HOST_INFO.get("affinity_cpus"),
+                    "sample": f"{ka} outer iterations of the same solve on {ta} threads = os.cpu_count() "
+                              f"(OMP_PROC_BIND {os.environ.get('OMP_PROC_BIND')}; this process may run on "
+                              f"{HOST_INFO.get('affinity_cpus')} of them)"}
             log(f"[cpu] all cores: {allc['value']:.4f} it/s on {ta} threads")
         finally:
             po.lib().or_set_threads(threads)
+            del HA
     del H, host
     return ({"value": k / secs, "unit": "V-cycle iters/s", "cores": threads, "kind": "port",
              "sample": f"{k} outer iterations (V(1,1) Jacobi + residual + norm) of the same "
