@@ -216,6 +216,7 @@ PROTOTYPES = {
     "amg_dist_async_update_rows": (_i, [_p, _i, _i, _dp, _i, _ip]),
     "amg_dist_async_jacobi": (_i, [_p, _dp, _i, _i, _dp]),
     "amg_dist_async_jacobi_stats": (_i, [_p, _dp, _i]),
+    "amg_dist_async_jacobi_log": (_i, [_p, _dp, _i, _ip]),
     "amg_dist_async_sps": (_i, [_p, _dp, _i, _dp, C.POINTER(C.c_longlong)]),
     "amg_rand_double_stream": (_i, [C.c_uint, _i, _d, _d, _dp]),
     "amg_dist_structured_row_starts": (_i, [_p, _i, _llp]),

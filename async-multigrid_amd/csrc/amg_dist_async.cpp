@@ -1027,6 +1027,14 @@ extern "C" int amg_dist_async_jacobi(amg_dist_hier *D, const double *f_local, in
    return async_jacobi_run(D, f_local, sweeps, l1, false, relres, nullptr);
 }
 
+extern "C" int amg_dist_async_jacobi_log(const amg_dist_hier *D, double *events, int cap, int *count)
+{
+   AMG_ARG(D && count && cap >= 0, "amg_dist_async_jacobi_log: bad argument");
+   *count = (int)(D->ajac_log.size() / 5);
+   for (int i = 0; i < (int)D->ajac_log.size() && i < 5 * cap && events; i++) events[i] = D->ajac_log[i];
+   return AMG_OK;
+}
+
 extern "C" int amg_dist_async_jacobi_stats(const amg_dist_hier *D, double *stats, int n)
 {
    AMG_ARG(D && stats && n >= 0, "amg_dist_async_jacobi_stats: bad argument");
@@ -1166,6 +1174,11 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
    }
    if (use_links && (st = link_reset(D->ajac_links, true)) != AMG_OK) return fail(st);
    std::vector<long long> got_cnt(np, 0);
+   D->ajac_log.clear();
+   auto logev = [&](int type, double a, double b = 0.0, double c = 0.0, double d = 0.0) {
+      if (sps) return;
+      for (double v : {(double)type, a, b, c, d}) D->ajac_log.push_back(v);
+   };
    long long on_time = 0, late = 0;
    double send_wait_ms = 0.0; // host time a send waited for its slot (flow control)
    // r -= A_offd g on the rows that have ghost columns (outside the interior [b0, b1))
@@ -1191,6 +1204,7 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
             if (!got) break;
             if (got_cnt[i] == k) on_time++;
             else late++;
+            logev(3, M.peers[i], (double)got_cnt[i]);
             got_cnt[i]++;
             apply_offd();
             amgk::vset(s, gext + no + M.roff[i], 0.0, 0, M.rcnt[i]);
@@ -1211,6 +1225,7 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
                                 hipMemcpyDeviceToDevice, s));
       }
       amgk::spgemv(s, M.A, gext, r, upd, r, 0, n, nullptr); // r -= A_offd g
+      logev(4, k);
       return AMG_OK;
    };
    // the sweeps, the drain and the final checks; every failure after this point
@@ -1242,6 +1257,7 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
                                           count);
          }
          ajac_update_k<<<nb, 256, 0, s>>>(r, wv, eext, x, dacc, n, am, om1, omd, gate);
+         logev(1, k, am, om1, omd);
          if (use_links) {
             if (np > 0) {
                launch_gather(s, eext, M.d_send_idx, sbuf + (size_t)q * SS, (int)M.nsend);
@@ -1279,6 +1295,7 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
             // r -= A_diag e (ghost region of e_ext stays zero), overlapping the sends
             AMG_HIP(hipEventRecord(ti0(k), s));
             amgk::spgemv(s, M.A, eext, r, upd, r, 0, n, nullptr);
+            logev(2, k);
             AMG_HIP(hipEventRecord(ti1(k), s));
             if ((st = poll_links(k, false)) != AMG_OK) break;
             D->iter = k + 1;
@@ -1314,6 +1331,7 @@ int async_jacobi_run(amg_dist_hier *D, const double *f_local, int sweeps, int l1
          // r -= A_diag e (ghost region of e_ext stays zero), overlapping the exchange
          AMG_HIP(hipEventRecord(ti0(k), s));
          amgk::spgemv(s, M.A, eext, r, upd, r, 0, n, nullptr);
+         logev(2, k);
          AMG_HIP(hipEventRecord(ti1(k), s));
          // deltas that have already arrived (host poll: never blocks)
          for (size_t i = 0; i < pending.size();) {

@@ -228,6 +228,13 @@ struct amg_dist_hier {
    // amg_dist_async_jacobi_stats: the last asynchronous Jacobi run's overlap
    // and delta accounting
    std::vector<double> ajac_stats;
+   // the last DMEM_AsyncSmooth run's schedule, 5 doubles per event in the
+   // order its work entered the compute stream: {1, sweep, accel mode, om1,
+   // omd} the relaxation update, {2, sweep} the interior product, {3, peer,
+   // delta index} one peer's ghost delta applied, {4, sweep} every peer's
+   // deltas of that sweep applied (the transport path); empty under SPS
+   // (its gate is decided on the device)
+   std::vector<double> ajac_log;
    std::vector<amg_mat *> cA, cP, cR; // replicated levels' operators (level Ld + i)
    std::vector<double *> cl1;         // and their l1 norms
    // DMEM_Mult with acceleration (accel_type != 0): x (the iterate; lv[0].u

@@ -372,6 +372,16 @@ class DistHier:
                 "late_deltas", "incremental_resnorm", "true_resnorm", "device_links", "send_wait_ms_per_sweep")
         return dict(zip(keys, st.tolist()))
 
+    def async_jacobi_log(self):
+        """the last async_jacobi run's schedule on this rank: (events, 5) array --
+        [1, sweep, accel mode, om1, omd] update, [2, sweep] interior product,
+        [3, peer, j] peer's delta j applied, [4, sweep] all peers' deltas of a sweep"""
+        cnt = np.zeros(1, dtype=np.int32)
+        check(lib.amg_dist_async_jacobi_log(self.h, None, 0, _ip(cnt)))
+        ev = np.zeros(max(1, 5 * int(cnt[0])))
+        check(lib.amg_dist_async_jacobi_log(self.h, _dp(ev), int(cnt[0]), _ip(cnt)))
+        return ev[:5 * int(cnt[0])].reshape(int(cnt[0]), 5)
+
     def async_sps(self, f_local, sweeps):
         """-smoother async_sps (stochastic parallel Southwell gating of the
         asynchronous Jacobi, opts.sps_*): (relres, sweeps this rank relaxed in)."""

@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--seq-cycles", type=int, default=200,
                    help="outer iterations of the config-1 (64^3) SEQ leg on one core, and of its GPU rate")
     p.add_argument("--spmv-reps", type=int, default=20)
+    p.add_argument("--ajac-ranks", type=int, default=2,
+                   help="ranks (processes) of the DMEM_AsyncSmooth overlap leg on the same operator; <2: off")
+    p.add_argument("--ajac-sweeps", type=int, default=12)
     p.add_argument("--force-dist", type=int, default=0,
                    help="run the distributed (RCCL) path even at one rank")
     p.add_argument("--dist-form", choices=("slab", "rows"), default="slab",
@@ -303,6 +306,31 @@ def general_csr_vcycle(amg, gen, f_host, args):
     return out
 
 
+def async_jacobi_overlap(args):
+    """DMEM_AsyncSmooth (DMEM_Smooth.cpp:16-313) on the same 512^3 operator as
+    args.ajac_ranks row-partitioned ranks, one PROCESS each on this GPU (the
+    production layout: every process with the box's default hardware queues),
+    under torch.distributed.run as child processes (tools/bench_async_jacobi.py):
+    per rank the fraction of each sweep's exchange window (the delta copies on
+    the communication stream) that the interior product on the compute stream
+    covers (amg_dist_async_jacobi_stats), and the sweeps per second"""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.ajac_ranks}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tools", "bench_async_jacobi.py"),
+           "--grid", str(args.n), "--sweeps", str(args.ajac_sweeps), "--omega", str(args.smooth_weight)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if p.returncode != 0:
+        raise RuntimeError(f"async Jacobi leg exit {p.returncode}: {p.stderr[-800:]}")
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    log(f"[ajac] {args.ajac_ranks} processes: {res['sweeps_per_s']:.1f} sweeps/s, exchange hidden "
+        f"{res['hidden_fraction_min']:.3f} (min) / {res['hidden_fraction_mean']:.3f} (mean)")
+    return res
+
+
 def cpu_baseline(gen, amg, f, args):
     """The oracle (C restatement of SMEM_Solve, OpenMP) on the host cores, on a
     bounded sample of the same workload: args.cpu_cycles outer iterations of
@@ -511,6 +539,12 @@ def main():
         M.free()
     ctx.close()
 
+    ajac = None
+    if args.ajac_ranks > 1:
+        try:
+            ajac = async_jacobi_overlap(args)
+        except Exception as e:  # noqa: BLE001
+            log(f"[ajac] failed: {e!r}")
     vgen = None
     if args.general:
         try:
@@ -571,6 +605,7 @@ def main():
         "cpu_baseline": cpu,
         "cpu_baseline_seq": seq,
         "vcycle_general_csr": vgen,
+        "async_jacobi_overlap": ajac,
         "parity": parity,
         "final_relres": rn / r0,
     }

@@ -699,6 +699,12 @@ int amg_dist_async_level_ms(const amg_dist_hier *D, double *ms);
  * ms per sweep a send waited for its channel slot (flow control; the
  * exchange window [1] starts at the first copy's issue, after that wait) */
 int amg_dist_async_jacobi_stats(const amg_dist_hier *D, double *stats, int n);
+/* the last amg_dist_async_jacobi's schedule on this rank: *count events of 5 doubles each, in
+ * the order their work entered the compute stream -- {1, sweep, accel mode, om1, omd} the
+ * relaxation update, {2, sweep} the interior product, {3, peer rank, delta index} one peer's
+ * ghost delta applied, {4, sweep} every peer's deltas of that sweep applied (transport path);
+ * the first min(count, cap) events written (0 events after an SPS run) */
+int amg_dist_async_jacobi_log(const amg_dist_hier *D, double *events, int cap, int *count);
 /* AMG_SCHED_TIMED on the distributed solve: level k's time per correction
  * (every rank passes the same values, so every rank issues the same order) */
 int amg_dist_hier_set_async_durations(amg_dist_hier *D, const double *ms, int n);

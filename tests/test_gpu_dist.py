@@ -441,11 +441,12 @@ def test_dist_async_jacobi(amg, oracle, ctx, nranks, l1):
         rel = D.async_jacobi(f[D.row0:D.row0 + D.n0], K, l1)
         x = D.get_u()
         st = D.async_jacobi_stats()
+        log = D.async_jacobi_log()
         row0 = D.row0
         D.free()
         amg.dist.finalize(c)
         c.close()
-        return row0, x, rel, st
+        return row0, x, rel, st, log
 
     res = sorted(run_ranks(nranks, rank), key=lambda t: t[0])
     x = np.concatenate([t[1] for t in res])
@@ -459,9 +460,12 @@ def test_dist_async_jacobi(amg, oracle, ctx, nranks, l1):
     if nranks == 1:  # nothing to wait for: exactly synchronous Jacobi, rounding aside
         np.testing.assert_allclose(res[0][2], ref_rel, rtol=1e-8)
         np.testing.assert_allclose(x, u, rtol=1e-9, atol=1e-12 * np.abs(u).max())
-    else:  # late deltas are applied one relaxation later: a band
-        assert 0.5 * ref_rel <= res[0][2] <= 2.0 * ref_rel, (res[0][2], ref_rel)
-        assert np.all(np.isfinite(x))
+    # the run against the replay of its own schedule (which relaxation of each
+    # peer every rank's residual had seen when it relaxed, tests/ajac_replay.py)
+    from ajac_replay import check_replay, host_csr
+    rs = [t[0] for t in res] + [nr]
+    check_replay(host_csr(nr, nc, rp, cj, cv), f, rs, [t[4] for t in res], x, res[0][2], w,
+                 l1=oracle.l1_norms(A) if l1 else None, what=f"async jacobi {nranks} ranks l1={l1}")
     gen.free()
 
 
@@ -505,14 +509,15 @@ def test_dist_async_jacobi_one_way_peers(amg, oracle, ctx):
         rel = D.async_jacobi(f[D.row0:D.row0 + D.n0], K)
         st = D.async_jacobi_stats()
         x = D.get_u()
+        log = D.async_jacobi_log()
         row0 = D.row0
         D.free()
         amg.dist.finalize(c)
         c.close()
-        return rel, st, x, row0
+        return rel, st, x, row0, log
 
     res = sorted(run_ranks(2, rank), key=lambda t: t[3])
-    for rel, st, x, row0 in res:
+    for rel, st, x, row0, _ in res:
         print(f"one-way peers: rank at row {row0}: relres {rel:.6e} (sync {ref_rel:.6e}), {st}")
         assert np.all(np.isfinite(x))
         assert st["device_links"] == 1.0, st
@@ -520,6 +525,9 @@ def test_dist_async_jacobi_one_way_peers(amg, oracle, ctx):
         assert rel < 0.1, rel
     x0 = res[0][2]
     np.testing.assert_allclose(x0, u[:x0.size], rtol=1e-9, atol=1e-12 * np.abs(u).max())
+    from ajac_replay import check_replay, host_csr
+    check_replay(host_csr(n, n, up.rowptr, up.col, up.val), f, [0, res[1][3], n], [t[4] for t in res],
+                 np.concatenate([t[2] for t in res]), res[0][0], w, what="one-way peers")
 
 
 # ---------------------------------------------------------------------------
@@ -606,11 +614,12 @@ def test_dist_async_jacobi_accel(amg, oracle, ctx, nranks, l1, accel, grid):
         D = amg.dist.DistHier(c, gen, opts)
         rel = D.async_jacobi(f[D.row0:D.row0 + D.n0], K, l1)
         x = D.get_u()
+        log = D.async_jacobi_log()
         row0 = D.row0
         D.free()
         amg.dist.finalize(c)
         c.close()
-        return row0, x, rel
+        return row0, x, rel, log
 
     res = sorted(run_ranks(nranks, rank), key=lambda t: t[0])
     x = np.concatenate([t[1] for t in res])
@@ -620,10 +629,16 @@ def test_dist_async_jacobi_accel(amg, oracle, ctx, nranks, l1, accel, grid):
     if x_o is not None and nranks == 1:
         assert_bitwise(x, x_o, "accelerated async Jacobi (one rank)")
         np.testing.assert_allclose(rel, rn_o / fn, rtol=1e-12)
+        if grid == 0:
+            assert rel < rn_plain / fn  # the momentum helps on the Laplacian
     elif x_o is not None:
-        assert 0.5 * rn_o / fn <= rel <= 2.0 * rn_o / fn, (rel, rn_o / fn)
-    if grid == 0:
-        assert rel < rn_plain / fn  # the momentum helps on the Laplacian
+        print(f"accelerated async jacobi {nranks} ranks: relres {rel:.4e}, one rank {rn_o / fn:.4e}")
+    # more ranks: late ghost deltas; the run against the replay of its own
+    # schedule with the same ChebyUpdate coefficients (tests/ajac_replay.py)
+    from ajac_replay import check_replay, host_csr
+    rs = [t[0] for t in res] + [nr]
+    check_replay(host_csr(nr, nc, rp, cj, cv), f, rs, [t[3] for t in res], x, rel, w, l1=l1n,
+                 what=f"accelerated async jacobi {nranks} ranks {accel} grid {grid}")
     gen.free()
 
 
