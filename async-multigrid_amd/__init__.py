@@ -172,8 +172,18 @@ class Context:
 
     def set_fuse_outer(self, mode):
         """level 0's last post sweep + the outer residual as one march (0 off, 1 on, 2 on with u'
-        stored only at the end of an iterate batch; bit-identical)"""
+        stored only at the end of an iterate batch, 3 the two sweeps slab by slab over z through the
+        Infinity Cache, u' stored as in 2; bit-identical)"""
         check(lib.amg_set_fuse_outer(self.h, int(mode)))
+
+    def set_outer_slab(self, planes):
+        """planes per z-slab of fuse_outer mode 3"""
+        check(lib.amg_set_outer_slab(self.h, int(planes)))
+
+    def set_long_form(self, form, xcd=1):
+        """long-row CSR kernel: 0 workgroup chunks, 1 / 2 wave-independent chunks of 8 / 16
+        entries per lane, xcd: XCD-contiguous row blocks (bit-identical)"""
+        check(lib.amg_set_long_form(self.h, int(form), int(xcd)))
 
     def set_graphs(self, enable):
         """hipGraphs of the additive cycles' launch-bound loops (bit-identical)."""

@@ -146,6 +146,8 @@ PROTOTYPES = {
     "amg_set_march_lines_gemv": (_i, [_p, _i]),
     "amg_set_march_tuning": (_i, [_p, _i, _i, _i, _i]),
     "amg_set_fuse_outer": (_i, [_p, _i]),
+    "amg_set_outer_slab": (_i, [_p, _i]),
+    "amg_set_long_form": (_i, [_p, _i, _i]),
     "amg_hier_fused_outer": (_i, [_p]),
     "amg_set_graphs": (_i, [_p, _i]),
     "amg_hier_set_opts": (_i, [_p, C.POINTER(AmgOpts)]),

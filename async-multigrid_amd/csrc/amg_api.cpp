@@ -163,7 +163,10 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_FUSE_TRANSFER")) c->fuse_transfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_XFER")) c->fuse_xfer = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_GRAPHS")) c->graphs = std::atoi(v) != 0;
-   if (const char *v = std::getenv("AMG_FUSE_OUTER")) c->fuse_outer = std::max(0, std::min(2, std::atoi(v)));
+   if (const char *v = std::getenv("AMG_LONG_FORM")) c->long_form = std::max(0, std::min(2, std::atoi(v)));
+   if (const char *v = std::getenv("AMG_LONG_XCD")) c->long_xcd = std::atoi(v) != 0;
+   if (const char *v = std::getenv("AMG_OUTER_SLAB")) c->outer_slab = std::max(1, std::atoi(v));
+   if (const char *v = std::getenv("AMG_FUSE_OUTER")) c->fuse_outer = std::max(0, std::min(3, std::atoi(v)));
    if (const char *v = std::getenv("AMG_FUSE_XFP_SLAB")) c->fuse_xfp_slab = std::atoi(v) != 0;
    if (const char *v = std::getenv("AMG_FUSE_PROLONG")) c->fuse_prolong = std::max(0, std::min(7, std::atoi(v)));
    if (const char *v = std::getenv("AMG_JGS_SMALL")) c->jgs_small = std::max(0, std::min(2, std::atoi(v)));
@@ -175,7 +178,7 @@ extern "C" int amg_init(amg_ctx **out, int device, int nstreams)
    if (const char *v = std::getenv("AMG_MZ27_OCC")) c->mz27_occ = std::max(-1, std::min(8, std::atoi(v)));
    if (const char *v = std::getenv("AMG_MZ_OCC")) c->mz_occ = std::max(-1, std::min(8, std::atoi(v)));
    if (const char *v = std::getenv("AMG_MZ_PF")) c->mz_pf = std::atoi(v) == 2 ? 2 : (std::atoi(v) == 1 ? 1 : 3);
-   if (const char *v = std::getenv("AMG_MZ27_PF")) c->mz27_pf = std::atoi(v) == 1 ? 1 : 2;
+   if (const char *v = std::getenv("AMG_MZ27_PF")) c->mz27_pf = std::atoi(v) == 1 ? 1 : (std::atoi(v) == 3 ? 3 : 2);
    if (const char *v = std::getenv("AMG_RR_LINES")) c->rr_lines = std::atoi(v) == 2 ? 2 : 1;
    if (const char *v = std::getenv("AMG_RR_OCC")) c->rr_occ = std::atoi(v);
    if (const char *v = std::getenv("AMG_RR_FPF")) c->rr_fpf = std::atoi(v);
@@ -962,9 +965,26 @@ extern "C" int amg_set_march_lines_gemv(amg_ctx *c, int lines)
 
 extern "C" int amg_set_fuse_outer(amg_ctx *c, int mode)
 {
-   AMG_ARG(c && mode >= 0 && mode <= 2, "amg_set_fuse_outer: mode 0, 1 or 2");
+   AMG_ARG(c && mode >= 0 && mode <= 3, "amg_set_fuse_outer: mode 0, 1, 2 or 3");
    c->knob_gen++; // cached hipGraphs were captured with the old setting
    c->fuse_outer = mode;
+   return AMG_OK;
+}
+
+extern "C" int amg_set_outer_slab(amg_ctx *c, int planes)
+{
+   AMG_ARG(c && planes >= 1, "amg_set_outer_slab: planes must be >= 1");
+   c->knob_gen++;
+   c->outer_slab = planes;
+   return AMG_OK;
+}
+
+extern "C" int amg_set_long_form(amg_ctx *c, int form, int xcd)
+{
+   AMG_ARG(c && form >= 0 && form <= 2, "amg_set_long_form: form 0, 1 or 2");
+   c->knob_gen++;
+   c->long_form = form;
+   c->long_xcd = xcd != 0;
    return AMG_OK;
 }
 
@@ -980,7 +1000,8 @@ extern "C" int amg_set_march_tuning(amg_ctx *c, int mz_pf, int mz27_pf, int mz_o
 {
    AMG_ARG(c, "amg_set_march_tuning: null context");
    AMG_ARG(mz_pf == -2 || (mz_pf >= 1 && mz_pf <= 3), "amg_set_march_tuning: 7-pt prefetch distance %d", mz_pf);
-   AMG_ARG(mz27_pf == -2 || mz27_pf == 1 || mz27_pf == 2, "amg_set_march_tuning: 27-pt prefetch distance %d",
+   AMG_ARG(mz27_pf == -2 || mz27_pf == 1 || mz27_pf == 2 || mz27_pf == 3,
+           "amg_set_march_tuning: 27-pt prefetch distance %d (3: the LDS plane ring)",
            mz27_pf);
    AMG_ARG(mz_occ >= -2 && mz_occ <= 8 && mz27_occ >= -2 && mz27_occ <= 8,
            "amg_set_march_tuning: occupancy %d / %d outside [-1, 8]", mz_occ, mz27_occ);

@@ -308,7 +308,10 @@ struct amg_ctx {
    int fuse_prolong = 0;   // prolongation fused into the first post sweep (measured slower: off)
    int bsr3_xs = 1;        // 3x3 block kernel: one x load per lane, shared over the triplet (AMG_BSR3_XS)
    int fuse_outer = 0;     // level 0's last post sweep + the outer residual as one march (AMG_FUSE_OUTER;
-                           // 1: u' stored every step, 2: only at the end of an iterate batch)
+                           // 1: u' stored every step, 2: only at the end of an iterate batch;
+                           // 3: the two sweeps slab by slab over z through the Infinity Cache, u' as in 2)
+   int outer_slab = 32;    // planes per z-slab of fuse_outer 3 (AMG_OUTER_SLAB): a slab's u, f and u'
+                           // (3 x 32 x 2 MB at 512^2 planes) stay in the 256 MiB Infinity Cache
    int rr_lines = 1;       // coarse lines per lane of the fused residual + restriction (1 or 2)
    int mz_lines = 1;       // 7-pt plane march: lines per lane (1, 2 or 4, AMG_MZ_LINES)
    int mz_lines_gemv = 2;  // the same for SpMV / SpGEMV (AMG_MZ_LINES_GEMV; 2: -8 % on the 512^3 SpMV)
@@ -316,6 +319,9 @@ struct amg_ctx {
    int rr_ring = 0;        // wave-edge residuals through a flag-ordered LDS ring (measured slower: off)
    int rr_occ = 0;         // 5: the fused residual + restriction compiled for 5 waves / SIMD
    int rr_fpf = 0;         // 1: its right-hand side a fine plane ahead (AMG_RR_FPF)
+   int long_form = 0;      // long-row CSR kernel: 0 workgroup chunks (csr_long_kernel), 1 / 2 wave-independent
+                           // chunks of 8 / 16 entries per lane (csr_longw_kernel; AMG_LONG_FORM)
+   int long_xcd = 1;       // ... with XCD-contiguous row blocks (AMG_LONG_XCD)
    int rr_zc = 0;          // coarse planes per chunk of the fused residual + restriction (0: mz_zc / 2)
    int jgs_wave = 1;       // hybrid JGS form: 1 8 blocks per wave, 2 one wave per block, 0 one lane per block, 3 LDS tile
    int jgs_small = 2;      // small levels' hybrid JGS form (amg_set_jgs_small)

@@ -1528,6 +1528,169 @@ __global__ __launch_bounds__(256) void csr_mz27_kernel(
    }
 }
 
+// LDS plane-ring form of the 27-point march (ctx->mz27_pf 3).  The workgroup's
+// 512 in-plane positions plus S + 2 on each side (its +-S lines and the
+// wave-edge neighbours: one contiguous range of the plane) are staged once per
+// plane into a 4-slot LDS ring -- 16-byte loads, two planes ahead in
+// registers, one barrier per plane step -- and every lane reads the nine
+// lines of its 3 x 3 x 3 neighbourhood (x - 1 .. x + 2 of each) from the ring
+// instead of carrying them in registers across the march (no +-1 shuffles,
+// no wave-edge loads).  The row arithmetic is csr_mz27_kernel's: the same
+// fast / edge / masked paths, the same operands in master order
+// (bit-identical); the non-dominant patterns' values come from global memory
+// (L1 / L2) so the ring and mask table fit four workgroups per CU.  Staged
+// elements outside the box (clamped or zero planes) feed only masked entries.
+template <int NEG, bool NEED_DIAG, class Epi, bool UNI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void csr_mz27l_kernel(
+   const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
+   const v2d *__restrict__ mval, MpSten Sv, int dom, int xlo, int xhi, Val27 Hv, const double *__restrict__ x,
+   int P, int S, int nz, int zc, int npb, int xcd, Epi epi, double *__restrict__ partials, int kb, int ke)
+{
+   constexpr unsigned long long FULL = (1ull << 54) - 1;
+   extern __shared__ v2d ring[]; // 4 slots of NPR pairs
+   __shared__ unsigned long long mtab[256];
+   __shared__ double red[AMG_MZ_MAXZC * 8];
+   const bool xc_pf = pf_is_x<Epi>::value && epi_pf_vec(epi) == x;
+   const int tid = (int)threadIdx.x;
+   if (tid < np) mtab[tid] = mmask_g[tid];
+   const int G = (int)gridDim.x;
+   int lg = (int)blockIdx.x;
+   if (xcd && (G & 7) == 0) lg = (lg & 7) * (G >> 3) + (lg >> 3);
+   const int pblk = lg % npb, chunk = lg / npb;
+   const int k0 = kb + chunk * zc, k1 = min(k0 + zc, ke);
+   const int pos = pblk * 512 + 2 * tid;
+   const unsigned Nu = (unsigned)((long long)nz * P);
+   const int NPR = 258 + S;                            // pairs per slot: 512 + 2 S + 4 elements
+   const long long e0 = (long long)pblk * 512 - S - 2; // in-plane position of a slot's element 0
+   // plane p's staged pairs of this lane (pairs tid, tid + 256, tid + 512)
+   auto stage_ld = [&](int p, v2d (&st)[3]) {
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+         st[r] = v2d{0.0, 0.0};
+         const int q = tid + 256 * r;
+         if (q < NPR && p >= 0 && p < nz) {
+            long long i = (long long)p * P + e0 + 2 * q;
+            i = i < 0 ? 0 : (i + 2 > (long long)Nu ? (long long)Nu - 2 : i);
+            st[r] = ld2u(x, (unsigned)i);
+         }
+      }
+   };
+   auto stage_st = [&](int p, const v2d (&st)[3]) {
+      v2d *sl = ring + (p & 3) * NPR;
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+         const int q = tid + 256 * r;
+         if (q < NPR) sl[q] = st[r];
+      }
+   };
+   {
+      v2d st[3];
+      for (int p = k0 - 1; p <= k0 + 1 && p <= k1; p++) {
+         stage_ld(p, st);
+         stage_st(p, st);
+      }
+   }
+   v2d sa[3], sb[3]; // planes k + 2 (loaded one step ago) and k + 3
+   stage_ld(k0 + 2 <= k1 ? k0 + 2 : -1, sa);
+   __syncthreads();
+   for (int k = k0; k < k1; k++) {
+      stage_ld(k + 3 <= k1 ? k + 3 : -1, sb);
+      const unsigned row = (unsigned)k * P + pos;
+      // line d of plane k - 1 + m at the pair's x - 1 .. x + 2, from the ring
+      auto ldline = [&](int m, int d) {
+         const double *rl = reinterpret_cast<const double *>(ring + ((k - 1 + m) & 3) * NPR);
+         const int e = 2 * tid + d * S + 2;
+         return Ln4{rl[e - 1], rl[e], rl[e + 1], rl[e + 2]};
+      };
+      auto opnd4 = [](const Ln4 &q, int dx) {
+         return dx == 0 ? v2d{q.l, q.a} : (dx == 1 ? v2d{q.a, q.b} : v2d{q.b, q.r});
+      };
+      // f(j, operand pair) for the 27 master entries in master order (j = 0:
+      // the centre, then the lexicographic slots), each line read once
+      auto visit = [&](auto &&f) {
+         const Ln4 c = ldline(1, 1);
+         f(0, opnd4(c, 1));
+         Ln4 q = c;
+#pragma unroll
+         for (int L = 0; L < 27; L++) {
+            if (L == 13) continue;
+            if (L % 3 == 0) q = (L / 3 == 4) ? c : ldline(L / 9, (L / 3) % 3);
+            f(L < 13 ? L + 1 : L, opnd4(q, L % 3));
+         }
+      };
+      const int pid = ppat[row >> 1];
+      const v2d acc0 = epi.init2((int)row);
+      v2d acc = acc0;
+      v2d pf;
+      if (xc_pf) {
+         const Ln4 c = ldline(1, 1);
+         pf = v2d{c.a, c.b};
+      } else {
+         pf = epi.pf2((int)row);
+      }
+      const bool fast = UNI ? __all(mtab[pid] == FULL) : __all(pid == dom || pid == xlo || pid == xhi);
+      if (fast) {
+         visit([&](int jj, v2d o) {
+            const double v = Sv.val[jj];
+            acc.x = NEG ? acc.x - v * o.x : acc.x + v * o.x;
+            acc.y = NEG ? acc.y - v * o.y : acc.y + v * o.y;
+         });
+         if (!UNI && pid == xlo) {
+            acc.x = acc0.x;
+            visit([&](int jj, v2d o) {
+               if (mz27_slot(jj) % 3 == 0) return; // dx = -1
+               const double v = Sv.val[jj];
+               acc.x = NEG ? acc.x - v * o.x : acc.x + v * o.x;
+            });
+         }
+         if (!UNI && pid == xhi) {
+            acc.y = acc0.y;
+            visit([&](int jj, v2d o) {
+               if (mz27_slot(jj) % 3 == 2) return; // dx = +1
+               const double v = Hv.v[jj];
+               acc.y = NEG ? acc.y - v * o.y : acc.y + v * o.y;
+            });
+         }
+      } else {
+         const unsigned long long mk = mtab[pid];
+         const v2d *vp = mval + (UNI ? 0 : pid * 27);
+         visit([&](int jj, v2d o) {
+            const unsigned int b = (unsigned int)(mk >> (2 * jj)) & 3u;
+            const v2d v = UNI ? v2d{Sv.val[jj], Sv.val[jj]} : vp[jj];
+            if (b & 1) acc.x = NEG ? acc.x - v.x * o.x : acc.x + v.x * o.x;
+            if (b & 2) acc.y = NEG ? acc.y - v.y * o.y : acc.y + v.y * o.y;
+         });
+      }
+      v2d dg{0.0, 0.0};
+      if (NEED_DIAG) {
+         dg = (UNI || fast) ? v2d{Sv.val[0], Sv.val[0]} : mval[pid * 27];
+         if (!UNI && fast && pid == xhi) dg.y = Hv.v[0];
+      }
+      const v2d out = epi.finish2((int)row, acc, dg, pf);
+      if (partials) {
+         double a = out.x * out.x, b = out.y * out.y;
+#pragma unroll
+         for (int off = 16; off > 0; off >>= 1) {
+            a += __shfl_down(a, off, 32);
+            b += __shfl_down(b, off, 32);
+         }
+         if ((tid & 31) == 0) red[(k - k0) * 8 + (tid >> 5)] = a + b;
+      }
+      // plane k + 2 into the slot of plane k - 2 (read by no lane this step)
+      if (k + 2 <= k1) stage_st(k + 2, sa);
+#pragma unroll
+      for (int r = 0; r < 3; r++) sa[r] = sb[r];
+      __syncthreads();
+   }
+   if (partials) {
+      for (int w = tid; w < 2 * (k1 - k0); w += 256) {
+         const int it = w >> 1, h = w & 1;
+         const double *g = red + it * 8 + 4 * h;
+         partials[((long long)(k0 + it - kb) * P + pblk * 512) / 256 + h] = ((g[0] + g[1]) + g[2]) + g[3];
+      }
+   }
+}
+
 template <int NEG, bool NEED_DIAG, class Epi>
 static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const Epi &e, double *partials, int kb,
                         int ke)
@@ -1549,13 +1712,35 @@ static void launch_mz27(hipStream_t s, const amg_mat *A, const double *x, const 
    else
       fn = A->mp_uni ? (const void *)csr_mz27_kernel<NEG, NEED_DIAG, Epi, true, 1>
                      : (const void *)csr_mz27_kernel<NEG, NEED_DIAG, Epi, false, 1>;
-   const int zc = occ_chunk(A, nk, npb, A->ctx->mz27_occ, fn);
-   const int nch = (nk + zc - 1) / zc;
    const v2d *mv = reinterpret_cast<const v2d *>(A->mpval);
    Val27 H;
    for (int j = 0; j < 27; j++) H.v[j] = A->mz_hival[j];
    // the x-edge fast path needs the dominant pattern (ctx->mz_edge: on)
    const int xlo = A->ctx->mz_edge ? A->mz_xlo : -1, xhi = A->ctx->mz_edge ? A->mz_xhi : -1;
+   if (A->ctx->mz27_pf == 3 && A->mz_S <= 512) {
+      // the LDS plane-ring form: four workgroups per CU at S = 256 (33 KB ring)
+      const size_t lds = (size_t)4 * (258 + A->mz_S) * sizeof(v2d);
+      const void *fl = A->mp_uni ? (const void *)csr_mz27l_kernel<NEG, NEED_DIAG, Epi, true>
+                                 : (const void *)csr_mz27l_kernel<NEG, NEED_DIAG, Epi, false>;
+      int occ = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fl, 256, lds) != hipSuccess) {
+         (void)hipGetLastError();
+         occ = 0;
+      }
+      const int zcl = occ_chunk(A, nk, npb, occ > 0 ? occ : 0, nullptr);
+      const int nchl = (nk + zcl - 1) / zcl;
+      if (A->mp_uni)
+         csr_mz27l_kernel<NEG, NEED_DIAG, Epi, true><<<npb * nchl, 256, lds, s>>>(
+            A->ppat, A->mpmask, A->pp_n, mv, S, -1, -1, -1, H, x, P, A->mz_S, nz, zcl, npb, A->ctx->mz_xcd, e,
+            partials, kb, ke);
+      else
+         csr_mz27l_kernel<NEG, NEED_DIAG, Epi, false><<<npb * nchl, 256, lds, s>>>(
+            A->ppat, A->mpmask, A->pp_n, mv, S, A->mz_dom, A->mz_dom >= 0 ? xlo : -1, A->mz_dom >= 0 ? xhi : -1,
+            H, x, P, A->mz_S, nz, zcl, npb, A->ctx->mz_xcd, e, partials, kb, ke);
+      return;
+   }
+   const int zc = occ_chunk(A, nk, npb, A->ctx->mz27_occ, fn);
+   const int nch = (nk + zc - 1) / zc;
    auto go = [&](auto pf) {
       constexpr int PF = decltype(pf)::value;
       if (A->mp_uni)
@@ -3238,6 +3423,103 @@ __global__ __launch_bounds__(TB) void csr_long_kernel(
    }
 }
 
+// Wave-independent long-row form (ctx->long_form 1 / 2: CW = 8 / 16).  Each
+// wave owns RPW consecutive rows (lane r < RPW: row r0 + r) and streams their
+// entries itself in chunks of 64 CW (entry k of the chunk on lane k % 64, all
+// CW column / value loads and then all CW gathers of a lane in flight), rounds
+// the products into its own LDS slab, and each lane then adds its row's
+// products in CSR order -- csr_long_kernel's exact summation, but with no
+// workgroup barrier: the slab is the wave's own (the LDS executes a wave's
+// operations in issue order, so the next chunk's stores follow this chunk's
+// reads), and the waves' load and summation phases overlap.  XCD-contiguous
+// row blocks (xcd) keep a block's gathered x in its XCD's L2.  Norm partials
+// (one per 256-row tile) only with RPW = 64.
+template <int NEG, bool NEED_DIAG, class Epi, bool VI, int CW>
+__global__ __launch_bounds__(256) void csr_longw_kernel(
+   const int *__restrict__ rowptr, const int *__restrict__ col, const double *__restrict__ val,
+   const unsigned char *__restrict__ vidx, const double *__restrict__ vtab_g, const double *__restrict__ x,
+   int rb, int re, int rpw, int xcd, Epi epi, double *__restrict__ partials)
+{
+   __shared__ double prod[4][64 * CW];
+   __shared__ double vtab[VI ? 256 : 1];
+   __shared__ double red[4];
+   const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
+   int blk = (int)blockIdx.x;
+   if (xcd) {
+      // bijective: the blocks dealt to one XCD (b % 8) get a contiguous range
+      const int nb = (int)gridDim.x, q = nb >> 3, r = nb & 7, xg = blk & 7, idx = blk >> 3;
+      blk = (xg < r ? xg * (q + 1) : r * (q + 1) + (xg - r) * q) + idx;
+   }
+   if (VI) {
+      vtab[tid] = vtab_g[tid];
+      __syncthreads();
+   }
+   const long long r0l = (long long)rb + ((long long)blk * 4 + w) * rpw;
+   const int r0 = (int)min(r0l, (long long)re), r1 = min(r0 + rpw, re);
+   const int row = r0 + lane;
+   const bool own = lane < rpw && row < r1;
+   int rs = 0, rend = 0;
+   double acc = 0.0, pf = 0.0, dg = 0.0;
+   if (own) {
+      rs = rowptr[row];
+      rend = rowptr[row + 1];
+      acc = epi.init(row);
+      pf = epi.pf(row);
+      if (NEED_DIAG) dg = VI ? vtab[vidx[rs]] : val[rs];
+   }
+   if (r0 < r1) {
+      const int tb = rowptr[r0], te = rowptr[r1];
+      double *pw = prod[w];
+      for (int cs = tb; cs < te; cs += 64 * CW) {
+         const int ce = min(cs + 64 * CW, te);
+         int cj[CW];
+         double av[CW];
+#pragma unroll
+         for (int j = 0; j < CW; j++) {
+            const int k = cs + j * 64 + lane;
+            const int kk = k < ce ? k : cs; // past the chunk: a valid entry, never summed
+            cj[j] = col[kk];
+            av[j] = VI ? vtab[vidx[kk]] : val[kk];
+         }
+         double xv[CW];
+#pragma unroll
+         for (int j = 0; j < CW; j++) xv[j] = x[cj[j]];
+#pragma unroll
+         for (int j = 0; j < CW; j++) pw[j * 64 + lane] = av[j] * xv[j];
+         __builtin_amdgcn_wave_barrier();
+         if (own) {
+            const int a0 = max(rs, cs), a1 = min(rend, ce);
+            int k = a0;
+            for (; k + 8 <= a1; k += 8) {
+               double p[8];
+#pragma unroll
+               for (int j = 0; j < 8; j++) p[j] = pw[k + j - cs];
+#pragma unroll
+               for (int j = 0; j < 8; j++) {
+                  if (NEG)
+                     acc -= p[j];
+                  else
+                     acc += p[j];
+               }
+            }
+            for (; k < a1; k++) {
+               if (NEG)
+                  acc -= pw[k - cs];
+               else
+                  acc += pw[k - cs];
+            }
+         }
+         __builtin_amdgcn_wave_barrier();
+      }
+   }
+   double out = 0.0;
+   if (own) out = epi.finish(row, acc, dg, pf);
+   if (partials) {
+      const double sblk = block_sum_256(out * out, red);
+      if (tid == 0) partials[blk] = sblk;
+   }
+}
+
 // long rows: at least 64 entries per row on average
 static inline bool long_rows(const amg_mat *A) { return A->nnz >= 64LL * A->nrows; }
 
@@ -3261,6 +3543,26 @@ static void launch_long(hipStream_t s, const amg_mat *A, const double *x, int rb
                         double *partials = nullptr)
 {
    const int n = re - rb;
+   if (A->ctx->long_form) {
+      // rows per wave: the most that still gives >= 4096 workgroups (64 .. 8);
+      // with norm partials 64 (one 256-row tile per workgroup)
+      const int rpw = partials ? 64 : n >= 256 * 4096 ? 64 : n >= 128 * 4096 ? 32 : n >= 64 * 4096 ? 16 : 8;
+      const int nb = (int)(((long long)n + 4 * rpw - 1) / (4 * rpw));
+      auto go = [&](auto cw) {
+         constexpr int W = decltype(cw)::value;
+         if (A->vidx)
+            csr_longw_kernel<NEG, NEED_DIAG, Epi, true, W><<<nb, 256, 0, s>>>(
+               A->rowptr, A->col, A->val, A->vidx, A->vtab, x, rb, re, rpw, A->ctx->long_xcd, e, partials);
+         else
+            csr_longw_kernel<NEG, NEED_DIAG, Epi, false, W><<<nb, 256, 0, s>>>(
+               A->rowptr, A->col, A->val, nullptr, nullptr, x, rb, re, rpw, A->ctx->long_xcd, e, partials);
+      };
+      if (A->ctx->long_form == 2)
+         go(std::integral_constant<int, 16>{});
+      else
+         go(std::integral_constant<int, 8>{});
+      return;
+   }
    // AMG_LONG_RW=128 / 256: rows per workgroup on the largest levels (the rows'
    // sequential sums then spread over 2 / 4 waves instead of one)
    static const int lrw = [] {

@@ -103,6 +103,9 @@ struct amg_hier {
    bool post_deferred = false;
    bool store_u1 = true;
    double *u2 = nullptr;
+   // fuse_outer 3 without a stored u': u' of one z-slab (slab_planes + 2 planes)
+   double *slab_scr = nullptr;
+   long long slab_cap = 0;
    // AMG_SCHED_TIMED: per-level correction time (amg_hier_set_async_durations)
    // or recorded end times (amg_hier_set_async_times)
    std::vector<double> async_dur;
@@ -972,8 +975,46 @@ static bool reuse_applies(const amg_hier *H)
 static bool fused_outer_applies(const amg_hier *H)
 {
    const amg_opts &o = H->o;
+   if (H->ctx->fuse_outer == 3) {
+      // the slab form: any plane-marched level 0 whose planes are whole
+      // 256-row norm tiles, Jacobi or L1 Jacobi
+      const amg_mat *A = H->lv[0].A;
+      return reuse_applies(H) && o.num_post_smooth_sweeps >= 1 && (H->psw.empty() || !H->psw[0]) && A->mz_P &&
+             A->didx && A->mz_P % 256 == 0 && H->lv[0].n % A->mz_P == 0;
+   }
    return H->ctx->fuse_outer && reuse_applies(H) && o.smoother == AMG_JACOBI && o.num_post_smooth_sweeps >= 1 &&
           (H->psw.empty() || !H->psw[0]) && amgk::mz_sweep_outer_ok(H->lv[0].A);
+}
+
+// fuse_outer 3: level 0's deferred last post sweep and the outer residual
+// (+ the next cycle's first sweep) slab by slab over z.  Slab [s0, s1):
+// sweep 1 u' = u + w (f - A u) ./ a over planes [s0-1, s1+1) (the z halo the
+// residual's +-P operands need), then the residual sweep r = f - A u',
+// u'' = u' + w r ./ a over [s0, s1), which reads u' and f back from the
+// Infinity Cache instead of HBM.  Both are the ordinary marched kernels over
+// plane ranges (the same per-row operand order), and the norm partials land
+// at their global tiles: u', u'', r and every partial are bit-identical to the
+// two full sweeps.  Without a stored u' the slab's u' lives in a (Z + 2)-plane
+// scratch re-used by every slab (its dirty lines are overwritten in the cache,
+// not written back).
+static void outer_slabs(amg_hier *H, double *p, bool skip_r)
+{
+   hipStream_t s = H->ctx->stream;
+   Level &v = H->lv[0];
+   const amg_mat *A = v.A;
+   const long long P = A->mz_P;
+   const int nz = (int)(v.n / P), Z = std::min(H->ctx->outer_slab, nz);
+   const double *l1 = H->o.smoother == AMG_L1_JACOBI ? v.l1 : nullptr;
+   const double w = H->o.smooth_weight;
+   for (int s0 = 0; s0 < nz; s0 += Z) {
+      const int s1 = std::min(nz, s0 + Z);
+      const int a = std::max(0, s0 - 1), b = std::min(nz, s1 + 1);
+      // plane k of u' at xs + k P (the scratch holds planes s0-1 .. s1)
+      double *xs = H->store_u1 ? v.u_alt : H->slab_scr + P * (1 - (long long)s0);
+      amgk::jacobi_sweep(s, A, v.f, v.u, l1, w, xs, (int)(a * P), (int)(b * P));
+      amgk::residual_jacobi(s, A, v.f, xs, l1, w, skip_r ? nullptr : H->r0, H->u2, (int)(s0 * P), (int)(s1 * P),
+                            p + s0 * P / 256);
+   }
 }
 
 extern "C" int amg_hier_fused_outer(const amg_hier *H)
@@ -998,10 +1039,20 @@ static int outer_residual(amg_hier *H, int slot)
    if (H->post_deferred) {
       if (!H->u2) AMG_TRY(dalloc(H, v.n, &H->u2));
       const bool skip_r = H->o.reuse_outer_residual >= 2;
+      if (c->fuse_outer == 3 && !H->store_u1) {
+         const long long need = (long long)(std::min(c->outer_slab, v.n / v.A->mz_P) + 2) * v.A->mz_P;
+         if (H->slab_cap < need) {
+            AMG_TRY(dalloc(H, need, &H->slab_scr));
+            H->slab_cap = need;
+         }
+      }
       {
          ProfScope ps(H, PROF_OUTER, c->stream);
-         amgk::mz_sweep_outer(c->stream, v.A, v.f, v.u, H->store_u1 ? v.u_alt : nullptr, skip_r ? nullptr : H->r0,
-                              H->u2, H->o.smooth_weight, p);
+         if (c->fuse_outer == 3)
+            outer_slabs(H, p, skip_r);
+         else
+            amgk::mz_sweep_outer(c->stream, v.A, v.f, v.u, H->store_u1 ? v.u_alt : nullptr,
+                                 skip_r ? nullptr : H->r0, H->u2, H->o.smooth_weight, p);
       }
       std::swap(v.u, v.u_alt);  // u = u' (when stored)
       std::swap(v.u_alt, H->u2); // u_alt = u''
@@ -1195,7 +1246,7 @@ extern "C" int amg_solve_iterate(amg_hier *H, int k)
       // fuse_outer 2: the fused post sweep writes u' only in the batch's last
       // step (the iterate the caller can observe); the steps before consume it
       // in registers
-      H->store_u1 = H->ctx->fuse_outer != 2 || i == k - 1;
+      H->store_u1 = H->ctx->fuse_outer < 2 || i == k - 1;
       const int st = solve_step(H);
       H->store_u1 = true;
       AMG_TRY(st);

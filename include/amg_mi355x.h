@@ -419,8 +419,21 @@ int amg_hier_fused_prolong(const amg_hier *H);
  * reuse_outer_residual on a 7-pt master-form A0 whose lines are 512 long):
  * mode 0 off, 1 on (u' written every step), 2 on with u' written only in the
  * last step of each amg_solve_iterate batch (the steps before consume it in
- * registers); bit-identical to the two marches.  AMG_FUSE_OUTER sets it too. */
+ * registers); 3: the two sweeps as ordinary marches slab by slab over z
+ * (amg_set_outer_slab planes each), the second reading u' and f back from the
+ * Infinity Cache, u' written as in mode 2 (any plane-marched A0 whose planes
+ * are multiples of 256 rows, Jacobi or L1 Jacobi); bit-identical to the two
+ * marches.  AMG_FUSE_OUTER sets it too. */
 int amg_set_fuse_outer(amg_ctx *ctx, int mode);
+/* planes per z-slab of fuse_outer mode 3 (default 32; env AMG_OUTER_SLAB) */
+int amg_set_outer_slab(amg_ctx *ctx, int planes);
+/* long-row CSR kernel (operators of >= 64 entries per row: classical coarse
+ * levels, smoothed transfers; SMEM_MatVec.cpp:123-259): form 0 workgroup
+ * chunks with one summing wave, 1 / 2 wave-independent chunks of 8 / 16
+ * entries per lane; xcd: XCD-contiguous row blocks (forms 1, 2).  Every form
+ * adds each row's rounded products in CSR order: bit-identical.  Env
+ * AMG_LONG_FORM / AMG_LONG_XCD. */
+int amg_set_long_form(amg_ctx *ctx, int form, int xcd);
 /* the fused post sweep + outer residual mode this hierarchy runs (0: not fused) */
 int amg_hier_fused_outer(const amg_hier *H);
 int amg_set_fuse_prolong(amg_ctx *ctx, int enable);

@@ -85,17 +85,22 @@ def test_classical_distributed(amg, oracle, ctx):
     np.testing.assert_allclose(hd, h1, rtol=1e-12, atol=0)
 
 
-@pytest.mark.parametrize("r,ct", [(2, 9), (3, 10)])
-def test_elasticity_solve_matches_oracle(amg, oracle, ctx, r, ct):
+@pytest.mark.parametrize("r,ct,lf", [(2, 9, 0), (3, 10, 0), (3, 9, 1), (3, 9, 2)])
+def test_elasticity_solve_matches_oracle(amg, oracle, ctx, r, ct, lf):
     """The DMEM elasticity problem (81-entry rows, value-indexed: the two
     materials give ~120 distinct values) on a classical num_functions = 3
-    hierarchy: bit-identical to the oracle, residual decreasing."""
+    hierarchy: bit-identical to the oracle, residual decreasing; lf: the
+    long-row kernel form of the coarse levels (ctx long_form)."""
     n, rp, cj, v, b = amg.classical.elasticity(r)
     H = amg.classical.ClassicalAMG(n, rp, cj, v, coarsen_type=ct, strong_threshold=0.5, num_functions=3)
     lv = host_levels(amg, H)
     host = {k: [oracle.Csr(*m) for m in lv_] for k, lv_ in lv.items()}
     opts = amg.default_opts(smooth_weight=0.6, num_cycles=10, tol=0.0)
-    u, hist = compare_solve(amg, oracle, ctx, host, opts, b)
+    ctx.set_long_form(lf)
+    try:
+        u, hist = compare_solve(amg, oracle, ctx, host, opts, b)
+    finally:
+        ctx.set_long_form(0)
     assert np.all(np.diff(hist) < 0)
     M = ctx.csr(*lv["A"][0])
     assert M.value_index > 0 and M.dict_index == 0

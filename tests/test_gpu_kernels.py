@@ -303,6 +303,45 @@ def test_matvec(mats, ctx, oracle, amg, name):
     assert_bitwise(y.download(), ref, name)
 
 
+@pytest.mark.parametrize("form,xcd", [(1, 1), (2, 1), (1, 0)])
+@pytest.mark.parametrize("name", ["dense", "dense_q", "longrows", "longrows_q"])
+def test_long_forms(mats, ctx, oracle, amg, name, form, xcd):
+    """The wave-independent long-row kernel (csr_longw_kernel, ctx long_form 1 / 2,
+    with and without XCD-contiguous row blocks) on rows of 90..> 2048 entries,
+    plain and value-indexed: SpMV, two SpGEMV branches over a row range, the
+    two-pass residual, weighted and L1 Jacobi, bit-identical to the oracle."""
+    host, dev = mats
+    A, dA = host[name], dev[name]
+    x, b = _vecs(A.ncols, 40), _vecs(A.nrows, 41)
+    ctx.set_long_form(form, xcd)
+    try:
+        y = ctx.vec(A.nrows)
+        amg.smem.SMEM_Sync_Parfor_MatVec(ctx, dA, ctx.vec(x), y)
+        assert_bitwise(y.download(), oracle.smem_matvec(A, x, np.zeros(A.nrows)), "matvec")
+        for alpha, beta in ((-1, 1), (1.7, -0.4)):
+            u = _vecs(A.nrows, 42)
+            ref = u.copy()
+            oracle.smem_spgemv(A, x, b, alpha, beta, ref, 5, A.nrows - 3)
+            du = ctx.vec(u)
+            amg.smem.SMEM_SpGEMV(ctx, dA, ctx.vec(x), ctx.vec(b), alpha, beta, du, 5, A.nrows - 3)
+            assert_bitwise(du.download(), ref, f"spgemv {alpha} {beta}")
+        y0, r0 = np.zeros(A.nrows), np.zeros(A.nrows)
+        oracle.smem_residual(A, b, x, y0, r0, 3, A.nrows - 5)
+        y, r = ctx.vec(A.nrows), ctx.vec(A.nrows)
+        amg.smem.SMEM_Residual(ctx, dA, ctx.vec(b), ctx.vec(x), y, r, 3, A.nrows - 5)
+        assert_bitwise(y.download(), y0, "residual y")
+        assert_bitwise(r.download(), r0, "residual r")
+        if A.nrows == A.ncols:
+            f, u = _vecs(A.nrows, 43), _vecs(A.nrows, 44)
+            ru, rp = u.copy(), np.zeros(A.nrows)
+            oracle.smem_jacobi(A, f, ru, rp, 0.8, 3, 0)
+            du, dp = ctx.vec(u), ctx.vec(A.nrows)
+            amg.smem.SMEM_Sync_Parfor_Jacobi(ctx, dA, ctx.vec(f), du, dp, 3, 0, 0.8)
+            assert_bitwise(du.download(), ru, "jacobi u")
+    finally:
+        ctx.set_long_form(0, 1)
+
+
 @pytest.mark.parametrize("name", ["lap16", "rand_rect", "longrows", "P0", "Rs0"])
 @pytest.mark.parametrize("ab", [(1, 0), (-1, 0), (2.5, 0), (1, -1), (-1, 1), (0.5, -0.5),
                                 (1, 1), (-1, -1), (3, 3), (1, 0.3), (-1, 0.7), (1.7, -0.4)])

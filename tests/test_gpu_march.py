@@ -466,6 +466,68 @@ def test_fused_prolong_sweep(ctx, amg, oracle, dims, zc, sm, post, form):
 
 
 
+@pytest.mark.parametrize("dims,zc,post,reuse,slab,sm", [((512, 8, 6), 4, 1, 2, 2, "jacobi"),
+                                                         ((512, 16, 12), 3, 1, 2, 5, "jacobi"),
+                                                         ((256, 8, 11), 64, 2, 2, 3, "l1"),
+                                                         ((512, 2, 5), 1, 1, 1, 1, "jacobi"),
+                                                         ((512, 6, 9), 5, 1, 1, 4, "l1"),
+                                                         ((512, 4, 16), 16, 2, 2, 64, "jacobi")])
+def test_slab_sweep_outer(ctx, amg, oracle, dims, zc, post, reuse, slab, sm):
+    """fuse_outer 3: level 0's last post sweep and the outer residual + the next
+    cycle's first sweep slab by slab over z (sweep 1 over a slab plus its z
+    halo into a slab scratch, then the residual sweep of the slab; the
+    Infinity-Cache form): iterate and norm history bit-identical to the
+    unfused run and the iterate to the oracle, through amg_solve (u' stored)
+    and iterate batches (u' only in a batch's last step); slabs of 1..64
+    planes (one slab, ragged last slabs), Jacobi and L1 Jacobi, r stored or not."""
+    from oracle import pyoracle as po
+    g = amg.Gen(*dims, interp=amg.AMG_INTERP_LINEAR)
+    host = {w: [po.Csr(*g.host_csr(c, l)) for l in range(cnt)]
+            for w, c, cnt in (("A", amg.AMG_GEN_A, g.L), ("P", amg.AMG_GEN_P, g.L - 1),
+                              ("R", amg.AMG_GEN_R, g.L - 1))}
+    n = dims[0] * dims[1] * dims[2]
+    f = amg.rhs_rand(0, n)
+    smoother = amg.AMG_JACOBI if sm == "jacobi" else amg.AMG_L1_JACOBI
+    res = {}
+    ctx.set_plane_march(1, zc, 1)
+    ctx.set_outer_slab(slab)
+    try:
+        for fo in (3, 0):
+            ctx.set_fuse_outer(fo)
+            dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v] for k, v in host.items()}
+            opts = amg.default_opts(smooth_weight=0.8, num_cycles=6, tol=0.0, reuse_outer_residual=reuse,
+                                    smoother=smoother, num_post_smooth_sweeps=post)
+            H = amg.Hier(ctx, dev["A"], dev["P"], dev["R"], opts)
+            sol = H.solve(f)
+            fv, uv = ctx.vec(f), ctx.vec(np.zeros(n))
+            r0 = H.solve_start(fv, uv)
+            hist = [r0]
+            for b in (2, 3, 1):
+                H.iterate(b)
+                hist.append(H.resnorm())
+            H.get_u(uv)
+            res[fo] = (H.fused_outer, sol, uv.download(), np.array(hist))
+            H.free()
+            for v in dev.values():
+                for M in v:
+                    M.free()
+    finally:
+        ctx.set_plane_march(1, -1, 1)
+        ctx.set_fuse_outer(0)
+        ctx.set_outer_slab(32)
+    (fo1, (u1, h1, k1), ui1, hi1), (fo0, (u0, h0, k0), ui0, hi0) = res[3], res[0]
+    assert fo1 == 3 and fo0 == 0, (fo1, fo0)
+    OH = po.Hier(host["A"], host["P"], host["R"],
+                 po.make_opts(smooth_weight=0.8, num_cycles=6, smoother=smoother, num_post=post))
+    u_cpu, hist_cpu, _ = OH.solve(f)
+    assert_bitwise(u1, u0, "slab vs unfused iterate")
+    assert_bitwise(u1, u_cpu, "slab vs oracle iterate")
+    assert_bitwise(h1[:k1 + 1], h0[:k0 + 1], "norm history")
+    np.testing.assert_allclose(h1[:k1 + 1], hist_cpu[:k1 + 1], rtol=1e-12)
+    assert_bitwise(ui1, ui0, "slab vs unfused iterate (batches)")
+    assert_bitwise(hi1, hi0, "slab vs unfused norm history (batches)")
+
+
 @pytest.mark.parametrize("dims,zc,post,reuse,mode", [((512, 8, 6), 4, 1, 2, 1), ((512, 16, 12), 3, 1, 2, 2),
                                                       ((512, 6, 10), 64, 2, 2, 1), ((512, 2, 5), 1, 1, 1, 1),
                                                       ((512, 12, 9), 5, 1, 1, 2), ((512, 4, 16), 16, 2, 2, 2)])

@@ -142,3 +142,80 @@ def test_slab_fused_prolong_bitwise(amg, oracle, ctx, monkeypatch, nranks, sched
     from test_gpu_slab_async import test_slab_async_schedule_bitwise
     monkeypatch.setenv("AMG_FUSE_XFP_SLAB", "1")
     test_slab_async_schedule_bitwise(amg, oracle, ctx, "multadd", True, nranks, sched, 64)
+
+
+@pytest.mark.parametrize("name", ["galerkin32", "pat32x16x5", "uni64x8x4"])
+def test_march27_lds_ring_bitwise(ctx, amg, oracle, boxes27, name):
+    """the 27-pt march's LDS plane-ring form (csr_mz27l_kernel, march tuning
+    mz27_pf = 3): SpGEMV in three branches, weighted and L1 Jacobi, bit-identical
+    to plain CSR -- dominant, x-edge and masked (boundary-pattern) rows"""
+    A = boxes27[name]
+    ctx.set_plane_march(1, -1, 1)
+    ctx.set_march_tuning(3, 3, 0, -1)
+    try:
+        mz = register(ctx, A)
+        pl = register(ctx, A, plain=True)
+        assert mz.march_points == 27
+        n = A.nrows
+        x = ctx.vec(_vecs(n, 81))
+        b = ctx.vec(_vecs(n, 82))
+        l1 = ctx.vec(oracle.l1_norms(A))
+        for ab in ((1.0, 0.0), (-1.0, 1.0), (2.5, -0.5)):
+            ys = []
+            for M in (pl, mz):
+                y = ctx.vec(n)
+                amg.smem.SMEM_SpGEMV(ctx, M, x, b, ab[0], ab[1], y, 0, n)
+                ys.append(y.download())
+            assert_bitwise(ys[1], ys[0], f"{name} spgemv {ab}")
+        for l1j in (False, True):
+            us = []
+            for M in (pl, mz):
+                u = ctx.vec(_vecs(n, 83))
+                if l1j:
+                    amg.smem.SMEM_Sync_Parfor_L1Jacobi(ctx, M, b, u, ctx.vec(n), l1, 2, 0)
+                else:
+                    amg.smem.SMEM_Sync_Parfor_Jacobi(ctx, M, b, u, ctx.vec(n), 3, 0, 0.7)
+                us.append(u.download())
+            assert_bitwise(us[1], us[0], f"{name} {'l1 ' if l1j else ''}jacobi")
+        mz.free()
+        pl.free()
+    finally:
+        ctx.set_march_tuning(3, 2, 0, -1)  # the defaults
+
+
+@pytest.mark.parametrize("zc", [-1, 3])
+def test_march27_lds_ring_solve(ctx, amg, oracle, zc):
+    """SMEM_Solve on a hierarchy whose fine operator is 27-pt (levels 1.. of the
+    64^3 linear hierarchy): the outer residual + first sweep with its norm
+    partials, the residuals and sweeps all through the LDS plane ring; iterate
+    and norm history bit-identical to the register-march run, iterate to the
+    oracle"""
+    from oracle import pyoracle as po
+    g = amg.Gen(64, interp=amg.AMG_INTERP_LINEAR)
+    host = {w: [po.Csr(*g.host_csr(c, l)) for l in range(lo, cnt)]
+            for w, c, lo, cnt in (("A", amg.AMG_GEN_A, 1, g.L), ("P", amg.AMG_GEN_P, 1, g.L - 1),
+                                  ("R", amg.AMG_GEN_R, 1, g.L - 1))}
+    f = amg.rhs_rand(0, host["A"][0].nrows)
+    res = {}
+    ctx.set_plane_march(1, zc, 1)
+    try:
+        for pf in (3, 2):
+            ctx.set_march_tuning(3, pf, 0, -1)
+            dev = {k: [ctx.csr(M.nrows, M.ncols, M.rowptr, M.col, M.val) for M in v] for k, v in host.items()}
+            assert dev["A"][0].march_points == 27
+            opts = amg.default_opts(smooth_weight=0.8, num_cycles=8, tol=0.0, reuse_outer_residual=2)
+            H = amg.Hier(ctx, dev["A"], dev["P"], dev["R"], opts)
+            res[pf] = H.solve(f)
+            H.free()
+            for v in dev.values():
+                for M in v:
+                    M.free()
+    finally:
+        ctx.set_march_tuning(3, 2, 0, -1)
+        ctx.set_plane_march(1, -1, 1)
+    (u3, h3, k3), (u2, h2, k2) = res[3], res[2]
+    assert_bitwise(u3, u2, "lds ring vs register march iterate")
+    assert_bitwise(np.asarray(h3[:k3 + 1]), np.asarray(h2[:k2 + 1]), "norm history")
+    OH = po.Hier(host["A"], host["P"], host["R"], po.make_opts(smooth_weight=0.8, num_cycles=8))
+    u_cpu, _, _ = OH.solve(f)
+    assert_bitwise(u3, u_cpu, "lds ring vs oracle iterate")

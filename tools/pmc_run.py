@@ -1,4 +1,4 @@
-"""Workload for the rocprofv3 --pmc passes (tools/gpu_r05_r.sh): PMC calibration
+"""Workload for the rocprofv3 --pmc passes (tools/rounds/gpu_r05_r.sh): PMC calibration
 streams of known size per access width, then 512^3 V-cycles (default storage:
 row-pattern-coded) and fine residuals of the same operator stored
 dictionary-coded, value-indexed and as plain CSR.  tools/pmc_traffic.py reads

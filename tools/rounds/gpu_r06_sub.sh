@@ -1,4 +1,4 @@
-# a subset of the GPU suite in one process: ./tools/gpu_r06_sub.sh OUTDIR pytest-args...
+# a subset of the GPU suite in one process: ./tools/rounds/gpu_r06_sub.sh OUTDIR pytest-args...
 set -o pipefail
 O=$1; shift
 mkdir -p $O

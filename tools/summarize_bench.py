@@ -1,5 +1,5 @@
 """One-line summaries of the JSON outputs of a measurement batch
-(tools/gpu_r05_r.sh): bench.py lines (it/s, ms per step, the fine kernels'
+(tools/rounds/gpu_r05_r.sh): bench.py lines (it/s, ms per step, the fine kernels'
 fractions of peak, the parity leg), bench_async.py (async / sync cycles/s) and
 bench_dist_async.py (additive cycles/s, relres).  usage:
 summarize_bench.py <dir with *.json>"""
