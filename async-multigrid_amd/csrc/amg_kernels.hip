@@ -3841,13 +3841,18 @@ struct EpiResJacobi {
 constexpr int AMG_MZF_NL = 2;
 constexpr int AMG_MZF_NT = AMG_MZF_NL + 2;
 
-template <bool STORE_U, int MINB>
+// PD: prefetch depth -- 1: u of plane k + 2 and the halo / f / pattern
+// operands of plane k + 1 in flight during step k; 2: u of plane k + 3 and the
+// operands of plane k + 2 (twice the bytes in flight per lane at one workgroup
+// per CU).  dq / rq: the uniform diagonal and its reciprocal for the exact
+// reciprocal division (jac_div2; dq = 0: the division itself).
+template <bool STORE_U, int MINB, int PD = 1>
 __global__ __launch_bounds__(256 * AMG_MZF_NT) __attribute__((amdgpu_waves_per_eu(MINB * 4))) void
 mz_sweep_outer_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np, MpSten Sv,
    const double *__restrict__ f, const double *__restrict__ u, double *__restrict__ u1out,
    double *__restrict__ rout, double *__restrict__ unext, double omega, int P, int nz, int zc, int npb, int xcd,
-   double *__restrict__ partials)
+   double *__restrict__ partials, double dq, double rq)
 {
    constexpr int NL = AMG_MZF_NL, NT = AMG_MZF_NT, S = 512;
    __shared__ unsigned long long mtab[256];
@@ -3867,9 +3872,10 @@ mz_sweep_outer_kernel(
    const unsigned pos = (unsigned)(ly * S + 2 * lt);
    const unsigned Nu = (unsigned)((long long)nz * P);
    const double a0 = Sv.val[0];
+   const v2d a2{a0, a0};
    auto ldp = [&](int k) { return (k >= 0 && k < nz) ? ld2u(u, (unsigned)k * P + pos) : v2d{0.0, 0.0}; };
-   // u of planes k-1, k, k+1 (sweep 1 at plane k)
-   v2d xm = ldp(k0 - 2), xc = ldp(k0 - 1), xq = ldp(k0);
+   // u of planes k-1, k, k+1 (sweep 1 at plane k), then k + 2 (PD 2)
+   v2d xm = ldp(k0 - 2), xc = ldp(k0 - 1), xq = ldp(k0), xn = PD == 2 ? ldp(k0 + 1) : v2d{0.0, 0.0};
    struct PlaneIn {
       v2d ym, yp, fv;
       double e;
@@ -3887,15 +3893,16 @@ mz_sweep_outer_kernel(
       if (lane == 0 && row > 0) in.e = ld1u(u, row - 1);
       if (lane == 63 && row + 2 < Nu) in.e = ld1u(u, row + 2);
    };
-   PlaneIn cur;
+   PlaneIn cur, nx1{};
    fetch(k0 - 1, cur);
+   if (PD == 2 && k0 <= k1) fetch(k0, nx1);
    // sweep-2 state: u' of planes k-2, k-1 of the own pair; f and pattern of plane k-1
    v2d wm{0.0, 0.0}, wc{0.0, 0.0}, fm{0.0, 0.0};
    int pidm = 0;
    __syncthreads();
    for (int k = k0 - 1; k <= k1; k++) {
-      const bool s1 = k >= 0 && k < nz;  // workgroup-uniform
-      v2d xn = ldp(k + 2);               // u of plane k + 2, one step ahead
+      const bool s1 = k >= 0 && k < nz;       // workgroup-uniform
+      const v2d xnn = ldp(k + 1 + PD);        // u of plane k + 1 + PD, PD steps ahead
       // ---- sweep 1 at plane k: u' = u + w (f - A u) ./ a (EpiJacobi) ----
       v2d w1{0.0, 0.0};
       if (s1) {
@@ -3913,15 +3920,17 @@ mz_sweep_outer_kernel(
          xv[5] = cur.yp;
          xv[6] = xq;
          const v2d acc = mz_acc7<1, true>(cur.fv, xv, mk, Sv, nullptr);
-         w1 = v2d{(a0 != 0.0) ? xc.x + omega * acc.x / a0 : xc.x, (a0 != 0.0) ? xc.y + omega * acc.y / a0 : xc.y};
+         const v2d q = jac_div2(v2d{omega * acc.x, omega * acc.y}, a2, dq, rq);
+         w1 = v2d{(a0 != 0.0) ? xc.x + q.x : xc.x, (a0 != 0.0) ? xc.y + q.y : xc.y};
          if (STORE_U && inner && y < ny && k >= k0 && k < k1)
             *reinterpret_cast<v2du *>(u1out + (size_t)((unsigned)k * P + pos)) = w1;
       }
       ring[k & 1][team][lt] = w1;
       const v2d fk = cur.fv;
       const int pidk = cur.pid;
-      // the next plane's operands, in flight across the barrier below
-      if (k + 1 <= k1) fetch(k + 1, cur);
+      // the operands of plane k + PD, in flight across the barrier below
+      PlaneIn nxt{};
+      if (k + PD <= k1) fetch(k + PD, nxt);
       // ---- sweep 2 at plane k - 1 (inner teams): r = f - A u', u'' = u' + w r ./ a ----
       const int km = k - 1;
       if (km >= k0 && km < k1) {
@@ -3943,8 +3952,8 @@ mz_sweep_outer_kernel(
             const v2d res = mz_acc7<1, true>(fm, xv, mk, Sv, nullptr);
             const unsigned row = (unsigned)km * P + pos;
             if (rout) *reinterpret_cast<v2du *>(rout + (size_t)row) = res;
-            const v2d v{(a0 != 0.0) ? wc.x + omega * res.x / a0 : wc.x,
-                        (a0 != 0.0) ? wc.y + omega * res.y / a0 : wc.y};
+            const v2d q = jac_div2(v2d{omega * res.x, omega * res.y}, a2, dq, rq);
+            const v2d v{(a0 != 0.0) ? wc.x + q.x : wc.x, (a0 != 0.0) ? wc.y + q.y : wc.y};
             *reinterpret_cast<v2du *>(unext + (size_t)row) = v;
             if (partials) {
                double a = res.x * res.x, b = res.y * res.y;
@@ -3964,7 +3973,15 @@ mz_sweep_outer_kernel(
       pidm = pidk;
       xm = xc;
       xc = xq;
-      xq = xn;
+      if (PD == 2) {
+         xq = xn;
+         xn = xnn;
+         cur = nx1;
+         nx1 = nxt;
+      } else {
+         xq = xnn;
+         cur = nxt;
+      }
    }
    if (partials) {
       for (int w = tid; w < 2 * NL * (k1 - k0); w += 256 * NT) {
@@ -3982,6 +3999,8 @@ bool mz_sweep_outer_ok(const amg_mat *A)
    return A->mz_P && !A->mz27 && A->mp_uni && A->mz_S == 512 && A->mz_P % 512 == 0 &&
           (A->mz_P / 512) % AMG_MZF_NL == 0 && A->ppat && A->mpmask;
 }
+
+static bool fast_div_of(const amg_mat *A, double *d, double *y);
 
 // the fused pair (see mz_sweep_outer_kernel): u1out = u' (when non-null),
 // rout = r (when non-null), unext = u'', partials: the outer residual's
@@ -4003,12 +4022,24 @@ void mz_sweep_outer(hipStream_t s, const amg_mat *A, const double *f, const doub
       const char *e = std::getenv("AMG_FUSE_OUTER_OCC");
       return e && std::atoi(e) == 2;
    }();
+   // AMG_FUSE_OUTER_PD=2: operands two planes ahead
+   static const int pd = [] {
+      const char *e = std::getenv("AMG_FUSE_OUTER_PD");
+      return e && std::atoi(e) == 2 ? 2 : 1;
+   }();
+   double dq = 0.0, rq = 0.0;
+   if (!fast_div_of(A, &dq, &rq)) dq = rq = 0.0;
    auto go = [&](auto store, auto minb) {
       constexpr bool ST = decltype(store)::value;
       constexpr int MB = decltype(minb)::value;
-      mz_sweep_outer_kernel<ST, MB><<<npb * nch, 256 * AMG_MZF_NT, 0, s>>>(
-         A->ppat, A->mpmask, A->pp_n, Sv, f, u, u1out, rout, unext, omega, P, nz, zc, npb, A->ctx->mz_xcd,
-         partials);
+      if (pd == 2)
+         mz_sweep_outer_kernel<ST, MB, 2><<<npb * nch, 256 * AMG_MZF_NT, 0, s>>>(
+            A->ppat, A->mpmask, A->pp_n, Sv, f, u, u1out, rout, unext, omega, P, nz, zc, npb, A->ctx->mz_xcd,
+            partials, dq, rq);
+      else
+         mz_sweep_outer_kernel<ST, MB, 1><<<npb * nch, 256 * AMG_MZF_NT, 0, s>>>(
+            A->ppat, A->mpmask, A->pp_n, Sv, f, u, u1out, rout, unext, omega, P, nz, zc, npb, A->ctx->mz_xcd,
+            partials, dq, rq);
    };
    using T = std::true_type;
    using F = std::false_type;

@@ -23,7 +23,7 @@ rows = list(csv.DictReader(open(ks)))
 out = []
 for r in rows:
     n = r["Name"]
-    for key in ("csr_mz27_kernel", "mz_res_restrict", "csr_mz_kernel", "geo_prolong_march"):
+    for key in ("csr_mz27", "mz_res_restrict", "csr_mz_kernel", "geo_prolong_march", "mz_sweep_outer"):
         if key in n:
             out.append((float(r["TotalDurationNs"]), n[:70], float(r["AverageNs"]) / 1e3, int(r["Calls"])))
 out.sort(reverse=True)
