@@ -54,8 +54,10 @@ def _rank(rank, world, port, n, optd, rep, runs, q):
             rel, cnt = D.async_solve(f[D.row0:D.row0 + D.n0])
             from async_band import race_tables
             e_, s_ = race_tables(D)
+            # the per-row update times / values travel too: the replay of a
+            # process run is then the exact row replay, as for thread ranks
             out.append((float(rel), [int(x) for x in cnt], D.get_u(), [list(map(float, t)) for t in e_],
-                        [list(map(float, t)) for t in s_]))
+                        [list(map(float, t)) for t in s_], getattr(e_, "rows", None), getattr(e_, "vals", None)))
         row0 = D.row0
         D.free()
         amg.dist.finalize(c)
@@ -95,13 +97,20 @@ def slab_async_procs(n, optd, world, rep=1 << 10, runs=1):
     for r in range(world):
         assert got[r][1] is not None, got[r][2]
     order = sorted(range(world), key=lambda r: got[r][1])
+    from async_band import Ends
+
+    def ends_of(t):
+        e = Ends(t[3])
+        e.rows, e.vals = t[5], t[6]
+        return e
+
     out = []
     for k in range(runs):
         rel = got[0][2][k][0]
         assert all(got[r][2][k][0] == rel for r in range(world))  # one allreduced norm
         u = np.concatenate([got[r][2][k][2] for r in order])
         rs = [got[r][1] for r in order] + [got[order[-1]][1] + got[order[-1]][2][k][2].size]
-        out.append((rel, got[0][2][k][1], u, [got[r][2][k][3] for r in order], rs,
+        out.append((rel, got[0][2][k][1], u, [ends_of(got[r][2][k]) for r in order], rs,
                     [got[r][2][k][4] for r in order]))  # per rank
     return out
 
