@@ -201,7 +201,11 @@ struct AmgCorrTimes {
       if (hipMemcpy(h.data(), d_st, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
          return -1;
       const double tpm = wall_khz > 0 ? (double)wall_khz : 1e5; // ticks per ms
-      std::vector<unsigned> hr((size_t)nrow);
+      // the host copy of a correction's row times only where rows were
+      // recorded (nrow is the level-0 row count: a per-solve zero-filled
+      // buffer of that size cost 12 % of config 3's asynchronous cycle)
+      std::vector<unsigned> hr;
+      if (rows_j > 0) hr.resize((size_t)nrow);
       for (int k = 0; k < st_L && k < (int)cnt.size(); k++)
          for (int j = 0; j < cnt[k] && j < st_cap; j++) {
             const unsigned long long a = h[4 * ((size_t)k * st_cap + j)], b = h[4 * ((size_t)k * st_cap + j) + 1];
