@@ -165,6 +165,12 @@ struct AmgCorrTimes {
             rows_alloc = need;
          }
       }
+      if (rows_j == 0) {
+         // no row arrays: the records set on the device, in stream order (a
+         // pageable host copy per solve serialises the ranks sharing a GPU)
+         amgk::stamp_init(s, d_st, L * cap);
+         return 0;
+      }
       h_init.assign((size_t)4 * L * cap, 0ull);
       for (int k = 0; k < L; k++)
          for (int j = 0; j < cap; j++) {

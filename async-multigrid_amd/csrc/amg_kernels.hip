@@ -2649,8 +2649,11 @@ __global__ __launch_bounds__(256) void mz_prolong_sweep_kernel(
 //          value after this level's update (old + ef);
 //   OUT 2: u = u + ef (the synchronous cycle's vaxpy with a = 1).
 // a_ii := master entry 0 (the diagonal-first rows' first value, = diag).
+// held to 5 waves per SIMD (<= 96 VGPRs): the per-row race records took the
+// non-uniform forms to 97-99 VGPRs and 4 waves, and config 4's asynchronous
+// cycle from 23.4 to 19.0 cycles/s (profiles/r06/bisect*)
 template <bool UNI, int OUT>
-__global__ __launch_bounds__(256) void mz_xfer_prolong_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mz_xfer_prolong_kernel(
    const unsigned char *__restrict__ ppat, const unsigned long long *__restrict__ mmask_g, int np,
    const v2d *__restrict__ mval_g, MpSten Sv, const double *__restrict__ e, const double *__restrict__ wg,
    double mw, int nx, int ny, int nz, int zc, int npb, int xcd, double *__restrict__ out, double *__restrict__ u_priv,
@@ -6336,12 +6339,16 @@ void atomic_correct(hipStream_t s, double *u, const double *e, double *u_priv, i
    else atomic_correct_k<false><<<ew_blocks(n), 256, 0, s>>>(u, e, u_priv, n, stamp);
 }
 
+// the n 4-word correction records of AmgCorrTimes: window start (min'ed),
+// window end (max'ed), no row arrays
 __global__ void stamp_init_k(unsigned long long *st, int n)
 {
    EW_LOOP(i, 0, n)
    {
-      st[2 * i] = ~0ull;
-      st[2 * i + 1] = 0ull;
+      st[4 * i] = ~0ull;
+      st[4 * i + 1] = 0ull;
+      st[4 * i + 2] = 0ull;
+      st[4 * i + 3] = 0ull;
    }
 }
 void stamp_init(hipStream_t s, unsigned long long *stamps, int n)
