@@ -192,7 +192,11 @@ struct AmgCorrTimes {
    }
    unsigned long long *stamp(int k, int j) const
    {
-      return (d_st && k >= 0 && k < st_L && j >= 0 && j < st_cap) ? d_st + 4 * ((size_t)k * st_cap + j) : nullptr;
+      if (!(d_st && k >= 0 && k < st_L && j >= 0 && j < st_cap)) return nullptr;
+      unsigned long long *p = d_st + 4 * ((size_t)k * st_cap + j);
+      // low bit: the record carries row arrays (stamp_rows reads them only then)
+      return (j < rows_j && nrow > 0) ? reinterpret_cast<unsigned long long *>(reinterpret_cast<uintptr_t>(p) | 1)
+                                      : p;
    }
    // after the solve (the stream has finished): windows of the first cnt[k]
    // corrections of every level, and their row times where recorded

@@ -1865,12 +1865,22 @@ constexpr int AMG_RR_RING = 4;
 // a stamp from every workgroup would queue tens of thousands of atomics on one
 // word and slow the kernel it measures several-fold); vector atomics
 __device__ __forceinline__ bool stamp_wg() { return (blockIdx.x & 63) == 0 || blockIdx.x == gridDim.x - 1; }
+// a record pointer's low bit (AmgCorrTimes::stamp) says whether the record
+// carries row arrays: without it the update kernels never read the record
+// (its line takes the window atomics; loading the row pointers from it in
+// every wave cost config 4's asynchronous cycle 18 %)
+__device__ __forceinline__ unsigned long long *stamp_rec(unsigned long long *st)
+{
+   return reinterpret_cast<unsigned long long *>(reinterpret_cast<uintptr_t>(st) & ~(uintptr_t)7);
+}
 __device__ __forceinline__ void stamp_begin(unsigned long long *st)
 {
+   st = stamp_rec(st);
    if (st && threadIdx.x == 0 && stamp_wg()) atomicMin(st, (unsigned long long)wall_clock64());
 }
 __device__ __forceinline__ void stamp_end(unsigned long long *st)
 {
+   st = stamp_rec(st);
    if (st && stamp_wg()) {
       __syncthreads();
       if (threadIdx.x == 0) atomicMax(st + 1, (unsigned long long)wall_clock64());
@@ -1891,7 +1901,8 @@ struct RowRec {
 };
 __device__ __forceinline__ RowRec stamp_rows(const unsigned long long *st)
 {
-   if (!st) return RowRec{nullptr, nullptr};
+   if (!(reinterpret_cast<uintptr_t>(st) & 1)) return RowRec{nullptr, nullptr};
+   st = reinterpret_cast<const unsigned long long *>(reinterpret_cast<uintptr_t>(st) & ~(uintptr_t)7);
    return RowRec{reinterpret_cast<unsigned *>(static_cast<uintptr_t>(st[2])),
                  reinterpret_cast<double *>(static_cast<uintptr_t>(st[3]))};
 }
